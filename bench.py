@@ -1,0 +1,171 @@
+"""bench.py -- TPE suggestion-round throughput on MI355X.
+
+Workload (BASELINE.json configs[2], the metric's "10k-trial history"):
+32 hyperparameters, kind = i mod 5 in {uniform(-5,5), loguniform(-5,2),
+quniform(0,100,1), normal(0,3), choice(5)}, N = 10000 synthetic trials,
+2^21 EI candidates per label per GPU (2^24 at 8 GPUs, weak scaling).
+
+One step = one fused suggestion round on the resident posterior: Philox
+sampling of every label's candidates from l(x), lpdf under l and g for every
+(candidate, component) pair, broadcast_best maxloc per label, and (N > 1) the
+cross-GPU winner exchange over RCCL.  Inputs (the posterior descriptors) are
+resident in HBM before the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--precision f64|f32]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+# Executed FP64 FLOPs per (candidate, component) evaluation of each kernel
+# family, counted from the gfx950 ISA of the inner loop (FMA = 2, other f64
+# arithmetic = 1, compares excluded); see DESIGN.md "Roofline".
+FLOPS_PER_EVAL = {'dense_gmm1': 35.0, 'dense_lgmm1': 35.0}
+PEAK_FP64_VECTOR_TFLOPS = 78.6        # MI355X spec (MI355X_MICROARCH.md)
+PEAK_FP32_VECTOR_TFLOPS = 157.3
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--precision', default='f64', choices=['f64', 'f32'])
+    ap.add_argument('--labels', type=int, default=32)
+    ap.add_argument('--trials', type=int, default=10000)
+    ap.add_argument('--cand-log2', type=int, default=21)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-sample', type=int, default=2048,
+                    help='candidates per label in the CPU baseline sample')
+    return ap.parse_args()
+
+
+def cpu_baseline(hist, posts, n_cand):
+    """The oracle (numpy restatement of the reference, test infra) timed on
+    the host: sample + score + argmax for every label on a bounded sample."""
+    from oracle import tpe_oracle as O
+    rng = np.random.RandomState(1)
+    evals = 0
+    t0 = time.perf_counter()
+    for p in posts:
+        if p.family == 'categorical':
+            cand = rng.multinomial(1, p.below, size=n_cand).argmax(1)
+            lb, la = O.categorical_lpdf(cand, p.below), O.categorical_lpdf(cand, p.above)
+            evals += 2 * n_cand
+        else:
+            samp = O.gmm1_sample if p.family == 'GMM1' else O.lgmm1_sample
+            f = O.gmm1_lpdf if p.family == 'GMM1' else O.lgmm1_lpdf
+            cand = samp(*p.below, low=p.low, high=p.high, q=p.q, rng=rng, size=(n_cand,))
+            lb = f(cand, *p.below, low=p.low, high=p.high, q=p.q)
+            la = f(cand, *p.above, low=p.low, high=p.high, q=p.q)
+            evals += n_cand * (len(p.below[0]) + len(p.above[0]))
+        O.broadcast_best_index(lb, la)
+    dt = time.perf_counter() - t0
+    return evals / dt, dt, evals
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl')
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.engine import Engine, RESULT_DTYPE, merge_results
+    from hyperopt_amd.workloads import mixed_history
+
+    hist = mixed_history(args.labels, args.trials, seed=0)
+    posts = hist.posteriors()
+    descs, w, m, s = P.pack(posts)
+    eng = Engine(local, args.precision)
+    eng.set_posterior(descs, w, m, s)
+    C = 1 << args.cand_log2
+    L = len(posts)
+
+    def step(i):
+        res = eng.suggest(seed=1234 + i, n_candidates=C, round=i, cand_offset=rank * C)
+        if dist is not None:   # exchange per-GPU winners (L x 48 B) over RCCL
+            t = torch.from_numpy(res.view(np.uint8).copy()).cuda(local)
+            g = torch.empty(world * t.numel(), dtype=torch.uint8, device=t.device)
+            dist.all_gather_into_tensor(g, t)
+            parts = g.cpu().numpy().view(RESULT_DTYPE).reshape(world, L)
+            res = merge_results(parts)
+        return res
+
+    for i in range(args.warmup):
+        step(i)
+    mode_ms = {}
+    mode_ev = {}
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+        for k, (ms, ev) in eng.last_mode_stats().items():
+            mode_ms[k] = mode_ms.get(k, 0.0) + ms
+            mode_ev[k] = mode_ev.get(k, 0) + ev
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64, device='cuda')
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    evals_per_step = sum(mode_ev.values()) // max(args.steps, 1)
+    total_evals = evals_per_step * args.steps * world
+    value = total_evals / dt
+
+    # roofline of the dominant kernel family (device time from HIP events on
+    # the engine's stream, summed over the timed steps)
+    dom = max((k for k in mode_ms if k in FLOPS_PER_EVAL), key=lambda k: mode_ms[k])
+    dom_rate = mode_ev[dom] / (mode_ms[dom] * 1e-3)
+    peak = PEAK_FP64_VECTOR_TFLOPS if args.precision == 'f64' else PEAK_FP32_VECTOR_TFLOPS
+    achieved = dom_rate * FLOPS_PER_EVAL[dom] / 1e12
+    roof = {'bound': 'valu', 'kernel': 'k_round<%s,%s>' % (args.precision, dom),
+            'achieved': round(achieved, 3), 'peak': peak, 'unit': 'TFLOP/s',
+            'frac': round(achieved / peak, 4), 'traffic': None,
+            'evals_per_s': dom_rate, 'flops_per_eval': FLOPS_PER_EVAL[dom],
+            'launch_ms': mode_ms[dom] / args.steps}
+    line = {
+        'metric': 'TPE candidate x component lpdf evals/sec (10k-trial history)',
+        'value': value, 'unit': 'evals/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3,
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+        'dtype': args.precision, 'data': 'synthetic (prior draws, seed 0)',
+        'config': {'workload': 'config3: %d-dim mixed space, N=%d history, 2^%d EI candidates '
+                               'per label per GPU' % (args.labels, args.trials, args.cand_log2),
+                   'labels': L, 'history': args.trials, 'candidates_per_label_per_gpu': C,
+                   'parallelism': 'candidate-sharded x%d' % world},
+        'per_family_ms': {k: round(v / args.steps, 3) for k, v in mode_ms.items() if v},
+        'roofline': roof,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        rate, sec, ev = cpu_baseline(hist, posts, args.cpu_sample)
+        line['cpu_baseline'] = {'value': rate, 'unit': 'evals/s', 'cores': 1, 'kind': 'port',
+                                'sample': 'all %d labels x %d candidates (of 2^%d) sampled, '
+                                          'scored under l and g and argmaxed by the numpy '
+                                          'restatement of the reference; %.1f s, %.3g evals'
+                                          % (L, args.cpu_sample, args.cand_log2, sec, ev)}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,116 @@
+"""ctypes binding of the C ABI in include/hyperopt_tpe.h.
+
+The shared library `libhyperopt_tpe.so` is built in-tree (see
+`hyperopt_amd/_build.py`).  There is no fallback: if it is missing or a
+symbol is absent, importing the engine raises.
+
+PyTorch, when importable, is imported BEFORE the library is loaded so that the
+process holds exactly one HIP runtime (torch's bundled libamdhip64.so.7 has
+the same SONAME, so the dynamic loader binds our library to it).
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libhyperopt_tpe.so')
+HEADER = os.path.join(os.path.dirname(HERE), 'include', 'hyperopt_tpe.h')
+
+TPE_OK = 0
+TPE_ERR_VALUE = -1
+TPE_ERR_TYPE = -2
+TPE_ERR_ARG = -3
+TPE_ERR_HIP = -4
+TPE_ERR_SAMPLE = -5
+
+TPE_F64 = 0
+TPE_F32 = 1
+
+TPE_GMM1 = 0
+TPE_LGMM1 = 1
+TPE_CATEGORICAL = 2
+
+TPE_HAS_LOW = 1
+TPE_HAS_HIGH = 2
+TPE_HAS_Q = 4
+
+
+class LabelDesc(ctypes.Structure):
+    _fields_ = [('kind', ctypes.c_int32), ('flags', ctypes.c_int32),
+                ('low', ctypes.c_double), ('high', ctypes.c_double), ('q', ctypes.c_double),
+                ('below_off', ctypes.c_int64), ('above_off', ctypes.c_int64),
+                ('n_below', ctypes.c_int32), ('n_above', ctypes.c_int32)]
+
+
+class LabelResult(ctypes.Structure):
+    _fields_ = [('value', ctypes.c_double), ('score', ctypes.c_double),
+                ('lpdf_below', ctypes.c_double), ('lpdf_above', ctypes.c_double),
+                ('index', ctypes.c_int64), ('label', ctypes.c_int32), ('status', ctypes.c_int32)]
+
+
+assert ctypes.sizeof(LabelDesc) == 56
+assert ctypes.sizeof(LabelResult) == 48
+
+_P = ctypes.c_void_p
+_I32, _I64, _U32, _U64, _D = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
+                              ctypes.c_uint64, ctypes.c_double)
+_PD = ctypes.POINTER(ctypes.c_double)
+
+# name -> (restype, argtypes); every function declared in include/hyperopt_tpe.h
+SIGNATURES = {
+    'tpe_abi_version': (ctypes.c_int, []),
+    'tpe_ctx_create': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]),
+    'tpe_ctx_destroy': (None, [_P]),
+    'tpe_last_error': (ctypes.c_char_p, [_P]),
+    'tpe_gmm1_lpdf': (ctypes.c_int, [_P, _P, _I64, _P, _P, _P, _I32, _I32, _D, _D, _D, _P]),
+    'tpe_lgmm1_lpdf': (ctypes.c_int, [_P, _P, _I64, _P, _P, _P, _I32, _I32, _D, _D, _D, _P]),
+    'tpe_categorical_lpdf': (ctypes.c_int, [_P, _P, _I64, _P, _I32, _P]),
+    'tpe_broadcast_best': (ctypes.c_int, [_P, _P, _P, _I64, _P]),
+    'tpe_gmm1_sample': (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _D, _D, _D, _U64, _U32, _U32,
+                                       _I64, _I64, _P]),
+    'tpe_lgmm1_sample': (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _D, _D, _D, _U64, _U32, _U32,
+                                        _I64, _I64, _P]),
+    'tpe_categorical_sample': (ctypes.c_int, [_P, _P, _I32, _U64, _U32, _U32, _I64, _I64, _P]),
+    'tpe_set_posterior': (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _I64]),
+    'tpe_suggest': (ctypes.c_int, [_P, _U64, _U32, _I64, _I64, _P]),
+    'tpe_suggest_batch': (ctypes.c_int, [_P, _U64, _P, _I32, _I64, _I64, _P]),
+    'tpe_score': (ctypes.c_int, [_P, _I32, _P, _I64, _P, _P, _P]),
+    'tpe_merge_results': (ctypes.c_int, [_P, _I32, _I32, _P]),
+    'tpe_last_timing': (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float),
+                                       ctypes.POINTER(ctypes.c_float)]),
+    'tpe_last_evals': (ctypes.c_int64, [_P]),
+    'tpe_last_mode_stats': (ctypes.c_int, [_P, _P, _P]),
+}
+
+_lib = None
+
+
+def load():
+    """Load and bind the library once.  Raises OSError / AttributeError if the
+    native build is missing or stale -- there is no Python fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    try:  # one HIP runtime per process: let torch bring its libamdhip64 first
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise OSError('hyperopt_amd native library not built: %s (run '
+                      '`python -m hyperopt_amd._build` or __graft_entry__.build())' % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.tpe_abi_version() != 1:
+        raise OSError('ABI version mismatch')
+    _lib = lib
+    return lib
+
+
+def header_functions(path=HEADER):
+    """Names of the functions declared in the C header (for export checks)."""
+    import re
+    txt = open(path).read()
+    txt = re.sub(r'/\*.*?\*/', '', txt, flags=re.S)
+    return sorted(set(re.findall(r'\b(tpe_[a-z0-9_]+)\s*\(', txt)))

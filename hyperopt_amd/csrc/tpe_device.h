@@ -1,0 +1,252 @@
+// tpe_device.h -- device-side building blocks of the gfx950 TPE engine:
+// Philox4x32-10 counter RNG, the truncated-mixture samplers, the
+// log-sum-exp / quantized-mass scorers and the broadcast_best comparator.
+//
+// Reference semantics are cited per function (mvanveen/hyperopt,
+// hyperopt/tpe.py).  Everything here is wave64 VALU code: one candidate per
+// lane (R per thread), mixture components are wave-uniform and are read
+// through the scalar unit (s_load into SGPRs), so no LDS is needed for them.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tpe {
+
+constexpr double kEps = 1e-12;  // tpe.py:31
+
+enum Mode : int { DENSE_GMM = 0, DENSE_LGMM = 1, QUANT_GMM = 2, QUANT_LGMM = 3, CAT = 4 };
+
+// One resident label, prepared on the host by tpe_set_posterior.
+struct DLabel {
+    int32_t mode;
+    int32_t flags;      // TPE_HAS_LOW | TPE_HAS_HIGH | TPE_HAS_Q
+    double low, high, q;
+    double exp_low, exp_high;   // LGMM1 quantized bounds in sample space
+    double shift_b, shift_a;    // dense: LSE shift M (max_k log coef_k)
+    double logpacc_b, logpacc_a;// quantized: log(p_accept) per mixture
+    int64_t comp_b, comp_a;     // record offsets into the component arrays
+    int32_t nb, na;
+    int64_t samp_off;           // offset of the below mixture's sampling records
+    int32_t ns;
+    int32_t stream;             // Philox stream id (label position)
+};
+
+// Component record.  dense: (mu, a = sqrt(.5)/max(sigma,EPS), c = log coef - M, -)
+// quantized: (mu, a = 1/max(sqrt(2) sigma, EPS), -, w).  categorical: c = log p.
+template <typename T>
+struct alignas(4 * sizeof(T)) Comp {
+    T mu, a, c, w;
+};
+
+// Sampling record of the below mixture: cumulative weight, raw mu and sigma.
+struct alignas(32) SampRec {
+    double cdf, mu, sigma, pad;
+};
+
+struct Partial {
+    uint64_t key;
+    int64_t idx;
+    double value, lb, la;
+};
+
+// ---------------------------------------------------------------- Philox ----
+struct U4 {
+    uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+        const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+        c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+
+// 53-bit uniform in (0, 1] (never 0: Box-Muller takes its log).
+__device__ __forceinline__ double u01_open0(uint32_t hi, uint32_t lo) {
+    const uint64_t k = ((uint64_t)hi << 21) ^ (uint64_t)(lo >> 11);
+    return (double)(k + 1) * 0x1.0p-53;
+}
+
+// first k with cdf[k] > u (cdf[n-1] == 1 exactly, u < 1).
+__device__ __forceinline__ int cdf_search(const SampRec* __restrict__ s, int n, double u) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s[mid].cdf > u) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+}
+
+// Draw one sample of the below posterior for global candidate g.
+// GMM1 / LGMM1 (tpe.py:68-99 / 222-256): component ~ weights, x ~ N(mu, sigma),
+// bounded: retry until low <= x < high (re-selecting the component, exactly as
+// the reference loop does), LGMM1 then exp(x); finally round(x / q) * q.
+// categorical (stochastic.py:109-147): index ~ p.
+// Returns false if the truncation interval was not reached within the cap.
+template <int MODE>
+__device__ __forceinline__ bool sample_below(const DLabel& L, const SampRec* __restrict__ s,
+                                             uint64_t seed, uint32_t round, uint32_t g,
+                                             double& out) {
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    if constexpr (MODE == CAT) {
+        const U4 r = philox4x32_10(U4{g, 0u, (uint32_t)L.stream, round}, k0, k1);
+        out = (double)cdf_search(s, L.ns, (double)r.x * 0x1.0p-32);
+        return true;
+    } else {
+        const bool bounded = (L.flags & 3) == 3;
+        for (uint32_t it = 0; it < (1u << 16); ++it) {
+            const U4 r = philox4x32_10(U4{g, it, (uint32_t)L.stream, round}, k0, k1);
+            const int k = cdf_search(s, L.ns, (double)r.x * 0x1.0p-32);
+            const double u1 = u01_open0(r.y, r.z);
+            const double rad = sqrt(-2.0 * log(u1));
+            const double nrm = rad * cospi(2.0 * ((double)r.w * 0x1.0p-32));
+            const double draw = s[k].mu + s[k].sigma * nrm;
+            if (!bounded || (L.low <= draw && draw < L.high)) {
+                double v = (MODE == DENSE_LGMM || MODE == QUANT_LGMM) ? exp(draw) : draw;
+                if (L.flags & 4) v = rint(v / L.q) * L.q;
+                out = v;
+                return true;
+            }
+        }
+        out = __builtin_nan("");
+        return false;
+    }
+}
+
+// numpy minimum/maximum: NaN propagates.
+__device__ __forceinline__ double np_min(double a, double b) { return (a != a || a < b) ? a : b; }
+__device__ __forceinline__ double np_max(double a, double b) { return (a != a || a > b) ? a : b; }
+
+// ------------------------------------------------------------ dense LSE ----
+// log sum_k exp(-z_k^2 + c_k) + M with z_k = (x - mu_k) a_k; tpe.py:144-150 and
+// 284-287 (+ logsum_rows :259-262).  c_k <= 0 after the host shift by M, so the
+// one-pass sum cannot overflow; if it underflows (candidate ~ > 36 sigma from
+// every component) the lane recomputes the reference's two-pass form.
+__device__ __forceinline__ double lse_twopass(const Comp<double>* __restrict__ c, int n, double x) {
+    double m = -__builtin_inf();
+    for (int k = 0; k < n; ++k) {
+        const double z = (x - c[k].mu) * c[k].a;
+        m = fmax(m, fma(-z, z, c[k].c));
+    }
+    if (!(m > -__builtin_inf())) return __builtin_nan("");  // all -inf or NaN: reference gives NaN
+    double s = 0.0;
+    for (int k = 0; k < n; ++k) {
+        const double z = (x - c[k].mu) * c[k].a;
+        s += exp(fma(-z, z, c[k].c) - m);
+    }
+    return log(s) + m;
+}
+
+__device__ __forceinline__ float lse_twopass(const Comp<float>* __restrict__ c, int n, float x) {
+    float m = -__builtin_inff();
+    for (int k = 0; k < n; ++k) {
+        const float z = (x - c[k].mu) * c[k].a;
+        m = fmaxf(m, fmaf(-z, z, c[k].c));
+    }
+    if (!(m > -__builtin_inff())) return __builtin_nanf("");
+    float s = 0.0f;
+    for (int k = 0; k < n; ++k) {
+        const float z = (x - c[k].mu) * c[k].a;
+        s += __builtin_amdgcn_exp2f(fmaf(-z, z, c[k].c) - m);
+    }
+    return (__builtin_log2f(s) + m) * 0.69314718055994531f;  // back to natural log
+}
+
+template <int R>
+__device__ __forceinline__ void lse_dense(const Comp<double>* __restrict__ c, int n, double shift,
+                                          const double (&x)[R], double (&out)[R]) {
+    double acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0.0;
+    for (int k = 0; k < n; ++k) {
+        const double mu = c[k].mu, a = c[k].a, cc = c[k].c;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const double z = (x[r] - mu) * a;
+            acc[r] += exp(fma(-z, z, cc));
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        double v = log(acc[r]);
+        if (!(acc[r] >= 1e-290)) v = lse_twopass(c, n, x[r]);  // rare: underflow / NaN
+        out[r] = v + shift;
+    }
+}
+
+// fp32 fast path: constants pre-scaled by log2(e) so the hardware v_exp_f32
+// (exp2) is used directly; shift is in natural-log units.
+template <int R>
+__device__ __forceinline__ void lse_dense(const Comp<float>* __restrict__ c, int n, double shift,
+                                          const double (&xd)[R], double (&out)[R]) {
+    float x[R], acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        x[r] = (float)xd[r];
+        acc[r] = 0.0f;
+    }
+    for (int k = 0; k < n; ++k) {
+        const float mu = c[k].mu, a = c[k].a, cc = c[k].c;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const float z = (x[r] - mu) * a;
+            acc[r] += __builtin_amdgcn_exp2f(fmaf(-z, z, cc));
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        float v = __builtin_log2f(acc[r]) * 0.69314718055994531f;
+        if (!(acc[r] >= 1e-30f)) v = lse_twopass(c, n, x[r]);
+        out[r] = (double)v + shift;
+    }
+}
+
+// ------------------------------------------------------- quantized mass ----
+// GMM1_lpdf q != None (tpe.py:151-166) and LGMM1_lpdf q != None (:288-305):
+// prob = sum_k [w_k Phi(ub) - w_k Phi(lb)] accumulated sequentially over k in
+// linear space, exactly like the reference (no FMA contraction here, so the
+// cancellation behaves the same); lpdf = log(prob) - log(p_accept).
+template <bool LOG>
+__device__ __forceinline__ double quant_lpdf(const Comp<double>* __restrict__ c, int n,
+                                             double ub, double lb, double logpacc) {
+#pragma clang fp contract(off)
+    double prob = 0.0;
+    for (int k = 0; k < n; ++k) {
+        const double mu = c[k].mu, a = c[k].a, w = c[k].w;
+        double pu, pl;
+        if (LOG) {  // lognormal_cdf: .5 + .5 * erf(z)     tpe.py:194
+            pu = 0.5 + 0.5 * erf((ub - mu) * a);
+            pl = 0.5 + 0.5 * erf((lb - mu) * a);
+        } else {    // normal_cdf: 0.5 * (1 + erf(z))      tpe.py:107
+            pu = 0.5 * (1.0 + erf((ub - mu) * a));
+            pl = 0.5 * (1.0 + erf((lb - mu) * a));
+        }
+        double inc = w * pu;
+        inc -= w * pl;
+        prob += inc;
+    }
+    return log(prob) - logpacc;
+}
+
+// -------------------------------------------------------- broadcast_best ----
+// np.argmax over score = below - above: NaN is greatest (first NaN wins),
+// -0 == +0, and ties go to the lowest index.  Encoded as a total order key.
+__device__ __host__ __forceinline__ uint64_t order_key(double s) {
+    if (s != s) return ~0ull;
+    if (s == 0.0) s = 0.0;
+    uint64_t b;
+    __builtin_memcpy(&b, &s, 8);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+__device__ __forceinline__ bool better(uint64_t ka, int64_t ia, uint64_t kb, int64_t ib) {
+    return ka > kb || (ka == kb && ia < ib);
+}
+
+}  // namespace tpe

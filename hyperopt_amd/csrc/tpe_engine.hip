@@ -1,0 +1,998 @@
+// tpe_engine.hip -- gfx950 kernels + C ABI (include/hyperopt_tpe.h) of the
+// TPE suggestion hot path (mvanveen/hyperopt hyperopt/tpe.py:651-916).
+//
+// Layout in HBM (resident per context, replaced by tpe_set_posterior):
+//   labels_  : DLabel[L]                  per-label mode, bounds, shifts, offsets
+//   comps64_ : Comp<double>[n_records]    below then above mixture of each label
+//   comps32_ : Comp<float>[n_records]     fp32 copy of the dense records (TPE_F32)
+//   samp_    : SampRec[sum K_b]           cumulative weights + mu/sigma of l(x)
+//   partials_: Partial[rounds][L][tiles]  per-workgroup winners
+//   results_ : tpe_label_result[rounds][L]
+// Kernels: k_round<T, MODE, SAMPLE> (sample -> lpdf below/above -> block
+// maxloc, one launch per mode group), k_reduce (per label winner).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/hyperopt_tpe.h"
+#include "tpe_device.h"
+
+using namespace tpe;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kR = 4;                 // candidates per thread
+constexpr int kTile = kBlock * kR;    // candidates per workgroup
+
+thread_local std::string g_create_error;
+
+// --------------------------------------------------------------- kernels ----
+
+template <typename T, int MODE, bool SAMPLE>
+__global__ __launch_bounds__(kBlock) void k_round(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<T>* __restrict__ comps, const Comp<double>* __restrict__ comps64,
+    const SampRec* __restrict__ samp, const double* __restrict__ cand_in, int64_t n,
+    int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, int32_t n_labels,
+    int32_t tiles, Partial* __restrict__ partials, double* __restrict__ out_lb,
+    double* __restrict__ out_la, int32_t* __restrict__ err) {
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    const uint32_t round = rounds[blockIdx.z];
+    const int tid = threadIdx.x;
+    const int64_t base = (int64_t)blockIdx.x * kTile;
+
+    double x[kR], lb[kR], la[kR];
+    bool valid[kR];
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+        const int64_t i = base + r * kBlock + tid;
+        valid[r] = i < n;
+        double v = 0.0;
+        if (valid[r]) {
+            if constexpr (SAMPLE) {
+                if (!sample_below<MODE>(L, samp + L.samp_off, seed, round,
+                                        (uint32_t)(cand_offset + i), v))
+                    atomicOr(err, 1);
+            } else {
+                v = cand_in[i];
+            }
+        } else if constexpr (MODE == CAT) {
+            v = 0.0;
+        } else {
+            v = (MODE == DENSE_LGMM || MODE == QUANT_LGMM) ? 1.0 : 0.0;
+        }
+        x[r] = v;
+    }
+
+    if constexpr (MODE == DENSE_GMM) {
+        lse_dense<kR>(comps + L.comp_b, L.nb, L.shift_b, x, lb);
+        lse_dense<kR>(comps + L.comp_a, L.na, L.shift_a, x, la);
+    } else if constexpr (MODE == DENSE_LGMM) {
+        double y[kR], lx[kR];
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+            lx[r] = log(x[r]);
+            y[r] = lx[r];
+        }
+        lse_dense<kR>(comps + L.comp_b, L.nb, L.shift_b, y, lb);
+        lse_dense<kR>(comps + L.comp_a, L.na, L.shift_a, y, la);
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+            lb[r] -= lx[r];
+            la[r] -= lx[r];
+        }
+    } else if constexpr (MODE == QUANT_GMM || MODE == QUANT_LGMM) {
+        const double half = L.q / 2.0;
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+            double ub = x[r] + half, lo = x[r] - half;
+            if (MODE == QUANT_GMM) {
+                if (L.flags & 2) ub = np_min(ub, L.high);
+                if (L.flags & 1) lo = np_max(lo, L.low);
+            } else {
+                if (L.flags & 2) ub = np_min(ub, L.exp_high);
+                if (L.flags & 1) lo = np_max(lo, L.exp_low);
+                lo = np_max(0.0, lo);
+                if (valid[r] && ub < 0.0) atomicOr(err, 2);  // tpe.py:187-188
+                ub = log(np_max(ub, kEps));
+                lo = log(np_max(lo, kEps));
+            }
+            lb[r] = quant_lpdf<MODE == QUANT_LGMM>(comps64 + L.comp_b, L.nb, ub, lo, L.logpacc_b);
+            la[r] = quant_lpdf<MODE == QUANT_LGMM>(comps64 + L.comp_a, L.na, ub, lo, L.logpacc_a);
+        }
+    } else {  // CAT: categorical_lpdf = log(p[sample])   tpe.py:56-63
+#pragma unroll
+        for (int r = 0; r < kR; ++r) {
+            const int64_t s = (int64_t)x[r];
+            if (valid[r] && (s < 0 || s >= L.nb || (double)s != x[r])) atomicOr(err, 4);
+            const int64_t sc = s < 0 ? 0 : (s >= L.nb ? L.nb - 1 : s);
+            lb[r] = comps64[L.comp_b + sc].c;
+            la[r] = comps64[L.comp_a + sc].c;
+        }
+    }
+
+    // per-thread winner over its R candidates
+    uint64_t bk = 0;
+    int64_t bi = INT64_MAX;
+    double bv = 0.0, bl = 0.0, ba = 0.0;
+    const size_t row = ((size_t)blockIdx.z * n_labels + li) * (size_t)n;
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+        if (!valid[r]) continue;
+        const int64_t i = base + r * kBlock + tid;
+        if (out_lb) {
+            out_lb[row + i] = lb[r];
+            out_la[row + i] = la[r];
+        }
+        const uint64_t key = order_key(lb[r] - la[r]);
+        const int64_t gi = cand_offset + i;
+        if (better(key, gi, bk, bi)) {
+            bk = key;
+            bi = gi;
+            bv = x[r];
+            bl = lb[r];
+            ba = la[r];
+        }
+    }
+    // wave64 reduction
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t ok = __shfl_xor(bk, off);
+        const int64_t oi = __shfl_xor(bi, off);
+        const double ov = __shfl_xor(bv, off), ol = __shfl_xor(bl, off), oa = __shfl_xor(ba, off);
+        if (better(ok, oi, bk, bi)) {
+            bk = ok;
+            bi = oi;
+            bv = ov;
+            bl = ol;
+            ba = oa;
+        }
+    }
+    __shared__ Partial sh[kBlock / 64];
+    if ((tid & 63) == 0) sh[tid >> 6] = Partial{bk, bi, bv, bl, ba};
+    __syncthreads();
+    if (tid == 0) {
+        Partial best = sh[0];
+        for (int w = 1; w < kBlock / 64; ++w)
+            if (better(sh[w].key, sh[w].idx, best.key, best.idx)) best = sh[w];
+        partials[((size_t)blockIdx.z * n_labels + li) * tiles + blockIdx.x] = best;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_reduce(const Partial* __restrict__ partials,
+                                                   int32_t tiles, int32_t n_labels,
+                                                   tpe_label_result* __restrict__ out) {
+    const int li = blockIdx.x, rz = blockIdx.y, tid = threadIdx.x;
+    const Partial* p = partials + ((size_t)rz * n_labels + li) * tiles;
+    Partial best{0, INT64_MAX, 0.0, 0.0, 0.0};
+    for (int t = tid; t < tiles; t += kBlock)
+        if (better(p[t].key, p[t].idx, best.key, best.idx)) best = p[t];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        Partial o;
+        o.key = __shfl_xor(best.key, off);
+        o.idx = __shfl_xor(best.idx, off);
+        o.value = __shfl_xor(best.value, off);
+        o.lb = __shfl_xor(best.lb, off);
+        o.la = __shfl_xor(best.la, off);
+        if (better(o.key, o.idx, best.key, best.idx)) best = o;
+    }
+    __shared__ Partial sh[kBlock / 64];
+    if ((tid & 63) == 0) sh[tid >> 6] = best;
+    __syncthreads();
+    if (tid == 0) {
+        best = sh[0];
+        for (int w = 1; w < kBlock / 64; ++w)
+            if (better(sh[w].key, sh[w].idx, best.key, best.idx)) best = sh[w];
+        tpe_label_result r;
+        const bool any = best.idx != INT64_MAX;
+        r.value = best.value;
+        r.score = best.lb - best.la;
+        r.lpdf_below = best.lb;
+        r.lpdf_above = best.la;
+        r.index = any ? best.idx : -1;
+        r.label = li;
+        r.status = 0;
+        out[(size_t)rz * n_labels + li] = r;
+    }
+}
+
+// argmax of below - above over caller arrays (tpe_broadcast_best)
+__global__ __launch_bounds__(kBlock) void k_argmax(const double* __restrict__ b,
+                                                   const double* __restrict__ a, int64_t n,
+                                                   Partial* __restrict__ partials) {
+    uint64_t bk = 0;
+    int64_t bi = INT64_MAX;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * kBlock) {
+        const uint64_t k = order_key(b[i] - a[i]);
+        if (better(k, i, bk, bi)) {
+            bk = k;
+            bi = i;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t ok = __shfl_xor(bk, off);
+        const int64_t oi = __shfl_xor(bi, off);
+        if (better(ok, oi, bk, bi)) {
+            bk = ok;
+            bi = oi;
+        }
+    }
+    __shared__ Partial sh[kBlock / 64];
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = Partial{bk, bi, 0, 0, 0};
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        Partial best = sh[0];
+        for (int w = 1; w < kBlock / 64; ++w)
+            if (better(sh[w].key, sh[w].idx, best.key, best.idx)) best = sh[w];
+        partials[blockIdx.x] = best;
+    }
+}
+
+// ------------------------------------------------------------ host side ----
+
+inline bool host_better(uint64_t ka, int64_t ia, uint64_t kb, int64_t ib) {
+    return ka > kb || (ka == kb && ia < ib);
+}
+
+// numpy-style pairwise summation (what np.sum does for float64 vectors)
+double np_pairwise_sum(const double* a, size_t n) {
+    if (n < 8) {
+        double r = 0.0;
+        for (size_t i = 0; i < n; ++i) r += a[i];
+        return r;
+    }
+    if (n <= 128) {
+        double r[8];
+        for (int j = 0; j < 8; ++j) r[j] = a[j];
+        size_t i = 8;
+        for (; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; ++i) res += a[i];
+        return res;
+    }
+    size_t n2 = n / 2;
+    n2 -= n2 % 8;
+    return np_pairwise_sum(a, n2) + np_pairwise_sum(a + n2, n - n2);
+}
+
+// normal_cdf, tpe.py:102-107
+double host_normal_cdf(double x, double mu, double sigma) {
+    const double bottom = std::max(std::sqrt(2.0) * sigma, kEps);
+    return 0.5 * (1.0 + std::erf((x - mu) / bottom));
+}
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T));
+        if (e == hipSuccess) cap = std::max<size_t>(n, 1);
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+}  // namespace
+
+struct tpe_ctx {
+    int device = 0;
+    int precision = TPE_F64;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    hipEvent_t evm[5][2] = {};         // per-mode kernel brackets
+    bool mode_ran[5] = {};
+    float mode_ms[5] = {};
+    int64_t mode_evals[5] = {};
+    std::string err;
+    float score_ms = 0.f, round_ms = 0.f;
+    int64_t evals = 0;
+
+    // resident posterior
+    std::vector<DLabel> h_labels;
+    std::vector<int32_t> h_group[5];   // label ids per mode
+    int32_t n_labels = 0;
+    DevBuf<DLabel> labels;
+    DevBuf<Comp<double>> comps64;
+    DevBuf<Comp<float>> comps32;
+    DevBuf<SampRec> samp;
+    DevBuf<int32_t> groups;            // concatenated h_group
+    int32_t group_off[5] = {0, 0, 0, 0, 0};
+
+    // per-round scratch
+    DevBuf<Partial> partials;
+    DevBuf<tpe_label_result> results;
+    DevBuf<uint32_t> rounds;
+    DevBuf<int32_t> errflag;
+    DevBuf<double> cand, out_lb, out_la;
+    DevBuf<int32_t> one_group;
+
+    int fail(int code, const std::string& m) {
+        err = m;
+        return code;
+    }
+    int hip(hipError_t e, const char* what) {
+        if (e == hipSuccess) return TPE_OK;
+        err = std::string(what) + ": " + hipGetErrorString(e);
+        return TPE_ERR_HIP;
+    }
+};
+
+#define HIPCHK(ctx, call)                                  \
+    do {                                                   \
+        int _rc = (ctx)->hip((call), #call);               \
+        if (_rc != TPE_OK) return _rc;                     \
+    } while (0)
+
+namespace {
+
+// Fold one GMM1/LGMM1 mixture into device records (host fp64, reference
+// formulas).  Returns the LSE shift (dense) or log p_accept (quantized).
+struct Folded {
+    double shift = 0.0, logpacc = 0.0;
+};
+
+Folded fold_mixture(int kind, bool quant, int flags, double low, double high, const double* w,
+                    const double* mu, const double* sg, int n, Comp<double>* out64,
+                    Comp<float>* out32) {
+    Folded f;
+    const bool bounded = (flags & 3) != 0;
+    double p_accept = 1.0;
+    if (bounded) {  // tpe.py:139-142 / 279-282
+        std::vector<double> t(n);
+        for (int k = 0; k < n; ++k)
+            t[k] = w[k] * (host_normal_cdf(high, mu[k], sg[k]) - host_normal_cdf(low, mu[k], sg[k]));
+        p_accept = np_pairwise_sum(t.data(), n);
+    }
+    if (quant) {
+        f.logpacc = std::log(p_accept);
+        for (int k = 0; k < n; ++k) {
+            const double a = 1.0 / std::max(std::sqrt(2.0) * sg[k], kEps);
+            out64[k] = Comp<double>{mu[k], a, 0.0, w[k]};
+            if (out32) out32[k] = Comp<float>{(float)mu[k], (float)a, 0.f, (float)w[k]};
+        }
+        return f;
+    }
+    std::vector<double> c(n);
+    std::vector<double> a(n);
+    for (int k = 0; k < n; ++k) {
+        if (kind == TPE_GMM1) {  // log(w / sqrt(2 pi sigma^2) / p_accept), tpe.py:148-150
+            const double Z = std::sqrt(2.0 * M_PI * (sg[k] * sg[k]));
+            c[k] = std::log(w[k] / Z / p_accept);
+            a[k] = std::sqrt(0.5) / std::max(sg[k], kEps);
+        } else {  // log w - log(max(sigma,EPS) sqrt(2 pi)); -log x per candidate, tpe.py:199-208
+            const double s = std::max(sg[k], kEps);
+            c[k] = std::log(w[k]) - std::log(s * std::sqrt(2.0 * M_PI));
+            a[k] = std::sqrt(0.5) / s;
+        }
+    }
+    double M = -INFINITY;
+    for (int k = 0; k < n; ++k)
+        if (c[k] > M) M = c[k];
+    if (!std::isfinite(M)) M = 0.0;
+    f.shift = M;
+    const double l2e = 1.4426950408889634;
+    for (int k = 0; k < n; ++k) {
+        out64[k] = Comp<double>{mu[k], a[k], c[k] - M, w[k]};
+        if (out32)
+            out32[k] = Comp<float>{(float)mu[k], (float)(a[k] * std::sqrt(l2e)),
+                                   (float)((c[k] - M) * l2e), (float)w[k]};
+    }
+    return f;
+}
+
+int validate_mixture(tpe_ctx* ctx, int32_t k, int32_t flags, double low, double high,
+                     bool sampler_checks) {
+    if (k <= 0) return ctx->fail(TPE_ERR_TYPE, "need vector of weights (empty mixture)");
+    if ((flags & 3) == 1 || (flags & 3) == 2)
+        return ctx->fail(TPE_ERR_TYPE, "low and high must both be given or both be None");
+    if (sampler_checks && (flags & 3) == 3 && !(low < high))  // GMM1/LGMM1 only, tpe.py:86
+        return ctx->fail(TPE_ERR_VALUE, "low >= high");
+    return TPE_OK;
+}
+
+struct Groups {
+    const int32_t* dev[5];   // device pointers to label ids per mode
+    int32_t count[5];
+};
+
+template <typename T, int MODE, bool SAMPLE>
+void launch_mode(tpe_ctx* ctx, const Groups& g, int64_t n, int64_t cand_offset, uint64_t seed,
+                 int32_t n_rounds, int32_t tiles, const double* cand_in, double* olb,
+                 double* ola) {
+    const int nl = g.count[MODE];
+    if (nl == 0 || tiles == 0) return;
+    ctx->mode_ran[MODE] = true;
+    (void)hipEventRecord(ctx->evm[MODE][0], ctx->stream);
+    dim3 grid(tiles, nl, n_rounds);
+    const Comp<T>* comps;
+    if constexpr (sizeof(T) == 8) comps = ctx->comps64.p; else comps = ctx->comps32.p;
+    hipLaunchKernelGGL((k_round<T, MODE, SAMPLE>), grid, dim3(kBlock), 0, ctx->stream,
+                       ctx->labels.p, g.dev[MODE], comps, ctx->comps64.p, ctx->samp.p, cand_in,
+                       n, cand_offset, seed, ctx->rounds.p, ctx->n_labels, tiles,
+                       ctx->partials.p, olb, ola, ctx->errflag.p);
+    (void)hipEventRecord(ctx->evm[MODE][1], ctx->stream);
+}
+
+template <bool SAMPLE>
+void launch_all(tpe_ctx* ctx, const Groups& g, int64_t n, int64_t cand_offset, uint64_t seed,
+                int32_t n_rounds, int32_t tiles, const double* cand_in, double* olb, double* ola) {
+    // heaviest groups first
+    launch_mode<double, QUANT_GMM, SAMPLE>(ctx, g, n, cand_offset, seed, n_rounds, tiles, cand_in, olb, ola);
+    launch_mode<double, QUANT_LGMM, SAMPLE>(ctx, g, n, cand_offset, seed, n_rounds, tiles, cand_in, olb, ola);
+    if (ctx->precision == TPE_F32) {
+        launch_mode<float, DENSE_GMM, SAMPLE>(ctx, g, n, cand_offset, seed, n_rounds, tiles, cand_in, olb, ola);
+        launch_mode<float, DENSE_LGMM, SAMPLE>(ctx, g, n, cand_offset, seed, n_rounds, tiles, cand_in, olb, ola);
+    } else {
+        launch_mode<double, DENSE_GMM, SAMPLE>(ctx, g, n, cand_offset, seed, n_rounds, tiles, cand_in, olb, ola);
+        launch_mode<double, DENSE_LGMM, SAMPLE>(ctx, g, n, cand_offset, seed, n_rounds, tiles, cand_in, olb, ola);
+    }
+    launch_mode<double, CAT, SAMPLE>(ctx, g, n, cand_offset, seed, n_rounds, tiles, cand_in, olb, ola);
+}
+
+int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_rounds, int64_t n,
+              int64_t cand_offset, const double* cand_in_dev, double* olb, double* ola,
+              tpe_label_result* out, int32_t only_label) {
+    if (ctx->n_labels == 0) return ctx->fail(TPE_ERR_ARG, "no posterior set (tpe_set_posterior)");
+    if (n < 0 || n_rounds <= 0) return ctx->fail(TPE_ERR_ARG, "bad candidate/round count");
+    if (cand_offset < 0 || cand_offset + n > (int64_t)UINT32_MAX)
+        return ctx->fail(TPE_ERR_ARG, "candidate indices must stay below 2^32");
+    const int32_t tiles = (int32_t)((n + kTile - 1) / kTile);
+    const int32_t L = ctx->n_labels;
+    HIPCHK(ctx, ctx->partials.reserve((size_t)n_rounds * L * std::max(tiles, 1)));
+    HIPCHK(ctx, ctx->results.reserve((size_t)n_rounds * L));
+    HIPCHK(ctx, ctx->rounds.reserve(n_rounds));
+    HIPCHK(ctx, ctx->errflag.reserve(1));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->rounds.p, rounds_h, n_rounds * sizeof(uint32_t),
+                               hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->errflag.p, 0, sizeof(int32_t), ctx->stream));
+    Groups g;
+    for (int m = 0; m < 5; ++m) {
+        g.dev[m] = ctx->groups.p + ctx->group_off[m];
+        g.count[m] = (int32_t)ctx->h_group[m].size();
+    }
+    if (only_label >= 0) {  // tpe_score: launch the one label's mode only
+        HIPCHK(ctx, ctx->one_group.reserve(1));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->one_group.p, &only_label, sizeof(int32_t),
+                                   hipMemcpyHostToDevice, ctx->stream));
+        for (int m = 0; m < 5; ++m) g.count[m] = 0;
+        const int m = ctx->h_labels[only_label].mode;
+        g.dev[m] = ctx->one_group.p;
+        g.count[m] = 1;
+    }
+    for (int m = 0; m < 5; ++m) {
+        ctx->mode_ran[m] = false;
+        ctx->mode_ms[m] = 0.f;
+        ctx->mode_evals[m] = 0;
+    }
+    HIPCHK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+    if (cand_in_dev)
+        launch_all<false>(ctx, g, n, cand_offset, seed, n_rounds, tiles, cand_in_dev, olb, ola);
+    else
+        launch_all<true>(ctx, g, n, cand_offset, seed, n_rounds, tiles, nullptr, olb, ola);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+    if (tiles > 0) {
+        hipLaunchKernelGGL(k_reduce, dim3(L, n_rounds), dim3(kBlock), 0, ctx->stream,
+                           ctx->partials.p, tiles, L, ctx->results.p);
+        HIPCHK(ctx, hipGetLastError());
+    }
+    HIPCHK(ctx, hipEventRecord(ctx->ev2, ctx->stream));
+    int32_t errh = 0;
+    HIPCHK(ctx, hipMemcpyAsync(&errh, ctx->errflag.p, sizeof(int32_t), hipMemcpyDeviceToHost,
+                               ctx->stream));
+    if (tiles > 0 && out)
+        HIPCHK(ctx, hipMemcpyAsync(out, ctx->results.p,
+                                   (size_t)n_rounds * L * sizeof(tpe_label_result),
+                                   hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, hipEventElapsedTime(&ctx->score_ms, ctx->ev0, ctx->ev1));
+    HIPCHK(ctx, hipEventElapsedTime(&ctx->round_ms, ctx->ev0, ctx->ev2));
+    for (int m = 0; m < 5; ++m)
+        if (ctx->mode_ran[m])
+            HIPCHK(ctx, hipEventElapsedTime(&ctx->mode_ms[m], ctx->evm[m][0], ctx->evm[m][1]));
+    int64_t evals = 0;
+    for (int32_t l = 0; l < L; ++l) {
+        if (only_label >= 0 && l != only_label) continue;
+        const DLabel& d = ctx->h_labels[l];
+        const int64_t e = ((d.mode == CAT) ? 2 * n : n * (int64_t)(d.nb + d.na)) * n_rounds;
+        evals += e;
+        ctx->mode_evals[d.mode] += e;
+    }
+    ctx->evals = evals;
+    if (tiles == 0 && out) {
+        for (int32_t j = 0; j < n_rounds * L; ++j) {
+            out[j] = tpe_label_result{NAN, NAN, NAN, NAN, -1, j % L, 0};
+        }
+    }
+    if (errh & 1) return ctx->fail(TPE_ERR_SAMPLE, "truncated sampler: interval [low, high) not reached");
+    if (errh & 2) return ctx->fail(TPE_ERR_VALUE, "negative arg to lognormal_cdf");
+    if (errh & 4) return ctx->fail(TPE_ERR_VALUE, "categorical sample out of range");
+    return TPE_OK;
+}
+
+}  // namespace
+
+void tpe_launch_sample_only(tpe_ctx* ctx, int mode, int64_t n, int64_t offset, uint64_t seed,
+                            double* out);
+
+// ================================================================ C ABI ====
+extern "C" {
+
+int tpe_abi_version(void) { return TPE_ABI_VERSION; }
+
+int tpe_ctx_create(int device, int precision, tpe_ctx** out) {
+    if (!out) return TPE_ERR_ARG;
+    *out = nullptr;
+    if (precision != TPE_F64 && precision != TPE_F32) {
+        g_create_error = "precision must be TPE_F64 or TPE_F32";
+        return TPE_ERR_ARG;
+    }
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || device < 0 || device >= ndev) {
+        g_create_error = std::string("no HIP device ") + std::to_string(device) + " (" +
+                         (e == hipSuccess ? "count " + std::to_string(ndev) : hipGetErrorString(e)) + ")";
+        return TPE_ERR_HIP;
+    }
+    e = hipSetDevice(device);
+    if (e != hipSuccess) {
+        g_create_error = hipGetErrorString(e);
+        return TPE_ERR_HIP;
+    }
+    tpe_ctx* c = new tpe_ctx();
+    c->device = device;
+    c->precision = precision;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipEventCreate(&c->ev2) != hipSuccess) {
+        g_create_error = "stream/event creation failed";
+        tpe_ctx_destroy(c);
+        return TPE_ERR_HIP;
+    }
+    bool ok = true;
+    for (int m = 0; m < 5; ++m)
+        ok = ok && hipEventCreate(&c->evm[m][0]) == hipSuccess &&
+             hipEventCreate(&c->evm[m][1]) == hipSuccess;
+    if (!ok) {
+        g_create_error = "stream/event creation failed";
+        tpe_ctx_destroy(c);
+        return TPE_ERR_HIP;
+    }
+    *out = c;
+    return TPE_OK;
+}
+
+void tpe_ctx_destroy(tpe_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    c->labels.release();
+    c->comps64.release();
+    c->comps32.release();
+    c->samp.release();
+    c->groups.release();
+    c->partials.release();
+    c->results.release();
+    c->rounds.release();
+    c->errflag.release();
+    c->cand.release();
+    c->out_lb.release();
+    c->out_la.release();
+    c->one_group.release();
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->ev2) (void)hipEventDestroy(c->ev2);
+    for (int m = 0; m < 5; ++m)
+        for (int j = 0; j < 2; ++j)
+            if (c->evm[m][j]) (void)hipEventDestroy(c->evm[m][j]);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* tpe_last_error(const tpe_ctx* c) {
+    return c ? c->err.c_str() : g_create_error.c_str();
+}
+
+static int set_posterior_impl(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_labels,
+                              const double* weights, const double* mus, const double* sigmas,
+                              int64_t n_components, bool sampler_checks) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (n_labels <= 0 || !labels || !weights) return ctx->fail(TPE_ERR_ARG, "empty posterior");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    std::vector<DLabel> dl(n_labels);
+    std::vector<Comp<double>> c64;
+    std::vector<Comp<float>> c32;
+    std::vector<SampRec> sr;
+    for (int m = 0; m < 5; ++m) ctx->h_group[m].clear();
+    for (int32_t l = 0; l < n_labels; ++l) {
+        const tpe_label_desc& d = labels[l];
+        DLabel& o = dl[l];
+        std::memset(&o, 0, sizeof(o));
+        const bool quant = (d.flags & TPE_HAS_Q) != 0;
+        if (d.kind == TPE_CATEGORICAL) o.mode = CAT;
+        else if (d.kind == TPE_GMM1) o.mode = quant ? QUANT_GMM : DENSE_GMM;
+        else if (d.kind == TPE_LGMM1) o.mode = quant ? QUANT_LGMM : DENSE_LGMM;
+        else return ctx->fail(TPE_ERR_ARG, "label " + std::to_string(l) + ": unknown kind");
+        if (d.n_below <= 0 || d.n_above <= 0 || d.below_off < 0 || d.above_off < 0 ||
+            d.below_off + d.n_below > n_components || d.above_off + d.n_above > n_components)
+            return ctx->fail(TPE_ERR_ARG, "label " + std::to_string(l) + ": component range");
+        if (d.kind == TPE_CATEGORICAL && d.n_below != d.n_above)
+            return ctx->fail(TPE_ERR_ARG, "categorical: below/above sizes differ");
+        if (d.kind != TPE_CATEGORICAL) {
+            if (!mus || !sigmas) return ctx->fail(TPE_ERR_ARG, "mus/sigmas required");
+            int rc = validate_mixture(ctx, d.n_below, d.flags, d.low, d.high, sampler_checks);
+            if (rc) return rc;
+            if (quant && !(d.q > 0) && !(d.q < 0)) return ctx->fail(TPE_ERR_VALUE, "q must be non-zero");
+        }
+        o.flags = d.flags;
+        o.low = d.low;
+        o.high = d.high;
+        o.q = d.q;
+        o.exp_low = std::exp(d.low);
+        o.exp_high = std::exp(d.high);
+        o.nb = d.n_below;
+        o.na = d.n_above;
+        o.stream = l;
+        // below + above records
+        for (int side = 0; side < 2; ++side) {
+            const int64_t off = side ? d.above_off : d.below_off;
+            const int32_t n = side ? d.n_above : d.n_below;
+            const int64_t at = (int64_t)c64.size();
+            c64.resize(at + n);
+            c32.resize(at + n);
+            if (d.kind == TPE_CATEGORICAL) {
+                for (int k = 0; k < n; ++k) {
+                    const double lp = std::log(weights[off + k]);
+                    c64[at + k] = Comp<double>{0.0, 0.0, lp, weights[off + k]};
+                    c32[at + k] = Comp<float>{0.f, 0.f, (float)lp, (float)weights[off + k]};
+                }
+            } else {
+                Folded f = fold_mixture(d.kind, quant, d.flags, d.low, d.high, weights + off,
+                                        mus + off, sigmas + off, n, c64.data() + at, c32.data() + at);
+                (side ? o.shift_a : o.shift_b) = f.shift;
+                (side ? o.logpacc_a : o.logpacc_b) = f.logpacc;
+            }
+            (side ? o.comp_a : o.comp_b) = at;
+        }
+        // sampling records of the below mixture (cumulative normalised weights)
+        o.samp_off = (int64_t)sr.size();
+        o.ns = d.n_below;
+        double tot = 0.0;
+        for (int k = 0; k < d.n_below; ++k) tot += weights[d.below_off + k];
+        if (!(tot > 0)) {
+            if (sampler_checks) return ctx->fail(TPE_ERR_VALUE, "below weights sum to zero");
+            tot = 1.0;
+        }
+        double run = 0.0;
+        for (int k = 0; k < d.n_below; ++k) {
+            run += weights[d.below_off + k];
+            SampRec s;
+            s.cdf = (k == d.n_below - 1) ? 1.0 : run / tot;
+            s.mu = d.kind == TPE_CATEGORICAL ? 0.0 : mus[d.below_off + k];
+            s.sigma = d.kind == TPE_CATEGORICAL ? 0.0 : sigmas[d.below_off + k];
+            s.pad = 0.0;
+            sr.push_back(s);
+        }
+        ctx->h_group[o.mode].push_back(l);
+    }
+    std::vector<int32_t> cat;
+    for (int m = 0; m < 5; ++m) {
+        ctx->group_off[m] = (int32_t)cat.size();
+        cat.insert(cat.end(), ctx->h_group[m].begin(), ctx->h_group[m].end());
+    }
+    HIPCHK(ctx, ctx->labels.reserve(n_labels));
+    HIPCHK(ctx, ctx->comps64.reserve(c64.size()));
+    HIPCHK(ctx, ctx->comps32.reserve(c32.size()));
+    HIPCHK(ctx, ctx->samp.reserve(sr.size()));
+    HIPCHK(ctx, ctx->groups.reserve(cat.size()));
+    HIPCHK(ctx, hipMemcpy(ctx->labels.p, dl.data(), dl.size() * sizeof(DLabel), hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->comps64.p, c64.data(), c64.size() * sizeof(Comp<double>), hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->comps32.p, c32.data(), c32.size() * sizeof(Comp<float>), hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->samp.p, sr.data(), sr.size() * sizeof(SampRec), hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->groups.p, cat.data(), cat.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    ctx->h_labels = dl;
+    ctx->n_labels = n_labels;
+    return TPE_OK;
+}
+
+int tpe_set_posterior(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_labels,
+                      const double* weights, const double* mus, const double* sigmas,
+                      int64_t n_components) {
+    return set_posterior_impl(ctx, labels, n_labels, weights, mus, sigmas, n_components, true);
+}
+
+int tpe_suggest(tpe_ctx* ctx, uint64_t seed, uint32_t round, int64_t n_candidates,
+                int64_t cand_offset, tpe_label_result* out) {
+    if (!ctx || !out) return TPE_ERR_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    return run_round(ctx, seed, &round, 1, n_candidates, cand_offset, nullptr, nullptr, nullptr,
+                     out, -1);
+}
+
+int tpe_suggest_batch(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds, int32_t n_rounds,
+                      int64_t n_candidates, int64_t cand_offset, tpe_label_result* out) {
+    if (!ctx || !out || !rounds) return TPE_ERR_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    return run_round(ctx, seed, rounds, n_rounds, n_candidates, cand_offset, nullptr, nullptr,
+                     nullptr, out, -1);
+}
+
+int tpe_score(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, double* lpdf_below,
+              double* lpdf_above, tpe_label_result* out) {
+    if (!ctx || (!cand && n > 0)) return TPE_ERR_ARG;
+    if (label < 0 || label >= ctx->n_labels) return ctx->fail(TPE_ERR_ARG, "label out of range");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    // host-side argument checks that the reference raises before computing
+    const DLabel& d = ctx->h_labels[label];
+    if (d.mode == QUANT_LGMM) {
+        for (int64_t i = 0; i < n; ++i) {
+            double ub = cand[i] + d.q / 2.0;
+            if ((d.flags & 2) && ub > d.exp_high) ub = d.exp_high;
+            if (ub < 0) return ctx->fail(TPE_ERR_VALUE, "negative arg to lognormal_cdf");
+        }
+    }
+    if (d.mode == CAT) {
+        for (int64_t i = 0; i < n; ++i)
+            if (!(cand[i] >= 0 && cand[i] < d.nb) || cand[i] != std::floor(cand[i]))
+                return ctx->fail(TPE_ERR_VALUE, "categorical sample out of range");
+    }
+    const size_t rows = (size_t)ctx->n_labels * std::max<int64_t>(n, 1);
+    HIPCHK(ctx, ctx->cand.reserve(std::max<int64_t>(n, 1)));
+    HIPCHK(ctx, ctx->out_lb.reserve(rows));
+    HIPCHK(ctx, ctx->out_la.reserve(rows));
+    if (n > 0)
+        HIPCHK(ctx, hipMemcpyAsync(ctx->cand.p, cand, n * sizeof(double), hipMemcpyHostToDevice,
+                                   ctx->stream));
+    std::vector<tpe_label_result> all(ctx->n_labels);
+    uint32_t round = 0;
+    int rc = run_round(ctx, 0, &round, 1, n, 0, ctx->cand.p, ctx->out_lb.p, ctx->out_la.p,
+                       all.data(), label);
+    if (rc) return rc;
+    const size_t row = (size_t)label * n;
+    if (lpdf_below && n > 0)
+        HIPCHK(ctx, hipMemcpy(lpdf_below, ctx->out_lb.p + row, n * sizeof(double), hipMemcpyDeviceToHost));
+    if (lpdf_above && n > 0)
+        HIPCHK(ctx, hipMemcpy(lpdf_above, ctx->out_la.p + row, n * sizeof(double), hipMemcpyDeviceToHost));
+    if (out) {
+        *out = all[label];
+        if (n == 0) *out = tpe_label_result{NAN, NAN, NAN, NAN, -1, label, 0};
+    }
+    return TPE_OK;
+}
+
+int tpe_merge_results(const tpe_label_result* parts, int32_t n_parts, int32_t n,
+                      tpe_label_result* out) {
+    if (!parts || !out || n_parts <= 0 || n < 0) return TPE_ERR_ARG;
+    for (int32_t j = 0; j < n; ++j) {
+        tpe_label_result best = parts[j];
+        for (int32_t p = 1; p < n_parts; ++p) {
+            const tpe_label_result& c = parts[(size_t)p * n + j];
+            if (c.index < 0) continue;
+            if (best.index < 0 ||
+                host_better(order_key(c.score), c.index, order_key(best.score), best.index))
+                best = c;
+        }
+        out[j] = best;
+    }
+    return TPE_OK;
+}
+
+int tpe_last_timing(const tpe_ctx* ctx, float* score_ms, float* round_ms) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (score_ms) *score_ms = ctx->score_ms;
+    if (round_ms) *round_ms = ctx->round_ms;
+    return TPE_OK;
+}
+
+int64_t tpe_last_evals(const tpe_ctx* ctx) { return ctx ? ctx->evals : -1; }
+
+int tpe_last_mode_stats(const tpe_ctx* ctx, float* ms, int64_t* evals) {
+    if (!ctx) return TPE_ERR_ARG;
+    for (int m = 0; m < 5; ++m) {
+        if (ms) ms[m] = ctx->mode_ms[m];
+        if (evals) evals[m] = ctx->mode_evals[m];
+    }
+    return TPE_OK;
+}
+
+// ---- single-op entry points: a one-label posterior with both sides equal ----
+
+static int one_label_lpdf(tpe_ctx* ctx, int kind, const double* samples, int64_t n,
+                          const double* w, const double* mu, const double* sg, int32_t k,
+                          int32_t flags, double low, double high, double q, double* out) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (n == 0) return TPE_OK;  // empty samples -> empty result (tpe.py:115-116)
+    if (!samples || !out || !w || !mu || !sg) return ctx->fail(TPE_ERR_ARG, "null pointer");
+    tpe_label_desc d{};
+    d.kind = kind;
+    d.flags = flags;
+    d.low = low;
+    d.high = high;
+    d.q = q;
+    d.n_below = d.n_above = k;
+    // the lpdf never checks low < high (only the samplers do)
+    int rc = set_posterior_impl(ctx, &d, 1, w, mu, sg, k, false);
+    if (rc) return rc;
+    tpe_label_result r;
+    return tpe_score(ctx, 0, samples, n, out, nullptr, &r);
+}
+
+int tpe_gmm1_lpdf(tpe_ctx* ctx, const double* samples, int64_t n, const double* weights,
+                  const double* mus, const double* sigmas, int32_t k, int32_t flags, double low,
+                  double high, double q, double* out) {
+    return one_label_lpdf(ctx, TPE_GMM1, samples, n, weights, mus, sigmas, k, flags, low, high, q, out);
+}
+
+int tpe_lgmm1_lpdf(tpe_ctx* ctx, const double* samples, int64_t n, const double* weights,
+                   const double* mus, const double* sigmas, int32_t k, int32_t flags, double low,
+                   double high, double q, double* out) {
+    return one_label_lpdf(ctx, TPE_LGMM1, samples, n, weights, mus, sigmas, k, flags, low, high, q, out);
+}
+
+int tpe_categorical_lpdf(tpe_ctx* ctx, const int64_t* samples, int64_t n, const double* p,
+                         int32_t upper, double* out) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (n == 0) return TPE_OK;
+    if (!samples || !p || !out || upper <= 0) return ctx->fail(TPE_ERR_ARG, "bad arguments");
+    tpe_label_desc d{};
+    d.kind = TPE_CATEGORICAL;
+    d.n_below = d.n_above = upper;
+    int rc = set_posterior_impl(ctx, &d, 1, p, nullptr, nullptr, upper, false);
+    if (rc) return rc;
+    std::vector<double> c(n);
+    for (int64_t i = 0; i < n; ++i) c[i] = (double)samples[i];
+    tpe_label_result r;
+    return tpe_score(ctx, 0, c.data(), n, out, nullptr, &r);
+}
+
+int tpe_broadcast_best(tpe_ctx* ctx, const double* below, const double* above, int64_t n,
+                       int64_t* best) {
+    if (!ctx || !best) return TPE_ERR_ARG;
+    if (n <= 0) {
+        *best = -1;
+        return TPE_OK;
+    }
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, ctx->out_lb.reserve(n));
+    HIPCHK(ctx, ctx->out_la.reserve(n));
+    const int blocks = (int)std::min<int64_t>((n + kBlock - 1) / kBlock, 1024);
+    HIPCHK(ctx, ctx->partials.reserve(blocks));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->out_lb.p, below, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->out_la.p, above, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_argmax, dim3(blocks), dim3(kBlock), 0, ctx->stream, ctx->out_lb.p,
+                       ctx->out_la.p, n, ctx->partials.p);
+    HIPCHK(ctx, hipGetLastError());
+    std::vector<Partial> parts(blocks);
+    HIPCHK(ctx, hipMemcpyAsync(parts.data(), ctx->partials.p, blocks * sizeof(Partial),
+                               hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    uint64_t bk = 0;
+    int64_t bi = INT64_MAX;
+    for (const Partial& p : parts)
+        if (host_better(p.key, p.idx, bk, bi)) {
+            bk = p.key;
+            bi = p.idx;
+        }
+    *best = bi;
+    return TPE_OK;
+}
+
+static int one_label_sample(tpe_ctx* ctx, int kind, const double* w, const double* mu,
+                            const double* sg, int32_t k, int32_t flags, double low, double high,
+                            double q, uint64_t seed, uint32_t stream, uint32_t round,
+                            int64_t offset, int64_t n, double* out) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (n == 0) return TPE_OK;
+    if (!out) return ctx->fail(TPE_ERR_ARG, "null output");
+    tpe_label_desc d{};
+    d.kind = kind;
+    d.flags = flags;
+    d.low = low;
+    d.high = high;
+    d.q = q;
+    d.n_below = d.n_above = k;
+    int rc = tpe_set_posterior(ctx, &d, 1, w, mu, sg, k);
+    if (rc) return rc;
+    ctx->h_labels[0].stream = (int32_t)stream;
+    HIPCHK(ctx, hipMemcpy(ctx->labels.p, ctx->h_labels.data(), sizeof(DLabel), hipMemcpyHostToDevice));
+    // score the draws against themselves; lpdf_below of the winner is unused,
+    // the samples come back through a sample-only pass below.
+    HIPCHK(ctx, ctx->out_lb.reserve(std::max<int64_t>(n, 1)));
+    HIPCHK(ctx, ctx->out_la.reserve(std::max<int64_t>(n, 1)));
+    HIPCHK(ctx, ctx->cand.reserve(std::max<int64_t>(n, 1)));
+    HIPCHK(ctx, ctx->rounds.reserve(1));
+    HIPCHK(ctx, ctx->errflag.reserve(1));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->rounds.p, &round, sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->errflag.p, 0, sizeof(int32_t), ctx->stream));
+    tpe_launch_sample_only(ctx, ctx->h_labels[0].mode, n, offset, seed, ctx->cand.p);
+    HIPCHK(ctx, hipGetLastError());
+    int32_t errh = 0;
+    HIPCHK(ctx, hipMemcpyAsync(&errh, ctx->errflag.p, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(out, ctx->cand.p, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (errh & 1) return ctx->fail(TPE_ERR_SAMPLE, "truncated sampler: interval [low, high) not reached");
+    return TPE_OK;
+}
+
+int tpe_gmm1_sample(tpe_ctx* ctx, const double* w, const double* mu, const double* sg, int32_t k,
+                    int32_t flags, double low, double high, double q, uint64_t seed,
+                    uint32_t stream, uint32_t round, int64_t offset, int64_t n, double* out) {
+    return one_label_sample(ctx, TPE_GMM1, w, mu, sg, k, flags, low, high, q, seed, stream, round,
+                            offset, n, out);
+}
+
+int tpe_lgmm1_sample(tpe_ctx* ctx, const double* w, const double* mu, const double* sg, int32_t k,
+                     int32_t flags, double low, double high, double q, uint64_t seed,
+                     uint32_t stream, uint32_t round, int64_t offset, int64_t n, double* out) {
+    return one_label_sample(ctx, TPE_LGMM1, w, mu, sg, k, flags, low, high, q, seed, stream, round,
+                            offset, n, out);
+}
+
+int tpe_categorical_sample(tpe_ctx* ctx, const double* p, int32_t upper, uint64_t seed,
+                           uint32_t stream, uint32_t round, int64_t offset, int64_t n,
+                           int64_t* out) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (n == 0) return TPE_OK;
+    std::vector<double> tmp(n);
+    int rc = one_label_sample(ctx, TPE_CATEGORICAL, p, nullptr, nullptr, upper, 0, 0, 0, 0, seed,
+                              stream, round, offset, n, tmp.data());
+    if (rc) return rc;
+    for (int64_t i = 0; i < n; ++i) out[i] = (int64_t)tmp[i];
+    return TPE_OK;
+}
+
+}  // extern "C"
+
+// sample-only kernel (tpe_*_sample): one draw per thread, no scoring
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_sample_only(const DLabel* __restrict__ labels,
+                                                        const SampRec* __restrict__ samp,
+                                                        int64_t n, int64_t offset, uint64_t seed,
+                                                        const uint32_t* __restrict__ rounds,
+                                                        double* __restrict__ out,
+                                                        int32_t* __restrict__ err) {
+    const DLabel L = labels[0];
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    double v;
+    if (!sample_below<MODE>(L, samp + L.samp_off, seed, rounds[0], (uint32_t)(offset + i), v))
+        atomicOr(err, 1);
+    out[i] = v;
+}
+
+void tpe_launch_sample_only(tpe_ctx* ctx, int mode, int64_t n, int64_t offset, uint64_t seed,
+                            double* out) {
+    const int blocks = (int)((n + kBlock - 1) / kBlock);
+#define TPE_SO(M)                                                                             \
+    hipLaunchKernelGGL(k_sample_only<M>, dim3(blocks), dim3(kBlock), 0, ctx->stream,         \
+                       ctx->labels.p, ctx->samp.p, n, offset, seed, ctx->rounds.p, out,       \
+                       ctx->errflag.p)
+    switch (mode) {
+        case DENSE_GMM: TPE_SO(DENSE_GMM); break;
+        case DENSE_LGMM: TPE_SO(DENSE_LGMM); break;
+        case QUANT_GMM: TPE_SO(QUANT_GMM); break;
+        case QUANT_LGMM: TPE_SO(QUANT_LGMM); break;
+        default: TPE_SO(CAT); break;
+    }
+#undef TPE_SO
+}

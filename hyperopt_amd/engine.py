@@ -1,0 +1,244 @@
+"""Host-side mirror of the reference's TPE operator interface, running on the
+gfx950 HIP engine through the C ABI (include/hyperopt_tpe.h).
+
+`GMM1_lpdf`, `LGMM1_lpdf`, `categorical_lpdf`, `broadcast_best`, `GMM1`,
+`LGMM1` and `categorical` keep the argument meaning and the error behaviour of
+the reference functions they replace (hyperopt/tpe.py:56-307, 769-778 and
+hyperopt/pyll/stochastic.py:109-147); `Engine` holds a device context with a
+resident posterior and runs fused suggestion rounds.
+"""
+import ctypes
+import threading
+
+import numpy as np
+
+from . import _lib as L
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def _raise(code, msg):
+    msg = msg.decode() if isinstance(msg, bytes) else msg
+    if code == L.TPE_ERR_VALUE:
+        raise ValueError(msg)
+    if code == L.TPE_ERR_TYPE:
+        raise TypeError(msg)
+    raise EngineError('%s (code %d)' % (msg, code))
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def _f64(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+
+
+RESULT_DTYPE = np.dtype([('value', '<f8'), ('score', '<f8'), ('lpdf_below', '<f8'),
+                         ('lpdf_above', '<f8'), ('index', '<i8'), ('label', '<i4'),
+                         ('status', '<i4')])
+assert RESULT_DTYPE.itemsize == ctypes.sizeof(L.LabelResult)
+
+DESC_DTYPE = np.dtype([('kind', '<i4'), ('flags', '<i4'), ('low', '<f8'), ('high', '<f8'),
+                       ('q', '<f8'), ('below_off', '<i8'), ('above_off', '<i8'),
+                       ('n_below', '<i4'), ('n_above', '<i4')])
+assert DESC_DTYPE.itemsize == ctypes.sizeof(L.LabelDesc)
+
+
+def bounds_flags(low, high, q):
+    f = 0
+    if low is not None:
+        f |= L.TPE_HAS_LOW
+    if high is not None:
+        f |= L.TPE_HAS_HIGH
+    if q is not None:
+        f |= L.TPE_HAS_Q
+    return f
+
+
+class Engine(object):
+    """One device context (one GPU, one HIP stream).  Not thread-safe; the
+    module-level helpers keep one Engine per (thread, device, precision)."""
+
+    def __init__(self, device=0, precision='f64'):
+        self.lib = L.load()
+        self.precision = precision
+        prec = {'f64': L.TPE_F64, 'f32': L.TPE_F32}[precision]
+        h = ctypes.c_void_p()
+        rc = self.lib.tpe_ctx_create(int(device), prec, ctypes.byref(h))
+        if rc != L.TPE_OK:
+            raise EngineError('tpe_ctx_create(device=%d): %s' % (
+                device, self.lib.tpe_last_error(None).decode()))
+        self.h = h
+        self.device = device
+        self.n_labels = 0
+
+    def close(self):
+        if getattr(self, 'h', None):
+            self.lib.tpe_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != L.TPE_OK:
+            _raise(rc, self.lib.tpe_last_error(self.h))
+
+    # -- resident posterior --------------------------------------------------
+    def set_posterior(self, descs, weights, mus, sigmas):
+        """descs: structured array of DESC_DTYPE (one row per label)."""
+        descs = np.ascontiguousarray(descs, dtype=DESC_DTYPE)
+        w, m, s = _f64(weights), _f64(mus), _f64(sigmas)
+        self._check(self.lib.tpe_set_posterior(self.h, _ptr(descs), len(descs), _ptr(w),
+                                               _ptr(m), _ptr(s), len(w)))
+        self.n_labels = len(descs)
+
+    def suggest(self, seed, n_candidates, round=0, cand_offset=0):
+        out = np.zeros(self.n_labels, dtype=RESULT_DTYPE)
+        self._check(self.lib.tpe_suggest(self.h, int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                         int(round) & 0xFFFFFFFF, int(n_candidates),
+                                         int(cand_offset), _ptr(out)))
+        return out
+
+    def suggest_batch(self, seed, rounds, n_candidates, cand_offset=0):
+        rounds = np.ascontiguousarray(np.asarray(rounds, dtype=np.uint32))
+        out = np.zeros(len(rounds) * self.n_labels, dtype=RESULT_DTYPE)
+        self._check(self.lib.tpe_suggest_batch(self.h, int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                               _ptr(rounds), len(rounds), int(n_candidates),
+                                               int(cand_offset), _ptr(out)))
+        return out.reshape(len(rounds), self.n_labels)
+
+    def score(self, label, cand, want_lpdf=True):
+        cand = _f64(cand).ravel()
+        lb = np.empty(len(cand)) if want_lpdf else None
+        la = np.empty(len(cand)) if want_lpdf else None
+        out = np.zeros(1, dtype=RESULT_DTYPE)
+        self._check(self.lib.tpe_score(self.h, int(label), _ptr(cand), len(cand), _ptr(lb),
+                                       _ptr(la), _ptr(out)))
+        return lb, la, out[0]
+
+    def last_timing(self):
+        a, b = ctypes.c_float(), ctypes.c_float()
+        self._check(self.lib.tpe_last_timing(self.h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+    def last_evals(self):
+        return int(self.lib.tpe_last_evals(self.h))
+
+    MODES = ('dense_gmm1', 'dense_lgmm1', 'quant_gmm1', 'quant_lgmm1', 'categorical')
+
+    def last_mode_stats(self):
+        """{family: (device_ms, evals)} of the last round."""
+        ms = np.zeros(5, dtype=np.float32)
+        ev = np.zeros(5, dtype=np.int64)
+        self._check(self.lib.tpe_last_mode_stats(self.h, _ptr(ms), _ptr(ev)))
+        return {m: (float(ms[i]), int(ev[i])) for i, m in enumerate(self.MODES)}
+
+    # -- single reference ops --------------------------------------------------
+    def _mix_lpdf(self, fn, samples, weights, mus, sigmas, low, high, q):
+        samples = np.asarray(samples, dtype=np.float64)
+        weights, mus, sigmas = (np.asarray(a, dtype=np.float64) for a in (weights, mus, sigmas))
+        if samples.size == 0:
+            return np.asarray([])
+        for nm, a in (('weights', weights), ('mus', mus), ('sigmas', sigmas)):
+            if a.ndim != 1:
+                raise TypeError('need vector of %s' % nm, a.shape)
+        assert len(weights) == len(mus) == len(sigmas)
+        x = np.ascontiguousarray(samples.ravel())
+        out = np.empty(x.shape)
+        self._check(fn(self.h, _ptr(x), len(x), _ptr(_f64(weights)), _ptr(_f64(mus)),
+                       _ptr(_f64(sigmas)), len(weights), bounds_flags(low, high, q),
+                       float(low or 0.0), float(high or 0.0), float(q or 0.0), _ptr(out)))
+        return out.reshape(samples.shape)
+
+    def GMM1_lpdf(self, samples, weights, mus, sigmas, low=None, high=None, q=None):
+        return self._mix_lpdf(self.lib.tpe_gmm1_lpdf, samples, weights, mus, sigmas, low, high, q)
+
+    def LGMM1_lpdf(self, samples, weights, mus, sigmas, low=None, high=None, q=None):
+        return self._mix_lpdf(self.lib.tpe_lgmm1_lpdf, samples, weights, mus, sigmas, low, high, q)
+
+    def categorical_lpdf(self, sample, p, upper=None):
+        sample = np.asarray(sample)
+        if sample.size == 0:
+            return np.asarray([])
+        p = _f64(p)
+        s = np.ascontiguousarray(sample.ravel().astype(np.int64))
+        out = np.empty(s.shape)
+        self._check(self.lib.tpe_categorical_lpdf(self.h, _ptr(s), len(s), _ptr(p), len(p),
+                                                  _ptr(out)))
+        return out.reshape(sample.shape)
+
+    def broadcast_best(self, samples, below_llik, above_llik):
+        if len(samples):
+            b, a = _f64(below_llik).ravel(), _f64(above_llik).ravel()
+            if len(samples) != len(b) or len(b) != len(a):
+                raise ValueError()
+            best = ctypes.c_int64()
+            self._check(self.lib.tpe_broadcast_best(self.h, _ptr(b), _ptr(a), len(b),
+                                                    ctypes.byref(best)))
+            return [samples[best.value]] * len(samples)
+        return []
+
+    def _mix_sample(self, fn, weights, mus, sigmas, low, high, q, seed, size, stream, round,
+                    offset):
+        weights, mus, sigmas = (_f64(a) for a in (weights, mus, sigmas))
+        assert len(weights) == len(mus) == len(sigmas)
+        n = int(np.prod(size))
+        out = np.empty(n)
+        self._check(fn(self.h, _ptr(weights), _ptr(mus), _ptr(sigmas), len(weights),
+                       bounds_flags(low, high, q), float(low or 0.0), float(high or 0.0),
+                       float(q or 0.0), int(seed), int(stream), int(round), int(offset), n,
+                       _ptr(out)))
+        return out.reshape(size)
+
+    def GMM1(self, weights, mus, sigmas, low=None, high=None, q=None, seed=0, size=(),
+             stream=0, round=0, offset=0):
+        return self._mix_sample(self.lib.tpe_gmm1_sample, weights, mus, sigmas, low, high, q,
+                                seed, size, stream, round, offset)
+
+    def LGMM1(self, weights, mus, sigmas, low=None, high=None, q=None, seed=0, size=(),
+              stream=0, round=0, offset=0):
+        return self._mix_sample(self.lib.tpe_lgmm1_sample, weights, mus, sigmas, low, high, q,
+                                seed, size, stream, round, offset)
+
+    def categorical(self, p, upper=None, seed=0, size=(), stream=0, round=0, offset=0):
+        p = _f64(p)
+        n = int(np.prod(size)) if size != () else 1
+        out = np.empty(n, dtype=np.int64)
+        self._check(self.lib.tpe_categorical_sample(self.h, _ptr(p), len(p), int(seed),
+                                                    int(stream), int(round), int(offset), n,
+                                                    _ptr(out)))
+        return out.reshape(size if size != () else (1,))
+
+
+def merge_results(parts):
+    """Merge per-shard winners (n_parts x n) with the broadcast_best order."""
+    lib = L.load()
+    parts = np.ascontiguousarray(parts, dtype=RESULT_DTYPE)
+    if parts.ndim == 1:
+        parts = parts[None]
+    out = np.zeros(parts.shape[1], dtype=RESULT_DTYPE)
+    rc = lib.tpe_merge_results(_ptr(parts), parts.shape[0], parts.shape[1], _ptr(out))
+    if rc != L.TPE_OK:
+        raise EngineError('tpe_merge_results failed (%d)' % rc)
+    return out
+
+
+_tls = threading.local()
+
+
+def get_engine(device=0, precision='f64'):
+    """Per-thread cached Engine (contexts are not thread-safe)."""
+    cache = getattr(_tls, 'engines', None)
+    if cache is None:
+        cache = _tls.engines = {}
+    key = (int(device), precision)
+    if key not in cache:
+        cache[key] = Engine(device, precision)
+    return cache[key]

@@ -1,0 +1,187 @@
+"""Per-label posterior descriptors: the host half of the hot path.
+
+Replaces the graph rewrite of `build_posterior` (hyperopt/tpe.py:651-739)
+with a flat table: for every hyperparameter label, the below (l) and above (g)
+Parzen mixtures as rows of a `tpe_label_desc` plus flat weight/mu/sigma
+arrays, uploaded once per suggestion round to the GPU engine.
+
+The arithmetic reproduces the reference bit-for-bit (same numpy calls in the
+same order, including the default, non-stable np.argsort tie order):
+  split         ap_filter_trials              tpe.py:624-648
+  LF weights    linear_forgetting_weights     tpe.py:385-398
+  Parzen        adaptive_parzen_normal        tpe.py:404-477
+  priors        ap_*_sampler registry         tpe.py:493-576
+  categorical   pseudocount posteriors        tpe.py:581-617
+It is vectorised over the history (no per-trial Python loops).
+"""
+import numpy as np
+
+from . import _lib as L
+from .engine import DESC_DTYPE
+
+EPS = 1e-12
+DEFAULT_LF = 25
+
+CONTINUOUS = ('uniform', 'quniform', 'loguniform', 'qloguniform',
+              'normal', 'qnormal', 'lognormal', 'qlognormal')
+CATEGORICAL = ('randint', 'categorical')
+
+
+def split_history(l_idxs, l_vals, gamma, gamma_cap=DEFAULT_LF):
+    """Global loss-rank split (tpe.py:636-645): tids of the n_below best
+    trials and of the rest."""
+    l_idxs = np.asarray(l_idxs)
+    l_vals = np.asarray(l_vals)
+    n_below = min(int(np.ceil(gamma * np.sqrt(len(l_vals)))), gamma_cap)
+    order = np.argsort(l_vals)
+    return l_idxs[order[:n_below]], l_idxs[order[n_below:]]
+
+
+def split_label(o_idxs, o_vals, below_tids, above_tids):
+    """Observations of one label that belong to below / above trials, in
+    their original order (tpe.py:640, :646)."""
+    o_idxs = np.asarray(o_idxs)
+    o_vals = np.asarray(o_vals)
+    if len(o_idxs) == 0:
+        return np.asarray([]), np.asarray([])
+    return (o_vals[np.isin(o_idxs, below_tids)], o_vals[np.isin(o_idxs, above_tids)])
+
+
+def linear_forgetting_weights(n, lf):
+    if n == 0:
+        return np.asarray([])
+    if n < lf:
+        return np.ones(n)
+    return np.concatenate([np.linspace(1.0 / n, 1.0, num=n - lf), np.ones(lf)], axis=0)
+
+
+def adaptive_parzen_normal(mus, prior_weight, prior_mu, prior_sigma, lf=DEFAULT_LF):
+    """(weights, mus, sigmas), sorted by mu, prior inserted (tpe.py:404-477)."""
+    mus = np.asarray(mus, dtype=float)
+    if mus.ndim != 1:
+        raise TypeError('mus must be vector', mus)
+    n = len(mus)
+    order = None
+    if n == 0:
+        srtd = np.asarray([prior_mu], dtype=float)
+        sigma = np.asarray([prior_sigma], dtype=float)
+        pos = 0
+    elif n == 1:
+        pos = 0 if prior_mu < mus[0] else 1
+        srtd = np.asarray([prior_mu, mus[0]] if pos == 0 else [mus[0], prior_mu], dtype=float)
+        sigma = np.asarray([prior_sigma, prior_sigma * .5] if pos == 0
+                           else [prior_sigma * .5, prior_sigma], dtype=float)
+    else:
+        order = np.argsort(mus)
+        sorted_mus = mus[order]
+        pos = int(np.searchsorted(sorted_mus, prior_mu))
+        srtd = np.insert(sorted_mus, pos, prior_mu)
+        sigma = np.empty_like(srtd)
+        gaps = np.diff(srtd)
+        sigma[1:-1] = np.maximum(gaps[:-1], gaps[1:])
+        sigma[0] = gaps[0]
+        sigma[-1] = gaps[-1]
+    if lf and lf < n:
+        lfw = linear_forgetting_weights(n, lf)
+        weights = np.insert(lfw[order], pos, prior_weight)
+    else:
+        weights = np.ones(len(srtd))
+        weights[pos] = prior_weight
+    maxsigma = prior_sigma / 1.0
+    minsigma = prior_sigma / min(100.0, (1.0 + len(srtd)))
+    sigma = np.clip(sigma, minsigma, maxsigma)
+    sigma[pos] = prior_sigma
+    if not (prior_sigma > 0 and np.all(sigma > 0)):
+        raise AssertionError('non-positive sigma in adaptive_parzen_normal')
+    return weights / weights.sum(), srtd, sigma
+
+
+class LabelPosterior(object):
+    """Both posteriors of one label, ready to pack into a descriptor row."""
+    __slots__ = ('label', 'family', 'low', 'high', 'q', 'below', 'above', 'upper')
+
+    def __init__(self, label, family, below, above, low=None, high=None, q=None, upper=None):
+        self.label, self.family = label, family
+        self.below, self.above = below, above   # (w, mu, sigma) or p
+        self.low, self.high, self.q, self.upper = low, high, q, upper
+
+
+def label_posterior(label, kind, args, below, above, prior_weight):
+    """Prior mapping of the adaptive-Parzen sampler registry."""
+    pw = float(prior_weight)
+    if kind in CATEGORICAL:
+        upper = int(args['upper'])
+        ps = []
+        for obs in (below, above):
+            obs = np.asarray(obs)
+            lfw = linear_forgetting_weights(len(obs), DEFAULT_LF)
+            counts = (np.bincount(obs.astype(int), minlength=upper, weights=lfw)
+                      if len(obs) else np.zeros(upper))
+            if kind == 'randint':                              # tpe.py:584-588
+                pseudo = counts + pw
+            else:                                              # tpe.py:605-606
+                pseudo = counts + upper * (pw * np.asarray(args['p'], dtype=float))
+            ps.append(pseudo / np.sum(pseudo))
+        return LabelPosterior(label, 'categorical', ps[0], ps[1], upper=upper)
+    if kind in ('uniform', 'quniform', 'loguniform', 'qloguniform'):
+        low, high = float(args['low']), float(args['high'])
+        prior_mu, prior_sigma = 0.5 * (high + low), 1.0 * (high - low)
+        q = float(args['q']) if kind in ('quniform', 'qloguniform') else None
+        if kind in ('uniform', 'quniform'):
+            tr, fam = (lambda o: o), 'GMM1'
+        elif kind == 'loguniform':
+            tr, fam = np.log, 'LGMM1'
+        else:
+            floor = np.maximum(EPS, np.exp(low))              # tpe.py:536-540
+            tr, fam = (lambda o: np.log(np.maximum(o, floor))), 'LGMM1'
+        mix = [adaptive_parzen_normal(tr(np.asarray(o, dtype=float)), pw, prior_mu, prior_sigma)
+               for o in (below, above)]
+        return LabelPosterior(label, fam, mix[0], mix[1], low=low, high=high, q=q)
+    mu, sigma = float(args['mu']), float(args['sigma'])
+    q = float(args['q']) if kind in ('qnormal', 'qlognormal') else None
+    if kind in ('normal', 'qnormal'):
+        tr, fam = (lambda o: o), 'GMM1'
+    elif kind == 'lognormal':
+        tr, fam = np.log, 'LGMM1'
+    elif kind == 'qlognormal':
+        tr, fam = (lambda o: np.log(np.maximum(o, EPS))), 'LGMM1'
+    else:
+        raise ValueError('unknown distribution %r' % kind)
+    mix = [adaptive_parzen_normal(tr(np.asarray(o, dtype=float)), pw, mu, sigma)
+           for o in (below, above)]
+    return LabelPosterior(label, fam, mix[0], mix[1], q=q)
+
+
+def pack(posts):
+    """Flatten a list of LabelPosterior into (descs, weights, mus, sigmas)."""
+    descs = np.zeros(len(posts), dtype=DESC_DTYPE)
+    ws, ms, ss = [], [], []
+    off = 0
+    for i, p in enumerate(posts):
+        d = descs[i]
+        if p.family == 'categorical':
+            d['kind'] = L.TPE_CATEGORICAL
+            parts = [(p.below, np.zeros_like(p.below), np.zeros_like(p.below)),
+                     (p.above, np.zeros_like(p.above), np.zeros_like(p.above))]
+        else:
+            d['kind'] = L.TPE_GMM1 if p.family == 'GMM1' else L.TPE_LGMM1
+            flags = 0
+            if p.low is not None:
+                flags |= L.TPE_HAS_LOW
+                d['low'] = p.low
+            if p.high is not None:
+                flags |= L.TPE_HAS_HIGH
+                d['high'] = p.high
+            if p.q is not None:
+                flags |= L.TPE_HAS_Q
+                d['q'] = p.q
+            d['flags'] = flags
+            parts = [p.below, p.above]
+        for side, (w, m, s) in zip(('below', 'above'), parts):
+            d[side + '_off'] = off
+            d['n_' + side] = len(w)
+            ws.append(np.asarray(w, dtype=float))
+            ms.append(np.asarray(m, dtype=float))
+            ss.append(np.asarray(s, dtype=float))
+            off += len(w)
+    return descs, np.concatenate(ws), np.concatenate(ms), np.concatenate(ss)

@@ -1,0 +1,147 @@
+"""Synthetic trial histories for the BASELINE.json configurations (SURVEY.md
+§8(d)).  Values come from each hyperparameter's prior, drawn with
+np.random.RandomState(seed); losses are a separable bowl plus noise.  Used by
+bench.py and the tests; no data files, no network."""
+import numpy as np
+
+from . import posterior as P
+
+# config-3 kind cycle: kind = i mod 5
+CYCLE = (('uniform', dict(low=-5.0, high=5.0)),
+         ('loguniform', dict(low=-5.0, high=2.0)),
+         ('quniform', dict(low=0.0, high=100.0, q=1.0)),
+         ('normal', dict(mu=0.0, sigma=3.0)),
+         ('randint', dict(upper=5)))
+
+
+def prior_draw(kind, args, rng, n):
+    if kind == 'uniform':
+        return rng.uniform(args['low'], args['high'], n)
+    if kind == 'quniform':
+        return np.round(rng.uniform(args['low'], args['high'], n) / args['q']) * args['q']
+    if kind == 'loguniform':
+        return np.exp(rng.uniform(args['low'], args['high'], n))
+    if kind == 'qloguniform':
+        return np.round(np.exp(rng.uniform(args['low'], args['high'], n)) / args['q']) * args['q']
+    if kind == 'normal':
+        return rng.normal(args['mu'], args['sigma'], n)
+    if kind == 'qnormal':
+        return np.round(rng.normal(args['mu'], args['sigma'], n) / args['q']) * args['q']
+    if kind == 'lognormal':
+        return np.exp(rng.normal(args['mu'], args['sigma'], n))
+    if kind == 'qlognormal':
+        return np.round(np.exp(rng.normal(args['mu'], args['sigma'], n)) / args['q']) * args['q']
+    if kind in ('randint', 'categorical'):
+        return rng.randint(args['upper'], size=n).astype(float)
+    raise ValueError(kind)
+
+
+def bowl(kind, x):
+    if kind == 'uniform':
+        return (x - 1.0) ** 2
+    if kind == 'loguniform':
+        return (np.log(x) + 1.0) ** 2
+    if kind == 'quniform':
+        return ((x - 30.0) / 10.0) ** 2
+    if kind == 'normal':
+        return (x - 0.5) ** 2
+    if kind == 'randint':
+        return (x != 2).astype(float)
+    return np.zeros_like(x)
+
+
+def hartmann6(x):
+    """Standard Hartmann-6 (config 2 objective)."""
+    alpha = np.array([1.0, 1.2, 3.0, 3.2])
+    A = np.array([[10, 3, 17, 3.5, 1.7, 8], [.05, 10, 17, .1, 8, 14],
+                  [3, 3.5, 1.7, 10, 17, 8], [17, 8, .05, 10, .1, 14]])
+    Pm = 1e-4 * np.array([[1312, 1696, 5569, 124, 8283, 5886], [2329, 4135, 8307, 3736, 1004, 9991],
+                          [2348, 1451, 3522, 2883, 3047, 6650], [4047, 8828, 8732, 5743, 1091, 381]])
+    inner = ((x[:, None, :] - Pm[None]) ** 2 * A[None]).sum(-1)
+    return -(alpha[None] * np.exp(-inner)).sum(-1)
+
+
+class History(object):
+    """Flat history: labels, per-label active (tids, vals), per-trial losses."""
+
+    def __init__(self, labels, tids, losses, obs):
+        self.labels = labels          # [(name, kind, args)]
+        self.tids = tids              # (N,) int64, sorted
+        self.losses = losses          # (N,) float64
+        self.obs = obs                # name -> (idxs, vals)
+
+    def posteriors(self, gamma=0.25, prior_weight=1.0):
+        bt, at = P.split_history(self.tids, self.losses, gamma)
+        posts = []
+        for name, kind, args in self.labels:
+            oi, ov = self.obs[name]
+            b, a = P.split_label(oi, ov, bt, at)
+            posts.append(P.label_posterior(name, kind, args, b, a, prior_weight))
+        return posts
+
+
+def mixed_space(n_labels):
+    return [('x%03d' % i,) + CYCLE[i % 5] for i in range(n_labels)]
+
+
+def mixed_history(n_labels=32, n_trials=10000, seed=0):
+    """Configs 3 and 5: kind = i mod 5; loss = sum of bowls + 0.1 N(0,1)."""
+    rng = np.random.RandomState(seed)
+    labels = mixed_space(n_labels)
+    tids = np.arange(n_trials, dtype=np.int64)
+    loss = 0.1 * rng.normal(size=n_trials)
+    obs = {}
+    for name, kind, args in labels:
+        v = prior_draw(kind, args, rng, n_trials)
+        loss = loss + bowl(kind, v)
+        obs[name] = (tids, v)
+    return History(labels, tids, loss, obs)
+
+
+def hartmann_history(n_trials=2000, seed=0):
+    """Config 2: Hartmann-6 over hp.uniform('x{i}', 0, 1)."""
+    rng = np.random.RandomState(seed)
+    x = rng.uniform(0, 1, size=(n_trials, 6))
+    tids = np.arange(n_trials, dtype=np.int64)
+    labels = [('x%d' % i, 'uniform', dict(low=0.0, high=1.0)) for i in range(6)]
+    obs = {labels[i][0]: (tids, x[:, i]) for i in range(6)}
+    return History(labels, tids, hartmann6(x), obs)
+
+
+def conditional_history(n_trials=5000, seed=0):
+    """Config 4: hp.choice('clf', [svm{...}, rf{...}, gbm{...}]) -- children are
+    active only in the trials that chose their branch."""
+    rng = np.random.RandomState(seed)
+    ln = np.log
+    branches = [
+        [('svm_C', 'loguniform', dict(low=-5.0, high=5.0)),
+         ('svm_gamma', 'loguniform', dict(low=-8.0, high=2.0)),
+         ('svm_kernel', 'randint', dict(upper=3)),
+         ('svm_degree', 'quniform', dict(low=2.0, high=5.0, q=1.0))],
+        [('rf_n', 'qloguniform', dict(low=float(ln(10)), high=float(ln(1000)), q=1.0)),
+         ('rf_depth', 'quniform', dict(low=1.0, high=30.0, q=1.0)),
+         ('rf_max_feat', 'uniform', dict(low=0.1, high=1.0)),
+         ('rf_crit', 'randint', dict(upper=2))],
+        [('gbm_lr', 'loguniform', dict(low=float(ln(1e-3)), high=0.0)),
+         ('gbm_n', 'qloguniform', dict(low=float(ln(10)), high=float(ln(1000)), q=1.0)),
+         ('gbm_subsample', 'uniform', dict(low=0.5, high=1.0)),
+         ('gbm_depth', 'quniform', dict(low=1.0, high=10.0, q=1.0))],
+    ]
+    labels = [('clf', 'randint', dict(upper=3))] + [l for b in branches for l in b]
+    tids = np.arange(n_trials, dtype=np.int64)
+    clf = rng.randint(3, size=n_trials)
+    loss = 0.1 * rng.normal(size=n_trials) + 0.3 * clf
+    obs = {'clf': (tids, clf.astype(float))}
+    for bi, br in enumerate(branches):
+        act = tids[clf == bi]
+        for name, kind, args in br:
+            v = prior_draw(kind, args, rng, len(act))
+            if kind in ('uniform', 'loguniform', 'quniform', 'qloguniform'):
+                lv = np.log(v) if 'log' in kind else v
+                lo, hi = args['low'], args['high']
+                contrib = ((lv - lo) / (hi - lo) - 0.3) ** 2
+            else:
+                contrib = (v != 1).astype(float) * 0.2
+            loss[clf == bi] += contrib
+            obs[name] = (act, v)
+    return History(labels, tids, loss, obs)

@@ -1,0 +1,192 @@
+/*
+ * hyperopt_tpe.h -- C ABI of the MI355X (gfx950) TPE suggestion engine.
+ *
+ * Plain C, plain pointers and sizes; no torch or HIP types cross this
+ * boundary.  Every entry point cites the reference function it replaces
+ * (mvanveen/hyperopt, paths relative to the repository root).  The reference
+ * is pure Python, so its "FFI" is the pyll operator registry: `scope.define`
+ * (hyperopt/pyll/base.py:132-138) registers each numeric op by name and
+ * `build_posterior` (hyperopt/tpe.py:651-739) wires them per hyperparameter.
+ * The ops below are those registry entries, plus one fused entry point
+ * (`tpe_suggest`) that runs the whole per-label chain on the GPU.
+ *
+ * All calls are synchronous with respect to the host: on return, outputs are
+ * in the caller's buffers.  A context is not thread-safe; use one per thread.
+ * Return value: TPE_OK (0) or a negative TPE_ERR_*; the message is available
+ * from tpe_last_error(ctx) (or tpe_last_error(NULL) for tpe_ctx_create).
+ */
+#ifndef HYPEROPT_TPE_H
+#define HYPEROPT_TPE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TPE_ABI_VERSION 1
+
+/* error codes; the Python layer maps them to the reference's exception types */
+#define TPE_OK 0
+#define TPE_ERR_VALUE (-1)   /* ValueError (e.g. 'low >= high', tpe.py:86-87)      */
+#define TPE_ERR_TYPE (-2)    /* TypeError (e.g. non-vector params, tpe.py:117-122)  */
+#define TPE_ERR_ARG (-3)     /* bad pointer / size / state                          */
+#define TPE_ERR_HIP (-4)     /* HIP runtime failure                                 */
+#define TPE_ERR_SAMPLE (-5)  /* truncated sampler could not reach the interval     */
+
+/* arithmetic of the dense (unquantized) lpdf paths; quantized and sampling
+ * paths always run in fp64 */
+#define TPE_F64 0
+#define TPE_F32 1
+
+/* posterior families (the `<sampler>` names of tpe.py:712) */
+#define TPE_GMM1 0         /* truncated Gaussian mixture            tpe.py:68-172  */
+#define TPE_LGMM1 1        /* log-space Gaussian mixture            tpe.py:222-307 */
+#define TPE_CATEGORICAL 2  /* categorical over 0..upper-1           tpe.py:56-63   */
+
+/* presence flags for the optional `low`, `high`, `q` arguments (None in Python) */
+#define TPE_HAS_LOW 1
+#define TPE_HAS_HIGH 2
+#define TPE_HAS_Q 4
+
+typedef struct tpe_ctx tpe_ctx;
+
+/* One hyperparameter's pair of posteriors (the below/`l` and above/`g`
+ * mixtures that build_posterior makes per label, tpe.py:684-692).
+ * Mixture components live in flat arrays passed to tpe_set_posterior:
+ *   GMM1/LGMM1: weights[off+k], mus[off+k], sigmas[off+k], k < n (as returned
+ *               by adaptive_parzen_normal, tpe.py:404-477);
+ *   CATEGORICAL: weights[off+k] = p[k] (pseudocount posterior,
+ *               tpe.py:581-617); n == upper; mus/sigmas unused.
+ * low/high/q are the GMM1/LGMM1 keyword arguments; for LGMM1 low/high are in
+ * log space exactly as in the reference call LGMM1(..., low, high, q). */
+typedef struct {
+    int32_t kind;       /* TPE_GMM1 / TPE_LGMM1 / TPE_CATEGORICAL */
+    int32_t flags;      /* TPE_HAS_LOW | TPE_HAS_HIGH | TPE_HAS_Q */
+    double low;
+    double high;
+    double q;
+    int64_t below_off;
+    int64_t above_off;
+    int32_t n_below;
+    int32_t n_above;
+} tpe_label_desc;       /* 56 bytes */
+
+/* Winner of one label's candidate set (broadcast_best, tpe.py:769-778). */
+typedef struct {
+    double value;       /* samples[best] (categorical: the integer index as double) */
+    double score;       /* lpdf_below[best] - lpdf_above[best]                      */
+    double lpdf_below;
+    double lpdf_above;
+    int64_t index;      /* GLOBAL candidate index of the winner (-1: no candidates) */
+    int32_t label;
+    int32_t status;     /* 0 ok                                                     */
+} tpe_label_result;     /* 48 bytes */
+
+int tpe_abi_version(void);
+
+/* device: HIP ordinal; precision: TPE_F64 or TPE_F32 */
+int tpe_ctx_create(int device, int precision, tpe_ctx **out);
+void tpe_ctx_destroy(tpe_ctx *ctx);
+const char *tpe_last_error(const tpe_ctx *ctx);
+
+/* ---- reference operators, 1:1 (host buffers in and out) ------------------ */
+
+/* GMM1_lpdf(samples, weights, mus, sigmas, low, high, q)   tpe.py:110-172 */
+int tpe_gmm1_lpdf(tpe_ctx *ctx, const double *samples, int64_t n,
+                  const double *weights, const double *mus, const double *sigmas,
+                  int32_t k, int32_t flags, double low, double high, double q,
+                  double *out);
+
+/* LGMM1_lpdf(samples, weights, mus, sigmas, low, high, q)  tpe.py:265-307 */
+int tpe_lgmm1_lpdf(tpe_ctx *ctx, const double *samples, int64_t n,
+                   const double *weights, const double *mus, const double *sigmas,
+                   int32_t k, int32_t flags, double low, double high, double q,
+                   double *out);
+
+/* categorical_lpdf(sample, p, upper)                        tpe.py:56-63 */
+int tpe_categorical_lpdf(tpe_ctx *ctx, const int64_t *samples, int64_t n,
+                         const double *p, int32_t upper, double *out);
+
+/* np.argmax(below_llik - above_llik) of broadcast_best      tpe.py:769-778
+ * (first NaN wins, NaN above +inf, lowest index wins ties) */
+int tpe_broadcast_best(tpe_ctx *ctx, const double *below, const double *above,
+                       int64_t n, int64_t *best);
+
+/* GMM1(weights, mus, sigmas, low, high, q, rng, size)      tpe.py:68-99
+ * Same distribution as the reference (component ~ weights, Gaussian draw,
+ * accept iff low <= draw < high, round(x/q)*q); the random stream is
+ * Philox4x32-10 keyed by `seed`, counter = (offset + i, attempt, stream,
+ * round), so draw i is the same whatever the batching or GPU count. */
+int tpe_gmm1_sample(tpe_ctx *ctx, const double *weights, const double *mus,
+                    const double *sigmas, int32_t k, int32_t flags, double low,
+                    double high, double q, uint64_t seed, uint32_t stream,
+                    uint32_t round, int64_t offset, int64_t n, double *out);
+
+/* LGMM1(weights, mus, sigmas, low, high, q, rng, size)     tpe.py:222-256 */
+int tpe_lgmm1_sample(tpe_ctx *ctx, const double *weights, const double *mus,
+                     const double *sigmas, int32_t k, int32_t flags, double low,
+                     double high, double q, uint64_t seed, uint32_t stream,
+                     uint32_t round, int64_t offset, int64_t n, double *out);
+
+/* categorical(p, upper, rng, size)            hyperopt/pyll/stochastic.py:109-147 */
+int tpe_categorical_sample(tpe_ctx *ctx, const double *p, int32_t upper,
+                           uint64_t seed, uint32_t stream, uint32_t round,
+                           int64_t offset, int64_t n, int64_t *out);
+
+/* ---- resident posterior + fused suggestion round ------------------------- */
+
+/* Upload the per-label posteriors (replaces the graph that
+ * build_posterior/tpe_transform rebuild on every call, tpe.py:651-739,
+ * 794-820).  Arrays are copied; the device copy stays resident until the
+ * next call or tpe_ctx_destroy. */
+int tpe_set_posterior(tpe_ctx *ctx, const tpe_label_desc *labels, int32_t n_labels,
+                      const double *weights, const double *mus, const double *sigmas,
+                      int64_t n_components);
+
+/* One suggestion round over every resident label: sample n_candidates per
+ * label from the below posterior (global candidate indices
+ * cand_offset .. cand_offset+n_candidates-1), score them under both
+ * posteriors and keep the best (the GMM1 -> *_lpdf x2 -> broadcast_best
+ * chain of tpe.py:686-724, rec_eval'd per label at tpe.py:900).
+ * out[label] receives the winner.  `round` separates independent rounds
+ * (e.g. new_id) under one seed. */
+int tpe_suggest(tpe_ctx *ctx, uint64_t seed, uint32_t round, int64_t n_candidates,
+                int64_t cand_offset, tpe_label_result *out);
+
+/* Batched independent rounds (several new_ids at once): round j uses
+ * rounds[j]; out has n_rounds * n_labels entries, round-major. */
+int tpe_suggest_batch(tpe_ctx *ctx, uint64_t seed, const uint32_t *rounds,
+                      int32_t n_rounds, int64_t n_candidates, int64_t cand_offset,
+                      tpe_label_result *out);
+
+/* Score a caller-supplied candidate set for one resident label (the parity
+ * entry point: identical candidates in, both lpdf vectors and the winner
+ * out).  lpdf_below / lpdf_above may be NULL. */
+int tpe_score(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
+              double *lpdf_below, double *lpdf_above, tpe_label_result *out);
+
+/* Merge per-shard winners (e.g. gathered from every GPU over RCCL) with the
+ * broadcast_best comparator: larger score, NaN greatest, then lowest global
+ * index.  parts: n_parts blocks of n results each.  Host-only, no ctx. */
+int tpe_merge_results(const tpe_label_result *parts, int32_t n_parts, int32_t n,
+                      tpe_label_result *out);
+
+/* Device time (ms, HIP events on the context stream) of the last fused round:
+ * scoring kernels only, and the whole round including the reduction. */
+int tpe_last_timing(const tpe_ctx *ctx, float *score_ms, float *round_ms);
+
+/* Number of (candidate, component) lpdf evaluations the last round executed,
+ * counted over both mixtures (categorical: 2 per candidate). */
+int64_t tpe_last_evals(const tpe_ctx *ctx);
+
+/* Per kernel family of the last round (index: 0 dense GMM1, 1 dense LGMM1,
+ * 2 quantized GMM1, 3 quantized LGMM1, 4 categorical): device ms of that
+ * family's launch and the evaluations it executed.  Arrays of 5. */
+int tpe_last_mode_stats(const tpe_ctx *ctx, float *ms, int64_t *evals);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HYPEROPT_TPE_H */

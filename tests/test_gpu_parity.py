@@ -1,0 +1,215 @@
+"""GPU parity of the HIP engine against the reference's golden vectors and the
+CPU oracle, through the C ABI.  Requires a real MI355X (`-m gpu`)."""
+import numpy as np
+import pytest
+
+from oracle import tpe_oracle as O
+from tests import golden_io
+from tests.helpers import assert_lpdf_close, desc_from_case, is_quantized, stack_cases
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def eng():
+    from hyperopt_amd.engine import Engine
+    e = Engine(0, 'f64')
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope='module')
+def eng32():
+    from hyperopt_amd.engine import Engine
+    e = Engine(0, 'f32')
+    yield e
+    e.close()
+
+
+def _all_cases():
+    for fx in ('labels_small.npz', 'labels_medium.npz'):
+        for meta, rec in golden_io.cases(fx):
+            yield fx, meta, rec
+
+
+@pytest.mark.parametrize('fixture', ['labels_small.npz', 'labels_medium.npz'])
+def test_score_matches_reference_golden(eng, fixture):
+    """Identical candidate sets: both lpdf vectors within the fp64 bar and the
+    broadcast_best winner bit-identical to the reference's."""
+    for meta, rec in golden_io.cases(fixture):
+        d, w, m, s = desc_from_case(meta, rec)
+        eng.set_posterior(d, w, m, s)
+        cand = rec['samples']
+        lb, la, res = eng.score(0, cand)
+        q = is_quantized(meta)
+        assert_lpdf_close(lb, rec['lpdf_below'], quantized=q)
+        assert_lpdf_close(la, rec['lpdf_above'], quantized=q)
+        assert int(res['index']) == int(rec['best_idx']), (meta['kind'], meta['n_hist'])
+        assert res['value'] == cand[int(rec['best_idx'])]
+
+
+def test_reference_op_entry_points(eng):
+    """tpe_gmm1_lpdf / tpe_lgmm1_lpdf on the reference's edge inputs (far
+    tails, quantized cancellation to -inf, x=0 for LGMM1 -> NaN)."""
+    z, meta = golden_io.load('lpdf_edges.npz')
+    w, mu, sg = (np.asarray(meta[k]) for k in ('w', 'mu', 'sigma'))
+    for cid, call in enumerate(meta['calls']):
+        x = z['e%03d/x' % cid]
+        f = eng.GMM1_lpdf if call['fn'] == 'GMM1_lpdf' else eng.LGMM1_lpdf
+        got = f(x, w, mu, sg, **call['kwargs'])
+        assert_lpdf_close(got, z['e%03d/out' % cid], quantized='q' in call['kwargs'])
+
+
+def test_broadcast_best_semantics(eng):
+    z, meta = golden_io.load('lpdf_edges.npz')
+    for i in range(meta['n_bb']):
+        s = z['bb%02d/score' % i]
+        samples = list(range(len(s)))
+        got = eng.broadcast_best(samples, s, np.zeros_like(s))
+        assert got == [int(z['bb%02d/best' % i])] * len(s)
+    assert eng.broadcast_best([], [], []) == []
+    with pytest.raises(ValueError):
+        eng.broadcast_best([1, 2], [0.0], [0.0])
+
+
+def test_categorical_lpdf(eng):
+    p = np.array([0.1, 0.2, 0.7])
+    s = np.array([0, 2, 1, 2])
+    assert np.array_equal(eng.categorical_lpdf(s, p), np.log(p[s]))
+    assert len(eng.categorical_lpdf(np.array([], dtype=int), p)) == 0
+
+
+def test_fused_round_matches_oracle(eng):
+    """Full round (in-kernel Philox sampling -> both lpdfs -> maxloc) over a
+    multi-label posterior; the candidates are re-drawn through the sampler
+    entry point with the same (seed, stream, round) and scored by the CPU
+    oracle, whose argmax must equal the engine's."""
+    pairs = [(m, r) for fx, m, r in _all_cases()
+             if m['n_hist'] in (26, 300) and m['variant'] == 'plain']
+    d, w, m, s = stack_cases(pairs)
+    eng.set_posterior(d, w, m, s)
+    C, seed, rnd = 3000, 12345, 7
+    res = eng.suggest(seed, C, round=rnd)
+    for li, (meta, rec) in enumerate(pairs):
+        kw = meta['lpdf_kwargs']
+        if meta['sampler'] == 'categorical':
+            cand = eng.categorical(rec['p_below'], seed=seed, size=(C,), stream=li, round=rnd)
+            lb = O.categorical_lpdf(cand, rec['p_below'])
+            la = O.categorical_lpdf(cand, rec['p_above'])
+        else:
+            samp = eng.GMM1 if meta['sampler'] == 'GMM1' else eng.LGMM1
+            cand = samp(rec['w_b'], rec['mu_b'], rec['sigma_b'], seed=seed, size=(C,),
+                        stream=li, round=rnd, **kw)
+            f = O.gmm1_lpdf if meta['sampler'] == 'GMM1' else O.lgmm1_lpdf
+            lb = f(cand, rec['w_b'], rec['mu_b'], rec['sigma_b'], **kw)
+            la = f(cand, rec['w_a'], rec['mu_a'], rec['sigma_a'], **kw)
+        best = O.broadcast_best_index(lb, la)
+        assert int(res[li]['index']) == best, (li, meta['kind'])
+        assert res[li]['value'] == cand[best]
+        assert_lpdf_close([res[li]['lpdf_below']], [lb[best]], quantized=is_quantized(meta))
+
+
+def test_shard_invariance(eng):
+    """Candidate i is the same draw whatever the sharding: splitting the set
+    over 'GPUs' via cand_offset and merging gives the single-shard winner."""
+    from hyperopt_amd.engine import merge_results
+    pairs = [(m, r) for fx, m, r in _all_cases() if m['variant'] == 'medium'][:4]
+    d, w, m, s = stack_cases(pairs)
+    eng.set_posterior(d, w, m, s)
+    C = 10000
+    full = eng.suggest(99, C, round=3)
+    parts = np.stack([eng.suggest(99, C // 4, round=3, cand_offset=k * (C // 4))
+                      for k in range(4)])
+    merged = merge_results(parts)
+    assert np.array_equal(merged['index'], full['index'])
+    assert np.array_equal(merged['value'], full['value'])
+    assert np.array_equal(merged['score'], full['score'])
+
+
+def test_batch_rounds_equal_single_rounds(eng):
+    pairs = [(m, r) for fx, m, r in _all_cases() if m['variant'] == 'medium'][:3]
+    d, w, m, s = stack_cases(pairs)
+    eng.set_posterior(d, w, m, s)
+    rounds = [5, 9, 11]
+    batch = eng.suggest_batch(4, rounds, 2048)
+    for j, r in enumerate(rounds):
+        single = eng.suggest(4, 2048, round=r)
+        assert np.array_equal(batch[j]['index'], single['index'])
+        assert np.array_equal(batch[j]['value'], single['value'])
+
+
+# -- sampler distributions: the reference's own statistical checks -----------
+# (test_tpe.py:203-528: histogram of draws vs exp(lpdf); same thresholds)
+
+def _hist_check(samples, lpdf_fn, per_bin, centers=False):
+    samples = np.sort(samples)
+    edges = samples[::per_bin]
+    xs = .5 * edges[:-1] + .5 * edges[1:] if centers else edges[:-1]
+    pdf = np.exp(lpdf_fn(xs))
+    dx = edges[1:] - edges[:-1]
+    y = 1 / dx / len(dx)
+    err = (pdf - y) ** 2
+    assert np.max(err) < .1 and np.mean(err) < .01 and np.median(err) < .01
+
+
+W4, MU4, S4 = [.1, .3, .4, .2], [1.0, 2.0, 3.0, 4.0], [.1, .4, .8, 2.0]
+
+
+@pytest.mark.parametrize('bounds', [{}, dict(low=2.5, high=3.5)])
+def test_gmm1_sampler_distribution(eng, bounds):
+    x = eng.GMM1(W4, MU4, S4, seed=234, size=(10001,), **bounds)
+    if bounds:
+        assert x.min() >= bounds['low'] and x.max() < bounds['high']
+    _hist_check(x, lambda v: O.gmm1_lpdf(v, W4, MU4, S4, **bounds), 500)
+
+
+@pytest.mark.parametrize('kw', [dict(q=1), dict(q=2), dict(q=0.5), dict(q=1, low=2, high=4),
+                                dict(q=2, low=1, high=4.1)])
+def test_qgmm1_sampler_distribution(eng, kw):
+    n = 1001
+    x = eng.GMM1(W4, MU4, S4, seed=234, size=(n,), **kw) / kw['q']
+    assert np.all(x == x.astype(int))
+    lo = int(x.min())
+    counts = np.bincount(x.astype(int) - lo)
+    xc = np.arange(lo, int(x.max()) + 1) * kw['q']
+    prob = np.exp(O.gmm1_lpdf(xc, W4, MU4, S4, **kw))
+    err = (prob - counts / float(n)) ** 2
+    assert np.max(err) < .1 and np.mean(err) < .01 and np.median(err) < .01
+
+
+@pytest.mark.parametrize('bounds', [{}, dict(low=2, high=4)])
+def test_lgmm1_sampler_distribution(eng, bounds):
+    mus = [-2.0, 1.0, 0.0, 3.0]
+    x = eng.LGMM1(W4, mus, S4, seed=234, size=(10001,), **bounds)
+    _hist_check(x, lambda v: O.lgmm1_lpdf(v, W4, mus, S4, **bounds), 200, centers=True)
+
+
+def test_categorical_sampler_distribution(eng):
+    p = np.array([0.1, 0.2, 0.3, 0.4])
+    x = eng.categorical(p, seed=5, size=(200000,))
+    freq = np.bincount(x, minlength=4) / len(x)
+    assert np.max(np.abs(freq - p)) < 0.005
+
+
+def test_sampler_errors(eng):
+    with pytest.raises(ValueError):
+        eng.GMM1([1.0], [0.0], [1.0], low=2.0, high=1.0, seed=0, size=(4,))
+    with pytest.raises(TypeError):
+        eng.GMM1_lpdf([1.0], [[1.0]], [0.0], [1.0])
+
+
+# -- fp32 fast path: 1e-4 relative on the dense lpdfs, argmax agreement -------
+
+def test_fp32_dense_path(eng32):
+    agree = total = 0
+    for fx, meta, rec in _all_cases():
+        if is_quantized(meta) or meta['sampler'] == 'categorical' or meta['n_hist'] < 26:
+            continue
+        d, w, m, s = desc_from_case(meta, rec)
+        eng32.set_posterior(d, w, m, s)
+        lb, la, res = eng32.score(0, rec['samples'])
+        assert_lpdf_close(lb, rec['lpdf_below'], rtol=1e-4, atol=1e-4)
+        assert_lpdf_close(la, rec['lpdf_above'], rtol=1e-4, atol=1e-4)
+        total += 1
+        agree += int(res['index']) == int(rec['best_idx'])
+    assert total > 0 and agree >= 0.8 * total
