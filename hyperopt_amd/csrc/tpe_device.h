@@ -83,16 +83,17 @@ __device__ __forceinline__ int cdf_search(const SampRec* __restrict__ s, int n, 
     return lo;
 }
 
-// Draw one sample of the below posterior for global candidate g.
+// Draw one sample of the below posterior for global candidate g, BEFORE
+// quantization (LGMM1: after the exp).
 // GMM1 / LGMM1 (tpe.py:68-99 / 222-256): component ~ weights, x ~ N(mu, sigma),
 // bounded: retry until low <= x < high (re-selecting the component, exactly as
-// the reference loop does), LGMM1 then exp(x); finally round(x / q) * q.
+// the reference loop does), LGMM1 then exp(x).
 // categorical (stochastic.py:109-147): index ~ p.
 // Returns false if the truncation interval was not reached within the cap.
 template <int MODE>
-__device__ __forceinline__ bool sample_below(const DLabel& L, const SampRec* __restrict__ s,
-                                             uint64_t seed, uint32_t round, uint32_t g,
-                                             double& out) {
+__device__ __forceinline__ bool sample_raw(const DLabel& L, const SampRec* __restrict__ s,
+                                           uint64_t seed, uint32_t round, uint32_t g,
+                                           double& out) {
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     if constexpr (MODE == CAT) {
         const U4 r = philox4x32_10(U4{g, 0u, (uint32_t)L.stream, round}, k0, k1);
@@ -108,15 +109,25 @@ __device__ __forceinline__ bool sample_below(const DLabel& L, const SampRec* __r
             const double nrm = rad * cospi(2.0 * ((double)r.w * 0x1.0p-32));
             const double draw = s[k].mu + s[k].sigma * nrm;
             if (!bounded || (L.low <= draw && draw < L.high)) {
-                double v = (MODE == DENSE_LGMM || MODE == QUANT_LGMM) ? exp(draw) : draw;
-                if (L.flags & 4) v = rint(v / L.q) * L.q;
-                out = v;
+                out = (MODE == DENSE_LGMM || MODE == QUANT_LGMM) ? exp(draw) : draw;
                 return true;
             }
         }
         out = __builtin_nan("");
         return false;
     }
+}
+
+// np.round(x / q) * q (round half to even), tpe.py:99 / :255
+__device__ __forceinline__ double quantize(double v, double q) { return rint(v / q) * q; }
+
+template <int MODE>
+__device__ __forceinline__ bool sample_below(const DLabel& L, const SampRec* __restrict__ s,
+                                             uint64_t seed, uint32_t round, uint32_t g,
+                                             double& out) {
+    const bool ok = sample_raw<MODE>(L, s, seed, round, g, out);
+    if (MODE != CAT && (L.flags & 4)) out = quantize(out, L.q);
+    return ok;
 }
 
 // numpy minimum/maximum: NaN propagates.
@@ -232,6 +243,59 @@ __device__ __forceinline__ double quant_lpdf(const Comp<double>* __restrict__ c,
         prob += inc;
     }
     return log(prob) - logpacc;
+}
+
+// Integration interval of a quantized candidate x (tpe.py:154-161 / 292-300);
+// for LGMM1 the lognormal_cdf log(max(v, EPS)) is applied here, once per
+// candidate, so the per-component loop is identical for both families.
+template <int MODE>
+__device__ __forceinline__ void quant_bounds(const DLabel& L, double x, double& ub, double& lb,
+                                             bool& negative) {
+    const double half = L.q / 2.0;
+    ub = x + half;
+    lb = x - half;
+    negative = false;
+    if constexpr (MODE == QUANT_GMM) {
+        if (L.flags & 2) ub = np_min(ub, L.high);
+        if (L.flags & 1) lb = np_max(lb, L.low);
+    } else {
+        if (L.flags & 2) ub = np_min(ub, L.exp_high);
+        if (L.flags & 1) lb = np_max(lb, L.exp_low);
+        lb = np_max(0.0, lb);
+        negative = ub < 0.0;  // tpe.py:187-188 raises
+        ub = log(np_max(ub, kEps));
+        lb = log(np_max(lb, kEps));
+    }
+}
+
+// Lane-strided share of prob = sum_k [w Phi(ub) - w Phi(lb)] (components
+// k = lane, lane+64, ...); the wave sums the 64 shares afterwards.
+template <bool LOG>
+__device__ __forceinline__ double quant_share(const Comp<double>* __restrict__ c, int n, double ub,
+                                              double lb, int lane) {
+#pragma clang fp contract(off)
+    double prob = 0.0;
+    for (int k = lane; k < n; k += 64) {
+        const double mu = c[k].mu, a = c[k].a, w = c[k].w;
+        double pu, pl;
+        if (LOG) {
+            pu = 0.5 + 0.5 * erf((ub - mu) * a);
+            pl = 0.5 + 0.5 * erf((lb - mu) * a);
+        } else {
+            pu = 0.5 * (1.0 + erf((ub - mu) * a));
+            pl = 0.5 * (1.0 + erf((lb - mu) * a));
+        }
+        double inc = w * pu;
+        inc -= w * pl;
+        prob += inc;
+    }
+    return prob;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
 }
 
 // -------------------------------------------------------- broadcast_best ----

@@ -2,14 +2,22 @@
 // TPE suggestion hot path (mvanveen/hyperopt hyperopt/tpe.py:651-916).
 //
 // Layout in HBM (resident per context, replaced by tpe_set_posterior):
-//   labels_  : DLabel[L]                  per-label mode, bounds, shifts, offsets
-//   comps64_ : Comp<double>[n_records]    below then above mixture of each label
-//   comps32_ : Comp<float>[n_records]     fp32 copy of the dense records (TPE_F32)
-//   samp_    : SampRec[sum K_b]           cumulative weights + mu/sigma of l(x)
-//   partials_: Partial[rounds][L][tiles]  per-workgroup winners
-//   results_ : tpe_label_result[rounds][L]
-// Kernels: k_round<T, MODE, SAMPLE> (sample -> lpdf below/above -> block
-// maxloc, one launch per mode group), k_reduce (per label winner).
+//   labels   : DLabel[L]                  per-label mode, bounds, shifts, offsets
+//   comps64  : Comp<double>[records]      below then above mixture of each label
+//   comps32  : Comp<float>[records]       fp32 copy of the dense records (TPE_F32)
+//   samp     : SampRec[sum K_b]           cumulative weights + mu/sigma of l(x)
+// Per round:
+//   partials : Partial[rounds][L][tiles]  per-workgroup winners
+//   results  : tpe_label_result[rounds][L]
+//   qj       : int64[rounds][Lq][C]       grid index of every quantized candidate
+//   qtab     : double2[sum G]             lpdf pair per distinct grid value
+// Kernels
+//   k_round<T, MODE, SAMPLE>  sample -> lpdf under l and g -> block maxloc
+//                             (dense families, categorical, supplied candidates)
+//   k_qsample<MODE>           quantized families: draw, store grid index j, min/max
+//   k_qtable<MODE>            one wave per distinct grid value: lpdf pair
+//   k_qscan<MODE>             per candidate: table lookup -> block maxloc
+//   k_reduce                  per (round, label) winner over the partials
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -29,8 +37,70 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kR = 4;                 // candidates per thread
 constexpr int kTile = kBlock * kR;    // candidates per workgroup
+constexpr int kNumModes = 5;
 
 thread_local std::string g_create_error;
+
+// Per (round, quantized label) grid window decided on the host after k_qsample.
+struct QInfo {
+    int64_t jmin;
+    int64_t G;        // table slots; 0 = evaluate every candidate directly
+    int64_t tab_off;
+    int64_t pad;
+};
+
+// ---------------------------------------------------------- block maxloc ----
+// broadcast_best (tpe.py:769-778) over one workgroup's candidates: per-thread
+// best of its R, wave64 butterfly, then the 4 waves through LDS.
+__device__ __forceinline__ void block_maxloc(uint64_t bk, int64_t bi, double bv, double bl,
+                                             double ba, Partial* __restrict__ dst) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t ok = __shfl_xor(bk, off);
+        const int64_t oi = __shfl_xor(bi, off);
+        const double ov = __shfl_xor(bv, off), ol = __shfl_xor(bl, off), oa = __shfl_xor(ba, off);
+        if (better(ok, oi, bk, bi)) {
+            bk = ok;
+            bi = oi;
+            bv = ov;
+            bl = ol;
+            ba = oa;
+        }
+    }
+    __shared__ Partial sh[kBlock / 64];
+    const int tid = threadIdx.x;
+    if ((tid & 63) == 0) sh[tid >> 6] = Partial{bk, bi, bv, bl, ba};
+    __syncthreads();
+    if (tid == 0) {
+        Partial best = sh[0];
+        for (int w = 1; w < kBlock / 64; ++w)
+            if (better(sh[w].key, sh[w].idx, best.key, best.idx)) best = sh[w];
+        *dst = best;
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void thread_best(const double (&x)[R], const double (&lb)[R],
+                                            const double (&la)[R], const bool (&valid)[R],
+                                            int64_t gbase, uint64_t& bk, int64_t& bi, double& bv,
+                                            double& bl, double& ba) {
+    bk = 0;
+    bi = INT64_MAX;
+    bv = bl = ba = 0.0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (!valid[r]) continue;
+        const uint64_t key = order_key(lb[r] - la[r]);
+        const int64_t gi = gbase + r * kBlock;
+        if (better(key, gi, bk, bi)) {
+            bk = key;
+            bi = gi;
+            bv = x[r];
+            bl = lb[r];
+            ba = la[r];
+        }
+    }
+}
 
 // --------------------------------------------------------------- kernels ----
 
@@ -46,15 +116,15 @@ __global__ __launch_bounds__(kBlock) void k_round(
     const DLabel L = labels[li];
     const uint32_t round = rounds[blockIdx.z];
     const int tid = threadIdx.x;
-    const int64_t base = (int64_t)blockIdx.x * kTile;
+    const int64_t base = (int64_t)blockIdx.x * kTile + tid;
 
     double x[kR], lb[kR], la[kR];
     bool valid[kR];
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
-        const int64_t i = base + r * kBlock + tid;
+        const int64_t i = base + r * kBlock;
         valid[r] = i < n;
-        double v = 0.0;
+        double v = (MODE == DENSE_LGMM || MODE == QUANT_LGMM) ? 1.0 : 0.0;
         if (valid[r]) {
             if constexpr (SAMPLE) {
                 if (!sample_below<MODE>(L, samp + L.samp_off, seed, round,
@@ -63,10 +133,6 @@ __global__ __launch_bounds__(kBlock) void k_round(
             } else {
                 v = cand_in[i];
             }
-        } else if constexpr (MODE == CAT) {
-            v = 0.0;
-        } else {
-            v = (MODE == DENSE_LGMM || MODE == QUANT_LGMM) ? 1.0 : 0.0;
         }
         x[r] = v;
     }
@@ -75,35 +141,23 @@ __global__ __launch_bounds__(kBlock) void k_round(
         lse_dense<kR>(comps + L.comp_b, L.nb, L.shift_b, x, lb);
         lse_dense<kR>(comps + L.comp_a, L.na, L.shift_a, x, la);
     } else if constexpr (MODE == DENSE_LGMM) {
-        double y[kR], lx[kR];
+        double y[kR];
 #pragma unroll
-        for (int r = 0; r < kR; ++r) {
-            lx[r] = log(x[r]);
-            y[r] = lx[r];
-        }
+        for (int r = 0; r < kR; ++r) y[r] = log(x[r]);
         lse_dense<kR>(comps + L.comp_b, L.nb, L.shift_b, y, lb);
         lse_dense<kR>(comps + L.comp_a, L.na, L.shift_a, y, la);
 #pragma unroll
         for (int r = 0; r < kR; ++r) {
-            lb[r] -= lx[r];
-            la[r] -= lx[r];
+            lb[r] -= y[r];
+            la[r] -= y[r];
         }
     } else if constexpr (MODE == QUANT_GMM || MODE == QUANT_LGMM) {
-        const double half = L.q / 2.0;
 #pragma unroll
         for (int r = 0; r < kR; ++r) {
-            double ub = x[r] + half, lo = x[r] - half;
-            if (MODE == QUANT_GMM) {
-                if (L.flags & 2) ub = np_min(ub, L.high);
-                if (L.flags & 1) lo = np_max(lo, L.low);
-            } else {
-                if (L.flags & 2) ub = np_min(ub, L.exp_high);
-                if (L.flags & 1) lo = np_max(lo, L.exp_low);
-                lo = np_max(0.0, lo);
-                if (valid[r] && ub < 0.0) atomicOr(err, 2);  // tpe.py:187-188
-                ub = log(np_max(ub, kEps));
-                lo = log(np_max(lo, kEps));
-            }
+            double ub, lo;
+            bool neg;
+            quant_bounds<MODE>(L, x[r], ub, lo, neg);
+            if (valid[r] && neg) atomicOr(err, 2);
             lb[r] = quant_lpdf<MODE == QUANT_LGMM>(comps64 + L.comp_b, L.nb, ub, lo, L.logpacc_b);
             la[r] = quant_lpdf<MODE == QUANT_LGMM>(comps64 + L.comp_a, L.na, ub, lo, L.logpacc_a);
         }
@@ -118,52 +172,133 @@ __global__ __launch_bounds__(kBlock) void k_round(
         }
     }
 
-    // per-thread winner over its R candidates
-    uint64_t bk = 0;
-    int64_t bi = INT64_MAX;
-    double bv = 0.0, bl = 0.0, ba = 0.0;
-    const size_t row = ((size_t)blockIdx.z * n_labels + li) * (size_t)n;
+    if (out_lb) {
+        const size_t row = ((size_t)blockIdx.z * n_labels + li) * (size_t)n;
+#pragma unroll
+        for (int r = 0; r < kR; ++r)
+            if (valid[r]) {
+                out_lb[row + base + r * kBlock] = lb[r];
+                out_la[row + base + r * kBlock] = la[r];
+            }
+    }
+    uint64_t bk;
+    int64_t bi;
+    double bv, bl, ba;
+    thread_best<kR>(x, lb, la, valid, cand_offset + base, bk, bi, bv, bl, ba);
+    block_maxloc(bk, bi, bv, bl, ba,
+                 partials + ((size_t)blockIdx.z * n_labels + li) * tiles + blockIdx.x);
+}
+
+// Quantized families, pass 1: draw every candidate, keep its grid index
+// j = rint(v / q) (so x = j * q exactly as np.round(v / q) * q), and the
+// per-(round, label) min/max of j (order-preserving biased unsigned).
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_qsample(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const SampRec* __restrict__ samp, int64_t n, int64_t cand_offset, uint64_t seed,
+    const uint32_t* __restrict__ rounds, int32_t nq, int32_t qbase, int64_t* __restrict__ qj,
+    unsigned long long* __restrict__ qmin, unsigned long long* __restrict__ qmax,
+    int32_t* __restrict__ err) {
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    const uint32_t round = rounds[blockIdx.z];
+    const size_t slot = (size_t)blockIdx.z * nq + qbase + blockIdx.y;
+    int64_t* out = qj + slot * (size_t)n;
+    unsigned long long mn = ~0ull, mx = 0ull;
+    const int64_t base = (int64_t)blockIdx.x * kTile + threadIdx.x;
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
-        if (!valid[r]) continue;
-        const int64_t i = base + r * kBlock + tid;
-        if (out_lb) {
-            out_lb[row + i] = lb[r];
-            out_la[row + i] = la[r];
-        }
-        const uint64_t key = order_key(lb[r] - la[r]);
-        const int64_t gi = cand_offset + i;
-        if (better(key, gi, bk, bi)) {
-            bk = key;
-            bi = gi;
-            bv = x[r];
-            bl = lb[r];
-            ba = la[r];
-        }
+        const int64_t i = base + r * kBlock;
+        if (i >= n) continue;
+        double v;
+        if (!sample_raw<MODE>(L, samp + L.samp_off, seed, round, (uint32_t)(cand_offset + i), v))
+            atomicOr(err, 1);
+        const double jd = rint(v / L.q);
+        int64_t j = 0;
+        if (jd >= -0x1.0p52 && jd <= 0x1.0p52) j = (int64_t)jd;
+        else atomicOr(err, 8);
+        out[i] = j;
+        const unsigned long long u = (unsigned long long)j ^ 0x8000000000000000ull;
+        mn = u < mn ? u : mn;
+        mx = u > mx ? u : mx;
     }
-    // wave64 reduction
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t ok = __shfl_xor(bk, off);
-        const int64_t oi = __shfl_xor(bi, off);
-        const double ov = __shfl_xor(bv, off), ol = __shfl_xor(bl, off), oa = __shfl_xor(ba, off);
-        if (better(ok, oi, bk, bi)) {
-            bk = ok;
-            bi = oi;
-            bv = ov;
-            bl = ol;
-            ba = oa;
+        const unsigned long long a = __shfl_xor(mn, off), b = __shfl_xor(mx, off);
+        mn = a < mn ? a : mn;
+        mx = b > mx ? b : mx;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(qmin + slot, mn);
+        atomicMax(qmax + slot, mx);
+    }
+}
+
+// Quantized families, pass 2: one wave per distinct grid value x = j * q,
+// lane-strided component sums for both mixtures, written once to the table.
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_qtable(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<double>* __restrict__ comps64, const QInfo* __restrict__ qinfo, int32_t nq,
+    int32_t qbase, double2* __restrict__ tab) {
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    const QInfo Q = qinfo[(size_t)blockIdx.z * nq + qbase + blockIdx.y];
+    const int lane = threadIdx.x & 63;
+    const int64_t s = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (s >= Q.G) return;
+    const double x = (double)(Q.jmin + s) * L.q;
+    double ub, lo;
+    bool neg;
+    quant_bounds<MODE>(L, x, ub, lo, neg);
+    const double pb = wave_sum(quant_share<MODE == QUANT_LGMM>(comps64 + L.comp_b, L.nb, ub, lo, lane));
+    const double pa = wave_sum(quant_share<MODE == QUANT_LGMM>(comps64 + L.comp_a, L.na, ub, lo, lane));
+    if (lane == 0) tab[Q.tab_off + s] = make_double2(log(pb) - L.logpacc_b, log(pa) - L.logpacc_a);
+}
+
+// Quantized families, pass 3: per candidate look up its grid value's lpdf
+// pair (direct evaluation when the label's window was too wide for a table),
+// then the same block maxloc as k_round.
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_qscan(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<double>* __restrict__ comps64, const int64_t* __restrict__ qj,
+    const QInfo* __restrict__ qinfo, const double2* __restrict__ tab, int64_t n,
+    int64_t cand_offset, int32_t nq, int32_t qbase, int32_t n_labels, int32_t tiles,
+    Partial* __restrict__ partials) {
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    const size_t slot = (size_t)blockIdx.z * nq + qbase + blockIdx.y;
+    const QInfo Q = qinfo[slot];
+    const int64_t* js = qj + slot * (size_t)n;
+    const int64_t base = (int64_t)blockIdx.x * kTile + threadIdx.x;
+    double x[kR], lb[kR], la[kR];
+    bool valid[kR];
+#pragma unroll
+    for (int r = 0; r < kR; ++r) {
+        const int64_t i = base + r * kBlock;
+        valid[r] = i < n;
+        const int64_t j = valid[r] ? js[i] : Q.jmin;
+        x[r] = (double)j * L.q;
+        const int64_t s = j - Q.jmin;
+        if (s >= 0 && s < Q.G) {
+            const double2 t = tab[Q.tab_off + s];
+            lb[r] = t.x;
+            la[r] = t.y;
+        } else {
+            double ub, lo;
+            bool neg;
+            quant_bounds<MODE>(L, x[r], ub, lo, neg);
+            lb[r] = quant_lpdf<MODE == QUANT_LGMM>(comps64 + L.comp_b, L.nb, ub, lo, L.logpacc_b);
+            la[r] = quant_lpdf<MODE == QUANT_LGMM>(comps64 + L.comp_a, L.na, ub, lo, L.logpacc_a);
         }
     }
-    __shared__ Partial sh[kBlock / 64];
-    if ((tid & 63) == 0) sh[tid >> 6] = Partial{bk, bi, bv, bl, ba};
-    __syncthreads();
-    if (tid == 0) {
-        Partial best = sh[0];
-        for (int w = 1; w < kBlock / 64; ++w)
-            if (better(sh[w].key, sh[w].idx, best.key, best.idx)) best = sh[w];
-        partials[((size_t)blockIdx.z * n_labels + li) * tiles + blockIdx.x] = best;
-    }
+    uint64_t bk;
+    int64_t bi;
+    double bv, bl, ba;
+    thread_best<kR>(x, lb, la, valid, cand_offset + base, bk, bi, bv, bl, ba);
+    block_maxloc(bk, bi, bv, bl, ba,
+                 partials + ((size_t)blockIdx.z * n_labels + li) * tiles + blockIdx.x);
 }
 
 __global__ __launch_bounds__(kBlock) void k_reduce(const Partial* __restrict__ partials,
@@ -174,30 +309,17 @@ __global__ __launch_bounds__(kBlock) void k_reduce(const Partial* __restrict__ p
     Partial best{0, INT64_MAX, 0.0, 0.0, 0.0};
     for (int t = tid; t < tiles; t += kBlock)
         if (better(p[t].key, p[t].idx, best.key, best.idx)) best = p[t];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        Partial o;
-        o.key = __shfl_xor(best.key, off);
-        o.idx = __shfl_xor(best.idx, off);
-        o.value = __shfl_xor(best.value, off);
-        o.lb = __shfl_xor(best.lb, off);
-        o.la = __shfl_xor(best.la, off);
-        if (better(o.key, o.idx, best.key, best.idx)) best = o;
-    }
-    __shared__ Partial sh[kBlock / 64];
-    if ((tid & 63) == 0) sh[tid >> 6] = best;
+    __shared__ Partial res;
+    block_maxloc(best.key, best.idx, best.value, best.lb, best.la, &res);
     __syncthreads();
     if (tid == 0) {
-        best = sh[0];
-        for (int w = 1; w < kBlock / 64; ++w)
-            if (better(sh[w].key, sh[w].idx, best.key, best.idx)) best = sh[w];
         tpe_label_result r;
-        const bool any = best.idx != INT64_MAX;
-        r.value = best.value;
-        r.score = best.lb - best.la;
-        r.lpdf_below = best.lb;
-        r.lpdf_above = best.la;
-        r.index = any ? best.idx : -1;
+        const bool any = res.idx != INT64_MAX;
+        r.value = res.value;
+        r.score = res.lb - res.la;
+        r.lpdf_below = res.lb;
+        r.lpdf_above = res.la;
+        r.index = any ? res.idx : -1;
         r.label = li;
         r.status = 0;
         out[(size_t)rz * n_labels + li] = r;
@@ -218,24 +340,24 @@ __global__ __launch_bounds__(kBlock) void k_argmax(const double* __restrict__ b,
             bi = i;
         }
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t ok = __shfl_xor(bk, off);
-        const int64_t oi = __shfl_xor(bi, off);
-        if (better(ok, oi, bk, bi)) {
-            bk = ok;
-            bi = oi;
-        }
-    }
-    __shared__ Partial sh[kBlock / 64];
-    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = Partial{bk, bi, 0, 0, 0};
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        Partial best = sh[0];
-        for (int w = 1; w < kBlock / 64; ++w)
-            if (better(sh[w].key, sh[w].idx, best.key, best.idx)) best = sh[w];
-        partials[blockIdx.x] = best;
-    }
+    block_maxloc(bk, bi, 0.0, 0.0, 0.0, partials + blockIdx.x);
+}
+
+// sample-only kernel (tpe_*_sample): one draw per thread, no scoring
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_sample_only(const DLabel* __restrict__ labels,
+                                                        const SampRec* __restrict__ samp,
+                                                        int64_t n, int64_t offset, uint64_t seed,
+                                                        const uint32_t* __restrict__ rounds,
+                                                        double* __restrict__ out,
+                                                        int32_t* __restrict__ err) {
+    const DLabel L = labels[0];
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    double v;
+    if (!sample_below<MODE>(L, samp + L.samp_off, seed, rounds[0], (uint32_t)(offset + i), v))
+        atomicOr(err, 1);
+    out[i] = v;
 }
 
 // ------------------------------------------------------------ host side ----
@@ -299,24 +421,25 @@ struct tpe_ctx {
     int precision = TPE_F64;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
-    hipEvent_t evm[5][2] = {};         // per-mode kernel brackets
-    bool mode_ran[5] = {};
-    float mode_ms[5] = {};
-    int64_t mode_evals[5] = {};
+    hipEvent_t evm[kNumModes][2] = {};   // per-family kernel brackets
+    bool mode_ran[kNumModes] = {};
+    float mode_ms[kNumModes] = {};
+    int64_t mode_evals[kNumModes] = {};
     std::string err;
     float score_ms = 0.f, round_ms = 0.f;
     int64_t evals = 0;
+    bool dedup = true;                   // quantized grid-value tables
 
     // resident posterior
     std::vector<DLabel> h_labels;
-    std::vector<int32_t> h_group[5];   // label ids per mode
+    std::vector<int32_t> h_group[kNumModes];   // label ids per mode
     int32_t n_labels = 0;
     DevBuf<DLabel> labels;
     DevBuf<Comp<double>> comps64;
     DevBuf<Comp<float>> comps32;
     DevBuf<SampRec> samp;
-    DevBuf<int32_t> groups;            // concatenated h_group
-    int32_t group_off[5] = {0, 0, 0, 0, 0};
+    DevBuf<int32_t> groups;              // concatenated h_group
+    int32_t group_off[kNumModes] = {};
 
     // per-round scratch
     DevBuf<Partial> partials;
@@ -325,6 +448,10 @@ struct tpe_ctx {
     DevBuf<int32_t> errflag;
     DevBuf<double> cand, out_lb, out_la;
     DevBuf<int32_t> one_group;
+    DevBuf<int64_t> qj;
+    DevBuf<unsigned long long> qmm;
+    DevBuf<QInfo> qinfo;
+    DevBuf<double2> qtab;
 
     int fail(int code, const std::string& m) {
         err = m;
@@ -411,42 +538,117 @@ int validate_mixture(tpe_ctx* ctx, int32_t k, int32_t flags, double low, double 
 }
 
 struct Groups {
-    const int32_t* dev[5];   // device pointers to label ids per mode
-    int32_t count[5];
+    const int32_t* dev[kNumModes];   // device pointers to label ids per mode
+    int32_t count[kNumModes];
 };
 
-template <typename T, int MODE, bool SAMPLE>
-void launch_mode(tpe_ctx* ctx, const Groups& g, int64_t n, int64_t cand_offset, uint64_t seed,
-                 int32_t n_rounds, int32_t tiles, const double* cand_in, double* olb,
-                 double* ola) {
-    const int nl = g.count[MODE];
-    if (nl == 0 || tiles == 0) return;
-    ctx->mode_ran[MODE] = true;
-    (void)hipEventRecord(ctx->evm[MODE][0], ctx->stream);
-    dim3 grid(tiles, nl, n_rounds);
-    const Comp<T>* comps;
-    if constexpr (sizeof(T) == 8) comps = ctx->comps64.p; else comps = ctx->comps32.p;
-    hipLaunchKernelGGL((k_round<T, MODE, SAMPLE>), grid, dim3(kBlock), 0, ctx->stream,
-                       ctx->labels.p, g.dev[MODE], comps, ctx->comps64.p, ctx->samp.p, cand_in,
-                       n, cand_offset, seed, ctx->rounds.p, ctx->n_labels, tiles,
-                       ctx->partials.p, olb, ola, ctx->errflag.p);
-    (void)hipEventRecord(ctx->evm[MODE][1], ctx->stream);
+struct RoundArgs {
+    int64_t n, cand_offset;
+    uint64_t seed;
+    int32_t n_rounds, tiles;
+    const double* cand_in;
+    double *olb, *ola;
+};
+
+void bracket(tpe_ctx* ctx, int mode, int which) {
+    ctx->mode_ran[mode] = true;
+    (void)hipEventRecord(ctx->evm[mode][which], ctx->stream);
 }
 
-template <bool SAMPLE>
-void launch_all(tpe_ctx* ctx, const Groups& g, int64_t n, int64_t cand_offset, uint64_t seed,
-                int32_t n_rounds, int32_t tiles, const double* cand_in, double* olb, double* ola) {
-    // heaviest groups first
-    launch_mode<double, QUANT_GMM, SAMPLE>(ctx, g, n, cand_offset, seed, n_rounds, tiles, cand_in, olb, ola);
-    launch_mode<double, QUANT_LGMM, SAMPLE>(ctx, g, n, cand_offset, seed, n_rounds, tiles, cand_in, olb, ola);
-    if (ctx->precision == TPE_F32) {
-        launch_mode<float, DENSE_GMM, SAMPLE>(ctx, g, n, cand_offset, seed, n_rounds, tiles, cand_in, olb, ola);
-        launch_mode<float, DENSE_LGMM, SAMPLE>(ctx, g, n, cand_offset, seed, n_rounds, tiles, cand_in, olb, ola);
-    } else {
-        launch_mode<double, DENSE_GMM, SAMPLE>(ctx, g, n, cand_offset, seed, n_rounds, tiles, cand_in, olb, ola);
-        launch_mode<double, DENSE_LGMM, SAMPLE>(ctx, g, n, cand_offset, seed, n_rounds, tiles, cand_in, olb, ola);
+template <typename T, int MODE, bool SAMPLE>
+void launch_round(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
+    const int nl = g.count[MODE];
+    if (nl == 0 || a.tiles == 0) return;
+    bracket(ctx, MODE, 0);
+    const Comp<T>* comps;
+    if constexpr (sizeof(T) == 8) comps = ctx->comps64.p; else comps = ctx->comps32.p;
+    hipLaunchKernelGGL((k_round<T, MODE, SAMPLE>), dim3(a.tiles, nl, a.n_rounds), dim3(kBlock), 0,
+                       ctx->stream, ctx->labels.p, g.dev[MODE], comps, ctx->comps64.p,
+                       ctx->samp.p, a.cand_in, a.n, a.cand_offset, a.seed, ctx->rounds.p,
+                       ctx->n_labels, a.tiles, ctx->partials.p, a.olb, a.ola, ctx->errflag.p);
+    bracket(ctx, MODE, 1);
+}
+
+// Quantized families in a sampled round: qsample (both families) -> host
+// decides each label's table window -> qtable + qscan per family.
+int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t* evals_q) {
+    const int nqg = g.count[QUANT_GMM], nql = g.count[QUANT_LGMM];
+    const int nq = nqg + nql;
+    evals_q[0] = evals_q[1] = 0;
+    if (nq == 0 || a.tiles == 0) return TPE_OK;
+    const size_t slots = (size_t)a.n_rounds * nq;
+    HIPCHK(ctx, ctx->qj.reserve(slots * (size_t)a.n));
+    HIPCHK(ctx, ctx->qmm.reserve(2 * slots));
+    HIPCHK(ctx, ctx->qinfo.reserve(slots));
+    HIPCHK(ctx, hipMemsetAsync(ctx->qmm.p, 0xFF, slots * sizeof(unsigned long long), ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->qmm.p + slots, 0, slots * sizeof(unsigned long long), ctx->stream));
+    if (nqg)
+        hipLaunchKernelGGL(k_qsample<QUANT_GMM>, dim3(a.tiles, nqg, a.n_rounds), dim3(kBlock), 0,
+                           ctx->stream, ctx->labels.p, g.dev[QUANT_GMM], ctx->samp.p, a.n,
+                           a.cand_offset, a.seed, ctx->rounds.p, nq, 0, ctx->qj.p, ctx->qmm.p,
+                           ctx->qmm.p + slots, ctx->errflag.p);
+    if (nql)
+        hipLaunchKernelGGL(k_qsample<QUANT_LGMM>, dim3(a.tiles, nql, a.n_rounds), dim3(kBlock), 0,
+                           ctx->stream, ctx->labels.p, g.dev[QUANT_LGMM], ctx->samp.p, a.n,
+                           a.cand_offset, a.seed, ctx->rounds.p, nq, nqg, ctx->qj.p, ctx->qmm.p,
+                           ctx->qmm.p + slots, ctx->errflag.p);
+    HIPCHK(ctx, hipGetLastError());
+    std::vector<unsigned long long> mm(2 * slots);
+    HIPCHK(ctx, hipMemcpyAsync(mm.data(), ctx->qmm.p, 2 * slots * sizeof(unsigned long long),
+                               hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    // table window per (round, label): worth it when the grid is narrower
+    // than the candidate set (each slot costs one candidate's work)
+    std::vector<QInfo> qi(slots);
+    int64_t tab = 0, maxG = 0;
+    const int64_t cap = std::max<int64_t>(a.n / 2, 4096);
+    for (size_t s = 0; s < slots; ++s) {
+        const int64_t jmin = (int64_t)(mm[s] ^ 0x8000000000000000ull);
+        const int64_t jmax = (int64_t)(mm[slots + s] ^ 0x8000000000000000ull);
+        const int64_t G = (mm[s] <= mm[slots + s]) ? jmax - jmin + 1 : 0;
+        qi[s] = QInfo{jmin, (ctx->dedup && G > 0 && G <= cap) ? G : 0, tab, 0};
+        tab += qi[s].G;
+        maxG = std::max(maxG, qi[s].G);
+        const int qpos = (int)(s % nq);
+        const int li = qpos < nqg ? ctx->h_group[QUANT_GMM][qpos] : ctx->h_group[QUANT_LGMM][qpos - nqg];
+        const DLabel& d = ctx->h_labels[li];
+        evals_q[qpos < nqg ? 0 : 1] += (qi[s].G ? qi[s].G : a.n) * (int64_t)(d.nb + d.na);
     }
-    launch_mode<double, CAT, SAMPLE>(ctx, g, n, cand_offset, seed, n_rounds, tiles, cand_in, olb, ola);
+    HIPCHK(ctx, ctx->qtab.reserve(std::max<int64_t>(tab, 1)));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->qinfo.p, qi.data(), slots * sizeof(QInfo),
+                               hipMemcpyHostToDevice, ctx->stream));
+    for (int fam = 0; fam < 2; ++fam) {
+        const int mode = fam ? QUANT_LGMM : QUANT_GMM;
+        const int cnt = fam ? nql : nqg;
+        const int qbase = fam ? nqg : 0;
+        if (!cnt) continue;
+        bracket(ctx, mode, 0);
+        if (maxG > 0) {
+            dim3 tg((unsigned)((maxG + kBlock / 64 - 1) / (kBlock / 64)), cnt, a.n_rounds);
+            if (fam)
+                hipLaunchKernelGGL(k_qtable<QUANT_LGMM>, tg, dim3(kBlock), 0, ctx->stream,
+                                   ctx->labels.p, g.dev[mode], ctx->comps64.p, ctx->qinfo.p, nq,
+                                   qbase, ctx->qtab.p);
+            else
+                hipLaunchKernelGGL(k_qtable<QUANT_GMM>, tg, dim3(kBlock), 0, ctx->stream,
+                                   ctx->labels.p, g.dev[mode], ctx->comps64.p, ctx->qinfo.p, nq,
+                                   qbase, ctx->qtab.p);
+        }
+        dim3 sg(a.tiles, cnt, a.n_rounds);
+        if (fam)
+            hipLaunchKernelGGL(k_qscan<QUANT_LGMM>, sg, dim3(kBlock), 0, ctx->stream, ctx->labels.p,
+                               g.dev[mode], ctx->comps64.p, ctx->qj.p, ctx->qinfo.p, ctx->qtab.p,
+                               a.n, a.cand_offset, nq, qbase, ctx->n_labels, a.tiles,
+                               ctx->partials.p);
+        else
+            hipLaunchKernelGGL(k_qscan<QUANT_GMM>, sg, dim3(kBlock), 0, ctx->stream, ctx->labels.p,
+                               g.dev[mode], ctx->comps64.p, ctx->qj.p, ctx->qinfo.p, ctx->qtab.p,
+                               a.n, a.cand_offset, nq, qbase, ctx->n_labels, a.tiles,
+                               ctx->partials.p);
+        bracket(ctx, mode, 1);
+    }
+    HIPCHK(ctx, hipGetLastError());
+    return TPE_OK;
 }
 
 int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_rounds, int64_t n,
@@ -466,29 +668,49 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
                                hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->errflag.p, 0, sizeof(int32_t), ctx->stream));
     Groups g;
-    for (int m = 0; m < 5; ++m) {
+    for (int m = 0; m < kNumModes; ++m) {
         g.dev[m] = ctx->groups.p + ctx->group_off[m];
         g.count[m] = (int32_t)ctx->h_group[m].size();
+        ctx->mode_ran[m] = false;
+        ctx->mode_ms[m] = 0.f;
+        ctx->mode_evals[m] = 0;
     }
     if (only_label >= 0) {  // tpe_score: launch the one label's mode only
         HIPCHK(ctx, ctx->one_group.reserve(1));
         HIPCHK(ctx, hipMemcpyAsync(ctx->one_group.p, &only_label, sizeof(int32_t),
                                    hipMemcpyHostToDevice, ctx->stream));
-        for (int m = 0; m < 5; ++m) g.count[m] = 0;
+        for (int m = 0; m < kNumModes; ++m) g.count[m] = 0;
         const int m = ctx->h_labels[only_label].mode;
         g.dev[m] = ctx->one_group.p;
         g.count[m] = 1;
     }
-    for (int m = 0; m < 5; ++m) {
-        ctx->mode_ran[m] = false;
-        ctx->mode_ms[m] = 0.f;
-        ctx->mode_evals[m] = 0;
-    }
+    RoundArgs a{n, cand_offset, seed, n_rounds, tiles, cand_in_dev, olb, ola};
+    const bool sample = cand_in_dev == nullptr;
+    int64_t evals_q[2] = {0, 0};
     HIPCHK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
-    if (cand_in_dev)
-        launch_all<false>(ctx, g, n, cand_offset, seed, n_rounds, tiles, cand_in_dev, olb, ola);
-    else
-        launch_all<true>(ctx, g, n, cand_offset, seed, n_rounds, tiles, nullptr, olb, ola);
+    if (sample) {
+        int rc = launch_quantized(ctx, g, a, evals_q);
+        if (rc) return rc;
+        if (ctx->precision == TPE_F32) {
+            launch_round<float, DENSE_GMM, true>(ctx, g, a);
+            launch_round<float, DENSE_LGMM, true>(ctx, g, a);
+        } else {
+            launch_round<double, DENSE_GMM, true>(ctx, g, a);
+            launch_round<double, DENSE_LGMM, true>(ctx, g, a);
+        }
+        launch_round<double, CAT, true>(ctx, g, a);
+    } else {
+        launch_round<double, QUANT_GMM, false>(ctx, g, a);
+        launch_round<double, QUANT_LGMM, false>(ctx, g, a);
+        if (ctx->precision == TPE_F32) {
+            launch_round<float, DENSE_GMM, false>(ctx, g, a);
+            launch_round<float, DENSE_LGMM, false>(ctx, g, a);
+        } else {
+            launch_round<double, DENSE_GMM, false>(ctx, g, a);
+            launch_round<double, DENSE_LGMM, false>(ctx, g, a);
+        }
+        launch_round<double, CAT, false>(ctx, g, a);
+    }
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(ctx->ev1, ctx->stream));
     if (tiles > 0) {
@@ -507,115 +729,52 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     HIPCHK(ctx, hipEventElapsedTime(&ctx->score_ms, ctx->ev0, ctx->ev1));
     HIPCHK(ctx, hipEventElapsedTime(&ctx->round_ms, ctx->ev0, ctx->ev2));
-    for (int m = 0; m < 5; ++m)
+    for (int m = 0; m < kNumModes; ++m)
         if (ctx->mode_ran[m])
             HIPCHK(ctx, hipEventElapsedTime(&ctx->mode_ms[m], ctx->evm[m][0], ctx->evm[m][1]));
     int64_t evals = 0;
     for (int32_t l = 0; l < L; ++l) {
         if (only_label >= 0 && l != only_label) continue;
         const DLabel& d = ctx->h_labels[l];
+        if (sample && (d.mode == QUANT_GMM || d.mode == QUANT_LGMM)) continue;  // counted below
         const int64_t e = ((d.mode == CAT) ? 2 * n : n * (int64_t)(d.nb + d.na)) * n_rounds;
         evals += e;
         ctx->mode_evals[d.mode] += e;
     }
-    ctx->evals = evals;
+    ctx->mode_evals[QUANT_GMM] += evals_q[0];
+    ctx->mode_evals[QUANT_LGMM] += evals_q[1];
+    ctx->evals = evals + evals_q[0] + evals_q[1];
     if (tiles == 0 && out) {
-        for (int32_t j = 0; j < n_rounds * L; ++j) {
+        for (int32_t j = 0; j < n_rounds * L; ++j)
             out[j] = tpe_label_result{NAN, NAN, NAN, NAN, -1, j % L, 0};
-        }
     }
     if (errh & 1) return ctx->fail(TPE_ERR_SAMPLE, "truncated sampler: interval [low, high) not reached");
     if (errh & 2) return ctx->fail(TPE_ERR_VALUE, "negative arg to lognormal_cdf");
     if (errh & 4) return ctx->fail(TPE_ERR_VALUE, "categorical sample out of range");
+    if (errh & 8) return ctx->fail(TPE_ERR_VALUE, "quantized sample beyond 2^52 grid steps");
     return TPE_OK;
 }
 
-}  // namespace
-
-void tpe_launch_sample_only(tpe_ctx* ctx, int mode, int64_t n, int64_t offset, uint64_t seed,
-                            double* out);
-
-// ================================================================ C ABI ====
-extern "C" {
-
-int tpe_abi_version(void) { return TPE_ABI_VERSION; }
-
-int tpe_ctx_create(int device, int precision, tpe_ctx** out) {
-    if (!out) return TPE_ERR_ARG;
-    *out = nullptr;
-    if (precision != TPE_F64 && precision != TPE_F32) {
-        g_create_error = "precision must be TPE_F64 or TPE_F32";
-        return TPE_ERR_ARG;
+void launch_sample_only(tpe_ctx* ctx, int mode, int64_t n, int64_t offset, uint64_t seed,
+                        double* out) {
+    const int blocks = (int)((n + kBlock - 1) / kBlock);
+#define TPE_SO(M)                                                                             \
+    hipLaunchKernelGGL(k_sample_only<M>, dim3(blocks), dim3(kBlock), 0, ctx->stream,         \
+                       ctx->labels.p, ctx->samp.p, n, offset, seed, ctx->rounds.p, out,       \
+                       ctx->errflag.p)
+    switch (mode) {
+        case DENSE_GMM: TPE_SO(DENSE_GMM); break;
+        case DENSE_LGMM: TPE_SO(DENSE_LGMM); break;
+        case QUANT_GMM: TPE_SO(QUANT_GMM); break;
+        case QUANT_LGMM: TPE_SO(QUANT_LGMM); break;
+        default: TPE_SO(CAT); break;
     }
-    int ndev = 0;
-    hipError_t e = hipGetDeviceCount(&ndev);
-    if (e != hipSuccess || device < 0 || device >= ndev) {
-        g_create_error = std::string("no HIP device ") + std::to_string(device) + " (" +
-                         (e == hipSuccess ? "count " + std::to_string(ndev) : hipGetErrorString(e)) + ")";
-        return TPE_ERR_HIP;
-    }
-    e = hipSetDevice(device);
-    if (e != hipSuccess) {
-        g_create_error = hipGetErrorString(e);
-        return TPE_ERR_HIP;
-    }
-    tpe_ctx* c = new tpe_ctx();
-    c->device = device;
-    c->precision = precision;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipEventCreate(&c->ev2) != hipSuccess) {
-        g_create_error = "stream/event creation failed";
-        tpe_ctx_destroy(c);
-        return TPE_ERR_HIP;
-    }
-    bool ok = true;
-    for (int m = 0; m < 5; ++m)
-        ok = ok && hipEventCreate(&c->evm[m][0]) == hipSuccess &&
-             hipEventCreate(&c->evm[m][1]) == hipSuccess;
-    if (!ok) {
-        g_create_error = "stream/event creation failed";
-        tpe_ctx_destroy(c);
-        return TPE_ERR_HIP;
-    }
-    *out = c;
-    return TPE_OK;
+#undef TPE_SO
 }
 
-void tpe_ctx_destroy(tpe_ctx* c) {
-    if (!c) return;
-    (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
-    c->labels.release();
-    c->comps64.release();
-    c->comps32.release();
-    c->samp.release();
-    c->groups.release();
-    c->partials.release();
-    c->results.release();
-    c->rounds.release();
-    c->errflag.release();
-    c->cand.release();
-    c->out_lb.release();
-    c->out_la.release();
-    c->one_group.release();
-    if (c->ev0) (void)hipEventDestroy(c->ev0);
-    if (c->ev1) (void)hipEventDestroy(c->ev1);
-    if (c->ev2) (void)hipEventDestroy(c->ev2);
-    for (int m = 0; m < 5; ++m)
-        for (int j = 0; j < 2; ++j)
-            if (c->evm[m][j]) (void)hipEventDestroy(c->evm[m][j]);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
-    delete c;
-}
-
-const char* tpe_last_error(const tpe_ctx* c) {
-    return c ? c->err.c_str() : g_create_error.c_str();
-}
-
-static int set_posterior_impl(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_labels,
-                              const double* weights, const double* mus, const double* sigmas,
-                              int64_t n_components, bool sampler_checks) {
+int set_posterior_impl(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_labels,
+                       const double* weights, const double* mus, const double* sigmas,
+                       int64_t n_components, bool sampler_checks) {
     if (!ctx) return TPE_ERR_ARG;
     if (n_labels <= 0 || !labels || !weights) return ctx->fail(TPE_ERR_ARG, "empty posterior");
     HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -623,7 +782,7 @@ static int set_posterior_impl(tpe_ctx* ctx, const tpe_label_desc* labels, int32_
     std::vector<Comp<double>> c64;
     std::vector<Comp<float>> c32;
     std::vector<SampRec> sr;
-    for (int m = 0; m < 5; ++m) ctx->h_group[m].clear();
+    std::vector<int32_t> grp[kNumModes];
     for (int32_t l = 0; l < n_labels; ++l) {
         const tpe_label_desc& d = labels[l];
         DLabel& o = dl[l];
@@ -653,7 +812,6 @@ static int set_posterior_impl(tpe_ctx* ctx, const tpe_label_desc* labels, int32_
         o.nb = d.n_below;
         o.na = d.n_above;
         o.stream = l;
-        // below + above records
         for (int side = 0; side < 2; ++side) {
             const int64_t off = side ? d.above_off : d.below_off;
             const int32_t n = side ? d.n_above : d.n_below;
@@ -693,12 +851,13 @@ static int set_posterior_impl(tpe_ctx* ctx, const tpe_label_desc* labels, int32_
             s.pad = 0.0;
             sr.push_back(s);
         }
-        ctx->h_group[o.mode].push_back(l);
+        grp[o.mode].push_back(l);
     }
     std::vector<int32_t> cat;
-    for (int m = 0; m < 5; ++m) {
+    for (int m = 0; m < kNumModes; ++m) {
         ctx->group_off[m] = (int32_t)cat.size();
-        cat.insert(cat.end(), ctx->h_group[m].begin(), ctx->h_group[m].end());
+        cat.insert(cat.end(), grp[m].begin(), grp[m].end());
+        ctx->h_group[m] = grp[m];
     }
     HIPCHK(ctx, ctx->labels.reserve(n_labels));
     HIPCHK(ctx, ctx->comps64.reserve(c64.size()));
@@ -713,6 +872,87 @@ static int set_posterior_impl(tpe_ctx* ctx, const tpe_label_desc* labels, int32_
     ctx->h_labels = dl;
     ctx->n_labels = n_labels;
     return TPE_OK;
+}
+
+}  // namespace
+
+// ================================================================ C ABI ====
+extern "C" {
+
+int tpe_abi_version(void) { return TPE_ABI_VERSION; }
+
+int tpe_ctx_create(int device, int precision, tpe_ctx** out) {
+    if (!out) return TPE_ERR_ARG;
+    *out = nullptr;
+    if (precision != TPE_F64 && precision != TPE_F32) {
+        g_create_error = "precision must be TPE_F64 or TPE_F32";
+        return TPE_ERR_ARG;
+    }
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || device < 0 || device >= ndev) {
+        g_create_error = std::string("no HIP device ") + std::to_string(device) + " (" +
+                         (e == hipSuccess ? "count " + std::to_string(ndev) : hipGetErrorString(e)) + ")";
+        return TPE_ERR_HIP;
+    }
+    e = hipSetDevice(device);
+    if (e != hipSuccess) {
+        g_create_error = hipGetErrorString(e);
+        return TPE_ERR_HIP;
+    }
+    tpe_ctx* c = new tpe_ctx();
+    c->device = device;
+    c->precision = precision;
+    bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreate(&c->ev0) == hipSuccess && hipEventCreate(&c->ev1) == hipSuccess &&
+              hipEventCreate(&c->ev2) == hipSuccess;
+    for (int m = 0; m < kNumModes; ++m)
+        ok = ok && hipEventCreate(&c->evm[m][0]) == hipSuccess &&
+             hipEventCreate(&c->evm[m][1]) == hipSuccess;
+    if (!ok) {
+        g_create_error = "stream/event creation failed";
+        tpe_ctx_destroy(c);
+        return TPE_ERR_HIP;
+    }
+    const char* dd = getenv("TPE_NO_DEDUP");
+    c->dedup = !(dd && dd[0] == '1');
+    *out = c;
+    return TPE_OK;
+}
+
+void tpe_ctx_destroy(tpe_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    c->labels.release();
+    c->comps64.release();
+    c->comps32.release();
+    c->samp.release();
+    c->groups.release();
+    c->partials.release();
+    c->results.release();
+    c->rounds.release();
+    c->errflag.release();
+    c->cand.release();
+    c->out_lb.release();
+    c->out_la.release();
+    c->one_group.release();
+    c->qj.release();
+    c->qmm.release();
+    c->qinfo.release();
+    c->qtab.release();
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->ev2) (void)hipEventDestroy(c->ev2);
+    for (int m = 0; m < kNumModes; ++m)
+        for (int j = 0; j < 2; ++j)
+            if (c->evm[m][j]) (void)hipEventDestroy(c->evm[m][j]);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* tpe_last_error(const tpe_ctx* c) {
+    return c ? c->err.c_str() : g_create_error.c_str();
 }
 
 int tpe_set_posterior(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_labels,
@@ -808,7 +1048,7 @@ int64_t tpe_last_evals(const tpe_ctx* ctx) { return ctx ? ctx->evals : -1; }
 
 int tpe_last_mode_stats(const tpe_ctx* ctx, float* ms, int64_t* evals) {
     if (!ctx) return TPE_ERR_ARG;
-    for (int m = 0; m < 5; ++m) {
+    for (int m = 0; m < kNumModes; ++m) {
         if (ms) ms[m] = ctx->mode_ms[m];
         if (evals) evals[m] = ctx->mode_evals[m];
     }
@@ -903,7 +1143,9 @@ static int one_label_sample(tpe_ctx* ctx, int kind, const double* w, const doubl
                             int64_t offset, int64_t n, double* out) {
     if (!ctx) return TPE_ERR_ARG;
     if (n == 0) return TPE_OK;
-    if (!out) return ctx->fail(TPE_ERR_ARG, "null output");
+    if (!out || !w) return ctx->fail(TPE_ERR_ARG, "null pointer");
+    if (offset < 0 || offset + n > (int64_t)UINT32_MAX)
+        return ctx->fail(TPE_ERR_ARG, "candidate indices must stay below 2^32");
     tpe_label_desc d{};
     d.kind = kind;
     d.flags = flags;
@@ -911,20 +1153,16 @@ static int one_label_sample(tpe_ctx* ctx, int kind, const double* w, const doubl
     d.high = high;
     d.q = q;
     d.n_below = d.n_above = k;
-    int rc = tpe_set_posterior(ctx, &d, 1, w, mu, sg, k);
+    int rc = set_posterior_impl(ctx, &d, 1, w, mu, sg, k, true);
     if (rc) return rc;
     ctx->h_labels[0].stream = (int32_t)stream;
     HIPCHK(ctx, hipMemcpy(ctx->labels.p, ctx->h_labels.data(), sizeof(DLabel), hipMemcpyHostToDevice));
-    // score the draws against themselves; lpdf_below of the winner is unused,
-    // the samples come back through a sample-only pass below.
-    HIPCHK(ctx, ctx->out_lb.reserve(std::max<int64_t>(n, 1)));
-    HIPCHK(ctx, ctx->out_la.reserve(std::max<int64_t>(n, 1)));
     HIPCHK(ctx, ctx->cand.reserve(std::max<int64_t>(n, 1)));
     HIPCHK(ctx, ctx->rounds.reserve(1));
     HIPCHK(ctx, ctx->errflag.reserve(1));
     HIPCHK(ctx, hipMemcpyAsync(ctx->rounds.p, &round, sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->errflag.p, 0, sizeof(int32_t), ctx->stream));
-    tpe_launch_sample_only(ctx, ctx->h_labels[0].mode, n, offset, seed, ctx->cand.p);
+    launch_sample_only(ctx, ctx->h_labels[0].mode, n, offset, seed, ctx->cand.p);
     HIPCHK(ctx, hipGetLastError());
     int32_t errh = 0;
     HIPCHK(ctx, hipMemcpyAsync(&errh, ctx->errflag.p, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
@@ -953,6 +1191,7 @@ int tpe_categorical_sample(tpe_ctx* ctx, const double* p, int32_t upper, uint64_
                            int64_t* out) {
     if (!ctx) return TPE_ERR_ARG;
     if (n == 0) return TPE_OK;
+    if (!out) return ctx->fail(TPE_ERR_ARG, "null pointer");
     std::vector<double> tmp(n);
     int rc = one_label_sample(ctx, TPE_CATEGORICAL, p, nullptr, nullptr, upper, 0, 0, 0, 0, seed,
                               stream, round, offset, n, tmp.data());
@@ -962,37 +1201,3 @@ int tpe_categorical_sample(tpe_ctx* ctx, const double* p, int32_t upper, uint64_
 }
 
 }  // extern "C"
-
-// sample-only kernel (tpe_*_sample): one draw per thread, no scoring
-template <int MODE>
-__global__ __launch_bounds__(kBlock) void k_sample_only(const DLabel* __restrict__ labels,
-                                                        const SampRec* __restrict__ samp,
-                                                        int64_t n, int64_t offset, uint64_t seed,
-                                                        const uint32_t* __restrict__ rounds,
-                                                        double* __restrict__ out,
-                                                        int32_t* __restrict__ err) {
-    const DLabel L = labels[0];
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    double v;
-    if (!sample_below<MODE>(L, samp + L.samp_off, seed, rounds[0], (uint32_t)(offset + i), v))
-        atomicOr(err, 1);
-    out[i] = v;
-}
-
-void tpe_launch_sample_only(tpe_ctx* ctx, int mode, int64_t n, int64_t offset, uint64_t seed,
-                            double* out) {
-    const int blocks = (int)((n + kBlock - 1) / kBlock);
-#define TPE_SO(M)                                                                             \
-    hipLaunchKernelGGL(k_sample_only<M>, dim3(blocks), dim3(kBlock), 0, ctx->stream,         \
-                       ctx->labels.p, ctx->samp.p, n, offset, seed, ctx->rounds.p, out,       \
-                       ctx->errflag.p)
-    switch (mode) {
-        case DENSE_GMM: TPE_SO(DENSE_GMM); break;
-        case DENSE_LGMM: TPE_SO(DENSE_LGMM); break;
-        case QUANT_GMM: TPE_SO(QUANT_GMM); break;
-        case QUANT_LGMM: TPE_SO(QUANT_LGMM); break;
-        default: TPE_SO(CAT); break;
-    }
-#undef TPE_SO
-}
