@@ -24,12 +24,20 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-# Executed FP64 FLOPs per (candidate, component) evaluation of each kernel
-# family, counted from the gfx950 ISA of the inner loop (FMA = 2, other f64
-# arithmetic = 1, compares excluded); see DESIGN.md "Roofline".
-FLOPS_PER_EVAL = {'dense_gmm1': 35.0, 'dense_lgmm1': 35.0}
+# Per (candidate, component) evaluation of the dense kernel families, counted
+# from the gfx950 ISA of the inner loop (DESIGN.md "Roofline"):
+#   fp64: v_add, v_mul, v_fma (exponent), v_rndne, v_cvt_i32, v_add (f),
+#         5 x v_fma (2^(f/64) poly), v_mul (table), v_ldexp, v_add (acc)
+#         = 14 fp64 VALU instructions = 20 FLOP with FMA = 2
+#   fp32: v_sub, v_mul, v_fma, v_exp_f32, v_add = 5 VALU instructions, 6 FLOP
+FLOPS_PER_EVAL = {'f64': 20.0, 'f32': 6.0}
+VALU_INSTR_PER_EVAL = {'f64': 14.0, 'f32': 5.0}
 PEAK_FP64_VECTOR_TFLOPS = 78.6        # MI355X spec (MI355X_MICROARCH.md)
 PEAK_FP32_VECTOR_TFLOPS = 157.3
+# wave64 VALU lane-instructions per second at 2.4 GHz: 256 CU x 4 SIMD x
+# (16 fp64 / 32 fp32 lanes per clock)
+PEAK_VALU_LANE_INSTR = {'f64': 256 * 4 * 16 * 2.4e9, 'f32': 256 * 4 * 32 * 2.4e9}
+DENSE = ('dense_gmm1', 'dense_lgmm1')
 
 
 def parse():
@@ -131,14 +139,17 @@ def main():
 
     # roofline of the dominant kernel family (device time from HIP events on
     # the engine's stream, summed over the timed steps)
-    dom = max((k for k in mode_ms if k in FLOPS_PER_EVAL), key=lambda k: mode_ms[k])
+    dom = max((k for k in mode_ms if k in DENSE), key=lambda k: mode_ms[k])
     dom_rate = mode_ev[dom] / (mode_ms[dom] * 1e-3)
-    peak = PEAK_FP64_VECTOR_TFLOPS if args.precision == 'f64' else PEAK_FP32_VECTOR_TFLOPS
-    achieved = dom_rate * FLOPS_PER_EVAL[dom] / 1e12
-    roof = {'bound': 'valu', 'kernel': 'k_round<%s,%s>' % (args.precision, dom),
+    prec = args.precision
+    peak = PEAK_FP64_VECTOR_TFLOPS if prec == 'f64' else PEAK_FP32_VECTOR_TFLOPS
+    achieved = dom_rate * FLOPS_PER_EVAL[prec] / 1e12
+    roof = {'bound': 'valu', 'kernel': 'k_round<%s,%s>' % (prec, dom),
             'achieved': round(achieved, 3), 'peak': peak, 'unit': 'TFLOP/s',
             'frac': round(achieved / peak, 4), 'traffic': None,
-            'evals_per_s': dom_rate, 'flops_per_eval': FLOPS_PER_EVAL[dom],
+            'evals_per_s': dom_rate, 'flops_per_eval': FLOPS_PER_EVAL[prec],
+            'valu_issue_frac': round(dom_rate * VALU_INSTR_PER_EVAL[prec] /
+                                     PEAK_VALU_LANE_INSTR[prec], 4),
             'launch_ms': mode_ms[dom] / args.steps}
     line = {
         'metric': 'TPE candidate x component lpdf evals/sec (10k-trial history)',

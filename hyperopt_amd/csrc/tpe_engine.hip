@@ -117,6 +117,8 @@ __global__ __launch_bounds__(kBlock) void k_round(
     const uint32_t round = rounds[blockIdx.z];
     const int tid = threadIdx.x;
     const int64_t base = (int64_t)blockIdx.x * kTile + tid;
+    __shared__ double exp_tab[64];
+    if constexpr (MODE == DENSE_GMM || MODE == DENSE_LGMM) load_exp_table(exp_tab);
 
     double x[kR], lb[kR], la[kR];
     bool valid[kR];
@@ -138,14 +140,14 @@ __global__ __launch_bounds__(kBlock) void k_round(
     }
 
     if constexpr (MODE == DENSE_GMM) {
-        lse_dense<kR>(comps + L.comp_b, L.nb, L.shift_b, x, lb);
-        lse_dense<kR>(comps + L.comp_a, L.na, L.shift_a, x, la);
+        lse_dense<kR>(comps + L.comp_b, L.nb, L.shift_b, x, lb, exp_tab);
+        lse_dense<kR>(comps + L.comp_a, L.na, L.shift_a, x, la, exp_tab);
     } else if constexpr (MODE == DENSE_LGMM) {
         double y[kR];
 #pragma unroll
         for (int r = 0; r < kR; ++r) y[r] = log(x[r]);
-        lse_dense<kR>(comps + L.comp_b, L.nb, L.shift_b, y, lb);
-        lse_dense<kR>(comps + L.comp_a, L.na, L.shift_a, y, la);
+        lse_dense<kR>(comps + L.comp_b, L.nb, L.shift_b, y, lb, exp_tab);
+        lse_dense<kR>(comps + L.comp_a, L.na, L.shift_a, y, la, exp_tab);
 #pragma unroll
         for (int r = 0; r < kR; ++r) {
             lb[r] -= y[r];
@@ -518,8 +520,10 @@ Folded fold_mixture(int kind, bool quant, int flags, double low, double high, co
     if (!std::isfinite(M)) M = 0.0;
     f.shift = M;
     const double l2e = 1.4426950408889634;
+    const double sK = std::sqrt(kExpScale);
     for (int k = 0; k < n; ++k) {
-        out64[k] = Comp<double>{mu[k], a[k], c[k] - M, w[k]};
+        // fp64 records in exp_scaled units (see tpe_device.h: u = K t)
+        out64[k] = Comp<double>{mu[k], a[k] * sK, (c[k] - M) * kExpScale, w[k]};
         if (out32)
             out32[k] = Comp<float>{(float)mu[k], (float)(a[k] * std::sqrt(l2e)),
                                    (float)((c[k] - M) * l2e), (float)w[k]};
