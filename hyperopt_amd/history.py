@@ -1,0 +1,138 @@
+"""Columnar trial history for `tpe.suggest`.
+
+The reference rebuilds, on every call, the loss of each tid (tpe.py:839-861)
+and the per-label (idxs, vals) lists with a Python loop over all docs and all
+labels (`miscs_to_idxs_vals`, base.py:192-207) -- O(N x L) Python work per
+suggestion.  Here each doc's hyperparameter values are
+ingested once into per-label arrays; a suggestion only re-reads the losses
+(results change as trials finish) and masks the arrays.
+
+Semantics kept from the reference:
+  * group key = misc.get('from_tid', tid); loss None -> +inf; the doc with the
+    smallest loss represents its group; a group whose first loss is NaN is
+    dropped (`loss <= best` is False for NaN, tpe.py:850-853);
+  * docs ordered by group key; observations of a label are the represented
+    docs' misc idxs/vals in that order (the idxs stay the doc's own tid, as
+    in miscs_to_idxs_vals).
+"""
+import math
+import weakref
+
+import numpy as np
+
+
+class _LabelColumn(object):
+    __slots__ = ('tids', 'vals', 'n', 'ptids', 'pvals')
+
+    def __init__(self):
+        self.tids, self.vals = [], []
+        self.n = 0
+        self.ptids = np.zeros(0, dtype=np.int64)
+        self.pvals = np.zeros(0, dtype=np.float64)
+
+    def arrays(self):
+        if len(self.tids) != self.n:
+            self.ptids = np.concatenate([self.ptids, np.asarray(self.tids[self.n:], dtype=np.int64)])
+            self.pvals = np.concatenate([self.pvals, np.asarray(self.vals[self.n:], dtype=np.float64)])
+            self.n = len(self.tids)
+        return self.ptids, self.pvals
+
+
+class HistoryCache(object):
+    def __init__(self, labels):
+        self.labels = list(labels)
+        self.cols = {k: _LabelColumn() for k in self.labels}
+        self.seen = {}          # id(doc) -> doc (keeps ids unique while cached)
+
+    def ingest(self, docs):
+        for d in docs:
+            if id(d) in self.seen:
+                continue
+            self.seen[id(d)] = d
+            m = d['misc']
+            idxs, vals = m['idxs'], m['vals']
+            for k in self.labels:
+                ti = idxs.get(k, [])
+                if ti:
+                    c = self.cols[k]
+                    c.tids.append(ti[0])
+                    c.vals.append(vals[k][0])
+
+    def gather(self, domain, trials):
+        """(tids, losses, obs) where obs[label] = (idxs, vals) arrays."""
+        docs = trials.trials
+        self.ingest(docs)
+        groups = {}
+        any_from = False
+        for d in docs:
+            m = d['misc']
+            g = m.get('from_tid', d['tid'])
+            if g != d['tid']:
+                any_from = True
+            loss = domain.loss(d['result'], d['spec'])
+            loss = float('inf') if loss is None else float(loss)
+            if g not in groups:
+                if loss == loss:                       # NaN never becomes best
+                    groups[g] = (loss, d)
+                else:
+                    groups[g] = (loss, None)
+            else:
+                best_loss, best = groups[g]
+                if loss <= best_loss:
+                    groups[g] = (loss, d)
+        items = sorted((g, v) for g, v in groups.items() if v[1] is not None)
+        tids = np.asarray([g for g, _ in items], dtype=np.int64)
+        losses = np.asarray([v[0] for _, v in items], dtype=np.float64)
+        rep = [v[1] for _, v in items]
+        obs = {}
+        if not any_from:
+            # each doc is its own group: mask the columns to the represented
+            # docs (drops errored / NaN-loss ones) and keep tid order
+            every = len(rep) == len(self.seen)
+            rep_tids = None if every else np.asarray([d['tid'] for d in rep], dtype=np.int64)
+            for k in self.labels:
+                ti, tv = self.cols[k].arrays()
+                if rep_tids is not None:
+                    keep = np.isin(ti, rep_tids)
+                    ti, tv = ti[keep], tv[keep]
+                if len(ti) > 1 and not np.all(ti[1:] > ti[:-1]):
+                    o = np.argsort(ti, kind='stable')
+                    ti, tv = ti[o], tv[o]
+                obs[k] = (ti, tv)
+        else:
+            # general case: restrict to represented docs, keep group order
+            for k in self.labels:
+                ti, tv = [], []
+                for d in rep:
+                    m = d['misc']
+                    x = m['idxs'].get(k, [])
+                    if x:
+                        ti.append(x[0])
+                        tv.append(m['vals'][k][0])
+                obs[k] = (np.asarray(ti, dtype=np.int64), np.asarray(tv, dtype=np.float64))
+        return tids, losses, obs
+
+
+_caches = weakref.WeakKeyDictionary()
+
+
+def gather(domain, trials, labels):
+    key = tuple(labels)
+    try:
+        cache = _caches.get(trials)
+    except TypeError:            # not weak-referenceable: no caching
+        cache = None
+    if cache is None or cache.labels != list(key):
+        cache = HistoryCache(key)
+        try:
+            _caches[trials] = cache
+        except TypeError:
+            pass
+    return cache.gather(domain, trials)
+
+
+def isnan(x):
+    try:
+        return math.isnan(x)
+    except TypeError:
+        return False

@@ -1,0 +1,167 @@
+"""Tree-structured Parzen Estimator: drop-in `tpe.suggest` running on MI355X.
+
+    from hyperopt_amd import fmin, hp, tpe, Trials
+    fmin(fn, space, algo=tpe.suggest, max_evals=100, trials=Trials())
+
+`suggest` keeps the reference's signature, defaults and returned document
+(hyperopt/tpe.py:823-916).  Per call:
+  1. history: tids, losses (None -> +inf, min per from_tid group) and per-label
+     observations, from a columnar cache (history.py);
+  2. fewer than n_startup_jobs docs -> random search (rand.suggest);
+  3. posteriors: split by loss rank + adaptive Parzen mixtures / categorical
+     pseudocounts per label, bit-identical to the reference (posterior.py);
+  4. one fused GPU round over ALL labels (engine.Engine.suggest): sample
+     n_EI_candidates per label from l(x) (Philox, stream = label, counter =
+     candidate index, round = new_id), lpdf under l and g, broadcast_best;
+  5. labels under an un-chosen hp.choice branch are dropped (the reference
+     routes every candidate id to the winning branch, vectorize.py:25-43;
+     labels are independent given the history, so evaluating every branch
+     and keeping the selected one is the same distribution).
+
+Extra keyword arguments (not in the reference): `precision` ('f64' default,
+'f32' fast path), `device` (HIP ordinal), `batch` (True: one independent
+suggestion per new_id instead of only new_ids[0]).
+"""
+import logging
+import time
+
+import numpy as np
+
+from . import engine as _engine
+from . import history as _history
+from . import labels as _labels
+from . import posterior as _post
+from . import rand
+from .base import miscs_update_idxs_vals
+
+logger = logging.getLogger(__name__)
+
+EPS = 1e-12
+DEFAULT_LF = 25
+_default_prior_weight = 1.0
+_default_n_EI_candidates = 24
+_default_gamma = 0.25
+_default_n_startup_jobs = 20
+_default_linear_forgetting = DEFAULT_LF
+
+# host-side restatements, exported under the reference's names
+ap_filter_trials_split = _post.split_history
+adaptive_parzen_normal = _post.adaptive_parzen_normal
+linear_forgetting_weights = _post.linear_forgetting_weights
+
+
+def ap_filter_trials(o_idxs, o_vals, l_idxs, l_vals, gamma, gamma_cap=DEFAULT_LF):
+    """tpe.py:624-648."""
+    bt, at = _post.split_history(l_idxs, l_vals, gamma, gamma_cap)
+    return _post.split_label(o_idxs, o_vals, bt, at)
+
+
+def specs_of(domain):
+    specs = getattr(domain, 'specs', None)
+    if isinstance(specs, dict) and specs and isinstance(next(iter(specs.values())),
+                                                        _labels.LabelSpec):
+        return specs
+    cached = getattr(domain, '_hyperopt_amd_specs', None)
+    if cached is None:
+        cached = _labels.compile_space(domain.expr)
+        try:
+            domain._hyperopt_amd_specs = cached
+        except AttributeError:
+            pass
+    return cached
+
+
+def build_posteriors(domain, trials, prior_weight=_default_prior_weight,
+                     gamma=_default_gamma):
+    """(specs, n_docs, posteriors) for the current history."""
+    specs = specs_of(domain)
+    tids, losses, obs = _history.gather(domain, trials, list(specs))
+    if len(tids) == 0:
+        return specs, 0, None
+    below_tids, above_tids = _post.split_history(tids, losses, gamma)
+    posts = []
+    for label, s in specs.items():
+        oi, ov = obs[label]
+        b, a = _post.split_label(oi, ov, below_tids, above_tids)
+        posts.append(_post.label_posterior(label, s.kind, s.args, b, a, prior_weight))
+    return specs, len(tids), posts
+
+
+def _doc(new_id, domain, trials, specs, values):
+    active = _labels.active_labels(domain.expr, values)
+    idxs = {k: ([new_id] if k in active else []) for k in specs}
+    vals = {k: ([values[k]] if k in active else []) for k in specs}
+    misc = dict(tid=new_id, cmd=domain.cmd, workdir=domain.workdir)
+    miscs_update_idxs_vals([misc], idxs, vals)
+    return trials.new_trial_docs([new_id], [None], [domain.new_result()], [misc])
+
+
+def suggest(new_ids, domain, trials, seed,
+            prior_weight=_default_prior_weight,
+            n_startup_jobs=_default_n_startup_jobs,
+            n_EI_candidates=_default_n_EI_candidates,
+            gamma=_default_gamma,
+            linear_forgetting=_default_linear_forgetting,
+            precision='f64', device=0, batch=False):
+    t0 = time.time()
+    specs, n_docs, posts = build_posteriors(domain, trials, prior_weight, gamma)
+    if n_docs < n_startup_jobs or posts is None:
+        if posts is None and n_startup_jobs <= 0:
+            logger.info('TPE using 0 trials')
+        return rand.suggest(list(new_ids[:1]) if not batch else new_ids, domain, trials, seed)
+    eng = _engine.get_engine(device, precision)
+    eng.set_posterior(*_post.pack(posts))
+    ids = list(new_ids) if batch else [new_ids[0]]
+    if len(ids) == 1:
+        res = eng.suggest(seed, n_EI_candidates, round=ids[0])[None]
+    else:
+        res = eng.suggest_batch(seed, ids, n_EI_candidates)
+    rval = []
+    for j, new_id in enumerate(ids):
+        values = {s.label: _labels.coerce(s.kind, res[j][i]['value'])
+                  for i, s in enumerate(specs.values())}
+        rval.extend(_doc(new_id, domain, trials, specs, values))
+    logger.info('tpe.suggest: %d trials, %d labels, %.1f ms' % (
+        n_docs, len(specs), (time.time() - t0) * 1e3))
+    return rval
+
+
+# -- reference operators on the GPU engine (tpe.py:56-307, 769-778) ----------
+
+def _eng():
+    return _engine.get_engine(0, 'f64')
+
+
+def GMM1_lpdf(samples, weights, mus, sigmas, low=None, high=None, q=None):
+    return _eng().GMM1_lpdf(samples, weights, mus, sigmas, low, high, q)
+
+
+def LGMM1_lpdf(samples, weights, mus, sigmas, low=None, high=None, q=None):
+    return _eng().LGMM1_lpdf(samples, weights, mus, sigmas, low, high, q)
+
+
+def categorical_lpdf(sample, p, upper=None):
+    return _eng().categorical_lpdf(sample, p, upper)
+
+
+def broadcast_best(samples, below_llik, above_llik):
+    return _eng().broadcast_best(samples, below_llik, above_llik)
+
+
+def _seed_from(rng):
+    if rng is None:
+        return np.random.randint(2 ** 31 - 1)
+    return int(rng.randint(2 ** 31 - 1))
+
+
+def GMM1(weights, mus, sigmas, low=None, high=None, q=None, rng=None, size=()):
+    """Draws from the truncated mixture (Philox stream seeded from `rng`)."""
+    out = _eng().GMM1(weights, mus, sigmas, low, high, q, seed=_seed_from(rng),
+                      size=size if size != () else (1,))
+    return out if size != () else out[0]
+
+
+def LGMM1(weights, mus, sigmas, low=None, high=None, q=None, rng=None, size=()):
+    out = _eng().LGMM1(weights, mus, sigmas, low, high, q, seed=_seed_from(rng),
+                       size=size if size != () else (1,))
+    return out if size != () else out[0]

