@@ -52,6 +52,7 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-sample', type=int, default=2048,
                     help='candidates per label in the CPU baseline sample')
+    ap.add_argument('--no-latency', action='store_true')
     return ap.parse_args()
 
 
@@ -79,6 +80,24 @@ def cpu_baseline(hist, posts, n_cand):
     return evals / dt, dt, evals
 
 
+def suggest_latency(n_labels, n_trials, n_reps=20, n_warm=3):
+    """End-to-end tpe.suggest wall time (history gather + posterior build +
+    H2D + fused GPU round + D2H + trial doc) at the reference defaults
+    (n_EI_candidates=24), median of n_reps after n_warm warm-ups."""
+    from hyperopt_amd import tpe
+    from hyperopt_amd.base import Domain
+    from hyperopt_amd.workloads import history_trials, hp_space, mixed_history
+    hist = mixed_history(n_labels, n_trials, seed=0)
+    trials = history_trials(hist)
+    domain = Domain(lambda d: 0.0, hp_space(hist.labels))
+    times = []
+    for i in range(n_warm + n_reps):
+        t0 = time.perf_counter()
+        tpe.suggest([n_trials + i], domain, trials, 1000 + i)
+        times.append(time.perf_counter() - t0)
+    return float(np.median(times[n_warm:])) * 1e3
+
+
 def main():
     args = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -91,7 +110,7 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group('nccl')
     from hyperopt_amd import posterior as P
-    from hyperopt_amd.engine import Engine, RESULT_DTYPE, merge_results
+    from hyperopt_amd.engine import Engine
     from hyperopt_amd.workloads import mixed_history
 
     hist = mixed_history(args.labels, args.trials, seed=0)
@@ -102,14 +121,12 @@ def main():
     C = 1 << args.cand_log2
     L = len(posts)
 
+    from hyperopt_amd.parallel import exchange_winners
+
     def step(i):
         res = eng.suggest(seed=1234 + i, n_candidates=C, round=i, cand_offset=rank * C)
         if dist is not None:   # exchange per-GPU winners (L x 48 B) over RCCL
-            t = torch.from_numpy(res.view(np.uint8).copy()).cuda(local)
-            g = torch.empty(world * t.numel(), dtype=torch.uint8, device=t.device)
-            dist.all_gather_into_tensor(g, t)
-            parts = g.cpu().numpy().view(RESULT_DTYPE).reshape(world, L)
-            res = merge_results(parts)
+            res = exchange_winners(res)
         return res
 
     for i in range(args.warmup):
@@ -164,6 +181,12 @@ def main():
         'per_family_ms': {k: round(v / args.steps, 3) for k, v in mode_ms.items() if v},
         'roofline': roof,
     }
+    if rank == 0 and not args.no_latency:
+        lat = suggest_latency(args.labels, args.trials)
+        line['suggest_latency_ms'] = {
+            'value': round(lat, 3), 'n_EI_candidates': 24, 'history': args.trials,
+            'labels': args.labels, 'note': 'end-to-end tpe.suggest wall time, median of 20; '
+                                           'reference CPU: 1330 ms (BASELINE.md)'}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rate, sec, ev = cpu_baseline(hist, posts, args.cpu_sample)
         line['cpu_baseline'] = {'value': rate, 'unit': 'evals/s', 'cores': 1, 'kind': 'port',

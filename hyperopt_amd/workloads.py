@@ -145,3 +145,48 @@ def conditional_history(n_trials=5000, seed=0):
             loss[clf == bi] += contrib
             obs[name] = (act, v)
     return History(labels, tids, loss, obs)
+
+
+def hp_space(labels):
+    """The hp.* space of a synthetic label list (randint -> hp.choice)."""
+    from . import hp
+    space = {}
+    for name, kind, args in labels:
+        if kind == 'randint':
+            space[name] = hp.choice(name, list(range(int(args['upper']))))
+        else:
+            space[name] = getattr(hp, kind)(name, *[args[k] for k in
+                                                    (('low', 'high', 'q') if 'low' in args
+                                                     else ('mu', 'sigma', 'q')) if k in args])
+    return space
+
+
+def history_trials(hist):
+    """A Trials object holding the synthetic history as finished trial docs."""
+    from .base import JOB_STATE_DONE, STATUS_OK, Trials
+    trials = Trials()
+    names = [n for n, _, _ in hist.labels]
+    cols = {}
+    for n in names:
+        oi, ov = hist.obs[n]
+        cols[n] = dict(zip(oi.tolist(), ov.tolist()))
+    kinds = {n: k for n, k, _ in hist.labels}
+    docs = []
+    for tid, loss in zip(hist.tids.tolist(), hist.losses.tolist()):
+        idxs, vals = {}, {}
+        for n in names:
+            v = cols[n].get(tid)
+            if v is None:
+                idxs[n], vals[n] = [], []
+            else:
+                idxs[n] = [tid]
+                vals[n] = [int(v) if kinds[n] in ('randint', 'categorical') else float(v)]
+        docs.append(dict(state=JOB_STATE_DONE, tid=tid, spec=None,
+                         result={'status': STATUS_OK, 'loss': float(loss)},
+                         misc=dict(tid=tid, cmd=('domain_attachment', 'FMinIter_Domain'),
+                                   workdir=None, idxs=idxs, vals=vals),
+                         exp_key=None, owner=None, version=0, book_time=None,
+                         refresh_time=None))
+    trials._insert_trial_docs(docs)
+    trials.refresh()
+    return trials

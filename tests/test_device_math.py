@@ -1,0 +1,81 @@
+"""Host checks of the device math constants (no GPU): the fp64 exp scheme
+of tpe_device.h (scaled exponent, degree-5 polynomial, 64-entry table) is
+re-evaluated in numpy from the constants parsed out of the header and
+compared with a 60-digit reference; the Philox4x32-10 round function is
+checked against its published known-answer vectors."""
+import os
+import re
+from decimal import Decimal, getcontext
+
+import numpy as np
+
+HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                   'hyperopt_amd', 'csrc', 'tpe_device.h')
+
+
+def _consts():
+    txt = open(HDR).read()
+    num = r'([-+0-9.eEx]+)'
+    scale = float(re.search(r'kExpScale = ' + num, txt).group(1))
+    c = [float(re.search(r'kExpC%d = ' % i + num, txt).group(1)) for i in range(1, 6)]
+    body = re.search(r'kExp2Tab64\[64\] = \{(.*?)\};', txt, re.S).group(1)
+    tab = np.array([float.fromhex(t.strip()) for t in body.split(',') if t.strip()])
+    return scale, c, tab
+
+
+def _exp_scaled(u, c, tab):
+    k = np.rint(u)
+    f = u - k
+    p = c[4] * f + c[3]
+    for j in (2, 1, 0):
+        p = p * f + c[j]
+    p = p * f + 1.0
+    ki = k.astype(np.int64)
+    return np.ldexp(p * tab[ki & 63], (ki >> 6).astype(np.int32))
+
+
+def test_exp_constants_and_accuracy():
+    getcontext().prec = 60
+    ln2 = Decimal(2).ln()
+    scale, c, tab = _consts()
+    assert len(tab) == 64
+    assert scale == float(Decimal(64) / ln2)
+    for i in range(64):
+        assert tab[i] == float(Decimal(2) ** (Decimal(i) / 64))
+    x = ln2 / 64
+    fact = Decimal(1)
+    for n in range(1, 6):
+        fact *= n
+        assert c[n - 1] == float(x ** n / fact)
+    L = np.longdouble(str(ln2))
+    rng = np.random.RandomState(0)
+    for lo in (-1.0, -300.0, -64 * 700 / float(ln2)):
+        u = rng.uniform(lo, 0, 200000)
+        ref = np.exp(u.astype(np.longdouble) * L / 64)
+        rel = np.abs((_exp_scaled(u, c, tab) - ref) / ref)
+        assert float(rel.max()) < 4e-16
+
+
+def _philox(c, k):
+    M0, M1, W0, W1 = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85
+    c = list(c)
+    k0, k1 = k
+    for _ in range(10):
+        p0, p1 = M0 * c[0], M1 * c[2]
+        c = [((p1 >> 32) ^ c[1] ^ k0) & 0xFFFFFFFF, p1 & 0xFFFFFFFF,
+             ((p0 >> 32) ^ c[3] ^ k1) & 0xFFFFFFFF, p0 & 0xFFFFFFFF]
+        k0, k1 = (k0 + W0) & 0xFFFFFFFF, (k1 + W1) & 0xFFFFFFFF
+    return c
+
+
+def test_philox_known_answers():
+    """Random123 kat_vectors for philox4x32-10 -- the round structure used by
+    tpe_device.h:philox4x32_10."""
+    assert _philox([0, 0, 0, 0], [0, 0]) == [0x6627e8d5, 0xe169c58d, 0xbc57ac4c, 0x9b00dbd8]
+    assert _philox([0xffffffff] * 4, [0xffffffff] * 2) == \
+        [0x408f276d, 0x41c83b0e, 0xa20bc7c6, 0x6d5451fd]
+    assert _philox([0x243f6a88, 0x85a308d3, 0x13198a2e, 0x03707344],
+                   [0xa4093822, 0x299f31d0]) == [0xd16cfe09, 0x94fdcceb, 0x5001e420, 0x24126ea1]
+    txt = open(HDR).read()
+    for const in ('0xD2511F53u', '0xCD9E8D57u', '0x9E3779B9u', '0xBB67AE85u'):
+        assert const in txt
