@@ -27,11 +27,14 @@ sys.path.insert(0, REPO)
 # Per (candidate, component) evaluation of the dense kernel families, counted
 # from the gfx950 ISA of the inner loop (DESIGN.md "Roofline"):
 #   fp64: v_add, v_mul, v_fma (exponent), v_rndne, v_cvt_i32, v_add (f),
-#         5 x v_fma (2^(f/64) poly), v_mul (table), v_ldexp, v_add (acc)
-#         = 14 fp64 VALU instructions = 20 FLOP with FMA = 2
+#         3 x v_fma (2^(f/2048) poly), v_mul (table), v_ldexp, v_add (acc)
+#         = 12 fp64 VALU instructions = 16 FLOP with FMA = 2, plus 3 int32
+#         ops (table index, exponent) and one ds_read_b64
 #   fp32: v_sub, v_mul, v_fma, v_exp_f32, v_add = 5 VALU instructions, 6 FLOP
-FLOPS_PER_EVAL = {'f64': 20.0, 'f32': 6.0}
-VALU_INSTR_PER_EVAL = {'f64': 14.0, 'f32': 5.0}
+FLOPS_PER_EVAL = {'f64': 16.0, 'f32': 6.0}
+# issue slots per eval in units of that precision's VALU op (an int32 op
+# issues at twice the fp64 rate)
+VALU_INSTR_PER_EVAL = {'f64': 12.0 + 3 * 0.5, 'f32': 5.0}
 PEAK_FP64_VECTOR_TFLOPS = 78.6        # MI355X spec (MI355X_MICROARCH.md)
 PEAK_FP32_VECTOR_TFLOPS = 157.3
 # wave64 VALU lane-instructions per second at 2.4 GHz: 256 CU x 4 SIMD x

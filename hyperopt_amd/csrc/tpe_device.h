@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "tpe_exp_table.h"
+
 namespace tpe {
 
 constexpr double kEps = 1e-12;  // tpe.py:31
@@ -141,87 +143,18 @@ __device__ __forceinline__ double np_max(double a, double b) { return (a != a ||
 // every component) or is NaN, the lane recomputes the reference's two-pass
 // form (row max first).
 //
-// fp64 records are pre-scaled by K = 64/ln 2 on the host (a' = a sqrt(K),
-// c' = (c - M) K), so the fma that forms the exponent directly yields
-// u = K t <= 0 and exp(t) = 2^(u/64) is evaluated as
+// fp64 records are pre-scaled by K = N/ln 2 (N = 2048, tpe_exp_table.h) on
+// the host (a' = a sqrt(K), c' = (c - M) K), so the fma that forms the
+// exponent directly yields u = K t <= 0, and exp(t) = 2^(u/N) is evaluated as
 //   k = rint(u), f = u - k (exact, |f| <= 1/2),
-//   2^(f/64) by a degree-5 polynomial (|f ln2/64| <= 0.0054: 3.5e-17 truncation),
-//   times 2^((k mod 64)/64) from a 64-entry LDS table, scaled by 2^(k div 64)
-// -- about 1.5 ulp, 15 fp64 operations per (candidate, component) pair
-// instead of the ~23 (plus range selects) of a general-purpose exp.
-constexpr double kExpScale = 92.33248261689366;       // 64 / ln 2
-constexpr double kExpScaleInv = 0.010830424696249145;    // ln 2 / 64
-constexpr double kExpC1 = 0.010830424696249145, kExpC2 = 5.86490495505617e-05, kExpC3 = 2.1173137155464776e-07,
-                 kExpC4 = 5.732851688640402e-10, kExpC5 = 1.2417843701716925e-12;
-
-__constant__ double kExp2Tab64[64] = {
-    0x1.0000000000000p+0,
-    0x1.02c9a3e778061p+0,
-    0x1.059b0d3158574p+0,
-    0x1.0874518759bc8p+0,
-    0x1.0b5586cf9890fp+0,
-    0x1.0e3ec32d3d1a2p+0,
-    0x1.11301d0125b51p+0,
-    0x1.1429aaea92de0p+0,
-    0x1.172b83c7d517bp+0,
-    0x1.1a35beb6fcb75p+0,
-    0x1.1d4873168b9aap+0,
-    0x1.2063b88628cd6p+0,
-    0x1.2387a6e756238p+0,
-    0x1.26b4565e27cddp+0,
-    0x1.29e9df51fdee1p+0,
-    0x1.2d285a6e4030bp+0,
-    0x1.306fe0a31b715p+0,
-    0x1.33c08b26416ffp+0,
-    0x1.371a7373aa9cbp+0,
-    0x1.3a7db34e59ff7p+0,
-    0x1.3dea64c123422p+0,
-    0x1.4160a21f72e2ap+0,
-    0x1.44e086061892dp+0,
-    0x1.486a2b5c13cd0p+0,
-    0x1.4bfdad5362a27p+0,
-    0x1.4f9b2769d2ca7p+0,
-    0x1.5342b569d4f82p+0,
-    0x1.56f4736b527dap+0,
-    0x1.5ab07dd485429p+0,
-    0x1.5e76f15ad2148p+0,
-    0x1.6247eb03a5585p+0,
-    0x1.6623882552225p+0,
-    0x1.6a09e667f3bcdp+0,
-    0x1.6dfb23c651a2fp+0,
-    0x1.71f75e8ec5f74p+0,
-    0x1.75feb564267c9p+0,
-    0x1.7a11473eb0187p+0,
-    0x1.7e2f336cf4e62p+0,
-    0x1.82589994cce13p+0,
-    0x1.868d99b4492edp+0,
-    0x1.8ace5422aa0dbp+0,
-    0x1.8f1ae99157736p+0,
-    0x1.93737b0cdc5e5p+0,
-    0x1.97d829fde4e50p+0,
-    0x1.9c49182a3f090p+0,
-    0x1.a0c667b5de565p+0,
-    0x1.a5503b23e255dp+0,
-    0x1.a9e6b5579fdbfp+0,
-    0x1.ae89f995ad3adp+0,
-    0x1.b33a2b84f15fbp+0,
-    0x1.b7f76f2fb5e47p+0,
-    0x1.bcc1e904bc1d2p+0,
-    0x1.c199bdd85529cp+0,
-    0x1.c67f12e57d14bp+0,
-    0x1.cb720dcef9069p+0,
-    0x1.d072d4a07897cp+0,
-    0x1.d5818dcfba487p+0,
-    0x1.da9e603db3285p+0,
-    0x1.dfc97337b9b5fp+0,
-    0x1.e502ee78b3ff6p+0,
-    0x1.ea4afa2a490dap+0,
-    0x1.efa1bee615a27p+0,
-    0x1.f50765b6e4540p+0,
-    0x1.fa7c1819e90d8p+0};
-
+//   2^(f/N) by a degree-3 polynomial (|f ln2/N| <= 1.7e-4: 3.5e-17 truncation),
+//   times 2^((k mod N)/N) from an N-entry LDS table, scaled by 2^(k div N)
+// -- about 1.5 ulp, 12 fp64 + 3 integer VALU operations per (candidate,
+// component) pair instead of ~23 fp64 (plus range selects) for a general exp.
+// The table costs 16 KB of LDS per workgroup; a wave's 32-lane groups hit
+// ~3.5-way bank conflicts on it whatever its size (bank pair = j mod 32).
 __device__ __forceinline__ void load_exp_table(double* lds) {
-    if (threadIdx.x < 64) lds[threadIdx.x] = kExp2Tab64[threadIdx.x];
+    for (int i = threadIdx.x; i < kExpTabSize; i += blockDim.x) lds[i] = kExp2Tab[i];
     __syncthreads();
 }
 
@@ -229,13 +162,11 @@ __device__ __forceinline__ void load_exp_table(double* lds) {
 __device__ __forceinline__ double exp_scaled(double u, const double* __restrict__ tab) {
     const double k = rint(u);
     const double f = u - k;
-    double p = fma(kExpC5, f, kExpC4);
-    p = fma(p, f, kExpC3);
-    p = fma(p, f, kExpC2);
+    double p = fma(kExpC3, f, kExpC2);
     p = fma(p, f, kExpC1);
     p = fma(p, f, 1.0);
     const int ki = (int)k;
-    return ldexp(p * tab[ki & 63], ki >> 6);
+    return ldexp(p * tab[ki & (kExpTabSize - 1)], ki >> kExpTabBits);
 }
 
 __device__ __forceinline__ double lse_twopass(const Comp<double>* __restrict__ c, int n, double x) {

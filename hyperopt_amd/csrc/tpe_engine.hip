@@ -117,7 +117,7 @@ __global__ __launch_bounds__(kBlock) void k_round(
     const uint32_t round = rounds[blockIdx.z];
     const int tid = threadIdx.x;
     const int64_t base = (int64_t)blockIdx.x * kTile + tid;
-    __shared__ double exp_tab[64];
+    __shared__ double exp_tab[kExpTabSize];
     if constexpr (MODE == DENSE_GMM || MODE == DENSE_LGMM) load_exp_table(exp_tab);
 
     double x[kR], lb[kR], la[kR];

@@ -9,50 +9,57 @@ from decimal import Decimal, getcontext
 
 import numpy as np
 
-HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                   'hyperopt_amd', 'csrc', 'tpe_device.h')
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                    'hyperopt_amd', 'csrc')
+HDR = os.path.join(CSRC, 'tpe_device.h')
+TAB = os.path.join(CSRC, 'tpe_exp_table.h')
 
 
 def _consts():
-    txt = open(HDR).read()
+    txt = open(TAB).read()
     num = r'([-+0-9.eEx]+)'
+    bits = int(re.search(r'kExpTabBits = (\d+)', txt).group(1))
     scale = float(re.search(r'kExpScale = ' + num, txt).group(1))
-    c = [float(re.search(r'kExpC%d = ' % i + num, txt).group(1)) for i in range(1, 6)]
-    body = re.search(r'kExp2Tab64\[64\] = \{(.*?)\};', txt, re.S).group(1)
+    c = [float(m) for m in re.findall(r'kExpC\d = ' + num, txt)]
+    body = re.search(r'kExp2Tab\[\d+\] = \{(.*?)\};', txt, re.S).group(1)
     tab = np.array([float.fromhex(t.strip()) for t in body.split(',') if t.strip()])
-    return scale, c, tab
+    return bits, scale, c, tab
 
 
-def _exp_scaled(u, c, tab):
+def _exp_scaled(u, bits, c, tab):
+    """numpy restatement of tpe_device.h:exp_scaled"""
     k = np.rint(u)
     f = u - k
-    p = c[4] * f + c[3]
-    for j in (2, 1, 0):
-        p = p * f + c[j]
+    p = c[-1]
+    for cj in reversed(c[:-1]):
+        p = p * f + cj
     p = p * f + 1.0
     ki = k.astype(np.int64)
-    return np.ldexp(p * tab[ki & 63], (ki >> 6).astype(np.int32))
+    return np.ldexp(p * tab[ki & ((1 << bits) - 1)], (ki >> bits).astype(np.int32))
 
 
 def test_exp_constants_and_accuracy():
     getcontext().prec = 60
     ln2 = Decimal(2).ln()
-    scale, c, tab = _consts()
-    assert len(tab) == 64
-    assert scale == float(Decimal(64) / ln2)
-    for i in range(64):
-        assert tab[i] == float(Decimal(2) ** (Decimal(i) / 64))
-    x = ln2 / 64
+    bits, scale, c, tab = _consts()
+    N = 1 << bits
+    assert len(tab) == N
+    assert scale == float(Decimal(N) / ln2)
+    for i in range(0, N, 7):
+        assert tab[i] == float(Decimal(2) ** (Decimal(i) / N))
+    x = ln2 / N
     fact = Decimal(1)
-    for n in range(1, 6):
+    for n in range(1, len(c) + 1):
         fact *= n
         assert c[n - 1] == float(x ** n / fact)
+    # truncation error of the polynomial below 1e-16 at |f| = 1/2
+    assert float((x / 2) ** (len(c) + 1) / (fact * (len(c) + 1))) < 1e-16
     L = np.longdouble(str(ln2))
     rng = np.random.RandomState(0)
-    for lo in (-1.0, -300.0, -64 * 700 / float(ln2)):
+    for lo in (-1.0, -300.0, -N * 700 / float(ln2)):
         u = rng.uniform(lo, 0, 200000)
-        ref = np.exp(u.astype(np.longdouble) * L / 64)
-        rel = np.abs((_exp_scaled(u, c, tab) - ref) / ref)
+        ref = np.exp(u.astype(np.longdouble) * L / N)
+        rel = np.abs((_exp_scaled(u, bits, c, tab) - ref) / ref)
         assert float(rel.max()) < 4e-16
 
 
