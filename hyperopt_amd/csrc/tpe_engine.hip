@@ -79,26 +79,78 @@ __device__ __forceinline__ void block_maxloc(uint64_t bk, int64_t bi, double bv,
     }
 }
 
+// ------------------------------------------------------------ slot maps ----
+// Where slot r of a thread lives.  Tile map (pbits == 0): one round per
+// grid.z, that round's candidates spread over the workgroup (large C).
+// Group map (pbits > 0): P = 2^pbits <= 64 consecutive lanes per round, rounds
+// packed along grid.x -- batched rounds with small C (e.g. 4096 new_ids x 24
+// candidates) keep every lane busy and reduce inside the wave.
+struct Slots {
+    int32_t pbits;
+    int32_t n_rounds;
+
+    __device__ __forceinline__ void at(int r, int64_t n, int64_t& z, int64_t& i,
+                                       bool& valid) const {
+        const int64_t q = (int64_t)blockIdx.x * kTile + r * kBlock + threadIdx.x;
+        if (pbits == 0) {
+            z = blockIdx.z;
+            i = q;
+            valid = i < n;
+        } else {
+            z = q >> pbits;
+            i = q & ((1 << pbits) - 1);
+            valid = i < n && z < n_rounds;
+        }
+    }
+};
+
+// broadcast_best epilogue for either map: block maxloc into the tile's
+// partial, or per-round maxloc over each P-lane group written by its leader.
 template <int R>
-__device__ __forceinline__ void thread_best(const double (&x)[R], const double (&lb)[R],
-                                            const double (&la)[R], const bool (&valid)[R],
-                                            int64_t gbase, uint64_t& bk, int64_t& bi, double& bv,
-                                            double& bl, double& ba) {
-    bk = 0;
-    bi = INT64_MAX;
-    bv = bl = ba = 0.0;
+__device__ __forceinline__ void finish_slots(const Slots& S, const double (&x)[R],
+                                             const double (&lb)[R], const double (&la)[R],
+                                             const bool (&valid)[R], const int64_t (&z)[R],
+                                             const int64_t (&gi)[R], int li, int32_t n_labels,
+                                             int32_t tiles, Partial* __restrict__ partials) {
+    if (S.pbits == 0) {
+        uint64_t bk = 0;
+        int64_t bi = INT64_MAX;
+        double bv = 0.0, bl = 0.0, ba = 0.0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (!valid[r]) continue;
+            const uint64_t key = order_key(lb[r] - la[r]);
+            if (better(key, gi[r], bk, bi)) {
+                bk = key;
+                bi = gi[r];
+                bv = x[r];
+                bl = lb[r];
+                ba = la[r];
+            }
+        }
+        block_maxloc(bk, bi, bv, bl, ba,
+                     partials + ((size_t)blockIdx.z * n_labels + li) * tiles + blockIdx.x);
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        if (!valid[r]) continue;
-        const uint64_t key = order_key(lb[r] - la[r]);
-        const int64_t gi = gbase + r * kBlock;
-        if (better(key, gi, bk, bi)) {
-            bk = key;
-            bi = gi;
-            bv = x[r];
-            bl = lb[r];
-            ba = la[r];
+        uint64_t bk = valid[r] ? order_key(lb[r] - la[r]) : 0;
+        int64_t bi = valid[r] ? gi[r] : INT64_MAX;
+        double bv = x[r], bl = lb[r], ba = la[r];
+        for (int off = (1 << S.pbits) >> 1; off > 0; off >>= 1) {
+            const uint64_t ok = __shfl_xor(bk, off);
+            const int64_t oi = __shfl_xor(bi, off);
+            const double ov = __shfl_xor(bv, off), ol = __shfl_xor(bl, off), oa = __shfl_xor(ba, off);
+            if (better(ok, oi, bk, bi)) {
+                bk = ok;
+                bi = oi;
+                bv = ov;
+                bl = ol;
+                ba = oa;
+            }
         }
+        if ((threadIdx.x & ((1 << S.pbits) - 1)) == 0 && z[r] < S.n_rounds)
+            partials[(size_t)z[r] * n_labels + li] = Partial{bk, bi, bv, bl, ba};
     }
 }
 
@@ -111,29 +163,27 @@ __global__ __launch_bounds__(kBlock) void k_round(
     const SampRec* __restrict__ samp, const double* __restrict__ cand_in, int64_t n,
     int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, int32_t n_labels,
     int32_t tiles, Partial* __restrict__ partials, double* __restrict__ out_lb,
-    double* __restrict__ out_la, int32_t* __restrict__ err) {
+    double* __restrict__ out_la, int32_t* __restrict__ err, Slots S) {
     const int li = group[blockIdx.y];
     const DLabel L = labels[li];
-    const uint32_t round = rounds[blockIdx.z];
-    const int tid = threadIdx.x;
-    const int64_t base = (int64_t)blockIdx.x * kTile + tid;
     __shared__ double exp_tab[kExpTabSize];
     if constexpr (MODE == DENSE_GMM || MODE == DENSE_LGMM) load_exp_table(exp_tab);
 
     double x[kR], lb[kR], la[kR];
+    int64_t z[kR], ci[kR], gi[kR];
     bool valid[kR];
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
-        const int64_t i = base + r * kBlock;
-        valid[r] = i < n;
+        S.at(r, n, z[r], ci[r], valid[r]);
+        gi[r] = cand_offset + ci[r];
         double v = (MODE == DENSE_LGMM || MODE == QUANT_LGMM) ? 1.0 : 0.0;
         if (valid[r]) {
             if constexpr (SAMPLE) {
-                if (!sample_below<MODE>(L, samp + L.samp_off, seed, round,
-                                        (uint32_t)(cand_offset + i), v))
+                if (!sample_below<MODE>(L, samp + L.samp_off, seed, rounds[z[r]],
+                                        (uint32_t)gi[r], v))
                     atomicOr(err, 1);
             } else {
-                v = cand_in[i];
+                v = cand_in[ci[r]];
             }
         }
         x[r] = v;
@@ -175,20 +225,15 @@ __global__ __launch_bounds__(kBlock) void k_round(
     }
 
     if (out_lb) {
-        const size_t row = ((size_t)blockIdx.z * n_labels + li) * (size_t)n;
 #pragma unroll
         for (int r = 0; r < kR; ++r)
             if (valid[r]) {
-                out_lb[row + base + r * kBlock] = lb[r];
-                out_la[row + base + r * kBlock] = la[r];
+                const size_t row = ((size_t)z[r] * n_labels + li) * (size_t)n;
+                out_lb[row + ci[r]] = lb[r];
+                out_la[row + ci[r]] = la[r];
             }
     }
-    uint64_t bk;
-    int64_t bi;
-    double bv, bl, ba;
-    thread_best<kR>(x, lb, la, valid, cand_offset + base, bk, bi, bv, bl, ba);
-    block_maxloc(bk, bi, bv, bl, ba,
-                 partials + ((size_t)blockIdx.z * n_labels + li) * tiles + blockIdx.x);
+    finish_slots<kR>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials);
 }
 
 // Quantized families, pass 1: draw every candidate, keep its grid index
@@ -200,39 +245,38 @@ __global__ __launch_bounds__(kBlock) void k_qsample(
     const SampRec* __restrict__ samp, int64_t n, int64_t cand_offset, uint64_t seed,
     const uint32_t* __restrict__ rounds, int32_t nq, int32_t qbase, int64_t* __restrict__ qj,
     unsigned long long* __restrict__ qmin, unsigned long long* __restrict__ qmax,
-    int32_t* __restrict__ err) {
+    int32_t* __restrict__ err, Slots S) {
     const int li = group[blockIdx.y];
     const DLabel L = labels[li];
-    const uint32_t round = rounds[blockIdx.z];
-    const size_t slot = (size_t)blockIdx.z * nq + qbase + blockIdx.y;
-    int64_t* out = qj + slot * (size_t)n;
-    unsigned long long mn = ~0ull, mx = 0ull;
-    const int64_t base = (int64_t)blockIdx.x * kTile + threadIdx.x;
+    const int width = S.pbits ? (1 << S.pbits) : 64;   // lanes sharing one (round, label)
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
-        const int64_t i = base + r * kBlock;
-        if (i >= n) continue;
-        double v;
-        if (!sample_raw<MODE>(L, samp + L.samp_off, seed, round, (uint32_t)(cand_offset + i), v))
-            atomicOr(err, 1);
-        const double jd = rint(v / L.q);
-        int64_t j = 0;
-        if (jd >= -0x1.0p52 && jd <= 0x1.0p52) j = (int64_t)jd;
-        else atomicOr(err, 8);
-        out[i] = j;
-        const unsigned long long u = (unsigned long long)j ^ 0x8000000000000000ull;
-        mn = u < mn ? u : mn;
-        mx = u > mx ? u : mx;
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const unsigned long long a = __shfl_xor(mn, off), b = __shfl_xor(mx, off);
-        mn = a < mn ? a : mn;
-        mx = b > mx ? b : mx;
-    }
-    if ((threadIdx.x & 63) == 0) {
-        atomicMin(qmin + slot, mn);
-        atomicMax(qmax + slot, mx);
+        int64_t z, i;
+        bool valid;
+        S.at(r, n, z, i, valid);
+        unsigned long long mn = ~0ull, mx = 0ull;
+        if (valid) {
+            double v;
+            if (!sample_raw<MODE>(L, samp + L.samp_off, seed, rounds[z],
+                                  (uint32_t)(cand_offset + i), v))
+                atomicOr(err, 1);
+            const double jd = rint(v / L.q);
+            int64_t j = 0;
+            if (jd >= -0x1.0p52 && jd <= 0x1.0p52) j = (int64_t)jd;
+            else atomicOr(err, 8);
+            qj[((size_t)z * nq + qbase + blockIdx.y) * (size_t)n + i] = j;
+            mn = mx = (unsigned long long)j ^ 0x8000000000000000ull;
+        }
+        for (int off = width >> 1; off > 0; off >>= 1) {
+            const unsigned long long a = __shfl_xor(mn, off), b = __shfl_xor(mx, off);
+            mn = a < mn ? a : mn;
+            mx = b > mx ? b : mx;
+        }
+        if ((threadIdx.x & (width - 1)) == 0 && mn <= mx) {
+            const size_t slot = (size_t)z * nq + qbase + blockIdx.y;
+            atomicMin(qmin + slot, mn);
+            atomicMax(qmax + slot, mx);
+        }
     }
 }
 
@@ -267,20 +311,19 @@ __global__ __launch_bounds__(kBlock) void k_qscan(
     const Comp<double>* __restrict__ comps64, const int64_t* __restrict__ qj,
     const QInfo* __restrict__ qinfo, const double2* __restrict__ tab, int64_t n,
     int64_t cand_offset, int32_t nq, int32_t qbase, int32_t n_labels, int32_t tiles,
-    Partial* __restrict__ partials) {
+    Partial* __restrict__ partials, Slots S) {
     const int li = group[blockIdx.y];
     const DLabel L = labels[li];
-    const size_t slot = (size_t)blockIdx.z * nq + qbase + blockIdx.y;
-    const QInfo Q = qinfo[slot];
-    const int64_t* js = qj + slot * (size_t)n;
-    const int64_t base = (int64_t)blockIdx.x * kTile + threadIdx.x;
     double x[kR], lb[kR], la[kR];
+    int64_t z[kR], ci[kR], gi[kR];
     bool valid[kR];
 #pragma unroll
     for (int r = 0; r < kR; ++r) {
-        const int64_t i = base + r * kBlock;
-        valid[r] = i < n;
-        const int64_t j = valid[r] ? js[i] : Q.jmin;
+        S.at(r, n, z[r], ci[r], valid[r]);
+        gi[r] = cand_offset + ci[r];
+        const size_t slot = (size_t)(valid[r] ? z[r] : 0) * nq + qbase + blockIdx.y;
+        const QInfo Q = qinfo[slot];
+        const int64_t j = valid[r] ? qj[slot * (size_t)n + ci[r]] : Q.jmin;
         x[r] = (double)j * L.q;
         const int64_t s = j - Q.jmin;
         if (s >= 0 && s < Q.G) {
@@ -295,12 +338,7 @@ __global__ __launch_bounds__(kBlock) void k_qscan(
             la[r] = quant_lpdf<MODE == QUANT_LGMM>(comps64 + L.comp_a, L.na, ub, lo, L.logpacc_a);
         }
     }
-    uint64_t bk;
-    int64_t bi;
-    double bv, bl, ba;
-    thread_best<kR>(x, lb, la, valid, cand_offset + base, bk, bi, bv, bl, ba);
-    block_maxloc(bk, bi, bv, bl, ba,
-                 partials + ((size_t)blockIdx.z * n_labels + li) * tiles + blockIdx.x);
+    finish_slots<kR>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials);
 }
 
 __global__ __launch_bounds__(kBlock) void k_reduce(const Partial* __restrict__ partials,
@@ -549,9 +587,11 @@ struct Groups {
 struct RoundArgs {
     int64_t n, cand_offset;
     uint64_t seed;
-    int32_t n_rounds, tiles;
+    int32_t n_rounds, tiles;   // tiles: partials per (round, label)
     const double* cand_in;
     double *olb, *ola;
+    Slots S;                   // slot map (tile or grouped)
+    uint32_t gx, gz;           // grid.x / grid.z of the per-candidate kernels
 };
 
 void bracket(tpe_ctx* ctx, int mode, int which) {
@@ -566,10 +606,11 @@ void launch_round(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
     bracket(ctx, MODE, 0);
     const Comp<T>* comps;
     if constexpr (sizeof(T) == 8) comps = ctx->comps64.p; else comps = ctx->comps32.p;
-    hipLaunchKernelGGL((k_round<T, MODE, SAMPLE>), dim3(a.tiles, nl, a.n_rounds), dim3(kBlock), 0,
+    hipLaunchKernelGGL((k_round<T, MODE, SAMPLE>), dim3(a.gx, nl, a.gz), dim3(kBlock), 0,
                        ctx->stream, ctx->labels.p, g.dev[MODE], comps, ctx->comps64.p,
                        ctx->samp.p, a.cand_in, a.n, a.cand_offset, a.seed, ctx->rounds.p,
-                       ctx->n_labels, a.tiles, ctx->partials.p, a.olb, a.ola, ctx->errflag.p);
+                       ctx->n_labels, a.tiles, ctx->partials.p, a.olb, a.ola, ctx->errflag.p,
+                       a.S);
     bracket(ctx, MODE, 1);
 }
 
@@ -587,15 +628,15 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
     HIPCHK(ctx, hipMemsetAsync(ctx->qmm.p, 0xFF, slots * sizeof(unsigned long long), ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->qmm.p + slots, 0, slots * sizeof(unsigned long long), ctx->stream));
     if (nqg)
-        hipLaunchKernelGGL(k_qsample<QUANT_GMM>, dim3(a.tiles, nqg, a.n_rounds), dim3(kBlock), 0,
+        hipLaunchKernelGGL(k_qsample<QUANT_GMM>, dim3(a.gx, nqg, a.gz), dim3(kBlock), 0,
                            ctx->stream, ctx->labels.p, g.dev[QUANT_GMM], ctx->samp.p, a.n,
                            a.cand_offset, a.seed, ctx->rounds.p, nq, 0, ctx->qj.p, ctx->qmm.p,
-                           ctx->qmm.p + slots, ctx->errflag.p);
+                           ctx->qmm.p + slots, ctx->errflag.p, a.S);
     if (nql)
-        hipLaunchKernelGGL(k_qsample<QUANT_LGMM>, dim3(a.tiles, nql, a.n_rounds), dim3(kBlock), 0,
+        hipLaunchKernelGGL(k_qsample<QUANT_LGMM>, dim3(a.gx, nql, a.gz), dim3(kBlock), 0,
                            ctx->stream, ctx->labels.p, g.dev[QUANT_LGMM], ctx->samp.p, a.n,
                            a.cand_offset, a.seed, ctx->rounds.p, nq, nqg, ctx->qj.p, ctx->qmm.p,
-                           ctx->qmm.p + slots, ctx->errflag.p);
+                           ctx->qmm.p + slots, ctx->errflag.p, a.S);
     HIPCHK(ctx, hipGetLastError());
     std::vector<unsigned long long> mm(2 * slots);
     HIPCHK(ctx, hipMemcpyAsync(mm.data(), ctx->qmm.p, 2 * slots * sizeof(unsigned long long),
@@ -638,17 +679,17 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
                                    ctx->labels.p, g.dev[mode], ctx->comps64.p, ctx->qinfo.p, nq,
                                    qbase, ctx->qtab.p);
         }
-        dim3 sg(a.tiles, cnt, a.n_rounds);
+        dim3 sg(a.gx, cnt, a.gz);
         if (fam)
             hipLaunchKernelGGL(k_qscan<QUANT_LGMM>, sg, dim3(kBlock), 0, ctx->stream, ctx->labels.p,
                                g.dev[mode], ctx->comps64.p, ctx->qj.p, ctx->qinfo.p, ctx->qtab.p,
                                a.n, a.cand_offset, nq, qbase, ctx->n_labels, a.tiles,
-                               ctx->partials.p);
+                               ctx->partials.p, a.S);
         else
             hipLaunchKernelGGL(k_qscan<QUANT_GMM>, sg, dim3(kBlock), 0, ctx->stream, ctx->labels.p,
                                g.dev[mode], ctx->comps64.p, ctx->qj.p, ctx->qinfo.p, ctx->qtab.p,
                                a.n, a.cand_offset, nq, qbase, ctx->n_labels, a.tiles,
-                               ctx->partials.p);
+                               ctx->partials.p, a.S);
         bracket(ctx, mode, 1);
     }
     HIPCHK(ctx, hipGetLastError());
@@ -662,7 +703,23 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     if (n < 0 || n_rounds <= 0) return ctx->fail(TPE_ERR_ARG, "bad candidate/round count");
     if (cand_offset < 0 || cand_offset + n > (int64_t)UINT32_MAX)
         return ctx->fail(TPE_ERR_ARG, "candidate indices must stay below 2^32");
-    const int32_t tiles = (int32_t)((n + kTile - 1) / kTile);
+    // slot map: grouped (P = 2^pbits lanes per round) for small candidate
+    // sets, tiled otherwise
+    Slots S{0, n_rounds};
+    int32_t tiles;
+    uint32_t gx, gz;
+    if (n > 0 && n <= 64) {
+        int pb = 1;
+        while ((1 << pb) < n) ++pb;
+        S.pbits = pb;
+        tiles = 1;
+        gx = (uint32_t)(((int64_t)n_rounds * (1 << pb) + kTile - 1) / kTile);
+        gz = 1;
+    } else {
+        tiles = (int32_t)((n + kTile - 1) / kTile);
+        gx = (uint32_t)tiles;
+        gz = (uint32_t)n_rounds;
+    }
     const int32_t L = ctx->n_labels;
     HIPCHK(ctx, ctx->partials.reserve((size_t)n_rounds * L * std::max(tiles, 1)));
     HIPCHK(ctx, ctx->results.reserve((size_t)n_rounds * L));
@@ -688,7 +745,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         g.dev[m] = ctx->one_group.p;
         g.count[m] = 1;
     }
-    RoundArgs a{n, cand_offset, seed, n_rounds, tiles, cand_in_dev, olb, ola};
+    RoundArgs a{n, cand_offset, seed, n_rounds, tiles, cand_in_dev, olb, ola, S, gx, gz};
     const bool sample = cand_in_dev == nullptr;
     int64_t evals_q[2] = {0, 0};
     HIPCHK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
