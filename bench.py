@@ -49,6 +49,12 @@ def parse():
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--precision', default='f64', choices=['f64', 'f32'])
+    ap.add_argument('--config', type=int, default=3, choices=[2, 3, 5],
+                    help='BASELINE.json config: 3 (headline, default), 2 (Hartmann-6, 2k '
+                         'history, 2^20 candidates), 5 (128 labels, 50k history, batched '
+                         'new_ids x 24 candidates)')
+    ap.add_argument('--rounds-per-gpu', type=int, default=512,
+                    help='config 5: new_ids per GPU per step (4096 over 8 GPUs)')
     ap.add_argument('--labels', type=int, default=32)
     ap.add_argument('--trials', type=int, default=10000)
     ap.add_argument('--cand-log2', type=int, default=21)
@@ -118,6 +124,17 @@ def measured_traffic(kernel_prefix):
     return None, None
 
 
+def workload_name(args, C):
+    if args.config == 2:
+        return 'config2: Hartmann-6 over hp.uniform, N=2000 history, 2^20 EI candidates ' \
+               'per label per GPU'
+    if args.config == 5:
+        return 'config5: 128-dim mixed space, N=50000 history, %d new_ids per GPU per step ' \
+               'x 24 EI candidates' % args.rounds_per_gpu
+    return 'config3: %d-dim mixed space, N=%d history, 2^%d EI candidates per label per GPU' % (
+        args.labels, args.trials, args.cand_log2)
+
+
 def main():
     args = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -132,19 +149,32 @@ def main():
         dist.init_process_group(args.dist_backend)
     from hyperopt_amd import posterior as P
     from hyperopt_amd.engine import Engine
-    from hyperopt_amd.workloads import mixed_history
+    from hyperopt_amd.workloads import hartmann_history, mixed_history
 
-    hist = mixed_history(args.labels, args.trials, seed=0)
+    if args.config == 2:
+        args.labels, args.trials, args.cand_log2 = 6, 2000, 20
+        hist = hartmann_history(args.trials, seed=0)
+    elif args.config == 5:
+        args.labels, args.trials = 128, 50000
+        hist = mixed_history(args.labels, args.trials, seed=0)
+    else:
+        hist = mixed_history(args.labels, args.trials, seed=0)
+    t_post = time.perf_counter()
     posts = hist.posteriors()
     descs, w, m, s = P.pack(posts)
+    t_post = time.perf_counter() - t_post
     eng = Engine(local, args.precision)
     eng.set_posterior(descs, w, m, s)
-    C = 1 << args.cand_log2
+    C = 24 if args.config == 5 else 1 << args.cand_log2
     L = len(posts)
 
     from hyperopt_amd.parallel import exchange_winners
 
     def step(i):
+        if args.config == 5:   # independent new_ids sharded over GPUs: no collective
+            ids = [(i * world + rank) * args.rounds_per_gpu + k
+                   for k in range(args.rounds_per_gpu)]
+            return eng.suggest_batch(seed=1234, rounds=ids, n_candidates=C)
         res = eng.suggest(seed=1234 + i, n_candidates=C, round=i, cand_offset=rank * C)
         if dist is not None:   # exchange per-GPU winners (L x 48 B) over RCCL
             res = exchange_winners(res)
@@ -199,20 +229,23 @@ def main():
         'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3,
         'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
         'dtype': args.precision, 'data': 'synthetic (prior draws, seed 0)',
-        'config': {'workload': 'config3: %d-dim mixed space, N=%d history, 2^%d EI candidates '
-                               'per label per GPU' % (args.labels, args.trials, args.cand_log2),
+        'config': {'workload': workload_name(args, C),
                    'labels': L, 'history': args.trials, 'candidates_per_label_per_gpu': C,
-                   'parallelism': 'candidate-sharded x%d' % world},
+                   'parallelism': ('new_id-sharded x%d' if args.config == 5
+                                   else 'candidate-sharded x%d') % world},
+        'host_posterior_build_ms': round(t_post * 1e3, 2),
         'per_family_ms': {k: round(v / args.steps, 3) for k, v in mode_ms.items() if v},
         'roofline': roof,
     }
-    if rank == 0 and not args.no_latency:
+    if args.config == 5:
+        line['config']['new_ids_per_gpu_per_step'] = args.rounds_per_gpu
+    if rank == 0 and not args.no_latency and args.config == 3:
         lat = suggest_latency(args.labels, args.trials)
         line['suggest_latency_ms'] = {
             'value': round(lat, 3), 'n_EI_candidates': 24, 'history': args.trials,
             'labels': args.labels, 'note': 'end-to-end tpe.suggest wall time, median of 20; '
                                            'reference CPU: 1330 ms (BASELINE.md)'}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == 3:
         rate, sec, ev = cpu_baseline(hist, posts, args.cpu_sample)
         line['cpu_baseline'] = {'value': rate, 'unit': 'evals/s', 'cores': 1, 'kind': 'port',
                                 'sample': 'all %d labels x %d candidates (of 2^%d) sampled, '
