@@ -272,10 +272,9 @@ __global__ __launch_bounds__(kBlock) void k_qsample(
             mn = a < mn ? a : mn;
             mx = b > mx ? b : mx;
         }
-        if ((threadIdx.x & (width - 1)) == 0 && mn <= mx) {
-            const size_t slot = (size_t)z * nq + qbase + blockIdx.y;
-            atomicMin(qmin + slot, mn);
-            atomicMax(qmax + slot, mx);
+        if ((threadIdx.x & (width - 1)) == 0 && mn <= mx) {   // window per label, all rounds
+            atomicMin(qmin + qbase + blockIdx.y, mn);
+            atomicMax(qmax + qbase + blockIdx.y, mx);
         }
     }
 }
@@ -289,7 +288,7 @@ __global__ __launch_bounds__(kBlock) void k_qtable(
     int32_t qbase, double2* __restrict__ tab) {
     const int li = group[blockIdx.y];
     const DLabel L = labels[li];
-    const QInfo Q = qinfo[(size_t)blockIdx.z * nq + qbase + blockIdx.y];
+    const QInfo Q = qinfo[qbase + blockIdx.y];
     const int lane = threadIdx.x & 63;
     const int64_t s = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     if (s >= Q.G) return;
@@ -321,8 +320,8 @@ __global__ __launch_bounds__(kBlock) void k_qscan(
     for (int r = 0; r < kR; ++r) {
         S.at(r, n, z[r], ci[r], valid[r]);
         gi[r] = cand_offset + ci[r];
+        const QInfo Q = qinfo[qbase + blockIdx.y];         // window shared by all rounds
         const size_t slot = (size_t)(valid[r] ? z[r] : 0) * nq + qbase + blockIdx.y;
-        const QInfo Q = qinfo[slot];
         const int64_t j = valid[r] ? qj[slot * (size_t)n + ci[r]] : Q.jmin;
         x[r] = (double)j * L.q;
         const int64_t s = j - Q.jmin;
@@ -621,46 +620,47 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
     const int nq = nqg + nql;
     evals_q[0] = evals_q[1] = 0;
     if (nq == 0 || a.tiles == 0) return TPE_OK;
-    const size_t slots = (size_t)a.n_rounds * nq;
+    const size_t slots = (size_t)a.n_rounds * nq;   // candidate rows
     HIPCHK(ctx, ctx->qj.reserve(slots * (size_t)a.n));
-    HIPCHK(ctx, ctx->qmm.reserve(2 * slots));
-    HIPCHK(ctx, ctx->qinfo.reserve(slots));
-    HIPCHK(ctx, hipMemsetAsync(ctx->qmm.p, 0xFF, slots * sizeof(unsigned long long), ctx->stream));
-    HIPCHK(ctx, hipMemsetAsync(ctx->qmm.p + slots, 0, slots * sizeof(unsigned long long), ctx->stream));
+    HIPCHK(ctx, ctx->qmm.reserve(2 * (size_t)nq));
+    HIPCHK(ctx, ctx->qinfo.reserve(nq));
+    HIPCHK(ctx, hipMemsetAsync(ctx->qmm.p, 0xFF, nq * sizeof(unsigned long long), ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(ctx->qmm.p + nq, 0, nq * sizeof(unsigned long long), ctx->stream));
     if (nqg)
         hipLaunchKernelGGL(k_qsample<QUANT_GMM>, dim3(a.gx, nqg, a.gz), dim3(kBlock), 0,
                            ctx->stream, ctx->labels.p, g.dev[QUANT_GMM], ctx->samp.p, a.n,
                            a.cand_offset, a.seed, ctx->rounds.p, nq, 0, ctx->qj.p, ctx->qmm.p,
-                           ctx->qmm.p + slots, ctx->errflag.p, a.S);
+                           ctx->qmm.p + nq, ctx->errflag.p, a.S);
     if (nql)
         hipLaunchKernelGGL(k_qsample<QUANT_LGMM>, dim3(a.gx, nql, a.gz), dim3(kBlock), 0,
                            ctx->stream, ctx->labels.p, g.dev[QUANT_LGMM], ctx->samp.p, a.n,
                            a.cand_offset, a.seed, ctx->rounds.p, nq, nqg, ctx->qj.p, ctx->qmm.p,
-                           ctx->qmm.p + slots, ctx->errflag.p, a.S);
+                           ctx->qmm.p + nq, ctx->errflag.p, a.S);
     HIPCHK(ctx, hipGetLastError());
-    std::vector<unsigned long long> mm(2 * slots);
-    HIPCHK(ctx, hipMemcpyAsync(mm.data(), ctx->qmm.p, 2 * slots * sizeof(unsigned long long),
+    std::vector<unsigned long long> mm(2 * (size_t)nq);
+    HIPCHK(ctx, hipMemcpyAsync(mm.data(), ctx->qmm.p, 2 * nq * sizeof(unsigned long long),
                                hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    // table window per (round, label): worth it when the grid is narrower
-    // than the candidate set (each slot costs one candidate's work)
-    std::vector<QInfo> qi(slots);
+    // one table per label, shared by every round (the posterior does not
+    // depend on the round); worth it when the label's grid window is smaller
+    // than half its candidates over all rounds (each slot costs one
+    // candidate's work)
+    std::vector<QInfo> qi(nq);
     int64_t tab = 0, maxG = 0;
-    const int64_t cap = std::max<int64_t>(a.n / 2, 4096);
-    for (size_t s = 0; s < slots; ++s) {
-        const int64_t jmin = (int64_t)(mm[s] ^ 0x8000000000000000ull);
-        const int64_t jmax = (int64_t)(mm[slots + s] ^ 0x8000000000000000ull);
-        const int64_t G = (mm[s] <= mm[slots + s]) ? jmax - jmin + 1 : 0;
-        qi[s] = QInfo{jmin, (ctx->dedup && G > 0 && G <= cap) ? G : 0, tab, 0};
-        tab += qi[s].G;
-        maxG = std::max(maxG, qi[s].G);
-        const int qpos = (int)(s % nq);
+    const int64_t total = a.n * (int64_t)a.n_rounds;
+    for (int qpos = 0; qpos < nq; ++qpos) {
+        const int64_t jmin = (int64_t)(mm[qpos] ^ 0x8000000000000000ull);
+        const int64_t jmax = (int64_t)(mm[nq + qpos] ^ 0x8000000000000000ull);
+        const int64_t G = (mm[qpos] <= mm[nq + qpos]) ? jmax - jmin + 1 : 0;
+        qi[qpos] = QInfo{jmin, (ctx->dedup && G > 0 && 2 * G <= total) ? G : 0, tab, 0};
+        tab += qi[qpos].G;
+        maxG = std::max(maxG, qi[qpos].G);
         const int li = qpos < nqg ? ctx->h_group[QUANT_GMM][qpos] : ctx->h_group[QUANT_LGMM][qpos - nqg];
         const DLabel& d = ctx->h_labels[li];
-        evals_q[qpos < nqg ? 0 : 1] += (qi[s].G ? qi[s].G : a.n) * (int64_t)(d.nb + d.na);
+        evals_q[qpos < nqg ? 0 : 1] += (qi[qpos].G ? qi[qpos].G : total) * (int64_t)(d.nb + d.na);
     }
     HIPCHK(ctx, ctx->qtab.reserve(std::max<int64_t>(tab, 1)));
-    HIPCHK(ctx, hipMemcpyAsync(ctx->qinfo.p, qi.data(), slots * sizeof(QInfo),
+    HIPCHK(ctx, hipMemcpyAsync(ctx->qinfo.p, qi.data(), nq * sizeof(QInfo),
                                hipMemcpyHostToDevice, ctx->stream));
     for (int fam = 0; fam < 2; ++fam) {
         const int mode = fam ? QUANT_LGMM : QUANT_GMM;
@@ -669,7 +669,7 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
         if (!cnt) continue;
         bracket(ctx, mode, 0);
         if (maxG > 0) {
-            dim3 tg((unsigned)((maxG + kBlock / 64 - 1) / (kBlock / 64)), cnt, a.n_rounds);
+            dim3 tg((unsigned)((maxG + kBlock / 64 - 1) / (kBlock / 64)), cnt, 1);
             if (fam)
                 hipLaunchKernelGGL(k_qtable<QUANT_LGMM>, tg, dim3(kBlock), 0, ctx->stream,
                                    ctx->labels.p, g.dev[mode], ctx->comps64.p, ctx->qinfo.p, nq,

@@ -275,6 +275,17 @@ def test_quantized_dedup_equals_direct(eng, monkeypatch):
     q_fast = stats['quant_gmm1'][1] + stats['quant_lgmm1'][1]
     q_slow = slow_stats['quant_gmm1'][1] + slow_stats['quant_lgmm1'][1]
     assert q_fast < q_slow
+    # batched small rounds share one table per label across the rounds
+    rounds = list(range(500, 2500))
+    fast_b = eng.suggest_batch(31, rounds, 24)
+    sb = eng.last_mode_stats()
+    slow_eng = Engine(0, 'f64')
+    slow_eng.set_posterior(d, w, m, s)
+    slow_b = slow_eng.suggest_batch(31, rounds, 24)
+    slow_eng.close()
+    assert np.array_equal(fast_b['index'], slow_b['index'])
+    assert np.array_equal(fast_b['value'], slow_b['value'])
+    assert sb['quant_gmm1'][1] + sb['quant_lgmm1'][1] < q_slow
 
 
 def _oracle_winner(eng, meta, rec, li, C, seed, rnd):
