@@ -35,8 +35,9 @@ using namespace tpe;
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kR = 4;                 // candidates per thread
-constexpr int kTile = kBlock * kR;    // candidates per workgroup
+constexpr int kR = 4;                 // candidates per thread, tile map
+constexpr int kRGroup = 1;            // candidates per thread, grouped map (more waves)
+constexpr int kTile = kBlock * kR;    // candidates per workgroup, tile map
 constexpr int kNumModes = 5;
 
 thread_local std::string g_create_error;
@@ -89,9 +90,10 @@ struct Slots {
     int32_t pbits;
     int32_t n_rounds;
 
+    template <int R>
     __device__ __forceinline__ void at(int r, int64_t n, int64_t& z, int64_t& i,
                                        bool& valid) const {
-        const int64_t q = (int64_t)blockIdx.x * kTile + r * kBlock + threadIdx.x;
+        const int64_t q = (int64_t)blockIdx.x * (R * kBlock) + r * kBlock + threadIdx.x;
         if (pbits == 0) {
             z = blockIdx.z;
             i = q;
@@ -156,7 +158,7 @@ __device__ __forceinline__ void finish_slots(const Slots& S, const double (&x)[R
 
 // --------------------------------------------------------------- kernels ----
 
-template <typename T, int MODE, bool SAMPLE>
+template <typename T, int MODE, bool SAMPLE, int R>
 __global__ __launch_bounds__(kBlock) void k_round(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
     const Comp<T>* __restrict__ comps, const Comp<double>* __restrict__ comps64,
@@ -169,12 +171,12 @@ __global__ __launch_bounds__(kBlock) void k_round(
     __shared__ double exp_tab[kExpTabSize];
     if constexpr (MODE == DENSE_GMM || MODE == DENSE_LGMM) load_exp_table(exp_tab);
 
-    double x[kR], lb[kR], la[kR];
-    int64_t z[kR], ci[kR], gi[kR];
-    bool valid[kR];
+    double x[R], lb[R], la[R];
+    int64_t z[R], ci[R], gi[R];
+    bool valid[R];
 #pragma unroll
-    for (int r = 0; r < kR; ++r) {
-        S.at(r, n, z[r], ci[r], valid[r]);
+    for (int r = 0; r < R; ++r) {
+        S.template at<R>(r, n, z[r], ci[r], valid[r]);
         gi[r] = cand_offset + ci[r];
         double v = (MODE == DENSE_LGMM || MODE == QUANT_LGMM) ? 1.0 : 0.0;
         if (valid[r]) {
@@ -190,22 +192,22 @@ __global__ __launch_bounds__(kBlock) void k_round(
     }
 
     if constexpr (MODE == DENSE_GMM) {
-        lse_dense<kR>(comps + L.comp_b, L.nb, L.shift_b, x, lb, exp_tab);
-        lse_dense<kR>(comps + L.comp_a, L.na, L.shift_a, x, la, exp_tab);
+        lse_dense<R>(comps + L.comp_b, L.nb, L.shift_b, x, lb, exp_tab);
+        lse_dense<R>(comps + L.comp_a, L.na, L.shift_a, x, la, exp_tab);
     } else if constexpr (MODE == DENSE_LGMM) {
-        double y[kR];
+        double y[R];
 #pragma unroll
-        for (int r = 0; r < kR; ++r) y[r] = log(x[r]);
-        lse_dense<kR>(comps + L.comp_b, L.nb, L.shift_b, y, lb, exp_tab);
-        lse_dense<kR>(comps + L.comp_a, L.na, L.shift_a, y, la, exp_tab);
+        for (int r = 0; r < R; ++r) y[r] = log(x[r]);
+        lse_dense<R>(comps + L.comp_b, L.nb, L.shift_b, y, lb, exp_tab);
+        lse_dense<R>(comps + L.comp_a, L.na, L.shift_a, y, la, exp_tab);
 #pragma unroll
-        for (int r = 0; r < kR; ++r) {
+        for (int r = 0; r < R; ++r) {
             lb[r] -= y[r];
             la[r] -= y[r];
         }
     } else if constexpr (MODE == QUANT_GMM || MODE == QUANT_LGMM) {
 #pragma unroll
-        for (int r = 0; r < kR; ++r) {
+        for (int r = 0; r < R; ++r) {
             double ub, lo;
             bool neg;
             quant_bounds<MODE>(L, x[r], ub, lo, neg);
@@ -215,7 +217,7 @@ __global__ __launch_bounds__(kBlock) void k_round(
         }
     } else {  // CAT: categorical_lpdf = log(p[sample])   tpe.py:56-63
 #pragma unroll
-        for (int r = 0; r < kR; ++r) {
+        for (int r = 0; r < R; ++r) {
             const int64_t s = (int64_t)x[r];
             if (valid[r] && (s < 0 || s >= L.nb || (double)s != x[r])) atomicOr(err, 4);
             const int64_t sc = s < 0 ? 0 : (s >= L.nb ? L.nb - 1 : s);
@@ -226,20 +228,20 @@ __global__ __launch_bounds__(kBlock) void k_round(
 
     if (out_lb) {
 #pragma unroll
-        for (int r = 0; r < kR; ++r)
+        for (int r = 0; r < R; ++r)
             if (valid[r]) {
                 const size_t row = ((size_t)z[r] * n_labels + li) * (size_t)n;
                 out_lb[row + ci[r]] = lb[r];
                 out_la[row + ci[r]] = la[r];
             }
     }
-    finish_slots<kR>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials);
+    finish_slots<R>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials);
 }
 
 // Quantized families, pass 1: draw every candidate, keep its grid index
 // j = rint(v / q) (so x = j * q exactly as np.round(v / q) * q), and the
 // per-(round, label) min/max of j (order-preserving biased unsigned).
-template <int MODE>
+template <int MODE, int R>
 __global__ __launch_bounds__(kBlock) void k_qsample(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
     const SampRec* __restrict__ samp, int64_t n, int64_t cand_offset, uint64_t seed,
@@ -250,10 +252,10 @@ __global__ __launch_bounds__(kBlock) void k_qsample(
     const DLabel L = labels[li];
     const int width = S.pbits ? (1 << S.pbits) : 64;   // lanes sharing one (round, label)
 #pragma unroll
-    for (int r = 0; r < kR; ++r) {
+    for (int r = 0; r < R; ++r) {
         int64_t z, i;
         bool valid;
-        S.at(r, n, z, i, valid);
+        S.template at<R>(r, n, z, i, valid);
         unsigned long long mn = ~0ull, mx = 0ull;
         if (valid) {
             double v;
@@ -304,7 +306,7 @@ __global__ __launch_bounds__(kBlock) void k_qtable(
 // Quantized families, pass 3: per candidate look up its grid value's lpdf
 // pair (direct evaluation when the label's window was too wide for a table),
 // then the same block maxloc as k_round.
-template <int MODE>
+template <int MODE, int R>
 __global__ __launch_bounds__(kBlock) void k_qscan(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
     const Comp<double>* __restrict__ comps64, const int64_t* __restrict__ qj,
@@ -313,12 +315,12 @@ __global__ __launch_bounds__(kBlock) void k_qscan(
     Partial* __restrict__ partials, Slots S) {
     const int li = group[blockIdx.y];
     const DLabel L = labels[li];
-    double x[kR], lb[kR], la[kR];
-    int64_t z[kR], ci[kR], gi[kR];
-    bool valid[kR];
+    double x[R], lb[R], la[R];
+    int64_t z[R], ci[R], gi[R];
+    bool valid[R];
 #pragma unroll
-    for (int r = 0; r < kR; ++r) {
-        S.at(r, n, z[r], ci[r], valid[r]);
+    for (int r = 0; r < R; ++r) {
+        S.template at<R>(r, n, z[r], ci[r], valid[r]);
         gi[r] = cand_offset + ci[r];
         const QInfo Q = qinfo[qbase + blockIdx.y];         // window shared by all rounds
         const size_t slot = (size_t)(valid[r] ? z[r] : 0) * nq + qbase + blockIdx.y;
@@ -337,7 +339,7 @@ __global__ __launch_bounds__(kBlock) void k_qscan(
             la[r] = quant_lpdf<MODE == QUANT_LGMM>(comps64 + L.comp_a, L.na, ub, lo, L.logpacc_a);
         }
     }
-    finish_slots<kR>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials);
+    finish_slots<R>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials);
 }
 
 __global__ __launch_bounds__(kBlock) void k_reduce(const Partial* __restrict__ partials,
@@ -605,11 +607,18 @@ void launch_round(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
     bracket(ctx, MODE, 0);
     const Comp<T>* comps;
     if constexpr (sizeof(T) == 8) comps = ctx->comps64.p; else comps = ctx->comps32.p;
-    hipLaunchKernelGGL((k_round<T, MODE, SAMPLE>), dim3(a.gx, nl, a.gz), dim3(kBlock), 0,
-                       ctx->stream, ctx->labels.p, g.dev[MODE], comps, ctx->comps64.p,
-                       ctx->samp.p, a.cand_in, a.n, a.cand_offset, a.seed, ctx->rounds.p,
-                       ctx->n_labels, a.tiles, ctx->partials.p, a.olb, a.ola, ctx->errflag.p,
-                       a.S);
+    if (a.S.pbits)
+        hipLaunchKernelGGL((k_round<T, MODE, SAMPLE, kRGroup>), dim3(a.gx, nl, a.gz), dim3(kBlock),
+                           0, ctx->stream, ctx->labels.p, g.dev[MODE], comps, ctx->comps64.p,
+                           ctx->samp.p, a.cand_in, a.n, a.cand_offset, a.seed, ctx->rounds.p,
+                           ctx->n_labels, a.tiles, ctx->partials.p, a.olb, a.ola, ctx->errflag.p,
+                           a.S);
+    else
+        hipLaunchKernelGGL((k_round<T, MODE, SAMPLE, kR>), dim3(a.gx, nl, a.gz), dim3(kBlock), 0,
+                           ctx->stream, ctx->labels.p, g.dev[MODE], comps, ctx->comps64.p,
+                           ctx->samp.p, a.cand_in, a.n, a.cand_offset, a.seed, ctx->rounds.p,
+                           ctx->n_labels, a.tiles, ctx->partials.p, a.olb, a.ola, ctx->errflag.p,
+                           a.S);
     bracket(ctx, MODE, 1);
 }
 
@@ -626,16 +635,20 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
     HIPCHK(ctx, ctx->qinfo.reserve(nq));
     HIPCHK(ctx, hipMemsetAsync(ctx->qmm.p, 0xFF, nq * sizeof(unsigned long long), ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->qmm.p + nq, 0, nq * sizeof(unsigned long long), ctx->stream));
-    if (nqg)
-        hipLaunchKernelGGL(k_qsample<QUANT_GMM>, dim3(a.gx, nqg, a.gz), dim3(kBlock), 0,
-                           ctx->stream, ctx->labels.p, g.dev[QUANT_GMM], ctx->samp.p, a.n,
-                           a.cand_offset, a.seed, ctx->rounds.p, nq, 0, ctx->qj.p, ctx->qmm.p,
-                           ctx->qmm.p + nq, ctx->errflag.p, a.S);
-    if (nql)
-        hipLaunchKernelGGL(k_qsample<QUANT_LGMM>, dim3(a.gx, nql, a.gz), dim3(kBlock), 0,
-                           ctx->stream, ctx->labels.p, g.dev[QUANT_LGMM], ctx->samp.p, a.n,
-                           a.cand_offset, a.seed, ctx->rounds.p, nq, nqg, ctx->qj.p, ctx->qmm.p,
-                           ctx->qmm.p + nq, ctx->errflag.p, a.S);
+#define TPE_QSAMPLE(M, CNT, BASE, RR)                                                         \
+    hipLaunchKernelGGL((k_qsample<M, RR>), dim3(a.gx, CNT, a.gz), dim3(kBlock), 0, ctx->stream, \
+                       ctx->labels.p, g.dev[M], ctx->samp.p, a.n, a.cand_offset, a.seed,      \
+                       ctx->rounds.p, nq, BASE, ctx->qj.p, ctx->qmm.p, ctx->qmm.p + nq,        \
+                       ctx->errflag.p, a.S)
+    if (nqg) {
+        if (a.S.pbits) TPE_QSAMPLE(QUANT_GMM, nqg, 0, kRGroup);
+        else TPE_QSAMPLE(QUANT_GMM, nqg, 0, kR);
+    }
+    if (nql) {
+        if (a.S.pbits) TPE_QSAMPLE(QUANT_LGMM, nql, nqg, kRGroup);
+        else TPE_QSAMPLE(QUANT_LGMM, nql, nqg, kR);
+    }
+#undef TPE_QSAMPLE
     HIPCHK(ctx, hipGetLastError());
     std::vector<unsigned long long> mm(2 * (size_t)nq);
     HIPCHK(ctx, hipMemcpyAsync(mm.data(), ctx->qmm.p, 2 * nq * sizeof(unsigned long long),
@@ -680,16 +693,18 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
                                    qbase, ctx->qtab.p);
         }
         dim3 sg(a.gx, cnt, a.gz);
-        if (fam)
-            hipLaunchKernelGGL(k_qscan<QUANT_LGMM>, sg, dim3(kBlock), 0, ctx->stream, ctx->labels.p,
-                               g.dev[mode], ctx->comps64.p, ctx->qj.p, ctx->qinfo.p, ctx->qtab.p,
-                               a.n, a.cand_offset, nq, qbase, ctx->n_labels, a.tiles,
-                               ctx->partials.p, a.S);
-        else
-            hipLaunchKernelGGL(k_qscan<QUANT_GMM>, sg, dim3(kBlock), 0, ctx->stream, ctx->labels.p,
-                               g.dev[mode], ctx->comps64.p, ctx->qj.p, ctx->qinfo.p, ctx->qtab.p,
-                               a.n, a.cand_offset, nq, qbase, ctx->n_labels, a.tiles,
-                               ctx->partials.p, a.S);
+#define TPE_QSCAN(M, RR)                                                                      \
+    hipLaunchKernelGGL((k_qscan<M, RR>), sg, dim3(kBlock), 0, ctx->stream, ctx->labels.p,     \
+                       g.dev[mode], ctx->comps64.p, ctx->qj.p, ctx->qinfo.p, ctx->qtab.p, a.n, \
+                       a.cand_offset, nq, qbase, ctx->n_labels, a.tiles, ctx->partials.p, a.S)
+        if (fam) {
+            if (a.S.pbits) TPE_QSCAN(QUANT_LGMM, kRGroup);
+            else TPE_QSCAN(QUANT_LGMM, kR);
+        } else {
+            if (a.S.pbits) TPE_QSCAN(QUANT_GMM, kRGroup);
+            else TPE_QSCAN(QUANT_GMM, kR);
+        }
+#undef TPE_QSCAN
         bracket(ctx, mode, 1);
     }
     HIPCHK(ctx, hipGetLastError());
@@ -713,7 +728,8 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         while ((1 << pb) < n) ++pb;
         S.pbits = pb;
         tiles = 1;
-        gx = (uint32_t)(((int64_t)n_rounds * (1 << pb) + kTile - 1) / kTile);
+        const int64_t per_block = (int64_t)kBlock * kRGroup;
+        gx = (uint32_t)(((int64_t)n_rounds * (1 << pb) + per_block - 1) / per_block);
         gz = 1;
     } else {
         tiles = (int32_t)((n + kTile - 1) / kTile);
