@@ -36,7 +36,7 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kR = 4;                 // candidates per thread, tile map
-constexpr int kRGroup = 1;            // candidates per thread, grouped map (more waves)
+constexpr int kRGroup = 1;            // candidates per thread, packed map with C <= 256
 constexpr int kTile = kBlock * kR;    // candidates per workgroup, tile map
 constexpr int kNumModes = 5;
 
@@ -81,40 +81,48 @@ __device__ __forceinline__ void block_maxloc(uint64_t bk, int64_t bi, double bv,
 }
 
 // ------------------------------------------------------------ slot maps ----
-// Where slot r of a thread lives.  Tile map (pbits == 0): one round per
-// grid.z, that round's candidates spread over the workgroup (large C).
-// Group map (pbits > 0): P = 2^pbits <= 64 consecutive lanes per round, rounds
-// packed along grid.x -- batched rounds with small C (e.g. 4096 new_ids x 24
-// candidates) keep every lane busy and reduce inside the wave.
+// Where slot r of a thread lives.
+//  * Tile map (cpack == 0): one round per grid.z, that round's candidates
+//    spread over the grid (large C).
+//  * Packed map (cpack == C < 256 R): rpb = floor(256 R / C) whole rounds per
+//    workgroup, rounds along grid.x -- batched rounds with small C (e.g. 4096
+//    new_ids x 24 candidates) keep the lanes busy; the per-round maxloc goes
+//    through LDS.
 struct Slots {
-    int32_t pbits;
+    int32_t cpack;      // candidates per round in the packed map, 0 = tile map
+    int32_t rpb;        // rounds per workgroup (packed map)
     int32_t n_rounds;
 
     template <int R>
     __device__ __forceinline__ void at(int r, int64_t n, int64_t& z, int64_t& i,
                                        bool& valid) const {
-        const int64_t q = (int64_t)blockIdx.x * (R * kBlock) + r * kBlock + threadIdx.x;
-        if (pbits == 0) {
+        if (cpack == 0) {
             z = blockIdx.z;
-            i = q;
+            i = (int64_t)blockIdx.x * (R * kBlock) + r * kBlock + threadIdx.x;
             valid = i < n;
         } else {
-            z = q >> pbits;
-            i = q & ((1 << pbits) - 1);
-            valid = i < n && z < n_rounds;
+            const int local = r * kBlock + threadIdx.x;
+            const int zr = local / cpack;
+            z = (int64_t)blockIdx.x * rpb + zr;
+            i = local - zr * cpack;
+            valid = zr < rpb && z < n_rounds;
         }
     }
 };
 
 // broadcast_best epilogue for either map: block maxloc into the tile's
-// partial, or per-round maxloc over each P-lane group written by its leader.
+// partial, or, packed, one winner per round: every slot posts its key to
+// LDS, a reducer per round picks the best slot (slots of a round are in
+// candidate order, so the lowest slot among equal keys is the lowest index),
+// and the owner of that slot writes the round's record.
 template <int R>
 __device__ __forceinline__ void finish_slots(const Slots& S, const double (&x)[R],
                                              const double (&lb)[R], const double (&la)[R],
                                              const bool (&valid)[R], const int64_t (&z)[R],
                                              const int64_t (&gi)[R], int li, int32_t n_labels,
-                                             int32_t tiles, Partial* __restrict__ partials) {
-    if (S.pbits == 0) {
+                                             int32_t tiles, Partial* __restrict__ partials,
+                                             void* lds_scratch) {
+    if (S.cpack == 0) {
         uint64_t bk = 0;
         int64_t bi = INT64_MAX;
         double bv = 0.0, bl = 0.0, ba = 0.0;
@@ -134,25 +142,38 @@ __device__ __forceinline__ void finish_slots(const Slots& S, const double (&x)[R
                      partials + ((size_t)blockIdx.z * n_labels + li) * tiles + blockIdx.x);
         return;
     }
+    // scratch: R*256 keys + R*256 winners (12 KB at R = 4), aliased on the
+    // exp table, which every wave has finished reading at the barrier
+    static_assert(R * kBlock * (sizeof(uint64_t) + sizeof(int32_t)) <=
+                  kExpTabSize * sizeof(double), "packed scratch exceeds the LDS table");
+    __syncthreads();
+    uint64_t* keys = reinterpret_cast<uint64_t*>(lds_scratch);
+    int32_t* win = reinterpret_cast<int32_t*>(keys + R * kBlock);
+    uint64_t key[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        uint64_t bk = valid[r] ? order_key(lb[r] - la[r]) : 0;
-        int64_t bi = valid[r] ? gi[r] : INT64_MAX;
-        double bv = x[r], bl = lb[r], ba = la[r];
-        for (int off = (1 << S.pbits) >> 1; off > 0; off >>= 1) {
-            const uint64_t ok = __shfl_xor(bk, off);
-            const int64_t oi = __shfl_xor(bi, off);
-            const double ov = __shfl_xor(bv, off), ol = __shfl_xor(bl, off), oa = __shfl_xor(ba, off);
-            if (better(ok, oi, bk, bi)) {
-                bk = ok;
-                bi = oi;
-                bv = ov;
-                bl = ol;
-                ba = oa;
+        key[r] = valid[r] ? order_key(lb[r] - la[r]) : 0;
+        keys[r * kBlock + threadIdx.x] = key[r];
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < S.rpb; t += kBlock) {
+        const int s0 = t * S.cpack;
+        int best = s0;
+        uint64_t bk = keys[s0];
+        for (int c = 1; c < S.cpack; ++c)
+            if (keys[s0 + c] > bk) {
+                bk = keys[s0 + c];
+                best = s0 + c;
             }
-        }
-        if ((threadIdx.x & ((1 << S.pbits) - 1)) == 0 && z[r] < S.n_rounds)
-            partials[(size_t)z[r] * n_labels + li] = Partial{bk, bi, bv, bl, ba};
+        win[t] = best;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (!valid[r]) continue;
+        const int local = r * kBlock + threadIdx.x;
+        if (win[local / S.cpack] == local)
+            partials[(size_t)z[r] * n_labels + li] = Partial{key[r], gi[r], x[r], lb[r], la[r]};
     }
 }
 
@@ -235,7 +256,7 @@ __global__ __launch_bounds__(kBlock) void k_round(
                 out_la[row + ci[r]] = la[r];
             }
     }
-    finish_slots<R>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials);
+    finish_slots<R>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials, exp_tab);
 }
 
 // Quantized families, pass 1: draw every candidate, keep its grid index
@@ -250,7 +271,6 @@ __global__ __launch_bounds__(kBlock) void k_qsample(
     int32_t* __restrict__ err, Slots S) {
     const int li = group[blockIdx.y];
     const DLabel L = labels[li];
-    const int width = S.pbits ? (1 << S.pbits) : 64;   // lanes sharing one (round, label)
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         int64_t z, i;
@@ -269,12 +289,12 @@ __global__ __launch_bounds__(kBlock) void k_qsample(
             qj[((size_t)z * nq + qbase + blockIdx.y) * (size_t)n + i] = j;
             mn = mx = (unsigned long long)j ^ 0x8000000000000000ull;
         }
-        for (int off = width >> 1; off > 0; off >>= 1) {
+        for (int off = 32; off > 0; off >>= 1) {   // the window is per label: whole wave
             const unsigned long long a = __shfl_xor(mn, off), b = __shfl_xor(mx, off);
             mn = a < mn ? a : mn;
             mx = b > mx ? b : mx;
         }
-        if ((threadIdx.x & (width - 1)) == 0 && mn <= mx) {   // window per label, all rounds
+        if ((threadIdx.x & 63) == 0 && mn <= mx) {
             atomicMin(qmin + qbase + blockIdx.y, mn);
             atomicMax(qmax + qbase + blockIdx.y, mx);
         }
@@ -339,7 +359,8 @@ __global__ __launch_bounds__(kBlock) void k_qscan(
             la[r] = quant_lpdf<MODE == QUANT_LGMM>(comps64 + L.comp_a, L.na, ub, lo, L.logpacc_a);
         }
     }
-    finish_slots<R>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials);
+    __shared__ double scratch[R * kBlock * 3 / 2];
+    finish_slots<R>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials, scratch);
 }
 
 __global__ __launch_bounds__(kBlock) void k_reduce(const Partial* __restrict__ partials,
@@ -607,7 +628,7 @@ void launch_round(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
     bracket(ctx, MODE, 0);
     const Comp<T>* comps;
     if constexpr (sizeof(T) == 8) comps = ctx->comps64.p; else comps = ctx->comps32.p;
-    if (a.S.pbits)
+    if (a.S.cpack && a.S.cpack <= kBlock * kRGroup)
         hipLaunchKernelGGL((k_round<T, MODE, SAMPLE, kRGroup>), dim3(a.gx, nl, a.gz), dim3(kBlock),
                            0, ctx->stream, ctx->labels.p, g.dev[MODE], comps, ctx->comps64.p,
                            ctx->samp.p, a.cand_in, a.n, a.cand_offset, a.seed, ctx->rounds.p,
@@ -641,11 +662,11 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
                        ctx->rounds.p, nq, BASE, ctx->qj.p, ctx->qmm.p, ctx->qmm.p + nq,        \
                        ctx->errflag.p, a.S)
     if (nqg) {
-        if (a.S.pbits) TPE_QSAMPLE(QUANT_GMM, nqg, 0, kRGroup);
+        if (a.S.cpack && a.S.cpack <= kBlock * kRGroup) TPE_QSAMPLE(QUANT_GMM, nqg, 0, kRGroup);
         else TPE_QSAMPLE(QUANT_GMM, nqg, 0, kR);
     }
     if (nql) {
-        if (a.S.pbits) TPE_QSAMPLE(QUANT_LGMM, nql, nqg, kRGroup);
+        if (a.S.cpack && a.S.cpack <= kBlock * kRGroup) TPE_QSAMPLE(QUANT_LGMM, nql, nqg, kRGroup);
         else TPE_QSAMPLE(QUANT_LGMM, nql, nqg, kR);
     }
 #undef TPE_QSAMPLE
@@ -698,10 +719,10 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
                        g.dev[mode], ctx->comps64.p, ctx->qj.p, ctx->qinfo.p, ctx->qtab.p, a.n, \
                        a.cand_offset, nq, qbase, ctx->n_labels, a.tiles, ctx->partials.p, a.S)
         if (fam) {
-            if (a.S.pbits) TPE_QSCAN(QUANT_LGMM, kRGroup);
+            if (a.S.cpack && a.S.cpack <= kBlock * kRGroup) TPE_QSCAN(QUANT_LGMM, kRGroup);
             else TPE_QSCAN(QUANT_LGMM, kR);
         } else {
-            if (a.S.pbits) TPE_QSCAN(QUANT_GMM, kRGroup);
+            if (a.S.cpack && a.S.cpack <= kBlock * kRGroup) TPE_QSCAN(QUANT_GMM, kRGroup);
             else TPE_QSCAN(QUANT_GMM, kR);
         }
 #undef TPE_QSCAN
@@ -718,18 +739,17 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     if (n < 0 || n_rounds <= 0) return ctx->fail(TPE_ERR_ARG, "bad candidate/round count");
     if (cand_offset < 0 || cand_offset + n > (int64_t)UINT32_MAX)
         return ctx->fail(TPE_ERR_ARG, "candidate indices must stay below 2^32");
-    // slot map: grouped (P = 2^pbits lanes per round) for small candidate
-    // sets, tiled otherwise
-    Slots S{0, n_rounds};
+    // slot map: packed (whole rounds per workgroup) for candidate sets smaller
+    // than a tile, tiled otherwise
+    Slots S{0, 0, n_rounds};
     int32_t tiles;
     uint32_t gx, gz;
-    if (n > 0 && n <= 64) {
-        int pb = 1;
-        while ((1 << pb) < n) ++pb;
-        S.pbits = pb;
+    if (n > 0 && n < kTile) {
+        const int per_block = n <= kBlock * kRGroup ? kBlock * kRGroup : kTile;
+        S.cpack = (int32_t)n;
+        S.rpb = per_block / (int32_t)n;
         tiles = 1;
-        const int64_t per_block = (int64_t)kBlock * kRGroup;
-        gx = (uint32_t)(((int64_t)n_rounds * (1 << pb) + per_block - 1) / per_block);
+        gx = (uint32_t)((n_rounds + S.rpb - 1) / S.rpb);
         gz = 1;
     } else {
         tiles = (int32_t)((n + kTile - 1) / kTile);

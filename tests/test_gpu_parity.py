@@ -305,12 +305,13 @@ def _oracle_winner(eng, meta, rec, li, C, seed, rnd):
     return best, cand[best]
 
 
-@pytest.mark.parametrize('C', [1, 2, 24, 33, 64, 65])
+@pytest.mark.parametrize('C', [1, 2, 24, 33, 64, 65, 256, 257, 700, 1023, 1024])
 def test_batched_small_candidate_sets(eng, C):
-    """Batched rounds with small candidate sets use the grouped slot map
-    (P-lane groups per round, in-wave maxloc); every round's winner must equal
-    the oracle's on the same draws, for dense, quantized and categorical
-    labels."""
+    """Batched rounds with candidate sets smaller than a tile use the packed
+    slot map (whole rounds per workgroup, per-round maxloc through LDS; one
+    candidate per thread up to 256, four above); every round's winner must
+    equal the oracle's on the same draws, for dense, quantized and
+    categorical labels."""
     pairs = [(m, r) for fx, m, r in _all_cases()
              if m['n_hist'] == 300 and m['variant'] == 'plain']
     d, w, m, s = stack_cases(pairs)
