@@ -47,6 +47,32 @@ def split_label(o_idxs, o_vals, below_tids, above_tids):
     return (o_vals[np.isin(o_idxs, below_tids)], o_vals[np.isin(o_idxs, above_tids)])
 
 
+class Splitter(object):
+    """split_history + split_label for many labels sharing one history: the
+    membership of a tid is looked up by binary search in the sorted tids
+    (one O(M log N) pass per label instead of np.isin's sorts)."""
+
+    def __init__(self, l_idxs, l_vals, gamma, gamma_cap=DEFAULT_LF):
+        below, above = split_history(l_idxs, l_vals, gamma, gamma_cap)
+        tids = np.concatenate([below, above])
+        side = np.concatenate([np.ones(len(below), dtype=np.int8),
+                               np.full(len(above), 2, dtype=np.int8)])
+        order = np.argsort(tids, kind='stable')
+        self.tids = tids[order]
+        self.side = side[order]
+
+    def split(self, o_idxs, o_vals):
+        o_idxs = np.asarray(o_idxs)
+        o_vals = np.asarray(o_vals)
+        if len(o_idxs) == 0 or len(self.tids) == 0:
+            return np.asarray([]), np.asarray([])
+        pos = np.searchsorted(self.tids, o_idxs)
+        pos_c = np.minimum(pos, len(self.tids) - 1)
+        hit = self.tids[pos_c] == o_idxs
+        side = np.where(hit, self.side[pos_c], 0)
+        return o_vals[side == 1], o_vals[side == 2]
+
+
 def linear_forgetting_weights(n, lf):
     if n == 0:
         return np.asarray([])

@@ -78,11 +78,11 @@ def build_posteriors(domain, trials, prior_weight=_default_prior_weight,
     tids, losses, obs = _history.gather(domain, trials, list(specs))
     if len(tids) == 0:
         return specs, 0, None
-    below_tids, above_tids = _post.split_history(tids, losses, gamma)
+    splitter = _post.Splitter(tids, losses, gamma)
     posts = []
     for label, s in specs.items():
         oi, ov = obs[label]
-        b, a = _post.split_label(oi, ov, below_tids, above_tids)
+        b, a = splitter.split(oi, ov)
         posts.append(_post.label_posterior(label, s.kind, s.args, b, a, prior_weight))
     return specs, len(tids), posts
 

@@ -71,11 +71,11 @@ class History(object):
         self.obs = obs                # name -> (idxs, vals)
 
     def posteriors(self, gamma=0.25, prior_weight=1.0):
-        bt, at = P.split_history(self.tids, self.losses, gamma)
+        splitter = P.Splitter(self.tids, self.losses, gamma)
         posts = []
         for name, kind, args in self.labels:
             oi, ov = self.obs[name]
-            b, a = P.split_label(oi, ov, bt, at)
+            b, a = splitter.split(oi, ov)
             posts.append(P.label_posterior(name, kind, args, b, a, prior_weight))
         return posts
 

@@ -1,5 +1,5 @@
 """Host checks of the device math constants (no GPU): the fp64 exp scheme
-of tpe_device.h (scaled exponent, degree-5 polynomial, 64-entry table) is
+of tpe_device.h (scaled exponent, degree-3 polynomial, 2048-entry table) is
 re-evaluated in numpy from the constants parsed out of the header and
 compared with a 60-digit reference; the Philox4x32-10 round function is
 checked against its published known-answer vectors."""

@@ -1,0 +1,104 @@
+"""Parity at the BASELINE.json sizes through size-independent properties
+(the oracle cannot score 2^21 x 10^4 pairs in test time):
+
+* the reported winner value is the draw at the reported global index
+  (re-drawn through the sampler entry point);
+* its lpdf pair equals the CPU oracle's at that value (fp64 bar);
+* no candidate of a random sample of the same set, scored by the oracle,
+  beats it;
+* splitting the candidate set over shards does not change it.
+"""
+import numpy as np
+import pytest
+
+from oracle import tpe_oracle as O
+from tests.helpers import assert_lpdf_close
+
+pytestmark = pytest.mark.gpu
+
+
+def _draw(eng, p, li, seed, rnd, offset, n):
+    if p.family == 'categorical':
+        return eng.categorical(p.below, seed=seed, size=(n,), stream=li, round=rnd,
+                               offset=offset).astype(float)
+    samp = eng.GMM1 if p.family == 'GMM1' else eng.LGMM1
+    return samp(*p.below, low=p.low, high=p.high, q=p.q, seed=seed, size=(n,), stream=li,
+                round=rnd, offset=offset)
+
+
+def _score(p, x):
+    if p.family == 'categorical':
+        return O.categorical_lpdf(x.astype(int), p.below), O.categorical_lpdf(x.astype(int), p.above)
+    f = O.gmm1_lpdf if p.family == 'GMM1' else O.lgmm1_lpdf
+    return (f(x, *p.below, low=p.low, high=p.high, q=p.q),
+            f(x, *p.above, low=p.low, high=p.high, q=p.q))
+
+
+@pytest.mark.parametrize('config', ['config2', 'config3'])
+def test_fullsize_winner_properties(config):
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.engine import Engine
+    from hyperopt_amd.workloads import hartmann_history, mixed_history
+    if config == 'config2':
+        hist, C = hartmann_history(2000, seed=0), 1 << 20
+    else:
+        hist, C = mixed_history(32, 10000, seed=0), 1 << 21
+    posts = hist.posteriors()
+    eng = Engine(0, 'f64')
+    try:
+        eng.set_posterior(*P.pack(posts))
+        seed, rnd = 77, 5
+        res = eng.suggest(seed, C, round=rnd)
+        rng = np.random.RandomState(3)
+        for li, p in enumerate(posts):
+            r = res[li]
+            idx = int(r['index'])
+            assert 0 <= idx < C
+            v = _draw(eng, p, li, seed, rnd, idx, 1)[0]
+            assert v == r['value'], (li, p.family)
+            lb, la = _score(p, np.array([v]))
+            q = p.family != 'categorical' and p.q is not None
+            assert_lpdf_close([r['lpdf_below']], lb, quantized=q)
+            assert_lpdf_close([r['lpdf_above']], la, quantized=q)
+            # a random sample of the same candidate set never beats the winner
+            offs = rng.randint(0, C - 128, size=8)
+            sample = np.concatenate([_draw(eng, p, li, seed, rnd, int(o), 128) for o in offs])
+            sb, sa = _score(p, sample)
+            best = np.nanmax(sb - sa)
+            assert best <= r['score'] + 1e-9 * max(1.0, abs(r['score'])), (li, best, r['score'])
+        # shard invariance at full size (2 and 8 shards)
+        for shards in (2, 8):
+            from hyperopt_amd.engine import merge_results
+            parts = np.stack([eng.suggest(seed, C // shards, round=rnd, cand_offset=k * (C // shards))
+                              for k in range(shards)])
+            m = merge_results(parts)
+            assert np.array_equal(m['index'], res['index'])
+            assert np.array_equal(m['value'], res['value'])
+    finally:
+        eng.close()
+
+
+def test_fullsize_config5_batched_rounds():
+    """Config-5 shape: 128 labels, 50k history, batched new_ids x 24
+    candidates; every sampled round's winner is the oracle's argmax."""
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.engine import Engine
+    from hyperopt_amd.workloads import mixed_history
+    hist = mixed_history(128, 50000, seed=0)
+    posts = hist.posteriors()
+    eng = Engine(0, 'f64')
+    try:
+        eng.set_posterior(*P.pack(posts))
+        ids = list(range(100000, 100512))
+        out = eng.suggest_batch(9, ids, 24)
+        rng = np.random.RandomState(0)
+        for j in rng.choice(len(ids), 3, replace=False):
+            for li in rng.choice(len(posts), 12, replace=False):
+                p = posts[li]
+                cand = _draw(eng, p, int(li), 9, ids[j], 0, 24)
+                lb, la = _score(p, cand)
+                best = O.broadcast_best_index(lb, la)
+                assert int(out[j][li]['index']) == best
+                assert out[j][li]['value'] == cand[best]
+    finally:
+        eng.close()

@@ -48,3 +48,14 @@ def test_pack_layout():
     assert list(d['below_off']) == [0, 3, 7] and list(d['above_off']) == [2, 5, 8]
     assert list(d['n_below']) == [2, 2, 1] and len(w) == 9
     assert np.array_equal(w[3:7], [.2, .8, .5, .5])
+
+
+@pytest.mark.parametrize('fixture', ['labels_small.npz', 'labels_medium.npz'])
+def test_splitter_equals_split_label(fixture):
+    """The binary-search Splitter used by tpe.suggest gives the reference's
+    split (same as the np.isin form pinned above)."""
+    for meta, rec in golden_io.cases(fixture):
+        sp = P.Splitter(rec['l_idxs'], rec['l_vals'], meta['gamma'])
+        b, a = sp.split(rec['o_idxs'], rec['o_vals'])
+        assert np.array_equal(np.asarray(b, float), rec['below'])
+        assert np.array_equal(np.asarray(a, float), rec['above'])
