@@ -476,6 +476,26 @@ struct DevBuf {
     }
 };
 
+struct Posterior {
+    std::vector<DLabel> h_labels;
+    std::vector<int32_t> h_group[kNumModes];   // label ids per mode
+    int32_t n_labels = 0;
+    DevBuf<DLabel> labels;
+    DevBuf<Comp<double>> comps64;
+    DevBuf<Comp<float>> comps32;
+    DevBuf<SampRec> samp;
+    DevBuf<int32_t> groups;              // concatenated h_group
+    int32_t group_off[kNumModes] = {};
+    void release() {
+        labels.release();
+        comps64.release();
+        comps32.release();
+        samp.release();
+        groups.release();
+        n_labels = 0;
+    }
+};
+
 }  // namespace
 
 struct tpe_ctx {
@@ -492,16 +512,11 @@ struct tpe_ctx {
     int64_t evals = 0;
     bool dedup = true;                   // quantized grid-value tables
 
-    // resident posterior
-    std::vector<DLabel> h_labels;
-    std::vector<int32_t> h_group[kNumModes];   // label ids per mode
-    int32_t n_labels = 0;
-    DevBuf<DLabel> labels;
-    DevBuf<Comp<double>> comps64;
-    DevBuf<Comp<float>> comps32;
-    DevBuf<SampRec> samp;
-    DevBuf<int32_t> groups;              // concatenated h_group
-    int32_t group_off[kNumModes] = {};
+    // The resident posterior (tpe_set_posterior) and a separate one-label
+    // slot for the single-op entry points, so that GMM1_lpdf / GMM1 sampling
+    // calls never clobber the posterior a suggestion loop has uploaded.
+    Posterior resident, single;
+    Posterior* P = &resident;
 
     // per-round scratch
     DevBuf<Partial> partials;
@@ -627,18 +642,18 @@ void launch_round(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
     if (nl == 0 || a.tiles == 0) return;
     bracket(ctx, MODE, 0);
     const Comp<T>* comps;
-    if constexpr (sizeof(T) == 8) comps = ctx->comps64.p; else comps = ctx->comps32.p;
+    if constexpr (sizeof(T) == 8) comps = ctx->P->comps64.p; else comps = ctx->P->comps32.p;
     if (a.S.cpack && a.S.cpack <= kBlock * kRGroup)
         hipLaunchKernelGGL((k_round<T, MODE, SAMPLE, kRGroup>), dim3(a.gx, nl, a.gz), dim3(kBlock),
-                           0, ctx->stream, ctx->labels.p, g.dev[MODE], comps, ctx->comps64.p,
-                           ctx->samp.p, a.cand_in, a.n, a.cand_offset, a.seed, ctx->rounds.p,
-                           ctx->n_labels, a.tiles, ctx->partials.p, a.olb, a.ola, ctx->errflag.p,
+                           0, ctx->stream, ctx->P->labels.p, g.dev[MODE], comps, ctx->P->comps64.p,
+                           ctx->P->samp.p, a.cand_in, a.n, a.cand_offset, a.seed, ctx->rounds.p,
+                           ctx->P->n_labels, a.tiles, ctx->partials.p, a.olb, a.ola, ctx->errflag.p,
                            a.S);
     else
         hipLaunchKernelGGL((k_round<T, MODE, SAMPLE, kR>), dim3(a.gx, nl, a.gz), dim3(kBlock), 0,
-                           ctx->stream, ctx->labels.p, g.dev[MODE], comps, ctx->comps64.p,
-                           ctx->samp.p, a.cand_in, a.n, a.cand_offset, a.seed, ctx->rounds.p,
-                           ctx->n_labels, a.tiles, ctx->partials.p, a.olb, a.ola, ctx->errflag.p,
+                           ctx->stream, ctx->P->labels.p, g.dev[MODE], comps, ctx->P->comps64.p,
+                           ctx->P->samp.p, a.cand_in, a.n, a.cand_offset, a.seed, ctx->rounds.p,
+                           ctx->P->n_labels, a.tiles, ctx->partials.p, a.olb, a.ola, ctx->errflag.p,
                            a.S);
     bracket(ctx, MODE, 1);
 }
@@ -658,7 +673,7 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
     HIPCHK(ctx, hipMemsetAsync(ctx->qmm.p + nq, 0, nq * sizeof(unsigned long long), ctx->stream));
 #define TPE_QSAMPLE(M, CNT, BASE, RR)                                                         \
     hipLaunchKernelGGL((k_qsample<M, RR>), dim3(a.gx, CNT, a.gz), dim3(kBlock), 0, ctx->stream, \
-                       ctx->labels.p, g.dev[M], ctx->samp.p, a.n, a.cand_offset, a.seed,      \
+                       ctx->P->labels.p, g.dev[M], ctx->P->samp.p, a.n, a.cand_offset, a.seed,      \
                        ctx->rounds.p, nq, BASE, ctx->qj.p, ctx->qmm.p, ctx->qmm.p + nq,        \
                        ctx->errflag.p, a.S)
     if (nqg) {
@@ -689,8 +704,8 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
         qi[qpos] = QInfo{jmin, (ctx->dedup && G > 0 && 2 * G <= total) ? G : 0, tab, 0};
         tab += qi[qpos].G;
         maxG = std::max(maxG, qi[qpos].G);
-        const int li = qpos < nqg ? ctx->h_group[QUANT_GMM][qpos] : ctx->h_group[QUANT_LGMM][qpos - nqg];
-        const DLabel& d = ctx->h_labels[li];
+        const int li = qpos < nqg ? ctx->P->h_group[QUANT_GMM][qpos] : ctx->P->h_group[QUANT_LGMM][qpos - nqg];
+        const DLabel& d = ctx->P->h_labels[li];
         evals_q[qpos < nqg ? 0 : 1] += (qi[qpos].G ? qi[qpos].G : total) * (int64_t)(d.nb + d.na);
     }
     HIPCHK(ctx, ctx->qtab.reserve(std::max<int64_t>(tab, 1)));
@@ -706,18 +721,18 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
             dim3 tg((unsigned)((maxG + kBlock / 64 - 1) / (kBlock / 64)), cnt, 1);
             if (fam)
                 hipLaunchKernelGGL(k_qtable<QUANT_LGMM>, tg, dim3(kBlock), 0, ctx->stream,
-                                   ctx->labels.p, g.dev[mode], ctx->comps64.p, ctx->qinfo.p, nq,
+                                   ctx->P->labels.p, g.dev[mode], ctx->P->comps64.p, ctx->qinfo.p, nq,
                                    qbase, ctx->qtab.p);
             else
                 hipLaunchKernelGGL(k_qtable<QUANT_GMM>, tg, dim3(kBlock), 0, ctx->stream,
-                                   ctx->labels.p, g.dev[mode], ctx->comps64.p, ctx->qinfo.p, nq,
+                                   ctx->P->labels.p, g.dev[mode], ctx->P->comps64.p, ctx->qinfo.p, nq,
                                    qbase, ctx->qtab.p);
         }
         dim3 sg(a.gx, cnt, a.gz);
 #define TPE_QSCAN(M, RR)                                                                      \
-    hipLaunchKernelGGL((k_qscan<M, RR>), sg, dim3(kBlock), 0, ctx->stream, ctx->labels.p,     \
-                       g.dev[mode], ctx->comps64.p, ctx->qj.p, ctx->qinfo.p, ctx->qtab.p, a.n, \
-                       a.cand_offset, nq, qbase, ctx->n_labels, a.tiles, ctx->partials.p, a.S)
+    hipLaunchKernelGGL((k_qscan<M, RR>), sg, dim3(kBlock), 0, ctx->stream, ctx->P->labels.p,     \
+                       g.dev[mode], ctx->P->comps64.p, ctx->qj.p, ctx->qinfo.p, ctx->qtab.p, a.n, \
+                       a.cand_offset, nq, qbase, ctx->P->n_labels, a.tiles, ctx->partials.p, a.S)
         if (fam) {
             if (a.S.cpack && a.S.cpack <= kBlock * kRGroup) TPE_QSCAN(QUANT_LGMM, kRGroup);
             else TPE_QSCAN(QUANT_LGMM, kR);
@@ -735,7 +750,7 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
 int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_rounds, int64_t n,
               int64_t cand_offset, const double* cand_in_dev, double* olb, double* ola,
               tpe_label_result* out, int32_t only_label) {
-    if (ctx->n_labels == 0) return ctx->fail(TPE_ERR_ARG, "no posterior set (tpe_set_posterior)");
+    if (ctx->P->n_labels == 0) return ctx->fail(TPE_ERR_ARG, "no posterior set (tpe_set_posterior)");
     if (n < 0 || n_rounds <= 0) return ctx->fail(TPE_ERR_ARG, "bad candidate/round count");
     if (cand_offset < 0 || cand_offset + n > (int64_t)UINT32_MAX)
         return ctx->fail(TPE_ERR_ARG, "candidate indices must stay below 2^32");
@@ -756,7 +771,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         gx = (uint32_t)tiles;
         gz = (uint32_t)n_rounds;
     }
-    const int32_t L = ctx->n_labels;
+    const int32_t L = ctx->P->n_labels;
     HIPCHK(ctx, ctx->partials.reserve((size_t)n_rounds * L * std::max(tiles, 1)));
     HIPCHK(ctx, ctx->results.reserve((size_t)n_rounds * L));
     HIPCHK(ctx, ctx->rounds.reserve(n_rounds));
@@ -766,8 +781,8 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     HIPCHK(ctx, hipMemsetAsync(ctx->errflag.p, 0, sizeof(int32_t), ctx->stream));
     Groups g;
     for (int m = 0; m < kNumModes; ++m) {
-        g.dev[m] = ctx->groups.p + ctx->group_off[m];
-        g.count[m] = (int32_t)ctx->h_group[m].size();
+        g.dev[m] = ctx->P->groups.p + ctx->P->group_off[m];
+        g.count[m] = (int32_t)ctx->P->h_group[m].size();
         ctx->mode_ran[m] = false;
         ctx->mode_ms[m] = 0.f;
         ctx->mode_evals[m] = 0;
@@ -777,7 +792,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         HIPCHK(ctx, hipMemcpyAsync(ctx->one_group.p, &only_label, sizeof(int32_t),
                                    hipMemcpyHostToDevice, ctx->stream));
         for (int m = 0; m < kNumModes; ++m) g.count[m] = 0;
-        const int m = ctx->h_labels[only_label].mode;
+        const int m = ctx->P->h_labels[only_label].mode;
         g.dev[m] = ctx->one_group.p;
         g.count[m] = 1;
     }
@@ -832,7 +847,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     int64_t evals = 0;
     for (int32_t l = 0; l < L; ++l) {
         if (only_label >= 0 && l != only_label) continue;
-        const DLabel& d = ctx->h_labels[l];
+        const DLabel& d = ctx->P->h_labels[l];
         if (sample && (d.mode == QUANT_GMM || d.mode == QUANT_LGMM)) continue;  // counted below
         const int64_t e = ((d.mode == CAT) ? 2 * n : n * (int64_t)(d.nb + d.na)) * n_rounds;
         evals += e;
@@ -857,7 +872,7 @@ void launch_sample_only(tpe_ctx* ctx, int mode, int64_t n, int64_t offset, uint6
     const int blocks = (int)((n + kBlock - 1) / kBlock);
 #define TPE_SO(M)                                                                             \
     hipLaunchKernelGGL(k_sample_only<M>, dim3(blocks), dim3(kBlock), 0, ctx->stream,         \
-                       ctx->labels.p, ctx->samp.p, n, offset, seed, ctx->rounds.p, out,       \
+                       ctx->P->labels.p, ctx->P->samp.p, n, offset, seed, ctx->rounds.p, out,       \
                        ctx->errflag.p)
     switch (mode) {
         case DENSE_GMM: TPE_SO(DENSE_GMM); break;
@@ -952,22 +967,22 @@ int set_posterior_impl(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_lab
     }
     std::vector<int32_t> cat;
     for (int m = 0; m < kNumModes; ++m) {
-        ctx->group_off[m] = (int32_t)cat.size();
+        ctx->P->group_off[m] = (int32_t)cat.size();
         cat.insert(cat.end(), grp[m].begin(), grp[m].end());
-        ctx->h_group[m] = grp[m];
+        ctx->P->h_group[m] = grp[m];
     }
-    HIPCHK(ctx, ctx->labels.reserve(n_labels));
-    HIPCHK(ctx, ctx->comps64.reserve(c64.size()));
-    HIPCHK(ctx, ctx->comps32.reserve(c32.size()));
-    HIPCHK(ctx, ctx->samp.reserve(sr.size()));
-    HIPCHK(ctx, ctx->groups.reserve(cat.size()));
-    HIPCHK(ctx, hipMemcpy(ctx->labels.p, dl.data(), dl.size() * sizeof(DLabel), hipMemcpyHostToDevice));
-    HIPCHK(ctx, hipMemcpy(ctx->comps64.p, c64.data(), c64.size() * sizeof(Comp<double>), hipMemcpyHostToDevice));
-    HIPCHK(ctx, hipMemcpy(ctx->comps32.p, c32.data(), c32.size() * sizeof(Comp<float>), hipMemcpyHostToDevice));
-    HIPCHK(ctx, hipMemcpy(ctx->samp.p, sr.data(), sr.size() * sizeof(SampRec), hipMemcpyHostToDevice));
-    HIPCHK(ctx, hipMemcpy(ctx->groups.p, cat.data(), cat.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-    ctx->h_labels = dl;
-    ctx->n_labels = n_labels;
+    HIPCHK(ctx, ctx->P->labels.reserve(n_labels));
+    HIPCHK(ctx, ctx->P->comps64.reserve(c64.size()));
+    HIPCHK(ctx, ctx->P->comps32.reserve(c32.size()));
+    HIPCHK(ctx, ctx->P->samp.reserve(sr.size()));
+    HIPCHK(ctx, ctx->P->groups.reserve(cat.size()));
+    HIPCHK(ctx, hipMemcpy(ctx->P->labels.p, dl.data(), dl.size() * sizeof(DLabel), hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->P->comps64.p, c64.data(), c64.size() * sizeof(Comp<double>), hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->P->comps32.p, c32.data(), c32.size() * sizeof(Comp<float>), hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->P->samp.p, sr.data(), sr.size() * sizeof(SampRec), hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->P->groups.p, cat.data(), cat.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    ctx->P->h_labels = dl;
+    ctx->P->n_labels = n_labels;
     return TPE_OK;
 }
 
@@ -1021,11 +1036,8 @@ void tpe_ctx_destroy(tpe_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    c->labels.release();
-    c->comps64.release();
-    c->comps32.release();
-    c->samp.release();
-    c->groups.release();
+    c->resident.release();
+    c->single.release();
     c->partials.release();
     c->results.release();
     c->rounds.release();
@@ -1077,10 +1089,10 @@ int tpe_suggest_batch(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds, int32
 int tpe_score(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, double* lpdf_below,
               double* lpdf_above, tpe_label_result* out) {
     if (!ctx || (!cand && n > 0)) return TPE_ERR_ARG;
-    if (label < 0 || label >= ctx->n_labels) return ctx->fail(TPE_ERR_ARG, "label out of range");
+    if (label < 0 || label >= ctx->P->n_labels) return ctx->fail(TPE_ERR_ARG, "label out of range");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     // host-side argument checks that the reference raises before computing
-    const DLabel& d = ctx->h_labels[label];
+    const DLabel& d = ctx->P->h_labels[label];
     if (d.mode == QUANT_LGMM) {
         for (int64_t i = 0; i < n; ++i) {
             double ub = cand[i] + d.q / 2.0;
@@ -1093,14 +1105,14 @@ int tpe_score(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, double
             if (!(cand[i] >= 0 && cand[i] < d.nb) || cand[i] != std::floor(cand[i]))
                 return ctx->fail(TPE_ERR_VALUE, "categorical sample out of range");
     }
-    const size_t rows = (size_t)ctx->n_labels * std::max<int64_t>(n, 1);
+    const size_t rows = (size_t)ctx->P->n_labels * std::max<int64_t>(n, 1);
     HIPCHK(ctx, ctx->cand.reserve(std::max<int64_t>(n, 1)));
     HIPCHK(ctx, ctx->out_lb.reserve(rows));
     HIPCHK(ctx, ctx->out_la.reserve(rows));
     if (n > 0)
         HIPCHK(ctx, hipMemcpyAsync(ctx->cand.p, cand, n * sizeof(double), hipMemcpyHostToDevice,
                                    ctx->stream));
-    std::vector<tpe_label_result> all(ctx->n_labels);
+    std::vector<tpe_label_result> all(ctx->P->n_labels);
     uint32_t round = 0;
     int rc = run_round(ctx, 0, &round, 1, n, 0, ctx->cand.p, ctx->out_lb.p, ctx->out_la.p,
                        all.data(), label);
@@ -1153,11 +1165,22 @@ int tpe_last_mode_stats(const tpe_ctx* ctx, float* ms, int64_t* evals) {
 }
 
 // ---- single-op entry points: a one-label posterior with both sides equal ----
+// They run on the context's one-label slot; the resident posterior is
+// untouched (restored on every return path).
+
+namespace {
+struct SingleSlot {
+    tpe_ctx* ctx;
+    explicit SingleSlot(tpe_ctx* c) : ctx(c) { ctx->P = &ctx->single; }
+    ~SingleSlot() { ctx->P = &ctx->resident; }
+};
+}  // namespace
 
 static int one_label_lpdf(tpe_ctx* ctx, int kind, const double* samples, int64_t n,
                           const double* w, const double* mu, const double* sg, int32_t k,
                           int32_t flags, double low, double high, double q, double* out) {
     if (!ctx) return TPE_ERR_ARG;
+    SingleSlot slot(ctx);
     if (n == 0) return TPE_OK;  // empty samples -> empty result (tpe.py:115-116)
     if (!samples || !out || !w || !mu || !sg) return ctx->fail(TPE_ERR_ARG, "null pointer");
     tpe_label_desc d{};
@@ -1189,6 +1212,7 @@ int tpe_lgmm1_lpdf(tpe_ctx* ctx, const double* samples, int64_t n, const double*
 int tpe_categorical_lpdf(tpe_ctx* ctx, const int64_t* samples, int64_t n, const double* p,
                          int32_t upper, double* out) {
     if (!ctx) return TPE_ERR_ARG;
+    SingleSlot slot(ctx);
     if (n == 0) return TPE_OK;
     if (!samples || !p || !out || upper <= 0) return ctx->fail(TPE_ERR_ARG, "bad arguments");
     tpe_label_desc d{};
@@ -1239,6 +1263,7 @@ static int one_label_sample(tpe_ctx* ctx, int kind, const double* w, const doubl
                             double q, uint64_t seed, uint32_t stream, uint32_t round,
                             int64_t offset, int64_t n, double* out) {
     if (!ctx) return TPE_ERR_ARG;
+    SingleSlot slot(ctx);
     if (n == 0) return TPE_OK;
     if (!out || !w) return ctx->fail(TPE_ERR_ARG, "null pointer");
     if (offset < 0 || offset + n > (int64_t)UINT32_MAX)
@@ -1252,14 +1277,14 @@ static int one_label_sample(tpe_ctx* ctx, int kind, const double* w, const doubl
     d.n_below = d.n_above = k;
     int rc = set_posterior_impl(ctx, &d, 1, w, mu, sg, k, true);
     if (rc) return rc;
-    ctx->h_labels[0].stream = (int32_t)stream;
-    HIPCHK(ctx, hipMemcpy(ctx->labels.p, ctx->h_labels.data(), sizeof(DLabel), hipMemcpyHostToDevice));
+    ctx->P->h_labels[0].stream = (int32_t)stream;
+    HIPCHK(ctx, hipMemcpy(ctx->P->labels.p, ctx->P->h_labels.data(), sizeof(DLabel), hipMemcpyHostToDevice));
     HIPCHK(ctx, ctx->cand.reserve(std::max<int64_t>(n, 1)));
     HIPCHK(ctx, ctx->rounds.reserve(1));
     HIPCHK(ctx, ctx->errflag.reserve(1));
     HIPCHK(ctx, hipMemcpyAsync(ctx->rounds.p, &round, sizeof(uint32_t), hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->errflag.p, 0, sizeof(int32_t), ctx->stream));
-    launch_sample_only(ctx, ctx->h_labels[0].mode, n, offset, seed, ctx->cand.p);
+    launch_sample_only(ctx, ctx->P->h_labels[0].mode, n, offset, seed, ctx->cand.p);
     HIPCHK(ctx, hipGetLastError());
     int32_t errh = 0;
     HIPCHK(ctx, hipMemcpyAsync(&errh, ctx->errflag.p, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));

@@ -324,3 +324,17 @@ def test_batched_small_candidate_sets(eng, C):
             best, val = _oracle_winner(eng, meta, rec, li, C, seed, rnd)
             assert int(batch[j][li]['index']) == best, (C, rnd, meta['kind'])
             assert batch[j][li]['value'] == val
+
+
+def test_single_ops_leave_resident_posterior(eng):
+    """GMM1_lpdf / samplers between rounds do not disturb the uploaded
+    posterior (they run on the context's one-label slot)."""
+    pairs = [(m, r) for fx, m, r in _all_cases() if m['variant'] == 'medium'][:4]
+    d, w, m, s = stack_cases(pairs)
+    eng.set_posterior(d, w, m, s)
+    before = eng.suggest(5, 4096, round=1)
+    eng.GMM1_lpdf(np.array([0.1, 0.2]), [0.5, 0.5], [0.0, 1.0], [1.0, 1.0])
+    eng.GMM1([1.0], [0.0], [1.0], seed=1, size=(16,))
+    eng.categorical(np.array([0.3, 0.7]), seed=2, size=(8,))
+    after = eng.suggest(5, 4096, round=1)
+    assert np.array_equal(before, after)
