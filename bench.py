@@ -24,17 +24,20 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-# Per (candidate, component) evaluation of the dense kernel families, counted
-# from the gfx950 ISA of the inner loop (DESIGN.md "Roofline"):
-#   fp64: v_add, v_mul, v_fma (exponent), v_rndne, v_cvt_i32, v_add (f),
-#         3 x v_fma (2^(f/2048) poly), v_mul (table), v_ldexp, v_add (acc)
-#         = 12 fp64 VALU instructions = 16 FLOP with FMA = 2, plus 3 int32
-#         ops (table index, exponent) and one ds_read_b64
-#   fp32: v_sub, v_mul, v_fma, v_exp_f32, v_add = 5 VALU instructions, 6 FLOP
-FLOPS_PER_EVAL = {'f64': 16.0, 'f32': 6.0}
-# issue slots per eval in units of that precision's VALU op (an int32 op
-# issues at twice the fp64 rate)
-VALU_INSTR_PER_EVAL = {'f64': 12.0 + 3 * 0.5, 'f32': 5.0}
+# Roofline of the dominant kernel (VALU-bound: neither HBM nor MFMA applies,
+# DESIGN.md "Roofline").  `achieved` counts ALGORITHMIC work, SURVEY.md 8(d):
+# per (candidate, component) eval d = x - mu, z = d s, t = fma(-z, z, c),
+# e = exp(t), acc += e = 5 FLOP + 1 exp, quoted as 6 FLOP/eval, against the
+# vendor vector peak for the dtype.
+FLOPS_PER_EVAL = {'f64': 6.0, 'f32': 6.0}
+# The issue-slot roofline (what actually bounds the kernel) counts the
+# instructions of the gfx950 inner loop per eval:
+#   fp64: v_fma (z), v_fma (t), v_rndne, v_add (f), 3 x v_fma (2^(f/2048)),
+#         v_cvt_i32, v_ldexp, v_fma (table product + accumulate) = 10 fp64
+#         VALU instructions, plus 3 int32 (table index, exponent) that issue at
+#         twice the fp64 rate, and one ds_read_b64
+#   fp32: v_sub, v_mul, v_fma, v_exp_f32, v_add = 5 VALU instructions
+VALU_INSTR_PER_EVAL = {'f64': 10.0 + 3 * 0.5, 'f32': 5.0}
 PEAK_FP64_VECTOR_TFLOPS = 78.6        # MI355X spec (MI355X_MICROARCH.md)
 PEAK_FP32_VECTOR_TFLOPS = 157.3
 # wave64 VALU lane-instructions per second at 2.4 GHz: 256 CU x 4 SIMD x
@@ -119,8 +122,8 @@ def measured_traffic(kernel_prefix):
         return None, None
     d = json.load(open(files[-1]))
     for name, v in d.items():
-        if name.startswith(kernel_prefix) and 'FETCH_SIZE' in v and 'WRITE_SIZE' in v:
-            return (v['FETCH_SIZE'] * 2 + v['WRITE_SIZE']) * 1024.0, os.path.relpath(files[-1], REPO)
+        if name.startswith(kernel_prefix) and '_hbm_bytes_per_launch' in v:
+            return v['_hbm_bytes_per_launch'], os.path.relpath(files[-1], REPO)
     return None, None
 
 
@@ -212,7 +215,7 @@ def main():
     dom_rate = mode_ev[dom] / (mode_ms[dom] * 1e-3)
     prec = args.precision
     peak = PEAK_FP64_VECTOR_TFLOPS if prec == 'f64' else PEAK_FP32_VECTOR_TFLOPS
-    kname = 'k_round<%s, %d, true>' % ('double' if prec == 'f64' else 'float', DENSE.index(dom))
+    kname = 'k_round<%s, %d, true,' % ('double' if prec == 'f64' else 'float', DENSE.index(dom))
     traffic, traffic_src = measured_traffic(kname)
     achieved = dom_rate * FLOPS_PER_EVAL[prec] / 1e12
     roof = {'bound': 'valu', 'kernel': 'k_round<%s,%s>' % (prec, dom),
@@ -235,6 +238,7 @@ def main():
                                    else 'candidate-sharded x%d') % world},
         'host_posterior_build_ms': round(t_post * 1e3, 2),
         'per_family_ms': {k: round(v / args.steps, 3) for k, v in mode_ms.items() if v},
+        'per_family_evals': {k: v // args.steps for k, v in mode_ev.items() if v},
         'roofline': roof,
     }
     if args.config == 5:

@@ -26,6 +26,7 @@ struct DLabel {
     double low, high, q;
     double exp_low, exp_high;   // LGMM1 quantized bounds in sample space
     double shift_b, shift_a;    // dense: LSE shift M (max_k log coef_k)
+    double centre;              // dense fp64: origin of the recentred records
     double logpacc_b, logpacc_a;// quantized: log(p_accept) per mixture
     int64_t comp_b, comp_a;     // record offsets into the component arrays
     int32_t nb, na;
@@ -34,8 +35,10 @@ struct DLabel {
     int32_t stream;             // Philox stream id (label position)
 };
 
-// Component record.  dense: (mu, a = sqrt(.5)/max(sigma,EPS), c = log coef - M, -)
-// quantized: (mu, a = 1/max(sqrt(2) sigma, EPS), -, w).  categorical: c = log p.
+// Component record.  dense fp64: (m = (mu - centre) a, a = sqrt(K/2)/max(sigma,EPS),
+// c = K (log coef - M), w) so that z = x' a - m with x' = x - centre (one FMA);
+// dense fp32: (mu, a, c, w) in log2 units.  quantized: (mu, a = 1/max(sqrt(2)
+// sigma, EPS), -, w).  categorical: c = log p.
 template <typename T>
 struct alignas(4 * sizeof(T)) Comp {
     T mu, a, c, w;
@@ -169,16 +172,30 @@ __device__ __forceinline__ double exp_scaled(double u, const double* __restrict_
     return ldexp(p * tab[ki & (kExpTabSize - 1)], ki >> kExpTabBits);
 }
 
+// acc + exp_scaled(u): the power of two is applied to the polynomial first so
+// the table product and the accumulation fuse into one FMA.
+__device__ __forceinline__ double exp_scaled_acc(double u, const double* __restrict__ tab,
+                                                 double acc) {
+    const double k = rint(u);
+    const double f = u - k;
+    double p = fma(kExpC3, f, kExpC2);
+    p = fma(p, f, kExpC1);
+    p = fma(p, f, 1.0);
+    const int ki = (int)k;
+    return fma(ldexp(p, ki >> kExpTabBits), tab[ki & (kExpTabSize - 1)], acc);
+}
+
+// x: recentred candidate (x - centre), records as documented at Comp.
 __device__ __forceinline__ double lse_twopass(const Comp<double>* __restrict__ c, int n, double x) {
     double m = -__builtin_inf();
     for (int k = 0; k < n; ++k) {
-        const double z = (x - c[k].mu) * c[k].a;
+        const double z = fma(x, c[k].a, -c[k].mu);
         m = fmax(m, fma(-z, z, c[k].c));
     }
     if (!(m > -__builtin_inf())) return __builtin_nan("");  // all -inf or NaN: reference gives NaN
     double s = 0.0;
     for (int k = 0; k < n; ++k) {
-        const double z = (x - c[k].mu) * c[k].a;
+        const double z = fma(x, c[k].a, -c[k].mu);
         s += exp((fma(-z, z, c[k].c) - m) * kExpScaleInv);
     }
     return log(s) + m * kExpScaleInv;
@@ -201,17 +218,20 @@ __device__ __forceinline__ float lse_twopass(const Comp<float>* __restrict__ c, 
 
 template <int R>
 __device__ __forceinline__ void lse_dense(const Comp<double>* __restrict__ c, int n, double shift,
-                                          const double (&x)[R], double (&out)[R],
-                                          const double* __restrict__ tab) {
-    double acc[R];
+                                          double centre, const double (&xin)[R],
+                                          double (&out)[R], const double* __restrict__ tab) {
+    double acc[R], x[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) acc[r] = 0.0;
+    for (int r = 0; r < R; ++r) {
+        acc[r] = 0.0;
+        x[r] = xin[r] - centre;
+    }
     for (int k = 0; k < n; ++k) {
-        const double mu = c[k].mu, a = c[k].a, cc = c[k].c;
+        const double m = c[k].mu, a = c[k].a, cc = c[k].c;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const double z = (x[r] - mu) * a;
-            acc[r] += exp_scaled(fma(-z, z, cc), tab);
+            const double z = fma(x[r], a, -m);
+            acc[r] = exp_scaled_acc(fma(-z, z, cc), tab, acc[r]);
         }
     }
 #pragma unroll
@@ -226,7 +246,7 @@ __device__ __forceinline__ void lse_dense(const Comp<double>* __restrict__ c, in
 // (exp2) is used directly; shift is in natural-log units.
 template <int R>
 __device__ __forceinline__ void lse_dense(const Comp<float>* __restrict__ c, int n, double shift,
-                                          const double (&xd)[R], double (&out)[R],
+                                          double, const double (&xd)[R], double (&out)[R],
                                           const double* __restrict__) {
     float x[R], acc[R];
 #pragma unroll

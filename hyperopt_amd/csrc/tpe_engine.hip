@@ -213,14 +213,14 @@ __global__ __launch_bounds__(kBlock) void k_round(
     }
 
     if constexpr (MODE == DENSE_GMM) {
-        lse_dense<R>(comps + L.comp_b, L.nb, L.shift_b, x, lb, exp_tab);
-        lse_dense<R>(comps + L.comp_a, L.na, L.shift_a, x, la, exp_tab);
+        lse_dense<R>(comps + L.comp_b, L.nb, L.shift_b, L.centre, x, lb, exp_tab);
+        lse_dense<R>(comps + L.comp_a, L.na, L.shift_a, L.centre, x, la, exp_tab);
     } else if constexpr (MODE == DENSE_LGMM) {
         double y[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) y[r] = log(x[r]);
-        lse_dense<R>(comps + L.comp_b, L.nb, L.shift_b, y, lb, exp_tab);
-        lse_dense<R>(comps + L.comp_a, L.na, L.shift_a, y, la, exp_tab);
+        lse_dense<R>(comps + L.comp_b, L.nb, L.shift_b, L.centre, y, lb, exp_tab);
+        lse_dense<R>(comps + L.comp_a, L.na, L.shift_a, L.centre, y, la, exp_tab);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             lb[r] -= y[r];
@@ -555,9 +555,9 @@ struct Folded {
     double shift = 0.0, logpacc = 0.0;
 };
 
-Folded fold_mixture(int kind, bool quant, int flags, double low, double high, const double* w,
-                    const double* mu, const double* sg, int n, Comp<double>* out64,
-                    Comp<float>* out32) {
+Folded fold_mixture(int kind, bool quant, int flags, double low, double high, double centre,
+                    const double* w, const double* mu, const double* sg, int n,
+                    Comp<double>* out64, Comp<float>* out32) {
     Folded f;
     const bool bounded = (flags & 3) != 0;
     double p_accept = 1.0;
@@ -598,7 +598,8 @@ Folded fold_mixture(int kind, bool quant, int flags, double low, double high, co
     const double sK = std::sqrt(kExpScale);
     for (int k = 0; k < n; ++k) {
         // fp64 records in exp_scaled units (see tpe_device.h: u = K t)
-        out64[k] = Comp<double>{mu[k], a[k] * sK, (c[k] - M) * kExpScale, w[k]};
+        out64[k] = Comp<double>{(mu[k] - centre) * (a[k] * sK), a[k] * sK, (c[k] - M) * kExpScale,
+                                w[k]};
         if (out32)
             out32[k] = Comp<float>{(float)mu[k], (float)(a[k] * std::sqrt(l2e)),
                                    (float)((c[k] - M) * l2e), (float)w[k]};
@@ -924,6 +925,20 @@ int set_posterior_impl(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_lab
         o.nb = d.n_below;
         o.na = d.n_above;
         o.stream = l;
+        if (d.kind != TPE_CATEGORICAL && !quant) {
+            // recentre both mixtures on the middle of their means: keeps
+            // (mu - centre) a small, so z = x' a - m loses nothing to rounding
+            double lo = INFINITY, hi = -INFINITY;
+            for (int side = 0; side < 2; ++side) {
+                const int64_t off = side ? d.above_off : d.below_off;
+                const int32_t n = side ? d.n_above : d.n_below;
+                for (int k = 0; k < n; ++k) {
+                    lo = std::min(lo, mus[off + k]);
+                    hi = std::max(hi, mus[off + k]);
+                }
+            }
+            o.centre = (std::isfinite(lo) && std::isfinite(hi)) ? 0.5 * lo + 0.5 * hi : 0.0;
+        }
         for (int side = 0; side < 2; ++side) {
             const int64_t off = side ? d.above_off : d.below_off;
             const int32_t n = side ? d.n_above : d.n_below;
@@ -937,7 +952,7 @@ int set_posterior_impl(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_lab
                     c32[at + k] = Comp<float>{0.f, 0.f, (float)lp, (float)weights[off + k]};
                 }
             } else {
-                Folded f = fold_mixture(d.kind, quant, d.flags, d.low, d.high, weights + off,
+                Folded f = fold_mixture(d.kind, quant, d.flags, d.low, d.high, o.centre, weights + off,
                                         mus + off, sigmas + off, n, c64.data() + at, c32.data() + at);
                 (side ? o.shift_a : o.shift_b) = f.shift;
                 (side ? o.logpacc_a : o.logpacc_b) = f.logpacc;

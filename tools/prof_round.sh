@@ -2,7 +2,7 @@
 # One measurement round on the GPU box: bench, kernel-trace stats, PMC passes.
 # Every GPU step has its own time limit; stop at the first abnormal exit.
 set -u
-R=${1:-r1}
+R=${1:?round tag}
 OUT=gpurun_out/$R
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
