@@ -31,18 +31,19 @@ sys.path.insert(0, REPO)
 # vendor vector peak for the dtype.
 FLOPS_PER_EVAL = {'f64': 6.0, 'f32': 6.0}
 # The issue-slot roofline (what actually bounds the kernel) counts the
-# instructions of the gfx950 inner loop per eval:
-#   fp64: v_fma (z), v_fma (t), v_rndne, v_add (f), 3 x v_fma (2^(f/2048)),
-#         v_cvt_i32, v_ldexp, v_fma (table product + accumulate) = 10 fp64
-#         VALU instructions, plus 3 int32 (table index, exponent) that issue at
-#         twice the fp64 rate, and one ds_read_b64
-#   fp32: v_sub, v_mul, v_fma, v_exp_f32, v_add = 5 VALU instructions
-VALU_INSTR_PER_EVAL = {'f64': 10.0 + 3 * 0.5, 'f32': 5.0}
+# instructions of the gfx950 inner loop per eval (tools/isa_loop_mix.py):
+#   fp64: v_fma (z), v_fma (u), v_rndne, v_add (f), 2 x v_fma (2^(f/4096)),
+#         v_cvt_i32, v_ldexp, v_fmac (table product + accumulate) = 9 fp64,
+#         3 int32 (table index, byte offset, exponent) and 1/4 v_mov_b64 (the
+#         component's mu, shared by 4 candidates) = 12.25 VALU instructions,
+#         each a 4-cycle wave64 issue on a 16-lane SIMD, plus one ds_read_b64
+#   fp32: v_sub, v_mul, v_fma, v_exp_f32 (8-cycle issue), v_add = 6 slots
+VALU_INSTR_PER_EVAL = {'f64': 12.25, 'f32': 6.0}
 PEAK_FP64_VECTOR_TFLOPS = 78.6        # MI355X spec (MI355X_MICROARCH.md)
 PEAK_FP32_VECTOR_TFLOPS = 157.3
-# wave64 VALU lane-instructions per second at 2.4 GHz: 256 CU x 4 SIMD x
-# (16 fp64 / 32 fp32 lanes per clock)
-PEAK_VALU_LANE_INSTR = {'f64': 256 * 4 * 16 * 2.4e9, 'f32': 256 * 4 * 32 * 2.4e9}
+# 4-cycle wave64 VALU issue slots per second at 2.4 GHz, in lanes: 256 CU x
+# 4 SIMD x 16 lanes per clock (unpacked fp32 and fp64 issue at the same rate)
+PEAK_VALU_LANE_INSTR = {'f64': 256 * 4 * 16 * 2.4e9, 'f32': 256 * 4 * 16 * 2.4e9}
 DENSE = ('dense_gmm1', 'dense_lgmm1')
 
 

@@ -146,28 +146,38 @@ __device__ __forceinline__ double np_max(double a, double b) { return (a != a ||
 // every component) or is NaN, the lane recomputes the reference's two-pass
 // form (row max first).
 //
-// fp64 records are pre-scaled by K = N/ln 2 (N = 2048, tpe_exp_table.h) on
+// fp64 records are pre-scaled by K = N/ln 2 (N = 4096, tpe_exp_table.h) on
 // the host (a' = a sqrt(K), c' = (c - M) K), so the fma that forms the
 // exponent directly yields u = K t <= 0, and exp(t) = 2^(u/N) is evaluated as
 //   k = rint(u), f = u - k (exact, |f| <= 1/2),
-//   2^(f/N) by a degree-3 polynomial (|f ln2/N| <= 1.7e-4: 3.5e-17 truncation),
+//   2^(f/N) by the degree-2 relative-minimax polynomial 1 + c1 f + c2 f^2
+//   (|f ln2/N| <= 8.5e-5: 2.5e-14 max relative error, tools/gen_exp_table.py),
 //   times 2^((k mod N)/N) from an N-entry LDS table, scaled by 2^(k div N)
-// -- about 1.5 ulp, 12 fp64 + 3 integer VALU operations per (candidate,
-// component) pair instead of ~23 fp64 (plus range selects) for a general exp.
-// The table costs 16 KB of LDS per workgroup; a wave's 32-lane groups hit
-// ~3.5-way bank conflicts on it whatever its size (bank pair = j mod 32).
+// -- 9 fp64 + 3 integer VALU operations per (candidate, component) pair
+// instead of ~23 fp64 (plus range selects) for a general exp.  The error
+// (~2.5e-14 + 2 ulp per term) is 4-5 orders below the 1e-9 parity bar.
+// The table costs 32 KB of LDS per workgroup (4 workgroups = 4 waves/SIMD per
+// CU, the same occupancy the kernel's 105 VGPRs allow); a wave's 32-lane
+// groups hit ~3.5-way bank conflicts on it whatever its size.
 __device__ __forceinline__ void load_exp_table(double* lds) {
     for (int i = threadIdx.x; i < kExpTabSize; i += blockDim.x) lds[i] = kExp2Tab[i];
     __syncthreads();
+}
+
+// 2^(f/N) for |f| <= 1/2 (Horner, kExpDeg fp64 FMAs)
+static_assert(kExpDeg == 2 || kExpDeg == 3, "tpe_exp_table.h: degree 2 or 3");
+__device__ __forceinline__ double exp_poly(double f) {
+    if constexpr (kExpDeg == 2)
+        return fma(fma(kExpC2, f, kExpC1), f, 1.0);
+    else
+        return fma(fma(fma(kExpC3, f, kExpC2), f, kExpC1), f, 1.0);
 }
 
 // exp(u / K) for u <= 0 (NaN / -inf propagate to NaN and trigger the fallback)
 __device__ __forceinline__ double exp_scaled(double u, const double* __restrict__ tab) {
     const double k = rint(u);
     const double f = u - k;
-    double p = fma(kExpC3, f, kExpC2);
-    p = fma(p, f, kExpC1);
-    p = fma(p, f, 1.0);
+    const double p = exp_poly(f);
     const int ki = (int)k;
     return ldexp(p * tab[ki & (kExpTabSize - 1)], ki >> kExpTabBits);
 }
@@ -178,9 +188,7 @@ __device__ __forceinline__ double exp_scaled_acc(double u, const double* __restr
                                                  double acc) {
     const double k = rint(u);
     const double f = u - k;
-    double p = fma(kExpC3, f, kExpC2);
-    p = fma(p, f, kExpC1);
-    p = fma(p, f, 1.0);
+    const double p = exp_poly(f);
     const int ki = (int)k;
     return fma(ldexp(p, ki >> kExpTabBits), tab[ki & (kExpTabSize - 1)], acc);
 }

@@ -53,8 +53,11 @@ struct QInfo {
 // ---------------------------------------------------------- block maxloc ----
 // broadcast_best (tpe.py:769-778) over one workgroup's candidates: per-thread
 // best of its R, wave64 butterfly, then the 4 waves through LDS.
+// `sh` is the calling kernel's kBlock/64-entry LDS array (declared in the
+// kernel, so every kernel owns exactly the LDS it declares).
 __device__ __forceinline__ void block_maxloc(uint64_t bk, int64_t bi, double bv, double bl,
-                                             double ba, Partial* __restrict__ dst) {
+                                             double ba, Partial* __restrict__ dst,
+                                             Partial* __restrict__ sh) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         const uint64_t ok = __shfl_xor(bk, off);
@@ -68,7 +71,6 @@ __device__ __forceinline__ void block_maxloc(uint64_t bk, int64_t bi, double bv,
             ba = oa;
         }
     }
-    __shared__ Partial sh[kBlock / 64];
     const int tid = threadIdx.x;
     if ((tid & 63) == 0) sh[tid >> 6] = Partial{bk, bi, bv, bl, ba};
     __syncthreads();
@@ -121,7 +123,7 @@ __device__ __forceinline__ void finish_slots(const Slots& S, const double (&x)[R
                                              const bool (&valid)[R], const int64_t (&z)[R],
                                              const int64_t (&gi)[R], int li, int32_t n_labels,
                                              int32_t tiles, Partial* __restrict__ partials,
-                                             void* lds_scratch) {
+                                             void* lds_scratch, Partial* __restrict__ sh) {
     if (S.cpack == 0) {
         uint64_t bk = 0;
         int64_t bi = INT64_MAX;
@@ -139,7 +141,7 @@ __device__ __forceinline__ void finish_slots(const Slots& S, const double (&x)[R
             }
         }
         block_maxloc(bk, bi, bv, bl, ba,
-                     partials + ((size_t)blockIdx.z * n_labels + li) * tiles + blockIdx.x);
+                     partials + ((size_t)blockIdx.z * n_labels + li) * tiles + blockIdx.x, sh);
         return;
     }
     // scratch: R*256 keys + R*256 winners (12 KB at R = 4), aliased on the
@@ -256,7 +258,8 @@ __global__ __launch_bounds__(kBlock) void k_round(
                 out_la[row + ci[r]] = la[r];
             }
     }
-    finish_slots<R>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials, exp_tab);
+    __shared__ Partial sh[kBlock / 64];
+    finish_slots<R>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials, exp_tab, sh);
 }
 
 // Quantized families, pass 1: draw every candidate, keep its grid index
@@ -360,7 +363,8 @@ __global__ __launch_bounds__(kBlock) void k_qscan(
         }
     }
     __shared__ double scratch[R * kBlock * 3 / 2];
-    finish_slots<R>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials, scratch);
+    __shared__ Partial sh[kBlock / 64];
+    finish_slots<R>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials, scratch, sh);
 }
 
 __global__ __launch_bounds__(kBlock) void k_reduce(const Partial* __restrict__ partials,
@@ -372,7 +376,8 @@ __global__ __launch_bounds__(kBlock) void k_reduce(const Partial* __restrict__ p
     for (int t = tid; t < tiles; t += kBlock)
         if (better(p[t].key, p[t].idx, best.key, best.idx)) best = p[t];
     __shared__ Partial res;
-    block_maxloc(best.key, best.idx, best.value, best.lb, best.la, &res);
+    __shared__ Partial sh[kBlock / 64];
+    block_maxloc(best.key, best.idx, best.value, best.lb, best.la, &res, sh);
     __syncthreads();
     if (tid == 0) {
         tpe_label_result r;
@@ -402,7 +407,8 @@ __global__ __launch_bounds__(kBlock) void k_argmax(const double* __restrict__ b,
             bi = i;
         }
     }
-    block_maxloc(bk, bi, 0.0, 0.0, 0.0, partials + blockIdx.x);
+    __shared__ Partial sh[kBlock / 64];
+    block_maxloc(bk, bi, 0.0, 0.0, 0.0, partials + blockIdx.x, sh);
 }
 
 // sample-only kernel (tpe_*_sample): one draw per thread, no scoring
