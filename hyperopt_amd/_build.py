@@ -12,8 +12,9 @@ REPO = os.path.dirname(HERE)
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = 'gfx950'
 
-SOURCES = [os.path.join(HERE, 'csrc', 'tpe_engine.hip')]
+SOURCES = [os.path.join(HERE, 'csrc', 'tpe_engine.hip'), os.path.join(HERE, 'csrc', 'tpe_build.hip')]
 DEPS = SOURCES + [os.path.join(HERE, 'csrc', 'tpe_device.h'),
+                  os.path.join(HERE, 'csrc', 'tpe_ctx.h'),
                   os.path.join(HERE, 'csrc', 'tpe_exp_table.h'),
                   os.path.join(REPO, 'include', 'hyperopt_tpe.h')]
 TARGET = os.path.join(HERE, 'libhyperopt_tpe.so')

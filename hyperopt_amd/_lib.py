@@ -33,12 +33,23 @@ TPE_HAS_LOW = 1
 TPE_HAS_HIGH = 2
 TPE_HAS_Q = 4
 
+TPE_OBS_IDENTITY = 0
+TPE_OBS_LOG = 1
+TPE_OBS_LOG_FLOOR = 2
+
 
 class LabelDesc(ctypes.Structure):
     _fields_ = [('kind', ctypes.c_int32), ('flags', ctypes.c_int32),
                 ('low', ctypes.c_double), ('high', ctypes.c_double), ('q', ctypes.c_double),
                 ('below_off', ctypes.c_int64), ('above_off', ctypes.c_int64),
                 ('n_below', ctypes.c_int32), ('n_above', ctypes.c_int32)]
+
+
+class LabelSpec(ctypes.Structure):
+    _fields_ = [('kind', ctypes.c_int32), ('flags', ctypes.c_int32),
+                ('low', ctypes.c_double), ('high', ctypes.c_double), ('q', ctypes.c_double),
+                ('prior_mu', ctypes.c_double), ('prior_sigma', ctypes.c_double),
+                ('upper', ctypes.c_int32), ('randint', ctypes.c_int32), ('p_off', ctypes.c_int64)]
 
 
 class LabelResult(ctypes.Structure):
@@ -49,6 +60,7 @@ class LabelResult(ctypes.Structure):
 
 assert ctypes.sizeof(LabelDesc) == 56
 assert ctypes.sizeof(LabelResult) == 48
+assert ctypes.sizeof(LabelSpec) == 64
 
 _P = ctypes.c_void_p
 _I32, _I64, _U32, _U64, _D = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
@@ -79,6 +91,10 @@ SIGNATURES = {
                                        ctypes.POINTER(ctypes.c_float)]),
     'tpe_last_evals': (ctypes.c_int64, [_P]),
     'tpe_last_mode_stats': (ctypes.c_int, [_P, _P, _P]),
+    'tpe_build_posterior': (ctypes.c_int, [_P, _P, _I32, _P, _I64, _P, _I64, _P, _P, _P, _D, _D,
+                                           _I32, _P]),
+    'tpe_get_mixture': (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _I32, _P]),
+    'tpe_last_build_ms': (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float)]),
 }
 
 _lib = None

@@ -1,0 +1,793 @@
+// tpe_build.hip -- the device posterior builder:
+// the per-suggestion descriptor build that the reference redoes in Python on
+// every call -- ap_filter_trials (hyperopt/tpe.py:624-648),
+// linear_forgetting_weights (:385-398), adaptive_parzen_normal (:404-477),
+// the categorical pseudocount posteriors (:581-617) -- for every label at
+// once, followed by the fold into the engine's resident records (the same
+// records tpe_set_posterior uploads).  Entry point: tpe_build_posterior.
+//
+// Pipeline (one HIP stream, no host round trip until the final DLabel read):
+//   k_split      one workgroup: the n_below lowest losses (lexicographic
+//                (loss, position) order -> a flag per trial)
+//   k_partition  one workgroup per label: order-preserving split of the
+//                label's observations into below / above (ballot + scan)
+//   segmented radix sort (hipCUB) of every above list, stable
+//   k_parzen     one workgroup per (label, side): sorted means with the prior
+//                inserted, gap sigmas, clip, linear-forgetting weights,
+//                numpy-ordered normalisation; categorical: weighted bincount
+//                in observation order + pseudocounts
+//   k_fold       one workgroup per label: p_accept, LSE shift, recentred
+//                exp-scaled records, sampling records, DLabel fields
+//
+// Bit-exactness: every arithmetic step of the mixture build is an IEEE
+// add/sub/mul/div/max in the reference's order (no FMA contraction), and sums
+// follow numpy's pairwise summation tree, so (weights, mus, sigmas) equal the
+// reference's for the same observations -- except where the reference itself
+// is implementation-defined: np.argsort's (unstable quicksort) order of tied
+// losses and tied observations.  Here ties are ordered by position (stable).
+#include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/hyperopt_tpe.h"
+#include "tpe_ctx.h"
+#include "tpe_device.h"
+
+using namespace tpe;
+using namespace tpe_rt;
+
+namespace {
+
+constexpr int kSplitBlock = 1024;
+constexpr int kPartBlock = 1024;
+constexpr int kParzenBlock = 256;
+constexpr int kMaxLF = 64;          // below-list capacity per label (lf <= kMaxLF)
+
+// ------------------------------------------------ numpy pairwise summation --
+// np.sum of a contiguous float64 vector: chunks of 8192 (numpy's reduction
+// buffer) added in order to 0.0; each chunk summed pairwise -- split n > 128
+// at n2 = n/2 - (n/2) % 8, leaves of <= 128 with 8 accumulators
+// (numpy/_core/src/umath/loops_utils.h.src).  On the device the leaves are
+// summed in parallel and combined in the same tree order.
+
+__device__ double pw_leaf(const double* __restrict__ a, int64_t n) {
+#pragma clang fp contract(off)
+    if (n < 8) {
+        double r = 0.0;
+        for (int64_t i = 0; i < n; ++i) r += a[i];
+        return r;
+    }
+    double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
+    int64_t i = 8;
+    for (; i < n - (n % 8); i += 8) {
+        r0 += a[i + 0];
+        r1 += a[i + 1];
+        r2 += a[i + 2];
+        r3 += a[i + 3];
+        r4 += a[i + 4];
+        r5 += a[i + 5];
+        r6 += a[i + 6];
+        r7 += a[i + 7];
+    }
+    double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+    for (; i < n; ++i) res += a[i];
+    return res;
+}
+
+// leaf starts of the pairwise tree of n, in order (one thread)
+__device__ int pw_enumerate(int64_t n, int64_t* __restrict__ starts) {
+    int64_t ss[64], sn[64];
+    int sp = 0, cnt = 0;
+    ss[sp] = 0;
+    sn[sp++] = n;
+    while (sp) {
+        --sp;
+        const int64_t s = ss[sp], m = sn[sp];
+        if (m <= 128) {
+            starts[cnt++] = s;
+        } else {
+            int64_t n2 = m / 2;
+            n2 -= n2 % 8;
+            ss[sp] = s + n2;   // right child, popped second
+            sn[sp++] = m - n2;
+            ss[sp] = s;
+            sn[sp++] = n2;
+        }
+    }
+    return cnt;
+}
+
+// the tree's post-order combination of the leaf sums (one thread)
+__device__ double pw_combine(int64_t n, const double* __restrict__ leaf) {
+#pragma clang fp contract(off)
+    int64_t fm[64];
+    int phase[64];
+    double acc[64];
+    int sp = 0, next = 0;
+    fm[sp] = n;
+    phase[sp++] = 0;
+    bool have = false;
+    double val = 0.0;
+    while (true) {
+        const int top = sp - 1;
+        if (have) {
+            if (phase[top] == 0) {          // left child done: descend right
+                acc[top] = val;
+                phase[top] = 1;
+                have = false;
+                int64_t n2 = fm[top] / 2;
+                n2 -= n2 % 8;
+                fm[sp] = fm[top] - n2;
+                phase[sp++] = 0;
+            } else {                        // both done
+                val = acc[top] + val;
+                if (--sp == 0) return val;
+            }
+            continue;
+        }
+        if (fm[top] <= 128) {
+            val = leaf[next++];
+            have = true;
+            if (--sp == 0) return val;
+            continue;
+        }
+        int64_t n2 = fm[top] / 2;
+        n2 -= n2 % 8;
+        fm[sp] = n2;
+        phase[sp++] = 0;
+    }
+}
+
+// np.sum(a[0:n]) by one workgroup: numpy reduces in buffer-sized chunks of
+// 8192 elements, accumulated sequentially from 0.0, each chunk summed
+// pairwise.  leaf_start / leaf_sum are this call's private global scratch
+// (capacity >= n / 56 + n / 8192 + 1).  Every thread returns the sum.
+constexpr int64_t kNpChunk = 8192;
+constexpr int kNpChunkLeaves = 64;   // 8192 = 64 leaves of 128
+
+__device__ double block_np_sum(const double* __restrict__ a, int64_t n, int64_t* __restrict__ leaf_start,
+                               double* __restrict__ leaf_sum) {
+#pragma clang fp contract(off)
+    __shared__ int cnt_sh;
+    __shared__ double res_sh;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int cnt = 0;
+        for (int64_t c = 0; c < n; c += kNpChunk) {
+            const int k = pw_enumerate(n - c < kNpChunk ? n - c : kNpChunk, leaf_start + cnt);
+            for (int i = 0; i < k; ++i) leaf_start[cnt + i] += c;
+            cnt += k;
+        }
+        cnt_sh = cnt;
+    }
+    __syncthreads();
+    const int cnt = cnt_sh;
+    for (int t = threadIdx.x; t < cnt; t += blockDim.x) {
+        const int64_t s = leaf_start[t];
+        const int64_t e = t + 1 < cnt ? leaf_start[t + 1] : n;
+        leaf_sum[t] = pw_leaf(a + s, e - s);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double r = 0.0;
+        int lp = 0;
+        for (int64_t c = 0; c < n; c += kNpChunk) {
+            const int64_t m = n - c < kNpChunk ? n - c : kNpChunk;
+            r += pw_combine(m, leaf_sum + lp);
+            lp += kNpChunkLeaves;   // only the last chunk may be partial
+        }
+        res_sh = r;
+    }
+    __syncthreads();
+    return res_sh;
+}
+
+// ------------------------------------------------------ reference helpers --
+// ascending total order of a loss (np.argsort puts NaN last; -0 == +0)
+__device__ __forceinline__ uint64_t asc_key(double s) {
+    if (s != s) return ~0ull;
+    if (s == 0.0) s = 0.0;
+    uint64_t b;
+    __builtin_memcpy(&b, &s, 8);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+// linear_forgetting_weights(n, lf)[i]  (tpe.py:385-398): a linspace(1/n, 1,
+// n - lf) ramp (numpy: i * step + start, last element = stop exactly) and
+// lf trailing ones.
+__device__ __forceinline__ double lf_weight(int64_t i, int64_t n, int32_t lf) {
+#pragma clang fp contract(off)
+    if (n < lf) return 1.0;
+    const int64_t num = n - lf;
+    if (i >= num) return 1.0;
+    const double start = 1.0 / (double)n;
+    if (num == 1) return start;
+    if (i == num - 1) return 1.0;
+    const double step = (1.0 - start) / (double)(num - 1);
+    return (double)i * step + start;
+}
+
+__device__ __forceinline__ double np_maximum(double a, double b) { return (a != a || a > b) ? a : b; }
+__device__ __forceinline__ double np_minimum(double a, double b) { return (a != a || a < b) ? a : b; }
+
+// --------------------------------------------------------------- kernels --
+
+// ap_filter_trials' split (tpe.py:636-645): flag the n_below lowest losses
+// (ties by position), by n_below rounds of a workgroup-wide lexicographic
+// argmin above the previous pick.
+__global__ __launch_bounds__(kSplitBlock) void k_split(const double* __restrict__ losses, int64_t T,
+                                                       int32_t n_below, uint8_t* __restrict__ below) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (int64_t i = tid; i < T; i += kSplitBlock) below[i] = 0;
+    __shared__ uint64_t wk[kSplitBlock / 64];
+    __shared__ int64_t wi[kSplitBlock / 64];
+    __shared__ uint64_t prev_k;
+    __shared__ int64_t prev_i;
+    if (tid == 0) {
+        prev_k = 0;
+        prev_i = -1;
+    }
+    __syncthreads();
+    for (int r = 0; r < n_below; ++r) {
+        const uint64_t pk = prev_k;
+        const int64_t pi = prev_i;
+        uint64_t bk = ~0ull;
+        int64_t bi = INT64_MAX;
+        for (int64_t i = tid; i < T; i += kSplitBlock) {
+            const uint64_t k = asc_key(losses[i]);
+            const bool after = k > pk || (k == pk && i > pi);
+            if (after && (k < bk || (k == bk && i < bi))) {
+                bk = k;
+                bi = i;
+            }
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint64_t ok = __shfl_xor(bk, off);
+            const int64_t oi = __shfl_xor(bi, off);
+            if (ok < bk || (ok == bk && oi < bi)) {
+                bk = ok;
+                bi = oi;
+            }
+        }
+        if (lane == 0) {
+            wk[wv] = bk;
+            wi[wv] = bi;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int w = 1; w < kSplitBlock / 64; ++w)
+                if (wk[w] < bk || (wk[w] == bk && wi[w] < bi)) {
+                    bk = wk[w];
+                    bi = wi[w];
+                }
+            if (bi != INT64_MAX) below[bi] = 1;
+            prev_k = bk;
+            prev_i = bi;
+        }
+        __syncthreads();
+    }
+}
+
+// ap_filter_trials' membership (tpe.py:639-646): the label's observations
+// whose trial is in the below set, and those whose trial is in the rest, in
+// their original (tid) order.  Observations whose trial is not among the
+// losses (obs_trial < 0) belong to neither, as in the reference.
+__global__ __launch_bounds__(kPartBlock) void k_partition(
+    const tpe_label_spec* __restrict__ specs, const int64_t* __restrict__ obs_off,
+    const int32_t* __restrict__ obs_trial, const double* __restrict__ obs_val,
+    const uint8_t* __restrict__ below, int64_t T, double* __restrict__ below_val,
+    double* __restrict__ keys, int32_t* __restrict__ idx, int32_t* __restrict__ counts,
+    int32_t* __restrict__ seg_begin, int32_t* __restrict__ seg_end, int32_t* __restrict__ err) {
+    const int l = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int64_t off = obs_off[l], M = obs_off[l + 1] - off;
+    __shared__ int wb[kPartBlock / 64], wa[kPartBlock / 64];
+    __shared__ int base_b, base_a;
+    if (tid == 0) base_b = base_a = 0;
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int64_t c0 = 0; c0 < M; c0 += kPartBlock) {
+        const int64_t i = c0 + tid;
+        bool isb = false, isa = false;
+        double v = 0.0;
+        if (i < M) {
+            const int32_t t = obs_trial[off + i];
+            v = obs_val[off + i];
+            if (t >= 0 && t < T) {
+                isb = below[t] != 0;
+                isa = !isb;
+            } else if (t >= T) {
+                atomicOr(err, 1);
+            }
+        }
+        const uint64_t bb = __ballot(isb), ba = __ballot(isa);
+        if (lane == 0) {
+            wb[wv] = __popcll(bb);
+            wa[wv] = __popcll(ba);
+        }
+        __syncthreads();
+        int ob = base_b, oa = base_a;
+        for (int w = 0; w < wv; ++w) {
+            ob += wb[w];
+            oa += wa[w];
+        }
+        if (isb) {
+            const int p = ob + __popcll(bb & lt);
+            if (p < kMaxLF) below_val[(size_t)l * kMaxLF + p] = v;
+            else atomicOr(err, 2);
+        }
+        if (isa) {
+            const int p = oa + __popcll(ba & lt);
+            keys[off + p] = v;
+            idx[off + p] = p;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            for (int w = 0; w < kPartBlock / 64; ++w) {
+                base_b += wb[w];
+                base_a += wa[w];
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        counts[2 * l] = base_b;
+        counts[2 * l + 1] = base_a;
+        seg_begin[l] = (int32_t)off;
+        seg_end[l] = (int32_t)(specs[l].kind == TPE_CATEGORICAL ? off : off + base_a);
+    }
+}
+
+// adaptive_parzen_normal (tpe.py:404-477) / categorical pseudocounts
+// (tpe.py:581-617) of one (label, side).  Output: (w, mu, sigma) at
+// mix_off[2 l + side], component count in kcount[2 l + side].
+__global__ __launch_bounds__(kParzenBlock) void k_parzen(
+    const tpe_label_spec* __restrict__ specs, const double* __restrict__ cat_p,
+    const int64_t* __restrict__ obs_off, const int32_t* __restrict__ counts,
+    const double* __restrict__ below_val, const double* __restrict__ keys_unsorted,
+    const double* __restrict__ keys_sorted, const int32_t* __restrict__ idx_sorted,
+    const int64_t* __restrict__ mix_off, double prior_weight, int32_t lf, double* __restrict__ w,
+    double* __restrict__ mu, double* __restrict__ sigma, int32_t* __restrict__ kcount,
+    int64_t* __restrict__ leaf_start, double* __restrict__ leaf_sum) {
+#pragma clang fp contract(off)
+    const int l = blockIdx.x, side = blockIdx.y, tid = threadIdx.x;
+    const tpe_label_spec sp = specs[l];
+    const int64_t n = counts[2 * l + side];
+    const int64_t o = mix_off[2 * l + side];
+    const int64_t off = obs_off[l];
+    const double pw = prior_weight;
+    __shared__ double bk[kMaxLF];
+    __shared__ int32_t bi[kMaxLF];
+
+    if (sp.kind == TPE_CATEGORICAL) {
+        // weights = linear_forgetting_weights(len(obs)); counts = bincount(obs,
+        // minlength=upper, weights) -- each bin a sequential sum in
+        // observation order; pseudocounts; / np.sum(pseudocounts)
+        const double* list = side == 0 ? below_val + (size_t)l * kMaxLF : keys_unsorted + off;
+        const int32_t upper = sp.upper;
+        for (int b = tid; b < upper; b += kParzenBlock) {
+            double cnt = 0.0;
+            for (int64_t i = 0; i < n; ++i)
+                if ((int64_t)list[i] == b) cnt += lf_weight(i, n, lf);
+            const double pseudo = sp.randint ? cnt + pw
+                                             : cnt + (double)upper * (pw * cat_p[sp.p_off + b]);
+            w[o + b] = pseudo;
+            mu[o + b] = 0.0;
+            sigma[o + b] = 0.0;
+        }
+        const double tot = block_np_sum(w + o, upper, leaf_start + o, leaf_sum + o);
+        for (int b = tid; b < upper; b += kParzenBlock) w[o + b] = w[o + b] / tot;
+        if (tid == 0) kcount[2 * l + side] = upper;
+        return;
+    }
+
+    // sorted observations: below lists (<= lf) by a stable insertion sort in
+    // LDS, above lists from the segmented radix sort (stable)
+    const double* sk;
+    const int32_t* si;
+    if (side == 0) {
+        if (tid == 0) {
+            for (int64_t i = 0; i < n; ++i) {
+                const double v = below_val[(size_t)l * kMaxLF + i];
+                int64_t j = i;
+                while (j > 0 && bk[j - 1] > v) {
+                    bk[j] = bk[j - 1];
+                    bi[j] = bi[j - 1];
+                    --j;
+                }
+                bk[j] = v;
+                bi[j] = (int32_t)i;
+            }
+        }
+        __syncthreads();
+        sk = bk;
+        si = bi;
+    } else {
+        sk = keys_sorted + off;
+        si = idx_sorted + off;
+    }
+    const double pmu = sp.prior_mu, psig = sp.prior_sigma;
+    __shared__ int64_t pos_sh;
+    if (tid == 0) {
+        int64_t pos = 0;
+        if (n == 1) {
+            pos = pmu < sk[0] ? 0 : 1;
+        } else if (n >= 2) {  // np.searchsorted(sorted, prior_mu), side='left'
+            int64_t lo = 0, hi = n;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (sk[mid] < pmu) lo = mid + 1; else hi = mid;
+            }
+            pos = lo;
+        }
+        pos_sh = pos;
+    }
+    __syncthreads();
+    const int64_t pos = pos_sh, K = n + 1;
+    const bool use_lf = lf > 0 && lf < n;
+    const double maxsigma = psig / 1.0;
+    const double minsigma = psig / fmin(100.0, 1.0 + (double)K);
+    for (int64_t j = tid; j < K; j += kParzenBlock) {
+        auto srtd = [&](int64_t q) { return q < pos ? sk[q] : (q == pos ? pmu : sk[q - 1]); };
+        double s;
+        if (n == 0) {
+            s = psig;
+        } else if (n == 1) {
+            s = (j == pos) ? psig : psig * .5;
+        } else if (j == 0) {
+            s = srtd(1) - srtd(0);
+        } else if (j == K - 1) {
+            s = srtd(K - 1) - srtd(K - 2);
+        } else {
+            s = np_maximum(srtd(j) - srtd(j - 1), srtd(j + 1) - srtd(j));
+        }
+        s = np_minimum(np_maximum(s, minsigma), maxsigma);   // np.clip
+        if (j == pos) s = psig;
+        double wt;
+        if (j == pos) wt = pw;
+        else wt = use_lf ? lf_weight(si[j < pos ? j : j - 1], n, lf) : 1.0;
+        w[o + j] = wt;
+        mu[o + j] = srtd(j);
+        sigma[o + j] = s;
+    }
+    const double tot = block_np_sum(w + o, K, leaf_start + o, leaf_sum + o);
+    for (int64_t j = tid; j < K; j += kParzenBlock) w[o + j] = w[o + j] / tot;
+    if (tid == 0) kcount[2 * l + side] = (int32_t)K;
+}
+
+__device__ __forceinline__ double dev_normal_cdf(double x, double m, double s) {
+#pragma clang fp contract(off)
+    const double bottom = fmax(sqrt(2.0) * s, kEps);   // tpe.py:102-107
+    return 0.5 * (1.0 + erf((x - m) / bottom));
+}
+
+__device__ double block_max(double v) {
+    __shared__ double wm[kParzenBlock / 64];
+    __shared__ double res;
+    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double m = wm[0];
+        for (int i = 1; i < kParzenBlock / 64; ++i) m = fmax(m, wm[i]);
+        res = m;
+    }
+    __syncthreads();
+    return res;
+}
+
+__device__ double block_min(double v) { return -block_max(-v); }
+
+// The fold of tpe_set_posterior (tpe_engine.hip:fold_mixture) on the device:
+// p_accept, the LSE shift M, the recentred exp-scaled fp64 records, fp32
+// records, the below mixture's sampling records and the DLabel fields.
+__global__ __launch_bounds__(kParzenBlock) void k_fold(
+    DLabel* __restrict__ labels, const int32_t* __restrict__ kcount,
+    const int64_t* __restrict__ mix_off, const double* __restrict__ w, const double* __restrict__ mu,
+    const double* __restrict__ sigma, Comp<double>* __restrict__ c64, Comp<float>* __restrict__ c32,
+    SampRec* __restrict__ samp, double* __restrict__ terms, int64_t* __restrict__ leaf_start,
+    double* __restrict__ leaf_sum, int32_t* __restrict__ err) {
+#pragma clang fp contract(off)
+    const int l = blockIdx.x, tid = threadIdx.x;
+    DLabel d = labels[l];
+    const int64_t Kb = kcount[2 * l], Ka = kcount[2 * l + 1];
+    const int64_t ob = mix_off[2 * l], oa = mix_off[2 * l + 1];
+    const bool quant = d.mode == QUANT_GMM || d.mode == QUANT_LGMM;
+    const bool is_lgmm = d.mode == DENSE_LGMM || d.mode == QUANT_LGMM;
+    if (d.mode == CAT) {
+        for (int side = 0; side < 2; ++side) {
+            const int64_t o = side ? oa : ob, K = side ? Ka : Kb;
+            for (int64_t k = tid; k < K; k += kParzenBlock) {
+                const double p = w[o + k], lp = log(p);
+                c64[o + k] = Comp<double>{0.0, 0.0, lp, p};
+                c32[o + k] = Comp<float>{0.f, 0.f, (float)lp, (float)p};
+            }
+        }
+    } else {
+        double centre = 0.0;
+        if (!quant) {  // recentre on the middle of both mixtures' means
+            double lo = INFINITY, hi = -INFINITY;
+            for (int64_t k = tid; k < Kb; k += kParzenBlock) {
+                lo = fmin(lo, mu[ob + k]);
+                hi = fmax(hi, mu[ob + k]);
+            }
+            for (int64_t k = tid; k < Ka; k += kParzenBlock) {
+                lo = fmin(lo, mu[oa + k]);
+                hi = fmax(hi, mu[oa + k]);
+            }
+            lo = block_min(lo);
+            hi = block_max(hi);
+            centre = (isfinite(lo) && isfinite(hi)) ? 0.5 * lo + 0.5 * hi : 0.0;
+        }
+        d.centre = centre;
+        const bool bounded = (d.flags & 3) != 0;
+        const double sK = sqrt(kExpScale), l2e = 1.4426950408889634;
+        for (int side = 0; side < 2; ++side) {
+            const int64_t o = side ? oa : ob, K = side ? Ka : Kb;
+            double p_accept = 1.0;
+            if (bounded) {  // tpe.py:139-142 / 279-282
+                for (int64_t k = tid; k < K; k += kParzenBlock)
+                    terms[o + k] = w[o + k] * (dev_normal_cdf(d.high, mu[o + k], sigma[o + k]) -
+                                               dev_normal_cdf(d.low, mu[o + k], sigma[o + k]));
+                p_accept = block_np_sum(terms + o, K, leaf_start + o, leaf_sum + o);
+            }
+            if (quant) {
+                (side ? d.logpacc_a : d.logpacc_b) = log(p_accept);
+                for (int64_t k = tid; k < K; k += kParzenBlock) {
+                    const double a = 1.0 / fmax(sqrt(2.0) * sigma[o + k], kEps);
+                    c64[o + k] = Comp<double>{mu[o + k], a, 0.0, w[o + k]};
+                    c32[o + k] = Comp<float>{(float)mu[o + k], (float)a, 0.f, (float)w[o + k]};
+                }
+                continue;
+            }
+            double M = -INFINITY;
+            for (int64_t k = tid; k < K; k += kParzenBlock) {
+                const double sg = sigma[o + k];
+                double c;
+                if (!is_lgmm) {  // log(w / sqrt(2 pi sigma^2) / p_accept), tpe.py:148-150
+                    const double Z = sqrt(2.0 * M_PI * (sg * sg));
+                    c = log(w[o + k] / Z / p_accept);
+                } else {         // log w - log(max(sigma,EPS) sqrt(2 pi)), tpe.py:199-208
+                    const double s = fmax(sg, kEps);
+                    c = log(w[o + k]) - log(s * sqrt(2.0 * M_PI));
+                }
+                terms[o + k] = c;
+                M = fmax(M, c);
+            }
+            M = block_max(M);
+            if (!isfinite(M)) M = 0.0;
+            (side ? d.shift_a : d.shift_b) = M;
+            for (int64_t k = tid; k < K; k += kParzenBlock) {
+                const double s = fmax(sigma[o + k], kEps);
+                const double a = sqrt(0.5) / s;
+                const double c = terms[o + k];
+                c64[o + k] = Comp<double>{(mu[o + k] - centre) * (a * sK), a * sK, (c - M) * kExpScale,
+                                          w[o + k]};
+                c32[o + k] = Comp<float>{(float)mu[o + k], (float)(a * sqrt(l2e)), (float)((c - M) * l2e),
+                                         (float)w[o + k]};
+            }
+        }
+    }
+    // sampling records of the below mixture: cumulative normalised weights
+    if (tid == 0) {
+        double tot = 0.0;
+        for (int64_t k = 0; k < Kb; ++k) tot += w[ob + k];
+        if (!(tot > 0)) {
+            atomicOr(err, 4);
+            tot = 1.0;
+        }
+        double run = 0.0;
+        for (int64_t k = 0; k < Kb; ++k) {
+            run += w[ob + k];
+            SampRec s;
+            s.cdf = (k == Kb - 1) ? 1.0 : run / tot;
+            s.mu = d.mode == CAT ? 0.0 : mu[ob + k];
+            s.sigma = d.mode == CAT ? 0.0 : sigma[ob + k];
+            s.pad = 0.0;
+            samp[d.samp_off + k] = s;
+        }
+        d.nb = (int32_t)Kb;
+        d.na = (int32_t)Ka;
+        d.ns = (int32_t)Kb;
+        labels[l] = d;
+    }
+}
+
+}  // namespace
+
+// ================================================================ C ABI ====
+extern "C" {
+
+int tpe_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
+                        const double* cat_p, int64_t n_cat_p, const double* losses,
+                        int64_t n_trials, const int64_t* obs_off, const int32_t* obs_trial,
+                        const double* obs_val, double gamma, double prior_weight, int32_t lf,
+                        int32_t* n_below_out) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (n_labels <= 0 || !specs || !obs_off || n_trials < 0 || (n_trials > 0 && !losses))
+        return ctx->fail(TPE_ERR_ARG, "tpe_build_posterior: bad arguments");
+    if (lf < 1 || lf >= kMaxLF) return ctx->fail(TPE_ERR_ARG, "linear forgetting must be in [1, 63]");
+    if (n_trials >= INT32_MAX) return ctx->fail(TPE_ERR_ARG, "too many trials");
+    const int64_t n_obs = obs_off[n_labels];
+    if (obs_off[0] != 0 || n_obs < 0 || n_obs >= INT32_MAX || (n_obs > 0 && (!obs_trial || !obs_val)))
+        return ctx->fail(TPE_ERR_ARG, "observation offsets");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    auto& B = ctx->build;
+    Posterior& P = ctx->resident;
+    ctx->P = &ctx->resident;
+
+    // n_below = min(ceil(gamma sqrt(len(l_vals))), gamma_cap)   tpe.py:636
+    const double nbd = std::ceil(gamma * std::sqrt((double)n_trials));
+    const int32_t n_below = (int32_t)std::min<double>(nbd, (double)lf);
+
+    // static label fields, mixture / record regions
+    std::vector<DLabel> dl(n_labels);
+    std::vector<int64_t> mix(2 * (size_t)n_labels);
+    std::vector<int32_t> grp[kNumModes];
+    int64_t total = 0, samp_total = 0;
+    for (int32_t l = 0; l < n_labels; ++l) {
+        const tpe_label_spec& s = specs[l];
+        DLabel& o = dl[l];
+        std::memset(&o, 0, sizeof(o));
+        const int64_t M = obs_off[l + 1] - obs_off[l];
+        if (M < 0) return ctx->fail(TPE_ERR_ARG, "observation offsets must not decrease");
+        const bool quant = (s.flags & TPE_HAS_Q) != 0;
+        int64_t cap_b, cap_a;
+        if (s.kind == TPE_CATEGORICAL) {
+            if (s.upper <= 0) return ctx->fail(TPE_ERR_ARG, "categorical upper must be positive");
+            if (!s.randint && (s.p_off < 0 || s.p_off + s.upper > n_cat_p || !cat_p))
+                return ctx->fail(TPE_ERR_ARG, "categorical p out of range");
+            o.mode = CAT;
+            cap_b = cap_a = s.upper;
+        } else if (s.kind == TPE_GMM1 || s.kind == TPE_LGMM1) {
+            if ((s.flags & 3) == 1 || (s.flags & 3) == 2)
+                return ctx->fail(TPE_ERR_TYPE, "low and high must both be given or both be None");
+            if ((s.flags & 3) == 3 && !(s.low < s.high)) return ctx->fail(TPE_ERR_VALUE, "low >= high");
+            if (quant && !(s.q > 0) && !(s.q < 0)) return ctx->fail(TPE_ERR_VALUE, "q must be non-zero");
+            if (!(s.prior_sigma > 0)) return ctx->fail(TPE_ERR_VALUE, "prior sigma must be positive");
+            o.mode = s.kind == TPE_GMM1 ? (quant ? QUANT_GMM : DENSE_GMM) : (quant ? QUANT_LGMM : DENSE_LGMM);
+            cap_b = lf + 1;
+            cap_a = M + 1;
+        } else {
+            return ctx->fail(TPE_ERR_ARG, "label " + std::to_string(l) + ": unknown kind");
+        }
+        o.flags = s.kind == TPE_CATEGORICAL ? 0 : s.flags;
+        o.low = s.low;
+        o.high = s.high;
+        o.q = s.q;
+        o.exp_low = std::exp(s.low);
+        o.exp_high = std::exp(s.high);
+        o.stream = l;
+        o.comp_b = mix[2 * l] = total;
+        total += cap_b;
+        o.comp_a = mix[2 * l + 1] = total;
+        total += cap_a;
+        o.samp_off = samp_total;
+        samp_total += cap_b;
+        grp[o.mode].push_back(l);
+    }
+    const int64_t T = n_trials;
+    HIPCHK(ctx, B.specs.reserve(n_labels));
+    HIPCHK(ctx, B.cat_p.reserve(std::max<int64_t>(n_cat_p, 1)));
+    HIPCHK(ctx, B.losses.reserve(std::max<int64_t>(T, 1)));
+    HIPCHK(ctx, B.below.reserve(std::max<int64_t>(T, 1)));
+    HIPCHK(ctx, B.obs_off.reserve(n_labels + 1));
+    HIPCHK(ctx, B.obs_trial.reserve(std::max<int64_t>(n_obs, 1)));
+    HIPCHK(ctx, B.obs_val.reserve(std::max<int64_t>(n_obs, 1)));
+    HIPCHK(ctx, B.keys_in.reserve(std::max<int64_t>(n_obs, 1)));
+    HIPCHK(ctx, B.keys_out.reserve(std::max<int64_t>(n_obs, 1)));
+    HIPCHK(ctx, B.idx_in.reserve(std::max<int64_t>(n_obs, 1)));
+    HIPCHK(ctx, B.idx_out.reserve(std::max<int64_t>(n_obs, 1)));
+    HIPCHK(ctx, B.below_val.reserve((size_t)n_labels * kMaxLF));
+    HIPCHK(ctx, B.counts.reserve(2 * (size_t)n_labels));
+    HIPCHK(ctx, B.kcount.reserve(2 * (size_t)n_labels));
+    HIPCHK(ctx, B.seg_begin.reserve(n_labels));
+    HIPCHK(ctx, B.seg_end.reserve(n_labels));
+    HIPCHK(ctx, B.w.reserve(total));
+    HIPCHK(ctx, B.mu.reserve(total));
+    HIPCHK(ctx, B.sigma.reserve(total));
+    HIPCHK(ctx, B.mix_off.reserve(2 * (size_t)n_labels));
+    HIPCHK(ctx, B.scratch.reserve(2 * (size_t)total));
+    HIPCHK(ctx, B.leaf.reserve(total));
+    HIPCHK(ctx, P.labels.reserve(n_labels));
+    HIPCHK(ctx, P.comps64.reserve(total));
+    HIPCHK(ctx, P.comps32.reserve(total));
+    HIPCHK(ctx, P.samp.reserve(samp_total));
+    HIPCHK(ctx, ctx->errflag.reserve(1));
+    hipStream_t st = ctx->stream;
+    HIPCHK(ctx, hipMemcpyAsync(B.specs.p, specs, n_labels * sizeof(tpe_label_spec), hipMemcpyHostToDevice, st));
+    if (n_cat_p > 0 && cat_p)
+        HIPCHK(ctx, hipMemcpyAsync(B.cat_p.p, cat_p, n_cat_p * sizeof(double), hipMemcpyHostToDevice, st));
+    if (T > 0) HIPCHK(ctx, hipMemcpyAsync(B.losses.p, losses, T * sizeof(double), hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(B.obs_off.p, obs_off, (n_labels + 1) * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    if (n_obs > 0) {
+        HIPCHK(ctx, hipMemcpyAsync(B.obs_trial.p, obs_trial, n_obs * sizeof(int32_t), hipMemcpyHostToDevice, st));
+        HIPCHK(ctx, hipMemcpyAsync(B.obs_val.p, obs_val, n_obs * sizeof(double), hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(ctx, hipMemcpyAsync(B.mix_off.p, mix.data(), mix.size() * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemcpyAsync(P.labels.p, dl.data(), n_labels * sizeof(DLabel), hipMemcpyHostToDevice, st));
+    HIPCHK(ctx, hipMemsetAsync(ctx->errflag.p, 0, sizeof(int32_t), st));
+
+    HIPCHK(ctx, hipEventRecord(ctx->ev0, st));
+    if (T > 0)
+        hipLaunchKernelGGL(k_split, dim3(1), dim3(kSplitBlock), 0, st, B.losses.p, T, n_below, B.below.p);
+    hipLaunchKernelGGL(k_partition, dim3(n_labels), dim3(kPartBlock), 0, st, B.specs.p, B.obs_off.p,
+                       B.obs_trial.p, B.obs_val.p, B.below.p, T, B.below_val.p, B.keys_in.p, B.idx_in.p,
+                       B.counts.p, B.seg_begin.p, B.seg_end.p, ctx->errflag.p);
+    HIPCHK(ctx, hipGetLastError());
+    if (n_obs > 0) {  // stable segmented radix sort of every above list
+        size_t bytes = 0;
+        HIPCHK(ctx, hipcub::DeviceSegmentedRadixSort::SortPairs(
+                        nullptr, bytes, B.keys_in.p, B.keys_out.p, B.idx_in.p, B.idx_out.p, (int)n_obs,
+                        n_labels, B.seg_begin.p, B.seg_end.p, 0, 64, st));
+        HIPCHK(ctx, B.sort_tmp.reserve(std::max<size_t>(bytes, 1)));
+        HIPCHK(ctx, hipcub::DeviceSegmentedRadixSort::SortPairs(
+                        B.sort_tmp.p, bytes, B.keys_in.p, B.keys_out.p, B.idx_in.p, B.idx_out.p,
+                        (int)n_obs, n_labels, B.seg_begin.p, B.seg_end.p, 0, 64, st));
+    }
+    hipLaunchKernelGGL(k_parzen, dim3(n_labels, 2), dim3(kParzenBlock), 0, st, B.specs.p, B.cat_p.p,
+                       B.obs_off.p, B.counts.p, B.below_val.p, B.keys_in.p, B.keys_out.p, B.idx_out.p,
+                       B.mix_off.p, prior_weight, lf, B.w.p, B.mu.p, B.sigma.p, B.kcount.p, B.leaf.p,
+                       B.scratch.p + total);
+    hipLaunchKernelGGL(k_fold, dim3(n_labels), dim3(kParzenBlock), 0, st, P.labels.p, B.kcount.p,
+                       B.mix_off.p, B.w.p, B.mu.p, B.sigma.p, P.comps64.p, P.comps32.p, P.samp.p,
+                       B.scratch.p, B.leaf.p, B.scratch.p + total, ctx->errflag.p);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipEventRecord(ctx->ev1, st));
+    int32_t errh = 0;
+    HIPCHK(ctx, hipMemcpyAsync(dl.data(), P.labels.p, n_labels * sizeof(DLabel), hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(&errh, ctx->errflag.p, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    HIPCHK(ctx, hipEventElapsedTime(&ctx->build_ms, ctx->ev0, ctx->ev1));
+    if (errh & 1) return ctx->fail(TPE_ERR_ARG, "observation trial position out of range");
+    if (errh & 2) return ctx->fail(TPE_ERR_ARG, "more below observations than the below set (duplicate trial in a label?)");
+    if (errh & 4) return ctx->fail(TPE_ERR_VALUE, "below weights sum to zero");
+
+    std::vector<int32_t> cat;
+    for (int m = 0; m < kNumModes; ++m) {
+        P.group_off[m] = (int32_t)cat.size();
+        cat.insert(cat.end(), grp[m].begin(), grp[m].end());
+        P.h_group[m] = grp[m];
+    }
+    HIPCHK(ctx, P.groups.reserve(std::max<size_t>(cat.size(), 1)));
+    HIPCHK(ctx, hipMemcpy(P.groups.p, cat.data(), cat.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    P.h_labels = dl;
+    P.n_labels = n_labels;
+    B.n_labels = n_labels;
+    B.mix_h = mix;
+    if (n_below_out) *n_below_out = n_below;
+    return TPE_OK;
+}
+
+int tpe_get_mixture(tpe_ctx* ctx, int32_t label, int32_t side, double* weights, double* mus,
+                    double* sigmas, int32_t cap, int32_t* n) {
+    if (!ctx) return TPE_ERR_ARG;
+    auto& B = ctx->build;
+    if (label < 0 || label >= B.n_labels || side < 0 || side > 1 || ctx->resident.n_labels != B.n_labels)
+        return ctx->fail(TPE_ERR_ARG, "tpe_get_mixture: no such built mixture");
+    const DLabel& d = ctx->resident.h_labels[label];
+    const int32_t K = side ? d.na : d.nb;
+    if (n) *n = K;
+    const int32_t m = std::min(K, std::max(cap, 0));
+    const int64_t o = B.mix_h[2 * (size_t)label + side];
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    if (m > 0) {
+        if (weights) HIPCHK(ctx, hipMemcpy(weights, B.w.p + o, m * sizeof(double), hipMemcpyDeviceToHost));
+        if (mus) HIPCHK(ctx, hipMemcpy(mus, B.mu.p + o, m * sizeof(double), hipMemcpyDeviceToHost));
+        if (sigmas) HIPCHK(ctx, hipMemcpy(sigmas, B.sigma.p + o, m * sizeof(double), hipMemcpyDeviceToHost));
+    }
+    return TPE_OK;
+}
+
+int tpe_last_build_ms(const tpe_ctx* ctx, float* ms) {
+    if (!ctx || !ms) return TPE_ERR_ARG;
+    *ms = ctx->build_ms;
+    return TPE_OK;
+}
+
+}  // extern "C"

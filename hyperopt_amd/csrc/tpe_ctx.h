@@ -1,0 +1,170 @@
+// tpe_ctx.h -- the context shared by the suggestion engine (tpe_engine.hip)
+// and the device posterior builder (tpe_build.hip): device buffers, the
+// resident posterior, per-round scratch.  Host-side C++ only.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/hyperopt_tpe.h"
+#include "tpe_device.h"
+
+namespace tpe_rt {
+
+using tpe::Comp;
+using tpe::DLabel;
+using tpe::Partial;
+using tpe::SampRec;
+
+constexpr int kBlock = 256;
+constexpr int kNumModes = 5;
+
+// Per (round, quantized label) grid window decided on the host after k_qsample.
+struct QInfo {
+    int64_t jmin;
+    int64_t G;        // table slots; 0 = evaluate every candidate directly
+    int64_t tab_off;
+    int64_t pad;
+};
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T));
+        if (e == hipSuccess) cap = std::max<size_t>(n, 1);
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct Posterior {
+    std::vector<DLabel> h_labels;
+    std::vector<int32_t> h_group[kNumModes];   // label ids per mode
+    int32_t n_labels = 0;
+    DevBuf<DLabel> labels;
+    DevBuf<Comp<double>> comps64;
+    DevBuf<Comp<float>> comps32;
+    DevBuf<SampRec> samp;
+    DevBuf<int32_t> groups;              // concatenated h_group
+    int32_t group_off[kNumModes] = {};
+    void release() {
+        labels.release();
+        comps64.release();
+        comps32.release();
+        samp.release();
+        groups.release();
+        n_labels = 0;
+    }
+};
+
+// Scratch of the device posterior builder (tpe_build.hip), grown on demand.
+struct BuildBufs {
+    DevBuf<tpe_label_spec> specs;
+    DevBuf<double> cat_p;
+    DevBuf<double> losses;
+    DevBuf<uint8_t> below;         // per trial: in the below set
+    DevBuf<int64_t> obs_off;       // CSR offsets of the observations per label
+    DevBuf<int32_t> obs_trial;
+    DevBuf<double> obs_val;
+    DevBuf<double> keys_in, keys_out;   // above observations (sort keys)
+    DevBuf<int32_t> idx_in, idx_out;    // their position in the above list
+    DevBuf<double> below_val;      // per label, <= lf below observations
+    DevBuf<int32_t> counts;        // per label: below / above observation counts
+    DevBuf<int32_t> kcount;        // per label: below / above component counts
+    DevBuf<int32_t> seg_begin, seg_end;
+    DevBuf<uint8_t> sort_tmp;
+    DevBuf<double> w, mu, sigma;   // the built mixtures (tpe_get_mixture)
+    DevBuf<int64_t> mix_off;       // per label: below / above offsets into w/mu/sigma
+    DevBuf<double> scratch;        // per-component terms | pairwise leaf sums
+    DevBuf<int64_t> leaf;          // pairwise-summation leaf starts
+    int32_t n_labels = 0;          // labels of the last build (0: none resident)
+    std::vector<int64_t> mix_h;    // host copy of mix_off
+    void release() {
+        specs.release(); cat_p.release(); losses.release(); below.release();
+        obs_off.release(); obs_trial.release(); obs_val.release();
+        keys_in.release(); keys_out.release(); idx_in.release(); idx_out.release();
+        below_val.release(); counts.release(); seg_begin.release(); seg_end.release();
+        sort_tmp.release(); w.release(); mu.release(); sigma.release(); mix_off.release();
+        scratch.release(); kcount.release(); leaf.release();
+        n_labels = 0;
+    }
+};
+
+// numpy's pairwise float64 summation (np.sum of a contiguous vector)
+double np_pairwise_sum(const double* a, size_t n);
+
+}  // namespace tpe_rt
+
+struct tpe_ctx {
+    using Partial = tpe::Partial;
+    using QInfo = tpe_rt::QInfo;
+    template <typename T>
+    using DevBuf = tpe_rt::DevBuf<T>;
+    using Posterior = tpe_rt::Posterior;
+    static constexpr int kNumModes = tpe_rt::kNumModes;
+
+    int device = 0;
+    int precision = TPE_F64;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr;
+    hipEvent_t evm[kNumModes][2] = {};   // per-family kernel brackets
+    bool mode_ran[kNumModes] = {};
+    float mode_ms[kNumModes] = {};
+    int64_t mode_evals[kNumModes] = {};
+    std::string err;
+    float score_ms = 0.f, round_ms = 0.f;
+    int64_t evals = 0;
+    bool dedup = true;                   // quantized grid-value tables
+
+    // The resident posterior (tpe_set_posterior) and a separate one-label
+    // slot for the single-op entry points, so that GMM1_lpdf / GMM1 sampling
+    // calls never clobber the posterior a suggestion loop has uploaded.
+    Posterior resident, single;
+    Posterior* P = &resident;
+
+    // per-round scratch
+    DevBuf<Partial> partials;
+    DevBuf<tpe_label_result> results;
+    DevBuf<uint32_t> rounds;
+    DevBuf<int32_t> errflag;
+    DevBuf<double> cand, out_lb, out_la;
+    DevBuf<int32_t> one_group;
+    DevBuf<int64_t> qj;
+    DevBuf<unsigned long long> qmm;
+    DevBuf<QInfo> qinfo;
+    DevBuf<double2> qtab;
+    tpe_rt::BuildBufs build;             // device posterior builder scratch
+    int64_t built_n_trials = 0;          // last tpe_build_posterior: history size
+    int32_t built_n_below = 0;           //   and its below-set size
+    float build_ms = 0.f;                // device time of the last build
+
+    int fail(int code, const std::string& m) {
+        err = m;
+        return code;
+    }
+    int hip(hipError_t e, const char* what) {
+        if (e == hipSuccess) return TPE_OK;
+        err = std::string(what) + ": " + hipGetErrorString(e);
+        return TPE_ERR_HIP;
+    }
+};
+
+#define HIPCHK(ctx, call)                                  \
+    do {                                                   \
+        int _rc = (ctx)->hip((call), #call);               \
+        if (_rc != TPE_OK) return _rc;                     \
+    } while (0)

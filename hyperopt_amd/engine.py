@@ -47,6 +47,12 @@ DESC_DTYPE = np.dtype([('kind', '<i4'), ('flags', '<i4'), ('low', '<f8'), ('high
 assert DESC_DTYPE.itemsize == ctypes.sizeof(L.LabelDesc)
 
 
+SPEC_DTYPE = np.dtype([('kind', '<i4'), ('flags', '<i4'), ('low', '<f8'), ('high', '<f8'),
+                       ('q', '<f8'), ('prior_mu', '<f8'), ('prior_sigma', '<f8'),
+                       ('upper', '<i4'), ('randint', '<i4'), ('p_off', '<i8')])
+assert SPEC_DTYPE.itemsize == ctypes.sizeof(L.LabelSpec)
+
+
 def bounds_flags(low, high, q):
     f = 0
     if low is not None:
@@ -98,6 +104,41 @@ class Engine(object):
         self._check(self.lib.tpe_set_posterior(self.h, _ptr(descs), len(descs), _ptr(w),
                                                _ptr(m), _ptr(s), len(w)))
         self.n_labels = len(descs)
+
+    def build_posterior(self, specs, cat_p, losses, obs_off, obs_trial, obs_val, gamma,
+                        prior_weight, lf=25):
+        """Device posterior build from the history (tpe_build_posterior):
+        specs is a SPEC_DTYPE array, observations in CSR form (obs_off per
+        label; obs_trial = position in `losses`, -1 for none; obs_val already
+        transformed).  Returns n_below."""
+        specs = np.ascontiguousarray(specs, dtype=SPEC_DTYPE)
+        cat_p = _f64(cat_p)
+        losses = _f64(losses)
+        obs_off = np.ascontiguousarray(obs_off, dtype=np.int64)
+        obs_trial = np.ascontiguousarray(obs_trial, dtype=np.int32)
+        obs_val = _f64(obs_val)
+        nb = ctypes.c_int32()
+        self._check(self.lib.tpe_build_posterior(
+            self.h, _ptr(specs), len(specs), _ptr(cat_p), len(cat_p), _ptr(losses), len(losses),
+            _ptr(obs_off), _ptr(obs_trial), _ptr(obs_val), float(gamma), float(prior_weight),
+            int(lf), ctypes.byref(nb)))
+        self.n_labels = len(specs)
+        return nb.value
+
+    def get_mixture(self, label, side):
+        """(weights, mus, sigmas) of a built mixture (side 0 below, 1 above)."""
+        n = ctypes.c_int32()
+        self._check(self.lib.tpe_get_mixture(self.h, int(label), int(side), None, None, None, 0,
+                                             ctypes.byref(n)))
+        w, m, s = np.empty(n.value), np.empty(n.value), np.empty(n.value)
+        self._check(self.lib.tpe_get_mixture(self.h, int(label), int(side), _ptr(w), _ptr(m),
+                                             _ptr(s), n.value, ctypes.byref(n)))
+        return w, m, s
+
+    def last_build_ms(self):
+        ms = ctypes.c_float()
+        self._check(self.lib.tpe_last_build_ms(self.h, ctypes.byref(ms)))
+        return ms.value
 
     def suggest(self, seed, n_candidates, round=0, cand_offset=0):
         out = np.zeros(self.n_labels, dtype=RESULT_DTYPE)

@@ -178,6 +178,86 @@ def label_posterior(label, kind, args, below, above, prior_weight):
     return LabelPosterior(label, fam, mix[0], mix[1], q=q)
 
 
+def label_spec(kind, args):
+    """The tpe_label_spec fields of one hyperparameter and its observation
+    transform (the prior mapping of the ap_*_sampler registry, tpe.py:493-617):
+    (spec dict, transform function, categorical p or None)."""
+    if kind in CATEGORICAL:
+        upper = int(args['upper'])
+        p = None if kind == 'randint' else np.asarray(args['p'], dtype=float)
+        return dict(kind=L.TPE_CATEGORICAL, flags=0, upper=upper,
+                    randint=1 if kind == 'randint' else 0), None, p
+    if kind in ('uniform', 'quniform', 'loguniform', 'qloguniform'):
+        low, high = float(args['low']), float(args['high'])
+        spec = dict(low=low, high=high, prior_mu=0.5 * (high + low), prior_sigma=1.0 * (high - low),
+                    flags=L.TPE_HAS_LOW | L.TPE_HAS_HIGH)
+        if kind in ('quniform', 'qloguniform'):
+            spec['q'] = float(args['q'])
+            spec['flags'] |= L.TPE_HAS_Q
+        if kind in ('uniform', 'quniform'):
+            spec['kind'], tr = L.TPE_GMM1, None
+        elif kind == 'loguniform':
+            spec['kind'], tr = L.TPE_LGMM1, np.log
+        else:
+            floor = np.maximum(EPS, np.exp(low))              # tpe.py:536-540
+            spec['kind'], tr = L.TPE_LGMM1, (lambda o: np.log(np.maximum(o, floor)))
+        return spec, tr, None
+    spec = dict(prior_mu=float(args['mu']), prior_sigma=float(args['sigma']), flags=0)
+    if kind in ('qnormal', 'qlognormal'):
+        spec['q'] = float(args['q'])
+        spec['flags'] = L.TPE_HAS_Q
+    if kind in ('normal', 'qnormal'):
+        spec['kind'], tr = L.TPE_GMM1, None
+    elif kind == 'lognormal':
+        spec['kind'], tr = L.TPE_LGMM1, np.log
+    elif kind == 'qlognormal':
+        spec['kind'], tr = L.TPE_LGMM1, (lambda o: np.log(np.maximum(o, EPS)))
+    else:
+        raise ValueError('unknown distribution %r' % kind)
+    return spec, tr, None
+
+
+def device_inputs(labels, tids, losses, obs):
+    """Arguments of Engine.build_posterior (tpe_build_posterior) for a
+    history: labels = [(name, kind, args)], tids/losses of the represented
+    trials in tid order, obs[name] = (idxs, vals) in tid order.  Observations
+    are transformed here with the reference's own numpy expressions, and
+    mapped to their trial's position (-1 when the tid has no loss entry,
+    which ap_filter_trials drops, tpe.py:639-646)."""
+    from .engine import SPEC_DTYPE
+    tids = np.asarray(tids, dtype=np.int64)
+    specs = np.zeros(len(labels), dtype=SPEC_DTYPE)
+    cat_p, p_len = [], 0
+    off = [0]
+    trial_parts, val_parts = [], []
+    for i, (name, kind, args) in enumerate(labels):
+        sp, tr, p = label_spec(kind, args)
+        for k, v in sp.items():
+            specs[i][k] = v
+        if p is not None:
+            specs[i]['p_off'] = p_len
+            cat_p.append(p)
+            p_len += len(p)
+        oi, ov = obs[name]
+        oi = np.asarray(oi, dtype=np.int64)
+        ov = np.asarray(ov, dtype=float)
+        if tr is not None and len(ov):
+            ov = tr(ov)
+        if len(tids) and len(oi):
+            pos = np.searchsorted(tids, oi)
+            pc = np.minimum(pos, len(tids) - 1)
+            pos = np.where(tids[pc] == oi, pc, -1)
+        else:
+            pos = np.full(len(oi), -1, dtype=np.int64)
+        trial_parts.append(pos.astype(np.int32))
+        val_parts.append(ov)
+        off.append(off[-1] + len(oi))
+    cat = np.concatenate(cat_p) if cat_p else np.zeros(0)
+    return (specs, cat, np.asarray(losses, dtype=float), np.asarray(off, dtype=np.int64),
+            np.concatenate(trial_parts) if trial_parts else np.zeros(0, np.int32),
+            np.concatenate(val_parts) if val_parts else np.zeros(0))
+
+
 def pack(posts):
     """Flatten a list of LabelPosterior into (descs, weights, mus, sigmas)."""
     descs = np.zeros(len(posts), dtype=DESC_DTYPE)

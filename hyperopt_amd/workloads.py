@@ -80,6 +80,12 @@ class History(object):
         return posts
 
 
+    def device_inputs(self):
+        """Arguments of Engine.build_posterior for this history (after gamma,
+        prior_weight: see posterior.device_inputs)."""
+        return P.device_inputs(self.labels, self.tids, self.losses, self.obs)
+
+
 def mixed_space(n_labels):
     return [('x%03d' % i,) + CYCLE[i % 5] for i in range(n_labels)]
 

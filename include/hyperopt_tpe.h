@@ -72,6 +72,34 @@ typedef struct {
     int32_t n_above;
 } tpe_label_desc;       /* 56 bytes */
 
+/* Observation transforms of the adaptive-Parzen samplers (tpe.py:493-576),
+ * applied by the caller before tpe_build_posterior (so the transform is the
+ * caller's own float64 log, bit-for-bit the reference's np.log):
+ *   IDENTITY   uniform, quniform, normal, qnormal, randint, categorical
+ *   LOG        loguniform, lognormal:          log(obs)
+ *   LOG_FLOOR  qloguniform, qlognormal:        log(max(obs, floor)) */
+#define TPE_OBS_IDENTITY 0
+#define TPE_OBS_LOG 1
+#define TPE_OBS_LOG_FLOOR 2
+
+/* One hyperparameter as build_posterior sees it (tpe.py:678-692): the
+ * sampler arguments of its posterior and the prior of its adaptive-Parzen
+ * estimator. */
+typedef struct {
+    int32_t kind;        /* TPE_GMM1 / TPE_LGMM1 / TPE_CATEGORICAL             */
+    int32_t flags;       /* TPE_HAS_LOW | TPE_HAS_HIGH | TPE_HAS_Q             */
+    double low;          /* sampler arguments, as in tpe_label_desc            */
+    double high;
+    double q;
+    double prior_mu;     /* ap_*_sampler prior (tpe.py:493-576)                */
+    double prior_sigma;
+    int32_t upper;       /* categorical: number of categories                  */
+    int32_t randint;     /* categorical: 1 randint (counts + prior_weight,
+                            tpe.py:581-589), 0 pchoice (counts + upper *
+                            prior_weight * p, tpe.py:598-617)                  */
+    int64_t p_off;       /* pchoice: offset of its p vector in cat_p           */
+} tpe_label_spec;        /* 64 bytes */
+
 /* Winner of one label's candidate set (broadcast_best, tpe.py:769-778). */
 typedef struct {
     double value;       /* samples[best] (categorical: the integer index as double) */
@@ -143,6 +171,39 @@ int tpe_categorical_sample(tpe_ctx *ctx, const double *p, int32_t upper,
 int tpe_set_posterior(tpe_ctx *ctx, const tpe_label_desc *labels, int32_t n_labels,
                       const double *weights, const double *mus, const double *sigmas,
                       int64_t n_components);
+
+/* Build the resident posterior ON THE DEVICE from the trial history
+ * (replaces ap_filter_trials tpe.py:624-648, linear_forgetting_weights
+ * :385-398, adaptive_parzen_normal :404-477 and the categorical pseudocount
+ * posteriors :581-617 for every label, then the same upload as
+ * tpe_set_posterior).
+ *   losses[t], t < n_trials: loss of trial t, trials in tid order (the
+ *       order suggest() sorts docs in, tpe.py:858); +inf for no loss;
+ *   per label l, observations obs_off[l] .. obs_off[l+1]-1 in tid order:
+ *       obs_trial = position t of the observation's trial in `losses`,
+ *       obs_val   = the (already transformed, TPE_OBS_*) value;
+ *   gamma, prior_weight: the tpe.suggest arguments; lf: linear forgetting
+ *       (25 in the reference, DEFAULT_LF tpe.py:29 and gamma_cap :636).
+ * The below set is the n_below = min(ceil(gamma sqrt(n_trials)), lf) lowest
+ * losses; equal losses and equal observations are ordered by position
+ * (a stable sort; the reference's np.argsort order for ties is numpy's
+ * unstable quicksort).  n_below_out (may be NULL) receives n_below. */
+int tpe_build_posterior(tpe_ctx *ctx, const tpe_label_spec *specs, int32_t n_labels,
+                        const double *cat_p, int64_t n_cat_p,
+                        const double *losses, int64_t n_trials,
+                        const int64_t *obs_off, const int32_t *obs_trial,
+                        const double *obs_val, double gamma, double prior_weight,
+                        int32_t lf, int32_t *n_below_out);
+
+/* Read back one mixture of the resident posterior built by
+ * tpe_build_posterior (side 0 below, 1 above): the (weights, mus, sigmas)
+ * that adaptive_parzen_normal returns (categorical: p in weights).  *n
+ * receives the component count; at most `cap` entries are written. */
+int tpe_get_mixture(tpe_ctx *ctx, int32_t label, int32_t side, double *weights,
+                    double *mus, double *sigmas, int32_t cap, int32_t *n);
+
+/* Device time (ms, HIP events) of the last tpe_build_posterior's kernels. */
+int tpe_last_build_ms(const tpe_ctx *ctx, float *ms);
 
 /* One suggestion round over every resident label: sample n_candidates per
  * label from the below posterior (global candidate indices

@@ -92,3 +92,47 @@ def test_philox_known_answers():
     txt = open(HDR).read()
     for const in ('0xD2511F53u', '0xCD9E8D57u', '0x9E3779B9u', '0xBB67AE85u'):
         assert const in txt
+
+
+def _np_sum_restated(a):
+    """The summation order tpe_build.hip:block_np_sum and the host fold
+    (tpe_engine.hip:np_pairwise_sum) implement: 8192-element chunks added in
+    order to 0.0, each chunk summed pairwise (leaves <= 128, 8 accumulators)."""
+    def leaf(x):
+        n = len(x)
+        if n < 8:
+            r = 0.0
+            for v in x:
+                r += v
+            return r
+        r = list(x[:8])
+        i = 8
+        while i < n - (n % 8):
+            for j in range(8):
+                r[j] += x[i + j]
+            i += 8
+        res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))
+        for v in x[i:]:
+            res += v
+        return res
+
+    def pw(x):
+        if len(x) <= 128:
+            return leaf(x)
+        n2 = len(x) // 2
+        n2 -= n2 % 8
+        return pw(x[:n2]) + pw(x[n2:])
+
+    r = 0.0
+    for c in range(0, len(a), 8192):
+        r += pw(a[c:c + 8192])
+    return r
+
+
+def test_numpy_sum_order():
+    """np.sum's float64 summation order, which the device posterior builder
+    reproduces to get bit-identical normalised weights and p_accept."""
+    rng = np.random.RandomState(0)
+    for n in list(range(1, 40)) + [127, 128, 129, 1000, 8191, 8192, 8193, 9976, 20000, 50001]:
+        a = rng.uniform(0, 1, n) * 10 ** rng.uniform(-3, 3, n)
+        assert _np_sum_restated(a.tolist()) == np.sum(a), n

@@ -1,0 +1,174 @@
+"""Device posterior builder (tpe_build_posterior, hyperopt_amd/csrc/tpe_build.hip)
+against the CPU oracle's restatement of ap_filter_trials + adaptive_parzen_normal
++ the categorical pseudocount posteriors (tpe.py:385-477, 581-648).
+
+Bar: the built (weights, mus, sigmas) are BIT-IDENTICAL to the oracle's with
+stable tie order (sort_kind='stable'; the device orders tied losses / tied
+observations by position, the reference's np.argsort leaves that to numpy's
+unstable quicksort), and identical to the default-order oracle on tie-free
+histories.  The folded records are checked through a full suggestion round
+against the same mixtures uploaded with tpe_set_posterior (host fold)."""
+import numpy as np
+import pytest
+
+from oracle import tpe_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+ALL_KINDS = [
+    ('u', 'uniform', dict(low=-5.0, high=5.0)),
+    ('qu', 'quniform', dict(low=0.0, high=20.0, q=1.0)),
+    ('lu', 'loguniform', dict(low=-5.0, high=2.0)),
+    ('qlu', 'qloguniform', dict(low=0.0, high=4.0, q=1.0)),
+    ('n', 'normal', dict(mu=0.0, sigma=3.0)),
+    ('qn', 'qnormal', dict(mu=0.0, sigma=3.0, q=0.5)),
+    ('ln', 'lognormal', dict(mu=0.0, sigma=1.0)),
+    ('qln', 'qlognormal', dict(mu=1.0, sigma=1.0, q=1.0)),
+    ('ri', 'randint', dict(upper=7)),
+    ('pc', 'categorical', dict(upper=4, p=[0.1, 0.2, 0.3, 0.4])),
+]
+
+
+def make_history(labels, n_trials, seed, active_frac=1.0, loss_round=None, orphan=0):
+    """Synthetic history: prior draws, each label active in a random subset,
+    losses optionally rounded (ties), `orphan` observations whose tid has no
+    loss entry (the reference drops them)."""
+    from hyperopt_amd.workloads import History, prior_draw
+    rng = np.random.RandomState(seed)
+    tids = np.arange(n_trials, dtype=np.int64) * 3 + 5          # sparse, sorted tids
+    losses = rng.normal(size=n_trials)
+    if loss_round is not None:
+        losses = np.round(losses, loss_round)
+    obs = {}
+    for name, kind, args in labels:
+        act = tids[rng.uniform(size=n_trials) < active_frac] if active_frac < 1 else tids
+        v = prior_draw(kind, args, rng, len(act))
+        if orphan:
+            extra = np.arange(orphan, dtype=np.int64) * 3 + 6        # never a trial tid
+            act = np.concatenate([act, extra])
+            v = np.concatenate([v, prior_draw(kind, args, rng, orphan)])
+            o = np.argsort(act, kind='stable')
+            act, v = act[o], v[o]
+        obs[name] = (act, v)
+    return History(labels, tids, losses, obs)
+
+
+def oracle_mixtures(hist, gamma=0.25, pw=1.0, sort_kind='stable'):
+    out = []
+    for name, kind, args in hist.labels:
+        oi, ov = hist.obs[name]
+        r = O.label_posteriors(kind, args, oi, ov, hist.tids, hist.losses, gamma, pw,
+                               sort_kind=sort_kind)
+        if r[0] == 'CAT':
+            out.append(((r[1],), (r[2],)))
+        else:
+            out.append((r[0][1:4], r[1][1:4]))
+    return out
+
+
+@pytest.fixture(scope='module')
+def eng():
+    from hyperopt_amd.engine import Engine
+    e = Engine(0, 'f64')
+    yield e
+    e.close()
+
+
+def _build(eng, hist, gamma=0.25, pw=1.0):
+    return eng.build_posterior(*hist.device_inputs(), gamma=gamma, prior_weight=pw)
+
+
+def _check_bit_exact(eng, hist, want):
+    for li, (name, kind, _) in enumerate(hist.labels):
+        for side in (0, 1):
+            w, m, s = eng.get_mixture(li, side)
+            ref = want[li][side]
+            if kind in ('randint', 'categorical'):
+                assert np.array_equal(w, ref[0]), (name, side, w, ref[0])
+            else:
+                rw, rm, rs = ref
+                assert len(w) == len(rw), (name, side, len(w), len(rw))
+                assert np.array_equal(m, rm), (name, side, 'mus')
+                assert np.array_equal(s, rs), (name, side, 'sigmas')
+                assert np.array_equal(w, rw), (name, side, 'weights',
+                                               np.max(np.abs(w - rw)))
+
+
+@pytest.mark.parametrize('n_trials', [1, 2, 3, 25, 26, 27, 200, 3000])
+def test_build_all_kinds_bit_exact(eng, n_trials):
+    hist = make_history(ALL_KINDS, n_trials, seed=n_trials)
+    nb = _build(eng, hist)
+    assert nb == min(int(np.ceil(0.25 * np.sqrt(n_trials))), 25)
+    _check_bit_exact(eng, hist, oracle_mixtures(hist))
+
+
+def test_build_conditional_ties_orphans(eng):
+    """Labels active in subsets, tied losses, observations of trials without
+    a loss entry (dropped from both sets, tpe.py:639-646)."""
+    hist = make_history(ALL_KINDS, 1500, seed=7, active_frac=0.4, loss_round=1, orphan=17)
+    _build(eng, hist)
+    _check_bit_exact(eng, hist, oracle_mixtures(hist, sort_kind='stable'))
+
+
+def test_build_matches_default_order_when_tie_free(eng):
+    """Continuous kinds and distinct losses: the stable order IS numpy's
+    order, so the build equals the reference's default-order mixtures."""
+    labels = [l for l in ALL_KINDS if l[1] in ('uniform', 'loguniform', 'normal', 'lognormal')]
+    hist = make_history(labels, 5000, seed=3)
+    _build(eng, hist)
+    _check_bit_exact(eng, hist, oracle_mixtures(hist, sort_kind=None))
+
+
+@pytest.mark.parametrize('gamma,pw', [(0.25, 1.0), (0.5, 0.3), (0.1, 4.0)])
+def test_build_gamma_prior_weight(eng, gamma, pw):
+    hist = make_history(ALL_KINDS, 700, seed=11, active_frac=0.7)
+    _build(eng, hist, gamma, pw)
+    _check_bit_exact(eng, hist, oracle_mixtures(hist, gamma, pw))
+
+
+def test_build_config3_and_round_matches_host_fold(eng):
+    """Config-3 history (32 labels, 10k trials): bit-exact mixtures, then one
+    fused round on the device-folded records against the same mixtures folded
+    on the host (tpe_set_posterior): same winners, lpdfs within 1e-12."""
+    from hyperopt_amd.engine import Engine
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.workloads import mixed_history
+    hist = mixed_history(32, 10000, seed=0)
+    _build(eng, hist)
+    want = oracle_mixtures(hist)
+    _check_bit_exact(eng, hist, want)
+    res_dev = eng.suggest(seed=99, n_candidates=1 << 16, round=3)
+    posts = []
+    for li, (name, kind, args) in enumerate(hist.labels):
+        b, a = (eng.get_mixture(li, 0), eng.get_mixture(li, 1))
+        if kind in ('randint', 'categorical'):
+            posts.append(P.LabelPosterior(name, 'categorical', b[0], a[0], upper=len(b[0])))
+        else:
+            spec, _, _ = P.label_spec(kind, args)
+            fam = 'GMM1' if spec['kind'] == 0 else 'LGMM1'
+            posts.append(P.LabelPosterior(name, fam, b, a, low=args.get('low'),
+                                          high=args.get('high'), q=args.get('q')))
+    e2 = Engine(0, 'f64')
+    try:
+        e2.set_posterior(*P.pack(posts))
+        res_host = e2.suggest(seed=99, n_candidates=1 << 16, round=3)
+    finally:
+        e2.close()
+    assert np.array_equal(res_dev['index'], res_host['index'])
+    assert np.array_equal(res_dev['value'], res_host['value'])
+    for f in ('lpdf_below', 'lpdf_above'):
+        np.testing.assert_allclose(res_dev[f], res_host[f], rtol=1e-12, atol=1e-12)
+
+
+def test_build_errors(eng):
+    from hyperopt_amd.engine import SPEC_DTYPE
+    hist = make_history(ALL_KINDS[:1], 50, seed=1)
+    specs, cat, losses, off, tr, val = hist.device_inputs()
+    bad = specs.copy()
+    bad[0]['low'], bad[0]['high'] = 1.0, 1.0
+    with pytest.raises(ValueError, match='low >= high'):
+        eng.build_posterior(bad, cat, losses, off, tr, val, 0.25, 1.0)
+    bad = np.zeros(1, dtype=SPEC_DTYPE)
+    bad[0]['kind'] = 9
+    with pytest.raises(Exception):
+        eng.build_posterior(bad, cat, losses, off, tr, val, 0.25, 1.0)
