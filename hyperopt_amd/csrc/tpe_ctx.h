@@ -147,6 +147,8 @@ struct tpe_ctx {
     DevBuf<unsigned long long> qmm;
     DevBuf<QInfo> qinfo;
     DevBuf<double2> qtab;
+    DevBuf<double> xs, slice_part;       // split-K map: candidates, slice sums
+    bool splitk = true;                  // split-K for small sampled rounds
     tpe_rt::BuildBufs build;             // device posterior builder scratch
     int64_t built_n_trials = 0;          // last tpe_build_posterior: history size
     int32_t built_n_below = 0;           //   and its below-set size

@@ -255,6 +255,174 @@ __global__ __launch_bounds__(kBlock) void k_round(
     finish_slots<R>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials, exp_tab, sh);
 }
 
+// ------------------------------------------------------- split-K map ----
+// Small candidate sets (tpe.suggest's default n_EI_candidates = 24, one
+// round): one workgroup per label would walk all K components serially and
+// leave the chip idle, so the component loop is split instead -- each wave
+// sums one slice of kSlice components of one mixture for every candidate of
+// the round (partial sums relative to the same LSE shift, or partial
+// probabilities for quantized labels), and a finishing kernel adds the
+// slices in order, takes the log and does the broadcast_best maxloc.
+constexpr int kSlice = 256;
+constexpr int kSliceWaves = kBlock / 64;
+
+// candidates of one (round, label): the same Philox draws as k_round / k_qsample
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_sample_small(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const SampRec* __restrict__ samp, int64_t n, int64_t cand_offset, uint64_t seed,
+    const uint32_t* __restrict__ rounds, int32_t n_rounds, int32_t n_labels,
+    double* __restrict__ xs, int32_t* __restrict__ err) {
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (s >= (int64_t)n_rounds * n) return;
+    const int64_t z = s / n, i = s - z * n;
+    double v;
+    if (!sample_below<MODE>(L, samp + L.samp_off, seed, rounds[z], (uint32_t)(cand_offset + i), v))
+        atomicOr(err, 1);
+    xs[((size_t)z * n_labels + li) * n + i] = v;
+}
+
+// one slice [k0, k1) of a mixture for candidate x (dense: sum of exp terms
+// relative to the mixture's shift; quantized: partial probability)
+template <typename T, int MODE>
+__device__ __forceinline__ double slice_sum(const DLabel& L, const Comp<T>* __restrict__ c,
+                                            const Comp<double>* __restrict__ c64, int k0, int k1,
+                                            double x, const double* __restrict__ tab) {
+    if constexpr (MODE == DENSE_GMM || MODE == DENSE_LGMM) {
+        const double v = (MODE == DENSE_LGMM) ? log(x) : x;
+        if constexpr (sizeof(T) == 8) {
+            const double xr = v - L.centre;
+            double acc = 0.0;
+            for (int k = k0; k < k1; ++k) {
+                const double z = fma(xr, c[k].a, -c[k].mu);
+                acc = exp_scaled_acc(fma(-z, z, c[k].c), tab, acc);
+            }
+            return acc;
+        } else {
+            const float xf = (float)v;
+            float acc = 0.0f;
+            for (int k = k0; k < k1; ++k) {
+                const float z = (xf - c[k].mu) * c[k].a;
+                acc += __builtin_amdgcn_exp2f(fmaf(-z, z, c[k].c));
+            }
+            return (double)acc;
+        }
+    } else {
+#pragma clang fp contract(off)
+        double ub, lb;
+        bool neg;
+        quant_bounds<MODE>(L, x, ub, lb, neg);
+        double prob = 0.0;
+        for (int k = k0; k < k1; ++k) {
+            const double mu = c64[k].mu, a = c64[k].a, w = c64[k].w;
+            double pu, pl;
+            if (MODE == QUANT_LGMM) {
+                pu = 0.5 + 0.5 * erf((ub - mu) * a);
+                pl = 0.5 + 0.5 * erf((lb - mu) * a);
+            } else {
+                pu = 0.5 * (1.0 + erf((ub - mu) * a));
+                pl = 0.5 * (1.0 + erf((lb - mu) * a));
+            }
+            double inc = w * pu;
+            inc -= w * pl;
+            prob += inc;
+        }
+        return prob;
+    }
+}
+
+// grid (slice groups, labels, rounds); wave w of workgroup b takes slice
+// b * kSliceWaves + w: below slices first, then above slices.
+template <typename T, int MODE>
+__global__ __launch_bounds__(kBlock) void k_score_slices(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<T>* __restrict__ comps, const Comp<double>* __restrict__ comps64, int64_t n,
+    int32_t n_labels, int32_t s_max, const double* __restrict__ xs, double* __restrict__ part) {
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    const int64_t z = blockIdx.z;
+    constexpr bool kTab = (MODE == DENSE_GMM || MODE == DENSE_LGMM) && sizeof(T) == 8;
+    __shared__ double exp_tab[kTab ? kExpTabSize : 1];
+    if constexpr (kTab) load_exp_table(exp_tab);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int nsb = (L.nb + kSlice - 1) / kSlice, nsa = (L.na + kSlice - 1) / kSlice;
+    const int slice = blockIdx.x * kSliceWaves + wave;
+    if (slice >= nsb + nsa) return;
+    const bool above = slice >= nsb;
+    const int k0 = (above ? slice - nsb : slice) * kSlice;
+    const int k1 = min(k0 + kSlice, above ? L.na : L.nb);
+    const int64_t base = above ? L.comp_a : L.comp_b;
+    const double* xrow = xs + ((size_t)z * n_labels + li) * n;
+    double* prow = part + (((size_t)z * n_labels + li) * s_max + slice) * n;
+    for (int64_t c = lane; c < n; c += 64)
+        prow[c] = slice_sum<T, MODE>(L, comps + base, comps64 + base, k0, k1, xrow[c], exp_tab);
+}
+
+// per (label, round): add the slices in order, log / shift, broadcast_best
+template <typename T, int MODE>
+__global__ __launch_bounds__(kBlock) void k_finish_slices(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<T>* __restrict__ comps, int64_t n, int64_t cand_offset, int32_t n_labels,
+    int32_t s_max, const double* __restrict__ xs, const double* __restrict__ part,
+    Partial* __restrict__ partials, int32_t* __restrict__ err) {
+    const int li = group[blockIdx.x];
+    const DLabel L = labels[li];
+    const int64_t z = blockIdx.y;
+    const int nsb = (L.nb + kSlice - 1) / kSlice, nsa = (L.na + kSlice - 1) / kSlice;
+    const double* xrow = xs + ((size_t)z * n_labels + li) * n;
+    const double* prow = part + ((size_t)z * n_labels + li) * s_max * n;
+    uint64_t bk = 0;
+    int64_t bi = INT64_MAX;
+    double bv = 0.0, bl = 0.0, ba = 0.0;
+    for (int64_t c = threadIdx.x; c < n; c += kBlock) {
+        const double x = xrow[c];
+        double sb = 0.0, sa = 0.0;
+        for (int s = 0; s < nsb; ++s) sb += prow[(size_t)s * n + c];
+        for (int s = 0; s < nsa; ++s) sa += prow[(size_t)(nsb + s) * n + c];
+        double lb, la;
+        if constexpr (MODE == DENSE_GMM || MODE == DENSE_LGMM) {
+            const double y = (MODE == DENSE_LGMM) ? log(x) : x;
+            if constexpr (sizeof(T) == 8) {
+                const double xr = y - L.centre;
+                lb = (sb >= 1e-290) ? log(sb) : lse_twopass(comps + L.comp_b, L.nb, xr);
+                la = (sa >= 1e-290) ? log(sa) : lse_twopass(comps + L.comp_a, L.na, xr);
+            } else {
+                const float yf = (float)y;
+                lb = (sb >= 1e-30) ? (double)(__builtin_log2f((float)sb) * 0.69314718055994531f)
+                                   : (double)lse_twopass(comps + L.comp_b, L.nb, yf);
+                la = (sa >= 1e-30) ? (double)(__builtin_log2f((float)sa) * 0.69314718055994531f)
+                                   : (double)lse_twopass(comps + L.comp_a, L.na, yf);
+            }
+            lb += L.shift_b;
+            la += L.shift_a;
+            if (MODE == DENSE_LGMM) {
+                lb -= y;
+                la -= y;
+            }
+        } else {
+            double ub, lo;
+            bool neg;
+            quant_bounds<MODE>(L, x, ub, lo, neg);
+            if (neg) atomicOr(err, 2);
+            lb = log(sb) - L.logpacc_b;
+            la = log(sa) - L.logpacc_a;
+        }
+        const int64_t gi = cand_offset + c;
+        const uint64_t key = order_key(lb - la);
+        if (better(key, gi, bk, bi)) {
+            bk = key;
+            bi = gi;
+            bv = x;
+            bl = lb;
+            ba = la;
+        }
+    }
+    __shared__ Partial sh[kBlock / 64];
+    block_maxloc(bk, bi, bv, bl, ba, partials + (size_t)z * n_labels + li, sh);
+}
+
 // Quantized families, pass 1: draw every candidate, keep its grid index
 // j = rint(v / q) (so x = j * q exactly as np.round(v / q) * q), and the
 // per-(round, label) min/max of j (order-preserving biased unsigned).
@@ -680,6 +848,39 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
     return TPE_OK;
 }
 
+// Split-K map (small sampled candidate sets): sample -> slice sums ->
+// finish, per family.  Returns the evaluations executed.
+constexpr int64_t kSplitKMaxSlots = 2048;   // n * n_rounds per label
+
+inline int slices_of(const DLabel& d) {
+    return (d.nb + kSlice - 1) / kSlice + (d.na + kSlice - 1) / kSlice;
+}
+
+template <typename T, int MODE>
+int launch_splitk(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int32_t s_max) {
+    const int nl = g.count[MODE];
+    if (nl == 0) return TPE_OK;
+    int32_t s_mode = 0;
+    for (int li : ctx->P->h_group[MODE]) s_mode = std::max(s_mode, slices_of(ctx->P->h_labels[li]));
+    const Comp<T>* comps;
+    if constexpr (sizeof(T) == 8) comps = ctx->P->comps64.p; else comps = ctx->P->comps32.p;
+    const int32_t L = ctx->P->n_labels;
+    bracket(ctx, MODE, 0);
+    const unsigned sb = (unsigned)((a.n * a.n_rounds + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_sample_small<MODE>, dim3(sb, nl), dim3(kBlock), 0, ctx->stream,
+                       ctx->P->labels.p, g.dev[MODE], ctx->P->samp.p, a.n, a.cand_offset, a.seed,
+                       ctx->rounds.p, a.n_rounds, L, ctx->xs.p, ctx->errflag.p);
+    hipLaunchKernelGGL((k_score_slices<T, MODE>),
+                       dim3((unsigned)((s_mode + kSliceWaves - 1) / kSliceWaves), nl, a.n_rounds),
+                       dim3(kBlock), 0, ctx->stream, ctx->P->labels.p, g.dev[MODE], comps,
+                       ctx->P->comps64.p, a.n, L, s_max, ctx->xs.p, ctx->slice_part.p);
+    hipLaunchKernelGGL((k_finish_slices<T, MODE>), dim3(nl, a.n_rounds), dim3(kBlock), 0,
+                       ctx->stream, ctx->P->labels.p, g.dev[MODE], comps, a.n, a.cand_offset, L, s_max,
+                       ctx->xs.p, ctx->slice_part.p, ctx->partials.p, ctx->errflag.p);
+    bracket(ctx, MODE, 1);
+    return ctx->hip(hipGetLastError(), "split-K launch");
+}
+
 int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_rounds, int64_t n,
               int64_t cand_offset, const double* cand_in_dev, double* olb, double* ola,
               tpe_label_result* out, int32_t only_label) {
@@ -733,7 +934,32 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     const bool sample = cand_in_dev == nullptr;
     int64_t evals_q[2] = {0, 0};
     HIPCHK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
-    if (sample) {
+    // split-K for small sampled rounds (packed map, one tile per label)
+    const bool splitk = sample && ctx->splitk && n > 0 && S.cpack != 0 &&
+                        (int64_t)n * n_rounds <= kSplitKMaxSlots;
+    if (splitk) {
+        int32_t s_max = 1;
+        for (int m = 0; m < CAT; ++m)
+            for (int li : ctx->P->h_group[m]) s_max = std::max(s_max, slices_of(ctx->P->h_labels[li]));
+        HIPCHK(ctx, ctx->xs.reserve((size_t)n_rounds * L * n));
+        HIPCHK(ctx, ctx->slice_part.reserve((size_t)n_rounds * L * s_max * n));
+        int rc;
+        if (ctx->precision == TPE_F32) {
+            if ((rc = launch_splitk<float, DENSE_GMM>(ctx, g, a, s_max))) return rc;
+            if ((rc = launch_splitk<float, DENSE_LGMM>(ctx, g, a, s_max))) return rc;
+        } else {
+            if ((rc = launch_splitk<double, DENSE_GMM>(ctx, g, a, s_max))) return rc;
+            if ((rc = launch_splitk<double, DENSE_LGMM>(ctx, g, a, s_max))) return rc;
+        }
+        if ((rc = launch_splitk<double, QUANT_GMM>(ctx, g, a, s_max))) return rc;
+        if ((rc = launch_splitk<double, QUANT_LGMM>(ctx, g, a, s_max))) return rc;
+        for (int q = 0; q < 2; ++q)
+            for (int li : ctx->P->h_group[q ? QUANT_LGMM : QUANT_GMM]) {
+                const DLabel& d = ctx->P->h_labels[li];
+                evals_q[q] += n * (int64_t)n_rounds * (d.nb + d.na);
+            }
+        launch_round<double, CAT, true>(ctx, g, a);
+    } else if (sample) {
         int rc = launch_quantized(ctx, g, a, evals_q);
         if (rc) return rc;
         if (ctx->precision == TPE_F32) {
@@ -984,6 +1210,8 @@ int tpe_ctx_create(int device, int precision, tpe_ctx** out) {
     }
     const char* dd = getenv("TPE_NO_DEDUP");
     c->dedup = !(dd && dd[0] == '1');
+    const char* sk = getenv("TPE_NO_SPLITK");   // tests: force the packed map
+    c->splitk = !(sk && sk[0] == '1');
     *out = c;
     return TPE_OK;
 }
@@ -1006,6 +1234,8 @@ void tpe_ctx_destroy(tpe_ctx* c) {
     c->qmm.release();
     c->qinfo.release();
     c->qtab.release();
+    c->xs.release();
+    c->slice_part.release();
     c->build.release();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);

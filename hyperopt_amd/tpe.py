@@ -20,7 +20,12 @@
 
 Extra keyword arguments (not in the reference): `precision` ('f64' default,
 'f32' fast path), `device` (HIP ordinal), `batch` (True: one independent
-suggestion per new_id instead of only new_ids[0]).
+suggestion per new_id instead of only new_ids[0]), `posterior_builder`:
+'host' (numpy, posterior.py -- the reference's own np.argsort tie order),
+'device' (tpe_build_posterior on the GPU: split, sort, Parzen and fold in
+HIP kernels, ties ordered by position) or 'auto' (device once the history
+holds DEVICE_BUILD_MIN_OBS observations over all labels, where the host build
+starts to dominate the suggestion).
 """
 import logging
 import time
@@ -43,6 +48,7 @@ _default_n_EI_candidates = 24
 _default_gamma = 0.25
 _default_n_startup_jobs = 20
 _default_linear_forgetting = DEFAULT_LF
+DEVICE_BUILD_MIN_OBS = 16384
 
 # host-side restatements, exported under the reference's names
 ap_filter_trials_split = _post.split_history
@@ -87,6 +93,12 @@ def build_posteriors(domain, trials, prior_weight=_default_prior_weight,
     return specs, len(tids), posts
 
 
+def device_inputs(specs, tids, losses, obs):
+    """Arguments of Engine.build_posterior for a gathered history."""
+    labels = [(s.label, s.kind, s.args) for s in specs.values()]
+    return _post.device_inputs(labels, tids, losses, obs)
+
+
 def _doc(new_id, domain, trials, specs, values):
     active = _labels.active_labels(domain.expr, values)
     idxs = {k: ([new_id] if k in active else []) for k in specs}
@@ -102,15 +114,30 @@ def suggest(new_ids, domain, trials, seed,
             n_EI_candidates=_default_n_EI_candidates,
             gamma=_default_gamma,
             linear_forgetting=_default_linear_forgetting,
-            precision='f64', device=0, batch=False):
+            precision='f64', device=0, batch=False, posterior_builder='auto'):
     t0 = time.time()
-    specs, n_docs, posts = build_posteriors(domain, trials, prior_weight, gamma)
-    if n_docs < n_startup_jobs or posts is None:
-        if posts is None and n_startup_jobs <= 0:
+    if posterior_builder not in ('auto', 'host', 'device'):
+        raise ValueError('posterior_builder must be auto, host or device')
+    specs = specs_of(domain)
+    tids, losses, obs = _history.gather(domain, trials, list(specs))
+    n_docs = len(tids)
+    if n_docs < n_startup_jobs or n_docs == 0:
+        if n_docs == 0 and n_startup_jobs <= 0:
             logger.info('TPE using 0 trials')
         return rand.suggest(list(new_ids[:1]) if not batch else new_ids, domain, trials, seed)
     eng = _engine.get_engine(device, precision)
-    eng.set_posterior(*_post.pack(posts))
+    n_obs = sum(len(obs[k][0]) for k in specs)
+    if posterior_builder == 'device' or (posterior_builder == 'auto' and
+                                         n_obs >= DEVICE_BUILD_MIN_OBS):
+        eng.build_posterior(*device_inputs(specs, tids, losses, obs), gamma=gamma,
+                            prior_weight=prior_weight)
+    else:
+        splitter = _post.Splitter(tids, losses, gamma)
+        posts = []
+        for label, sp in specs.items():
+            b, a = splitter.split(*obs[label])
+            posts.append(_post.label_posterior(label, sp.kind, sp.args, b, a, prior_weight))
+        eng.set_posterior(*_post.pack(posts))
     ids = list(new_ids) if batch else [new_ids[0]]
     if len(ids) == 1:
         res = eng.suggest(seed, n_EI_candidates, round=ids[0])[None]

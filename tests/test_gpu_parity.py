@@ -79,7 +79,8 @@ def test_categorical_lpdf(eng):
     assert len(eng.categorical_lpdf(np.array([], dtype=int), p)) == 0
 
 
-def test_fused_round_matches_oracle(eng):
+@pytest.mark.parametrize('C', [24, 700, 3000])
+def test_fused_round_matches_oracle(eng, C):
     """Full round (in-kernel Philox sampling -> both lpdfs -> maxloc) over a
     multi-label posterior; the candidates are re-drawn through the sampler
     entry point with the same (seed, stream, round) and scored by the CPU
@@ -88,7 +89,7 @@ def test_fused_round_matches_oracle(eng):
              if m['n_hist'] in (26, 300) and m['variant'] == 'plain']
     d, w, m, s = stack_cases(pairs)
     eng.set_posterior(d, w, m, s)
-    C, seed, rnd = 3000, 12345, 7
+    seed, rnd = 12345, 7
     res = eng.suggest(seed, C, round=rnd)
     for li, (meta, rec) in enumerate(pairs):
         kw = meta['lpdf_kwargs']
@@ -107,6 +108,31 @@ def test_fused_round_matches_oracle(eng):
         assert int(res[li]['index']) == best, (li, meta['kind'])
         assert res[li]['value'] == cand[best]
         assert_lpdf_close([res[li]['lpdf_below']], [lb[best]], quantized=is_quantized(meta))
+
+
+def test_splitk_equals_packed_map(eng, monkeypatch):
+    """Small rounds (C = 24, the tpe.suggest default) run on the split-K map
+    (component slices summed by separate waves); forcing the packed map
+    (one workgroup walks every component) gives the same winners and lpdfs
+    up to the summation order."""
+    from hyperopt_amd.engine import Engine
+    pairs = [(m, r) for fx, m, r in _all_cases()
+             if m['variant'] in ('medium', 'plain') and m['n_hist'] in (26, 300, 2000)]
+    d, w, m, s = stack_cases(pairs)
+    eng.set_posterior(d, w, m, s)
+    monkeypatch.setenv('TPE_NO_SPLITK', '1')
+    e2 = Engine(0, 'f64')
+    try:
+        e2.set_posterior(d, w, m, s)
+        for C, rounds in ((24, [5]), (24, list(range(40))), (500, [1, 2, 3])):
+            a = eng.suggest_batch(77, rounds, C)
+            b = e2.suggest_batch(77, rounds, C)
+            assert np.array_equal(a['index'], b['index']), C
+            assert np.array_equal(a['value'], b['value']), C
+            np.testing.assert_allclose(a['lpdf_below'], b['lpdf_below'], rtol=1e-9, atol=1e-9)
+            np.testing.assert_allclose(a['lpdf_above'], b['lpdf_above'], rtol=1e-9, atol=1e-9)
+    finally:
+        e2.close()
 
 
 def test_shard_invariance(eng):

@@ -102,3 +102,41 @@ def test_suggest_deterministic_in_seed():
     b = tpe.suggest([100], dom, trials, 5)[0]['misc']['vals']
     c = tpe.suggest([100], dom, trials, 6)[0]['misc']['vals']
     assert a == b and a != c
+
+
+@pytest.mark.parametrize('name', ['quadratic1', 'many_dists', 'n_arms', 'q1_lognormal'])
+def test_opt_thresholds_device_posterior(name):
+    """The same TestOpt thresholds with the posterior built on the device
+    (tpe_build_posterior) at every suggestion."""
+    algo = partial(tpe.suggest, gamma=GAMMA.get(name, tpe._default_gamma),
+                   prior_weight=PW.get(name, tpe._default_prior_weight),
+                   n_EI_candidates=NEI.get(name, tpe._default_n_EI_candidates),
+                   posterior_builder='device')
+    n = LEN.get(name, 50)
+    best = []
+    for seed in (123, 7, 11):
+        trials = H.Trials()
+        H.fmin(passthrough, space=domains.ALL[name](), algo=algo, trials=trials,
+               max_evals=n, rstate=np.random.RandomState(seed))
+        best.append(min(trials.losses()))
+        if best[-1] < THRESH[name]:
+            return
+    raise AssertionError('%s: best losses %s, threshold %s' % (name, best, THRESH[name]))
+
+
+def test_device_and_host_posterior_same_suggestion():
+    """Tie-free history (continuous labels, distinct losses): the device and
+    host builders give identical mixtures, so the suggested documents match;
+    conditional branches included."""
+    space = {'c': hp.choice('c', [{'u': hp.uniform('u', 0, 1)},
+                                  {'v': hp.normal('v', 0, 2), 'w': hp.lognormal('w', 0, 1)}]),
+             'x': hp.loguniform('x', -3, 3)}
+    trials = H.Trials()
+    H.fmin(lambda d: d['x'] + d['c'].get('u', 0.3) + 1e-3 * d['c'].get('v', 0.0),
+           space, algo=partial(tpe.suggest, posterior_builder='host'), max_evals=120,
+           trials=trials, rstate=np.random.RandomState(3))
+    dom = H.Domain(lambda d: 0, space)
+    for seed in (1, 2, 3):
+        a = tpe.suggest([500], dom, trials, seed, posterior_builder='host')[0]['misc']['vals']
+        b = tpe.suggest([500], dom, trials, seed, posterior_builder='device')[0]['misc']['vals']
+        assert a == b, (seed, a, b)
