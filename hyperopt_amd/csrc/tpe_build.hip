@@ -367,14 +367,43 @@ __global__ __launch_bounds__(kParzenBlock) void k_parzen(
         // weights = linear_forgetting_weights(len(obs)); counts = bincount(obs,
         // minlength=upper, weights) -- each bin a sequential sum in
         // observation order; pseudocounts; / np.sum(pseudocounts)
+        // The observations pass through LDS in chunks (bin index + LF weight
+        // per observation, computed in parallel); each bin's thread then
+        // accumulates its matches in observation order.
         const double* list = side == 0 ? below_val + (size_t)l * kMaxLF : keys_unsorted + off;
         const int32_t upper = sp.upper;
+        constexpr int kChunk = 2048;
+        __shared__ int32_t cb[kChunk];
+        __shared__ double cw[kChunk];
+        double cnt[4] = {0.0, 0.0, 0.0, 0.0};      // bins tid + 256 j, j < 4
+        for (int64_t c0 = 0; c0 < n; c0 += kChunk) {
+            const int m = (int)(n - c0 < kChunk ? n - c0 : kChunk);
+            __syncthreads();
+            for (int i = tid; i < m; i += kParzenBlock) {
+                cb[i] = (int32_t)(int64_t)list[c0 + i];
+                cw[i] = lf_weight(c0 + i, n, lf);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int b = tid + j * kParzenBlock;
+                if (b < upper)
+                    for (int i = 0; i < m; ++i)
+                        if (cb[i] == b) cnt[j] += cw[i];
+            }
+        }
+        if (upper > 4 * kParzenBlock) {   // very wide categoricals: direct scan
+            for (int b = tid + 4 * kParzenBlock; b < upper; b += kParzenBlock) {
+                double c = 0.0;
+                for (int64_t i = 0; i < n; ++i)
+                    if ((int64_t)list[i] == b) c += lf_weight(i, n, lf);
+                w[o + b] = c;
+            }
+        }
         for (int b = tid; b < upper; b += kParzenBlock) {
-            double cnt = 0.0;
-            for (int64_t i = 0; i < n; ++i)
-                if ((int64_t)list[i] == b) cnt += lf_weight(i, n, lf);
-            const double pseudo = sp.randint ? cnt + pw
-                                             : cnt + (double)upper * (pw * cat_p[sp.p_off + b]);
+            const double c = b < 4 * kParzenBlock ? cnt[b / kParzenBlock] : w[o + b];
+            const double pseudo = sp.randint ? c + pw
+                                             : c + (double)upper * (pw * cat_p[sp.p_off + b]);
             w[o + b] = pseudo;
             mu[o + b] = 0.0;
             sigma[o + b] = 0.0;

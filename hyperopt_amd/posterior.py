@@ -243,7 +243,10 @@ def device_inputs(labels, tids, losses, obs):
         ov = np.asarray(ov, dtype=float)
         if tr is not None and len(ov):
             ov = tr(ov)
-        if len(tids) and len(oi):
+        if len(oi) == len(tids) and len(oi) and oi[0] == tids[0] and oi[-1] == tids[-1] \
+                and np.array_equal(oi, tids):
+            pos = np.arange(len(oi))                 # label active in every trial
+        elif len(tids) and len(oi):
             pos = np.searchsorted(tids, oi)
             pc = np.minimum(pos, len(tids) - 1)
             pos = np.where(tids[pc] == oi, pc, -1)
