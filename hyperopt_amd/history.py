@@ -20,6 +20,10 @@ import weakref
 
 import numpy as np
 
+from .base import Domain
+
+_plain_loss = Domain.loss
+
 
 class _LabelColumn(object):
     __slots__ = ('tids', 'vals', 'n', 'ptids', 'pvals')
@@ -43,33 +47,65 @@ class HistoryCache(object):
         self.labels = list(labels)
         self.cols = {k: _LabelColumn() for k in self.labels}
         self.seen = {}          # id(doc) -> doc (keeps ids unique while cached)
+        self.n_ingested = 0
+        self.last_doc = None
+        self.order = []         # ingested docs in order (the fast path's view)
+        self.doc_tids = []      # their tids
+        self.tid_set = set()
+        self.has_from = False   # any doc with misc.from_tid != tid
+        self.dup_tid = False
+        self._tid_arr = np.zeros(0, dtype=np.int64)
 
     def ingest(self, docs):
-        for d in docs:
+        # fast path: the docs list grew by appending (Trials.refresh keeps the
+        # same doc objects in order) -- only the tail is new
+        k = self.n_ingested
+        if k and len(docs) >= k and docs[k - 1] is self.last_doc and id(docs[k - 1]) in self.seen:
+            new = docs[k:]
+        else:
+            new = docs
+        if new is docs:                      # not append-only: rebuild the order view
+            self.order, self.doc_tids, self.tid_set = [], [], set()
+            self.has_from = self.dup_tid = False
+            self._tid_arr = np.zeros(0, dtype=np.int64)
+        for d in new:
+            m = d['misc']
+            t = d['tid']
+            self.order.append(d)
+            self.doc_tids.append(t)
+            if t in self.tid_set:
+                self.dup_tid = True
+            self.tid_set.add(t)
+            if m.get('from_tid', t) != t:
+                self.has_from = True
             if id(d) in self.seen:
                 continue
             self.seen[id(d)] = d
-            m = d['misc']
             idxs, vals = m['idxs'], m['vals']
-            for k in self.labels:
-                ti = idxs.get(k, [])
+            for k2 in self.labels:
+                ti = idxs.get(k2, [])
                 if ti:
-                    c = self.cols[k]
+                    c = self.cols[k2]
                     c.tids.append(ti[0])
-                    c.vals.append(vals[k][0])
+                    c.vals.append(vals[k2][0])
+        self.n_ingested = len(docs)
+        self.last_doc = docs[-1] if docs else None
 
     def gather(self, domain, trials):
         """(tids, losses, obs) where obs[label] = (idxs, vals) arrays."""
         docs = trials.trials
         self.ingest(docs)
+        if type(domain).loss is _plain_loss:       # result.get('loss'), base.py Domain.loss
+            raw = [d['result'].get('loss') for d in docs]
+        else:
+            raw = [domain.loss(d['result'], d['spec']) for d in docs]
+        if not self.has_from and not self.dup_tid and len(self.order) == len(docs):
+            return self._gather_own(docs, raw)
+        own = [d['tid'] for d in docs]
+        keys = [d['misc'].get('from_tid', t) for d, t in zip(docs, own)]
         groups = {}
-        any_from = False
-        for d in docs:
-            m = d['misc']
-            g = m.get('from_tid', d['tid'])
-            if g != d['tid']:
-                any_from = True
-            loss = domain.loss(d['result'], d['spec'])
+        any_from = keys != own
+        for d, g, loss in zip(docs, keys, raw):
             loss = float('inf') if loss is None else float(loss)
             if g not in groups:
                 if loss == loss:                       # NaN never becomes best
@@ -110,6 +146,39 @@ class HistoryCache(object):
                         ti.append(x[0])
                         tv.append(m['vals'][k][0])
                 obs[k] = (np.asarray(ti, dtype=np.int64), np.asarray(tv, dtype=np.float64))
+        return tids, losses, obs
+
+
+    def _gather_own(self, docs, raw):
+        """Every doc is its own group (no from_tid, unique tids): vectorised,
+        with the tids kept incrementally."""
+        n = len(docs)
+        if len(self._tid_arr) != n:
+            self._tid_arr = np.concatenate([self._tid_arr, np.asarray(
+                self.doc_tids[len(self._tid_arr):], dtype=np.int64)])
+        tids = self._tid_arr
+        if None not in raw:                         # np.array would turn None into NaN
+            losses = np.array(raw, dtype=np.float64)
+        else:                                       # pending / failed: +inf (tpe.py:844-847)
+            losses = np.array([float('inf') if v is None else float(v) for v in raw],
+                              dtype=np.float64)
+        if n > 1 and not np.all(tids[1:] > tids[:-1]):
+            o = np.argsort(tids, kind='stable')
+            tids, losses = tids[o], losses[o]
+        keep = losses == losses                     # a NaN loss never becomes best
+        every = bool(keep.all()) and n == len(self.seen)
+        if not keep.all():
+            tids, losses = tids[keep], losses[keep]
+        obs = {}
+        for k in self.labels:
+            ti, tv = self.cols[k].arrays()
+            if not every:
+                m = np.isin(ti, tids)
+                ti, tv = ti[m], tv[m]
+            if len(ti) > 1 and not np.all(ti[1:] > ti[:-1]):
+                o = np.argsort(ti, kind='stable')
+                ti, tv = ti[o], tv[o]
+            obs[k] = (ti, tv)
         return tids, losses, obs
 
 

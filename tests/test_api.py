@@ -193,6 +193,50 @@ def test_scope_arithmetic_spaces():
     assert (a, b) == (2, 3)
 
 
+def _reference_gather(domain, trials):
+    """tpe.py:839-861 restated: best doc per from_tid group, None -> +inf,
+    sorted by group key."""
+    best_docs, best_loss = {}, {}
+    for doc in trials.trials:
+        tid = doc['misc'].get('from_tid', doc['tid'])
+        loss = domain.loss(doc['result'], doc['spec'])
+        loss = float('inf') if loss is None else float(loss)
+        best_loss.setdefault(tid, loss)
+        if loss <= best_loss[tid]:
+            best_loss[tid] = loss
+            best_docs[tid] = doc
+    items = sorted(best_docs.items())
+    return (np.asarray([k for k, _ in items], dtype=np.int64),
+            np.asarray([best_loss[k] for k, _ in items]))
+
+
+def test_history_gather_fast_path_incremental():
+    """The vectorised gather (own-group docs, incrementally cached tids)
+    against the reference's loop while trials are appended, left pending
+    (loss None -> +inf), given NaN losses, and re-ordered."""
+    from hyperopt_amd import history
+    space = {'x': hp.uniform('x', 0, 1), 'k': hp.choice('k', [0, 1, 2])}
+    domain = Domain(lambda d: 0.0, space)
+    trials = Trials()
+    H.fmin(lambda d: d['x'] + d['k'], space, algo=rand.suggest, max_evals=30, trials=trials,
+           rstate=np.random.RandomState(2))
+    specs = list(tpe.specs_of(domain))
+    for step in range(4):
+        if step == 1:                      # append more trials
+            H.fmin(lambda d: d['x'], space, algo=rand.suggest, max_evals=45, trials=trials,
+                   rstate=np.random.RandomState(3))
+        if step == 2:                      # pending (no loss) and NaN loss
+            trials.trials[4]['result'] = {'status': 'new'}
+            trials.trials[9]['result']['loss'] = float('nan')
+        if step == 3:                      # out-of-order doc list
+            trials._trials = trials._trials[::-1]
+        tids, losses, obs = history.gather(domain, trials, specs)
+        rt, rl = _reference_gather(domain, trials)
+        assert np.array_equal(tids, rt) and np.array_equal(losses, rl), step
+        xi, xv = obs['x']
+        assert np.all(np.diff(xi) > 0) and set(xi.tolist()) <= set(tids.tolist())
+
+
 REF = '/root/reference'
 
 
