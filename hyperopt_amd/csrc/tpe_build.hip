@@ -79,108 +79,108 @@ __device__ double pw_leaf(const double* __restrict__ a, int64_t n) {
     return res;
 }
 
-// leaf starts of the pairwise tree of n, in order (one thread)
-__device__ int pw_enumerate(int64_t n, int64_t* __restrict__ starts) {
-    int64_t ss[64], sn[64];
-    int sp = 0, cnt = 0;
-    ss[sp] = 0;
-    sn[sp++] = n;
-    while (sp) {
-        --sp;
-        const int64_t s = ss[sp], m = sn[sp];
-        if (m <= 128) {
-            starts[cnt++] = s;
-        } else {
-            int64_t n2 = m / 2;
-            n2 -= n2 % 8;
-            ss[sp] = s + n2;   // right child, popped second
-            sn[sp++] = m - n2;
-            ss[sp] = s;
-            sn[sp++] = n2;
-        }
-    }
-    return cnt;
+// The tree of one chunk (<= 8192 elements) has depth <= 8; the functions
+// below walk it by compile-time-unrolled recursion (distinct template
+// instances, no stack arrays, no device recursion).
+constexpr int64_t kNpChunk = 8192;
+constexpr int kNpChunkLeaves = 64;   // a full chunk: 64 leaves of 128
+constexpr int kPwDepth = 8;
+
+__device__ __forceinline__ int64_t pw_split(int64_t n) {
+    int64_t n2 = n / 2;
+    return n2 - n2 % 8;
 }
 
-// the tree's post-order combination of the leaf sums (one thread)
-__device__ double pw_combine(int64_t n, const double* __restrict__ leaf) {
+// number of leaves of the tree of n
+template <int D>
+__device__ __attribute__((noinline)) int pw_leaves(int64_t n) {
+    if constexpr (D == 0) {
+        return 1;
+    } else {
+        if (n <= 128) return 1;
+        const int64_t n2 = pw_split(n);
+        return pw_leaves<D - 1>(n2) + pw_leaves<D - 1>(n - n2);
+    }
+}
+
+// start and length of leaf t of the tree of n
+template <int D>
+__device__ __attribute__((noinline)) void pw_leaf_at(int64_t n, int t, int64_t& s, int64_t& len) {
+    if constexpr (D == 0) {
+        s = 0;
+        len = n;
+    } else {
+        if (n <= 128) {
+            s = 0;
+            len = n;
+            return;
+        }
+        const int64_t n2 = pw_split(n);
+        const int nl = pw_leaves<D - 1>(n2);
+        if (t < nl) {
+            pw_leaf_at<D - 1>(n2, t, s, len);
+        } else {
+            pw_leaf_at<D - 1>(n - n2, t - nl, s, len);
+            s += n2;
+        }
+    }
+}
+
+// the tree's combination of its leaf sums, left to right
+template <int D>
+__device__ __attribute__((noinline)) double pw_tree(int64_t n, const double* __restrict__ leaf, int& next) {
 #pragma clang fp contract(off)
-    int64_t fm[64];
-    int phase[64];
-    double acc[64];
-    int sp = 0, next = 0;
-    fm[sp] = n;
-    phase[sp++] = 0;
-    bool have = false;
-    double val = 0.0;
-    while (true) {
-        const int top = sp - 1;
-        if (have) {
-            if (phase[top] == 0) {          // left child done: descend right
-                acc[top] = val;
-                phase[top] = 1;
-                have = false;
-                int64_t n2 = fm[top] / 2;
-                n2 -= n2 % 8;
-                fm[sp] = fm[top] - n2;
-                phase[sp++] = 0;
-            } else {                        // both done
-                val = acc[top] + val;
-                if (--sp == 0) return val;
-            }
-            continue;
-        }
-        if (fm[top] <= 128) {
-            val = leaf[next++];
-            have = true;
-            if (--sp == 0) return val;
-            continue;
-        }
-        int64_t n2 = fm[top] / 2;
-        n2 -= n2 % 8;
-        fm[sp] = n2;
-        phase[sp++] = 0;
+    if constexpr (D == 0) {
+        return leaf[next++];
+    } else {
+        if (n <= 128) return leaf[next++];
+        const int64_t n2 = pw_split(n);
+        const double a = pw_tree<D - 1>(n2, leaf, next);
+        const double b = pw_tree<D - 1>(n - n2, leaf, next);
+        return a + b;
     }
 }
 
 // np.sum(a[0:n]) by one workgroup: numpy reduces in buffer-sized chunks of
 // 8192 elements, accumulated sequentially from 0.0, each chunk summed
-// pairwise.  leaf_start / leaf_sum are this call's private global scratch
-// (capacity >= n / 56 + n / 8192 + 1).  Every thread returns the sum.
-constexpr int64_t kNpChunk = 8192;
-constexpr int kNpChunkLeaves = 64;   // 8192 = 64 leaves of 128
-
-__device__ double block_np_sum(const double* __restrict__ a, int64_t n, int64_t* __restrict__ leaf_start,
-                               double* __restrict__ leaf_sum) {
+// pairwise.  Leaves are summed in parallel (full chunks: 64 leaves of 128;
+// the last chunk's leaves located by descent), chunk trees combined one
+// chunk per thread, chunks added in order.  leaf_sum is this call's private
+// global scratch (capacity >= n / 56 + 1).  Every thread returns the sum.
+__device__ double block_np_sum(const double* __restrict__ a, int64_t n, double* __restrict__ leaf_sum) {
 #pragma clang fp contract(off)
-    __shared__ int cnt_sh;
+    __shared__ double chunk_sum[64];
     __shared__ double res_sh;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int cnt = 0;
-        for (int64_t c = 0; c < n; c += kNpChunk) {
-            const int k = pw_enumerate(n - c < kNpChunk ? n - c : kNpChunk, leaf_start + cnt);
-            for (int i = 0; i < k; ++i) leaf_start[cnt + i] += c;
-            cnt += k;
+    const int64_t n_chunks = (n + kNpChunk - 1) / kNpChunk;
+    const int64_t full = n / kNpChunk;
+    const int64_t tail = n - full * kNpChunk;
+    const int tail_leaves = tail ? pw_leaves<kPwDepth>(tail) : 0;
+    const int64_t total = full * kNpChunkLeaves + tail_leaves;
+    for (int64_t t = threadIdx.x; t < total; t += blockDim.x) {
+        int64_t s, len;
+        if (t < full * kNpChunkLeaves) {
+            s = t * 128;
+            len = 128;
+        } else {
+            pw_leaf_at<kPwDepth>(tail, (int)(t - full * kNpChunkLeaves), s, len);
+            s += full * kNpChunk;
         }
-        cnt_sh = cnt;
+        leaf_sum[t] = pw_leaf(a + s, len);
     }
     __syncthreads();
-    const int cnt = cnt_sh;
-    for (int t = threadIdx.x; t < cnt; t += blockDim.x) {
-        const int64_t s = leaf_start[t];
-        const int64_t e = t + 1 < cnt ? leaf_start[t + 1] : n;
-        leaf_sum[t] = pw_leaf(a + s, e - s);
+    // chunk trees: one thread per chunk; sums beyond 64 chunks go through the
+    // leaf buffer's own slots (each chunk's first leaf slot is free once read)
+    for (int64_t c = threadIdx.x; c < n_chunks; c += blockDim.x) {
+        int next = 0;
+        const int64_t m = c < full ? kNpChunk : tail;
+        const double v = pw_tree<kPwDepth>(m, leaf_sum + c * kNpChunkLeaves, next);
+        if (c < 64) chunk_sum[c] = v;
+        else leaf_sum[c * kNpChunkLeaves] = v;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         double r = 0.0;
-        int lp = 0;
-        for (int64_t c = 0; c < n; c += kNpChunk) {
-            const int64_t m = n - c < kNpChunk ? n - c : kNpChunk;
-            r += pw_combine(m, leaf_sum + lp);
-            lp += kNpChunkLeaves;   // only the last chunk may be partial
-        }
+        for (int64_t c = 0; c < n_chunks; ++c) r += c < 64 ? chunk_sum[c] : leaf_sum[c * kNpChunkLeaves];
         res_sh = r;
     }
     __syncthreads();
@@ -199,17 +199,27 @@ __device__ __forceinline__ uint64_t asc_key(double s) {
 
 // linear_forgetting_weights(n, lf)[i]  (tpe.py:385-398): a linspace(1/n, 1,
 // n - lf) ramp (numpy: i * step + start, last element = stop exactly) and
-// lf trailing ones.
-__device__ __forceinline__ double lf_weight(int64_t i, int64_t n, int32_t lf) {
+// lf trailing ones.  The ramp constants are computed once per list.
+struct LFRamp {
+    int64_t num;      // ramp length n - lf (<= 0: all ones)
+    double start, step;
+};
+
+__device__ __forceinline__ LFRamp lf_ramp(int64_t n, int32_t lf) {
 #pragma clang fp contract(off)
-    if (n < lf) return 1.0;
-    const int64_t num = n - lf;
-    if (i >= num) return 1.0;
-    const double start = 1.0 / (double)n;
-    if (num == 1) return start;
-    if (i == num - 1) return 1.0;
-    const double step = (1.0 - start) / (double)(num - 1);
-    return (double)i * step + start;
+    LFRamp r;
+    r.num = n < lf ? 0 : n - lf;
+    r.start = n > 0 ? 1.0 / (double)n : 0.0;
+    r.step = r.num > 1 ? (1.0 - r.start) / (double)(r.num - 1) : 0.0;
+    return r;
+}
+
+__device__ __forceinline__ double lf_weight(int64_t i, const LFRamp& r) {
+#pragma clang fp contract(off)
+    if (i >= r.num) return 1.0;
+    if (r.num == 1) return r.start;
+    if (i == r.num - 1) return 1.0;
+    return (double)i * r.step + r.start;
 }
 
 __device__ __forceinline__ double np_maximum(double a, double b) { return (a != a || a > b) ? a : b; }
@@ -367,48 +377,46 @@ __global__ __launch_bounds__(kParzenBlock) void k_parzen(
         // weights = linear_forgetting_weights(len(obs)); counts = bincount(obs,
         // minlength=upper, weights) -- each bin a sequential sum in
         // observation order; pseudocounts; / np.sum(pseudocounts)
-        // The observations pass through LDS in chunks (bin index + LF weight
-        // per observation, computed in parallel); each bin's thread then
-        // accumulates its matches in observation order.
+        // One wave per bin: ballots over the list find the bin's observations
+        // in order, and the wave adds their weights one by one through scalar
+        // registers (v_readlane) -- the sequential order of np.bincount.
         const double* list = side == 0 ? below_val + (size_t)l * kMaxLF : keys_unsorted + off;
         const int32_t upper = sp.upper;
-        constexpr int kChunk = 2048;
-        __shared__ int32_t cb[kChunk];
-        __shared__ double cw[kChunk];
-        double cnt[4] = {0.0, 0.0, 0.0, 0.0};      // bins tid + 256 j, j < 4
-        for (int64_t c0 = 0; c0 < n; c0 += kChunk) {
-            const int m = (int)(n - c0 < kChunk ? n - c0 : kChunk);
-            __syncthreads();
-            for (int i = tid; i < m; i += kParzenBlock) {
-                cb[i] = (int32_t)(int64_t)list[c0 + i];
-                cw[i] = lf_weight(c0 + i, n, lf);
+        const LFRamp ramp = lf_ramp(n, lf);
+        const int wave = tid >> 6, lane = tid & 63;
+        for (int b = wave; b < upper; b += kParzenBlock / 64) {
+            double cnt = 0.0;
+            for (int64_t c0 = 0; c0 < n; c0 += 64) {
+                const int64_t i = c0 + lane;
+                const bool hit = i < n && (int64_t)list[i] == b;
+                uint64_t m = __ballot(hit);
+                if (!m) continue;
+                const double wl = hit ? lf_weight(i, ramp) : 0.0;
+                int64_t bits;
+                __builtin_memcpy(&bits, &wl, 8);
+                const int lo = (int)(uint32_t)bits, hi = (int)(uint32_t)(bits >> 32);
+                while (m) {
+                    const int j = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const uint64_t vb = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, j) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readlane(lo, j);
+                    double v;
+                    __builtin_memcpy(&v, &vb, 8);
+                    cnt += v;
+                }
             }
-            __syncthreads();
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int b = tid + j * kParzenBlock;
-                if (b < upper)
-                    for (int i = 0; i < m; ++i)
-                        if (cb[i] == b) cnt[j] += cw[i];
-            }
+            if (lane == 0) w[o + b] = cnt;
         }
-        if (upper > 4 * kParzenBlock) {   // very wide categoricals: direct scan
-            for (int b = tid + 4 * kParzenBlock; b < upper; b += kParzenBlock) {
-                double c = 0.0;
-                for (int64_t i = 0; i < n; ++i)
-                    if ((int64_t)list[i] == b) c += lf_weight(i, n, lf);
-                w[o + b] = c;
-            }
-        }
+        __syncthreads();
         for (int b = tid; b < upper; b += kParzenBlock) {
-            const double c = b < 4 * kParzenBlock ? cnt[b / kParzenBlock] : w[o + b];
+            const double c = w[o + b];
             const double pseudo = sp.randint ? c + pw
                                              : c + (double)upper * (pw * cat_p[sp.p_off + b]);
             w[o + b] = pseudo;
             mu[o + b] = 0.0;
             sigma[o + b] = 0.0;
         }
-        const double tot = block_np_sum(w + o, upper, leaf_start + o, leaf_sum + o);
+        const double tot = block_np_sum(w + o, upper, leaf_sum + o);
         for (int b = tid; b < upper; b += kParzenBlock) w[o + b] = w[o + b] / tot;
         if (tid == 0) kcount[2 * l + side] = upper;
         return;
@@ -458,6 +466,7 @@ __global__ __launch_bounds__(kParzenBlock) void k_parzen(
     __syncthreads();
     const int64_t pos = pos_sh, K = n + 1;
     const bool use_lf = lf > 0 && lf < n;
+    const LFRamp ramp = lf_ramp(n, lf);
     const double maxsigma = psig / 1.0;
     const double minsigma = psig / fmin(100.0, 1.0 + (double)K);
     for (int64_t j = tid; j < K; j += kParzenBlock) {
@@ -478,12 +487,12 @@ __global__ __launch_bounds__(kParzenBlock) void k_parzen(
         if (j == pos) s = psig;
         double wt;
         if (j == pos) wt = pw;
-        else wt = use_lf ? lf_weight(si[j < pos ? j : j - 1], n, lf) : 1.0;
+        else wt = use_lf ? lf_weight(si[j < pos ? j : j - 1], ramp) : 1.0;
         w[o + j] = wt;
         mu[o + j] = srtd(j);
         sigma[o + j] = s;
     }
-    const double tot = block_np_sum(w + o, K, leaf_start + o, leaf_sum + o);
+    const double tot = block_np_sum(w + o, K, leaf_sum + o);
     for (int64_t j = tid; j < K; j += kParzenBlock) w[o + j] = w[o + j] / tot;
     if (tid == 0) kcount[2 * l + side] = (int32_t)K;
 }
@@ -563,7 +572,7 @@ __global__ __launch_bounds__(kParzenBlock) void k_fold(
                 for (int64_t k = tid; k < K; k += kParzenBlock)
                     terms[o + k] = w[o + k] * (dev_normal_cdf(d.high, mu[o + k], sigma[o + k]) -
                                                dev_normal_cdf(d.low, mu[o + k], sigma[o + k]));
-                p_accept = block_np_sum(terms + o, K, leaf_start + o, leaf_sum + o);
+                p_accept = block_np_sum(terms + o, K, leaf_sum + o);
             }
             if (quant) {
                 (side ? d.logpacc_a : d.logpacc_b) = log(p_accept);
