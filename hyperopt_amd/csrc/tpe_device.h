@@ -234,6 +234,10 @@ __device__ __forceinline__ void lse_dense(const Comp<double>* __restrict__ c, in
         acc[r] = 0.0;
         x[r] = xin[r] - centre;
     }
+    // few candidates per thread: unroll further so the scalar loads of
+    // several components are in flight at once (latency of s_load)
+    constexpr int kUnroll = R >= 4 ? 2 : (R == 2 ? 4 : 8);
+#pragma unroll kUnroll
     for (int k = 0; k < n; ++k) {
         const double m = c[k].mu, a = c[k].a, cc = c[k].c;
 #pragma unroll

@@ -37,7 +37,7 @@ using namespace tpe_rt;
 namespace {
 
 constexpr int kR = 4;                 // candidates per thread, tile map
-constexpr int kRGroup = 1;            // candidates per thread, packed map with C <= 256
+constexpr int kRGroup = 2;            // candidates per thread, packed map with C <= 512
 constexpr int kTile = kBlock * kR;    // candidates per workgroup, tile map
 
 thread_local std::string g_create_error;
