@@ -234,16 +234,61 @@ __device__ __forceinline__ void lse_dense(const Comp<double>* __restrict__ c, in
         acc[r] = 0.0;
         x[r] = xin[r] - centre;
     }
-    // few candidates per thread: unroll further so the scalar loads of
-    // several components are in flight at once (latency of s_load)
-    constexpr int kUnroll = R >= 4 ? 2 : (R == 2 ? 4 : 8);
-#pragma unroll kUnroll
-    for (int k = 0; k < n; ++k) {
-        const double m = c[k].mu, a = c[k].a, cc = c[k].c;
+    if constexpr (R >= 4) {
+#pragma unroll 2
+        for (int k = 0; k < n; ++k) {
+            const double m = c[k].mu, a = c[k].a, cc = c[k].c;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const double z = fma(x[r], a, -m);
-            acc[r] = exp_scaled_acc(fma(-z, z, cc), tab, acc[r]);
+            for (int r = 0; r < R; ++r) {
+                const double z = fma(x[r], a, -m);
+                acc[r] = exp_scaled_acc(fma(-z, z, cc), tab, acc[r]);
+            }
+        }
+    } else {
+        // few candidates per thread: software-pipelined batches of U records
+        // (the scalar loads of batch b+1 are issued before batch b is
+        // computed, so their latency hides behind U x R evaluations)
+        constexpr int U = R == 2 ? 4 : 8;
+        const int nfull = n - n % U;
+        double bm[U], ba[U], bc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int k = u < n ? u : n - 1;
+            bm[u] = c[k].mu;
+            ba[u] = c[k].a;
+            bc[u] = c[k].c;
+        }
+        for (int k0 = 0; k0 < nfull; k0 += U) {
+            double nm[U], na[U], nc[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {   // next batch (clamped, no branch)
+                const int k = min(k0 + U + u, n - 1);
+                nm[u] = c[k].mu;
+                na[u] = c[k].a;
+                nc[u] = c[k].c;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const double z = fma(x[r], ba[u], -bm[u]);
+                    acc[r] = exp_scaled_acc(fma(-z, z, bc[u]), tab, acc[r]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                bm[u] = nm[u];
+                ba[u] = na[u];
+                bc[u] = nc[u];
+            }
+        }
+        for (int k = nfull; k < n; ++k) {
+            const double m = c[k].mu, a = c[k].a, cc = c[k].c;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const double z = fma(x[r], a, -m);
+                acc[r] = exp_scaled_acc(fma(-z, z, cc), tab, acc[r]);
+            }
         }
     }
 #pragma unroll
