@@ -113,19 +113,19 @@ def suggest_latency(n_labels, n_trials, n_reps=20, n_warm=3):
     return float(np.median(times[n_warm:])) * 1e3
 
 
-def measured_traffic(kernel_prefix):
-    """HBM bytes per launch of the dominant kernel from the committed PMC
-    summary (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench,
-    FETCH doubled per the gfx950 correction) -- None if absent."""
+def measured_pmc(kernel_prefix):
+    """HBM bytes per launch and VALU issue utilisation of the dominant kernel
+    from the newest committed PMC summary that has it (rocprofv3 --pmc passes
+    of this bench, tools/prof_round.sh + tools/pmc_summary.py; FETCH doubled
+    per the gfx950 correction) -- (None, None, None) if absent."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_pmc_summary.json')))
-    if not files:
-        return None, None
-    d = json.load(open(files[-1]))
-    for name, v in d.items():
-        if name.startswith(kernel_prefix) and '_hbm_bytes_per_launch' in v:
-            return v['_hbm_bytes_per_launch'], os.path.relpath(files[-1], REPO)
-    return None, None
+    for f in reversed(files):
+        d = json.load(open(f))
+        for name, v in d.items():
+            if name.startswith(kernel_prefix) and '_hbm_bytes_per_launch' in v:
+                return v['_hbm_bytes_per_launch'], v.get('_valu_busy'), os.path.relpath(f, REPO)
+    return None, None, None
 
 
 def workload_name(args, C):
@@ -163,12 +163,26 @@ def main():
         hist = mixed_history(args.labels, args.trials, seed=0)
     else:
         hist = mixed_history(args.labels, args.trials, seed=0)
-    t_post = time.perf_counter()
+    # the resident posterior: built on the device from the history (the
+    # product path for histories this size, tpe.suggest posterior_builder
+    # 'auto'); the host numpy build is timed beside it
+    eng = Engine(local, args.precision)
+    t_host = time.perf_counter()
     posts = hist.posteriors()
     descs, w, m, s = P.pack(posts)
-    t_post = time.perf_counter() - t_post
-    eng = Engine(local, args.precision)
-    eng.set_posterior(descs, w, m, s)
+    t_host = time.perf_counter() - t_host
+    inputs = hist.device_inputs()
+    dev_call, dev_kern = [], []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        eng.build_posterior(*inputs, gamma=0.25, prior_weight=1.0)
+        dev_call.append(time.perf_counter() - t0)
+        dev_kern.append(eng.last_build_ms())
+    post_build = {'device_call_ms': round(1e3 * float(np.median(dev_call)), 3),
+                  'device_kernels_ms': round(float(np.median(dev_kern)), 3),
+                  'host_numpy_ms': round(1e3 * t_host, 3),
+                  'note': 'tpe_build_posterior (split, sort, Parzen, fold on the GPU; call '
+                          'includes the H2D of the history) vs posterior.py + pack'}
     C = 24 if args.config == 5 else 1 << args.cand_log2
     L = len(posts)
 
@@ -217,12 +231,12 @@ def main():
     prec = args.precision
     peak = PEAK_FP64_VECTOR_TFLOPS if prec == 'f64' else PEAK_FP32_VECTOR_TFLOPS
     kname = 'k_round<%s, %d, true,' % ('double' if prec == 'f64' else 'float', DENSE.index(dom))
-    traffic, traffic_src = measured_traffic(kname)
+    traffic, valu_busy, traffic_src = measured_pmc(kname)
     achieved = dom_rate * FLOPS_PER_EVAL[prec] / 1e12
     roof = {'bound': 'valu', 'kernel': 'k_round<%s,%s>' % (prec, dom),
             'achieved': round(achieved, 3), 'peak': peak, 'unit': 'TFLOP/s',
             'frac': round(achieved / peak, 4), 'traffic': traffic,
-            'traffic_source': traffic_src,
+            'traffic_source': traffic_src, 'valu_busy_measured': valu_busy,
             'evals_per_s': dom_rate, 'flops_per_eval': FLOPS_PER_EVAL[prec],
             'valu_issue_frac': round(dom_rate * VALU_INSTR_PER_EVAL[prec] /
                                      PEAK_VALU_LANE_INSTR[prec], 4),
@@ -237,7 +251,7 @@ def main():
                    'labels': L, 'history': args.trials, 'candidates_per_label_per_gpu': C,
                    'parallelism': ('new_id-sharded x%d' if args.config == 5
                                    else 'candidate-sharded x%d') % world},
-        'host_posterior_build_ms': round(t_post * 1e3, 2),
+        'posterior_build': post_build,
         'per_family_ms': {k: round(v / args.steps, 3) for k, v in mode_ms.items() if v},
         'per_family_evals': {k: v // args.steps for k, v in mode_ev.items() if v},
         'roofline': roof,
