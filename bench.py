@@ -37,8 +37,10 @@ FLOPS_PER_EVAL = {'f64': 6.0, 'f32': 6.0}
 #         3 int32 (table index, byte offset, exponent) and 1/4 v_mov_b64 (the
 #         component's mu, shared by 4 candidates) = 12.25 VALU instructions,
 #         each a 4-cycle wave64 issue on a 16-lane SIMD, plus one ds_read_b64
-#   fp32: v_sub, v_mul, v_fma, v_exp_f32 (8-cycle issue), v_add = 6 slots
-VALU_INSTR_PER_EVAL = {'f64': 12.25, 'f32': 6.0}
+#   fp32: candidate pairs in packed fp32 -- v_pk_add_f32 (x - mu), v_pk_mul_f32,
+#         v_pk_fma_f32, v_pk_add_f32 (accumulate) per two evals + one
+#         v_exp_f32 (8-cycle issue) per eval = 4 four-cycle slots per eval
+VALU_INSTR_PER_EVAL = {'f64': 12.25, 'f32': 4.0}
 PEAK_FP64_VECTOR_TFLOPS = 78.6        # MI355X spec (MI355X_MICROARCH.md)
 PEAK_FP32_VECTOR_TFLOPS = 157.3
 # 4-cycle wave64 VALU issue slots per second at 2.4 GHz, in lanes: 256 CU x

@@ -300,30 +300,66 @@ __device__ __forceinline__ void lse_dense(const Comp<double>* __restrict__ c, in
 }
 
 // fp32 fast path: constants pre-scaled by log2(e) so the hardware v_exp_f32
-// (exp2) is used directly; shift is in natural-log units.
+// (exp2) is used directly; shift is in natural-log units.  Candidates go in
+// pairs through packed fp32 (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32 on a
+// float2, the component constants broadcast from SGPRs): 3 packed
+// instructions + 2 v_exp_f32 per two evaluations.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 template <int R>
 __device__ __forceinline__ void lse_dense(const Comp<float>* __restrict__ c, int n, double shift,
                                           double, const double (&xd)[R], double (&out)[R],
                                           const double* __restrict__) {
-    float x[R], acc[R];
+    if constexpr (R % 2 == 0) {
+        constexpr int P = R / 2;
+        f32x2 x[P], acc[P];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        x[r] = (float)xd[r];
-        acc[r] = 0.0f;
-    }
-    for (int k = 0; k < n; ++k) {
-        const float mu = c[k].mu, a = c[k].a, cc = c[k].c;
+        for (int p = 0; p < P; ++p) {
+            x[p] = f32x2{(float)xd[2 * p], (float)xd[2 * p + 1]};
+            acc[p] = f32x2{0.0f, 0.0f};
+        }
+#pragma unroll 2
+        for (int k = 0; k < n; ++k) {
+            const float mu = c[k].mu, a = c[k].a, cc = c[k].c;
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                const f32x2 z = (x[p] - mu) * a;
+                const f32x2 t = __builtin_elementwise_fma(-z, z, f32x2{cc, cc});
+                acc[p] += f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const float s = h ? acc[p].y : acc[p].x;
+                const float xv = h ? x[p].y : x[p].x;
+                float v = __builtin_log2f(s) * 0.69314718055994531f;
+                if (!(s >= 1e-30f)) v = lse_twopass(c, n, xv);
+                out[2 * p + h] = (double)v + shift;
+            }
+        }
+    } else {
+        float x[R], acc[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const float z = (x[r] - mu) * a;
-            acc[r] += __builtin_amdgcn_exp2f(fmaf(-z, z, cc));
+            x[r] = (float)xd[r];
+            acc[r] = 0.0f;
         }
-    }
+        for (int k = 0; k < n; ++k) {
+            const float mu = c[k].mu, a = c[k].a, cc = c[k].c;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        float v = __builtin_log2f(acc[r]) * 0.69314718055994531f;
-        if (!(acc[r] >= 1e-30f)) v = lse_twopass(c, n, x[r]);
-        out[r] = (double)v + shift;
+            for (int r = 0; r < R; ++r) {
+                const float z = (x[r] - mu) * a;
+                acc[r] += __builtin_amdgcn_exp2f(fmaf(-z, z, cc));
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            float v = __builtin_log2f(acc[r]) * 0.69314718055994531f;
+            if (!(acc[r] >= 1e-30f)) v = lse_twopass(c, n, x[r]);
+            out[r] = (double)v + shift;
+        }
     }
 }
 
