@@ -66,16 +66,18 @@ def parse():
     ap.add_argument('--cand-log2', type=int, default=21)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-sample', type=int, default=2048,
-                    help='candidates per label in the CPU baseline sample')
+                    help='candidates per label in the single-core numpy baseline sample')
+    ap.add_argument('--cpu-sample-c', type=int, default=16384,
+                    help='candidates per label in the all-cores C baseline sample')
     ap.add_argument('--no-latency', action='store_true')
     ap.add_argument('--dist-backend', default='nccl',
                     help='nccl (RCCL over xGMI); gloo only to rehearse N ranks on one GPU')
     return ap.parse_args()
 
 
-def cpu_baseline(hist, posts, n_cand):
-    """The oracle (numpy restatement of the reference, test infra) timed on
-    the host: sample + score + argmax for every label on a bounded sample."""
+def cpu_baseline_numpy(posts, n_cand):
+    """The numpy restatement of the reference (oracle/tpe_oracle.py, test
+    infra) on ONE host core: sample + score + argmax for every label."""
     from oracle import tpe_oracle as O
     rng = np.random.RandomState(1)
     evals = 0
@@ -95,6 +97,36 @@ def cpu_baseline(hist, posts, n_cand):
         O.broadcast_best_index(lb, la)
     dt = time.perf_counter() - t0
     return evals / dt, dt, evals
+
+
+def cpu_baseline_c(eng, posts, n_cand, seed, rnd):
+    """The C restatement of the reference's scoring (oracle/tpe_score.c, test
+    infra, OpenMP over candidates on all the threads OMP gives it): the first
+    n_cand candidates of every label's GPU candidate set (re-drawn through the
+    engine's sampler entry points, untimed) scored under l and g + argmax."""
+    from oracle import c_oracle as C
+    cands = []
+    for li, p in enumerate(posts):
+        if p.family == 'categorical':
+            cands.append(eng.categorical(p.below, seed=seed, size=(n_cand,), stream=li, round=rnd))
+        else:
+            samp = eng.GMM1 if p.family == 'GMM1' else eng.LGMM1
+            cands.append(samp(*p.below, low=p.low, high=p.high, q=p.q, seed=seed,
+                              size=(n_cand,), stream=li, round=rnd))
+    evals = 0
+    t0 = time.perf_counter()
+    for p, cand in zip(posts, cands):
+        if p.family == 'categorical':
+            lb, la = C.categorical_lpdf(cand, p.below), C.categorical_lpdf(cand, p.above)
+            evals += 2 * n_cand
+        else:
+            f = C.gmm1_lpdf if p.family == 'GMM1' else C.lgmm1_lpdf
+            lb = f(cand, *p.below, low=p.low, high=p.high, q=p.q)
+            la = f(cand, *p.above, low=p.low, high=p.high, q=p.q)
+            evals += n_cand * (len(p.below[0]) + len(p.above[0]))
+        C.broadcast_best_index(lb, la)
+    dt = time.perf_counter() - t0
+    return evals / dt, dt, evals, C.threads()
 
 
 def suggest_latency(n_labels, n_trials, n_reps=20, n_warm=3):
@@ -267,12 +299,19 @@ def main():
             'labels': args.labels, 'note': 'end-to-end tpe.suggest wall time, median of 20; '
                                            'reference CPU: 1330 ms (BASELINE.md)'}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == 3:
-        rate, sec, ev = cpu_baseline(hist, posts, args.cpu_sample)
-        line['cpu_baseline'] = {'value': rate, 'unit': 'evals/s', 'cores': 1, 'kind': 'port',
-                                'sample': 'all %d labels x %d candidates (of 2^%d) sampled, '
-                                          'scored under l and g and argmaxed by the numpy '
-                                          'restatement of the reference; %.1f s, %.3g evals'
-                                          % (L, args.cpu_sample, args.cand_log2, sec, ev)}
+        rate, sec, ev, thr = cpu_baseline_c(eng, posts, args.cpu_sample_c, 1234, 0)
+        nrate, nsec, nev = cpu_baseline_numpy(posts, args.cpu_sample)
+        line['cpu_baseline'] = {
+            'value': rate, 'unit': 'evals/s', 'cores': thr, 'kind': 'port',
+            'sample': 'the first %d of the 2^%d candidates of all %d labels (the GPU round\'s '
+                      'own draws), scored under l and g and argmaxed by oracle/tpe_score.c, '
+                      'the C restatement of tpe.py, OpenMP on %d threads; %.1f s, %.3g evals'
+                      % (args.cpu_sample_c, args.cand_log2, L, thr, sec, ev),
+            'single_core_numpy': {
+                'value': nrate, 'cores': 1,
+                'sample': 'all %d labels x %d candidates sampled, scored and argmaxed by the '
+                          'numpy restatement (oracle/tpe_oracle.py); %.1f s, %.3g evals'
+                          % (L, args.cpu_sample, nsec, nev)}}
     if rank == 0:
         print(json.dumps(line), flush=True)
     eng.close()
