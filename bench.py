@@ -67,7 +67,7 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-sample', type=int, default=2048,
                     help='candidates per label in the single-core numpy baseline sample')
-    ap.add_argument('--cpu-sample-c', type=int, default=16384,
+    ap.add_argument('--cpu-sample-c', type=int, default=49152,
                     help='candidates per label in the all-cores C baseline sample')
     ap.add_argument('--no-latency', action='store_true')
     ap.add_argument('--dist-backend', default='nccl',

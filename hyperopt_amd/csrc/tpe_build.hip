@@ -283,18 +283,103 @@ __global__ __launch_bounds__(kSplitBlock) void k_split(const double* __restrict_
     }
 }
 
-// ap_filter_trials' membership (tpe.py:639-646): the label's observations
-// whose trial is in the below set, and those whose trial is in the rest, in
-// their original (tid) order.  Observations whose trial is not among the
-// losses (obs_trial < 0) belong to neither, as in the reference.
+// ---------------------------------------------- device-resident history --
+// Every label's observations live in a pool region [off, off + cap): in
+// observation (tid) order (trial position, value) and, for continuous labels,
+// also sorted by value with ties in observation order (key, observation
+// index).  Appends sort only the new observations and merge them in.
+
+// new observations of every label -> pool tail; st_idx = local index (sort values)
+__global__ __launch_bounds__(kBlock) void k_hist_append(
+    const int64_t* __restrict__ st_off, const int32_t* __restrict__ st_trial,
+    const double* __restrict__ st_val, const int64_t* __restrict__ p_off,
+    const int32_t* __restrict__ cnt_old, int32_t* __restrict__ p_trial, double* __restrict__ p_val,
+    int32_t* __restrict__ st_idx) {
+    const int l = blockIdx.y;
+    const int64_t s0 = st_off[l], m = st_off[l + 1] - s0;
+    const int64_t base = p_off[l] + cnt_old[l];
+    for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < m; j += (int64_t)gridDim.x * kBlock) {
+        p_trial[base + j] = st_trial[s0 + j];
+        p_val[base + j] = st_val[s0 + j];
+        st_idx[s0 + j] = (int32_t)j;
+    }
+}
+
+// copy every label's live prefix into a re-laid-out pool (growth)
+__global__ __launch_bounds__(kBlock) void k_hist_regrow(
+    const int64_t* __restrict__ off_old, const int64_t* __restrict__ off_new,
+    const int32_t* __restrict__ cnt, const int32_t* __restrict__ t_old,
+    const double* __restrict__ v_old, const double* __restrict__ k_old,
+    const int32_t* __restrict__ i_old, int32_t* __restrict__ t_new, double* __restrict__ v_new,
+    double* __restrict__ k_new, int32_t* __restrict__ i_new) {
+    const int l = blockIdx.y;
+    const int64_t a = off_old[l], b = off_new[l];
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < cnt[l]; i += (int64_t)gridDim.x * kBlock) {
+        t_new[b + i] = t_old[a + i];
+        v_new[b + i] = v_old[a + i];
+        k_new[b + i] = k_old[a + i];
+        i_new[b + i] = i_old[a + i];
+    }
+}
+
+// stable merge of the sorted existing keys with the sorted new batch:
+// existing element i -> i + #(new keys < key), new element j -> j +
+// #(existing keys <= key): equal keys keep observation order
+__global__ __launch_bounds__(kBlock) void k_hist_merge(
+    const tpe_label_spec* __restrict__ specs, const int64_t* __restrict__ p_off,
+    const int32_t* __restrict__ cnt_old, const int64_t* __restrict__ st_off,
+    const double* __restrict__ s_key, const int32_t* __restrict__ s_idx,
+    const double* __restrict__ n_key, const int32_t* __restrict__ n_idx,
+    double* __restrict__ o_key, int32_t* __restrict__ o_idx) {
+    const int l = blockIdx.y;
+    if (specs[l].kind == TPE_CATEGORICAL) return;   // categorical: observation order only
+    const int64_t off = p_off[l], c = cnt_old[l];
+    const int64_t s0 = st_off[l], m = st_off[l + 1] - s0;
+    const double* ok = s_key + off;
+    const double* nk = n_key + s0;
+    for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < c + m; e += (int64_t)gridDim.x * kBlock) {
+        if (e < c) {
+            const double k = ok[e];
+            int64_t lo = 0, hi = m;                 // lower bound in the new batch
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (nk[mid] < k) lo = mid + 1; else hi = mid;
+            }
+            o_key[off + e + lo] = k;
+            o_idx[off + e + lo] = s_idx[off + e];
+        } else {
+            const int64_t j = e - c;
+            const double k = nk[j];
+            int64_t lo = 0, hi = c;                 // upper bound in the existing keys
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (ok[mid] <= k) lo = mid + 1; else hi = mid;
+            }
+            o_key[off + j + lo] = k;
+            o_idx[off + j + lo] = (int32_t)(c + n_idx[s0 + j]);
+        }
+    }
+}
+
+// ap_filter_trials' membership (tpe.py:639-646) from the resident history:
+// phase A walks the observations in (tid) order -- the below list (<= lf, in
+// order) and, per observation, its rank in the above list (-1 if it is not
+// there); categorical labels keep their above list in observation order.
+// Phase B walks a continuous label's value-sorted observations and keeps the
+// above ones, in sorted order, with their above-list rank (the index the
+// linear-forgetting weights are taken at).  Observations of trials without a
+// loss (position < 0 or NaN loss) belong to neither set, as in the reference.
 __global__ __launch_bounds__(kPartBlock) void k_partition(
-    const tpe_label_spec* __restrict__ specs, const int64_t* __restrict__ obs_off,
-    const int32_t* __restrict__ obs_trial, const double* __restrict__ obs_val,
-    const uint8_t* __restrict__ below, int64_t T, double* __restrict__ below_val,
-    double* __restrict__ keys, int32_t* __restrict__ idx, int32_t* __restrict__ counts,
-    int32_t* __restrict__ seg_begin, int32_t* __restrict__ seg_end, int32_t* __restrict__ err) {
+    const tpe_label_spec* __restrict__ specs, const int64_t* __restrict__ p_off,
+    const int32_t* __restrict__ cnt, const int32_t* __restrict__ p_trial,
+    const double* __restrict__ p_val, const double* __restrict__ s_key,
+    const int32_t* __restrict__ s_idx, const uint8_t* __restrict__ below,
+    const double* __restrict__ losses, int64_t T, double* __restrict__ below_val,
+    int32_t* __restrict__ arank, double* __restrict__ keys, int32_t* __restrict__ idx,
+    int32_t* __restrict__ counts, int32_t* __restrict__ err) {
     const int l = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int64_t off = obs_off[l], M = obs_off[l + 1] - off;
+    const int64_t off = p_off[l], M = cnt[l];
+    const bool cat = specs[l].kind == TPE_CATEGORICAL;
     __shared__ int wb[kPartBlock / 64], wa[kPartBlock / 64];
     __shared__ int base_b, base_a;
     if (tid == 0) base_b = base_a = 0;
@@ -305,11 +390,12 @@ __global__ __launch_bounds__(kPartBlock) void k_partition(
         bool isb = false, isa = false;
         double v = 0.0;
         if (i < M) {
-            const int32_t t = obs_trial[off + i];
-            v = obs_val[off + i];
+            const int32_t t = p_trial[off + i];
+            v = p_val[off + i];
             if (t >= 0 && t < T) {
+                const double ls = losses[t];
                 isb = below[t] != 0;
-                isa = !isb;
+                isa = !isb && ls == ls;
             } else if (t >= T) {
                 atomicOr(err, 1);
             }
@@ -330,10 +416,13 @@ __global__ __launch_bounds__(kPartBlock) void k_partition(
             if (p < kMaxLF) below_val[(size_t)l * kMaxLF + p] = v;
             else atomicOr(err, 2);
         }
-        if (isa) {
+        if (i < M) {
             const int p = oa + __popcll(ba & lt);
-            keys[off + p] = v;
-            idx[off + p] = p;
+            if (cat) {
+                if (isa) keys[off + p] = v;
+            } else {
+                arank[off + i] = isa ? p : -1;
+            }
         }
         __syncthreads();
         if (tid == 0) {
@@ -344,11 +433,39 @@ __global__ __launch_bounds__(kPartBlock) void k_partition(
         }
         __syncthreads();
     }
+    const int nb = base_b, na = base_a;
+    if (!cat) {   // phase B: sorted order
+        __syncthreads();
+        if (tid == 0) base_a = 0;
+        __syncthreads();
+        for (int64_t c0 = 0; c0 < M; c0 += kPartBlock) {
+            const int64_t i = c0 + tid;
+            int32_t r = -1;
+            double k = 0.0;
+            if (i < M) {
+                k = s_key[off + i];
+                r = arank[off + s_idx[off + i]];
+            }
+            const bool keep = r >= 0;
+            const uint64_t ba = __ballot(keep);
+            if (lane == 0) wa[wv] = __popcll(ba);
+            __syncthreads();
+            int oa = base_a;
+            for (int w = 0; w < wv; ++w) oa += wa[w];
+            if (keep) {
+                const int p = oa + __popcll(ba & lt);
+                keys[off + p] = k;
+                idx[off + p] = r;
+            }
+            __syncthreads();
+            if (tid == 0)
+                for (int w = 0; w < kPartBlock / 64; ++w) base_a += wa[w];
+            __syncthreads();
+        }
+    }
     if (tid == 0) {
-        counts[2 * l] = base_b;
-        counts[2 * l + 1] = base_a;
-        seg_begin[l] = (int32_t)off;
-        seg_end[l] = (int32_t)(specs[l].kind == TPE_CATEGORICAL ? off : off + base_a);
+        counts[2 * l] = nb;
+        counts[2 * l + 1] = na;
     }
 }
 
@@ -638,29 +755,186 @@ __global__ __launch_bounds__(kParzenBlock) void k_fold(
 
 }  // namespace
 
-// ================================================================ C ABI ====
-extern "C" {
+// ============================================================ host side ====
+namespace {
 
-int tpe_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
-                        const double* cat_p, int64_t n_cat_p, const double* losses,
-                        int64_t n_trials, const int64_t* obs_off, const int32_t* obs_trial,
-                        const double* obs_val, double gamma, double prior_weight, int32_t lf,
-                        int32_t* n_below_out) {
-    if (!ctx) return TPE_ERR_ARG;
-    if (n_labels <= 0 || !specs || !obs_off || n_trials < 0 || (n_trials > 0 && !losses))
-        return ctx->fail(TPE_ERR_ARG, "tpe_build_posterior: bad arguments");
-    if (lf < 1 || lf >= kMaxLF) return ctx->fail(TPE_ERR_ARG, "linear forgetting must be in [1, 63]");
-    if (n_trials >= INT32_MAX) return ctx->fail(TPE_ERR_ARG, "too many trials");
-    const int64_t n_obs = obs_off[n_labels];
-    if (obs_off[0] != 0 || n_obs < 0 || n_obs >= INT32_MAX || (n_obs > 0 && (!obs_trial || !obs_val)))
-        return ctx->fail(TPE_ERR_ARG, "observation offsets");
+int check_specs(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels, int64_t n_cat_p,
+                const double* cat_p) {
+    for (int32_t l = 0; l < n_labels; ++l) {
+        const tpe_label_spec& s = specs[l];
+        if (s.kind == TPE_CATEGORICAL) {
+            if (s.upper <= 0) return ctx->fail(TPE_ERR_ARG, "categorical upper must be positive");
+            if (!s.randint && (s.p_off < 0 || s.p_off + s.upper > n_cat_p || !cat_p))
+                return ctx->fail(TPE_ERR_ARG, "categorical p out of range");
+        } else if (s.kind == TPE_GMM1 || s.kind == TPE_LGMM1) {
+            if ((s.flags & 3) == 1 || (s.flags & 3) == 2)
+                return ctx->fail(TPE_ERR_TYPE, "low and high must both be given or both be None");
+            if ((s.flags & 3) == 3 && !(s.low < s.high)) return ctx->fail(TPE_ERR_VALUE, "low >= high");
+            if ((s.flags & TPE_HAS_Q) && !(s.q > 0) && !(s.q < 0))
+                return ctx->fail(TPE_ERR_VALUE, "q must be non-zero");
+            if (!(s.prior_sigma > 0)) return ctx->fail(TPE_ERR_VALUE, "prior sigma must be positive");
+        } else {
+            return ctx->fail(TPE_ERR_ARG, "label " + std::to_string(l) + ": unknown kind");
+        }
+    }
+    return TPE_OK;
+}
+
+int history_reset(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels, const double* cat_p,
+                  int64_t n_cat_p) {
+    if (n_labels <= 0 || !specs) return ctx->fail(TPE_ERR_ARG, "tpe_history_reset: no labels");
+    int rc = check_specs(ctx, specs, n_labels, n_cat_p, cat_p);
+    if (rc) return rc;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     auto& B = ctx->build;
+    B.specs_h.assign(specs, specs + n_labels);
+    B.cap_h.assign(n_labels, 0);
+    B.off_h.assign(n_labels, 0);
+    B.cnt_h.assign(n_labels, 0);
+    B.pool_cap = 0;
+    HIPCHK(ctx, B.specs.reserve(n_labels));
+    HIPCHK(ctx, B.cat_p.reserve(std::max<int64_t>(n_cat_p, 1)));
+    HIPCHK(ctx, B.p_off.reserve(n_labels));
+    HIPCHK(ctx, B.cnt.reserve(n_labels));
+    HIPCHK(ctx, hipMemcpyAsync(B.specs.p, specs, n_labels * sizeof(tpe_label_spec),
+                               hipMemcpyHostToDevice, ctx->stream));
+    if (n_cat_p > 0 && cat_p)
+        HIPCHK(ctx, hipMemcpyAsync(B.cat_p.p, cat_p, n_cat_p * sizeof(double), hipMemcpyHostToDevice,
+                                   ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(B.cnt.p, 0, n_labels * sizeof(int32_t), ctx->stream));
+    HIPCHK(ctx, hipMemsetAsync(B.p_off.p, 0, n_labels * sizeof(int64_t), ctx->stream));
+    B.hist_ready = true;
+    return TPE_OK;
+}
+
+int history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial, const double* obs_val) {
+    auto& B = ctx->build;
+    if (!B.hist_ready) return ctx->fail(TPE_ERR_ARG, "tpe_history_append before tpe_history_reset");
+    const int32_t L = (int32_t)B.specs_h.size();
+    std::vector<int64_t> st(L + 1, 0);
+    for (int32_t l = 0; l < L; ++l) {
+        if (n_new[l] < 0) return ctx->fail(TPE_ERR_ARG, "negative observation count");
+        st[l + 1] = st[l] + n_new[l];
+    }
+    const int64_t total = st[L];
+    if (total == 0) return TPE_OK;
+    if (!obs_trial || !obs_val) return ctx->fail(TPE_ERR_ARG, "observations missing");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    hipStream_t sm = ctx->stream;
+    // growth: re-lay the pool out when a label outgrows its region
+    bool grow = false;
+    for (int32_t l = 0; l < L; ++l)
+        if (B.cnt_h[l] + n_new[l] > B.cap_h[l]) grow = true;
+    if (grow) {
+        std::vector<int64_t> cap(L), off(L);
+        int64_t pc = 0;
+        for (int32_t l = 0; l < L; ++l) {
+            const int64_t need = B.cnt_h[l] + n_new[l];
+            cap[l] = need > B.cap_h[l] ? std::max<int64_t>(2 * need, 256) : B.cap_h[l];
+            off[l] = pc;
+            pc += cap[l];
+        }
+        if (pc >= INT32_MAX) return ctx->fail(TPE_ERR_ARG, "history too large");
+        DevBuf<int32_t> t2, i2;
+        DevBuf<double> v2, k2;
+        DevBuf<int64_t> o2;
+        HIPCHK(ctx, t2.reserve(pc));
+        HIPCHK(ctx, i2.reserve(pc));
+        HIPCHK(ctx, v2.reserve(pc));
+        HIPCHK(ctx, k2.reserve(pc));
+        HIPCHK(ctx, o2.reserve(L));
+        HIPCHK(ctx, hipMemcpyAsync(o2.p, off.data(), L * sizeof(int64_t), hipMemcpyHostToDevice, sm));
+        int32_t mx = 0;
+        for (int32_t l = 0; l < L; ++l) mx = std::max(mx, B.cnt_h[l]);
+        if (mx > 0 && B.pool_cap > 0)
+            hipLaunchKernelGGL(k_hist_regrow, dim3((unsigned)std::min<int64_t>((mx + kBlock - 1) / kBlock, 1024), L),
+                               dim3(kBlock), 0, sm, B.p_off.p, o2.p, B.cnt.p, B.p_trial.p, B.p_val.p,
+                               B.s_key.p, B.s_idx.p, t2.p, v2.p, k2.p, i2.p);
+        HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, hipStreamSynchronize(sm));
+        std::swap(B.p_trial, t2);
+        std::swap(B.p_val, v2);
+        std::swap(B.s_key, k2);
+        std::swap(B.s_idx, i2);
+        std::swap(B.p_off, o2);
+        t2.release();
+        v2.release();
+        k2.release();
+        i2.release();
+        o2.release();
+        HIPCHK(ctx, B.s_key2.reserve(pc));
+        HIPCHK(ctx, B.s_idx2.reserve(pc));
+        HIPCHK(ctx, B.arank.reserve(pc));
+        HIPCHK(ctx, B.keys.reserve(pc));
+        HIPCHK(ctx, B.idx.reserve(pc));
+        B.cap_h = cap;
+        B.off_h = off;
+        B.pool_cap = pc;
+    }
+    HIPCHK(ctx, B.st_off.reserve(L + 1));
+    HIPCHK(ctx, B.st_trial.reserve(total));
+    HIPCHK(ctx, B.st_val.reserve(total));
+    HIPCHK(ctx, B.st_idx.reserve(total));
+    HIPCHK(ctx, B.st_idx_sorted.reserve(total));
+    HIPCHK(ctx, B.st_key_sorted.reserve(total));
+    HIPCHK(ctx, B.seg_begin.reserve(L));
+    HIPCHK(ctx, B.seg_end.reserve(L));
+    std::vector<int32_t> sb(L), se(L);
+    for (int32_t l = 0; l < L; ++l) {
+        sb[l] = (int32_t)st[l];
+        se[l] = (int32_t)(B.specs_h[l].kind == TPE_CATEGORICAL ? st[l] : st[l + 1]);
+    }
+    HIPCHK(ctx, hipMemcpyAsync(B.st_off.p, st.data(), (L + 1) * sizeof(int64_t), hipMemcpyHostToDevice, sm));
+    HIPCHK(ctx, hipMemcpyAsync(B.st_trial.p, obs_trial, total * sizeof(int32_t), hipMemcpyHostToDevice, sm));
+    HIPCHK(ctx, hipMemcpyAsync(B.st_val.p, obs_val, total * sizeof(double), hipMemcpyHostToDevice, sm));
+    HIPCHK(ctx, hipMemcpyAsync(B.seg_begin.p, sb.data(), L * sizeof(int32_t), hipMemcpyHostToDevice, sm));
+    HIPCHK(ctx, hipMemcpyAsync(B.seg_end.p, se.data(), L * sizeof(int32_t), hipMemcpyHostToDevice, sm));
+    int64_t mx_new = 0, mx_all = 0;
+    for (int32_t l = 0; l < L; ++l) {
+        mx_new = std::max(mx_new, n_new[l]);
+        mx_all = std::max<int64_t>(mx_all, B.cnt_h[l] + n_new[l]);
+    }
+    hipLaunchKernelGGL(k_hist_append, dim3((unsigned)std::min<int64_t>((mx_new + kBlock - 1) / kBlock, 1024), L),
+                       dim3(kBlock), 0, sm, B.st_off.p, B.st_trial.p, B.st_val.p, B.p_off.p, B.cnt.p,
+                       B.p_trial.p, B.p_val.p, B.st_idx.p);
+    HIPCHK(ctx, hipGetLastError());
+    size_t bytes = 0;   // stable segmented radix sort of the new batch
+    HIPCHK(ctx, hipcub::DeviceSegmentedRadixSort::SortPairs(
+                    nullptr, bytes, B.st_val.p, B.st_key_sorted.p, B.st_idx.p, B.st_idx_sorted.p,
+                    (int)total, L, B.seg_begin.p, B.seg_end.p, 0, 64, sm));
+    HIPCHK(ctx, B.sort_tmp.reserve(std::max<size_t>(bytes, 1)));
+    HIPCHK(ctx, hipcub::DeviceSegmentedRadixSort::SortPairs(
+                    B.sort_tmp.p, bytes, B.st_val.p, B.st_key_sorted.p, B.st_idx.p, B.st_idx_sorted.p,
+                    (int)total, L, B.seg_begin.p, B.seg_end.p, 0, 64, sm));
+    hipLaunchKernelGGL(k_hist_merge, dim3((unsigned)std::min<int64_t>((mx_all + kBlock - 1) / kBlock, 1024), L),
+                       dim3(kBlock), 0, sm, B.specs.p, B.p_off.p, B.cnt.p, B.st_off.p, B.s_key.p,
+                       B.s_idx.p, B.st_key_sorted.p, B.st_idx_sorted.p, B.s_key2.p, B.s_idx2.p);
+    HIPCHK(ctx, hipGetLastError());
+    std::swap(B.s_key, B.s_key2);
+    std::swap(B.s_idx, B.s_idx2);
+    for (int32_t l = 0; l < L; ++l) B.cnt_h[l] += (int32_t)n_new[l];
+    HIPCHK(ctx, hipMemcpyAsync(B.cnt.p, B.cnt_h.data(), L * sizeof(int32_t), hipMemcpyHostToDevice, sm));
+    // the host staging buffers are the caller's: make sure the copies are done
+    HIPCHK(ctx, hipStreamSynchronize(sm));
+    return TPE_OK;
+}
+
+int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t n_valid,
+                   double gamma, double prior_weight, int32_t lf, int32_t* n_below_out) {
+    auto& B = ctx->build;
+    if (!B.hist_ready) return ctx->fail(TPE_ERR_ARG, "no resident history (tpe_history_reset)");
+    if (lf < 1 || lf >= kMaxLF) return ctx->fail(TPE_ERR_ARG, "linear forgetting must be in [1, 63]");
+    if (n_trials < 0 || n_trials >= INT32_MAX || (n_trials > 0 && !losses) || n_valid < 0 ||
+        n_valid > n_trials)
+        return ctx->fail(TPE_ERR_ARG, "tpe_build_posterior: bad trial arguments");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    const int32_t n_labels = (int32_t)B.specs_h.size();
     Posterior& P = ctx->resident;
     ctx->P = &ctx->resident;
+    hipStream_t st = ctx->stream;
 
     // n_below = min(ceil(gamma sqrt(len(l_vals))), gamma_cap)   tpe.py:636
-    const double nbd = std::ceil(gamma * std::sqrt((double)n_trials));
+    const double nbd = std::ceil(gamma * std::sqrt((double)n_valid));
     const int32_t n_below = (int32_t)std::min<double>(nbd, (double)lf);
 
     // static label fields, mixture / record regions
@@ -669,30 +943,18 @@ int tpe_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_lab
     std::vector<int32_t> grp[kNumModes];
     int64_t total = 0, samp_total = 0;
     for (int32_t l = 0; l < n_labels; ++l) {
-        const tpe_label_spec& s = specs[l];
+        const tpe_label_spec& s = B.specs_h[l];
         DLabel& o = dl[l];
         std::memset(&o, 0, sizeof(o));
-        const int64_t M = obs_off[l + 1] - obs_off[l];
-        if (M < 0) return ctx->fail(TPE_ERR_ARG, "observation offsets must not decrease");
         const bool quant = (s.flags & TPE_HAS_Q) != 0;
         int64_t cap_b, cap_a;
         if (s.kind == TPE_CATEGORICAL) {
-            if (s.upper <= 0) return ctx->fail(TPE_ERR_ARG, "categorical upper must be positive");
-            if (!s.randint && (s.p_off < 0 || s.p_off + s.upper > n_cat_p || !cat_p))
-                return ctx->fail(TPE_ERR_ARG, "categorical p out of range");
             o.mode = CAT;
             cap_b = cap_a = s.upper;
-        } else if (s.kind == TPE_GMM1 || s.kind == TPE_LGMM1) {
-            if ((s.flags & 3) == 1 || (s.flags & 3) == 2)
-                return ctx->fail(TPE_ERR_TYPE, "low and high must both be given or both be None");
-            if ((s.flags & 3) == 3 && !(s.low < s.high)) return ctx->fail(TPE_ERR_VALUE, "low >= high");
-            if (quant && !(s.q > 0) && !(s.q < 0)) return ctx->fail(TPE_ERR_VALUE, "q must be non-zero");
-            if (!(s.prior_sigma > 0)) return ctx->fail(TPE_ERR_VALUE, "prior sigma must be positive");
+        } else {
             o.mode = s.kind == TPE_GMM1 ? (quant ? QUANT_GMM : DENSE_GMM) : (quant ? QUANT_LGMM : DENSE_LGMM);
             cap_b = lf + 1;
-            cap_a = M + 1;
-        } else {
-            return ctx->fail(TPE_ERR_ARG, "label " + std::to_string(l) + ": unknown kind");
+            cap_a = (int64_t)B.cnt_h[l] + 1;
         }
         o.flags = s.kind == TPE_CATEGORICAL ? 0 : s.flags;
         o.low = s.low;
@@ -710,22 +972,14 @@ int tpe_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_lab
         grp[o.mode].push_back(l);
     }
     const int64_t T = n_trials;
-    HIPCHK(ctx, B.specs.reserve(n_labels));
-    HIPCHK(ctx, B.cat_p.reserve(std::max<int64_t>(n_cat_p, 1)));
     HIPCHK(ctx, B.losses.reserve(std::max<int64_t>(T, 1)));
     HIPCHK(ctx, B.below.reserve(std::max<int64_t>(T, 1)));
-    HIPCHK(ctx, B.obs_off.reserve(n_labels + 1));
-    HIPCHK(ctx, B.obs_trial.reserve(std::max<int64_t>(n_obs, 1)));
-    HIPCHK(ctx, B.obs_val.reserve(std::max<int64_t>(n_obs, 1)));
-    HIPCHK(ctx, B.keys_in.reserve(std::max<int64_t>(n_obs, 1)));
-    HIPCHK(ctx, B.keys_out.reserve(std::max<int64_t>(n_obs, 1)));
-    HIPCHK(ctx, B.idx_in.reserve(std::max<int64_t>(n_obs, 1)));
-    HIPCHK(ctx, B.idx_out.reserve(std::max<int64_t>(n_obs, 1)));
     HIPCHK(ctx, B.below_val.reserve((size_t)n_labels * kMaxLF));
     HIPCHK(ctx, B.counts.reserve(2 * (size_t)n_labels));
     HIPCHK(ctx, B.kcount.reserve(2 * (size_t)n_labels));
-    HIPCHK(ctx, B.seg_begin.reserve(n_labels));
-    HIPCHK(ctx, B.seg_end.reserve(n_labels));
+    HIPCHK(ctx, B.keys.reserve(std::max<int64_t>(B.pool_cap, 1)));
+    HIPCHK(ctx, B.idx.reserve(std::max<int64_t>(B.pool_cap, 1)));
+    HIPCHK(ctx, B.arank.reserve(std::max<int64_t>(B.pool_cap, 1)));
     HIPCHK(ctx, B.w.reserve(total));
     HIPCHK(ctx, B.mu.reserve(total));
     HIPCHK(ctx, B.sigma.reserve(total));
@@ -737,16 +991,7 @@ int tpe_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_lab
     HIPCHK(ctx, P.comps32.reserve(total));
     HIPCHK(ctx, P.samp.reserve(samp_total));
     HIPCHK(ctx, ctx->errflag.reserve(1));
-    hipStream_t st = ctx->stream;
-    HIPCHK(ctx, hipMemcpyAsync(B.specs.p, specs, n_labels * sizeof(tpe_label_spec), hipMemcpyHostToDevice, st));
-    if (n_cat_p > 0 && cat_p)
-        HIPCHK(ctx, hipMemcpyAsync(B.cat_p.p, cat_p, n_cat_p * sizeof(double), hipMemcpyHostToDevice, st));
     if (T > 0) HIPCHK(ctx, hipMemcpyAsync(B.losses.p, losses, T * sizeof(double), hipMemcpyHostToDevice, st));
-    HIPCHK(ctx, hipMemcpyAsync(B.obs_off.p, obs_off, (n_labels + 1) * sizeof(int64_t), hipMemcpyHostToDevice, st));
-    if (n_obs > 0) {
-        HIPCHK(ctx, hipMemcpyAsync(B.obs_trial.p, obs_trial, n_obs * sizeof(int32_t), hipMemcpyHostToDevice, st));
-        HIPCHK(ctx, hipMemcpyAsync(B.obs_val.p, obs_val, n_obs * sizeof(double), hipMemcpyHostToDevice, st));
-    }
     HIPCHK(ctx, hipMemcpyAsync(B.mix_off.p, mix.data(), mix.size() * sizeof(int64_t), hipMemcpyHostToDevice, st));
     HIPCHK(ctx, hipMemcpyAsync(P.labels.p, dl.data(), n_labels * sizeof(DLabel), hipMemcpyHostToDevice, st));
     HIPCHK(ctx, hipMemsetAsync(ctx->errflag.p, 0, sizeof(int32_t), st));
@@ -754,23 +999,12 @@ int tpe_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_lab
     HIPCHK(ctx, hipEventRecord(ctx->ev0, st));
     if (T > 0)
         hipLaunchKernelGGL(k_split, dim3(1), dim3(kSplitBlock), 0, st, B.losses.p, T, n_below, B.below.p);
-    hipLaunchKernelGGL(k_partition, dim3(n_labels), dim3(kPartBlock), 0, st, B.specs.p, B.obs_off.p,
-                       B.obs_trial.p, B.obs_val.p, B.below.p, T, B.below_val.p, B.keys_in.p, B.idx_in.p,
-                       B.counts.p, B.seg_begin.p, B.seg_end.p, ctx->errflag.p);
-    HIPCHK(ctx, hipGetLastError());
-    if (n_obs > 0) {  // stable segmented radix sort of every above list
-        size_t bytes = 0;
-        HIPCHK(ctx, hipcub::DeviceSegmentedRadixSort::SortPairs(
-                        nullptr, bytes, B.keys_in.p, B.keys_out.p, B.idx_in.p, B.idx_out.p, (int)n_obs,
-                        n_labels, B.seg_begin.p, B.seg_end.p, 0, 64, st));
-        HIPCHK(ctx, B.sort_tmp.reserve(std::max<size_t>(bytes, 1)));
-        HIPCHK(ctx, hipcub::DeviceSegmentedRadixSort::SortPairs(
-                        B.sort_tmp.p, bytes, B.keys_in.p, B.keys_out.p, B.idx_in.p, B.idx_out.p,
-                        (int)n_obs, n_labels, B.seg_begin.p, B.seg_end.p, 0, 64, st));
-    }
+    hipLaunchKernelGGL(k_partition, dim3(n_labels), dim3(kPartBlock), 0, st, B.specs.p, B.p_off.p, B.cnt.p,
+                       B.p_trial.p, B.p_val.p, B.s_key.p, B.s_idx.p, B.below.p, B.losses.p, T,
+                       B.below_val.p, B.arank.p, B.keys.p, B.idx.p, B.counts.p, ctx->errflag.p);
     hipLaunchKernelGGL(k_parzen, dim3(n_labels, 2), dim3(kParzenBlock), 0, st, B.specs.p, B.cat_p.p,
-                       B.obs_off.p, B.counts.p, B.below_val.p, B.keys_in.p, B.keys_out.p, B.idx_out.p,
-                       B.mix_off.p, prior_weight, lf, B.w.p, B.mu.p, B.sigma.p, B.kcount.p, B.leaf.p,
+                       B.p_off.p, B.counts.p, B.below_val.p, B.keys.p, B.keys.p, B.idx.p, B.mix_off.p,
+                       prior_weight, lf, B.w.p, B.mu.p, B.sigma.p, B.kcount.p, B.leaf.p,
                        B.scratch.p + total);
     hipLaunchKernelGGL(k_fold, dim3(n_labels), dim3(kParzenBlock), 0, st, P.labels.p, B.kcount.p,
                        B.mix_off.p, B.w.p, B.mu.p, B.sigma.p, P.comps64.p, P.comps32.p, P.samp.p,
@@ -800,6 +1034,54 @@ int tpe_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_lab
     B.mix_h = mix;
     if (n_below_out) *n_below_out = n_below;
     return TPE_OK;
+}
+
+}  // namespace
+
+// ================================================================ C ABI ====
+extern "C" {
+
+int tpe_history_reset(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
+                      const double* cat_p, int64_t n_cat_p) {
+    if (!ctx) return TPE_ERR_ARG;
+    return history_reset(ctx, specs, n_labels, cat_p, n_cat_p);
+}
+
+int tpe_history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial,
+                       const double* obs_val) {
+    if (!ctx || !n_new) return TPE_ERR_ARG;
+    return history_append(ctx, n_new, obs_trial, obs_val);
+}
+
+int tpe_build_posterior_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials,
+                                 int64_t n_valid, double gamma, double prior_weight, int32_t lf,
+                                 int32_t* n_below_out) {
+    if (!ctx) return TPE_ERR_ARG;
+    return build_resident(ctx, losses, n_trials, n_valid, gamma, prior_weight, lf, n_below_out);
+}
+
+int tpe_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
+                        const double* cat_p, int64_t n_cat_p, const double* losses,
+                        int64_t n_trials, const int64_t* obs_off, const int32_t* obs_trial,
+                        const double* obs_val, double gamma, double prior_weight, int32_t lf,
+                        int32_t* n_below_out) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (n_labels <= 0 || !specs || !obs_off || n_trials < 0 || (n_trials > 0 && !losses))
+        return ctx->fail(TPE_ERR_ARG, "tpe_build_posterior: bad arguments");
+    if (obs_off[0] != 0 || obs_off[n_labels] < 0 || obs_off[n_labels] >= INT32_MAX)
+        return ctx->fail(TPE_ERR_ARG, "observation offsets");
+    std::vector<int64_t> n_new(n_labels);
+    for (int32_t l = 0; l < n_labels; ++l) {
+        n_new[l] = obs_off[l + 1] - obs_off[l];
+        if (n_new[l] < 0) return ctx->fail(TPE_ERR_ARG, "observation offsets must not decrease");
+    }
+    int64_t n_valid = 0;
+    for (int64_t t = 0; t < n_trials; ++t) n_valid += losses[t] == losses[t];
+    int rc = history_reset(ctx, specs, n_labels, cat_p, n_cat_p);
+    if (!rc) rc = history_append(ctx, n_new.data(), obs_trial, obs_val);
+    if (!rc) rc = build_resident(ctx, losses, n_trials, n_valid, gamma, prior_weight, lf, n_below_out);
+    if (rc) ctx->build.hist_ready = false;
+    return rc;
 }
 
 int tpe_get_mixture(tpe_ctx* ctx, int32_t label, int32_t side, double* weights, double* mus,

@@ -71,36 +71,54 @@ struct Posterior {
     }
 };
 
-// Scratch of the device posterior builder (tpe_build.hip), grown on demand.
+// The device posterior builder (tpe_build.hip): the resident history pool
+// and the per-build scratch, grown on demand.
 struct BuildBufs {
+    // resident history (tpe_history_reset / tpe_history_append)
+    std::vector<tpe_label_spec> specs_h;
+    std::vector<int64_t> cap_h, off_h;   // per label pool capacity / offset
+    std::vector<int32_t> cnt_h;          // per label observations held
+    int64_t pool_cap = 0;
+    bool hist_ready = false;
     DevBuf<tpe_label_spec> specs;
     DevBuf<double> cat_p;
+    DevBuf<int64_t> p_off;         // pool offsets [L]
+    DevBuf<int32_t> cnt;           // observations held [L]
+    DevBuf<int32_t> p_trial;       // pool, observation order: trial position
+    DevBuf<double> p_val;          //   and (transformed) value
+    DevBuf<double> s_key, s_key2;  // pool, value order (continuous labels)
+    DevBuf<int32_t> s_idx, s_idx2; //   observation index of each sorted key
+    DevBuf<int32_t> arank;         // pool: rank in the above list, -1 if not above
+    DevBuf<int64_t> st_off;        // staging of an append: CSR offsets [L + 1]
+    DevBuf<int32_t> st_trial, st_idx, st_idx_sorted;
+    DevBuf<double> st_val, st_key_sorted;
+    DevBuf<int32_t> seg_begin, seg_end;
+    DevBuf<uint8_t> sort_tmp;
+    // per build
     DevBuf<double> losses;
     DevBuf<uint8_t> below;         // per trial: in the below set
-    DevBuf<int64_t> obs_off;       // CSR offsets of the observations per label
-    DevBuf<int32_t> obs_trial;
-    DevBuf<double> obs_val;
-    DevBuf<double> keys_in, keys_out;   // above observations (sort keys)
-    DevBuf<int32_t> idx_in, idx_out;    // their position in the above list
+    DevBuf<double> keys;           // per label: above observations (sorted / in order)
+    DevBuf<int32_t> idx;           //   and their above-list rank
     DevBuf<double> below_val;      // per label, <= lf below observations
     DevBuf<int32_t> counts;        // per label: below / above observation counts
     DevBuf<int32_t> kcount;        // per label: below / above component counts
-    DevBuf<int32_t> seg_begin, seg_end;
-    DevBuf<uint8_t> sort_tmp;
     DevBuf<double> w, mu, sigma;   // the built mixtures (tpe_get_mixture)
     DevBuf<int64_t> mix_off;       // per label: below / above offsets into w/mu/sigma
     DevBuf<double> scratch;        // per-component terms | pairwise leaf sums
-    DevBuf<int64_t> leaf;          // pairwise-summation leaf starts
+    DevBuf<int64_t> leaf;
     int32_t n_labels = 0;          // labels of the last build (0: none resident)
     std::vector<int64_t> mix_h;    // host copy of mix_off
     void release() {
-        specs.release(); cat_p.release(); losses.release(); below.release();
-        obs_off.release(); obs_trial.release(); obs_val.release();
-        keys_in.release(); keys_out.release(); idx_in.release(); idx_out.release();
-        below_val.release(); counts.release(); seg_begin.release(); seg_end.release();
-        sort_tmp.release(); w.release(); mu.release(); sigma.release(); mix_off.release();
-        scratch.release(); kcount.release(); leaf.release();
+        specs.release(); cat_p.release(); p_off.release(); cnt.release(); p_trial.release();
+        p_val.release(); s_key.release(); s_key2.release(); s_idx.release(); s_idx2.release();
+        arank.release(); st_off.release(); st_trial.release(); st_idx.release();
+        st_idx_sorted.release(); st_val.release(); st_key_sorted.release(); seg_begin.release();
+        seg_end.release(); sort_tmp.release(); losses.release(); below.release(); keys.release();
+        idx.release(); below_val.release(); counts.release(); kcount.release(); w.release();
+        mu.release(); sigma.release(); mix_off.release(); scratch.release(); leaf.release();
         n_labels = 0;
+        hist_ready = false;
+        pool_cap = 0;
     }
 };
 

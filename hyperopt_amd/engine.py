@@ -125,6 +125,34 @@ class Engine(object):
         self.n_labels = len(specs)
         return nb.value
 
+    # -- device-resident history -----------------------------------------------
+    def history_reset(self, specs, cat_p):
+        specs = np.ascontiguousarray(specs, dtype=SPEC_DTYPE)
+        cat_p = _f64(cat_p)
+        self._check(self.lib.tpe_history_reset(self.h, _ptr(specs), len(specs), _ptr(cat_p),
+                                               len(cat_p)))
+        self.hist_labels = len(specs)
+
+    def history_append(self, n_new, obs_trial, obs_val):
+        """n_new[l] new observations of label l (concatenated label-major):
+        trial positions (tid order) and transformed values."""
+        n_new = np.ascontiguousarray(n_new, dtype=np.int64)
+        obs_trial = np.ascontiguousarray(obs_trial, dtype=np.int32)
+        obs_val = _f64(obs_val)
+        self._check(self.lib.tpe_history_append(self.h, _ptr(n_new), _ptr(obs_trial),
+                                                _ptr(obs_val)))
+
+    def build_posterior_resident(self, losses, n_valid, gamma, prior_weight, lf=25):
+        """Rebuild the posterior from the resident history; losses per trial
+        position, NaN for a trial outside the history.  Returns n_below."""
+        losses = _f64(losses)
+        nb = ctypes.c_int32()
+        self._check(self.lib.tpe_build_posterior_resident(
+            self.h, _ptr(losses), len(losses), int(n_valid), float(gamma), float(prior_weight),
+            int(lf), ctypes.byref(nb)))
+        self.n_labels = self.hist_labels
+        return nb.value
+
     def get_mixture(self, label, side):
         """(weights, mus, sigmas) of a built mixture (side 0 below, 1 above)."""
         n = ctypes.c_int32()

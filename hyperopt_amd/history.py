@@ -182,6 +182,38 @@ class HistoryCache(object):
         return tids, losses, obs
 
 
+    def device_view(self, domain, trials):
+        """The whole history as the device-resident store wants it, or None
+        when the fast layout does not apply (from_tid groups, duplicate tids,
+        docs not in increasing tid order): (tids of ALL docs in order, their
+        losses -- None -> +inf, NaN kept, so NaN-loss docs stay out of both
+        sets --, the number of non-NaN losses, the append-only per-label
+        columns {label: (tids, vals)}, self)."""
+        docs = trials.trials
+        self.ingest(docs)
+        if self.has_from or self.dup_tid or len(self.order) != len(docs):
+            return None
+        n = len(docs)
+        if len(self._tid_arr) != n:
+            self._tid_arr = np.concatenate([self._tid_arr, np.asarray(
+                self.doc_tids[len(self._tid_arr):], dtype=np.int64)])
+        tids = self._tid_arr
+        if n > 1 and not np.all(tids[1:] > tids[:-1]):
+            return None
+        if type(domain).loss is _plain_loss:
+            raw = [d['result'].get('loss') for d in docs]
+        else:
+            raw = [domain.loss(d['result'], d['spec']) for d in docs]
+        if None not in raw:
+            losses = np.array(raw, dtype=np.float64)
+        else:
+            losses = np.array([float('inf') if v is None else float(v) for v in raw],
+                              dtype=np.float64)
+        n_valid = int(np.count_nonzero(losses == losses))
+        cols = {k: self.cols[k].arrays() for k in self.labels}
+        return tids, losses, n_valid, cols, self
+
+
 _caches = weakref.WeakKeyDictionary()
 
 
@@ -198,6 +230,22 @@ def gather(domain, trials, labels):
         except TypeError:
             pass
     return cache.gather(domain, trials)
+
+
+def device_view(domain, trials, labels):
+    """HistoryCache.device_view through the per-Trials cache."""
+    key = tuple(labels)
+    try:
+        cache = _caches.get(trials)
+    except TypeError:
+        cache = None
+    if cache is None or cache.labels != list(key):
+        cache = HistoryCache(key)
+        try:
+            _caches[trials] = cache
+        except TypeError:
+            pass
+    return cache.device_view(domain, trials)
 
 
 def isnan(x):

@@ -217,6 +217,73 @@ def label_spec(kind, args):
     return spec, tr, None
 
 
+def spec_table(labels):
+    """(SPEC_DTYPE array, concatenated categorical p, per-label observation
+    transform or None) for labels = [(name, kind, args)]."""
+    from .engine import SPEC_DTYPE
+    specs = np.zeros(len(labels), dtype=SPEC_DTYPE)
+    cat_p, p_len, trs = [], 0, []
+    for i, (name, kind, args) in enumerate(labels):
+        sp, tr, p = label_spec(kind, args)
+        for k, v in sp.items():
+            specs[i][k] = v
+        if p is not None:
+            specs[i]['p_off'] = p_len
+            cat_p.append(p)
+            p_len += len(p)
+        trs.append(tr)
+    return specs, (np.concatenate(cat_p) if cat_p else np.zeros(0)), trs
+
+
+class DeviceHistoryUploader(object):
+    """Keeps an Engine's device-resident history (tpe_history_*) in step with
+    a growing trial history: only observations added since the last call are
+    transformed and uploaded; anything else (new labels, another history, a
+    trial inserted before existing ones) resets it."""
+
+    def __init__(self):
+        self.key = None
+
+    def build(self, eng, labels, view, gamma, prior_weight, lf=DEFAULT_LF):
+        tids, losses, n_valid, cols, owner = view
+        key = (id(owner), tuple((n, k) for n, k, _ in labels))
+        fresh = (self.key != key or len(tids) < self.n_trials or
+                 (self.n_trials and tids[self.n_trials - 1] != self.last_tid) or
+                 any(len(cols[n][0]) < c for (n, _, _), c in zip(labels, self.prev_counts)))
+        if fresh:
+            specs, cat_p, self.trs = spec_table(labels)
+            eng.history_reset(specs, cat_p)
+            self.prev_counts = [0] * len(labels)
+        n_new, trial_parts, val_parts = [], [], []
+        for i, (name, _, _) in enumerate(labels):
+            oi, ov = cols[name]
+            c0 = self.prev_counts[i]
+            ni, nv = oi[c0:], ov[c0:]
+            if len(ni):
+                tr = self.trs[i]
+                if tr is not None:
+                    nv = tr(nv)
+                pos = np.searchsorted(tids, ni)
+                pc = np.minimum(pos, len(tids) - 1)
+                pos = np.where(tids[pc] == ni, pc, -1)
+                trial_parts.append(pos.astype(np.int32))
+                val_parts.append(np.asarray(nv, dtype=float))
+            n_new.append(len(ni))
+            self.prev_counts[i] = len(oi)
+        if sum(n_new):
+            eng.history_append(np.asarray(n_new, dtype=np.int64), np.concatenate(trial_parts),
+                               np.concatenate(val_parts))
+        self.key = key
+        self.n_trials = len(tids)
+        self.last_tid = tids[-1] if len(tids) else None
+        return eng.build_posterior_resident(losses, n_valid, gamma, prior_weight, lf)
+
+    prev_counts = ()
+    n_trials = 0
+    last_tid = None
+    trs = ()
+
+
 def device_inputs(labels, tids, losses, obs):
     """Arguments of Engine.build_posterior (tpe_build_posterior) for a
     history: labels = [(name, kind, args)], tids/losses of the represented

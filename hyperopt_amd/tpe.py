@@ -129,8 +129,16 @@ def suggest(new_ids, domain, trials, seed,
     n_obs = sum(len(obs[k][0]) for k in specs)
     if posterior_builder == 'device' or (posterior_builder == 'auto' and
                                          n_obs >= DEVICE_BUILD_MIN_OBS):
-        eng.build_posterior(*device_inputs(specs, tids, losses, obs), gamma=gamma,
-                            prior_weight=prior_weight)
+        view = _history.device_view(domain, trials, list(specs))
+        if view is not None:      # device-resident history: upload only what is new
+            up = getattr(eng, '_history_uploader', None)
+            if up is None:
+                up = eng._history_uploader = _post.DeviceHistoryUploader()
+            up.build(eng, [(s.label, s.kind, s.args) for s in specs.values()], view, gamma,
+                     prior_weight)
+        else:
+            eng.build_posterior(*device_inputs(specs, tids, losses, obs), gamma=gamma,
+                                prior_weight=prior_weight)
     else:
         splitter = _post.Splitter(tids, losses, gamma)
         posts = []

@@ -195,6 +195,25 @@ int tpe_build_posterior(tpe_ctx *ctx, const tpe_label_spec *specs, int32_t n_lab
                         const double *obs_val, double gamma, double prior_weight,
                         int32_t lf, int32_t *n_below_out);
 
+/* Device-resident history (the columnar trial history of SURVEY §8f rank 1,
+ * kept on the GPU): tpe_history_reset fixes the labels; tpe_history_append
+ * adds only NEW observations (per label n_new[l] of them, concatenated
+ * label-major: trial position in tid order and transformed value, as for
+ * tpe_build_posterior) -- each label's observations are kept in observation
+ * order and value-sorted (a stable merge of the sorted new batch), so a
+ * rebuild sorts nothing; tpe_build_posterior_resident then rebuilds the
+ * posterior from the current losses.  losses[t] = NaN marks a trial that is
+ * not in the history (its observations join neither set, like a NaN-loss doc
+ * in tpe.py:849-853); n_valid = the number of non-NaN losses (len(l_vals)).
+ * tpe_build_posterior is reset + append(all) + build_resident. */
+int tpe_history_reset(tpe_ctx *ctx, const tpe_label_spec *specs, int32_t n_labels,
+                      const double *cat_p, int64_t n_cat_p);
+int tpe_history_append(tpe_ctx *ctx, const int64_t *n_new, const int32_t *obs_trial,
+                       const double *obs_val);
+int tpe_build_posterior_resident(tpe_ctx *ctx, const double *losses, int64_t n_trials,
+                                 int64_t n_valid, double gamma, double prior_weight,
+                                 int32_t lf, int32_t *n_below_out);
+
 /* Read back one mixture of the resident posterior built by
  * tpe_build_posterior (side 0 below, 1 above): the (weights, mus, sigmas)
  * that adaptive_parzen_normal returns (categorical: p in weights).  *n

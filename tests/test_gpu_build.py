@@ -172,3 +172,42 @@ def test_build_errors(eng):
     bad[0]['kind'] = 9
     with pytest.raises(Exception):
         eng.build_posterior(bad, cat, losses, off, tr, val, 0.25, 1.0)
+
+
+def test_resident_history_incremental(eng):
+    """Device-resident history: observations appended in several batches
+    (sorted per batch, merged into each label's value order) give, after
+    every append, the same mixtures as the oracle on the history so far --
+    with tied losses and values, conditional labels, pending trials (+inf)
+    and NaN-loss trials (outside the history: their observations join
+    neither set, as the reference drops such docs)."""
+    from hyperopt_amd import posterior as P
+    hist = make_history(ALL_KINDS, 2400, seed=21, active_frac=0.6, loss_round=1)
+    losses = hist.losses.copy()
+    losses[7] = np.inf
+    losses[100] = np.nan
+    losses[1500] = np.nan
+    specs, cat_p, trs = P.spec_table(hist.labels)
+    eng.history_reset(specs, cat_p)
+    counts = [0] * len(hist.labels)
+    for cut in (30, 31, 400, 1999, 2400):
+        n_new, tr_parts, val_parts = [], [], []
+        for i, (name, kind, args) in enumerate(hist.labels):
+            oi, ov = hist.obs[name]
+            keep = oi < hist.tids[cut - 1] + 1
+            oi, ov = oi[keep], ov[keep]
+            ni, nv = oi[counts[i]:], ov[counts[i]:]
+            if trs[i] is not None and len(nv):
+                nv = trs[i](nv)
+            tr_parts.append(np.searchsorted(hist.tids, ni).astype(np.int32))
+            val_parts.append(np.asarray(nv, dtype=float))
+            n_new.append(len(ni))
+            counts[i] = len(oi)
+        eng.history_append(np.asarray(n_new), np.concatenate(tr_parts), np.concatenate(val_parts))
+        lsub = losses[:cut]
+        eng.build_posterior_resident(lsub, int(np.count_nonzero(lsub == lsub)), 0.25, 1.0)
+        ok = lsub == lsub
+        from hyperopt_amd.workloads import History
+        sub = History(hist.labels, hist.tids[:cut][ok], lsub[ok],
+                      {n: hist.obs[n] for n, _, _ in hist.labels})
+        _check_bit_exact(eng, sub, oracle_mixtures(sub, sort_kind='stable'))
