@@ -119,33 +119,43 @@ def suggest(new_ids, domain, trials, seed,
     if posterior_builder not in ('auto', 'host', 'device'):
         raise ValueError('posterior_builder must be auto, host or device')
     specs = specs_of(domain)
-    tids, losses, obs = _history.gather(domain, trials, list(specs))
-    n_docs = len(tids)
+    labels = list(specs)
+    # the device-resident history's view of the trials (None when the fast
+    # layout does not apply); otherwise the general gather
+    view = _history.device_view(domain, trials, labels) if posterior_builder != 'host' else None
+    if view is not None:
+        n_docs = view[2]
+        n_obs = sum(len(view[3][k][0]) for k in labels)
+    else:
+        tids, losses, obs = _history.gather(domain, trials, labels)
+        n_docs = len(tids)
+        n_obs = sum(len(obs[k][0]) for k in labels)
     if n_docs < n_startup_jobs or n_docs == 0:
         if n_docs == 0 and n_startup_jobs <= 0:
             logger.info('TPE using 0 trials')
         return rand.suggest(list(new_ids[:1]) if not batch else new_ids, domain, trials, seed)
     eng = _engine.get_engine(device, precision)
-    n_obs = sum(len(obs[k][0]) for k in specs)
-    if posterior_builder == 'device' or (posterior_builder == 'auto' and
-                                         n_obs >= DEVICE_BUILD_MIN_OBS):
-        view = _history.device_view(domain, trials, list(specs))
-        if view is not None:      # device-resident history: upload only what is new
-            up = getattr(eng, '_history_uploader', None)
-            if up is None:
-                up = eng._history_uploader = _post.DeviceHistoryUploader()
-            up.build(eng, [(s.label, s.kind, s.args) for s in specs.values()], view, gamma,
-                     prior_weight)
-        else:
+    on_device = posterior_builder == 'device' or (posterior_builder == 'auto' and
+                                                  n_obs >= DEVICE_BUILD_MIN_OBS)
+    if on_device and view is not None:   # upload only the observations that are new
+        up = getattr(eng, '_history_uploader', None)
+        if up is None:
+            up = eng._history_uploader = _post.DeviceHistoryUploader()
+        up.build(eng, [(s.label, s.kind, s.args) for s in specs.values()], view, gamma,
+                 prior_weight)
+    else:
+        if view is not None:
+            tids, losses, obs = _history.gather(domain, trials, labels)
+        if on_device:
             eng.build_posterior(*device_inputs(specs, tids, losses, obs), gamma=gamma,
                                 prior_weight=prior_weight)
-    else:
-        splitter = _post.Splitter(tids, losses, gamma)
-        posts = []
-        for label, sp in specs.items():
-            b, a = splitter.split(*obs[label])
-            posts.append(_post.label_posterior(label, sp.kind, sp.args, b, a, prior_weight))
-        eng.set_posterior(*_post.pack(posts))
+        else:
+            splitter = _post.Splitter(tids, losses, gamma)
+            posts = []
+            for label, sp in specs.items():
+                b, a = splitter.split(*obs[label])
+                posts.append(_post.label_posterior(label, sp.kind, sp.args, b, a, prior_weight))
+            eng.set_posterior(*_post.pack(posts))
     ids = list(new_ids) if batch else [new_ids[0]]
     if len(ids) == 1:
         res = eng.suggest(seed, n_EI_candidates, round=ids[0])[None]
