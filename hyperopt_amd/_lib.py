@@ -94,6 +94,7 @@ SIGNATURES = {
     'tpe_build_posterior': (ctypes.c_int, [_P, _P, _I32, _P, _I64, _P, _I64, _P, _P, _P, _D, _D,
                                            _I32, _P]),
     'tpe_get_mixture': (ctypes.c_int, [_P, _I32, _I32, _P, _P, _P, _I32, _P]),
+    'tpe_resident_labels': (ctypes.c_int32, [_P]),
     'tpe_history_reset': (ctypes.c_int, [_P, _P, _I32, _P, _I64]),
     'tpe_history_append': (ctypes.c_int, [_P, _P, _P, _P]),
     'tpe_build_posterior_resident': (ctypes.c_int, [_P, _P, _I64, _I64, _D, _D, _I32, _P]),

@@ -45,7 +45,7 @@ namespace {
 
 constexpr int kSplitBlock = 1024;
 constexpr int kPartBlock = 1024;
-constexpr int kParzenBlock = 256;
+constexpr int kParzenBlock = 1024;
 constexpr int kMaxLF = 64;          // below-list capacity per label (lf <= kMaxLF)
 
 // ------------------------------------------------ numpy pairwise summation --
@@ -156,6 +156,7 @@ __device__ double block_np_sum(const double* __restrict__ a, int64_t n, double* 
     const int64_t tail = n - full * kNpChunk;
     const int tail_leaves = tail ? pw_leaves<kPwDepth>(tail) : 0;
     const int64_t total = full * kNpChunkLeaves + tail_leaves;
+    __syncthreads();   // a[] was just written by the other threads of the block
     for (int64_t t = threadIdx.x; t < total; t += blockDim.x) {
         int64_t s, len;
         if (t < full * kNpChunkLeaves) {
@@ -228,27 +229,36 @@ __device__ __forceinline__ double np_minimum(double a, double b) { return (a != 
 // --------------------------------------------------------------- kernels --
 
 // ap_filter_trials' split (tpe.py:636-645): flag the n_below lowest losses
-// (ties by position), by n_below rounds of a workgroup-wide lexicographic
-// argmin above the previous pick.
+// (ties by position).  Two-level selection in one workgroup: every wave
+// takes the n_below lexicographically smallest (loss, position) pairs of its
+// share by n_below wave-wide argmin rounds (shuffles only, no barriers), and
+// one wave then picks the n_below smallest of those <= 16 n_below finalists.
+__device__ __forceinline__ void wave_argmin(uint64_t& k, int64_t& i) {
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t ok = __shfl_xor(k, off);
+        const int64_t oi = __shfl_xor(i, off);
+        if (ok < k || (ok == k && oi < i)) {
+            k = ok;
+            i = oi;
+        }
+    }
+}
+
 __global__ __launch_bounds__(kSplitBlock) void k_split(const double* __restrict__ losses, int64_t T,
                                                        int32_t n_below, uint8_t* __restrict__ below) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    constexpr int W = kSplitBlock / 64;
     for (int64_t i = tid; i < T; i += kSplitBlock) below[i] = 0;
-    __shared__ uint64_t wk[kSplitBlock / 64];
-    __shared__ int64_t wi[kSplitBlock / 64];
-    __shared__ uint64_t prev_k;
-    __shared__ int64_t prev_i;
-    if (tid == 0) {
-        prev_k = 0;
-        prev_i = -1;
-    }
-    __syncthreads();
+    __shared__ uint64_t fk[W * kMaxLF];
+    __shared__ int64_t fi[W * kMaxLF];
+    // level 1: wave wv owns elements wv * 64 + lane + j * kSplitBlock
+    uint64_t pk = 0;
+    int64_t pi = -1;
     for (int r = 0; r < n_below; ++r) {
-        const uint64_t pk = prev_k;
-        const int64_t pi = prev_i;
         uint64_t bk = ~0ull;
         int64_t bi = INT64_MAX;
-        for (int64_t i = tid; i < T; i += kSplitBlock) {
+#pragma unroll 8
+        for (int64_t i = wv * 64 + lane; i < T; i += kSplitBlock) {
             const uint64_t k = asc_key(losses[i]);
             const bool after = k > pk || (k == pk && i > pi);
             if (after && (k < bk || (k == bk && i < bi))) {
@@ -256,30 +266,39 @@ __global__ __launch_bounds__(kSplitBlock) void k_split(const double* __restrict_
                 bi = i;
             }
         }
-        for (int off = 32; off > 0; off >>= 1) {
-            const uint64_t ok = __shfl_xor(bk, off);
-            const int64_t oi = __shfl_xor(bi, off);
-            if (ok < bk || (ok == bk && oi < bi)) {
-                bk = ok;
-                bi = oi;
-            }
-        }
+        wave_argmin(bk, bi);
         if (lane == 0) {
-            wk[wv] = bk;
-            wi[wv] = bi;
+            fk[wv * kMaxLF + r] = bk;
+            fi[wv * kMaxLF + r] = bi;
         }
-        __syncthreads();
-        if (tid == 0) {
-            for (int w = 1; w < kSplitBlock / 64; ++w)
-                if (wk[w] < bk || (wk[w] == bk && wi[w] < bi)) {
-                    bk = wk[w];
-                    bi = wi[w];
+        pk = bk;
+        pi = bi;
+    }
+    __syncthreads();
+    // level 2: wave 0 over the finalists
+    if (wv == 0) {
+        pk = 0;
+        pi = -1;
+        const int nf = W * n_below;
+        for (int r = 0; r < n_below; ++r) {
+            uint64_t bk = ~0ull;
+            int64_t bi = INT64_MAX;
+            for (int f = lane; f < nf; f += 64) {
+                const int w = f / n_below, j = f - w * n_below;
+                const uint64_t k = fk[w * kMaxLF + j];
+                const int64_t i = fi[w * kMaxLF + j];
+                if (i == INT64_MAX) continue;
+                const bool after = k > pk || (k == pk && i > pi);
+                if (after && (k < bk || (k == bk && i < bi))) {
+                    bk = k;
+                    bi = i;
                 }
-            if (bi != INT64_MAX) below[bi] = 1;
-            prev_k = bk;
-            prev_i = bi;
+            }
+            wave_argmin(bk, bi);
+            if (lane == 0 && bi != INT64_MAX) below[bi] = 1;
+            pk = bk;
+            pi = bi;
         }
-        __syncthreads();
     }
 }
 
@@ -1103,6 +1122,8 @@ int tpe_get_mixture(tpe_ctx* ctx, int32_t label, int32_t side, double* weights, 
     }
     return TPE_OK;
 }
+
+int32_t tpe_resident_labels(const tpe_ctx* ctx) { return ctx ? ctx->resident.n_labels : 0; }
 
 int tpe_last_build_ms(const tpe_ctx* ctx, float* ms) {
     if (!ctx || !ms) return TPE_ERR_ARG;

@@ -263,8 +263,13 @@ __global__ __launch_bounds__(kBlock) void k_round(
 // the round (partial sums relative to the same LSE shift, or partial
 // probabilities for quantized labels), and a finishing kernel adds the
 // slices in order, takes the log and does the broadcast_best maxloc.
-constexpr int kSlice = 256;
+constexpr int kSlice = 256;      // dense: ~12 VALU per component
+constexpr int kSliceQ = 64;      // quantized: two erf per component
 constexpr int kSliceWaves = kBlock / 64;
+
+__host__ __device__ constexpr int slice_len(int mode) {
+    return (mode == QUANT_GMM || mode == QUANT_LGMM) ? kSliceQ : kSlice;
+}
 
 // candidates of one (round, label): the same Philox draws as k_round / k_qsample
 template <int MODE>
@@ -347,12 +352,13 @@ __global__ __launch_bounds__(kBlock) void k_score_slices(
     __shared__ double exp_tab[kTab ? kExpTabSize : 1];
     if constexpr (kTab) load_exp_table(exp_tab);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int nsb = (L.nb + kSlice - 1) / kSlice, nsa = (L.na + kSlice - 1) / kSlice;
+    constexpr int S = slice_len(MODE);
+    const int nsb = (L.nb + S - 1) / S, nsa = (L.na + S - 1) / S;
     const int slice = blockIdx.x * kSliceWaves + wave;
     if (slice >= nsb + nsa) return;
     const bool above = slice >= nsb;
-    const int k0 = (above ? slice - nsb : slice) * kSlice;
-    const int k1 = min(k0 + kSlice, above ? L.na : L.nb);
+    const int k0 = (above ? slice - nsb : slice) * S;
+    const int k1 = min(k0 + S, above ? L.na : L.nb);
     const int64_t base = above ? L.comp_a : L.comp_b;
     const double* xrow = xs + ((size_t)z * n_labels + li) * n;
     double* prow = part + (((size_t)z * n_labels + li) * s_max + slice) * n;
@@ -370,7 +376,8 @@ __global__ __launch_bounds__(kBlock) void k_finish_slices(
     const int li = group[blockIdx.x];
     const DLabel L = labels[li];
     const int64_t z = blockIdx.y;
-    const int nsb = (L.nb + kSlice - 1) / kSlice, nsa = (L.na + kSlice - 1) / kSlice;
+    constexpr int S = slice_len(MODE);
+    const int nsb = (L.nb + S - 1) / S, nsa = (L.na + S - 1) / S;
     const double* xrow = xs + ((size_t)z * n_labels + li) * n;
     const double* prow = part + ((size_t)z * n_labels + li) * s_max * n;
     uint64_t bk = 0;
@@ -853,7 +860,8 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
 constexpr int64_t kSplitKMaxSlots = 2048;   // n * n_rounds per label
 
 inline int slices_of(const DLabel& d) {
-    return (d.nb + kSlice - 1) / kSlice + (d.na + kSlice - 1) / kSlice;
+    const int S = slice_len(d.mode);
+    return (d.nb + S - 1) / S + (d.na + S - 1) / S;
 }
 
 template <typename T, int MODE>

@@ -122,7 +122,7 @@ class Engine(object):
             self.h, _ptr(specs), len(specs), _ptr(cat_p), len(cat_p), _ptr(losses), len(losses),
             _ptr(obs_off), _ptr(obs_trial), _ptr(obs_val), float(gamma), float(prior_weight),
             int(lf), ctypes.byref(nb)))
-        self.n_labels = len(specs)
+        self.n_labels = self.hist_labels = len(specs)
         return nb.value
 
     # -- device-resident history -----------------------------------------------
@@ -168,8 +168,14 @@ class Engine(object):
         self._check(self.lib.tpe_last_build_ms(self.h, ctypes.byref(ms)))
         return ms.value
 
+    def _labels(self):
+        """Rows tpe_suggest writes per round: asked from the library, so an
+        output buffer can never be shorter than the resident posterior."""
+        self.n_labels = int(self.lib.tpe_resident_labels(self.h))
+        return self.n_labels
+
     def suggest(self, seed, n_candidates, round=0, cand_offset=0):
-        out = np.zeros(self.n_labels, dtype=RESULT_DTYPE)
+        out = np.zeros(self._labels(), dtype=RESULT_DTYPE)
         self._check(self.lib.tpe_suggest(self.h, int(seed) & 0xFFFFFFFFFFFFFFFF,
                                          int(round) & 0xFFFFFFFF, int(n_candidates),
                                          int(cand_offset), _ptr(out)))
@@ -177,7 +183,7 @@ class Engine(object):
 
     def suggest_batch(self, seed, rounds, n_candidates, cand_offset=0):
         rounds = np.ascontiguousarray(np.asarray(rounds, dtype=np.uint32))
-        out = np.zeros(len(rounds) * self.n_labels, dtype=RESULT_DTYPE)
+        out = np.zeros(len(rounds) * self._labels(), dtype=RESULT_DTYPE)
         self._check(self.lib.tpe_suggest_batch(self.h, int(seed) & 0xFFFFFFFFFFFFFFFF,
                                                _ptr(rounds), len(rounds), int(n_candidates),
                                                int(cand_offset), _ptr(out)))

@@ -221,6 +221,10 @@ int tpe_build_posterior_resident(tpe_ctx *ctx, const double *losses, int64_t n_t
 int tpe_get_mixture(tpe_ctx *ctx, int32_t label, int32_t side, double *weights,
                     double *mus, double *sigmas, int32_t cap, int32_t *n);
 
+/* Number of labels of the resident posterior (the row count tpe_suggest
+ * writes per round). */
+int32_t tpe_resident_labels(const tpe_ctx *ctx);
+
 /* Device time (ms, HIP events) of the last tpe_build_posterior's kernels. */
 int tpe_last_build_ms(const tpe_ctx *ctx, float *ms);
 
