@@ -172,9 +172,21 @@ __device__ double block_np_sum(const double* __restrict__ a, int64_t n, double* 
     // chunk trees: one thread per chunk; sums beyond 64 chunks go through the
     // leaf buffer's own slots (each chunk's first leaf slot is free once read)
     for (int64_t c = threadIdx.x; c < n_chunks; c += blockDim.x) {
-        int next = 0;
-        const int64_t m = c < full ? kNpChunk : tail;
-        const double v = pw_tree<kPwDepth>(m, leaf_sum + c * kNpChunkLeaves, next);
+        double v;
+        if (c < full) {   // a full chunk's tree is perfectly balanced: pairs up, level by level
+            double t[kNpChunkLeaves / 2];
+            const double* ls = leaf_sum + c * kNpChunkLeaves;
+#pragma unroll
+            for (int j = 0; j < kNpChunkLeaves / 2; ++j) t[j] = ls[2 * j] + ls[2 * j + 1];
+#pragma unroll
+            for (int w = kNpChunkLeaves / 4; w >= 1; w /= 2)
+#pragma unroll
+                for (int j = 0; j < w; ++j) t[j] = t[2 * j] + t[2 * j + 1];
+            v = t[0];
+        } else {
+            int next = 0;
+            v = pw_tree<kPwDepth>(tail, leaf_sum + c * kNpChunkLeaves, next);
+        }
         if (c < 64) chunk_sum[c] = v;
         else leaf_sum[c * kNpChunkLeaves] = v;
     }
