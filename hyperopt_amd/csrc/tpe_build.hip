@@ -240,77 +240,69 @@ __device__ __forceinline__ double np_minimum(double a, double b) { return (a != 
 
 // --------------------------------------------------------------- kernels --
 
-// ap_filter_trials' split (tpe.py:636-645): flag the n_below lowest losses
-// (ties by position).  Two-level selection in one workgroup: every wave
-// takes the n_below lexicographically smallest (loss, position) pairs of its
-// share by n_below wave-wide argmin rounds (shuffles only, no barriers), and
-// one wave then picks the n_below smallest of those <= 16 n_below finalists.
-__device__ __forceinline__ void wave_argmin(uint64_t& k, int64_t& i) {
-    for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t ok = __shfl_xor(k, off);
-        const int64_t oi = __shfl_xor(i, off);
-        if (ok < k || (ok == k && oi < i)) {
-            k = ok;
-            i = oi;
-        }
-    }
-}
-
+// ap_filter_trials' split (tpe.py:636-645): flag the n_below lowest losses,
+// ties by position.  Radix select in one workgroup: 8 passes of 8-bit digits
+// over the order-preserving 64-bit keys locate the n_below-th smallest key
+// K* (LDS histograms), then one ordered pass flags every key < K* and the
+// first (by position) of the keys == K* that complete n_below.
 __global__ __launch_bounds__(kSplitBlock) void k_split(const double* __restrict__ losses, int64_t T,
                                                        int32_t n_below, uint8_t* __restrict__ below) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    constexpr int W = kSplitBlock / 64;
+    __shared__ uint32_t hist[256];
+    __shared__ uint64_t prefix_sh;
+    __shared__ int64_t need_sh;
+    __shared__ int wcnt[kSplitBlock / 64];
+    __shared__ int64_t base_sh;
     for (int64_t i = tid; i < T; i += kSplitBlock) below[i] = 0;
-    __shared__ uint64_t fk[W * kMaxLF];
-    __shared__ int64_t fi[W * kMaxLF];
-    // level 1: wave wv owns elements wv * 64 + lane + j * kSplitBlock
-    uint64_t pk = 0;
-    int64_t pi = -1;
-    for (int r = 0; r < n_below; ++r) {
-        uint64_t bk = ~0ull;
-        int64_t bi = INT64_MAX;
-#pragma unroll 8
-        for (int64_t i = wv * 64 + lane; i < T; i += kSplitBlock) {
-            const uint64_t k = asc_key(losses[i]);
-            const bool after = k > pk || (k == pk && i > pi);
-            if (after && (k < bk || (k == bk && i < bi))) {
-                bk = k;
-                bi = i;
-            }
-        }
-        wave_argmin(bk, bi);
-        if (lane == 0) {
-            fk[wv * kMaxLF + r] = bk;
-            fi[wv * kMaxLF + r] = bi;
-        }
-        pk = bk;
-        pi = bi;
+    if (n_below <= 0 || T <= 0) return;
+    if (tid == 0) {
+        prefix_sh = 0;
+        need_sh = n_below;   // rank (1-based) of K* among the keys matching the prefix
     }
-    __syncthreads();
-    // level 2: wave 0 over the finalists
-    if (wv == 0) {
-        pk = 0;
-        pi = -1;
-        const int nf = W * n_below;
-        for (int r = 0; r < n_below; ++r) {
-            uint64_t bk = ~0ull;
-            int64_t bi = INT64_MAX;
-            for (int f = lane; f < nf; f += 64) {
-                const int w = f / n_below, j = f - w * n_below;
-                const uint64_t k = fk[w * kMaxLF + j];
-                const int64_t i = fi[w * kMaxLF + j];
-                if (i == INT64_MAX) continue;
-                const bool after = k > pk || (k == pk && i > pi);
-                if (after && (k < bk || (k == bk && i < bi))) {
-                    bk = k;
-                    bi = i;
-                }
-            }
-            wave_argmin(bk, bi);
-            if (lane == 0 && bi != INT64_MAX) below[bi] = 1;
-            pk = bk;
-            pi = bi;
+    uint64_t mask = 0;
+    for (int shift = 56; shift >= 0; shift -= 8) {
+        for (int b = tid; b < 256; b += kSplitBlock) hist[b] = 0;
+        __syncthreads();
+        const uint64_t prefix = prefix_sh;
+#pragma unroll 4
+        for (int64_t i = tid; i < T; i += kSplitBlock) {
+            const uint64_t k = asc_key(losses[i]);
+            if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
         }
+        __syncthreads();
+        if (tid == 0) {
+            int64_t need = need_sh, acc = 0;
+            int d = 0;
+            for (; d < 255; ++d) {
+                if (acc + hist[d] >= need) break;
+                acc += hist[d];
+            }
+            need_sh = need - acc;
+            prefix_sh = prefix | ((uint64_t)d << shift);
+        }
+        mask |= 255ull << shift;
+        __syncthreads();
+    }
+    const uint64_t kstar = prefix_sh;
+    const int64_t take_eq = need_sh;      // how many keys == K* join, in position order
+    if (tid == 0) base_sh = 0;
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int64_t c0 = 0; c0 < T; c0 += kSplitBlock) {
+        const int64_t i = c0 + tid;
+        uint64_t k = ~0ull;
+        if (i < T) k = asc_key(losses[i]);
+        const bool eq = i < T && k == kstar;
+        const uint64_t m = __ballot(eq);
+        if (lane == 0) wcnt[wv] = __popcll(m);
+        __syncthreads();
+        int64_t r = base_sh + __popcll(m & lt);
+        for (int w = 0; w < wv; ++w) r += wcnt[w];
+        if (i < T && (k < kstar || (eq && r < take_eq))) below[i] = 1;
+        __syncthreads();
+        if (tid == 0)
+            for (int w = 0; w < kSplitBlock / 64; ++w) base_sh += wcnt[w];
+        __syncthreads();
     }
 }
 
