@@ -140,3 +140,39 @@ def test_device_and_host_posterior_same_suggestion():
         a = tpe.suggest([500], dom, trials, seed, posterior_builder='host')[0]['misc']['vals']
         b = tpe.suggest([500], dom, trials, seed, posterior_builder='device')[0]['misc']['vals']
         assert a == b, (seed, a, b)
+
+
+def test_device_history_uploader_follows_trials():
+    """tpe.suggest with the device-resident history while the Trials object
+    evolves: trials appended one by one, a pending trial (no loss -> +inf),
+    a NaN loss (dropped), an errored trial removed by refresh (forces a
+    re-upload), more trials appended.  Each step suggests the same document
+    as the host builder (tie-free continuous space)."""
+    from hyperopt_amd.base import JOB_STATE_ERROR
+    space = {'a': hp.uniform('a', -3, 3), 'b': hp.loguniform('b', -2, 2),
+             'c': hp.normal('c', 0, 1)}
+    trials = H.Trials()
+    H.fmin(lambda d: d['a'] ** 2 + d['b'] + 0.1 * d['c'], space,
+           algo=partial(tpe.suggest, posterior_builder='device'), max_evals=60,
+           trials=trials, rstate=np.random.RandomState(9))
+    dom = H.Domain(lambda d: 0, space)
+
+    def same(seed):
+        a = tpe.suggest([1000], dom, trials, seed, posterior_builder='host')[0]['misc']['vals']
+        b = tpe.suggest([1000], dom, trials, seed, posterior_builder='device')[0]['misc']['vals']
+        assert a == b, (seed, a, b)
+
+    same(1)
+    trials.trials[-1]['result'] = {'status': 'new'}           # pending
+    same(2)
+    keep = trials.trials[10]['result']['loss']
+    trials.trials[10]['result']['loss'] = float('nan')          # NaN loss
+    same(3)
+    trials.trials[10]['result']['loss'] = keep
+    trials._dynamic_trials[5]['state'] = JOB_STATE_ERROR        # errored -> removed
+    trials.refresh()
+    same(4)
+    H.fmin(lambda d: d['a'] ** 2 + d['b'] + 0.1 * d['c'], space,
+           algo=partial(tpe.suggest, posterior_builder='device'), max_evals=70,
+           trials=trials, rstate=np.random.RandomState(10))
+    same(5)
