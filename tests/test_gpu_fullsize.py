@@ -34,19 +34,43 @@ def _score(p, x):
             f(x, *p.above, low=p.low, high=p.high, q=p.q))
 
 
-@pytest.mark.parametrize('config', ['config2', 'config3'])
-def test_fullsize_winner_properties(config):
+def _device_posts(eng, hist):
+    """Build the posterior on the device and read the mixtures back as
+    LabelPosterior objects (for the oracle)."""
+    from hyperopt_amd import posterior as P
+    eng.build_posterior(*hist.device_inputs(), gamma=0.25, prior_weight=1.0)
+    posts = []
+    for li, (name, kind, args) in enumerate(hist.labels):
+        b, a = eng.get_mixture(li, 0), eng.get_mixture(li, 1)
+        if kind in ('randint', 'categorical'):
+            posts.append(P.LabelPosterior(name, 'categorical', b[0], a[0], upper=len(b[0])))
+        else:
+            spec, _, _ = P.label_spec(kind, args)
+            posts.append(P.LabelPosterior(name, 'GMM1' if spec['kind'] == 0 else 'LGMM1', b, a,
+                                          low=args.get('low'), high=args.get('high'),
+                                          q=args.get('q')))
+    return posts
+
+
+@pytest.mark.parametrize('config,builder', [('config2', 'host'), ('config3', 'host'),
+                                            ('config3', 'device'), ('config4', 'device')])
+def test_fullsize_winner_properties(config, builder):
     from hyperopt_amd import posterior as P
     from hyperopt_amd.engine import Engine
-    from hyperopt_amd.workloads import hartmann_history, mixed_history
+    from hyperopt_amd.workloads import conditional_history, hartmann_history, mixed_history
     if config == 'config2':
         hist, C = hartmann_history(2000, seed=0), 1 << 20
+    elif config == 'config4':
+        hist, C = conditional_history(5000, seed=0), 1 << 20
     else:
         hist, C = mixed_history(32, 10000, seed=0), 1 << 21
-    posts = hist.posteriors()
     eng = Engine(0, 'f64')
     try:
-        eng.set_posterior(*P.pack(posts))
+        if builder == 'device':
+            posts = _device_posts(eng, hist)
+        else:
+            posts = hist.posteriors()
+            eng.set_posterior(*P.pack(posts))
         seed, rnd = 77, 5
         res = eng.suggest(seed, C, round=rnd)
         rng = np.random.RandomState(3)
