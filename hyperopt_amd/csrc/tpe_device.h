@@ -18,6 +18,9 @@ namespace tpe {
 constexpr double kEps = 1e-12;  // tpe.py:31
 
 enum Mode : int { DENSE_GMM = 0, DENSE_LGMM = 1, QUANT_GMM = 2, QUANT_LGMM = 3, CAT = 4 };
+// kernel-template only (never a label's mode): one launch over the dense
+// GMM1 and LGMM1 labels together, the family read from each label
+constexpr int DENSE_ANY = 8;
 
 // One resident label, prepared on the host by tpe_set_posterior.
 struct DLabel {

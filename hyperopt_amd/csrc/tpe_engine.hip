@@ -185,7 +185,11 @@ __global__ __launch_bounds__(kBlock) void k_round(
     const int li = group[blockIdx.y];
     const DLabel L = labels[li];
     __shared__ double exp_tab[kExpTabSize];
-    if constexpr (MODE == DENSE_GMM || MODE == DENSE_LGMM) load_exp_table(exp_tab);
+    constexpr bool kDense = MODE == DENSE_GMM || MODE == DENSE_LGMM || MODE == DENSE_ANY;
+    if constexpr (kDense) load_exp_table(exp_tab);
+    // LGMM1 label? (compile-time, or per label -- uniform over the workgroup)
+    const bool lgmm = MODE == DENSE_LGMM || MODE == QUANT_LGMM ||
+                      (MODE == DENSE_ANY && L.mode == DENSE_LGMM);
 
     double x[R], lb[R], la[R];
     int64_t z[R], ci[R], gi[R];
@@ -194,12 +198,19 @@ __global__ __launch_bounds__(kBlock) void k_round(
     for (int r = 0; r < R; ++r) {
         S.template at<R>(r, n, z[r], ci[r], valid[r]);
         gi[r] = cand_offset + ci[r];
-        double v = (MODE == DENSE_LGMM || MODE == QUANT_LGMM) ? 1.0 : 0.0;
+        double v = lgmm ? 1.0 : 0.0;
         if (valid[r]) {
             if constexpr (SAMPLE) {
-                if (!sample_below<MODE>(L, samp + L.samp_off, seed, rounds[z[r]],
-                                        (uint32_t)gi[r], v))
-                    atomicOr(err, 1);
+                bool ok;
+                if constexpr (MODE == DENSE_ANY)
+                    ok = lgmm ? sample_below<DENSE_LGMM>(L, samp + L.samp_off, seed, rounds[z[r]],
+                                                         (uint32_t)gi[r], v)
+                              : sample_below<DENSE_GMM>(L, samp + L.samp_off, seed, rounds[z[r]],
+                                                        (uint32_t)gi[r], v);
+                else
+                    ok = sample_below<MODE>(L, samp + L.samp_off, seed, rounds[z[r]],
+                                            (uint32_t)gi[r], v);
+                if (!ok) atomicOr(err, 1);
             } else {
                 v = cand_in[ci[r]];
             }
@@ -207,19 +218,23 @@ __global__ __launch_bounds__(kBlock) void k_round(
         x[r] = v;
     }
 
-    if constexpr (MODE == DENSE_GMM) {
-        lse_dense<R>(comps + L.comp_b, L.nb, L.shift_b, L.centre, x, lb, exp_tab);
-        lse_dense<R>(comps + L.comp_a, L.na, L.shift_a, L.centre, x, la, exp_tab);
-    } else if constexpr (MODE == DENSE_LGMM) {
+    if constexpr (kDense) {
         double y[R];
+        if (lgmm) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) y[r] = log(x[r]);
+            for (int r = 0; r < R; ++r) y[r] = log(x[r]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) y[r] = x[r];
+        }
         lse_dense<R>(comps + L.comp_b, L.nb, L.shift_b, L.centre, y, lb, exp_tab);
         lse_dense<R>(comps + L.comp_a, L.na, L.shift_a, L.centre, y, la, exp_tab);
+        if (lgmm) {
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            lb[r] -= y[r];
-            la[r] -= y[r];
+            for (int r = 0; r < R; ++r) {
+                lb[r] -= y[r];
+                la[r] -= y[r];
+            }
         }
     } else if constexpr (MODE == QUANT_GMM || MODE == QUANT_LGMM) {
 #pragma unroll
@@ -762,6 +777,32 @@ void launch_round(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
     bracket(ctx, MODE, 1);
 }
 
+// Sampled rounds: the dense GMM1 and LGMM1 labels in ONE launch (their
+// groups are adjacent), so both families fill the chip together instead of
+// leaving each other's tail idle.  Timed and counted in the DENSE_GMM slot.
+template <typename T>
+void launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
+    const int nl = g.count[DENSE_GMM] + g.count[DENSE_LGMM];
+    if (nl == 0 || a.tiles == 0) return;
+    bracket(ctx, DENSE_GMM, 0);
+    const Comp<T>* comps;
+    if constexpr (sizeof(T) == 8) comps = ctx->P->comps64.p; else comps = ctx->P->comps32.p;
+    const int32_t* grp = ctx->P->groups.p + ctx->P->group_off[DENSE_GMM];
+    if (a.S.cpack && a.S.cpack <= kBlock * kRGroup)
+        hipLaunchKernelGGL((k_round<T, DENSE_ANY, true, kRGroup>), dim3(a.gx, nl, a.gz), dim3(kBlock),
+                           0, ctx->stream, ctx->P->labels.p, grp, comps, ctx->P->comps64.p,
+                           ctx->P->samp.p, a.cand_in, a.n, a.cand_offset, a.seed, ctx->rounds.p,
+                           ctx->P->n_labels, a.tiles, ctx->partials.p, a.olb, a.ola, ctx->errflag.p,
+                           a.S);
+    else
+        hipLaunchKernelGGL((k_round<T, DENSE_ANY, true, kR>), dim3(a.gx, nl, a.gz), dim3(kBlock), 0,
+                           ctx->stream, ctx->P->labels.p, grp, comps, ctx->P->comps64.p,
+                           ctx->P->samp.p, a.cand_in, a.n, a.cand_offset, a.seed, ctx->rounds.p,
+                           ctx->P->n_labels, a.tiles, ctx->partials.p, a.olb, a.ola, ctx->errflag.p,
+                           a.S);
+    bracket(ctx, DENSE_GMM, 1);
+}
+
 // Quantized families in a sampled round: qsample (both families) -> host
 // decides each label's table window -> qtable + qscan per family.
 int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t* evals_q) {
@@ -970,13 +1011,8 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     } else if (sample) {
         int rc = launch_quantized(ctx, g, a, evals_q);
         if (rc) return rc;
-        if (ctx->precision == TPE_F32) {
-            launch_round<float, DENSE_GMM, true>(ctx, g, a);
-            launch_round<float, DENSE_LGMM, true>(ctx, g, a);
-        } else {
-            launch_round<double, DENSE_GMM, true>(ctx, g, a);
-            launch_round<double, DENSE_LGMM, true>(ctx, g, a);
-        }
+        if (ctx->precision == TPE_F32) launch_dense<float>(ctx, g, a);
+        else launch_dense<double>(ctx, g, a);
         launch_round<double, CAT, true>(ctx, g, a);
     } else {
         launch_round<double, QUANT_GMM, false>(ctx, g, a);
@@ -1018,7 +1054,9 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         if (sample && (d.mode == QUANT_GMM || d.mode == QUANT_LGMM)) continue;  // counted below
         const int64_t e = ((d.mode == CAT) ? 2 * n : n * (int64_t)(d.nb + d.na)) * n_rounds;
         evals += e;
-        ctx->mode_evals[d.mode] += e;
+        // sampled tile / packed rounds time both dense families in one launch
+        const bool merged = sample && !splitk && d.mode == DENSE_LGMM;
+        ctx->mode_evals[merged ? DENSE_GMM : d.mode] += e;
     }
     ctx->mode_evals[QUANT_GMM] += evals_q[0];
     ctx->mode_evals[QUANT_LGMM] += evals_q[1];

@@ -206,7 +206,9 @@ class Engine(object):
     def last_evals(self):
         return int(self.lib.tpe_last_evals(self.h))
 
-    MODES = ('dense_gmm1', 'dense_lgmm1', 'quant_gmm1', 'quant_lgmm1', 'categorical')
+    # slot 0: dense GMM1 -- and, in sampled tile/packed rounds, the dense
+    # LGMM1 labels too (one merged launch; slot 1 then stays 0)
+    MODES = ('dense', 'dense_lgmm1', 'quant_gmm1', 'quant_lgmm1', 'categorical')
 
     def last_mode_stats(self):
         """{family: (device_ms, evals)} of the last round."""

@@ -266,7 +266,9 @@ int64_t tpe_last_evals(const tpe_ctx *ctx);
 
 /* Per kernel family of the last round (index: 0 dense GMM1, 1 dense LGMM1,
  * 2 quantized GMM1, 3 quantized LGMM1, 4 categorical): device ms of that
- * family's launch and the evaluations it executed.  Arrays of 5. */
+ * family's launch and the evaluations it executed.  Arrays of 5.  Sampled
+ * tile/packed rounds launch both dense families together: slot 0 then holds
+ * the GMM1 + LGMM1 launch and its evaluations, slot 1 stays 0. */
 int tpe_last_mode_stats(const tpe_ctx *ctx, float *ms, int64_t *evals);
 
 #ifdef __cplusplus

@@ -17,8 +17,9 @@ import shutil
 import sys
 from collections import defaultdict
 
-FAMILY = {'k_round<double, 0,': 'dense_gmm1', 'k_round<double, 1,': 'dense_lgmm1',
-          'k_round<float, 0,': 'dense_gmm1', 'k_round<float, 1,': 'dense_lgmm1'}
+FAMILY = {'k_round<double, 0,': 'dense', 'k_round<double, 1,': 'dense_lgmm1',
+          'k_round<float, 0,': 'dense', 'k_round<float, 1,': 'dense_lgmm1',
+          'k_round<double, 8,': 'dense', 'k_round<float, 8,': 'dense'}
 
 
 def short(name):
