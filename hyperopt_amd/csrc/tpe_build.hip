@@ -502,7 +502,7 @@ __global__ __launch_bounds__(kParzenBlock) void k_parzen(
     const double* __restrict__ keys_sorted, const int32_t* __restrict__ idx_sorted,
     const int64_t* __restrict__ mix_off, double prior_weight, int32_t lf, double* __restrict__ w,
     double* __restrict__ mu, double* __restrict__ sigma, int32_t* __restrict__ kcount,
-    int64_t* __restrict__ leaf_start, double* __restrict__ leaf_sum) {
+    double* __restrict__ leaf_sum) {
 #pragma clang fp contract(off)
     const int l = blockIdx.x, side = blockIdx.y, tid = threadIdx.x;
     const tpe_label_spec sp = specs[l];
@@ -668,7 +668,7 @@ __global__ __launch_bounds__(kParzenBlock) void k_fold(
     DLabel* __restrict__ labels, const int32_t* __restrict__ kcount,
     const int64_t* __restrict__ mix_off, const double* __restrict__ w, const double* __restrict__ mu,
     const double* __restrict__ sigma, Comp<double>* __restrict__ c64, Comp<float>* __restrict__ c32,
-    SampRec* __restrict__ samp, double* __restrict__ terms, int64_t* __restrict__ leaf_start,
+    SampRec* __restrict__ samp, double* __restrict__ terms,
     double* __restrict__ leaf_sum, int32_t* __restrict__ err) {
 #pragma clang fp contract(off)
     const int l = blockIdx.x, tid = threadIdx.x;
@@ -1008,7 +1008,6 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     HIPCHK(ctx, B.sigma.reserve(total));
     HIPCHK(ctx, B.mix_off.reserve(2 * (size_t)n_labels));
     HIPCHK(ctx, B.scratch.reserve(2 * (size_t)total));
-    HIPCHK(ctx, B.leaf.reserve(total));
     HIPCHK(ctx, P.labels.reserve(n_labels));
     HIPCHK(ctx, P.comps64.reserve(total));
     HIPCHK(ctx, P.comps32.reserve(total));
@@ -1027,11 +1026,10 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
                        B.below_val.p, B.arank.p, B.keys.p, B.idx.p, B.counts.p, ctx->errflag.p);
     hipLaunchKernelGGL(k_parzen, dim3(n_labels, 2), dim3(kParzenBlock), 0, st, B.specs.p, B.cat_p.p,
                        B.p_off.p, B.counts.p, B.below_val.p, B.keys.p, B.keys.p, B.idx.p, B.mix_off.p,
-                       prior_weight, lf, B.w.p, B.mu.p, B.sigma.p, B.kcount.p, B.leaf.p,
-                       B.scratch.p + total);
+                       prior_weight, lf, B.w.p, B.mu.p, B.sigma.p, B.kcount.p, B.scratch.p + total);
     hipLaunchKernelGGL(k_fold, dim3(n_labels), dim3(kParzenBlock), 0, st, P.labels.p, B.kcount.p,
                        B.mix_off.p, B.w.p, B.mu.p, B.sigma.p, P.comps64.p, P.comps32.p, P.samp.p,
-                       B.scratch.p, B.leaf.p, B.scratch.p + total, ctx->errflag.p);
+                       B.scratch.p, B.scratch.p + total, ctx->errflag.p);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(ctx->ev1, st));
     int32_t errh = 0;

@@ -105,7 +105,6 @@ struct BuildBufs {
     DevBuf<double> w, mu, sigma;   // the built mixtures (tpe_get_mixture)
     DevBuf<int64_t> mix_off;       // per label: below / above offsets into w/mu/sigma
     DevBuf<double> scratch;        // per-component terms | pairwise leaf sums
-    DevBuf<int64_t> leaf;
     int32_t n_labels = 0;          // labels of the last build (0: none resident)
     std::vector<int64_t> mix_h;    // host copy of mix_off
     void release() {
@@ -115,7 +114,7 @@ struct BuildBufs {
         st_idx_sorted.release(); st_val.release(); st_key_sorted.release(); seg_begin.release();
         seg_end.release(); sort_tmp.release(); losses.release(); below.release(); keys.release();
         idx.release(); below_val.release(); counts.release(); kcount.release(); w.release();
-        mu.release(); sigma.release(); mix_off.release(); scratch.release(); leaf.release();
+        mu.release(); sigma.release(); mix_off.release(); scratch.release();
         n_labels = 0;
         hist_ready = false;
         pool_cap = 0;
