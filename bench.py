@@ -61,6 +61,8 @@ def parse():
                          'new_ids x 24 candidates)')
     ap.add_argument('--rounds-per-gpu', type=int, default=512,
                     help='config 5: new_ids per GPU per step (4096 over 8 GPUs)')
+    ap.add_argument('--c5-history', type=int, default=50000,
+                    help='config 5 history size (50000 = BASELINE.json; smaller only for experiments)')
     ap.add_argument('--labels', type=int, default=32)
     ap.add_argument('--trials', type=int, default=10000)
     ap.add_argument('--cand-log2', type=int, default=21)
@@ -193,7 +195,7 @@ def main():
         args.labels, args.trials, args.cand_log2 = 6, 2000, 20
         hist = hartmann_history(args.trials, seed=0)
     elif args.config == 5:
-        args.labels, args.trials = 128, 50000
+        args.labels, args.trials = 128, args.c5_history
         hist = mixed_history(args.labels, args.trials, seed=0)
     else:
         hist = mixed_history(args.labels, args.trials, seed=0)
