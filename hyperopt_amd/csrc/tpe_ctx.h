@@ -166,6 +166,9 @@ struct tpe_ctx {
     DevBuf<double2> qtab;
     DevBuf<double> xs, slice_part;       // split-K map: candidates, slice sums
     bool splitk = true;                  // split-K for small sampled rounds
+    DevBuf<double> chunk_part;           // chunked packed map: x | below sum | above chunk sums
+    int32_t chunks_forced = 0;           // TPE_CHUNKS: 1 = off, > 1 = fixed, 0 = auto
+    bool pack_wide = false;              // TPE_PACK_WIDE: packed rounds over kR slots per thread
     tpe_rt::BuildBufs build;             // device posterior builder scratch
     int64_t built_n_trials = 0;          // last tpe_build_posterior: history size
     int32_t built_n_below = 0;           //   and its below-set size

@@ -227,16 +227,12 @@ __device__ __forceinline__ float lse_twopass(const Comp<float>* __restrict__ c, 
     return (__builtin_log2f(s) + m) * 0.69314718055994531f;  // back to natural log
 }
 
+// acc[r] += sum_{k < n} exp_scaled(-z_k^2 + c_k) for the recentred x[r]
 template <int R>
-__device__ __forceinline__ void lse_dense(const Comp<double>* __restrict__ c, int n, double shift,
-                                          double centre, const double (&xin)[R],
-                                          double (&out)[R], const double* __restrict__ tab) {
-    double acc[R], x[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        acc[r] = 0.0;
-        x[r] = xin[r] - centre;
-    }
+__device__ __forceinline__ void lse_acc(const Comp<double>* __restrict__ c, int n,
+                                        const double (&x)[R], double (&acc)[R],
+                                        const double* __restrict__ tab) {
+    if (n <= 0) return;
     if constexpr (R >= 4) {
 #pragma unroll 2
         for (int k = 0; k < n; ++k) {
@@ -248,42 +244,58 @@ __device__ __forceinline__ void lse_dense(const Comp<double>* __restrict__ c, in
             }
         }
     } else {
-        // few candidates per thread: software-pipelined batches of U records
-        // (the scalar loads of batch b+1 are issued before batch b is
-        // computed, so their latency hides behind U x R evaluations)
+        // few candidates per thread: scalar-loaded records, double-buffered
+        // in batches of U (A/B, no register copies).  Scalar and LDS loads
+        // share lgkmcnt and scalar loads return out of order, so the wait
+        // for a batch's exp-table reads also waits for every scalar load in
+        // flight: the next batch's loads are therefore issued right after
+        // the exponents of the current batch are formed (its first use of
+        // its records) and ~10 VALU per evaluation before that wait.
         constexpr int U = R == 2 ? 4 : 8;
-        const int nfull = n - n % U;
-        double bm[U], ba[U], bc[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int k = u < n ? u : n - 1;
-            bm[u] = c[k].mu;
-            ba[u] = c[k].a;
-            bc[u] = c[k].c;
-        }
-        for (int k0 = 0; k0 < nfull; k0 += U) {
-            double nm[U], na[U], nc[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {   // next batch (clamped, no branch)
-                const int k = min(k0 + U + u, n - 1);
-                nm[u] = c[k].mu;
-                na[u] = c[k].a;
-                nc[u] = c[k].c;
-            }
+        const int nbat = n / U, nfull = nbat * U;
+        double Am[U], Aa[U], Ac[U], Bm[U], Ba[U], Bc[U], t[U][R];
+        // batch at record k0; a prefetch past the last full batch re-reads it
+        auto load = [&](double (&m)[U], double (&a)[U], double (&cc)[U], int k0) {
+            const Comp<double>* p = c + min(k0, nfull - U);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
+                m[u] = p[u].mu;
+                a[u] = p[u].a;
+                cc[u] = p[u].c;
+            }
+        };
+        auto expo = [&](const double (&m)[U], const double (&a)[U], const double (&cc)[U]) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
-                    const double z = fma(x[r], ba[u], -bm[u]);
-                    acc[r] = exp_scaled_acc(fma(-z, z, bc[u]), tab, acc[r]);
+                    const double z = fma(x[r], a[u], -m[u]);
+                    t[u][r] = fma(-z, z, cc[u]);
                 }
-            }
+        };
+        auto accum = [&]() {
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                bm[u] = nm[u];
-                ba[u] = na[u];
-                bc[u] = nc[u];
-            }
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int r = 0; r < R; ++r) acc[r] = exp_scaled_acc(t[u][r], tab, acc[r]);
+        };
+        if (nbat > 0) load(Am, Aa, Ac, 0);
+        int b = 0;
+        for (; b + 2 <= nbat; b += 2) {
+            expo(Am, Aa, Ac);
+            __builtin_amdgcn_sched_barrier(0);
+            load(Bm, Ba, Bc, (b + 1) * U);
+            __builtin_amdgcn_sched_barrier(0);
+            accum();
+            expo(Bm, Ba, Bc);
+            __builtin_amdgcn_sched_barrier(0);
+            load(Am, Aa, Ac, (b + 2) * U);
+            __builtin_amdgcn_sched_barrier(0);
+            accum();
+        }
+        if (b < nbat) {
+            expo(Am, Aa, Ac);
+            accum();
         }
         for (int k = nfull; k < n; ++k) {
             const double m = c[k].mu, a = c[k].a, cc = c[k].c;
@@ -294,12 +306,29 @@ __device__ __forceinline__ void lse_dense(const Comp<double>* __restrict__ c, in
             }
         }
     }
+}
+
+// log(acc) + shift, or the two-pass form when the sum underflowed / is NaN
+__device__ __forceinline__ double lse_finish(const Comp<double>* __restrict__ c, int n, double acc,
+                                             double xr, double shift) {
+    double v = log(acc);
+    if (!(acc >= 1e-290)) v = lse_twopass(c, n, xr);  // rare: underflow / NaN
+    return v + shift;
+}
+
+template <int R>
+__device__ __forceinline__ void lse_dense(const Comp<double>* __restrict__ c, int n, double shift,
+                                          double centre, const double (&xin)[R],
+                                          double (&out)[R], const double* __restrict__ tab) {
+    double acc[R], x[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        double v = log(acc[r]);
-        if (!(acc[r] >= 1e-290)) v = lse_twopass(c, n, x[r]);  // rare: underflow / NaN
-        out[r] = v + shift;
+        acc[r] = 0.0;
+        x[r] = xin[r] - centre;
     }
+    lse_acc<R>(c, n, x, acc, tab);
+#pragma unroll
+    for (int r = 0; r < R; ++r) out[r] = lse_finish(c, n, acc[r], x[r], shift);
 }
 
 // fp32 fast path: constants pre-scaled by log2(e) so the hardware v_exp_f32
@@ -310,9 +339,8 @@ __device__ __forceinline__ void lse_dense(const Comp<double>* __restrict__ c, in
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int R>
-__device__ __forceinline__ void lse_dense(const Comp<float>* __restrict__ c, int n, double shift,
-                                          double, const double (&xd)[R], double (&out)[R],
-                                          const double* __restrict__) {
+__device__ __forceinline__ void lse_acc(const Comp<float>* __restrict__ c, int n,
+                                        const double (&xd)[R], float (&out)[R]) {
     if constexpr (R % 2 == 0) {
         constexpr int P = R / 2;
         f32x2 x[P], acc[P];
@@ -333,37 +361,42 @@ __device__ __forceinline__ void lse_dense(const Comp<float>* __restrict__ c, int
         }
 #pragma unroll
         for (int p = 0; p < P; ++p) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const float s = h ? acc[p].y : acc[p].x;
-                const float xv = h ? x[p].y : x[p].x;
-                float v = __builtin_log2f(s) * 0.69314718055994531f;
-                if (!(s >= 1e-30f)) v = lse_twopass(c, n, xv);
-                out[2 * p + h] = (double)v + shift;
-            }
+            out[2 * p] = acc[p].x;
+            out[2 * p + 1] = acc[p].y;
         }
     } else {
-        float x[R], acc[R];
+        float x[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             x[r] = (float)xd[r];
-            acc[r] = 0.0f;
+            out[r] = 0.0f;
         }
         for (int k = 0; k < n; ++k) {
             const float mu = c[k].mu, a = c[k].a, cc = c[k].c;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const float z = (x[r] - mu) * a;
-                acc[r] += __builtin_amdgcn_exp2f(fmaf(-z, z, cc));
+                out[r] += __builtin_amdgcn_exp2f(fmaf(-z, z, cc));
             }
         }
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            float v = __builtin_log2f(acc[r]) * 0.69314718055994531f;
-            if (!(acc[r] >= 1e-30f)) v = lse_twopass(c, n, x[r]);
-            out[r] = (double)v + shift;
-        }
     }
+}
+
+__device__ __forceinline__ double lse_finish(const Comp<float>* __restrict__ c, int n, float acc,
+                                             float x, double shift) {
+    float v = __builtin_log2f(acc) * 0.69314718055994531f;
+    if (!(acc >= 1e-30f)) v = lse_twopass(c, n, x);
+    return (double)v + shift;
+}
+
+template <int R>
+__device__ __forceinline__ void lse_dense(const Comp<float>* __restrict__ c, int n, double shift,
+                                          double, const double (&xd)[R], double (&out)[R],
+                                          const double* __restrict__) {
+    float acc[R];
+    lse_acc<R>(c, n, xd, acc);
+#pragma unroll
+    for (int r = 0; r < R; ++r) out[r] = lse_finish(c, n, acc[r], (float)xd[r], shift);
 }
 
 // ------------------------------------------------------- quantized mass ----

@@ -105,6 +105,12 @@ struct Slots {
     }
 };
 
+// packed map with kRGroup slots per thread (else kR: tile map, or packed
+// rounds spread over kR * 256 slots)
+__host__ __device__ inline bool narrow(const Slots& S) {
+    return S.cpack != 0 && (int64_t)S.rpb * S.cpack <= kBlock * kRGroup;
+}
+
 // broadcast_best epilogue for either map: block maxloc into the tile's
 // partial, or, packed, one winner per round: every slot posts its key to
 // LDS, a reducer per round picks the best slot (slots of a round are in
@@ -174,26 +180,17 @@ __device__ __forceinline__ void finish_slots(const Slots& S, const double (&x)[R
 
 // --------------------------------------------------------------- kernels ----
 
-template <typename T, int MODE, bool SAMPLE, int R>
-__global__ __launch_bounds__(kBlock) void k_round(
-    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
-    const Comp<T>* __restrict__ comps, const Comp<double>* __restrict__ comps64,
-    const SampRec* __restrict__ samp, const double* __restrict__ cand_in, int64_t n,
-    int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, int32_t n_labels,
-    int32_t tiles, Partial* __restrict__ partials, double* __restrict__ out_lb,
-    double* __restrict__ out_la, int32_t* __restrict__ err, Slots S) {
-    const int li = group[blockIdx.y];
-    const DLabel L = labels[li];
-    __shared__ double exp_tab[kExpTabSize];
-    constexpr bool kDense = MODE == DENSE_GMM || MODE == DENSE_LGMM || MODE == DENSE_ANY;
-    if constexpr (kDense) load_exp_table(exp_tab);
-    // LGMM1 label? (compile-time, or per label -- uniform over the workgroup)
-    const bool lgmm = MODE == DENSE_LGMM || MODE == QUANT_LGMM ||
-                      (MODE == DENSE_ANY && L.mode == DENSE_LGMM);
-
-    double x[R], lb[R], la[R];
-    int64_t z[R], ci[R], gi[R];
-    bool valid[R];
+// The candidates of a thread's R slots: drawn from the below mixture (the
+// label's Philox stream, round key, candidate index) or read from cand_in.
+template <int MODE, bool SAMPLE, int R>
+__device__ __forceinline__ void draw_slots(const DLabel& L, const Slots& S, bool lgmm,
+                                           const SampRec* __restrict__ samp,
+                                           const double* __restrict__ cand_in, int64_t n,
+                                           int64_t cand_offset, uint64_t seed,
+                                           const uint32_t* __restrict__ rounds,
+                                           int32_t* __restrict__ err, double (&x)[R],
+                                           int64_t (&z)[R], int64_t (&ci)[R], int64_t (&gi)[R],
+                                           bool (&valid)[R]) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         S.template at<R>(r, n, z[r], ci[r], valid[r]);
@@ -217,6 +214,30 @@ __global__ __launch_bounds__(kBlock) void k_round(
         }
         x[r] = v;
     }
+}
+
+template <typename T, int MODE, bool SAMPLE, int R>
+__global__ __launch_bounds__(kBlock) void k_round(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<T>* __restrict__ comps, const Comp<double>* __restrict__ comps64,
+    const SampRec* __restrict__ samp, const double* __restrict__ cand_in, int64_t n,
+    int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, int32_t n_labels,
+    int32_t tiles, Partial* __restrict__ partials, double* __restrict__ out_lb,
+    double* __restrict__ out_la, int32_t* __restrict__ err, Slots S) {
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    __shared__ double exp_tab[kExpTabSize];
+    constexpr bool kDense = MODE == DENSE_GMM || MODE == DENSE_LGMM || MODE == DENSE_ANY;
+    if constexpr (kDense) load_exp_table(exp_tab);
+    // LGMM1 label? (compile-time, or per label -- uniform over the workgroup)
+    const bool lgmm = MODE == DENSE_LGMM || MODE == QUANT_LGMM ||
+                      (MODE == DENSE_ANY && L.mode == DENSE_LGMM);
+
+    double x[R], lb[R], la[R];
+    int64_t z[R], ci[R], gi[R];
+    bool valid[R];
+    draw_slots<MODE, SAMPLE, R>(L, S, lgmm, samp, cand_in, n, cand_offset, seed, rounds, err, x, z,
+                                ci, gi, valid);
 
     if constexpr (kDense) {
         double y[R];
@@ -268,6 +289,122 @@ __global__ __launch_bounds__(kBlock) void k_round(
     }
     __shared__ Partial sh[kBlock / 64];
     finish_slots<R>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials, exp_tab, sh);
+}
+
+// ------------------------------------------------- chunked packed map ----
+// Batched sampled rounds with small C (e.g. 512 new_ids x 24 candidates)
+// give the packed map only gx * labels workgroups -- for config 5 that is
+// 512, two waves per SIMD, too few to hide the LDS / scalar-load latency of
+// the dense loop.  The above mixture's components are then cut into `nch`
+// chunks along grid.z: each workgroup draws the same slots (Philox is
+// stateless), sums its chunk relative to the label's LSE shift (chunk 0 also
+// the below mixture) and stores the raw sums; k_finish_chunks adds the
+// chunks in order, takes the logs and does the per-round maxloc.
+//
+// part layout per (label position y, plane p, workgroup x): R * 256 slots,
+// planes 0 = candidate, 1 = below sum, 2 + c = above sum of chunk c.
+__device__ __forceinline__ size_t chunk_plane(int y, int p, int nch, int x, int gx, int R) {
+    return (((size_t)y * (nch + 2) + p) * gx + x) * (size_t)(R * kBlock);
+}
+
+template <typename T, int R>
+__global__ __launch_bounds__(kBlock) void k_round_chunk(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<T>* __restrict__ comps, const SampRec* __restrict__ samp, int64_t n,
+    int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, int32_t chunk,
+    double* __restrict__ part, int32_t* __restrict__ err, Slots S) {
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    constexpr bool kTab = sizeof(T) == 8;
+    __shared__ double exp_tab[kTab ? kExpTabSize : 1];
+    if constexpr (kTab) load_exp_table(exp_tab);
+    const bool lgmm = L.mode == DENSE_LGMM;
+    const int nch = gridDim.z, c = blockIdx.z;
+    double x[R], y[R];
+    int64_t z[R], ci[R], gi[R];
+    bool valid[R];
+    draw_slots<DENSE_ANY, true, R>(L, S, lgmm, samp, nullptr, n, cand_offset, seed, rounds, err, x,
+                                   z, ci, gi, valid);
+#pragma unroll
+    for (int r = 0; r < R; ++r) y[r] = lgmm ? log(x[r]) : x[r];
+    const int k0 = min(c * chunk, L.na), k1 = min(k0 + chunk, L.na);
+    double sb[R], sa[R];
+    if constexpr (kTab) {
+        double xr[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            xr[r] = y[r] - L.centre;
+            sb[r] = 0.0;
+            sa[r] = 0.0;
+        }
+        if (c == 0) lse_acc<R>(comps + L.comp_b, L.nb, xr, sb, exp_tab);
+        lse_acc<R>(comps + L.comp_a + k0, k1 - k0, xr, sa, exp_tab);
+    } else {
+        float fb[R], fa[R];
+        if (c == 0) lse_acc<R>(comps + L.comp_b, L.nb, y, fb);
+        lse_acc<R>(comps + L.comp_a + k0, k1 - k0, y, fa);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            sb[r] = c == 0 ? (double)fb[r] : 0.0;
+            sa[r] = (double)fa[r];
+        }
+    }
+    const int gx = gridDim.x, bx = blockIdx.x, by = blockIdx.y;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int s = r * kBlock + threadIdx.x;
+        if (c == 0) {
+            part[chunk_plane(by, 0, nch, bx, gx, R) + s] = x[r];
+            part[chunk_plane(by, 1, nch, bx, gx, R) + s] = sb[r];
+        }
+        part[chunk_plane(by, 2 + c, nch, bx, gx, R) + s] = sa[r];
+    }
+}
+
+template <typename T, int R>
+__global__ __launch_bounds__(kBlock) void k_finish_chunks(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<T>* __restrict__ comps, int64_t n, int64_t cand_offset, int32_t n_labels,
+    int32_t tiles, int32_t nch, const double* __restrict__ part, Partial* __restrict__ partials,
+    double* __restrict__ out_lb, double* __restrict__ out_la, Slots S) {
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    const bool lgmm = L.mode == DENSE_LGMM;
+    const int gx = gridDim.x, bx = blockIdx.x, by = blockIdx.y;
+    double x[R], lb[R], la[R];
+    int64_t z[R], gi[R];
+    bool valid[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        int64_t ci;
+        S.template at<R>(r, n, z[r], ci, valid[r]);
+        gi[r] = cand_offset + ci;
+        const int s = r * kBlock + threadIdx.x;
+        x[r] = part[chunk_plane(by, 0, nch, bx, gx, R) + s];
+        const double sb = part[chunk_plane(by, 1, nch, bx, gx, R) + s];
+        double sa = 0.0;
+        for (int c = 0; c < nch; ++c) sa += part[chunk_plane(by, 2 + c, nch, bx, gx, R) + s];
+        const double y = lgmm ? log(x[r]) : x[r];
+        if constexpr (sizeof(T) == 8) {
+            lb[r] = lse_finish(comps + L.comp_b, L.nb, sb, y - L.centre, L.shift_b);
+            la[r] = lse_finish(comps + L.comp_a, L.na, sa, y - L.centre, L.shift_a);
+        } else {
+            lb[r] = lse_finish(comps + L.comp_b, L.nb, (float)sb, (float)y, L.shift_b);
+            la[r] = lse_finish(comps + L.comp_a, L.na, (float)sa, (float)y, L.shift_a);
+        }
+        if (lgmm) {
+            lb[r] -= y;
+            la[r] -= y;
+        }
+        if (out_lb && valid[r]) {
+            const size_t row = ((size_t)z[r] * n_labels + li) * (size_t)n;
+            out_lb[row + ci] = lb[r];
+            out_la[row + ci] = la[r];
+        }
+    }
+    __shared__ uint64_t scratch[R * kBlock * 3 / 2];   // finish_slots: keys + winners
+    __shared__ Partial sh[kBlock / 64];
+    finish_slots<R>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials, scratch, sh);
 }
 
 // ------------------------------------------------------- split-K map ----
@@ -762,7 +899,7 @@ void launch_round(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
     bracket(ctx, MODE, 0);
     const Comp<T>* comps;
     if constexpr (sizeof(T) == 8) comps = ctx->P->comps64.p; else comps = ctx->P->comps32.p;
-    if (a.S.cpack && a.S.cpack <= kBlock * kRGroup)
+    if (narrow(a.S))
         hipLaunchKernelGGL((k_round<T, MODE, SAMPLE, kRGroup>), dim3(a.gx, nl, a.gz), dim3(kBlock),
                            0, ctx->stream, ctx->P->labels.p, g.dev[MODE], comps, ctx->P->comps64.p,
                            ctx->P->samp.p, a.cand_in, a.n, a.cand_offset, a.seed, ctx->rounds.p,
@@ -777,18 +914,59 @@ void launch_round(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
     bracket(ctx, MODE, 1);
 }
 
+// Chunks of the above mixtures for a packed sampled round: enough
+// workgroups for ~6-8 generations of the 1280 resident ones (5 per CU: the
+// 32 KB exp table is k_round_chunk's only LDS), so the tail is short; no
+// chunk shorter than kMinChunk components, where the redundant sampling of
+// every chunk would start to show.  Config 5 (512 workgroups): 16 chunks,
+// 72% -> 87% of the VALU issue rate (measured sweep 1..32 in DESIGN.md).
+constexpr int64_t kChunkTargetWG = 8192;
+constexpr int32_t kMinChunk = 2048;
+
+int dense_chunks(const tpe_ctx* ctx, uint32_t gx, int nl) {
+    if (ctx->chunks_forced) return ctx->chunks_forced;
+    int32_t na_max = 0;
+    for (int m : {DENSE_GMM, DENSE_LGMM})
+        for (int li : ctx->P->h_group[m]) na_max = std::max(na_max, ctx->P->h_labels[li].na);
+    const int64_t wg = (int64_t)gx * nl;
+    if (wg >= kChunkTargetWG / 2) return 1;
+    const int64_t want = (kChunkTargetWG + wg - 1) / wg;
+    return (int)std::max<int64_t>(1, std::min<int64_t>(want, na_max / kMinChunk));
+}
+
 // Sampled rounds: the dense GMM1 and LGMM1 labels in ONE launch (their
 // groups are adjacent), so both families fill the chip together instead of
 // leaving each other's tail idle.  Timed and counted in the DENSE_GMM slot.
 template <typename T>
-void launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
+int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
     const int nl = g.count[DENSE_GMM] + g.count[DENSE_LGMM];
-    if (nl == 0 || a.tiles == 0) return;
+    if (nl == 0 || a.tiles == 0) return TPE_OK;
     bracket(ctx, DENSE_GMM, 0);
     const Comp<T>* comps;
     if constexpr (sizeof(T) == 8) comps = ctx->P->comps64.p; else comps = ctx->P->comps32.p;
     const int32_t* grp = ctx->P->groups.p + ctx->P->group_off[DENSE_GMM];
-    if (a.S.cpack && a.S.cpack <= kBlock * kRGroup)
+    const int nch = a.S.cpack ? dense_chunks(ctx, a.gx, nl) : 1;
+    if (nch > 1) {
+        int32_t na_max = 1;
+        for (int m : {DENSE_GMM, DENSE_LGMM})
+            for (int li : ctx->P->h_group[m]) na_max = std::max(na_max, ctx->P->h_labels[li].na);
+        const int32_t chunk = (na_max + nch - 1) / nch;
+        const size_t planes = (size_t)nl * (nch + 2) * a.gx * (kR * kBlock);
+        HIPCHK(ctx, ctx->chunk_part.reserve(planes));
+#define TPE_CHUNKED(RR)                                                                          \
+    hipLaunchKernelGGL((k_round_chunk<T, RR>), dim3(a.gx, nl, nch), dim3(kBlock), 0, ctx->stream, \
+                       ctx->P->labels.p, grp, comps, ctx->P->samp.p, a.n, a.cand_offset, a.seed,    \
+                       ctx->rounds.p, chunk, ctx->chunk_part.p, ctx->errflag.p, a.S);              \
+    hipLaunchKernelGGL((k_finish_chunks<T, RR>), dim3(a.gx, nl), dim3(kBlock), 0, ctx->stream,   \
+                       ctx->P->labels.p, grp, comps, a.n, a.cand_offset, ctx->P->n_labels, a.tiles, \
+                       nch, ctx->chunk_part.p, ctx->partials.p, a.olb, a.ola, a.S)
+        if (narrow(a.S)) {
+            TPE_CHUNKED(kRGroup);
+        } else {
+            TPE_CHUNKED(kR);
+        }
+#undef TPE_CHUNKED
+    } else if (narrow(a.S))
         hipLaunchKernelGGL((k_round<T, DENSE_ANY, true, kRGroup>), dim3(a.gx, nl, a.gz), dim3(kBlock),
                            0, ctx->stream, ctx->P->labels.p, grp, comps, ctx->P->comps64.p,
                            ctx->P->samp.p, a.cand_in, a.n, a.cand_offset, a.seed, ctx->rounds.p,
@@ -801,6 +979,7 @@ void launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                            ctx->P->n_labels, a.tiles, ctx->partials.p, a.olb, a.ola, ctx->errflag.p,
                            a.S);
     bracket(ctx, DENSE_GMM, 1);
+    return TPE_OK;
 }
 
 // Quantized families in a sampled round: qsample (both families) -> host
@@ -826,11 +1005,11 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
                        ctx->rounds.p, nq, BASE, ctx->qj.p, ctx->qmm.p, ctx->qmm.p + nq,        \
                        ctx->errflag.p, a.S)
     if (nqg) {
-        if (a.S.cpack && a.S.cpack <= kBlock * kRGroup) TPE_QSAMPLE(QUANT_GMM, nqg, 0, kRGroup);
+        if (narrow(a.S)) TPE_QSAMPLE(QUANT_GMM, nqg, 0, kRGroup);
         else TPE_QSAMPLE(QUANT_GMM, nqg, 0, kR);
     }
     if (nql) {
-        if (a.S.cpack && a.S.cpack <= kBlock * kRGroup) TPE_QSAMPLE(QUANT_LGMM, nql, nqg, kRGroup);
+        if (narrow(a.S)) TPE_QSAMPLE(QUANT_LGMM, nql, nqg, kRGroup);
         else TPE_QSAMPLE(QUANT_LGMM, nql, nqg, kR);
     }
 #undef TPE_QSAMPLE
@@ -883,10 +1062,10 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
                        g.dev[mode], ctx->P->comps64.p, ctx->qj.p, ctx->qinfo.p, ctx->qtab.p, a.n, \
                        a.cand_offset, nq, qbase, ctx->P->n_labels, a.tiles, ctx->partials.p, a.S)
         if (fam) {
-            if (a.S.cpack && a.S.cpack <= kBlock * kRGroup) TPE_QSCAN(QUANT_LGMM, kRGroup);
+            if (narrow(a.S)) TPE_QSCAN(QUANT_LGMM, kRGroup);
             else TPE_QSCAN(QUANT_LGMM, kR);
         } else {
-            if (a.S.cpack && a.S.cpack <= kBlock * kRGroup) TPE_QSCAN(QUANT_GMM, kRGroup);
+            if (narrow(a.S)) TPE_QSCAN(QUANT_GMM, kRGroup);
             else TPE_QSCAN(QUANT_GMM, kR);
         }
 #undef TPE_QSCAN
@@ -943,7 +1122,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     int32_t tiles;
     uint32_t gx, gz;
     if (n > 0 && n < kTile) {
-        const int per_block = n <= kBlock * kRGroup ? kBlock * kRGroup : kTile;
+        const int per_block = (n <= kBlock * kRGroup && !ctx->pack_wide) ? kBlock * kRGroup : kTile;
         S.cpack = (int32_t)n;
         S.rpb = per_block / (int32_t)n;
         tiles = 1;
@@ -1011,8 +1190,8 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     } else if (sample) {
         int rc = launch_quantized(ctx, g, a, evals_q);
         if (rc) return rc;
-        if (ctx->precision == TPE_F32) launch_dense<float>(ctx, g, a);
-        else launch_dense<double>(ctx, g, a);
+        rc = ctx->precision == TPE_F32 ? launch_dense<float>(ctx, g, a) : launch_dense<double>(ctx, g, a);
+        if (rc) return rc;
         launch_round<double, CAT, true>(ctx, g, a);
     } else {
         launch_round<double, QUANT_GMM, false>(ctx, g, a);
@@ -1258,6 +1437,10 @@ int tpe_ctx_create(int device, int precision, tpe_ctx** out) {
     c->dedup = !(dd && dd[0] == '1');
     const char* sk = getenv("TPE_NO_SPLITK");   // tests: force the packed map
     c->splitk = !(sk && sk[0] == '1');
+    const char* ch = getenv("TPE_CHUNKS");      // tests / experiments: chunking of the packed map
+    c->chunks_forced = ch ? std::max(1, atoi(ch)) : 0;
+    const char* pw = getenv("TPE_PACK_WIDE");   // experiments: kR slots per thread when packed
+    c->pack_wide = pw && pw[0] == '1';
     *out = c;
     return TPE_OK;
 }

@@ -364,3 +364,72 @@ def test_single_ops_leave_resident_posterior(eng):
     eng.categorical(np.array([0.3, 0.7]), seed=2, size=(8,))
     after = eng.suggest(5, 4096, round=1)
     assert np.array_equal(before, after)
+
+
+def _chunk_engine(monkeypatch, prec, chunks, hist):
+    from hyperopt_amd.engine import Engine
+    if chunks is None:
+        monkeypatch.delenv('TPE_CHUNKS', raising=False)
+    else:
+        monkeypatch.setenv('TPE_CHUNKS', str(chunks))
+    e = Engine(0, prec)
+    e.build_posterior(*hist.device_inputs(), gamma=0.25, prior_weight=1.0)
+    return e
+
+
+@pytest.mark.parametrize('prec,C,n_rounds', [('f64', 24, 300), ('f32', 24, 300), ('f64', 700, 12)])
+def test_chunked_packed_map(monkeypatch, prec, C, n_rounds):
+    """Batched small rounds over long above mixtures (the config-5 shape,
+    scaled down): the packed map cuts each above mixture into chunks along
+    grid.z (k_round_chunk) and adds them in order (k_finish_chunks).  Forced
+    chunk counts, the automatic choice and the unchunked map give the same
+    winners and lpdfs up to the summation order; the f64 winners equal the
+    oracle's argmax on the re-drawn candidates."""
+    from hyperopt_amd.workloads import mixed_history
+    hist = mixed_history(10, 6000, seed=5)
+    # C = 24: 7200 slots per label, the narrow packed map (2 slots per
+    # thread), not split-K; C = 700: one round per workgroup, 4 slots per thread
+    rounds = list(range(n_rounds))
+    seed = 4242
+    res = {}
+    for ch in (1, 3, 7, None):
+        e = _chunk_engine(monkeypatch, prec, ch, hist)
+        try:
+            res[ch] = e.suggest_batch(seed, rounds, C)
+            if ch is None and prec == 'f64':
+                mix = {li: e.get_mixture(li, 0) for li in range(len(hist.labels))}
+                a_mix = {li: e.get_mixture(li, 1) for li in range(len(hist.labels))}
+                draws = {}
+                for li, (name, kind, args) in enumerate(hist.labels):
+                    if kind not in ('uniform', 'loguniform', 'normal'):
+                        continue
+                    samp = e.LGMM1 if kind == 'loguniform' else e.GMM1
+                    for rnd in (0, n_rounds // 2, n_rounds - 1):
+                        draws[li, rnd] = samp(*mix[li], low=args.get('low'), high=args.get('high'),
+                                              seed=seed, size=(C,), stream=li, round=rnd)
+        finally:
+            e.close()
+    base = res[1]
+    tol = 1e-12 if prec == 'f64' else 2e-5
+    for ch in (3, 7, None):
+        r = res[ch]
+        same = r['index'] == base['index']
+        if prec == 'f64':
+            assert same.all(), ch
+        else:                            # fp32 sums in another order may flip near-ties
+            assert same.mean() > 0.99, (ch, same.mean())
+        for f in ('lpdf_below', 'lpdf_above'):
+            np.testing.assert_allclose(r[f][same], base[f][same], rtol=tol, atol=tol)
+    if prec != 'f64':
+        return
+    r = res[None]
+    for (li, rnd), cand in draws.items():
+        name, kind, args = hist.labels[li]
+        f = O.lgmm1_lpdf if kind == 'loguniform' else O.gmm1_lpdf
+        kw = dict(low=args.get('low'), high=args.get('high'))
+        lb = f(cand, *mix[li], **kw)
+        la = f(cand, *a_mix[li], **kw)
+        best = O.broadcast_best_index(lb, la)
+        assert int(r[rnd, li]['index']) == best, (name, rnd)
+        assert r[rnd, li]['value'] == cand[best]
+        np.testing.assert_allclose(r[rnd, li]['lpdf_above'], la[best], rtol=1e-9, atol=1e-9)
