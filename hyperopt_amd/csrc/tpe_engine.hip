@@ -11,13 +11,19 @@
 //   results  : tpe_label_result[rounds][L]
 //   qj       : int64[rounds][Lq][C]       grid index of every quantized candidate
 //   qtab     : double2[sum G]             lpdf pair per distinct grid value
+//   chunk_part: double[labels][chunks + 2][gx][R * 256]  chunked packed map sums
 // Kernels
 //   k_round<T, MODE, SAMPLE>  sample -> lpdf under l and g -> block maxloc
 //                             (dense families, categorical, supplied candidates)
+//   k_round_chunk / k_finish_chunks
+//                             packed rounds with the above mixture cut into
+//                             chunks along grid.z, then in-order sum -> maxloc
+//   k_sample_small / k_score_slices / k_finish_slices
+//                             split-K map of small rounds (C * rounds <= 2048)
 //   k_qsample<MODE>           quantized families: draw, store grid index j, min/max
 //   k_qtable<MODE>            one wave per distinct grid value: lpdf pair
 //   k_qscan<MODE>             per candidate: table lookup -> block maxloc
-//   k_reduce                  per (round, label) winner over the partials
+//   k_reduce / k_emit         per (round, label) winner over the partials
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -703,6 +709,18 @@ __global__ __launch_bounds__(kBlock) void k_qscan(
     finish_slots<R>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials, scratch, sh);
 }
 
+__device__ __forceinline__ tpe_label_result to_result(const Partial& p, int li) {
+    tpe_label_result r;
+    r.value = p.value;
+    r.score = p.lb - p.la;
+    r.lpdf_below = p.lb;
+    r.lpdf_above = p.la;
+    r.index = p.idx != INT64_MAX ? p.idx : -1;
+    r.label = li;
+    r.status = 0;
+    return r;
+}
+
 __global__ __launch_bounds__(kBlock) void k_reduce(const Partial* __restrict__ partials,
                                                    int32_t tiles, int32_t n_labels,
                                                    tpe_label_result* __restrict__ out) {
@@ -715,18 +733,15 @@ __global__ __launch_bounds__(kBlock) void k_reduce(const Partial* __restrict__ p
     __shared__ Partial sh[kBlock / 64];
     block_maxloc(best.key, best.idx, best.value, best.lb, best.la, &res, sh);
     __syncthreads();
-    if (tid == 0) {
-        tpe_label_result r;
-        const bool any = res.idx != INT64_MAX;
-        r.value = res.value;
-        r.score = res.lb - res.la;
-        r.lpdf_below = res.lb;
-        r.lpdf_above = res.la;
-        r.index = any ? res.idx : -1;
-        r.label = li;
-        r.status = 0;
-        out[(size_t)rz * n_labels + li] = r;
-    }
+    if (tid == 0) out[(size_t)rz * n_labels + li] = to_result(res, li);
+}
+
+// one partial per (round, label) -- packed and split-K maps: a thread each
+__global__ __launch_bounds__(kBlock) void k_emit(const Partial* __restrict__ partials, int64_t n,
+                                                 int32_t n_labels,
+                                                 tpe_label_result* __restrict__ out) {
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j < n) out[j] = to_result(partials[j], (int)(j % n_labels));
 }
 
 // argmax of below - above over caller arrays (tpe_broadcast_best)
@@ -1207,7 +1222,12 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     }
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(ctx->ev1, ctx->stream));
-    if (tiles > 0) {
+    if (tiles == 1) {
+        const int64_t nr = (int64_t)n_rounds * L;
+        hipLaunchKernelGGL(k_emit, dim3((unsigned)((nr + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                           ctx->stream, ctx->partials.p, nr, L, ctx->results.p);
+        HIPCHK(ctx, hipGetLastError());
+    } else if (tiles > 1) {
         hipLaunchKernelGGL(k_reduce, dim3(L, n_rounds), dim3(kBlock), 0, ctx->stream,
                            ctx->partials.p, tiles, L, ctx->results.p);
         HIPCHK(ctx, hipGetLastError());
