@@ -227,83 +227,73 @@ __device__ __forceinline__ float lse_twopass(const Comp<float>* __restrict__ c, 
     return (__builtin_log2f(s) + m) * 0.69314718055994531f;  // back to natural log
 }
 
-// acc[r] += sum_{k < n} exp_scaled(-z_k^2 + c_k) for the recentred x[r]
+// acc[r] += sum_{k < n} exp_scaled(-z_k^2 + c_k) for the recentred x[r].
+//
+// The records are wave-uniform and come through the scalar cache,
+// double-buffered in batches of U (A/B, no register copies).  Scalar and LDS
+// loads share lgkmcnt and scalar loads return out of order, so the wait for
+// a batch's exp-table reads also waits for every scalar load in flight: the
+// next batch's loads are issued right after the current batch's exponents
+// are formed (its first use of its records), ~10 VALU per evaluation before
+// that wait.  The plain loop issued them just before it (config 3: 97 ->
+// 98 % of the issue rate; config 5: +25 %).
 template <int R>
 __device__ __forceinline__ void lse_acc(const Comp<double>* __restrict__ c, int n,
                                         const double (&x)[R], double (&acc)[R],
                                         const double* __restrict__ tab) {
     if (n <= 0) return;
-    if constexpr (R >= 4) {
-#pragma unroll 2
-        for (int k = 0; k < n; ++k) {
-            const double m = c[k].mu, a = c[k].a, cc = c[k].c;
+    constexpr int U = R >= 2 ? 4 : 8;
+    const int nbat = n / U, nfull = nbat * U;
+    double Am[U], Aa[U], Ac[U], Bm[U], Ba[U], Bc[U], t[U][R];
+    // batch at record k0; a prefetch past the last full batch re-reads it
+    auto load = [&](double (&m)[U], double (&a)[U], double (&cc)[U], int k0) {
+        const Comp<double>* p = c + min(k0, nfull - U);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            m[u] = p[u].mu;
+            a[u] = p[u].a;
+            cc[u] = p[u].c;
+        }
+    };
+    auto expo = [&](const double (&m)[U], const double (&a)[U], const double (&cc)[U]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const double z = fma(x[r], a, -m);
-                acc[r] = exp_scaled_acc(fma(-z, z, cc), tab, acc[r]);
+                const double z = fma(x[r], a[u], -m[u]);
+                t[u][r] = fma(-z, z, cc[u]);
             }
-        }
-    } else {
-        // few candidates per thread: scalar-loaded records, double-buffered
-        // in batches of U (A/B, no register copies).  Scalar and LDS loads
-        // share lgkmcnt and scalar loads return out of order, so the wait
-        // for a batch's exp-table reads also waits for every scalar load in
-        // flight: the next batch's loads are therefore issued right after
-        // the exponents of the current batch are formed (its first use of
-        // its records) and ~10 VALU per evaluation before that wait.
-        constexpr int U = R == 2 ? 4 : 8;
-        const int nbat = n / U, nfull = nbat * U;
-        double Am[U], Aa[U], Ac[U], Bm[U], Ba[U], Bc[U], t[U][R];
-        // batch at record k0; a prefetch past the last full batch re-reads it
-        auto load = [&](double (&m)[U], double (&a)[U], double (&cc)[U], int k0) {
-            const Comp<double>* p = c + min(k0, nfull - U);
+    };
+    auto accum = [&]() {
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                m[u] = p[u].mu;
-                a[u] = p[u].a;
-                cc[u] = p[u].c;
-            }
-        };
-        auto expo = [&](const double (&m)[U], const double (&a)[U], const double (&cc)[U]) {
+        for (int u = 0; u < U; ++u)
 #pragma unroll
-            for (int u = 0; u < U; ++u)
+            for (int r = 0; r < R; ++r) acc[r] = exp_scaled_acc(t[u][r], tab, acc[r]);
+    };
+    if (nbat > 0) load(Am, Aa, Ac, 0);
+    int b = 0;
+    for (; b + 2 <= nbat; b += 2) {
+        expo(Am, Aa, Ac);
+        __builtin_amdgcn_sched_barrier(0);
+        load(Bm, Ba, Bc, (b + 1) * U);
+        __builtin_amdgcn_sched_barrier(0);
+        accum();
+        expo(Bm, Ba, Bc);
+        __builtin_amdgcn_sched_barrier(0);
+        load(Am, Aa, Ac, (b + 2) * U);
+        __builtin_amdgcn_sched_barrier(0);
+        accum();
+    }
+    if (b < nbat) {
+        expo(Am, Aa, Ac);
+        accum();
+    }
+    for (int k = nfull; k < n; ++k) {
+        const double m = c[k].mu, a = c[k].a, cc = c[k].c;
 #pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    const double z = fma(x[r], a[u], -m[u]);
-                    t[u][r] = fma(-z, z, cc[u]);
-                }
-        };
-        auto accum = [&]() {
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-#pragma unroll
-                for (int r = 0; r < R; ++r) acc[r] = exp_scaled_acc(t[u][r], tab, acc[r]);
-        };
-        if (nbat > 0) load(Am, Aa, Ac, 0);
-        int b = 0;
-        for (; b + 2 <= nbat; b += 2) {
-            expo(Am, Aa, Ac);
-            __builtin_amdgcn_sched_barrier(0);
-            load(Bm, Ba, Bc, (b + 1) * U);
-            __builtin_amdgcn_sched_barrier(0);
-            accum();
-            expo(Bm, Ba, Bc);
-            __builtin_amdgcn_sched_barrier(0);
-            load(Am, Aa, Ac, (b + 2) * U);
-            __builtin_amdgcn_sched_barrier(0);
-            accum();
-        }
-        if (b < nbat) {
-            expo(Am, Aa, Ac);
-            accum();
-        }
-        for (int k = nfull; k < n; ++k) {
-            const double m = c[k].mu, a = c[k].a, cc = c[k].c;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const double z = fma(x[r], a, -m);
-                acc[r] = exp_scaled_acc(fma(-z, z, cc), tab, acc[r]);
-            }
+        for (int r = 0; r < R; ++r) {
+            const double z = fma(x[r], a, -m);
+            acc[r] = exp_scaled_acc(fma(-z, z, cc), tab, acc[r]);
         }
     }
 }

@@ -43,7 +43,7 @@ using namespace tpe_rt;
 namespace {
 
 constexpr int kR = 4;                 // candidates per thread, tile map
-constexpr int kRGroup = 2;            // candidates per thread, packed map with C <= 512
+constexpr int kRGroup = 3;            // candidates per thread, packed map with C <= 768
 constexpr int kTile = kBlock * kR;    // candidates per workgroup, tile map
 
 thread_local std::string g_create_error;
@@ -300,8 +300,7 @@ __global__ __launch_bounds__(kBlock) void k_round(
 // ------------------------------------------------- chunked packed map ----
 // Batched sampled rounds with small C (e.g. 512 new_ids x 24 candidates)
 // give the packed map only gx * labels workgroups -- for config 5 that is
-// 512, two waves per SIMD, too few to hide the LDS / scalar-load latency of
-// the dense loop.  The above mixture's components are then cut into `nch`
+// ~1200, one generation of workgroups with a long tail.  The above mixture's components are then cut into `nch`
 // chunks along grid.z: each workgroup draws the same slots (Philox is
 // stateless), sums its chunk relative to the label's LSE shift (chunk 0 also
 // the below mixture) and stores the raw sums; k_finish_chunks adds the
@@ -933,8 +932,8 @@ void launch_round(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
 // workgroups for ~6-8 generations of the 1280 resident ones (5 per CU: the
 // 32 KB exp table is k_round_chunk's only LDS), so the tail is short; no
 // chunk shorter than kMinChunk components, where the redundant sampling of
-// every chunk would start to show.  Config 5 (512 workgroups): 16 chunks,
-// 72% -> 87% of the VALU issue rate (measured sweep 1..32 in DESIGN.md).
+// every chunk would start to show.  Config 5 (~1200 workgroups): 7 chunks
+// (sweep in DESIGN.md section 6).
 constexpr int64_t kChunkTargetWG = 8192;
 constexpr int32_t kMinChunk = 2048;
 
