@@ -331,45 +331,96 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <int R>
 __device__ __forceinline__ void lse_acc(const Comp<float>* __restrict__ c, int n,
                                         const double (&xd)[R], float (&out)[R]) {
-    if constexpr (R % 2 == 0) {
-        constexpr int P = R / 2;
-        f32x2 x[P], acc[P];
+    // candidate pairs through packed fp32, an odd one scalar; the record
+    // stream double-buffered as in the fp64 lse_acc (no LDS here, but a use
+    // of a scalar-loaded record while the next batch is in flight still
+    // waits for all of it: the loads go out after the batch's exponents)
+    constexpr int P = R / 2;
+    constexpr bool kOdd = R % 2 != 0;
+    constexpr int PP = P > 0 ? P : 1;
+    f32x2 x2[PP], acc2[PP];
+    float x1 = kOdd ? (float)xd[R - 1] : 0.0f, acc1 = 0.0f;
 #pragma unroll
-        for (int p = 0; p < P; ++p) {
-            x[p] = f32x2{(float)xd[2 * p], (float)xd[2 * p + 1]};
-            acc[p] = f32x2{0.0f, 0.0f};
+    for (int p = 0; p < PP; ++p) {
+        x2[p] = P > 0 ? f32x2{(float)xd[2 * p], (float)xd[2 * p + 1]} : f32x2{0.0f, 0.0f};
+        acc2[p] = f32x2{0.0f, 0.0f};
+    }
+    if (n > 0) {
+        constexpr int U = 8;
+        const int nbat = n / U, nfull = nbat * U;
+        float Am[U], Aa[U], Ac[U], Bm[U], Ba[U], Bc[U], t1[U];
+        f32x2 t2[U][PP];
+        auto load = [&](float (&m)[U], float (&a)[U], float (&cc)[U], int k0) {
+            const Comp<float>* q = c + min(k0, nfull - U);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                m[u] = q[u].mu;
+                a[u] = q[u].a;
+                cc[u] = q[u].c;
+            }
+        };
+        auto expo = [&](const float (&m)[U], const float (&a)[U], const float (&cc)[U]) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+#pragma unroll
+                for (int p = 0; p < P; ++p) {
+                    const f32x2 z = (x2[p] - m[u]) * a[u];
+                    t2[u][p] = __builtin_elementwise_fma(-z, z, f32x2{cc[u], cc[u]});
+                }
+                if constexpr (kOdd) {
+                    const float z = (x1 - m[u]) * a[u];
+                    t1[u] = fmaf(-z, z, cc[u]);
+                }
+            }
+        };
+        auto accum = [&]() {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+#pragma unroll
+                for (int p = 0; p < P; ++p)
+                    acc2[p] += f32x2{__builtin_amdgcn_exp2f(t2[u][p].x),
+                                     __builtin_amdgcn_exp2f(t2[u][p].y)};
+                if constexpr (kOdd) acc1 += __builtin_amdgcn_exp2f(t1[u]);
+            }
+        };
+        if (nbat > 0) load(Am, Aa, Ac, 0);
+        int b = 0;
+        for (; b + 2 <= nbat; b += 2) {
+            expo(Am, Aa, Ac);
+            __builtin_amdgcn_sched_barrier(0);
+            load(Bm, Ba, Bc, (b + 1) * U);
+            __builtin_amdgcn_sched_barrier(0);
+            accum();
+            expo(Bm, Ba, Bc);
+            __builtin_amdgcn_sched_barrier(0);
+            load(Am, Aa, Ac, (b + 2) * U);
+            __builtin_amdgcn_sched_barrier(0);
+            accum();
         }
-#pragma unroll 2
-        for (int k = 0; k < n; ++k) {
+        if (b < nbat) {
+            expo(Am, Aa, Ac);
+            accum();
+        }
+        for (int k = nfull; k < n; ++k) {
             const float mu = c[k].mu, a = c[k].a, cc = c[k].c;
 #pragma unroll
             for (int p = 0; p < P; ++p) {
-                const f32x2 z = (x[p] - mu) * a;
+                const f32x2 z = (x2[p] - mu) * a;
                 const f32x2 t = __builtin_elementwise_fma(-z, z, f32x2{cc, cc});
-                acc[p] += f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+                acc2[p] += f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
             }
-        }
-#pragma unroll
-        for (int p = 0; p < P; ++p) {
-            out[2 * p] = acc[p].x;
-            out[2 * p + 1] = acc[p].y;
-        }
-    } else {
-        float x[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            x[r] = (float)xd[r];
-            out[r] = 0.0f;
-        }
-        for (int k = 0; k < n; ++k) {
-            const float mu = c[k].mu, a = c[k].a, cc = c[k].c;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const float z = (x[r] - mu) * a;
-                out[r] += __builtin_amdgcn_exp2f(fmaf(-z, z, cc));
+            if constexpr (kOdd) {
+                const float z = (x1 - mu) * a;
+                acc1 += __builtin_amdgcn_exp2f(fmaf(-z, z, cc));
             }
         }
     }
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        out[2 * p] = acc2[p].x;
+        out[2 * p + 1] = acc2[p].y;
+    }
+    if constexpr (kOdd) out[R - 1] = acc1;
 }
 
 __device__ __forceinline__ double lse_finish(const Comp<float>* __restrict__ c, int n, float acc,
