@@ -47,6 +47,7 @@ constexpr int kSplitBlock = 1024;
 constexpr int kPartBlock = 1024;
 constexpr int kParzenBlock = 1024;
 constexpr int kMaxLF = 64;          // below-list capacity per label (lf <= kMaxLF)
+constexpr int kCatChunk = 8192;     // categorical bincount: observations staged in LDS
 
 // ------------------------------------------------ numpy pairwise summation --
 // np.sum of a contiguous float64 vector: chunks of 8192 (numpy's reduction
@@ -54,30 +55,6 @@ constexpr int kMaxLF = 64;          // below-list capacity per label (lf <= kMax
 // at n2 = n/2 - (n/2) % 8, leaves of <= 128 with 8 accumulators
 // (numpy/_core/src/umath/loops_utils.h.src).  On the device the leaves are
 // summed in parallel and combined in the same tree order.
-
-__device__ double pw_leaf(const double* __restrict__ a, int64_t n) {
-#pragma clang fp contract(off)
-    if (n < 8) {
-        double r = 0.0;
-        for (int64_t i = 0; i < n; ++i) r += a[i];
-        return r;
-    }
-    double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
-    int64_t i = 8;
-    for (; i < n - (n % 8); i += 8) {
-        r0 += a[i + 0];
-        r1 += a[i + 1];
-        r2 += a[i + 2];
-        r3 += a[i + 3];
-        r4 += a[i + 4];
-        r5 += a[i + 5];
-        r6 += a[i + 6];
-        r7 += a[i + 7];
-    }
-    double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-    for (; i < n; ++i) res += a[i];
-    return res;
-}
 
 // The tree of one chunk (<= 8192 elements) has depth <= 8; the functions
 // below walk it by compile-time-unrolled recursion (distinct template
@@ -150,6 +127,7 @@ __device__ __attribute__((noinline)) double pw_tree(int64_t n, const double* __r
 __device__ double block_np_sum(const double* __restrict__ a, int64_t n, double* __restrict__ leaf_sum) {
 #pragma clang fp contract(off)
     __shared__ double chunk_sum[64];
+    __shared__ double tail_leaf[kNpChunkLeaves + 8];   // a tail chunk has <= 65 leaves
     __shared__ double res_sh;
     const int64_t n_chunks = (n + kNpChunk - 1) / kNpChunk;
     const int64_t full = n / kNpChunk;
@@ -157,7 +135,13 @@ __device__ double block_np_sum(const double* __restrict__ a, int64_t n, double* 
     const int tail_leaves = tail ? pw_leaves<kPwDepth>(tail) : 0;
     const int64_t total = full * kNpChunkLeaves + tail_leaves;
     __syncthreads();   // a[] was just written by the other threads of the block
-    for (int64_t t = threadIdx.x; t < total; t += blockDim.x) {
+    // leaves: 8 lanes per leaf, lane j accumulating pairwise_sum's r_j (the
+    // stride-8 elements j, j + 8, ... in order -- all its loads in flight at
+    // once), the ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) combine by
+    // xor shuffles, then lane 0 adds the leaf's last n % 8 elements in order
+    for (int64_t t8 = threadIdx.x; t8 < total * 8; t8 += blockDim.x) {
+        const int64_t t = t8 >> 3;
+        const int j = (int)(t8 & 7);
         int64_t s, len;
         if (t < full * kNpChunkLeaves) {
             s = t * 128;
@@ -166,7 +150,33 @@ __device__ double block_np_sum(const double* __restrict__ a, int64_t n, double* 
             pw_leaf_at<kPwDepth>(tail, (int)(t - full * kNpChunkLeaves), s, len);
             s += full * kNpChunk;
         }
-        leaf_sum[t] = pw_leaf(a + s, len);
+        const double* x = a + s;
+        const int64_t body = len - len % 8;
+        double r = 0.0;
+        if (len >= 8) {
+            double v[16];
+#pragma unroll
+            for (int m = 0; m < 16; ++m) v[m] = (8 * m + j < body) ? x[8 * m + j] : 0.0;
+            r = v[0];
+#pragma unroll
+            for (int m = 1; m < 16; ++m)
+                if (8 * m + j < body) r += v[m];
+        }
+        r += __shfl_xor(r, 1);
+        r += __shfl_xor(r, 2);
+        r += __shfl_xor(r, 4);
+        if (j == 0) {
+            double res;
+            if (len < 8) {
+                res = 0.0;
+                for (int64_t i = 0; i < len; ++i) res += x[i];
+            } else {
+                res = r;
+                for (int64_t i = body; i < len; ++i) res += x[i];
+            }
+            if (t < full * kNpChunkLeaves) leaf_sum[t] = res;
+            else tail_leaf[t - full * kNpChunkLeaves] = res;   // the tail's tree walks LDS
+        }
     }
     __syncthreads();
     // chunk trees: one thread per chunk; sums beyond 64 chunks go through the
@@ -185,7 +195,7 @@ __device__ double block_np_sum(const double* __restrict__ a, int64_t n, double* 
             v = t[0];
         } else {
             int next = 0;
-            v = pw_tree<kPwDepth>(tail, leaf_sum + c * kNpChunkLeaves, next);
+            v = pw_tree<kPwDepth>(tail, tail_leaf, next);
         }
         if (c < 64) chunk_sum[c] = v;
         else leaf_sum[c * kNpChunkLeaves] = v;
@@ -252,6 +262,7 @@ __global__ __launch_bounds__(kSplitBlock) void k_split(const double* __restrict_
     __shared__ uint64_t prefix_sh;
     __shared__ int64_t need_sh;
     __shared__ int wcnt[kSplitBlock / 64];
+    __shared__ uint32_t wsum[4];
     __shared__ int64_t base_sh;
     for (int64_t i = tid; i < T; i += kSplitBlock) below[i] = 0;
     if (n_below <= 0 || T <= 0) return;
@@ -270,15 +281,28 @@ __global__ __launch_bounds__(kSplitBlock) void k_split(const double* __restrict_
             if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
         }
         __syncthreads();
-        if (tid == 0) {
-            int64_t need = need_sh, acc = 0;
-            int d = 0;
-            for (; d < 255; ++d) {
-                if (acc + hist[d] >= need) break;
-                acc += hist[d];
+        // the digit holding the need-th key: inclusive scan of the histogram
+        // over the first four waves (shuffles, then the wave totals); the
+        // bin whose range [excl, incl) of ranks holds need takes over
+        const int64_t need = need_sh;
+        uint32_t h = 0, incl = 0;
+        if (tid < 256) {
+            h = hist[tid];
+            incl = h;
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t t = __shfl_up(incl, off);
+                if (lane >= off) incl += t;
             }
-            need_sh = need - acc;
-            prefix_sh = prefix | ((uint64_t)d << shift);
+            if (lane == 63) wsum[wv] = incl;
+        }
+        __syncthreads();
+        if (tid < 256) {
+            for (int w = 0; w < wv; ++w) incl += wsum[w];
+            const uint32_t excl = incl - h;
+            if ((int64_t)excl < need && (int64_t)incl >= need) {
+                need_sh = need - excl;
+                prefix_sh = prefix | ((uint64_t)tid << shift);
+            }
         }
         mask |= 255ull << shift;
         __syncthreads();
@@ -519,33 +543,47 @@ __global__ __launch_bounds__(kParzenBlock) void k_parzen(
         // observation order; pseudocounts; / np.sum(pseudocounts)
         // One wave per bin: ballots over the list find the bin's observations
         // in order, and the wave adds their weights one by one through scalar
-        // registers (v_readlane) -- the sequential order of np.bincount.
+        // registers (v_readlane) -- the sequential order of np.bincount.  The
+        // list goes through LDS as bin ids, kCatChunk observations at a time
+        // (coalesced loads by the whole block; the waves then scan LDS).
         const double* list = side == 0 ? below_val + (size_t)l * kMaxLF : keys_unsorted + off;
         const int32_t upper = sp.upper;
         const LFRamp ramp = lf_ramp(n, lf);
         const int wave = tid >> 6, lane = tid & 63;
-        for (int b = wave; b < upper; b += kParzenBlock / 64) {
-            double cnt = 0.0;
-            for (int64_t c0 = 0; c0 < n; c0 += 64) {
-                const int64_t i = c0 + lane;
-                const bool hit = i < n && (int64_t)list[i] == b;
-                uint64_t m = __ballot(hit);
-                if (!m) continue;
-                const double wl = hit ? lf_weight(i, ramp) : 0.0;
-                int64_t bits;
-                __builtin_memcpy(&bits, &wl, 8);
-                const int lo = (int)(uint32_t)bits, hi = (int)(uint32_t)(bits >> 32);
-                while (m) {
-                    const int j = __builtin_ctzll(m);
-                    m &= m - 1;
-                    const uint64_t vb = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, j) << 32) |
-                                        (uint32_t)__builtin_amdgcn_readlane(lo, j);
-                    double v;
-                    __builtin_memcpy(&v, &vb, 8);
-                    cnt += v;
-                }
+        __shared__ int32_t cbin[kCatChunk];
+        for (int b = tid; b < upper; b += kParzenBlock) w[o + b] = 0.0;
+        for (int64_t c0 = 0; c0 < n; c0 += kCatChunk) {
+            const int64_t m = n - c0 < kCatChunk ? n - c0 : kCatChunk;
+            for (int64_t i = tid; i < m; i += kParzenBlock) {
+                const double v = list[c0 + i];   // (int64_t)v == b for some bin b, else -1
+                cbin[i] = (v > -1.0 && v < (double)upper) ? (int32_t)(int64_t)v : -1;
             }
-            if (lane == 0) w[o + b] = cnt;
+            __syncthreads();
+            for (int b = wave; b < upper; b += kParzenBlock / 64) {
+                double cnt = w[o + b];
+                for (int64_t i0 = 0; i0 < m; i0 += 64) {
+                    const int64_t i = i0 + lane;
+                    const bool hit = i < m && cbin[i] == b;
+                    uint64_t hm = __ballot(hit);
+                    if (!hm) continue;
+                    const double wl = hit ? lf_weight(c0 + i, ramp) : 0.0;
+                    int64_t bits;
+                    __builtin_memcpy(&bits, &wl, 8);
+                    const int lo = (int)(uint32_t)bits, hi = (int)(uint32_t)(bits >> 32);
+                    while (hm) {
+                        const int j = __builtin_ctzll(hm);
+                        hm &= hm - 1;
+                        const uint64_t vb =
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, j) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane(lo, j);
+                        double v;
+                        __builtin_memcpy(&v, &vb, 8);
+                        cnt += v;
+                    }
+                }
+                if (lane == 0) w[o + b] = cnt;
+            }
+            __syncthreads();
         }
         __syncthreads();
         for (int b = tid; b < upper; b += kParzenBlock) {
@@ -567,18 +605,19 @@ __global__ __launch_bounds__(kParzenBlock) void k_parzen(
     const double* sk;
     const int32_t* si;
     if (side == 0) {
-        if (tid == 0) {
-            for (int64_t i = 0; i < n; ++i) {
-                const double v = below_val[(size_t)l * kMaxLF + i];
-                int64_t j = i;
-                while (j > 0 && bk[j - 1] > v) {
-                    bk[j] = bk[j - 1];
-                    bi[j] = bi[j - 1];
-                    --j;
-                }
-                bk[j] = v;
-                bi[j] = (int32_t)i;
+        // stable rank sort of the <= kMaxLF below values (ascending total
+        // order: NaN last, as np.argsort; ties by position): a thread each
+        if (tid < n) {
+            const double* bv = below_val + (size_t)l * kMaxLF;
+            const double v = bv[tid];
+            const uint64_t kv = asc_key(v);
+            int rank = 0;
+            for (int64_t j = 0; j < n; ++j) {
+                const uint64_t kj = asc_key(bv[j]);
+                rank += (kj < kv || (kj == kv && j < tid)) ? 1 : 0;
             }
+            bk[rank] = v;
+            bi[rank] = (int32_t)tid;
         }
         __syncthreads();
         sk = bk;
@@ -588,20 +627,18 @@ __global__ __launch_bounds__(kParzenBlock) void k_parzen(
         si = idx_sorted + off;
     }
     const double pmu = sp.prior_mu, psig = sp.prior_sigma;
-    __shared__ int64_t pos_sh;
-    if (tid == 0) {
-        int64_t pos = 0;
-        if (n == 1) {
-            pos = pmu < sk[0] ? 0 : 1;
-        } else if (n >= 2) {  // np.searchsorted(sorted, prior_mu), side='left'
-            int64_t lo = 0, hi = n;
-            while (lo < hi) {
-                const int64_t mid = (lo + hi) >> 1;
-                if (sk[mid] < pmu) lo = mid + 1; else hi = mid;
-            }
-            pos = lo;
-        }
-        pos_sh = pos;
+    __shared__ int pos_sh;
+    if (tid == 0) pos_sh = 0;
+    __syncthreads();
+    if (n == 1) {
+        if (tid == 0) pos_sh = pmu < sk[0] ? 0 : 1;
+    } else if (n >= 2) {
+        // np.searchsorted(sorted, prior_mu), side='left' = the number of
+        // sorted values < prior_mu: counted by every thread, summed per wave
+        int cnt = 0;
+        for (int64_t j = tid; j < n; j += kParzenBlock) cnt += sk[j] < pmu ? 1 : 0;
+        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+        if ((tid & 63) == 0 && cnt) atomicAdd(&pos_sh, cnt);
     }
     __syncthreads();
     const int64_t pos = pos_sh, K = n + 1;
@@ -751,28 +788,43 @@ __global__ __launch_bounds__(kParzenBlock) void k_fold(
             }
         }
     }
-    // sampling records of the below mixture: cumulative normalised weights
+    // sampling records of the below mixture: cumulative normalised weights,
+    // summed in order by one thread -- over an LDS copy of the weights when
+    // they fit (the serial walk then costs LDS, not global, latency)
+    __shared__ double wst[kParzenBlock];
+    const bool staged = Kb <= kParzenBlock;
+    if (staged) {
+        if (tid < Kb) wst[tid] = w[ob + tid];
+        __syncthreads();
+    }
+    const double* wb = staged ? wst : w + ob;
     if (tid == 0) {
         double tot = 0.0;
-        for (int64_t k = 0; k < Kb; ++k) tot += w[ob + k];
+        for (int64_t k = 0; k < Kb; ++k) tot += wb[k];
         if (!(tot > 0)) {
             atomicOr(err, 4);
             tot = 1.0;
         }
         double run = 0.0;
         for (int64_t k = 0; k < Kb; ++k) {
-            run += w[ob + k];
-            SampRec s;
-            s.cdf = (k == Kb - 1) ? 1.0 : run / tot;
-            s.mu = d.mode == CAT ? 0.0 : mu[ob + k];
-            s.sigma = d.mode == CAT ? 0.0 : sigma[ob + k];
-            s.pad = 0.0;
-            samp[d.samp_off + k] = s;
+            run += wb[k];
+            const double cdf = (k == Kb - 1) ? 1.0 : run / tot;
+            if (staged) wst[k] = cdf;
+            else samp[d.samp_off + k].cdf = cdf;
         }
         d.nb = (int32_t)Kb;
         d.na = (int32_t)Ka;
         d.ns = (int32_t)Kb;
         labels[l] = d;
+    }
+    __syncthreads();
+    for (int64_t k = tid; k < Kb; k += kParzenBlock) {
+        SampRec r;
+        r.cdf = staged ? wst[k] : samp[d.samp_off + k].cdf;
+        r.mu = d.mode == CAT ? 0.0 : mu[ob + k];
+        r.sigma = d.mode == CAT ? 0.0 : sigma[ob + k];
+        r.pad = 0.0;
+        samp[d.samp_off + k] = r;
     }
 }
 

@@ -441,8 +441,14 @@ __global__ __launch_bounds__(kBlock) void k_sample_small(
     if (s >= (int64_t)n_rounds * n) return;
     const int64_t z = s / n, i = s - z * n;
     double v;
-    if (!sample_below<MODE>(L, samp + L.samp_off, seed, rounds[z], (uint32_t)(cand_offset + i), v))
-        atomicOr(err, 1);
+    bool ok;
+    if constexpr (MODE == DENSE_ANY)
+        ok = L.mode == DENSE_LGMM
+                 ? sample_below<DENSE_LGMM>(L, samp + L.samp_off, seed, rounds[z], (uint32_t)(cand_offset + i), v)
+                 : sample_below<DENSE_GMM>(L, samp + L.samp_off, seed, rounds[z], (uint32_t)(cand_offset + i), v);
+    else
+        ok = sample_below<MODE>(L, samp + L.samp_off, seed, rounds[z], (uint32_t)(cand_offset + i), v);
+    if (!ok) atomicOr(err, 1);
     xs[((size_t)z * n_labels + li) * n + i] = v;
 }
 
@@ -452,24 +458,19 @@ template <typename T, int MODE>
 __device__ __forceinline__ double slice_sum(const DLabel& L, const Comp<T>* __restrict__ c,
                                             const Comp<double>* __restrict__ c64, int k0, int k1,
                                             double x, const double* __restrict__ tab) {
-    if constexpr (MODE == DENSE_GMM || MODE == DENSE_LGMM) {
-        const double v = (MODE == DENSE_LGMM) ? log(x) : x;
+    if constexpr (MODE == DENSE_GMM || MODE == DENSE_LGMM || MODE == DENSE_ANY) {
+        const bool lgmm = MODE == DENSE_LGMM || (MODE == DENSE_ANY && L.mode == DENSE_LGMM);
+        const double v = lgmm ? log(x) : x;
         if constexpr (sizeof(T) == 8) {
-            const double xr = v - L.centre;
-            double acc = 0.0;
-            for (int k = k0; k < k1; ++k) {
-                const double z = fma(xr, c[k].a, -c[k].mu);
-                acc = exp_scaled_acc(fma(-z, z, c[k].c), tab, acc);
-            }
-            return acc;
+            const double xr[1] = {v - L.centre};
+            double acc[1] = {0.0};
+            lse_acc<1>(c + k0, k1 - k0, xr, acc, tab);
+            return acc[0];
         } else {
-            const float xf = (float)v;
-            float acc = 0.0f;
-            for (int k = k0; k < k1; ++k) {
-                const float z = (xf - c[k].mu) * c[k].a;
-                acc += __builtin_amdgcn_exp2f(fmaf(-z, z, c[k].c));
-            }
-            return (double)acc;
+            const double xv[1] = {v};
+            float acc[1];
+            lse_acc<1>(c + k0, k1 - k0, xv, acc);
+            return (double)acc[0];
         }
     } else {
 #pragma clang fp contract(off)
@@ -505,7 +506,8 @@ __global__ __launch_bounds__(kBlock) void k_score_slices(
     const int li = group[blockIdx.y];
     const DLabel L = labels[li];
     const int64_t z = blockIdx.z;
-    constexpr bool kTab = (MODE == DENSE_GMM || MODE == DENSE_LGMM) && sizeof(T) == 8;
+    constexpr bool kTab =
+        (MODE == DENSE_GMM || MODE == DENSE_LGMM || MODE == DENSE_ANY) && sizeof(T) == 8;
     __shared__ double exp_tab[kTab ? kExpTabSize : 1];
     if constexpr (kTab) load_exp_table(exp_tab);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -540,28 +542,35 @@ __global__ __launch_bounds__(kBlock) void k_finish_slices(
     uint64_t bk = 0;
     int64_t bi = INT64_MAX;
     double bv = 0.0, bl = 0.0, ba = 0.0;
+    // the slices of one mixture, added in order (loads issued 8 ahead)
+    auto add_slices = [&](int s0, int ns, int64_t c) {
+        double acc = 0.0;
+        int s = 0;
+        for (; s + 8 <= ns; s += 8) {
+            double v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = prow[(size_t)(s0 + s + j) * n + c];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc += v[j];
+        }
+        for (; s < ns; ++s) acc += prow[(size_t)(s0 + s) * n + c];
+        return acc;
+    };
     for (int64_t c = threadIdx.x; c < n; c += kBlock) {
         const double x = xrow[c];
-        double sb = 0.0, sa = 0.0;
-        for (int s = 0; s < nsb; ++s) sb += prow[(size_t)s * n + c];
-        for (int s = 0; s < nsa; ++s) sa += prow[(size_t)(nsb + s) * n + c];
+        const double sb = add_slices(0, nsb, c), sa = add_slices(nsb, nsa, c);
         double lb, la;
-        if constexpr (MODE == DENSE_GMM || MODE == DENSE_LGMM) {
-            const double y = (MODE == DENSE_LGMM) ? log(x) : x;
+        if constexpr (MODE == DENSE_GMM || MODE == DENSE_LGMM || MODE == DENSE_ANY) {
+            const bool lgmm = MODE == DENSE_LGMM || (MODE == DENSE_ANY && L.mode == DENSE_LGMM);
+            const double y = lgmm ? log(x) : x;
             if constexpr (sizeof(T) == 8) {
-                const double xr = y - L.centre;
-                lb = (sb >= 1e-290) ? log(sb) : lse_twopass(comps + L.comp_b, L.nb, xr);
-                la = (sa >= 1e-290) ? log(sa) : lse_twopass(comps + L.comp_a, L.na, xr);
+                lb = lse_finish(comps + L.comp_b, L.nb, sb, y - L.centre, L.shift_b);
+                la = lse_finish(comps + L.comp_a, L.na, sa, y - L.centre, L.shift_a);
             } else {
-                const float yf = (float)y;
-                lb = (sb >= 1e-30) ? (double)(__builtin_log2f((float)sb) * 0.69314718055994531f)
-                                   : (double)lse_twopass(comps + L.comp_b, L.nb, yf);
-                la = (sa >= 1e-30) ? (double)(__builtin_log2f((float)sa) * 0.69314718055994531f)
-                                   : (double)lse_twopass(comps + L.comp_a, L.na, yf);
+                lb = lse_finish(comps + L.comp_b, L.nb, (float)sb, (float)y, L.shift_b);
+                la = lse_finish(comps + L.comp_a, L.na, (float)sa, (float)y, L.shift_a);
             }
-            lb += L.shift_b;
-            la += L.shift_a;
-            if (MODE == DENSE_LGMM) {
+            if (lgmm) {
                 lb -= y;
                 la -= y;
             }
@@ -1098,28 +1107,34 @@ inline int slices_of(const DLabel& d) {
     return (d.nb + S - 1) / S + (d.na + S - 1) / S;
 }
 
+// MODE = DENSE_ANY: the GMM1 and LGMM1 labels in one chain (their groups are
+// adjacent), timed in the DENSE_GMM slot
 template <typename T, int MODE>
 int launch_splitk(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int32_t s_max) {
-    const int nl = g.count[MODE];
+    constexpr bool kAny = MODE == DENSE_ANY;
+    const int nl = kAny ? g.count[DENSE_GMM] + g.count[DENSE_LGMM] : g.count[MODE];
     if (nl == 0) return TPE_OK;
+    const int32_t* grp = kAny ? ctx->P->groups.p + ctx->P->group_off[DENSE_GMM] : g.dev[MODE];
     int32_t s_mode = 0;
-    for (int li : ctx->P->h_group[MODE]) s_mode = std::max(s_mode, slices_of(ctx->P->h_labels[li]));
+    for (int m : {kAny ? DENSE_GMM : MODE, kAny ? DENSE_LGMM : MODE})
+        for (int li : ctx->P->h_group[m]) s_mode = std::max(s_mode, slices_of(ctx->P->h_labels[li]));
     const Comp<T>* comps;
     if constexpr (sizeof(T) == 8) comps = ctx->P->comps64.p; else comps = ctx->P->comps32.p;
     const int32_t L = ctx->P->n_labels;
-    bracket(ctx, MODE, 0);
+    const int slot = kAny ? DENSE_GMM : MODE;
+    bracket(ctx, slot, 0);
     const unsigned sb = (unsigned)((a.n * a.n_rounds + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_sample_small<MODE>, dim3(sb, nl), dim3(kBlock), 0, ctx->stream,
-                       ctx->P->labels.p, g.dev[MODE], ctx->P->samp.p, a.n, a.cand_offset, a.seed,
+                       ctx->P->labels.p, grp, ctx->P->samp.p, a.n, a.cand_offset, a.seed,
                        ctx->rounds.p, a.n_rounds, L, ctx->xs.p, ctx->errflag.p);
     hipLaunchKernelGGL((k_score_slices<T, MODE>),
                        dim3((unsigned)((s_mode + kSliceWaves - 1) / kSliceWaves), nl, a.n_rounds),
-                       dim3(kBlock), 0, ctx->stream, ctx->P->labels.p, g.dev[MODE], comps,
+                       dim3(kBlock), 0, ctx->stream, ctx->P->labels.p, grp, comps,
                        ctx->P->comps64.p, a.n, L, s_max, ctx->xs.p, ctx->slice_part.p);
     hipLaunchKernelGGL((k_finish_slices<T, MODE>), dim3(nl, a.n_rounds), dim3(kBlock), 0,
-                       ctx->stream, ctx->P->labels.p, g.dev[MODE], comps, a.n, a.cand_offset, L, s_max,
+                       ctx->stream, ctx->P->labels.p, grp, comps, a.n, a.cand_offset, L, s_max,
                        ctx->xs.p, ctx->slice_part.p, ctx->partials.p, ctx->errflag.p);
-    bracket(ctx, MODE, 1);
+    bracket(ctx, slot, 1);
     return ctx->hip(hipGetLastError(), "split-K launch");
 }
 
@@ -1187,11 +1202,9 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         HIPCHK(ctx, ctx->slice_part.reserve((size_t)n_rounds * L * s_max * n));
         int rc;
         if (ctx->precision == TPE_F32) {
-            if ((rc = launch_splitk<float, DENSE_GMM>(ctx, g, a, s_max))) return rc;
-            if ((rc = launch_splitk<float, DENSE_LGMM>(ctx, g, a, s_max))) return rc;
+            if ((rc = launch_splitk<float, DENSE_ANY>(ctx, g, a, s_max))) return rc;
         } else {
-            if ((rc = launch_splitk<double, DENSE_GMM>(ctx, g, a, s_max))) return rc;
-            if ((rc = launch_splitk<double, DENSE_LGMM>(ctx, g, a, s_max))) return rc;
+            if ((rc = launch_splitk<double, DENSE_ANY>(ctx, g, a, s_max))) return rc;
         }
         if ((rc = launch_splitk<double, QUANT_GMM>(ctx, g, a, s_max))) return rc;
         if ((rc = launch_splitk<double, QUANT_LGMM>(ctx, g, a, s_max))) return rc;
@@ -1252,8 +1265,8 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         if (sample && (d.mode == QUANT_GMM || d.mode == QUANT_LGMM)) continue;  // counted below
         const int64_t e = ((d.mode == CAT) ? 2 * n : n * (int64_t)(d.nb + d.na)) * n_rounds;
         evals += e;
-        // sampled tile / packed rounds time both dense families in one launch
-        const bool merged = sample && !splitk && d.mode == DENSE_LGMM;
+        // sampled rounds time both dense families in one launch (chain)
+        const bool merged = sample && d.mode == DENSE_LGMM;
         ctx->mode_evals[merged ? DENSE_GMM : d.mode] += e;
     }
     ctx->mode_evals[QUANT_GMM] += evals_q[0];
