@@ -56,85 +56,102 @@ constexpr int kCatChunk = 8192;     // categorical bincount: observations staged
 // (numpy/_core/src/umath/loops_utils.h.src).  On the device the leaves are
 // summed in parallel and combined in the same tree order.
 
-// The tree of one chunk (<= 8192 elements) has depth <= 8; the functions
-// below walk it by compile-time-unrolled recursion (distinct template
-// instances, no stack arrays, no device recursion).
+// The tree of one chunk (<= 8192 elements) has depth <= 8 and <= 65 leaves.
+// A partial (tail) chunk's tree is walked once, iteratively, by one thread:
+// depth-first, left first, which lists the leaves left to right and, in a
+// second walk, combines their sums in the tree's order.
 constexpr int64_t kNpChunk = 8192;
 constexpr int kNpChunkLeaves = 64;   // a full chunk: 64 leaves of 128
-constexpr int kPwDepth = 8;
+constexpr int kTailLeaves = 72;      // a partial chunk: <= 65 leaves
+constexpr int kPwStack = 12;         // > tree depth
 
 __device__ __forceinline__ int64_t pw_split(int64_t n) {
     int64_t n2 = n / 2;
     return n2 - n2 % 8;
 }
 
-// number of leaves of the tree of n
-template <int D>
-__device__ __attribute__((noinline)) int pw_leaves(int64_t n) {
-    if constexpr (D == 0) {
-        return 1;
-    } else {
-        if (n <= 128) return 1;
-        const int64_t n2 = pw_split(n);
-        return pw_leaves<D - 1>(n2) + pw_leaves<D - 1>(n - n2);
+// leaves (start, length) of the tree of n, left to right; returns the count
+__device__ int pw_leaf_list(int32_t n, int32_t* __restrict__ ls, int32_t* __restrict__ ln) {
+    int32_t st_s[kPwStack], st_n[kPwStack];
+    int sp = 0, cnt = 0;
+    st_s[0] = 0;
+    st_n[0] = n;
+    while (sp >= 0) {
+        const int32_t s0 = st_s[sp], n0 = st_n[sp];
+        --sp;
+        if (n0 <= 128) {
+            ls[cnt] = s0;
+            ln[cnt] = n0;
+            ++cnt;
+            continue;
+        }
+        const int32_t n2 = (int32_t)pw_split(n0);
+        st_s[++sp] = s0 + n2;   // right pushed first: the left is walked first
+        st_n[sp] = n0 - n2;
+        st_s[++sp] = s0;
+        st_n[sp] = n2;
     }
+    return cnt;
 }
 
-// start and length of leaf t of the tree of n
-template <int D>
-__device__ __attribute__((noinline)) void pw_leaf_at(int64_t n, int t, int64_t& s, int64_t& len) {
-    if constexpr (D == 0) {
-        s = 0;
-        len = n;
-    } else {
-        if (n <= 128) {
-            s = 0;
-            len = n;
-            return;
-        }
-        const int64_t n2 = pw_split(n);
-        const int nl = pw_leaves<D - 1>(n2);
-        if (t < nl) {
-            pw_leaf_at<D - 1>(n2, t, s, len);
-        } else {
-            pw_leaf_at<D - 1>(n - n2, t - nl, s, len);
-            s += n2;
-        }
-    }
-}
-
-// the tree's combination of its leaf sums, left to right
-template <int D>
-__device__ __attribute__((noinline)) double pw_tree(int64_t n, const double* __restrict__ leaf, int& next) {
+// the tree's combination of its leaf sums (left to right), post-order
+__device__ double pw_tree_sum(int32_t n, const double* __restrict__ leaf) {
 #pragma clang fp contract(off)
-    if constexpr (D == 0) {
-        return leaf[next++];
-    } else {
-        if (n <= 128) return leaf[next++];
-        const int64_t n2 = pw_split(n);
-        const double a = pw_tree<D - 1>(n2, leaf, next);
-        const double b = pw_tree<D - 1>(n - n2, leaf, next);
-        return a + b;
+    int32_t st_n[kPwStack];
+    int st_state[kPwStack];
+    double st_a[kPwStack];
+    int sp = 0, next = 0;
+    st_n[0] = n;
+    st_state[0] = 0;
+    double ret = 0.0;
+    while (sp >= 0) {
+        const int32_t n0 = st_n[sp];
+        if (n0 <= 128) {
+            ret = leaf[next++];
+            --sp;
+            continue;
+        }
+        const int32_t n2 = (int32_t)pw_split(n0);
+        if (st_state[sp] == 0) {
+            st_state[sp] = 1;
+            ++sp;
+            st_n[sp] = n2;
+            st_state[sp] = 0;
+        } else if (st_state[sp] == 1) {
+            st_a[sp] = ret;
+            st_state[sp] = 2;
+            ++sp;
+            st_n[sp] = n0 - n2;
+            st_state[sp] = 0;
+        } else {
+            ret = st_a[sp] + ret;
+            --sp;
+        }
     }
+    return ret;
 }
 
 // np.sum(a[0:n]) by one workgroup: numpy reduces in buffer-sized chunks of
 // 8192 elements, accumulated sequentially from 0.0, each chunk summed
 // pairwise.  Leaves are summed in parallel (full chunks: 64 leaves of 128;
-// the last chunk's leaves located by descent), chunk trees combined one
-// chunk per thread, chunks added in order.  leaf_sum is this call's private
-// global scratch (capacity >= n / 56 + 1).  Every thread returns the sum.
+// the last chunk's leaves listed once by thread 0), chunk trees combined
+// one chunk per thread, chunks added in order.  leaf_sum is this call's
+// private global scratch (capacity >= n / 56 + 1).  Every thread returns
+// the sum.
 __device__ double block_np_sum(const double* __restrict__ a, int64_t n, double* __restrict__ leaf_sum) {
 #pragma clang fp contract(off)
     __shared__ double chunk_sum[64];
-    __shared__ double tail_leaf[kNpChunkLeaves + 8];   // a tail chunk has <= 65 leaves
+    __shared__ double tail_leaf[kTailLeaves];
+    __shared__ int32_t tail_s[kTailLeaves], tail_n[kTailLeaves];
+    __shared__ int tail_cnt;
     __shared__ double res_sh;
     const int64_t n_chunks = (n + kNpChunk - 1) / kNpChunk;
     const int64_t full = n / kNpChunk;
     const int64_t tail = n - full * kNpChunk;
-    const int tail_leaves = tail ? pw_leaves<kPwDepth>(tail) : 0;
-    const int64_t total = full * kNpChunkLeaves + tail_leaves;
     __syncthreads();   // a[] was just written by the other threads of the block
+    if (threadIdx.x == 0) tail_cnt = tail ? pw_leaf_list((int32_t)tail, tail_s, tail_n) : 0;
+    __syncthreads();
+    const int64_t total = full * kNpChunkLeaves + tail_cnt;
     // leaves: 8 lanes per leaf, lane j accumulating pairwise_sum's r_j (the
     // stride-8 elements j, j + 8, ... in order -- all its loads in flight at
     // once), the ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) combine by
@@ -147,8 +164,8 @@ __device__ double block_np_sum(const double* __restrict__ a, int64_t n, double* 
             s = t * 128;
             len = 128;
         } else {
-            pw_leaf_at<kPwDepth>(tail, (int)(t - full * kNpChunkLeaves), s, len);
-            s += full * kNpChunk;
+            s = full * kNpChunk + tail_s[t - full * kNpChunkLeaves];
+            len = tail_n[t - full * kNpChunkLeaves];
         }
         const double* x = a + s;
         const int64_t body = len - len % 8;
@@ -194,8 +211,7 @@ __device__ double block_np_sum(const double* __restrict__ a, int64_t n, double* 
                 for (int j = 0; j < w; ++j) t[j] = t[2 * j] + t[2 * j + 1];
             v = t[0];
         } else {
-            int next = 0;
-            v = pw_tree<kPwDepth>(tail, tail_leaf, next);
+            v = pw_tree_sum((int32_t)tail, tail_leaf);
         }
         if (c < 64) chunk_sum[c] = v;
         else leaf_sum[c * kNpChunkLeaves] = v;
