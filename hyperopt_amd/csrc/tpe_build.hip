@@ -56,116 +56,95 @@ constexpr int kCatChunk = 8192;     // categorical bincount: observations staged
 // (numpy/_core/src/umath/loops_utils.h.src).  On the device the leaves are
 // summed in parallel and combined in the same tree order.
 
-// The tree of one chunk (<= 8192 elements) has depth <= 8 and <= 65 leaves.
-// A partial (tail) chunk's tree is walked once, iteratively, by one thread:
-// depth-first, left first, which lists the leaves left to right and, in a
-// second walk, combines their sums in the tree's order.
+// The tree of one chunk (<= 8192 elements) has depth <= 7 and <= 65 leaves;
+// every split point is a multiple of 8, so every leaf starts at a multiple
+// of 8.  A partial (tail) chunk's tree is handled in parallel from register
+// descents only: each 8-lane group descends from the root to the leaf holding
+// its position 8q and sums it if the leaf starts there (the sum lands in LDS
+// slot q), then the inner nodes are combined bottom-up, one level per
+// barrier, each node adding its right child's slot into its left child's --
+// the (left + right) order of numpy's recursion.
 constexpr int64_t kNpChunk = 8192;
 constexpr int kNpChunkLeaves = 64;   // a full chunk: 64 leaves of 128
-constexpr int kTailLeaves = 72;      // a partial chunk: <= 65 leaves
-constexpr int kPwStack = 12;         // > tree depth
+constexpr int kPwDepth = 7;          // >= the depth of any tree of n < 8192
+constexpr int kTailSlots = kNpChunk / 8;
 
-__device__ __forceinline__ int64_t pw_split(int64_t n) {
-    int64_t n2 = n / 2;
+__device__ __forceinline__ int32_t pw_split(int32_t n) {
+    int32_t n2 = n / 2;
     return n2 - n2 % 8;
 }
 
-// leaves (start, length) of the tree of n, left to right; returns the count
-__device__ int pw_leaf_list(int32_t n, int32_t* __restrict__ ls, int32_t* __restrict__ ln) {
-    int32_t st_s[kPwStack], st_n[kPwStack];
-    int sp = 0, cnt = 0;
-    st_s[0] = 0;
-    st_n[0] = n;
-    while (sp >= 0) {
-        const int32_t s0 = st_s[sp], n0 = st_n[sp];
-        --sp;
-        if (n0 <= 128) {
-            ls[cnt] = s0;
-            ln[cnt] = n0;
-            ++cnt;
-            continue;
+// the leaf (start, length) of the tree of n that holds position p
+__device__ __forceinline__ void pw_leaf_at(int32_t n, int32_t p, int32_t& s0, int32_t& n0) {
+    s0 = 0;
+    n0 = n;
+#pragma unroll
+    for (int d = 0; d <= kPwDepth; ++d) {
+        if (n0 <= 128) break;
+        const int32_t n2 = pw_split(n0);
+        if (p < s0 + n2) {
+            n0 = n2;
+        } else {
+            s0 += n2;
+            n0 -= n2;
         }
-        const int32_t n2 = (int32_t)pw_split(n0);
-        st_s[++sp] = s0 + n2;   // right pushed first: the left is walked first
-        st_n[sp] = n0 - n2;
-        st_s[++sp] = s0;
-        st_n[sp] = n2;
     }
-    return cnt;
 }
 
-// the tree's combination of its leaf sums (left to right), post-order
-__device__ double pw_tree_sum(int32_t n, const double* __restrict__ leaf) {
-#pragma clang fp contract(off)
-    int32_t st_n[kPwStack];
-    int st_state[kPwStack];
-    double st_a[kPwStack];
-    int sp = 0, next = 0;
-    st_n[0] = n;
-    st_state[0] = 0;
-    double ret = 0.0;
-    while (sp >= 0) {
-        const int32_t n0 = st_n[sp];
-        if (n0 <= 128) {
-            ret = leaf[next++];
-            --sp;
-            continue;
-        }
-        const int32_t n2 = (int32_t)pw_split(n0);
-        if (st_state[sp] == 0) {
-            st_state[sp] = 1;
-            ++sp;
-            st_n[sp] = n2;
-            st_state[sp] = 0;
-        } else if (st_state[sp] == 1) {
-            st_a[sp] = ret;
-            st_state[sp] = 2;
-            ++sp;
-            st_n[sp] = n0 - n2;
-            st_state[sp] = 0;
+// the node at depth d on path `path` (bit d-1 first; 0 = left); false if a
+// leaf ends the path earlier
+__device__ __forceinline__ bool pw_node_at(int32_t n, int d, int path, int32_t& s0, int32_t& n0) {
+    s0 = 0;
+    n0 = n;
+    for (int k = d - 1; k >= 0; --k) {
+        if (n0 <= 128) return false;
+        const int32_t n2 = pw_split(n0);
+        if ((path >> k) & 1) {
+            s0 += n2;
+            n0 -= n2;
         } else {
-            ret = st_a[sp] + ret;
-            --sp;
+            n0 = n2;
         }
     }
-    return ret;
+    return true;
 }
 
 // np.sum(a[0:n]) by one workgroup: numpy reduces in buffer-sized chunks of
 // 8192 elements, accumulated sequentially from 0.0, each chunk summed
 // pairwise.  Leaves are summed in parallel (full chunks: 64 leaves of 128;
-// the last chunk's leaves listed once by thread 0), chunk trees combined
-// one chunk per thread, chunks added in order.  leaf_sum is this call's
-// private global scratch (capacity >= n / 56 + 1).  Every thread returns
-// the sum.
+// the tail chunk's leaves found by register descents), the full chunks'
+// balanced trees combined one chunk per thread, the tail's tree level by
+// level, chunks added in order.  leaf_sum is this call's private global
+// scratch (capacity >= n / 56 + 1).  Every thread returns the sum.
 __device__ double block_np_sum(const double* __restrict__ a, int64_t n, double* __restrict__ leaf_sum) {
 #pragma clang fp contract(off)
     __shared__ double chunk_sum[64];
-    __shared__ double tail_leaf[kTailLeaves];
-    __shared__ int32_t tail_s[kTailLeaves], tail_n[kTailLeaves];
-    __shared__ int tail_cnt;
+    __shared__ double tail_slot[kTailSlots];
     __shared__ double res_sh;
     const int64_t n_chunks = (n + kNpChunk - 1) / kNpChunk;
     const int64_t full = n / kNpChunk;
-    const int64_t tail = n - full * kNpChunk;
+    const int32_t tail = (int32_t)(n - full * kNpChunk);
+    const int64_t n_full_leaves = full * kNpChunkLeaves;
+    const int64_t total = n_full_leaves + (tail + 7) / 8;   // full leaves + tail positions
     __syncthreads();   // a[] was just written by the other threads of the block
-    if (threadIdx.x == 0) tail_cnt = tail ? pw_leaf_list((int32_t)tail, tail_s, tail_n) : 0;
-    __syncthreads();
-    const int64_t total = full * kNpChunkLeaves + tail_cnt;
     // leaves: 8 lanes per leaf, lane j accumulating pairwise_sum's r_j (the
     // stride-8 elements j, j + 8, ... in order -- all its loads in flight at
     // once), the ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) combine by
-    // xor shuffles, then lane 0 adds the leaf's last n % 8 elements in order
+    // xor shuffles, then lane 0 adds the leaf's last n % 8 elements in order.
+    // Tail positions that do not start a leaf have len 0 (uniform per group).
     for (int64_t t8 = threadIdx.x; t8 < total * 8; t8 += blockDim.x) {
         const int64_t t = t8 >> 3;
         const int j = (int)(t8 & 7);
         int64_t s, len;
-        if (t < full * kNpChunkLeaves) {
+        if (t < n_full_leaves) {
             s = t * 128;
             len = 128;
         } else {
-            s = full * kNpChunk + tail_s[t - full * kNpChunkLeaves];
-            len = tail_n[t - full * kNpChunkLeaves];
+            const int32_t p = (int32_t)(t - n_full_leaves) * 8;
+            int32_t s0, n0;
+            pw_leaf_at(tail, p, s0, n0);
+            s = full * kNpChunk + p;
+            len = s0 == p ? n0 : 0;
         }
         const double* x = a + s;
         const int64_t body = len - len % 8;
@@ -182,7 +161,7 @@ __device__ double block_np_sum(const double* __restrict__ a, int64_t n, double* 
         r += __shfl_xor(r, 1);
         r += __shfl_xor(r, 2);
         r += __shfl_xor(r, 4);
-        if (j == 0) {
+        if (j == 0 && (t < n_full_leaves || len > 0)) {
             double res;
             if (len < 8) {
                 res = 0.0;
@@ -191,13 +170,26 @@ __device__ double block_np_sum(const double* __restrict__ a, int64_t n, double* 
                 res = r;
                 for (int64_t i = body; i < len; ++i) res += x[i];
             }
-            if (t < full * kNpChunkLeaves) leaf_sum[t] = res;
-            else tail_leaf[t - full * kNpChunkLeaves] = res;   // the tail's tree walks LDS
+            if (t < n_full_leaves) leaf_sum[t] = res;
+            else tail_slot[t - n_full_leaves] = res;
         }
     }
     __syncthreads();
-    // chunk trees: one thread per chunk; sums beyond 64 chunks go through the
-    // leaf buffer's own slots (each chunk's first leaf slot is free once read)
+    // the tail's inner nodes, deepest level first: node (s0, n0) adds its
+    // right child's slot into its left child's (= its own) slot
+    if (tail > 128) {
+        for (int d = kPwDepth - 1; d >= 0; --d) {
+            for (int path = threadIdx.x; path < (1 << d); path += blockDim.x) {
+                int32_t s0, n0;
+                if (pw_node_at(tail, d, path, s0, n0) && n0 > 128)
+                    tail_slot[s0 / 8] = tail_slot[s0 / 8] + tail_slot[(s0 + pw_split(n0)) / 8];
+            }
+            __syncthreads();
+        }
+    }
+    // full chunk trees: one thread per chunk; sums beyond 64 chunks go
+    // through the leaf buffer's own slots (each chunk's first leaf slot is
+    // free once read)
     for (int64_t c = threadIdx.x; c < n_chunks; c += blockDim.x) {
         double v;
         if (c < full) {   // a full chunk's tree is perfectly balanced: pairs up, level by level
@@ -211,7 +203,7 @@ __device__ double block_np_sum(const double* __restrict__ a, int64_t n, double* 
                 for (int j = 0; j < w; ++j) t[j] = t[2 * j] + t[2 * j + 1];
             v = t[0];
         } else {
-            v = pw_tree_sum((int32_t)tail, tail_leaf);
+            v = tail_slot[0];
         }
         if (c < 64) chunk_sum[c] = v;
         else leaf_sum[c * kNpChunkLeaves] = v;
@@ -758,6 +750,7 @@ __global__ __launch_bounds__(kParzenBlock) void k_fold(
         d.centre = centre;
         const bool bounded = (d.flags & 3) != 0;
         const double sK = sqrt(kExpScale), l2e = 1.4426950408889634;
+#pragma unroll   // constant side: d's fields stay in registers
         for (int side = 0; side < 2; ++side) {
             const int64_t o = side ? oa : ob, K = side ? Ka : Kb;
             double p_accept = 1.0;
