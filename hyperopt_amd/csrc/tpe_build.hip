@@ -48,6 +48,8 @@ constexpr int kPartBlock = 1024;
 constexpr int kParzenBlock = 1024;
 constexpr int kMaxLF = 64;          // below-list capacity per label (lf <= kMaxLF)
 constexpr int kCatChunk = 8192;     // categorical bincount: observations staged in LDS
+constexpr int kCatFewBins = 32;     // categorical bincount by ordered bin compaction up to here
+constexpr int kCatFewChunk = 4096;  // its chunk: 64 groups of 64 (one wave scans the groups)
 
 // ------------------------------------------------ numpy pairwise summation --
 // np.sum of a contiguous float64 vector: chunks of 8192 (numpy's reduction
@@ -524,6 +526,114 @@ __global__ __launch_bounds__(kPartBlock) void k_partition(
     }
 }
 
+// np.bincount(obs, weights=lf, minlength=upper) for upper <= kCatFewBins:
+// every bin is a sequential sum in observation order, so the work is
+// reordered around that chain instead of walking the list once per bin.
+// Per chunk of kCatFewChunk observations:
+//   1. per 64-observation group, a ballot per bin -> the group's bin counts;
+//   2. one wave per bin scans its counts over the (<= 64) groups, and wave 0
+//      scans the bin totals: every observation's slot in a bin-major list
+//      whose bins keep observation order (a stable counting sort);
+//   3. each observation's weight goes to its slot;
+//   4. lane 0 of one wave per bin adds its bin's run in order, 16 LDS reads
+//      in flight per batch -- the same additions, in the same order, as
+//      np.bincount's loop.
+// `out` (= w + o, zeroed) receives the counts; cbin is the caller's LDS.
+__device__ void cat_bincount_few(const double* __restrict__ list, int64_t n, int32_t upper,
+                                 const LFRamp& ramp, double* __restrict__ out,
+                                 int32_t* __restrict__ cbin) {
+#pragma clang fp contract(off)
+    constexpr int kGroups = kCatFewChunk / 64;
+    static_assert(kGroups <= 64, "one wave scans the groups");
+    static_assert(kCatFewChunk <= kCatChunk, "cbin holds a chunk");
+    __shared__ double cw[kCatFewChunk];
+    __shared__ int32_t gcnt[kGroups][kCatFewBins];
+    __shared__ int32_t btot[kCatFewBins], bbase[kCatFewBins];
+    __shared__ double bsum[kCatFewBins];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    constexpr int kWaves = kParzenBlock / 64;
+    if (tid < upper) bsum[tid] = 0.0;
+    for (int64_t c0 = 0; c0 < n; c0 += kCatFewChunk) {
+        const int m = (int)(n - c0 < kCatFewChunk ? n - c0 : kCatFewChunk);
+        const int groups = (m + 63) / 64;
+        // 1. bin ids (-1: not a bin) and per-group counts
+        for (int g = wave; g < groups; g += kWaves) {
+            const int i = g * 64 + lane;
+            int32_t cb = -1;
+            if (i < m) {
+                const double v = list[c0 + i];   // (int64_t)v == b for some bin b, else -1
+                cb = (v > -1.0 && v < (double)upper) ? (int32_t)(int64_t)v : -1;
+                cbin[i] = cb;
+            }
+            for (int b = 0; b < upper; ++b) {
+                const uint64_t mb = __ballot(cb == b);
+                if (lane == b) gcnt[g][b] = __popcll(mb);
+            }
+        }
+        __syncthreads();
+        // 2. exclusive prefix of each bin's counts over the groups; bin totals
+        for (int b = wave; b < upper; b += kWaves) {
+            const int v = lane < groups ? gcnt[lane][b] : 0;
+            int inc = v;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int u = __shfl_up(inc, d);
+                if (lane >= d) inc += u;
+            }
+            if (lane < groups) gcnt[lane][b] = inc - v;
+            if (lane == 63) btot[b] = inc;
+        }
+        __syncthreads();
+        if (wave == 0) {
+            const int v = lane < upper ? btot[lane] : 0;
+            int inc = v;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int u = __shfl_up(inc, d);
+                if (lane >= d) inc += u;
+            }
+            if (lane < upper) bbase[lane] = inc - v;
+        }
+        __syncthreads();
+        // 3. weights to their slots (rank within the group's bin by mbcnt)
+        for (int g = wave; g < groups; g += kWaves) {
+            const int i = g * 64 + lane;
+            const int32_t cb = i < m ? cbin[i] : -1;
+            uint64_t own = 0;
+            for (int b = 0; b < upper; ++b) {
+                const uint64_t mb = __ballot(cb == b);
+                if (cb == b) own = mb;
+            }
+            if (cb >= 0) {
+                const int below = (int)__builtin_amdgcn_mbcnt_hi(
+                    (uint32_t)(own >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)own, 0u));
+                cw[bbase[cb] + gcnt[g][cb] + below] = lf_weight(c0 + i, ramp);
+            }
+        }
+        __syncthreads();
+        // 4. each bin's run, in order, by one lane
+        for (int b = wave; b < upper; b += kWaves) {
+            if (lane == 0) {
+                const double* run = cw + bbase[b];
+                const int cnt = btot[b];
+                double acc = bsum[b];
+                int k = 0;
+                for (; k + 16 <= cnt; k += 16) {
+                    double v[16];
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) v[j] = run[k + j];
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) acc += v[j];
+                }
+                for (; k < cnt; ++k) acc += run[k];
+                bsum[b] = acc;
+            }
+        }
+        __syncthreads();
+    }
+    if (tid < upper) out[tid] = bsum[tid];
+}
+
 // adaptive_parzen_normal (tpe.py:404-477) / categorical pseudocounts
 // (tpe.py:581-617) of one (label, side).  Output: (w, mu, sigma) at
 // mix_off[2 l + side], component count in kcount[2 l + side].
@@ -549,49 +659,55 @@ __global__ __launch_bounds__(kParzenBlock) void k_parzen(
         // weights = linear_forgetting_weights(len(obs)); counts = bincount(obs,
         // minlength=upper, weights) -- each bin a sequential sum in
         // observation order; pseudocounts; / np.sum(pseudocounts)
-        // One wave per bin: ballots over the list find the bin's observations
-        // in order, and the wave adds their weights one by one through scalar
-        // registers (v_readlane) -- the sequential order of np.bincount.  The
-        // list goes through LDS as bin ids, kCatChunk observations at a time
-        // (coalesced loads by the whole block; the waves then scan LDS).
+        // Up to kCatFewBins bins: ordered compaction by bin, then one lane
+        // per bin adds its run (cat_bincount_few).  More bins: one wave per
+        // bin; ballots over the list find the bin's observations in order,
+        // and the wave adds their weights one by one through scalar registers
+        // (v_readlane) -- the sequential order of np.bincount.  The list goes
+        // through LDS as bin ids, kCatChunk observations at a time (coalesced
+        // loads by the whole block; the waves then scan LDS).
         const double* list = side == 0 ? below_val + (size_t)l * kMaxLF : keys_unsorted + off;
         const int32_t upper = sp.upper;
         const LFRamp ramp = lf_ramp(n, lf);
         const int wave = tid >> 6, lane = tid & 63;
         __shared__ int32_t cbin[kCatChunk];
         for (int b = tid; b < upper; b += kParzenBlock) w[o + b] = 0.0;
-        for (int64_t c0 = 0; c0 < n; c0 += kCatChunk) {
-            const int64_t m = n - c0 < kCatChunk ? n - c0 : kCatChunk;
-            for (int64_t i = tid; i < m; i += kParzenBlock) {
-                const double v = list[c0 + i];   // (int64_t)v == b for some bin b, else -1
-                cbin[i] = (v > -1.0 && v < (double)upper) ? (int32_t)(int64_t)v : -1;
-            }
-            __syncthreads();
-            for (int b = wave; b < upper; b += kParzenBlock / 64) {
-                double cnt = w[o + b];
-                for (int64_t i0 = 0; i0 < m; i0 += 64) {
-                    const int64_t i = i0 + lane;
-                    const bool hit = i < m && cbin[i] == b;
-                    uint64_t hm = __ballot(hit);
-                    if (!hm) continue;
-                    const double wl = hit ? lf_weight(c0 + i, ramp) : 0.0;
-                    int64_t bits;
-                    __builtin_memcpy(&bits, &wl, 8);
-                    const int lo = (int)(uint32_t)bits, hi = (int)(uint32_t)(bits >> 32);
-                    while (hm) {
-                        const int j = __builtin_ctzll(hm);
-                        hm &= hm - 1;
-                        const uint64_t vb =
-                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, j) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane(lo, j);
-                        double v;
-                        __builtin_memcpy(&v, &vb, 8);
-                        cnt += v;
-                    }
+        if (upper <= kCatFewBins) {
+            cat_bincount_few(list, n, upper, ramp, w + o, cbin);
+        } else {   // many bins: one wave per bin walks the list
+            for (int64_t c0 = 0; c0 < n; c0 += kCatChunk) {
+                const int64_t m = n - c0 < kCatChunk ? n - c0 : kCatChunk;
+                for (int64_t i = tid; i < m; i += kParzenBlock) {
+                    const double v = list[c0 + i];   // (int64_t)v == b for some bin b, else -1
+                    cbin[i] = (v > -1.0 && v < (double)upper) ? (int32_t)(int64_t)v : -1;
                 }
-                if (lane == 0) w[o + b] = cnt;
+                __syncthreads();
+                for (int b = wave; b < upper; b += kParzenBlock / 64) {
+                    double cnt = w[o + b];
+                    for (int64_t i0 = 0; i0 < m; i0 += 64) {
+                        const int64_t i = i0 + lane;
+                        const bool hit = i < m && cbin[i] == b;
+                        uint64_t hm = __ballot(hit);
+                        if (!hm) continue;
+                        const double wl = hit ? lf_weight(c0 + i, ramp) : 0.0;
+                        int64_t bits;
+                        __builtin_memcpy(&bits, &wl, 8);
+                        const int lo = (int)(uint32_t)bits, hi = (int)(uint32_t)(bits >> 32);
+                        while (hm) {
+                            const int j = __builtin_ctzll(hm);
+                            hm &= hm - 1;
+                            const uint64_t vb =
+                                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, j) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane(lo, j);
+                            double v;
+                            __builtin_memcpy(&v, &vb, 8);
+                            cnt += v;
+                        }
+                    }
+                    if (lane == 0) w[o + b] = cnt;
+                }
+                __syncthreads();
             }
-            __syncthreads();
         }
         __syncthreads();
         for (int b = tid; b < upper; b += kParzenBlock) {

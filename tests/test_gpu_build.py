@@ -102,6 +102,19 @@ def test_build_all_kinds_bit_exact(eng, n_trials):
     _check_bit_exact(eng, hist, oracle_mixtures(hist))
 
 
+@pytest.mark.parametrize('n_trials', [4095, 4097, 9000])
+def test_build_categorical_bin_counts(eng, n_trials):
+    """Categorical bincounts on both device paths -- ordered compaction by bin
+    (upper <= 32, chunks of 4096) and wave-per-bin walks (upper > 32, chunks
+    of 8192) -- across chunk boundaries, with empty bins: bit-exact."""
+    labels = [('r2', 'randint', dict(upper=2)), ('r32', 'randint', dict(upper=32)),
+              ('r33', 'randint', dict(upper=33)), ('r200', 'randint', dict(upper=200)),
+              ('pc', 'categorical', dict(upper=6, p=[0.5, 0.0, 0.2, 0.1, 0.1, 0.1]))]
+    hist = make_history(labels, n_trials, seed=n_trials, active_frac=0.9)
+    _build(eng, hist)
+    _check_bit_exact(eng, hist, oracle_mixtures(hist))
+
+
 def test_build_conditional_ties_orphans(eng):
     """Labels active in subsets, tied losses, observations of trials without
     a loss entry (dropped from both sets, tpe.py:639-646)."""
