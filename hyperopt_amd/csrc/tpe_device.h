@@ -492,12 +492,12 @@ __device__ __forceinline__ void quant_bounds(const DLabel& L, double x, double& 
 
 // Lane-strided share of prob = sum_k [w Phi(ub) - w Phi(lb)] (components
 // k = lane, lane+64, ...); the wave sums the 64 shares afterwards.
-template <bool LOG>
+template <bool LOG, int STRIDE = 64>
 __device__ __forceinline__ double quant_share(const Comp<double>* __restrict__ c, int n, double ub,
                                               double lb, int lane) {
 #pragma clang fp contract(off)
     double prob = 0.0;
-    for (int k = lane; k < n; k += 64) {
+    for (int k = lane; k < n; k += STRIDE) {
         const double mu = c[k].mu, a = c[k].a, w = c[k].w;
         double pu, pl;
         if (LOG) {

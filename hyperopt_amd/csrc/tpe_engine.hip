@@ -21,7 +21,7 @@
 //   k_sample_small / k_score_slices / k_finish_slices
 //                             split-K map of small rounds (C * rounds <= 2048)
 //   k_qsample<MODE>           quantized families: draw, store grid index j, min/max
-//   k_qtable<MODE>            one wave per distinct grid value: lpdf pair
+//   k_qtable<MODE>            one workgroup per distinct grid value: lpdf pair
 //   k_qscan<MODE>             per candidate: table lookup -> block maxloc
 //   k_reduce / k_emit         per (round, label) winner over the partials
 #include <hip/hip_runtime.h>
@@ -654,8 +654,9 @@ __global__ __launch_bounds__(kBlock) void k_qsample(
     }
 }
 
-// Quantized families, pass 2: one wave per distinct grid value x = j * q,
-// lane-strided component sums for both mixtures, written once to the table.
+// Quantized families, pass 2: one workgroup per distinct grid value x = j * q
+// (a wave each left config 5's ~2.6k waves at 0.59 VALU busy), thread-strided
+// component sums for both mixtures, written once to the table.
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_qtable(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
@@ -664,16 +665,28 @@ __global__ __launch_bounds__(kBlock) void k_qtable(
     const int li = group[blockIdx.y];
     const DLabel L = labels[li];
     const QInfo Q = qinfo[qbase + blockIdx.y];
-    const int lane = threadIdx.x & 63;
-    const int64_t s = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-    if (s >= Q.G) return;
+    const int64_t s = blockIdx.x;
+    if (s >= Q.G) return;   // uniform over the workgroup
     const double x = (double)(Q.jmin + s) * L.q;
     double ub, lo;
     bool neg;
     quant_bounds<MODE>(L, x, ub, lo, neg);
-    const double pb = wave_sum(quant_share<MODE == QUANT_LGMM>(comps64 + L.comp_b, L.nb, ub, lo, lane));
-    const double pa = wave_sum(quant_share<MODE == QUANT_LGMM>(comps64 + L.comp_a, L.na, ub, lo, lane));
-    if (lane == 0) tab[Q.tab_off + s] = make_double2(log(pb) - L.logpacc_b, log(pa) - L.logpacc_a);
+    constexpr bool kLog = MODE == QUANT_LGMM;
+    double pb = wave_sum(quant_share<kLog, kBlock>(comps64 + L.comp_b, L.nb, ub, lo, threadIdx.x));
+    double pa = wave_sum(quant_share<kLog, kBlock>(comps64 + L.comp_a, L.na, ub, lo, threadIdx.x));
+    __shared__ double2 wp[kBlock / 64];
+    if ((threadIdx.x & 63) == 0) wp[threadIdx.x >> 6] = make_double2(pb, pa);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        pb = wp[0].x;
+        pa = wp[0].y;
+#pragma unroll
+        for (int w = 1; w < kBlock / 64; ++w) {
+            pb += wp[w].x;
+            pa += wp[w].y;
+        }
+        tab[Q.tab_off + s] = make_double2(log(pb) - L.logpacc_b, log(pa) - L.logpacc_a);
+    }
 }
 
 // Quantized families, pass 3: per candidate look up its grid value's lpdf
@@ -1069,7 +1082,7 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
         if (!cnt) continue;
         if (mode != first_mode) bracket(ctx, mode, 0);
         if (maxG > 0) {
-            dim3 tg((unsigned)((maxG + kBlock / 64 - 1) / (kBlock / 64)), cnt, 1);
+            dim3 tg((unsigned)maxG, cnt, 1);
             if (fam)
                 hipLaunchKernelGGL(k_qtable<QUANT_LGMM>, tg, dim3(kBlock), 0, ctx->stream,
                                    ctx->P->labels.p, g.dev[mode], ctx->P->comps64.p, ctx->qinfo.p, nq,
