@@ -263,8 +263,9 @@ __device__ __forceinline__ double np_minimum(double a, double b) { return (a != 
 // ap_filter_trials' split (tpe.py:636-645): flag the n_below lowest losses,
 // ties by position.  Radix select in one workgroup: 8 passes of 8-bit digits
 // over the order-preserving 64-bit keys locate the n_below-th smallest key
-// K* (LDS histograms), then one ordered pass flags every key < K* and the
-// first (by position) of the keys == K* that complete n_below.
+// K* (LDS histograms, wave-aggregated adds), then one pass flags every key
+// < K* and the first (by position) of the keys == K* that complete n_below
+// -- an ordered pass only when some keys == K* stay out.
 __global__ __launch_bounds__(kSplitBlock) void k_split(const double* __restrict__ losses, int64_t T,
                                                        int32_t n_below, uint8_t* __restrict__ below) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -274,6 +275,7 @@ __global__ __launch_bounds__(kSplitBlock) void k_split(const double* __restrict_
     __shared__ int wcnt[kSplitBlock / 64];
     __shared__ uint32_t wsum[4];
     __shared__ int64_t base_sh;
+    __shared__ uint32_t eq_sh;
     for (int64_t i = tid; i < T; i += kSplitBlock) below[i] = 0;
     if (n_below <= 0 || T <= 0) return;
     if (tid == 0) {
@@ -285,10 +287,19 @@ __global__ __launch_bounds__(kSplitBlock) void k_split(const double* __restrict_
         for (int b = tid; b < 256; b += kSplitBlock) hist[b] = 0;
         __syncthreads();
         const uint64_t prefix = prefix_sh;
-#pragma unroll 4
+        // the high digits of similar losses are mostly equal: the lanes that
+        // share the first participating lane's digit add once per wave
         for (int64_t i = tid; i < T; i += kSplitBlock) {
             const uint64_t k = asc_key(losses[i]);
-            if ((k & mask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+            const bool part = (k & mask) == prefix;
+            const uint32_t d = (uint32_t)(k >> shift) & 255u;
+            const uint64_t pm = __ballot(part);
+            if (!pm) continue;
+            const int first = __builtin_ctzll(pm);
+            const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)d, first);
+            const uint64_t same = __ballot(part && d == d0);
+            if (lane == first) atomicAdd(&hist[d0], (uint32_t)__popcll(same));
+            else if (part && d != d0) atomicAdd(&hist[d], 1u);
         }
         __syncthreads();
         // the digit holding the need-th key: inclusive scan of the histogram
@@ -312,6 +323,7 @@ __global__ __launch_bounds__(kSplitBlock) void k_split(const double* __restrict_
             if ((int64_t)excl < need && (int64_t)incl >= need) {
                 need_sh = need - excl;
                 prefix_sh = prefix | ((uint64_t)tid << shift);
+                eq_sh = h;   // after the last digit: the number of keys == K*
             }
         }
         mask |= 255ull << shift;
@@ -319,6 +331,11 @@ __global__ __launch_bounds__(kSplitBlock) void k_split(const double* __restrict_
     }
     const uint64_t kstar = prefix_sh;
     const int64_t take_eq = need_sh;      // how many keys == K* join, in position order
+    if (take_eq == (int64_t)eq_sh) {      // every key == K* joins: no position order needed
+        for (int64_t i = tid; i < T; i += kSplitBlock)
+            if (asc_key(losses[i]) <= kstar) below[i] = 1;
+        return;
+    }
     if (tid == 0) base_sh = 0;
     __syncthreads();
     const uint64_t lt = (1ull << lane) - 1ull;
