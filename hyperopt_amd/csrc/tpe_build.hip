@@ -839,6 +839,44 @@ __device__ double block_max(double v) {
 
 __device__ double block_min(double v) { return -block_max(-v); }
 
+// k_fold's per-component transcendentals, spread over the chip (one
+// workgroup per label would do them on one CU): the p_accept terms
+// w (Phi(high) - Phi(low)) of bounded GMM1 / quantized mixtures, and the
+// log-density constant -- w / sqrt(2 pi sigma^2) for GMM1 (k_fold divides by
+// p_accept and takes the log, the reference's order), the whole
+// log w - log(max(sigma, EPS) sqrt(2 pi)) for LGMM1 -- and the records'
+// scale sqrt(1/2) / max(sigma, EPS).  Grid (slices, labels, sides).
+constexpr int kTermBlock = 256;
+__global__ __launch_bounds__(kTermBlock) void k_fold_terms(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ kcount,
+    const int64_t* __restrict__ mix_off, const double* __restrict__ w, const double* __restrict__ mu,
+    const double* __restrict__ sigma, double* __restrict__ terms, double* __restrict__ cterm,
+    double* __restrict__ ascale) {
+#pragma clang fp contract(off)
+    const int l = blockIdx.y, side = blockIdx.z;
+    const int mode = labels[l].mode;
+    if (mode == CAT) return;
+    const int64_t K = kcount[2 * l + side];
+    const int64_t k = (int64_t)blockIdx.x * kTermBlock + threadIdx.x;
+    if (k >= K) return;
+    const int64_t o = mix_off[2 * l + side];
+    const bool quant = mode == QUANT_GMM || mode == QUANT_LGMM;
+    const bool is_lgmm = mode == DENSE_LGMM || mode == QUANT_LGMM;
+    const double wk = w[o + k], mk = mu[o + k], sg = sigma[o + k];
+    if ((labels[l].flags & 3) != 0 && (quant || !is_lgmm))   // tpe.py:139-142 / 279-282
+        terms[o + k] = wk * (dev_normal_cdf(labels[l].high, mk, sg) -
+                             dev_normal_cdf(labels[l].low, mk, sg));
+    if (quant) return;
+    ascale[o + k] = sqrt(0.5) / fmax(sg, kEps);   // the records' 1 / (sqrt 2 max(sigma, EPS))
+    if (!is_lgmm) {   // log(w / sqrt(2 pi sigma^2) / p_accept), tpe.py:148-150
+        const double Z = sqrt(2.0 * M_PI * (sg * sg));
+        cterm[o + k] = wk / Z;
+    } else {          // log w - log(max(sigma,EPS) sqrt(2 pi)), tpe.py:199-208
+        const double s = fmax(sg, kEps);
+        cterm[o + k] = log(wk) - log(s * sqrt(2.0 * M_PI));
+    }
+}
+
 // The fold of tpe_set_posterior (tpe_engine.hip:fold_mixture) on the device:
 // p_accept, the LSE shift M, the recentred exp-scaled fp64 records, fp32
 // records, the below mixture's sampling records and the DLabel fields.
@@ -846,8 +884,8 @@ __global__ __launch_bounds__(kParzenBlock) void k_fold(
     DLabel* __restrict__ labels, const int32_t* __restrict__ kcount,
     const int64_t* __restrict__ mix_off, const double* __restrict__ w, const double* __restrict__ mu,
     const double* __restrict__ sigma, Comp<double>* __restrict__ c64, Comp<float>* __restrict__ c32,
-    SampRec* __restrict__ samp, double* __restrict__ terms,
-    double* __restrict__ leaf_sum, int32_t* __restrict__ err) {
+    SampRec* __restrict__ samp, const double* __restrict__ terms, double* __restrict__ cterm,
+    const double* __restrict__ ascale, double* __restrict__ leaf_sum, int32_t* __restrict__ err) {
 #pragma clang fp contract(off)
     const int l = blockIdx.x, tid = threadIdx.x;
     DLabel d = labels[l];
@@ -886,13 +924,9 @@ __global__ __launch_bounds__(kParzenBlock) void k_fold(
 #pragma unroll   // constant side: d's fields stay in registers
         for (int side = 0; side < 2; ++side) {
             const int64_t o = side ? oa : ob, K = side ? Ka : Kb;
-            double p_accept = 1.0;
-            if (bounded) {  // tpe.py:139-142 / 279-282
-                for (int64_t k = tid; k < K; k += kParzenBlock)
-                    terms[o + k] = w[o + k] * (dev_normal_cdf(d.high, mu[o + k], sigma[o + k]) -
-                                               dev_normal_cdf(d.low, mu[o + k], sigma[o + k]));
+            double p_accept = 1.0;   // (unused by dense LGMM1, tpe.py:265-307)
+            if (bounded && (quant || !is_lgmm))   // terms from k_fold_terms
                 p_accept = block_np_sum(terms + o, K, leaf_sum + o);
-            }
             if (quant) {
                 (side ? d.logpacc_a : d.logpacc_b) = log(p_accept);
                 for (int64_t k = tid; k < K; k += kParzenBlock) {
@@ -904,25 +938,18 @@ __global__ __launch_bounds__(kParzenBlock) void k_fold(
             }
             double M = -INFINITY;
             for (int64_t k = tid; k < K; k += kParzenBlock) {
-                const double sg = sigma[o + k];
-                double c;
-                if (!is_lgmm) {  // log(w / sqrt(2 pi sigma^2) / p_accept), tpe.py:148-150
-                    const double Z = sqrt(2.0 * M_PI * (sg * sg));
-                    c = log(w[o + k] / Z / p_accept);
-                } else {         // log w - log(max(sigma,EPS) sqrt(2 pi)), tpe.py:199-208
-                    const double s = fmax(sg, kEps);
-                    c = log(w[o + k]) - log(s * sqrt(2.0 * M_PI));
-                }
-                terms[o + k] = c;
+                // GMM1: (w / Z) from k_fold_terms, then / p_accept and log
+                // (tpe.py:148-150); LGMM1: the whole constant (tpe.py:199-208)
+                const double c = !is_lgmm ? log(cterm[o + k] / p_accept) : cterm[o + k];
+                cterm[o + k] = c;
                 M = fmax(M, c);
             }
             M = block_max(M);
             if (!isfinite(M)) M = 0.0;
             (side ? d.shift_a : d.shift_b) = M;
             for (int64_t k = tid; k < K; k += kParzenBlock) {
-                const double s = fmax(sigma[o + k], kEps);
-                const double a = sqrt(0.5) / s;
-                const double c = terms[o + k];
+                const double a = ascale[o + k];
+                const double c = cterm[o + k];
                 c64[o + k] = Comp<double>{(mu[o + k] - centre) * (a * sK), a * sK, (c - M) * kExpScale,
                                           w[o + k]};
                 c32[o + k] = Comp<float>{(float)mu[o + k], (float)(a * sqrt(l2e)), (float)((c - M) * l2e),
@@ -1158,7 +1185,7 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     std::vector<DLabel> dl(n_labels);
     std::vector<int64_t> mix(2 * (size_t)n_labels);
     std::vector<int32_t> grp[kNumModes];
-    int64_t total = 0, samp_total = 0;
+    int64_t total = 0, samp_total = 0, max_cap = 1;
     for (int32_t l = 0; l < n_labels; ++l) {
         const tpe_label_spec& s = B.specs_h[l];
         DLabel& o = dl[l];
@@ -1184,6 +1211,7 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
         total += cap_b;
         o.comp_a = mix[2 * l + 1] = total;
         total += cap_a;
+        max_cap = std::max(max_cap, std::max(cap_b, cap_a));
         o.samp_off = samp_total;
         samp_total += cap_b;
         grp[o.mode].push_back(l);
@@ -1201,7 +1229,7 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     HIPCHK(ctx, B.mu.reserve(total));
     HIPCHK(ctx, B.sigma.reserve(total));
     HIPCHK(ctx, B.mix_off.reserve(2 * (size_t)n_labels));
-    HIPCHK(ctx, B.scratch.reserve(2 * (size_t)total));
+    HIPCHK(ctx, B.scratch.reserve(4 * (size_t)total));   // terms | leaf sums | constants | scales
     HIPCHK(ctx, P.labels.reserve(n_labels));
     HIPCHK(ctx, P.comps64.reserve(total));
     HIPCHK(ctx, P.comps32.reserve(total));
@@ -1221,9 +1249,13 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     hipLaunchKernelGGL(k_parzen, dim3(n_labels, 2), dim3(kParzenBlock), 0, st, B.specs.p, B.cat_p.p,
                        B.p_off.p, B.counts.p, B.below_val.p, B.keys.p, B.keys.p, B.idx.p, B.mix_off.p,
                        prior_weight, lf, B.w.p, B.mu.p, B.sigma.p, B.kcount.p, B.scratch.p + total);
+    hipLaunchKernelGGL(k_fold_terms, dim3((unsigned)((max_cap + kTermBlock - 1) / kTermBlock), n_labels, 2),
+                       dim3(kTermBlock), 0, st, P.labels.p, B.kcount.p, B.mix_off.p, B.w.p, B.mu.p,
+                       B.sigma.p, B.scratch.p, B.scratch.p + 2 * total, B.scratch.p + 3 * total);
     hipLaunchKernelGGL(k_fold, dim3(n_labels), dim3(kParzenBlock), 0, st, P.labels.p, B.kcount.p,
                        B.mix_off.p, B.w.p, B.mu.p, B.sigma.p, P.comps64.p, P.comps32.p, P.samp.p,
-                       B.scratch.p, B.scratch.p + total, ctx->errflag.p);
+                       B.scratch.p, B.scratch.p + 2 * total, B.scratch.p + 3 * total, B.scratch.p + total,
+                       ctx->errflag.p);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(ctx->ev1, st));
     int32_t errh = 0;
