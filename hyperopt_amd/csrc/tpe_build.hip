@@ -379,6 +379,41 @@ __global__ __launch_bounds__(kBlock) void k_hist_append(
     }
 }
 
+// Large appends (a whole history at once) sort the staging batch with two
+// chip-wide stable radix sorts instead of one block per label: by value, then
+// by label.  Same key order and tie order as the segmented sort.
+constexpr int64_t kGlobalSortMin = 4096;
+__global__ __launch_bounds__(kBlock) void k_iota(int32_t* __restrict__ g, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+        g[i] = (int32_t)i;
+}
+
+// label of each staging position (upper bound in the CSR offsets, minus one)
+__global__ __launch_bounds__(kBlock) void k_label_of(
+    const int64_t* __restrict__ st_off, int32_t L, const int32_t* __restrict__ g,
+    uint32_t* __restrict__ lab, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        const int64_t p = g[i];
+        int32_t lo = 0, hi = L + 1;
+        while (lo < hi) {
+            const int32_t mid = (lo + hi) >> 1;
+            if (st_off[mid] <= p) lo = mid + 1; else hi = mid;
+        }
+        lab[i] = (uint32_t)(lo - 1);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_sorted_gather(
+    const int32_t* __restrict__ g, const double* __restrict__ st_val,
+    const int32_t* __restrict__ st_idx, double* __restrict__ key_out,
+    int32_t* __restrict__ idx_out, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+        const int32_t p = g[i];
+        key_out[i] = st_val[p];
+        idx_out[i] = st_idx[p];
+    }
+}
+
 // copy every label's live prefix into a re-laid-out pool (growth)
 __global__ __launch_bounds__(kBlock) void k_hist_regrow(
     const int64_t* __restrict__ off_old, const int64_t* __restrict__ off_new,
@@ -1142,14 +1177,42 @@ int history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial,
                        dim3(kBlock), 0, sm, B.st_off.p, B.st_trial.p, B.st_val.p, B.p_off.p, B.cnt.p,
                        B.p_trial.p, B.p_val.p, B.st_idx.p);
     HIPCHK(ctx, hipGetLastError());
-    size_t bytes = 0;   // stable segmented radix sort of the new batch
-    HIPCHK(ctx, hipcub::DeviceSegmentedRadixSort::SortPairs(
-                    nullptr, bytes, B.st_val.p, B.st_key_sorted.p, B.st_idx.p, B.st_idx_sorted.p,
-                    (int)total, L, B.seg_begin.p, B.seg_end.p, 0, 64, sm));
-    HIPCHK(ctx, B.sort_tmp.reserve(std::max<size_t>(bytes, 1)));
-    HIPCHK(ctx, hipcub::DeviceSegmentedRadixSort::SortPairs(
-                    B.sort_tmp.p, bytes, B.st_val.p, B.st_key_sorted.p, B.st_idx.p, B.st_idx_sorted.p,
-                    (int)total, L, B.seg_begin.p, B.seg_end.p, 0, 64, sm));
+    if (total >= kGlobalSortMin) {
+        // two stable chip-wide sorts: by value, then by label
+        HIPCHK(ctx, B.gs_a.reserve(total));
+        HIPCHK(ctx, B.gs_b.reserve(total));
+        HIPCHK(ctx, B.gs_lab.reserve(total));
+        HIPCHK(ctx, B.gs_lab2.reserve(total));
+        int lab_bits = 1;
+        while ((1LL << lab_bits) < (int64_t)L) ++lab_bits;
+        const unsigned gb = (unsigned)std::min<int64_t>((total + kBlock - 1) / kBlock, 2048);
+        hipLaunchKernelGGL(k_iota, dim3(gb), dim3(kBlock), 0, sm, B.gs_a.p, total);
+        HIPCHK(ctx, hipGetLastError());
+        size_t b1 = 0, b2 = 0;
+        HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, b1, B.st_val.p, B.st_key_sorted.p, B.gs_a.p,
+                                                         B.gs_b.p, (int)total, 0, 64, sm));
+        HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, b2, B.gs_lab.p, B.gs_lab2.p, B.gs_b.p,
+                                                         B.gs_a.p, (int)total, 0, lab_bits, sm));
+        HIPCHK(ctx, B.sort_tmp.reserve(std::max<size_t>(std::max(b1, b2), 1)));
+        HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(B.sort_tmp.p, b1, B.st_val.p, B.st_key_sorted.p,
+                                                         B.gs_a.p, B.gs_b.p, (int)total, 0, 64, sm));
+        hipLaunchKernelGGL(k_label_of, dim3(gb), dim3(kBlock), 0, sm, B.st_off.p, L, B.gs_b.p, B.gs_lab.p, total);
+        HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(B.sort_tmp.p, b2, B.gs_lab.p, B.gs_lab2.p, B.gs_b.p,
+                                                         B.gs_a.p, (int)total, 0, lab_bits, sm));
+        hipLaunchKernelGGL(k_sorted_gather, dim3(gb), dim3(kBlock), 0, sm, B.gs_a.p, B.st_val.p, B.st_idx.p,
+                           B.st_key_sorted.p, B.st_idx_sorted.p, total);
+        HIPCHK(ctx, hipGetLastError());
+    } else {
+        size_t bytes = 0;   // stable segmented radix sort of the new batch
+        HIPCHK(ctx, hipcub::DeviceSegmentedRadixSort::SortPairs(
+                        nullptr, bytes, B.st_val.p, B.st_key_sorted.p, B.st_idx.p, B.st_idx_sorted.p,
+                        (int)total, L, B.seg_begin.p, B.seg_end.p, 0, 64, sm));
+        HIPCHK(ctx, B.sort_tmp.reserve(std::max<size_t>(bytes, 1)));
+        HIPCHK(ctx, hipcub::DeviceSegmentedRadixSort::SortPairs(
+                        B.sort_tmp.p, bytes, B.st_val.p, B.st_key_sorted.p, B.st_idx.p, B.st_idx_sorted.p,
+                        (int)total, L, B.seg_begin.p, B.seg_end.p, 0, 64, sm));
+    }
     hipLaunchKernelGGL(k_hist_merge, dim3((unsigned)std::min<int64_t>((mx_all + kBlock - 1) / kBlock, 1024), L),
                        dim3(kBlock), 0, sm, B.specs.p, B.p_off.p, B.cnt.p, B.st_off.p, B.s_key.p,
                        B.s_idx.p, B.st_key_sorted.p, B.st_idx_sorted.p, B.s_key2.p, B.s_idx2.p);

@@ -94,6 +94,8 @@ struct BuildBufs {
     DevBuf<double> st_val, st_key_sorted;
     DevBuf<int32_t> seg_begin, seg_end;
     DevBuf<uint8_t> sort_tmp;
+    DevBuf<int32_t> gs_a, gs_b;    // large appends: staging positions through the two sorts
+    DevBuf<uint32_t> gs_lab, gs_lab2; //   and the label of each position
     // per build
     DevBuf<double> losses;
     DevBuf<uint8_t> below;         // per trial: in the below set
@@ -112,7 +114,8 @@ struct BuildBufs {
         p_val.release(); s_key.release(); s_key2.release(); s_idx.release(); s_idx2.release();
         arank.release(); st_off.release(); st_trial.release(); st_idx.release();
         st_idx_sorted.release(); st_val.release(); st_key_sorted.release(); seg_begin.release();
-        seg_end.release(); sort_tmp.release(); losses.release(); below.release(); keys.release();
+        seg_end.release(); sort_tmp.release(); gs_a.release(); gs_b.release(); gs_lab.release();
+        gs_lab2.release(); losses.release(); below.release(); keys.release();
         idx.release(); below_val.release(); counts.release(); kcount.release(); w.release();
         mu.release(); sigma.release(); mix_off.release(); scratch.release();
         n_labels = 0;
