@@ -193,7 +193,9 @@ def test_resident_history_incremental(eng):
     every append, the same mixtures as the oracle on the history so far --
     with tied losses and values, conditional labels, pending trials (+inf)
     and NaN-loss trials (outside the history: their observations join
-    neither set, as the reference drops such docs)."""
+    neither set, as the reference drops such docs).  The 400 -> 1999 batch
+    (~9.6k staged observations) takes the chip-wide two-sort path of the
+    append (>= 4096), the others the per-label segmented sort."""
     from hyperopt_amd import posterior as P
     hist = make_history(ALL_KINDS, 2400, seed=21, active_frac=0.6, loss_round=1)
     losses = hist.losses.copy()
