@@ -3,7 +3,10 @@
 Workload (BASELINE.json configs[2], the metric's "10k-trial history"):
 32 hyperparameters, kind = i mod 5 in {uniform(-5,5), loguniform(-5,2),
 quniform(0,100,1), normal(0,3), choice(5)}, N = 10000 synthetic trials,
-2^21 EI candidates per label per GPU (2^24 at 8 GPUs, weak scaling).
+2^24 EI candidates per label in total, strong-scaled: each of the N ranks
+scores the contiguous global slice [rank C/N, (rank+1) C/N) (the Philox
+counter is the global candidate index, so the candidate set and the winner do
+not depend on N).
 
 One step = one fused suggestion round on the resident posterior: Philox
 sampling of every label's candidates from l(x), lpdf under l and g for every
@@ -59,13 +62,14 @@ def parse():
                     help='BASELINE.json config: 3 (headline, default), 2 (Hartmann-6, 2k '
                          'history, 2^20 candidates), 5 (128 labels, 50k history, batched '
                          'new_ids x 24 candidates)')
-    ap.add_argument('--rounds-per-gpu', type=int, default=512,
-                    help='config 5: new_ids per GPU per step (4096 over 8 GPUs)')
+    ap.add_argument('--new-ids', type=int, default=4096,
+                    help='config 5: new_ids per step in total, split over the ranks')
     ap.add_argument('--c5-history', type=int, default=50000,
                     help='config 5 history size (50000 = BASELINE.json; smaller only for experiments)')
     ap.add_argument('--labels', type=int, default=32)
     ap.add_argument('--trials', type=int, default=10000)
-    ap.add_argument('--cand-log2', type=int, default=21)
+    ap.add_argument('--cand-log2', type=int, default=24,
+                    help='log2 of the EI candidates per label in total (split over the ranks)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-sample', type=int, default=2048,
                     help='candidates per label in the single-core numpy baseline sample')
@@ -167,12 +171,13 @@ def measured_pmc(kernel_prefix):
 def workload_name(args, C):
     if args.config == 2:
         return 'config2: Hartmann-6 over hp.uniform, N=2000 history, 2^20 EI candidates ' \
-               'per label per GPU'
+               'per label (C/N per GPU)'
     if args.config == 5:
-        return 'config5: 128-dim mixed space, N=50000 history, %d new_ids per GPU per step ' \
-               'x 24 EI candidates' % args.rounds_per_gpu
-    return 'config3: %d-dim mixed space, N=%d history, 2^%d EI candidates per label per GPU' % (
-        args.labels, args.trials, args.cand_log2)
+        return 'config5: 128-dim mixed space, N=%d history, %d new_ids per step x 24 EI ' \
+               'candidates (new_ids split over the GPUs, winners all-gathered)' % (
+                   args.trials, args.new_ids)
+    return 'config3: %d-dim mixed space, N=%d history, 2^%d EI candidates per label ' \
+           '(C/N per GPU)' % (args.labels, args.trials, args.cand_log2)
 
 
 def main():
@@ -219,16 +224,26 @@ def main():
                   'host_numpy_ms': round(1e3 * t_host, 3),
                   'note': 'tpe_build_posterior (split, sort, Parzen, fold on the GPU; call '
                           'includes the H2D of the history) vs posterior.py + pack'}
-    C = 24 if args.config == 5 else 1 << args.cand_log2
+    C_total = 24 if args.config == 5 else 1 << args.cand_log2
+    if args.config == 5:
+        if args.new_ids % world:
+            raise SystemExit('--new-ids must divide over %d ranks' % world)
+        ids_local, C = args.new_ids // world, C_total
+    else:
+        if C_total % world:
+            raise SystemExit('2^%d candidates must divide over %d ranks' % (args.cand_log2, world))
+        C = C_total // world
     L = len(posts)
 
-    from hyperopt_amd.parallel import exchange_winners
+    from hyperopt_amd.parallel import exchange_winners, gather_rounds
 
     def step(i):
-        if args.config == 5:   # independent new_ids sharded over GPUs: no collective
-            ids = [(i * world + rank) * args.rounds_per_gpu + k
-                   for k in range(args.rounds_per_gpu)]
-            return eng.suggest_batch(seed=1234, rounds=ids, n_candidates=C)
+        if args.config == 5:   # independent new_ids split over the GPUs
+            ids = [i * args.new_ids + rank * ids_local + k for k in range(ids_local)]
+            res = eng.suggest_batch(seed=1234, rounds=ids, n_candidates=C)
+            if dist is not None:   # every rank ends with every new_id's winners
+                res = gather_rounds(res)
+            return res
         res = eng.suggest(seed=1234 + i, n_candidates=C, round=i, cand_offset=rank * C)
         if dist is not None:   # exchange per-GPU winners (L x 48 B) over RCCL
             res = exchange_winners(res)
@@ -274,6 +289,7 @@ def main():
             'achieved': round(achieved, 3), 'peak': peak, 'unit': 'TFLOP/s',
             'frac': round(achieved / peak, 4), 'traffic': traffic,
             'traffic_source': traffic_src, 'valu_busy_measured': valu_busy,
+            'valu_busy_source': traffic_src,
             'evals_per_s': dom_rate, 'flops_per_eval': FLOPS_PER_EVAL[prec],
             'valu_issue_frac': round(dom_rate * VALU_INSTR_PER_EVAL[prec] /
                                      PEAK_VALU_LANE_INSTR[prec], 4),
@@ -282,10 +298,11 @@ def main():
         'metric': 'TPE candidate x component lpdf evals/sec (10k-trial history)',
         'value': value, 'unit': 'evals/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3,
-        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+        'higher_is_better': True, 'scaling': 'strong', 'vs_baseline': None,
         'dtype': args.precision, 'data': 'synthetic (prior draws, seed 0)',
         'config': {'workload': workload_name(args, C),
-                   'labels': L, 'history': args.trials, 'candidates_per_label_per_gpu': C,
+                   'labels': L, 'history': args.trials,
+                   'candidates_per_label': C_total, 'candidates_per_label_per_gpu': C,
                    'parallelism': ('new_id-sharded x%d' if args.config == 5
                                    else 'candidate-sharded x%d') % world},
         'posterior_build': post_build,
@@ -294,7 +311,8 @@ def main():
         'roofline': roof,
     }
     if args.config == 5:
-        line['config']['new_ids_per_gpu_per_step'] = args.rounds_per_gpu
+        line['config']['new_ids_per_step'] = args.new_ids
+        line['config']['new_ids_per_gpu_per_step'] = ids_local
     if rank == 0 and not args.no_latency and args.config == 3:
         lat = suggest_latency(args.labels, args.trials)
         line['suggest_latency_ms'] = {

@@ -1,8 +1,14 @@
-"""In-tree build of the native pieces (no JIT cache, so the .so files travel
-with the repository snapshot to the GPU box).
+"""In-tree build of the gfx950 engine library (no JIT cache, so the .so
+travels with the repository snapshot to the GPU box).
 
-    python -m hyperopt_amd._build
+    python -m hyperopt_amd._build [--force]
+
+The library is stamped with a hash of the sources it was compiled from
+(`tpe_source_hash()`); `_lib.load()` recomputes the hash from the sources in
+the tree and refuses a library built from anything else, so a stale `.so`
+can never run in place of HEAD's code.
 """
+import hashlib
 import os
 import subprocess
 import sys
@@ -12,7 +18,8 @@ REPO = os.path.dirname(HERE)
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = 'gfx950'
 
-SOURCES = [os.path.join(HERE, 'csrc', 'tpe_engine.hip'), os.path.join(HERE, 'csrc', 'tpe_build.hip')]
+SOURCES = [os.path.join(HERE, 'csrc', 'tpe_engine.hip'),
+           os.path.join(HERE, 'csrc', 'tpe_build.hip')]
 DEPS = SOURCES + [os.path.join(HERE, 'csrc', 'tpe_device.h'),
                   os.path.join(HERE, 'csrc', 'tpe_ctx.h'),
                   os.path.join(HERE, 'csrc', 'tpe_exp_table.h'),
@@ -23,35 +30,47 @@ FLAGS = ['--offload-arch=' + ARCH, '-O3', '-std=c++17', '-fPIC', '-shared',
          '-Wall', '-Wno-unused-function', '-I' + os.path.join(REPO, 'include')]
 
 
-def _stale(target, deps):
+def source_hash(deps=DEPS):
+    """sha256 (first 16 hex digits) over the build inputs and the flags."""
+    h = hashlib.sha256()
+    for d in deps:
+        h.update(os.path.basename(d).encode())
+        with open(d, 'rb') as f:
+            h.update(f.read())
+    h.update(' '.join(FLAGS).encode())
+    return h.hexdigest()[:16]
+
+
+def built_hash(target=TARGET):
+    """The hash stamped into an existing library (None if absent/unstamped);
+    read from the file's bytes, without loading it."""
     if not os.path.exists(target):
-        return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(d) > t for d in deps)
+        return None
+    with open(target, 'rb') as f:
+        data = f.read()
+    tag = b'TPE_SOURCE_HASH='
+    i = data.find(tag)
+    if i < 0:
+        return None
+    return data[i + len(tag):i + len(tag) + 16].decode('ascii', 'replace')
 
 
 def build_engine(force=False, verbose=True):
-    if not force and not _stale(TARGET, DEPS):
+    want = source_hash()
+    if not force and built_hash() == want:
         return TARGET
-    cmd = [HIPCC] + FLAGS + ['-o', TARGET] + SOURCES
+    cmd = [HIPCC] + FLAGS + ['-DTPE_SOURCE_HASH="%s"' % want, '-o', TARGET] + SOURCES
     if verbose:
         print(' '.join(cmd), flush=True)
     subprocess.check_call(cmd)
+    got = built_hash()
+    if got != want:
+        raise RuntimeError('built library carries hash %r, expected %r' % (got, want))
     return TARGET
 
 
-def build_oracle(force=False, verbose=True):
-    """The C restatement of the scorer lives under oracle/ (test infra)."""
-    mk = os.path.join(REPO, 'oracle', 'Makefile')
-    if os.path.exists(mk):
-        subprocess.check_call(['make', '-s', '-C', os.path.join(REPO, 'oracle')] +
-                              (['-B'] if force else []))
-
-
 def main(argv):
-    force = '--force' in argv
-    build_engine(force=force)
-    build_oracle(force=force)
+    build_engine(force='--force' in argv)
 
 
 if __name__ == '__main__':

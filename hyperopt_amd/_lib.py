@@ -15,6 +15,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libhyperopt_tpe.so')
 HEADER = os.path.join(os.path.dirname(HERE), 'include', 'hyperopt_tpe.h')
 
+ABI_VERSION = 1
+
 TPE_OK = 0
 TPE_ERR_VALUE = -1
 TPE_ERR_TYPE = -2
@@ -70,6 +72,7 @@ _PD = ctypes.POINTER(ctypes.c_double)
 # name -> (restype, argtypes); every function declared in include/hyperopt_tpe.h
 SIGNATURES = {
     'tpe_abi_version': (ctypes.c_int, []),
+    'tpe_source_hash': (ctypes.c_char_p, []),
     'tpe_ctx_create': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]),
     'tpe_ctx_destroy': (None, [_P]),
     'tpe_last_error': (ctypes.c_char_p, [_P]),
@@ -122,10 +125,22 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.tpe_abi_version() != 1:
+    if lib.tpe_abi_version() != ABI_VERSION:
         raise OSError('ABI version mismatch')
+    check_stamp(lib)
     _lib = lib
     return lib
+
+
+def check_stamp(lib):
+    """Refuse a library that was not built from the sources in this tree
+    (its embedded hash, hyperopt_amd/_build.py, must match theirs)."""
+    from . import _build
+    want = _build.source_hash()
+    got = lib.tpe_source_hash().decode()
+    if got != want:
+        raise OSError('hyperopt_amd native library %s is stale: built from sources %s, tree '
+                      'has %s (run `python -m hyperopt_amd._build`)' % (LIB_PATH, got, want))
 
 
 def header_functions(path=HEADER):

@@ -1445,6 +1445,15 @@ extern "C" {
 
 int tpe_abi_version(void) { return TPE_ABI_VERSION; }
 
+// Hash of the sources this library was compiled from (hyperopt_amd/_build.py
+// passes it; the "TPE_SOURCE_HASH=" prefix lets the build script find it in
+// the file without loading the library).
+#ifndef TPE_SOURCE_HASH
+#define TPE_SOURCE_HASH "unstamped000000"
+#endif
+static const char kSourceStamp[] __attribute__((used)) = "TPE_SOURCE_HASH=" TPE_SOURCE_HASH;
+const char* tpe_source_hash(void) { return kSourceStamp + 16; }
+
 int tpe_ctx_create(int device, int precision, tpe_ctx** out) {
     if (!out) return TPE_ERR_ARG;
     *out = nullptr;

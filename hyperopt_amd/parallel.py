@@ -14,21 +14,41 @@ import numpy as np
 from .engine import RESULT_DTYPE, merge_results
 
 
-def exchange_winners(res, group=None):
-    """All-gather per-rank winners and merge; returns the merged winners."""
+def _all_gather_results(res, group):
+    """(world,) + res.shape array of every rank's result records (one RCCL
+    all-gather of the raw 48-byte records; gloo on CPU)."""
     import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    res = np.ascontiguousarray(res, dtype=RESULT_DTYPE)
+    raw = torch.from_numpy(res.view(np.uint8).reshape(-1))
+    if dist.get_backend(group) == 'nccl':
+        raw = raw.cuda(non_blocking=True)
+    out = torch.empty(world * raw.numel(), dtype=torch.uint8, device=raw.device)
+    dist.all_gather_into_tensor(out, raw, group=group)
+    return out.cpu().numpy().view(RESULT_DTYPE).reshape((world,) + res.shape)
+
+
+def exchange_winners(res, group=None):
+    """All-gather per-rank winners of the SAME rounds (candidate shards) and
+    merge them; every rank returns the merged winners."""
     import torch.distributed as dist
     world = dist.get_world_size(group)
     if world == 1:
         return res
-    res = np.ascontiguousarray(res, dtype=RESULT_DTYPE)
-    raw = torch.from_numpy(res.view(np.uint8).copy())
-    if dist.get_backend(group) == 'nccl':
-        raw = raw.cuda()
-    out = torch.empty(world * raw.numel(), dtype=torch.uint8, device=raw.device)
-    dist.all_gather_into_tensor(out, raw, group=group)
-    parts = out.cpu().numpy().view(RESULT_DTYPE).reshape((world,) + res.shape)
-    return merge_results(parts.reshape(world, -1)).reshape(res.shape)
+    parts = _all_gather_results(res, group)
+    return merge_results(parts.reshape(world, -1)).reshape(np.shape(res))
+
+
+def gather_rounds(res, group=None):
+    """All-gather per-rank winners of DIFFERENT rounds (new_id shards, rank r
+    holding rounds [r n, (r+1) n)); every rank returns all rounds in order."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    if world == 1:
+        return res
+    parts = _all_gather_results(res, group)
+    return parts.reshape((world * np.shape(res)[0],) + np.shape(res)[1:])
 
 
 class ShardedSuggest(object):

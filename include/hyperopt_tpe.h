@@ -113,6 +113,10 @@ typedef struct {
 
 int tpe_abi_version(void);
 
+/* Hash of the sources the library was built from (16 hex digits); the
+ * loader compares it with the sources in the tree and refuses a stale build. */
+const char *tpe_source_hash(void);
+
 /* device: HIP ordinal; precision: TPE_F64 or TPE_F32 */
 int tpe_ctx_create(int device, int precision, tpe_ctx **out);
 void tpe_ctx_destroy(tpe_ctx *ctx);
