@@ -34,16 +34,18 @@ sys.path.insert(0, REPO)
 # vendor vector peak for the dtype.
 FLOPS_PER_EVAL = {'f64': 6.0, 'f32': 6.0}
 # The issue-slot roofline (what actually bounds the kernel) counts the
-# instructions of the gfx950 inner loop per eval (tools/isa_loop_mix.py):
-#   fp64: v_fma (z), v_fma (u), v_rndne, v_add (f), 2 x v_fma (2^(f/4096)),
-#         v_cvt_i32, v_ldexp, v_fmac (table product + accumulate) = 9 fp64,
-#         3 int32 (table index, byte offset, exponent) and 1/4 v_mov_b64 (the
-#         component's mu, shared by 4 candidates) = 12.25 VALU instructions,
-#         each a 4-cycle wave64 issue on a 16-lane SIMD, plus one ds_read_b64
-#   fp32: candidate pairs in packed fp32 -- v_pk_add_f32 (x - mu), v_pk_mul_f32,
-#         v_pk_fma_f32, v_pk_add_f32 (accumulate) per two evals + one
-#         v_exp_f32 (8-cycle issue) per eval = 4 four-cycle slots per eval
-VALU_INSTR_PER_EVAL = {'f64': 12.25, 'f32': 4.0}
+# 4-cycle wave64 issue slots of the gfx950 inner loop per eval
+# (tools/isa_loop_mix.py):
+#   fp64 (k_round): v_fma (z), v_fma (u), v_rndne, v_add (f), 2 x v_fma
+#         (2^(f/4096)), v_cvt_i32, v_ldexp, v_fmac (table product +
+#         accumulate) = 9 fp64, 3 int32 (table index, byte offset, exponent)
+#         and 1/4 v_mov_b64 (the component's m, shared by 4 candidates) =
+#         12.25 slots, plus one ds_read_b64
+#   fp32 (k_screen / k_round<float>): candidate pairs in packed fp32 --
+#         v_pk_fma_f32 (z), v_pk_fma_f32 (t) and 1/2 v_pk_add_f32 (tree of
+#         8, then the running sum) per two evals, 1/8 v_mov_b64 per eval, and
+#         one v_exp_f32 (8-cycle issue = 2 slots) per eval = 3.625 slots
+VALU_SLOTS_PER_EVAL = {'f64': 12.25, 'f32': 3.625}
 PEAK_FP64_VECTOR_TFLOPS = 78.6        # MI355X spec (MI355X_MICROARCH.md)
 PEAK_FP32_VECTOR_TFLOPS = 157.3
 # 4-cycle wave64 VALU issue slots per second at 2.4 GHz, in lanes: 256 CU x
@@ -76,6 +78,11 @@ def parse():
     ap.add_argument('--cpu-sample-c', type=int, default=49152,
                     help='candidates per label in the all-cores C baseline sample')
     ap.add_argument('--no-latency', action='store_true')
+    ap.add_argument('--no-screen', action='store_true',
+                    help='f64: plain fp64 rounds (no fp32 screen); the winners are the same')
+    ap.add_argument('--unscreened-steps', type=int, default=3,
+                    help='f64: steps of the plain fp64 round timed after the main run, for '
+                         'comparison (0 = skip)')
     ap.add_argument('--dist-backend', default='nccl',
                     help='nccl (RCCL over xGMI); gloo only to rehearse N ranks on one GPU')
     return ap.parse_args()
@@ -249,57 +256,79 @@ def main():
             res = exchange_winners(res)
         return res
 
+    def timed(n_steps, first):
+        """Run n_steps steps (barrier + sync on both sides); returns wall
+        seconds (max over ranks) and the summed per-family / screen stats."""
+        mode_ms, mode_ev, scr = {}, {}, [0, 0, 0.0]
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(n_steps):
+            step(first + i)
+            for k, (ms, ev) in eng.last_mode_stats().items():
+                mode_ms[k] = mode_ms.get(k, 0.0) + ms
+                mode_ev[k] = mode_ev.get(k, 0) + ev
+            a, b, ms = eng.last_screen(with_ms=True)
+            scr[0] += a
+            scr[1] += b
+            scr[2] += ms
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if dist is not None:
+            tt = torch.tensor([dt], dtype=torch.float64,
+                              device='cuda' if args.dist_backend == 'nccl' else 'cpu')
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = float(tt.item())
+        return dt, mode_ms, mode_ev, scr
+
+    screen = args.precision == 'f64' and not args.no_screen
+    eng.set_option('screen', int(screen))
     for i in range(args.warmup):
         step(i)
-    mode_ms = {}
-    mode_ev = {}
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
-        for k, (ms, ev) in eng.last_mode_stats().items():
-            mode_ms[k] = mode_ms.get(k, 0.0) + ms
-            mode_ev[k] = mode_ev.get(k, 0) + ev
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if dist is not None:
-        tt = torch.tensor([dt], dtype=torch.float64,
-                          device='cuda' if args.dist_backend == 'nccl' else 'cpu')
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    dt, mode_ms, mode_ev, scr = timed(args.steps, args.warmup)
     evals_per_step = sum(mode_ev.values()) // max(args.steps, 1)
     total_evals = evals_per_step * args.steps * world
     value = total_evals / dt
 
-    # roofline of the dominant kernel family (device time from HIP events on
-    # the engine's stream, summed over the timed steps)
-    dom = max((k for k in mode_ms if k in DENSE), key=lambda k: mode_ms[k])
-    dom_rate = mode_ev[dom] / (mode_ms[dom] * 1e-3)
+    # roofline of the dominant kernel (device time from HIP events on the
+    # engine's stream, summed over the timed steps)
     prec = args.precision
-    peak = PEAK_FP64_VECTOR_TFLOPS if prec == 'f64' else PEAK_FP32_VECTOR_TFLOPS
-    kname = 'k_round<%s, %d, true,' % ('double' if prec == 'f64' else 'float',
-                                       8 if dom == 'dense' else 1)
+    dom = max((k for k in mode_ms if k in DENSE), key=lambda k: mode_ms[k])
+    screened = scr[0] > 0
+    if screened:
+        # k_screen: every dense (candidate, component) pair in packed fp32
+        dom_ms = scr[2]
+        kprec, kname, kdesc = 'f32', 'k_screen<4, true>', 'k_screen<4,true> (fp32 screen of the ' \
+            'fp64 round, GMM1+LGMM1 labels)'
+    else:
+        dom_ms = mode_ms[dom]
+        kprec = prec
+        kname = 'k_round<%s, %d, true,' % ('double' if prec == 'f64' else 'float',
+                                           8 if dom == 'dense' else 1)
+        kdesc = 'k_round<%s,%s>' % (prec, dom + ' (GMM1+LGMM1 labels)')
+    dom_rate = mode_ev[dom] / (dom_ms * 1e-3)
+    peak = PEAK_FP64_VECTOR_TFLOPS if kprec == 'f64' else PEAK_FP32_VECTOR_TFLOPS
     traffic, valu_busy, traffic_src = measured_pmc(kname)
-    achieved = dom_rate * FLOPS_PER_EVAL[prec] / 1e12
-    roof = {'bound': 'valu', 'kernel': 'k_round<%s,%s>' % (prec, dom + ' (GMM1+LGMM1 labels)'),
+    achieved = dom_rate * FLOPS_PER_EVAL[kprec] / 1e12
+    roof = {'bound': 'valu', 'kernel': kdesc,
             'achieved': round(achieved, 3), 'peak': peak, 'unit': 'TFLOP/s',
             'frac': round(achieved / peak, 4), 'traffic': traffic,
             'traffic_source': traffic_src, 'valu_busy_measured': valu_busy,
             'valu_busy_source': traffic_src,
-            'evals_per_s': dom_rate, 'flops_per_eval': FLOPS_PER_EVAL[prec],
-            'valu_issue_frac': round(dom_rate * VALU_INSTR_PER_EVAL[prec] /
-                                     PEAK_VALU_LANE_INSTR[prec], 4),
-            'launch_ms': mode_ms[dom] / args.steps}
+            'evals_per_s': dom_rate, 'flops_per_eval': FLOPS_PER_EVAL[kprec],
+            'valu_issue_frac': round(dom_rate * VALU_SLOTS_PER_EVAL[kprec] /
+                                     PEAK_VALU_LANE_INSTR[kprec], 4),
+            'launch_ms': dom_ms / args.steps}
     line = {
         'metric': 'TPE candidate x component lpdf evals/sec (10k-trial history)',
         'value': value, 'unit': 'evals/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3,
         'higher_is_better': True, 'scaling': 'strong', 'vs_baseline': None,
-        'dtype': args.precision, 'data': 'synthetic (prior draws, seed 0)',
+        'dtype': ('f32+f64' if screened else args.precision),
+        'data': 'synthetic (prior draws, seed 0)',
         'config': {'workload': workload_name(args, C),
                    'labels': L, 'history': args.trials,
                    'candidates_per_label': C_total, 'candidates_per_label_per_gpu': C,
@@ -310,6 +339,27 @@ def main():
         'per_family_evals': {k: v // args.steps for k, v in mode_ev.items() if v},
         'roofline': roof,
     }
+    if screened:
+        line['screen'] = {
+            'screened_per_step': scr[0] // args.steps, 'rescored_per_step': scr[1] // args.steps,
+            'rescored_fraction': scr[1] / max(scr[0], 1),
+            'screen_kernel_ms': round(scr[2] / args.steps, 3),
+            'select_and_rescore_ms': round((mode_ms[dom] - scr[2]) / args.steps, 3),
+            'note': 'dense labels: every (candidate, component) pair evaluated in packed fp32 '
+                    'with a rigorous error bound; candidates whose bound interval reaches the '
+                    'round\'s best lower bound re-scored in fp64 -- winners and lpdfs are '
+                    'bit-identical to the plain fp64 round (tests/test_screen.py); evals are '
+                    'counted once per pair'}
+        if args.unscreened_steps > 0 and world == 1:
+            eng.set_option('screen', 0)
+            step(args.warmup + args.steps)
+            udt, ums, uev, _ = timed(args.unscreened_steps, args.warmup + args.steps + 1)
+            eng.set_option('screen', 1)
+            line['screen']['unscreened_fp64'] = {
+                'steps': args.unscreened_steps,
+                'ms_per_step': round(udt / args.unscreened_steps * 1e3, 3),
+                'value': sum(uev.values()) / udt,
+                'dense_ms': round(ums[dom] / args.unscreened_steps, 3)}
     if args.config == 5:
         line['config']['new_ids_per_step'] = args.new_ids
         line['config']['new_ids_per_gpu_per_step'] = ids_local

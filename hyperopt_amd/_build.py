@@ -37,7 +37,8 @@ def source_hash(deps=DEPS):
         h.update(os.path.basename(d).encode())
         with open(d, 'rb') as f:
             h.update(f.read())
-    h.update(' '.join(FLAGS).encode())
+    # flags without the tree's absolute location (the GPU box unpacks it elsewhere)
+    h.update(' '.join(f for f in FLAGS if not f.startswith('-I')).encode())
     return h.hexdigest()[:16]
 
 

@@ -35,6 +35,11 @@ TPE_HAS_LOW = 1
 TPE_HAS_HIGH = 2
 TPE_HAS_Q = 4
 
+TPE_OPT_SCREEN = 1
+TPE_OPT_SPLITK = 2
+TPE_OPT_DEDUP = 3
+TPE_OPT_CHUNKS = 4
+
 TPE_OBS_IDENTITY = 0
 TPE_OBS_LOG = 1
 TPE_OBS_LOG_FLOOR = 2
@@ -102,6 +107,9 @@ SIGNATURES = {
     'tpe_history_append': (ctypes.c_int, [_P, _P, _P, _P]),
     'tpe_build_posterior_resident': (ctypes.c_int, [_P, _P, _I64, _I64, _D, _D, _I32, _P]),
     'tpe_last_build_ms': (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float)]),
+    'tpe_last_screen': (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_float)]),
+    'tpe_set_option': (ctypes.c_int, [_P, _I32, _I64]),
+    'tpe_screen_probe': (ctypes.c_int, [_P, _I32, _P, _I64, _P, _P]),
 }
 
 _lib = None

@@ -982,14 +982,20 @@ __global__ __launch_bounds__(kParzenBlock) void k_fold(
             M = block_max(M);
             if (!isfinite(M)) M = 0.0;
             (side ? d.shift_a : d.shift_b) = M;
+            double amax = 0.0;
             for (int64_t k = tid; k < K; k += kParzenBlock) {
                 const double a = ascale[o + k];
                 const double c = cterm[o + k];
                 c64[o + k] = Comp<double>{(mu[o + k] - centre) * (a * sK), a * sK, (c - M) * kExpScale,
                                           w[o + k]};
-                c32[o + k] = Comp<float>{(float)mu[o + k], (float)(a * sqrt(l2e)), (float)((c - M) * l2e),
+                const double a2 = a * sqrt(l2e);
+                const float a32 = (float)a2;
+                c32[o + k] = Comp<float>{(float)((mu[o + k] - centre) * a2), a32, (float)((c - M) * l2e),
                                          (float)w[o + k]};
+                amax = fmax(amax, (double)a32);
             }
+            amax = block_max(amax);
+            (side ? d.amax_a : d.amax_b) = (float)amax;
         }
     }
     // sampling records of the below mixture: cumulative normalised weights,

@@ -172,6 +172,19 @@ struct tpe_ctx {
     DevBuf<double> chunk_part;           // chunked packed map: x | below sum | above chunk sums
     int32_t chunks_forced = 0;           // TPE_CHUNKS: 1 = off, > 1 = fixed, 0 = auto
     bool pack_wide = false;              // TPE_PACK_WIDE: packed rounds over kR slots per thread
+    // fp32 screen of the fp64 round (sampled tile-map rounds, TPE_F64): per
+    // candidate an upper bound of its score, per (round, label) the largest
+    // lower bound and the compacted candidates that can still win
+    bool screen = true;                  // TPE_NO_SCREEN=1 / TPE_OPT_SCREEN
+    DevBuf<float> scr_hi;
+    DevBuf<int32_t> scr_idx;
+    DevBuf<unsigned long long> scr_lb;
+    DevBuf<int32_t> scr_cnt;
+    std::vector<int32_t> scr_cnt_h;
+    int64_t screen_total = 0, screen_rescored = 0;   // last round
+    bool screen_pending = false;         // scr_cnt_h awaits the round's final sync
+    hipEvent_t evs[2] = {};              // brackets k_screen alone
+    float screen_ms = 0.f;
     tpe_rt::BuildBufs build;             // device posterior builder scratch
     int64_t built_n_trials = 0;          // last tpe_build_posterior: history size
     int32_t built_n_below = 0;           //   and its below-set size

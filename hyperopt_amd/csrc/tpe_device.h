@@ -36,11 +36,13 @@ struct DLabel {
     int64_t samp_off;           // offset of the below mixture's sampling records
     int32_t ns;
     int32_t stream;             // Philox stream id (label position)
+    float amax_b, amax_a;       // dense: largest fp32 record scale a per mixture (screen_err)
 };
 
 // Component record.  dense fp64: (m = (mu - centre) a, a = sqrt(K/2)/max(sigma,EPS),
 // c = K (log coef - M), w) so that z = x' a - m with x' = x - centre (one FMA);
-// dense fp32: (mu, a, c, w) in log2 units.  quantized: (mu, a = 1/max(sqrt(2)
+// dense fp32: the same form in log2 units (a = sqrt(log2(e)/2)/max(sigma,EPS),
+// c = log2(e) (log coef - M)).  quantized: (mu, a = 1/max(sqrt(2)
 // sigma, EPS), -, w).  categorical: c = log p.
 template <typename T>
 struct alignas(4 * sizeof(T)) Comp {
@@ -212,16 +214,17 @@ __device__ __forceinline__ double lse_twopass(const Comp<double>* __restrict__ c
     return log(s) + m * kExpScaleInv;
 }
 
+// fp32 records: (m = (mu - centre) a, a, c, w) in log2 units, x recentred
 __device__ __forceinline__ float lse_twopass(const Comp<float>* __restrict__ c, int n, float x) {
     float m = -__builtin_inff();
     for (int k = 0; k < n; ++k) {
-        const float z = (x - c[k].mu) * c[k].a;
+        const float z = fmaf(x, c[k].a, -c[k].mu);
         m = fmaxf(m, fmaf(-z, z, c[k].c));
     }
     if (!(m > -__builtin_inff())) return __builtin_nanf("");
     float s = 0.0f;
     for (int k = 0; k < n; ++k) {
-        const float z = (x - c[k].mu) * c[k].a;
+        const float z = fmaf(x, c[k].a, -c[k].mu);
         s += __builtin_amdgcn_exp2f(fmaf(-z, z, c[k].c) - m);
     }
     return (__builtin_log2f(s) + m) * 0.69314718055994531f;  // back to natural log
@@ -321,16 +324,19 @@ __device__ __forceinline__ void lse_dense(const Comp<double>* __restrict__ c, in
     for (int r = 0; r < R; ++r) out[r] = lse_finish(c, n, acc[r], x[r], shift);
 }
 
-// fp32 fast path: constants pre-scaled by log2(e) so the hardware v_exp_f32
-// (exp2) is used directly; shift is in natural-log units.  Candidates go in
-// pairs through packed fp32 (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32 on a
-// float2, the component constants broadcast from SGPRs): 3 packed
-// instructions + 2 v_exp_f32 per two evaluations.
+// fp32 path: records (m, a, c) pre-scaled by log2(e) and recentred like the
+// fp64 ones, so z = fma(x', a, -m), t = fma(-z, z, c) and the hardware
+// v_exp_f32 (exp2) is used directly; the shift is in natural-log units.
+// Candidates go in pairs through packed fp32 (v_pk_fma_f32 on a float2, the
+// component constants broadcast from SGPRs): 2 packed FMAs + 2 v_exp_f32 +
+// one packed add per two evaluations.  The 8 terms of a record batch are
+// added as a tree before they join the running sum, which keeps the
+// summation error bound at (K/8 + 11) u instead of K u (screen_bound).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int R>
 __device__ __forceinline__ void lse_acc(const Comp<float>* __restrict__ c, int n,
-                                        const double (&xd)[R], float (&out)[R]) {
+                                        const float (&xf)[R], float (&out)[R]) {
     // candidate pairs through packed fp32, an odd one scalar; the record
     // stream double-buffered as in the fp64 lse_acc (no LDS here, but a use
     // of a scalar-loaded record while the next batch is in flight still
@@ -339,10 +345,10 @@ __device__ __forceinline__ void lse_acc(const Comp<float>* __restrict__ c, int n
     constexpr bool kOdd = R % 2 != 0;
     constexpr int PP = P > 0 ? P : 1;
     f32x2 x2[PP], acc2[PP];
-    float x1 = kOdd ? (float)xd[R - 1] : 0.0f, acc1 = 0.0f;
+    float x1 = kOdd ? xf[R - 1] : 0.0f, acc1 = 0.0f;
 #pragma unroll
     for (int p = 0; p < PP; ++p) {
-        x2[p] = P > 0 ? f32x2{(float)xd[2 * p], (float)xd[2 * p + 1]} : f32x2{0.0f, 0.0f};
+        x2[p] = P > 0 ? f32x2{xf[2 * p], xf[2 * p + 1]} : f32x2{0.0f, 0.0f};
         acc2[p] = f32x2{0.0f, 0.0f};
     }
     if (n > 0) {
@@ -364,23 +370,30 @@ __device__ __forceinline__ void lse_acc(const Comp<float>* __restrict__ c, int n
             for (int u = 0; u < U; ++u) {
 #pragma unroll
                 for (int p = 0; p < P; ++p) {
-                    const f32x2 z = (x2[p] - m[u]) * a[u];
+                    const f32x2 z = __builtin_elementwise_fma(x2[p], f32x2{a[u], a[u]},
+                                                              f32x2{-m[u], -m[u]});
                     t2[u][p] = __builtin_elementwise_fma(-z, z, f32x2{cc[u], cc[u]});
                 }
                 if constexpr (kOdd) {
-                    const float z = (x1 - m[u]) * a[u];
+                    const float z = fmaf(x1, a[u], -m[u]);
                     t1[u] = fmaf(-z, z, cc[u]);
                 }
             }
         };
         auto accum = [&]() {
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
+            for (int p = 0; p < P; ++p) {
+                f32x2 e[U];
 #pragma unroll
-                for (int p = 0; p < P; ++p)
-                    acc2[p] += f32x2{__builtin_amdgcn_exp2f(t2[u][p].x),
-                                     __builtin_amdgcn_exp2f(t2[u][p].y)};
-                if constexpr (kOdd) acc1 += __builtin_amdgcn_exp2f(t1[u]);
+                for (int u = 0; u < U; ++u)
+                    e[u] = f32x2{__builtin_amdgcn_exp2f(t2[u][p].x), __builtin_amdgcn_exp2f(t2[u][p].y)};
+                acc2[p] += ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
+            }
+            if constexpr (kOdd) {
+                float e[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) e[u] = __builtin_amdgcn_exp2f(t1[u]);
+                acc1 += ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
             }
         };
         if (nbat > 0) load(Am, Aa, Ac, 0);
@@ -402,15 +415,15 @@ __device__ __forceinline__ void lse_acc(const Comp<float>* __restrict__ c, int n
             accum();
         }
         for (int k = nfull; k < n; ++k) {
-            const float mu = c[k].mu, a = c[k].a, cc = c[k].c;
+            const float m = c[k].mu, a = c[k].a, cc = c[k].c;
 #pragma unroll
             for (int p = 0; p < P; ++p) {
-                const f32x2 z = (x2[p] - mu) * a;
+                const f32x2 z = __builtin_elementwise_fma(x2[p], f32x2{a, a}, f32x2{-m, -m});
                 const f32x2 t = __builtin_elementwise_fma(-z, z, f32x2{cc, cc});
                 acc2[p] += f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
             }
             if constexpr (kOdd) {
-                const float z = (x1 - mu) * a;
+                const float z = fmaf(x1, a, -m);
                 acc1 += __builtin_amdgcn_exp2f(fmaf(-z, z, cc));
             }
         }
@@ -423,6 +436,7 @@ __device__ __forceinline__ void lse_acc(const Comp<float>* __restrict__ c, int n
     if constexpr (kOdd) out[R - 1] = acc1;
 }
 
+// x: recentred candidate (y - centre) in fp32
 __device__ __forceinline__ double lse_finish(const Comp<float>* __restrict__ c, int n, float acc,
                                              float x, double shift) {
     float v = __builtin_log2f(acc) * 0.69314718055994531f;
@@ -432,12 +446,58 @@ __device__ __forceinline__ double lse_finish(const Comp<float>* __restrict__ c, 
 
 template <int R>
 __device__ __forceinline__ void lse_dense(const Comp<float>* __restrict__ c, int n, double shift,
-                                          double, const double (&xd)[R], double (&out)[R],
+                                          double centre, const double (&xd)[R], double (&out)[R],
                                           const double* __restrict__) {
-    float acc[R];
-    lse_acc<R>(c, n, xd, acc);
+    float acc[R], xf[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) out[r] = lse_finish(c, n, acc[r], (float)xd[r], shift);
+    for (int r = 0; r < R; ++r) xf[r] = (float)(xd[r] - centre);
+    lse_acc<R>(c, n, xf, acc);
+#pragma unroll
+    for (int r = 0; r < R; ++r) out[r] = lse_finish(c, n, acc[r], xf[r], shift);
+}
+
+// -------------------------------------------------------- fp32 screen ----
+// The exact fp64 round screens every candidate with the fp32 sums above and
+// re-scores in fp64 only those that can still win.  screen_err bounds
+// |lpdf32 - lpdf| of ONE mixture (natural-log units) for a candidate at
+// recentred |x'| = X, rigorously, from the fp32 arithmetic (u = 2^-24):
+//  * a term is "relevant" if its exact exponent t = c' - z^2 >= -T0 (T0 =
+//    125, log2 units, so it stays a normal fp32 number); since c' <= 0 then
+//    |z| <= sqrt(T0) and |c'| <= T0;
+//  * z = fma(x32, a32, -m32): |z32 - z| <= zeta = (3 X amax + 2 sqrt(T0)) u
+//    (x32 and a32 rounded once each, |m| <= X a + sqrt(T0) for a relevant
+//    term, one rounding of the fma);
+//  * t = fma(-z, z, c32): |t32 - t| <= dt = (2 T0 + 1) u + zeta (2 sqrt(T0)
+//    + zeta);
+//  * v_exp_f32: 2 ulp (2^-22) relative; so a relevant term is within
+//    rho = 0.7 dt + 2.5e-7 relative (dt <= 0.01);
+//  * the sum of positive terms: (K/8 + 11) u relative (tree of 8, then a
+//    running sum; a tail of < 8 terms added one by one);
+//  * the irrelevant terms (< 2^-124 each, exact or computed -- dt <= 0.01
+//    keeps |z32| within 1e-4 relative of |z|) add at most K 2^-124 / S,
+//    S >= 2^-60 for a certified candidate;
+//  * v_log_f32: 2^-22 (|log2 S| + 1) absolute.
+// Uncertified (S < 2^-60, NaN, dt > 0.01) returns +inf: the candidate is
+// always re-scored, which also keeps the reference's NaN-greatest order.
+constexpr float kScreenMinAcc = 0x1.0p-60f;
+
+__device__ __forceinline__ double screen_err(float amax, int K, double X, float acc, float l2) {
+    if (!(acc >= kScreenMinAcc) || !(acc <= 0x1.0p+100f) || !(X <= 1e30)) return __builtin_inf();
+    constexpr double u = 0x1.0p-24, sqT0 = 11.1804, T0 = 125.0;
+    const double zeta = (3.0 * X * (double)amax * 1.001 + 2.0 * sqT0) * u * 1.001;
+    const double dt = (2.0 * T0 + 1.0) * u + zeta * (2.0 * sqT0 + zeta);
+    if (!(dt <= 0.01)) return __builtin_inf();
+    const double rho = 0.7 * dt + 2.5e-7;
+    const double gsum = ((double)(K / 8) + 11.0) * u * 1.01;
+    const double negl = (double)K * 0x1.0p-64;
+    const double rel = rho + gsum + negl;
+    return 1.02 * rel + 0x1.0p-22 * 0.6931471805599453 * (fabs((double)l2) + 1.0);
+}
+
+// |lpdf64 - lpdf| of the fp64 path (tpe_device.h lse_acc<double>): a
+// sequential sum of K terms, each within ~2.5e-14 + 2 ulp
+__device__ __forceinline__ double fp64_err(int K, double mag) {
+    return ((double)K + 64.0) * 0x1.0p-52 + 1e-13 + mag * 0x1.0p-50;
 }
 
 // ------------------------------------------------------- quantized mass ----

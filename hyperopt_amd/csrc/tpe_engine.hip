@@ -345,9 +345,11 @@ __global__ __launch_bounds__(kBlock) void k_round_chunk(
         if (c == 0) lse_acc<R>(comps + L.comp_b, L.nb, xr, sb, exp_tab);
         lse_acc<R>(comps + L.comp_a + k0, k1 - k0, xr, sa, exp_tab);
     } else {
-        float fb[R], fa[R];
-        if (c == 0) lse_acc<R>(comps + L.comp_b, L.nb, y, fb);
-        lse_acc<R>(comps + L.comp_a + k0, k1 - k0, y, fa);
+        float fb[R], fa[R], xf[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) xf[r] = (float)(y[r] - L.centre);
+        if (c == 0) lse_acc<R>(comps + L.comp_b, L.nb, xf, fb);
+        lse_acc<R>(comps + L.comp_a + k0, k1 - k0, xf, fa);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             sb[r] = c == 0 ? (double)fb[r] : 0.0;
@@ -394,8 +396,8 @@ __global__ __launch_bounds__(kBlock) void k_finish_chunks(
             lb[r] = lse_finish(comps + L.comp_b, L.nb, sb, y - L.centre, L.shift_b);
             la[r] = lse_finish(comps + L.comp_a, L.na, sa, y - L.centre, L.shift_a);
         } else {
-            lb[r] = lse_finish(comps + L.comp_b, L.nb, (float)sb, (float)y, L.shift_b);
-            la[r] = lse_finish(comps + L.comp_a, L.na, (float)sa, (float)y, L.shift_a);
+            lb[r] = lse_finish(comps + L.comp_b, L.nb, (float)sb, (float)(y - L.centre), L.shift_b);
+            la[r] = lse_finish(comps + L.comp_a, L.na, (float)sa, (float)(y - L.centre), L.shift_a);
         }
         if (lgmm) {
             lb[r] -= y;
@@ -410,6 +412,190 @@ __global__ __launch_bounds__(kBlock) void k_finish_chunks(
     __shared__ uint64_t scratch[R * kBlock * 3 / 2];   // finish_slots: keys + winners
     __shared__ Partial sh[kBlock / 64];
     finish_slots<R>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials, scratch, sh);
+}
+
+// ------------------------------------------------ fp32 screen (tile map) ----
+// The exact fp64 round of the dense labels in three kernels:
+//   k_screen   every candidate in packed fp32 (3.5 issue slots per eval
+//              instead of 12.25): an upper bound hi = s32 + E of its score
+//              and, per (round, label), the largest lower bound s32 - E
+//              (E: screen_err + fp64_err, tpe_device.h, x 1.25);
+//   k_select   compacts the candidates with hi >= that lower bound -- the
+//              only ones whose fp64 score can reach the fp64 maximum;
+//   k_rescore  draws them again (Philox is stateless) and scores them with
+//              the fp64 code of k_round, so the winner, its value and its
+//              lpdfs are bit-identical to the unscreened round's.
+// Scores are per (round, label) rows of n candidates; hi and the compacted
+// indices use the label's position in the dense group (blockIdx.y).
+__device__ __forceinline__ float float_up(double v) {   // smallest float >= v (finite v)
+    float f = (float)v;
+    if ((double)f < v) {
+        uint32_t b = __float_as_uint(f);
+        b = f > 0.0f ? b + 1u : (f < 0.0f ? b - 1u : 1u);
+        f = __uint_as_float(b);
+    }
+    return f;
+}
+
+__device__ __forceinline__ uint64_t block_max_key(uint64_t k, uint64_t* __restrict__ sh) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(k, off);
+        k = o > k ? o : k;
+    }
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = k;
+    __syncthreads();
+    uint64_t m = sh[0];
+#pragma unroll
+    for (int w = 1; w < kBlock / 64; ++w) m = sh[w] > m ? sh[w] : m;
+    return m;
+}
+
+// SAMPLE = false (tpe_screen_probe, tests): candidates from cand_in, and the
+// fp32 score and its error bound written per candidate instead
+template <int R, bool SAMPLE>
+__global__ __launch_bounds__(kBlock) void k_screen(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<float>* __restrict__ comps32, const SampRec* __restrict__ samp, int64_t n,
+    int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, int32_t nl,
+    float* __restrict__ hi, unsigned long long* __restrict__ lbkey, int32_t* __restrict__ err,
+    Slots S, const double* __restrict__ cand_in, double* __restrict__ s_out,
+    double* __restrict__ e_out) {
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    const bool lgmm = L.mode == DENSE_LGMM;
+    double x[R];
+    int64_t z[R], ci[R], gi[R];
+    bool valid[R];
+    draw_slots<DENSE_ANY, SAMPLE, R>(L, S, lgmm, samp, cand_in, n, cand_offset, seed, rounds, err,
+                                     x, z, ci, gi, valid);
+    double y[R], X[R];
+    float xf[R], ab[R], aa[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        y[r] = lgmm ? log(x[r]) : x[r];
+        const double xr = y[r] - L.centre;
+        xf[r] = (float)xr;
+        X[r] = fabs(xr);
+    }
+    lse_acc<R>(comps32 + L.comp_b, L.nb, xf, ab);
+    lse_acc<R>(comps32 + L.comp_a, L.na, xf, aa);
+    const size_t row = ((size_t)blockIdx.z * nl + blockIdx.y) * (size_t)n;
+    uint64_t bk = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (!valid[r]) continue;
+        const float l2b = __builtin_log2f(ab[r]), l2a = __builtin_log2f(aa[r]);
+        const double lb = (double)l2b * 0.6931471805599453 + L.shift_b;
+        const double la = (double)l2a * 0.6931471805599453 + L.shift_a;
+        const double s = lb - la;
+        const double E = 1.25 * (screen_err(L.amax_b, L.nb, X[r], ab[r], l2b) +
+                                 screen_err(L.amax_a, L.na, X[r], aa[r], l2a) +
+                                 fp64_err(L.nb + L.na, fabs(lb) + fabs(la) + fabs(y[r])));
+        if constexpr (!SAMPLE) {
+            s_out[ci[r]] = s;
+            e_out[ci[r]] = E;
+            continue;
+        }
+        float h = __builtin_inff();
+        if (E <= 1e30 && s == s) {
+            h = float_up(s + E);
+            const uint64_t k = order_key(s - E);
+            bk = k > bk ? k : bk;
+        }
+        hi[row + ci[r]] = h;
+    }
+    if constexpr (!SAMPLE) return;
+    __shared__ uint64_t sh[kBlock / 64];
+    bk = block_max_key(bk, sh);
+    if (threadIdx.x == 0 && bk) atomicMax(lbkey + (size_t)blockIdx.z * nl + blockIdx.y, bk);
+}
+
+__global__ __launch_bounds__(kBlock) void k_select(const float* __restrict__ hi, int64_t n, int32_t nl,
+                                                   const unsigned long long* __restrict__ lbkey,
+                                                   int32_t* __restrict__ cnt, int32_t* __restrict__ idx) {
+    const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
+    const size_t row = cell * (size_t)n;
+    const uint64_t lb = lbkey[cell];
+    const int lane = threadIdx.x & 63;
+    for (int64_t i0 = (int64_t)blockIdx.x * kBlock; i0 < n; i0 += (int64_t)gridDim.x * kBlock) {
+        const int64_t i = i0 + threadIdx.x;
+        const bool take = i < n && order_key((double)hi[row + i]) >= lb;
+        const uint64_t m = __ballot(take);
+        if (m == 0) continue;   // wave-uniform
+        int base = 0;
+        if (lane == 0) base = atomicAdd(cnt + cell, (int)__popcll(m));
+        base = __shfl(base, 0);
+        if (take) idx[row + base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)i;
+    }
+}
+
+template <int R>
+__global__ __launch_bounds__(kBlock) void k_rescore(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<double>* __restrict__ comps64, const SampRec* __restrict__ samp, int64_t n,
+    int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, int32_t nl,
+    int32_t n_labels, int32_t tiles, const int32_t* __restrict__ cnt, const int32_t* __restrict__ idx,
+    Partial* __restrict__ partials) {
+    const int li = group[blockIdx.y];
+    const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
+    Partial* prow = partials + ((size_t)blockIdx.z * n_labels + li) * tiles;
+    const Partial empty{0, INT64_MAX, 0.0, 0.0, 0.0};
+    if (threadIdx.x == 0)   // the round's partial slots beyond this grid: empty
+        for (int64_t t = (int64_t)gridDim.x + blockIdx.x; t < tiles; t += gridDim.x) prow[t] = empty;
+    const int64_t count = cnt[cell];
+    constexpr int64_t per = (int64_t)R * kBlock;
+    if ((int64_t)blockIdx.x * per >= count) {   // uniform: no share of the list
+        if (threadIdx.x == 0) prow[blockIdx.x] = empty;
+        return;
+    }
+    const DLabel L = labels[li];
+    __shared__ double exp_tab[kExpTabSize];
+    load_exp_table(exp_tab);
+    const bool lgmm = L.mode == DENSE_LGMM;
+    const int32_t* list = idx + cell * (size_t)n;
+    const uint32_t rk = rounds[blockIdx.z];
+    uint64_t bk = 0;
+    int64_t bi = INT64_MAX;
+    double bv = 0.0, bl = 0.0, ba = 0.0;
+    for (int64_t base = (int64_t)blockIdx.x * per; base < count; base += (int64_t)gridDim.x * per) {
+        double x[R], y[R], lb[R], la[R];
+        int64_t gi[R];
+        bool valid[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int64_t j = base + r * kBlock + threadIdx.x;
+            valid[r] = j < count;
+            gi[r] = cand_offset + (valid[r] ? list[j] : 0);
+            double v = lgmm ? 1.0 : 0.0;
+            if (valid[r]) {
+                if (lgmm) (void)sample_below<DENSE_LGMM>(L, samp + L.samp_off, seed, rk, (uint32_t)gi[r], v);
+                else (void)sample_below<DENSE_GMM>(L, samp + L.samp_off, seed, rk, (uint32_t)gi[r], v);
+            }
+            x[r] = v;
+            y[r] = lgmm ? log(v) : v;
+        }
+        lse_dense<R>(comps64 + L.comp_b, L.nb, L.shift_b, L.centre, y, lb, exp_tab);
+        lse_dense<R>(comps64 + L.comp_a, L.na, L.shift_a, L.centre, y, la, exp_tab);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (lgmm) {
+                lb[r] -= y[r];
+                la[r] -= y[r];
+            }
+            if (!valid[r]) continue;
+            const uint64_t key = order_key(lb[r] - la[r]);
+            if (better(key, gi[r], bk, bi)) {
+                bk = key;
+                bi = gi[r];
+                bv = x[r];
+                bl = lb[r];
+                ba = la[r];
+            }
+        }
+    }
+    __shared__ Partial sh[kBlock / 64];
+    block_maxloc(bk, bi, bv, bl, ba, prow + blockIdx.x, sh);
 }
 
 // ------------------------------------------------------- split-K map ----
@@ -467,7 +653,7 @@ __device__ __forceinline__ double slice_sum(const DLabel& L, const Comp<T>* __re
             lse_acc<1>(c + k0, k1 - k0, xr, acc, tab);
             return acc[0];
         } else {
-            const double xv[1] = {v};
+            const float xv[1] = {(float)(v - L.centre)};
             float acc[1];
             lse_acc<1>(c + k0, k1 - k0, xv, acc);
             return (double)acc[0];
@@ -567,8 +753,8 @@ __global__ __launch_bounds__(kBlock) void k_finish_slices(
                 lb = lse_finish(comps + L.comp_b, L.nb, sb, y - L.centre, L.shift_b);
                 la = lse_finish(comps + L.comp_a, L.na, sa, y - L.centre, L.shift_a);
             } else {
-                lb = lse_finish(comps + L.comp_b, L.nb, (float)sb, (float)y, L.shift_b);
-                la = lse_finish(comps + L.comp_a, L.na, (float)sa, (float)y, L.shift_a);
+                lb = lse_finish(comps + L.comp_b, L.nb, (float)sb, (float)(y - L.centre), L.shift_b);
+                la = lse_finish(comps + L.comp_a, L.na, (float)sa, (float)(y - L.centre), L.shift_a);
             }
             if (lgmm) {
                 lb -= y;
@@ -843,7 +1029,7 @@ namespace {
 // Fold one GMM1/LGMM1 mixture into device records (host fp64, reference
 // formulas).  Returns the LSE shift (dense) or log p_accept (quantized).
 struct Folded {
-    double shift = 0.0, logpacc = 0.0;
+    double shift = 0.0, logpacc = 0.0, amax = 0.0;
 };
 
 Folded fold_mixture(int kind, bool quant, int flags, double low, double high, double centre,
@@ -891,9 +1077,12 @@ Folded fold_mixture(int kind, bool quant, int flags, double low, double high, do
         // fp64 records in exp_scaled units (see tpe_device.h: u = K t)
         out64[k] = Comp<double>{(mu[k] - centre) * (a[k] * sK), a[k] * sK, (c[k] - M) * kExpScale,
                                 w[k]};
-        if (out32)
-            out32[k] = Comp<float>{(float)mu[k], (float)(a[k] * std::sqrt(l2e)),
+        if (out32) {
+            const double a2 = a[k] * std::sqrt(l2e);
+            out32[k] = Comp<float>{(float)((mu[k] - centre) * a2), (float)a2,
                                    (float)((c[k] - M) * l2e), (float)w[k]};
+            f.amax = std::max(f.amax, (double)out32[k].a);
+        }
     }
     return f;
 }
@@ -957,6 +1146,9 @@ void launch_round(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
 // every chunk would start to show.  Config 5 (~1200 workgroups): 7 chunks
 // (sweep in DESIGN.md section 6).
 constexpr int64_t kChunkTargetWG = 8192;
+// k_rescore workgroups per (round, label): each walks its share of the
+// compacted list in steps of kR * 256 candidates
+constexpr int32_t kRescoreWG = 128;
 constexpr int32_t kMinChunk = 2048;
 
 int dense_chunks(const tpe_ctx* ctx, uint32_t gx, int nl) {
@@ -982,6 +1174,36 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
     if constexpr (sizeof(T) == 8) comps = ctx->P->comps64.p; else comps = ctx->P->comps32.p;
     const int32_t* grp = ctx->P->groups.p + ctx->P->group_off[DENSE_GMM];
     const int nch = a.S.cpack ? dense_chunks(ctx, a.gx, nl) : 1;
+    if (sizeof(T) == 8 && ctx->screen && a.S.cpack == 0) {   // fp32 screen + fp64 re-score
+        const size_t cells = (size_t)a.n_rounds * nl;
+        HIPCHK(ctx, ctx->scr_hi.reserve(cells * a.n));
+        HIPCHK(ctx, ctx->scr_idx.reserve(cells * a.n));
+        HIPCHK(ctx, ctx->scr_lb.reserve(cells));
+        HIPCHK(ctx, ctx->scr_cnt.reserve(cells));
+        HIPCHK(ctx, hipMemsetAsync(ctx->scr_lb.p, 0, cells * sizeof(unsigned long long), ctx->stream));
+        HIPCHK(ctx, hipMemsetAsync(ctx->scr_cnt.p, 0, cells * sizeof(int32_t), ctx->stream));
+        HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
+        hipLaunchKernelGGL((k_screen<kR, true>), dim3(a.gx, nl, a.gz), dim3(kBlock), 0, ctx->stream,
+                           ctx->P->labels.p, grp, ctx->P->comps32.p, ctx->P->samp.p, a.n,
+                           a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->scr_hi.p, ctx->scr_lb.p,
+                           ctx->errflag.p, a.S, nullptr, nullptr, nullptr);
+        HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
+        const unsigned sx = (unsigned)std::min<int64_t>((a.n + kBlock - 1) / kBlock, 1024);
+        hipLaunchKernelGGL(k_select, dim3(sx, nl, a.gz), dim3(kBlock), 0, ctx->stream, ctx->scr_hi.p,
+                           a.n, nl, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p);
+        const unsigned G = (unsigned)std::min<int32_t>(a.tiles, kRescoreWG);
+        hipLaunchKernelGGL((k_rescore<kR>), dim3(G, nl, a.gz), dim3(kBlock), 0, ctx->stream,
+                           ctx->P->labels.p, grp, ctx->P->comps64.p, ctx->P->samp.p, a.n,
+                           a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->P->n_labels, a.tiles,
+                           ctx->scr_cnt.p, ctx->scr_idx.p, ctx->partials.p);
+        ctx->scr_cnt_h.resize(cells);
+        HIPCHK(ctx, hipMemcpyAsync(ctx->scr_cnt_h.data(), ctx->scr_cnt.p, cells * sizeof(int32_t),
+                                   hipMemcpyDeviceToHost, ctx->stream));
+        ctx->screen_total += (int64_t)cells * a.n;
+        ctx->screen_pending = true;
+        bracket(ctx, DENSE_GMM, 1);
+        return ctx->hip(hipGetLastError(), "screen launch");
+    }
     if (nch > 1) {
         int32_t na_max = 1;
         for (int m : {DENSE_GMM, DENSE_LGMM})
@@ -1201,6 +1423,8 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         g.count[m] = 1;
     }
     RoundArgs a{n, cand_offset, seed, n_rounds, tiles, cand_in_dev, olb, ola, S, gx, gz};
+    ctx->screen_total = ctx->screen_rescored = 0;
+    ctx->screen_pending = false;
     const bool sample = cand_in_dev == nullptr;
     int64_t evals_q[2] = {0, 0};
     HIPCHK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
@@ -1266,6 +1490,17 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
                                    (size_t)n_rounds * L * sizeof(tpe_label_result),
                                    hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->screen_ms = 0.f;
+    if (ctx->screen_pending) {
+        for (int32_t c : ctx->scr_cnt_h) ctx->screen_rescored += c;
+        if (getenv("TPE_SCREEN_DEBUG")) {
+            fprintf(stderr, "screen counts:");
+            for (int32_t c : ctx->scr_cnt_h) fprintf(stderr, " %d", c);
+            fprintf(stderr, "\n");
+        }
+        ctx->screen_pending = false;
+        HIPCHK(ctx, hipEventElapsedTime(&ctx->screen_ms, ctx->evs[0], ctx->evs[1]));
+    }
     HIPCHK(ctx, hipEventElapsedTime(&ctx->score_ms, ctx->ev0, ctx->ev1));
     HIPCHK(ctx, hipEventElapsedTime(&ctx->round_ms, ctx->ev0, ctx->ev2));
     for (int m = 0; m < kNumModes; ++m)
@@ -1385,6 +1620,7 @@ int set_posterior_impl(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_lab
                                         mus + off, sigmas + off, n, c64.data() + at, c32.data() + at);
                 (side ? o.shift_a : o.shift_b) = f.shift;
                 (side ? o.logpacc_a : o.logpacc_b) = f.logpacc;
+                (side ? o.amax_a : o.amax_b) = (float)f.amax;
             }
             (side ? o.comp_a : o.comp_b) = at;
         }
@@ -1482,6 +1718,7 @@ int tpe_ctx_create(int device, int precision, tpe_ctx** out) {
     for (int m = 0; m < kNumModes; ++m)
         ok = ok && hipEventCreate(&c->evm[m][0]) == hipSuccess &&
              hipEventCreate(&c->evm[m][1]) == hipSuccess;
+    ok = ok && hipEventCreate(&c->evs[0]) == hipSuccess && hipEventCreate(&c->evs[1]) == hipSuccess;
     if (!ok) {
         g_create_error = "stream/event creation failed";
         tpe_ctx_destroy(c);
@@ -1495,6 +1732,8 @@ int tpe_ctx_create(int device, int precision, tpe_ctx** out) {
     c->chunks_forced = ch ? std::max(1, atoi(ch)) : 0;
     const char* pw = getenv("TPE_PACK_WIDE");   // experiments: kR slots per thread when packed
     c->pack_wide = pw && pw[0] == '1';
+    const char* ns = getenv("TPE_NO_SCREEN");   // tests / experiments: unscreened fp64 rounds
+    c->screen = !(ns && ns[0] == '1');
     *out = c;
     return TPE_OK;
 }
@@ -1526,6 +1765,13 @@ void tpe_ctx_destroy(tpe_ctx* c) {
     for (int m = 0; m < kNumModes; ++m)
         for (int j = 0; j < 2; ++j)
             if (c->evm[m][j]) (void)hipEventDestroy(c->evm[m][j]);
+    for (int j = 0; j < 2; ++j)
+        if (c->evs[j]) (void)hipEventDestroy(c->evs[j]);
+    c->scr_hi.release();
+    c->scr_idx.release();
+    c->scr_lb.release();
+    c->scr_cnt.release();
+    c->chunk_part.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -1599,6 +1845,35 @@ int tpe_score(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, double
     return TPE_OK;
 }
 
+int tpe_screen_probe(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, double* score32,
+                     double* err_bound) {
+    if (!ctx || (n > 0 && (!cand || !score32 || !err_bound))) return TPE_ERR_ARG;
+    if (label < 0 || label >= ctx->P->n_labels) return ctx->fail(TPE_ERR_ARG, "label out of range");
+    const DLabel& d = ctx->P->h_labels[label];
+    if (d.mode != DENSE_GMM && d.mode != DENSE_LGMM)
+        return ctx->fail(TPE_ERR_ARG, "screen probe: label is not a dense GMM1/LGMM1 label");
+    if (n == 0) return TPE_OK;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    HIPCHK(ctx, ctx->cand.reserve(n));
+    HIPCHK(ctx, ctx->out_lb.reserve(n));
+    HIPCHK(ctx, ctx->out_la.reserve(n));
+    HIPCHK(ctx, ctx->one_group.reserve(1));
+    HIPCHK(ctx, ctx->rounds.reserve(1));
+    HIPCHK(ctx, ctx->errflag.reserve(1));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->one_group.p, &label, sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->cand.p, cand, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    const uint32_t tiles = (uint32_t)((n + kTile - 1) / kTile);
+    hipLaunchKernelGGL((k_screen<kR, false>), dim3(tiles, 1, 1), dim3(kBlock), 0, ctx->stream,
+                       ctx->P->labels.p, ctx->one_group.p, ctx->P->comps32.p, ctx->P->samp.p, n, 0,
+                       0, ctx->rounds.p, 1, nullptr, nullptr, ctx->errflag.p, Slots{0, 0, 1},
+                       ctx->cand.p, ctx->out_lb.p, ctx->out_la.p);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipMemcpyAsync(score32, ctx->out_lb.p, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(err_bound, ctx->out_la.p, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return TPE_OK;
+}
+
 int tpe_merge_results(const tpe_label_result* parts, int32_t n_parts, int32_t n,
                       tpe_label_result* out) {
     if (!parts || !out || n_parts <= 0 || n < 0) return TPE_ERR_ARG;
@@ -1624,6 +1899,29 @@ int tpe_last_timing(const tpe_ctx* ctx, float* score_ms, float* round_ms) {
 }
 
 int64_t tpe_last_evals(const tpe_ctx* ctx) { return ctx ? ctx->evals : -1; }
+
+int tpe_last_screen(const tpe_ctx* ctx, int64_t* screened, int64_t* rescored, float* screen_ms) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (screened) *screened = ctx->screen_total;
+    if (rescored) *rescored = ctx->screen_rescored;
+    if (screen_ms) *screen_ms = ctx->screen_ms;
+    return TPE_OK;
+}
+
+int tpe_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
+    if (!ctx) return TPE_ERR_ARG;
+    switch (option) {
+        case TPE_OPT_SCREEN: ctx->screen = value != 0; break;
+        case TPE_OPT_SPLITK: ctx->splitk = value != 0; break;
+        case TPE_OPT_DEDUP: ctx->dedup = value != 0; break;
+        case TPE_OPT_CHUNKS:
+            if (value < 0 || value > 4096) return ctx->fail(TPE_ERR_ARG, "chunks must be in [0, 4096]");
+            ctx->chunks_forced = (int32_t)value;
+            break;
+        default: return ctx->fail(TPE_ERR_ARG, "unknown option " + std::to_string(option));
+    }
+    return TPE_OK;
+}
 
 int tpe_last_mode_stats(const tpe_ctx* ctx, float* ms, int64_t* evals) {
     if (!ctx) return TPE_ERR_ARG;

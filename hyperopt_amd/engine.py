@@ -206,6 +206,32 @@ class Engine(object):
     def last_evals(self):
         return int(self.lib.tpe_last_evals(self.h))
 
+    def last_screen(self, with_ms=False):
+        """(candidates screened in fp32, candidates re-scored in fp64) of the
+        last round ((0, 0) when the round was not screened); with_ms adds the
+        device ms of the fp32 screening kernel."""
+        a, b, ms = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_float()
+        self._check(self.lib.tpe_last_screen(self.h, ctypes.byref(a), ctypes.byref(b),
+                                             ctypes.byref(ms)))
+        return (a.value, b.value, ms.value) if with_ms else (a.value, b.value)
+
+    OPTIONS = {'screen': L.TPE_OPT_SCREEN, 'splitk': L.TPE_OPT_SPLITK, 'dedup': L.TPE_OPT_DEDUP,
+               'chunks': L.TPE_OPT_CHUNKS}
+
+    def set_option(self, name, value):
+        """Engine switches (include/hyperopt_tpe.h TPE_OPT_*): 'screen',
+        'splitk', 'dedup' (bool), 'chunks' (int, 0 = auto)."""
+        self._check(self.lib.tpe_set_option(self.h, self.OPTIONS[name], int(value)))
+
+    def screen_probe(self, label, cand):
+        """fp32 screen score and its error bound for supplied candidates of a
+        dense resident label (diagnostic, tpe_screen_probe)."""
+        cand = _f64(cand).ravel()
+        s, e = np.empty(len(cand)), np.empty(len(cand))
+        self._check(self.lib.tpe_screen_probe(self.h, int(label), _ptr(cand), len(cand), _ptr(s),
+                                              _ptr(e)))
+        return s, e
+
     # slot 0: dense GMM1 -- and, in sampled tile/packed rounds, the dense
     # LGMM1 labels too (one merged launch; slot 1 then stays 0)
     MODES = ('dense', 'dense_lgmm1', 'quant_gmm1', 'quant_lgmm1', 'categorical')

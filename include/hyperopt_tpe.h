@@ -275,6 +275,34 @@ int64_t tpe_last_evals(const tpe_ctx *ctx);
  * the GMM1 + LGMM1 launch and its evaluations, slot 1 stays 0. */
 int tpe_last_mode_stats(const tpe_ctx *ctx, float *ms, int64_t *evals);
 
+/* Candidates the last round screened in fp32 (sampled tile-map rounds of
+ * the dense GMM1/LGMM1 labels, TPE_F64 contexts) and how many of them it
+ * re-scored in fp64 -- those whose rigorous fp32 error interval reaches the
+ * largest lower bound of their round; the winner and its lpdfs are those
+ * of the plain fp64 round (tpe_device.h screen_err).  screen_ms: device
+ * time of the fp32 screening kernel alone (HIP events). */
+int tpe_last_screen(const tpe_ctx *ctx, int64_t *screened, int64_t *rescored,
+                    float *screen_ms);
+
+/* Diagnostic of the screen (tests): for caller-supplied candidates of one
+ * dense resident label, the fp32 score lpdf_below - lpdf_above the screen
+ * computes and its rigorous error bound (x 1.25, as used by the round):
+ * |score32 - score64| <= err_bound for every finite bound. */
+int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
+                     double *score32, double *err_bound);
+
+/* Engine options (defaults in brackets):
+ *   TPE_OPT_SCREEN  fp32 screen + fp64 re-score of sampled tile rounds [1]
+ *   TPE_OPT_SPLITK  split-K map for small sampled rounds                [1]
+ *   TPE_OPT_DEDUP   quantized labels scored once per grid value         [1]
+ *   TPE_OPT_CHUNKS  chunks of the packed map's above mixtures (0 auto)  [0]
+ * None of them changes a winner; they exist for tests and experiments. */
+#define TPE_OPT_SCREEN 1
+#define TPE_OPT_SPLITK 2
+#define TPE_OPT_DEDUP 3
+#define TPE_OPT_CHUNKS 4
+int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
+
 #ifdef __cplusplus
 }
 #endif

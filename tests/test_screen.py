@@ -1,0 +1,119 @@
+"""The fp32 screen of the fp64 round (tpe_engine.hip k_screen / k_select /
+k_rescore): every dense candidate is scored in packed fp32 with a rigorous
+error bound, and only the candidates whose bound interval reaches the
+round's largest lower bound are re-scored in fp64.
+
+* the bound holds: |score32 - score64| <= bound for every candidate of a
+  config-3 posterior (sampled, far-tail and boundary candidates), where
+  score64 is the plain fp64 path (tpe_score);
+* the screened round is the fp64 round: winners, values, scores and lpdfs
+  are bit-identical with the screen on and off (configs 2, 3 and 4, host and
+  device posteriors, a posterior whose candidates all fail certification).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _dense_labels(posts):
+    return [i for i, p in enumerate(posts) if p.family != 'categorical' and p.q is None]
+
+
+@pytest.fixture(scope='module')
+def eng():
+    from hyperopt_amd.engine import Engine
+    e = Engine(0, 'f64')
+    yield e
+    e.close()
+
+
+def test_screen_bound_holds(eng):
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.workloads import mixed_history
+    hist = mixed_history(32, 10000, seed=0)
+    posts = hist.posteriors()
+    eng.set_posterior(*P.pack(posts))
+    worst, cert = 0.0, []
+    for li in _dense_labels(posts):
+        p = posts[li]
+        samp = eng.GMM1 if p.family == 'GMM1' else eng.LGMM1
+        x = samp(*p.below, low=p.low, high=p.high, q=None, seed=11, size=(20000,), stream=li)
+        # plus far tails and the bounds themselves
+        if p.family == 'GMM1':
+            lo, hi = (p.low, p.high) if p.low is not None else (-30.0, 30.0)
+            extra = np.concatenate([np.linspace(lo, hi, 2001), [lo, hi, 0.0, 1e-9]])
+        else:
+            extra = np.exp(np.linspace(p.low, p.high, 2001))
+        x = np.concatenate([x, extra])
+        s32, err = eng.screen_probe(li, x)
+        lb, la, _ = eng.score(li, x)
+        s64 = lb - la
+        ok = np.isfinite(err) & np.isfinite(s64)
+        cert.append(ok.mean())
+        assert np.all(np.abs(s32[ok] - s64[ok]) <= err[ok]), li
+        worst = max(worst, float(np.max(np.abs(s32[ok] - s64[ok]) / err[ok])))
+    # the bound is rigorous, not tight: observed error well inside it
+    assert worst < 0.5, worst
+    assert min(cert) > 0.9, cert
+    print('screen bound: worst |s32 - s64| / bound = %.3g, certified %.4f..%.4f'
+          % (worst, min(cert), max(cert)))
+
+
+def _suggest_both(eng, C, rnd, seed):
+    eng.set_option('screen', 1)
+    a = eng.suggest(seed, C, round=rnd)
+    screened, rescored = eng.last_screen()
+    eng.set_option('screen', 0)
+    b = eng.suggest(seed, C, round=rnd)
+    assert eng.last_screen() == (0, 0)
+    eng.set_option('screen', 1)
+    return a, b, screened, rescored
+
+
+def _assert_same(a, b):
+    for f in ('index', 'value', 'score', 'lpdf_below', 'lpdf_above', 'label'):
+        assert np.array_equal(a[f], b[f], equal_nan=f != 'index' and f != 'label'), f
+
+
+@pytest.mark.parametrize('config', ['config2', 'config3', 'config3_device', 'config4_device'])
+def test_screened_round_is_the_fp64_round(eng, config):
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.workloads import conditional_history, hartmann_history, mixed_history
+    if config == 'config2':
+        hist = hartmann_history(2000, seed=0)
+    elif config.startswith('config4'):
+        hist = conditional_history(5000, seed=0)
+    else:
+        hist = mixed_history(32, 10000, seed=0)
+    if config.endswith('device'):
+        eng.build_posterior(*hist.device_inputs(), gamma=0.25, prior_weight=1.0)
+    else:
+        eng.set_posterior(*P.pack(hist.posteriors()))
+    fracs = []
+    for rnd, (C, seed) in enumerate([(1 << 20, 5), (3000, 6), (1 << 16, 7), (5000, 8)]):
+        a, b, screened, rescored = _suggest_both(eng, C, rnd, seed)
+        _assert_same(a, b)
+        assert screened > 0 and 0 < rescored <= screened
+        fracs.append(rescored / screened)
+    print('%s: re-scored fraction per round %s' % (config, ['%.4f' % f for f in fracs]))
+
+
+def test_screen_uncertified_candidates(eng):
+    """A posterior whose above mixture sits thousands of sigmas away from
+    every candidate: the fp32 sums underflow, nothing is certified, every
+    candidate is re-scored and the round is still the fp64 round."""
+    from hyperopt_amd import posterior as P
+    lp = [P.LabelPosterior('far', 'GMM1',
+                           (np.array([1.0]), np.array([0.0]), np.array([0.01])),
+                           (np.array([0.5, 0.5]), np.array([-50.0, 50.0]), np.array([0.01, 0.01])),
+                           low=None, high=None, q=None),
+          P.LabelPosterior('near', 'GMM1',
+                           (np.array([0.5, 0.5]), np.array([0.0, 1.0]), np.array([0.3, 0.2])),
+                           (np.array([1.0]), np.array([0.5]), np.array([2.0])),
+                           low=-3.0, high=3.0, q=None)]
+    eng.set_posterior(*P.pack(lp))
+    a, b, screened, rescored = _suggest_both(eng, 1 << 14, 3, 21)
+    _assert_same(a, b)
+    # label 0: all 2^14 re-scored; label 1: a few
+    assert rescored >= (1 << 14) and rescored < screened
