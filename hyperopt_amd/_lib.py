@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libhyperopt_tpe.so')
 HEADER = os.path.join(os.path.dirname(HERE), 'include', 'hyperopt_tpe.h')
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 TPE_OK = 0
 TPE_ERR_VALUE = -1
@@ -79,6 +79,8 @@ SIGNATURES = {
     'tpe_abi_version': (ctypes.c_int, []),
     'tpe_source_hash': (ctypes.c_char_p, []),
     'tpe_ctx_create': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]),
+    'tpe_ctx_create_multi': (ctypes.c_int, [_P, _I32, ctypes.c_int, ctypes.POINTER(_P)]),
+    'tpe_ctx_devices': (ctypes.c_int32, [_P, _P, _I32]),
     'tpe_ctx_destroy': (None, [_P]),
     'tpe_last_error': (ctypes.c_char_p, [_P]),
     'tpe_gmm1_lpdf': (ctypes.c_int, [_P, _P, _I64, _P, _P, _P, _I32, _I32, _D, _D, _D, _P]),

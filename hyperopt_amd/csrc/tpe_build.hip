@@ -1357,26 +1357,26 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
 // ================================================================ C ABI ====
 extern "C" {
 
-int tpe_history_reset(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
+TPE_DEV int tpe1_history_reset(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
                       const double* cat_p, int64_t n_cat_p) {
     if (!ctx) return TPE_ERR_ARG;
     return history_reset(ctx, specs, n_labels, cat_p, n_cat_p);
 }
 
-int tpe_history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial,
+TPE_DEV int tpe1_history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial,
                        const double* obs_val) {
     if (!ctx || !n_new) return TPE_ERR_ARG;
     return history_append(ctx, n_new, obs_trial, obs_val);
 }
 
-int tpe_build_posterior_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials,
+TPE_DEV int tpe1_build_posterior_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials,
                                  int64_t n_valid, double gamma, double prior_weight, int32_t lf,
                                  int32_t* n_below_out) {
     if (!ctx) return TPE_ERR_ARG;
     return build_resident(ctx, losses, n_trials, n_valid, gamma, prior_weight, lf, n_below_out);
 }
 
-int tpe_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
+TPE_DEV int tpe1_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
                         const double* cat_p, int64_t n_cat_p, const double* losses,
                         int64_t n_trials, const int64_t* obs_off, const int32_t* obs_trial,
                         const double* obs_val, double gamma, double prior_weight, int32_t lf,

@@ -13,7 +13,13 @@
 #include "../../include/hyperopt_tpe.h"
 #include "tpe_device.h"
 
+struct tpe_ctx;
+
 namespace tpe_rt {
+
+struct RescoreChunkH {   // k_rescore work item: (round * labels + label position, chunk)
+    int32_t cell, j;
+};
 
 using tpe::Comp;
 using tpe::DLabel;
@@ -127,6 +133,15 @@ struct BuildBufs {
 // numpy's pairwise float64 summation (np.sum of a contiguous vector)
 double np_pairwise_sum(const double* a, size_t n);
 
+// Cross-shard exchange of the quantized labels' grid windows (per label the
+// order-preserving min and max grid index, mm[0..nq) and mm[nq..2nq)): every
+// shard of a multi-device round waits for all of them and continues with
+// the window of the whole candidate set (tpe_multi.hip).
+struct QExchange {
+    virtual int exchange(tpe_ctx* ctx, std::vector<unsigned long long>& mm) = 0;
+    virtual ~QExchange() {}
+};
+
 }  // namespace tpe_rt
 
 struct tpe_ctx {
@@ -181,6 +196,8 @@ struct tpe_ctx {
     DevBuf<unsigned long long> scr_lb;
     DevBuf<int32_t> scr_cnt;
     std::vector<int32_t> scr_cnt_h;
+    DevBuf<int64_t> scr_chunks;          // k_rescore chunk table ({cell, chunk} int32 pairs)
+    std::vector<tpe_rt::RescoreChunkH> scr_chunks_h;
     int64_t screen_total = 0, screen_rescored = 0;   // last round
     bool screen_pending = false;         // scr_cnt_h awaits the round's final sync
     hipEvent_t evs[2] = {};              // brackets k_screen alone
@@ -189,6 +206,14 @@ struct tpe_ctx {
     int64_t built_n_trials = 0;          // last tpe_build_posterior: history size
     int32_t built_n_below = 0;           //   and its below-set size
     float build_ms = 0.f;                // device time of the last build
+
+    // multi-device contexts (tpe_ctx_create_multi): the primary context owns
+    // one peer context per further device; a peer running one shard of a
+    // round gets the whole problem's size and the window exchange
+    std::vector<tpe_ctx*> peers;
+    int64_t hint_n = 0;                  // candidates per round over all shards (0: this call's)
+    int32_t hint_rounds = 0;             // rounds over all shards (0: this call's)
+    tpe_rt::QExchange* qx = nullptr;
 
     int fail(int code, const std::string& m) {
         err = m;
@@ -200,6 +225,34 @@ struct tpe_ctx {
         return TPE_ERR_HIP;
     }
 };
+
+// per-device implementations of the entry points a multi-device context
+// forwards or shards (tpe_multi.hip exports the public names)
+#define TPE_DEV __attribute__((visibility("hidden")))
+extern "C" {
+TPE_DEV int tpe1_set_posterior(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_labels,
+                               const double* weights, const double* mus, const double* sigmas,
+                               int64_t n_components);
+TPE_DEV int tpe1_suggest(tpe_ctx* ctx, uint64_t seed, uint32_t round, int64_t n_candidates,
+                         int64_t cand_offset, tpe_label_result* out);
+TPE_DEV int tpe1_suggest_batch(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds,
+                               int32_t n_rounds, int64_t n_candidates, int64_t cand_offset,
+                               tpe_label_result* out);
+TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value);
+TPE_DEV int tpe1_history_reset(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
+                               const double* cat_p, int64_t n_cat_p);
+TPE_DEV int tpe1_history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial,
+                                const double* obs_val);
+TPE_DEV int tpe1_build_posterior_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials,
+                                          int64_t n_valid, double gamma, double prior_weight,
+                                          int32_t lf, int32_t* n_below_out);
+TPE_DEV int tpe1_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
+                                 const double* cat_p, int64_t n_cat_p, const double* losses,
+                                 int64_t n_trials, const int64_t* obs_off, const int32_t* obs_trial,
+                                 const double* obs_val, double gamma, double prior_weight,
+                                 int32_t lf, int32_t* n_below_out);
+TPE_DEV void tpe1_ctx_destroy(tpe_ctx* ctx);
+}
 
 #define HIPCHK(ctx, call)                                  \
     do {                                                   \

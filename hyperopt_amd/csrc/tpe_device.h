@@ -330,8 +330,9 @@ __device__ __forceinline__ void lse_dense(const Comp<double>* __restrict__ c, in
 // Candidates go in pairs through packed fp32 (v_pk_fma_f32 on a float2, the
 // component constants broadcast from SGPRs): 2 packed FMAs + 2 v_exp_f32 +
 // one packed add per two evaluations.  The 8 terms of a record batch are
-// added as a tree before they join the running sum, which keeps the
-// summation error bound at (K/8 + 11) u instead of K u (screen_bound).
+// added as a tree, 16 batch sums into a mid sum, and the mid sums into the
+// running sum, which keeps the summation error bound at (K/128 + 27) u
+// instead of K u (screen_err).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int R>
@@ -380,6 +381,12 @@ __device__ __forceinline__ void lse_acc(const Comp<float>* __restrict__ c, int n
                 }
             }
         };
+        // batch trees go into mid sums, flushed into the running sums every
+        // 16 batches (128 records)
+        f32x2 mid2[PP];
+        float mid1 = 0.0f;
+#pragma unroll
+        for (int p = 0; p < PP; ++p) mid2[p] = f32x2{0.0f, 0.0f};
         auto accum = [&]() {
 #pragma unroll
             for (int p = 0; p < P; ++p) {
@@ -387,13 +394,24 @@ __device__ __forceinline__ void lse_acc(const Comp<float>* __restrict__ c, int n
 #pragma unroll
                 for (int u = 0; u < U; ++u)
                     e[u] = f32x2{__builtin_amdgcn_exp2f(t2[u][p].x), __builtin_amdgcn_exp2f(t2[u][p].y)};
-                acc2[p] += ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
+                mid2[p] += ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
             }
             if constexpr (kOdd) {
                 float e[U];
 #pragma unroll
                 for (int u = 0; u < U; ++u) e[u] = __builtin_amdgcn_exp2f(t1[u]);
-                acc1 += ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
+                mid1 += ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
+            }
+        };
+        auto flush = [&]() {
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+                acc2[p] += mid2[p];
+                mid2[p] = f32x2{0.0f, 0.0f};
+            }
+            if constexpr (kOdd) {
+                acc1 += mid1;
+                mid1 = 0.0f;
             }
         };
         if (nbat > 0) load(Am, Aa, Ac, 0);
@@ -409,11 +427,13 @@ __device__ __forceinline__ void lse_acc(const Comp<float>* __restrict__ c, int n
             load(Am, Aa, Ac, (b + 2) * U);
             __builtin_amdgcn_sched_barrier(0);
             accum();
+            if (((b + 2) & 15) == 0) flush();
         }
         if (b < nbat) {
             expo(Am, Aa, Ac);
             accum();
         }
+        flush();
         for (int k = nfull; k < n; ++k) {
             const float m = c[k].mu, a = c[k].a, cc = c[k].c;
 #pragma unroll
@@ -460,37 +480,44 @@ __device__ __forceinline__ void lse_dense(const Comp<float>* __restrict__ c, int
 // The exact fp64 round screens every candidate with the fp32 sums above and
 // re-scores in fp64 only those that can still win.  screen_err bounds
 // |lpdf32 - lpdf| of ONE mixture (natural-log units) for a candidate at
-// recentred |x'| = X, rigorously, from the fp32 arithmetic (u = 2^-24):
-//  * a term is "relevant" if its exact exponent t = c' - z^2 >= -T0 (T0 =
-//    125, log2 units, so it stays a normal fp32 number); since c' <= 0 then
-//    |z| <= sqrt(T0) and |c'| <= T0;
-//  * z = fma(x32, a32, -m32): |z32 - z| <= zeta = (3 X amax + 2 sqrt(T0)) u
-//    (x32 and a32 rounded once each, |m| <= X a + sqrt(T0) for a relevant
-//    term, one rounding of the fma);
-//  * t = fma(-z, z, c32): |t32 - t| <= dt = (2 T0 + 1) u + zeta (2 sqrt(T0)
+// recentred x' (|x'| = X, |fl32(x') - x'| = dx), rigorously, from the fp32
+// arithmetic (u = 2^-24), with S32 its fp32 sum (log2 S32 = l2):
+//  * split the terms at an exponent cut -T (log2 units), T chosen per
+//    candidate so that the terms below it are negligible:
+//    T = (43 + log2(2K) - l2) / 0.9997, clamped to [16, 125] (so relevant
+//    terms stay normal fp32 numbers);
+//  * a "relevant" term has exact t = c' - z^2 >= -T; since c' <= 0 then
+//    |z| <= sqrt(T) and |c'| <= T;
+//  * z = fma(x32, a32, -m32): |z32 - z| <= zeta = dx amax + (2 X amax +
+//    2 sqrt(T)) u (x32 rounded, a32 rounded, |m| <= X a + sqrt(T) for a
+//    relevant term, one rounding of the fma);
+//  * t = fma(-z, z, c32): |t32 - t| <= dt = (2 T + 1) u + zeta (2 sqrt(T)
 //    + zeta);
 //  * v_exp_f32: 2 ulp (2^-22) relative; so a relevant term is within
 //    rho = 0.7 dt + 2.5e-7 relative (dt <= 0.01);
-//  * the sum of positive terms: (K/8 + 11) u relative (tree of 8, then a
-//    running sum; a tail of < 8 terms added one by one);
-//  * the irrelevant terms (< 2^-124 each, exact or computed -- dt <= 0.01
-//    keeps |z32| within 1e-4 relative of |z|) add at most K 2^-124 / S,
-//    S >= 2^-60 for a certified candidate;
+//  * the sum of positive terms: (K/128 + 27) u relative (tree of 8, mid sum
+//    of 16 batches, running sum, a tail of < 8 terms added one by one);
+//  * the other terms: exact < 2^-T, computed < 2^-0.9997T (dt <= 0.01 keeps
+//    |z32| within 1e-4 relative of |z|), at most 2 K 2^-0.9997T / S <=
+//    2^-42 relative (S >= S32 / 1.01);
 //  * v_log_f32: 2^-22 (|log2 S| + 1) absolute.
 // Uncertified (S < 2^-60, NaN, dt > 0.01) returns +inf: the candidate is
 // always re-scored, which also keeps the reference's NaN-greatest order.
 constexpr float kScreenMinAcc = 0x1.0p-60f;
 
-__device__ __forceinline__ double screen_err(float amax, int K, double X, float acc, float l2) {
+__device__ __forceinline__ double screen_err(float amax, int K, double X, double dx, float acc,
+                                             float l2) {
     if (!(acc >= kScreenMinAcc) || !(acc <= 0x1.0p+100f) || !(X <= 1e30)) return __builtin_inf();
-    constexpr double u = 0x1.0p-24, sqT0 = 11.1804, T0 = 125.0;
-    const double zeta = (3.0 * X * (double)amax * 1.001 + 2.0 * sqT0) * u * 1.001;
-    const double dt = (2.0 * T0 + 1.0) * u + zeta * (2.0 * sqT0 + zeta);
+    constexpr double u = 0x1.0p-24;
+    const double T = fmin(125.0, fmax(16.0, (43.0 + log2(2.0 * (double)K) - (double)l2) / 0.9997));
+    const double sqT = sqrt(T) * (1.0 + 1e-12);
+    const double A = (double)amax * 1.001;
+    const double zeta = (dx * A + (2.0 * X * A + 2.0 * sqT) * u) * 1.001;
+    const double dt = (2.0 * T + 1.0) * u + zeta * (2.0 * sqT + zeta);
     if (!(dt <= 0.01)) return __builtin_inf();
     const double rho = 0.7 * dt + 2.5e-7;
-    const double gsum = ((double)(K / 8) + 11.0) * u * 1.01;
-    const double negl = (double)K * 0x1.0p-64;
-    const double rel = rho + gsum + negl;
+    const double gsum = ((double)(K / 128) + 28.0) * u * 1.01;
+    const double rel = rho + gsum + 0x1.0p-41;
     return 1.02 * rel + 0x1.0p-22 * 0.6931471805599453 * (fabs((double)l2) + 1.0);
 }
 

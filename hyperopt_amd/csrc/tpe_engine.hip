@@ -469,7 +469,7 @@ __global__ __launch_bounds__(kBlock) void k_screen(
     bool valid[R];
     draw_slots<DENSE_ANY, SAMPLE, R>(L, S, lgmm, samp, cand_in, n, cand_offset, seed, rounds, err,
                                      x, z, ci, gi, valid);
-    double y[R], X[R];
+    double y[R], X[R], dx[R];
     float xf[R], ab[R], aa[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -477,6 +477,7 @@ __global__ __launch_bounds__(kBlock) void k_screen(
         const double xr = y[r] - L.centre;
         xf[r] = (float)xr;
         X[r] = fabs(xr);
+        dx[r] = fabs((double)xf[r] - xr);
     }
     lse_acc<R>(comps32 + L.comp_b, L.nb, xf, ab);
     lse_acc<R>(comps32 + L.comp_a, L.na, xf, aa);
@@ -489,8 +490,8 @@ __global__ __launch_bounds__(kBlock) void k_screen(
         const double lb = (double)l2b * 0.6931471805599453 + L.shift_b;
         const double la = (double)l2a * 0.6931471805599453 + L.shift_a;
         const double s = lb - la;
-        const double E = 1.25 * (screen_err(L.amax_b, L.nb, X[r], ab[r], l2b) +
-                                 screen_err(L.amax_a, L.na, X[r], aa[r], l2a) +
+        const double E = 1.25 * (screen_err(L.amax_b, L.nb, X[r], dx[r], ab[r], l2b) +
+                                 screen_err(L.amax_a, L.na, X[r], dx[r], aa[r], l2a) +
                                  fp64_err(L.nb + L.na, fabs(lb) + fabs(la) + fabs(y[r])));
         if constexpr (!SAMPLE) {
             s_out[ci[r]] = s;
@@ -511,24 +512,64 @@ __global__ __launch_bounds__(kBlock) void k_screen(
     if (threadIdx.x == 0 && bk) atomicMax(lbkey + (size_t)blockIdx.z * nl + blockIdx.y, bk);
 }
 
+// Each workgroup owns a contiguous slice of its (round, label) row: it
+// counts its takers, reserves their places with ONE atomic (a per-wave
+// atomic on the row's counter serialised ~1.3M same-address atomics at
+// config 3: 12.5 ms), then writes them.
 __global__ __launch_bounds__(kBlock) void k_select(const float* __restrict__ hi, int64_t n, int32_t nl,
                                                    const unsigned long long* __restrict__ lbkey,
                                                    int32_t* __restrict__ cnt, int32_t* __restrict__ idx) {
     const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
     const size_t row = cell * (size_t)n;
     const uint64_t lb = lbkey[cell];
-    const int lane = threadIdx.x & 63;
-    for (int64_t i0 = (int64_t)blockIdx.x * kBlock; i0 < n; i0 += (int64_t)gridDim.x * kBlock) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t span = ((n + gridDim.x - 1) / gridDim.x + kBlock - 1) / kBlock * kBlock;
+    const int64_t lo = (int64_t)blockIdx.x * span, hi_end = min(n, lo + span);
+    int mine = 0;   // this wave's takers (lane 0's copy is authoritative)
+    for (int64_t i0 = lo; i0 < hi_end; i0 += kBlock) {
         const int64_t i = i0 + threadIdx.x;
-        const bool take = i < n && order_key((double)hi[row + i]) >= lb;
+        const bool take = i < hi_end && order_key((double)hi[row + i]) >= lb;
+        mine += (int)__popcll(__ballot(take));
+    }
+    __shared__ int wcount[kBlock / 64], wbase[kBlock / 64];
+    if (lane == 0) wcount[wave] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) tot += wcount[w];
+        int base = tot ? atomicAdd(cnt + cell, tot) : 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            wbase[w] = base;
+            base += wcount[w];
+        }
+    }
+    __syncthreads();
+    if (!wcount[wave]) return;   // wave-uniform; no barrier below
+    int at = wbase[wave];
+    for (int64_t i0 = lo; i0 < hi_end; i0 += kBlock) {
+        const int64_t i = i0 + threadIdx.x;
+        const bool take = i < hi_end && order_key((double)hi[row + i]) >= lb;
         const uint64_t m = __ballot(take);
-        if (m == 0) continue;   // wave-uniform
-        int base = 0;
-        if (lane == 0) base = atomicAdd(cnt + cell, (int)__popcll(m));
-        base = __shfl(base, 0);
-        if (take) idx[row + base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)i;
+        if (take) idx[row + at + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)i;
+        at += (int)__popcll(m);
     }
 }
+
+// empty partials for the rows (round blockIdx.z, label group[blockIdx.y])
+__global__ __launch_bounds__(kBlock) void k_fill_empty(const int32_t* __restrict__ group,
+                                                       int32_t n_labels, int32_t tiles,
+                                                       Partial* __restrict__ partials) {
+    Partial* prow = partials + ((size_t)blockIdx.z * n_labels + group[blockIdx.y]) * tiles;
+    for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < tiles; t += (int64_t)gridDim.x * kBlock)
+        prow[t] = Partial{0, INT64_MAX, 0.0, 0.0, 0.0};
+}
+
+// One workgroup per kR * 256 re-scored candidates of one (round, label)
+// (chunk table from the host: cell = round * nl + label position, chunk j
+// writes partial slot j of its row -- j < tiles because the row holds at
+// most n candidates).  Sized after the counts are read back, so the
+// hardware scheduler balances the chunks over the chip.
+using RescoreChunk = tpe_rt::RescoreChunkH;
 
 template <int R>
 __global__ __launch_bounds__(kBlock) void k_rescore(
@@ -536,66 +577,59 @@ __global__ __launch_bounds__(kBlock) void k_rescore(
     const Comp<double>* __restrict__ comps64, const SampRec* __restrict__ samp, int64_t n,
     int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, int32_t nl,
     int32_t n_labels, int32_t tiles, const int32_t* __restrict__ cnt, const int32_t* __restrict__ idx,
-    Partial* __restrict__ partials) {
-    const int li = group[blockIdx.y];
-    const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
-    Partial* prow = partials + ((size_t)blockIdx.z * n_labels + li) * tiles;
-    const Partial empty{0, INT64_MAX, 0.0, 0.0, 0.0};
-    if (threadIdx.x == 0)   // the round's partial slots beyond this grid: empty
-        for (int64_t t = (int64_t)gridDim.x + blockIdx.x; t < tiles; t += gridDim.x) prow[t] = empty;
-    const int64_t count = cnt[cell];
+    const RescoreChunk* __restrict__ chunks, Partial* __restrict__ partials) {
+    const RescoreChunk ch = chunks[blockIdx.x];
+    const int32_t z = ch.cell / nl, y = ch.cell % nl;
+    const int li = group[y];
+    Partial* prow = partials + ((size_t)z * n_labels + li) * tiles;
+    const int64_t count = cnt[ch.cell];
     constexpr int64_t per = (int64_t)R * kBlock;
-    if ((int64_t)blockIdx.x * per >= count) {   // uniform: no share of the list
-        if (threadIdx.x == 0) prow[blockIdx.x] = empty;
-        return;
-    }
+    const int64_t base = (int64_t)ch.j * per;
     const DLabel L = labels[li];
     __shared__ double exp_tab[kExpTabSize];
     load_exp_table(exp_tab);
     const bool lgmm = L.mode == DENSE_LGMM;
-    const int32_t* list = idx + cell * (size_t)n;
-    const uint32_t rk = rounds[blockIdx.z];
+    const int32_t* list = idx + (size_t)ch.cell * (size_t)n;
+    const uint32_t rk = rounds[z];
     uint64_t bk = 0;
     int64_t bi = INT64_MAX;
     double bv = 0.0, bl = 0.0, ba = 0.0;
-    for (int64_t base = (int64_t)blockIdx.x * per; base < count; base += (int64_t)gridDim.x * per) {
-        double x[R], y[R], lb[R], la[R];
-        int64_t gi[R];
-        bool valid[R];
+    double x[R], yv[R], lb[R], la[R];
+    int64_t gi[R];
+    bool valid[R];
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int64_t j = base + r * kBlock + threadIdx.x;
-            valid[r] = j < count;
-            gi[r] = cand_offset + (valid[r] ? list[j] : 0);
-            double v = lgmm ? 1.0 : 0.0;
-            if (valid[r]) {
-                if (lgmm) (void)sample_below<DENSE_LGMM>(L, samp + L.samp_off, seed, rk, (uint32_t)gi[r], v);
-                else (void)sample_below<DENSE_GMM>(L, samp + L.samp_off, seed, rk, (uint32_t)gi[r], v);
-            }
-            x[r] = v;
-            y[r] = lgmm ? log(v) : v;
+    for (int r = 0; r < R; ++r) {
+        const int64_t j = base + r * kBlock + threadIdx.x;
+        valid[r] = j < count;
+        gi[r] = cand_offset + (valid[r] ? list[j] : 0);
+        double v = lgmm ? 1.0 : 0.0;
+        if (valid[r]) {
+            if (lgmm) (void)sample_below<DENSE_LGMM>(L, samp + L.samp_off, seed, rk, (uint32_t)gi[r], v);
+            else (void)sample_below<DENSE_GMM>(L, samp + L.samp_off, seed, rk, (uint32_t)gi[r], v);
         }
-        lse_dense<R>(comps64 + L.comp_b, L.nb, L.shift_b, L.centre, y, lb, exp_tab);
-        lse_dense<R>(comps64 + L.comp_a, L.na, L.shift_a, L.centre, y, la, exp_tab);
+        x[r] = v;
+        yv[r] = lgmm ? log(v) : v;
+    }
+    lse_dense<R>(comps64 + L.comp_b, L.nb, L.shift_b, L.centre, yv, lb, exp_tab);
+    lse_dense<R>(comps64 + L.comp_a, L.na, L.shift_a, L.centre, yv, la, exp_tab);
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            if (lgmm) {
-                lb[r] -= y[r];
-                la[r] -= y[r];
-            }
-            if (!valid[r]) continue;
-            const uint64_t key = order_key(lb[r] - la[r]);
-            if (better(key, gi[r], bk, bi)) {
-                bk = key;
-                bi = gi[r];
-                bv = x[r];
-                bl = lb[r];
-                ba = la[r];
-            }
+    for (int r = 0; r < R; ++r) {
+        if (lgmm) {
+            lb[r] -= yv[r];
+            la[r] -= yv[r];
+        }
+        if (!valid[r]) continue;
+        const uint64_t key = order_key(lb[r] - la[r]);
+        if (better(key, gi[r], bk, bi)) {
+            bk = key;
+            bi = gi[r];
+            bv = x[r];
+            bl = lb[r];
+            ba = la[r];
         }
     }
     __shared__ Partial sh[kBlock / 64];
-    block_maxloc(bk, bi, bv, bl, ba, prow + blockIdx.x, sh);
+    block_maxloc(bk, bi, bv, bl, ba, prow + ch.j, sh);
 }
 
 // ------------------------------------------------------- split-K map ----
@@ -1110,6 +1144,12 @@ struct RoundArgs {
     double *olb, *ola;
     Slots S;                   // slot map (tile or grouped)
     uint32_t gx, gz;           // grid.x / grid.z of the per-candidate kernels
+    // the whole problem when this context runs one shard of it (multi-device
+    // contexts, tpe_multi.hip): decisions that change a summation order --
+    // chunking, table vs direct quantized scoring -- follow the whole
+    // problem, so every sharding gives bit-identical winners
+    int64_t total_slots;       // candidates x rounds over all shards
+    uint32_t gx_whole;         // grid.x the whole problem would use
 };
 
 void bracket(tpe_ctx* ctx, int mode, int which) {
@@ -1146,9 +1186,7 @@ void launch_round(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
 // every chunk would start to show.  Config 5 (~1200 workgroups): 7 chunks
 // (sweep in DESIGN.md section 6).
 constexpr int64_t kChunkTargetWG = 8192;
-// k_rescore workgroups per (round, label): each walks its share of the
-// compacted list in steps of kR * 256 candidates
-constexpr int32_t kRescoreWG = 128;
+
 constexpr int32_t kMinChunk = 2048;
 
 int dense_chunks(const tpe_ctx* ctx, uint32_t gx, int nl) {
@@ -1173,7 +1211,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
     const Comp<T>* comps;
     if constexpr (sizeof(T) == 8) comps = ctx->P->comps64.p; else comps = ctx->P->comps32.p;
     const int32_t* grp = ctx->P->groups.p + ctx->P->group_off[DENSE_GMM];
-    const int nch = a.S.cpack ? dense_chunks(ctx, a.gx, nl) : 1;
+    const int nch = a.S.cpack ? dense_chunks(ctx, a.gx_whole, nl) : 1;
     if (sizeof(T) == 8 && ctx->screen && a.S.cpack == 0) {   // fp32 screen + fp64 re-score
         const size_t cells = (size_t)a.n_rounds * nl;
         HIPCHK(ctx, ctx->scr_hi.reserve(cells * a.n));
@@ -1188,17 +1226,32 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                            a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->scr_hi.p, ctx->scr_lb.p,
                            ctx->errflag.p, a.S, nullptr, nullptr, nullptr);
         HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
-        const unsigned sx = (unsigned)std::min<int64_t>((a.n + kBlock - 1) / kBlock, 1024);
+        const unsigned sx = (unsigned)std::min<int64_t>((a.n + 8 * kBlock - 1) / (8 * kBlock), 1024);
         hipLaunchKernelGGL(k_select, dim3(sx, nl, a.gz), dim3(kBlock), 0, ctx->stream, ctx->scr_hi.p,
                            a.n, nl, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p);
-        const unsigned G = (unsigned)std::min<int32_t>(a.tiles, kRescoreWG);
-        hipLaunchKernelGGL((k_rescore<kR>), dim3(G, nl, a.gz), dim3(kBlock), 0, ctx->stream,
-                           ctx->P->labels.p, grp, ctx->P->comps64.p, ctx->P->samp.p, a.n,
-                           a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->P->n_labels, a.tiles,
-                           ctx->scr_cnt.p, ctx->scr_idx.p, ctx->partials.p);
+        // the dense rows' partial slots start empty; the re-score chunks
+        // overwrite theirs (one chunk table per round trip: the counts)
+        hipLaunchKernelGGL(k_fill_empty, dim3((unsigned)std::min<int64_t>((a.tiles + kBlock - 1) / kBlock, 64), nl, a.gz),
+                           dim3(kBlock), 0, ctx->stream, grp, ctx->P->n_labels, a.tiles, ctx->partials.p);
         ctx->scr_cnt_h.resize(cells);
         HIPCHK(ctx, hipMemcpyAsync(ctx->scr_cnt_h.data(), ctx->scr_cnt.p, cells * sizeof(int32_t),
                                    hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        constexpr int64_t per = (int64_t)kR * kBlock;
+        std::vector<RescoreChunk>& tab = ctx->scr_chunks_h;
+        tab.clear();
+        for (size_t c = 0; c < cells; ++c)
+            for (int32_t j = 0; (int64_t)j * per < ctx->scr_cnt_h[c]; ++j) tab.push_back(RescoreChunk{(int32_t)c, j});
+        if (!tab.empty()) {
+            HIPCHK(ctx, ctx->scr_chunks.reserve(tab.size()));
+            HIPCHK(ctx, hipMemcpyAsync(ctx->scr_chunks.p, tab.data(), tab.size() * sizeof(RescoreChunk),
+                                       hipMemcpyHostToDevice, ctx->stream));
+            hipLaunchKernelGGL((k_rescore<kR>), dim3((unsigned)tab.size()), dim3(kBlock), 0, ctx->stream,
+                               ctx->P->labels.p, grp, ctx->P->comps64.p, ctx->P->samp.p, a.n,
+                               a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->P->n_labels, a.tiles,
+                               ctx->scr_cnt.p, ctx->scr_idx.p,
+                               reinterpret_cast<const RescoreChunk*>(ctx->scr_chunks.p), ctx->partials.p);
+        }
         ctx->screen_total += (int64_t)cells * a.n;
         ctx->screen_pending = true;
         bracket(ctx, DENSE_GMM, 1);
@@ -1276,13 +1329,17 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
     HIPCHK(ctx, hipMemcpyAsync(mm.data(), ctx->qmm.p, 2 * nq * sizeof(unsigned long long),
                                hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->qx) {   // one shard of a multi-device round: the window of the whole set
+        int rc = ctx->qx->exchange(ctx, mm);
+        if (rc) return rc;
+    }
     // one table per label, shared by every round (the posterior does not
     // depend on the round); worth it when the label's grid window is smaller
     // than half its candidates over all rounds (each slot costs one
     // candidate's work)
     std::vector<QInfo> qi(nq);
     int64_t tab = 0, maxG = 0;
-    const int64_t total = a.n * (int64_t)a.n_rounds;
+    const int64_t total = a.total_slots;
     for (int qpos = 0; qpos < nq; ++qpos) {
         const int64_t jmin = (int64_t)(mm[qpos] ^ 0x8000000000000000ull);
         const int64_t jmax = (int64_t)(mm[nq + qpos] ^ 0x8000000000000000ull);
@@ -1422,7 +1479,13 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         g.dev[m] = ctx->one_group.p;
         g.count[m] = 1;
     }
-    RoundArgs a{n, cand_offset, seed, n_rounds, tiles, cand_in_dev, olb, ola, S, gx, gz};
+    // the whole problem (ctx->hint_*: set by a multi-device context for its shards)
+    const int64_t n_whole = ctx->hint_n > 0 ? ctx->hint_n : n;
+    const int32_t rounds_whole = ctx->hint_rounds > 0 ? ctx->hint_rounds : n_rounds;
+    const uint32_t gx_whole =
+        S.cpack ? (uint32_t)((rounds_whole + S.rpb - 1) / S.rpb) : gx;
+    RoundArgs a{n, cand_offset, seed, n_rounds, tiles, cand_in_dev, olb, ola, S, gx, gz,
+                n_whole * rounds_whole, gx_whole};
     ctx->screen_total = ctx->screen_rescored = 0;
     ctx->screen_pending = false;
     const bool sample = cand_in_dev == nullptr;
@@ -1430,7 +1493,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     HIPCHK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     // split-K for small sampled rounds (packed map, one tile per label)
     const bool splitk = sample && ctx->splitk && n > 0 && S.cpack != 0 &&
-                        (int64_t)n * n_rounds <= kSplitKMaxSlots;
+                        a.total_slots <= kSplitKMaxSlots;
     if (splitk) {
         int32_t s_max = 1;
         for (int m = 0; m < CAT; ++m)
@@ -1738,7 +1801,7 @@ int tpe_ctx_create(int device, int precision, tpe_ctx** out) {
     return TPE_OK;
 }
 
-void tpe_ctx_destroy(tpe_ctx* c) {
+TPE_DEV void tpe1_ctx_destroy(tpe_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -1780,13 +1843,13 @@ const char* tpe_last_error(const tpe_ctx* c) {
     return c ? c->err.c_str() : g_create_error.c_str();
 }
 
-int tpe_set_posterior(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_labels,
+TPE_DEV int tpe1_set_posterior(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_labels,
                       const double* weights, const double* mus, const double* sigmas,
                       int64_t n_components) {
     return set_posterior_impl(ctx, labels, n_labels, weights, mus, sigmas, n_components, true);
 }
 
-int tpe_suggest(tpe_ctx* ctx, uint64_t seed, uint32_t round, int64_t n_candidates,
+TPE_DEV int tpe1_suggest(tpe_ctx* ctx, uint64_t seed, uint32_t round, int64_t n_candidates,
                 int64_t cand_offset, tpe_label_result* out) {
     if (!ctx || !out) return TPE_ERR_ARG;
     HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -1794,7 +1857,7 @@ int tpe_suggest(tpe_ctx* ctx, uint64_t seed, uint32_t round, int64_t n_candidate
                      out, -1);
 }
 
-int tpe_suggest_batch(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds, int32_t n_rounds,
+TPE_DEV int tpe1_suggest_batch(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds, int32_t n_rounds,
                       int64_t n_candidates, int64_t cand_offset, tpe_label_result* out) {
     if (!ctx || !out || !rounds) return TPE_ERR_ARG;
     HIPCHK(ctx, hipSetDevice(ctx->device));
@@ -1908,7 +1971,7 @@ int tpe_last_screen(const tpe_ctx* ctx, int64_t* screened, int64_t* rescored, fl
     return TPE_OK;
 }
 
-int tpe_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
+TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
     if (!ctx) return TPE_ERR_ARG;
     switch (option) {
         case TPE_OPT_SCREEN: ctx->screen = value != 0; break;

@@ -64,21 +64,38 @@ def bounds_flags(low, high, q):
     return f
 
 
+def _devices(device):
+    if isinstance(device, (list, tuple)):
+        if not device:
+            raise ValueError('devices must not be empty')
+        return tuple(int(d) for d in device)
+    return (int(device),)
+
+
 class Engine(object):
-    """One device context (one GPU, one HIP stream).  Not thread-safe; the
-    module-level helpers keep one Engine per (thread, device, precision)."""
+    """A device context: one GPU and HIP stream, or -- `device` a list of
+    ordinals -- a multi-device context whose suggestion rounds are split over
+    the GPUs with bit-identical results (tpe_ctx_create_multi).  Not
+    thread-safe; the module-level helpers keep one Engine per (thread,
+    devices, precision)."""
 
     def __init__(self, device=0, precision='f64'):
         self.lib = L.load()
         self.precision = precision
         prec = {'f64': L.TPE_F64, 'f32': L.TPE_F32}[precision]
+        devs = _devices(device)
         h = ctypes.c_void_p()
-        rc = self.lib.tpe_ctx_create(int(device), prec, ctypes.byref(h))
+        if len(devs) == 1:
+            rc = self.lib.tpe_ctx_create(devs[0], prec, ctypes.byref(h))
+        else:
+            arr = (ctypes.c_int * len(devs))(*devs)
+            rc = self.lib.tpe_ctx_create_multi(arr, len(devs), prec, ctypes.byref(h))
         if rc != L.TPE_OK:
-            raise EngineError('tpe_ctx_create(device=%d): %s' % (
-                device, self.lib.tpe_last_error(None).decode()))
+            raise EngineError('tpe_ctx_create(devices=%s): %s' % (
+                list(devs), self.lib.tpe_last_error(None).decode()))
         self.h = h
-        self.device = device
+        self.devices = devs
+        self.device = devs[0]
         self.n_labels = 0
 
     def close(self):
@@ -337,11 +354,12 @@ _tls = threading.local()
 
 
 def get_engine(device=0, precision='f64'):
-    """Per-thread cached Engine (contexts are not thread-safe)."""
+    """Per-thread cached Engine (contexts are not thread-safe); `device` an
+    ordinal or a list of them."""
     cache = getattr(_tls, 'engines', None)
     if cache is None:
         cache = _tls.engines = {}
-    key = (int(device), precision)
+    key = (_devices(device), precision)
     if key not in cache:
         cache[key] = Engine(device, precision)
     return cache[key]

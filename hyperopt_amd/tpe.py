@@ -19,7 +19,9 @@
      and keeping the selected one is the same distribution).
 
 Extra keyword arguments (not in the reference): `precision` ('f64' default,
-'f32' fast path), `device` (HIP ordinal), `batch` (True: one independent
+'f32' fast path), `device` (HIP ordinal), `devices` (a list of ordinals: one
+multi-device context splits every round over those GPUs, same documents as
+one GPU; tpe_ctx_create_multi), `batch` (True: one independent
 suggestion per new_id instead of only new_ids[0]), `posterior_builder`:
 'host' (numpy, posterior.py -- the reference's own np.argsort tie order),
 'device' (tpe_build_posterior on the GPU: split, sort, Parzen and fold in
@@ -114,7 +116,7 @@ def suggest(new_ids, domain, trials, seed,
             n_EI_candidates=_default_n_EI_candidates,
             gamma=_default_gamma,
             linear_forgetting=_default_linear_forgetting,
-            precision='f64', device=0, batch=False, posterior_builder='auto'):
+            precision='f64', device=0, batch=False, posterior_builder='auto', devices=None):
     t0 = time.time()
     if posterior_builder not in ('auto', 'host', 'device'):
         raise ValueError('posterior_builder must be auto, host or device')
@@ -134,7 +136,7 @@ def suggest(new_ids, domain, trials, seed,
         if n_docs == 0 and n_startup_jobs <= 0:
             logger.info('TPE using 0 trials')
         return rand.suggest(list(new_ids[:1]) if not batch else new_ids, domain, trials, seed)
-    eng = _engine.get_engine(device, precision)
+    eng = _engine.get_engine(list(devices) if devices else device, precision)
     on_device = posterior_builder == 'device' or (posterior_builder == 'auto' and
                                                   n_obs >= DEVICE_BUILD_MIN_OBS)
     if on_device and view is not None:   # upload only the observations that are new

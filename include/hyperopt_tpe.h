@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 1
+#define TPE_ABI_VERSION 2
 
 /* error codes; the Python layer maps them to the reference's exception types */
 #define TPE_OK 0
@@ -119,6 +119,23 @@ const char *tpe_source_hash(void);
 
 /* device: HIP ordinal; precision: TPE_F64 or TPE_F32 */
 int tpe_ctx_create(int device, int precision, tpe_ctx **out);
+
+/* One context over several GPUs of the node (devices[0] first; a device may
+ * repeat, e.g. to test sharding on one GPU).  Every entry point keeps its
+ * meaning: posterior uploads, device builds, history appends and options
+ * go to every device; tpe_suggest / tpe_suggest_batch split each round over
+ * the devices -- contiguous global candidate ranges when every device gets
+ * at least 1024 candidates of each round, else whole rounds -- one host
+ * thread and HIP stream per device, and merge the per-device winners with
+ * the broadcast_best order.  The results are bit-identical to a one-device
+ * context's (the reference's single synchronous algo call per
+ * round, hyperopt/fmin.py:201-202, keeps the fan-out inside the call).  The
+ * single-op entry points, tpe_score and tpe_get_mixture use devices[0]. */
+int tpe_ctx_create_multi(const int *devices, int32_t n_devices, int precision, tpe_ctx **out);
+
+/* Devices of a context (writes at most cap ordinals); returns their count. */
+int32_t tpe_ctx_devices(const tpe_ctx *ctx, int32_t *devices, int32_t cap);
+
 void tpe_ctx_destroy(tpe_ctx *ctx);
 const char *tpe_last_error(const tpe_ctx *ctx);
 

@@ -62,8 +62,8 @@ def test_fullsize_winner_properties(config, builder):
         hist, C = hartmann_history(2000, seed=0), 1 << 20
     elif config == 'config4':
         hist, C = conditional_history(5000, seed=0), 1 << 20
-    else:
-        hist, C = mixed_history(32, 10000, seed=0), 1 << 21
+    else:   # BASELINE.json configs[2]: 2^24 candidates per label on one GPU
+        hist, C = mixed_history(32, 10000, seed=0), 1 << 24
     eng = Engine(0, 'f64')
     try:
         if builder == 'device':
@@ -103,8 +103,9 @@ def test_fullsize_winner_properties(config, builder):
 
 
 def test_fullsize_config5_batched_rounds():
-    """Config-5 shape: 128 labels, 50k history, batched new_ids x 24
-    candidates; every sampled round's winner is the oracle's argmax."""
+    """Config 5 at its BASELINE size on one GPU: 128 labels, 50k history,
+    4096 new_ids x 24 candidates in one batched call; sampled rounds' winners
+    are the oracle's argmax."""
     from hyperopt_amd import posterior as P
     from hyperopt_amd.engine import Engine
     from hyperopt_amd.workloads import mixed_history
@@ -113,16 +114,51 @@ def test_fullsize_config5_batched_rounds():
     eng = Engine(0, 'f64')
     try:
         eng.set_posterior(*P.pack(posts))
-        ids = list(range(100000, 100512))
+        ids = list(range(100000, 100000 + 4096))
         out = eng.suggest_batch(9, ids, 24)
+        assert out.shape == (4096, 128)
+        assert np.all(out['index'] >= 0) and np.all(out['index'] < 24)
         rng = np.random.RandomState(0)
-        for j in rng.choice(len(ids), 3, replace=False):
-            for li in rng.choice(len(posts), 12, replace=False):
+        for j in rng.choice(len(ids), 4, replace=False):
+            for li in rng.choice(len(posts), 16, replace=False):
                 p = posts[li]
                 cand = _draw(eng, p, int(li), 9, ids[j], 0, 24)
                 lb, la = _score(p, cand)
                 best = O.broadcast_best_index(lb, la)
                 assert int(out[j][li]['index']) == best
                 assert out[j][li]['value'] == cand[best]
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize('builder', ['host', 'device'])
+def test_config4_c24_oracle_argmax(builder):
+    """Config 4 (nested hp.choice SVM/RF/GBM space, 5k trials) at the
+    reference default n_EI_candidates = 24: over several rounds, every
+    label's winner is the oracle's np.argmax on the same 24 candidates, with
+    the same value and lpdfs (LGMM1 + q, categorical and GMM1 q paths)."""
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.engine import Engine
+    from hyperopt_amd.workloads import conditional_history
+    hist = conditional_history(5000, seed=0)
+    eng = Engine(0, 'f64')
+    try:
+        if builder == 'device':
+            posts = _device_posts(eng, hist)
+        else:
+            posts = hist.posteriors()
+            eng.set_posterior(*P.pack(posts))
+        for rnd, seed in [(1, 101), (2, 202), (5000, 7), (77, 123456)]:
+            res = eng.suggest(seed, 24, round=rnd)
+            for li, p in enumerate(posts):
+                cand = _draw(eng, p, li, seed, rnd, 0, 24)
+                lb, la = _score(p, cand)
+                best = O.broadcast_best_index(lb, la)
+                r = res[li]
+                assert int(r['index']) == best, (rnd, li, p.label)
+                assert r['value'] == cand[best]
+                q = p.family != 'categorical' and p.q is not None
+                assert_lpdf_close([r['lpdf_below']], [lb[best]], quantized=q)
+                assert_lpdf_close([r['lpdf_above']], [la[best]], quantized=q)
     finally:
         eng.close()
