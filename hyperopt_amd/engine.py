@@ -97,6 +97,9 @@ class Engine(object):
         self.devices = devs
         self.device = devs[0]
         self.n_labels = 0
+        # bumped by every call that replaces the device-resident history, so
+        # a DeviceHistoryUploader can tell its history is no longer there
+        self.history_generation = 0
 
     def close(self):
         if getattr(self, 'h', None):
@@ -135,6 +138,7 @@ class Engine(object):
         obs_trial = np.ascontiguousarray(obs_trial, dtype=np.int32)
         obs_val = _f64(obs_val)
         nb = ctypes.c_int32()
+        self.history_generation += 1      # tpe_build_posterior resets the resident history
         self._check(self.lib.tpe_build_posterior(
             self.h, _ptr(specs), len(specs), _ptr(cat_p), len(cat_p), _ptr(losses), len(losses),
             _ptr(obs_off), _ptr(obs_trial), _ptr(obs_val), float(gamma), float(prior_weight),
@@ -146,6 +150,7 @@ class Engine(object):
     def history_reset(self, specs, cat_p):
         specs = np.ascontiguousarray(specs, dtype=SPEC_DTYPE)
         cat_p = _f64(cat_p)
+        self.history_generation += 1
         self._check(self.lib.tpe_history_reset(self.h, _ptr(specs), len(specs), _ptr(cat_p),
                                                len(cat_p)))
         self.hist_labels = len(specs)

@@ -14,6 +14,8 @@ same order, including the default, non-stable np.argsort tie order):
   categorical   pseudocount posteriors        tpe.py:581-617
 It is vectorised over the history (no per-trial Python loops).
 """
+import weakref
+
 import numpy as np
 
 from . import _lib as L
@@ -235,45 +237,69 @@ def spec_table(labels):
     return specs, (np.concatenate(cat_p) if cat_p else np.zeros(0)), trs
 
 
+class NonFiniteObservation(ValueError):
+    """A transformed observation is NaN (e.g. the log of a non-positive value
+    of a log-scale label inserted through points_to_evaluate).  The
+    reference's adaptive_parzen_normal then trips its `sigma > 0` assertion
+    (tpe.py:469) in the host build; the device builder cannot order NaN
+    keys, so it refuses them (tpe.suggest falls back to the host builder)."""
+
+
+def _check_finite(label, vals):
+    if np.isnan(vals).any():
+        raise NonFiniteObservation('label %r: NaN observation value' % (label,))
+
+
 class DeviceHistoryUploader(object):
     """Keeps an Engine's device-resident history (tpe_history_*) in step with
     a growing trial history: only observations added since the last call are
-    transformed and uploaded; anything else (new labels, another history, a
-    trial inserted before existing ones) resets it."""
+    transformed and uploaded; anything else (new labels, another history --
+    the owner is held by weak reference, so a collected history's address
+    reused by a new one does not match --, a history replaced on the device
+    by another call, a trial inserted before existing ones) resets it."""
 
     def __init__(self):
         self.key = None
+        self.owner = None
 
     def build(self, eng, labels, view, gamma, prior_weight, lf=DEFAULT_LF):
         tids, losses, n_valid, cols, owner = view
-        key = (id(owner), tuple((n, k) for n, k, _ in labels))
-        fresh = (self.key != key or len(tids) < self.n_trials or
+        key = (tuple((n, k) for n, k, _ in labels), eng.history_generation)
+        same_owner = self.owner is not None and self.owner() is owner
+        fresh = (not same_owner or self.key != key or len(tids) < self.n_trials or
                  (self.n_trials and tids[self.n_trials - 1] != self.last_tid) or
                  any(len(cols[n][0]) < c for (n, _, _), c in zip(labels, self.prev_counts)))
+        # invalid until the device holds exactly what prev_counts says
+        self.key, self.owner = None, None
         if fresh:
             specs, cat_p, self.trs = spec_table(labels)
             eng.history_reset(specs, cat_p)
             self.prev_counts = [0] * len(labels)
+        counts = list(self.prev_counts)
         n_new, trial_parts, val_parts = [], [], []
         for i, (name, _, _) in enumerate(labels):
             oi, ov = cols[name]
-            c0 = self.prev_counts[i]
+            c0 = counts[i]
             ni, nv = oi[c0:], ov[c0:]
             if len(ni):
                 tr = self.trs[i]
                 if tr is not None:
                     nv = tr(nv)
+                nv = np.asarray(nv, dtype=float)
+                _check_finite(name, nv)
                 pos = np.searchsorted(tids, ni)
                 pc = np.minimum(pos, len(tids) - 1)
                 pos = np.where(tids[pc] == ni, pc, -1)
                 trial_parts.append(pos.astype(np.int32))
-                val_parts.append(np.asarray(nv, dtype=float))
+                val_parts.append(nv)
             n_new.append(len(ni))
-            self.prev_counts[i] = len(oi)
+            counts[i] = len(oi)
         if sum(n_new):
             eng.history_append(np.asarray(n_new, dtype=np.int64), np.concatenate(trial_parts),
                                np.concatenate(val_parts))
-        self.key = key
+        self.prev_counts = counts                  # committed only after the append
+        self.key = (key[0], eng.history_generation)
+        self.owner = weakref.ref(owner)
         self.n_trials = len(tids)
         self.last_tid = tids[-1] if len(tids) else None
         return eng.build_posterior_resident(losses, n_valid, gamma, prior_weight, lf)
@@ -310,6 +336,7 @@ def device_inputs(labels, tids, losses, obs):
         ov = np.asarray(ov, dtype=float)
         if tr is not None and len(ov):
             ov = tr(ov)
+        _check_finite(name, ov)
         if len(oi) == len(tids) and len(oi) and oi[0] == tids[0] and oi[-1] == tids[-1] \
                 and np.array_equal(oi, tids):
             pos = np.arange(len(oi))                 # label active in every trial

@@ -110,6 +110,65 @@ def _doc(new_id, domain, trials, specs, values):
     return trials.new_trial_docs([new_id], [None], [domain.new_result()], [misc])
 
 
+class _PendingView(object):
+    """The trials a sequential caller would see after inserting a batch's
+    earlier suggestions: the real documents plus those, still pending (state
+    new, result {'status': 'new'}: loss None -> +inf, tpe.py:844-847)."""
+
+    def __init__(self, trials):
+        self._base = trials
+        self.trials = list(trials.trials)
+
+    def new_trial_docs(self, *args, **kwargs):
+        return self._base.new_trial_docs(*args, **kwargs)
+
+    def __len__(self):
+        return len(self.trials)
+
+
+def _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior_weight,
+                        builder):
+    """Put the posterior of the current history on the engine, from the
+    device-resident history's `view` or the general gather (tids, losses,
+    obs); returns the number of trial documents it was built from."""
+    labels = list(specs)
+    if view is not None:
+        n_docs = view[2]
+        n_obs = sum(len(view[3][k][0]) for k in labels)
+    if view is None or n_docs == 0:
+        tids, losses, obs = gathered or _history.gather(domain, trials, labels)
+        n_docs = len(tids)
+        n_obs = sum(len(obs[k][0]) for k in labels)
+    on_device = n_docs > 0 and (builder == 'device' or (builder == 'auto' and
+                                                         n_obs >= DEVICE_BUILD_MIN_OBS))
+    if on_device:
+        try:
+            if view is not None:   # upload only the observations that are new
+                up = getattr(eng, '_history_uploader', None)
+                if up is None:
+                    up = eng._history_uploader = _post.DeviceHistoryUploader()
+                up.build(eng, [(s.label, s.kind, s.args) for s in specs.values()], view, gamma,
+                         prior_weight)
+            else:
+                eng.build_posterior(*device_inputs(specs, tids, losses, obs), gamma=gamma,
+                                    prior_weight=prior_weight)
+            return n_docs
+        except _post.NonFiniteObservation:
+            # NaN observations: the host build raises what the reference's
+            # adaptive_parzen_normal raises (tpe.py:469)
+            if view is not None:
+                tids, losses, obs = _history.gather(domain, trials, labels)
+    elif view is not None and n_docs > 0:
+        tids, losses, obs = _history.gather(domain, trials, labels)
+    splitter = _post.Splitter(tids, losses, gamma)
+    posts = []
+    for label, sp in specs.items():
+        b, a = splitter.split(*obs[label])
+        posts.append(_post.label_posterior(label, sp.kind, sp.args, b, a, prior_weight))
+    eng.set_posterior(*_post.pack(posts))
+    return n_docs
+
+
 def suggest(new_ids, domain, trials, seed,
             prior_weight=_default_prior_weight,
             n_startup_jobs=_default_n_startup_jobs,
@@ -117,47 +176,55 @@ def suggest(new_ids, domain, trials, seed,
             gamma=_default_gamma,
             linear_forgetting=_default_linear_forgetting,
             precision='f64', device=0, batch=False, posterior_builder='auto', devices=None):
+    """tpe.py:823-916.  Past the startup phase one document for new_ids[0],
+    like the reference; `batch` (not in the reference) asks for one document
+    per new_id:
+
+    * batch=True -- the documents K sequential calls suggest([new_ids[j]],
+      domain, trials, seed) would return with `trials` unchanged between
+      them: one posterior, the batch's other suggestions excluded from it;
+    * batch='pending' -- the documents K sequential calls return when each
+      call's document is inserted into the trials, still pending, before the
+      next call (the reference's view of queued trials: loss None -> +inf,
+      tpe.py:844-847; fmin with max_queue_len, fmin.py:193-202).
+
+    During the startup phase (fewer than n_startup_jobs documents) the
+    reference's rand.suggest(new_ids, ...) answers, for every new_id."""
     t0 = time.time()
     if posterior_builder not in ('auto', 'host', 'device'):
         raise ValueError('posterior_builder must be auto, host or device')
+    if batch not in (False, True, 'pending'):
+        raise ValueError("batch must be False, True or 'pending'")
+    kw = dict(prior_weight=prior_weight, n_startup_jobs=n_startup_jobs,
+              n_EI_candidates=n_EI_candidates, gamma=gamma, linear_forgetting=linear_forgetting,
+              precision=precision, device=device, posterior_builder=posterior_builder,
+              devices=devices)
+    if batch == 'pending' and len(new_ids) > 1:
+        view = _PendingView(trials)
+        rval = []
+        for new_id in new_ids:
+            docs = suggest([new_id], domain, view, seed, batch=False, **kw)
+            view.trials.extend(docs)
+            rval.extend(docs)
+        return rval
     specs = specs_of(domain)
     labels = list(specs)
     # the device-resident history's view of the trials (None when the fast
     # layout does not apply); otherwise the general gather
     view = _history.device_view(domain, trials, labels) if posterior_builder != 'host' else None
+    gathered = None
     if view is not None:
         n_docs = view[2]
-        n_obs = sum(len(view[3][k][0]) for k in labels)
     else:
-        tids, losses, obs = _history.gather(domain, trials, labels)
-        n_docs = len(tids)
-        n_obs = sum(len(obs[k][0]) for k in labels)
-    if n_docs < n_startup_jobs or n_docs == 0:
-        if n_docs == 0 and n_startup_jobs <= 0:
-            logger.info('TPE using 0 trials')
-        return rand.suggest(list(new_ids[:1]) if not batch else new_ids, domain, trials, seed)
+        gathered = _history.gather(domain, trials, labels)
+        n_docs = len(gathered[0])
+    if n_docs < n_startup_jobs:
+        return rand.suggest(new_ids, domain, trials, seed)      # tpe.py:869-871
+    if n_docs == 0:
+        logger.info('TPE using 0 trials')                     # the prior-only posterior
     eng = _engine.get_engine(list(devices) if devices else device, precision)
-    on_device = posterior_builder == 'device' or (posterior_builder == 'auto' and
-                                                  n_obs >= DEVICE_BUILD_MIN_OBS)
-    if on_device and view is not None:   # upload only the observations that are new
-        up = getattr(eng, '_history_uploader', None)
-        if up is None:
-            up = eng._history_uploader = _post.DeviceHistoryUploader()
-        up.build(eng, [(s.label, s.kind, s.args) for s in specs.values()], view, gamma,
-                 prior_weight)
-    else:
-        if view is not None:
-            tids, losses, obs = _history.gather(domain, trials, labels)
-        if on_device:
-            eng.build_posterior(*device_inputs(specs, tids, losses, obs), gamma=gamma,
-                                prior_weight=prior_weight)
-        else:
-            splitter = _post.Splitter(tids, losses, gamma)
-            posts = []
-            for label, sp in specs.items():
-                b, a = splitter.split(*obs[label])
-                posts.append(_post.label_posterior(label, sp.kind, sp.args, b, a, prior_weight))
-            eng.set_posterior(*_post.pack(posts))
+    _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior_weight,
+                        posterior_builder)
     ids = list(new_ids) if batch else [new_ids[0]]
     if len(ids) == 1:
         res = eng.suggest(seed, n_EI_candidates, round=ids[0])[None]

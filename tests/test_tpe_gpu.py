@@ -37,22 +37,31 @@ PW = dict(distractor=.01)
 NEI = dict(quadratic1=5, distractor=15)
 
 
+@pytest.fixture
+def np_raise():
+    """TestOpt.setUp/tearDown (test_tpe.py:587-592): numpy errors raise,
+    except underflow."""
+    old = np.seterr('raise')
+    np.seterr(under='ignore')
+    yield
+    np.seterr(**old)
+
+
 @pytest.mark.parametrize('name', sorted(THRESH))
-def test_opt_thresholds(name):
+def test_opt_thresholds(name, np_raise):
+    """TestOpt.work (test_tpe.py:594-656): one fmin from RandomState(123)
+    must beat the reference's threshold.  (The reference's MT19937 draw
+    order is not reproduced -- Philox candidates -- so this is the same test
+    on a different sample path.)"""
     algo = partial(tpe.suggest, gamma=GAMMA.get(name, tpe._default_gamma),
                    prior_weight=PW.get(name, tpe._default_prior_weight),
                    n_EI_candidates=NEI.get(name, tpe._default_n_EI_candidates))
     n = LEN.get(name, 50)
-    best = []
-    for seed in (123, 7, 11):     # the reference uses one seed of ITS rng stream
-        trials = H.Trials()
-        H.fmin(passthrough, space=domains.ALL[name](), algo=algo, trials=trials,
-               max_evals=n, rstate=np.random.RandomState(seed))
-        assert len(trials) == n
-        best.append(min(trials.losses()))
-        if best[-1] < THRESH[name]:
-            return
-    raise AssertionError('%s: best losses %s, threshold %s' % (name, best, THRESH[name]))
+    trials = H.Trials()
+    H.fmin(passthrough, space=domains.ALL[name](), algo=algo, trials=trials,
+           max_evals=n, rstate=np.random.RandomState(123), catch_eval_exceptions=False)
+    assert len(trials) == n
+    assert min(trials.losses()) < THRESH[name], (name, sorted(trials.losses())[:6])
 
 
 def test_suggest_document_and_conditional_space():
