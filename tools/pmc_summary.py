@@ -17,7 +17,8 @@ import shutil
 import sys
 from collections import defaultdict
 
-FAMILY = {'k_round<double, 0,': 'dense', 'k_round<double, 1,': 'dense_lgmm1',
+FAMILY = {'k_screen<4, true>': 'dense',
+          'k_round<double, 0,': 'dense', 'k_round<double, 1,': 'dense_lgmm1',
           'k_round<float, 0,': 'dense', 'k_round<float, 1,': 'dense_lgmm1',
           'k_round<double, 8,': 'dense', 'k_round<float, 8,': 'dense'}
 
@@ -70,17 +71,18 @@ def main(src, tag):
             nlaunch[k] = n[k]
     # evals per launch of each dense family from a 1-step bench line
     pmc_bench = os.path.join(src, 'pmc_valu.log')
-    fam_evals = None
+    fam_evals, steps = None, 1
     if os.path.exists(pmc_bench):
         for line in open(pmc_bench):
             if line.startswith('{"metric"'):
-                fam_evals = json.loads(line).get('per_family_evals')
+                d = json.loads(line)
+                fam_evals = d.get('per_family_evals')
+                steps = d.get('steps', 1) + d.get('warmup', 0)   # every step launches once
     for k, v in summary.items():
         v['_launches'] = nlaunch.get(k)
         for pre, fam in FAMILY.items():
             if k.startswith(pre) and fam_evals and fam in fam_evals and 'SQ_INSTS_VALU' in v:
-                # evals per launch = family evals per step / launches per step
-                steps = 1
+                # evals per launch = family evals per step x steps / launches
                 ev = fam_evals[fam] * steps / max(nlaunch.get(k, 1), 1)
                 v['_evals_per_launch'] = ev
                 v['_valu_instr_per_eval'] = v['SQ_INSTS_VALU'] * 64 / ev
@@ -88,7 +90,12 @@ def main(src, tag):
             # VALU issue utilisation: every wave64 VALU instruction holds a
             # 16-lane SIMD for 4 cycles; 1024 SIMDs; GRBM_GUI_ACTIVE / 8 XCDs
             # = the launch's GPU cycles
-            v['_valu_busy'] = v['SQ_INSTS_VALU'] * 4 / (1024 * v['GRBM_GUI_ACTIVE'] / 8)
+            cycles = 1024 * v['GRBM_GUI_ACTIVE'] / 8
+            v['_valu_busy'] = v['SQ_INSTS_VALU'] * 4 / cycles
+            if k.startswith('k_screen') and '_evals_per_launch' in v:
+                # one v_exp_f32 (8-cycle issue) per eval: 4 extra cycles per
+                # 64 evals on top of the 4-cycle count
+                v['_valu_busy'] = (v['SQ_INSTS_VALU'] + v['_evals_per_launch'] / 64) * 4 / cycles
         if 'FETCH_SIZE' in v:
             v['_hbm_bytes_per_launch'] = (v['FETCH_SIZE'] * 2 + v.get('WRITE_SIZE', 0)) * 1024
     summary['_note'] = ('counters averaged per launch; FETCH_SIZE/WRITE_SIZE in KB; '
@@ -99,7 +106,8 @@ def main(src, tag):
                         '(1024 SIMDs x GRBM_GUI_ACTIVE / 8)')
     json.dump(summary, open(os.path.join(dst, '%s_pmc_summary.json' % tag), 'w'), indent=1,
               sort_keys=True)
-    print(json.dumps({k: v for k, v in summary.items() if k.startswith('k_round')}, indent=1))
+    print(json.dumps({k: v for k, v in summary.items() if k.startswith(('k_round', 'k_screen'))},
+                     indent=1))
 
 
 if __name__ == '__main__':
