@@ -60,10 +60,13 @@ def parse():
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--precision', default='f64', choices=['f64', 'f32'])
-    ap.add_argument('--config', type=int, default=3, choices=[2, 3, 5],
+    ap.add_argument('--config', type=int, default=3, choices=[2, 3, 4, 5],
                     help='BASELINE.json config: 3 (headline, default), 2 (Hartmann-6, 2k '
+                         'history, 2^20 candidates), 4 (nested SVM/RF/GBM choice space, 5k '
                          'history, 2^20 candidates), 5 (128 labels, 50k history, batched '
                          'new_ids x 24 candidates)')
+    ap.add_argument('--agreement-steps', type=int, default=3,
+                    help='f32: steps whose winners are compared with the exact fp64 round')
     ap.add_argument('--new-ids', type=int, default=4096,
                     help='config 5: new_ids per step in total, split over the ranks')
     ap.add_argument('--c5-history', type=int, default=50000,
@@ -179,6 +182,9 @@ def workload_name(args, C):
     if args.config == 2:
         return 'config2: Hartmann-6 over hp.uniform, N=2000 history, 2^20 EI candidates ' \
                'per label (C/N per GPU)'
+    if args.config == 4:
+        return 'config4: nested hp.choice SVM/RF/GBM space (13 labels), N=5000 history, ' \
+               '2^%d EI candidates per label (C/N per GPU)' % args.cand_log2
     if args.config == 5:
         return 'config5: 128-dim mixed space, N=%d history, %d new_ids per step x 24 EI ' \
                'candidates (new_ids split over the GPUs, winners all-gathered)' % (
@@ -201,11 +207,15 @@ def main():
         dist.init_process_group(args.dist_backend)
     from hyperopt_amd import posterior as P
     from hyperopt_amd.engine import Engine
-    from hyperopt_amd.workloads import hartmann_history, mixed_history
+    from hyperopt_amd.workloads import conditional_history, hartmann_history, mixed_history
 
     if args.config == 2:
         args.labels, args.trials, args.cand_log2 = 6, 2000, 20
         hist = hartmann_history(args.trials, seed=0)
+    elif args.config == 4:
+        args.trials, args.cand_log2 = 5000, 20
+        hist = conditional_history(args.trials, seed=0)
+        args.labels = len(hist.labels)
     elif args.config == 5:
         args.labels, args.trials = 128, args.c5_history
         hist = mixed_history(args.labels, args.trials, seed=0)
@@ -311,7 +321,11 @@ def main():
         kdesc = 'k_round<%s,%s>' % (prec, dom + ' (GMM1+LGMM1 labels)')
     dom_rate = mode_ev[dom] / (dom_ms * 1e-3)
     peak = PEAK_FP64_VECTOR_TFLOPS if kprec == 'f64' else PEAK_FP32_VECTOR_TFLOPS
-    traffic, valu_busy, traffic_src = measured_pmc(kname)
+    # PMC figures come from the committed profile of the default workload
+    # (config 3, tools/prof_round.sh): only that workload's line carries them
+    traffic, valu_busy, traffic_src = (measured_pmc(kname) if args.config == 3 and world == 1
+                                       and args.cand_log2 == 24 and args.labels == 32
+                                       else (None, None, None))
     achieved = dom_rate * FLOPS_PER_EVAL[kprec] / 1e12
     roof = {'bound': 'valu', 'kernel': kdesc,
             'achieved': round(achieved, 3), 'peak': peak, 'unit': 'TFLOP/s',
@@ -360,6 +374,30 @@ def main():
                 'ms_per_step': round(udt / args.unscreened_steps * 1e3, 3),
                 'value': sum(uev.values()) / udt,
                 'dense_ms': round(ums[dom] / args.unscreened_steps, 3)}
+    if prec == 'f32' and args.agreement_steps > 0 and args.config != 5:
+        # fp32 winners vs the exact fp64 round's on the same candidate sets
+        ref = Engine(local, 'f64')
+        ref.build_posterior(*inputs, gamma=0.25, prior_weight=1.0)
+        same = total = 0
+        worst_regret = 0.0
+        for i in range(args.agreement_steps):
+            a = eng.suggest(seed=1234 + i, n_candidates=C, round=i, cand_offset=rank * C)
+            b = ref.suggest(seed=1234 + i, n_candidates=C, round=i, cand_offset=rank * C)
+            same += int(np.sum(a['index'] == b['index']))
+            total += len(a)
+            # regret in exact score of the fp32 winner (re-scored in fp64)
+            for li in np.nonzero(a['index'] != b['index'])[0]:
+                if posts[li].family == 'categorical':
+                    continue
+                lb, la, _ = ref.score(int(li), np.array([a[li]['value']]))
+                worst_regret = max(worst_regret, float(b[li]['score'] - (lb[0] - la[0])))
+        ref.close()
+        line['f32_argmax_agreement'] = {
+            'rate': same / max(total, 1), 'winners_compared': total,
+            'worst_fp64_score_regret': worst_regret,
+            'note': 'per (step, label): the fp32 round\'s winner index equals the exact fp64 '
+                    'round\'s on the same candidates; regret = fp64 score of the fp64 winner '
+                    'minus fp64 score of the fp32 winner'}
     if args.config == 5:
         line['config']['new_ids_per_step'] = args.new_ids
         line['config']['new_ids_per_gpu_per_step'] = ids_local
