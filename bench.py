@@ -86,6 +86,10 @@ def parse():
     ap.add_argument('--unscreened-steps', type=int, default=3,
                     help='f64: steps of the plain fp64 round timed after the main run, for '
                          'comparison (0 = skip)')
+    ap.add_argument('--devices', default=None,
+                    help='one process, one multi-device context over these HIP ordinals '
+                         '(e.g. 0,1,2,3; tpe_ctx_create_multi): the 1..8-GPU curve without '
+                         'torchrun; a repeated ordinal shares that GPU (tests)')
     ap.add_argument('--dist-backend', default='nccl',
                     help='nccl (RCCL over xGMI); gloo only to rehearse N ranks on one GPU')
     return ap.parse_args()
@@ -224,7 +228,10 @@ def main():
     # the resident posterior: built on the device from the history (the
     # product path for histories this size, tpe.suggest posterior_builder
     # 'auto'); the host numpy build is timed beside it
-    eng = Engine(local, args.precision)
+    devs = [int(d) for d in args.devices.split(',')] if args.devices else None
+    if devs and world > 1:
+        raise SystemExit('--devices is the single-process multi-GPU mode; not under torchrun')
+    eng = Engine(devs if devs else local, args.precision)
     t_host = time.perf_counter()
     posts = hist.posteriors()
     descs, w, m, s = P.pack(posts)
@@ -338,7 +345,8 @@ def main():
             'launch_ms': dom_ms / args.steps}
     line = {
         'metric': 'TPE candidate x component lpdf evals/sec (10k-trial history)',
-        'value': value, 'unit': 'evals/s', 'n_gpus': world, 'steps': args.steps,
+        'value': value, 'unit': 'evals/s', 'n_gpus': len(set(devs)) if devs else world,
+        'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3,
         'higher_is_better': True, 'scaling': 'strong', 'vs_baseline': None,
         'dtype': ('f32+f64' if screened else args.precision),
@@ -347,7 +355,9 @@ def main():
                    'labels': L, 'history': args.trials,
                    'candidates_per_label': C_total, 'candidates_per_label_per_gpu': C,
                    'parallelism': ('new_id-sharded x%d' if args.config == 5
-                                   else 'candidate-sharded x%d') % world},
+                                   else 'candidate-sharded x%d') % (len(devs) if devs else world)
+                                  + (' (one process, multi-device context %s)' % devs
+                                     if devs else '')},
         'posterior_build': post_build,
         'per_family_ms': {k: round(v / args.steps, 3) for k, v in mode_ms.items() if v},
         'per_family_evals': {k: v // args.steps for k, v in mode_ev.items() if v},
@@ -376,7 +386,7 @@ def main():
                 'dense_ms': round(ums[dom] / args.unscreened_steps, 3)}
     if prec == 'f32' and args.agreement_steps > 0 and args.config != 5:
         # fp32 winners vs the exact fp64 round's on the same candidate sets
-        ref = Engine(local, 'f64')
+        ref = Engine(devs if devs else local, 'f64')
         ref.build_posterior(*inputs, gamma=0.25, prior_weight=1.0)
         same = total = 0
         worst_regret = 0.0
