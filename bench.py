@@ -303,6 +303,9 @@ def main():
 
     screen = args.precision == 'f64' and not args.no_screen
     eng.set_option('screen', int(screen))
+    if world > 1:   # this rank holds one shard: size-dependent choices follow the whole round
+        eng.set_option('whole_rounds' if args.config == 5 else 'whole_n',
+                       args.new_ids if args.config == 5 else C_total)
     for i in range(args.warmup):
         step(i)
     dt, mode_ms, mode_ev, scr = timed(args.steps, args.warmup)

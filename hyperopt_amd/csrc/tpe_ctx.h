@@ -197,6 +197,11 @@ struct tpe_ctx {
     DevBuf<int32_t> scr_cnt;
     std::vector<int32_t> scr_cnt_h;
     DevBuf<int64_t> scr_chunks;          // k_rescore chunk table ({cell, chunk} int32 pairs)
+    DevBuf<int64_t> scr_list;            // packed map: per label, (round << 32 | candidate) to re-score
+    DevBuf<Partial> scr_res;             //   their fp64 results
+    DevBuf<int64_t> scr_rsel;            //   per (round, label): {first, count} int32 pairs
+    DevBuf<int64_t> scr_off;             //   per label: offset of its entries in the compacted order
+    DevBuf<double> scr_planes;           //   re-score sums: below | x | above chunk c, per entry
     std::vector<tpe_rt::RescoreChunkH> scr_chunks_h;
     int64_t screen_total = 0, screen_rescored = 0;   // last round
     bool screen_pending = false;         // scr_cnt_h awaits the round's final sync
@@ -213,6 +218,10 @@ struct tpe_ctx {
     std::vector<tpe_ctx*> peers;
     int64_t hint_n = 0;                  // candidates per round over all shards (0: this call's)
     int32_t hint_rounds = 0;             // rounds over all shards (0: this call's)
+    // the same, set by the caller for the life of the context (one process
+    // per GPU, each holding one shard: TPE_OPT_WHOLE_N / _ROUNDS)
+    int64_t opt_whole_n = 0;
+    int32_t opt_whole_rounds = 0;
     tpe_rt::QExchange* qx = nullptr;
 
     int fail(int code, const std::string& m) {

@@ -505,8 +505,11 @@ __device__ __forceinline__ void lse_dense(const Comp<float>* __restrict__ c, int
 // always re-scored, which also keeps the reference's NaN-greatest order.
 constexpr float kScreenMinAcc = 0x1.0p-60f;
 
-__device__ __forceinline__ double screen_err(float amax, int K, double X, double dx, float acc,
-                                             float l2) {
+// Kc: the longest run of terms one fp32 running sum adds (K, or a chunk's
+// length when the mixture is summed in chunks whose fp32 sums are added in
+// fp64 -- that addition adds nch 2^-53, inside the 2^-41 slack)
+__device__ __forceinline__ double screen_err(float amax, int K, int Kc, double X, double dx,
+                                             float acc, float l2) {
     if (!(acc >= kScreenMinAcc) || !(acc <= 0x1.0p+100f) || !(X <= 1e30)) return __builtin_inf();
     constexpr double u = 0x1.0p-24;
     const double T = fmin(125.0, fmax(16.0, (43.0 + log2(2.0 * (double)K) - (double)l2) / 0.9997));
@@ -516,7 +519,7 @@ __device__ __forceinline__ double screen_err(float amax, int K, double X, double
     const double dt = (2.0 * T + 1.0) * u + zeta * (2.0 * sqT + zeta);
     if (!(dt <= 0.01)) return __builtin_inf();
     const double rho = 0.7 * dt + 2.5e-7;
-    const double gsum = ((double)(K / 128) + 28.0) * u * 1.01;
+    const double gsum = ((double)(Kc / 128) + 28.0) * u * 1.01;
     const double rel = rho + gsum + 0x1.0p-41;
     return 1.02 * rel + 0x1.0p-22 * 0.6931471805599453 * (fabs((double)l2) + 1.0);
 }

@@ -490,8 +490,8 @@ __global__ __launch_bounds__(kBlock) void k_screen(
         const double lb = (double)l2b * 0.6931471805599453 + L.shift_b;
         const double la = (double)l2a * 0.6931471805599453 + L.shift_a;
         const double s = lb - la;
-        const double E = 1.25 * (screen_err(L.amax_b, L.nb, X[r], dx[r], ab[r], l2b) +
-                                 screen_err(L.amax_a, L.na, X[r], dx[r], aa[r], l2a) +
+        const double E = 1.25 * (screen_err(L.amax_b, L.nb, L.nb, X[r], dx[r], ab[r], l2b) +
+                                 screen_err(L.amax_a, L.na, L.na, X[r], dx[r], aa[r], l2a) +
                                  fp64_err(L.nb + L.na, fabs(lb) + fabs(la) + fabs(y[r])));
         if constexpr (!SAMPLE) {
             s_out[ci[r]] = s;
@@ -630,6 +630,204 @@ __global__ __launch_bounds__(kBlock) void k_rescore(
     }
     __shared__ Partial sh[kBlock / 64];
     block_maxloc(bk, bi, bv, bl, ba, prow + ch.j, sh);
+}
+
+// ---------------------------------------- fp32 screen (packed map) ----
+// Batched rounds with small C (config 5: 4096 new_ids x 24 candidates)
+// keep their whole rounds inside one workgroup, so the screen needs no
+// atomics for the bound: k_round_chunk<float> writes the fp32 sums (per
+// chunk of the above mixture, as the fp64 chunked map does), k_pick_packed
+// forms s32 and its bound per slot, takes the per-round largest lower
+// bound in LDS and compacts the slots that can still win -- about one per
+// (round, label) -- into a per-label list, with each round's [first, count)
+// range; k_rescore_packed re-draws them and runs the fp64 arithmetic of the
+// unscreened packed map (below sum, above sum chunk by chunk added in order,
+// lse_finish), and k_pick_rounds keeps each round's best.  The winners and
+// their lpdfs are those of the unscreened packed round, bit for bit.
+struct RoundSel {
+    int32_t first, count;
+};
+
+// entries per packed re-score block: kRP * 256 (a label's ~3k entries at
+// config 5 leave less of the last block idle than with kR)
+constexpr int kRP = 1;
+
+template <int R>
+__global__ __launch_bounds__(kBlock) void k_pick_packed(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group, int64_t n, int32_t nl,
+    int32_t nch, int32_t chunk, const double* __restrict__ part, int32_t* __restrict__ cnt,
+    int64_t* __restrict__ list, int64_t cap, RoundSel* __restrict__ rsel, Slots S) {
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    const bool lgmm = L.mode == DENSE_LGMM;
+    const int gx = gridDim.x, bx = blockIdx.x, by = blockIdx.y;
+    constexpr int NS = R * kBlock;
+    __shared__ uint64_t lo_key[NS];
+    __shared__ uint64_t hi_key[NS];
+    __shared__ uint64_t round_lb[NS];
+    __shared__ int32_t round_cnt[NS], round_first[NS];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        int64_t z, ci;
+        bool valid;
+        S.template at<R>(r, n, z, ci, valid);
+        const int s = r * kBlock + threadIdx.x;
+        const double x = part[chunk_plane(by, 0, nch, bx, gx, R) + s];
+        const double sb = part[chunk_plane(by, 1, nch, bx, gx, R) + s];
+        double sa = 0.0;
+        for (int c = 0; c < nch; ++c) sa += part[chunk_plane(by, 2 + c, nch, bx, gx, R) + s];
+        const double y = lgmm ? log(x) : x;
+        const double xr = y - L.centre;
+        const float xf = (float)xr;
+        const double X = fabs(xr), dx = fabs((double)xf - xr);
+        const double lb = log(sb) + L.shift_b, la = log(sa) + L.shift_a;
+        const double s32 = lb - la;
+        const double E = 1.25 * (screen_err(L.amax_b, L.nb, L.nb, X, dx, (float)sb, (float)log2(sb)) +
+                                 screen_err(L.amax_a, L.na, chunk, X, dx, (float)sa, (float)log2(sa)) +
+                                 fp64_err(L.nb + L.na, fabs(lb) + fabs(la) + fabs(y)));
+        const bool cert = valid && E <= 1e30 && s32 == s32;
+        lo_key[s] = cert ? order_key(s32 - E) : 0ull;
+        hi_key[s] = !valid ? 0ull : (cert ? order_key(s32 + E) : ~0ull);
+    }
+    __syncthreads();
+    // one thread per round of this workgroup: its largest lower bound
+    for (int t = threadIdx.x; t < S.rpb; t += kBlock) {
+        uint64_t m = 0;
+        for (int c = 0; c < S.cpack; ++c) m = lo_key[t * S.cpack + c] > m ? lo_key[t * S.cpack + c] : m;
+        round_lb[t] = m;
+        int k = 0;
+        for (int c = 0; c < S.cpack; ++c) k += (hi_key[t * S.cpack + c] >= m && hi_key[t * S.cpack + c]);
+        round_cnt[t] = k;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int t = 0; t < S.rpb; ++t) {
+            round_first[t] = tot;
+            tot += round_cnt[t];
+        }
+        const int base = tot ? atomicAdd(cnt + by, tot) : 0;
+        for (int t = 0; t < S.rpb; ++t) round_first[t] += base;
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < S.rpb; t += kBlock) {
+        const int64_t z = (int64_t)bx * S.rpb + t;
+        if (z >= S.n_rounds) continue;
+        const uint64_t m = round_lb[t];
+        int at = round_first[t];
+        rsel[(size_t)z * nl + by] = RoundSel{at, round_cnt[t]};
+        for (int c = 0; c < S.cpack; ++c) {
+            const uint64_t h = hi_key[t * S.cpack + c];
+            if (h && h >= m) list[(size_t)by * cap + at++] = (z << 32) | (int64_t)c;
+        }
+    }
+}
+
+// Re-score work item (label position, block j of kR * 256 entries) x chunk:
+// blockIdx.y = c sums the above mixture's chunk c (c = 0 also the below
+// mixture and the candidate) from zero -- the chunked map's own per-chunk
+// sums -- into plane 2 + c (0: below, 1: x) at the entry's place off[y] + e
+// of the compacted order; k_finish_rescore adds the chunks in order.
+template <int R>
+__global__ __launch_bounds__(kBlock) void k_rescore_packed(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<double>* __restrict__ comps64, const SampRec* __restrict__ samp,
+    int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, int32_t chunk,
+    const int32_t* __restrict__ cnt, const int64_t* __restrict__ list, int64_t cap,
+    const RescoreChunk* __restrict__ chunks, const int64_t* __restrict__ off, int64_t total,
+    double* __restrict__ planes) {
+    const RescoreChunk ch = chunks[blockIdx.x];
+    const int y = ch.cell, c = blockIdx.y;
+    const DLabel L = labels[group[y]];
+    const int64_t count = cnt[y];
+    constexpr int64_t per = (int64_t)R * kBlock;
+    __shared__ double exp_tab[kExpTabSize];
+    load_exp_table(exp_tab);
+    const bool lgmm = L.mode == DENSE_LGMM;
+    double x[R], xr[R], sb[R], sa[R];
+    int64_t e[R];
+    bool valid[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        e[r] = (int64_t)ch.j * per + r * kBlock + threadIdx.x;
+        valid[r] = e[r] < count;
+        const int64_t ent = valid[r] ? list[(size_t)y * cap + e[r]] : 0;
+        const int64_t z = ent >> 32, i = ent & 0xffffffffll;
+        double v = lgmm ? 1.0 : 0.0;
+        if (valid[r]) {
+            const uint32_t rk = rounds[z], gi = (uint32_t)(cand_offset + i);
+            if (lgmm) (void)sample_below<DENSE_LGMM>(L, samp + L.samp_off, seed, rk, gi, v);
+            else (void)sample_below<DENSE_GMM>(L, samp + L.samp_off, seed, rk, gi, v);
+        }
+        x[r] = v;
+        xr[r] = (lgmm ? log(v) : v) - L.centre;
+        sb[r] = 0.0;
+        sa[r] = 0.0;
+    }
+    if (c == 0) lse_acc<R>(comps64 + L.comp_b, L.nb, xr, sb, exp_tab);
+    const int k0 = min(c * chunk, L.na), k1 = min(k0 + chunk, L.na);
+    lse_acc<R>(comps64 + L.comp_a + k0, k1 - k0, xr, sa, exp_tab);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (!valid[r]) continue;
+        const size_t g = (size_t)(off[y] + e[r]);
+        if (c == 0) {
+            planes[g] = sb[r];
+            planes[(size_t)total + g] = x[r];
+        }
+        planes[(size_t)(2 + c) * total + g] = sa[r];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_finish_rescore(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<double>* __restrict__ comps64, int64_t cand_offset, int32_t nch,
+    const int32_t* __restrict__ cnt, const int64_t* __restrict__ list, int64_t cap,
+    const RescoreChunk* __restrict__ chunks, const int64_t* __restrict__ off, int64_t total,
+    const double* __restrict__ planes, Partial* __restrict__ res) {
+    const RescoreChunk ch = chunks[blockIdx.x];
+    const int y = ch.cell;
+    const DLabel L = labels[group[y]];
+    const bool lgmm = L.mode == DENSE_LGMM;
+    constexpr int64_t per = (int64_t)kRP * kBlock;
+    for (int r = 0; r < kRP; ++r) {
+        const int64_t e = (int64_t)ch.j * per + r * kBlock + threadIdx.x;
+        if (e >= cnt[y]) continue;
+        const size_t g = (size_t)(off[y] + e);
+        const double sb = planes[g], x = planes[(size_t)total + g];
+        double sa = 0.0;
+        for (int c = 0; c < nch; ++c) sa += planes[(size_t)(2 + c) * total + g];
+        const double yv = lgmm ? log(x) : x;
+        double lb = lse_finish(comps64 + L.comp_b, L.nb, sb, yv - L.centre, L.shift_b);
+        double la = lse_finish(comps64 + L.comp_a, L.na, sa, yv - L.centre, L.shift_a);
+        if (lgmm) {
+            lb -= yv;
+            la -= yv;
+        }
+        const int64_t i = list[(size_t)y * cap + e] & 0xffffffffll;
+        res[g] = Partial{order_key(lb - la), cand_offset + i, x, lb, la};
+    }
+}
+
+// one thread per (round, dense label): the best re-scored candidate of the
+// round (its entries are in candidate order) -> the round's partial
+__global__ __launch_bounds__(kBlock) void k_pick_rounds(const int32_t* __restrict__ group, int32_t nl,
+                                                        int32_t n_rounds, int32_t n_labels,
+                                                        const RoundSel* __restrict__ rsel,
+                                                        const Partial* __restrict__ res,
+                                                        const int64_t* __restrict__ off,
+                                                        Partial* __restrict__ partials) {
+    const int64_t cell = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (cell >= (int64_t)n_rounds * nl) return;
+    const int64_t z = cell / nl;
+    const int y = (int)(cell % nl);
+    const RoundSel rs = rsel[cell];
+    Partial best{0, INT64_MAX, 0.0, 0.0, 0.0};
+    for (int k = 0; k < rs.count; ++k) {
+        const Partial& p = res[(size_t)(off[y] + rs.first + k)];
+        if (better(p.key, p.idx, best.key, best.idx)) best = p;
+    }
+    partials[(size_t)z * n_labels + group[y]] = best;
 }
 
 // ------------------------------------------------------- split-K map ----
@@ -1200,6 +1398,78 @@ int dense_chunks(const tpe_ctx* ctx, uint32_t gx, int nl) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(want, na_max / kMinChunk));
 }
 
+// Packed-map sampled rounds of the dense labels, screened (see
+// k_pick_packed): fp32 chunk sums, per-round selection, fp64 re-score with
+// the chunked map's summation order, per-round pick.
+int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, const RoundArgs& a) {
+    int32_t na_max = 1;
+    for (int m : {DENSE_GMM, DENSE_LGMM})
+        for (int li : ctx->P->h_group[m]) na_max = std::max(na_max, ctx->P->h_labels[li].na);
+    const int32_t chunk = (na_max + nch - 1) / nch;
+    const size_t planes = (size_t)nl * (nch + 2) * a.gx * (kR * kBlock);
+    const int64_t cap = (int64_t)a.n_rounds * a.n;   // candidate slots per label
+    HIPCHK(ctx, ctx->chunk_part.reserve(planes));
+    HIPCHK(ctx, ctx->scr_list.reserve((size_t)nl * cap));
+    HIPCHK(ctx, ctx->scr_rsel.reserve((size_t)a.n_rounds * nl));
+    HIPCHK(ctx, ctx->scr_cnt.reserve(nl));
+    HIPCHK(ctx, hipMemsetAsync(ctx->scr_cnt.p, 0, nl * sizeof(int32_t), ctx->stream));
+    RoundSel* rsel = reinterpret_cast<RoundSel*>(ctx->scr_rsel.p);
+    HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
+#define TPE_SCREEN_PACKED(RR)                                                                      \
+    hipLaunchKernelGGL((k_round_chunk<float, RR>), dim3(a.gx, nl, nch), dim3(kBlock), 0, ctx->stream, \
+                       ctx->P->labels.p, grp, ctx->P->comps32.p, ctx->P->samp.p, a.n, a.cand_offset,   \
+                       a.seed, ctx->rounds.p, chunk, ctx->chunk_part.p, ctx->errflag.p, a.S);          \
+    HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));                                          \
+    hipLaunchKernelGGL((k_pick_packed<RR>), dim3(a.gx, nl), dim3(kBlock), 0, ctx->stream,           \
+                       ctx->P->labels.p, grp, a.n, nl, nch, chunk, ctx->chunk_part.p, ctx->scr_cnt.p,  \
+                       ctx->scr_list.p, cap, rsel, a.S)
+    if (narrow(a.S)) {
+        TPE_SCREEN_PACKED(kRGroup);
+    } else {
+        TPE_SCREEN_PACKED(kR);
+    }
+#undef TPE_SCREEN_PACKED
+    ctx->scr_cnt_h.resize(nl);
+    HIPCHK(ctx, hipMemcpyAsync(ctx->scr_cnt_h.data(), ctx->scr_cnt.p, nl * sizeof(int32_t),
+                               hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    constexpr int64_t per = (int64_t)kRP * kBlock;
+    std::vector<RescoreChunk>& tab = ctx->scr_chunks_h;
+    tab.clear();
+    std::vector<int64_t> off(nl + 1, 0);
+    for (int y = 0; y < nl; ++y) {
+        off[y + 1] = off[y] + ctx->scr_cnt_h[y];
+        for (int32_t j = 0; (int64_t)j * per < ctx->scr_cnt_h[y]; ++j) tab.push_back(RescoreChunk{y, j});
+    }
+    const int64_t total = std::max<int64_t>(off[nl], 1);
+    HIPCHK(ctx, ctx->scr_res.reserve(total));
+    HIPCHK(ctx, ctx->scr_off.reserve(nl + 1));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->scr_off.p, off.data(), (nl + 1) * sizeof(int64_t),
+                               hipMemcpyHostToDevice, ctx->stream));
+    if (!tab.empty()) {
+        HIPCHK(ctx, ctx->scr_chunks.reserve(tab.size()));
+        HIPCHK(ctx, ctx->scr_planes.reserve((size_t)(nch + 2) * total));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->scr_chunks.p, tab.data(), tab.size() * sizeof(RescoreChunk),
+                                   hipMemcpyHostToDevice, ctx->stream));
+        const RescoreChunk* tabd = reinterpret_cast<const RescoreChunk*>(ctx->scr_chunks.p);
+        hipLaunchKernelGGL((k_rescore_packed<kRP>), dim3((unsigned)tab.size(), nch), dim3(kBlock), 0,
+                           ctx->stream, ctx->P->labels.p, grp, ctx->P->comps64.p, ctx->P->samp.p,
+                           a.cand_offset, a.seed, ctx->rounds.p, chunk, ctx->scr_cnt.p,
+                           ctx->scr_list.p, cap, tabd, ctx->scr_off.p, total, ctx->scr_planes.p);
+        hipLaunchKernelGGL(k_finish_rescore, dim3((unsigned)tab.size()), dim3(kBlock), 0, ctx->stream,
+                           ctx->P->labels.p, grp, ctx->P->comps64.p, a.cand_offset, nch, ctx->scr_cnt.p,
+                           ctx->scr_list.p, cap, tabd, ctx->scr_off.p, total, ctx->scr_planes.p,
+                           ctx->scr_res.p);
+    }
+    const int64_t cells = (int64_t)a.n_rounds * nl;
+    hipLaunchKernelGGL(k_pick_rounds, dim3((unsigned)((cells + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       ctx->stream, grp, nl, a.n_rounds, ctx->P->n_labels, rsel, ctx->scr_res.p,
+                       ctx->scr_off.p, ctx->partials.p);
+    ctx->screen_total += cells * a.n;
+    ctx->screen_pending = true;
+    return ctx->hip(hipGetLastError(), "packed screen launch");
+}
+
 // Sampled rounds: the dense GMM1 and LGMM1 labels in ONE launch (their
 // groups are adjacent), so both families fill the chip together instead of
 // leaving each other's tail idle.  Timed and counted in the DENSE_GMM slot.
@@ -1256,6 +1526,11 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
         ctx->screen_pending = true;
         bracket(ctx, DENSE_GMM, 1);
         return ctx->hip(hipGetLastError(), "screen launch");
+    }
+    if (sizeof(T) == 8 && ctx->screen && a.S.cpack != 0) {   // packed map, screened
+        const int rc = launch_screen_packed(ctx, grp, nl, nch, a);
+        bracket(ctx, DENSE_GMM, 1);
+        return rc;
     }
     if (nch > 1) {
         int32_t na_max = 1;
@@ -1480,8 +1755,11 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         g.count[m] = 1;
     }
     // the whole problem (ctx->hint_*: set by a multi-device context for its shards)
-    const int64_t n_whole = ctx->hint_n > 0 ? ctx->hint_n : n;
-    const int32_t rounds_whole = ctx->hint_rounds > 0 ? ctx->hint_rounds : n_rounds;
+    const int64_t n_whole =
+        ctx->hint_n > 0 ? ctx->hint_n : (ctx->opt_whole_n > 0 ? ctx->opt_whole_n : n);
+    const int32_t rounds_whole = ctx->hint_rounds > 0
+                                     ? ctx->hint_rounds
+                                     : (ctx->opt_whole_rounds > 0 ? ctx->opt_whole_rounds : n_rounds);
     const uint32_t gx_whole =
         S.cpack ? (uint32_t)((rounds_whole + S.rpb - 1) / S.rpb) : gx;
     RoundArgs a{n, cand_offset, seed, n_rounds, tiles, cand_in_dev, olb, ola, S, gx, gz,
@@ -1834,6 +2112,12 @@ TPE_DEV void tpe1_ctx_destroy(tpe_ctx* c) {
     c->scr_idx.release();
     c->scr_lb.release();
     c->scr_cnt.release();
+    c->scr_chunks.release();
+    c->scr_list.release();
+    c->scr_res.release();
+    c->scr_rsel.release();
+    c->scr_off.release();
+    c->scr_planes.release();
     c->chunk_part.release();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1980,6 +2264,14 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
         case TPE_OPT_CHUNKS:
             if (value < 0 || value > 4096) return ctx->fail(TPE_ERR_ARG, "chunks must be in [0, 4096]");
             ctx->chunks_forced = (int32_t)value;
+            break;
+        case TPE_OPT_WHOLE_N:
+            if (value < 0) return ctx->fail(TPE_ERR_ARG, "whole candidate count must be >= 0");
+            ctx->opt_whole_n = value;
+            break;
+        case TPE_OPT_WHOLE_ROUNDS:
+            if (value < 0 || value > INT32_MAX) return ctx->fail(TPE_ERR_ARG, "whole round count");
+            ctx->opt_whole_rounds = (int32_t)value;
             break;
         default: return ctx->fail(TPE_ERR_ARG, "unknown option " + std::to_string(option));
     }

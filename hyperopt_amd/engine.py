@@ -238,11 +238,14 @@ class Engine(object):
         return (a.value, b.value, ms.value) if with_ms else (a.value, b.value)
 
     OPTIONS = {'screen': L.TPE_OPT_SCREEN, 'splitk': L.TPE_OPT_SPLITK, 'dedup': L.TPE_OPT_DEDUP,
-               'chunks': L.TPE_OPT_CHUNKS}
+               'chunks': L.TPE_OPT_CHUNKS, 'whole_n': L.TPE_OPT_WHOLE_N,
+               'whole_rounds': L.TPE_OPT_WHOLE_ROUNDS}
 
     def set_option(self, name, value):
         """Engine switches (include/hyperopt_tpe.h TPE_OPT_*): 'screen',
-        'splitk', 'dedup' (bool), 'chunks' (int, 0 = auto)."""
+        'splitk', 'dedup' (bool), 'chunks' (int, 0 = auto), 'whole_n' /
+        'whole_rounds' (the whole problem when this engine runs one shard of
+        it, 0 = the call's own)."""
         self._check(self.lib.tpe_set_option(self.h, self.OPTIONS[name], int(value)))
 
     def screen_probe(self, label, cand):

@@ -313,11 +313,19 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *   TPE_OPT_SPLITK  split-K map for small sampled rounds                [1]
  *   TPE_OPT_DEDUP   quantized labels scored once per grid value         [1]
  *   TPE_OPT_CHUNKS  chunks of the packed map's above mixtures (0 auto)  [0]
- * None of them changes a winner; they exist for tests and experiments. */
+ *   TPE_OPT_WHOLE_N, TPE_OPT_WHOLE_ROUNDS  the whole problem's candidates
+ *                   per round / rounds when this context computes one shard
+ *                   of it (one process per GPU); map choices that change a
+ *                   summation order follow the whole problem, so the merged
+ *                   shards equal one context's round bit for bit     [0: this call's]
+ * None of them changes a winner; they exist for tests, experiments and
+ * sharded runs. */
 #define TPE_OPT_SCREEN 1
 #define TPE_OPT_SPLITK 2
 #define TPE_OPT_DEDUP 3
 #define TPE_OPT_CHUNKS 4
+#define TPE_OPT_WHOLE_N 5
+#define TPE_OPT_WHOLE_ROUNDS 6
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
 
 #ifdef __cplusplus

@@ -1,6 +1,8 @@
-"""The cross-rank winner exchange (hyperopt_amd/parallel.py) with the gloo
-backend, world_size 2, on CPU: every rank ends with the broadcast_best merge
-of all ranks' winners."""
+"""The cross-rank exchanges (hyperopt_amd/parallel.py) with the gloo
+backend, world_size 2: every rank ends with the broadcast_best merge of all
+ranks' winners (candidate shards) or with every rank's rounds in order
+(new_id shards) -- on CPU with synthetic rows, and on the GPU box with real
+engine shards (two ranks sharing the card) against one unsharded engine."""
 import os
 import socket
 
@@ -34,9 +36,10 @@ def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
-        from hyperopt_amd.parallel import exchange_winners
+        from hyperopt_amd.parallel import exchange_winners, gather_rounds
         out = exchange_winners(_rank_results(rank))
-        q.put((rank, out.tobytes()))
+        rows = np.stack([_rank_results(rank), _rank_results(rank + 10)])   # 2 rounds per rank
+        q.put((rank, out.tobytes(), gather_rounds(rows).tobytes()))
     finally:
         dist.destroy_process_group()
 
@@ -50,10 +53,17 @@ def test_exchange_winners_gloo_world2():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=120) for _ in procs)
+    got, gathered = {}, {}
+    for _ in procs:
+        r, a, b = q.get(timeout=120)
+        got[r], gathered[r] = a, b
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    rounds = np.stack([_rank_results(0), _rank_results(10), _rank_results(1), _rank_results(11)])
+    for r in (0, 1):
+        g = np.frombuffer(gathered[r], dtype=RESULT_DTYPE).reshape(4, -1)
+        assert np.array_equal(g['index'], rounds['index'])
     want = merge_results(np.stack([_rank_results(0), _rank_results(1)]))
     for r in (0, 1):
         out = np.frombuffer(got[r], dtype=RESULT_DTYPE)
@@ -62,3 +72,61 @@ def test_exchange_winners_gloo_world2():
         assert out['index'][1] == 1001       # NaN on rank 1 wins
     assert np.array_equal(np.frombuffer(got[0], dtype=RESULT_DTYPE)['index'],
                           np.frombuffer(got[1], dtype=RESULT_DTYPE)['index'])
+
+
+def _engine_worker(rank, world, port, q):
+    """One rank of a config-3-shaped run on the GPU: its candidate shard
+    (global offset rank * C/world) and its share of batched new_ids."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from hyperopt_amd.engine import Engine
+        from hyperopt_amd.parallel import exchange_winners, gather_rounds
+        from hyperopt_amd.workloads import mixed_history
+        hist = mixed_history(16, 4000, seed=2)
+        eng = Engine(0)
+        eng.build_posterior(*hist.device_inputs(), gamma=0.25, prior_weight=1.0)
+        eng.set_option('whole_rounds', 128)     # 128 new_ids over the two ranks
+        C = 1 << 18
+        mine = eng.suggest(42, C // world, round=9, cand_offset=rank * (C // world))
+        merged = exchange_winners(mine)
+        ids = list(range(500 + rank * 64, 500 + (rank + 1) * 64))
+        rows = gather_rounds(eng.suggest_batch(7, ids, 24))
+        eng.set_option('whole_rounds', 0)
+        eng.close()
+        q.put((rank, merged.tobytes(), rows.tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_engine_shards_gloo_world2():
+    import multiprocessing as mp
+    from hyperopt_amd.engine import RESULT_DTYPE, Engine
+    from hyperopt_amd.workloads import mixed_history
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_engine_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in procs:
+        r, a, b = q.get(timeout=200)
+        got[r] = (a, b)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    hist = mixed_history(16, 4000, seed=2)
+    eng = Engine(0)
+    eng.build_posterior(*hist.device_inputs(), gamma=0.25, prior_weight=1.0)
+    want = eng.suggest(42, 1 << 18, round=9)
+    want_rows = eng.suggest_batch(7, list(range(500, 628)), 24)
+    eng.close()
+    for r in (0, 1):
+        merged = np.frombuffer(got[r][0], dtype=RESULT_DTYPE)
+        rows = np.frombuffer(got[r][1], dtype=RESULT_DTYPE).reshape(want_rows.shape)
+        for f in ('index', 'value', 'lpdf_below', 'lpdf_above'):
+            assert np.array_equal(merged[f], want[f]), f
+            assert np.array_equal(rows[f], want_rows[f]), f

@@ -117,3 +117,29 @@ def test_screen_uncertified_candidates(eng):
     _assert_same(a, b)
     # label 0: all 2^14 re-scored; label 1: a few
     assert rescored >= (1 << 14) and rescored < screened
+
+
+@pytest.mark.parametrize('rounds,C,chunks', [(512, 24, 0), (4096, 24, 0), (300, 24, 1),
+                                             (64, 100, 0), (40, 700, 3)])
+def test_screened_packed_rounds_are_the_fp64_rounds(eng, rounds, C, chunks):
+    """Batched rounds with small C (the packed map; config 5's shape) --
+    chunked or not -- screened and unscreened give identical winners and
+    lpdfs."""
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.workloads import mixed_history
+    hist = mixed_history(128, 50000, seed=0) if rounds >= 4096 else mixed_history(64, 20000, seed=1)
+    eng.set_posterior(*P.pack(hist.posteriors()))
+    eng.set_option('chunks', chunks)
+    try:
+        ids = list(range(7000, 7000 + rounds))
+        eng.set_option('screen', 1)
+        a = eng.suggest_batch(31, ids, C)
+        screened, rescored = eng.last_screen()
+        eng.set_option('screen', 0)
+        b = eng.suggest_batch(31, ids, C)
+        eng.set_option('screen', 1)
+    finally:
+        eng.set_option('chunks', 0)
+    _assert_same(a, b)
+    assert screened > 0 and rescored < screened
+    print('packed %d x %d (chunks %d): re-scored %.4f' % (rounds, C, chunks, rescored / screened))
