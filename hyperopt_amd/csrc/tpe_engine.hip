@@ -650,7 +650,7 @@ struct RoundSel {
 
 // entries per packed re-score block: kRP * 256 (a label's ~3k entries at
 // config 5 leave less of the last block idle than with kR)
-constexpr int kRP = 1;
+constexpr int kRP = 2;
 
 template <int R>
 __global__ __launch_bounds__(kBlock) void k_pick_packed(
