@@ -571,6 +571,13 @@ __global__ __launch_bounds__(kBlock) void k_fill_empty(const int32_t* __restrict
 // hardware scheduler balances the chunks over the chip.
 using RescoreChunk = tpe_rt::RescoreChunkH;
 
+// candidates per thread in k_screen (its own tile width): the component's
+// m shared by more candidates costs fewer v_mov_b64 per eval
+#ifndef TPE_SCREEN_R
+#define TPE_SCREEN_R 8
+#endif
+constexpr int kScreenR = TPE_SCREEN_R;
+
 template <int R>
 __global__ __launch_bounds__(kBlock) void k_rescore(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
@@ -1491,7 +1498,8 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
         HIPCHK(ctx, hipMemsetAsync(ctx->scr_lb.p, 0, cells * sizeof(unsigned long long), ctx->stream));
         HIPCHK(ctx, hipMemsetAsync(ctx->scr_cnt.p, 0, cells * sizeof(int32_t), ctx->stream));
         HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
-        hipLaunchKernelGGL((k_screen<kR, true>), dim3(a.gx, nl, a.gz), dim3(kBlock), 0, ctx->stream,
+        const unsigned sgx = (unsigned)((a.n + kScreenR * kBlock - 1) / (kScreenR * kBlock));
+        hipLaunchKernelGGL((k_screen<kScreenR, true>), dim3(sgx, nl, a.gz), dim3(kBlock), 0, ctx->stream,
                            ctx->P->labels.p, grp, ctx->P->comps32.p, ctx->P->samp.p, a.n,
                            a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->scr_hi.p, ctx->scr_lb.p,
                            ctx->errflag.p, a.S, nullptr, nullptr, nullptr);
