@@ -45,7 +45,9 @@ FLOPS_PER_EVAL = {'f64': 6.0, 'f32': 6.0}
 #         v_pk_fma_f32 (z), v_pk_fma_f32 (t) and 1/2 v_pk_add_f32 (tree of
 #         8, then the running sum) per two evals, 1/8 v_mov_b64 per eval, and
 #         one v_exp_f32 (8-cycle issue = 2 slots) per eval = 3.625 slots
-VALU_SLOTS_PER_EVAL = {'f64': 12.25, 'f32': 3.625}
+#   k_screen: the same with 8 candidates per thread (v_mov_b64 per 8 evals) =
+#         3.5625 slots
+VALU_SLOTS_PER_EVAL = {'f64': 12.25, 'f32': 3.625, 'screen': 3.5625}
 PEAK_FP64_VECTOR_TFLOPS = 78.6        # MI355X spec (MI355X_MICROARCH.md)
 PEAK_FP32_VECTOR_TFLOPS = 157.3
 # 4-cycle wave64 VALU issue slots per second at 2.4 GHz, in lanes: 256 CU x
@@ -321,8 +323,8 @@ def main():
     if screened:
         # k_screen: every dense (candidate, component) pair in packed fp32
         dom_ms = scr[2]
-        kprec, kname, kdesc = 'f32', 'k_screen<4, true>', 'k_screen<4,true> (fp32 screen of the ' \
-            'fp64 round, GMM1+LGMM1 labels)'
+        kprec, kname, kdesc = 'f32', 'k_screen<', 'k_screen (fp32 screen of the fp64 round, ' \
+            'GMM1+LGMM1 labels)'
     else:
         dom_ms = mode_ms[dom]
         kprec = prec
@@ -343,7 +345,7 @@ def main():
             'traffic_source': traffic_src, 'valu_busy_measured': valu_busy,
             'valu_busy_source': traffic_src,
             'evals_per_s': dom_rate, 'flops_per_eval': FLOPS_PER_EVAL[kprec],
-            'valu_issue_frac': round(dom_rate * VALU_SLOTS_PER_EVAL[kprec] /
+            'valu_issue_frac': round(dom_rate * VALU_SLOTS_PER_EVAL['screen' if screened else kprec] /
                                      PEAK_VALU_LANE_INSTR[kprec], 4),
             'launch_ms': dom_ms / args.steps}
     line = {

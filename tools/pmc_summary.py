@@ -17,7 +17,7 @@ import shutil
 import sys
 from collections import defaultdict
 
-FAMILY = {'k_screen<4, true>': 'dense',
+FAMILY = {'k_screen<': 'dense',
           'k_round<double, 0,': 'dense', 'k_round<double, 1,': 'dense_lgmm1',
           'k_round<float, 0,': 'dense', 'k_round<float, 1,': 'dense_lgmm1',
           'k_round<double, 8,': 'dense', 'k_round<float, 8,': 'dense'}
