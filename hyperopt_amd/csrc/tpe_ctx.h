@@ -223,6 +223,7 @@ struct tpe_ctx {
     int64_t opt_whole_n = 0;
     int32_t opt_whole_rounds = 0;
     tpe_rt::QExchange* qx = nullptr;
+    int32_t shard_id = 0;                // this context's position in a sharded round
 
     int fail(int code, const std::string& m) {
         err = m;

@@ -77,11 +77,13 @@ struct WindowExchange final : tpe_rt::QExchange {
     int expected, arrived = 0;
     bool aborted = false;
     std::vector<unsigned long long> mm;   // combined: min over [0, nq), max over [nq, 2 nq)
+    std::vector<char> posted;             // per device: reached the exchange
 
-    explicit WindowExchange(int n) : expected(n) {}
+    explicit WindowExchange(int n) : expected(n), posted(n, 0) {}
 
     int exchange(tpe_ctx* ctx, std::vector<unsigned long long>& local) override {
         std::unique_lock<std::mutex> lk(mu);
+        if (ctx->shard_id >= 0 && ctx->shard_id < expected) posted[ctx->shard_id] = 1;
         const size_t nq = local.size() / 2;
         if (mm.empty()) {
             mm.assign(local.size(), 0ull);
@@ -107,6 +109,17 @@ struct WindowExchange final : tpe_rt::QExchange {
         std::lock_guard<std::mutex> lk(mu);
         aborted = true;
         cv.notify_all();
+    }
+
+    // A shard that finished without posting (its round took a path without
+    // quantized tables while another's did -- the shards' paths are meant to
+    // be identical) must not leave the others waiting: fail them instead.
+    void finished(int d) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!posted[d] && arrived > 0 && arrived < expected) {
+            aborted = true;
+            cv.notify_all();
+        }
     }
 };
 
@@ -183,6 +196,7 @@ int sharded_round(tpe_ctx* c, uint64_t seed, const uint32_t* rounds, int32_t n_r
         x->hint_n = n;
         x->hint_rounds = n_rounds;
         x->qx = &wx;
+        x->shard_id = d;
         tpe_label_result* o = by_cand ? parts.data() + (size_t)d * n_rounds * L
                                       : out + (size_t)sh[d].round_lo * L;
         int r = tpe1_suggest_batch(x, seed, rounds + sh[d].round_lo, sh[d].n_rounds, sh[d].n_cand,
@@ -191,6 +205,7 @@ int sharded_round(tpe_ctx* c, uint64_t seed, const uint32_t* rounds, int32_t n_r
         x->hint_rounds = 0;
         x->qx = nullptr;
         if (r) wx.abort();
+        else wx.finished(d);
         return r;
     });
     if (rc) return rc;
