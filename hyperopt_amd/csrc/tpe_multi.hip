@@ -99,8 +99,10 @@ struct WindowExchange final : tpe_rt::QExchange {
             mm[nq + i] = local[nq + i] > mm[nq + i] ? local[nq + i] : mm[nq + i];
         }
         if (++arrived == expected) cv.notify_all();
-        cv.wait(lk, [&] { return arrived == expected || aborted; });
+        cv.wait(lk, [&] { return arrived == expected || aborted || arrived + unposted == expected; });
         if (aborted) return ctx->fail(TPE_ERR_ARG, "multi-device round: another device failed");
+        if (arrived != expected)
+            return ctx->fail(TPE_ERR_ARG, "multi-device round: shards took different paths");
         local = mm;
         return TPE_OK;
     }
@@ -116,11 +118,12 @@ struct WindowExchange final : tpe_rt::QExchange {
     // be identical) must not leave the others waiting: fail them instead.
     void finished(int d) {
         std::lock_guard<std::mutex> lk(mu);
-        if (!posted[d] && arrived > 0 && arrived < expected) {
-            aborted = true;
+        if (!posted[d]) {
+            ++unposted;
             cv.notify_all();
         }
     }
+    int unposted = 0;
 };
 
 struct Shard {
