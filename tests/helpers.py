@@ -72,9 +72,12 @@ def assert_lpdf_close(got, ref, quantized=False, rtol=1e-9, atol=1e-9, w_sum=1.0
     same_inf = np.isinf(got) & (got == ref)
     with np.errstate(invalid='ignore', over='ignore'):
         ok = both_nan | same_inf | (np.abs(got - ref) <= atol + rtol * np.abs(ref))
+        abs_only = np.zeros_like(ok)
         if quantized:
-            ok |= np.abs(np.exp(got) - np.exp(ref)) <= 1e-13 * w_sum
+            abs_only = ~ok & (np.abs(np.exp(got) - np.exp(ref)) <= 1e-13 * w_sum)
+            ok |= abs_only
     if not ok.all():
         bad = np.where(~ok)[0][:8]
         raise AssertionError('lpdf mismatch at %s: got %s ref %s' % (
             bad.tolist(), got[bad].tolist(), ref[bad].tolist()))
+    return abs_only

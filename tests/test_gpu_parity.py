@@ -48,6 +48,35 @@ def test_score_matches_reference_golden(eng, fixture):
         assert res['value'] == cand[int(rec['best_idx'])]
 
 
+def test_quantized_absolute_branch_is_reference_cancellation(eng):
+    """How many quantized lpdfs pass only through the absolute branch of the
+    bar (|exp(got) - exp(ref)| <= 1e-13), and why: every such case is a
+    probability the reference itself computes with cancellation -- its
+    linear-space sum of CDF differences is below 1e-4, where the
+    reference's own ~K ulp(1) rounding is already more than 1e-9 of it."""
+    n_q = n_abs = 0
+    worst = 0.0
+    for fx in ('labels_small.npz', 'labels_medium.npz'):
+        for meta, rec in golden_io.cases(fx):
+            if not is_quantized(meta):
+                continue
+            d, w, m, s = desc_from_case(meta, rec)
+            eng.set_posterior(d, w, m, s)
+            lb, la, _ = eng.score(0, rec['samples'])
+            for got, ref in ((lb, rec['lpdf_below']), (la, rec['lpdf_above'])):
+                a = assert_lpdf_close(got, ref, quantized=True)
+                n_q += a.size
+                n_abs += int(a.sum())
+                if a.any():
+                    p_ref = np.exp(ref[a])
+                    assert np.all(p_ref < 1e-4), p_ref.max()
+                    worst = max(worst, float(np.max(np.abs(got[a] - ref[a]))))
+    print('quantized lpdfs: %d checked, %d pass only through the absolute branch '
+          '(all with reference probability < 1e-4; worst log difference %.3g)'
+          % (n_q, n_abs, worst))
+    assert n_abs <= 0.01 * n_q
+
+
 def test_reference_op_entry_points(eng):
     """tpe_gmm1_lpdf / tpe_lgmm1_lpdf on the reference's edge inputs (far
     tails, quantized cancellation to -inf, x=0 for LGMM1 -> NaN)."""
