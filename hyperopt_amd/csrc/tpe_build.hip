@@ -1342,8 +1342,11 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
         cat.insert(cat.end(), grp[m].begin(), grp[m].end());
         P.h_group[m] = grp[m];
     }
-    HIPCHK(ctx, P.groups.reserve(std::max<size_t>(cat.size(), 1)));
-    HIPCHK(ctx, hipMemcpy(P.groups.p, cat.data(), cat.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    if (cat != P.groups_h || !P.groups.p) {   // unchanged between rebuilds of one history
+        HIPCHK(ctx, P.groups.reserve(std::max<size_t>(cat.size(), 1)));
+        HIPCHK(ctx, hipMemcpy(P.groups.p, cat.data(), cat.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+        P.groups_h = cat;
+    }
     P.h_labels = dl;
     P.n_labels = n_labels;
     B.n_labels = n_labels;

@@ -66,6 +66,7 @@ struct Posterior {
     DevBuf<Comp<float>> comps32;
     DevBuf<SampRec> samp;
     DevBuf<int32_t> groups;              // concatenated h_group
+    std::vector<int32_t> groups_h;       // host copy of what `groups` holds
     int32_t group_off[kNumModes] = {};
     void release() {
         labels.release();
@@ -73,6 +74,7 @@ struct Posterior {
         comps32.release();
         samp.release();
         groups.release();
+        groups_h.clear();
         n_labels = 0;
     }
 };

@@ -2010,6 +2010,7 @@ int set_posterior_impl(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_lab
     HIPCHK(ctx, hipMemcpy(ctx->P->comps32.p, c32.data(), c32.size() * sizeof(Comp<float>), hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->P->samp.p, sr.data(), sr.size() * sizeof(SampRec), hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->P->groups.p, cat.data(), cat.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    ctx->P->groups_h = cat;
     ctx->P->h_labels = dl;
     ctx->P->n_labels = n_labels;
     return TPE_OK;

@@ -199,12 +199,7 @@ class HistoryCache(object):
         tids = self._tid_arr
         if n > 1 and not np.all(tids[1:] > tids[:-1]):
             return None
-        raw = raw_losses(domain, docs)
-        if None not in raw:
-            losses = np.fromiter(raw, dtype=np.float64, count=n)
-        else:
-            losses = np.array([float('inf') if v is None else float(v) for v in raw],
-                              dtype=np.float64)
+        losses = loss_array(domain, docs)
         n_valid = int(np.count_nonzero(losses == losses))
         cols = {k: self.cols[k].arrays() for k in self.labels}
         return tids, losses, n_valid, cols, self
@@ -221,6 +216,26 @@ def raw_losses(domain, docs):
         except TypeError:                      # a result that is not a dict
             return [d['result'].get('loss') for d in docs]
     return [domain.loss(d['result'], d['spec']) for d in docs]
+
+
+def loss_array(domain, docs):
+    """float64 losses of the docs, None -> +inf (tpe.py:844-847): straight
+    from the result dicts into the array when every doc has a loss (the
+    steady state of fmin's serial loop), else through raw_losses.  (np.fromiter
+    turns None into NaN, which would drop a pending trial instead of giving
+    it +inf: any NaN sends the docs through the exact path.)"""
+    if type(domain).loss is _plain_loss:
+        try:
+            out = np.fromiter(map(dict.get, map(_result_of, docs), repeat('loss')),
+                              dtype=np.float64, count=len(docs))
+            if not np.isnan(out).any():
+                return out
+        except TypeError:                      # a non-dict result
+            pass
+    raw = raw_losses(domain, docs)
+    if None not in raw:
+        return np.fromiter(raw, dtype=np.float64, count=len(docs))
+    return np.array([float('inf') if v is None else float(v) for v in raw], dtype=np.float64)
 
 
 _result_of = itemgetter('result')

@@ -155,6 +155,18 @@ def active_labels(expr, values):
     return active
 
 
+def always_active(expr):
+    """True when no switch (hp.choice / pchoice) has a hyperparameter under
+    any of its options: every label then takes part in every evaluation and
+    active_labels need not walk the graph."""
+    for n in walk(as_apply(expr)):
+        if n.name == 'switch':
+            for opt in n.pos_args[1:]:
+                if any(m.name == 'hyperopt_param' for m in walk(opt)):
+                    return False
+    return True
+
+
 def coerce(kind, v):
     """Python type of a hyperparameter value in trial docs."""
     if kind in ('randint', 'categorical'):

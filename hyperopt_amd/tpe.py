@@ -102,7 +102,14 @@ def device_inputs(specs, tids, losses, obs):
 
 
 def _doc(new_id, domain, trials, specs, values):
-    active = _labels.active_labels(domain.expr, values)
+    flat = getattr(domain, '_hyperopt_amd_flat', None)
+    if flat is None:
+        flat = _labels.always_active(domain.expr)
+        try:
+            domain._hyperopt_amd_flat = flat
+        except AttributeError:
+            pass
+    active = specs if flat else _labels.active_labels(domain.expr, values)
     idxs = {k: ([new_id] if k in active else []) for k in specs}
     vals = {k: ([values[k]] if k in active else []) for k in specs}
     misc = dict(tid=new_id, cmd=domain.cmd, workdir=domain.workdir)

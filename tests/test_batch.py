@@ -136,3 +136,17 @@ def test_uploader_tracks_owner_and_generation():
         del C
         gc.collect()
     ref_eng.close()
+
+
+def test_loss_array_pending_is_inf_and_nan_kept():
+    """The fast loss read (history.loss_array): None -> +inf (a pending or
+    failed trial joins the above set, tpe.py:844-847), NaN stays NaN (the doc
+    is dropped), non-dict results go through domain.loss."""
+    from hyperopt_amd import history
+    dom = H.Domain(_loss, SPACE)
+    docs = [{'result': {'loss': 1.5}}, {'result': {'status': 'new'}},
+            {'result': {'loss': float('nan')}}, {'result': {'loss': 2}}]
+    out = history.loss_array(dom, docs)
+    assert out[0] == 1.5 and out[1] == np.inf and np.isnan(out[2]) and out[3] == 2.0
+    ok = [{'result': {'loss': 0.25}}, {'result': {'loss': -1.0}}]
+    assert list(history.loss_array(dom, ok)) == [0.25, -1.0]
