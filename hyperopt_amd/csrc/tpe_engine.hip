@@ -672,7 +672,7 @@ __global__ __launch_bounds__(kBlock) void k_pick_packed(
     __shared__ uint64_t lo_key[NS];
     __shared__ uint64_t hi_key[NS];
     __shared__ uint64_t round_lb[NS];
-    __shared__ int32_t round_cnt[NS], round_first[NS];
+    __shared__ int16_t round_cnt[NS], round_first[NS];   // <= R * 256 slots per workgroup
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         int64_t z, ci;
@@ -707,21 +707,21 @@ __global__ __launch_bounds__(kBlock) void k_pick_packed(
         round_cnt[t] = k;
     }
     __syncthreads();
+    __shared__ int base;
     if (threadIdx.x == 0) {
         int tot = 0;
         for (int t = 0; t < S.rpb; ++t) {
-            round_first[t] = tot;
+            round_first[t] = (int16_t)tot;
             tot += round_cnt[t];
         }
-        const int base = tot ? atomicAdd(cnt + by, tot) : 0;
-        for (int t = 0; t < S.rpb; ++t) round_first[t] += base;
+        base = tot ? atomicAdd(cnt + by, tot) : 0;
     }
     __syncthreads();
     for (int t = threadIdx.x; t < S.rpb; t += kBlock) {
         const int64_t z = (int64_t)bx * S.rpb + t;
         if (z >= S.n_rounds) continue;
         const uint64_t m = round_lb[t];
-        int at = round_first[t];
+        int at = base + round_first[t];
         rsel[(size_t)z * nl + by] = RoundSel{at, round_cnt[t]};
         for (int c = 0; c < S.cpack; ++c) {
             const uint64_t h = hi_key[t * S.cpack + c];
@@ -1393,16 +1393,21 @@ void launch_round(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
 constexpr int64_t kChunkTargetWG = 8192;
 
 constexpr int32_t kMinChunk = 2048;
+constexpr int32_t kMaxChunk = 16384;
 
 int dense_chunks(const tpe_ctx* ctx, uint32_t gx, int nl) {
     if (ctx->chunks_forced) return ctx->chunks_forced;
     int32_t na_max = 0;
     for (int m : {DENSE_GMM, DENSE_LGMM})
         for (int li : ctx->P->h_group[m]) na_max = std::max(na_max, ctx->P->h_labels[li].na);
+    // never longer than kMaxChunk components: the screened map's fp64
+    // re-score repeats these chunks, and ~1 candidate per (round, label)
+    // over an unchunked 50k-component mixture left it 2 waves per SIMD
+    const int min_nch = (int)((na_max + kMaxChunk - 1) / kMaxChunk);
     const int64_t wg = (int64_t)gx * nl;
-    if (wg >= kChunkTargetWG / 2) return 1;
+    if (wg >= kChunkTargetWG / 2) return std::max(1, min_nch);
     const int64_t want = (kChunkTargetWG + wg - 1) / wg;
-    return (int)std::max<int64_t>(1, std::min<int64_t>(want, na_max / kMinChunk));
+    return (int)std::max<int64_t>(std::max(1, min_nch), std::min<int64_t>(want, na_max / kMinChunk));
 }
 
 // Packed-map sampled rounds of the dense labels, screened (see
@@ -1413,7 +1418,12 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
     for (int m : {DENSE_GMM, DENSE_LGMM})
         for (int li : ctx->P->h_group[m]) na_max = std::max(na_max, ctx->P->h_labels[li].na);
     const int32_t chunk = (na_max + nch - 1) / nch;
-    const size_t planes = (size_t)nl * (nch + 2) * a.gx * (kR * kBlock);
+    // the fp32 pass and the pick use their own, wider slot map: kScreenR
+    // candidates per thread (whole rounds per workgroup, as the packed map);
+    // the chunks stay those of the fp64 packed map, which the re-score repeats
+    Slots S8{(int32_t)a.n, (int32_t)((kScreenR * kBlock) / a.n), a.n_rounds};
+    const uint32_t gx8 = (uint32_t)((a.n_rounds + S8.rpb - 1) / S8.rpb);
+    const size_t planes = (size_t)nl * (nch + 2) * gx8 * (kScreenR * kBlock);
     const int64_t cap = (int64_t)a.n_rounds * a.n;   // candidate slots per label
     HIPCHK(ctx, ctx->chunk_part.reserve(planes));
     HIPCHK(ctx, ctx->scr_list.reserve((size_t)nl * cap));
@@ -1422,20 +1432,14 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
     HIPCHK(ctx, hipMemsetAsync(ctx->scr_cnt.p, 0, nl * sizeof(int32_t), ctx->stream));
     RoundSel* rsel = reinterpret_cast<RoundSel*>(ctx->scr_rsel.p);
     HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
-#define TPE_SCREEN_PACKED(RR)                                                                      \
-    hipLaunchKernelGGL((k_round_chunk<float, RR>), dim3(a.gx, nl, nch), dim3(kBlock), 0, ctx->stream, \
-                       ctx->P->labels.p, grp, ctx->P->comps32.p, ctx->P->samp.p, a.n, a.cand_offset,   \
-                       a.seed, ctx->rounds.p, chunk, ctx->chunk_part.p, ctx->errflag.p, a.S);          \
-    HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));                                          \
-    hipLaunchKernelGGL((k_pick_packed<RR>), dim3(a.gx, nl), dim3(kBlock), 0, ctx->stream,           \
-                       ctx->P->labels.p, grp, a.n, nl, nch, chunk, ctx->chunk_part.p, ctx->scr_cnt.p,  \
-                       ctx->scr_list.p, cap, rsel, a.S)
-    if (narrow(a.S)) {
-        TPE_SCREEN_PACKED(kRGroup);
-    } else {
-        TPE_SCREEN_PACKED(kR);
-    }
-#undef TPE_SCREEN_PACKED
+    hipLaunchKernelGGL((k_round_chunk<float, kScreenR>), dim3(gx8, nl, nch), dim3(kBlock), 0,
+                       ctx->stream, ctx->P->labels.p, grp, ctx->P->comps32.p, ctx->P->samp.p, a.n,
+                       a.cand_offset, a.seed, ctx->rounds.p, chunk, ctx->chunk_part.p, ctx->errflag.p,
+                       S8);
+    HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
+    hipLaunchKernelGGL((k_pick_packed<kScreenR>), dim3(gx8, nl), dim3(kBlock), 0, ctx->stream,
+                       ctx->P->labels.p, grp, a.n, nl, nch, chunk, ctx->chunk_part.p, ctx->scr_cnt.p,
+                       ctx->scr_list.p, cap, rsel, S8);
     ctx->scr_cnt_h.resize(nl);
     HIPCHK(ctx, hipMemcpyAsync(ctx->scr_cnt_h.data(), ctx->scr_cnt.p, nl * sizeof(int32_t),
                                hipMemcpyDeviceToHost, ctx->stream));
