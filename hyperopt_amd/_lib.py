@@ -41,6 +41,7 @@ TPE_OPT_DEDUP = 3
 TPE_OPT_CHUNKS = 4
 TPE_OPT_WHOLE_N = 5
 TPE_OPT_WHOLE_ROUNDS = 6
+TPE_OPT_TIMING = 7
 
 TPE_OBS_IDENTITY = 0
 TPE_OBS_LOG = 1

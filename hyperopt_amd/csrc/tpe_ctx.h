@@ -166,6 +166,7 @@ struct tpe_ctx {
     float score_ms = 0.f, round_ms = 0.f;
     int64_t evals = 0;
     bool dedup = true;                   // quantized grid-value tables
+    bool timing = true;                  // HIP-event timing of rounds (TPE_OPT_TIMING)
 
     // The resident posterior (tpe_set_posterior) and a separate one-label
     // slot for the single-op entry points, so that GMM1_lpdf / GMM1 sampling

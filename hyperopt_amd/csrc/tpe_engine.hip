@@ -1359,7 +1359,7 @@ struct RoundArgs {
 
 void bracket(tpe_ctx* ctx, int mode, int which) {
     ctx->mode_ran[mode] = true;
-    (void)hipEventRecord(ctx->evm[mode][which], ctx->stream);
+    if (ctx->timing) (void)hipEventRecord(ctx->evm[mode][which], ctx->stream);
 }
 
 template <typename T, int MODE, bool SAMPLE>
@@ -1431,12 +1431,12 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
     HIPCHK(ctx, ctx->scr_cnt.reserve(nl));
     HIPCHK(ctx, hipMemsetAsync(ctx->scr_cnt.p, 0, nl * sizeof(int32_t), ctx->stream));
     RoundSel* rsel = reinterpret_cast<RoundSel*>(ctx->scr_rsel.p);
-    HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
+    if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
     hipLaunchKernelGGL((k_round_chunk<float, kScreenR>), dim3(gx8, nl, nch), dim3(kBlock), 0,
                        ctx->stream, ctx->P->labels.p, grp, ctx->P->comps32.p, ctx->P->samp.p, a.n,
                        a.cand_offset, a.seed, ctx->rounds.p, chunk, ctx->chunk_part.p, ctx->errflag.p,
                        S8);
-    HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
+    if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
     hipLaunchKernelGGL((k_pick_packed<kScreenR>), dim3(gx8, nl), dim3(kBlock), 0, ctx->stream,
                        ctx->P->labels.p, grp, a.n, nl, nch, chunk, ctx->chunk_part.p, ctx->scr_cnt.p,
                        ctx->scr_list.p, cap, rsel, S8);
@@ -1501,13 +1501,13 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
         HIPCHK(ctx, ctx->scr_cnt.reserve(cells));
         HIPCHK(ctx, hipMemsetAsync(ctx->scr_lb.p, 0, cells * sizeof(unsigned long long), ctx->stream));
         HIPCHK(ctx, hipMemsetAsync(ctx->scr_cnt.p, 0, cells * sizeof(int32_t), ctx->stream));
-        HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
+        if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
         const unsigned sgx = (unsigned)((a.n + kScreenR * kBlock - 1) / (kScreenR * kBlock));
         hipLaunchKernelGGL((k_screen<kScreenR, true>), dim3(sgx, nl, a.gz), dim3(kBlock), 0, ctx->stream,
                            ctx->P->labels.p, grp, ctx->P->comps32.p, ctx->P->samp.p, a.n,
                            a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->scr_hi.p, ctx->scr_lb.p,
                            ctx->errflag.p, a.S, nullptr, nullptr, nullptr);
-        HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
+        if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
         const unsigned sx = (unsigned)std::min<int64_t>((a.n + 8 * kBlock - 1) / (8 * kBlock), 1024);
         hipLaunchKernelGGL(k_select, dim3(sx, nl, a.gz), dim3(kBlock), 0, ctx->stream, ctx->scr_hi.p,
                            a.n, nl, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p);
@@ -1780,7 +1780,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     ctx->screen_pending = false;
     const bool sample = cand_in_dev == nullptr;
     int64_t evals_q[2] = {0, 0};
-    HIPCHK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+    if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
     // split-K for small sampled rounds (packed map, one tile per label)
     const bool splitk = sample && ctx->splitk && n > 0 && S.cpack != 0 &&
                         a.total_slots <= kSplitKMaxSlots;
@@ -1823,7 +1823,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         launch_round<double, CAT, false>(ctx, g, a);
     }
     HIPCHK(ctx, hipGetLastError());
-    HIPCHK(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+    if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->ev1, ctx->stream));
     if (tiles == 1) {
         const int64_t nr = (int64_t)n_rounds * L;
         hipLaunchKernelGGL(k_emit, dim3((unsigned)((nr + kBlock - 1) / kBlock)), dim3(kBlock), 0,
@@ -1834,7 +1834,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
                            ctx->partials.p, tiles, L, ctx->results.p);
         HIPCHK(ctx, hipGetLastError());
     }
-    HIPCHK(ctx, hipEventRecord(ctx->ev2, ctx->stream));
+    if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->ev2, ctx->stream));
     int32_t errh = 0;
     HIPCHK(ctx, hipMemcpyAsync(&errh, ctx->errflag.p, sizeof(int32_t), hipMemcpyDeviceToHost,
                                ctx->stream));
@@ -1852,13 +1852,18 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
             fprintf(stderr, "\n");
         }
         ctx->screen_pending = false;
-        HIPCHK(ctx, hipEventElapsedTime(&ctx->screen_ms, ctx->evs[0], ctx->evs[1]));
+        if (ctx->timing) HIPCHK(ctx, hipEventElapsedTime(&ctx->screen_ms, ctx->evs[0], ctx->evs[1]));
     }
-    HIPCHK(ctx, hipEventElapsedTime(&ctx->score_ms, ctx->ev0, ctx->ev1));
-    HIPCHK(ctx, hipEventElapsedTime(&ctx->round_ms, ctx->ev0, ctx->ev2));
+    if (ctx->timing) {
+        HIPCHK(ctx, hipEventElapsedTime(&ctx->score_ms, ctx->ev0, ctx->ev1));
+        HIPCHK(ctx, hipEventElapsedTime(&ctx->round_ms, ctx->ev0, ctx->ev2));
+    } else {
+        ctx->score_ms = ctx->round_ms = 0.f;
+    }
     for (int m = 0; m < kNumModes; ++m)
         if (ctx->mode_ran[m])
-            HIPCHK(ctx, hipEventElapsedTime(&ctx->mode_ms[m], ctx->evm[m][0], ctx->evm[m][1]));
+            if (ctx->timing)
+                HIPCHK(ctx, hipEventElapsedTime(&ctx->mode_ms[m], ctx->evm[m][0], ctx->evm[m][1]));
     int64_t evals = 0;
     for (int32_t l = 0; l < L; ++l) {
         if (only_label >= 0 && l != only_label) continue;
@@ -2278,6 +2283,7 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
             if (value < 0 || value > 4096) return ctx->fail(TPE_ERR_ARG, "chunks must be in [0, 4096]");
             ctx->chunks_forced = (int32_t)value;
             break;
+        case TPE_OPT_TIMING: ctx->timing = value != 0; break;
         case TPE_OPT_WHOLE_N:
             if (value < 0) return ctx->fail(TPE_ERR_ARG, "whole candidate count must be >= 0");
             ctx->opt_whole_n = value;

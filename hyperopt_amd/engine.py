@@ -239,13 +239,13 @@ class Engine(object):
 
     OPTIONS = {'screen': L.TPE_OPT_SCREEN, 'splitk': L.TPE_OPT_SPLITK, 'dedup': L.TPE_OPT_DEDUP,
                'chunks': L.TPE_OPT_CHUNKS, 'whole_n': L.TPE_OPT_WHOLE_N,
-               'whole_rounds': L.TPE_OPT_WHOLE_ROUNDS}
+               'whole_rounds': L.TPE_OPT_WHOLE_ROUNDS, 'timing': L.TPE_OPT_TIMING}
 
     def set_option(self, name, value):
         """Engine switches (include/hyperopt_tpe.h TPE_OPT_*): 'screen',
-        'splitk', 'dedup' (bool), 'chunks' (int, 0 = auto), 'whole_n' /
-        'whole_rounds' (the whole problem when this engine runs one shard of
-        it, 0 = the call's own)."""
+        'splitk', 'dedup', 'timing' (bool), 'chunks' (int, 0 = auto),
+        'whole_n' / 'whole_rounds' (the whole problem when this engine runs
+        one shard of it, 0 = the call's own)."""
         self._check(self.lib.tpe_set_option(self.h, self.OPTIONS[name], int(value)))
 
     def screen_probe(self, label, cand):
@@ -369,5 +369,7 @@ def get_engine(device=0, precision='f64'):
         cache = _tls.engines = {}
     key = (_devices(device), precision)
     if key not in cache:
-        cache[key] = Engine(device, precision)
+        eng = Engine(device, precision)
+        eng.set_option('timing', 0)          # tpe.suggest reads no device timings
+        cache[key] = eng
     return cache[key]

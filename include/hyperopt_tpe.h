@@ -313,6 +313,9 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *   TPE_OPT_SPLITK  split-K map for small sampled rounds                [1]
  *   TPE_OPT_DEDUP   quantized labels scored once per grid value         [1]
  *   TPE_OPT_CHUNKS  chunks of the packed map's above mixtures (0 auto)  [0]
+ *   TPE_OPT_TIMING  HIP-event timing of every round (tpe_last_timing,
+ *                   tpe_last_mode_stats, tpe_last_screen's ms); off saves
+ *                   ~20 event calls per round on latency-bound calls   [1]
  *   TPE_OPT_WHOLE_N, TPE_OPT_WHOLE_ROUNDS  the whole problem's candidates
  *                   per round / rounds when this context computes one shard
  *                   of it (one process per GPU); map choices that change a
@@ -326,6 +329,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_CHUNKS 4
 #define TPE_OPT_WHOLE_N 5
 #define TPE_OPT_WHOLE_ROUNDS 6
+#define TPE_OPT_TIMING 7
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
 
 #ifdef __cplusplus

@@ -32,6 +32,7 @@ def main():
     trials = history_trials(hist)
     domain = Domain(lambda d: 0.0, hp_space(hist.labels))
     eng = E.get_engine(0, 'f64')
+    eng.set_option('timing', 1)       # this tool reads the device timings
     for builder in ('host', 'device'):
         st = {k: [] for k in ('gather', 'posterior', 'round', 'docs', 'total', 'suggest_call')}
         for r in range(args.reps + 2):
