@@ -20,7 +20,8 @@ ARCH = 'gfx950'
 
 SOURCES = [os.path.join(HERE, 'csrc', 'tpe_engine.hip'),
            os.path.join(HERE, 'csrc', 'tpe_build.hip'),
-           os.path.join(HERE, 'csrc', 'tpe_multi.hip')]
+           os.path.join(HERE, 'csrc', 'tpe_multi.hip'),
+           os.path.join(HERE, 'csrc', 'tpe_window.hip')]
 DEPS = SOURCES + [os.path.join(HERE, 'csrc', 'tpe_device.h'),
                   os.path.join(HERE, 'csrc', 'tpe_ctx.h'),
                   os.path.join(HERE, 'csrc', 'tpe_exp_table.h'),

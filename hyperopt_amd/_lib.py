@@ -42,6 +42,7 @@ TPE_OPT_CHUNKS = 4
 TPE_OPT_WHOLE_N = 5
 TPE_OPT_WHOLE_ROUNDS = 6
 TPE_OPT_TIMING = 7
+TPE_OPT_WINDOW = 8
 
 TPE_OBS_IDENTITY = 0
 TPE_OBS_LOG = 1
@@ -114,6 +115,7 @@ SIGNATURES = {
     'tpe_last_build_ms': (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float)]),
     'tpe_last_screen': (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_float)]),
     'tpe_set_option': (ctypes.c_int, [_P, _I32, _I64]),
+    'tpe_last_screen_terms': (ctypes.c_int, [_P, _P]),
     'tpe_screen_probe': (ctypes.c_int, [_P, _I32, _P, _I64, _P, _P]),
 }
 

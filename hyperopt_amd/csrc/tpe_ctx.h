@@ -68,6 +68,14 @@ struct Posterior {
     DevBuf<int32_t> groups;              // concatenated h_group
     std::vector<int32_t> groups_h;       // host copy of what `groups` holds
     int32_t group_off[kNumModes] = {};
+    // window index of the dense labels' above mixtures (windowed fp32 screen,
+    // tpe_engine.hip k_win_*), built on first use after every posterior change
+    bool win_ready = false;
+    DevBuf<tpe::WinLabel> win;           // per label
+    DevBuf<double> win_p, win_q;         // per component: prefix max of hi / suffix min of lo
+    DevBuf<Comp<float>> win_wide;        // per label at comp_a: wide records, w = index bits
+    DevBuf<int2> win_bins;               // per label: kWinBins windows [k_lo, k_hi)
+    DevBuf<double> win_seg;              // per (label position, segment): max hi, min lo, wide count
     void release() {
         labels.release();
         comps64.release();
@@ -75,6 +83,13 @@ struct Posterior {
         samp.release();
         groups.release();
         groups_h.clear();
+        win.release();
+        win_p.release();
+        win_q.release();
+        win_wide.release();
+        win_bins.release();
+        win_seg.release();
+        win_ready = false;
         n_labels = 0;
     }
 };
@@ -208,6 +223,16 @@ struct tpe_ctx {
     std::vector<tpe_rt::RescoreChunkH> scr_chunks_h;
     int64_t screen_total = 0, screen_rescored = 0;   // last round
     bool screen_pending = false;         // scr_cnt_h awaits the round's final sync
+    // windowed screen (large tile-map rounds): candidates keyed by (round,
+    // label, bin) and stably sorted with their (x' fp32, index) values
+    bool window = true;                  // TPE_OPT_WINDOW
+    DevBuf<uint32_t> win_keys, win_keys2;
+    DevBuf<uint64_t> win_vals, win_vals2;
+    DevBuf<uint8_t> win_tmp;
+    DevBuf<unsigned long long> win_evals;   // (candidate, component) terms the screen summed
+    int64_t screen_exec = 0;             // last round: terms summed by the screen
+    bool screen_exec_pending = false;
+    unsigned long long screen_exec_h = 0;
     hipEvent_t evs[2] = {};              // brackets k_screen alone
     float screen_ms = 0.f;
     tpe_rt::BuildBufs build;             // device posterior builder scratch
@@ -238,6 +263,32 @@ struct tpe_ctx {
         return TPE_ERR_HIP;
     }
 };
+
+namespace tpe_rt {
+// The windowed screen (tpe_window.hip).  win_prepare builds the window index
+// of every dense label of the resident posterior (once per posterior);
+// win_screen keys, sorts and screens rounds [z0, z0 + nz) of the dense
+// group: per candidate its score's upper bound in `hi` at its SORTED
+// position ((z nl + y) n + p), per (round, label) the largest lower bound in
+// lbkey[z nl + y]; *sorted_vals maps the batch's sorted positions
+// ((z - z0) nl + y) n + p back to candidate indices (low 32 bits).  Probe
+// mode (cand_in != nullptr, one label, z0 = 0, nz = 1): the candidates are
+// cand_in and s_out / e_out receive the fp32 score and its bound per index.
+struct WinScreenArgs {
+    const int32_t* grp;
+    int32_t nl;
+    int64_t n, cand_offset;
+    uint64_t seed;
+    int32_t z0, nz;
+    const double* cand_in;
+    float* hi;
+    unsigned long long* lbkey;
+    double *s_out, *e_out;
+};
+int win_prepare(tpe_ctx* ctx);
+int win_screen(tpe_ctx* ctx, const WinScreenArgs& a, const uint64_t** sorted_vals);
+int64_t win_rounds_per_batch(int64_t n, int32_t nl);
+}  // namespace tpe_rt
 
 // per-device implementations of the entry points a multi-device context
 // forwards or shards (tpe_multi.hip exports the public names)

@@ -508,9 +508,14 @@ constexpr float kScreenMinAcc = 0x1.0p-60f;
 // Kc: the longest run of terms one fp32 running sum adds (K, or a chunk's
 // length when the mixture is summed in chunks whose fp32 sums are added in
 // fp64 -- that addition adds nch 2^-53, inside the 2^-41 slack)
+//
+// skip: the relative mass of terms left out of the sum altogether (the
+// windowed screen, below), each exactly < 2^-kWinT, so at most
+// nskip 2^-kWinT / S <= nskip 2^-kWinT 1.01 / S32.
 __device__ __forceinline__ double screen_err(float amax, int K, int Kc, double X, double dx,
-                                             float acc, float l2) {
+                                             float acc, float l2, double skip = 0.0) {
     if (!(acc >= kScreenMinAcc) || !(acc <= 0x1.0p+100f) || !(X <= 1e30)) return __builtin_inf();
+    if (!(skip <= 0.01)) return __builtin_inf();
     constexpr double u = 0x1.0p-24;
     const double T = fmin(125.0, fmax(16.0, (43.0 + log2(2.0 * (double)K) - (double)l2) / 0.9997));
     const double sqT = sqrt(T) * (1.0 + 1e-12);
@@ -520,8 +525,46 @@ __device__ __forceinline__ double screen_err(float amax, int K, int Kc, double X
     if (!(dt <= 0.01)) return __builtin_inf();
     const double rho = 0.7 * dt + 2.5e-7;
     const double gsum = ((double)(Kc / 128) + 28.0) * u * 1.01;
-    const double rel = rho + gsum + 0x1.0p-41;
+    const double rel = rho + gsum + skip + 0x1.0p-41;
     return 1.02 * rel + 0x1.0p-22 * 0.6931471805599453 * (fabs((double)l2) + 1.0);
+}
+
+// ------------------------------------------------------ windowed screen ----
+// Parzen components are narrow (sigma >= prior_sigma / min(100, N + 1),
+// tpe.py:404-477) and sorted by mu, so a candidate's above sum is decided by
+// the components near it: at config 3, 14 % of the (candidate, component)
+// terms are above 2^-64 of the largest.  The windowed screen sorts a round's
+// candidates by a coarse bin of x', and sums each tile of 2048 neighbouring
+// candidates only over the window of components whose term can reach
+// 2^-kWinT for some candidate of the tile, plus the "wide" components
+// (always summed).  Every term left out is exactly < 2^-kWinT (log2 units,
+// relative to the LSE shift), so screen_err's skip covers them; the fp64
+// re-score of the survivors still sums every component.
+constexpr double kWinT = 48.0;
+constexpr int kWinBinBits = 11;
+constexpr int kWinBins = 1 << kWinBinBits;
+
+struct WinLabel {
+    double xlo, inv_bw;   // bin of x': floor((x' - xlo) inv_bw), clamped to [0, kWinBins)
+    int32_t n_wide;       // wide components (listed at the label's comp_a in win_wide)
+    int32_t pad;
+};
+
+__device__ __host__ __forceinline__ int win_bin(const WinLabel& W, double x) {
+    const double f = (x - W.xlo) * W.inv_bw;
+    if (!(f >= 1.0)) return 0;   // also NaN
+    if (!(f < (double)(kWinBins - 1))) return kWinBins - 1;
+    return (int)f;
+}
+
+__device__ __forceinline__ float float_up(double v) {   // smallest float >= v (finite v)
+    float f = (float)v;
+    if ((double)f < v) {
+        uint32_t b = __float_as_uint(f);
+        b = f > 0.0f ? b + 1u : (f < 0.0f ? b - 1u : 1u);
+        f = __uint_as_float(b);
+    }
+    return f;
 }
 
 // |lpdf64 - lpdf| of the fp64 path (tpe_device.h lse_acc<double>): a

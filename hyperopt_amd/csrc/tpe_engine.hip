@@ -427,16 +427,6 @@ __global__ __launch_bounds__(kBlock) void k_finish_chunks(
 //              lpdfs are bit-identical to the unscreened round's.
 // Scores are per (round, label) rows of n candidates; hi and the compacted
 // indices use the label's position in the dense group (blockIdx.y).
-__device__ __forceinline__ float float_up(double v) {   // smallest float >= v (finite v)
-    float f = (float)v;
-    if ((double)f < v) {
-        uint32_t b = __float_as_uint(f);
-        b = f > 0.0f ? b + 1u : (f < 0.0f ? b - 1u : 1u);
-        f = __uint_as_float(b);
-    }
-    return f;
-}
-
 __device__ __forceinline__ uint64_t block_max_key(uint64_t k, uint64_t* __restrict__ sh) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -516,11 +506,15 @@ __global__ __launch_bounds__(kBlock) void k_screen(
 // counts its takers, reserves their places with ONE atomic (a per-wave
 // atomic on the row's counter serialised ~1.3M same-address atomics at
 // config 3: 12.5 ms), then writes them.
+// The windowed screen (tpe_window.hip) leaves hi in sorted order: vmap (the
+// batch of rounds from z0 on) gives each sorted position's candidate index.
 __global__ __launch_bounds__(kBlock) void k_select(const float* __restrict__ hi, int64_t n, int32_t nl,
                                                    const unsigned long long* __restrict__ lbkey,
-                                                   int32_t* __restrict__ cnt, int32_t* __restrict__ idx) {
-    const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
+                                                   int32_t* __restrict__ cnt, int32_t* __restrict__ idx,
+                                                   int32_t z0, const uint64_t* __restrict__ vmap) {
+    const size_t cell = (size_t)(z0 + blockIdx.z) * nl + blockIdx.y;
     const size_t row = cell * (size_t)n;
+    const uint64_t* vrow = vmap ? vmap + ((size_t)blockIdx.z * nl + blockIdx.y) * (size_t)n : nullptr;
     const uint64_t lb = lbkey[cell];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t span = ((n + gridDim.x - 1) / gridDim.x + kBlock - 1) / kBlock * kBlock;
@@ -550,7 +544,9 @@ __global__ __launch_bounds__(kBlock) void k_select(const float* __restrict__ hi,
         const int64_t i = i0 + threadIdx.x;
         const bool take = i < hi_end && order_key((double)hi[row + i]) >= lb;
         const uint64_t m = __ballot(take);
-        if (take) idx[row + at + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)i;
+        if (take)
+            idx[row + at + __popcll(m & ((1ull << lane) - 1ull))] =
+                vrow ? (int32_t)(uint32_t)vrow[i] : (int32_t)i;
         at += (int)__popcll(m);
     }
 }
@@ -1410,6 +1406,18 @@ int dense_chunks(const tpe_ctx* ctx, uint32_t gx, int nl) {
     return (int)std::max<int64_t>(std::max(1, min_nch), std::min<int64_t>(want, na_max / kMinChunk));
 }
 
+// nb + na summed over the dense labels: the terms an unwindowed screen sums
+// per candidate index (one candidate per dense label)
+int64_t dense_terms(const tpe_ctx* ctx) {
+    int64_t t = 0;
+    for (int m : {DENSE_GMM, DENSE_LGMM})
+        for (int li : ctx->P->h_group[m]) t += ctx->P->h_labels[li].nb + ctx->P->h_labels[li].na;
+    return t;
+}
+
+// tile-map rounds with at least this many candidates use the windowed screen
+constexpr int64_t kWinMinN = 8192;
+
 // Packed-map sampled rounds of the dense labels, screened (see
 // k_pick_packed): fp32 chunk sums, per-round selection, fp64 re-score with
 // the chunked map's summation order, per-round pick.
@@ -1477,6 +1485,7 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
                        ctx->stream, grp, nl, a.n_rounds, ctx->P->n_labels, rsel, ctx->scr_res.p,
                        ctx->scr_off.p, ctx->partials.p);
     ctx->screen_total += cells * a.n;
+    ctx->screen_exec += cells * a.n * dense_terms(ctx);
     ctx->screen_pending = true;
     return ctx->hip(hipGetLastError(), "packed screen launch");
 }
@@ -1501,16 +1510,39 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
         HIPCHK(ctx, ctx->scr_cnt.reserve(cells));
         HIPCHK(ctx, hipMemsetAsync(ctx->scr_lb.p, 0, cells * sizeof(unsigned long long), ctx->stream));
         HIPCHK(ctx, hipMemsetAsync(ctx->scr_cnt.p, 0, cells * sizeof(int32_t), ctx->stream));
-        if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
-        const unsigned sgx = (unsigned)((a.n + kScreenR * kBlock - 1) / (kScreenR * kBlock));
-        hipLaunchKernelGGL((k_screen<kScreenR, true>), dim3(sgx, nl, a.gz), dim3(kBlock), 0, ctx->stream,
-                           ctx->P->labels.p, grp, ctx->P->comps32.p, ctx->P->samp.p, a.n,
-                           a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->scr_hi.p, ctx->scr_lb.p,
-                           ctx->errflag.p, a.S, nullptr, nullptr, nullptr);
-        if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
         const unsigned sx = (unsigned)std::min<int64_t>((a.n + 8 * kBlock - 1) / (8 * kBlock), 1024);
-        hipLaunchKernelGGL(k_select, dim3(sx, nl, a.gz), dim3(kBlock), 0, ctx->stream, ctx->scr_hi.p,
-                           a.n, nl, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p);
+        if (ctx->window && a.n >= kWinMinN && a.cand_in == nullptr) {
+            // windowed: key + sort + screen per batch of rounds, select on the
+            // batch's sorted order
+            int rc = tpe_rt::win_prepare(ctx);
+            if (rc) return rc;
+            HIPCHK(ctx, ctx->win_evals.reserve(1));
+            HIPCHK(ctx, hipMemsetAsync(ctx->win_evals.p, 0, sizeof(unsigned long long), ctx->stream));
+            const int32_t zb = (int32_t)tpe_rt::win_rounds_per_batch(a.n, nl);
+            for (int32_t z0 = 0; z0 < a.n_rounds; z0 += zb) {
+                const int32_t nz = std::min(zb, a.n_rounds - z0);
+                const uint64_t* sorted = nullptr;
+                tpe_rt::WinScreenArgs wa{grp, nl, a.n, a.cand_offset, a.seed, z0, nz, nullptr,
+                                         ctx->scr_hi.p, ctx->scr_lb.p, nullptr, nullptr};
+                if ((rc = tpe_rt::win_screen(ctx, wa, &sorted))) return rc;
+                hipLaunchKernelGGL(k_select, dim3(sx, nl, nz), dim3(kBlock), 0, ctx->stream, ctx->scr_hi.p,
+                                   a.n, nl, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p, z0, sorted);
+            }
+            HIPCHK(ctx, hipMemcpyAsync(&ctx->screen_exec_h, ctx->win_evals.p, sizeof(unsigned long long),
+                                       hipMemcpyDeviceToHost, ctx->stream));
+            ctx->screen_exec_pending = true;
+        } else {
+            if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
+            const unsigned sgx = (unsigned)((a.n + kScreenR * kBlock - 1) / (kScreenR * kBlock));
+            hipLaunchKernelGGL((k_screen<kScreenR, true>), dim3(sgx, nl, a.gz), dim3(kBlock), 0, ctx->stream,
+                               ctx->P->labels.p, grp, ctx->P->comps32.p, ctx->P->samp.p, a.n,
+                               a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->scr_hi.p, ctx->scr_lb.p,
+                               ctx->errflag.p, a.S, nullptr, nullptr, nullptr);
+            if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
+            hipLaunchKernelGGL(k_select, dim3(sx, nl, a.gz), dim3(kBlock), 0, ctx->stream, ctx->scr_hi.p,
+                               a.n, nl, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p, 0, nullptr);
+            ctx->screen_exec += (int64_t)a.n_rounds * a.n * dense_terms(ctx);
+        }
         // the dense rows' partial slots start empty; the re-score chunks
         // overwrite theirs (one chunk table per round trip: the counts)
         hipLaunchKernelGGL(k_fill_empty, dim3((unsigned)std::min<int64_t>((a.tiles + kBlock - 1) / kBlock, 64), nl, a.gz),
@@ -1777,7 +1809,9 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     RoundArgs a{n, cand_offset, seed, n_rounds, tiles, cand_in_dev, olb, ola, S, gx, gz,
                 n_whole * rounds_whole, gx_whole};
     ctx->screen_total = ctx->screen_rescored = 0;
+    ctx->screen_exec = 0;
     ctx->screen_pending = false;
+    ctx->screen_exec_pending = false;
     const bool sample = cand_in_dev == nullptr;
     int64_t evals_q[2] = {0, 0};
     if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->ev0, ctx->stream));
@@ -1844,6 +1878,10 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
                                    hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     ctx->screen_ms = 0.f;
+    if (ctx->screen_exec_pending) {
+        ctx->screen_exec += (int64_t)ctx->screen_exec_h;
+        ctx->screen_exec_pending = false;
+    }
     if (ctx->screen_pending) {
         for (int32_t c : ctx->scr_cnt_h) ctx->screen_rescored += c;
         if (getenv("TPE_SCREEN_DEBUG")) {
@@ -2021,6 +2059,7 @@ int set_posterior_impl(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_lab
     HIPCHK(ctx, hipMemcpy(ctx->P->groups.p, cat.data(), cat.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     ctx->P->groups_h = cat;
     ctx->P->h_labels = dl;
+    ctx->P->win_ready = false;
     ctx->P->n_labels = n_labels;
     return TPE_OK;
 }
@@ -2227,11 +2266,21 @@ int tpe_screen_probe(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n,
     HIPCHK(ctx, ctx->errflag.reserve(1));
     HIPCHK(ctx, hipMemcpyAsync(ctx->one_group.p, &label, sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->cand.p, cand, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
-    const uint32_t tiles = (uint32_t)((n + kTile - 1) / kTile);
-    hipLaunchKernelGGL((k_screen<kR, false>), dim3(tiles, 1, 1), dim3(kBlock), 0, ctx->stream,
-                       ctx->P->labels.p, ctx->one_group.p, ctx->P->comps32.p, ctx->P->samp.p, n, 0,
-                       0, ctx->rounds.p, 1, nullptr, nullptr, ctx->errflag.p, Slots{0, 0, 1},
-                       ctx->cand.p, ctx->out_lb.p, ctx->out_la.p);
+    if (ctx->window && n >= 2048) {   // the windowed screen's tiles of sorted neighbours
+        int rc = tpe_rt::win_prepare(ctx);
+        if (rc) return rc;
+        if (n > ((int64_t)1 << 30)) return ctx->fail(TPE_ERR_ARG, "screen probe: too many candidates");
+        const uint64_t* sorted = nullptr;
+        tpe_rt::WinScreenArgs wa{ctx->one_group.p, 1, n, 0, 0, 0, 1, ctx->cand.p,
+                                 nullptr, nullptr, ctx->out_lb.p, ctx->out_la.p};
+        if ((rc = tpe_rt::win_screen(ctx, wa, &sorted))) return rc;
+    } else {
+        const uint32_t tiles = (uint32_t)((n + kTile - 1) / kTile);
+        hipLaunchKernelGGL((k_screen<kR, false>), dim3(tiles, 1, 1), dim3(kBlock), 0, ctx->stream,
+                           ctx->P->labels.p, ctx->one_group.p, ctx->P->comps32.p, ctx->P->samp.p, n, 0,
+                           0, ctx->rounds.p, 1, nullptr, nullptr, ctx->errflag.p, Slots{0, 0, 1},
+                           ctx->cand.p, ctx->out_lb.p, ctx->out_la.p);
+    }
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipMemcpyAsync(score32, ctx->out_lb.p, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(err_bound, ctx->out_la.p, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
@@ -2273,6 +2322,12 @@ int tpe_last_screen(const tpe_ctx* ctx, int64_t* screened, int64_t* rescored, fl
     return TPE_OK;
 }
 
+int tpe_last_screen_terms(const tpe_ctx* ctx, int64_t* terms) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (terms) *terms = ctx->screen_exec;
+    return TPE_OK;
+}
+
 TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
     if (!ctx) return TPE_ERR_ARG;
     switch (option) {
@@ -2284,6 +2339,7 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
             ctx->chunks_forced = (int32_t)value;
             break;
         case TPE_OPT_TIMING: ctx->timing = value != 0; break;
+        case TPE_OPT_WINDOW: ctx->window = value != 0; break;
         case TPE_OPT_WHOLE_N:
             if (value < 0) return ctx->fail(TPE_ERR_ARG, "whole candidate count must be >= 0");
             ctx->opt_whole_n = value;

@@ -1,0 +1,590 @@
+// tpe_window.hip -- the windowed fp32 screen of large sampled rounds
+// (tpe_device.h, "windowed screen").
+//
+// The plain screen (tpe_engine.hip k_screen) sums every candidate over every
+// component of both mixtures.  But the above mixture's Parzen components are
+// narrow and sorted by mu (adaptive_parzen_normal, tpe.py:404-477: sigma >=
+// prior_sigma / min(100, N + 1)), so only the components near a candidate can
+// move its sum.  Here:
+//
+//   per posterior (k_win_seg, k_win_carry, k_win_bins; once, lazily):
+//     each above component's interval [lo, hi] of recentred x' where its term
+//     can reach 2^-(kWinT + 1) (from its fp32 record; the extra 1 covers the
+//     records' rounding), the prefix max of hi and the suffix min of lo over
+//     the narrow components in record order, the list of wide components
+//     (interval longer than half the label's candidate range, or too far from
+//     the centre for the rounding margin), and for each of kWinBins bins of
+//     the candidate range the window [k_lo, k_hi) of record indices outside
+//     which no narrow component reaches 2^-kWinT anywhere in the bin;
+//
+//   per round (k_win_key, a stable radix sort, k_screen_win):
+//     every candidate keyed by (round, label, bin of x') and sorted with its
+//     (x' fp32, index) value, so a workgroup's 2048 candidates are neighbours;
+//     the tile's window is [k_lo(bin of its min), k_hi(bin of its max)), the
+//     below mixture and the wide components outside the window are summed in
+//     full, and the bound (screen_err) grows by the skipped mass,
+//     nskip 2^-kWinT / S.
+//
+// The selection (k_select) and the fp64 re-score (k_rescore, every
+// component) are the plain screen's, so winners and lpdfs are bit-identical
+// to the fp64 round's; only the set of re-scored candidates can differ.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+
+#include "../../include/hyperopt_tpe.h"
+#include "tpe_ctx.h"
+#include "tpe_device.h"
+
+using namespace tpe;
+using tpe_rt::kBlock;
+
+namespace {
+
+constexpr int kSegR = 8;
+constexpr int kSeg = kSegR * kBlock;     // components per prep workgroup
+constexpr int kKeyR = 4;                 // candidates per thread, k_win_key
+constexpr int kWinR = 8;                 // candidates per thread, k_screen_win (tile 2048)
+constexpr double kInf = __builtin_inf();
+
+// ---------------------------------------------------------- block helpers ----
+struct MaxOp {
+    __device__ double operator()(double a, double b) const { return a > b ? a : b; }
+};
+struct MinOp {
+    __device__ double operator()(double a, double b) const { return a < b ? a : b; }
+};
+struct AddOp {
+    __device__ int operator()(int a, int b) const { return a + b; }
+};
+
+// exclusive prefix (in thread order) of v under op, and the block total;
+// sh: kBlock / 64 entries
+template <typename T, typename Op>
+__device__ T block_prefix(T v, T id, Op op, T* sh, T& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    T inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const T o = __shfl_up(inc, off);
+        if (lane >= off) inc = op(inc, o);
+    }
+    T excl = __shfl_up(inc, 1);
+    if (lane == 0) excl = id;
+    if (lane == 63) sh[wave] = inc;
+    __syncthreads();
+    T before = id, tot = id;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+        if (w < wave) before = op(before, sh[w]);
+        tot = op(tot, sh[w]);
+    }
+    __syncthreads();
+    total = tot;
+    return op(before, excl);
+}
+
+// exclusive suffix (over the threads after this one) of v under op
+template <typename T, typename Op>
+__device__ T block_suffix(T v, T id, Op op, T* sh) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    T inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const T o = __shfl_down(inc, off);
+        if (lane + off < 64) inc = op(inc, o);
+    }
+    T excl = __shfl_down(inc, 1);
+    if (lane == 63) excl = id;
+    if (lane == 0) sh[wave] = inc;
+    __syncthreads();
+    T after = id;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w)
+        if (w > wave) after = op(after, sh[w]);
+    __syncthreads();
+    return op(after, excl);
+}
+
+template <typename T, typename Op>
+__device__ T block_reduce(T v, Op op, T* sh) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = op(v, __shfl_xor(v, off));
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    T r = sh[0];
+#pragma unroll
+    for (int w = 1; w < kBlock / 64; ++w) r = op(r, sh[w]);
+    __syncthreads();
+    return r;
+}
+
+// ------------------------------------------------------------- the index ----
+// The label's candidate range, recentred: [low, high) for a bounded label
+// (sample_raw's acceptance interval), else the below mixture's mu +- 8 sigma
+// hull.  Only the bins' placement depends on it (candidates outside fall in
+// the end bins, whose windows are open-ended).
+__device__ void label_range(const DLabel& L, const SampRec* __restrict__ samp, double& xlo,
+                            double& xhi, double* sh) {
+    double lo = kInf, hi = -kInf;
+    if ((L.flags & 3) == 3) {
+        lo = L.low;
+        hi = L.high;
+    } else {
+        for (int k = threadIdx.x; k < L.ns; k += kBlock) {
+            const SampRec s = samp[L.samp_off + k];
+            lo = fmin(lo, s.mu - 8.0 * s.sigma);
+            hi = fmax(hi, s.mu + 8.0 * s.sigma);
+        }
+        lo = block_reduce(lo, MinOp{}, sh);
+        hi = block_reduce(hi, MaxOp{}, sh);
+    }
+    xlo = lo - L.centre;
+    xhi = hi - L.centre;
+    if (!(fabs(xlo) < 1e300)) xlo = 0.0;
+    if (!(xhi > xlo) || !(fabs(xhi) < 1e300)) xhi = xlo + 1.0;
+}
+
+struct Interval {
+    double lo, hi;
+    bool wide;
+};
+
+// Where component r's term can reach 2^-(kWinT + 1): |x' a - m| <= s with
+// s = sqrt(c + kWinT + 1) (log2 units, c <= 0).  Outside it, the exact term
+// (from the unrounded a, m, c) stays below 2^-kWinT as long as the records'
+// rounding moves z by less than sqrt(c + T + 1) - sqrt(c + T) >= 1 / (2
+// sqrt(T + 1)) ~ 0.07, i.e. (|x' a| + |m|) 2^-23 < 0.07 for every x' near the
+// interval: |m| < 2^17 suffices; records beyond that are always summed.
+// Never-relevant components (c < -(kWinT + 1), also c = -inf) get an empty
+// interval and no wide flag.
+__device__ __forceinline__ Interval comp_interval(const Comp<float>& r, double span) {
+    Interval v{kInf, -kInf, false};
+    const double m = r.mu, a = r.a, cc = (double)r.c + (kWinT + 1.0);
+    if (cc < 0.0) return v;
+    if (!(cc <= 1e30) || !(a > 0.0) || !(a < 1e30) || !(fabs(m) < 131072.0)) {
+        v.wide = true;
+        return v;
+    }
+    const double s = sqrt(cc) * (1.0 + 1e-9);
+    double lo = (m - s) / a, hi = (m + s) / a;
+    lo -= fabs(lo) * 1e-12 + 1e-300;
+    hi += fabs(hi) * 1e-12 + 1e-300;
+    if (hi - lo > 0.5 * span) {
+        v.wide = true;
+        return v;
+    }
+    v.lo = lo;
+    v.hi = hi;
+    return v;
+}
+
+// grid (segments, dense labels): per kSeg components the segment-local
+// prefix max of hi and suffix min of lo (wide and dropped components are
+// neutral), and the segment's max hi, min lo and wide count
+__global__ __launch_bounds__(kBlock) void k_win_seg(const DLabel* __restrict__ labels,
+                                                    const int32_t* __restrict__ grp,
+                                                    const Comp<float>* __restrict__ comps32,
+                                                    const SampRec* __restrict__ samp, int32_t nseg,
+                                                    WinLabel* __restrict__ win, double* __restrict__ P,
+                                                    double* __restrict__ Q, double* __restrict__ seg) {
+    const int y = blockIdx.y, li = grp[y];
+    const DLabel L = labels[li];
+    __shared__ double shd[kBlock / 64];
+    __shared__ int shi[kBlock / 64];
+    double xlo, xhi;
+    label_range(L, samp, xlo, xhi, shd);
+    const int s = blockIdx.x;
+    if (s == 0 && threadIdx.x == 0) win[li] = WinLabel{xlo, (double)kWinBins / (xhi - xlo), 0, 0};
+    double* sg = seg + ((size_t)y * nseg + s) * 3;
+    const int64_t k0 = (int64_t)s * kSeg;
+    if (k0 >= L.na) {
+        if (threadIdx.x == 0) {
+            sg[0] = -kInf;
+            sg[1] = kInf;
+            sg[2] = 0.0;
+        }
+        return;
+    }
+    const Comp<float>* c = comps32 + L.comp_a;
+    double lo[kSegR], hi[kSegR];
+    int nw = 0;
+#pragma unroll
+    for (int j = 0; j < kSegR; ++j) {
+        const int64_t k = k0 + threadIdx.x * kSegR + j;
+        Interval v{kInf, -kInf, false};
+        if (k < L.na) v = comp_interval(c[k], xhi - xlo);
+        lo[j] = v.lo;
+        hi[j] = v.hi;
+        nw += v.wide;
+    }
+    double pm[kSegR], run = -kInf;
+#pragma unroll
+    for (int j = 0; j < kSegR; ++j) {
+        run = hi[j] > run ? hi[j] : run;
+        pm[j] = run;
+    }
+    double tot_hi;
+    const double before = block_prefix(run, -kInf, MaxOp{}, shd, tot_hi);
+    double sm[kSegR];
+    run = kInf;
+#pragma unroll
+    for (int j = kSegR - 1; j >= 0; --j) {
+        run = lo[j] < run ? lo[j] : run;
+        sm[j] = run;
+    }
+    const double after = block_suffix(run, kInf, MinOp{}, shd);
+    const double tot_lo = block_reduce(run, MinOp{}, shd);
+    int tot_w;
+    (void)block_prefix(nw, 0, AddOp{}, shi, tot_w);
+#pragma unroll
+    for (int j = 0; j < kSegR; ++j) {
+        const int64_t k = k0 + threadIdx.x * kSegR + j;
+        if (k < L.na) {
+            P[L.comp_a + k] = pm[j] > before ? pm[j] : before;
+            Q[L.comp_a + k] = sm[j] < after ? sm[j] : after;
+        }
+    }
+    if (threadIdx.x == 0) {
+        sg[0] = tot_hi;
+        sg[1] = tot_lo;
+        sg[2] = (double)tot_w;
+    }
+}
+
+// grid (segments, dense labels): carry the other segments into P and Q, and
+// list the wide components in record order (record .w = index bits)
+__global__ __launch_bounds__(kBlock) void k_win_carry(const DLabel* __restrict__ labels,
+                                                      const int32_t* __restrict__ grp,
+                                                      const Comp<float>* __restrict__ comps32,
+                                                      const SampRec* __restrict__ samp, int32_t nseg,
+                                                      WinLabel* __restrict__ win, double* __restrict__ P,
+                                                      double* __restrict__ Q,
+                                                      const double* __restrict__ seg,
+                                                      Comp<float>* __restrict__ wide) {
+    const int y = blockIdx.y, li = grp[y];
+    const DLabel L = labels[li];
+    __shared__ double shd[kBlock / 64];
+    __shared__ int shi[kBlock / 64];
+    double xlo, xhi;
+    label_range(L, samp, xlo, xhi, shd);
+    const int s = blockIdx.x;
+    const int64_t k0 = (int64_t)s * kSeg;
+    if (k0 >= L.na) return;
+    const int nseg_l = (int)((L.na + kSeg - 1) / kSeg);
+    const double* sg = seg + (size_t)y * nseg * 3;
+    double cp = -kInf, cq = kInf;
+    int woff = 0;
+    for (int t = 0; t < s; ++t) {
+        cp = sg[3 * t] > cp ? sg[3 * t] : cp;
+        woff += (int)sg[3 * t + 2];
+    }
+    for (int t = s + 1; t < nseg_l; ++t) cq = sg[3 * t + 1] < cq ? sg[3 * t + 1] : cq;
+    const Comp<float>* c = comps32 + L.comp_a;
+    bool fl[kSegR];
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < kSegR; ++j) {
+        const int64_t k = k0 + threadIdx.x * kSegR + j;
+        fl[j] = false;
+        if (k < L.na) {
+            const size_t at = L.comp_a + k;
+            P[at] = P[at] > cp ? P[at] : cp;
+            Q[at] = Q[at] < cq ? Q[at] : cq;
+            fl[j] = comp_interval(c[k], xhi - xlo).wide;
+        }
+        cnt += fl[j];
+    }
+    int tot;
+    int at = woff + block_prefix(cnt, 0, AddOp{}, shi, tot);
+#pragma unroll
+    for (int j = 0; j < kSegR; ++j)
+        if (fl[j]) {
+            const int k = (int)(k0 + threadIdx.x * kSegR + j);
+            Comp<float> r = c[k];
+            r.w = __int_as_float(k);
+            wide[L.comp_a + at++] = r;
+        }
+    if (s == nseg_l - 1 && threadIdx.x == 0) win[li].n_wide = woff + tot;
+}
+
+// grid (kWinBins / kBlock, dense labels): per bin the window [k_lo, k_hi):
+// components before k_lo have hi < the bin's lower edge (P[k] < edge), those
+// from k_hi on have lo > its upper edge (Q[k] > edge)
+__global__ __launch_bounds__(kBlock) void k_win_bins(const DLabel* __restrict__ labels,
+                                                     const int32_t* __restrict__ grp,
+                                                     const WinLabel* __restrict__ win,
+                                                     const double* __restrict__ P,
+                                                     const double* __restrict__ Q,
+                                                     int2* __restrict__ bins) {
+    const int li = grp[blockIdx.y];
+    const DLabel L = labels[li];
+    const WinLabel W = win[li];
+    const int b = blockIdx.x * kBlock + threadIdx.x;
+    if (b >= kWinBins) return;
+    const double bw = 1.0 / W.inv_bw;
+    double elo = b == 0 ? -kInf : W.xlo + b * bw;
+    double ehi = b == kWinBins - 1 ? kInf : W.xlo + (b + 1) * bw;
+    const double slack = (fabs(W.xlo) + bw * kWinBins) * 1e-12;
+    elo -= slack;
+    ehi += slack;
+    const double* p = P + L.comp_a;
+    const double* q = Q + L.comp_a;
+    int lo = 0, hi = L.na;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (p[mid] >= elo) hi = mid; else lo = mid + 1;
+    }
+    const int klo = lo;
+    lo = 0;
+    hi = L.na;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (q[mid] > ehi) hi = mid; else lo = mid + 1;
+    }
+    bins[(size_t)li * kWinBins + b] = int2{klo, lo > klo ? lo : klo};
+}
+
+// ------------------------------------------------------------- per round ----
+// grid (ceil(n / 1024), labels, rounds of the batch): key (round, label, bin)
+// and value (x' fp32 bits << 32 | candidate index) of every candidate, at
+// position ((z - z0) nl + y) n + i.  The candidates are drawn exactly as the
+// plain screen and the fp64 round draw them.
+template <bool SAMPLE>
+__global__ __launch_bounds__(kBlock) void k_win_key(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ grp,
+    const SampRec* __restrict__ samp, const WinLabel* __restrict__ win,
+    const double* __restrict__ cand_in, int64_t n, int64_t cand_offset, uint64_t seed,
+    const uint32_t* __restrict__ rounds, int32_t z0, int32_t nl, uint32_t* __restrict__ keys,
+    uint64_t* __restrict__ vals, int32_t* __restrict__ err) {
+    const int y = blockIdx.y, li = grp[y];
+    const DLabel L = labels[li];
+    const WinLabel W = win[li];
+    const bool lgmm = L.mode == DENSE_LGMM;
+    const uint32_t cell = blockIdx.z * (uint32_t)nl + y;
+#pragma unroll
+    for (int r = 0; r < kKeyR; ++r) {
+        const int64_t i = (int64_t)blockIdx.x * (kKeyR * kBlock) + r * kBlock + threadIdx.x;
+        if (i >= n) continue;
+        double v;
+        if constexpr (SAMPLE) {
+            const uint32_t g = (uint32_t)(cand_offset + i), rk = rounds[z0 + blockIdx.z];
+            const bool ok = lgmm ? sample_below<DENSE_LGMM>(L, samp + L.samp_off, seed, rk, g, v)
+                                 : sample_below<DENSE_GMM>(L, samp + L.samp_off, seed, rk, g, v);
+            if (!ok) atomicOr(err, 1);
+        } else {
+            v = cand_in[i];
+        }
+        const double xr = (lgmm ? log(v) : v) - L.centre;
+        const size_t pos = (size_t)cell * n + i;
+        keys[pos] = (cell << kWinBinBits) | (uint32_t)win_bin(W, xr);
+        vals[pos] = ((uint64_t)__float_as_uint((float)xr) << 32) | (uint32_t)i;
+    }
+}
+
+// grid (ceil(n / 2048), labels, rounds of the batch): one tile of 2048
+// sorted neighbours; see the file comment.  PROBE: per candidate index the
+// fp32 score and its bound (tests).
+template <bool PROBE>
+__global__ __launch_bounds__(kBlock) void k_screen_win(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ grp,
+    const Comp<float>* __restrict__ comps32, const WinLabel* __restrict__ win,
+    const int2* __restrict__ bins, const Comp<float>* __restrict__ wide,
+    const uint64_t* __restrict__ vals, int64_t n, int32_t z0, int32_t nl, float* __restrict__ hi_out,
+    unsigned long long* __restrict__ lbkey, unsigned long long* __restrict__ terms,
+    double* __restrict__ s_out, double* __restrict__ e_out) {
+    constexpr int R = kWinR;
+    const int y = blockIdx.y, li = grp[y];
+    const DLabel L = labels[li];
+    const WinLabel W = win[li];
+    const size_t bcell = (size_t)blockIdx.z * nl + y;
+    const size_t gcell = (size_t)(z0 + blockIdx.z) * nl + y;
+    const uint64_t* vrow = vals + bcell * n;
+    const int64_t t0 = (int64_t)blockIdx.x * (R * kBlock);
+    float xf[R];
+    uint32_t ci[R];
+    bool valid[R];
+    double mn = kInf, mx = -kInf;
+    int nv = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int64_t p = t0 + r * kBlock + threadIdx.x;
+        valid[r] = p < n;
+        const uint64_t v = valid[r] ? vrow[p] : 0ull;
+        xf[r] = __uint_as_float((uint32_t)(v >> 32));
+        ci[r] = (uint32_t)v;
+        if (valid[r]) {
+            mn = fmin(mn, (double)xf[r]);
+            mx = fmax(mx, (double)xf[r]);
+            ++nv;
+        } else {
+            xf[r] = 0.0f;
+        }
+    }
+    __shared__ double shd[kBlock / 64];
+    __shared__ int shi[kBlock / 64];
+    mn = block_reduce(mn, MinOp{}, shd);
+    mx = block_reduce(mx, MaxOp{}, shd);
+    int nvt;
+    (void)block_prefix(nv, 0, AddOp{}, shi, nvt);
+    // the true x' lies within 2^-24 |x'f| of the stored fp32 value
+    const int b1 = win_bin(W, mn - fabs(mn) * 0x1.0p-23 - 0x1.0p-149);
+    const int b2 = win_bin(W, mx + fabs(mx) * 0x1.0p-23 + 0x1.0p-149);
+    const int2 w1 = bins[(size_t)li * kWinBins + b1], w2 = bins[(size_t)li * kWinBins + b2];
+    const int klo = __builtin_amdgcn_readfirstlane(w1.x);
+    const int khi = __builtin_amdgcn_readfirstlane(w2.y > w1.x ? w2.y : w1.x);
+    float ab[R], aa[R];
+    lse_acc<R>(comps32 + L.comp_b, L.nb, xf, ab);
+    lse_acc<R>(comps32 + L.comp_a + klo, khi - klo, xf, aa);
+    // the wide components outside the window, one by one
+    float aw[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) aw[r] = 0.0f;
+    int nout = 0;
+    const Comp<float>* wl = wide + L.comp_a;
+    for (int j = 0; j < W.n_wide; ++j) {
+        const Comp<float> rec = wl[j];
+        const int k = __float_as_int(rec.w);
+        if (k >= klo && k < khi) continue;
+        ++nout;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const float z = fmaf(xf[r], rec.a, -rec.mu);
+            aw[r] += __builtin_amdgcn_exp2f(fmaf(-z, z, rec.c));
+        }
+    }
+    const int nwin = khi - klo;
+    const int nskip = L.na - nwin - nout;
+    // summation error: the window's run (nwin / 128 + 28) u, the wide run
+    // nout u, one more addition
+    const int Kc = nwin + 128 * (nout + 1);
+    uint64_t bk = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (!valid[r]) continue;
+        aa[r] += aw[r];
+        const float l2b = __builtin_log2f(ab[r]), l2a = __builtin_log2f(aa[r]);
+        const double lb = (double)l2b * 0.6931471805599453 + L.shift_b;
+        const double la = (double)l2a * 0.6931471805599453 + L.shift_a;
+        const double s = lb - la;
+        const double X = fabs((double)xf[r]) * (1.0 + 0x1.0p-23);
+        const double dx = X * 0x1.0p-24 + 0x1.0p-149;
+        const double skip = nskip > 0 ? (double)nskip * 0x1.0p-48 * 1.01 / (double)aa[r] : 0.0;
+        static_assert(kWinT == 48.0, "skip term uses 2^-48");
+        const double E = 1.25 * (screen_err(L.amax_b, L.nb, L.nb, X, dx, ab[r], l2b) +
+                                 screen_err(L.amax_a, L.na, Kc, X, dx, aa[r], l2a, skip) +
+                                 fp64_err(L.nb + L.na, fabs(lb) + fabs(la) + X + fabs(L.centre)));
+        if constexpr (PROBE) {
+            s_out[ci[r]] = s;
+            e_out[ci[r]] = E;
+            continue;
+        }
+        float h = __builtin_inff();
+        if (E <= 1e30 && s == s) {
+            h = float_up(s + E);
+            const uint64_t key = order_key(s - E);
+            bk = key > bk ? key : bk;
+        }
+        hi_out[gcell * n + t0 + r * kBlock + threadIdx.x] = h;
+    }
+    if (threadIdx.x == 0 && terms)
+        atomicAdd(terms, (unsigned long long)nvt * (unsigned long long)(L.nb + nwin + nout));
+    if constexpr (PROBE) return;
+    __shared__ unsigned long long shk[kBlock / 64];
+    struct KMax {
+        __device__ unsigned long long operator()(unsigned long long a, unsigned long long b) const {
+            return a > b ? a : b;
+        }
+    };
+    const unsigned long long m = block_reduce((unsigned long long)bk, KMax{}, shk);
+    if (threadIdx.x == 0 && m) atomicMax(lbkey + gcell, m);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ host ----
+int64_t tpe_rt::win_rounds_per_batch(int64_t n, int32_t nl) {
+    // the sort takes an int count: batches of at most 2^30 candidates
+    const int64_t per = std::max<int64_t>(1, n * (int64_t)nl);
+    return std::max<int64_t>(1, ((int64_t)1 << 30) / per);
+}
+
+int tpe_rt::win_prepare(tpe_ctx* ctx) {
+    tpe_rt::Posterior& P = *ctx->P;
+    if (P.win_ready) return TPE_OK;
+    const int nl = (int)(P.h_group[DENSE_GMM].size() + P.h_group[DENSE_LGMM].size());
+    if (nl == 0) {
+        P.win_ready = true;
+        return TPE_OK;
+    }
+    int32_t na_max = 1;
+    for (int m : {DENSE_GMM, DENSE_LGMM})
+        for (int li : P.h_group[m]) na_max = std::max(na_max, P.h_labels[li].na);
+    const int nseg = (na_max + kSeg - 1) / kSeg;
+    HIPCHK(ctx, P.win.reserve(P.n_labels));
+    HIPCHK(ctx, P.win_p.reserve(P.comps32.cap));
+    HIPCHK(ctx, P.win_q.reserve(P.comps32.cap));
+    HIPCHK(ctx, P.win_wide.reserve(P.comps32.cap));
+    HIPCHK(ctx, P.win_bins.reserve((size_t)P.n_labels * kWinBins));
+    HIPCHK(ctx, P.win_seg.reserve((size_t)nl * nseg * 3));
+    const int32_t* grp = P.groups.p + P.group_off[DENSE_GMM];
+    hipLaunchKernelGGL(k_win_seg, dim3(nseg, nl), dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
+                       P.comps32.p, P.samp.p, nseg, P.win.p, P.win_p.p, P.win_q.p, P.win_seg.p);
+    hipLaunchKernelGGL(k_win_carry, dim3(nseg, nl), dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
+                       P.comps32.p, P.samp.p, nseg, P.win.p, P.win_p.p, P.win_q.p, P.win_seg.p,
+                       P.win_wide.p);
+    hipLaunchKernelGGL(k_win_bins, dim3(kWinBins / kBlock, nl), dim3(kBlock), 0, ctx->stream,
+                       P.labels.p, grp, P.win.p, P.win_p.p, P.win_q.p, P.win_bins.p);
+    HIPCHK(ctx, hipGetLastError());
+    P.win_ready = true;
+    return TPE_OK;
+}
+
+int tpe_rt::win_screen(tpe_ctx* ctx, const WinScreenArgs& a, const uint64_t** sorted_vals) {
+    tpe_rt::Posterior& P = *ctx->P;
+    const bool probe = a.cand_in != nullptr;
+    const size_t total = (size_t)a.nz * a.nl * a.n;
+    if (total > ((size_t)1 << 30)) return ctx->fail(TPE_ERR_ARG, "windowed screen batch too large");
+    HIPCHK(ctx, ctx->win_keys.reserve(total));
+    HIPCHK(ctx, ctx->win_keys2.reserve(total));
+    HIPCHK(ctx, ctx->win_vals.reserve(total));
+    HIPCHK(ctx, ctx->win_vals2.reserve(total));
+    const dim3 gk((unsigned)((a.n + kKeyR * kBlock - 1) / (kKeyR * kBlock)), a.nl, a.nz);
+    if (probe)
+        hipLaunchKernelGGL(k_win_key<false>, gk, dim3(kBlock), 0, ctx->stream, P.labels.p, a.grp, P.samp.p,
+                           P.win.p, a.cand_in, a.n, a.cand_offset, a.seed, ctx->rounds.p, a.z0, a.nl,
+                           ctx->win_keys.p, ctx->win_vals.p, ctx->errflag.p);
+    else
+        hipLaunchKernelGGL(k_win_key<true>, gk, dim3(kBlock), 0, ctx->stream, P.labels.p, a.grp, P.samp.p,
+                           P.win.p, nullptr, a.n, a.cand_offset, a.seed, ctx->rounds.p, a.z0, a.nl,
+                           ctx->win_keys.p, ctx->win_vals.p, ctx->errflag.p);
+    HIPCHK(ctx, hipGetLastError());
+    int cell_bits = 0;
+    while (((int64_t)1 << cell_bits) < (int64_t)a.nz * a.nl) ++cell_bits;
+    const int end_bit = kWinBinBits + cell_bits;
+    hipcub::DoubleBuffer<uint32_t> kb(ctx->win_keys.p, ctx->win_keys2.p);
+    hipcub::DoubleBuffer<uint64_t> vb(ctx->win_vals.p, ctx->win_vals2.p);
+    size_t bytes = 0;
+    HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kb, vb, (int)total, 0, end_bit,
+                                                     ctx->stream));
+    HIPCHK(ctx, ctx->win_tmp.reserve(std::max<size_t>(bytes, 1)));
+    HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(ctx->win_tmp.p, bytes, kb, vb, (int)total, 0, end_bit,
+                                                     ctx->stream));
+    const uint64_t* sorted = vb.Current();
+    const dim3 gs((unsigned)((a.n + kWinR * kBlock - 1) / (kWinR * kBlock)), a.nl, a.nz);
+    if (ctx->timing && !probe && a.z0 == 0) HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
+    if (probe)
+        hipLaunchKernelGGL(k_screen_win<true>, gs, dim3(kBlock), 0, ctx->stream, P.labels.p, a.grp,
+                           P.comps32.p, P.win.p, P.win_bins.p, P.win_wide.p, sorted, a.n, a.z0, a.nl,
+                           nullptr, nullptr, nullptr, a.s_out, a.e_out);
+    else
+        hipLaunchKernelGGL(k_screen_win<false>, gs, dim3(kBlock), 0, ctx->stream, P.labels.p, a.grp,
+                           P.comps32.p, P.win.p, P.win_bins.p, P.win_wide.p, sorted, a.n, a.z0, a.nl,
+                           a.hi, a.lbkey, ctx->win_evals.p, nullptr, nullptr);
+    if (ctx->timing && !probe) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
+    HIPCHK(ctx, hipGetLastError());
+    *sorted_vals = sorted;
+    return TPE_OK;
+}

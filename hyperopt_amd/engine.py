@@ -237,13 +237,22 @@ class Engine(object):
                                              ctypes.byref(ms)))
         return (a.value, b.value, ms.value) if with_ms else (a.value, b.value)
 
+    def last_screen_terms(self):
+        """(candidate, component) terms the last round's screen summed over
+        both mixtures (the windowed screen skips the components that cannot
+        matter to a tile)."""
+        t = ctypes.c_int64()
+        self._check(self.lib.tpe_last_screen_terms(self.h, ctypes.byref(t)))
+        return t.value
+
     OPTIONS = {'screen': L.TPE_OPT_SCREEN, 'splitk': L.TPE_OPT_SPLITK, 'dedup': L.TPE_OPT_DEDUP,
                'chunks': L.TPE_OPT_CHUNKS, 'whole_n': L.TPE_OPT_WHOLE_N,
-               'whole_rounds': L.TPE_OPT_WHOLE_ROUNDS, 'timing': L.TPE_OPT_TIMING}
+               'whole_rounds': L.TPE_OPT_WHOLE_ROUNDS, 'timing': L.TPE_OPT_TIMING,
+               'window': L.TPE_OPT_WINDOW}
 
     def set_option(self, name, value):
         """Engine switches (include/hyperopt_tpe.h TPE_OPT_*): 'screen',
-        'splitk', 'dedup', 'timing' (bool), 'chunks' (int, 0 = auto),
+        'splitk', 'dedup', 'timing', 'window' (bool), 'chunks' (int, 0 = auto),
         'whole_n' / 'whole_rounds' (the whole problem when this engine runs
         one shard of it, 0 = the call's own)."""
         self._check(self.lib.tpe_set_option(self.h, self.OPTIONS[name], int(value)))

@@ -301,10 +301,18 @@ int tpe_last_mode_stats(const tpe_ctx *ctx, float *ms, int64_t *evals);
 int tpe_last_screen(const tpe_ctx *ctx, int64_t *screened, int64_t *rescored,
                     float *screen_ms);
 
+/* (candidate, component) terms the last round's screen actually summed
+ * (both mixtures).  The windowed screen (TPE_OPT_WINDOW) leaves out the
+ * components that cannot reach 2^-48 of a tile's sums; the plain screen sums
+ * them all (then this is screened x (nb + na)).  Winners are unaffected. */
+int tpe_last_screen_terms(const tpe_ctx *ctx, int64_t *terms);
+
 /* Diagnostic of the screen (tests): for caller-supplied candidates of one
  * dense resident label, the fp32 score lpdf_below - lpdf_above the screen
  * computes and its rigorous error bound (x 1.25, as used by the round):
- * |score32 - score64| <= err_bound for every finite bound. */
+ * |score32 - score64| <= err_bound for every finite bound.  With
+ * TPE_OPT_WINDOW on and n >= 2048 the candidates go through the windowed
+ * screen (sorted into tiles of neighbours, windows of components). */
 int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
                      double *score32, double *err_bound);
 
@@ -313,6 +321,9 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *   TPE_OPT_SPLITK  split-K map for small sampled rounds                [1]
  *   TPE_OPT_DEDUP   quantized labels scored once per grid value         [1]
  *   TPE_OPT_CHUNKS  chunks of the packed map's above mixtures (0 auto)  [0]
+ *   TPE_OPT_WINDOW  windowed screen of large tile rounds: candidates sorted
+ *                   into tiles of neighbours, each summed over the window of
+ *                   components that can matter to it                   [1]
  *   TPE_OPT_TIMING  HIP-event timing of every round (tpe_last_timing,
  *                   tpe_last_mode_stats, tpe_last_screen's ms); off saves
  *                   ~20 event calls per round on latency-bound calls   [1]
@@ -330,6 +341,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_WHOLE_N 5
 #define TPE_OPT_WHOLE_ROUNDS 6
 #define TPE_OPT_TIMING 7
+#define TPE_OPT_WINDOW 8
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
 
 #ifdef __cplusplus

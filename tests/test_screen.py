@@ -28,7 +28,11 @@ def eng():
     e.close()
 
 
-def test_screen_bound_holds(eng):
+@pytest.mark.parametrize('window', [1, 0])
+def test_screen_bound_holds(eng, window):
+    """window=1: the probe goes through the windowed screen (candidates
+    sorted into tiles of neighbours, components outside a tile's window left
+    out and covered by the bound's skip term)."""
     from hyperopt_amd import posterior as P
     from hyperopt_amd.workloads import mixed_history
     hist = mixed_history(32, 10000, seed=0)
@@ -46,7 +50,11 @@ def test_screen_bound_holds(eng):
         else:
             extra = np.exp(np.linspace(p.low, p.high, 2001))
         x = np.concatenate([x, extra])
-        s32, err = eng.screen_probe(li, x)
+        eng.set_option('window', window)
+        try:
+            s32, err = eng.screen_probe(li, x)
+        finally:
+            eng.set_option('window', 1)
         lb, la, _ = eng.score(li, x)
         s64 = lb - la
         ok = np.isfinite(err) & np.isfinite(s64)
@@ -56,8 +64,8 @@ def test_screen_bound_holds(eng):
     # the bound is rigorous, not tight: observed error well inside it
     assert worst < 0.5, worst
     assert min(cert) > 0.9, cert
-    print('screen bound: worst |s32 - s64| / bound = %.3g, certified %.4f..%.4f'
-          % (worst, min(cert), max(cert)))
+    print('screen bound (window %d): worst |s32 - s64| / bound = %.3g, certified %.4f..%.4f'
+          % (window, worst, min(cert), max(cert)))
 
 
 def _suggest_both(eng, C, rnd, seed):
@@ -76,12 +84,18 @@ def _assert_same(a, b):
         assert np.array_equal(a[f], b[f], equal_nan=f != 'index' and f != 'label'), f
 
 
-@pytest.mark.parametrize('config', ['config2', 'config3', 'config3_device', 'config4_device'])
+@pytest.mark.parametrize('config', ['config2', 'config3', 'config3_device', 'config4_device',
+                                    'hartmann_n30'])
 def test_screened_round_is_the_fp64_round(eng, config):
+    """C = 2^20 and 2^16 go through the windowed screen, 3000 and 5000
+    through the plain one; hartmann_n30 (30 trials: wide components, few
+    narrow ones) exercises the wide list."""
     from hyperopt_amd import posterior as P
     from hyperopt_amd.workloads import conditional_history, hartmann_history, mixed_history
     if config == 'config2':
         hist = hartmann_history(2000, seed=0)
+    elif config == 'hartmann_n30':
+        hist = hartmann_history(30, seed=3)
     elif config.startswith('config4'):
         hist = conditional_history(5000, seed=0)
     else:
@@ -143,3 +157,46 @@ def test_screened_packed_rounds_are_the_fp64_rounds(eng, rounds, C, chunks):
     _assert_same(a, b)
     assert screened > 0 and rescored < screened
     print('packed %d x %d (chunks %d): re-scored %.4f' % (rounds, C, chunks, rescored / screened))
+
+
+def test_windowed_screen_skips_terms(eng):
+    """Config 3's posterior, 2^20 candidates: the windowed screen sums a
+    fraction of the terms the plain screen sums, and both give the fp64
+    round's winners bit for bit."""
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.workloads import mixed_history
+    hist = mixed_history(32, 10000, seed=0)
+    eng.build_posterior(*hist.device_inputs(), gamma=0.25, prior_weight=1.0)
+    C = 1 << 20
+    eng.set_option('window', 1)
+    a = eng.suggest(9, C, round=2)
+    terms_w = eng.last_screen_terms()
+    eng.set_option('window', 0)
+    b = eng.suggest(9, C, round=2)
+    terms_p = eng.last_screen_terms()
+    eng.set_option('window', 1)
+    eng.set_option('screen', 0)
+    c = eng.suggest(9, C, round=2)
+    eng.set_option('screen', 1)
+    _assert_same(a, c)
+    _assert_same(b, c)
+    frac = terms_w / terms_p
+    print('windowed screen: %.4f of the plain screen\'s terms' % frac)
+    assert 0 < frac < 0.35
+
+
+def test_windowed_screen_batched_rounds(eng):
+    """Several tile-map rounds in one call (grid.z): keys carry the round,
+    so each round's candidates are sorted and selected on their own."""
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.workloads import mixed_history
+    hist = mixed_history(24, 6000, seed=4)
+    eng.set_posterior(*P.pack(hist.posteriors()))
+    ids = [11, 12, 13]
+    a = eng.suggest_batch(5, ids, 1 << 15)
+    screened, rescored = eng.last_screen()
+    eng.set_option('screen', 0)
+    b = eng.suggest_batch(5, ids, 1 << 15)
+    eng.set_option('screen', 1)
+    _assert_same(a, b)
+    assert 0 < rescored < screened

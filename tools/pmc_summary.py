@@ -7,7 +7,8 @@ rocprofv3 --stats tables), <tag>_bench.json (the bench line), and
 <tag>_pmc_summary.json: per kernel, each PMC counter averaged PER LAUNCH
 (FETCH_SIZE / WRITE_SIZE in KB as rocprofv3 reports them), plus for the dense
 round kernels the VALU instructions per eval (evals per launch from the bench
-line's per_family_evals over the bench's launches of that kernel)."""
+line's per_family_evals over the bench's launches of that kernel; for the
+windowed k_screen_win the terms it summed, screen.screen_terms_per_step)."""
 import csv
 import glob
 import json
@@ -71,13 +72,15 @@ def main(src, tag):
             nlaunch[k] = n[k]
     # evals per launch of each dense family from a 1-step bench line
     pmc_bench = os.path.join(src, 'pmc_valu.log')
-    fam_evals, steps = None, 1
+    fam_evals, steps, win_terms = None, 1, None
     if os.path.exists(pmc_bench):
         for line in open(pmc_bench):
             if line.startswith('{"metric"'):
                 d = json.loads(line)
                 fam_evals = d.get('per_family_evals')
                 steps = d.get('steps', 1) + d.get('warmup', 0)   # every step launches once
+                # the windowed screen's own terms (it skips the negligible pairs)
+                win_terms = d.get('screen', {}).get('screen_terms_per_step')
     for k, v in summary.items():
         v['_launches'] = nlaunch.get(k)
         for pre, fam in FAMILY.items():
@@ -86,6 +89,10 @@ def main(src, tag):
                 ev = fam_evals[fam] * steps / max(nlaunch.get(k, 1), 1)
                 v['_evals_per_launch'] = ev
                 v['_valu_instr_per_eval'] = v['SQ_INSTS_VALU'] * 64 / ev
+        if k.startswith('k_screen_win') and win_terms and 'SQ_INSTS_VALU' in v:
+            ev = win_terms * steps / max(nlaunch.get(k, 1), 1)
+            v['_evals_per_launch'] = ev
+            v['_valu_instr_per_eval'] = v['SQ_INSTS_VALU'] * 64 / ev
         if 'SQ_INSTS_VALU' in v and v.get('GRBM_GUI_ACTIVE'):
             # VALU issue utilisation: every wave64 VALU instruction holds a
             # 16-lane SIMD for 4 cycles; 1024 SIMDs; GRBM_GUI_ACTIVE / 8 XCDs
