@@ -76,6 +76,7 @@ struct Posterior {
     DevBuf<Comp<float>> win_wide;        // per label at comp_a: wide records, w = index bits
     DevBuf<int2> win_bins;               // per label: kWinBins windows [k_lo, k_hi)
     DevBuf<double> win_seg;              // per (label position, segment): max hi, min lo, wide count
+    DevBuf<int32_t> win_hist;            // per label position: histogram of log2 interval widths
     void release() {
         labels.release();
         comps64.release();
@@ -89,6 +90,7 @@ struct Posterior {
         win_wide.release();
         win_bins.release();
         win_seg.release();
+        win_hist.release();
         win_ready = false;
         n_labels = 0;
     }

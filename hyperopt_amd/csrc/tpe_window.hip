@@ -7,15 +7,16 @@
 // prior_sigma / min(100, N + 1)), so only the components near a candidate can
 // move its sum.  Here:
 //
-//   per posterior (k_win_seg, k_win_carry, k_win_bins; once, lazily):
+//   per posterior (k_win_hist, k_win_seg, k_win_carry, k_win_bins; once, lazily):
 //     each above component's interval [lo, hi] of recentred x' where its term
 //     can reach 2^-(kWinT + 1) (from its fp32 record; the extra 1 covers the
 //     records' rounding), the prefix max of hi and the suffix min of lo over
 //     the narrow components in record order, the list of wide components
-//     (interval longer than half the label's candidate range, or too far from
-//     the centre for the rounding margin), and for each of kWinBins bins of
-//     the candidate range the window [k_lo, k_hi) of record indices outside
-//     which no narrow component reaches 2^-kWinT anywhere in the bin;
+//     (interval longer than 4x the label's median or half its candidate
+//     range, or too far from the centre for the rounding margin), and for
+//     each of kWinBins bins of the candidate range the window [k_lo, k_hi) of
+//     record indices outside which no narrow component reaches 2^-kWinT
+//     anywhere in the bin;
 //
 //   per round (k_win_key, a stable radix sort, k_screen_win):
 //     every candidate keyed by (round, label, bin of x') and sorted with its
@@ -152,6 +153,22 @@ struct Interval {
     bool wide;
 };
 
+// Wide components: an interval longer than kWideF times the label's median
+// (a few edge or sparse-region components, whose long reach would flatten
+// the prefix max / suffix min for every bin after / before them), or longer
+// than half the candidate range (the prior component).  The median comes from
+// a histogram of log2 widths (kWidthBins half-octave bins, k_win_hist), so
+// the threshold is kWideF x the upper edge of the median's bin.
+constexpr double kWideF = 4.0;
+constexpr int kWidthBins = 256;          // log2 width in [-64, 64), half octaves
+
+__device__ __forceinline__ int width_bin(double w) {
+    const double b = 2.0 * (log2(w) + 64.0);
+    if (!(b >= 0.0)) return 0;
+    if (!(b < (double)(kWidthBins - 1))) return kWidthBins - 1;
+    return (int)b;
+}
+
 // Where component r's term can reach 2^-(kWinT + 1): |x' a - m| <= s with
 // s = sqrt(c + kWinT + 1) (log2 units, c <= 0).  Outside it, the exact term
 // (from the unrounded a, m, c) stays below 2^-kWinT as long as the records'
@@ -160,7 +177,7 @@ struct Interval {
 // interval: |m| < 2^17 suffices; records beyond that are always summed.
 // Never-relevant components (c < -(kWinT + 1), also c = -inf) get an empty
 // interval and no wide flag.
-__device__ __forceinline__ Interval comp_interval(const Comp<float>& r, double span) {
+__device__ __forceinline__ Interval comp_interval(const Comp<float>& r, double span, double thr) {
     Interval v{kInf, -kInf, false};
     const double m = r.mu, a = r.a, cc = (double)r.c + (kWinT + 1.0);
     if (cc < 0.0) return v;
@@ -172,13 +189,59 @@ __device__ __forceinline__ Interval comp_interval(const Comp<float>& r, double s
     double lo = (m - s) / a, hi = (m + s) / a;
     lo -= fabs(lo) * 1e-12 + 1e-300;
     hi += fabs(hi) * 1e-12 + 1e-300;
-    if (hi - lo > 0.5 * span) {
+    if (hi - lo > 0.5 * span || hi - lo > thr) {
         v.wide = true;
         return v;
     }
     v.lo = lo;
     v.hi = hi;
     return v;
+}
+
+// grid (segments, dense labels): histogram of the narrow-candidate
+// intervals' log2 widths (everything but never-relevant components)
+__global__ __launch_bounds__(kBlock) void k_win_hist(const DLabel* __restrict__ labels,
+                                                     const int32_t* __restrict__ grp,
+                                                     const Comp<float>* __restrict__ comps32,
+                                                     const SampRec* __restrict__ samp,
+                                                     int32_t* __restrict__ hist) {
+    const int y = blockIdx.y, li = grp[y];
+    const DLabel L = labels[li];
+    __shared__ double shd[kBlock / 64];
+    __shared__ int h[kWidthBins];
+    double xlo, xhi;
+    label_range(L, samp, xlo, xhi, shd);
+    for (int b = threadIdx.x; b < kWidthBins; b += kBlock) h[b] = 0;
+    __syncthreads();
+    const int64_t k0 = (int64_t)blockIdx.x * kSeg;
+    const Comp<float>* c = comps32 + L.comp_a;
+    for (int j = 0; j < kSegR; ++j) {
+        const int64_t k = k0 + j * kBlock + threadIdx.x;
+        if (k >= L.na) break;
+        const Interval v = comp_interval(c[k], xhi - xlo, kInf);
+        if (v.hi >= v.lo) atomicAdd(&h[width_bin(v.hi - v.lo)], 1);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < kWidthBins; b += kBlock)
+        if (h[b]) atomicAdd(&hist[(size_t)y * kWidthBins + b], h[b]);
+}
+
+// kWideF x the upper edge of the median width's bin (+inf without data)
+__device__ double wide_threshold(const int32_t* __restrict__ hist_row, int* sh) {
+    static_assert(kWidthBins == kBlock, "one bin per thread");
+    const int v = hist_row[threadIdx.x];
+    int tot;
+    const int before = block_prefix(v, 0, AddOp{}, sh, tot);
+    __shared__ int med;
+    if (threadIdx.x == 0) med = kWidthBins;
+    __syncthreads();
+    // the bin holding the (tot + 1) / 2-th width
+    if (tot > 0 && before < (tot + 1) / 2 && before + v >= (tot + 1) / 2) med = threadIdx.x;
+    __syncthreads();
+    const int m = med;
+    __syncthreads();
+    if (m >= kWidthBins) return kInf;
+    return kWideF * exp2(0.5 * (double)(m + 1) - 64.0);
 }
 
 // grid (segments, dense labels): per kSeg components the segment-local
@@ -188,6 +251,7 @@ __global__ __launch_bounds__(kBlock) void k_win_seg(const DLabel* __restrict__ l
                                                     const int32_t* __restrict__ grp,
                                                     const Comp<float>* __restrict__ comps32,
                                                     const SampRec* __restrict__ samp, int32_t nseg,
+                                                    const int32_t* __restrict__ hist,
                                                     WinLabel* __restrict__ win, double* __restrict__ P,
                                                     double* __restrict__ Q, double* __restrict__ seg) {
     const int y = blockIdx.y, li = grp[y];
@@ -196,6 +260,7 @@ __global__ __launch_bounds__(kBlock) void k_win_seg(const DLabel* __restrict__ l
     __shared__ int shi[kBlock / 64];
     double xlo, xhi;
     label_range(L, samp, xlo, xhi, shd);
+    const double thr = wide_threshold(hist + (size_t)y * kWidthBins, shi);
     const int s = blockIdx.x;
     if (s == 0 && threadIdx.x == 0) win[li] = WinLabel{xlo, (double)kWinBins / (xhi - xlo), 0, 0};
     double* sg = seg + ((size_t)y * nseg + s) * 3;
@@ -215,7 +280,7 @@ __global__ __launch_bounds__(kBlock) void k_win_seg(const DLabel* __restrict__ l
     for (int j = 0; j < kSegR; ++j) {
         const int64_t k = k0 + threadIdx.x * kSegR + j;
         Interval v{kInf, -kInf, false};
-        if (k < L.na) v = comp_interval(c[k], xhi - xlo);
+        if (k < L.na) v = comp_interval(c[k], xhi - xlo, thr);
         lo[j] = v.lo;
         hi[j] = v.hi;
         nw += v.wide;
@@ -260,6 +325,7 @@ __global__ __launch_bounds__(kBlock) void k_win_carry(const DLabel* __restrict__
                                                       const int32_t* __restrict__ grp,
                                                       const Comp<float>* __restrict__ comps32,
                                                       const SampRec* __restrict__ samp, int32_t nseg,
+                                                      const int32_t* __restrict__ hist,
                                                       WinLabel* __restrict__ win, double* __restrict__ P,
                                                       double* __restrict__ Q,
                                                       const double* __restrict__ seg,
@@ -270,6 +336,7 @@ __global__ __launch_bounds__(kBlock) void k_win_carry(const DLabel* __restrict__
     __shared__ int shi[kBlock / 64];
     double xlo, xhi;
     label_range(L, samp, xlo, xhi, shd);
+    const double thr = wide_threshold(hist + (size_t)y * kWidthBins, shi);
     const int s = blockIdx.x;
     const int64_t k0 = (int64_t)s * kSeg;
     if (k0 >= L.na) return;
@@ -293,7 +360,7 @@ __global__ __launch_bounds__(kBlock) void k_win_carry(const DLabel* __restrict__
             const size_t at = L.comp_a + k;
             P[at] = P[at] > cp ? P[at] : cp;
             Q[at] = Q[at] < cq ? Q[at] : cq;
-            fl[j] = comp_interval(c[k], xhi - xlo).wide;
+            fl[j] = comp_interval(c[k], xhi - xlo, thr).wide;
         }
         cnt += fl[j];
     }
@@ -529,12 +596,17 @@ int tpe_rt::win_prepare(tpe_ctx* ctx) {
     HIPCHK(ctx, P.win_wide.reserve(P.comps32.cap));
     HIPCHK(ctx, P.win_bins.reserve((size_t)P.n_labels * kWinBins));
     HIPCHK(ctx, P.win_seg.reserve((size_t)nl * nseg * 3));
+    HIPCHK(ctx, P.win_hist.reserve((size_t)nl * kWidthBins));
+    HIPCHK(ctx, hipMemsetAsync(P.win_hist.p, 0, (size_t)nl * kWidthBins * sizeof(int32_t), ctx->stream));
     const int32_t* grp = P.groups.p + P.group_off[DENSE_GMM];
+    hipLaunchKernelGGL(k_win_hist, dim3(nseg, nl), dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
+                       P.comps32.p, P.samp.p, P.win_hist.p);
     hipLaunchKernelGGL(k_win_seg, dim3(nseg, nl), dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
-                       P.comps32.p, P.samp.p, nseg, P.win.p, P.win_p.p, P.win_q.p, P.win_seg.p);
+                       P.comps32.p, P.samp.p, nseg, P.win_hist.p, P.win.p, P.win_p.p, P.win_q.p,
+                       P.win_seg.p);
     hipLaunchKernelGGL(k_win_carry, dim3(nseg, nl), dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
-                       P.comps32.p, P.samp.p, nseg, P.win.p, P.win_p.p, P.win_q.p, P.win_seg.p,
-                       P.win_wide.p);
+                       P.comps32.p, P.samp.p, nseg, P.win_hist.p, P.win.p, P.win_p.p, P.win_q.p,
+                       P.win_seg.p, P.win_wide.p);
     hipLaunchKernelGGL(k_win_bins, dim3(kWinBins / kBlock, nl), dim3(kBlock), 0, ctx->stream,
                        P.labels.p, grp, P.win.p, P.win_p.p, P.win_q.p, P.win_bins.p);
     HIPCHK(ctx, hipGetLastError());
