@@ -232,6 +232,7 @@ struct tpe_ctx {
     DevBuf<uint64_t> win_vals, win_vals2;
     DevBuf<uint8_t> win_tmp;
     DevBuf<unsigned long long> win_evals;   // (candidate, component) terms the screen summed
+    DevBuf<float2> win_lohi;             // packed map: per candidate (lower, upper) score bound
     int64_t screen_exec = 0;             // last round: terms summed by the screen
     bool screen_exec_pending = false;
     unsigned long long screen_exec_h = 0;
@@ -276,6 +277,10 @@ namespace tpe_rt {
 // ((z - z0) nl + y) n + p back to candidate indices (low 32 bits).  Probe
 // mode (cand_in != nullptr, one label, z0 = 0, nz = 1): the candidates are
 // cand_in and s_out / e_out receive the fp32 score and its bound per index.
+// Packed mode (cpack = C > 0, batched rounds with small C): one cell per
+// label holding all nz rounds' candidates j = z C + i, and lohi[y nz C + j]
+// receives (lower, upper) bound of each candidate's score (-inf, +inf:
+// uncertified) for the per-round selection.
 struct WinScreenArgs {
     const int32_t* grp;
     int32_t nl;
@@ -286,6 +291,8 @@ struct WinScreenArgs {
     float* hi;
     unsigned long long* lbkey;
     double *s_out, *e_out;
+    int32_t cpack = 0;
+    float2* lohi = nullptr;
 };
 int win_prepare(tpe_ctx* ctx);
 int win_screen(tpe_ctx* ctx, const WinScreenArgs& a, const uint64_t** sorted_vals);

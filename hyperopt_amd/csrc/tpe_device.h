@@ -567,6 +567,10 @@ __device__ __forceinline__ float float_up(double v) {   // smallest float >= v (
     return f;
 }
 
+__device__ __forceinline__ float float_down(double v) {   // largest float <= v (finite v)
+    return -float_up(-v);
+}
+
 // |lpdf64 - lpdf| of the fp64 path (tpe_device.h lse_acc<double>): a
 // sequential sum of K terms, each within ~2.5e-14 + 2 ulp
 __device__ __forceinline__ double fp64_err(int K, double mag) {

@@ -726,6 +726,53 @@ __global__ __launch_bounds__(kBlock) void k_pick_packed(
     }
 }
 
+// The windowed packed screen (tpe_window.hip) leaves each candidate's
+// (lower, upper) score bound in lohi[y n_rounds C + z C + i]: one thread per
+// (round, label) takes the round's largest lower bound and lists, in
+// candidate order, the candidates whose upper bound reaches it -- the same
+// list and per-round ranges k_pick_packed makes.
+__global__ __launch_bounds__(kBlock) void k_pick_win(const float2* __restrict__ lohi, int32_t n_rounds,
+                                                     int32_t C, int32_t* __restrict__ cnt,
+                                                     int64_t* __restrict__ list, int64_t cap,
+                                                     RoundSel* __restrict__ rsel, int32_t nl) {
+    const int y = blockIdx.y;
+    const int64_t z = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const bool valid = z < n_rounds;
+    const float2* row = lohi + ((size_t)y * n_rounds + (valid ? z : 0)) * C;
+    float m = -__builtin_inff();
+    int k = 0;
+    if (valid) {
+        for (int c = 0; c < C; ++c) m = fmaxf(m, row[c].x);
+        for (int c = 0; c < C; ++c) k += row[c].y >= m;
+    }
+    __shared__ int sh[kBlock / 64 + 1];
+    // exclusive prefix of the counts over the workgroup's rounds
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int inc = k;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(inc, off);
+        if (lane >= off) inc += o;
+    }
+    if (lane == 63) sh[wave] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            const int t = sh[w];
+            sh[w] = tot;
+            tot += t;
+        }
+        sh[kBlock / 64] = tot ? atomicAdd(cnt + y, tot) : 0;
+    }
+    __syncthreads();
+    if (!valid) return;
+    int at = sh[kBlock / 64] + sh[wave] + inc - k;
+    rsel[(size_t)z * nl + y] = RoundSel{at, k};
+    for (int c = 0; c < C; ++c)
+        if (row[c].y >= m) list[(size_t)y * cap + at++] = (z << 32) | (int64_t)c;
+}
+
 // Re-score work item (label position, block j of kR * 256 entries) x chunk:
 // blockIdx.y = c sums the above mixture's chunk c (c = 0 also the below
 // mixture and the candidate) from zero -- the chunked map's own per-chunk
@@ -1433,21 +1480,43 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
     const uint32_t gx8 = (uint32_t)((a.n_rounds + S8.rpb - 1) / S8.rpb);
     const size_t planes = (size_t)nl * (nch + 2) * gx8 * (kScreenR * kBlock);
     const int64_t cap = (int64_t)a.n_rounds * a.n;   // candidate slots per label
-    HIPCHK(ctx, ctx->chunk_part.reserve(planes));
     HIPCHK(ctx, ctx->scr_list.reserve((size_t)nl * cap));
     HIPCHK(ctx, ctx->scr_rsel.reserve((size_t)a.n_rounds * nl));
     HIPCHK(ctx, ctx->scr_cnt.reserve(nl));
     HIPCHK(ctx, hipMemsetAsync(ctx->scr_cnt.p, 0, nl * sizeof(int32_t), ctx->stream));
     RoundSel* rsel = reinterpret_cast<RoundSel*>(ctx->scr_rsel.p);
-    if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
-    hipLaunchKernelGGL((k_round_chunk<float, kScreenR>), dim3(gx8, nl, nch), dim3(kBlock), 0,
-                       ctx->stream, ctx->P->labels.p, grp, ctx->P->comps32.p, ctx->P->samp.p, a.n,
-                       a.cand_offset, a.seed, ctx->rounds.p, chunk, ctx->chunk_part.p, ctx->errflag.p,
-                       S8);
-    if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
-    hipLaunchKernelGGL((k_pick_packed<kScreenR>), dim3(gx8, nl), dim3(kBlock), 0, ctx->stream,
-                       ctx->P->labels.p, grp, a.n, nl, nch, chunk, ctx->chunk_part.p, ctx->scr_cnt.p,
-                       ctx->scr_list.p, cap, rsel, S8);
+    if (ctx->window && cap >= kWinMinN && (int64_t)nl * cap <= ((int64_t)1 << 30)) {
+        // windowed: every round's candidates of a label sorted together into
+        // tiles of neighbours (tpe_window.hip), bounds per candidate, then
+        // the per-round selection
+        int rc = tpe_rt::win_prepare(ctx);
+        if (rc) return rc;
+        HIPCHK(ctx, ctx->win_evals.reserve(1));
+        HIPCHK(ctx, hipMemsetAsync(ctx->win_evals.p, 0, sizeof(unsigned long long), ctx->stream));
+        HIPCHK(ctx, ctx->win_lohi.reserve((size_t)nl * cap));
+        const uint64_t* sorted = nullptr;
+        tpe_rt::WinScreenArgs wa{grp, nl, a.n, a.cand_offset, a.seed, 0, a.n_rounds, nullptr,
+                                 nullptr, nullptr, nullptr, nullptr, (int32_t)a.n, ctx->win_lohi.p};
+        if ((rc = tpe_rt::win_screen(ctx, wa, &sorted))) return rc;
+        hipLaunchKernelGGL(k_pick_win, dim3((unsigned)((a.n_rounds + kBlock - 1) / kBlock), nl),
+                           dim3(kBlock), 0, ctx->stream, ctx->win_lohi.p, a.n_rounds, (int32_t)a.n,
+                           ctx->scr_cnt.p, ctx->scr_list.p, cap, rsel, nl);
+        HIPCHK(ctx, hipMemcpyAsync(&ctx->screen_exec_h, ctx->win_evals.p, sizeof(unsigned long long),
+                                   hipMemcpyDeviceToHost, ctx->stream));
+        ctx->screen_exec_pending = true;
+    } else {
+        HIPCHK(ctx, ctx->chunk_part.reserve(planes));
+        if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
+        hipLaunchKernelGGL((k_round_chunk<float, kScreenR>), dim3(gx8, nl, nch), dim3(kBlock), 0,
+                           ctx->stream, ctx->P->labels.p, grp, ctx->P->comps32.p, ctx->P->samp.p, a.n,
+                           a.cand_offset, a.seed, ctx->rounds.p, chunk, ctx->chunk_part.p, ctx->errflag.p,
+                           S8);
+        if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
+        hipLaunchKernelGGL((k_pick_packed<kScreenR>), dim3(gx8, nl), dim3(kBlock), 0, ctx->stream,
+                           ctx->P->labels.p, grp, a.n, nl, nch, chunk, ctx->chunk_part.p, ctx->scr_cnt.p,
+                           ctx->scr_list.p, cap, rsel, S8);
+        ctx->screen_exec += (int64_t)a.n_rounds * a.n * dense_terms(ctx);
+    }
     ctx->scr_cnt_h.resize(nl);
     HIPCHK(ctx, hipMemcpyAsync(ctx->scr_cnt_h.data(), ctx->scr_cnt.p, nl * sizeof(int32_t),
                                hipMemcpyDeviceToHost, ctx->stream));
@@ -1485,7 +1554,6 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
                        ctx->stream, grp, nl, a.n_rounds, ctx->P->n_labels, rsel, ctx->scr_res.p,
                        ctx->scr_off.p, ctx->partials.p);
     ctx->screen_total += cells * a.n;
-    ctx->screen_exec += cells * a.n * dense_terms(ctx);
     ctx->screen_pending = true;
     return ctx->hip(hipGetLastError(), "packed screen launch");
 }

@@ -419,13 +419,15 @@ __global__ __launch_bounds__(kBlock) void k_win_bins(const DLabel* __restrict__ 
 // and value (x' fp32 bits << 32 | candidate index) of every candidate, at
 // position ((z - z0) nl + y) n + i.  The candidates are drawn exactly as the
 // plain screen and the fp64 round draw them.
+// Packed (cpack = C > 0, grid.z = 1): one cell per label, candidate j = z C
+// + i of round z0 + z, value index j.
 template <bool SAMPLE>
 __global__ __launch_bounds__(kBlock) void k_win_key(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ grp,
     const SampRec* __restrict__ samp, const WinLabel* __restrict__ win,
-    const double* __restrict__ cand_in, int64_t n, int64_t cand_offset, uint64_t seed,
-    const uint32_t* __restrict__ rounds, int32_t z0, int32_t nl, uint32_t* __restrict__ keys,
-    uint64_t* __restrict__ vals, int32_t* __restrict__ err) {
+    const double* __restrict__ cand_in, int64_t ncell, int32_t cpack, int64_t cand_offset,
+    uint64_t seed, const uint32_t* __restrict__ rounds, int32_t z0, int32_t nl,
+    uint32_t* __restrict__ keys, uint64_t* __restrict__ vals, int32_t* __restrict__ err) {
     const int y = blockIdx.y, li = grp[y];
     const DLabel L = labels[li];
     const WinLabel W = win[li];
@@ -433,11 +435,16 @@ __global__ __launch_bounds__(kBlock) void k_win_key(
     const uint32_t cell = blockIdx.z * (uint32_t)nl + y;
 #pragma unroll
     for (int r = 0; r < kKeyR; ++r) {
-        const int64_t i = (int64_t)blockIdx.x * (kKeyR * kBlock) + r * kBlock + threadIdx.x;
-        if (i >= n) continue;
+        const int64_t j = (int64_t)blockIdx.x * (kKeyR * kBlock) + r * kBlock + threadIdx.x;
+        if (j >= ncell) continue;
+        int64_t i = j, z = z0 + blockIdx.z;
+        if (cpack) {
+            z = z0 + j / cpack;
+            i = j - (j / cpack) * cpack;
+        }
         double v;
         if constexpr (SAMPLE) {
-            const uint32_t g = (uint32_t)(cand_offset + i), rk = rounds[z0 + blockIdx.z];
+            const uint32_t g = (uint32_t)(cand_offset + i), rk = rounds[z];
             const bool ok = lgmm ? sample_below<DENSE_LGMM>(L, samp + L.samp_off, seed, rk, g, v)
                                  : sample_below<DENSE_GMM>(L, samp + L.samp_off, seed, rk, g, v);
             if (!ok) atomicOr(err, 1);
@@ -445,9 +452,9 @@ __global__ __launch_bounds__(kBlock) void k_win_key(
             v = cand_in[i];
         }
         const double xr = (lgmm ? log(v) : v) - L.centre;
-        const size_t pos = (size_t)cell * n + i;
+        const size_t pos = (size_t)cell * ncell + j;
         keys[pos] = (cell << kWinBinBits) | (uint32_t)win_bin(W, xr);
-        vals[pos] = ((uint64_t)__float_as_uint((float)xr) << 32) | (uint32_t)i;
+        vals[pos] = ((uint64_t)__float_as_uint((float)xr) << 32) | (uint32_t)j;
     }
 }
 
@@ -461,7 +468,7 @@ __global__ __launch_bounds__(kBlock) void k_screen_win(
     const int2* __restrict__ bins, const Comp<float>* __restrict__ wide,
     const uint64_t* __restrict__ vals, int64_t n, int32_t z0, int32_t nl, float* __restrict__ hi_out,
     unsigned long long* __restrict__ lbkey, unsigned long long* __restrict__ terms,
-    double* __restrict__ s_out, double* __restrict__ e_out) {
+    double* __restrict__ s_out, double* __restrict__ e_out, float2* __restrict__ lohi) {
     constexpr int R = kWinR;
     const int y = blockIdx.y, li = grp[y];
     const DLabel L = labels[li];
@@ -548,8 +555,14 @@ __global__ __launch_bounds__(kBlock) void k_screen_win(
             e_out[ci[r]] = E;
             continue;
         }
+        const bool cert = E <= 1e30 && s == s;
+        if (lohi) {   // packed: per candidate, selected per round by k_pick_win
+            lohi[bcell * n + ci[r]] = cert ? float2{float_down(s - E), float_up(s + E)}
+                                           : float2{-__builtin_inff(), __builtin_inff()};
+            continue;
+        }
         float h = __builtin_inff();
-        if (E <= 1e30 && s == s) {
+        if (cert) {
             h = float_up(s + E);
             const uint64_t key = order_key(s - E);
             bk = key > bk ? key : bk;
@@ -558,7 +571,7 @@ __global__ __launch_bounds__(kBlock) void k_screen_win(
     }
     if (threadIdx.x == 0 && terms)
         atomicAdd(terms, (unsigned long long)nvt * (unsigned long long)(L.nb + nwin + nout));
-    if constexpr (PROBE) return;
+    if (PROBE || lohi) return;
     __shared__ unsigned long long shk[kBlock / 64];
     struct KMax {
         __device__ unsigned long long operator()(unsigned long long a, unsigned long long b) const {
@@ -617,24 +630,28 @@ int tpe_rt::win_prepare(tpe_ctx* ctx) {
 int tpe_rt::win_screen(tpe_ctx* ctx, const WinScreenArgs& a, const uint64_t** sorted_vals) {
     tpe_rt::Posterior& P = *ctx->P;
     const bool probe = a.cand_in != nullptr;
-    const size_t total = (size_t)a.nz * a.nl * a.n;
+    // candidates per cell; cells: (round, label), or one per label packed
+    const int64_t ncell = a.cpack ? (int64_t)a.nz * a.cpack : a.n;
+    const int64_t cells = a.cpack ? a.nl : (int64_t)a.nz * a.nl;
+    const size_t total = (size_t)cells * ncell;
     if (total > ((size_t)1 << 30)) return ctx->fail(TPE_ERR_ARG, "windowed screen batch too large");
     HIPCHK(ctx, ctx->win_keys.reserve(total));
     HIPCHK(ctx, ctx->win_keys2.reserve(total));
     HIPCHK(ctx, ctx->win_vals.reserve(total));
     HIPCHK(ctx, ctx->win_vals2.reserve(total));
-    const dim3 gk((unsigned)((a.n + kKeyR * kBlock - 1) / (kKeyR * kBlock)), a.nl, a.nz);
+    const dim3 gk((unsigned)((ncell + kKeyR * kBlock - 1) / (kKeyR * kBlock)), a.nl,
+                  a.cpack ? 1 : a.nz);
     if (probe)
         hipLaunchKernelGGL(k_win_key<false>, gk, dim3(kBlock), 0, ctx->stream, P.labels.p, a.grp, P.samp.p,
-                           P.win.p, a.cand_in, a.n, a.cand_offset, a.seed, ctx->rounds.p, a.z0, a.nl,
-                           ctx->win_keys.p, ctx->win_vals.p, ctx->errflag.p);
+                           P.win.p, a.cand_in, ncell, 0, a.cand_offset, a.seed, ctx->rounds.p, a.z0,
+                           a.nl, ctx->win_keys.p, ctx->win_vals.p, ctx->errflag.p);
     else
         hipLaunchKernelGGL(k_win_key<true>, gk, dim3(kBlock), 0, ctx->stream, P.labels.p, a.grp, P.samp.p,
-                           P.win.p, nullptr, a.n, a.cand_offset, a.seed, ctx->rounds.p, a.z0, a.nl,
-                           ctx->win_keys.p, ctx->win_vals.p, ctx->errflag.p);
+                           P.win.p, nullptr, ncell, a.cpack, a.cand_offset, a.seed, ctx->rounds.p, a.z0,
+                           a.nl, ctx->win_keys.p, ctx->win_vals.p, ctx->errflag.p);
     HIPCHK(ctx, hipGetLastError());
     int cell_bits = 0;
-    while (((int64_t)1 << cell_bits) < (int64_t)a.nz * a.nl) ++cell_bits;
+    while (((int64_t)1 << cell_bits) < cells) ++cell_bits;
     const int end_bit = kWinBinBits + cell_bits;
     hipcub::DoubleBuffer<uint32_t> kb(ctx->win_keys.p, ctx->win_keys2.p);
     hipcub::DoubleBuffer<uint64_t> vb(ctx->win_vals.p, ctx->win_vals2.p);
@@ -645,16 +662,17 @@ int tpe_rt::win_screen(tpe_ctx* ctx, const WinScreenArgs& a, const uint64_t** so
     HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(ctx->win_tmp.p, bytes, kb, vb, (int)total, 0, end_bit,
                                                      ctx->stream));
     const uint64_t* sorted = vb.Current();
-    const dim3 gs((unsigned)((a.n + kWinR * kBlock - 1) / (kWinR * kBlock)), a.nl, a.nz);
+    const dim3 gs((unsigned)((ncell + kWinR * kBlock - 1) / (kWinR * kBlock)), a.nl,
+                  a.cpack ? 1 : a.nz);
     if (ctx->timing && !probe && a.z0 == 0) HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
     if (probe)
         hipLaunchKernelGGL(k_screen_win<true>, gs, dim3(kBlock), 0, ctx->stream, P.labels.p, a.grp,
-                           P.comps32.p, P.win.p, P.win_bins.p, P.win_wide.p, sorted, a.n, a.z0, a.nl,
-                           nullptr, nullptr, nullptr, a.s_out, a.e_out);
+                           P.comps32.p, P.win.p, P.win_bins.p, P.win_wide.p, sorted, ncell, a.z0,
+                           a.nl, nullptr, nullptr, nullptr, a.s_out, a.e_out, nullptr);
     else
         hipLaunchKernelGGL(k_screen_win<false>, gs, dim3(kBlock), 0, ctx->stream, P.labels.p, a.grp,
-                           P.comps32.p, P.win.p, P.win_bins.p, P.win_wide.p, sorted, a.n, a.z0, a.nl,
-                           a.hi, a.lbkey, ctx->win_evals.p, nullptr, nullptr);
+                           P.comps32.p, P.win.p, P.win_bins.p, P.win_wide.p, sorted, ncell, a.z0,
+                           a.nl, a.hi, a.lbkey, ctx->win_evals.p, nullptr, nullptr, a.lohi);
     if (ctx->timing && !probe) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
     HIPCHK(ctx, hipGetLastError());
     *sorted_vals = sorted;
