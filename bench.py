@@ -87,6 +87,8 @@ def parse():
                     help='f64: plain fp64 rounds (no fp32 screen); the winners are the same')
     ap.add_argument('--no-window', action='store_true',
                     help='f64: the plain fp32 screen (every term) instead of the windowed one')
+    ap.add_argument('--win-t', type=int, default=40,
+                    help='the windowed screen\'s cut T (components left out stay below 2^-T)')
     ap.add_argument('--unscreened-steps', type=int, default=3,
                     help='f64: steps of the plain fp64 round timed after the main run, for '
                          'comparison (0 = skip)')
@@ -309,6 +311,7 @@ def main():
     screen = args.precision == 'f64' and not args.no_screen
     eng.set_option('screen', int(screen))
     eng.set_option('window', int(not args.no_window))
+    eng.set_option('win_t', args.win_t)
     if world > 1:   # this rank holds one shard: size-dependent choices follow the whole round
         eng.set_option('whole_rounds' if args.config == 5 else 'whole_n',
                        args.new_ids if args.config == 5 else C_total)
@@ -390,7 +393,7 @@ def main():
             'screen_terms_fraction': scr[3] / max(mode_ev[dom], 1),
             'note': 'dense labels: every (candidate, component) pair is either evaluated in '
                     'packed fp32 with a rigorous error bound, or (windowed screen: candidates '
-                    'sorted into tiles of neighbours) proven below 2^-48 of its tile\'s sums and '
+                    'sorted into tiles of neighbours) proven below 2^-T (win_t) of the largest term and '
                     'covered by the bound; candidates whose bound interval reaches the '
                     'round\'s best lower bound are re-scored in fp64 over every component -- '
                     'winners and lpdfs are bit-identical to the plain fp64 round '

@@ -71,6 +71,7 @@ struct Posterior {
     // window index of the dense labels' above mixtures (windowed fp32 screen,
     // tpe_engine.hip k_win_*), built on first use after every posterior change
     bool win_ready = false;
+    int32_t win_t = 0;                   // the cut T the index was built for
     DevBuf<tpe::WinLabel> win;           // per label
     DevBuf<double> win_p, win_q;         // per component: prefix max of hi / suffix min of lo
     DevBuf<Comp<float>> win_wide;        // per label at comp_a: wide records, w = index bits
@@ -228,6 +229,7 @@ struct tpe_ctx {
     // windowed screen (large tile-map rounds): candidates keyed by (round,
     // label, bin) and stably sorted with their (x' fp32, index) values
     bool window = true;                  // TPE_OPT_WINDOW
+    int32_t win_t = tpe::kWinTDefault;   // TPE_OPT_WIN_T
     DevBuf<uint32_t> win_keys, win_keys2;
     DevBuf<uint64_t> win_vals, win_vals2;
     DevBuf<uint8_t> win_tmp;

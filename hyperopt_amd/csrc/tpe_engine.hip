@@ -2408,6 +2408,10 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
             break;
         case TPE_OPT_TIMING: ctx->timing = value != 0; break;
         case TPE_OPT_WINDOW: ctx->window = value != 0; break;
+        case TPE_OPT_WIN_T:
+            if (value < 16 || value > 62) return ctx->fail(TPE_ERR_ARG, "window cut must be in [16, 62]");
+            ctx->win_t = (int32_t)value;
+            break;
         case TPE_OPT_WHOLE_N:
             if (value < 0) return ctx->fail(TPE_ERR_ARG, "whole candidate count must be >= 0");
             ctx->opt_whole_n = value;

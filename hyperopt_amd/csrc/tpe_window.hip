@@ -9,13 +9,13 @@
 //
 //   per posterior (k_win_hist, k_win_seg, k_win_carry, k_win_bins; once, lazily):
 //     each above component's interval [lo, hi] of recentred x' where its term
-//     can reach 2^-(kWinT + 1) (from its fp32 record; the extra 1 covers the
+//     can reach 2^-(T + 1) (from its fp32 record; the extra 1 covers the
 //     records' rounding), the prefix max of hi and the suffix min of lo over
 //     the narrow components in record order, the list of wide components
 //     (interval longer than 4x the label's median or half its candidate
 //     range, or too far from the centre for the rounding margin), and for
 //     each of kWinBins bins of the candidate range the window [k_lo, k_hi) of
-//     record indices outside which no narrow component reaches 2^-kWinT
+//     record indices outside which no narrow component reaches 2^-T
 //     anywhere in the bin;
 //
 //   per round (k_win_key, a stable radix sort, k_screen_win):
@@ -24,7 +24,7 @@
 //     the tile's window is [k_lo(bin of its min), k_hi(bin of its max)), the
 //     below mixture and the wide components outside the window are summed in
 //     full, and the bound (screen_err) grows by the skipped mass,
-//     nskip 2^-kWinT / S.
+//     nskip 2^-T / S.
 //
 // The selection (k_select) and the fp64 re-score (k_rescore, every
 // component) are the plain screen's, so winners and lpdfs are bit-identical
@@ -169,17 +169,18 @@ __device__ __forceinline__ int width_bin(double w) {
     return (int)b;
 }
 
-// Where component r's term can reach 2^-(kWinT + 1): |x' a - m| <= s with
-// s = sqrt(c + kWinT + 1) (log2 units, c <= 0).  Outside it, the exact term
-// (from the unrounded a, m, c) stays below 2^-kWinT as long as the records'
+// Where component r's term can reach 2^-(T + 1): |x' a - m| <= s with
+// s = sqrt(c + T + 1) (log2 units, c <= 0).  Outside it, the exact term
+// (from the unrounded a, m, c) stays below 2^-T as long as the records'
 // rounding moves z by less than sqrt(c + T + 1) - sqrt(c + T) >= 1 / (2
 // sqrt(T + 1)) ~ 0.07, i.e. (|x' a| + |m|) 2^-23 < 0.07 for every x' near the
 // interval: |m| < 2^17 suffices; records beyond that are always summed.
-// Never-relevant components (c < -(kWinT + 1), also c = -inf) get an empty
+// Never-relevant components (c < -(T + 1), also c = -inf) get an empty
 // interval and no wide flag.
-__device__ __forceinline__ Interval comp_interval(const Comp<float>& r, double span, double thr) {
+__device__ __forceinline__ Interval comp_interval(const Comp<float>& r, double span, double thr,
+                                                 double T) {
     Interval v{kInf, -kInf, false};
-    const double m = r.mu, a = r.a, cc = (double)r.c + (kWinT + 1.0);
+    const double m = r.mu, a = r.a, cc = (double)r.c + (T + 1.0);
     if (cc < 0.0) return v;
     if (!(cc <= 1e30) || !(a > 0.0) || !(a < 1e30) || !(fabs(m) < 131072.0)) {
         v.wide = true;
@@ -204,7 +205,7 @@ __global__ __launch_bounds__(kBlock) void k_win_hist(const DLabel* __restrict__ 
                                                      const int32_t* __restrict__ grp,
                                                      const Comp<float>* __restrict__ comps32,
                                                      const SampRec* __restrict__ samp,
-                                                     int32_t* __restrict__ hist) {
+                                                     int32_t* __restrict__ hist, double T) {
     const int y = blockIdx.y, li = grp[y];
     const DLabel L = labels[li];
     __shared__ double shd[kBlock / 64];
@@ -218,7 +219,7 @@ __global__ __launch_bounds__(kBlock) void k_win_hist(const DLabel* __restrict__ 
     for (int j = 0; j < kSegR; ++j) {
         const int64_t k = k0 + j * kBlock + threadIdx.x;
         if (k >= L.na) break;
-        const Interval v = comp_interval(c[k], xhi - xlo, kInf);
+        const Interval v = comp_interval(c[k], xhi - xlo, kInf, T);
         if (v.hi >= v.lo) atomicAdd(&h[width_bin(v.hi - v.lo)], 1);
     }
     __syncthreads();
@@ -253,7 +254,8 @@ __global__ __launch_bounds__(kBlock) void k_win_seg(const DLabel* __restrict__ l
                                                     const SampRec* __restrict__ samp, int32_t nseg,
                                                     const int32_t* __restrict__ hist,
                                                     WinLabel* __restrict__ win, double* __restrict__ P,
-                                                    double* __restrict__ Q, double* __restrict__ seg) {
+                                                    double* __restrict__ Q, double* __restrict__ seg,
+                                                    double T) {
     const int y = blockIdx.y, li = grp[y];
     const DLabel L = labels[li];
     __shared__ double shd[kBlock / 64];
@@ -280,7 +282,7 @@ __global__ __launch_bounds__(kBlock) void k_win_seg(const DLabel* __restrict__ l
     for (int j = 0; j < kSegR; ++j) {
         const int64_t k = k0 + threadIdx.x * kSegR + j;
         Interval v{kInf, -kInf, false};
-        if (k < L.na) v = comp_interval(c[k], xhi - xlo, thr);
+        if (k < L.na) v = comp_interval(c[k], xhi - xlo, thr, T);
         lo[j] = v.lo;
         hi[j] = v.hi;
         nw += v.wide;
@@ -329,7 +331,7 @@ __global__ __launch_bounds__(kBlock) void k_win_carry(const DLabel* __restrict__
                                                       WinLabel* __restrict__ win, double* __restrict__ P,
                                                       double* __restrict__ Q,
                                                       const double* __restrict__ seg,
-                                                      Comp<float>* __restrict__ wide) {
+                                                      Comp<float>* __restrict__ wide, double T) {
     const int y = blockIdx.y, li = grp[y];
     const DLabel L = labels[li];
     __shared__ double shd[kBlock / 64];
@@ -360,7 +362,7 @@ __global__ __launch_bounds__(kBlock) void k_win_carry(const DLabel* __restrict__
             const size_t at = L.comp_a + k;
             P[at] = P[at] > cp ? P[at] : cp;
             Q[at] = Q[at] < cq ? Q[at] : cq;
-            fl[j] = comp_interval(c[k], xhi - xlo, thr).wide;
+            fl[j] = comp_interval(c[k], xhi - xlo, thr, T).wide;
         }
         cnt += fl[j];
     }
@@ -468,7 +470,8 @@ __global__ __launch_bounds__(kBlock) void k_screen_win(
     const int2* __restrict__ bins, const Comp<float>* __restrict__ wide,
     const uint64_t* __restrict__ vals, int64_t n, int32_t z0, int32_t nl, float* __restrict__ hi_out,
     unsigned long long* __restrict__ lbkey, unsigned long long* __restrict__ terms,
-    double* __restrict__ s_out, double* __restrict__ e_out, float2* __restrict__ lohi) {
+    double* __restrict__ s_out, double* __restrict__ e_out, float2* __restrict__ lohi,
+    double skip_unit) {
     constexpr int R = kWinR;
     const int y = blockIdx.y, li = grp[y];
     const DLabel L = labels[li];
@@ -545,8 +548,7 @@ __global__ __launch_bounds__(kBlock) void k_screen_win(
         const double s = lb - la;
         const double X = fabs((double)xf[r]) * (1.0 + 0x1.0p-23);
         const double dx = X * 0x1.0p-24 + 0x1.0p-149;
-        const double skip = nskip > 0 ? (double)nskip * 0x1.0p-48 * 1.01 / (double)aa[r] : 0.0;
-        static_assert(kWinT == 48.0, "skip term uses 2^-48");
+        const double skip = nskip > 0 ? (double)nskip * skip_unit * 1.01 / (double)aa[r] : 0.0;
         const double E = 1.25 * (screen_err(L.amax_b, L.nb, L.nb, X, dx, ab[r], l2b) +
                                  screen_err(L.amax_a, L.na, Kc, X, dx, aa[r], l2a, skip) +
                                  fp64_err(L.nb + L.na, fabs(lb) + fabs(la) + X + fabs(L.centre)));
@@ -593,7 +595,9 @@ int64_t tpe_rt::win_rounds_per_batch(int64_t n, int32_t nl) {
 
 int tpe_rt::win_prepare(tpe_ctx* ctx) {
     tpe_rt::Posterior& P = *ctx->P;
-    if (P.win_ready) return TPE_OK;
+    if (P.win_ready && P.win_t == ctx->win_t) return TPE_OK;
+    P.win_t = ctx->win_t;
+    const double T = (double)ctx->win_t;
     const int nl = (int)(P.h_group[DENSE_GMM].size() + P.h_group[DENSE_LGMM].size());
     if (nl == 0) {
         P.win_ready = true;
@@ -613,13 +617,13 @@ int tpe_rt::win_prepare(tpe_ctx* ctx) {
     HIPCHK(ctx, hipMemsetAsync(P.win_hist.p, 0, (size_t)nl * kWidthBins * sizeof(int32_t), ctx->stream));
     const int32_t* grp = P.groups.p + P.group_off[DENSE_GMM];
     hipLaunchKernelGGL(k_win_hist, dim3(nseg, nl), dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
-                       P.comps32.p, P.samp.p, P.win_hist.p);
+                       P.comps32.p, P.samp.p, P.win_hist.p, T);
     hipLaunchKernelGGL(k_win_seg, dim3(nseg, nl), dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
                        P.comps32.p, P.samp.p, nseg, P.win_hist.p, P.win.p, P.win_p.p, P.win_q.p,
-                       P.win_seg.p);
+                       P.win_seg.p, T);
     hipLaunchKernelGGL(k_win_carry, dim3(nseg, nl), dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
                        P.comps32.p, P.samp.p, nseg, P.win_hist.p, P.win.p, P.win_p.p, P.win_q.p,
-                       P.win_seg.p, P.win_wide.p);
+                       P.win_seg.p, P.win_wide.p, T);
     hipLaunchKernelGGL(k_win_bins, dim3(kWinBins / kBlock, nl), dim3(kBlock), 0, ctx->stream,
                        P.labels.p, grp, P.win.p, P.win_p.p, P.win_q.p, P.win_bins.p);
     HIPCHK(ctx, hipGetLastError());
@@ -662,17 +666,18 @@ int tpe_rt::win_screen(tpe_ctx* ctx, const WinScreenArgs& a, const uint64_t** so
     HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(ctx->win_tmp.p, bytes, kb, vb, (int)total, 0, end_bit,
                                                      ctx->stream));
     const uint64_t* sorted = vb.Current();
+    const double skip_unit = std::ldexp(1.0, -P.win_t);   // 2^-T of the index in use
     const dim3 gs((unsigned)((ncell + kWinR * kBlock - 1) / (kWinR * kBlock)), a.nl,
                   a.cpack ? 1 : a.nz);
     if (ctx->timing && !probe && a.z0 == 0) HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
     if (probe)
         hipLaunchKernelGGL(k_screen_win<true>, gs, dim3(kBlock), 0, ctx->stream, P.labels.p, a.grp,
                            P.comps32.p, P.win.p, P.win_bins.p, P.win_wide.p, sorted, ncell, a.z0,
-                           a.nl, nullptr, nullptr, nullptr, a.s_out, a.e_out, nullptr);
+                           a.nl, nullptr, nullptr, nullptr, a.s_out, a.e_out, nullptr, skip_unit);
     else
         hipLaunchKernelGGL(k_screen_win<false>, gs, dim3(kBlock), 0, ctx->stream, P.labels.p, a.grp,
                            P.comps32.p, P.win.p, P.win_bins.p, P.win_wide.p, sorted, ncell, a.z0,
-                           a.nl, a.hi, a.lbkey, ctx->win_evals.p, nullptr, nullptr, a.lohi);
+                           a.nl, a.hi, a.lbkey, ctx->win_evals.p, nullptr, nullptr, a.lohi, skip_unit);
     if (ctx->timing && !probe) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
     HIPCHK(ctx, hipGetLastError());
     *sorted_vals = sorted;

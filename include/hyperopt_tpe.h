@@ -303,8 +303,9 @@ int tpe_last_screen(const tpe_ctx *ctx, int64_t *screened, int64_t *rescored,
 
 /* (candidate, component) terms the last round's screen actually summed
  * (both mixtures).  The windowed screen (TPE_OPT_WINDOW) leaves out the
- * components that cannot reach 2^-48 of a tile's sums; the plain screen sums
- * them all (then this is screened x (nb + na)).  Winners are unaffected. */
+ * components whose terms stay below 2^-T (TPE_OPT_WIN_T) of the largest
+ * coefficient over a whole tile; the plain screen sums them all (then this
+ * is screened x (nb + na)).  Winners are unaffected. */
 int tpe_last_screen_terms(const tpe_ctx *ctx, int64_t *terms);
 
 /* Diagnostic of the screen (tests): for caller-supplied candidates of one
@@ -324,6 +325,8 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *   TPE_OPT_WINDOW  windowed screen of large tile rounds: candidates sorted
  *                   into tiles of neighbours, each summed over the window of
  *                   components that can matter to it                   [1]
+ *   TPE_OPT_WIN_T   the windowed screen's cut T: components left out of a
+ *                   tile stay below 2^-T of the largest term (16..62)   [40]
  *   TPE_OPT_TIMING  HIP-event timing of every round (tpe_last_timing,
  *                   tpe_last_mode_stats, tpe_last_screen's ms); off saves
  *                   ~20 event calls per round on latency-bound calls   [1]
@@ -342,6 +345,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_WHOLE_ROUNDS 6
 #define TPE_OPT_TIMING 7
 #define TPE_OPT_WINDOW 8
+#define TPE_OPT_WIN_T 9
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
 
 #ifdef __cplusplus
