@@ -87,7 +87,7 @@ def parse():
                     help='f64: plain fp64 rounds (no fp32 screen); the winners are the same')
     ap.add_argument('--no-window', action='store_true',
                     help='f64: the plain fp32 screen (every term) instead of the windowed one')
-    ap.add_argument('--win-t', type=int, default=40,
+    ap.add_argument('--win-t', type=int, default=16,
                     help='the windowed screen\'s cut T (components left out stay below 2^-T)')
     ap.add_argument('--unscreened-steps', type=int, default=3,
                     help='f64: steps of the plain fp64 round timed after the main run, for '

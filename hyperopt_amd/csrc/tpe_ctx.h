@@ -78,6 +78,8 @@ struct Posterior {
     DevBuf<int2> win_bins;               // per label: kWinBins windows [k_lo, k_hi)
     DevBuf<double> win_seg;              // per (label position, segment): max hi, min lo, wide count
     DevBuf<int32_t> win_hist;            // per label position: histogram of log2 interval widths
+    DevBuf<uint8_t> win_flag;            // per component: 1 = wide
+    DevBuf<double> win_skip;             // per label: kWinBins bounds of the mass a bin's window skips
     void release() {
         labels.release();
         comps64.release();
@@ -92,6 +94,8 @@ struct Posterior {
         win_bins.release();
         win_seg.release();
         win_hist.release();
+        win_flag.release();
+        win_skip.release();
         win_ready = false;
         n_labels = 0;
     }
@@ -230,9 +234,14 @@ struct tpe_ctx {
     // label, bin) and stably sorted with their (x' fp32, index) values
     bool window = true;                  // TPE_OPT_WINDOW
     int32_t win_t = tpe::kWinTDefault;   // TPE_OPT_WIN_T
-    DevBuf<uint32_t> win_keys, win_keys2;
-    DevBuf<uint64_t> win_vals, win_vals2;
-    DevBuf<uint8_t> win_tmp;
+    int32_t win_groups = 0;              // TPE_OPT_WIN_GROUPS (0: auto)
+    DevBuf<uint32_t> win_keys[2], win_keys2[2];   // two slots: sort of group g + 1
+    DevBuf<uint64_t> win_vals[2], win_vals2[2];   //   while group g is screened
+    DevBuf<uint8_t> win_tmp[2];
+    hipStream_t aux = nullptr;           // key + sort of the next label group
+    hipEvent_t ev_fork = nullptr, ev_sorted[2] = {}, ev_done[2] = {};
+    std::vector<hipEvent_t> evw;         // per unit: k_screen_win brackets (timing)
+    int32_t evw_used = 0;
     DevBuf<unsigned long long> win_evals;   // (candidate, component) terms the screen summed
     DevBuf<float2> win_lohi;             // packed map: per candidate (lower, upper) score bound
     int64_t screen_exec = 0;             // last round: terms summed by the screen
@@ -295,9 +304,20 @@ struct WinScreenArgs {
     double *s_out, *e_out;
     int32_t cpack = 0;
     float2* lohi = nullptr;
+    // a group of the round's labels: positions [y0, y0 + nl) of nl_all
+    // (0: nl) -- the grp pointer is already offset by y0
+    int32_t y0 = 0, nl_all = 0;
+    int slot = 0;                        // sort buffers (two, for the pipeline)
 };
 int win_prepare(tpe_ctx* ctx);
+// whole screen on ctx->stream (slot 0): reserve, key + sort, tiles
 int win_screen(tpe_ctx* ctx, const WinScreenArgs& a, const uint64_t** sorted_vals);
+// the pieces, for pipelining label groups over two streams: buffers for
+// `nslots` slots of up to `total` candidates in `cells` cells (before any
+// launch: growing a buffer frees it), key + sort into a.slot, the tiles
+int win_reserve(tpe_ctx* ctx, size_t total, int64_t cells, int nslots);
+int win_sort(tpe_ctx* ctx, const WinScreenArgs& a, hipStream_t st, const uint64_t** sorted);
+int win_tiles(tpe_ctx* ctx, const WinScreenArgs& a, const uint64_t* sorted, hipStream_t st);
 int64_t win_rounds_per_batch(int64_t n, int32_t nl);
 }  // namespace tpe_rt
 

@@ -510,8 +510,8 @@ constexpr float kScreenMinAcc = 0x1.0p-60f;
 // fp64 -- that addition adds nch 2^-53, inside the 2^-41 slack)
 //
 // skip: the relative mass of terms left out of the sum altogether (the
-// windowed screen, below), each exactly < 2^-T, so at most
-// nskip 2^-T / S <= nskip 2^-T 1.01 / S32.
+// windowed screen, below): a bound B of their sum over S, B / S <= B 1.01 /
+// S32.
 __device__ __forceinline__ double screen_err(float amax, int K, int Kc, double X, double dx,
                                              float acc, float l2, double skip = 0.0) {
     if (!(acc >= kScreenMinAcc) || !(acc <= 0x1.0p+100f) || !(X <= 1e30)) return __builtin_inf();
@@ -538,9 +538,10 @@ __device__ __forceinline__ double screen_err(float amax, int K, int Kc, double X
 // candidates only over the window of components whose term can reach
 // 2^-T for some candidate of the tile, plus the "wide" components
 // (always summed).  Every term left out is exactly < 2^-T (log2 units,
-// relative to the LSE shift), so screen_err's skip covers them; the fp64
-// re-score of the survivors still sums every component.
-constexpr int kWinTDefault = 40;   // TPE_OPT_WIN_T: the cut T, in [16, 62]
+// relative to the LSE shift); their total, bounded per bin of x'
+// (tpe_window.hip k_win_skip), enters screen_err as skip.  The fp64 re-score
+// of the survivors still sums every component.
+constexpr int kWinTDefault = 16;   // TPE_OPT_WIN_T: the cut T, in [8, 62]
 constexpr int kWinBinBits = 11;
 constexpr int kWinBins = 1 << kWinBinBits;
 

@@ -507,14 +507,17 @@ __global__ __launch_bounds__(kBlock) void k_screen(
 // atomic on the row's counter serialised ~1.3M same-address atomics at
 // config 3: 12.5 ms), then writes them.
 // The windowed screen (tpe_window.hip) leaves hi in sorted order: vmap (the
-// batch of rounds from z0 on) gives each sorted position's candidate index.
+// unit of rounds from z0 on and labels from position y0 on, nl_unit of them)
+// gives each sorted position's candidate index.
 __global__ __launch_bounds__(kBlock) void k_select(const float* __restrict__ hi, int64_t n, int32_t nl,
                                                    const unsigned long long* __restrict__ lbkey,
                                                    int32_t* __restrict__ cnt, int32_t* __restrict__ idx,
-                                                   int32_t z0, const uint64_t* __restrict__ vmap) {
-    const size_t cell = (size_t)(z0 + blockIdx.z) * nl + blockIdx.y;
+                                                   int32_t z0, int32_t y0, int32_t nl_unit,
+                                                   const uint64_t* __restrict__ vmap) {
+    const size_t cell = (size_t)(z0 + blockIdx.z) * nl + y0 + blockIdx.y;
     const size_t row = cell * (size_t)n;
-    const uint64_t* vrow = vmap ? vmap + ((size_t)blockIdx.z * nl + blockIdx.y) * (size_t)n : nullptr;
+    const uint64_t* vrow =
+        vmap ? vmap + ((size_t)blockIdx.z * nl_unit + blockIdx.y) * (size_t)n : nullptr;
     const uint64_t lb = lbkey[cell];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t span = ((n + gridDim.x - 1) / gridDim.x + kBlock - 1) / kBlock * kBlock;
@@ -1464,6 +1467,10 @@ int64_t dense_terms(const tpe_ctx* ctx) {
 
 // tile-map rounds with at least this many candidates use the windowed screen
 constexpr int64_t kWinMinN = 8192;
+// a batch of at least kWinPipeMin candidates is split into kWinGroups label
+// groups, sorted on the aux stream while the previous group is screened
+constexpr int64_t kWinPipeMin = (int64_t)1 << 26;
+constexpr int32_t kWinGroups = 4;
 
 // Packed-map sampled rounds of the dense labels, screened (see
 // k_pick_packed): fp32 chunk sums, per-round selection, fp64 re-score with
@@ -1580,21 +1587,73 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
         HIPCHK(ctx, hipMemsetAsync(ctx->scr_cnt.p, 0, cells * sizeof(int32_t), ctx->stream));
         const unsigned sx = (unsigned)std::min<int64_t>((a.n + 8 * kBlock - 1) / (8 * kBlock), 1024);
         if (ctx->window && a.n >= kWinMinN && a.cand_in == nullptr) {
-            // windowed: key + sort + screen per batch of rounds, select on the
-            // batch's sorted order
+            // windowed: units of (batch of rounds, group of labels), each
+            // keyed and sorted on the aux stream into one of two buffer
+            // slots while the main stream screens and selects the previous
+            // unit (the sort is HBM-bound, the screen VALU-bound)
             int rc = tpe_rt::win_prepare(ctx);
             if (rc) return rc;
             HIPCHK(ctx, ctx->win_evals.reserve(1));
             HIPCHK(ctx, hipMemsetAsync(ctx->win_evals.p, 0, sizeof(unsigned long long), ctx->stream));
+            struct Unit {
+                int32_t z0, nz, y0, ny;
+            };
+            std::vector<Unit> units;
             const int32_t zb = (int32_t)tpe_rt::win_rounds_per_batch(a.n, nl);
-            for (int32_t z0 = 0; z0 < a.n_rounds; z0 += zb) {
-                const int32_t nz = std::min(zb, a.n_rounds - z0);
-                const uint64_t* sorted = nullptr;
-                tpe_rt::WinScreenArgs wa{grp, nl, a.n, a.cand_offset, a.seed, z0, nz, nullptr,
+            // label groups only when a batch is big enough to hide its sort
+            const int32_t ng =
+                ctx->win_groups > 0 ? std::min<int32_t>(ctx->win_groups, nl)
+                : (a.n * (int64_t)nl * std::min(zb, a.n_rounds) >= kWinPipeMin) ? std::min<int32_t>(kWinGroups, nl)
+                                                                                : 1;
+            size_t max_total = 0;
+            int64_t max_cells = 1;
+            for (int32_t z0 = 0; z0 < a.n_rounds; z0 += zb)
+                for (int32_t g = 0; g < ng; ++g) {
+                    const int32_t y0 = (int32_t)((int64_t)nl * g / ng), y1 = (int32_t)((int64_t)nl * (g + 1) / ng);
+                    const Unit u{z0, std::min(zb, a.n_rounds - z0), y0, y1 - y0};
+                    units.push_back(u);
+                    max_total = std::max(max_total, (size_t)u.nz * u.ny * a.n);
+                    max_cells = std::max<int64_t>(max_cells, (int64_t)u.nz * u.ny);
+                }
+            const int nslots = units.size() > 1 ? 2 : 1;
+            if ((rc = tpe_rt::win_reserve(ctx, max_total, max_cells, nslots))) return rc;
+            const size_t nev = 2 * units.size();
+            while (ctx->evw.size() < nev) {
+                hipEvent_t e;
+                HIPCHK(ctx, hipEventCreate(&e));
+                ctx->evw.push_back(e);
+            }
+            ctx->evw_used = ctx->timing ? (int32_t)units.size() : 0;
+            const bool pipe = units.size() > 1;
+            if (pipe) {   // the aux stream starts after this round's setup on the main one
+                HIPCHK(ctx, hipEventRecord(ctx->ev_fork, ctx->stream));
+                HIPCHK(ctx, hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0));
+            }
+            for (size_t ui = 0; ui < units.size(); ++ui) {
+                const Unit& u = units[ui];
+                const int slot = (int)(ui & 1);
+                tpe_rt::WinScreenArgs wa{grp + u.y0, u.ny, a.n, a.cand_offset, a.seed, u.z0, u.nz, nullptr,
                                          ctx->scr_hi.p, ctx->scr_lb.p, nullptr, nullptr};
-                if ((rc = tpe_rt::win_screen(ctx, wa, &sorted))) return rc;
-                hipLaunchKernelGGL(k_select, dim3(sx, nl, nz), dim3(kBlock), 0, ctx->stream, ctx->scr_hi.p,
-                                   a.n, nl, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p, z0, sorted);
+                wa.y0 = u.y0;
+                wa.nl_all = nl;
+                wa.slot = slot;
+                const uint64_t* sorted = nullptr;
+                if (pipe) {
+                    // the slot's previous unit must be screened and selected first
+                    if (ui >= 2) HIPCHK(ctx, hipStreamWaitEvent(ctx->aux, ctx->ev_done[slot], 0));
+                    if ((rc = tpe_rt::win_sort(ctx, wa, ctx->aux, &sorted))) return rc;
+                    HIPCHK(ctx, hipEventRecord(ctx->ev_sorted[slot], ctx->aux));
+                    HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_sorted[slot], 0));
+                } else if ((rc = tpe_rt::win_sort(ctx, wa, ctx->stream, &sorted))) {
+                    return rc;
+                }
+                if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evw[2 * ui], ctx->stream));
+                if ((rc = tpe_rt::win_tiles(ctx, wa, sorted, ctx->stream))) return rc;
+                if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evw[2 * ui + 1], ctx->stream));
+                hipLaunchKernelGGL(k_select, dim3(sx, u.ny, u.nz), dim3(kBlock), 0, ctx->stream, ctx->scr_hi.p,
+                                   a.n, nl, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p, u.z0, u.y0, u.ny,
+                                   sorted);
+                if (pipe) HIPCHK(ctx, hipEventRecord(ctx->ev_done[slot], ctx->stream));
             }
             HIPCHK(ctx, hipMemcpyAsync(&ctx->screen_exec_h, ctx->win_evals.p, sizeof(unsigned long long),
                                        hipMemcpyDeviceToHost, ctx->stream));
@@ -1608,7 +1667,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                                ctx->errflag.p, a.S, nullptr, nullptr, nullptr);
             if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
             hipLaunchKernelGGL(k_select, dim3(sx, nl, a.gz), dim3(kBlock), 0, ctx->stream, ctx->scr_hi.p,
-                               a.n, nl, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p, 0, nullptr);
+                               a.n, nl, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p, 0, 0, nl, nullptr);
             ctx->screen_exec += (int64_t)a.n_rounds * a.n * dense_terms(ctx);
         }
         // the dense rows' partial slots start empty; the re-score chunks
@@ -1878,6 +1937,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
                 n_whole * rounds_whole, gx_whole};
     ctx->screen_total = ctx->screen_rescored = 0;
     ctx->screen_exec = 0;
+    ctx->evw_used = 0;
     ctx->screen_pending = false;
     ctx->screen_exec_pending = false;
     const bool sample = cand_in_dev == nullptr;
@@ -1958,7 +2018,15 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
             fprintf(stderr, "\n");
         }
         ctx->screen_pending = false;
-        if (ctx->timing) HIPCHK(ctx, hipEventElapsedTime(&ctx->screen_ms, ctx->evs[0], ctx->evs[1]));
+        if (ctx->timing && ctx->evw_used > 0) {   // windowed tile rounds: the units' k_screen_win
+            for (int32_t u = 0; u < ctx->evw_used; ++u) {
+                float ms = 0.f;
+                HIPCHK(ctx, hipEventElapsedTime(&ms, ctx->evw[2 * u], ctx->evw[2 * u + 1]));
+                ctx->screen_ms += ms;
+            }
+        } else if (ctx->timing) {
+            HIPCHK(ctx, hipEventElapsedTime(&ctx->screen_ms, ctx->evs[0], ctx->evs[1]));
+        }
     }
     if (ctx->timing) {
         HIPCHK(ctx, hipEventElapsedTime(&ctx->score_ms, ctx->ev0, ctx->ev1));
@@ -2185,6 +2253,11 @@ int tpe_ctx_create(int device, int precision, tpe_ctx** out) {
         ok = ok && hipEventCreate(&c->evm[m][0]) == hipSuccess &&
              hipEventCreate(&c->evm[m][1]) == hipSuccess;
     ok = ok && hipEventCreate(&c->evs[0]) == hipSuccess && hipEventCreate(&c->evs[1]) == hipSuccess;
+    ok = ok && hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess &&
+         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess;
+    for (int j = 0; j < 2; ++j)
+        ok = ok && hipEventCreateWithFlags(&c->ev_sorted[j], hipEventDisableTiming) == hipSuccess &&
+             hipEventCreateWithFlags(&c->ev_done[j], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         g_create_error = "stream/event creation failed";
         tpe_ctx_destroy(c);
@@ -2208,6 +2281,7 @@ TPE_DEV void tpe1_ctx_destroy(tpe_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->aux) (void)hipStreamSynchronize(c->aux);
     c->resident.release();
     c->single.release();
     c->partials.release();
@@ -2244,6 +2318,20 @@ TPE_DEV void tpe1_ctx_destroy(tpe_ctx* c) {
     c->scr_off.release();
     c->scr_planes.release();
     c->chunk_part.release();
+    for (int j = 0; j < 2; ++j) {
+        c->win_keys[j].release();
+        c->win_keys2[j].release();
+        c->win_vals[j].release();
+        c->win_vals2[j].release();
+        c->win_tmp[j].release();
+        if (c->ev_sorted[j]) (void)hipEventDestroy(c->ev_sorted[j]);
+        if (c->ev_done[j]) (void)hipEventDestroy(c->ev_done[j]);
+    }
+    c->win_evals.release();
+    c->win_lohi.release();
+    for (hipEvent_t e : c->evw) (void)hipEventDestroy(e);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->aux) (void)hipStreamDestroy(c->aux);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -2408,8 +2496,12 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
             break;
         case TPE_OPT_TIMING: ctx->timing = value != 0; break;
         case TPE_OPT_WINDOW: ctx->window = value != 0; break;
+        case TPE_OPT_WIN_GROUPS:
+            if (value < 0 || value > 64) return ctx->fail(TPE_ERR_ARG, "window groups must be in [0, 64]");
+            ctx->win_groups = (int32_t)value;
+            break;
         case TPE_OPT_WIN_T:
-            if (value < 16 || value > 62) return ctx->fail(TPE_ERR_ARG, "window cut must be in [16, 62]");
+            if (value < 8 || value > 62) return ctx->fail(TPE_ERR_ARG, "window cut must be in [8, 62]");
             ctx->win_t = (int32_t)value;
             break;
         case TPE_OPT_WHOLE_N:

@@ -7,7 +7,8 @@
 // prior_sigma / min(100, N + 1)), so only the components near a candidate can
 // move its sum.  Here:
 //
-//   per posterior (k_win_hist, k_win_seg, k_win_carry, k_win_bins; once, lazily):
+//   per posterior (k_win_hist, k_win_seg, k_win_carry, k_win_bins, k_win_skip;
+//   once, lazily):
 //     each above component's interval [lo, hi] of recentred x' where its term
 //     can reach 2^-(T + 1) (from its fp32 record; the extra 1 covers the
 //     records' rounding), the prefix max of hi and the suffix min of lo over
@@ -23,8 +24,8 @@
 //     (x' fp32, index) value, so a workgroup's 2048 candidates are neighbours;
 //     the tile's window is [k_lo(bin of its min), k_hi(bin of its max)), the
 //     below mixture and the wide components outside the window are summed in
-//     full, and the bound (screen_err) grows by the skipped mass,
-//     nskip 2^-T / S.
+//     full, and the bound (screen_err) grows by the skipped mass relative to
+//     the sum, bounded per bin of the candidate (k_win_skip).
 //
 // The selection (k_select) and the fp64 re-score (k_rescore, every
 // component) are the plain screen's, so winners and lpdfs are bit-identical
@@ -331,7 +332,8 @@ __global__ __launch_bounds__(kBlock) void k_win_carry(const DLabel* __restrict__
                                                       WinLabel* __restrict__ win, double* __restrict__ P,
                                                       double* __restrict__ Q,
                                                       const double* __restrict__ seg,
-                                                      Comp<float>* __restrict__ wide, double T) {
+                                                      Comp<float>* __restrict__ wide,
+                                                      uint8_t* __restrict__ wflag, double T) {
     const int y = blockIdx.y, li = grp[y];
     const DLabel L = labels[li];
     __shared__ double shd[kBlock / 64];
@@ -363,6 +365,7 @@ __global__ __launch_bounds__(kBlock) void k_win_carry(const DLabel* __restrict__
             P[at] = P[at] > cp ? P[at] : cp;
             Q[at] = Q[at] < cq ? Q[at] : cq;
             fl[j] = comp_interval(c[k], xhi - xlo, thr, T).wide;
+            wflag[at] = fl[j];
         }
         cnt += fl[j];
     }
@@ -379,6 +382,18 @@ __global__ __launch_bounds__(kBlock) void k_win_carry(const DLabel* __restrict__
     if (s == nseg_l - 1 && threadIdx.x == 0) win[li].n_wide = woff + tot;
 }
 
+// the recentred interval of bin b (open-ended at both ends), widened so that
+// every x' with win_bin(x') == b lies inside despite the bin arithmetic's
+// rounding
+__device__ __forceinline__ void bin_edges(const WinLabel& W, int b, double& elo, double& ehi) {
+    const double bw = 1.0 / W.inv_bw;
+    elo = b == 0 ? -kInf : W.xlo + b * bw;
+    ehi = b == kWinBins - 1 ? kInf : W.xlo + (b + 1) * bw;
+    const double slack = (fabs(W.xlo) + bw * kWinBins) * 1e-12;
+    elo -= slack;
+    ehi += slack;
+}
+
 // grid (kWinBins / kBlock, dense labels): per bin the window [k_lo, k_hi):
 // components before k_lo have hi < the bin's lower edge (P[k] < edge), those
 // from k_hi on have lo > its upper edge (Q[k] > edge)
@@ -393,12 +408,8 @@ __global__ __launch_bounds__(kBlock) void k_win_bins(const DLabel* __restrict__ 
     const WinLabel W = win[li];
     const int b = blockIdx.x * kBlock + threadIdx.x;
     if (b >= kWinBins) return;
-    const double bw = 1.0 / W.inv_bw;
-    double elo = b == 0 ? -kInf : W.xlo + b * bw;
-    double ehi = b == kWinBins - 1 ? kInf : W.xlo + (b + 1) * bw;
-    const double slack = (fabs(W.xlo) + bw * kWinBins) * 1e-12;
-    elo -= slack;
-    ehi += slack;
+    double elo, ehi;
+    bin_edges(W, b, elo, ehi);
     const double* p = P + L.comp_a;
     const double* q = Q + L.comp_a;
     int lo = 0, hi = L.na;
@@ -414,6 +425,53 @@ __global__ __launch_bounds__(kBlock) void k_win_bins(const DLabel* __restrict__ 
         if (q[mid] > ehi) hi = mid; else lo = mid + 1;
     }
     bins[(size_t)li * kWinBins + b] = int2{klo, lo > klo ? lo : klo};
+}
+
+// grid (kWinBins / kBlock, dense labels): per bin an upper bound of the
+// skipped mass, sum over the narrow (and never-relevant) components outside
+// the bin's window of the largest exact term they reach anywhere in the bin
+// (widened by the candidates' fp32 rounding, 2^-22 relative).  A tile's
+// window contains the window of every bin its candidates fall in, and its
+// wide components are summed, so this bounds the mass the tile leaves out
+// for each of its candidates.  Per component, from its fp32 record (m, a, c,
+// log2 units): distance d of the centre m/a from the bin, |z| >= d a - delta
+// with delta covering the record's rounding ((|x'| a + |m|) 2^-23), term <=
+// 2^(c + |c| 2^-22 - z^2); fp32 exp2 (2 ulp), summed in fp64, x 1.01, plus
+// na 2^-126 for the terms fp32 flushes.
+__global__ __launch_bounds__(kBlock) void k_win_skip(const DLabel* __restrict__ labels,
+                                                     const int32_t* __restrict__ grp,
+                                                     const Comp<float>* __restrict__ comps32,
+                                                     const WinLabel* __restrict__ win,
+                                                     const int2* __restrict__ bins,
+                                                     const uint8_t* __restrict__ wflag,
+                                                     double* __restrict__ skipm) {
+    const int li = grp[blockIdx.y];
+    const DLabel L = labels[li];
+    const WinLabel W = win[li];
+    const int b = blockIdx.x * kBlock + threadIdx.x;
+    const bool on = b < kWinBins;
+    double elo, ehi;
+    bin_edges(W, on ? b : 0, elo, ehi);
+    const double wl = fmax(fabs(elo) < kInf ? fabs(elo) : 0.0, fabs(ehi) < kInf ? fabs(ehi) : 0.0);
+    elo -= wl * 0x1.0p-22;
+    ehi += wl * 0x1.0p-22;
+    const int2 w = on ? bins[(size_t)li * kWinBins + b] : int2{0, 0};
+    const Comp<float>* c = comps32 + L.comp_a;
+    const uint8_t* fl = wflag + L.comp_a;
+    double acc = 0.0;
+    for (int k = 0; k < L.na; ++k) {
+        if (fl[k]) continue;                       // wide: summed by every tile
+        if (k >= w.x && k < w.y) continue;         // in the bin's window
+        const Comp<float> r = c[k];
+        const double a = r.a, m = r.mu, cc = r.c;
+        const double ctr = m / a;
+        const double d = fmax(0.0, fmax(elo - ctr, ctr - ehi));
+        const double xmax = fabs(ctr) + d;
+        const double zl = fmax(0.0, d * a * (1.0 - 1e-9) - ((xmax * a + fabs(m)) * 0x1.0p-23 + 1e-9));
+        const double t = cc + fabs(cc) * 0x1.0p-22 + 1e-9 - zl * zl;
+        if (t > -126.0) acc += (double)__builtin_amdgcn_exp2f((float)(t + 1e-6 * (1.0 + fabs(t))));
+    }
+    if (on) skipm[(size_t)li * kWinBins + b] = acc * 1.01 + (double)L.na * 0x1.0p-126;
 }
 
 // ------------------------------------------------------------- per round ----
@@ -468,16 +526,17 @@ __global__ __launch_bounds__(kBlock) void k_screen_win(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ grp,
     const Comp<float>* __restrict__ comps32, const WinLabel* __restrict__ win,
     const int2* __restrict__ bins, const Comp<float>* __restrict__ wide,
-    const uint64_t* __restrict__ vals, int64_t n, int32_t z0, int32_t nl, float* __restrict__ hi_out,
+    const double* __restrict__ skipm,
+    const uint64_t* __restrict__ vals, int64_t n, int32_t z0, int32_t nl, int32_t y0, int32_t nl_all,
+    float* __restrict__ hi_out,
     unsigned long long* __restrict__ lbkey, unsigned long long* __restrict__ terms,
-    double* __restrict__ s_out, double* __restrict__ e_out, float2* __restrict__ lohi,
-    double skip_unit) {
+    double* __restrict__ s_out, double* __restrict__ e_out, float2* __restrict__ lohi) {
     constexpr int R = kWinR;
     const int y = blockIdx.y, li = grp[y];
     const DLabel L = labels[li];
     const WinLabel W = win[li];
     const size_t bcell = (size_t)blockIdx.z * nl + y;
-    const size_t gcell = (size_t)(z0 + blockIdx.z) * nl + y;
+    const size_t gcell = (size_t)(z0 + blockIdx.z) * nl_all + y0 + y;   // the whole round's cell
     const uint64_t* vrow = vals + bcell * n;
     const int64_t t0 = (int64_t)blockIdx.x * (R * kBlock);
     float xf[R];
@@ -533,7 +592,6 @@ __global__ __launch_bounds__(kBlock) void k_screen_win(
         }
     }
     const int nwin = khi - klo;
-    const int nskip = L.na - nwin - nout;
     // summation error: the window's run (nwin / 128 + 28) u, the wide run
     // nout u, one more addition
     const int Kc = nwin + 128 * (nout + 1);
@@ -548,7 +606,8 @@ __global__ __launch_bounds__(kBlock) void k_screen_win(
         const double s = lb - la;
         const double X = fabs((double)xf[r]) * (1.0 + 0x1.0p-23);
         const double dx = X * 0x1.0p-24 + 0x1.0p-149;
-        const double skip = nskip > 0 ? (double)nskip * skip_unit * 1.01 / (double)aa[r] : 0.0;
+        // the mass left out, bounded per bin of the candidate's own x'
+        const double skip = skipm[(size_t)li * kWinBins + win_bin(W, (double)xf[r])] * 1.01 / (double)aa[r];
         const double E = 1.25 * (screen_err(L.amax_b, L.nb, L.nb, X, dx, ab[r], l2b) +
                                  screen_err(L.amax_a, L.na, Kc, X, dx, aa[r], l2a, skip) +
                                  fp64_err(L.nb + L.na, fabs(lb) + fabs(la) + X + fabs(L.centre)));
@@ -614,6 +673,8 @@ int tpe_rt::win_prepare(tpe_ctx* ctx) {
     HIPCHK(ctx, P.win_bins.reserve((size_t)P.n_labels * kWinBins));
     HIPCHK(ctx, P.win_seg.reserve((size_t)nl * nseg * 3));
     HIPCHK(ctx, P.win_hist.reserve((size_t)nl * kWidthBins));
+    HIPCHK(ctx, P.win_flag.reserve(P.comps32.cap));
+    HIPCHK(ctx, P.win_skip.reserve((size_t)P.n_labels * kWinBins));
     HIPCHK(ctx, hipMemsetAsync(P.win_hist.p, 0, (size_t)nl * kWidthBins * sizeof(int32_t), ctx->stream));
     const int32_t* grp = P.groups.p + P.group_off[DENSE_GMM];
     hipLaunchKernelGGL(k_win_hist, dim3(nseg, nl), dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
@@ -623,63 +684,106 @@ int tpe_rt::win_prepare(tpe_ctx* ctx) {
                        P.win_seg.p, T);
     hipLaunchKernelGGL(k_win_carry, dim3(nseg, nl), dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
                        P.comps32.p, P.samp.p, nseg, P.win_hist.p, P.win.p, P.win_p.p, P.win_q.p,
-                       P.win_seg.p, P.win_wide.p, T);
+                       P.win_seg.p, P.win_wide.p, P.win_flag.p, T);
     hipLaunchKernelGGL(k_win_bins, dim3(kWinBins / kBlock, nl), dim3(kBlock), 0, ctx->stream,
                        P.labels.p, grp, P.win.p, P.win_p.p, P.win_q.p, P.win_bins.p);
+    hipLaunchKernelGGL(k_win_skip, dim3(kWinBins / kBlock, nl), dim3(kBlock), 0, ctx->stream,
+                       P.labels.p, grp, P.comps32.p, P.win.p, P.win_bins.p, P.win_flag.p, P.win_skip.p);
     HIPCHK(ctx, hipGetLastError());
     P.win_ready = true;
     return TPE_OK;
 }
 
-int tpe_rt::win_screen(tpe_ctx* ctx, const WinScreenArgs& a, const uint64_t** sorted_vals) {
-    tpe_rt::Posterior& P = *ctx->P;
-    const bool probe = a.cand_in != nullptr;
+namespace {
+struct Shape {
+    int64_t ncell, cells;
+    size_t total;
+};
+Shape shape_of(const tpe_rt::WinScreenArgs& a) {
     // candidates per cell; cells: (round, label), or one per label packed
-    const int64_t ncell = a.cpack ? (int64_t)a.nz * a.cpack : a.n;
-    const int64_t cells = a.cpack ? a.nl : (int64_t)a.nz * a.nl;
-    const size_t total = (size_t)cells * ncell;
-    if (total > ((size_t)1 << 30)) return ctx->fail(TPE_ERR_ARG, "windowed screen batch too large");
-    HIPCHK(ctx, ctx->win_keys.reserve(total));
-    HIPCHK(ctx, ctx->win_keys2.reserve(total));
-    HIPCHK(ctx, ctx->win_vals.reserve(total));
-    HIPCHK(ctx, ctx->win_vals2.reserve(total));
-    const dim3 gk((unsigned)((ncell + kKeyR * kBlock - 1) / (kKeyR * kBlock)), a.nl,
-                  a.cpack ? 1 : a.nz);
-    if (probe)
-        hipLaunchKernelGGL(k_win_key<false>, gk, dim3(kBlock), 0, ctx->stream, P.labels.p, a.grp, P.samp.p,
-                           P.win.p, a.cand_in, ncell, 0, a.cand_offset, a.seed, ctx->rounds.p, a.z0,
-                           a.nl, ctx->win_keys.p, ctx->win_vals.p, ctx->errflag.p);
-    else
-        hipLaunchKernelGGL(k_win_key<true>, gk, dim3(kBlock), 0, ctx->stream, P.labels.p, a.grp, P.samp.p,
-                           P.win.p, nullptr, ncell, a.cpack, a.cand_offset, a.seed, ctx->rounds.p, a.z0,
-                           a.nl, ctx->win_keys.p, ctx->win_vals.p, ctx->errflag.p);
-    HIPCHK(ctx, hipGetLastError());
+    Shape sh;
+    sh.ncell = a.cpack ? (int64_t)a.nz * a.cpack : a.n;
+    sh.cells = a.cpack ? a.nl : (int64_t)a.nz * a.nl;
+    sh.total = (size_t)sh.cells * sh.ncell;
+    return sh;
+}
+int end_bit_of(int64_t cells) {
     int cell_bits = 0;
     while (((int64_t)1 << cell_bits) < cells) ++cell_bits;
-    const int end_bit = kWinBinBits + cell_bits;
-    hipcub::DoubleBuffer<uint32_t> kb(ctx->win_keys.p, ctx->win_keys2.p);
-    hipcub::DoubleBuffer<uint64_t> vb(ctx->win_vals.p, ctx->win_vals2.p);
-    size_t bytes = 0;
-    HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kb, vb, (int)total, 0, end_bit,
-                                                     ctx->stream));
-    HIPCHK(ctx, ctx->win_tmp.reserve(std::max<size_t>(bytes, 1)));
-    HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(ctx->win_tmp.p, bytes, kb, vb, (int)total, 0, end_bit,
-                                                     ctx->stream));
-    const uint64_t* sorted = vb.Current();
-    const double skip_unit = std::ldexp(1.0, -P.win_t);   // 2^-T of the index in use
-    const dim3 gs((unsigned)((ncell + kWinR * kBlock - 1) / (kWinR * kBlock)), a.nl,
+    return kWinBinBits + cell_bits;
+}
+}  // namespace
+
+int tpe_rt::win_reserve(tpe_ctx* ctx, size_t total, int64_t cells, int nslots) {
+    if (total > ((size_t)1 << 30)) return ctx->fail(TPE_ERR_ARG, "windowed screen batch too large");
+    for (int k = 0; k < nslots; ++k) {
+        HIPCHK(ctx, ctx->win_keys[k].reserve(total));
+        HIPCHK(ctx, ctx->win_keys2[k].reserve(total));
+        HIPCHK(ctx, ctx->win_vals[k].reserve(total));
+        HIPCHK(ctx, ctx->win_vals2[k].reserve(total));
+        hipcub::DoubleBuffer<uint32_t> kb(ctx->win_keys[k].p, ctx->win_keys2[k].p);
+        hipcub::DoubleBuffer<uint64_t> vb(ctx->win_vals[k].p, ctx->win_vals2[k].p);
+        size_t bytes = 0;
+        HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kb, vb, (int)total, 0,
+                                                         end_bit_of(cells), ctx->stream));
+        HIPCHK(ctx, ctx->win_tmp[k].reserve(std::max<size_t>(bytes, 1)));
+    }
+    return TPE_OK;
+}
+
+int tpe_rt::win_sort(tpe_ctx* ctx, const WinScreenArgs& a, hipStream_t st, const uint64_t** sorted) {
+    tpe_rt::Posterior& P = *ctx->P;
+    const Shape sh = shape_of(a);
+    const int k = a.slot;
+    if (sh.total > ctx->win_vals[k].cap || sh.total > ((size_t)1 << 30))
+        return ctx->fail(TPE_ERR_ARG, "windowed screen: slot buffers not reserved");
+    const dim3 gk((unsigned)((sh.ncell + kKeyR * kBlock - 1) / (kKeyR * kBlock)), a.nl,
                   a.cpack ? 1 : a.nz);
-    if (ctx->timing && !probe && a.z0 == 0) HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
-    if (probe)
-        hipLaunchKernelGGL(k_screen_win<true>, gs, dim3(kBlock), 0, ctx->stream, P.labels.p, a.grp,
-                           P.comps32.p, P.win.p, P.win_bins.p, P.win_wide.p, sorted, ncell, a.z0,
-                           a.nl, nullptr, nullptr, nullptr, a.s_out, a.e_out, nullptr, skip_unit);
+    if (a.cand_in)
+        hipLaunchKernelGGL(k_win_key<false>, gk, dim3(kBlock), 0, st, P.labels.p, a.grp, P.samp.p,
+                           P.win.p, a.cand_in, sh.ncell, 0, a.cand_offset, a.seed, ctx->rounds.p, a.z0,
+                           a.nl, ctx->win_keys[k].p, ctx->win_vals[k].p, ctx->errflag.p);
     else
-        hipLaunchKernelGGL(k_screen_win<false>, gs, dim3(kBlock), 0, ctx->stream, P.labels.p, a.grp,
-                           P.comps32.p, P.win.p, P.win_bins.p, P.win_wide.p, sorted, ncell, a.z0,
-                           a.nl, a.hi, a.lbkey, ctx->win_evals.p, nullptr, nullptr, a.lohi, skip_unit);
-    if (ctx->timing && !probe) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
+        hipLaunchKernelGGL(k_win_key<true>, gk, dim3(kBlock), 0, st, P.labels.p, a.grp, P.samp.p,
+                           P.win.p, nullptr, sh.ncell, a.cpack, a.cand_offset, a.seed, ctx->rounds.p,
+                           a.z0, a.nl, ctx->win_keys[k].p, ctx->win_vals[k].p, ctx->errflag.p);
     HIPCHK(ctx, hipGetLastError());
-    *sorted_vals = sorted;
+    hipcub::DoubleBuffer<uint32_t> kb(ctx->win_keys[k].p, ctx->win_keys2[k].p);
+    hipcub::DoubleBuffer<uint64_t> vb(ctx->win_vals[k].p, ctx->win_vals2[k].p);
+    size_t bytes = ctx->win_tmp[k].cap;
+    HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(ctx->win_tmp[k].p, bytes, kb, vb, (int)sh.total, 0,
+                                                     end_bit_of(sh.cells), st));
+    *sorted = vb.Current();
+    return TPE_OK;
+}
+
+int tpe_rt::win_tiles(tpe_ctx* ctx, const WinScreenArgs& a, const uint64_t* sorted, hipStream_t st) {
+    tpe_rt::Posterior& P = *ctx->P;
+    const Shape sh = shape_of(a);
+    const dim3 gs((unsigned)((sh.ncell + kWinR * kBlock - 1) / (kWinR * kBlock)), a.nl,
+                  a.cpack ? 1 : a.nz);
+    const int32_t nl_all = a.nl_all ? a.nl_all : a.nl;
+    if (a.cand_in)
+        hipLaunchKernelGGL(k_screen_win<true>, gs, dim3(kBlock), 0, st, P.labels.p, a.grp, P.comps32.p,
+                           P.win.p, P.win_bins.p, P.win_wide.p, P.win_skip.p, sorted, sh.ncell, a.z0,
+                           a.nl, a.y0, nl_all, nullptr, nullptr, nullptr, a.s_out, a.e_out, nullptr);
+    else
+        hipLaunchKernelGGL(k_screen_win<false>, gs, dim3(kBlock), 0, st, P.labels.p, a.grp, P.comps32.p,
+                           P.win.p, P.win_bins.p, P.win_wide.p, P.win_skip.p, sorted, sh.ncell, a.z0,
+                           a.nl, a.y0, nl_all, a.hi, a.lbkey, ctx->win_evals.p, nullptr, nullptr, a.lohi);
+    return ctx->hip(hipGetLastError(), "k_screen_win launch");
+}
+
+int tpe_rt::win_screen(tpe_ctx* ctx, const WinScreenArgs& a, const uint64_t** sorted_vals) {
+    const Shape sh = shape_of(a);
+    int rc = win_reserve(ctx, sh.total, sh.cells, 1);
+    if (rc) return rc;
+    WinScreenArgs b = a;
+    b.slot = 0;
+    if ((rc = win_sort(ctx, b, ctx->stream, sorted_vals))) return rc;
+    const bool timed = ctx->timing && !a.cand_in;
+    if (timed) HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
+    if ((rc = win_tiles(ctx, b, *sorted_vals, ctx->stream))) return rc;
+    if (timed) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
     return TPE_OK;
 }

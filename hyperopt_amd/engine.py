@@ -248,12 +248,14 @@ class Engine(object):
     OPTIONS = {'screen': L.TPE_OPT_SCREEN, 'splitk': L.TPE_OPT_SPLITK, 'dedup': L.TPE_OPT_DEDUP,
                'chunks': L.TPE_OPT_CHUNKS, 'whole_n': L.TPE_OPT_WHOLE_N,
                'whole_rounds': L.TPE_OPT_WHOLE_ROUNDS, 'timing': L.TPE_OPT_TIMING,
-               'window': L.TPE_OPT_WINDOW, 'win_t': L.TPE_OPT_WIN_T}
+               'window': L.TPE_OPT_WINDOW, 'win_t': L.TPE_OPT_WIN_T,
+               'win_groups': L.TPE_OPT_WIN_GROUPS}
 
     def set_option(self, name, value):
         """Engine switches (include/hyperopt_tpe.h TPE_OPT_*): 'screen',
         'splitk', 'dedup', 'timing', 'window' (bool), 'chunks' (int, 0 = auto),
-        'win_t' (the windowed screen's cut, 16..62),
+        'win_t' (the windowed screen's cut, 8..62), 'win_groups' (label
+        groups pipelined over two streams, 0 = auto),
         'whole_n' / 'whole_rounds' (the whole problem when this engine runs
         one shard of it, 0 = the call's own)."""
         self._check(self.lib.tpe_set_option(self.h, self.OPTIONS[name], int(value)))

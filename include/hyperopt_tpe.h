@@ -326,7 +326,10 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *                   into tiles of neighbours, each summed over the window of
  *                   components that can matter to it                   [1]
  *   TPE_OPT_WIN_T   the windowed screen's cut T: components left out of a
- *                   tile stay below 2^-T of the largest term (16..62)   [40]
+ *                   tile stay below 2^-T of the largest term (8..62)    [16]
+ *   TPE_OPT_WIN_GROUPS  label groups of a windowed round, each sorted on a
+ *                   second stream while the previous one is screened
+ *                   (0: 4 for rounds of >= 2^26 candidates, else 1)      [0]
  *   TPE_OPT_TIMING  HIP-event timing of every round (tpe_last_timing,
  *                   tpe_last_mode_stats, tpe_last_screen's ms); off saves
  *                   ~20 event calls per round on latency-bound calls   [1]
@@ -346,6 +349,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_TIMING 7
 #define TPE_OPT_WINDOW 8
 #define TPE_OPT_WIN_T 9
+#define TPE_OPT_WIN_GROUPS 10
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
 
 #ifdef __cplusplus

@@ -28,11 +28,14 @@ def eng():
     e.close()
 
 
-@pytest.mark.parametrize('window', [1, 0])
-def test_screen_bound_holds(eng, window):
+@pytest.mark.parametrize('window,win_t', [(1, 40), (1, 16), (1, 8), (0, 16)])
+def test_screen_bound_holds(eng, window, win_t):
     """window=1: the probe goes through the windowed screen (candidates
     sorted into tiles of neighbours, components outside a tile's window left
-    out and covered by the bound's skip term)."""
+    out and covered by the bound's skip term); at win_t = 16 (the default)
+    and 8 the terms left out reach 2^-16 / 2^-8 of the largest, where the
+    per-bin skipped-mass bound carries real weight (at 8 it is the rigour,
+    not the certification rate, that is checked)."""
     from hyperopt_amd import posterior as P
     from hyperopt_amd.workloads import mixed_history
     hist = mixed_history(32, 10000, seed=0)
@@ -51,21 +54,25 @@ def test_screen_bound_holds(eng, window):
             extra = np.exp(np.linspace(p.low, p.high, 2001))
         x = np.concatenate([x, extra])
         eng.set_option('window', window)
+        eng.set_option('win_t', win_t)
         try:
             s32, err = eng.screen_probe(li, x)
         finally:
             eng.set_option('window', 1)
+            eng.set_option('win_t', 16)
         lb, la, _ = eng.score(li, x)
         s64 = lb - la
         ok = np.isfinite(err) & np.isfinite(s64)
         cert.append(ok.mean())
         assert np.all(np.abs(s32[ok] - s64[ok]) <= err[ok]), li
         worst = max(worst, float(np.max(np.abs(s32[ok] - s64[ok]) / err[ok])))
-    # the bound is rigorous, not tight: observed error well inside it
-    assert worst < 0.5, worst
-    assert min(cert) > 0.9, cert
-    print('screen bound (window %d): worst |s32 - s64| / bound = %.3g, certified %.4f..%.4f'
-          % (window, worst, min(cert), max(cert)))
+    # the bound is rigorous, and (but for T = 8, where the skipped mass is a
+    # real share of the fp32 error) not tight
+    assert worst < (1.0 if win_t < 16 else 0.5), worst
+    if win_t >= 16:
+        assert min(cert) > 0.9, cert
+    print('screen bound (window %d, T %d): worst |s32 - s64| / bound = %.3g, certified %.4f..%.4f'
+          % (window, win_t, worst, min(cert), max(cert)))
 
 
 def _suggest_both(eng, C, rnd, seed):
@@ -185,18 +192,26 @@ def test_windowed_screen_skips_terms(eng):
     assert 0 < frac < 0.35
 
 
-def test_windowed_screen_batched_rounds(eng):
+@pytest.mark.parametrize('groups', [0, 3, 5])
+def test_windowed_screen_batched_rounds(eng, groups):
     """Several tile-map rounds in one call (grid.z): keys carry the round,
-    so each round's candidates are sorted and selected on their own."""
+    so each round's candidates are sorted and selected on their own.
+    groups > 0: the labels in that many groups, each keyed and sorted on the
+    second stream while the previous group is screened (two buffer slots,
+    so 3 and 5 groups reuse them)."""
     from hyperopt_amd import posterior as P
     from hyperopt_amd.workloads import mixed_history
     hist = mixed_history(24, 6000, seed=4)
     eng.set_posterior(*P.pack(hist.posteriors()))
     ids = [11, 12, 13]
-    a = eng.suggest_batch(5, ids, 1 << 15)
-    screened, rescored = eng.last_screen()
-    eng.set_option('screen', 0)
-    b = eng.suggest_batch(5, ids, 1 << 15)
-    eng.set_option('screen', 1)
+    eng.set_option('win_groups', groups)
+    try:
+        a = eng.suggest_batch(5, ids, 1 << 15)
+        screened, rescored = eng.last_screen()
+        eng.set_option('screen', 0)
+        b = eng.suggest_batch(5, ids, 1 << 15)
+        eng.set_option('screen', 1)
+    finally:
+        eng.set_option('win_groups', 0)
     _assert_same(a, b)
     assert 0 < rescored < screened
