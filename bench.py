@@ -89,6 +89,8 @@ def parse():
                     help='f64: the plain fp32 screen (every term) instead of the windowed one')
     ap.add_argument('--win-t', type=int, default=16,
                     help='the windowed screen\'s cut T (components left out stay below 2^-T)')
+    ap.add_argument('--win-groups', type=int, default=0,
+                    help='label groups of a windowed round sorted on a second stream (0 = auto)')
     ap.add_argument('--unscreened-steps', type=int, default=3,
                     help='f64: steps of the plain fp64 round timed after the main run, for '
                          'comparison (0 = skip)')
@@ -312,6 +314,7 @@ def main():
     eng.set_option('screen', int(screen))
     eng.set_option('window', int(not args.no_window))
     eng.set_option('win_t', args.win_t)
+    eng.set_option('win_groups', args.win_groups)
     if world > 1:   # this rank holds one shard: size-dependent choices follow the whole round
         eng.set_option('whole_rounds' if args.config == 5 else 'whole_n',
                        args.new_ids if args.config == 5 else C_total)

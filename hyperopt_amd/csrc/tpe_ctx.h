@@ -80,6 +80,7 @@ struct Posterior {
     DevBuf<int32_t> win_hist;            // per label position: histogram of log2 interval widths
     DevBuf<uint8_t> win_flag;            // per component: 1 = wide
     DevBuf<double> win_skip;             // per label: kWinBins bounds of the mass a bin's window skips
+    DevBuf<double> win_skip_part;        //   their partial sums per chunk of components
     void release() {
         labels.release();
         comps64.release();
@@ -96,6 +97,7 @@ struct Posterior {
         win_hist.release();
         win_flag.release();
         win_skip.release();
+        win_skip_part.release();
         win_ready = false;
         n_labels = 0;
     }
@@ -236,6 +238,7 @@ struct tpe_ctx {
     int32_t win_t = tpe::kWinTDefault;   // TPE_OPT_WIN_T
     int32_t win_groups = 0;              // TPE_OPT_WIN_GROUPS (0: auto)
     DevBuf<uint32_t> win_keys[2], win_keys2[2];   // two slots: sort of group g + 1
+    DevBuf<uint8_t> win_keys8[2], win_keys8b[2];  //   (coarse per-cell keys of large cells)
     DevBuf<uint64_t> win_vals[2], win_vals2[2];   //   while group g is screened
     DevBuf<uint8_t> win_tmp[2];
     hipStream_t aux = nullptr;           // key + sort of the next label group

@@ -563,12 +563,20 @@ __global__ __launch_bounds__(kBlock) void k_fill_empty(const int32_t* __restrict
         prow[t] = Partial{0, INT64_MAX, 0.0, 0.0, 0.0};
 }
 
-// One workgroup per kR * 256 re-scored candidates of one (round, label)
-// (chunk table from the host: cell = round * nl + label position, chunk j
-// writes partial slot j of its row -- j < tiles because the row holds at
-// most n candidates).  Sized after the counts are read back, so the
-// hardware scheduler balances the chunks over the chip.
+// One workgroup per kRescoreR * 256 re-scored candidates of one (round,
+// label) (chunk table from the host: cell = round * nl + label position);
+// each writes its block maxloc to res[chunk], and k_rescore_merge keeps
+// each cell's best.  Sized after the counts are read back, so the hardware
+// scheduler balances the chunks over the chip.
 using RescoreChunk = tpe_rt::RescoreChunkH;
+
+// candidates per thread in k_rescore: config 3 re-scores ~24k candidates
+// per (round, label), ~3k workgroups at 2 per thread (4: 3.75 ms at ~2
+// workgroups per CU)
+#ifndef TPE_RESCORE_R
+#define TPE_RESCORE_R 2
+#endif
+constexpr int kRescoreR = TPE_RESCORE_R;
 
 // candidates per thread in k_screen (its own tile width): the component's
 // m shared by more candidates costs fewer v_mov_b64 per eval
@@ -583,11 +591,10 @@ __global__ __launch_bounds__(kBlock) void k_rescore(
     const Comp<double>* __restrict__ comps64, const SampRec* __restrict__ samp, int64_t n,
     int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, int32_t nl,
     int32_t n_labels, int32_t tiles, const int32_t* __restrict__ cnt, const int32_t* __restrict__ idx,
-    const RescoreChunk* __restrict__ chunks, Partial* __restrict__ partials) {
+    const RescoreChunk* __restrict__ chunks, Partial* __restrict__ res) {
     const RescoreChunk ch = chunks[blockIdx.x];
     const int32_t z = ch.cell / nl, y = ch.cell % nl;
     const int li = group[y];
-    Partial* prow = partials + ((size_t)z * n_labels + li) * tiles;
     const int64_t count = cnt[ch.cell];
     constexpr int64_t per = (int64_t)R * kBlock;
     const int64_t base = (int64_t)ch.j * per;
@@ -635,7 +642,27 @@ __global__ __launch_bounds__(kBlock) void k_rescore(
         }
     }
     __shared__ Partial sh[kBlock / 64];
-    block_maxloc(bk, bi, bv, bl, ba, prow + ch.j, sh);
+    block_maxloc(bk, bi, bv, bl, ba, res + blockIdx.x, sh);
+    (void)z;
+}
+
+// one thread per (round, dense label) cell: the best of its re-score chunks
+// (consecutive in the table from first = range >> 32, count = low bits) into
+// the row's first partial slot (k_fill_empty cleared the row)
+__global__ __launch_bounds__(kBlock) void k_rescore_merge(const int32_t* __restrict__ group, int32_t nl,
+                                                          int64_t cells, int32_t n_labels, int32_t tiles,
+                                                          const int64_t* __restrict__ range,
+                                                          const Partial* __restrict__ res,
+                                                          Partial* __restrict__ partials) {
+    const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (c >= cells) return;
+    const int64_t first = range[c] >> 32, count = range[c] & 0xffffffffll;
+    if (count == 0) return;
+    Partial best = res[first];
+    for (int64_t j = 1; j < count; ++j)
+        if (better(res[first + j].key, res[first + j].idx, best.key, best.idx)) best = res[first + j];
+    const int64_t z = c / nl;
+    partials[((size_t)z * n_labels + group[c % nl]) * tiles] = best;
 }
 
 // ---------------------------------------- fp32 screen (packed map) ----
@@ -1467,10 +1494,10 @@ int64_t dense_terms(const tpe_ctx* ctx) {
 
 // tile-map rounds with at least this many candidates use the windowed screen
 constexpr int64_t kWinMinN = 8192;
-// a batch of at least kWinPipeMin candidates is split into kWinGroups label
-// groups, sorted on the aux stream while the previous group is screened
-constexpr int64_t kWinPipeMin = (int64_t)1 << 26;
-constexpr int32_t kWinGroups = 4;
+// TPE_OPT_WIN_GROUPS > 1 splits a batch into label groups, each sorted on
+// the aux stream while the previous group is screened.  Off by default: the
+// chip is busy either way (config 3: 47.6 ms in one group, 47.1 in 2, 47.1
+// in 4, 47.2 in 8), and one group keeps k_screen_win's own time clean.
 
 // Packed-map sampled rounds of the dense labels, screened (see
 // k_pick_packed): fp32 chunk sums, per-round selection, fp64 re-score with
@@ -1587,10 +1614,10 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
         HIPCHK(ctx, hipMemsetAsync(ctx->scr_cnt.p, 0, cells * sizeof(int32_t), ctx->stream));
         const unsigned sx = (unsigned)std::min<int64_t>((a.n + 8 * kBlock - 1) / (8 * kBlock), 1024);
         if (ctx->window && a.n >= kWinMinN && a.cand_in == nullptr) {
-            // windowed: units of (batch of rounds, group of labels), each
-            // keyed and sorted on the aux stream into one of two buffer
-            // slots while the main stream screens and selects the previous
-            // unit (the sort is HBM-bound, the screen VALU-bound)
+            // windowed: units of (batch of rounds, group of labels); with
+            // several units each is keyed and sorted on the aux stream into
+            // one of two buffer slots while the main stream screens and
+            // selects the previous one
             int rc = tpe_rt::win_prepare(ctx);
             if (rc) return rc;
             HIPCHK(ctx, ctx->win_evals.reserve(1));
@@ -1601,10 +1628,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
             std::vector<Unit> units;
             const int32_t zb = (int32_t)tpe_rt::win_rounds_per_batch(a.n, nl);
             // label groups only when a batch is big enough to hide its sort
-            const int32_t ng =
-                ctx->win_groups > 0 ? std::min<int32_t>(ctx->win_groups, nl)
-                : (a.n * (int64_t)nl * std::min(zb, a.n_rounds) >= kWinPipeMin) ? std::min<int32_t>(kWinGroups, nl)
-                                                                                : 1;
+            const int32_t ng = ctx->win_groups > 0 ? std::min<int32_t>(ctx->win_groups, nl) : 1;
             size_t max_total = 0;
             int64_t max_cells = 1;
             for (int32_t z0 = 0; z0 < a.n_rounds; z0 += zb)
@@ -1678,20 +1702,31 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
         HIPCHK(ctx, hipMemcpyAsync(ctx->scr_cnt_h.data(), ctx->scr_cnt.p, cells * sizeof(int32_t),
                                    hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-        constexpr int64_t per = (int64_t)kR * kBlock;
+        constexpr int64_t per = (int64_t)kRescoreR * kBlock;
         std::vector<RescoreChunk>& tab = ctx->scr_chunks_h;
         tab.clear();
-        for (size_t c = 0; c < cells; ++c)
+        std::vector<int64_t> range(cells);
+        for (size_t c = 0; c < cells; ++c) {
+            const int64_t first = (int64_t)tab.size();
             for (int32_t j = 0; (int64_t)j * per < ctx->scr_cnt_h[c]; ++j) tab.push_back(RescoreChunk{(int32_t)c, j});
+            range[c] = (first << 32) | ((int64_t)tab.size() - first);
+        }
         if (!tab.empty()) {
             HIPCHK(ctx, ctx->scr_chunks.reserve(tab.size()));
+            HIPCHK(ctx, ctx->scr_res.reserve(tab.size()));
+            HIPCHK(ctx, ctx->scr_off.reserve(cells));
             HIPCHK(ctx, hipMemcpyAsync(ctx->scr_chunks.p, tab.data(), tab.size() * sizeof(RescoreChunk),
                                        hipMemcpyHostToDevice, ctx->stream));
-            hipLaunchKernelGGL((k_rescore<kR>), dim3((unsigned)tab.size()), dim3(kBlock), 0, ctx->stream,
+            HIPCHK(ctx, hipMemcpyAsync(ctx->scr_off.p, range.data(), cells * sizeof(int64_t),
+                                       hipMemcpyHostToDevice, ctx->stream));
+            hipLaunchKernelGGL((k_rescore<kRescoreR>), dim3((unsigned)tab.size()), dim3(kBlock), 0, ctx->stream,
                                ctx->P->labels.p, grp, ctx->P->comps64.p, ctx->P->samp.p, a.n,
                                a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->P->n_labels, a.tiles,
                                ctx->scr_cnt.p, ctx->scr_idx.p,
-                               reinterpret_cast<const RescoreChunk*>(ctx->scr_chunks.p), ctx->partials.p);
+                               reinterpret_cast<const RescoreChunk*>(ctx->scr_chunks.p), ctx->scr_res.p);
+            hipLaunchKernelGGL(k_rescore_merge, dim3((unsigned)((cells + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                               ctx->stream, grp, nl, (int64_t)cells, ctx->P->n_labels, a.tiles, ctx->scr_off.p,
+                               ctx->scr_res.p, ctx->partials.p);
         }
         ctx->screen_total += (int64_t)cells * a.n;
         ctx->screen_pending = true;
@@ -2321,6 +2356,8 @@ TPE_DEV void tpe1_ctx_destroy(tpe_ctx* c) {
     for (int j = 0; j < 2; ++j) {
         c->win_keys[j].release();
         c->win_keys2[j].release();
+        c->win_keys8[j].release();
+        c->win_keys8b[j].release();
         c->win_vals[j].release();
         c->win_vals2[j].release();
         c->win_tmp[j].release();

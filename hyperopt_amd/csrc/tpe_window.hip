@@ -50,6 +50,8 @@ constexpr int kSeg = kSegR * kBlock;     // components per prep workgroup
 constexpr int kKeyR = 4;                 // candidates per thread, k_win_key
 constexpr int kWinR = 8;                 // candidates per thread, k_screen_win (tile 2048)
 constexpr double kInf = __builtin_inf();
+constexpr int kCoarseBits = 8;                    // per-cell sort key: bin >> 3
+constexpr int64_t kCellSortMin = (int64_t)1 << 20;
 
 // ---------------------------------------------------------- block helpers ----
 struct MaxOp {
@@ -438,13 +440,19 @@ __global__ __launch_bounds__(kBlock) void k_win_bins(const DLabel* __restrict__ 
 // with delta covering the record's rounding ((|x'| a + |m|) 2^-23), term <=
 // 2^(c + |c| 2^-22 - z^2); fp32 exp2 (2 ulp), summed in fp64, x 1.01, plus
 // na 2^-126 for the terms fp32 flushes.
+//
+// grid (kWinBins / kBlock, dense labels, component chunks of kSkipChunk):
+// each chunk's partial sum per bin into part[(y nchunk + chunk) kWinBins + b];
+// k_win_skip_sum adds the chunks in order (deterministic).
+constexpr int kSkipChunk = 1024;
+
 __global__ __launch_bounds__(kBlock) void k_win_skip(const DLabel* __restrict__ labels,
                                                      const int32_t* __restrict__ grp,
                                                      const Comp<float>* __restrict__ comps32,
                                                      const WinLabel* __restrict__ win,
                                                      const int2* __restrict__ bins,
                                                      const uint8_t* __restrict__ wflag,
-                                                     double* __restrict__ skipm) {
+                                                     double* __restrict__ part) {
     const int li = grp[blockIdx.y];
     const DLabel L = labels[li];
     const WinLabel W = win[li];
@@ -459,7 +467,8 @@ __global__ __launch_bounds__(kBlock) void k_win_skip(const DLabel* __restrict__ 
     const Comp<float>* c = comps32 + L.comp_a;
     const uint8_t* fl = wflag + L.comp_a;
     double acc = 0.0;
-    for (int k = 0; k < L.na; ++k) {
+    const int k0 = blockIdx.z * kSkipChunk, k1 = min(L.na, k0 + kSkipChunk);
+    for (int k = k0; k < k1; ++k) {
         if (fl[k]) continue;                       // wide: summed by every tile
         if (k >= w.x && k < w.y) continue;         // in the bin's window
         const Comp<float> r = c[k];
@@ -471,7 +480,20 @@ __global__ __launch_bounds__(kBlock) void k_win_skip(const DLabel* __restrict__ 
         const double t = cc + fabs(cc) * 0x1.0p-22 + 1e-9 - zl * zl;
         if (t > -126.0) acc += (double)__builtin_amdgcn_exp2f((float)(t + 1e-6 * (1.0 + fabs(t))));
     }
-    if (on) skipm[(size_t)li * kWinBins + b] = acc * 1.01 + (double)L.na * 0x1.0p-126;
+    if (on) part[((size_t)blockIdx.y * gridDim.z + blockIdx.z) * kWinBins + b] = acc;
+}
+
+__global__ __launch_bounds__(kBlock) void k_win_skip_sum(const DLabel* __restrict__ labels,
+                                                         const int32_t* __restrict__ grp, int32_t nchunk,
+                                                         const double* __restrict__ part,
+                                                         double* __restrict__ skipm) {
+    const int li = grp[blockIdx.y];
+    const int b = blockIdx.x * kBlock + threadIdx.x;
+    if (b >= kWinBins) return;
+    const int nc = (labels[li].na + kSkipChunk - 1) / kSkipChunk;
+    double acc = 0.0;
+    for (int c = 0; c < nc; ++c) acc += part[((size_t)blockIdx.y * nchunk + c) * kWinBins + b];
+    skipm[(size_t)li * kWinBins + b] = acc * 1.01 + (double)labels[li].na * 0x1.0p-126;
 }
 
 // ------------------------------------------------------------- per round ----
@@ -480,14 +502,17 @@ __global__ __launch_bounds__(kBlock) void k_win_skip(const DLabel* __restrict__ 
 // position ((z - z0) nl + y) n + i.  The candidates are drawn exactly as the
 // plain screen and the fp64 round draw them.
 // Packed (cpack = C > 0, grid.z = 1): one cell per label, candidate j = z C
-// + i of round z0 + z, value index j.
+// + i of round z0 + z, value index j.  keys8: cells of >= kCellSortMin
+// candidates are sorted one by one on a coarse 8-bit bin (one radix pass;
+// the windows still come from the fine bins of each tile's min and max).
 template <bool SAMPLE>
 __global__ __launch_bounds__(kBlock) void k_win_key(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ grp,
     const SampRec* __restrict__ samp, const WinLabel* __restrict__ win,
     const double* __restrict__ cand_in, int64_t ncell, int32_t cpack, int64_t cand_offset,
     uint64_t seed, const uint32_t* __restrict__ rounds, int32_t z0, int32_t nl,
-    uint32_t* __restrict__ keys, uint64_t* __restrict__ vals, int32_t* __restrict__ err) {
+    uint32_t* __restrict__ keys, uint8_t* __restrict__ keys8, uint64_t* __restrict__ vals,
+    int32_t* __restrict__ err) {
     const int y = blockIdx.y, li = grp[y];
     const DLabel L = labels[li];
     const WinLabel W = win[li];
@@ -513,7 +538,9 @@ __global__ __launch_bounds__(kBlock) void k_win_key(
         }
         const double xr = (lgmm ? log(v) : v) - L.centre;
         const size_t pos = (size_t)cell * ncell + j;
-        keys[pos] = (cell << kWinBinBits) | (uint32_t)win_bin(W, xr);
+        const uint32_t bin = (uint32_t)win_bin(W, xr);
+        if (keys8) keys8[pos] = (uint8_t)(bin >> (kWinBinBits - kCoarseBits));
+        else keys[pos] = (cell << kWinBinBits) | bin;
         vals[pos] = ((uint64_t)__float_as_uint((float)xr) << 32) | (uint32_t)j;
     }
 }
@@ -687,8 +714,13 @@ int tpe_rt::win_prepare(tpe_ctx* ctx) {
                        P.win_seg.p, P.win_wide.p, P.win_flag.p, T);
     hipLaunchKernelGGL(k_win_bins, dim3(kWinBins / kBlock, nl), dim3(kBlock), 0, ctx->stream,
                        P.labels.p, grp, P.win.p, P.win_p.p, P.win_q.p, P.win_bins.p);
-    hipLaunchKernelGGL(k_win_skip, dim3(kWinBins / kBlock, nl), dim3(kBlock), 0, ctx->stream,
-                       P.labels.p, grp, P.comps32.p, P.win.p, P.win_bins.p, P.win_flag.p, P.win_skip.p);
+    const int nchunk = (na_max + kSkipChunk - 1) / kSkipChunk;
+    HIPCHK(ctx, P.win_skip_part.reserve((size_t)nl * nchunk * kWinBins));
+    hipLaunchKernelGGL(k_win_skip, dim3(kWinBins / kBlock, nl, nchunk), dim3(kBlock), 0, ctx->stream,
+                       P.labels.p, grp, P.comps32.p, P.win.p, P.win_bins.p, P.win_flag.p,
+                       P.win_skip_part.p);
+    hipLaunchKernelGGL(k_win_skip_sum, dim3(kWinBins / kBlock, nl), dim3(kBlock), 0, ctx->stream,
+                       P.labels.p, grp, nchunk, P.win_skip_part.p, P.win_skip.p);
     HIPCHK(ctx, hipGetLastError());
     P.win_ready = true;
     return TPE_OK;
@@ -716,16 +748,27 @@ int end_bit_of(int64_t cells) {
 
 int tpe_rt::win_reserve(tpe_ctx* ctx, size_t total, int64_t cells, int nslots) {
     if (total > ((size_t)1 << 30)) return ctx->fail(TPE_ERR_ARG, "windowed screen batch too large");
+    const int64_t ncell = (int64_t)(total / (size_t)std::max<int64_t>(cells, 1));
+    const bool per_cell = ncell >= kCellSortMin;
     for (int k = 0; k < nslots; ++k) {
-        HIPCHK(ctx, ctx->win_keys[k].reserve(total));
-        HIPCHK(ctx, ctx->win_keys2[k].reserve(total));
         HIPCHK(ctx, ctx->win_vals[k].reserve(total));
         HIPCHK(ctx, ctx->win_vals2[k].reserve(total));
-        hipcub::DoubleBuffer<uint32_t> kb(ctx->win_keys[k].p, ctx->win_keys2[k].p);
-        hipcub::DoubleBuffer<uint64_t> vb(ctx->win_vals[k].p, ctx->win_vals2[k].p);
         size_t bytes = 0;
-        HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kb, vb, (int)total, 0,
-                                                         end_bit_of(cells), ctx->stream));
+        if (per_cell) {
+            HIPCHK(ctx, ctx->win_keys8[k].reserve(total));
+            HIPCHK(ctx, ctx->win_keys8b[k].reserve(total));
+            hipcub::DoubleBuffer<uint8_t> kb(ctx->win_keys8[k].p, ctx->win_keys8b[k].p);
+            hipcub::DoubleBuffer<uint64_t> vb(ctx->win_vals[k].p, ctx->win_vals2[k].p);
+            HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kb, vb, (int)ncell, 0,
+                                                             kCoarseBits, ctx->stream));
+        } else {
+            HIPCHK(ctx, ctx->win_keys[k].reserve(total));
+            HIPCHK(ctx, ctx->win_keys2[k].reserve(total));
+            hipcub::DoubleBuffer<uint32_t> kb(ctx->win_keys[k].p, ctx->win_keys2[k].p);
+            hipcub::DoubleBuffer<uint64_t> vb(ctx->win_vals[k].p, ctx->win_vals2[k].p);
+            HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, kb, vb, (int)total, 0,
+                                                             end_bit_of(cells), ctx->stream));
+        }
         HIPCHK(ctx, ctx->win_tmp[k].reserve(std::max<size_t>(bytes, 1)));
     }
     return TPE_OK;
@@ -735,19 +778,39 @@ int tpe_rt::win_sort(tpe_ctx* ctx, const WinScreenArgs& a, hipStream_t st, const
     tpe_rt::Posterior& P = *ctx->P;
     const Shape sh = shape_of(a);
     const int k = a.slot;
-    if (sh.total > ctx->win_vals[k].cap || sh.total > ((size_t)1 << 30))
+    const bool per_cell = sh.ncell >= kCellSortMin;
+    if (sh.total > ctx->win_vals[k].cap || sh.total > ((size_t)1 << 30) ||
+        sh.total > (per_cell ? ctx->win_keys8[k].cap : ctx->win_keys[k].cap))
         return ctx->fail(TPE_ERR_ARG, "windowed screen: slot buffers not reserved");
+    uint32_t* keys = per_cell ? nullptr : ctx->win_keys[k].p;
+    uint8_t* keys8 = per_cell ? ctx->win_keys8[k].p : nullptr;
     const dim3 gk((unsigned)((sh.ncell + kKeyR * kBlock - 1) / (kKeyR * kBlock)), a.nl,
                   a.cpack ? 1 : a.nz);
     if (a.cand_in)
         hipLaunchKernelGGL(k_win_key<false>, gk, dim3(kBlock), 0, st, P.labels.p, a.grp, P.samp.p,
                            P.win.p, a.cand_in, sh.ncell, 0, a.cand_offset, a.seed, ctx->rounds.p, a.z0,
-                           a.nl, ctx->win_keys[k].p, ctx->win_vals[k].p, ctx->errflag.p);
+                           a.nl, keys, keys8, ctx->win_vals[k].p, ctx->errflag.p);
     else
         hipLaunchKernelGGL(k_win_key<true>, gk, dim3(kBlock), 0, st, P.labels.p, a.grp, P.samp.p,
                            P.win.p, nullptr, sh.ncell, a.cpack, a.cand_offset, a.seed, ctx->rounds.p,
-                           a.z0, a.nl, ctx->win_keys[k].p, ctx->win_vals[k].p, ctx->errflag.p);
+                           a.z0, a.nl, keys, keys8, ctx->win_vals[k].p, ctx->errflag.p);
     HIPCHK(ctx, hipGetLastError());
+    if (per_cell) {   // one single-pass sort per cell, all ending in the same buffer
+        const uint64_t* out = nullptr;
+        for (int64_t c = 0; c < sh.cells; ++c) {
+            const size_t off = (size_t)c * sh.ncell;
+            hipcub::DoubleBuffer<uint8_t> kb(ctx->win_keys8[k].p + off, ctx->win_keys8b[k].p + off);
+            hipcub::DoubleBuffer<uint64_t> vb(ctx->win_vals[k].p + off, ctx->win_vals2[k].p + off);
+            size_t bytes = ctx->win_tmp[k].cap;
+            HIPCHK(ctx, hipcub::DeviceRadixSort::SortPairs(ctx->win_tmp[k].p, bytes, kb, vb, (int)sh.ncell,
+                                                             0, kCoarseBits, st));
+            const uint64_t* base = vb.Current() - off;
+            if (out && base != out) return ctx->fail(TPE_ERR_HIP, "windowed screen: sort buffers diverged");
+            out = base;
+        }
+        *sorted = out;
+        return TPE_OK;
+    }
     hipcub::DoubleBuffer<uint32_t> kb(ctx->win_keys[k].p, ctx->win_keys2[k].p);
     hipcub::DoubleBuffer<uint64_t> vb(ctx->win_vals[k].p, ctx->win_vals2[k].p);
     size_t bytes = ctx->win_tmp[k].cap;

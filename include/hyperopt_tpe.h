@@ -329,7 +329,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *                   tile stay below 2^-T of the largest term (8..62)    [16]
  *   TPE_OPT_WIN_GROUPS  label groups of a windowed round, each sorted on a
  *                   second stream while the previous one is screened
- *                   (0: 4 for rounds of >= 2^26 candidates, else 1)      [0]
+ *                   (0: one group; the chip is busy either way)          [0]
  *   TPE_OPT_TIMING  HIP-event timing of every round (tpe_last_timing,
  *                   tpe_last_mode_stats, tpe_last_screen's ms); off saves
  *                   ~20 event calls per round on latency-bound calls   [1]
