@@ -181,7 +181,9 @@ def measured_pmc(kernel_prefix):
     of this bench, tools/prof_round.sh + tools/pmc_summary.py; FETCH doubled
     per the gfx950 correction) -- (None, None, None) if absent."""
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_pmc_summary.json')))
+    # tags sort by length, then name: r2z < r2aa < r2ai (newest last)
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_pmc_summary.json')),
+                   key=lambda f: (len(os.path.basename(f)), os.path.basename(f)))
     for f in reversed(files):
         d = json.load(open(f))
         for name, v in d.items():
@@ -284,7 +286,7 @@ def main():
     def timed(n_steps, first):
         """Run n_steps steps (barrier + sync on both sides); returns wall
         seconds (max over ranks) and the summed per-family / screen stats."""
-        mode_ms, mode_ev, scr = {}, {}, [0, 0, 0.0, 0]
+        mode_ms, mode_ev, scr = {}, {}, [0, 0, 0.0, 0, 0]
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
@@ -299,6 +301,7 @@ def main():
             scr[1] += b
             scr[2] += ms
             scr[3] += eng.last_screen_terms()
+            scr[4] += eng.last_rescore_terms()
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
@@ -321,9 +324,18 @@ def main():
     for i in range(args.warmup):
         step(i)
     dt, mode_ms, mode_ev, scr = timed(args.steps, args.warmup)
-    evals_per_step = sum(mode_ev.values()) // max(args.steps, 1)
-    total_evals = evals_per_step * args.steps * world
-    value = total_evals / dt
+    # `value` counts EXECUTED (candidate, component) lpdf terms (BASELINE.md
+    # section 3): quantized labels their grid-table evals, screened dense
+    # labels the fp32 terms the screen summed plus the fp64 terms of the
+    # re-scored candidates; the reference-equivalent rate (every pair of
+    # the round, as the reference's numpy evaluates them) is reported beside
+    executed = sum(mode_ev.values())
+    if scr[0] > 0:
+        executed += scr[3] + scr[4] - sum(mode_ev.get(k, 0) for k in DENSE)
+    value = executed * world / dt
+    rounds_per_step = args.new_ids if args.config == 5 else 1
+    ref_equiv_per_step = sum((2 if p.family == 'categorical' else len(p.below[0]) + len(p.above[0]))
+                             * C_total * rounds_per_step for p in posts)
 
     # roofline of the dominant kernel (device time from HIP events on the
     # engine's stream, summed over the timed steps)
@@ -384,10 +396,20 @@ def main():
         'per_family_ms': {k: round(v / args.steps, 3) for k, v in mode_ms.items() if v},
         'per_family_evals': {k: v // args.steps for k, v in mode_ev.items() if v},
         'roofline': roof,
+        'evals_basis': {
+            'value': 'executed terms per second, whole job',
+            'executed_per_step': executed * world // max(args.steps, 1),
+            'reference_equivalent_per_step': ref_equiv_per_step,
+            'reference_equivalent_per_s': ref_equiv_per_step * args.steps / dt,
+            'note': 'reference_equivalent: every (candidate, component) pair of the step '
+                    '(C x (K_b + K_a) per numeric label, 2 C per categorical) -- the terms the '
+                    'reference\'s GMM1_lpdf / LGMM1_lpdf / categorical_lpdf evaluate for the '
+                    'same candidates, i.e. the step\'s work at the cpu_baseline\'s counting'},
     }
     if screened:
         line['screen'] = {
             'screened_per_step': scr[0] // args.steps, 'rescored_per_step': scr[1] // args.steps,
+            'rescore_terms_per_step': scr[4] // args.steps,
             'rescored_fraction': scr[1] / max(scr[0], 1),
             'screen_kernel_ms': round(scr[2] / args.steps, 3),
             'other_dense_ms': round((mode_ms[dom] - scr[2]) / args.steps, 3),
@@ -400,9 +422,9 @@ def main():
                     'covered by the bound; candidates whose bound interval reaches the '
                     'round\'s best lower bound are re-scored in fp64 over every component -- '
                     'winners and lpdfs are bit-identical to the plain fp64 round '
-                    '(tests/test_screen.py).  `value` counts every pair of the round once '
-                    '(the reference evaluates them all); the roofline counts the terms the '
-                    'screening kernel summed.  other_dense_ms: keys + sort, select, re-score'}
+                    '(tests/test_screen.py).  `value` counts the terms executed (screen + '
+                    're-score); the roofline counts the terms the screening kernel summed.  '
+                    'other_dense_ms: keys + sort, select, re-score'}
         if args.unscreened_steps > 0 and world == 1:
             eng.set_option('screen', 0)
             step(args.warmup + args.steps)

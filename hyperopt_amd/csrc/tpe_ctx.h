@@ -248,6 +248,7 @@ struct tpe_ctx {
     DevBuf<unsigned long long> win_evals;   // (candidate, component) terms the screen summed
     DevBuf<float2> win_lohi;             // packed map: per candidate (lower, upper) score bound
     int64_t screen_exec = 0;             // last round: terms summed by the screen
+    int64_t screen_rescore_terms = 0;    // last round: fp64 terms of the re-scored candidates
     bool screen_exec_pending = false;
     unsigned long long screen_exec_h = 0;
     hipEvent_t evs[2] = {};              // brackets k_screen alone

@@ -1972,6 +1972,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
                 n_whole * rounds_whole, gx_whole};
     ctx->screen_total = ctx->screen_rescored = 0;
     ctx->screen_exec = 0;
+    ctx->screen_rescore_terms = 0;
     ctx->evw_used = 0;
     ctx->screen_pending = false;
     ctx->screen_exec_pending = false;
@@ -2046,7 +2047,17 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         ctx->screen_exec_pending = false;
     }
     if (ctx->screen_pending) {
-        for (int32_t c : ctx->scr_cnt_h) ctx->screen_rescored += c;
+        // cell = round x (dense GMM1 labels, then dense LGMM1 labels)
+        const std::vector<int32_t>& gg = ctx->P->h_group[DENSE_GMM];
+        const std::vector<int32_t>& gl = ctx->P->h_group[DENSE_LGMM];
+        const size_t nld = gg.size() + gl.size();
+        for (size_t c = 0; c < ctx->scr_cnt_h.size(); ++c) {
+            const int32_t cnt = ctx->scr_cnt_h[c];
+            const size_t y = c % nld;
+            const DLabel& d = ctx->P->h_labels[y < gg.size() ? gg[y] : gl[y - gg.size()]];
+            ctx->screen_rescored += cnt;
+            ctx->screen_rescore_terms += (int64_t)cnt * (d.nb + d.na);
+        }
         if (getenv("TPE_SCREEN_DEBUG")) {
             fprintf(stderr, "screen counts:");
             for (int32_t c : ctx->scr_cnt_h) fprintf(stderr, " %d", c);
@@ -2518,6 +2529,12 @@ int tpe_last_screen(const tpe_ctx* ctx, int64_t* screened, int64_t* rescored, fl
 int tpe_last_screen_terms(const tpe_ctx* ctx, int64_t* terms) {
     if (!ctx) return TPE_ERR_ARG;
     if (terms) *terms = ctx->screen_exec;
+    return TPE_OK;
+}
+
+int tpe_last_rescore_terms(const tpe_ctx* ctx, int64_t* terms) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (terms) *terms = ctx->screen_rescore_terms;
     return TPE_OK;
 }
 

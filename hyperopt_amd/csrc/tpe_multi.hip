@@ -135,7 +135,7 @@ struct Shard {
 // work summed, times the slowest device's.
 void aggregate_stats(tpe_ctx* c) {
     const int n = ndev(c);
-    int64_t evals = 0, scr_t = 0, scr_r = 0, scr_x = 0;
+    int64_t evals = 0, scr_t = 0, scr_r = 0, scr_x = 0, scr_rt = 0;
     float score_ms = 0.f, round_ms = 0.f, scr_ms = 0.f;
     float mode_ms[tpe_rt::kNumModes] = {};
     int64_t mode_ev[tpe_rt::kNumModes] = {};
@@ -145,6 +145,7 @@ void aggregate_stats(tpe_ctx* c) {
         scr_t += x->screen_total;
         scr_r += x->screen_rescored;
         scr_x += x->screen_exec;
+        scr_rt += x->screen_rescore_terms;
         score_ms = std::max(score_ms, x->score_ms);
         round_ms = std::max(round_ms, x->round_ms);
         scr_ms = std::max(scr_ms, x->screen_ms);
@@ -157,6 +158,7 @@ void aggregate_stats(tpe_ctx* c) {
     c->screen_total = scr_t;
     c->screen_rescored = scr_r;
     c->screen_exec = scr_x;
+    c->screen_rescore_terms = scr_rt;
     c->score_ms = score_ms;
     c->round_ms = round_ms;
     c->screen_ms = scr_ms;

@@ -245,6 +245,13 @@ class Engine(object):
         self._check(self.lib.tpe_last_screen_terms(self.h, ctypes.byref(t)))
         return t.value
 
+    def last_rescore_terms(self):
+        """(candidate, component) terms the last round's fp64 re-score
+        evaluated (every re-scored candidate over both of its mixtures)."""
+        t = ctypes.c_int64()
+        self._check(self.lib.tpe_last_rescore_terms(self.h, ctypes.byref(t)))
+        return t.value
+
     OPTIONS = {'screen': L.TPE_OPT_SCREEN, 'splitk': L.TPE_OPT_SPLITK, 'dedup': L.TPE_OPT_DEDUP,
                'chunks': L.TPE_OPT_CHUNKS, 'whole_n': L.TPE_OPT_WHOLE_N,
                'whole_rounds': L.TPE_OPT_WHOLE_ROUNDS, 'timing': L.TPE_OPT_TIMING,

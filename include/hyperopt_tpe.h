@@ -308,6 +308,12 @@ int tpe_last_screen(const tpe_ctx *ctx, int64_t *screened, int64_t *rescored,
  * is screened x (nb + na)).  Winners are unaffected. */
 int tpe_last_screen_terms(const tpe_ctx *ctx, int64_t *terms);
 
+/* (candidate, component) terms the last round's fp64 re-score evaluated:
+ * every re-scored candidate over both mixtures of its label (the exact
+ * GMM1_lpdf / LGMM1_lpdf of tpe.py:110-172,265-307 on that candidate).
+ * With tpe_last_screen_terms this is the dense work the round executed. */
+int tpe_last_rescore_terms(const tpe_ctx *ctx, int64_t *terms);
+
 /* Diagnostic of the screen (tests): for caller-supplied candidates of one
  * dense resident label, the fp32 score lpdf_below - lpdf_above the screen
  * computes and its rigorous error bound (x 1.25, as used by the round):
