@@ -21,7 +21,8 @@ ARCH = 'gfx950'
 SOURCES = [os.path.join(HERE, 'csrc', 'tpe_engine.hip'),
            os.path.join(HERE, 'csrc', 'tpe_build.hip'),
            os.path.join(HERE, 'csrc', 'tpe_multi.hip'),
-           os.path.join(HERE, 'csrc', 'tpe_window.hip')]
+           os.path.join(HERE, 'csrc', 'tpe_window.hip'),
+           os.path.join(HERE, 'csrc', 'tpe_expand.hip')]
 DEPS = SOURCES + [os.path.join(HERE, 'csrc', 'tpe_device.h'),
                   os.path.join(HERE, 'csrc', 'tpe_ctx.h'),
                   os.path.join(HERE, 'csrc', 'tpe_exp_table.h'),
@@ -59,13 +60,29 @@ def built_hash(target=TARGET):
 
 
 def build_engine(force=False, verbose=True):
+    """Compile every source to an object in parallel (each carries its own
+    gfx950 code object), then link the shared library."""
+    import tempfile
     want = source_hash()
     if not force and built_hash() == want:
         return TARGET
-    cmd = [HIPCC] + FLAGS + ['-DTPE_SOURCE_HASH="%s"' % want, '-o', TARGET] + SOURCES
-    if verbose:
-        print(' '.join(cmd), flush=True)
-    subprocess.check_call(cmd)
+    flags = FLAGS + ['-DTPE_SOURCE_HASH="%s"' % want]
+    with tempfile.TemporaryDirectory(prefix='tpe_build_') as tmp:
+        objs, procs = [], []
+        for src in SOURCES:
+            obj = os.path.join(tmp, os.path.basename(src) + '.o')
+            cmd = [HIPCC] + [f for f in flags if f != '-shared'] + ['-c', '-o', obj, src]
+            if verbose:
+                print(' '.join(cmd), flush=True)
+            procs.append(subprocess.Popen(cmd))
+            objs.append(obj)
+        bad = [src for src, p in zip(SOURCES, procs) if p.wait() != 0]
+        if bad:
+            raise RuntimeError('hipcc failed on %s' % ', '.join(os.path.basename(b) for b in bad))
+        cmd = [HIPCC] + flags + ['-o', TARGET] + objs
+        if verbose:
+            print(' '.join(cmd), flush=True)
+        subprocess.check_call(cmd)
     got = built_hash()
     if got != want:
         raise RuntimeError('built library carries hash %r, expected %r' % (got, want))

@@ -45,6 +45,7 @@ TPE_OPT_TIMING = 7
 TPE_OPT_WINDOW = 8
 TPE_OPT_WIN_T = 9
 TPE_OPT_WIN_GROUPS = 10
+TPE_OPT_EXPAND = 11
 
 TPE_OBS_IDENTITY = 0
 TPE_OBS_LOG = 1

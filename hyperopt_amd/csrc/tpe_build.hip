@@ -1349,6 +1349,7 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     }
     P.h_labels = dl;
     P.win_ready = false;
+    P.bx_ready = false;
     P.n_labels = n_labels;
     B.n_labels = n_labels;
     B.mix_h = mix;

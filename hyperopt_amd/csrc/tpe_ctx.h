@@ -81,6 +81,17 @@ struct Posterior {
     DevBuf<uint8_t> win_flag;            // per component: 1 = wide
     DevBuf<double> win_skip;             // per label: kWinBins bounds of the mass a bin's window skips
     DevBuf<double> win_skip_part;        //   their partial sums per chunk of components
+    // expansion screen index (tpe_expand.hip), built on first use after every
+    // posterior change; bx_ok: every dense label has one (else the windowed
+    // screen runs)
+    bool bx_ready = false, bx_ok = false;
+    DevBuf<tpe::BxLabel> bx;             // per label
+    std::vector<tpe::BxLabel> bx_h;
+    DevBuf<double> bx_tab;               // per label: nbins rows of kBxRow doubles
+    DevBuf<int32_t> bx_nc;               // per label at comp_a: unclipped above components
+    DevBuf<int32_t> bx_loff;             // per label: nbins + 1 offsets into its list
+    DevBuf<int32_t> bx_list;             // per bin: the unclipped components reaching it
+    DevBuf<double> bx_scan;              // per dense label position: range, a*, counts
     void release() {
         labels.release();
         comps64.release();
@@ -99,6 +110,14 @@ struct Posterior {
         win_skip.release();
         win_skip_part.release();
         win_ready = false;
+        bx.release();
+        bx_h.clear();
+        bx_tab.release();
+        bx_nc.release();
+        bx_loff.release();
+        bx_list.release();
+        bx_scan.release();
+        bx_ready = bx_ok = false;
         n_labels = 0;
     }
 };
@@ -219,6 +238,8 @@ struct tpe_ctx {
     // lower bound and the compacted candidates that can still win
     bool screen = true;                  // TPE_NO_SCREEN=1 / TPE_OPT_SCREEN
     DevBuf<float> scr_hi;
+    DevBuf<double> scr_hid;              // expansion screen: fp64 upper bounds
+    bool expand = true;                  // TPE_OPT_EXPAND: expansion screen when eligible
     DevBuf<int32_t> scr_idx;
     DevBuf<unsigned long long> scr_lb;
     DevBuf<int32_t> scr_cnt;
@@ -323,6 +344,11 @@ int win_reserve(tpe_ctx* ctx, size_t total, int64_t cells, int nslots);
 int win_sort(tpe_ctx* ctx, const WinScreenArgs& a, hipStream_t st, const uint64_t** sorted);
 int win_tiles(tpe_ctx* ctx, const WinScreenArgs& a, const uint64_t* sorted, hipStream_t st);
 int64_t win_rounds_per_batch(int64_t n, int32_t nl);
+
+// The expansion screen (tpe_expand.hip).  bx_prepare builds the bin tables
+// and lists of every dense label of the resident posterior (once per
+// posterior) and sets P->bx_ok when every dense label has one.
+int bx_prepare(tpe_ctx* ctx);
 }  // namespace tpe_rt
 
 // per-device implementations of the entry points a multi-device context

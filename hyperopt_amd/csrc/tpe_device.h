@@ -558,6 +558,46 @@ __device__ __host__ __forceinline__ int win_bin(const WinLabel& W, double x) {
     return (int)f;
 }
 
+// ----------------------------------------------------- expansion screen ----
+// Past ~100 observations most above components share one sigma: the gaps
+// between sorted observations are narrower than prior_sigma / min(100, N +
+// 1), so adaptive_parzen_normal clips them all to it (tpe.py:404-477).  For
+// those "clipped" components (fp64 record scale a' = a*) the above sum over
+// a bin of x' with centre x_b, x' = x_b + delta, is
+//   sum_k exp(c_k - kappa (x' - mu_k)^2)
+//     = exp(-kappa delta^2) sum_n delta^n A_n,
+//   A_n = sum_k g_k (2 kappa d_k)^n / n!,  g_k = exp(c_k - kappa d_k^2),
+//   d_k = mu_k - x_b,  kappa = a*^2 / K (natural-log curvature),
+// a Taylor series in delta whose coefficients are per bin, not per
+// candidate.  tpe_expand.hip tabulates A_0..A_{P-1} per bin (in fp64, with a
+// rigorous absolute bound of truncation + rounding) and lists, per bin, the
+// other ("unclipped") components that can reach it; k_screen_bx scores a
+// candidate with the below mixture in full fp64 (the fp64 round's own code,
+// so lpdf_below is bit-identical), the above mixture as the bin's
+// polynomial plus its list, and a bound ~1e-12 wide: only near-ties of the
+// best score are re-scored.
+constexpr int kBxP = 13;          // Taylor coefficients per bin
+constexpr int kBxRow = 16;        // doubles per bin row: A_0..A_12, Eabs, G, W
+constexpr double kBxT = 96.0;     // components left out stay below 2^-kBxT
+
+struct BxLabel {
+    double xlo, inv_bw, bw;   // bin b = floor((x' - xlo) inv_bw), centre xlo + (b + 1/2) bw
+    double rmax;              // largest |delta| the bin's bound covers
+    double astar, kappa;      // clipped record scale, its curvature a*^2 / K
+    double dwin;              // window half-width: clipped components beyond never reach 2^-T
+    double rP;                // rmax^P
+    int64_t tab_off;          // first row of the label in bx_tab
+    int64_t cnt_off;          // first of its nbins + 1 list offsets in bx_loff
+    int64_t list_off;         // first of its entries in bx_list
+    int32_t nbins, n_nc;      // bins; unclipped components (listed at comp_a in bx_nc)
+};
+
+__device__ __host__ __forceinline__ int bx_bin(const BxLabel& B, double x) {
+    const double f = (x - B.xlo) * B.inv_bw;
+    if (!(f >= 0.0) || !(f < (double)B.nbins)) return -1;   // also NaN
+    return (int)f;
+}
+
 __device__ __forceinline__ float float_up(double v) {   // smallest float >= v (finite v)
     float f = (float)v;
     if ((double)f < v) {

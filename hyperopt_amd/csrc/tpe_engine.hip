@@ -502,6 +502,126 @@ __global__ __launch_bounds__(kBlock) void k_screen(
     if (threadIdx.x == 0 && bk) atomicMax(lbkey + (size_t)blockIdx.z * nl + blockIdx.y, bk);
 }
 
+// The expansion screen (tpe_device.h "expansion screen", index from
+// tpe_expand.hip): per candidate the below mixture through the fp64 round's
+// own code (lpdf_below bit-identical to it), the above mixture as its bin's
+// Taylor polynomial (clipped components) plus the bin's list of unclipped
+// components (direct fp64 terms), and a rigorous bound E of |s - s64|:
+//   |S - S_exact| <= Eabs_bin (truncation + rounding of the table)
+//                  + 8 u S_clip (exp(-kappa delta^2)) + na 2^-T (left out)
+//                  + (3e-14 + (n_list + 4) u) S_list + 2 u S,
+//   eps = that / S, |log S - log S_exact| <= 1.001 eps + 2u (|log S| + 1),
+//   E = 1.25 (that + fp64_err), the fp64 round's own distance from exact.
+// Candidates outside the bins, with S < 1e-280 or eps > 1e-6, or NaN, get
+// hi = +inf (always re-scored).  hi is stored in fp64: E is ~1e-12, far
+// below an fp32 rounding of the score.  DIRECT: the terms each candidate
+// summed (nb + list) are counted into *terms.
+template <int R, bool SAMPLE>
+__global__ __launch_bounds__(kBlock) void k_screen_bx(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<double>* __restrict__ comps64, const SampRec* __restrict__ samp,
+    const BxLabel* __restrict__ bx, const double* __restrict__ tab, const int32_t* __restrict__ loff,
+    const int32_t* __restrict__ list, int64_t n, int64_t cand_offset, uint64_t seed,
+    const uint32_t* __restrict__ rounds, int32_t nl, double* __restrict__ hi,
+    unsigned long long* __restrict__ lbkey, unsigned long long* __restrict__ terms,
+    int32_t* __restrict__ err, Slots S, const double* __restrict__ cand_in,
+    double* __restrict__ s_out, double* __restrict__ e_out) {
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    const BxLabel B = bx[li];
+    __shared__ double exp_tab[kExpTabSize];
+    load_exp_table(exp_tab);
+    const bool lgmm = L.mode == DENSE_LGMM;
+    double x[R];
+    int64_t z[R], ci[R], gi[R];
+    bool valid[R];
+    draw_slots<DENSE_ANY, SAMPLE, R>(L, S, lgmm, samp, cand_in, n, cand_offset, seed, rounds, err,
+                                     x, z, ci, gi, valid);
+    double y[R], xr[R], acc[R], lb[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        y[r] = lgmm ? log(x[r]) : x[r];
+        xr[r] = y[r] - L.centre;
+        acc[r] = 0.0;
+    }
+    // below: the fp64 round's lse_dense, term for term
+    lse_acc<R>(comps64 + L.comp_b, L.nb, xr, acc, exp_tab);
+#pragma unroll
+    for (int r = 0; r < R; ++r) lb[r] = lse_finish(comps64 + L.comp_b, L.nb, acc[r], xr[r], L.shift_b);
+    const Comp<double>* ca = comps64 + L.comp_a;
+    const double skip_abs = (double)L.na * exp2(-kBxT);
+    const size_t row0 = ((size_t)blockIdx.z * nl + blockIdx.y) * (size_t)n;
+    uint64_t bk = 0;
+    int nterms = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (!valid[r]) continue;
+        const int b = bx_bin(B, xr[r]);
+        double s = __builtin_nan(""), E = __builtin_inf();
+        if (b >= 0) {
+            const double delta = xr[r] - (B.xlo + ((double)b + 0.5) * B.bw);
+            const double* rw = tab + (size_t)(B.tab_off + b) * kBxRow;
+            double poly = rw[kBxP - 1];
+#pragma unroll
+            for (int k = kBxP - 2; k >= 0; --k) poly = fma(poly, delta, rw[k]);
+            const double eabs = rw[kBxP];
+            const double sclip = exp(-B.kappa * delta * delta) * poly;
+            const int j0 = loff[B.cnt_off + b], j1 = loff[B.cnt_off + b + 1];
+            const int32_t* lst = list + B.list_off;
+            double snc = 0.0;
+            for (int j = j0; j < j1; ++j) {
+                const Comp<double> rec = ca[lst[j]];
+                const double zz = fma(xr[r], rec.a, -rec.mu);
+                snc = exp_scaled_acc(fma(-zz, zz, rec.c), exp_tab, snc);
+            }
+            nterms += L.nb + (j1 - j0);
+            const double sum = sclip + snc;
+            const double ea = eabs + 8.0 * 0x1.0p-53 * fabs(sclip) + skip_abs +
+                              (3e-14 + (double)(j1 - j0 + 4) * 0x1.0p-53) * snc + 0x1.0p-52 * sum;
+            const double eps = ea / sum;
+            if (fabs(delta) <= B.rmax && sum >= 1e-280 && eps <= 1e-6 && lb[r] == lb[r]) {
+                const double ls = log(sum);
+                double la = ls + L.shift_a, lbr = lb[r];
+                if (lgmm) {
+                    lbr -= y[r];
+                    la -= y[r];
+                }
+                s = lbr - la;
+                E = 1.25 * (1.001 * eps + 0x1.0p-52 * (fabs(ls) + 1.0) +
+                            fp64_err(L.nb + L.na, fabs(lbr) + fabs(la) + fabs(y[r]) + fabs(L.centre)));
+            }
+        }
+        if constexpr (!SAMPLE) {
+            s_out[ci[r]] = s;
+            e_out[ci[r]] = E;
+            continue;
+        }
+        double h = __builtin_inf();
+        if (E <= 1e30 && s == s) {
+            h = s + E;
+            const uint64_t k = order_key(s - E);
+            bk = k > bk ? k : bk;
+        }
+        hi[row0 + ci[r]] = h;
+    }
+    if constexpr (!SAMPLE) return;
+    __shared__ uint64_t sh[kBlock / 64];
+    bk = block_max_key(bk, sh);
+    if (threadIdx.x == 0 && bk) atomicMax(lbkey + (size_t)blockIdx.z * nl + blockIdx.y, bk);
+    // (block_max_key's barrier orders sh's reuse)
+    __shared__ int shn[kBlock / 64];
+    int t = nterms;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+    if ((threadIdx.x & 63) == 0) shn[threadIdx.x >> 6] = t;
+    __syncthreads();
+    if (threadIdx.x == 0 && terms) {
+        unsigned long long tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) tot += (unsigned long long)shn[w];
+        atomicAdd(terms, tot);
+    }
+}
+
 // Each workgroup owns a contiguous slice of its (round, label) row: it
 // counts its takers, reserves their places with ONE atomic (a per-wave
 // atomic on the row's counter serialised ~1.3M same-address atomics at
@@ -509,7 +629,8 @@ __global__ __launch_bounds__(kBlock) void k_screen(
 // The windowed screen (tpe_window.hip) leaves hi in sorted order: vmap (the
 // unit of rounds from z0 on and labels from position y0 on, nl_unit of them)
 // gives each sorted position's candidate index.
-__global__ __launch_bounds__(kBlock) void k_select(const float* __restrict__ hi, int64_t n, int32_t nl,
+template <typename H>
+__global__ __launch_bounds__(kBlock) void k_select(const H* __restrict__ hi, int64_t n, int32_t nl,
                                                    const unsigned long long* __restrict__ lbkey,
                                                    int32_t* __restrict__ cnt, int32_t* __restrict__ idx,
                                                    int32_t z0, int32_t y0, int32_t nl_unit,
@@ -584,6 +705,13 @@ constexpr int kRescoreR = TPE_RESCORE_R;
 #define TPE_SCREEN_R 8
 #endif
 constexpr int kScreenR = TPE_SCREEN_R;
+
+// candidates per thread in k_screen_bx (the below mixture's records shared
+// by R candidates; the above part is per candidate)
+#ifndef TPE_BX_R
+#define TPE_BX_R 4
+#endif
+constexpr int kBxR = TPE_BX_R;
 
 template <int R>
 __global__ __launch_bounds__(kBlock) void k_rescore(
@@ -1606,14 +1734,38 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
     const int nch = a.S.cpack ? dense_chunks(ctx, a.gx_whole, nl) : 1;
     if (sizeof(T) == 8 && ctx->screen && a.S.cpack == 0) {   // fp32 screen + fp64 re-score
         const size_t cells = (size_t)a.n_rounds * nl;
-        HIPCHK(ctx, ctx->scr_hi.reserve(cells * a.n));
+        bool use_bx = false;
+        if (ctx->expand && a.n >= kWinMinN && a.cand_in == nullptr) {
+            int rc = tpe_rt::bx_prepare(ctx);
+            if (rc) return rc;
+            use_bx = ctx->P->bx_ok;
+        }
+        HIPCHK(ctx, use_bx ? ctx->scr_hid.reserve(cells * a.n) : ctx->scr_hi.reserve(cells * a.n));
         HIPCHK(ctx, ctx->scr_idx.reserve(cells * a.n));
         HIPCHK(ctx, ctx->scr_lb.reserve(cells));
         HIPCHK(ctx, ctx->scr_cnt.reserve(cells));
         HIPCHK(ctx, hipMemsetAsync(ctx->scr_lb.p, 0, cells * sizeof(unsigned long long), ctx->stream));
         HIPCHK(ctx, hipMemsetAsync(ctx->scr_cnt.p, 0, cells * sizeof(int32_t), ctx->stream));
         const unsigned sx = (unsigned)std::min<int64_t>((a.n + 8 * kBlock - 1) / (8 * kBlock), 1024);
-        if (ctx->window && a.n >= kWinMinN && a.cand_in == nullptr) {
+        if (use_bx) {
+            // expansion screen: no sort, ~1e-12 bounds, near-ties re-scored
+            tpe_rt::Posterior& P = *ctx->P;
+            HIPCHK(ctx, ctx->win_evals.reserve(1));
+            HIPCHK(ctx, hipMemsetAsync(ctx->win_evals.p, 0, sizeof(unsigned long long), ctx->stream));
+            if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
+            const unsigned bgx = (unsigned)((a.n + kBxR * kBlock - 1) / (kBxR * kBlock));
+            hipLaunchKernelGGL((k_screen_bx<kBxR, true>), dim3(bgx, nl, a.gz), dim3(kBlock), 0, ctx->stream,
+                               P.labels.p, grp, P.comps64.p, P.samp.p, P.bx.p, P.bx_tab.p, P.bx_loff.p,
+                               P.bx_list.p, a.n, a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->scr_hid.p,
+                               ctx->scr_lb.p, ctx->win_evals.p, ctx->errflag.p, a.S, nullptr, nullptr, nullptr);
+            if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
+            hipLaunchKernelGGL(k_select<double>, dim3(sx, nl, a.gz), dim3(kBlock), 0, ctx->stream,
+                               ctx->scr_hid.p, a.n, nl, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p, 0, 0, nl,
+                               nullptr);
+            HIPCHK(ctx, hipMemcpyAsync(&ctx->screen_exec_h, ctx->win_evals.p, sizeof(unsigned long long),
+                                       hipMemcpyDeviceToHost, ctx->stream));
+            ctx->screen_exec_pending = true;
+        } else if (ctx->window && a.n >= kWinMinN && a.cand_in == nullptr) {
             // windowed: units of (batch of rounds, group of labels); with
             // several units each is keyed and sorted on the aux stream into
             // one of two buffer slots while the main stream screens and
@@ -1674,7 +1826,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                 if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evw[2 * ui], ctx->stream));
                 if ((rc = tpe_rt::win_tiles(ctx, wa, sorted, ctx->stream))) return rc;
                 if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evw[2 * ui + 1], ctx->stream));
-                hipLaunchKernelGGL(k_select, dim3(sx, u.ny, u.nz), dim3(kBlock), 0, ctx->stream, ctx->scr_hi.p,
+                hipLaunchKernelGGL(k_select<float>, dim3(sx, u.ny, u.nz), dim3(kBlock), 0, ctx->stream, ctx->scr_hi.p,
                                    a.n, nl, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p, u.z0, u.y0, u.ny,
                                    sorted);
                 if (pipe) HIPCHK(ctx, hipEventRecord(ctx->ev_done[slot], ctx->stream));
@@ -1690,7 +1842,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                                a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->scr_hi.p, ctx->scr_lb.p,
                                ctx->errflag.p, a.S, nullptr, nullptr, nullptr);
             if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
-            hipLaunchKernelGGL(k_select, dim3(sx, nl, a.gz), dim3(kBlock), 0, ctx->stream, ctx->scr_hi.p,
+            hipLaunchKernelGGL(k_select<float>, dim3(sx, nl, a.gz), dim3(kBlock), 0, ctx->stream, ctx->scr_hi.p,
                                a.n, nl, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p, 0, 0, nl, nullptr);
             ctx->screen_exec += (int64_t)a.n_rounds * a.n * dense_terms(ctx);
         }
@@ -2242,6 +2394,7 @@ int set_posterior_impl(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_lab
     ctx->P->groups_h = cat;
     ctx->P->h_labels = dl;
     ctx->P->win_ready = false;
+    ctx->P->bx_ready = false;
     ctx->P->n_labels = n_labels;
     return TPE_OK;
 }
@@ -2470,7 +2623,20 @@ int tpe_screen_probe(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n,
     HIPCHK(ctx, ctx->errflag.reserve(1));
     HIPCHK(ctx, hipMemcpyAsync(ctx->one_group.p, &label, sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, hipMemcpyAsync(ctx->cand.p, cand, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
-    if (ctx->window && n >= 2048) {   // the windowed screen's tiles of sorted neighbours
+    bool use_bx = false;
+    if (ctx->expand && n >= 2048) {
+        int rc = tpe_rt::bx_prepare(ctx);
+        if (rc) return rc;
+        use_bx = ctx->P->bx_ok;
+    }
+    if (use_bx) {   // the expansion screen's per-candidate score and bound
+        tpe_rt::Posterior& P = *ctx->P;
+        const unsigned bgx = (unsigned)((n + kBxR * kBlock - 1) / (kBxR * kBlock));
+        hipLaunchKernelGGL((k_screen_bx<kBxR, false>), dim3(bgx, 1, 1), dim3(kBlock), 0, ctx->stream,
+                           P.labels.p, ctx->one_group.p, P.comps64.p, P.samp.p, P.bx.p, P.bx_tab.p,
+                           P.bx_loff.p, P.bx_list.p, n, 0, 0, ctx->rounds.p, 1, nullptr, nullptr, nullptr,
+                           ctx->errflag.p, Slots{0, 0, 1}, ctx->cand.p, ctx->out_lb.p, ctx->out_la.p);
+    } else if (ctx->window && n >= 2048) {   // the windowed screen's tiles of sorted neighbours
         int rc = tpe_rt::win_prepare(ctx);
         if (rc) return rc;
         if (n > ((int64_t)1 << 30)) return ctx->fail(TPE_ERR_ARG, "screen probe: too many candidates");
@@ -2550,6 +2716,7 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
             break;
         case TPE_OPT_TIMING: ctx->timing = value != 0; break;
         case TPE_OPT_WINDOW: ctx->window = value != 0; break;
+        case TPE_OPT_EXPAND: ctx->expand = value != 0; break;
         case TPE_OPT_WIN_GROUPS:
             if (value < 0 || value > 64) return ctx->fail(TPE_ERR_ARG, "window groups must be in [0, 64]");
             ctx->win_groups = (int32_t)value;

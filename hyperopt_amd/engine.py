@@ -256,7 +256,7 @@ class Engine(object):
                'chunks': L.TPE_OPT_CHUNKS, 'whole_n': L.TPE_OPT_WHOLE_N,
                'whole_rounds': L.TPE_OPT_WHOLE_ROUNDS, 'timing': L.TPE_OPT_TIMING,
                'window': L.TPE_OPT_WINDOW, 'win_t': L.TPE_OPT_WIN_T,
-               'win_groups': L.TPE_OPT_WIN_GROUPS}
+               'win_groups': L.TPE_OPT_WIN_GROUPS, 'expand': L.TPE_OPT_EXPAND}
 
     def set_option(self, name, value):
         """Engine switches (include/hyperopt_tpe.h TPE_OPT_*): 'screen',

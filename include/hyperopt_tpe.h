@@ -319,7 +319,9 @@ int tpe_last_rescore_terms(const tpe_ctx *ctx, int64_t *terms);
  * computes and its rigorous error bound (x 1.25, as used by the round):
  * |score32 - score64| <= err_bound for every finite bound.  With
  * TPE_OPT_WINDOW on and n >= 2048 the candidates go through the windowed
- * screen (sorted into tiles of neighbours, windows of components). */
+ * screen (sorted into tiles of neighbours, windows of components); with
+ * TPE_OPT_EXPAND on, n >= 2048 and an eligible posterior, through the
+ * expansion screen (score and bound in fp64). */
 int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
                      double *score32, double *err_bound);
 
@@ -333,6 +335,10 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *                   components that can matter to it                   [1]
  *   TPE_OPT_WIN_T   the windowed screen's cut T: components left out of a
  *                   tile stay below 2^-T of the largest term (8..62)    [16]
+ *   TPE_OPT_EXPAND  expansion screen of large tile rounds (taken before the
+ *                   windowed one when every dense label qualifies): the
+ *                   above mixture's equal-sigma components as a per-bin
+ *                   Taylor polynomial in fp64, bounds ~1e-12, no sort   [1]
  *   TPE_OPT_WIN_GROUPS  label groups of a windowed round, each sorted on a
  *                   second stream while the previous one is screened
  *                   (0: one group; the chip is busy either way)          [0]
@@ -356,6 +362,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_WINDOW 8
 #define TPE_OPT_WIN_T 9
 #define TPE_OPT_WIN_GROUPS 10
+#define TPE_OPT_EXPAND 11
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
 
 #ifdef __cplusplus

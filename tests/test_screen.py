@@ -28,9 +28,12 @@ def eng():
     e.close()
 
 
-@pytest.mark.parametrize('window,win_t', [(1, 40), (1, 16), (1, 8), (0, 16)])
-def test_screen_bound_holds(eng, window, win_t):
-    """window=1: the probe goes through the windowed screen (candidates
+@pytest.mark.parametrize('expand,window,win_t', [(1, 1, 16), (0, 1, 40), (0, 1, 16), (0, 1, 8),
+                                                  (0, 0, 16)])
+def test_screen_bound_holds(eng, expand, window, win_t):
+    """expand=1: the probe goes through the expansion screen (fp64 score
+    from the bin's Taylor polynomial + list, bound ~1e-12).
+    window=1: the probe goes through the windowed screen (candidates
     sorted into tiles of neighbours, components outside a tile's window left
     out and covered by the bound's skip term); at win_t = 16 (the default)
     and 8 the terms left out reach 2^-16 / 2^-8 of the largest, where the
@@ -41,7 +44,7 @@ def test_screen_bound_holds(eng, window, win_t):
     hist = mixed_history(32, 10000, seed=0)
     posts = hist.posteriors()
     eng.set_posterior(*P.pack(posts))
-    worst, cert = 0.0, []
+    worst, cert, emax = 0.0, [], 0.0
     for li in _dense_labels(posts):
         p = posts[li]
         samp = eng.GMM1 if p.family == 'GMM1' else eng.LGMM1
@@ -53,17 +56,20 @@ def test_screen_bound_holds(eng, window, win_t):
         else:
             extra = np.exp(np.linspace(p.low, p.high, 2001))
         x = np.concatenate([x, extra])
+        eng.set_option('expand', expand)
         eng.set_option('window', window)
         eng.set_option('win_t', win_t)
         try:
             s32, err = eng.screen_probe(li, x)
         finally:
+            eng.set_option('expand', 1)
             eng.set_option('window', 1)
             eng.set_option('win_t', 16)
         lb, la, _ = eng.score(li, x)
         s64 = lb - la
         ok = np.isfinite(err) & np.isfinite(s64)
         cert.append(ok.mean())
+        emax = max(emax, float(np.median(err[ok])))
         assert np.all(np.abs(s32[ok] - s64[ok]) <= err[ok]), li
         worst = max(worst, float(np.max(np.abs(s32[ok] - s64[ok]) / err[ok])))
     # the bound is rigorous, and (but for T = 8, where the skipped mass is a
@@ -71,8 +77,10 @@ def test_screen_bound_holds(eng, window, win_t):
     assert worst < (1.0 if win_t < 16 else 0.5), worst
     if win_t >= 16:
         assert min(cert) > 0.9, cert
-    print('screen bound (window %d, T %d): worst |s32 - s64| / bound = %.3g, certified %.4f..%.4f'
-          % (window, win_t, worst, min(cert), max(cert)))
+    if expand:   # fp64-accurate: the bound is ~1e-12, not ~1e-6
+        assert emax < 1e-9, emax
+    print('screen bound (expand %d, window %d, T %d): worst |s - s64| / bound = %.3g, '
+          'certified %.4f..%.4f' % (expand, window, win_t, worst, min(cert), max(cert)))
 
 
 def _suggest_both(eng, C, rnd, seed):
@@ -175,16 +183,20 @@ def test_windowed_screen_skips_terms(eng):
     hist = mixed_history(32, 10000, seed=0)
     eng.build_posterior(*hist.device_inputs(), gamma=0.25, prior_weight=1.0)
     C = 1 << 20
-    eng.set_option('window', 1)
-    a = eng.suggest(9, C, round=2)
-    terms_w = eng.last_screen_terms()
-    eng.set_option('window', 0)
-    b = eng.suggest(9, C, round=2)
-    terms_p = eng.last_screen_terms()
-    eng.set_option('window', 1)
-    eng.set_option('screen', 0)
-    c = eng.suggest(9, C, round=2)
-    eng.set_option('screen', 1)
+    eng.set_option('expand', 0)
+    try:
+        eng.set_option('window', 1)
+        a = eng.suggest(9, C, round=2)
+        terms_w = eng.last_screen_terms()
+        eng.set_option('window', 0)
+        b = eng.suggest(9, C, round=2)
+        terms_p = eng.last_screen_terms()
+        eng.set_option('window', 1)
+        eng.set_option('screen', 0)
+        c = eng.suggest(9, C, round=2)
+        eng.set_option('screen', 1)
+    finally:
+        eng.set_option('expand', 1)
     _assert_same(a, c)
     _assert_same(b, c)
     frac = terms_w / terms_p
@@ -215,3 +227,45 @@ def test_windowed_screen_batched_rounds(eng, groups):
         eng.set_option('win_groups', 0)
     _assert_same(a, b)
     assert 0 < rescored < screened
+
+
+@pytest.mark.parametrize('config', ['config3', 'config3_device', 'config2', 'config4_device'])
+def test_expansion_screen_rescores_near_ties_only(eng, config):
+    """The expansion screen's bound is ~1e-12: at 2^20 candidates per label
+    only the near-ties of each label's best score are re-scored (a handful
+    per label, against ~0.2 % with the fp32 screens), it sums a few dozen
+    direct terms per candidate, and the round is the fp64 round bit for bit
+    -- as is the windowed screen's round on the same candidates."""
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.workloads import conditional_history, hartmann_history, mixed_history
+    if config == 'config2':
+        hist = hartmann_history(2000, seed=0)
+    elif config.startswith('config4'):
+        hist = conditional_history(5000, seed=0)
+    else:
+        hist = mixed_history(32, 10000, seed=0)
+    if config.endswith('device'):
+        eng.build_posterior(*hist.device_inputs(), gamma=0.25, prior_weight=1.0)
+    else:
+        eng.set_posterior(*P.pack(hist.posteriors()))
+    C = 1 << 20
+    a = eng.suggest(13, C, round=4)
+    screened, rescored = eng.last_screen()
+    terms = eng.last_screen_terms()
+    eng.set_option('expand', 0)
+    try:
+        w = eng.suggest(13, C, round=4)
+        _, rescored_w = eng.last_screen()
+    finally:
+        eng.set_option('expand', 1)
+    eng.set_option('screen', 0)
+    b = eng.suggest(13, C, round=4)
+    eng.set_option('screen', 1)
+    _assert_same(a, b)
+    _assert_same(w, b)
+    n_dense = screened // C
+    assert n_dense > 0
+    print('%s: expansion screen re-scored %d of %d (windowed: %d), %.1f direct terms per '
+          'candidate' % (config, rescored, screened, rescored_w, terms / screened))
+    assert rescored <= 64 * n_dense, rescored
+    assert rescored < rescored_w
