@@ -60,17 +60,48 @@ struct Partial {
     double value, lb, la;
 };
 
+// -------------------------------------------------------------- fast log ----
+// Natural log of a positive normal fp64 number in ~30 VALU operations (the
+// library log takes ~85 issue slots): x = m 2^k with m in [sqrt(1/2),
+// sqrt(2)), f = m - 1 (exact), s = f / (2 + f), z = s^2,
+//   log(1 + f) = f - hf + s (hf + R(z)),  hf = f^2 / 2,
+// R a degree-7 minimax polynomial of 2 atanh(s)/s - 2 (the classic fdlibm
+// reduction and coefficients; < 1 ulp), plus k ln 2 in two parts.  Zero,
+// negatives, subnormals, infinities and NaN take the library log.  Every
+// kernel that logs a candidate or a sum uses this one function, so the
+// screen and the fp64 round agree bit for bit.
+__device__ __forceinline__ double flog(double x) {
+    if (!(x >= 0x1.0p-1022 && x < __builtin_inf())) return log(x);
+    int k;
+    double m = frexp(x, &k);   // [0.5, 1)
+    if (m < 0.70710678118654752440) {
+        m *= 2.0;
+        --k;
+    }
+    const double f = m - 1.0;
+    const double s = f / (2.0 + f), z = s * s;
+    const double R =
+        z * fma(fma(fma(fma(fma(fma(1.479819860511658591e-01, z, 1.531383769920937332e-01), z,
+                                1.818357216161805012e-01), z, 2.222219843214978396e-01), z,
+                        2.857142874366239149e-01), z, 3.999999999940941908e-01), z,
+                6.666666666666735130e-01);
+    const double hf = 0.5 * f * f;
+    const double dk = (double)k;
+    return dk * 6.93147180369123816490e-01 - ((hf - (s * (hf + R) + dk * 1.90821492927058770002e-10)) - f);
+}
+
 // ---------------------------------------------------------------- Philox ----
 struct U4 {
     uint32_t x, y, z, w;
 };
 
 __device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+    // one 32x32 -> 64-bit product per multiplier (v_mad_u64_u32) instead of
+    // separate low and high multiplies: the same words, a third faster
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
-        const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-        const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
-        c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+        c = U4{(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0};
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
     }
@@ -93,6 +124,21 @@ __device__ __forceinline__ int cdf_search(const SampRec* __restrict__ s, int n, 
     return lo;
 }
 
+// One attempt of the below mixture's draw for global candidate g: component
+// ~ weights (inverse cdf), x = mu + sigma N(0, 1) by Box-Muller, before any
+// truncation test.  The counter is (g, attempt, label stream, round).
+constexpr uint32_t kMaxAttempts = 1u << 16;
+
+__device__ __forceinline__ double draw_attempt(const DLabel& L, const SampRec* __restrict__ s, uint32_t k0,
+                                               uint32_t k1, uint32_t g, uint32_t it, uint32_t round) {
+    const U4 r = philox4x32_10(U4{g, it, (uint32_t)L.stream, round}, k0, k1);
+    const int k = cdf_search(s, L.ns, (double)r.x * 0x1.0p-32);
+    const double u1 = u01_open0(r.y, r.z);
+    const double rad = sqrt(-2.0 * flog(u1));
+    const double nrm = rad * cospi(2.0 * ((double)r.w * 0x1.0p-32));
+    return fma(s[k].sigma, nrm, s[k].mu);
+}
+
 // Draw one sample of the below posterior for global candidate g, BEFORE
 // quantization (LGMM1: after the exp).
 // GMM1 / LGMM1 (tpe.py:68-99 / 222-256): component ~ weights, x ~ N(mu, sigma),
@@ -111,13 +157,8 @@ __device__ __forceinline__ bool sample_raw(const DLabel& L, const SampRec* __res
         return true;
     } else {
         const bool bounded = (L.flags & 3) == 3;
-        for (uint32_t it = 0; it < (1u << 16); ++it) {
-            const U4 r = philox4x32_10(U4{g, it, (uint32_t)L.stream, round}, k0, k1);
-            const int k = cdf_search(s, L.ns, (double)r.x * 0x1.0p-32);
-            const double u1 = u01_open0(r.y, r.z);
-            const double rad = sqrt(-2.0 * log(u1));
-            const double nrm = rad * cospi(2.0 * ((double)r.w * 0x1.0p-32));
-            const double draw = s[k].mu + s[k].sigma * nrm;
+        for (uint32_t it = 0; it < kMaxAttempts; ++it) {
+            const double draw = draw_attempt(L, s, k0, k1, g, it, round);
             if (!bounded || (L.low <= draw && draw < L.high)) {
                 out = (MODE == DENSE_LGMM || MODE == QUANT_LGMM) ? exp(draw) : draw;
                 return true;
@@ -126,6 +167,55 @@ __device__ __forceinline__ bool sample_raw(const DLabel& L, const SampRec* __res
         out = __builtin_nan("");
         return false;
     }
+}
+
+// sample_raw for the R slots of a thread (bit for bit the same draws): the
+// lane keeps a queue of its pending slots (bit mask) and spends every
+// attempt of the rejection loop on the first of them, so a wave runs ~R +
+// (the largest excess of one lane) attempts instead of R times the largest
+// attempt count of each slot -- with a prior component reaching far out of
+// [low, high), nearly every wave has a lane that retries.  Slots outside
+// `pend` keep their value.  Returns false if a slot hit the attempt cap
+// (its value is NaN).
+template <int MODE, int R>
+__device__ __forceinline__ bool sample_slots(const DLabel& L, const SampRec* __restrict__ s, uint64_t seed,
+                                             const uint32_t (&rk)[R], const uint32_t (&g)[R], uint32_t pend,
+                                             double (&out)[R]) {
+    static_assert(MODE != CAT, "categorical slots draw once each");
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    const bool bounded = (L.flags & 3) == 3;
+    const uint32_t mask0 = pend;
+    bool ok = true;
+    uint32_t it = 0;
+    while (pend) {
+        const int cur = __builtin_ctz(pend);
+        uint32_t gg = g[0], rr = rk[0];
+#pragma unroll
+        for (int r = 1; r < R; ++r)
+            if (cur == r) {
+                gg = g[r];
+                rr = rk[r];
+            }
+        const double draw = draw_attempt(L, s, k0, k1, gg, it, rr);
+        const bool acc = !bounded || (L.low <= draw && draw < L.high);
+        if (acc || it + 1 >= kMaxAttempts) {
+            const double v = acc ? draw : __builtin_nan("");
+            ok = ok && acc;
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (cur == r) out[r] = v;
+            pend &= pend - 1;
+            it = 0;
+        } else {
+            ++it;
+        }
+    }
+    if constexpr (MODE == DENSE_LGMM || MODE == QUANT_LGMM) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if ((mask0 >> r) & 1u) out[r] = exp(out[r]);
+    }
+    return ok;
 }
 
 // np.round(x / q) * q (round half to even), tpe.py:99 / :255
@@ -304,7 +394,7 @@ __device__ __forceinline__ void lse_acc(const Comp<double>* __restrict__ c, int 
 // log(acc) + shift, or the two-pass form when the sum underflowed / is NaN
 __device__ __forceinline__ double lse_finish(const Comp<double>* __restrict__ c, int n, double acc,
                                              double xr, double shift) {
-    double v = log(acc);
+    double v = flog(acc);
     if (!(acc >= 1e-290)) v = lse_twopass(c, n, xr);  // rare: underflow / NaN
     return v + shift;
 }
@@ -642,7 +732,7 @@ __device__ __forceinline__ double quant_lpdf(const Comp<double>* __restrict__ c,
         inc -= w * pl;
         prob += inc;
     }
-    return log(prob) - logpacc;
+    return flog(prob) - logpacc;
 }
 
 // Integration interval of a quantized candidate x (tpe.py:154-161 / 292-300);
@@ -663,8 +753,8 @@ __device__ __forceinline__ void quant_bounds(const DLabel& L, double x, double& 
         if (L.flags & 1) lb = np_max(lb, L.exp_low);
         lb = np_max(0.0, lb);
         negative = ub < 0.0;  // tpe.py:187-188 raises
-        ub = log(np_max(ub, kEps));
-        lb = log(np_max(lb, kEps));
+        ub = flog(np_max(ub, kEps));
+        lb = flog(np_max(lb, kEps));
     }
 }
 

@@ -197,28 +197,39 @@ __device__ __forceinline__ void draw_slots(const DLabel& L, const Slots& S, bool
                                            int32_t* __restrict__ err, double (&x)[R],
                                            int64_t (&z)[R], int64_t (&ci)[R], int64_t (&gi)[R],
                                            bool (&valid)[R]) {
+    uint32_t g32[R], rk[R], pend = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         S.template at<R>(r, n, z[r], ci[r], valid[r]);
         gi[r] = cand_offset + ci[r];
-        double v = lgmm ? 1.0 : 0.0;
+        g32[r] = (uint32_t)gi[r];
+        rk[r] = 0;
+        x[r] = lgmm ? 1.0 : 0.0;
         if (valid[r]) {
-            if constexpr (SAMPLE) {
-                bool ok;
-                if constexpr (MODE == DENSE_ANY)
-                    ok = lgmm ? sample_below<DENSE_LGMM>(L, samp + L.samp_off, seed, rounds[z[r]],
-                                                         (uint32_t)gi[r], v)
-                              : sample_below<DENSE_GMM>(L, samp + L.samp_off, seed, rounds[z[r]],
-                                                        (uint32_t)gi[r], v);
-                else
-                    ok = sample_below<MODE>(L, samp + L.samp_off, seed, rounds[z[r]],
-                                            (uint32_t)gi[r], v);
-                if (!ok) atomicOr(err, 1);
-            } else {
-                v = cand_in[ci[r]];
+            pend |= 1u << r;
+            if constexpr (SAMPLE) rk[r] = rounds[z[r]];
+            else x[r] = cand_in[ci[r]];
+        }
+    }
+    if constexpr (SAMPLE) {
+        if constexpr (MODE == CAT) {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                if (valid[r]) (void)sample_below<CAT>(L, samp + L.samp_off, seed, rk[r], g32[r], x[r]);
+        } else {
+            bool ok;
+            if constexpr (MODE == DENSE_ANY)
+                ok = lgmm ? sample_slots<DENSE_LGMM, R>(L, samp + L.samp_off, seed, rk, g32, pend, x)
+                          : sample_slots<DENSE_GMM, R>(L, samp + L.samp_off, seed, rk, g32, pend, x);
+            else
+                ok = sample_slots<MODE, R>(L, samp + L.samp_off, seed, rk, g32, pend, x);
+            if (!ok) atomicOr(err, 1);
+            if (L.flags & 4) {
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    if (valid[r]) x[r] = quantize(x[r], L.q);
             }
         }
-        x[r] = v;
     }
 }
 
@@ -249,7 +260,7 @@ __global__ __launch_bounds__(kBlock) void k_round(
         double y[R];
         if (lgmm) {
 #pragma unroll
-            for (int r = 0; r < R; ++r) y[r] = log(x[r]);
+            for (int r = 0; r < R; ++r) y[r] = flog(x[r]);
         } else {
 #pragma unroll
             for (int r = 0; r < R; ++r) y[r] = x[r];
@@ -331,7 +342,7 @@ __global__ __launch_bounds__(kBlock) void k_round_chunk(
     draw_slots<DENSE_ANY, true, R>(L, S, lgmm, samp, nullptr, n, cand_offset, seed, rounds, err, x,
                                    z, ci, gi, valid);
 #pragma unroll
-    for (int r = 0; r < R; ++r) y[r] = lgmm ? log(x[r]) : x[r];
+    for (int r = 0; r < R; ++r) y[r] = lgmm ? flog(x[r]) : x[r];
     const int k0 = min(c * chunk, L.na), k1 = min(k0 + chunk, L.na);
     double sb[R], sa[R];
     if constexpr (kTab) {
@@ -391,7 +402,7 @@ __global__ __launch_bounds__(kBlock) void k_finish_chunks(
         const double sb = part[chunk_plane(by, 1, nch, bx, gx, R) + s];
         double sa = 0.0;
         for (int c = 0; c < nch; ++c) sa += part[chunk_plane(by, 2 + c, nch, bx, gx, R) + s];
-        const double y = lgmm ? log(x[r]) : x[r];
+        const double y = lgmm ? flog(x[r]) : x[r];
         if constexpr (sizeof(T) == 8) {
             lb[r] = lse_finish(comps + L.comp_b, L.nb, sb, y - L.centre, L.shift_b);
             la[r] = lse_finish(comps + L.comp_a, L.na, sa, y - L.centre, L.shift_a);
@@ -463,7 +474,7 @@ __global__ __launch_bounds__(kBlock) void k_screen(
     float xf[R], ab[R], aa[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        y[r] = lgmm ? log(x[r]) : x[r];
+        y[r] = lgmm ? flog(x[r]) : x[r];
         const double xr = y[r] - L.centre;
         xf[r] = (float)xr;
         X[r] = fabs(xr);
@@ -540,7 +551,7 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
     double y[R], xr[R], acc[R], lb[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        y[r] = lgmm ? log(x[r]) : x[r];
+        y[r] = lgmm ? flog(x[r]) : x[r];
         xr[r] = y[r] - L.centre;
         acc[r] = 0.0;
     }
@@ -565,7 +576,12 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
 #pragma unroll
             for (int k = kBxP - 2; k >= 0; --k) poly = fma(poly, delta, rw[k]);
             const double eabs = rw[kBxP];
-            const double sclip = exp(-B.kappa * delta * delta) * poly;
+            // exp(-t), t = kappa delta^2 <= kappa rmax^2 <= 0.0225 / (T ln 2) < 4e-4:
+            // degree 5 leaves t^6 / 720 < 1e-23 (inside the 8 u S_clip term)
+            const double t = B.kappa * delta * delta;
+            const double et = fma(fma(fma(fma(fma(-1.0 / 120.0, t, 1.0 / 24.0), t, -1.0 / 6.0), t, 0.5), t,
+                                      -1.0), t, 1.0);
+            const double sclip = et * poly;
             const int j0 = loff[B.cnt_off + b], j1 = loff[B.cnt_off + b + 1];
             const int32_t* lst = list + B.list_off;
             double snc = 0.0;
@@ -579,8 +595,8 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
             const double ea = eabs + 8.0 * 0x1.0p-53 * fabs(sclip) + skip_abs +
                               (3e-14 + (double)(j1 - j0 + 4) * 0x1.0p-53) * snc + 0x1.0p-52 * sum;
             const double eps = ea / sum;
-            if (fabs(delta) <= B.rmax && sum >= 1e-280 && eps <= 1e-6 && lb[r] == lb[r]) {
-                const double ls = log(sum);
+            if (fabs(delta) <= B.rmax && t <= 1e-3 && sum >= 1e-280 && eps <= 1e-6 && lb[r] == lb[r]) {
+                const double ls = flog(sum);
                 double la = ls + L.shift_a, lbr = lb[r];
                 if (lgmm) {
                     lbr -= y[r];
@@ -749,7 +765,7 @@ __global__ __launch_bounds__(kBlock) void k_rescore(
             else (void)sample_below<DENSE_GMM>(L, samp + L.samp_off, seed, rk, (uint32_t)gi[r], v);
         }
         x[r] = v;
-        yv[r] = lgmm ? log(v) : v;
+        yv[r] = lgmm ? flog(v) : v;
     }
     lse_dense<R>(comps64 + L.comp_b, L.nb, L.shift_b, L.centre, yv, lb, exp_tab);
     lse_dense<R>(comps64 + L.comp_a, L.na, L.shift_a, L.centre, yv, la, exp_tab);
@@ -837,11 +853,11 @@ __global__ __launch_bounds__(kBlock) void k_pick_packed(
         const double sb = part[chunk_plane(by, 1, nch, bx, gx, R) + s];
         double sa = 0.0;
         for (int c = 0; c < nch; ++c) sa += part[chunk_plane(by, 2 + c, nch, bx, gx, R) + s];
-        const double y = lgmm ? log(x) : x;
+        const double y = lgmm ? flog(x) : x;
         const double xr = y - L.centre;
         const float xf = (float)xr;
         const double X = fabs(xr), dx = fabs((double)xf - xr);
-        const double lb = log(sb) + L.shift_b, la = log(sa) + L.shift_a;
+        const double lb = flog(sb) + L.shift_b, la = flog(sa) + L.shift_a;
         const double s32 = lb - la;
         const double E = 1.25 * (screen_err(L.amax_b, L.nb, L.nb, X, dx, (float)sb, (float)log2(sb)) +
                                  screen_err(L.amax_a, L.na, chunk, X, dx, (float)sa, (float)log2(sa)) +
@@ -968,7 +984,7 @@ __global__ __launch_bounds__(kBlock) void k_rescore_packed(
             else (void)sample_below<DENSE_GMM>(L, samp + L.samp_off, seed, rk, gi, v);
         }
         x[r] = v;
-        xr[r] = (lgmm ? log(v) : v) - L.centre;
+        xr[r] = (lgmm ? flog(v) : v) - L.centre;
         sb[r] = 0.0;
         sa[r] = 0.0;
     }
@@ -1005,7 +1021,7 @@ __global__ __launch_bounds__(kBlock) void k_finish_rescore(
         const double sb = planes[g], x = planes[(size_t)total + g];
         double sa = 0.0;
         for (int c = 0; c < nch; ++c) sa += planes[(size_t)(2 + c) * total + g];
-        const double yv = lgmm ? log(x) : x;
+        const double yv = lgmm ? flog(x) : x;
         double lb = lse_finish(comps64 + L.comp_b, L.nb, sb, yv - L.centre, L.shift_b);
         double la = lse_finish(comps64 + L.comp_a, L.na, sa, yv - L.centre, L.shift_a);
         if (lgmm) {
@@ -1086,7 +1102,7 @@ __device__ __forceinline__ double slice_sum(const DLabel& L, const Comp<T>* __re
                                             double x, const double* __restrict__ tab) {
     if constexpr (MODE == DENSE_GMM || MODE == DENSE_LGMM || MODE == DENSE_ANY) {
         const bool lgmm = MODE == DENSE_LGMM || (MODE == DENSE_ANY && L.mode == DENSE_LGMM);
-        const double v = lgmm ? log(x) : x;
+        const double v = lgmm ? flog(x) : x;
         if constexpr (sizeof(T) == 8) {
             const double xr[1] = {v - L.centre};
             double acc[1] = {0.0};
@@ -1188,7 +1204,7 @@ __global__ __launch_bounds__(kBlock) void k_finish_slices(
         double lb, la;
         if constexpr (MODE == DENSE_GMM || MODE == DENSE_LGMM || MODE == DENSE_ANY) {
             const bool lgmm = MODE == DENSE_LGMM || (MODE == DENSE_ANY && L.mode == DENSE_LGMM);
-            const double y = lgmm ? log(x) : x;
+            const double y = lgmm ? flog(x) : x;
             if constexpr (sizeof(T) == 8) {
                 lb = lse_finish(comps + L.comp_b, L.nb, sb, y - L.centre, L.shift_b);
                 la = lse_finish(comps + L.comp_a, L.na, sa, y - L.centre, L.shift_a);
@@ -1205,8 +1221,8 @@ __global__ __launch_bounds__(kBlock) void k_finish_slices(
             bool neg;
             quant_bounds<MODE>(L, x, ub, lo, neg);
             if (neg) atomicOr(err, 2);
-            lb = log(sb) - L.logpacc_b;
-            la = log(sa) - L.logpacc_a;
+            lb = flog(sb) - L.logpacc_b;
+            la = flog(sa) - L.logpacc_a;
         }
         const int64_t gi = cand_offset + c;
         const uint64_t key = order_key(lb - la);
@@ -1237,16 +1253,24 @@ __global__ __launch_bounds__(kBlock) void k_qsample(
     // grid window of the label (all rounds of this launch share one table
     // window): thread -> wave -> workgroup, then one atomic pair per workgroup
     unsigned long long mn = ~0ull, mx = 0ull;
+    int64_t zs[R], is[R];
+    bool vs[R];
+    uint32_t g32[R], rk[R], pend = 0;
+    double xs[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        int64_t z, i;
-        bool valid;
-        S.template at<R>(r, n, z, i, valid);
-        if (valid) {
-            double v;
-            if (!sample_raw<MODE>(L, samp + L.samp_off, seed, rounds[z],
-                                  (uint32_t)(cand_offset + i), v))
-                atomicOr(err, 1);
+        S.template at<R>(r, n, zs[r], is[r], vs[r]);
+        g32[r] = (uint32_t)(cand_offset + is[r]);
+        rk[r] = vs[r] ? rounds[zs[r]] : 0u;
+        xs[r] = 0.0;
+        if (vs[r]) pend |= 1u << r;
+    }
+    if (!sample_slots<MODE, R>(L, samp + L.samp_off, seed, rk, g32, pend, xs)) atomicOr(err, 1);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int64_t z = zs[r], i = is[r];
+        if (vs[r]) {
+            const double v = xs[r];
             const double jd = rint(v / L.q);
             int64_t j = 0;
             if (jd >= -0x1.0p52 && jd <= 0x1.0p52) j = (int64_t)jd;
@@ -1311,7 +1335,7 @@ __global__ __launch_bounds__(kBlock) void k_qtable(
             pb += wp[w].x;
             pa += wp[w].y;
         }
-        tab[Q.tab_off + s] = make_double2(log(pb) - L.logpacc_b, log(pa) - L.logpacc_a);
+        tab[Q.tab_off + s] = make_double2(flog(pb) - L.logpacc_b, flog(pa) - L.logpacc_a);
     }
 }
 

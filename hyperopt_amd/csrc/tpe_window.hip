@@ -536,7 +536,7 @@ __global__ __launch_bounds__(kBlock) void k_win_key(
         } else {
             v = cand_in[i];
         }
-        const double xr = (lgmm ? log(v) : v) - L.centre;
+        const double xr = (lgmm ? flog(v) : v) - L.centre;
         const size_t pos = (size_t)cell * ncell + j;
         const uint32_t bin = (uint32_t)win_bin(W, xr);
         if (keys8) keys8[pos] = (uint8_t)(bin >> (kWinBinBits - kCoarseBits));
