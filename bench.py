@@ -48,6 +48,9 @@ FLOPS_PER_EVAL = {'f64': 6.0, 'f32': 6.0}
 #   k_screen: the same with 8 candidates per thread (v_mov_b64 per 8 evals) =
 #         3.5625 slots
 VALU_SLOTS_PER_EVAL = {'f64': 12.25, 'f32': 3.625, 'screen': 3.5625}
+# expansion screen (k_screen_bx): per candidate a 13-coefficient Horner
+# polynomial (13 FMA) and the degree-5 exp(-kappa delta^2) factor (5 FMA)
+BX_FLOPS_PER_CAND = 2 * 13 + 2 * 5
 PEAK_FP64_VECTOR_TFLOPS = 78.6        # MI355X spec (MI355X_MICROARCH.md)
 PEAK_FP32_VECTOR_TFLOPS = 157.3
 # 4-cycle wave64 VALU issue slots per second at 2.4 GHz, in lanes: 256 CU x
@@ -342,10 +345,25 @@ def main():
     prec = args.precision
     dom = max((k for k in mode_ms if k in DENSE), key=lambda k: mode_ms[k])
     screened = scr[0] > 0
-    windowed = screened and not args.no_window and C >= 8192 and args.config != 5
-    if screened:
-        # the screening kernel: the (candidate, component) terms it actually
-        # summed (tpe_last_screen_terms) over its own device time
+    smode = eng.last_screen_mode() if screened else 0
+    windowed = smode == 2
+    slots = None
+    if smode == 3:
+        # the expansion screen: per candidate the below mixture and the
+        # bin's list of unclipped components as direct fp64 terms (6 FLOP
+        # each; tpe_last_screen_terms) and the bin's 13-term
+        # polynomial + exp factor (BX_FLOPS_PER_CAND), over its device time
+        dom_ms = scr[2]
+        kprec = 'f64'
+        kname = 'k_screen_bx<'
+        kdesc = 'k_screen_bx (expansion screen of the fp64 round, GMM1+LGMM1 labels: below mixture ' \
+                'and unclipped components as fp64 terms, the equal-sigma above components as a ' \
+                'per-bin Taylor polynomial)'
+        dom_rate = scr[3] / (dom_ms * 1e-3)
+        dom_flops = scr[3] * FLOPS_PER_EVAL['f64'] + scr[0] * BX_FLOPS_PER_CAND
+    elif screened:
+        # the fp32 screening kernel: the (candidate, component) terms it
+        # actually summed (tpe_last_screen_terms) over its own device time
         dom_ms = scr[2]
         kprec = 'f32'
         if windowed:
@@ -354,6 +372,8 @@ def main():
         else:
             kname, kdesc = 'k_screen<', 'k_screen (fp32 screen of the fp64 round, GMM1+LGMM1 labels)'
         dom_rate = scr[3] / (dom_ms * 1e-3)
+        dom_flops = scr[3] * FLOPS_PER_EVAL['f32']
+        slots = VALU_SLOTS_PER_EVAL['screen']
     else:
         dom_ms = mode_ms[dom]
         kprec = prec
@@ -361,22 +381,30 @@ def main():
                                            8 if dom == 'dense' else 1)
         kdesc = 'k_round<%s,%s>' % (prec, dom + ' (GMM1+LGMM1 labels)')
         dom_rate = mode_ev[dom] / (dom_ms * 1e-3)
+        dom_flops = mode_ev[dom] * FLOPS_PER_EVAL[prec]
+        slots = VALU_SLOTS_PER_EVAL[prec]
     peak = PEAK_FP64_VECTOR_TFLOPS if kprec == 'f64' else PEAK_FP32_VECTOR_TFLOPS
     # PMC figures come from the committed profile of the default workload
     # (config 3, tools/prof_round.sh): only that workload's line carries them
     traffic, valu_busy, traffic_src = (measured_pmc(kname) if args.config == 3 and world == 1
                                        and args.cand_log2 == 24 and args.labels == 32
                                        else (None, None, None))
-    achieved = dom_rate * FLOPS_PER_EVAL[kprec] / 1e12
+    achieved = dom_flops / (dom_ms * 1e-3) / 1e12
     roof = {'bound': 'valu', 'kernel': kdesc,
             'achieved': round(achieved, 3), 'peak': peak, 'unit': 'TFLOP/s',
             'frac': round(achieved / peak, 4), 'traffic': traffic,
             'traffic_source': traffic_src, 'valu_busy_measured': valu_busy,
             'valu_busy_source': traffic_src,
             'evals_per_s': dom_rate, 'flops_per_eval': FLOPS_PER_EVAL[kprec],
-            'valu_issue_frac': round(dom_rate * VALU_SLOTS_PER_EVAL['screen' if screened else kprec] /
-                                     PEAK_VALU_LANE_INSTR[kprec], 4),
+            'valu_issue_frac': (round(dom_rate * slots / PEAK_VALU_LANE_INSTR[kprec], 4)
+                                if slots else None),
             'launch_ms': dom_ms / args.steps}
+    if smode == 3:
+        roof['flops_per_candidate_poly'] = BX_FLOPS_PER_CAND
+        roof['note'] = ('VALU-issue bound: per candidate the Philox + Box-Muller draw, the fp64 '
+                        'exp / log sequences and the bound take most of the instruction stream; '
+                        'achieved counts only the lpdf arithmetic (6 FLOP per direct term, 36 per '
+                        'polynomial); valu_busy_measured is the PMC utilisation of the same kernel')
     line = {
         'metric': 'TPE candidate x component lpdf evals/sec (10k-trial history)',
         'value': value, 'unit': 'evals/s', 'n_gpus': len(set(devs)) if devs else world,
@@ -414,6 +442,7 @@ def main():
             'screen_kernel_ms': round(scr[2] / args.steps, 3),
             'other_dense_ms': round((mode_ms[dom] - scr[2]) / args.steps, 3),
             'windowed': windowed,
+            'mode': {0: 'none', 1: 'plain fp32', 2: 'windowed fp32', 3: 'expansion (fp64)'}[smode],
             'screen_terms_per_step': scr[3] // args.steps,
             'screen_terms_fraction': scr[3] / max(mode_ev[dom], 1),
             'note': 'dense labels: every (candidate, component) pair is either evaluated in '
@@ -421,6 +450,7 @@ def main():
                     'sorted into tiles of neighbours) proven below 2^-T (win_t) of the largest term and '
                     'covered by the bound; candidates whose bound interval reaches the '
                     'round\'s best lower bound are re-scored in fp64 over every component -- '
+                    '(expansion screen: fp64 score, bound ~1e-12, so only near-ties) -- '
                     'winners and lpdfs are bit-identical to the plain fp64 round '
                     '(tests/test_screen.py).  `value` counts the terms executed (screen + '
                     're-score); the roofline counts the terms the screening kernel summed.  '

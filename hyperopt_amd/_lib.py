@@ -120,6 +120,7 @@ SIGNATURES = {
     'tpe_set_option': (ctypes.c_int, [_P, _I32, _I64]),
     'tpe_last_screen_terms': (ctypes.c_int, [_P, _P]),
     'tpe_last_rescore_terms': (ctypes.c_int, [_P, _P]),
+    'tpe_last_screen_mode': (ctypes.c_int32, [_P]),
     'tpe_screen_probe': (ctypes.c_int, [_P, _I32, _P, _I64, _P, _P]),
 }
 

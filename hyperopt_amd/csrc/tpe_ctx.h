@@ -250,8 +250,11 @@ struct tpe_ctx {
     DevBuf<int64_t> scr_rsel;            //   per (round, label): {first, count} int32 pairs
     DevBuf<int64_t> scr_off;             //   per label: offset of its entries in the compacted order
     DevBuf<double> scr_planes;           //   re-score sums: below | x | above chunk c, per entry
+    DevBuf<double> rs_x, rs_part;        // sliced re-score: candidates, slice sums
+    DevBuf<int64_t> rs_g;                //   and their global indices
     std::vector<tpe_rt::RescoreChunkH> scr_chunks_h;
     int64_t screen_total = 0, screen_rescored = 0;   // last round
+    int32_t screen_mode = 0;             // last round: tpe_last_screen_mode
     bool screen_pending = false;         // scr_cnt_h awaits the round's final sync
     // windowed screen (large tile-map rounds): candidates keyed by (round,
     // label, bin) and stably sorted with their (x' fp32, index) values

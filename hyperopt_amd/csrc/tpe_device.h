@@ -331,9 +331,9 @@ __device__ __forceinline__ float lse_twopass(const Comp<float>* __restrict__ c, 
 // that wait.  The plain loop issued them just before it (config 3: 97 ->
 // 98 % of the issue rate; config 5: +25 %).
 template <int R>
-__device__ __forceinline__ void lse_acc(const Comp<double>* __restrict__ c, int n,
-                                        const double (&x)[R], double (&acc)[R],
-                                        const double* __restrict__ tab) {
+__device__ __forceinline__ void lse_acc_run(const Comp<double>* __restrict__ c, int n,
+                                            const double (&x)[R], double (&acc)[R],
+                                            const double* __restrict__ tab) {
     if (n <= 0) return;
     constexpr int U = R >= 2 ? 4 : 8;
     const int nbat = n / U, nfull = nbat * U;
@@ -388,6 +388,27 @@ __device__ __forceinline__ void lse_acc(const Comp<double>* __restrict__ c, int 
             const double z = fma(x[r], a, -m);
             acc[r] = exp_scaled_acc(fma(-z, z, cc), tab, acc[r]);
         }
+    }
+}
+
+// The fp64 summation order of a dense mixture, shared by every fp64 kernel
+// (tile, split-K and packed maps, the re-scores): slices of kSumSlice
+// consecutive components, each summed in order from 0, the slice sums
+// added in order to acc.  Fixing it lets a sum be split across waves by
+// slices (k_score_slices, k_rescore_slices) with the same bits.
+constexpr int kSumSlice = 256;
+
+template <int R>
+__device__ __forceinline__ void lse_acc(const Comp<double>* __restrict__ c, int n,
+                                        const double (&x)[R], double (&acc)[R],
+                                        const double* __restrict__ tab) {
+    for (int k0 = 0; k0 < n; k0 += kSumSlice) {
+        double part[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) part[r] = 0.0;
+        lse_acc_run<R>(c + k0, min(kSumSlice, n - k0), x, part, tab);
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] += part[r];
     }
 }
 

@@ -534,7 +534,8 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
     const BxLabel* __restrict__ bx, const double* __restrict__ tab, const int32_t* __restrict__ loff,
     const int32_t* __restrict__ list, int64_t n, int64_t cand_offset, uint64_t seed,
     const uint32_t* __restrict__ rounds, int32_t nl, double* __restrict__ hi,
-    unsigned long long* __restrict__ lbkey, unsigned long long* __restrict__ terms,
+    unsigned long long* __restrict__ lbkey, int32_t* __restrict__ cnt, int32_t* __restrict__ idx,
+    unsigned long long* __restrict__ terms,
     int32_t* __restrict__ err, Slots S, const double* __restrict__ cand_in,
     double* __restrict__ s_out, double* __restrict__ e_out) {
     const int li = group[blockIdx.y];
@@ -548,9 +549,10 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
     bool valid[R];
     draw_slots<DENSE_ANY, SAMPLE, R>(L, S, lgmm, samp, cand_in, n, cand_offset, seed, rounds, err,
                                      x, z, ci, gi, valid);
-    double y[R], xr[R], acc[R], lb[R];
+    double y[R], xr[R], acc[R], lb[R], hv[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
+        hv[r] = __builtin_inf();
         y[r] = lgmm ? flog(x[r]) : x[r];
         xr[r] = y[r] - L.centre;
         acc[r] = 0.0;
@@ -561,7 +563,6 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
     for (int r = 0; r < R; ++r) lb[r] = lse_finish(comps64 + L.comp_b, L.nb, acc[r], xr[r], L.shift_b);
     const Comp<double>* ca = comps64 + L.comp_a;
     const double skip_abs = (double)L.na * exp2(-kBxT);
-    const size_t row0 = ((size_t)blockIdx.z * nl + blockIdx.y) * (size_t)n;
     uint64_t bk = 0;
     int nterms = 0;
 #pragma unroll
@@ -618,13 +619,47 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
             const uint64_t k = order_key(s - E);
             bk = k > bk ? k : bk;
         }
-        hi[row0 + ci[r]] = h;
+        hv[r] = h;
     }
     if constexpr (!SAMPLE) return;
     __shared__ uint64_t sh[kBlock / 64];
     bk = block_max_key(bk, sh);
-    if (threadIdx.x == 0 && bk) atomicMax(lbkey + (size_t)blockIdx.z * nl + blockIdx.y, bk);
-    // (block_max_key's barrier orders sh's reuse)
+    const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
+    if (threadIdx.x == 0 && bk) atomicMax(lbkey + cell, bk);
+    // candidates whose upper bound reaches this workgroup's best lower bound
+    // (every one the round's best lower bound can select is among them):
+    // appended to the cell's list with one atomic per workgroup
+    bool take[R];
+    int mine = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        take[r] = valid[r] && order_key(hv[r]) >= bk;
+        mine += take[r];
+    }
+    __shared__ int shc[kBlock / 64], shb;
+    int tw = mine;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(tw, off);
+        if ((threadIdx.x & 63) >= off) tw += o;
+    }
+    if ((threadIdx.x & 63) == 63) shc[threadIdx.x >> 6] = tw;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) tot += shc[w];
+        shb = tot ? atomicAdd(cnt + cell, tot) : 0;
+    }
+    __syncthreads();
+    int at = shb + tw - mine;
+    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) at += shc[w];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (take[r]) {
+            idx[cell * (size_t)n + at] = (int32_t)ci[r];
+            hi[cell * (size_t)n + at] = hv[r];
+            ++at;
+        }
     __shared__ int shn[kBlock / 64];
     int t = nterms;
 #pragma unroll
@@ -636,6 +671,41 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
         for (int w = 0; w < kBlock / 64; ++w) tot += (unsigned long long)shn[w];
         atomicAdd(terms, tot);
     }
+}
+
+// The expansion screen's per-cell lists (candidate index, upper bound) hold
+// every candidate whose bound reached its workgroup's best lower bound;
+// keep those that reach the cell's (the round's) best, compacted in place.
+// One workgroup per cell; chunks in order, so writes never pass reads.
+__global__ __launch_bounds__(kBlock) void k_select_list(const double* __restrict__ hi, int64_t n,
+                                                        const unsigned long long* __restrict__ lbkey,
+                                                        int32_t* __restrict__ cnt, int32_t* __restrict__ idx) {
+    const size_t cell = blockIdx.x;
+    const uint64_t lb = lbkey[cell];
+    const int len = cnt[cell];
+    int32_t* il = idx + cell * (size_t)n;
+    const double* hl = hi + cell * (size_t)n;
+    __shared__ int shc[kBlock / 64];
+    int out = 0;
+    for (int j0 = 0; j0 < len; j0 += kBlock) {
+        const int j = j0 + threadIdx.x;
+        const bool keep = j < len && order_key(hl[j]) >= lb;
+        const int32_t v = j < len ? il[j] : 0;
+        const uint64_t m = __ballot(keep);
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        if (lane == 0) shc[wave] = __popcll(m);
+        __syncthreads();   // every read of this chunk is done
+        int at = out + __popcll(m & ((1ull << lane) - 1ull));
+        int tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            if (w < wave) at += shc[w];
+            tot += shc[w];
+        }
+        if (keep) il[at] = v;
+        out += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) cnt[cell] = out;
 }
 
 // Each workgroup owns a contiguous slice of its (round, label) row: it
@@ -714,6 +784,8 @@ using RescoreChunk = tpe_rt::RescoreChunkH;
 #define TPE_RESCORE_R 2
 #endif
 constexpr int kRescoreR = TPE_RESCORE_R;
+// at most this many candidates to re-score in a round: split by slices
+constexpr int64_t kSlicedRescoreMax = 1 << 16;
 
 // candidates per thread in k_screen (its own tile width): the component's
 // m shared by more candidates costs fewer v_mov_b64 per eval
@@ -788,6 +860,111 @@ __global__ __launch_bounds__(kBlock) void k_rescore(
     __shared__ Partial sh[kBlock / 64];
     block_maxloc(bk, bi, bv, bl, ba, res + blockIdx.x, sh);
     (void)z;
+}
+
+// The re-score of a few candidates per (round, dense label) -- the
+// expansion screen leaves a handful of near-ties -- split by summation
+// slices so it fills the chip instead of one wave per label walking 10k
+// components: k_rescore_draw re-draws each listed candidate once,
+// k_rescore_slices sums one kSumSlice slice of one mixture for the 64
+// candidates of a table entry per wave, and k_rescore_fin adds the slices in
+// order (lse_acc's order: the bits of the fp64 round) and keeps the entry's
+// best.  Entry = RescoreChunk{cell, j}: candidates [64 j, 64 j + 64) of the
+// cell's list.  part: [entry][s_max slices][64].
+constexpr int kRsW = 64;
+
+__global__ __launch_bounds__(kBlock) void k_rescore_draw(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const SampRec* __restrict__ samp, int64_t n, int64_t cand_offset, uint64_t seed,
+    const uint32_t* __restrict__ rounds, int32_t nl, int32_t n_entries, const int32_t* __restrict__ cnt,
+    const int32_t* __restrict__ idx, const RescoreChunk* __restrict__ chunks, double* __restrict__ xbuf,
+    int64_t* __restrict__ gbuf) {
+    const int e = blockIdx.x * (kBlock / kRsW) + threadIdx.x / kRsW, lane = threadIdx.x % kRsW;
+    if (e >= n_entries) return;
+    const RescoreChunk ch = chunks[e];
+    const int32_t z = ch.cell / nl, y = ch.cell % nl;
+    const DLabel L = labels[group[y]];
+    const int64_t j = (int64_t)ch.j * kRsW + lane;
+    double v = __builtin_nan("");
+    int64_t g = -1;
+    if (j < cnt[ch.cell]) {
+        g = cand_offset + idx[(size_t)ch.cell * (size_t)n + j];
+        if (L.mode == DENSE_LGMM) (void)sample_below<DENSE_LGMM>(L, samp + L.samp_off, seed, rounds[z], (uint32_t)g, v);
+        else (void)sample_below<DENSE_GMM>(L, samp + L.samp_off, seed, rounds[z], (uint32_t)g, v);
+    }
+    xbuf[(size_t)e * kRsW + lane] = v;
+    gbuf[(size_t)e * kRsW + lane] = g;
+}
+
+__global__ __launch_bounds__(kBlock) void k_rescore_slices(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<double>* __restrict__ comps64, int32_t nl, const RescoreChunk* __restrict__ chunks,
+    const double* __restrict__ xbuf, int32_t s_max, double* __restrict__ part) {
+    __shared__ double exp_tab[kExpTabSize];
+    load_exp_table(exp_tab);   // (every wave takes part before any leaves)
+    const int e = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const RescoreChunk ch = chunks[e];
+    const DLabel L = labels[group[ch.cell % nl]];
+    const int nsb = (L.nb + kSumSlice - 1) / kSumSlice, nsa = (L.na + kSumSlice - 1) / kSumSlice;
+    const int slice = blockIdx.x * (kBlock / 64) + wave;
+    if (slice >= nsb + nsa) return;
+    const bool above = slice >= nsb;
+    const int k0 = (above ? slice - nsb : slice) * kSumSlice;
+    const int k1 = min(k0 + kSumSlice, above ? L.na : L.nb);
+    const double x = xbuf[(size_t)e * kRsW + lane];
+    const double xr[1] = {(L.mode == DENSE_LGMM ? flog(x) : x) - L.centre};
+    double acc[1] = {0.0};
+    lse_acc_run<1>(comps64 + (above ? L.comp_a : L.comp_b) + k0, k1 - k0, xr, acc, exp_tab);
+    part[((size_t)e * s_max + slice) * kRsW + lane] = acc[0];
+}
+
+__global__ __launch_bounds__(kRsW) void k_rescore_fin(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<double>* __restrict__ comps64, int32_t nl, const RescoreChunk* __restrict__ chunks,
+    const double* __restrict__ xbuf, const int64_t* __restrict__ gbuf, int32_t s_max,
+    const double* __restrict__ part, Partial* __restrict__ res) {
+    const int e = blockIdx.x, lane = threadIdx.x;
+    const RescoreChunk ch = chunks[e];
+    const DLabel L = labels[group[ch.cell % nl]];
+    const bool lgmm = L.mode == DENSE_LGMM;
+    const int nsb = (L.nb + kSumSlice - 1) / kSumSlice, nsa = (L.na + kSumSlice - 1) / kSumSlice;
+    const double x = xbuf[(size_t)e * kRsW + lane];
+    const int64_t g = gbuf[(size_t)e * kRsW + lane];
+    const double* p = part + (size_t)e * s_max * kRsW + lane;
+    uint64_t bk = 0;
+    int64_t bi = INT64_MAX;
+    double bv = 0.0, bl = 0.0, ba = 0.0;
+    if (g >= 0) {   // (padding lanes would take lse_finish's two-pass fallback)
+        double sb = 0.0, sa = 0.0;
+        for (int s = 0; s < nsb; ++s) sb += p[(size_t)s * kRsW];
+        for (int s = nsb; s < nsb + nsa; ++s) sa += p[(size_t)s * kRsW];
+        const double y = lgmm ? flog(x) : x;
+        double lb = lse_finish(comps64 + L.comp_b, L.nb, sb, y - L.centre, L.shift_b);
+        double la = lse_finish(comps64 + L.comp_a, L.na, sa, y - L.centre, L.shift_a);
+        if (lgmm) {
+            lb -= y;
+            la -= y;
+        }
+        bk = order_key(lb - la);
+        bi = g;
+        bv = x;
+        bl = lb;
+        ba = la;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t ok = __shfl_xor(bk, off);
+        const int64_t oi = __shfl_xor(bi, off);
+        const double ov = __shfl_xor(bv, off), ol = __shfl_xor(bl, off), oa = __shfl_xor(ba, off);
+        if (better(ok, oi, bk, bi)) {
+            bk = ok;
+            bi = oi;
+            bv = ov;
+            bl = ol;
+            ba = oa;
+        }
+    }
+    if (lane == 0) res[e] = Partial{bk, bi, bv, bl, ba};
 }
 
 // one thread per (round, dense label) cell: the best of its re-score chunks
@@ -1062,7 +1239,7 @@ __global__ __launch_bounds__(kBlock) void k_pick_rounds(const int32_t* __restric
 // the round (partial sums relative to the same LSE shift, or partial
 // probabilities for quantized labels), and a finishing kernel adds the
 // slices in order, takes the log and does the broadcast_best maxloc.
-constexpr int kSlice = 256;      // dense: ~12 VALU per component
+constexpr int kSlice = kSumSlice;   // dense (the fp64 sum order, tpe_device.h): ~12 VALU per component
 constexpr int kSliceQ = 64;      // quantized: two erf per component
 constexpr int kSliceWaves = kBlock / 64;
 
@@ -1771,6 +1948,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
         HIPCHK(ctx, hipMemsetAsync(ctx->scr_lb.p, 0, cells * sizeof(unsigned long long), ctx->stream));
         HIPCHK(ctx, hipMemsetAsync(ctx->scr_cnt.p, 0, cells * sizeof(int32_t), ctx->stream));
         const unsigned sx = (unsigned)std::min<int64_t>((a.n + 8 * kBlock - 1) / (8 * kBlock), 1024);
+        ctx->screen_mode = use_bx ? 3 : (ctx->window && a.n >= kWinMinN && a.cand_in == nullptr) ? 2 : 1;
         if (use_bx) {
             // expansion screen: no sort, ~1e-12 bounds, near-ties re-scored
             tpe_rt::Posterior& P = *ctx->P;
@@ -1781,11 +1959,11 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
             hipLaunchKernelGGL((k_screen_bx<kBxR, true>), dim3(bgx, nl, a.gz), dim3(kBlock), 0, ctx->stream,
                                P.labels.p, grp, P.comps64.p, P.samp.p, P.bx.p, P.bx_tab.p, P.bx_loff.p,
                                P.bx_list.p, a.n, a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->scr_hid.p,
-                               ctx->scr_lb.p, ctx->win_evals.p, ctx->errflag.p, a.S, nullptr, nullptr, nullptr);
+                               ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p, ctx->win_evals.p, ctx->errflag.p,
+                               a.S, nullptr, nullptr, nullptr);
             if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
-            hipLaunchKernelGGL(k_select<double>, dim3(sx, nl, a.gz), dim3(kBlock), 0, ctx->stream,
-                               ctx->scr_hid.p, a.n, nl, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p, 0, 0, nl,
-                               nullptr);
+            hipLaunchKernelGGL(k_select_list, dim3((unsigned)cells), dim3(kBlock), 0, ctx->stream, ctx->scr_hid.p,
+                               a.n, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p);
             HIPCHK(ctx, hipMemcpyAsync(&ctx->screen_exec_h, ctx->win_evals.p, sizeof(unsigned long long),
                                        hipMemcpyDeviceToHost, ctx->stream));
             ctx->screen_exec_pending = true;
@@ -1878,7 +2056,11 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
         HIPCHK(ctx, hipMemcpyAsync(ctx->scr_cnt_h.data(), ctx->scr_cnt.p, cells * sizeof(int32_t),
                                    hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-        constexpr int64_t per = (int64_t)kRescoreR * kBlock;
+        // few candidates (the expansion screen's near-ties): split by slices
+        int64_t total_rs = 0;
+        for (size_t c = 0; c < cells; ++c) total_rs += ctx->scr_cnt_h[c];
+        const bool sliced = total_rs <= kSlicedRescoreMax;
+        const int64_t per = sliced ? (int64_t)kRsW : (int64_t)kRescoreR * kBlock;
         std::vector<RescoreChunk>& tab = ctx->scr_chunks_h;
         tab.clear();
         std::vector<int64_t> range(cells);
@@ -1887,7 +2069,39 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
             for (int32_t j = 0; (int64_t)j * per < ctx->scr_cnt_h[c]; ++j) tab.push_back(RescoreChunk{(int32_t)c, j});
             range[c] = (first << 32) | ((int64_t)tab.size() - first);
         }
-        if (!tab.empty()) {
+        if (!tab.empty() && sliced) {
+            int32_t s_max = 1;
+            for (int m : {DENSE_GMM, DENSE_LGMM})
+                for (int li : ctx->P->h_group[m]) {
+                    const DLabel& d = ctx->P->h_labels[li];
+                    s_max = std::max(s_max, (d.nb + kSumSlice - 1) / kSumSlice + (d.na + kSumSlice - 1) / kSumSlice);
+                }
+            const int32_t ne = (int32_t)tab.size();
+            HIPCHK(ctx, ctx->scr_chunks.reserve(ne));
+            HIPCHK(ctx, ctx->scr_res.reserve(ne));
+            HIPCHK(ctx, ctx->scr_off.reserve(cells));
+            HIPCHK(ctx, ctx->rs_x.reserve((size_t)ne * kRsW));
+            HIPCHK(ctx, ctx->rs_g.reserve((size_t)ne * kRsW));
+            HIPCHK(ctx, ctx->rs_part.reserve((size_t)ne * s_max * kRsW));
+            HIPCHK(ctx, hipMemcpyAsync(ctx->scr_chunks.p, tab.data(), ne * sizeof(RescoreChunk),
+                                       hipMemcpyHostToDevice, ctx->stream));
+            HIPCHK(ctx, hipMemcpyAsync(ctx->scr_off.p, range.data(), cells * sizeof(int64_t),
+                                       hipMemcpyHostToDevice, ctx->stream));
+            const RescoreChunk* chp = reinterpret_cast<const RescoreChunk*>(ctx->scr_chunks.p);
+            hipLaunchKernelGGL(k_rescore_draw, dim3((unsigned)((ne + kBlock / kRsW - 1) / (kBlock / kRsW))),
+                               dim3(kBlock), 0, ctx->stream, ctx->P->labels.p, grp, ctx->P->samp.p, a.n,
+                               a.cand_offset, a.seed, ctx->rounds.p, nl, ne, ctx->scr_cnt.p, ctx->scr_idx.p, chp,
+                               ctx->rs_x.p, ctx->rs_g.p);
+            hipLaunchKernelGGL(k_rescore_slices, dim3((unsigned)((s_max + 3) / 4), (unsigned)ne), dim3(kBlock), 0,
+                               ctx->stream, ctx->P->labels.p, grp, ctx->P->comps64.p, nl, chp, ctx->rs_x.p, s_max,
+                               ctx->rs_part.p);
+            hipLaunchKernelGGL(k_rescore_fin, dim3((unsigned)ne), dim3(kRsW), 0, ctx->stream, ctx->P->labels.p, grp,
+                               ctx->P->comps64.p, nl, chp, ctx->rs_x.p, ctx->rs_g.p, s_max, ctx->rs_part.p,
+                               ctx->scr_res.p);
+            hipLaunchKernelGGL(k_rescore_merge, dim3((unsigned)((cells + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                               ctx->stream, grp, nl, (int64_t)cells, ctx->P->n_labels, a.tiles, ctx->scr_off.p,
+                               ctx->scr_res.p, ctx->partials.p);
+        } else if (!tab.empty()) {
             HIPCHK(ctx, ctx->scr_chunks.reserve(tab.size()));
             HIPCHK(ctx, ctx->scr_res.reserve(tab.size()));
             HIPCHK(ctx, ctx->scr_off.reserve(cells));
@@ -2147,6 +2361,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     RoundArgs a{n, cand_offset, seed, n_rounds, tiles, cand_in_dev, olb, ola, S, gx, gz,
                 n_whole * rounds_whole, gx_whole};
     ctx->screen_total = ctx->screen_rescored = 0;
+    ctx->screen_mode = 0;
     ctx->screen_exec = 0;
     ctx->screen_rescore_terms = 0;
     ctx->evw_used = 0;
@@ -2659,7 +2874,8 @@ int tpe_screen_probe(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n,
         hipLaunchKernelGGL((k_screen_bx<kBxR, false>), dim3(bgx, 1, 1), dim3(kBlock), 0, ctx->stream,
                            P.labels.p, ctx->one_group.p, P.comps64.p, P.samp.p, P.bx.p, P.bx_tab.p,
                            P.bx_loff.p, P.bx_list.p, n, 0, 0, ctx->rounds.p, 1, nullptr, nullptr, nullptr,
-                           ctx->errflag.p, Slots{0, 0, 1}, ctx->cand.p, ctx->out_lb.p, ctx->out_la.p);
+                           nullptr, nullptr, ctx->errflag.p, Slots{0, 0, 1}, ctx->cand.p, ctx->out_lb.p,
+                           ctx->out_la.p);
     } else if (ctx->window && n >= 2048) {   // the windowed screen's tiles of sorted neighbours
         int rc = tpe_rt::win_prepare(ctx);
         if (rc) return rc;
@@ -2721,6 +2937,8 @@ int tpe_last_screen_terms(const tpe_ctx* ctx, int64_t* terms) {
     if (terms) *terms = ctx->screen_exec;
     return TPE_OK;
 }
+
+int32_t tpe_last_screen_mode(const tpe_ctx* ctx) { return ctx ? ctx->screen_mode : -1; }
 
 int tpe_last_rescore_terms(const tpe_ctx* ctx, int64_t* terms) {
     if (!ctx) return TPE_ERR_ARG;

@@ -159,6 +159,7 @@ void aggregate_stats(tpe_ctx* c) {
     c->screen_rescored = scr_r;
     c->screen_exec = scr_x;
     c->screen_rescore_terms = scr_rt;
+    c->screen_mode = dev(c, 0)->screen_mode;
     c->score_ms = score_ms;
     c->round_ms = round_ms;
     c->screen_ms = scr_ms;

@@ -245,6 +245,11 @@ class Engine(object):
         self._check(self.lib.tpe_last_screen_terms(self.h, ctypes.byref(t)))
         return t.value
 
+    def last_screen_mode(self):
+        """0 none, 1 plain fp32 screen, 2 windowed fp32 screen, 3 expansion
+        screen (the last round's dense tile-map labels)."""
+        return int(self.lib.tpe_last_screen_mode(self.h))
+
     def last_rescore_terms(self):
         """(candidate, component) terms the last round's fp64 re-score
         evaluated (every re-scored candidate over both of its mixtures)."""

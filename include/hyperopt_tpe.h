@@ -314,6 +314,12 @@ int tpe_last_screen_terms(const tpe_ctx *ctx, int64_t *terms);
  * With tpe_last_screen_terms this is the dense work the round executed. */
 int tpe_last_rescore_terms(const tpe_ctx *ctx, int64_t *terms);
 
+/* Which screen the last round's dense tile-map labels went through: 0 none
+ * (unscreened fp64, fp32 precision, or no dense tile round), 1 the plain
+ * fp32 screen, 2 the windowed fp32 screen, 3 the expansion screen
+ * (TPE_OPT_EXPAND); packed-map rounds report 0 here. */
+int32_t tpe_last_screen_mode(const tpe_ctx *ctx);
+
 /* Diagnostic of the screen (tests): for caller-supplied candidates of one
  * dense resident label, the fp32 score lpdf_below - lpdf_above the screen
  * computes and its rigorous error bound (x 1.25, as used by the round):

@@ -72,7 +72,7 @@ def main(src, tag):
             nlaunch[k] = n[k]
     # evals per launch of each dense family from a 1-step bench line
     pmc_bench = os.path.join(src, 'pmc_valu.log')
-    fam_evals, steps, win_terms = None, 1, None
+    fam_evals, steps, win_terms, cands = None, 1, None, None
     if os.path.exists(pmc_bench):
         for line in open(pmc_bench):
             if line.startswith('{"metric"'):
@@ -81,6 +81,7 @@ def main(src, tag):
                 steps = d.get('steps', 1) + d.get('warmup', 0)   # every step launches once
                 # the windowed screen's own terms (it skips the negligible pairs)
                 win_terms = d.get('screen', {}).get('screen_terms_per_step')
+                cands = d.get('screen', {}).get('screened_per_step')
     for k, v in summary.items():
         v['_launches'] = nlaunch.get(k)
         for pre, fam in FAMILY.items():
@@ -93,6 +94,11 @@ def main(src, tag):
             ev = win_terms * steps / max(nlaunch.get(k, 1), 1)
             v['_evals_per_launch'] = ev
             v['_valu_instr_per_eval'] = v['SQ_INSTS_VALU'] * 64 / ev
+        if k.startswith('k_screen_bx') and cands and 'SQ_INSTS_VALU' in v:
+            # the expansion screen: VALU instructions per candidate
+            c = cands * steps / max(nlaunch.get(k, 1), 1)
+            v['_candidates_per_launch'] = c
+            v['_valu_instr_per_candidate'] = v['SQ_INSTS_VALU'] * 64 / c
         if 'SQ_INSTS_VALU' in v and v.get('GRBM_GUI_ACTIVE'):
             # VALU issue utilisation: every wave64 VALU instruction holds a
             # 16-lane SIMD for 4 cycles; 1024 SIMDs; GRBM_GUI_ACTIVE / 8 XCDs
