@@ -239,6 +239,7 @@ struct tpe_ctx {
     bool screen = true;                  // TPE_NO_SCREEN=1 / TPE_OPT_SCREEN
     DevBuf<float> scr_hi;
     DevBuf<double> scr_hid;              // expansion screen: fp64 upper bounds
+    DevBuf<double2> bx_lohi;             //   packed map: fp64 (lower, upper) per candidate
     bool expand = true;                  // TPE_OPT_EXPAND: expansion screen when eligible
     DevBuf<int32_t> scr_idx;
     DevBuf<unsigned long long> scr_lb;

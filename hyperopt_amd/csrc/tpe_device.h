@@ -129,14 +129,68 @@ __device__ __forceinline__ int cdf_search(const SampRec* __restrict__ s, int n, 
 // truncation test.  The counter is (g, attempt, label stream, round).
 constexpr uint32_t kMaxAttempts = 1u << 16;
 
-__device__ __forceinline__ double draw_attempt(const DLabel& L, const SampRec* __restrict__ s, uint32_t k0,
-                                               uint32_t k1, uint32_t g, uint32_t it, uint32_t round) {
+// Component lookup of the draw: the first k with cdf[k] > u.  SampGlobal
+// searches the records in global memory; SampShared (a workgroup's copy in
+// LDS, stage_samp) starts from a 64-entry guide table (guide[j] = the first
+// k with cdf[k] > j / 64) and steps forward -- ~1.4 LDS reads instead of
+// log2(K) dependent global loads.  Both return the same component.
+struct SampGlobal {
+    const SampRec* __restrict__ s;
+    int ns;
+    __device__ __forceinline__ void pick(double u, double& mu, double& sg) const {
+        const int k = cdf_search(s, ns, u);
+        mu = s[k].mu;
+        sg = s[k].sigma;
+    }
+};
+
+constexpr int kSampLds = 64;   // below components staged in LDS (K_b <= 26 in practice)
+struct SampLds {
+    double cdf[kSampLds], mu[kSampLds], sg[kSampLds];
+    uint8_t guide[64];
+};
+
+struct SampShared {
+    const SampLds* __restrict__ t;
+    __device__ __forceinline__ void pick(double u, double& mu, double& sg) const {
+        int k = t->guide[(int)(u * 64.0)];
+        while (t->cdf[k] <= u) ++k;
+        mu = t->mu[k];
+        sg = t->sg[k];
+    }
+};
+
+// a workgroup's LDS copy of label L's below sampling records (false, and
+// nothing staged, when K_b > kSampLds); every thread must call it
+__device__ __forceinline__ bool stage_samp(const DLabel& L, const SampRec* __restrict__ samp, SampLds* t) {
+    if (L.ns > kSampLds || L.ns < 1) return false;
+    for (int k = threadIdx.x; k < L.ns; k += blockDim.x) {
+        const SampRec r = samp[L.samp_off + k];
+        t->cdf[k] = r.cdf;
+        t->mu[k] = r.mu;
+        t->sg[k] = r.sigma;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const double v = (double)threadIdx.x / 64.0;
+        int k = 0;
+        while (k < L.ns - 1 && t->cdf[k] <= v) ++k;
+        t->guide[threadIdx.x] = (uint8_t)k;
+    }
+    __syncthreads();
+    return true;
+}
+
+template <typename Src>
+__device__ __forceinline__ double draw_attempt(const DLabel& L, const Src& src, uint32_t k0, uint32_t k1,
+                                               uint32_t g, uint32_t it, uint32_t round) {
     const U4 r = philox4x32_10(U4{g, it, (uint32_t)L.stream, round}, k0, k1);
-    const int k = cdf_search(s, L.ns, (double)r.x * 0x1.0p-32);
+    double mu, sg;
+    src.pick((double)r.x * 0x1.0p-32, mu, sg);
     const double u1 = u01_open0(r.y, r.z);
     const double rad = sqrt(-2.0 * flog(u1));
     const double nrm = rad * cospi(2.0 * ((double)r.w * 0x1.0p-32));
-    return fma(s[k].sigma, nrm, s[k].mu);
+    return fma(sg, nrm, mu);
 }
 
 // Draw one sample of the below posterior for global candidate g, BEFORE
@@ -158,7 +212,7 @@ __device__ __forceinline__ bool sample_raw(const DLabel& L, const SampRec* __res
     } else {
         const bool bounded = (L.flags & 3) == 3;
         for (uint32_t it = 0; it < kMaxAttempts; ++it) {
-            const double draw = draw_attempt(L, s, k0, k1, g, it, round);
+            const double draw = draw_attempt(L, SampGlobal{s, L.ns}, k0, k1, g, it, round);
             if (!bounded || (L.low <= draw && draw < L.high)) {
                 out = (MODE == DENSE_LGMM || MODE == QUANT_LGMM) ? exp(draw) : draw;
                 return true;
@@ -177,8 +231,8 @@ __device__ __forceinline__ bool sample_raw(const DLabel& L, const SampRec* __res
 // [low, high), nearly every wave has a lane that retries.  Slots outside
 // `pend` keep their value.  Returns false if a slot hit the attempt cap
 // (its value is NaN).
-template <int MODE, int R>
-__device__ __forceinline__ bool sample_slots(const DLabel& L, const SampRec* __restrict__ s, uint64_t seed,
+template <int MODE, int R, typename Src>
+__device__ __forceinline__ bool sample_slots(const DLabel& L, const Src& src, uint64_t seed,
                                              const uint32_t (&rk)[R], const uint32_t (&g)[R], uint32_t pend,
                                              double (&out)[R]) {
     static_assert(MODE != CAT, "categorical slots draw once each");
@@ -196,7 +250,7 @@ __device__ __forceinline__ bool sample_slots(const DLabel& L, const SampRec* __r
                 gg = g[r];
                 rr = rk[r];
             }
-        const double draw = draw_attempt(L, s, k0, k1, gg, it, rr);
+        const double draw = draw_attempt(L, src, k0, k1, gg, it, rr);
         const bool acc = !bounded || (L.low <= draw && draw < L.high);
         if (acc || it + 1 >= kMaxAttempts) {
             const double v = acc ? draw : __builtin_nan("");

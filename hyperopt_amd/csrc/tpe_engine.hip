@@ -196,7 +196,7 @@ __device__ __forceinline__ void draw_slots(const DLabel& L, const Slots& S, bool
                                            const uint32_t* __restrict__ rounds,
                                            int32_t* __restrict__ err, double (&x)[R],
                                            int64_t (&z)[R], int64_t (&ci)[R], int64_t (&gi)[R],
-                                           bool (&valid)[R]) {
+                                           bool (&valid)[R], const SampLds* sl = nullptr) {
     uint32_t g32[R], rk[R], pend = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -218,11 +218,21 @@ __device__ __forceinline__ void draw_slots(const DLabel& L, const Slots& S, bool
                 if (valid[r]) (void)sample_below<CAT>(L, samp + L.samp_off, seed, rk[r], g32[r], x[r]);
         } else {
             bool ok;
-            if constexpr (MODE == DENSE_ANY)
-                ok = lgmm ? sample_slots<DENSE_LGMM, R>(L, samp + L.samp_off, seed, rk, g32, pend, x)
-                          : sample_slots<DENSE_GMM, R>(L, samp + L.samp_off, seed, rk, g32, pend, x);
-            else
-                ok = sample_slots<MODE, R>(L, samp + L.samp_off, seed, rk, g32, pend, x);
+            if (sl) {
+                const SampShared src{sl};
+                if constexpr (MODE == DENSE_ANY)
+                    ok = lgmm ? sample_slots<DENSE_LGMM, R>(L, src, seed, rk, g32, pend, x)
+                              : sample_slots<DENSE_GMM, R>(L, src, seed, rk, g32, pend, x);
+                else
+                    ok = sample_slots<MODE, R>(L, src, seed, rk, g32, pend, x);
+            } else {
+                const SampGlobal src{samp + L.samp_off, L.ns};
+                if constexpr (MODE == DENSE_ANY)
+                    ok = lgmm ? sample_slots<DENSE_LGMM, R>(L, src, seed, rk, g32, pend, x)
+                              : sample_slots<DENSE_GMM, R>(L, src, seed, rk, g32, pend, x);
+                else
+                    ok = sample_slots<MODE, R>(L, src, seed, rk, g32, pend, x);
+            }
             if (!ok) atomicOr(err, 1);
             if (L.flags & 4) {
 #pragma unroll
@@ -537,18 +547,20 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
     unsigned long long* __restrict__ lbkey, int32_t* __restrict__ cnt, int32_t* __restrict__ idx,
     unsigned long long* __restrict__ terms,
     int32_t* __restrict__ err, Slots S, const double* __restrict__ cand_in,
-    double* __restrict__ s_out, double* __restrict__ e_out) {
+    double* __restrict__ s_out, double* __restrict__ e_out, double2* __restrict__ lohi) {
     const int li = group[blockIdx.y];
     const DLabel L = labels[li];
     const BxLabel B = bx[li];
     __shared__ double exp_tab[kExpTabSize];
+    __shared__ SampLds sl;
     load_exp_table(exp_tab);
+    const bool staged = SAMPLE && stage_samp(L, samp, &sl);
     const bool lgmm = L.mode == DENSE_LGMM;
     double x[R];
     int64_t z[R], ci[R], gi[R];
     bool valid[R];
     draw_slots<DENSE_ANY, SAMPLE, R>(L, S, lgmm, samp, cand_in, n, cand_offset, seed, rounds, err,
-                                     x, z, ci, gi, valid);
+                                     x, z, ci, gi, valid, staged ? &sl : nullptr);
     double y[R], xr[R], acc[R], lb[R], hv[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -613,8 +625,14 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
             e_out[ci[r]] = E;
             continue;
         }
+        const bool cert = E <= 1e30 && s == s;
+        if (lohi) {   // packed map: (lower, upper) per candidate, picked per round
+            lohi[((size_t)blockIdx.y * S.n_rounds + z[r]) * n + ci[r]] =
+                cert ? make_double2(s - E, s + E) : make_double2(-__builtin_inf(), __builtin_inf());
+            continue;
+        }
         double h = __builtin_inf();
-        if (E <= 1e30 && s == s) {
+        if (cert) {
             h = s + E;
             const uint64_t k = order_key(s - E);
             bk = k > bk ? k : bk;
@@ -622,6 +640,13 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
         hv[r] = h;
     }
     if constexpr (!SAMPLE) return;
+    if (lohi) {   // (one atomic per wave)
+        int t = nterms;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+        if ((threadIdx.x & 63) == 0 && terms) atomicAdd(terms, (unsigned long long)t);
+        return;
+    }
     __shared__ uint64_t sh[kBlock / 64];
     bk = block_max_key(bk, sh);
     const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
@@ -1082,18 +1107,20 @@ __global__ __launch_bounds__(kBlock) void k_pick_packed(
 // (round, label) takes the round's largest lower bound and lists, in
 // candidate order, the candidates whose upper bound reaches it -- the same
 // list and per-round ranges k_pick_packed makes.
-__global__ __launch_bounds__(kBlock) void k_pick_win(const float2* __restrict__ lohi, int32_t n_rounds,
+template <typename P2>
+__global__ __launch_bounds__(kBlock) void k_pick_win(const P2* __restrict__ lohi, int32_t n_rounds,
                                                      int32_t C, int32_t* __restrict__ cnt,
                                                      int64_t* __restrict__ list, int64_t cap,
                                                      RoundSel* __restrict__ rsel, int32_t nl) {
+    using V = decltype(lohi->x);
     const int y = blockIdx.y;
     const int64_t z = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const bool valid = z < n_rounds;
-    const float2* row = lohi + ((size_t)y * n_rounds + (valid ? z : 0)) * C;
-    float m = -__builtin_inff();
+    const P2* row = lohi + ((size_t)y * n_rounds + (valid ? z : 0)) * C;
+    V m = -(V)__builtin_inf();
     int k = 0;
     if (valid) {
-        for (int c = 0; c < C; ++c) m = fmaxf(m, row[c].x);
+        for (int c = 0; c < C; ++c) m = row[c].x > m ? row[c].x : m;
         for (int c = 0; c < C; ++c) k += row[c].y >= m;
     }
     __shared__ int sh[kBlock / 64 + 1];
@@ -1442,7 +1469,11 @@ __global__ __launch_bounds__(kBlock) void k_qsample(
         xs[r] = 0.0;
         if (vs[r]) pend |= 1u << r;
     }
-    if (!sample_slots<MODE, R>(L, samp + L.samp_off, seed, rk, g32, pend, xs)) atomicOr(err, 1);
+    __shared__ SampLds sl;
+    bool ok;
+    if (stage_samp(L, samp, &sl)) ok = sample_slots<MODE, R>(L, SampShared{&sl}, seed, rk, g32, pend, xs);
+    else ok = sample_slots<MODE, R>(L, SampGlobal{samp + L.samp_off, L.ns}, seed, rk, g32, pend, xs);
+    if (!ok) atomicOr(err, 1);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int64_t z = zs[r], i = is[r];
@@ -1848,7 +1879,37 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
     HIPCHK(ctx, ctx->scr_cnt.reserve(nl));
     HIPCHK(ctx, hipMemsetAsync(ctx->scr_cnt.p, 0, nl * sizeof(int32_t), ctx->stream));
     RoundSel* rsel = reinterpret_cast<RoundSel*>(ctx->scr_rsel.p);
-    if (ctx->window && cap >= kWinMinN && (int64_t)nl * cap <= ((int64_t)1 << 30)) {
+    bool use_bx = false;
+    if (ctx->expand && cap >= kWinMinN && a.n <= kBxR * kBlock) {
+        int rc = tpe_rt::bx_prepare(ctx);
+        if (rc) return rc;
+        use_bx = ctx->P->bx_ok;
+    }
+    if (use_bx) {
+        // expansion screen: fp64 (lower, upper) bounds per candidate over a
+        // packed slot map of kBxR candidates per thread, then the per-round
+        // selection -- ~1 candidate per (round, label) left to re-score
+        tpe_rt::Posterior& P = *ctx->P;
+        ctx->screen_mode = 3;
+        HIPCHK(ctx, ctx->win_evals.reserve(1));
+        HIPCHK(ctx, hipMemsetAsync(ctx->win_evals.p, 0, sizeof(unsigned long long), ctx->stream));
+        HIPCHK(ctx, ctx->bx_lohi.reserve((size_t)nl * cap));
+        const Slots Sb{(int32_t)a.n, (int32_t)((kBxR * kBlock) / a.n), a.n_rounds};
+        const uint32_t gxb = (uint32_t)((a.n_rounds + Sb.rpb - 1) / Sb.rpb);
+        if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
+        hipLaunchKernelGGL((k_screen_bx<kBxR, true>), dim3(gxb, nl, 1), dim3(kBlock), 0, ctx->stream,
+                           P.labels.p, grp, P.comps64.p, P.samp.p, P.bx.p, P.bx_tab.p, P.bx_loff.p,
+                           P.bx_list.p, a.n, a.cand_offset, a.seed, ctx->rounds.p, nl, nullptr, nullptr,
+                           nullptr, nullptr, ctx->win_evals.p, ctx->errflag.p, Sb, nullptr, nullptr, nullptr,
+                           ctx->bx_lohi.p);
+        if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
+        hipLaunchKernelGGL(k_pick_win<double2>, dim3((unsigned)((a.n_rounds + kBlock - 1) / kBlock), nl),
+                           dim3(kBlock), 0, ctx->stream, ctx->bx_lohi.p, a.n_rounds, (int32_t)a.n,
+                           ctx->scr_cnt.p, ctx->scr_list.p, cap, rsel, nl);
+        HIPCHK(ctx, hipMemcpyAsync(&ctx->screen_exec_h, ctx->win_evals.p, sizeof(unsigned long long),
+                                   hipMemcpyDeviceToHost, ctx->stream));
+        ctx->screen_exec_pending = true;
+    } else if (ctx->window && cap >= kWinMinN && (int64_t)nl * cap <= ((int64_t)1 << 30)) {
         // windowed: every round's candidates of a label sorted together into
         // tiles of neighbours (tpe_window.hip), bounds per candidate, then
         // the per-round selection
@@ -1861,7 +1922,7 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
         tpe_rt::WinScreenArgs wa{grp, nl, a.n, a.cand_offset, a.seed, 0, a.n_rounds, nullptr,
                                  nullptr, nullptr, nullptr, nullptr, (int32_t)a.n, ctx->win_lohi.p};
         if ((rc = tpe_rt::win_screen(ctx, wa, &sorted))) return rc;
-        hipLaunchKernelGGL(k_pick_win, dim3((unsigned)((a.n_rounds + kBlock - 1) / kBlock), nl),
+        hipLaunchKernelGGL(k_pick_win<float2>, dim3((unsigned)((a.n_rounds + kBlock - 1) / kBlock), nl),
                            dim3(kBlock), 0, ctx->stream, ctx->win_lohi.p, a.n_rounds, (int32_t)a.n,
                            ctx->scr_cnt.p, ctx->scr_list.p, cap, rsel, nl);
         HIPCHK(ctx, hipMemcpyAsync(&ctx->screen_exec_h, ctx->win_evals.p, sizeof(unsigned long long),
@@ -1960,7 +2021,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                                P.labels.p, grp, P.comps64.p, P.samp.p, P.bx.p, P.bx_tab.p, P.bx_loff.p,
                                P.bx_list.p, a.n, a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->scr_hid.p,
                                ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p, ctx->win_evals.p, ctx->errflag.p,
-                               a.S, nullptr, nullptr, nullptr);
+                               a.S, nullptr, nullptr, nullptr, nullptr);
             if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
             hipLaunchKernelGGL(k_select_list, dim3((unsigned)cells), dim3(kBlock), 0, ctx->stream, ctx->scr_hid.p,
                                a.n, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p);
@@ -2875,7 +2936,7 @@ int tpe_screen_probe(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n,
                            P.labels.p, ctx->one_group.p, P.comps64.p, P.samp.p, P.bx.p, P.bx_tab.p,
                            P.bx_loff.p, P.bx_list.p, n, 0, 0, ctx->rounds.p, 1, nullptr, nullptr, nullptr,
                            nullptr, nullptr, ctx->errflag.p, Slots{0, 0, 1}, ctx->cand.p, ctx->out_lb.p,
-                           ctx->out_la.p);
+                           ctx->out_la.p, nullptr);
     } else if (ctx->window && n >= 2048) {   // the windowed screen's tiles of sorted neighbours
         int rc = tpe_rt::win_prepare(ctx);
         if (rc) return rc;

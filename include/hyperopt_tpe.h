@@ -317,7 +317,8 @@ int tpe_last_rescore_terms(const tpe_ctx *ctx, int64_t *terms);
 /* Which screen the last round's dense tile-map labels went through: 0 none
  * (unscreened fp64, fp32 precision, or no dense tile round), 1 the plain
  * fp32 screen, 2 the windowed fp32 screen, 3 the expansion screen
- * (TPE_OPT_EXPAND); packed-map rounds report 0 here. */
+ * (TPE_OPT_EXPAND); packed-map rounds report 3 when the expansion screen
+ * ran, else 0. */
 int32_t tpe_last_screen_mode(const tpe_ctx *ctx);
 
 /* Diagnostic of the screen (tests): for caller-supplied candidates of one

@@ -53,6 +53,15 @@ __global__ __launch_bounds__(256) void k_bench(const DLabel* __restrict__ Lp, co
         } else if constexpr (V == 7) {   // fast log only
             const U4 r = philox4x32_10(U4{(uint32_t)g, 0u, 3u, 7u}, k0, k1);
             acc += flog(u01_open0(r.y, r.z)) + (double)(r.x ^ r.w);
+        } else if constexpr (V == 9 || V == 10) {   // 4 slots through sample_slots (10: unbounded)
+            if ((g & 3) == 0) {
+                uint32_t rk[4] = {7u, 7u, 7u, 7u}, gg[4] = {(uint32_t)g, (uint32_t)g + 1, (uint32_t)g + 2, (uint32_t)g + 3};
+                double o[4] = {0, 0, 0, 0};
+                DLabel L2 = L;
+                if (V == 10) L2.flags = 0;
+                sample_slots<DENSE_GMM, 4>(L2, s, 1234u, rk, gg, 15u, o);
+                acc += o[0] + o[1] + o[2] + o[3];
+            }
         } else if constexpr (V == 8) {   // Philox with 64-bit products
             U4 c{(uint32_t)g, 0u, 3u, 7u};
             uint32_t a0 = k0, a1 = k1;
@@ -99,8 +108,21 @@ int main() {
     }
     const int K = 26;
     std::vector<SampRec> hs(K);
-    for (int k = 0; k < K; ++k) hs[k] = SampRec{(k + 1.0) / K, -5.0 + 10.0 * k / K, 0.4, 0.0};
-    hs[K - 1].cdf = 1.0;
+    // 25 observations (sigma 0.4, linear-forgetting-like weights) and the
+    // prior (mu 0, sigma 10) at weight 1/26, in mu order
+    {
+        double w[K], tot = 0.0;
+        for (int k = 0; k < K; ++k) {
+            w[k] = (k == 12) ? 1.0 : 0.5 + 0.5 * k / K;
+            tot += w[k];
+        }
+        double c = 0.0;
+        for (int k = 0; k < K; ++k) {
+            c += w[k] / tot;
+            hs[k] = SampRec{c, k == 12 ? 0.0 : -4.8 + 9.6 * k / K, k == 12 ? 10.0 : 0.4, 0.0};
+        }
+        hs[K - 1].cdf = 1.0;
+    }
     DLabel hl{};
     hl.mode = DENSE_GMM;
     hl.flags = 3;
@@ -121,8 +143,9 @@ int main() {
     CHK(hipEventCreate(&a));
     CHK(hipEventCreate(&b));
     const char* names[] = {"philox", "+cdf_search", "+box-muller", "sample_raw bounded", "philox+box-muller",
-                           "philox+log", "philox+cospi", "philox+flog", "philox 64-bit mul"};
-    for (int v = 0; v < 9; ++v) {
+                           "philox+log", "philox+cospi", "philox+flog", "philox 64-bit mul",
+                           "sample_slots x4 bnd", "sample_slots x4 unb"};
+    for (int v = 0; v < 11; ++v) {
         for (int rep = 0; rep < 2; ++rep) {
             CHK(hipEventRecord(a));
             switch (v) {
@@ -135,6 +158,8 @@ int main() {
                 case 6: hipLaunchKernelGGL(k_bench<6>, dim3(grid), dim3(256), 0, 0, dl, ds, n, dout); break;
                 case 7: hipLaunchKernelGGL(k_bench<7>, dim3(grid), dim3(256), 0, 0, dl, ds, n, dout); break;
                 case 8: hipLaunchKernelGGL(k_bench<8>, dim3(grid), dim3(256), 0, 0, dl, ds, n, dout); break;
+                case 9: hipLaunchKernelGGL(k_bench<9>, dim3(grid), dim3(256), 0, 0, dl, ds, n * 4, dout); break;
+                case 10: hipLaunchKernelGGL(k_bench<10>, dim3(grid), dim3(256), 0, 0, dl, ds, n * 4, dout); break;
             }
             CHK(hipEventRecord(b));
             CHK(hipEventSynchronize(b));
