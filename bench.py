@@ -48,9 +48,9 @@ FLOPS_PER_EVAL = {'f64': 6.0, 'f32': 6.0}
 #   k_screen: the same with 8 candidates per thread (v_mov_b64 per 8 evals) =
 #         3.5625 slots
 VALU_SLOTS_PER_EVAL = {'f64': 12.25, 'f32': 3.625, 'screen': 3.5625}
-# expansion screen (k_screen_bx): per candidate a 13-coefficient Horner
-# polynomial (13 FMA) and the degree-5 exp(-kappa delta^2) factor (5 FMA)
-BX_FLOPS_PER_CAND = 2 * 13 + 2 * 5
+# expansion screen (k_screen_bx): per candidate a 15-coefficient Horner
+# polynomial (15 FMA) and the degree-5 exp(-kappa delta^2) factor (5 FMA)
+BX_FLOPS_PER_CAND = 2 * 15 + 2 * 5
 PEAK_FP64_VECTOR_TFLOPS = 78.6        # MI355X spec (MI355X_MICROARCH.md)
 PEAK_FP32_VECTOR_TFLOPS = 157.3
 # 4-cycle wave64 VALU issue slots per second at 2.4 GHz, in lanes: 256 CU x
@@ -403,7 +403,7 @@ def main():
         roof['flops_per_candidate_poly'] = BX_FLOPS_PER_CAND
         roof['note'] = ('VALU-issue bound: per candidate the Philox + Box-Muller draw, the fp64 '
                         'exp / log sequences and the bound take most of the instruction stream; '
-                        'achieved counts only the lpdf arithmetic (6 FLOP per direct term, 36 per '
+                        'achieved counts only the lpdf arithmetic (6 FLOP per direct term, 40 per '
                         'polynomial); valu_busy_measured is the PMC utilisation of the same kernel')
     line = {
         'metric': 'TPE candidate x component lpdf evals/sec (10k-trial history)',

@@ -741,8 +741,8 @@ __device__ __host__ __forceinline__ int win_bin(const WinLabel& W, double x) {
 // so lpdf_below is bit-identical), the above mixture as the bin's
 // polynomial plus its list, and a bound ~1e-12 wide: only near-ties of the
 // best score are re-scored.
-constexpr int kBxP = 13;          // Taylor coefficients per bin
-constexpr int kBxRow = 16;        // doubles per bin row: A_0..A_12, Eabs, G, W
+constexpr int kBxP = 15;          // Taylor coefficients per bin
+constexpr int kBxRow = 16;        // doubles per bin row (one 128-B line): A_0..A_14, Eabs
 constexpr double kBxT = 96.0;     // components left out stay below 2^-kBxT
 
 struct BxLabel {

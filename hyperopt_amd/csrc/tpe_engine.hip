@@ -561,7 +561,7 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
     bool valid[R];
     draw_slots<DENSE_ANY, SAMPLE, R>(L, S, lgmm, samp, cand_in, n, cand_offset, seed, rounds, err,
                                      x, z, ci, gi, valid, staged ? &sl : nullptr);
-    double y[R], xr[R], acc[R], lb[R], hv[R];
+    double y[R], xr[R], acc[R], hv[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         hv[r] = __builtin_inf();
@@ -571,8 +571,9 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
     }
     // below: the fp64 round's lse_dense, term for term
     lse_acc<R>(comps64 + L.comp_b, L.nb, xr, acc, exp_tab);
-#pragma unroll
-    for (int r = 0; r < R; ++r) lb[r] = lse_finish(comps64 + L.comp_b, L.nb, acc[r], xr[r], L.shift_b);
+    // (lb itself is not needed: s = log(acc_b / S) + shift_b - shift_a, one
+    // log instead of two; candidates whose below sum underflows -- the fp64
+    // round's two-pass fallback -- are uncertified)
     const Comp<double>* ca = comps64 + L.comp_a;
     const double skip_abs = (double)L.na * exp2(-kBxT);
     uint64_t bk = 0;
@@ -589,8 +590,8 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
 #pragma unroll
             for (int k = kBxP - 2; k >= 0; --k) poly = fma(poly, delta, rw[k]);
             const double eabs = rw[kBxP];
-            // exp(-t), t = kappa delta^2 <= kappa rmax^2 <= 0.0225 / (T ln 2) < 4e-4:
-            // degree 5 leaves t^6 / 720 < 1e-23 (inside the 8 u S_clip term)
+            // exp(-t), t = kappa delta^2 <= kappa rmax^2 <= 0.0625 / (T ln 2) < 1e-3:
+            // degree 5 leaves t^6 / 720 < 2e-21 (inside the 8 u S_clip term)
             const double t = B.kappa * delta * delta;
             const double et = fma(fma(fma(fma(fma(-1.0 / 120.0, t, 1.0 / 24.0), t, -1.0 / 6.0), t, 0.5), t,
                                       -1.0), t, 1.0);
@@ -607,17 +608,21 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
             const double sum = sclip + snc;
             const double ea = eabs + 8.0 * 0x1.0p-53 * fabs(sclip) + skip_abs +
                               (3e-14 + (double)(j1 - j0 + 4) * 0x1.0p-53) * snc + 0x1.0p-52 * sum;
-            const double eps = ea / sum;
-            if (fabs(delta) <= B.rmax && t <= 1e-3 && sum >= 1e-280 && eps <= 1e-6 && lb[r] == lb[r]) {
-                const double ls = flog(sum);
-                double la = ls + L.shift_a, lbr = lb[r];
-                if (lgmm) {
-                    lbr -= y[r];
-                    la -= y[r];
-                }
-                s = lbr - la;
-                E = 1.25 * (1.001 * eps + 0x1.0p-52 * (fabs(ls) + 1.0) +
-                            fp64_err(L.nb + L.na, fabs(lbr) + fabs(la) + fabs(y[r]) + fabs(L.centre)));
+            // 1 / sum: hardware reciprocal + one Newton step (relative error
+            // ~2^-50), and 1.0001 on top: eps only bounds
+            const double r0 = __builtin_amdgcn_rcp(sum);
+            const double rs = fma(fma(-sum, r0, 1.0), r0, r0);
+            const double eps = ea * rs * 1.0001;
+            const double ab = acc[r];
+            if (fabs(delta) <= B.rmax && t <= 2e-3 && sum >= 1e-280 && ab >= 1e-290 && eps <= 1e-6) {
+                // s = (log acc_b + shift_b) - (log S + shift_a): one log of the
+                // ratio; the fp64 round's own logs, shifts and (LGMM) - y terms
+                // add at most mag 2^-50 (fp64_err), mag from the exponents
+                const double lq = flog(ab / sum);
+                s = lq + (L.shift_b - L.shift_a);
+                const double mag = (double)(abs(ilogb(ab)) + abs(ilogb(sum)) + 2) * 0.6931471805599453 +
+                                   fabs(L.shift_b) + fabs(L.shift_a) + 2.0 * fabs(y[r]) + fabs(L.centre);
+                E = 1.25 * (1.001 * eps + 0x1.0p-52 * (fabs(lq) + 1.0) + fp64_err(L.nb + L.na, mag));
             }
         }
         if constexpr (!SAMPLE) {
@@ -1588,6 +1593,66 @@ __global__ __launch_bounds__(kBlock) void k_qscan(
     finish_slots<R>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials, scratch, sh);
 }
 
+// Bounded quantized labels whose grid window is known before sampling
+// (launch_quantized: [low, high] / q): the tables are built first and one
+// kernel draws, maps to the grid (k_qsample's arithmetic), looks up and
+// reduces -- no index array, no window round trip.  Same values as
+// k_qsample + k_qscan.
+template <int MODE, int R>
+__global__ __launch_bounds__(kBlock) void k_qfused(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<double>* __restrict__ comps64, const SampRec* __restrict__ samp,
+    const QInfo* __restrict__ qinfo, const double2* __restrict__ tab, int64_t n, int64_t cand_offset,
+    uint64_t seed, const uint32_t* __restrict__ rounds, int32_t qbase, int32_t n_labels, int32_t tiles,
+    Partial* __restrict__ partials, int32_t* __restrict__ err, Slots S) {
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    __shared__ SampLds sl;
+    const bool staged = stage_samp(L, samp, &sl);
+    const QInfo Q = qinfo[qbase + blockIdx.y];
+    double x[R], lb[R], la[R], v[R];
+    int64_t z[R], ci[R], gi[R];
+    bool valid[R];
+    uint32_t g32[R], rk[R], pend = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        S.template at<R>(r, n, z[r], ci[r], valid[r]);
+        gi[r] = cand_offset + ci[r];
+        g32[r] = (uint32_t)gi[r];
+        rk[r] = valid[r] ? rounds[z[r]] : 0u;
+        v[r] = 0.0;
+        if (valid[r]) pend |= 1u << r;
+    }
+    const bool ok = staged ? sample_slots<MODE, R>(L, SampShared{&sl}, seed, rk, g32, pend, v)
+                           : sample_slots<MODE, R>(L, SampGlobal{samp + L.samp_off, L.ns}, seed, rk, g32, pend, v);
+    if (!ok) atomicOr(err, 1);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const double jd = rint(v[r] / L.q);
+        int64_t j = Q.jmin;
+        if (valid[r]) {
+            if (jd >= -0x1.0p52 && jd <= 0x1.0p52) j = (int64_t)jd;
+            else atomicOr(err, 8);
+        }
+        x[r] = (double)j * L.q;
+        const int64_t s = j - Q.jmin;
+        if (s >= 0 && s < Q.G) {
+            const double2 t = tab[Q.tab_off + s];
+            lb[r] = t.x;
+            la[r] = t.y;
+        } else {
+            double ub, lo;
+            bool neg;
+            quant_bounds<MODE>(L, x[r], ub, lo, neg);
+            lb[r] = quant_lpdf<MODE == QUANT_LGMM>(comps64 + L.comp_b, L.nb, ub, lo, L.logpacc_b);
+            la[r] = quant_lpdf<MODE == QUANT_LGMM>(comps64 + L.comp_a, L.na, ub, lo, L.logpacc_a);
+        }
+    }
+    __shared__ double scratch[R * kBlock * 3 / 2];
+    __shared__ Partial sh[kBlock / 64];
+    finish_slots<R>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials, scratch, sh);
+}
+
 __device__ __forceinline__ tpe_label_result to_result(const Partial& p, int li) {
     tpe_label_result r;
     r.value = p.value;
@@ -2232,6 +2297,72 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
     const int nq = nqg + nql;
     evals_q[0] = evals_q[1] = 0;
     if (nq == 0 || a.tiles == 0) return TPE_OK;
+    // bounded labels: the grid window from [low, high] / q before sampling
+    // (a margin of one step each side); fused when every label has one
+    {
+        std::vector<QInfo> qi(nq);
+        int64_t tab = 0, maxG = 0;
+        bool fused = ctx->dedup;
+        const int64_t total = a.total_slots;
+        for (int qpos = 0; qpos < nq && fused; ++qpos) {
+            const int li = qpos < nqg ? ctx->P->h_group[QUANT_GMM][qpos] : ctx->P->h_group[QUANT_LGMM][qpos - nqg];
+            const DLabel& d = ctx->P->h_labels[li];
+            const bool lg = qpos >= nqg;
+            const double lo = lg ? d.exp_low : d.low, hi = lg ? d.exp_high : d.high;
+            if ((d.flags & 3) != 3 || !(d.q > 0.0) || !std::isfinite(lo / d.q) || !std::isfinite(hi / d.q) ||
+                std::fabs(lo / d.q) > 0x1.0p50 || std::fabs(hi / d.q) > 0x1.0p50) {
+                fused = false;
+                break;
+            }
+            const int64_t jmin = (int64_t)std::floor(lo / d.q) - 1, jmax = (int64_t)std::ceil(hi / d.q) + 1;
+            const int64_t G = jmax - jmin + 1;
+            if (G < 1 || 2 * G > total) {
+                fused = false;
+                break;
+            }
+            qi[qpos] = QInfo{jmin, G, tab, 0};
+            tab += G;
+            maxG = std::max(maxG, G);
+            evals_q[lg ? 1 : 0] += G * (int64_t)(d.nb + d.na);
+        }
+        if (fused) {
+            HIPCHK(ctx, ctx->qinfo.reserve(nq));
+            HIPCHK(ctx, ctx->qtab.reserve(std::max<int64_t>(tab, 1)));
+            HIPCHK(ctx, hipMemcpyAsync(ctx->qinfo.p, qi.data(), nq * sizeof(QInfo), hipMemcpyHostToDevice,
+                                       ctx->stream));
+            for (int fam = 0; fam < 2; ++fam) {
+                const int mode = fam ? QUANT_LGMM : QUANT_GMM;
+                const int cnt = fam ? nql : nqg;
+                const int qbase = fam ? nqg : 0;
+                if (!cnt) continue;
+                bracket(ctx, mode, 0);
+                dim3 tg((unsigned)maxG, cnt, 1);
+                if (fam)
+                    hipLaunchKernelGGL(k_qtable<QUANT_LGMM>, tg, dim3(kBlock), 0, ctx->stream, ctx->P->labels.p,
+                                       g.dev[mode], ctx->P->comps64.p, ctx->qinfo.p, nq, qbase, ctx->qtab.p);
+                else
+                    hipLaunchKernelGGL(k_qtable<QUANT_GMM>, tg, dim3(kBlock), 0, ctx->stream, ctx->P->labels.p,
+                                       g.dev[mode], ctx->P->comps64.p, ctx->qinfo.p, nq, qbase, ctx->qtab.p);
+                dim3 sg(a.gx, cnt, a.gz);
+#define TPE_QFUSED(M, RR)                                                                          \
+    hipLaunchKernelGGL((k_qfused<M, RR>), sg, dim3(kBlock), 0, ctx->stream, ctx->P->labels.p,         \
+                       g.dev[mode], ctx->P->comps64.p, ctx->P->samp.p, ctx->qinfo.p, ctx->qtab.p, a.n,  \
+                       a.cand_offset, a.seed, ctx->rounds.p, qbase, ctx->P->n_labels, a.tiles,          \
+                       ctx->partials.p, ctx->errflag.p, a.S)
+                if (fam) {
+                    if (narrow(a.S)) TPE_QFUSED(QUANT_LGMM, kRGroup);
+                    else TPE_QFUSED(QUANT_LGMM, kR);
+                } else {
+                    if (narrow(a.S)) TPE_QFUSED(QUANT_GMM, kRGroup);
+                    else TPE_QFUSED(QUANT_GMM, kR);
+                }
+#undef TPE_QFUSED
+                bracket(ctx, mode, 1);
+            }
+            return ctx->hip(hipGetLastError(), "fused quantized launch");
+        }
+        evals_q[0] = evals_q[1] = 0;
+    }
     const size_t slots = (size_t)a.n_rounds * nq;   // candidate rows
     HIPCHK(ctx, ctx->qj.reserve(slots * (size_t)a.n));
     HIPCHK(ctx, ctx->qmm.reserve(2 * (size_t)nq));

@@ -8,13 +8,13 @@
 //   k_bx_scan     per label: candidate range, a* (the largest above record
 //                 scale = the clipped sigma's), unclipped count
 //   (host)        bins per label from kappa and the cut T: the Taylor argument
-//                 2 kappa |d| |delta| stays <= ~0.3, so 13 terms leave a
-//                 truncation ~1e-17 of the bin's mass
+//                 2 kappa |d| |delta| stays <= ~0.5, so 15 terms leave a
+//                 truncation ~4e-17 of the bin's mass
 //   k_bx_compact  per label: the unclipped components in record order
 //   k_bx_count    per bin: unclipped components whose term can reach 2^-T in it
 //   k_bx_offsets  per label: their exclusive scan (list offsets), the total
 //   k_bx_fill     per bin: the list
-//   k_bx_table    per bin: A_0..A_12 over the clipped components within the
+//   k_bx_table    per bin: A_0..A_14 over the clipped components within the
 //                 window, and the absolute bound Eabs of truncation + rounding
 //
 // Bounds (natural-log units, records as tpe_device.h Comp: c'/K = log coef -
@@ -231,9 +231,9 @@ __global__ __launch_bounds__(kBlock) void k_bx_offsets(const int32_t* __restrict
     }
 }
 
-__constant__ double kInvN[kBxP + 1] = {1.0,       1.0,        1.0 / 2,  1.0 / 3,  1.0 / 4,
-                                       1.0 / 5,   1.0 / 6,    1.0 / 7,  1.0 / 8,  1.0 / 9,
-                                       1.0 / 10,  1.0 / 11,   1.0 / 12, 1.0 / 13};
+__constant__ double kInvN[kBxP + 1] = {1.0,      1.0,      1.0 / 2,  1.0 / 3,  1.0 / 4,  1.0 / 5,
+                                       1.0 / 6,  1.0 / 7,  1.0 / 8,  1.0 / 9,  1.0 / 10, 1.0 / 11,
+                                       1.0 / 12, 1.0 / 13, 1.0 / 14, 1.0 / 15};
 
 // first record index k in [0, n) with mu'_k >= v (mu' = m'/a', sorted by mu)
 __device__ __forceinline__ int lower_mu(const Comp<double>* __restrict__ c, int n, double v) {
@@ -277,7 +277,8 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
         const double arg = rec.c * kExpScaleInv - kap * d * d;
         if (!(arg > -740.0)) continue;   // below 2^-1067 in the whole bin: in the skip term
         const double g = exp(arg), two = 2.0 * kap * d;
-        const double yv = fabs(two) * r, ey = exp(yv);
+        // e^y only enters the bounds: 1 + y + y^2 >= e^y for 0 <= y <= 1.79
+        const double yv = fabs(two) * r, ey = yv <= 1.5 ? fma(yv, yv, 1.0 + yv) : exp(yv) * 1.000001;
         double t = g;
         A[0] += t;
 #pragma unroll
@@ -297,8 +298,6 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
 #pragma unroll
     for (int n = 0; n < kBxP; ++n) row[n] = A[n];
     row[kBxP] = 1.02 * (Rb + ERR + ((double)W + 2.0 * kBxP + 8.0) * kU * G) + 1e-300;
-    row[kBxP + 1] = G;
-    row[kBxP + 2] = (double)W;
 }
 
 }  // namespace
@@ -341,7 +340,7 @@ int tpe_rt::bx_prepare(tpe_ctx* ctx) {
             break;
         }
         const double d0 = std::sqrt(kBxT * kLn2 / kap);
-        const double r_target = 0.15 / (kap * d0);
+        const double r_target = 0.25 / (kap * d0);   // Taylor argument 2 kappa |d| r <= ~0.5
         const double want = (xhi - xlo) / (2.0 * r_target);
         if (!(want <= (double)kMaxBins)) {
             ok = false;
