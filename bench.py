@@ -289,7 +289,7 @@ def main():
     def timed(n_steps, first):
         """Run n_steps steps (barrier + sync on both sides); returns wall
         seconds (max over ranks) and the summed per-family / screen stats."""
-        mode_ms, mode_ev, scr = {}, {}, [0, 0, 0.0, 0, 0]
+        mode_ms, mode_ev, scr = {}, {}, [0, 0, 0.0, 0, 0, 0, 0]
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
@@ -305,6 +305,9 @@ def main():
             scr[2] += ms
             scr[3] += eng.last_screen_terms()
             scr[4] += eng.last_rescore_terms()
+            hl, hf = eng.last_hot()
+            scr[5] += max(hl, 0)
+            scr[6] += hf
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
@@ -444,6 +447,9 @@ def main():
             'windowed': windowed,
             'mode': {0: 'none', 1: 'plain fp32', 2: 'windowed fp32', 3: 'expansion (fp64)'}[smode],
             'screen_terms_per_step': scr[3] // args.steps,
+            'hot_listed_per_step': scr[5] // args.steps,
+            'hot_listed_fraction': scr[5] / max(scr[0], 1),
+            'hot_fallbacks': scr[6],
             'screen_terms_fraction': scr[3] / max(mode_ev[dom], 1),
             'note': 'dense labels: every (candidate, component) pair is either evaluated in '
                     'packed fp32 with a rigorous error bound, or (windowed screen: candidates '

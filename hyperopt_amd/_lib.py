@@ -46,6 +46,7 @@ TPE_OPT_WINDOW = 8
 TPE_OPT_WIN_T = 9
 TPE_OPT_WIN_GROUPS = 10
 TPE_OPT_EXPAND = 11
+TPE_OPT_HOT = 12
 
 TPE_OBS_IDENTITY = 0
 TPE_OBS_LOG = 1
@@ -121,6 +122,8 @@ SIGNATURES = {
     'tpe_last_screen_terms': (ctypes.c_int, [_P, _P]),
     'tpe_last_rescore_terms': (ctypes.c_int, [_P, _P]),
     'tpe_last_screen_mode': (ctypes.c_int32, [_P]),
+    'tpe_last_hot': (ctypes.c_int, [_P, _P, _P]),
+    'tpe_hot_probe': (ctypes.c_int, [_P, ctypes.c_int32, _P, ctypes.c_int64, _P, _P, _P]),
     'tpe_screen_probe': (ctypes.c_int, [_P, _I32, _P, _I64, _P, _P]),
 }
 

@@ -92,6 +92,9 @@ struct Posterior {
     DevBuf<int32_t> bx_loff;             // per label: nbins + 1 offsets into its list
     DevBuf<int32_t> bx_list;             // per bin: the unclipped components reaching it
     DevBuf<double> bx_scan;              // per dense label position: range, a*, counts
+    DevBuf<float2> bx_sb;                // hot-bin prefilter: per sub-bin (U, L) of the score
+    DevBuf<float> bx_sbp;                //   and the below mixture's sampling mass of it
+    int64_t bx_sb_max = 0;               //   the most sub-bins of one label
     void release() {
         labels.release();
         comps64.release();
@@ -117,6 +120,8 @@ struct Posterior {
         bx_loff.release();
         bx_list.release();
         bx_scan.release();
+        bx_sb.release();
+        bx_sbp.release();
         bx_ready = bx_ok = false;
         n_labels = 0;
     }
@@ -241,6 +246,17 @@ struct tpe_ctx {
     DevBuf<double> scr_hid;              // expansion screen: fp64 upper bounds
     DevBuf<double2> bx_lohi;             //   packed map: fp64 (lower, upper) per candidate
     bool expand = true;                  // TPE_OPT_EXPAND: expansion screen when eligible
+    // hot-bin prefilter of the expansion screen (TPE_OPT_HOT, tpe_device.h)
+    int32_t hot = 1;                     // 0 off, 1 on, 2 test: force the fallback
+    DevBuf<double> hot_x;                // per cell: listed candidates' x
+    DevBuf<int32_t> hot_i, hot_cnt;      //   their indices; per cell the count
+    DevBuf<unsigned long long> hot_t, hot_tau0;   // per cell largest L; per label tau0
+    DevBuf<int32_t> hot_flag;            // fallback flag
+    std::vector<int32_t> hot_cnt_h;
+    int32_t hot_flag_h = 0;
+    int64_t hot_listed = 0;              // last round: candidates the prefilter listed
+    int32_t hot_fallback = 0;            // last round: 1 if it re-ran the plain screen
+    bool hot_ran = false;
     DevBuf<int32_t> scr_idx;
     DevBuf<unsigned long long> scr_lb;
     DevBuf<int32_t> scr_cnt;

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "tpe_cos_table.h"
 #include "tpe_exp_table.h"
 
 namespace tpe {
@@ -181,6 +182,20 @@ __device__ __forceinline__ bool stage_samp(const DLabel& L, const SampRec* __res
     return true;
 }
 
+// cos(2 pi w / 2^32): (cos, sin) of the top 8 bits' angle from a 256-entry
+// table (tpe_cos_table.h), the residual t = 2 pi (w mod 2^24) / 2^32 <
+// 2 pi / 256 by its Taylor polynomials (t^10 / 10! < 1e-22), then
+// cos(a + t) = cos a cos t - sin a sin t -- ~15 VALU operations and one
+// 16-byte load instead of the library cospi's ~70 operations.
+__device__ __forceinline__ double cos_turn32(uint32_t w) {
+    const int k = (int)(w >> 24);
+    const double t = (double)(w & 0xFFFFFFu) * (6.283185307179586 * 0x1.0p-32);
+    const double t2 = t * t;
+    const double ct = fma(fma(fma(fma(1.0 / 40320.0, t2, -1.0 / 720.0), t2, 1.0 / 24.0), t2, -0.5), t2, 1.0);
+    const double st = t * fma(fma(fma(-1.0 / 5040.0, t2, 1.0 / 120.0), t2, -1.0 / 6.0), t2, 1.0);
+    return fma(kCosSinTab[2 * k], ct, -kCosSinTab[2 * k + 1] * st);
+}
+
 template <typename Src>
 __device__ __forceinline__ double draw_attempt(const DLabel& L, const Src& src, uint32_t k0, uint32_t k1,
                                                uint32_t g, uint32_t it, uint32_t round) {
@@ -188,10 +203,14 @@ __device__ __forceinline__ double draw_attempt(const DLabel& L, const Src& src, 
     double mu, sg;
     src.pick((double)r.x * 0x1.0p-32, mu, sg);
     const double u1 = u01_open0(r.y, r.z);
-    const double rad = sqrt(-2.0 * flog(u1));
-    const double nrm = rad * cospi(2.0 * ((double)r.w * 0x1.0p-32));
+    const double rad = __builtin_amdgcn_sqrt(-2.0 * flog(u1));
+    const double nrm = rad * cos_turn32(r.w);
     return fma(sg, nrm, mu);
 }
+
+// LGMM1 sample value of an accepted log-space draw (tpe.py:255: np.exp);
+// RAW sample_slots leave this step to the caller
+__device__ __forceinline__ double lgmm_value(double draw) { return exp(draw); }
 
 // Draw one sample of the below posterior for global candidate g, BEFORE
 // quantization (LGMM1: after the exp).
@@ -214,7 +233,7 @@ __device__ __forceinline__ bool sample_raw(const DLabel& L, const SampRec* __res
         for (uint32_t it = 0; it < kMaxAttempts; ++it) {
             const double draw = draw_attempt(L, SampGlobal{s, L.ns}, k0, k1, g, it, round);
             if (!bounded || (L.low <= draw && draw < L.high)) {
-                out = (MODE == DENSE_LGMM || MODE == QUANT_LGMM) ? exp(draw) : draw;
+                out = (MODE == DENSE_LGMM || MODE == QUANT_LGMM) ? lgmm_value(draw) : draw;
                 return true;
             }
         }
@@ -231,7 +250,7 @@ __device__ __forceinline__ bool sample_raw(const DLabel& L, const SampRec* __res
 // [low, high), nearly every wave has a lane that retries.  Slots outside
 // `pend` keep their value.  Returns false if a slot hit the attempt cap
 // (its value is NaN).
-template <int MODE, int R, typename Src>
+template <int MODE, int R, typename Src, bool RAW = false>
 __device__ __forceinline__ bool sample_slots(const DLabel& L, const Src& src, uint64_t seed,
                                              const uint32_t (&rk)[R], const uint32_t (&g)[R], uint32_t pend,
                                              double (&out)[R]) {
@@ -264,10 +283,10 @@ __device__ __forceinline__ bool sample_slots(const DLabel& L, const Src& src, ui
             ++it;
         }
     }
-    if constexpr (MODE == DENSE_LGMM || MODE == QUANT_LGMM) {
+    if constexpr ((MODE == DENSE_LGMM || MODE == QUANT_LGMM) && !RAW) {
 #pragma unroll
         for (int r = 0; r < R; ++r)
-            if ((mask0 >> r) & 1u) out[r] = exp(out[r]);
+            if ((mask0 >> r) & 1u) out[r] = lgmm_value(out[r]);
     }
     return ok;
 }
@@ -755,7 +774,30 @@ struct BxLabel {
     int64_t cnt_off;          // first of its nbins + 1 list offsets in bx_loff
     int64_t list_off;         // first of its entries in bx_list
     int32_t nbins, n_nc;      // bins; unclipped components (listed at comp_a in bx_nc)
+    double inv_sbw;           // kBxSub / bw: sub-bin of x' = floor((x' - xlo) inv_sbw)
+    int64_t sb_off;           // first of its nbins kBxSub sub-bins in bx_sb / bx_sbp
 };
+
+// Hot-bin prefilter of the expansion screen.  Each bin is cut into kBxSub
+// sub-bins, and tpe_expand.hip (k_bx_bounds) stores for each a rigorous
+// interval [L, U] of the fp64 round's score over every x' in it (both
+// mixtures bounded term by term / through the bin's polynomial, fp64 rounding
+// and the fp64 round's own error inside a generous margin), plus the below
+// mixture's sampling mass p of the sub-bin.  A round first draws every
+// candidate and reads only its sub-bin's (U, L) (k_hot_bx): tau = the largest
+// L over the candidates is a lower bound of the best fp64 score, so a
+// candidate with U < tau can never win (its score is strictly below the
+// candidate that attains tau).  tau is not known while drawing, so the
+// candidates are listed against tau0 = max L over the sub-bins (or short
+// runs of them) a round of n candidates fills with near certainty (mass p >=
+// kHotFill / n; the run's smallest L); the round checks
+// tau >= tau0 afterwards (then every candidate with U >= tau was listed) and
+// otherwise re-runs the plain expansion screen -- the filter never changes a
+// winner, tau0 only decides how often that fallback runs.  Only the listed
+// candidates go through the expansion screen (k_screen_hot).
+constexpr int kBxSubBits = 4;
+constexpr int kBxSub = 1 << kBxSubBits;
+constexpr double kHotFill = 16.0;   // P(a run of that mass stays empty) <= e^-16
 
 __device__ __host__ __forceinline__ int bx_bin(const BxLabel& B, double x) {
     const double f = (x - B.xlo) * B.inv_bw;

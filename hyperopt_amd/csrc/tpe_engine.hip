@@ -188,7 +188,9 @@ __device__ __forceinline__ void finish_slots(const Slots& S, const double (&x)[R
 
 // The candidates of a thread's R slots: drawn from the below mixture (the
 // label's Philox stream, round key, candidate index) or read from cand_in.
-template <int MODE, bool SAMPLE, int R>
+// RAW: LGMM1 slots keep the accepted log-space draw (no exp; the caller
+// applies lgmm_value where it needs the sample itself)
+template <int MODE, bool SAMPLE, int R, bool RAW = false>
 __device__ __forceinline__ void draw_slots(const DLabel& L, const Slots& S, bool lgmm,
                                            const SampRec* __restrict__ samp,
                                            const double* __restrict__ cand_in, int64_t n,
@@ -221,17 +223,17 @@ __device__ __forceinline__ void draw_slots(const DLabel& L, const Slots& S, bool
             if (sl) {
                 const SampShared src{sl};
                 if constexpr (MODE == DENSE_ANY)
-                    ok = lgmm ? sample_slots<DENSE_LGMM, R>(L, src, seed, rk, g32, pend, x)
-                              : sample_slots<DENSE_GMM, R>(L, src, seed, rk, g32, pend, x);
+                    ok = lgmm ? sample_slots<DENSE_LGMM, R, SampShared, RAW>(L, src, seed, rk, g32, pend, x)
+                              : sample_slots<DENSE_GMM, R, SampShared, RAW>(L, src, seed, rk, g32, pend, x);
                 else
-                    ok = sample_slots<MODE, R>(L, src, seed, rk, g32, pend, x);
+                    ok = sample_slots<MODE, R, SampShared, RAW>(L, src, seed, rk, g32, pend, x);
             } else {
                 const SampGlobal src{samp + L.samp_off, L.ns};
                 if constexpr (MODE == DENSE_ANY)
-                    ok = lgmm ? sample_slots<DENSE_LGMM, R>(L, src, seed, rk, g32, pend, x)
-                              : sample_slots<DENSE_GMM, R>(L, src, seed, rk, g32, pend, x);
+                    ok = lgmm ? sample_slots<DENSE_LGMM, R, SampGlobal, RAW>(L, src, seed, rk, g32, pend, x)
+                              : sample_slots<DENSE_GMM, R, SampGlobal, RAW>(L, src, seed, rk, g32, pend, x);
                 else
-                    ok = sample_slots<MODE, R>(L, src, seed, rk, g32, pend, x);
+                    ok = sample_slots<MODE, R, SampGlobal, RAW>(L, src, seed, rk, g32, pend, x);
             }
             if (!ok) atomicOr(err, 1);
             if (L.flags & 4) {
@@ -534,37 +536,20 @@ __global__ __launch_bounds__(kBlock) void k_screen(
 //   eps = that / S, |log S - log S_exact| <= 1.001 eps + 2u (|log S| + 1),
 //   E = 1.25 (that + fp64_err), the fp64 round's own distance from exact.
 // Candidates outside the bins, with S < 1e-280 or eps > 1e-6, or NaN, get
-// hi = +inf (always re-scored).  hi is stored in fp64: E is ~1e-12, far
-// below an fp32 rounding of the score.  DIRECT: the terms each candidate
-// summed (nb + list) are counted into *terms.
-template <int R, bool SAMPLE>
-__global__ __launch_bounds__(kBlock) void k_screen_bx(
-    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
-    const Comp<double>* __restrict__ comps64, const SampRec* __restrict__ samp,
-    const BxLabel* __restrict__ bx, const double* __restrict__ tab, const int32_t* __restrict__ loff,
-    const int32_t* __restrict__ list, int64_t n, int64_t cand_offset, uint64_t seed,
-    const uint32_t* __restrict__ rounds, int32_t nl, double* __restrict__ hi,
-    unsigned long long* __restrict__ lbkey, int32_t* __restrict__ cnt, int32_t* __restrict__ idx,
-    unsigned long long* __restrict__ terms,
-    int32_t* __restrict__ err, Slots S, const double* __restrict__ cand_in,
-    double* __restrict__ s_out, double* __restrict__ e_out, double2* __restrict__ lohi) {
-    const int li = group[blockIdx.y];
-    const DLabel L = labels[li];
-    const BxLabel B = bx[li];
-    __shared__ double exp_tab[kExpTabSize];
-    __shared__ SampLds sl;
-    load_exp_table(exp_tab);
-    const bool staged = SAMPLE && stage_samp(L, samp, &sl);
+// s = NaN, E = +inf (always re-scored).  E is ~1e-12, far below an fp32
+// rounding of the score.  Returns the terms the R candidates summed
+// directly (nb + list each).
+template <int R>
+__device__ __forceinline__ int bx_score(const DLabel& L, const BxLabel& B,
+                                        const Comp<double>* __restrict__ comps64,
+                                        const double* __restrict__ tab, const int32_t* __restrict__ loff,
+                                        const int32_t* __restrict__ list, const double* __restrict__ exp_tab,
+                                        const double (&x)[R], const bool (&valid)[R], double (&s)[R],
+                                        double (&E)[R]) {
     const bool lgmm = L.mode == DENSE_LGMM;
-    double x[R];
-    int64_t z[R], ci[R], gi[R];
-    bool valid[R];
-    draw_slots<DENSE_ANY, SAMPLE, R>(L, S, lgmm, samp, cand_in, n, cand_offset, seed, rounds, err,
-                                     x, z, ci, gi, valid, staged ? &sl : nullptr);
-    double y[R], xr[R], acc[R], hv[R];
+    double y[R], xr[R], acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        hv[r] = __builtin_inf();
         y[r] = lgmm ? flog(x[r]) : x[r];
         xr[r] = y[r] - L.centre;
         acc[r] = 0.0;
@@ -576,89 +561,72 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
     // round's two-pass fallback -- are uncertified)
     const Comp<double>* ca = comps64 + L.comp_a;
     const double skip_abs = (double)L.na * exp2(-kBxT);
-    uint64_t bk = 0;
     int nterms = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
+        s[r] = __builtin_nan("");
+        E[r] = __builtin_inf();
         if (!valid[r]) continue;
         const int b = bx_bin(B, xr[r]);
-        double s = __builtin_nan(""), E = __builtin_inf();
-        if (b >= 0) {
-            const double delta = xr[r] - (B.xlo + ((double)b + 0.5) * B.bw);
-            const double* rw = tab + (size_t)(B.tab_off + b) * kBxRow;
-            double poly = rw[kBxP - 1];
+        if (b < 0) continue;
+        const double delta = xr[r] - (B.xlo + ((double)b + 0.5) * B.bw);
+        const double* rw = tab + (size_t)(B.tab_off + b) * kBxRow;
+        double poly = rw[kBxP - 1];
 #pragma unroll
-            for (int k = kBxP - 2; k >= 0; --k) poly = fma(poly, delta, rw[k]);
-            const double eabs = rw[kBxP];
-            // exp(-t), t = kappa delta^2 <= kappa rmax^2 <= 0.0625 / (T ln 2) < 1e-3:
-            // degree 5 leaves t^6 / 720 < 2e-21 (inside the 8 u S_clip term)
-            const double t = B.kappa * delta * delta;
-            const double et = fma(fma(fma(fma(fma(-1.0 / 120.0, t, 1.0 / 24.0), t, -1.0 / 6.0), t, 0.5), t,
-                                      -1.0), t, 1.0);
-            const double sclip = et * poly;
-            const int j0 = loff[B.cnt_off + b], j1 = loff[B.cnt_off + b + 1];
-            const int32_t* lst = list + B.list_off;
-            double snc = 0.0;
-            for (int j = j0; j < j1; ++j) {
-                const Comp<double> rec = ca[lst[j]];
-                const double zz = fma(xr[r], rec.a, -rec.mu);
-                snc = exp_scaled_acc(fma(-zz, zz, rec.c), exp_tab, snc);
-            }
-            nterms += L.nb + (j1 - j0);
-            const double sum = sclip + snc;
-            const double ea = eabs + 8.0 * 0x1.0p-53 * fabs(sclip) + skip_abs +
-                              (3e-14 + (double)(j1 - j0 + 4) * 0x1.0p-53) * snc + 0x1.0p-52 * sum;
-            // 1 / sum: hardware reciprocal + one Newton step (relative error
-            // ~2^-50), and 1.0001 on top: eps only bounds
-            const double r0 = __builtin_amdgcn_rcp(sum);
-            const double rs = fma(fma(-sum, r0, 1.0), r0, r0);
-            const double eps = ea * rs * 1.0001;
-            const double ab = acc[r];
-            if (fabs(delta) <= B.rmax && t <= 2e-3 && sum >= 1e-280 && ab >= 1e-290 && eps <= 1e-6) {
-                // s = (log acc_b + shift_b) - (log S + shift_a): one log of the
-                // ratio; the fp64 round's own logs, shifts and (LGMM) - y terms
-                // add at most mag 2^-50 (fp64_err), mag from the exponents
-                const double lq = flog(ab / sum);
-                s = lq + (L.shift_b - L.shift_a);
-                const double mag = (double)(abs(ilogb(ab)) + abs(ilogb(sum)) + 2) * 0.6931471805599453 +
-                                   fabs(L.shift_b) + fabs(L.shift_a) + 2.0 * fabs(y[r]) + fabs(L.centre);
-                E = 1.25 * (1.001 * eps + 0x1.0p-52 * (fabs(lq) + 1.0) + fp64_err(L.nb + L.na, mag));
-            }
+        for (int k = kBxP - 2; k >= 0; --k) poly = fma(poly, delta, rw[k]);
+        const double eabs = rw[kBxP];
+        // exp(-t), t = kappa delta^2 <= kappa rmax^2 <= 0.0625 / (T ln 2) < 1e-3:
+        // degree 5 leaves t^6 / 720 < 2e-21 (inside the 8 u S_clip term)
+        const double t = B.kappa * delta * delta;
+        const double et = fma(fma(fma(fma(fma(-1.0 / 120.0, t, 1.0 / 24.0), t, -1.0 / 6.0), t, 0.5), t,
+                                  -1.0), t, 1.0);
+        const double sclip = et * poly;
+        const int j0 = loff[B.cnt_off + b], j1 = loff[B.cnt_off + b + 1];
+        const int32_t* lst = list + B.list_off;
+        double snc = 0.0;
+        for (int j = j0; j < j1; ++j) {
+            const Comp<double> rec = ca[lst[j]];
+            const double zz = fma(xr[r], rec.a, -rec.mu);
+            snc = exp_scaled_acc(fma(-zz, zz, rec.c), exp_tab, snc);
         }
-        if constexpr (!SAMPLE) {
-            s_out[ci[r]] = s;
-            e_out[ci[r]] = E;
-            continue;
+        nterms += L.nb + (j1 - j0);
+        const double sum = sclip + snc;
+        const double ea = eabs + 8.0 * 0x1.0p-53 * fabs(sclip) + skip_abs +
+                          (3e-14 + (double)(j1 - j0 + 4) * 0x1.0p-53) * snc + 0x1.0p-52 * sum;
+        // 1 / sum: hardware reciprocal + one Newton step (relative error
+        // ~2^-50), and 1.0001 on top: eps only bounds
+        const double r0 = __builtin_amdgcn_rcp(sum);
+        const double rs = fma(fma(-sum, r0, 1.0), r0, r0);
+        const double eps = ea * rs * 1.0001;
+        const double ab = acc[r];
+        if (fabs(delta) <= B.rmax && t <= 2e-3 && sum >= 1e-280 && ab >= 1e-290 && eps <= 1e-6) {
+            // s = (log acc_b + shift_b) - (log S + shift_a): one log of the
+            // ratio; the fp64 round's own logs, shifts and (LGMM) - y terms
+            // add at most mag 2^-50 (fp64_err), mag from the exponents
+            const double lq = flog(ab / sum);
+            s[r] = lq + (L.shift_b - L.shift_a);
+            const double mag = (double)(abs(ilogb(ab)) + abs(ilogb(sum)) + 2) * 0.6931471805599453 +
+                               fabs(L.shift_b) + fabs(L.shift_a) + 2.0 * fabs(y[r]) + fabs(L.centre);
+            E[r] = 1.25 * (1.001 * eps + 0x1.0p-52 * (fabs(lq) + 1.0) + fp64_err(L.nb + L.na, mag));
         }
-        const bool cert = E <= 1e30 && s == s;
-        if (lohi) {   // packed map: (lower, upper) per candidate, picked per round
-            lohi[((size_t)blockIdx.y * S.n_rounds + z[r]) * n + ci[r]] =
-                cert ? make_double2(s - E, s + E) : make_double2(-__builtin_inf(), __builtin_inf());
-            continue;
-        }
-        double h = __builtin_inf();
-        if (cert) {
-            h = s + E;
-            const uint64_t k = order_key(s - E);
-            bk = k > bk ? k : bk;
-        }
-        hv[r] = h;
     }
-    if constexpr (!SAMPLE) return;
-    if (lohi) {   // (one atomic per wave)
-        int t = nterms;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
-        if ((threadIdx.x & 63) == 0 && terms) atomicAdd(terms, (unsigned long long)t);
-        return;
-    }
+    return nterms;
+}
+
+// Every candidate of the workgroup whose upper bound hv reaches the
+// workgroup's best lower bound bk (every one the round's best lower bound
+// can select is among them) is appended to the cell's list (idx, hi) with one
+// atomic per workgroup; bk goes to lbkey[cell], the terms to *terms.  Every
+// thread of the workgroup must call it.
+template <int R>
+__device__ __forceinline__ void bx_append(const double (&hv)[R], const bool (&valid)[R],
+                                          const int64_t (&ci)[R], uint64_t bk, int nterms, size_t cell,
+                                          int64_t n, double* __restrict__ hi,
+                                          unsigned long long* __restrict__ lbkey, int32_t* __restrict__ cnt,
+                                          int32_t* __restrict__ idx, unsigned long long* __restrict__ terms) {
     __shared__ uint64_t sh[kBlock / 64];
     bk = block_max_key(bk, sh);
-    const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
     if (threadIdx.x == 0 && bk) atomicMax(lbkey + cell, bk);
-    // candidates whose upper bound reaches this workgroup's best lower bound
-    // (every one the round's best lower bound can select is among them):
-    // appended to the cell's list with one atomic per workgroup
     bool take[R];
     int mine = 0;
 #pragma unroll
@@ -701,6 +669,272 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
         for (int w = 0; w < kBlock / 64; ++w) tot += (unsigned long long)shn[w];
         atomicAdd(terms, tot);
     }
+    __syncthreads();   // the LDS above may be reused by the caller's next pass
+}
+
+// upper bound of a certified candidate (+inf otherwise); bk: the largest
+// order key of a certified lower bound
+template <int R>
+__device__ __forceinline__ void bx_bounds(const double (&s)[R], const double (&E)[R], const bool (&valid)[R],
+                                          double (&hv)[R], uint64_t& bk) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        hv[r] = __builtin_inf();
+        if (valid[r] && E[r] <= 1e30 && s[r] == s[r]) {
+            hv[r] = s[r] + E[r];
+            const uint64_t k = order_key(s[r] - E[r]);
+            bk = k > bk ? k : bk;
+        }
+    }
+}
+
+// The expansion screen over every candidate of the round (drawn here), or
+// (SAMPLE = false) over caller-supplied candidates -> s_out / e_out.  lohi:
+// packed map, (lower, upper) per candidate, picked per round.
+template <int R, bool SAMPLE>
+__global__ __launch_bounds__(kBlock) void k_screen_bx(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<double>* __restrict__ comps64, const SampRec* __restrict__ samp,
+    const BxLabel* __restrict__ bx, const double* __restrict__ tab, const int32_t* __restrict__ loff,
+    const int32_t* __restrict__ list, int64_t n, int64_t cand_offset, uint64_t seed,
+    const uint32_t* __restrict__ rounds, int32_t nl, double* __restrict__ hi,
+    unsigned long long* __restrict__ lbkey, int32_t* __restrict__ cnt, int32_t* __restrict__ idx,
+    unsigned long long* __restrict__ terms,
+    int32_t* __restrict__ err, Slots S, const double* __restrict__ cand_in,
+    double* __restrict__ s_out, double* __restrict__ e_out, double2* __restrict__ lohi) {
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    const BxLabel B = bx[li];
+    __shared__ double exp_tab[kExpTabSize];
+    __shared__ SampLds sl;
+    load_exp_table(exp_tab);
+    const bool staged = SAMPLE && stage_samp(L, samp, &sl);
+    const bool lgmm = L.mode == DENSE_LGMM;
+    double x[R];
+    int64_t z[R], ci[R], gi[R];
+    bool valid[R];
+    draw_slots<DENSE_ANY, SAMPLE, R>(L, S, lgmm, samp, cand_in, n, cand_offset, seed, rounds, err,
+                                     x, z, ci, gi, valid, staged ? &sl : nullptr);
+    double s[R], E[R];
+    const int nterms = bx_score<R>(L, B, comps64, tab, loff, list, exp_tab, x, valid, s, E);
+    if constexpr (!SAMPLE) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (valid[r]) {
+                s_out[ci[r]] = s[r];
+                e_out[ci[r]] = E[r];
+            }
+        return;
+    } else {
+        if (lohi) {   // packed map: (lower, upper) per candidate; one atomic per wave
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (!valid[r]) continue;
+                const bool cert = E[r] <= 1e30 && s[r] == s[r];
+                lohi[((size_t)blockIdx.y * S.n_rounds + z[r]) * n + ci[r]] =
+                    cert ? make_double2(s[r] - E[r], s[r] + E[r])
+                         : make_double2(-__builtin_inf(), __builtin_inf());
+            }
+            int t = nterms;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+            if ((threadIdx.x & 63) == 0 && terms) atomicAdd(terms, (unsigned long long)t);
+            return;
+        }
+        double hv[R];
+        uint64_t bk = 0;
+        bx_bounds<R>(s, E, valid, hv, bk);
+        bx_append<R>(hv, valid, ci, bk, nterms, (size_t)blockIdx.z * nl + blockIdx.y, n, hi, lbkey, cnt, idx,
+                     terms);
+    }
+}
+
+// ------------------------------------------------------ hot-bin prefilter ----
+// (tpe_device.h "hot-bin prefilter")  tau0 per label position: over runs
+// of 1, 2, 4, .. kHotRun consecutive sub-bins whose sampling mass reaches
+// pmin together (a candidate lands in the run with near certainty, and then
+// its L is at least the run's smallest), the largest smallest L (0 = no
+// such run: every candidate is listed).  grid (ceil(max sub-bins / 256),
+// dense labels), one run start per thread, atomicMax into tau0 (zeroed).
+constexpr int kHotRun = 32;
+__global__ __launch_bounds__(kBlock) void k_hot_tau0(const int32_t* __restrict__ group,
+                                                     const BxLabel* __restrict__ bx,
+                                                     const float2* __restrict__ sb,
+                                                     const float* __restrict__ sbp, float pmin,
+                                                     unsigned long long* __restrict__ tau0) {
+    const BxLabel B = bx[group[blockIdx.y]];
+    const int64_t nsb = (int64_t)B.nbins * kBxSub;
+    uint64_t k = 0;
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j < nsb) {
+        float p = 0.0f, lmin = __builtin_inff();
+        for (int w = 0; w < kHotRun && j + w < nsb; ++w) {
+            p += sbp[B.sb_off + j + w];
+            lmin = fminf(lmin, sb[B.sb_off + j + w].y);
+            if (p >= pmin) {
+                const uint64_t v = order_key((double)lmin);
+                k = v > k ? v : k;
+                break;
+            }
+        }
+    }
+    __shared__ uint64_t sh[kBlock / 64];
+    k = block_max_key(k, sh);
+    if (threadIdx.x == 0 && k) atomicMax(tau0 + blockIdx.y, k);
+}
+
+// Draw every candidate of the round (the same draws as k_screen_bx), read
+// its sub-bin's (U, L): the largest L of the cell goes to tkey[cell], and the
+// candidates with U >= tau0 (and those outside the sub-bins) are listed with
+// their x -- (hidx, hx)[cell n + position], hcnt[cell].
+template <int R>
+__global__ __launch_bounds__(kBlock) void k_hot_bx(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
+    const BxLabel* __restrict__ bx, const float2* __restrict__ sb,
+    const unsigned long long* __restrict__ tau0, int64_t n, int64_t cand_offset, uint64_t seed,
+    const uint32_t* __restrict__ rounds, int32_t nl, unsigned long long* __restrict__ tkey,
+    int32_t* __restrict__ hcnt, int32_t* __restrict__ hidx, double* __restrict__ hx,
+    int32_t* __restrict__ err, Slots S) {
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    const BxLabel B = bx[li];
+    __shared__ SampLds sl;
+    const bool staged = stage_samp(L, samp, &sl);
+    const bool lgmm = L.mode == DENSE_LGMM;
+    double x[R];
+    int64_t z[R], ci[R], gi[R];
+    bool valid[R];
+    // raw draws: an LGMM1 label's x' is log(exp(draw)) - centre, within a
+    // few ulp of draw - centre (the sub-bins' slack covers it); the list
+    // keeps the draw and k_screen_hot applies the exp
+    draw_slots<DENSE_ANY, true, R, true>(L, S, lgmm, samp, nullptr, n, cand_offset, seed, rounds, err, x, z,
+                                         ci, gi, valid, staged ? &sl : nullptr);
+    const uint64_t t0 = tau0[blockIdx.y];
+    const int64_t nsb = (int64_t)B.nbins * kBxSub;
+    uint64_t kl = 0;
+    bool take[R];
+    int mine = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        take[r] = false;
+        if (!valid[r]) continue;
+        const double f = (x[r] - L.centre - B.xlo) * B.inv_sbw;
+        if (f >= 0.0 && f < (double)nsb) {
+            const float2 v = sb[B.sb_off + (int64_t)f];
+            const uint64_t ku = order_key((double)v.x), klo = order_key((double)v.y);
+            kl = klo > kl ? klo : kl;
+            take[r] = ku >= t0;
+        } else {
+            take[r] = true;   // outside the bins (or NaN): always listed
+        }
+        mine += take[r];
+    }
+    const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
+    __shared__ uint64_t sh[kBlock / 64];
+    kl = block_max_key(kl, sh);
+    if (threadIdx.x == 0 && kl) atomicMax(tkey + cell, kl);
+    __shared__ int shc[kBlock / 64], shb;
+    int tw = mine;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(tw, off);
+        if ((threadIdx.x & 63) >= off) tw += o;
+    }
+    if ((threadIdx.x & 63) == 63) shc[threadIdx.x >> 6] = tw;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) tot += shc[w];
+        shb = tot ? atomicAdd(hcnt + cell, tot) : 0;
+    }
+    __syncthreads();
+    int at = shb + tw - mine;
+    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) at += shc[w];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (take[r]) {
+            hidx[cell * (size_t)n + at] = (int32_t)ci[r];
+            hx[cell * (size_t)n + at] = x[r];
+            ++at;
+        }
+}
+
+// The expansion screen over the listed candidates only: workgroups stride
+// over the cell's list in passes of R * 256; the same scores, bounds and
+// appends as k_screen_bx.
+template <int R>
+__global__ __launch_bounds__(kBlock) void k_screen_hot(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<double>* __restrict__ comps64, const BxLabel* __restrict__ bx, const double* __restrict__ tab,
+    const int32_t* __restrict__ loff, const int32_t* __restrict__ list, int64_t n, int32_t nl,
+    const int32_t* __restrict__ hcnt, const int32_t* __restrict__ hidx, const double* __restrict__ hx,
+    double* __restrict__ hi, unsigned long long* __restrict__ lbkey, int32_t* __restrict__ cnt,
+    int32_t* __restrict__ idx, unsigned long long* __restrict__ terms) {
+    const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
+    const int64_t m = hcnt[cell];
+    constexpr int64_t per = (int64_t)R * kBlock;
+    if ((int64_t)blockIdx.x * per >= m) return;   // uniform over the workgroup
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    const BxLabel B = bx[li];
+    __shared__ double exp_tab[kExpTabSize];
+    load_exp_table(exp_tab);
+    const bool lgmm = L.mode == DENSE_LGMM;
+    for (int64_t j0 = (int64_t)blockIdx.x * per; j0 < m; j0 += (int64_t)gridDim.x * per) {
+        double x[R];
+        int64_t ci[R];
+        bool valid[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int64_t j = j0 + r * kBlock + threadIdx.x;
+            valid[r] = j < m;
+            const double d = valid[r] ? hx[cell * (size_t)n + j] : 0.0;   // the raw draw
+            x[r] = lgmm ? lgmm_value(d) : d;
+            ci[r] = valid[r] ? hidx[cell * (size_t)n + j] : 0;
+        }
+        double s[R], E[R], hv[R];
+        const int nterms = bx_score<R>(L, B, comps64, tab, loff, list, exp_tab, x, valid, s, E);
+        uint64_t bk = 0;
+        bx_bounds<R>(s, E, valid, hv, bk);
+        bx_append<R>(hv, valid, ci, bk, nterms, cell, n, hi, lbkey, cnt, idx, terms);
+    }
+}
+
+// tpe_hot_probe: the sub-bin (U, L) of caller-supplied candidates of one
+// label, read exactly as k_hot_bx reads them
+__global__ __launch_bounds__(kBlock) void k_hot_probe(const DLabel* __restrict__ labels,
+                                                      const BxLabel* __restrict__ bx,
+                                                      const float2* __restrict__ sb,
+                                                      const float* __restrict__ sbp, int32_t label,
+                                                      const double* __restrict__ cand, int64_t n,
+                                                      double* __restrict__ u_out, double* __restrict__ l_out,
+                                                      double* __restrict__ p_out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const DLabel L = labels[label];
+    const BxLabel B = bx[label];
+    const double y = L.mode == DENSE_LGMM ? flog(cand[i]) : cand[i];
+    const double f = (y - L.centre - B.xlo) * B.inv_sbw;
+    double u = __builtin_inf(), l = -__builtin_inf(), pm = 0.0;
+    if (f >= 0.0 && f < (double)((int64_t)B.nbins * kBxSub)) {
+        const float2 v = sb[B.sb_off + (int64_t)f];
+        u = v.x;
+        l = v.y;
+        pm = sbp[B.sb_off + (int64_t)f];
+    }
+    u_out[i] = u;
+    l_out[i] = l;
+    p_out[i] = pm;
+}
+
+// fallback flag: a cell whose largest candidate L stayed below tau0 (the
+// list may miss candidates that can win: the round re-runs k_screen_bx)
+__global__ __launch_bounds__(kBlock) void k_hot_check(int64_t cells, int32_t nl,
+                                                      const unsigned long long* __restrict__ tkey,
+                                                      const unsigned long long* __restrict__ tau0,
+                                                      int32_t* __restrict__ flag) {
+    for (int64_t c = threadIdx.x; c < cells; c += kBlock)
+        if (tkey[c] < tau0[c % nl]) atomicOr(flag, 1);
 }
 
 // The expansion screen's per-cell lists (candidate index, upper bound) hold
@@ -830,6 +1064,14 @@ constexpr int kScreenR = TPE_SCREEN_R;
 #define TPE_BX_R 4
 #endif
 constexpr int kBxR = TPE_BX_R;
+
+// candidates per thread in k_hot_bx (draw + one sub-bin read each), and the
+// workgroups per cell striding over the listed candidates in k_screen_hot
+#ifndef TPE_HOT_R
+#define TPE_HOT_R 4
+#endif
+constexpr int kHotR = TPE_HOT_R;
+constexpr unsigned kHotScreenWgs = 128;
 
 template <int R>
 __global__ __launch_bounds__(kBlock) void k_rescore(
@@ -2050,6 +2292,16 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
 // Sampled rounds: the dense GMM1 and LGMM1 labels in ONE launch (their
 // groups are adjacent), so both families fill the chip together instead of
 // leaving each other's tail idle.  Timed and counted in the DENSE_GMM slot.
+// the expansion screen over every candidate of a sampled tile-map round
+void screen_bx_all(tpe_ctx* ctx, const int32_t* grp, int nl, const RoundArgs& a) {
+    tpe_rt::Posterior& P = *ctx->P;
+    const unsigned bgx = (unsigned)((a.n + kBxR * kBlock - 1) / (kBxR * kBlock));
+    hipLaunchKernelGGL((k_screen_bx<kBxR, true>), dim3(bgx, nl, a.gz), dim3(kBlock), 0, ctx->stream, P.labels.p,
+                       grp, P.comps64.p, P.samp.p, P.bx.p, P.bx_tab.p, P.bx_loff.p, P.bx_list.p, a.n,
+                       a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->scr_hid.p, ctx->scr_lb.p, ctx->scr_cnt.p,
+                       ctx->scr_idx.p, ctx->win_evals.p, ctx->errflag.p, a.S, nullptr, nullptr, nullptr, nullptr);
+}
+
 template <typename T>
 int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
     const int nl = g.count[DENSE_GMM] + g.count[DENSE_LGMM];
@@ -2061,7 +2313,10 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
     const int nch = a.S.cpack ? dense_chunks(ctx, a.gx_whole, nl) : 1;
     if (sizeof(T) == 8 && ctx->screen && a.S.cpack == 0) {   // fp32 screen + fp64 re-score
         const size_t cells = (size_t)a.n_rounds * nl;
-        bool use_bx = false;
+        bool use_bx = false, hot = false;
+        ctx->hot_ran = false;
+        ctx->hot_listed = 0;
+        ctx->hot_fallback = 0;
         if (ctx->expand && a.n >= kWinMinN && a.cand_in == nullptr) {
             int rc = tpe_rt::bx_prepare(ctx);
             if (rc) return rc;
@@ -2080,16 +2335,52 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
             tpe_rt::Posterior& P = *ctx->P;
             HIPCHK(ctx, ctx->win_evals.reserve(1));
             HIPCHK(ctx, hipMemsetAsync(ctx->win_evals.p, 0, sizeof(unsigned long long), ctx->stream));
+            hot = ctx->hot != 0 && P.bx_sb.p != nullptr;
             if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
-            const unsigned bgx = (unsigned)((a.n + kBxR * kBlock - 1) / (kBxR * kBlock));
-            hipLaunchKernelGGL((k_screen_bx<kBxR, true>), dim3(bgx, nl, a.gz), dim3(kBlock), 0, ctx->stream,
-                               P.labels.p, grp, P.comps64.p, P.samp.p, P.bx.p, P.bx_tab.p, P.bx_loff.p,
-                               P.bx_list.p, a.n, a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->scr_hid.p,
-                               ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p, ctx->win_evals.p, ctx->errflag.p,
-                               a.S, nullptr, nullptr, nullptr, nullptr);
+            if (hot) {
+                // hot-bin prefilter: draw + sub-bin bounds, then the
+                // expansion screen over the listed candidates only
+                HIPCHK(ctx, ctx->hot_x.reserve(cells * a.n));
+                HIPCHK(ctx, ctx->hot_i.reserve(cells * a.n));
+                HIPCHK(ctx, ctx->hot_cnt.reserve(cells));
+                HIPCHK(ctx, ctx->hot_t.reserve(cells));
+                HIPCHK(ctx, ctx->hot_tau0.reserve(nl));
+                HIPCHK(ctx, ctx->hot_flag.reserve(1));
+                HIPCHK(ctx, hipMemsetAsync(ctx->hot_cnt.p, 0, cells * sizeof(int32_t), ctx->stream));
+                HIPCHK(ctx, hipMemsetAsync(ctx->hot_t.p, 0, cells * sizeof(unsigned long long), ctx->stream));
+                HIPCHK(ctx, hipMemsetAsync(ctx->hot_flag.p, 0, sizeof(int32_t), ctx->stream));
+                HIPCHK(ctx, hipMemsetAsync(ctx->hot_tau0.p, 0, nl * sizeof(unsigned long long), ctx->stream));
+                hipLaunchKernelGGL(k_hot_tau0, dim3((unsigned)((P.bx_sb_max + kBlock - 1) / kBlock), nl),
+                                   dim3(kBlock), 0, ctx->stream, grp, P.bx.p, P.bx_sb.p, P.bx_sbp.p,
+                                   (float)(kHotFill / (double)a.n), ctx->hot_tau0.p);
+                if (ctx->hot == 2)   // test mode: a threshold no candidate reaches -> the fallback
+                    HIPCHK(ctx, hipMemsetAsync(ctx->hot_tau0.p, 0xff, nl * sizeof(unsigned long long), ctx->stream));
+                const unsigned hgx = (unsigned)((a.n + kHotR * kBlock - 1) / (kHotR * kBlock));
+                hipLaunchKernelGGL((k_hot_bx<kHotR>), dim3(hgx, nl, a.gz), dim3(kBlock), 0, ctx->stream,
+                                   P.labels.p, grp, P.samp.p, P.bx.p, P.bx_sb.p, ctx->hot_tau0.p, a.n,
+                                   a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->hot_t.p, ctx->hot_cnt.p,
+                                   ctx->hot_i.p, ctx->hot_x.p, ctx->errflag.p, a.S);
+                const unsigned bgx = (unsigned)((a.n + kBxR * kBlock - 1) / (kBxR * kBlock));
+                hipLaunchKernelGGL((k_screen_hot<kBxR>), dim3(std::min(bgx, kHotScreenWgs), nl, a.gz), dim3(kBlock),
+                                   0, ctx->stream, P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p, P.bx_loff.p,
+                                   P.bx_list.p, a.n, nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p,
+                                   ctx->scr_hid.p, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p,
+                                   ctx->win_evals.p);
+            } else {
+                screen_bx_all(ctx, grp, nl, a);
+            }
             if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
             hipLaunchKernelGGL(k_select_list, dim3((unsigned)cells), dim3(kBlock), 0, ctx->stream, ctx->scr_hid.p,
                                a.n, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p);
+            if (hot) {
+                hipLaunchKernelGGL(k_hot_check, dim3(1), dim3(kBlock), 0, ctx->stream, (int64_t)cells, nl,
+                                   ctx->hot_t.p, ctx->hot_tau0.p, ctx->hot_flag.p);
+                ctx->hot_cnt_h.resize(cells);
+                HIPCHK(ctx, hipMemcpyAsync(ctx->hot_cnt_h.data(), ctx->hot_cnt.p, cells * sizeof(int32_t),
+                                           hipMemcpyDeviceToHost, ctx->stream));
+                HIPCHK(ctx, hipMemcpyAsync(&ctx->hot_flag_h, ctx->hot_flag.p, sizeof(int32_t),
+                                           hipMemcpyDeviceToHost, ctx->stream));
+            }
             HIPCHK(ctx, hipMemcpyAsync(&ctx->screen_exec_h, ctx->win_evals.p, sizeof(unsigned long long),
                                        hipMemcpyDeviceToHost, ctx->stream));
             ctx->screen_exec_pending = true;
@@ -2182,6 +2473,25 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
         HIPCHK(ctx, hipMemcpyAsync(ctx->scr_cnt_h.data(), ctx->scr_cnt.p, cells * sizeof(int32_t),
                                    hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        if (hot) {
+            ctx->hot_ran = true;
+            for (size_t c = 0; c < cells; ++c) ctx->hot_listed += ctx->hot_cnt_h[c];
+            if (ctx->hot_flag_h) {
+                // a cell's best lower bound stayed below tau0: the list may
+                // miss winners -- screen every candidate instead
+                ctx->hot_fallback = 1;
+                HIPCHK(ctx, hipMemsetAsync(ctx->scr_lb.p, 0, cells * sizeof(unsigned long long), ctx->stream));
+                HIPCHK(ctx, hipMemsetAsync(ctx->scr_cnt.p, 0, cells * sizeof(int32_t), ctx->stream));
+                screen_bx_all(ctx, grp, nl, a);
+                hipLaunchKernelGGL(k_select_list, dim3((unsigned)cells), dim3(kBlock), 0, ctx->stream,
+                                   ctx->scr_hid.p, a.n, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p);
+                HIPCHK(ctx, hipMemcpyAsync(&ctx->screen_exec_h, ctx->win_evals.p, sizeof(unsigned long long),
+                                           hipMemcpyDeviceToHost, ctx->stream));
+                HIPCHK(ctx, hipMemcpyAsync(ctx->scr_cnt_h.data(), ctx->scr_cnt.p, cells * sizeof(int32_t),
+                                           hipMemcpyDeviceToHost, ctx->stream));
+                HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+            }
+        }
         // few candidates (the expansion screen's near-ties): split by slices
         int64_t total_rs = 0;
         for (size_t c = 0; c < cells; ++c) total_rs += ctx->scr_cnt_h[c];
@@ -3037,6 +3347,35 @@ int tpe_score(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, double
     return TPE_OK;
 }
 
+int tpe_hot_probe(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, double* upper, double* lower,
+                  double* mass) {
+    if (!ctx || (n > 0 && (!cand || !upper || !lower || !mass))) return TPE_ERR_ARG;
+    if (label < 0 || label >= ctx->P->n_labels) return ctx->fail(TPE_ERR_ARG, "label out of range");
+    const DLabel& d = ctx->P->h_labels[label];
+    if (d.mode != DENSE_GMM && d.mode != DENSE_LGMM)
+        return ctx->fail(TPE_ERR_ARG, "hot probe: label is not a dense GMM1/LGMM1 label");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    int rc = tpe_rt::bx_prepare(ctx);
+    if (rc) return rc;
+    tpe_rt::Posterior& P = *ctx->P;
+    if (!P.bx_ok) return ctx->fail(TPE_ERR_ARG, "hot probe: the posterior has no expansion index");
+    if (n == 0) return TPE_OK;
+    HIPCHK(ctx, ctx->cand.reserve(n));
+    HIPCHK(ctx, ctx->out_lb.reserve(n));
+    HIPCHK(ctx, ctx->out_la.reserve(n));
+    HIPCHK(ctx, ctx->xs.reserve(n));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->cand.p, cand, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(k_hot_probe, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
+                       P.labels.p, P.bx.p, P.bx_sb.p, P.bx_sbp.p, label, ctx->cand.p, n, ctx->out_lb.p,
+                       ctx->out_la.p, ctx->xs.p);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipMemcpyAsync(upper, ctx->out_lb.p, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(lower, ctx->out_la.p, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(mass, ctx->xs.p, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    return TPE_OK;
+}
+
 int tpe_screen_probe(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, double* score32,
                      double* err_bound) {
     if (!ctx || (n > 0 && (!cand || !score32 || !err_bound))) return TPE_ERR_ARG;
@@ -3132,6 +3471,13 @@ int tpe_last_screen_terms(const tpe_ctx* ctx, int64_t* terms) {
 
 int32_t tpe_last_screen_mode(const tpe_ctx* ctx) { return ctx ? ctx->screen_mode : -1; }
 
+int tpe_last_hot(const tpe_ctx* ctx, int64_t* listed, int32_t* fallback) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (listed) *listed = ctx->hot_ran ? ctx->hot_listed : -1;
+    if (fallback) *fallback = ctx->hot_fallback;
+    return TPE_OK;
+}
+
 int tpe_last_rescore_terms(const tpe_ctx* ctx, int64_t* terms) {
     if (!ctx) return TPE_ERR_ARG;
     if (terms) *terms = ctx->screen_rescore_terms;
@@ -3151,6 +3497,10 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
         case TPE_OPT_TIMING: ctx->timing = value != 0; break;
         case TPE_OPT_WINDOW: ctx->window = value != 0; break;
         case TPE_OPT_EXPAND: ctx->expand = value != 0; break;
+        case TPE_OPT_HOT:
+            if (value < 0 || value > 2) return ctx->fail(TPE_ERR_ARG, "hot must be 0, 1 or 2");
+            ctx->hot = (int32_t)value;
+            break;
         case TPE_OPT_WIN_GROUPS:
             if (value < 0 || value > 64) return ctx->fail(TPE_ERR_ARG, "window groups must be in [0, 64]");
             ctx->win_groups = (int32_t)value;

@@ -300,6 +300,151 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
     row[kBxP] = 1.02 * (Rb + ERR + ((double)W + 2.0 * kBxP + 8.0) * kU * G) + 1e-300;
 }
 
+// lo += the smallest, hi += the largest value of one component's term
+// exp(c - kappa (x' - mu)^2) over x' in [e0, e1] (the term is unimodal in
+// x'); eps covers the rounding of mu = m'/a', of the distances and of the
+// exponent, generously
+__device__ __forceinline__ void gauss_bounds(const Comp<double>& r, double e0, double e1, double& lo,
+                                             double& hi) {
+    const double c = r.c * kExpScaleInv;
+    if (!(c > -kInf)) return;   // zero weight: no term
+    const double kap = r.a * r.a * kExpScaleInv, mu = r.mu / r.a;
+    const double dn = mu < e0 ? e0 - mu : (mu > e1 ? mu - e1 : 0.0);
+    const double df = fmax(fabs(e0 - mu), fabs(e1 - mu));
+    const double eps = 1e-15 * (64.0 + 64.0 * sqrt(kap) * (fabs(e0) + fabs(e1) + fabs(mu)) + fabs(c));
+    hi += exp(c - kap * dn * dn + eps);
+    lo += exp(c - kap * df * df - eps);
+}
+
+// P(a0 <= draw < a1) of one sampling component N(mu, sg) (draw space)
+__device__ __forceinline__ double normal_mass(double mu, double sg, double a0, double a1) {
+    const double s = 1.0 / (sg * 1.4142135623730951);
+    const double z0 = (a0 - mu) * s, z1 = (a1 - mu) * s;
+    return z0 > 0.0 ? 0.5 * (erfc(z0) - erfc(z1)) : 0.5 * (erfc(-z1) - erfc(-z0));
+}
+
+// grid (ceil(max sub-bins / 256), dense labels): one sub-bin per thread --
+// the hot-bin prefilter's [L, U] of the fp64 score over the sub-bin (float,
+// rounded outward) and the sampling mass p of the sub-bin (tpe_device.h,
+// "hot-bin prefilter").  Below mixture: every component bounded term by
+// term.  Above mixture: the bin's polynomial Taylor-shifted to the sub-bin
+// centre (|A(dc + t) - A_0'| <= sum_n>0 |A_n'| h^n), +- its Eabs, times the
+// range of exp(-kappa delta^2); the bin's list term by term; the skipped
+// components' na 2^-T on the upper side.  U, L: log ratio of the bounds plus
+// the shift difference, widened by 1e-7 (1 + |v|) and the fp64 round's own
+// error; +inf / -inf where a sum is not safely inside the normal range or a
+// record is unusable.
+__global__ __launch_bounds__(kBlock) void k_bx_bounds(const DLabel* __restrict__ labels,
+                                                      const int32_t* __restrict__ grp,
+                                                      const Comp<double>* __restrict__ comps64,
+                                                      const SampRec* __restrict__ samp,
+                                                      const BxLabel* __restrict__ bx,
+                                                      const double* __restrict__ tab,
+                                                      const int32_t* __restrict__ loff,
+                                                      const int32_t* __restrict__ list,
+                                                      float2* __restrict__ sb, float* __restrict__ sbp) {
+    const int li = grp[blockIdx.y];
+    const DLabel L = labels[li];
+    const BxLabel B = bx[li];
+    const int64_t nsb = (int64_t)B.nbins * kBxSub;
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= nsb) return;
+    const int b = (int)(j >> kBxSubBits);
+    const double sw = B.bw / kBxSub;
+    const double e0n = B.xlo + (double)j * sw, e1n = e0n + sw;
+    // slack: the rounding of a candidate's sub-bin index, and (LGMM1: k_hot_bx
+    // bins the raw draw) |log(exp(draw)) - draw| <= ~4e-16 (2 + |draw|)
+    const double slack = 2e-10 * B.bw + 1e-15 * (fabs(e0n) + fabs(e1n) + fabs(L.centre) + 2.0);
+    const double e0 = e0n - slack, e1 = e1n + slack;
+    // sampling mass (steers tau0 only: nominal edges, bounded labels cut)
+    double p = 0.0;
+    {
+        double a0 = L.centre + e0n, a1 = L.centre + e1n;
+        if ((L.flags & 3) == 3) {
+            a0 = fmax(a0, L.low);
+            a1 = fmin(a1, L.high);
+        }
+        double prev = 0.0;
+        for (int k = 0; k < L.ns && a1 > a0; ++k) {
+            const SampRec s = samp[L.samp_off + k];
+            const double w = s.cdf - prev;
+            prev = s.cdf;
+            if (w > 0.0 && s.sigma > 0.0 && s.sigma < kInf) p += w * normal_mass(s.mu, s.sigma, a0, a1);
+        }
+    }
+    bool ok = true;
+    double blo = 0.0, bhi = 0.0;
+    for (int k = 0; k < L.nb; ++k) {
+        const Comp<double> r = comps64[L.comp_b + k];
+        if (!usable(r)) {
+            ok = ok && !(r.c > -kInf);
+            continue;
+        }
+        gauss_bounds(r, e0, e1, blo, bhi);
+    }
+    // clipped above components: the bin's polynomial around the sub-bin centre
+    const double xb = B.xlo + ((double)b + 0.5) * B.bw;
+    const double dc = 0.5 * (e0 + e1) - xb, h = 0.5 * (e1 - e0);
+    if (!(fabs(dc) + h <= B.rmax)) ok = false;
+    const double* rw = tab + (size_t)(B.tab_off + b) * kBxRow;
+    double c[kBxP];
+    double G = 0.0, rp = 1.0;
+#pragma unroll
+    for (int n = 0; n < kBxP; ++n) {
+        c[n] = rw[n];
+        G += fabs(c[n]) * rp;
+        rp *= fabs(dc) + h;
+    }
+    // Taylor shift: c <- coefficients of A(dc + t)
+#pragma unroll
+    for (int i = 0; i < kBxP - 1; ++i)
+#pragma unroll
+        for (int k = kBxP - 2; k >= i; --k) c[k] = fma(dc, c[k + 1], c[k]);
+    double dev = 0.0, hp = h;
+#pragma unroll
+    for (int n = 1; n < kBxP; ++n) {
+        dev += fabs(c[n]) * hp;
+        hp *= h;
+    }
+    const double eabs = rw[kBxP];
+    const double alo = c[0] - dev - 1e-13 * G - eabs, ahi = c[0] + dev + 1e-13 * G + eabs;
+    const double d0 = dc - h, d1 = dc + h;
+    const double dmin = (d0 <= 0.0 && d1 >= 0.0) ? 0.0 : fmin(fabs(d0), fabs(d1));
+    const double dmax = fmax(fabs(d0), fabs(d1));
+    const double emax = exp(-B.kappa * dmin * dmin) * (1.0 + 1e-14);
+    const double emin = exp(-B.kappa * dmax * dmax) * (1.0 - 1e-14);
+    double slo = alo > 0.0 ? emin * alo : 0.0, shi = ahi > 0.0 ? emax * ahi : 0.0;
+    const Comp<double>* ca = comps64 + L.comp_a;
+    const int j0 = loff[B.cnt_off + b], j1 = loff[B.cnt_off + b + 1];
+    for (int jj = j0; jj < j1; ++jj) {
+        const Comp<double> r = ca[list[B.list_off + jj]];
+        if (!usable(r)) {
+            ok = ok && !(r.c > -kInf);
+            continue;
+        }
+        gauss_bounds(r, e0, e1, slo, shi);
+    }
+    shi += (double)L.na * exp2(-kBxT);
+    const double dsh = L.shift_b - L.shift_a;
+    const double mag = fabs(L.shift_b) + fabs(L.shift_a) + 2.0 * (fabs(L.centre) + fabs(e0) + fabs(e1)) + 64.0;
+    const double fe = (double)(L.nb + L.na + 64) * 0x1.0p-50 + mag * 0x1.0p-48;
+    double U = kInf, Lo = -kInf;
+    if (ok && bhi >= 1e-280 && slo >= 1e-280) {
+        const double v = log(bhi) - log(slo) + dsh;
+        if (v == v) U = v + 1e-7 * (1.0 + fabs(v)) + fe;
+    }
+    if (ok && blo >= 1e-280 && shi > 0.0 && shi < kInf) {
+        const double v = log(blo) - log(shi) + dsh;
+        if (v == v) Lo = v - 1e-7 * (1.0 + fabs(v)) - fe;
+    }
+    if (!(U == U) || !(Lo == Lo) || U < Lo) {
+        U = kInf;
+        Lo = -kInf;
+    }
+    sb[B.sb_off + j] = make_float2(float_up(U), float_down(Lo));
+    sbp[B.sb_off + j] = (float)p;
+}
+
 }  // namespace
 
 int tpe_rt::bx_prepare(tpe_ctx* ctx) {
@@ -362,6 +507,8 @@ int tpe_rt::bx_prepare(tpe_ctx* ctx) {
         B.rP = std::pow(B.rmax, (double)kBxP) * (1.0 + 1e-12);
         B.nbins = nb;
         B.n_nc = n_nc;
+        B.inv_sbw = (double)kBxSub / B.bw;
+        B.sb_off = rows * kBxSub;
         B.tab_off = rows;
         B.cnt_off = cnts;
         rows += nb;
@@ -404,6 +551,12 @@ int tpe_rt::bx_prepare(tpe_ctx* ctx) {
                        P.bx.p, P.bx_nc.p, P.bx_loff.p, P.bx_list.p);
     hipLaunchKernelGGL(k_bx_table, gb, dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p, P.bx.p,
                        P.bx_tab.p);
+    HIPCHK(ctx, P.bx_sb.reserve((size_t)rows * kBxSub));
+    HIPCHK(ctx, P.bx_sbp.reserve((size_t)rows * kBxSub));
+    P.bx_sb_max = (int64_t)bins_max * kBxSub;
+    const dim3 gs((unsigned)((P.bx_sb_max + kBlock - 1) / kBlock), nl);
+    hipLaunchKernelGGL(k_bx_bounds, gs, dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p, P.samp.p,
+                       P.bx.p, P.bx_tab.p, P.bx_loff.p, P.bx_list.p, P.bx_sb.p, P.bx_sbp.p);
     HIPCHK(ctx, hipGetLastError());
     P.bx_ok = true;
     P.bx_ready = true;

@@ -250,6 +250,14 @@ class Engine(object):
         screen (the last round's dense tile-map labels)."""
         return int(self.lib.tpe_last_screen_mode(self.h))
 
+    def last_hot(self):
+        """(candidates the hot-bin prefilter listed for the expansion screen,
+        fallback) of the last round; listed is -1 when the prefilter did not
+        run, fallback 1 when the round screened every candidate instead."""
+        a, b = ctypes.c_int64(), ctypes.c_int32()
+        self._check(self.lib.tpe_last_hot(self.h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
     def last_rescore_terms(self):
         """(candidate, component) terms the last round's fp64 re-score
         evaluated (every re-scored candidate over both of its mixtures)."""
@@ -261,11 +269,13 @@ class Engine(object):
                'chunks': L.TPE_OPT_CHUNKS, 'whole_n': L.TPE_OPT_WHOLE_N,
                'whole_rounds': L.TPE_OPT_WHOLE_ROUNDS, 'timing': L.TPE_OPT_TIMING,
                'window': L.TPE_OPT_WINDOW, 'win_t': L.TPE_OPT_WIN_T,
-               'win_groups': L.TPE_OPT_WIN_GROUPS, 'expand': L.TPE_OPT_EXPAND}
+               'win_groups': L.TPE_OPT_WIN_GROUPS, 'expand': L.TPE_OPT_EXPAND,
+               'hot': L.TPE_OPT_HOT}
 
     def set_option(self, name, value):
         """Engine switches (include/hyperopt_tpe.h TPE_OPT_*): 'screen',
-        'splitk', 'dedup', 'timing', 'window' (bool), 'chunks' (int, 0 = auto),
+        'splitk', 'dedup', 'timing', 'window', 'expand', 'hot' (bool), 'chunks'
+        (int, 0 = auto),
         'win_t' (the windowed screen's cut, 8..62), 'win_groups' (label
         groups pipelined over two streams, 0 = auto),
         'whole_n' / 'whole_rounds' (the whole problem when this engine runs
@@ -280,6 +290,16 @@ class Engine(object):
         self._check(self.lib.tpe_screen_probe(self.h, int(label), _ptr(cand), len(cand), _ptr(s),
                                               _ptr(e)))
         return s, e
+
+    def hot_probe(self, label, cand):
+        """(upper, lower, mass): the fp64 score's interval over each supplied
+        candidate's sub-bin and the sub-bin's sampling mass (the hot-bin
+        prefilter's table, tpe_hot_probe)."""
+        cand = _f64(cand).ravel()
+        u, l, m = np.empty(len(cand)), np.empty(len(cand)), np.empty(len(cand))
+        self._check(self.lib.tpe_hot_probe(self.h, int(label), _ptr(cand), len(cand), _ptr(u), _ptr(l),
+                                           _ptr(m)))
+        return u, l, m
 
     # slot 0: dense GMM1 -- and, in sampled tile/packed rounds, the dense
     # LGMM1 labels too (one merged launch; slot 1 then stays 0)

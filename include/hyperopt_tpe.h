@@ -321,6 +321,22 @@ int tpe_last_rescore_terms(const tpe_ctx *ctx, int64_t *terms);
  * ran, else 0. */
 int32_t tpe_last_screen_mode(const tpe_ctx *ctx);
 
+/* The hot-bin prefilter of the last round's expansion screen (TPE_OPT_HOT):
+ * the candidates it listed for the expansion screen (-1: it did not run) --
+ * the others were proven unable to win from their sub-bin's score interval
+ * (tpe_device.h "hot-bin prefilter") -- and whether the round fell back to
+ * screening every candidate (1: a round's best lower bound stayed below the
+ * listing threshold).  Winners are unaffected either way. */
+int tpe_last_hot(const tpe_ctx *ctx, int64_t *listed, int32_t *fallback);
+
+/* Diagnostic of the hot-bin prefilter (tests): for caller-supplied
+ * candidates of one dense resident label, the interval [lower, upper] of
+ * the fp64 score over each candidate's sub-bin (+inf / -inf outside the
+ * bins): lower <= lpdf_below - lpdf_above <= upper of tpe_score; mass: the
+ * sub-bin's sampling mass under the below mixture (0 outside). */
+int tpe_hot_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
+                  double *upper, double *lower, double *mass);
+
 /* Diagnostic of the screen (tests): for caller-supplied candidates of one
  * dense resident label, the fp32 score lpdf_below - lpdf_above the screen
  * computes and its rigorous error bound (x 1.25, as used by the round):
@@ -346,6 +362,11 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *                   windowed one when every dense label qualifies): the
  *                   above mixture's equal-sigma components as a per-bin
  *                   Taylor polynomial in fp64, bounds ~1e-12, no sort   [1]
+ *   TPE_OPT_HOT     hot-bin prefilter of the expansion screen: every
+ *                   candidate is drawn and bounded by its sub-bin's score
+ *                   interval; only those that can still win are scored
+ *                   (2: tests -- a listing threshold no candidate reaches,
+ *                   so every round takes the fallback)                  [1]
  *   TPE_OPT_WIN_GROUPS  label groups of a windowed round, each sorted on a
  *                   second stream while the previous one is screened
  *                   (0: one group; the chip is busy either way)          [0]
@@ -370,6 +391,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_WIN_T 9
 #define TPE_OPT_WIN_GROUPS 10
 #define TPE_OPT_EXPAND 11
+#define TPE_OPT_HOT 12
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
 
 #ifdef __cplusplus

@@ -269,3 +269,88 @@ def test_expansion_screen_rescores_near_ties_only(eng, config):
           'candidate' % (config, rescored, screened, rescored_w, terms / screened))
     assert rescored <= 64 * n_dense, rescored
     assert rescored < rescored_w
+
+
+@pytest.mark.parametrize('config', ['config3_device', 'config2', 'config4_device', 'config3_batched'])
+def test_hot_prefilter_same_winners(eng, config):
+    """Hot-bin prefilter (tpe_device.h "hot-bin prefilter"): every candidate
+    is drawn and bounded by its sub-bin's score interval, only the ones that
+    can still win go through the expansion screen.  The round is the fp64
+    round bit for bit -- with the prefilter, without it, with the forced
+    fallback (hot = 2: nothing listed, every candidate screened), and with
+    the screen off -- and the prefilter lists a small part of the candidates."""
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.workloads import conditional_history, hartmann_history, mixed_history
+    if config == 'config2':
+        hist = hartmann_history(2000, seed=0)
+    elif config.startswith('config4'):
+        hist = conditional_history(5000, seed=0)
+    else:
+        hist = mixed_history(32, 10000, seed=0)
+    if config.endswith('device'):
+        eng.build_posterior(*hist.device_inputs(), gamma=0.25, prior_weight=1.0)
+    else:
+        eng.set_posterior(*P.pack(hist.posteriors()))
+    C = 1 << 20
+    run = (lambda: eng.suggest_batch(17, [5, 6, 7], C // 4)) if config.endswith('batched') else \
+        (lambda: eng.suggest(17, C, round=5))
+    a = run()
+    listed, fb = eng.last_hot()
+    screened, rescored = eng.last_screen()
+    assert eng.last_screen_mode() == 3
+    try:
+        eng.set_option('hot', 0)
+        b = run()
+        assert eng.last_hot() == (-1, 0)
+        eng.set_option('hot', 2)
+        c = run()
+        listed_c, fb_c = eng.last_hot()
+    finally:
+        eng.set_option('hot', 1)
+    eng.set_option('screen', 0)
+    d = run()
+    eng.set_option('screen', 1)
+    _assert_same(a, d)
+    _assert_same(b, d)
+    _assert_same(c, d)
+    assert fb == 0 and fb_c == 1
+    print('%s: hot prefilter listed %d of %d (%.4f), re-scored %d' %
+          (config, listed, screened, listed / screened, rescored))
+    assert 0 < listed < 0.25 * screened
+
+
+def test_hot_bounds_hold(eng):
+    """The hot-bin prefilter's table: lower <= score64 <= upper over each
+    candidate's sub-bin (sampled candidates, a grid over the whole range,
+    far tails), score64 from the plain fp64 path (tpe_score); the intervals
+    are narrow near each label's best score (the prefilter lists few)."""
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.workloads import mixed_history
+    hist = mixed_history(32, 10000, seed=0)
+    posts = hist.posteriors()
+    eng.set_posterior(*P.pack(posts))
+    for li in _dense_labels(posts):
+        p = posts[li]
+        samp = eng.GMM1 if p.family == 'GMM1' else eng.LGMM1
+        x = samp(*p.below, low=p.low, high=p.high, q=None, seed=12, size=(50000,), stream=li)
+        if p.family == 'GMM1':
+            lo, hi = (p.low, p.high) if p.low is not None else (-30.0, 30.0)
+            extra = np.concatenate([np.linspace(lo, hi, 20001), [lo, hi, 0.0, 1e-9]])
+        else:
+            extra = np.exp(np.linspace(p.low, p.high, 20001))
+        x = np.concatenate([x, extra])
+        u, l, m = eng.hot_probe(li, x)
+        lb, la, _ = eng.score(li, x)
+        s64 = lb - la
+        fin = np.isfinite(s64)
+        assert np.all(l[fin] <= s64[fin]) and np.all(s64[fin] <= u[fin]), li
+        ns = 50000
+        tau = np.max(l[:ns])
+        hot = np.mean(u[:ns] >= tau)
+        w = u[:ns] - l[:ns]
+        tau0 = np.max(np.where(m[:ns] >= 64.0 / (1 << 20), l[:ns], -np.inf))
+        print('label %d (%s): tau %.6f tau0(2^20) %.6f best %.6f, hot %.5f, median width %.3g, '
+              'mass at best %.3g, mean mass %.3g' %
+              (li, p.family, tau, tau0, np.max(s64[:ns]), hot, np.median(w[np.isfinite(w)]),
+               m[np.argmax(s64[:ns])], np.mean(m[:ns])))
+        assert hot < 0.02, (li, hot)
