@@ -109,10 +109,13 @@ __device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
     return c;
 }
 
-// 53-bit uniform in (0, 1] (never 0: Box-Muller takes its log).
+// 52-bit uniform in (0, 1] (never 0: Box-Muller takes its log): 2 - m for
+// m in [1, 2) with the 52 mantissa bits taken from the two words -- exact,
+// two integer operations and one subtraction instead of a 64-bit integer
+// conversion.
 __device__ __forceinline__ double u01_open0(uint32_t hi, uint32_t lo) {
-    const uint64_t k = ((uint64_t)hi << 21) ^ (uint64_t)(lo >> 11);
-    return (double)(k + 1) * 0x1.0p-53;
+    const uint64_t bits = (0x3FFull << 52) | ((uint64_t)(hi & 0xFFFFFu) << 32) | (uint64_t)lo;
+    return 2.0 - __builtin_bit_cast(double, bits);
 }
 
 // first k with cdf[k] > u (cdf[n-1] == 1 exactly, u < 1).
@@ -196,16 +199,28 @@ __device__ __forceinline__ double cos_turn32(uint32_t w) {
     return fma(kCosSinTab[2 * k], ct, -kCosSinTab[2 * k + 1] * st);
 }
 
-template <typename Src>
-__device__ __forceinline__ double draw_attempt(const DLabel& L, const Src& src, uint32_t k0, uint32_t k1,
-                                               uint32_t g, uint32_t it, uint32_t round) {
-    const U4 r = philox4x32_10(U4{g, it, (uint32_t)L.stream, round}, k0, k1);
-    double mu, sg;
-    src.pick((double)r.x * 0x1.0p-32, mu, sg);
+// One attempt in three parts: the Philox words of (candidate g, attempt,
+// label stream, round); the component ~ weights from word x; x = mu + sigma
+// N(0, 1) by Box-Muller from words y, z (radius) and w (angle).
+__device__ __forceinline__ U4 draw_words(const DLabel& L, uint32_t k0, uint32_t k1, uint32_t g, uint32_t it,
+                                         uint32_t round) {
+    return philox4x32_10(U4{g, it, (uint32_t)L.stream, round}, k0, k1);
+}
+
+__device__ __forceinline__ double box_muller(const U4& r, double mu, double sg) {
     const double u1 = u01_open0(r.y, r.z);
     const double rad = __builtin_amdgcn_sqrt(-2.0 * flog(u1));
     const double nrm = rad * cos_turn32(r.w);
     return fma(sg, nrm, mu);
+}
+
+template <typename Src>
+__device__ __forceinline__ double draw_attempt(const DLabel& L, const Src& src, uint32_t k0, uint32_t k1,
+                                               uint32_t g, uint32_t it, uint32_t round) {
+    const U4 r = draw_words(L, k0, k1, g, it, round);
+    double mu, sg;
+    src.pick((double)r.x * 0x1.0p-32, mu, sg);
+    return box_muller(r, mu, sg);
 }
 
 // LGMM1 sample value of an accepted log-space draw (tpe.py:255: np.exp);
@@ -259,7 +274,18 @@ __device__ __forceinline__ bool sample_slots(const DLabel& L, const Src& src, ui
     const bool bounded = (L.flags & 3) == 3;
     const uint32_t mask0 = pend;
     bool ok = true;
-    uint32_t it = 0;
+    // attempt 0 of every pending slot, straight-line; the queue below takes
+    // the rejected ones from attempt 1 (the same attempt sequence per slot)
+    uint32_t rej = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if ((pend >> r) & 1u) {
+            const double draw = draw_attempt(L, src, k0, k1, g[r], 0u, rk[r]);
+            out[r] = draw;
+            if (bounded && !(L.low <= draw && draw < L.high)) rej |= 1u << r;
+        }
+    pend = rej;
+    uint32_t it = 1;
     while (pend) {
         const int cur = __builtin_ctz(pend);
         uint32_t gg = g[0], rr = rk[0];
@@ -278,7 +304,7 @@ __device__ __forceinline__ bool sample_slots(const DLabel& L, const Src& src, ui
             for (int r = 0; r < R; ++r)
                 if (cur == r) out[r] = v;
             pend &= pend - 1;
-            it = 0;
+            it = 1;
         } else {
             ++it;
         }

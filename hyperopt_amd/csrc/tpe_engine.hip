@@ -786,77 +786,100 @@ __global__ __launch_bounds__(kBlock) void k_hot_tau0(const int32_t* __restrict__
 // Draw every candidate of the round (the same draws as k_screen_bx), read
 // its sub-bin's (U, L): the largest L of the cell goes to tkey[cell], and the
 // candidates with U >= tau0 (and those outside the sub-bins) are listed with
-// their x -- (hidx, hx)[cell n + position], hcnt[cell].
+// their draw -- (hidx, hx)[cell n + position], hcnt[cell].  Tile map only:
+// workgroups stride over the cell's tiles of R * 256 candidates (the
+// sampling records are staged once per workgroup, not once per tile).
 template <int R>
-__global__ __launch_bounds__(kBlock) void k_hot_bx(
+__global__ __launch_bounds__(kBlock, 4) void k_hot_bx(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
     const BxLabel* __restrict__ bx, const float2* __restrict__ sb,
     const unsigned long long* __restrict__ tau0, int64_t n, int64_t cand_offset, uint64_t seed,
     const uint32_t* __restrict__ rounds, int32_t nl, unsigned long long* __restrict__ tkey,
     int32_t* __restrict__ hcnt, int32_t* __restrict__ hidx, double* __restrict__ hx,
-    int32_t* __restrict__ err, Slots S) {
+    int32_t* __restrict__ err) {
     const int li = group[blockIdx.y];
     const DLabel L = labels[li];
     const BxLabel B = bx[li];
     __shared__ SampLds sl;
     const bool staged = stage_samp(L, samp, &sl);
     const bool lgmm = L.mode == DENSE_LGMM;
-    double x[R];
-    int64_t z[R], ci[R], gi[R];
-    bool valid[R];
-    // raw draws: an LGMM1 label's x' is log(exp(draw)) - centre, within a
-    // few ulp of draw - centre (the sub-bins' slack covers it); the list
-    // keeps the draw and k_screen_hot applies the exp
-    draw_slots<DENSE_ANY, true, R, true>(L, S, lgmm, samp, nullptr, n, cand_offset, seed, rounds, err, x, z,
-                                         ci, gi, valid, staged ? &sl : nullptr);
     const uint64_t t0 = tau0[blockIdx.y];
     const int64_t nsb = (int64_t)B.nbins * kBxSub;
-    uint64_t kl = 0;
-    bool take[R];
-    int mine = 0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        take[r] = false;
-        if (!valid[r]) continue;
-        const double f = (x[r] - L.centre - B.xlo) * B.inv_sbw;
-        if (f >= 0.0 && f < (double)nsb) {
-            const float2 v = sb[B.sb_off + (int64_t)f];
-            const uint64_t ku = order_key((double)v.x), klo = order_key((double)v.y);
-            kl = klo > kl ? klo : kl;
-            take[r] = ku >= t0;
-        } else {
-            take[r] = true;   // outside the bins (or NaN): always listed
-        }
-        mine += take[r];
-    }
     const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
+    const uint32_t rk = rounds[blockIdx.z];
+    constexpr int64_t per = (int64_t)R * kBlock;
+    uint64_t kl = 0;
+    __shared__ int shc[kBlock / 64], shb;
+    for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per) {
+        double x[R];
+        int64_t ci[R];
+        uint32_t g32[R], rks[R], pend = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            ci[r] = base + r * kBlock + threadIdx.x;
+            g32[r] = (uint32_t)(cand_offset + ci[r]);
+            rks[r] = rk;
+            x[r] = 0.0;
+            if (ci[r] < n) pend |= 1u << r;
+        }
+        // raw draws: an LGMM1 label's x' is log(exp(draw)) - centre, within a
+        // few ulp of draw - centre (the sub-bins' slack covers it); the list
+        // keeps the draw and k_screen_hot applies the exp
+        const bool ok = staged ? (lgmm ? sample_slots<DENSE_LGMM, R, SampShared, true>(L, SampShared{&sl}, seed,
+                                                                                     rks, g32, pend, x)
+                                       : sample_slots<DENSE_GMM, R, SampShared, true>(L, SampShared{&sl}, seed,
+                                                                                    rks, g32, pend, x))
+                               : (lgmm ? sample_slots<DENSE_LGMM, R, SampGlobal, true>(
+                                             L, SampGlobal{samp + L.samp_off, L.ns}, seed, rks, g32, pend, x)
+                                       : sample_slots<DENSE_GMM, R, SampGlobal, true>(
+                                             L, SampGlobal{samp + L.samp_off, L.ns}, seed, rks, g32, pend, x));
+        if (!ok) atomicOr(err, 1);
+        bool take[R];
+        int mine = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            take[r] = false;
+            if (!((pend >> r) & 1u)) continue;
+            const double f = (x[r] - L.centre - B.xlo) * B.inv_sbw;
+            if (f >= 0.0 && f < (double)nsb) {
+                const float2 v = sb[B.sb_off + (int64_t)f];
+                const uint64_t ku = order_key((double)v.x), klo = order_key((double)v.y);
+                kl = klo > kl ? klo : kl;
+                take[r] = ku >= t0;
+            } else {
+                take[r] = true;   // outside the bins (or NaN): always listed
+            }
+            mine += take[r];
+        }
+        // this tile's takers: one atomic per workgroup and tile
+        int tw = mine;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int o = __shfl_up(tw, off);
+            if ((threadIdx.x & 63) >= off) tw += o;
+        }
+        if ((threadIdx.x & 63) == 63) shc[threadIdx.x >> 6] = tw;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int tot = 0;
+            for (int w = 0; w < kBlock / 64; ++w) tot += shc[w];
+            shb = tot ? atomicAdd(hcnt + cell, tot) : 0;
+        }
+        __syncthreads();
+        int at = shb + tw - mine;
+        for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) at += shc[w];
+        __syncthreads();   // shc / shb are rewritten by the next tile
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (take[r]) {
+                hidx[cell * (size_t)n + at] = (int32_t)ci[r];
+                hx[cell * (size_t)n + at] = x[r];
+                ++at;
+            }
+    }
     __shared__ uint64_t sh[kBlock / 64];
     kl = block_max_key(kl, sh);
     if (threadIdx.x == 0 && kl) atomicMax(tkey + cell, kl);
-    __shared__ int shc[kBlock / 64], shb;
-    int tw = mine;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int o = __shfl_up(tw, off);
-        if ((threadIdx.x & 63) >= off) tw += o;
-    }
-    if ((threadIdx.x & 63) == 63) shc[threadIdx.x >> 6] = tw;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int tot = 0;
-        for (int w = 0; w < kBlock / 64; ++w) tot += shc[w];
-        shb = tot ? atomicAdd(hcnt + cell, tot) : 0;
-    }
-    __syncthreads();
-    int at = shb + tw - mine;
-    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) at += shc[w];
-#pragma unroll
-    for (int r = 0; r < R; ++r)
-        if (take[r]) {
-            hidx[cell * (size_t)n + at] = (int32_t)ci[r];
-            hx[cell * (size_t)n + at] = x[r];
-            ++at;
-        }
 }
 
 // The expansion screen over the listed candidates only: workgroups stride
@@ -1068,10 +1091,15 @@ constexpr int kBxR = TPE_BX_R;
 // candidates per thread in k_hot_bx (draw + one sub-bin read each), and the
 // workgroups per cell striding over the listed candidates in k_screen_hot
 #ifndef TPE_HOT_R
-#define TPE_HOT_R 4
+#define TPE_HOT_R 8
 #endif
 constexpr int kHotR = TPE_HOT_R;
 constexpr unsigned kHotScreenWgs = 128;
+#ifndef TPE_HOT_WGS
+#define TPE_HOT_WGS 16384
+#endif
+constexpr int64_t kHotWgs = TPE_HOT_WGS;
+constexpr int kQR = 8;   // candidates per thread, k_qfused_tiles
 
 template <int R>
 __global__ __launch_bounds__(kBlock) void k_rescore(
@@ -1895,6 +1923,84 @@ __global__ __launch_bounds__(kBlock) void k_qfused(
     finish_slots<R>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials, scratch, sh);
 }
 
+// k_qfused for the tile map with workgroups striding over the tiles of
+// R * 256 candidates (the sampling records staged once per workgroup, a
+// running best per thread): the block's winner goes to partial slot
+// blockIdx.x and the workgroup empties the slots t = blockIdx.x + k gridDim.x
+// beyond the grid, so k_reduce sees every tile slot.  Same candidates,
+// values and winner as k_qfused.
+template <int MODE, int R>
+__global__ __launch_bounds__(kBlock, 4) void k_qfused_tiles(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<double>* __restrict__ comps64, const SampRec* __restrict__ samp,
+    const QInfo* __restrict__ qinfo, const double2* __restrict__ tab, int64_t n, int64_t cand_offset,
+    uint64_t seed, const uint32_t* __restrict__ rounds, int32_t qbase, int32_t n_labels, int32_t tiles,
+    Partial* __restrict__ partials, int32_t* __restrict__ err) {
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    __shared__ SampLds sl;
+    const bool staged = stage_samp(L, samp, &sl);
+    const QInfo Q = qinfo[qbase + blockIdx.y];
+    const uint32_t rk = rounds[blockIdx.z];
+    constexpr int64_t per = (int64_t)R * kBlock;
+    uint64_t bk = 0;
+    int64_t bi = INT64_MAX;
+    double bv = 0.0, bl = 0.0, ba = 0.0;
+    for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per) {
+        double v[R];
+        uint32_t g32[R], rks[R], pend = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int64_t ci = base + r * kBlock + threadIdx.x;
+            g32[r] = (uint32_t)(cand_offset + ci);
+            rks[r] = rk;
+            v[r] = 0.0;
+            if (ci < n) pend |= 1u << r;
+        }
+        const bool ok = staged ? sample_slots<MODE, R>(L, SampShared{&sl}, seed, rks, g32, pend, v)
+                               : sample_slots<MODE, R>(L, SampGlobal{samp + L.samp_off, L.ns}, seed, rks, g32,
+                                                       pend, v);
+        if (!ok) atomicOr(err, 1);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (!((pend >> r) & 1u)) continue;
+            const double jd = rint(v[r] / L.q);
+            int64_t j = Q.jmin;
+            if (jd >= -0x1.0p52 && jd <= 0x1.0p52) j = (int64_t)jd;
+            else atomicOr(err, 8);
+            const double x = (double)j * L.q;
+            const int64_t sidx = j - Q.jmin;
+            double lb, la;
+            if (sidx >= 0 && sidx < Q.G) {
+                const double2 t = tab[Q.tab_off + sidx];
+                lb = t.x;
+                la = t.y;
+            } else {
+                double ub, lo;
+                bool neg;
+                quant_bounds<MODE>(L, x, ub, lo, neg);
+                lb = quant_lpdf<MODE == QUANT_LGMM>(comps64 + L.comp_b, L.nb, ub, lo, L.logpacc_b);
+                la = quant_lpdf<MODE == QUANT_LGMM>(comps64 + L.comp_a, L.na, ub, lo, L.logpacc_a);
+            }
+            const uint64_t key = order_key(lb - la);
+            const int64_t gi = cand_offset + base + r * kBlock + threadIdx.x;
+            if (better(key, gi, bk, bi)) {
+                bk = key;
+                bi = gi;
+                bv = x;
+                bl = lb;
+                ba = la;
+            }
+        }
+    }
+    Partial* prow = partials + ((size_t)blockIdx.z * n_labels + li) * tiles;
+    for (int64_t t = (int64_t)gridDim.x + blockIdx.x + (int64_t)threadIdx.x * gridDim.x; t < tiles;
+         t += (int64_t)kBlock * gridDim.x)
+        prow[t] = Partial{0, INT64_MAX, 0.0, 0.0, 0.0};
+    __shared__ Partial sh[kBlock / 64];
+    block_maxloc(bk, bi, bv, bl, ba, prow + blockIdx.x, sh);
+}
+
 __device__ __forceinline__ tpe_label_result to_result(const Partial& p, int li) {
     tpe_label_result r;
     r.value = p.value;
@@ -2355,11 +2461,31 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                                    (float)(kHotFill / (double)a.n), ctx->hot_tau0.p);
                 if (ctx->hot == 2)   // test mode: a threshold no candidate reaches -> the fallback
                     HIPCHK(ctx, hipMemsetAsync(ctx->hot_tau0.p, 0xff, nl * sizeof(unsigned long long), ctx->stream));
-                const unsigned hgx = (unsigned)((a.n + kHotR * kBlock - 1) / (kHotR * kBlock));
-                hipLaunchKernelGGL((k_hot_bx<kHotR>), dim3(hgx, nl, a.gz), dim3(kBlock), 0, ctx->stream,
-                                   P.labels.p, grp, P.samp.p, P.bx.p, P.bx_sb.p, ctx->hot_tau0.p, a.n,
-                                   a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->hot_t.p, ctx->hot_cnt.p,
-                                   ctx->hot_i.p, ctx->hot_x.p, ctx->errflag.p, a.S);
+                static const int hot_r = [] {   // experiments: TPE_HOT_R=4|8|16
+                    const char* e = getenv("TPE_HOT_R");
+                    const int v = e ? atoi(e) : kHotR;
+                    return v == 4 || v == 8 || v == 16 ? v : kHotR;
+                }();
+                // ~kHotWgs workgroups over the round (tiles strided), at most one per tile
+                static const int64_t hot_wgs = [] {   // experiments: TPE_HOT_WGS
+                    const char* e = getenv("TPE_HOT_WGS");
+                    const long v = e ? atol(e) : 0;
+                    return v >= 256 ? (int64_t)v : kHotWgs;
+                }();
+                const int64_t cells_l = (int64_t)nl * a.gz;
+#define TPE_HOT_LAUNCH(RR)                                                                                  \
+    hipLaunchKernelGGL((k_hot_bx<RR>),                                                                   \
+                       dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((a.n + RR * kBlock - 1) /      \
+                                                                                (RR * kBlock),            \
+                                                                             hot_wgs / cells_l)),         \
+                            nl, a.gz),                                                                    \
+                       dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.samp.p, P.bx.p, P.bx_sb.p,         \
+                       ctx->hot_tau0.p, a.n, a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->hot_t.p,        \
+                       ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p, ctx->errflag.p)
+                if (hot_r == 4) TPE_HOT_LAUNCH(4);
+                else if (hot_r == 16) TPE_HOT_LAUNCH(16);
+                else TPE_HOT_LAUNCH(8);
+#undef TPE_HOT_LAUNCH
                 const unsigned bgx = (unsigned)((a.n + kBxR * kBlock - 1) / (kBxR * kBlock));
                 hipLaunchKernelGGL((k_screen_hot<kBxR>), dim3(std::min(bgx, kHotScreenWgs), nl, a.gz), dim3(kBlock),
                                    0, ctx->stream, P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p, P.bx_loff.p,
@@ -2659,13 +2785,25 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
                        g.dev[mode], ctx->P->comps64.p, ctx->P->samp.p, ctx->qinfo.p, ctx->qtab.p, a.n,  \
                        a.cand_offset, a.seed, ctx->rounds.p, qbase, ctx->P->n_labels, a.tiles,          \
                        ctx->partials.p, ctx->errflag.p, a.S)
+                // tile map: workgroups stride over the tiles (a.gx slots)
+                const unsigned qgx = (unsigned)std::max<int64_t>(
+                    1, std::min<int64_t>({(int64_t)a.gx, (a.n + kQR * kBlock - 1) / (kQR * kBlock),
+                                          kHotWgs / std::max<int64_t>(1, (int64_t)cnt * a.gz)}));
+#define TPE_QTILES(M)                                                                                  \
+    hipLaunchKernelGGL((k_qfused_tiles<M, kQR>), dim3(qgx, cnt, a.gz), dim3(kBlock), 0, ctx->stream,   \
+                       ctx->P->labels.p, g.dev[mode], ctx->P->comps64.p, ctx->P->samp.p, ctx->qinfo.p,  \
+                       ctx->qtab.p, a.n, a.cand_offset, a.seed, ctx->rounds.p, qbase, ctx->P->n_labels, \
+                       a.tiles, ctx->partials.p, ctx->errflag.p)
                 if (fam) {
-                    if (narrow(a.S)) TPE_QFUSED(QUANT_LGMM, kRGroup);
+                    if (a.S.cpack == 0) TPE_QTILES(QUANT_LGMM);
+                    else if (narrow(a.S)) TPE_QFUSED(QUANT_LGMM, kRGroup);
                     else TPE_QFUSED(QUANT_LGMM, kR);
                 } else {
-                    if (narrow(a.S)) TPE_QFUSED(QUANT_GMM, kRGroup);
+                    if (a.S.cpack == 0) TPE_QTILES(QUANT_GMM);
+                    else if (narrow(a.S)) TPE_QFUSED(QUANT_GMM, kRGroup);
                     else TPE_QFUSED(QUANT_GMM, kR);
                 }
+#undef TPE_QTILES
 #undef TPE_QFUSED
                 bracket(ctx, mode, 1);
             }
