@@ -51,6 +51,14 @@ VALU_SLOTS_PER_EVAL = {'f64': 12.25, 'f32': 3.625, 'screen': 3.5625}
 # expansion screen (k_screen_bx): per candidate a 15-coefficient Horner
 # polynomial (15 FMA) and the degree-5 exp(-kappa delta^2) factor (5 FMA)
 BX_FLOPS_PER_CAND = 2 * 15 + 2 * 5
+# One draw of the below mixture (tpe_device.h draw_attempt), algorithmic fp64
+# FLOP as implemented: u1 = 2 - m (1), the fdlibm log (2 + f, f / (2 + f),
+# z = s^2, the 7-coefficient polynomial, hf and the recombination: 24),
+# -2 log, sqrt (2), the angle's residual, t^2, the cos / sin polynomials and
+# cos(a + t) (20), sg * n + mu (2): ~49, plus the sub-bin index (2).  The
+# Philox words (20 32x32-bit products + 40 xors per attempt) are integer work
+# and are not counted; neither are rejected attempts.
+DRAW_FLOPS_PER_CAND = 51
 PEAK_FP64_VECTOR_TFLOPS = 78.6        # MI355X spec (MI355X_MICROARCH.md)
 PEAK_FP32_VECTOR_TFLOPS = 157.3
 # 4-cycle wave64 VALU issue slots per second at 2.4 GHz, in lanes: 256 CU x
@@ -351,7 +359,21 @@ def main():
     smode = eng.last_screen_mode() if screened else 0
     windowed = smode == 2
     slots = None
-    if smode == 3:
+    hot = smode == 3 and scr[5] > 0
+    if hot:
+        # the hot-bin prefilter: every candidate drawn and bounded by its
+        # sub-bin (k_hot_bx, the dominant kernel), the listed ones through
+        # the expansion screen (k_screen_hot); the bracket holds both
+        dom_ms = scr[2]
+        kprec = 'f64'
+        kname = 'k_hot_bx<'
+        kdesc = 'k_hot_bx + k_screen_hot (hot-bin prefilter of the expansion screen: every candidate ' \
+                'drawn and bounded by its sub-bin\'s score interval, the 0.5 % that can still win ' \
+                'scored by the expansion screen), GMM1+LGMM1 labels'
+        dom_rate = scr[3] / (dom_ms * 1e-3)
+        dom_flops = (scr[0] * DRAW_FLOPS_PER_CAND + scr[3] * FLOPS_PER_EVAL['f64']
+                     + scr[5] * BX_FLOPS_PER_CAND)
+    elif smode == 3:
         # the expansion screen: per candidate the below mixture and the
         # bin's list of unclipped components as direct fp64 terms (6 FLOP
         # each; tpe_last_screen_terms) and the bin's 13-term
@@ -402,7 +424,16 @@ def main():
             'valu_issue_frac': (round(dom_rate * slots / PEAK_VALU_LANE_INSTR[kprec], 4)
                                 if slots else None),
             'launch_ms': dom_ms / args.steps}
-    if smode == 3:
+    if hot:
+        roof['flops_per_candidate_draw'] = DRAW_FLOPS_PER_CAND
+        roof['flops_per_listed_poly'] = BX_FLOPS_PER_CAND
+        roof['candidates_per_s'] = scr[0] / (dom_ms * 1e-3)
+        roof['note'] = ('VALU-issue bound: the step draws every candidate (Philox4x32-10 + Box-Muller, '
+                        'queued rejection); achieved counts the draw\'s fp64 arithmetic (51 FLOP per '
+                        'candidate, the Philox integer work not counted), the listed candidates\' '
+                        'polynomials (40) and direct lpdf terms (6 each) over the bracket\'s device '
+                        'time; valu_busy_measured is the PMC utilisation of k_hot_bx')
+    elif smode == 3:
         roof['flops_per_candidate_poly'] = BX_FLOPS_PER_CAND
         roof['note'] = ('VALU-issue bound: per candidate the Philox + Box-Muller draw, the fp64 '
                         'exp / log sequences and the bound take most of the instruction stream; '

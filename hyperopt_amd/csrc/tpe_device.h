@@ -11,7 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "tpe_cos_table.h"
+#include "tpe_bm_table.h"
 #include "tpe_exp_table.h"
 
 namespace tpe {
@@ -186,7 +186,7 @@ __device__ __forceinline__ bool stage_samp(const DLabel& L, const SampRec* __res
 }
 
 // cos(2 pi w / 2^32): (cos, sin) of the top 8 bits' angle from a 256-entry
-// table (tpe_cos_table.h), the residual t = 2 pi (w mod 2^24) / 2^32 <
+// table (tpe_bm_table.h), the residual t = 2 pi (w mod 2^24) / 2^32 <
 // 2 pi / 256 by its Taylor polynomials (t^10 / 10! < 1e-22), then
 // cos(a + t) = cos a cos t - sin a sin t -- ~15 VALU operations and one
 // 16-byte load instead of the library cospi's ~70 operations.
@@ -207,9 +207,30 @@ __device__ __forceinline__ U4 draw_words(const DLabel& L, uint32_t k0, uint32_t 
     return philox4x32_10(U4{g, it, (uint32_t)L.stream, round}, k0, k1);
 }
 
+// -log(u) for the Box-Muller uniform u in [2^-52, 1]: u = 2^e m, m in [1,
+// 2); the 7-bit interval j of m gives a 24-bit reciprocal inv ~ 1 / c_j
+// and log(1 / inv) (tpe_bm_table.h), r = m inv - 1 (|r| < 2^-8) and log1p(r)
+// by its degree-7 Taylor polynomial (r^8 / 8 < 2^-67) -- ~10 fp64
+// operations instead of flog's ~28 (its division); ~1 ulp.  (Only the
+// draw's radius uses it: every log of a candidate or a sum stays flog.)
+__device__ __forceinline__ double bm_neglog(double u) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, u);
+    const int e = (int)(b >> 52) - 1023;
+    const int j = (int)((b >> 45) & 127u);
+    const double m = __builtin_bit_cast(double, (b & 0xFFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
+    const double r = fma(m, kLogTab[2 * j], -1.0);
+    double q = fma(1.0 / 7.0, r, -1.0 / 6.0);
+    q = fma(q, r, 0.2);
+    q = fma(q, r, -0.25);
+    q = fma(q, r, 1.0 / 3.0);
+    q = fma(q, r, -0.5);
+    q = fma(q, r, 1.0);
+    return -fma((double)e, 6.93147180559945286e-01, fma(r, q, kLogTab[2 * j + 1]));
+}
+
 __device__ __forceinline__ double box_muller(const U4& r, double mu, double sg) {
     const double u1 = u01_open0(r.y, r.z);
-    const double rad = __builtin_amdgcn_sqrt(-2.0 * flog(u1));
+    const double rad = __builtin_amdgcn_sqrt(fmax(0.0, 2.0 * bm_neglog(u1)));
     const double nrm = rad * cos_turn32(r.w);
     return fma(sg, nrm, mu);
 }

@@ -1930,7 +1930,7 @@ __global__ __launch_bounds__(kBlock) void k_qfused(
 // beyond the grid, so k_reduce sees every tile slot.  Same candidates,
 // values and winner as k_qfused.
 template <int MODE, int R>
-__global__ __launch_bounds__(kBlock, 4) void k_qfused_tiles(
+__global__ __launch_bounds__(kBlock) void k_qfused_tiles(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
     const Comp<double>* __restrict__ comps64, const SampRec* __restrict__ samp,
     const QInfo* __restrict__ qinfo, const double2* __restrict__ tab, int64_t n, int64_t cand_offset,
