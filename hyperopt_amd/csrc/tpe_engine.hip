@@ -1100,6 +1100,7 @@ constexpr unsigned kHotScreenWgs = 128;
 #endif
 constexpr int64_t kHotWgs = TPE_HOT_WGS;
 constexpr int kQR = 8;   // candidates per thread, k_qfused_tiles
+constexpr int kCatR = 8;  // candidates per thread, k_cat_tiles
 
 template <int R>
 __global__ __launch_bounds__(kBlock) void k_rescore(
@@ -2001,6 +2002,62 @@ __global__ __launch_bounds__(kBlock) void k_qfused_tiles(
     block_maxloc(bk, bi, bv, bl, ba, prow + blockIdx.x, sh);
 }
 
+// Sampled categorical labels, tile map, workgroups striding over the tiles
+// of R * 256 candidates (sample_below<CAT>'s draws: the first category whose
+// cumulative weight exceeds the Philox word, here from the workgroup's LDS
+// copy of the weights when they fit), log p lookup (tpe.py:56-63), running
+// best per thread; partial slots as k_qfused_tiles.  Same winner as k_round<CAT>.
+template <int R>
+__global__ __launch_bounds__(kBlock) void k_cat_tiles(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
+    const Comp<double>* __restrict__ comps64, const SampRec* __restrict__ samp, int64_t n, int64_t cand_offset,
+    uint64_t seed, const uint32_t* __restrict__ rounds, int32_t n_labels, int32_t tiles,
+    Partial* __restrict__ partials) {
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    __shared__ SampLds sl;
+    const bool staged = stage_samp(L, samp, &sl);
+    const uint32_t rk = rounds[blockIdx.z];
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    constexpr int64_t per = (int64_t)R * kBlock;
+    uint64_t bk = 0;
+    int64_t bi = INT64_MAX;
+    double bv = 0.0, bl = 0.0, ba = 0.0;
+    for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int64_t ci = base + r * kBlock + threadIdx.x;
+            if (ci >= n) continue;
+            const int64_t gi = cand_offset + ci;
+            const U4 w = philox4x32_10(U4{(uint32_t)gi, 0u, (uint32_t)L.stream, rk}, k0, k1);
+            const double u = (double)w.x * 0x1.0p-32;
+            int k;
+            if (staged) {
+                k = sl.guide[(int)(u * 64.0)];
+                while (sl.cdf[k] <= u) ++k;
+            } else {
+                k = cdf_search(samp + L.samp_off, L.ns, u);
+            }
+            const int sc = k >= L.nb ? L.nb - 1 : k;
+            const double lb = comps64[L.comp_b + sc].c, la = comps64[L.comp_a + sc].c;
+            const uint64_t key = order_key(lb - la);
+            if (better(key, gi, bk, bi)) {
+                bk = key;
+                bi = gi;
+                bv = (double)k;
+                bl = lb;
+                ba = la;
+            }
+        }
+    }
+    Partial* prow = partials + ((size_t)blockIdx.z * n_labels + li) * tiles;
+    for (int64_t t = (int64_t)gridDim.x + blockIdx.x + (int64_t)threadIdx.x * gridDim.x; t < tiles;
+         t += (int64_t)kBlock * gridDim.x)
+        prow[t] = Partial{0, INT64_MAX, 0.0, 0.0, 0.0};
+    __shared__ Partial sh[kBlock / 64];
+    block_maxloc(bk, bi, bv, bl, ba, prow + blockIdx.x, sh);
+}
+
 __device__ __forceinline__ tpe_label_result to_result(const Partial& p, int li) {
     tpe_label_result r;
     r.value = p.value;
@@ -2213,6 +2270,18 @@ void launch_round(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
     const int nl = g.count[MODE];
     if (nl == 0 || a.tiles == 0) return;
     bracket(ctx, MODE, 0);
+    if constexpr (MODE == CAT && SAMPLE) {
+        if (a.S.cpack == 0 && a.olb == nullptr && a.cand_in == nullptr) {   // tile map: persistent
+            const unsigned cgx = (unsigned)std::max<int64_t>(
+                1, std::min<int64_t>({(int64_t)a.gx, (a.n + kCatR * kBlock - 1) / (kCatR * kBlock),
+                                      kHotWgs / std::max<int64_t>(1, (int64_t)nl * a.gz)}));
+            hipLaunchKernelGGL((k_cat_tiles<kCatR>), dim3(cgx, nl, a.gz), dim3(kBlock), 0, ctx->stream,
+                               ctx->P->labels.p, g.dev[MODE], ctx->P->comps64.p, ctx->P->samp.p, a.n,
+                               a.cand_offset, a.seed, ctx->rounds.p, ctx->P->n_labels, a.tiles, ctx->partials.p);
+            bracket(ctx, MODE, 1);
+            return;
+        }
+    }
     const Comp<T>* comps;
     if constexpr (sizeof(T) == 8) comps = ctx->P->comps64.p; else comps = ctx->P->comps32.p;
     if (narrow(a.S))
