@@ -1924,6 +1924,15 @@ __global__ __launch_bounds__(kBlock) void k_qfused(
     finish_slots<R>(S, x, lb, la, valid, z, gi, li, n_labels, tiles, partials, scratch, sh);
 }
 
+// both quantized lpdfs of one candidate evaluated directly (scalar
+// arguments: the call spills nothing outside its own branch)
+template <bool LOG>
+__device__ __noinline__ double2 quant_pair_direct(const Comp<double>* __restrict__ cb, int nb, double lpb,
+                                                  const Comp<double>* __restrict__ ca, int na, double lpa,
+                                                  double ub, double lo) {
+    return make_double2(quant_lpdf<LOG>(cb, nb, ub, lo, lpb), quant_lpdf<LOG>(ca, na, ub, lo, lpa));
+}
+
 // k_qfused for the tile map with workgroups striding over the tiles of
 // R * 256 candidates (the sampling records staged once per workgroup, a
 // running best per thread): the block's winner goes to partial slot
@@ -1931,7 +1940,7 @@ __global__ __launch_bounds__(kBlock) void k_qfused(
 // beyond the grid, so k_reduce sees every tile slot.  Same candidates,
 // values and winner as k_qfused.
 template <int MODE, int R>
-__global__ __launch_bounds__(kBlock) void k_qfused_tiles(
+__global__ __launch_bounds__(kBlock, 4) void k_qfused_tiles(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
     const Comp<double>* __restrict__ comps64, const SampRec* __restrict__ samp,
     const QInfo* __restrict__ qinfo, const double2* __restrict__ tab, int64_t n, int64_t cand_offset,
@@ -1976,12 +1985,14 @@ __global__ __launch_bounds__(kBlock) void k_qfused_tiles(
                 const double2 t = tab[Q.tab_off + sidx];
                 lb = t.x;
                 la = t.y;
-            } else {
+            } else {   // outside the table window (out of line: rare, register-heavy)
                 double ub, lo;
                 bool neg;
                 quant_bounds<MODE>(L, x, ub, lo, neg);
-                lb = quant_lpdf<MODE == QUANT_LGMM>(comps64 + L.comp_b, L.nb, ub, lo, L.logpacc_b);
-                la = quant_lpdf<MODE == QUANT_LGMM>(comps64 + L.comp_a, L.na, ub, lo, L.logpacc_a);
+                const double2 pr = quant_pair_direct<MODE == QUANT_LGMM>(
+                    comps64 + L.comp_b, L.nb, L.logpacc_b, comps64 + L.comp_a, L.na, L.logpacc_a, ub, lo);
+                lb = pr.x;
+                la = pr.y;
             }
             const uint64_t key = order_key(lb - la);
             const int64_t gi = cand_offset + base + r * kBlock + threadIdx.x;
