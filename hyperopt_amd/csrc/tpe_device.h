@@ -156,9 +156,13 @@ struct SampLds {
 
 struct SampShared {
     const SampLds* __restrict__ t;
+    // branch-free lower bound over the 64 staged cumulative weights (padded
+    // with 2.0 past the last): six LDS reads, no loop, so the draws of a
+    // thread's slots can interleave
     __device__ __forceinline__ void pick(double u, double& mu, double& sg) const {
-        int k = t->guide[(int)(u * 64.0)];
-        while (t->cdf[k] <= u) ++k;
+        int k = 0;
+#pragma unroll
+        for (int step = kSampLds / 2; step > 0; step >>= 1) k = t->cdf[k + step - 1] <= u ? k + step : k;
         mu = t->mu[k];
         sg = t->sg[k];
     }
@@ -168,11 +172,17 @@ struct SampShared {
 // nothing staged, when K_b > kSampLds); every thread must call it
 __device__ __forceinline__ bool stage_samp(const DLabel& L, const SampRec* __restrict__ samp, SampLds* t) {
     if (L.ns > kSampLds || L.ns < 1) return false;
-    for (int k = threadIdx.x; k < L.ns; k += blockDim.x) {
-        const SampRec r = samp[L.samp_off + k];
-        t->cdf[k] = r.cdf;
-        t->mu[k] = r.mu;
-        t->sg[k] = r.sigma;
+    for (int k = threadIdx.x; k < kSampLds; k += blockDim.x) {
+        if (k < L.ns) {
+            const SampRec r = samp[L.samp_off + k];
+            t->cdf[k] = r.cdf;
+            t->mu[k] = r.mu;
+            t->sg[k] = r.sigma;
+        } else {   // padding: never picked (u < 1 <= cdf[ns - 1])
+            t->cdf[k] = 2.0;
+            t->mu[k] = 0.0;
+            t->sg[k] = 0.0;
+        }
     }
     __syncthreads();
     if (threadIdx.x < 64) {
@@ -229,6 +239,9 @@ __device__ __forceinline__ double bm_neglog(double u) {
 }
 
 __device__ __forceinline__ double box_muller(const U4& r, double mu, double sg) {
+#ifdef TPE_EXP_BM_CHEAP   // timing experiments only: not a normal draw
+    return fma(sg, (double)(int32_t)r.w * 0x1.0p-29, mu);
+#endif
     const double u1 = u01_open0(r.y, r.z);
     const double rad = __builtin_amdgcn_sqrt(fmax(0.0, 2.0 * bm_neglog(u1)));
     const double nrm = rad * cos_turn32(r.w);
@@ -292,19 +305,25 @@ __device__ __forceinline__ bool sample_slots(const DLabel& L, const Src& src, ui
                                              double (&out)[R]) {
     static_assert(MODE != CAT, "categorical slots draw once each");
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#ifdef TPE_EXP_NO_REJECT   // timing experiments only: no truncation
+    const bool bounded = false;
+#else
     const bool bounded = (L.flags & 3) == 3;
+#endif
     const uint32_t mask0 = pend;
     bool ok = true;
     // attempt 0 of every pending slot, straight-line; the queue below takes
     // the rejected ones from attempt 1 (the same attempt sequence per slot)
+    // (every slot is drawn, pending or not: no branch, so with a branch-free
+    // pick the slots' sequences can interleave)
     uint32_t rej = 0;
 #pragma unroll
-    for (int r = 0; r < R; ++r)
-        if ((pend >> r) & 1u) {
-            const double draw = draw_attempt(L, src, k0, k1, g[r], 0u, rk[r]);
-            out[r] = draw;
-            if (bounded && !(L.low <= draw && draw < L.high)) rej |= 1u << r;
-        }
+    for (int r = 0; r < R; ++r) {
+        const double draw = draw_attempt(L, src, k0, k1, g[r], 0u, rk[r]);
+        const bool p = (pend >> r) & 1u;
+        out[r] = p ? draw : out[r];
+        if (p && bounded && !(L.low <= draw && draw < L.high)) rej |= 1u << r;
+    }
     pend = rej;
     uint32_t it = 1;
     while (pend) {

@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void k_bench(const DLabel* __restrict__ Lp, co
                 double o[4] = {0, 0, 0, 0};
                 DLabel L2 = L;
                 if (V == 10) L2.flags = 0;
-                sample_slots<DENSE_GMM, 4>(L2, s, 1234u, rk, gg, 15u, o);
+                sample_slots<DENSE_GMM, 4>(L2, SampGlobal{s, L2.ns}, 1234u, rk, gg, 15u, o);
                 acc += o[0] + o[1] + o[2] + o[3];
             }
         } else if constexpr (V == 8) {   // Philox with 64-bit products

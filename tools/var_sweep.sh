@@ -1,0 +1,6 @@
+# timing of engine variants (tools/var_*.so, experiment macros): swap each in, bench
+set -e
+for v in base bm norej; do
+  cp tools/var_$v.so hyperopt_amd/libhyperopt_tpe.so
+  bash tools/q_sweep.sh | sed "s/^/$v: /"
+done
