@@ -357,7 +357,71 @@ __device__ __forceinline__ bool sample_slots(const DLabel& L, const Src& src, ui
     return ok;
 }
 
-// np.round(x / q) * q (round half to even), tpe.py:99 / :255
+// The workgroup-cooperative form of sample_slots for tile kernels (every
+// thread of the workgroup calls it, uniform control flow): attempt 0 of
+// every slot straight-line; the rejected slots go to an LDS list and the
+// whole workgroup retries them together, each list entry walking its own
+// attempts 1, 2, .. -- so a rejection costs one lane-attempt instead of a
+// wave-wide queue iteration (the same draws, bit for bit).  g0 + slot is a
+// slot's global candidate index (slot = r * blockDim + threadIdx.x).
+template <int R>
+struct RetryLds {
+    int n;
+    int32_t slot[R * 256];
+    double val[R * 256];
+};
+
+template <int MODE, int R, typename Src, bool RAW = false>
+__device__ __forceinline__ bool sample_tile(const DLabel& L, const Src& src, uint64_t seed, uint32_t rk,
+                                            uint32_t g0, uint32_t pend, double (&out)[R], RetryLds<R>& q) {
+    static_assert(MODE != CAT, "categorical slots draw once each");
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    const bool bounded = (L.flags & 3) == 3;
+    __syncthreads();   // the previous tile's list is read
+    if (threadIdx.x == 0) q.n = 0;
+    __syncthreads();
+    int pos[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t slot = (uint32_t)(r * blockDim.x + threadIdx.x);
+        const double draw = draw_attempt(L, src, k0, k1, g0 + slot, 0u, rk);
+        const bool p = (pend >> r) & 1u;
+        out[r] = p ? draw : out[r];
+        pos[r] = -1;
+        if (p && bounded && !(L.low <= draw && draw < L.high)) {
+            pos[r] = atomicAdd(&q.n, 1);
+            q.slot[pos[r]] = (int32_t)slot;
+        }
+    }
+    __syncthreads();
+    const int n = q.n;
+    bool ok = true;
+    for (int e = threadIdx.x; e < n; e += blockDim.x) {
+        const uint32_t gg = g0 + (uint32_t)q.slot[e];
+        double v = __builtin_nan("");
+        for (uint32_t it = 1; it < kMaxAttempts; ++it) {
+            const double draw = draw_attempt(L, src, k0, k1, gg, it, rk);
+            if (L.low <= draw && draw < L.high) {
+                v = draw;
+                break;
+            }
+        }
+        ok = ok && v == v;
+        q.val[e] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (pos[r] >= 0) out[r] = q.val[pos[r]];
+    if constexpr ((MODE == DENSE_LGMM || MODE == QUANT_LGMM) && !RAW) {
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if ((pend >> r) & 1u) out[r] = lgmm_value(out[r]);
+    }
+    return ok;
+}
+
+// np.round(x / q) * q (round half to even), tpe.py:99 / :255// np.round(x / q) * q (round half to even), tpe.py:99 / :255
 __device__ __forceinline__ double quantize(double v, double q) { return rint(v / q) * q; }
 
 template <int MODE>

@@ -802,7 +802,6 @@ __global__ __launch_bounds__(kBlock, 4) void k_hot_bx(
     const BxLabel B = bx[li];
     __shared__ SampLds sl;
     const bool staged = stage_samp(L, samp, &sl);
-    const bool lgmm = L.mode == DENSE_LGMM;
     const uint64_t t0 = tau0[blockIdx.y];
     const int64_t nsb = (int64_t)B.nbins * kBxSub;
     const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
@@ -810,29 +809,26 @@ __global__ __launch_bounds__(kBlock, 4) void k_hot_bx(
     constexpr int64_t per = (int64_t)R * kBlock;
     uint64_t kl = 0;
     __shared__ int shc[kBlock / 64], shb;
+    __shared__ RetryLds<R> retry;
     for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per) {
         double x[R];
         int64_t ci[R];
-        uint32_t g32[R], rks[R], pend = 0;
+        uint32_t pend = 0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             ci[r] = base + r * kBlock + threadIdx.x;
-            g32[r] = (uint32_t)(cand_offset + ci[r]);
-            rks[r] = rk;
             x[r] = 0.0;
             if (ci[r] < n) pend |= 1u << r;
         }
         // raw draws: an LGMM1 label's x' is log(exp(draw)) - centre, within a
         // few ulp of draw - centre (the sub-bins' slack covers it); the list
-        // keeps the draw and k_screen_hot applies the exp
-        const bool ok = staged ? (lgmm ? sample_slots<DENSE_LGMM, R, SampShared, true>(L, SampShared{&sl}, seed,
-                                                                                     rks, g32, pend, x)
-                                       : sample_slots<DENSE_GMM, R, SampShared, true>(L, SampShared{&sl}, seed,
-                                                                                    rks, g32, pend, x))
-                               : (lgmm ? sample_slots<DENSE_LGMM, R, SampGlobal, true>(
-                                             L, SampGlobal{samp + L.samp_off, L.ns}, seed, rks, g32, pend, x)
-                                       : sample_slots<DENSE_GMM, R, SampGlobal, true>(
-                                             L, SampGlobal{samp + L.samp_off, L.ns}, seed, rks, g32, pend, x));
+        // keeps the draw and k_screen_hot applies the exp.  (The family only
+        // changes that exp, which RAW leaves out: one instantiation.)
+        const uint32_t g0 = (uint32_t)(cand_offset + base);
+        const bool ok = staged ? sample_tile<DENSE_GMM, R, SampShared, true>(L, SampShared{&sl}, seed, rk, g0,
+                                                                             pend, x, retry)
+                               : sample_tile<DENSE_GMM, R, SampGlobal, true>(
+                                     L, SampGlobal{samp + L.samp_off, L.ns}, seed, rk, g0, pend, x, retry);
         if (!ok) atomicOr(err, 1);
         bool take[R];
         int mine = 0;
@@ -1953,23 +1949,22 @@ __global__ __launch_bounds__(kBlock, 4) void k_qfused_tiles(
     const QInfo Q = qinfo[qbase + blockIdx.y];
     const uint32_t rk = rounds[blockIdx.z];
     constexpr int64_t per = (int64_t)R * kBlock;
+    __shared__ RetryLds<R> retry;
     uint64_t bk = 0;
     int64_t bi = INT64_MAX;
     double bv = 0.0, bl = 0.0, ba = 0.0;
     for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per) {
         double v[R];
-        uint32_t g32[R], rks[R], pend = 0;
+        uint32_t pend = 0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const int64_t ci = base + r * kBlock + threadIdx.x;
-            g32[r] = (uint32_t)(cand_offset + ci);
-            rks[r] = rk;
             v[r] = 0.0;
-            if (ci < n) pend |= 1u << r;
+            if (base + r * kBlock + threadIdx.x < n) pend |= 1u << r;
         }
-        const bool ok = staged ? sample_slots<MODE, R>(L, SampShared{&sl}, seed, rks, g32, pend, v)
-                               : sample_slots<MODE, R>(L, SampGlobal{samp + L.samp_off, L.ns}, seed, rks, g32,
-                                                       pend, v);
+        const uint32_t g0 = (uint32_t)(cand_offset + base);
+        const bool ok = staged ? sample_tile<MODE, R>(L, SampShared{&sl}, seed, rk, g0, pend, v, retry)
+                               : sample_tile<MODE, R>(L, SampGlobal{samp + L.samp_off, L.ns}, seed, rk, g0, pend,
+                                                      v, retry);
         if (!ok) atomicOr(err, 1);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -2541,10 +2536,10 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                                    (float)(kHotFill / (double)a.n), ctx->hot_tau0.p);
                 if (ctx->hot == 2)   // test mode: a threshold no candidate reaches -> the fallback
                     HIPCHK(ctx, hipMemsetAsync(ctx->hot_tau0.p, 0xff, nl * sizeof(unsigned long long), ctx->stream));
-                static const int hot_r = [] {   // experiments: TPE_HOT_R=4|8|16
+                static const int hot_r = [] {   // experiments: TPE_HOT_R=4|8
                     const char* e = getenv("TPE_HOT_R");
                     const int v = e ? atoi(e) : kHotR;
-                    return v == 4 || v == 8 || v == 16 ? v : kHotR;
+                    return v == 4 || v == 8 ? v : kHotR;
                 }();
                 // ~kHotWgs workgroups over the round (tiles strided), at most one per tile
                 static const int64_t hot_wgs = [] {   // experiments: TPE_HOT_WGS
@@ -2563,7 +2558,6 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                        ctx->hot_tau0.p, a.n, a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->hot_t.p,        \
                        ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p, ctx->errflag.p)
                 if (hot_r == 4) TPE_HOT_LAUNCH(4);
-                else if (hot_r == 16) TPE_HOT_LAUNCH(16);
                 else TPE_HOT_LAUNCH(8);
 #undef TPE_HOT_LAUNCH
                 const unsigned bgx = (unsigned)((a.n + kBxR * kBlock - 1) / (kBxR * kBlock));
