@@ -135,9 +135,10 @@ constexpr uint32_t kMaxAttempts = 1u << 16;
 
 // Component lookup of the draw: the first k with cdf[k] > u.  SampGlobal
 // searches the records in global memory; SampShared (a workgroup's copy in
-// LDS, stage_samp) starts from a 64-entry guide table (guide[j] = the first
-// k with cdf[k] > j / 64) and steps forward -- ~1.4 LDS reads instead of
-// log2(K) dependent global loads.  Both return the same component.
+// LDS, stage_samp, padded to 64 entries) runs a branch-free lower bound
+// over the LDS copy; the categorical tile kernel walks the 64-entry guide
+// table (guide[j] = the first k with cdf[k] > j / 64).  All return the same
+// component.
 struct SampGlobal {
     const SampRec* __restrict__ s;
     int ns;
