@@ -95,6 +95,7 @@ struct Posterior {
     DevBuf<float2> bx_sb;                // hot-bin prefilter: per sub-bin (U, L) of the score
     DevBuf<float> bx_sbp;                //   and the below mixture's sampling mass of it
     int64_t bx_sb_max = 0;               //   the most sub-bins of one label
+    uint64_t bx_gen = 0;                 // bumped by every build of the tables (never 0 once built)
     void release() {
         labels.release();
         comps64.release();
@@ -257,6 +258,8 @@ struct tpe_ctx {
     int64_t hot_listed = 0;              // last round: candidates the prefilter listed
     int32_t hot_fallback = 0;            // last round: 1 if it re-ran the plain screen
     bool hot_ran = false;
+    uint64_t hot_tau0_gen = 0;           // hot_tau0 holds tau0 of this table generation
+    int64_t hot_tau0_n = 0;              //   and this n
     DevBuf<int32_t> scr_idx;
     DevBuf<unsigned long long> scr_lb;
     DevBuf<int32_t> scr_cnt;

@@ -2525,17 +2525,25 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                 HIPCHK(ctx, ctx->hot_i.reserve(cells * a.n));
                 HIPCHK(ctx, ctx->hot_cnt.reserve(cells));
                 HIPCHK(ctx, ctx->hot_t.reserve(cells));
+                if (ctx->hot_tau0.cap < (size_t)nl) ctx->hot_tau0_gen = 0;   // (re)allocated: recompute
                 HIPCHK(ctx, ctx->hot_tau0.reserve(nl));
                 HIPCHK(ctx, ctx->hot_flag.reserve(1));
                 HIPCHK(ctx, hipMemsetAsync(ctx->hot_cnt.p, 0, cells * sizeof(int32_t), ctx->stream));
                 HIPCHK(ctx, hipMemsetAsync(ctx->hot_t.p, 0, cells * sizeof(unsigned long long), ctx->stream));
                 HIPCHK(ctx, hipMemsetAsync(ctx->hot_flag.p, 0, sizeof(int32_t), ctx->stream));
-                HIPCHK(ctx, hipMemsetAsync(ctx->hot_tau0.p, 0, nl * sizeof(unsigned long long), ctx->stream));
-                hipLaunchKernelGGL(k_hot_tau0, dim3((unsigned)((P.bx_sb_max + kBlock - 1) / kBlock), nl),
-                                   dim3(kBlock), 0, ctx->stream, grp, P.bx.p, P.bx_sb.p, P.bx_sbp.p,
-                                   (float)(kHotFill / (double)a.n), ctx->hot_tau0.p);
-                if (ctx->hot == 2)   // test mode: a threshold no candidate reaches -> the fallback
+                // tau0 depends on the posterior's tables and n only: kept across rounds
+                if (ctx->hot_tau0_gen != P.bx_gen || ctx->hot_tau0_n != a.n || ctx->hot == 2) {
+                    HIPCHK(ctx, hipMemsetAsync(ctx->hot_tau0.p, 0, nl * sizeof(unsigned long long), ctx->stream));
+                    hipLaunchKernelGGL(k_hot_tau0, dim3((unsigned)((P.bx_sb_max + kBlock - 1) / kBlock), nl),
+                                       dim3(kBlock), 0, ctx->stream, grp, P.bx.p, P.bx_sb.p, P.bx_sbp.p,
+                                       (float)(kHotFill / (double)a.n), ctx->hot_tau0.p);
+                    ctx->hot_tau0_gen = P.bx_gen;
+                    ctx->hot_tau0_n = a.n;
+                }
+                if (ctx->hot == 2) {   // test mode: a threshold no candidate reaches -> the fallback
                     HIPCHK(ctx, hipMemsetAsync(ctx->hot_tau0.p, 0xff, nl * sizeof(unsigned long long), ctx->stream));
+                    ctx->hot_tau0_gen = 0;
+                }
                 static const int hot_r = [] {   // experiments: TPE_HOT_R=4|8
                     const char* e = getenv("TPE_HOT_R");
                     const int v = e ? atoi(e) : kHotR;

@@ -554,6 +554,8 @@ int tpe_rt::bx_prepare(tpe_ctx* ctx) {
     HIPCHK(ctx, P.bx_sb.reserve((size_t)rows * kBxSub));
     HIPCHK(ctx, P.bx_sbp.reserve((size_t)rows * kBxSub));
     P.bx_sb_max = (int64_t)bins_max * kBxSub;
+    static uint64_t gen_counter = 0;   // unique over every posterior of the process
+    P.bx_gen = __atomic_add_fetch(&gen_counter, 1, __ATOMIC_RELAXED);
     const dim3 gs((unsigned)((P.bx_sb_max + kBlock - 1) / kBlock), nl);
     hipLaunchKernelGGL(k_bx_bounds, gs, dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p, P.samp.p,
                        P.bx.p, P.bx_tab.p, P.bx_loff.p, P.bx_list.p, P.bx_sb.p, P.bx_sbp.p);
