@@ -123,6 +123,7 @@ SIGNATURES = {
     'tpe_last_rescore_terms': (ctypes.c_int, [_P, _P]),
     'tpe_last_screen_mode': (ctypes.c_int32, [_P]),
     'tpe_last_hot': (ctypes.c_int, [_P, _P, _P]),
+    'tpe_last_prepare': (ctypes.c_int, [_P, _P]),
     'tpe_hot_probe': (ctypes.c_int, [_P, ctypes.c_int32, _P, ctypes.c_int64, _P, _P, _P]),
     'tpe_screen_probe': (ctypes.c_int, [_P, _I32, _P, _I64, _P, _P]),
 }

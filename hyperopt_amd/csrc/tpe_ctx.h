@@ -258,6 +258,7 @@ struct tpe_ctx {
     int64_t hot_listed = 0;              // last round: candidates the prefilter listed
     int32_t hot_fallback = 0;            // last round: 1 if it re-ran the plain screen
     bool hot_ran = false;
+    float prep_ms = 0.f;                 // wall ms of the last expansion-index build (bx_prepare)
     uint64_t hot_tau0_gen = 0;           // hot_tau0 holds tau0 of this table generation
     int64_t hot_tau0_n = 0;              //   and this n
     DevBuf<int32_t> scr_idx;
@@ -372,6 +373,7 @@ int64_t win_rounds_per_batch(int64_t n, int32_t nl);
 // and lists of every dense label of the resident posterior (once per
 // posterior) and sets P->bx_ok when every dense label has one.
 int bx_prepare(tpe_ctx* ctx);
+int bx_build(tpe_ctx* ctx);
 }  // namespace tpe_rt
 
 // per-device implementations of the entry points a multi-device context

@@ -3691,6 +3691,12 @@ int tpe_last_screen_terms(const tpe_ctx* ctx, int64_t* terms) {
 
 int32_t tpe_last_screen_mode(const tpe_ctx* ctx) { return ctx ? ctx->screen_mode : -1; }
 
+int tpe_last_prepare(const tpe_ctx* ctx, float* ms) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (ms) *ms = ctx->prep_ms;
+    return TPE_OK;
+}
+
 int tpe_last_hot(const tpe_ctx* ctx, int64_t* listed, int32_t* fallback) {
     if (!ctx) return TPE_ERR_ARG;
     if (listed) *listed = ctx->hot_ran ? ctx->hot_listed : -1;

@@ -14,7 +14,7 @@
 //   k_bx_count    per bin: unclipped components whose term can reach 2^-T in it
 //   k_bx_offsets  per label: their exclusive scan (list offsets), the total
 //   k_bx_fill     per bin: the list
-//   k_bx_table    per bin: A_0..A_14 over the clipped components within the
+//   k_bx_table    per bin (one wave): A_0..A_14 over the clipped components within the
 //                 window, and the absolute bound Eabs of truncation + rounding
 //
 // Bounds (natural-log units, records as tpe_device.h Comp: c'/K = log coef -
@@ -27,11 +27,13 @@
 //   rounding     g e^y ((3P + 10 + 4 |arg|) 2^-53        (g and the n-th term)
 //                       + 2 kappa (|d| + r)(|mu'| + |d| + r) 2^-51)
 //                                                         (mu' = m'/a', d, delta)
-// and per bin (W + 2P + 8) 2^-53 G for the sums and the Horner evaluation
+// and per bin (W + 6 + 2P + 8) 2^-53 G for the sums (per lane, then the
+// butterfly) and the Horner evaluation
 // (sum_n |A_n| |delta|^n <= G = sum_k g e^y), x 1.02.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 
 #include "../../include/hyperopt_tpe.h"
@@ -247,7 +249,10 @@ __device__ __forceinline__ int lower_mu(const Comp<double>* __restrict__ c, int 
     return lo;
 }
 
-// grid (ceil(max bins / 256), dense labels): one bin per thread
+// grid (ceil(max bins / 4), dense labels): one wave per bin, its lanes
+// striding over the window's clipped components, the partial sums added by a
+// butterfly at the end (a bin's window holds thousands of components: one
+// thread per bin left the chip ~0.6 waves per SIMD)
 __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ labels,
                                                      const int32_t* __restrict__ grp,
                                                      const Comp<double>* __restrict__ comps64,
@@ -256,8 +261,9 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
     const int li = grp[blockIdx.y];
     const DLabel L = labels[li];
     const BxLabel B = bx[li];
-    const int b = blockIdx.x * kBlock + threadIdx.x;
-    if (b >= B.nbins) return;
+    const int lane = threadIdx.x & 63;
+    const int b = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (b >= B.nbins) return;   // whole waves
     const Comp<double>* c = comps64 + L.comp_a;
     const double xb = B.xlo + ((double)b + 0.5) * B.bw;
     const double r = B.rmax, kap = B.kappa;
@@ -268,9 +274,8 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
     double A[kBxP];
 #pragma unroll
     for (int n = 0; n < kBxP; ++n) A[n] = 0.0;
-    double Rb = 0.0, G = 0.0, ERR = 0.0;
-    int W = 0;
-    for (int k = k0; k < k1; ++k) {
+    double Rb = 0.0, G = 0.0, ERR = 0.0, W = 0.0;
+    for (int k = k0 + lane; k < k1; k += 64) {
         const Comp<double> rec = c[k];
         if (rec.a != B.astar) continue;
         const double mu = rec.mu / B.astar, d = mu - xb;
@@ -292,12 +297,23 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
         G += gy;
         ERR += gy * ((3.0 * kBxP + 10.0 + 4.0 * fabs(arg)) * kU +
                      2.0 * kap * (fabs(d) + r) * (fabs(mu) + fabs(d) + r) * 0x1.0p-51);
-        ++W;
+        W += 1.0;
     }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+        for (int n = 0; n < kBxP; ++n) A[n] += __shfl_xor(A[n], off);
+        Rb += __shfl_xor(Rb, off);
+        G += __shfl_xor(G, off);
+        ERR += __shfl_xor(ERR, off);
+        W += __shfl_xor(W, off);
+    }
+    if (lane != 0) return;
     double* row = tab + (size_t)(B.tab_off + b) * kBxRow;
 #pragma unroll
     for (int n = 0; n < kBxP; ++n) row[n] = A[n];
-    row[kBxP] = 1.02 * (Rb + ERR + ((double)W + 2.0 * kBxP + 8.0) * kU * G) + 1e-300;
+    // sums: each lane's sequential part (<= W terms) then 6 butterfly levels
+    row[kBxP] = 1.02 * (Rb + ERR + (W + 6.0 + 2.0 * kBxP + 8.0) * kU * G) + 1e-300;
 }
 
 // lo += the smallest, hi += the largest value of one component's term
@@ -450,6 +466,18 @@ __global__ __launch_bounds__(kBlock) void k_bx_bounds(const DLabel* __restrict__
 int tpe_rt::bx_prepare(tpe_ctx* ctx) {
     tpe_rt::Posterior& P = *ctx->P;
     if (P.bx_ready) return TPE_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = bx_build(ctx);
+    if (rc == TPE_OK && ctx->timing) {   // the build's wall time, kernels included
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+        ctx->prep_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return rc;
+}
+
+// the tables, lists and sub-bin bounds of every dense label (bx_prepare)
+int tpe_rt::bx_build(tpe_ctx* ctx) {
+    tpe_rt::Posterior& P = *ctx->P;
     P.bx_ok = false;
     const std::vector<int32_t>& gg = P.h_group[DENSE_GMM];
     const std::vector<int32_t>& gl = P.h_group[DENSE_LGMM];
@@ -549,7 +577,8 @@ int tpe_rt::bx_prepare(tpe_ctx* ctx) {
                                ctx->stream));
     hipLaunchKernelGGL(k_bx_list<true>, gb, dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p,
                        P.bx.p, P.bx_nc.p, P.bx_loff.p, P.bx_list.p);
-    hipLaunchKernelGGL(k_bx_table, gb, dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p, P.bx.p,
+    const dim3 gt((unsigned)((bins_max + kBlock / 64 - 1) / (kBlock / 64)), nl);
+    hipLaunchKernelGGL(k_bx_table, gt, dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p, P.bx.p,
                        P.bx_tab.p);
     HIPCHK(ctx, P.bx_sb.reserve((size_t)rows * kBxSub));
     HIPCHK(ctx, P.bx_sbp.reserve((size_t)rows * kBxSub));

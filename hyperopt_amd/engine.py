@@ -258,6 +258,13 @@ class Engine(object):
         self._check(self.lib.tpe_last_hot(self.h, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
 
+    def last_prepare_ms(self):
+        """Wall ms of the last build of the expansion screen's index (once per
+        posterior, before its first large sampled round)."""
+        ms = ctypes.c_float()
+        self._check(self.lib.tpe_last_prepare(self.h, ctypes.byref(ms)))
+        return ms.value
+
     def last_rescore_terms(self):
         """(candidate, component) terms the last round's fp64 re-score
         evaluated (every re-scored candidate over both of its mixtures)."""

@@ -329,6 +329,12 @@ int32_t tpe_last_screen_mode(const tpe_ctx *ctx);
  * listing threshold).  Winners are unaffected either way. */
 int tpe_last_hot(const tpe_ctx *ctx, int64_t *listed, int32_t *fallback);
 
+/* Wall milliseconds (kernels included; TPE_OPT_TIMING on) of the last build
+ * of the expansion screen's index -- bin tables, lists and the prefilter's
+ * sub-bin bounds -- which runs once per posterior, before its first large
+ * sampled round (0 if it has not run). */
+int tpe_last_prepare(const tpe_ctx *ctx, float *ms);
+
 /* Diagnostic of the hot-bin prefilter (tests): for caller-supplied
  * candidates of one dense resident label, the interval [lower, upper] of
  * the fp64 score over each candidate's sub-bin (+inf / -inf outside the
