@@ -458,6 +458,8 @@ def main():
                                    else 'candidate-sharded x%d') % (len(devs) if devs else world)
                                   + (' (one process, multi-device context %s)' % devs
                                      if devs else '')},
+        'fresh_posterior_round_ms': (round(post_build['device_call_ms'] + prep_ms + dt / args.steps * 1e3, 3)
+                                     if prep_ms else None),
         'posterior_build': dict(post_build, expansion_index_ms=(round(prep_ms, 3) if prep_ms else None),
                                 expansion_index_note='once per posterior (bin tables, lists, sub-bin '
                                 'bounds; wall ms with the kernels), in its first large round; the '

@@ -233,9 +233,12 @@ __global__ __launch_bounds__(kBlock) void k_bx_offsets(const int32_t* __restrict
     }
 }
 
-__constant__ double kInvN[kBxP + 1] = {1.0,      1.0,      1.0 / 2,  1.0 / 3,  1.0 / 4,  1.0 / 5,
-                                       1.0 / 6,  1.0 / 7,  1.0 / 8,  1.0 / 9,  1.0 / 10, 1.0 / 11,
-                                       1.0 / 12, 1.0 / 13, 1.0 / 14, 1.0 / 15};
+// 1 / n!, n <= kBxP
+__constant__ double kInvFact[kBxP + 1] = {
+    1.0, 1.0, 1.0 / 2, 1.0 / 6, 1.0 / 24, 1.0 / 120, 1.0 / 720, 1.0 / 5040, 1.0 / 40320, 1.0 / 362880,
+    1.0 / 3628800, 1.0 / 39916800, 1.0 / 479001600, 1.0 / 6227020800.0, 1.0 / 87178291200.0,
+    1.0 / 1307674368000.0};
+
 
 // first record index k in [0, n) with mu'_k >= v (mu' = m'/a', sorted by mu)
 __device__ __forceinline__ int lower_mu(const Comp<double>* __restrict__ c, int n, double v) {
@@ -261,9 +264,11 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
     const int li = grp[blockIdx.y];
     const DLabel L = labels[li];
     const BxLabel B = bx[li];
+    __shared__ double exp_tab[kExpTabSize];
+    load_exp_table(exp_tab);
     const int lane = threadIdx.x & 63;
     const int b = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-    if (b >= B.nbins) return;   // whole waves
+    if (b >= B.nbins) return;   // whole waves (after the table's barrier)
     const Comp<double>* c = comps64 + L.comp_a;
     const double xb = B.xlo + ((double)b + 0.5) * B.bw;
     const double r = B.rmax, kap = B.kappa;
@@ -275,27 +280,32 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
 #pragma unroll
     for (int n = 0; n < kBxP; ++n) A[n] = 0.0;
     double Rb = 0.0, G = 0.0, ERR = 0.0, W = 0.0;
+    // mu' = m' (1 / a*): <= 1.5 ulp (inside the 2^-51 allowance below);
+    // g = exp(arg) through the fp64 round's table exp (<= 2.6e-14 relative,
+    // added to the rounding term); the powers g (2 kappa d)^n by one
+    // multiply each, A_n += that / n! (one rounding each, inside 3P + 10)
+    const double inv_a = 1.0 / B.astar;
     for (int k = k0 + lane; k < k1; k += 64) {
         const Comp<double> rec = c[k];
         if (rec.a != B.astar) continue;
-        const double mu = rec.mu / B.astar, d = mu - xb;
+        const double mu = rec.mu * inv_a, d = mu - xb;
         const double arg = rec.c * kExpScaleInv - kap * d * d;
         if (!(arg > -740.0)) continue;   // below 2^-1067 in the whole bin: in the skip term
-        const double g = exp(arg), two = 2.0 * kap * d;
+        const double g = exp_scaled(fmin(arg * kExpScale, 0.0), exp_tab), two = 2.0 * kap * d;
         // e^y only enters the bounds: 1 + y + y^2 >= e^y for 0 <= y <= 1.79
         const double yv = fabs(two) * r, ey = yv <= 1.5 ? fma(yv, yv, 1.0 + yv) : exp(yv) * 1.000001;
         double t = g;
         A[0] += t;
 #pragma unroll
         for (int n = 1; n < kBxP; ++n) {
-            t = t * two * kInvN[n];
-            A[n] += t;
+            t *= two;
+            A[n] = fma(t, kInvFact[n], A[n]);
         }
-        const double tP = fabs(t * two * kInvN[kBxP]);   // g |2 kappa d|^P / P!
+        const double tP = fabs(t * two) * kInvFact[kBxP];   // g |2 kappa d|^P / P!
         const double gy = g * ey;
         Rb += tP * B.rP * ey;
         G += gy;
-        ERR += gy * ((3.0 * kBxP + 10.0 + 4.0 * fabs(arg)) * kU +
+        ERR += gy * ((3.0 * kBxP + 10.0 + 4.0 * fabs(arg)) * kU + 2.6e-14 +
                      2.0 * kap * (fabs(d) + r) * (fabs(mu) + fabs(d) + r) * 0x1.0p-51);
         W += 1.0;
     }
