@@ -330,23 +330,27 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
 // exp(c - kappa (x' - mu)^2) over x' in [e0, e1] (the term is unimodal in
 // x'); eps covers the rounding of mu = m'/a', of the distances and of the
 // exponent, generously
+// (the exps through the fp64 round's LDS table: exp_scaled is within
+// 2.6e-14 relative of exp, so 3e-14 more in eps keeps both sides rigorous)
 __device__ __forceinline__ void gauss_bounds(const Comp<double>& r, double e0, double e1, double& lo,
-                                             double& hi) {
+                                             double& hi, const double* __restrict__ etab) {
     const double c = r.c * kExpScaleInv;
     if (!(c > -kInf)) return;   // zero weight: no term
     const double kap = r.a * r.a * kExpScaleInv, mu = r.mu / r.a;
     const double dn = mu < e0 ? e0 - mu : (mu > e1 ? mu - e1 : 0.0);
     const double df = fmax(fabs(e0 - mu), fabs(e1 - mu));
-    const double eps = 1e-15 * (64.0 + 64.0 * sqrt(kap) * (fabs(e0) + fabs(e1) + fabs(mu)) + fabs(c));
-    hi += exp(c - kap * dn * dn + eps);
-    lo += exp(c - kap * df * df - eps);
+    const double eps = 1e-15 * (64.0 + 64.0 * sqrt(kap) * (fabs(e0) + fabs(e1) + fabs(mu)) + fabs(c)) + 3e-14;
+    hi += exp_scaled((c - kap * dn * dn + eps) * kExpScale, etab);
+    const double ul = (c - kap * df * df - eps) * kExpScale;
+    lo += ul > -4.0e6 ? exp_scaled(ul, etab) : 0.0;   // (below ~2^-980: 0 is a lower bound)
 }
 
-// P(a0 <= draw < a1) of one sampling component N(mu, sg) (draw space)
+// P(a0 <= draw < a1) of one sampling component N(mu, sg) (draw space), in
+// fp32: the mass only steers tau0, never a bound
 __device__ __forceinline__ double normal_mass(double mu, double sg, double a0, double a1) {
     const double s = 1.0 / (sg * 1.4142135623730951);
-    const double z0 = (a0 - mu) * s, z1 = (a1 - mu) * s;
-    return z0 > 0.0 ? 0.5 * (erfc(z0) - erfc(z1)) : 0.5 * (erfc(-z1) - erfc(-z0));
+    const float z0 = (float)((a0 - mu) * s), z1 = (float)((a1 - mu) * s);
+    return z0 > 0.0f ? 0.5 * (double)(erfcf(z0) - erfcf(z1)) : 0.5 * (double)(erfcf(-z1) - erfcf(-z0));
 }
 
 // grid (ceil(max sub-bins / 256), dense labels): one sub-bin per thread --
@@ -372,6 +376,8 @@ __global__ __launch_bounds__(kBlock) void k_bx_bounds(const DLabel* __restrict__
     const int li = grp[blockIdx.y];
     const DLabel L = labels[li];
     const BxLabel B = bx[li];
+    __shared__ double etab[kExpTabSize];
+    load_exp_table(etab);
     const int64_t nsb = (int64_t)B.nbins * kBxSub;
     const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (j >= nsb) return;
@@ -406,7 +412,7 @@ __global__ __launch_bounds__(kBlock) void k_bx_bounds(const DLabel* __restrict__
             ok = ok && !(r.c > -kInf);
             continue;
         }
-        gauss_bounds(r, e0, e1, blo, bhi);
+        gauss_bounds(r, e0, e1, blo, bhi, etab);
     }
     // clipped above components: the bin's polynomial around the sub-bin centre
     const double xb = B.xlo + ((double)b + 0.5) * B.bw;
@@ -448,7 +454,7 @@ __global__ __launch_bounds__(kBlock) void k_bx_bounds(const DLabel* __restrict__
             ok = ok && !(r.c > -kInf);
             continue;
         }
-        gauss_bounds(r, e0, e1, slo, shi);
+        gauss_bounds(r, e0, e1, slo, shi, etab);
     }
     shi += (double)L.na * exp2(-kBxT);
     const double dsh = L.shift_b - L.shift_a;
