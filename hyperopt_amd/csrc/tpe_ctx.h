@@ -252,6 +252,7 @@ struct tpe_ctx {
     DevBuf<double> hot_x;                // per cell: listed candidates' x
     DevBuf<int32_t> hot_i, hot_cnt;      //   their indices; per cell the count
     DevBuf<unsigned long long> hot_t, hot_tau0;   // per cell largest L; per label tau0
+    DevBuf<uint32_t> hot_bits;           // per sub-bin: U >= tau0 (words at sb_off / 32)
     DevBuf<int32_t> hot_flag;            // fallback flag
     std::vector<int32_t> hot_cnt_h;
     int32_t hot_flag_h = 0;

@@ -783,31 +783,50 @@ __global__ __launch_bounds__(kBlock) void k_hot_tau0(const int32_t* __restrict__
     if (threadIdx.x == 0 && k) atomicMax(tau0 + blockIdx.y, k);
 }
 
-// Draw every candidate of the round (the same draws as k_screen_bx), read
-// its sub-bin's (U, L): the largest L of the cell goes to tkey[cell], and the
-// candidates with U >= tau0 (and those outside the sub-bins) are listed with
-// their draw -- (hidx, hx)[cell n + position], hcnt[cell].  Tile map only:
+// per label position: bit j of the label's words = (order key of U_j >=
+// tau0); grid (ceil(max words / 256), dense labels), one word per thread
+__global__ __launch_bounds__(kBlock) void k_hot_bits(const int32_t* __restrict__ group,
+                                                     const BxLabel* __restrict__ bx,
+                                                     const float2* __restrict__ sb,
+                                                     const unsigned long long* __restrict__ tau0,
+                                                     uint32_t* __restrict__ hbits) {
+    const BxLabel B = bx[group[blockIdx.y]];
+    const int64_t nsb = (int64_t)B.nbins * kBxSub;
+    const int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (w * 32 >= nsb) return;
+    const uint64_t t0 = tau0[blockIdx.y];
+    uint32_t word = 0;
+    for (int b = 0; b < 32; ++b) {
+        const int64_t j = w * 32 + b;
+        if (j < nsb && order_key((double)sb[B.sb_off + j].x) >= t0) word |= 1u << b;
+    }
+    hbits[(B.sb_off >> 5) + w] = word;
+}
+
+// Draw every candidate of the round (the same draws as k_screen_bx) and
+// test its sub-bin's bit (U >= tau0, k_hot_bits: 4 KB per label at config 3,
+// L1-resident): the candidates whose bit is set (and those outside the
+// sub-bins) are listed with their draw -- (hidx, hx)[cell n + position],
+// hcnt[cell].  The largest L of the cell is taken over the LISTED candidates
+// (k_screen_hot): a candidate left out has L <= U < tau0, so the cell's
+// largest L reaches tau0 iff a listed candidate's does.  Tile map only:
 // workgroups stride over the cell's tiles of R * 256 candidates (the
 // sampling records are staged once per workgroup, not once per tile).
 template <int R>
 __global__ __launch_bounds__(kBlock, 4) void k_hot_bx(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
-    const BxLabel* __restrict__ bx, const float2* __restrict__ sb,
-    const unsigned long long* __restrict__ tau0, int64_t n, int64_t cand_offset, uint64_t seed,
-    const uint32_t* __restrict__ rounds, int32_t nl, unsigned long long* __restrict__ tkey,
-    int32_t* __restrict__ hcnt, int32_t* __restrict__ hidx, double* __restrict__ hx,
-    int32_t* __restrict__ err) {
+    const BxLabel* __restrict__ bx, const uint32_t* __restrict__ hbits, int64_t n, int64_t cand_offset,
+    uint64_t seed, const uint32_t* __restrict__ rounds, int32_t nl, int32_t* __restrict__ hcnt,
+    int32_t* __restrict__ hidx, double* __restrict__ hx, int32_t* __restrict__ err) {
     const int li = group[blockIdx.y];
     const DLabel L = labels[li];
     const BxLabel B = bx[li];
     __shared__ SampLds sl;
     const bool staged = stage_samp(L, samp, &sl);
-    const uint64_t t0 = tau0[blockIdx.y];
     const int64_t nsb = (int64_t)B.nbins * kBxSub;
     const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
     const uint32_t rk = rounds[blockIdx.z];
     constexpr int64_t per = (int64_t)R * kBlock;
-    uint64_t kl = 0;
     __shared__ int shc[kBlock / 64], shb;
     __shared__ RetryLds<R> retry;
     for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per) {
@@ -838,10 +857,8 @@ __global__ __launch_bounds__(kBlock, 4) void k_hot_bx(
             if (!((pend >> r) & 1u)) continue;
             const double f = (x[r] - L.centre - B.xlo) * B.inv_sbw;
             if (f >= 0.0 && f < (double)nsb) {
-                const float2 v = sb[B.sb_off + (int64_t)f];
-                const uint64_t ku = order_key((double)v.x), klo = order_key((double)v.y);
-                kl = klo > kl ? klo : kl;
-                take[r] = ku >= t0;
+                const int64_t sbi = B.sb_off + (int64_t)f;   // (sb_off: a multiple of 32)
+                take[r] = (hbits[sbi >> 5] >> (sbi & 31)) & 1u;
             } else {
                 take[r] = true;   // outside the bins (or NaN): always listed
             }
@@ -873,9 +890,6 @@ __global__ __launch_bounds__(kBlock, 4) void k_hot_bx(
                 ++at;
             }
     }
-    __shared__ uint64_t sh[kBlock / 64];
-    kl = block_max_key(kl, sh);
-    if (threadIdx.x == 0 && kl) atomicMax(tkey + cell, kl);
 }
 
 // The expansion screen over the listed candidates only: workgroups stride
@@ -888,7 +902,8 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
     const int32_t* __restrict__ loff, const int32_t* __restrict__ list, int64_t n, int32_t nl,
     const int32_t* __restrict__ hcnt, const int32_t* __restrict__ hidx, const double* __restrict__ hx,
     double* __restrict__ hi, unsigned long long* __restrict__ lbkey, int32_t* __restrict__ cnt,
-    int32_t* __restrict__ idx, unsigned long long* __restrict__ terms) {
+    int32_t* __restrict__ idx, unsigned long long* __restrict__ terms, const float2* __restrict__ sb,
+    unsigned long long* __restrict__ tkey) {
     const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
     const int64_t m = hcnt[cell];
     constexpr int64_t per = (int64_t)R * kBlock;
@@ -899,6 +914,8 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
     __shared__ double exp_tab[kExpTabSize];
     load_exp_table(exp_tab);
     const bool lgmm = L.mode == DENSE_LGMM;
+    const int64_t nsb = (int64_t)B.nbins * kBxSub;
+    uint64_t kl = 0;   // the largest sub-bin L of the listed candidates
     for (int64_t j0 = (int64_t)blockIdx.x * per; j0 < m; j0 += (int64_t)gridDim.x * per) {
         double x[R];
         int64_t ci[R];
@@ -910,6 +927,11 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
             const double d = valid[r] ? hx[cell * (size_t)n + j] : 0.0;   // the raw draw
             x[r] = lgmm ? lgmm_value(d) : d;
             ci[r] = valid[r] ? hidx[cell * (size_t)n + j] : 0;
+            const double f = (d - L.centre - B.xlo) * B.inv_sbw;   // k_hot_bx's sub-bin
+            if (valid[r] && f >= 0.0 && f < (double)nsb) {
+                const uint64_t k = order_key((double)sb[B.sb_off + (int64_t)f].y);
+                kl = k > kl ? k : kl;
+            }
         }
         double s[R], E[R], hv[R];
         const int nterms = bx_score<R>(L, B, comps64, tab, loff, list, exp_tab, x, valid, s, E);
@@ -917,6 +939,9 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
         bx_bounds<R>(s, E, valid, hv, bk);
         bx_append<R>(hv, valid, ci, bk, nterms, cell, n, hi, lbkey, cnt, idx, terms);
     }
+    __shared__ uint64_t shk[kBlock / 64];
+    kl = block_max_key(kl, shk);
+    if (threadIdx.x == 0 && kl) atomicMax(tkey + cell, kl);
 }
 
 // tpe_hot_probe: the sub-bin (U, L) of caller-supplied candidates of one
@@ -2533,16 +2558,19 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                 HIPCHK(ctx, hipMemsetAsync(ctx->hot_flag.p, 0, sizeof(int32_t), ctx->stream));
                 // tau0 depends on the posterior's tables and n only: kept across rounds
                 if (ctx->hot_tau0_gen != P.bx_gen || ctx->hot_tau0_n != a.n || ctx->hot == 2) {
+                    HIPCHK(ctx, ctx->hot_bits.reserve((size_t)(P.bx_sb.cap + 31) / 32));
                     HIPCHK(ctx, hipMemsetAsync(ctx->hot_tau0.p, 0, nl * sizeof(unsigned long long), ctx->stream));
                     hipLaunchKernelGGL(k_hot_tau0, dim3((unsigned)((P.bx_sb_max + kBlock - 1) / kBlock), nl),
                                        dim3(kBlock), 0, ctx->stream, grp, P.bx.p, P.bx_sb.p, P.bx_sbp.p,
                                        (float)(kHotFill / (double)a.n), ctx->hot_tau0.p);
-                    ctx->hot_tau0_gen = P.bx_gen;
+                    if (ctx->hot == 2)   // test mode: a threshold no candidate reaches -> the fallback
+                        HIPCHK(ctx, hipMemsetAsync(ctx->hot_tau0.p, 0xff, nl * sizeof(unsigned long long),
+                                                   ctx->stream));
+                    const int64_t words = (P.bx_sb_max + 31) / 32;
+                    hipLaunchKernelGGL(k_hot_bits, dim3((unsigned)((words + kBlock - 1) / kBlock), nl), dim3(kBlock),
+                                       0, ctx->stream, grp, P.bx.p, P.bx_sb.p, ctx->hot_tau0.p, ctx->hot_bits.p);
+                    ctx->hot_tau0_gen = ctx->hot == 2 ? 0 : P.bx_gen;
                     ctx->hot_tau0_n = a.n;
-                }
-                if (ctx->hot == 2) {   // test mode: a threshold no candidate reaches -> the fallback
-                    HIPCHK(ctx, hipMemsetAsync(ctx->hot_tau0.p, 0xff, nl * sizeof(unsigned long long), ctx->stream));
-                    ctx->hot_tau0_gen = 0;
                 }
                 static const int hot_r = [] {   // experiments: TPE_HOT_R=4|8
                     const char* e = getenv("TPE_HOT_R");
@@ -2562,9 +2590,9 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                                                                                 (RR * kBlock),            \
                                                                              hot_wgs / cells_l)),         \
                             nl, a.gz),                                                                    \
-                       dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.samp.p, P.bx.p, P.bx_sb.p,         \
-                       ctx->hot_tau0.p, a.n, a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->hot_t.p,        \
-                       ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p, ctx->errflag.p)
+                       dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.samp.p, P.bx.p, ctx->hot_bits.p,    \
+                       a.n, a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->hot_cnt.p, ctx->hot_i.p,         \
+                       ctx->hot_x.p, ctx->errflag.p)
                 if (hot_r == 4) TPE_HOT_LAUNCH(4);
                 else TPE_HOT_LAUNCH(8);
 #undef TPE_HOT_LAUNCH
@@ -2573,7 +2601,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                                    0, ctx->stream, P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p, P.bx_loff.p,
                                    P.bx_list.p, a.n, nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p,
                                    ctx->scr_hid.p, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p,
-                                   ctx->win_evals.p);
+                                   ctx->win_evals.p, P.bx_sb.p, ctx->hot_t.p);
             } else {
                 screen_bx_all(ctx, grp, nl, a);
             }
