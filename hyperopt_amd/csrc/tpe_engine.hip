@@ -783,6 +783,8 @@ __global__ __launch_bounds__(kBlock) void k_hot_tau0(const int32_t* __restrict__
     if (threadIdx.x == 0 && k) atomicMax(tau0 + blockIdx.y, k);
 }
 
+constexpr int kHotLdsWords = 1024;   // k_hot_bx stages up to 32k sub-bin bits in LDS
+
 // per label position: bit j of the label's words = (order key of U_j >=
 // tau0); grid (ceil(max words / 256), dense labels), one word per thread
 __global__ __launch_bounds__(kBlock) void k_hot_bits(const int32_t* __restrict__ group,
@@ -828,6 +830,12 @@ __global__ __launch_bounds__(kBlock, 4) void k_hot_bx(
     const uint32_t rk = rounds[blockIdx.z];
     constexpr int64_t per = (int64_t)R * kBlock;
     __shared__ int shc[kBlock / 64], shb;
+    // the label's bits in LDS when they fit (config 3: 32k sub-bins, 4 KB)
+    __shared__ uint32_t sbits[kHotLdsWords];
+    const bool lds_bits = nsb <= (int64_t)kHotLdsWords * 32;
+    if (lds_bits)
+        for (int w = threadIdx.x; w < (int)(nsb >> 5); w += kBlock) sbits[w] = hbits[(B.sb_off >> 5) + w];
+    __syncthreads();
     __shared__ RetryLds<R> retry;
     for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per) {
         double x[R];
@@ -857,8 +865,9 @@ __global__ __launch_bounds__(kBlock, 4) void k_hot_bx(
             if (!((pend >> r) & 1u)) continue;
             const double f = (x[r] - L.centre - B.xlo) * B.inv_sbw;
             if (f >= 0.0 && f < (double)nsb) {
-                const int64_t sbi = B.sb_off + (int64_t)f;   // (sb_off: a multiple of 32)
-                take[r] = (hbits[sbi >> 5] >> (sbi & 31)) & 1u;
+                const int64_t j = (int64_t)f;   // (sb_off: a multiple of 32)
+                const uint32_t word = lds_bits ? sbits[j >> 5] : hbits[((B.sb_off + j) >> 5)];
+                take[r] = (word >> (j & 31)) & 1u;
             } else {
                 take[r] = true;   // outside the bins (or NaN): always listed
             }
