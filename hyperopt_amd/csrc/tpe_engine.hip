@@ -1130,6 +1130,7 @@ constexpr unsigned kHotScreenWgs = 128;
 #endif
 constexpr int64_t kHotWgs = TPE_HOT_WGS;
 constexpr int kQR = 8;   // candidates per thread, k_qfused_tiles
+constexpr int kQLdsKeys = 1024;   // grid values whose keys k_qfused_tiles stages in LDS
 constexpr int kCatR = 8;  // candidates per thread, k_cat_tiles
 
 template <int R>
@@ -1984,9 +1985,20 @@ __global__ __launch_bounds__(kBlock, 4) void k_qfused_tiles(
     const uint32_t rk = rounds[blockIdx.z];
     constexpr int64_t per = (int64_t)R * kBlock;
     __shared__ RetryLds<R> retry;
+    // the window's scores as order keys in LDS when they fit: per candidate
+    // one LDS read; the winner's lpdfs are read from the table at the end
+    __shared__ unsigned long long skey[kQLdsKeys];
+    const bool lds_keys = Q.G > 0 && Q.G <= kQLdsKeys;
+    if (lds_keys)
+        for (int t = threadIdx.x; t < (int)Q.G; t += kBlock) {
+            const double2 v = tab[Q.tab_off + t];
+            skey[t] = order_key(v.x - v.y);
+        }
+    __syncthreads();
     uint64_t bk = 0;
-    int64_t bi = INT64_MAX;
-    double bv = 0.0, bl = 0.0, ba = 0.0;
+    int64_t bi = INT64_MAX, bj = 0;
+    bool bdirect = false;
+    double bl = 0.0, ba = 0.0;
     for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per) {
         double v[R];
         uint32_t pend = 0;
@@ -2007,8 +2019,19 @@ __global__ __launch_bounds__(kBlock, 4) void k_qfused_tiles(
             int64_t j = Q.jmin;
             if (jd >= -0x1.0p52 && jd <= 0x1.0p52) j = (int64_t)jd;
             else atomicOr(err, 8);
-            const double x = (double)j * L.q;
             const int64_t sidx = j - Q.jmin;
+            const int64_t gi = cand_offset + base + r * kBlock + threadIdx.x;
+            if (lds_keys && sidx >= 0 && sidx < Q.G) {
+                const uint64_t key = skey[sidx];
+                if (better(key, gi, bk, bi)) {
+                    bk = key;
+                    bi = gi;
+                    bj = j;
+                    bdirect = false;
+                }
+                continue;
+            }
+            const double x = (double)j * L.q;
             double lb, la;
             if (sidx >= 0 && sidx < Q.G) {
                 const double2 t = tab[Q.tab_off + sidx];
@@ -2024,16 +2047,22 @@ __global__ __launch_bounds__(kBlock, 4) void k_qfused_tiles(
                 la = pr.y;
             }
             const uint64_t key = order_key(lb - la);
-            const int64_t gi = cand_offset + base + r * kBlock + threadIdx.x;
             if (better(key, gi, bk, bi)) {
                 bk = key;
                 bi = gi;
-                bv = x;
+                bj = j;
+                bdirect = true;
                 bl = lb;
                 ba = la;
             }
         }
     }
+    if (bi != INT64_MAX && !bdirect) {   // the winner came from the LDS keys
+        const double2 t = tab[Q.tab_off + (bj - Q.jmin)];
+        bl = t.x;
+        ba = t.y;
+    }
+    const double bv = (double)bj * L.q;
     Partial* prow = partials + ((size_t)blockIdx.z * n_labels + li) * tiles;
     for (int64_t t = (int64_t)gridDim.x + blockIdx.x + (int64_t)threadIdx.x * gridDim.x; t < tiles;
          t += (int64_t)kBlock * gridDim.x)
