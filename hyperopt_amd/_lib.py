@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libhyperopt_tpe.so')
 HEADER = os.path.join(os.path.dirname(HERE), 'include', 'hyperopt_tpe.h')
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 TPE_OK = 0
 TPE_ERR_VALUE = -1
@@ -116,6 +116,8 @@ SIGNATURES = {
     'tpe_history_reset': (ctypes.c_int, [_P, _P, _I32, _P, _I64]),
     'tpe_history_append': (ctypes.c_int, [_P, _P, _P, _P]),
     'tpe_build_posterior_resident': (ctypes.c_int, [_P, _P, _I64, _I64, _D, _D, _I32, _P]),
+    'tpe_build_posterior_resident_ordered': (ctypes.c_int, [_P, _P, _I64, _I64, _D, _D, _I32, _P, _P, _P,
+                                                            _P, _P]),
     'tpe_last_build_ms': (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float)]),
     'tpe_last_screen': (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_float)]),
     'tpe_set_option': (ctypes.c_int, [_P, _I32, _I64]),
@@ -141,17 +143,28 @@ def load():
         import torch  # noqa: F401
     except Exception:
         pass
-    if not os.path.exists(LIB_PATH):
+    variant = os.environ.get('HYPEROPT_AMD_VARIANT')
+    path = LIB_PATH
+    if variant:   # timing experiments only (tools/build_variant.py): explicit opt-in
+        import sys
+        path = os.path.abspath(variant)
+        sys.stderr.write('hyperopt_amd: loading the experiment variant %s, not the product '
+                         'library\n' % path)
+    if not os.path.exists(path):
         raise OSError('hyperopt_amd native library not built: %s (run '
-                      '`python -m hyperopt_amd._build` or __graft_entry__.build())' % LIB_PATH)
-    lib = ctypes.CDLL(LIB_PATH)
+                      '`python -m hyperopt_amd._build` or __graft_entry__.build())' % path)
+    lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
     if lib.tpe_abi_version() != ABI_VERSION:
         raise OSError('ABI version mismatch')
-    check_stamp(lib)
+    if variant:
+        if not lib.tpe_source_hash().decode().startswith('v:'):
+            raise OSError('%s is not a variant build (tools/build_variant.py)' % path)
+    else:
+        check_stamp(lib)
     _lib = lib
     return lib
 

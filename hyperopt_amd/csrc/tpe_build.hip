@@ -265,9 +265,14 @@ __device__ __forceinline__ double np_minimum(double a, double b) { return (a != 
 // over the order-preserving 64-bit keys locate the n_below-th smallest key
 // K* (LDS histograms, wave-aggregated adds), then one pass flags every key
 // < K* and the first (by position) of the keys == K* that complete n_below
-// -- an ordered pass only when some keys == K* stay out.
+// -- an ordered pass only when some keys == K* stay out.  That case is a tie
+// of equal losses across the n_below boundary, where the reference's
+// np.argsort (tpe.py:637, numpy's unstable sort) picks its own members:
+// *split_tie is set so the caller can supply the reference's below set
+// (tpe_build_posterior_resident_ordered).
 __global__ __launch_bounds__(kSplitBlock) void k_split(const double* __restrict__ losses, int64_t T,
-                                                       int32_t n_below, uint8_t* __restrict__ below) {
+                                                       int32_t n_below, uint8_t* __restrict__ below,
+                                                       int32_t* __restrict__ split_tie) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     __shared__ uint32_t hist[256];
     __shared__ uint64_t prefix_sh;
@@ -336,7 +341,10 @@ __global__ __launch_bounds__(kSplitBlock) void k_split(const double* __restrict_
             if (asc_key(losses[i]) <= kstar) below[i] = 1;
         return;
     }
-    if (tid == 0) base_sh = 0;
+    if (tid == 0) {
+        base_sh = 0;
+        *split_tie = 1;
+    }
     __syncthreads();
     const uint64_t lt = (1ull << lane) - 1ull;
     for (int64_t c0 = 0; c0 < T; c0 += kSplitBlock) {
@@ -696,7 +704,8 @@ __global__ __launch_bounds__(kParzenBlock) void k_parzen(
     const double* __restrict__ keys_sorted, const int32_t* __restrict__ idx_sorted,
     const int64_t* __restrict__ mix_off, double prior_weight, int32_t lf, double* __restrict__ w,
     double* __restrict__ mu, double* __restrict__ sigma, int32_t* __restrict__ kcount,
-    double* __restrict__ leaf_sum) {
+    double* __restrict__ leaf_sum, const int64_t* __restrict__ order_off, const int32_t* __restrict__ order,
+    int32_t* __restrict__ ties, int32_t* __restrict__ err) {
 #pragma clang fp contract(off)
     const int l = blockIdx.x, side = blockIdx.y, tid = threadIdx.x;
     const tpe_label_spec sp = specs[l];
@@ -802,6 +811,22 @@ __global__ __launch_bounds__(kParzenBlock) void k_parzen(
         sk = keys_sorted + off;
         si = idx_sorted + off;
     }
+    // a caller-supplied order of the above observations (the reference's
+    // np.argsort(mus), tpe.py:433, computed on the host): same sorted values,
+    // but tied observations -- and so their linear-forgetting weights -- in
+    // numpy's order instead of by position
+    bool supplied = false;
+    if (side == 1 && order_off) {
+        const int64_t b = order_off[l], e = order_off[l + 1];
+        if (e > b) {
+            if (e - b != n) {
+                if (tid == 0) atomicOr(err, 8);
+                return;
+            }
+            supplied = true;
+            si = order + b;
+        }
+    }
     const double pmu = sp.prior_mu, psig = sp.prior_sigma;
     __shared__ int pos_sh;
     if (tid == 0) pos_sh = 0;
@@ -839,11 +864,33 @@ __global__ __launch_bounds__(kParzenBlock) void k_parzen(
         s = np_minimum(np_maximum(s, minsigma), maxsigma);   // np.clip
         if (j == pos) s = psig;
         double wt;
-        if (j == pos) wt = pw;
-        else wt = use_lf ? lf_weight(si[j < pos ? j : j - 1], ramp) : 1.0;
+        if (j == pos) {
+            wt = pw;
+        } else {
+            const int32_t r = si[j < pos ? j : j - 1];
+            if (r < 0 || r >= n) {   // (a supplied order out of range)
+                atomicOr(err, 8);
+                wt = 0.0;
+            } else {
+                wt = use_lf ? lf_weight(r, ramp) : 1.0;
+            }
+        }
         w[o + j] = wt;
         mu[o + j] = srtd(j);
         sigma[o + j] = s;
+    }
+    __syncthreads();
+    // does the mixture depend on the order of tied observations?  Whenever
+    // the weights differ (linear forgetting) and two observations share a
+    // mu: the reference's np.argsort order then decides which weight sits in
+    // which slot -- which weight meets a run end's sigma (the gap to the
+    // neighbouring value) rather than the clipped minimum of its inner
+    // slots, and the order of the normalising np.sum.
+    if (use_lf && !supplied) {
+        bool dep = false;
+        for (int64_t j = 1 + tid; j < K; j += kParzenBlock)
+            if (j != pos && j - 1 != pos && mu[o + j] == mu[o + j - 1]) dep = true;
+        if (__ballot(dep) && (tid & 63) == 0) atomicOr(ties + l, 1 << side);
     }
     const double tot = block_np_sum(w + o, K, leaf_sum + o);
     for (int64_t j = tid; j < K; j += kParzenBlock) w[o + j] = w[o + j] / tot;
@@ -1232,8 +1279,16 @@ int history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial,
     return TPE_OK;
 }
 
+// below_h (optional): the below set per trial position, as the caller's
+// np.argsort of the losses picks it (tpe.py:637); order_off / order
+// (optional): per label, the order of its above observations (np.argsort,
+// tpe.py:433; empty range = the device's position order); ties_out
+// (optional, n_labels + 1): which mixtures depend on a tie order the caller
+// did not supply (k_parzen, k_split).
 int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t n_valid,
-                   double gamma, double prior_weight, int32_t lf, int32_t* n_below_out) {
+                   double gamma, double prior_weight, int32_t lf, int32_t* n_below_out,
+                   const uint8_t* below_h = nullptr, const int64_t* order_off_h = nullptr,
+                   const int32_t* order_h = nullptr, int32_t* ties_out = nullptr) {
     auto& B = ctx->build;
     if (!B.hist_ready) return ctx->fail(TPE_ERR_ARG, "no resident history (tpe_history_reset)");
     if (lf < 1 || lf >= kMaxLF) return ctx->fail(TPE_ERR_ARG, "linear forgetting must be in [1, 63]");
@@ -1249,6 +1304,15 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     // n_below = min(ceil(gamma sqrt(len(l_vals))), gamma_cap)   tpe.py:636
     const double nbd = std::ceil(gamma * std::sqrt((double)n_valid));
     const int32_t n_below = (int32_t)std::min<double>(nbd, (double)lf);
+    if (below_h) {   // a supplied below set: n_below trials, each with a loss
+        int64_t nb = 0;
+        for (int64_t t = 0; t < n_trials; ++t)
+            if (below_h[t]) {
+                if (!(losses[t] == losses[t])) return ctx->fail(TPE_ERR_ARG, "below set holds a trial without a loss");
+                ++nb;
+            }
+        if (nb != n_below) return ctx->fail(TPE_ERR_ARG, "below set size differs from n_below");
+    }
 
     // static label fields, mixture / record regions
     std::vector<DLabel> dl(n_labels);
@@ -1304,20 +1368,40 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     HIPCHK(ctx, P.comps32.reserve(total));
     HIPCHK(ctx, P.samp.reserve(samp_total));
     HIPCHK(ctx, ctx->errflag.reserve(1));
+    HIPCHK(ctx, B.ties.reserve(n_labels + 1));
+    HIPCHK(ctx, hipMemsetAsync(B.ties.p, 0, (n_labels + 1) * sizeof(int32_t), st));
+    const int64_t* order_off_d = nullptr;
+    const int32_t* order_d = nullptr;
+    if (order_off_h && order_h && order_off_h[n_labels] > 0) {
+        for (int32_t l = 0; l < n_labels; ++l)
+            if (order_off_h[l + 1] < order_off_h[l] || order_off_h[l] < 0)
+                return ctx->fail(TPE_ERR_ARG, "order offsets must not decrease");
+        HIPCHK(ctx, B.order_off.reserve(n_labels + 1));
+        HIPCHK(ctx, B.order.reserve(order_off_h[n_labels]));
+        HIPCHK(ctx, hipMemcpyAsync(B.order_off.p, order_off_h, (n_labels + 1) * sizeof(int64_t),
+                                   hipMemcpyHostToDevice, st));
+        HIPCHK(ctx, hipMemcpyAsync(B.order.p, order_h, order_off_h[n_labels] * sizeof(int32_t),
+                                   hipMemcpyHostToDevice, st));
+        order_off_d = B.order_off.p;
+        order_d = B.order.p;
+    }
     if (T > 0) HIPCHK(ctx, hipMemcpyAsync(B.losses.p, losses, T * sizeof(double), hipMemcpyHostToDevice, st));
+    if (T > 0 && below_h) HIPCHK(ctx, hipMemcpyAsync(B.below.p, below_h, T, hipMemcpyHostToDevice, st));
     HIPCHK(ctx, hipMemcpyAsync(B.mix_off.p, mix.data(), mix.size() * sizeof(int64_t), hipMemcpyHostToDevice, st));
     HIPCHK(ctx, hipMemcpyAsync(P.labels.p, dl.data(), n_labels * sizeof(DLabel), hipMemcpyHostToDevice, st));
     HIPCHK(ctx, hipMemsetAsync(ctx->errflag.p, 0, sizeof(int32_t), st));
 
     HIPCHK(ctx, hipEventRecord(ctx->ev0, st));
-    if (T > 0)
-        hipLaunchKernelGGL(k_split, dim3(1), dim3(kSplitBlock), 0, st, B.losses.p, T, n_below, B.below.p);
+    if (T > 0 && !below_h)
+        hipLaunchKernelGGL(k_split, dim3(1), dim3(kSplitBlock), 0, st, B.losses.p, T, n_below, B.below.p,
+                           B.ties.p + n_labels);
     hipLaunchKernelGGL(k_partition, dim3(n_labels), dim3(kPartBlock), 0, st, B.specs.p, B.p_off.p, B.cnt.p,
                        B.p_trial.p, B.p_val.p, B.s_key.p, B.s_idx.p, B.below.p, B.losses.p, T,
                        B.below_val.p, B.arank.p, B.keys.p, B.idx.p, B.counts.p, ctx->errflag.p);
     hipLaunchKernelGGL(k_parzen, dim3(n_labels, 2), dim3(kParzenBlock), 0, st, B.specs.p, B.cat_p.p,
                        B.p_off.p, B.counts.p, B.below_val.p, B.keys.p, B.keys.p, B.idx.p, B.mix_off.p,
-                       prior_weight, lf, B.w.p, B.mu.p, B.sigma.p, B.kcount.p, B.scratch.p + total);
+                       prior_weight, lf, B.w.p, B.mu.p, B.sigma.p, B.kcount.p, B.scratch.p + total, order_off_d,
+                       order_d, B.ties.p, ctx->errflag.p);
     hipLaunchKernelGGL(k_fold_terms, dim3((unsigned)((max_cap + kTermBlock - 1) / kTermBlock), n_labels, 2),
                        dim3(kTermBlock), 0, st, P.labels.p, B.kcount.p, B.mix_off.p, B.w.p, B.mu.p,
                        B.sigma.p, B.scratch.p, B.scratch.p + 2 * total, B.scratch.p + 3 * total);
@@ -1330,11 +1414,14 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     int32_t errh = 0;
     HIPCHK(ctx, hipMemcpyAsync(dl.data(), P.labels.p, n_labels * sizeof(DLabel), hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipMemcpyAsync(&errh, ctx->errflag.p, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    if (ties_out)
+        HIPCHK(ctx, hipMemcpyAsync(ties_out, B.ties.p, (n_labels + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
     HIPCHK(ctx, hipEventElapsedTime(&ctx->build_ms, ctx->ev0, ctx->ev1));
     if (errh & 1) return ctx->fail(TPE_ERR_ARG, "observation trial position out of range");
     if (errh & 2) return ctx->fail(TPE_ERR_ARG, "more below observations than the below set (duplicate trial in a label?)");
     if (errh & 4) return ctx->fail(TPE_ERR_VALUE, "below weights sum to zero");
+    if (errh & 8) return ctx->fail(TPE_ERR_ARG, "supplied observation order does not fit the above set");
 
     std::vector<int32_t> cat;
     for (int m = 0; m < kNumModes; ++m) {
@@ -1379,6 +1466,15 @@ TPE_DEV int tpe1_build_posterior_resident(tpe_ctx* ctx, const double* losses, in
                                  int32_t* n_below_out) {
     if (!ctx) return TPE_ERR_ARG;
     return build_resident(ctx, losses, n_trials, n_valid, gamma, prior_weight, lf, n_below_out);
+}
+
+TPE_DEV int tpe1_build_posterior_resident_ordered(tpe_ctx* ctx, const double* losses, int64_t n_trials,
+                                                  int64_t n_valid, double gamma, double prior_weight,
+                                                  int32_t lf, const uint8_t* below, const int64_t* order_off,
+                                                  const int32_t* order, int32_t* n_below_out, int32_t* ties) {
+    if (!ctx) return TPE_ERR_ARG;
+    return build_resident(ctx, losses, n_trials, n_valid, gamma, prior_weight, lf, n_below_out, below,
+                          order_off, order, ties);
 }
 
 TPE_DEV int tpe1_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,

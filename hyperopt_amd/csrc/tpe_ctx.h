@@ -164,6 +164,9 @@ struct BuildBufs {
     DevBuf<double> w, mu, sigma;   // the built mixtures (tpe_get_mixture)
     DevBuf<int64_t> mix_off;       // per label: below / above offsets into w/mu/sigma
     DevBuf<double> scratch;        // per-component terms | pairwise leaf sums
+    DevBuf<int32_t> ties;          // per label: mixtures that depend on a tie order; [L]: split tie
+    DevBuf<int64_t> order_off;     // supplied np.argsort orders of the above observations
+    DevBuf<int32_t> order;
     int32_t n_labels = 0;          // labels of the last build (0: none resident)
     std::vector<int64_t> mix_h;    // host copy of mix_off
     void release() {
@@ -174,7 +177,8 @@ struct BuildBufs {
         seg_end.release(); sort_tmp.release(); gs_a.release(); gs_b.release(); gs_lab.release();
         gs_lab2.release(); losses.release(); below.release(); keys.release();
         idx.release(); below_val.release(); counts.release(); kcount.release(); w.release();
-        mu.release(); sigma.release(); mix_off.release(); scratch.release();
+        mu.release(); sigma.release(); mix_off.release(); scratch.release(); ties.release();
+        order_off.release(); order.release();
         n_labels = 0;
         hist_ready = false;
         pool_cap = 0;
@@ -237,12 +241,11 @@ struct tpe_ctx {
     DevBuf<double> xs, slice_part;       // split-K map: candidates, slice sums
     bool splitk = true;                  // split-K for small sampled rounds
     DevBuf<double> chunk_part;           // chunked packed map: x | below sum | above chunk sums
-    int32_t chunks_forced = 0;           // TPE_CHUNKS: 1 = off, > 1 = fixed, 0 = auto
-    bool pack_wide = false;              // TPE_PACK_WIDE: packed rounds over kR slots per thread
+    int32_t chunks_forced = 0;           // TPE_OPT_CHUNKS: 1 = off, > 1 = fixed, 0 = auto
     // fp32 screen of the fp64 round (sampled tile-map rounds, TPE_F64): per
     // candidate an upper bound of its score, per (round, label) the largest
     // lower bound and the compacted candidates that can still win
-    bool screen = true;                  // TPE_NO_SCREEN=1 / TPE_OPT_SCREEN
+    bool screen = true;                  // TPE_OPT_SCREEN
     DevBuf<float> scr_hi;
     DevBuf<double> scr_hid;              // expansion screen: fp64 upper bounds
     DevBuf<double2> bx_lohi;             //   packed map: fp64 (lower, upper) per candidate
@@ -397,6 +400,10 @@ TPE_DEV int tpe1_history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_
 TPE_DEV int tpe1_build_posterior_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials,
                                           int64_t n_valid, double gamma, double prior_weight,
                                           int32_t lf, int32_t* n_below_out);
+TPE_DEV int tpe1_build_posterior_resident_ordered(tpe_ctx* ctx, const double* losses, int64_t n_trials,
+                                                  int64_t n_valid, double gamma, double prior_weight,
+                                                  int32_t lf, const uint8_t* below, const int64_t* order_off,
+                                                  const int32_t* order, int32_t* n_below_out, int32_t* ties);
 TPE_DEV int tpe1_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
                                  const double* cat_p, int64_t n_cat_p, const double* losses,
                                  int64_t n_trials, const int64_t* obs_off, const int32_t* obs_trial,

@@ -240,9 +240,6 @@ __device__ __forceinline__ double bm_neglog(double u) {
 }
 
 __device__ __forceinline__ double box_muller(const U4& r, double mu, double sg) {
-#ifdef TPE_EXP_BM_CHEAP   // timing experiments only: not a normal draw
-    return fma(sg, (double)(int32_t)r.w * 0x1.0p-29, mu);
-#endif
     const double u1 = u01_open0(r.y, r.z);
     const double rad = __builtin_amdgcn_sqrt(fmax(0.0, 2.0 * bm_neglog(u1)));
     const double nrm = rad * cos_turn32(r.w);
@@ -306,11 +303,7 @@ __device__ __forceinline__ bool sample_slots(const DLabel& L, const Src& src, ui
                                              double (&out)[R]) {
     static_assert(MODE != CAT, "categorical slots draw once each");
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-#ifdef TPE_EXP_NO_REJECT   // timing experiments only: no truncation
-    const bool bounded = false;
-#else
     const bool bounded = (L.flags & 3) == 3;
-#endif
     const uint32_t mask0 = pend;
     bool ok = true;
     // attempt 0 of every pending slot, straight-line; the queue below takes

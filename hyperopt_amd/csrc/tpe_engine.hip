@@ -2610,30 +2610,16 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                     ctx->hot_tau0_gen = ctx->hot == 2 ? 0 : P.bx_gen;
                     ctx->hot_tau0_n = a.n;
                 }
-                static const int hot_r = [] {   // experiments: TPE_HOT_R=4|8
-                    const char* e = getenv("TPE_HOT_R");
-                    const int v = e ? atoi(e) : kHotR;
-                    return v == 4 || v == 8 ? v : kHotR;
-                }();
-                // ~kHotWgs workgroups over the round (tiles strided), at most one per tile
-                static const int64_t hot_wgs = [] {   // experiments: TPE_HOT_WGS
-                    const char* e = getenv("TPE_HOT_WGS");
-                    const long v = e ? atol(e) : 0;
-                    return v >= 256 ? (int64_t)v : kHotWgs;
-                }();
                 const int64_t cells_l = (int64_t)nl * a.gz;
-#define TPE_HOT_LAUNCH(RR)                                                                                  \
-    hipLaunchKernelGGL((k_hot_bx<RR>),                                                                   \
-                       dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((a.n + RR * kBlock - 1) /      \
-                                                                                (RR * kBlock),            \
-                                                                             hot_wgs / cells_l)),         \
-                            nl, a.gz),                                                                    \
-                       dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.samp.p, P.bx.p, ctx->hot_bits.p,    \
-                       a.n, a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->hot_cnt.p, ctx->hot_i.p,         \
-                       ctx->hot_x.p, ctx->errflag.p)
-                if (hot_r == 4) TPE_HOT_LAUNCH(4);
-                else TPE_HOT_LAUNCH(8);
-#undef TPE_HOT_LAUNCH
+                // ~kHotWgs workgroups over the round (tiles strided), at most one per tile
+                hipLaunchKernelGGL((k_hot_bx<kHotR>),
+                                   dim3((unsigned)std::max<int64_t>(
+                                            1, std::min<int64_t>((a.n + kHotR * kBlock - 1) / (kHotR * kBlock),
+                                                                 kHotWgs / cells_l)),
+                                        nl, a.gz),
+                                   dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.samp.p, P.bx.p, ctx->hot_bits.p,
+                                   a.n, a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->hot_cnt.p, ctx->hot_i.p,
+                                   ctx->hot_x.p, ctx->errflag.p);
                 const unsigned bgx = (unsigned)((a.n + kBxR * kBlock - 1) / (kBxR * kBlock));
                 hipLaunchKernelGGL((k_screen_hot<kBxR>), dim3(std::min(bgx, kHotScreenWgs), nl, a.gz), dim3(kBlock),
                                    0, ctx->stream, P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p, P.bx_loff.p,
@@ -3102,7 +3088,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     int32_t tiles;
     uint32_t gx, gz;
     if (n > 0 && n < kTile) {
-        const int per_block = (n <= kBlock * kRGroup && !ctx->pack_wide) ? kBlock * kRGroup : kTile;
+        const int per_block = n <= kBlock * kRGroup ? kBlock * kRGroup : kTile;
         S.cpack = (int32_t)n;
         S.rpb = per_block / (int32_t)n;
         tiles = 1;
@@ -3236,11 +3222,6 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
             const DLabel& d = ctx->P->h_labels[y < gg.size() ? gg[y] : gl[y - gg.size()]];
             ctx->screen_rescored += cnt;
             ctx->screen_rescore_terms += (int64_t)cnt * (d.nb + d.na);
-        }
-        if (getenv("TPE_SCREEN_DEBUG")) {
-            fprintf(stderr, "screen counts:");
-            for (int32_t c : ctx->scr_cnt_h) fprintf(stderr, " %d", c);
-            fprintf(stderr, "\n");
         }
         ctx->screen_pending = false;
         if (ctx->timing && ctx->evw_used > 0) {   // windowed tile rounds: the units' k_screen_win
@@ -3489,16 +3470,6 @@ int tpe_ctx_create(int device, int precision, tpe_ctx** out) {
         tpe_ctx_destroy(c);
         return TPE_ERR_HIP;
     }
-    const char* dd = getenv("TPE_NO_DEDUP");
-    c->dedup = !(dd && dd[0] == '1');
-    const char* sk = getenv("TPE_NO_SPLITK");   // tests: force the packed map
-    c->splitk = !(sk && sk[0] == '1');
-    const char* ch = getenv("TPE_CHUNKS");      // tests / experiments: chunking of the packed map
-    c->chunks_forced = ch ? std::max(1, atoi(ch)) : 0;
-    const char* pw = getenv("TPE_PACK_WIDE");   // experiments: kR slots per thread when packed
-    c->pack_wide = pw && pw[0] == '1';
-    const char* ns = getenv("TPE_NO_SCREEN");   // tests / experiments: unscreened fp64 rounds
-    c->screen = !(ns && ns[0] == '1');
     *out = c;
     return TPE_OK;
 }

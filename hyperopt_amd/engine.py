@@ -126,17 +126,30 @@ class Engine(object):
         self.n_labels = len(descs)
 
     def build_posterior(self, specs, cat_p, losses, obs_off, obs_trial, obs_val, gamma,
-                        prior_weight, lf=25):
-        """Device posterior build from the history (tpe_build_posterior):
-        specs is a SPEC_DTYPE array, observations in CSR form (obs_off per
-        label; obs_trial = position in `losses`, -1 for none; obs_val already
-        transformed).  Returns n_below."""
+                        prior_weight, lf=25, tie_order='reference'):
+        """Device posterior build from the history: specs is a SPEC_DTYPE
+        array, observations in CSR form (obs_off per label; obs_trial =
+        position in `losses`, -1 for none; obs_val already transformed).
+        tie_order 'reference' (default): reset + append + the ordered build,
+        with numpy's np.argsort order wherever a mixture depends on the order
+        of ties (posterior.build_reference_order); 'position': one
+        tpe_build_posterior call, ties by position.  Returns n_below."""
+        from . import posterior as _post
         specs = np.ascontiguousarray(specs, dtype=SPEC_DTYPE)
         cat_p = _f64(cat_p)
         losses = _f64(losses)
         obs_off = np.ascontiguousarray(obs_off, dtype=np.int64)
         obs_trial = np.ascontiguousarray(obs_trial, dtype=np.int32)
         obs_val = _f64(obs_val)
+        if tie_order == 'reference':
+            self.history_reset(specs, cat_p)
+            self.history_append(np.diff(obs_off), obs_trial, obs_val)
+            n_valid = int(np.count_nonzero(losses == losses))
+            nb, self.tie_labels = _post.build_reference_order(
+                self, losses, n_valid, gamma, prior_weight, lf, _post._ObsOf(obs_off, obs_trial, obs_val))
+            return nb
+        if tie_order != 'position':
+            raise ValueError("tie_order must be 'reference' or 'position'")
         nb = ctypes.c_int32()
         self.history_generation += 1      # tpe_build_posterior resets the resident history
         self._check(self.lib.tpe_build_posterior(
@@ -174,6 +187,34 @@ class Engine(object):
             int(lf), ctypes.byref(nb)))
         self.n_labels = self.hist_labels
         return nb.value
+
+    def build_posterior_ordered(self, losses, n_valid, gamma, prior_weight, lf=25, below=None,
+                                order_off=None, order=None):
+        """build_posterior_resident with the reference's tie order where the
+        caller supplies it (tpe_build_posterior_resident_ordered): `below` a
+        uint8 mask per trial position, `order_off` / `order` per label the
+        np.argsort of its above observations.  Returns (n_below, ties):
+        ties[l] bit 1 (bit 0) when label l's above (below) mixture depends on
+        a tie order that was not supplied, ties[-1] when equal losses
+        straddle the split."""
+        losses = _f64(losses)
+        L_ = self.hist_labels
+        if below is not None:
+            below = np.ascontiguousarray(below, dtype=np.uint8)
+            if len(below) != len(losses):
+                raise ValueError('below mask must cover every trial position')
+        if order_off is not None:
+            order_off = np.ascontiguousarray(order_off, dtype=np.int64)
+            order = np.ascontiguousarray(order, dtype=np.int32)
+            if len(order_off) != L_ + 1 or order_off[-1] != len(order):
+                raise ValueError('order offsets must be n_labels + 1 long and end at len(order)')
+        nb = ctypes.c_int32()
+        ties = np.zeros(L_ + 1, dtype=np.int32)
+        self._check(self.lib.tpe_build_posterior_resident_ordered(
+            self.h, _ptr(losses), len(losses), int(n_valid), float(gamma), float(prior_weight),
+            int(lf), _ptr(below), _ptr(order_off), _ptr(order), ctypes.byref(nb), _ptr(ties)))
+        self.n_labels = self.hist_labels
+        return nb.value, ties
 
     def get_mixture(self, label, side):
         """(weights, mus, sigmas) of a built mixture (side 0 below, 1 above)."""

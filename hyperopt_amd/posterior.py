@@ -237,6 +237,104 @@ def spec_table(labels):
     return specs, (np.concatenate(cat_p) if cat_p else np.zeros(0)), trs
 
 
+def n_below_of(n_valid, gamma, lf=DEFAULT_LF):
+    """min(ceil(gamma sqrt(len(l_vals))), gamma_cap), tpe.py:636."""
+    return int(min(np.ceil(gamma * np.sqrt(n_valid)), lf))
+
+
+def reference_orders(losses, n_below, obs_of, labels):
+    """The reference's own np.argsort orders, for the device builder's
+    `tpe_build_posterior_resident_ordered`: the below set as
+    ap_filter_trials picks it (`l_order = np.argsort(l_vals)`, tpe.py:637;
+    l_vals = the losses of the trials that have one, in tid order) and, for
+    each label in `labels`, np.argsort of its above observations in
+    observation order (adaptive_parzen_normal's `order = np.argsort(mus)`,
+    tpe.py:433) -- numpy's unstable sort on the same arrays, so equal keys
+    land where the reference puts them.  obs_of(l) -> (trial position per
+    observation, -1 for none; transformed value); obs_of.n_labels = L.
+    Returns (below mask per trial position, order_off[L + 1], order), with
+    empty ranges for the labels not in `labels`."""
+    losses = np.asarray(losses, dtype=np.float64)
+    T = len(losses)
+    valid = np.flatnonzero(losses == losses)
+    lv = losses[valid]
+    below = np.zeros(T, dtype=np.uint8)
+    if 0 < n_below < len(lv):
+        # the n_below smallest: unique when the boundary values differ (an
+        # O(N) partition); a tie across the boundary takes np.argsort's pick
+        part = np.partition(lv, (n_below - 1, n_below))
+        if part[n_below - 1] < part[n_below]:
+            below[valid[lv <= part[n_below - 1]]] = 1
+        else:
+            below[valid[np.argsort(lv)[:n_below]]] = 1      # tpe.py:637
+    elif n_below > 0:
+        below[valid] = 1
+    n_labels = obs_of.n_labels
+    off = np.zeros(n_labels + 1, dtype=np.int64)
+    parts = []
+    for l in range(n_labels):
+        if l in labels:
+            pos, val = obs_of(l)
+            pos = np.asarray(pos, dtype=np.int64)
+            ok = (pos >= 0) & (pos < T)
+            p = pos[ok]
+            keep = (losses[p] == losses[p]) & (below[p] == 0)   # tpe.py:645-646
+            mus = np.asarray(val, dtype=np.float64)[ok][keep]
+            o = np.argsort(mus).astype(np.int32)                # tpe.py:433
+            parts.append(o)
+            off[l + 1] = off[l] + len(o)
+        else:
+            off[l + 1] = off[l]
+    order = np.concatenate(parts) if parts else np.zeros(0, dtype=np.int32)
+    return below, off, order
+
+
+def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of, known=()):
+    """Device build whose mixtures follow the reference's tie order
+    (tpe.py:433, 637): the device reports which mixtures depend on the order
+    of tied observations (or a tie of losses at the split), and only for
+    those the host computes numpy's own np.argsort and the build runs again
+    with it.  `known`: labels that needed an order in the previous build of
+    this history (their orders are supplied up front, saving the second
+    build).  Returns (n_below, the labels that needed an order)."""
+    n_below = n_below_of(n_valid, gamma, lf)
+    known = set(known)
+    if known:
+        below, off, order = reference_orders(losses, n_below, obs_of, known)
+        nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf, below, off, order)
+    else:
+        nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf)
+    if np.any(ties[:-1] & 1):
+        # a below mixture holds at most gamma_cap <= lf observations: its
+        # weights are all equal, so its order can never matter
+        raise AssertionError('below mixture depends on a tie order (n_below > lf?)')
+    need = known | set(np.flatnonzero(ties[:-1] & 2).tolist())
+    if need != known or ties[-1]:
+        below, off, order = reference_orders(losses, n_below, obs_of, need)
+        nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf, below, off, order)
+        if np.any(ties[:-1]):
+            # a supplied below set can move observations between the sets,
+            # creating a dependent label the first pass did not see
+            need |= set(np.flatnonzero(ties[:-1] & 2).tolist())
+            below, off, order = reference_orders(losses, n_below, obs_of, need)
+            nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf, below, off,
+                                                   order)
+            assert not np.any(ties[:-1])
+    return nb, frozenset(need)
+
+
+class _ObsOf(object):
+    """obs_of(l) over CSR observation arrays (tpe_build_posterior's layout)."""
+
+    def __init__(self, obs_off, obs_trial, obs_val):
+        self.off, self.trial, self.val = obs_off, obs_trial, obs_val
+        self.n_labels = len(obs_off) - 1
+
+    def __call__(self, l):
+        a, b = int(self.off[l]), int(self.off[l + 1])
+        return self.trial[a:b], self.val[a:b]
+
+
 class NonFiniteObservation(ValueError):
     """A transformed observation is NaN (e.g. the log of a non-positive value
     of a log-scale label inserted through points_to_evaluate).  The
@@ -275,6 +373,9 @@ class DeviceHistoryUploader(object):
             specs, cat_p, self.trs = spec_table(labels)
             eng.history_reset(specs, cat_p)
             self.prev_counts = [0] * len(labels)
+            self.pos_parts = [[] for _ in labels]    # what the device holds, per label
+            self.val_parts = [[] for _ in labels]
+            self.tie_labels = frozenset()
         counts = list(self.prev_counts)
         n_new, trial_parts, val_parts = [], [], []
         for i, (name, _, _) in enumerate(labels):
@@ -292,6 +393,8 @@ class DeviceHistoryUploader(object):
                 pos = np.where(tids[pc] == ni, pc, -1)
                 trial_parts.append(pos.astype(np.int32))
                 val_parts.append(nv)
+                self.pos_parts[i].append(trial_parts[-1])
+                self.val_parts[i].append(nv)
             n_new.append(len(ni))
             counts[i] = len(oi)
         if sum(n_new):
@@ -302,9 +405,24 @@ class DeviceHistoryUploader(object):
         self.owner = weakref.ref(owner)
         self.n_trials = len(tids)
         self.last_tid = tids[-1] if len(tids) else None
-        return eng.build_posterior_resident(losses, n_valid, gamma, prior_weight, lf)
+        nb, self.tie_labels = build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf,
+                                                    self._obs_of(len(labels)), self.tie_labels)
+        return nb
+
+    def _obs_of(self, n_labels):
+        def obs_of(l):
+            for parts in (self.pos_parts, self.val_parts):
+                if len(parts[l]) > 1:
+                    parts[l][:] = [np.concatenate(parts[l])]
+            if not self.pos_parts[l]:
+                return np.zeros(0, np.int32), np.zeros(0)
+            return self.pos_parts[l][0], self.val_parts[l][0]
+        obs_of.n_labels = n_labels
+        return obs_of
 
     prev_counts = ()
+    pos_parts = val_parts = ()
+    tie_labels = frozenset()
     n_trials = 0
     last_tid = None
     trs = ()

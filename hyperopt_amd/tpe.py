@@ -206,14 +206,6 @@ def suggest(new_ids, domain, trials, seed,
               n_EI_candidates=n_EI_candidates, gamma=gamma, linear_forgetting=linear_forgetting,
               precision=precision, device=device, posterior_builder=posterior_builder,
               devices=devices)
-    if batch == 'pending' and len(new_ids) > 1:
-        view = _PendingView(trials)
-        rval = []
-        for new_id in new_ids:
-            docs = suggest([new_id], domain, view, seed, batch=False, **kw)
-            view.trials.extend(docs)
-            rval.extend(docs)
-        return rval
     specs = specs_of(domain)
     labels = list(specs)
     # the device-resident history's view of the trials (None when the fast
@@ -225,6 +217,23 @@ def suggest(new_ids, domain, trials, seed,
     else:
         gathered = _history.gather(domain, trials, labels)
         n_docs = len(gathered[0])
+    if batch == 'pending' and len(new_ids) > 1:
+        # the calls that would still see fewer than n_startup_jobs documents
+        # are the startup phase: one rand.suggest over their ids, as the
+        # reference answers a startup batch (tpe.py:869-871; distinct draws
+        # from one RandomState(seed), the documents batch=True returns) --
+        # then one TPE call per remaining id, each seeing the earlier ones
+        # as pending trials
+        k = max(0, min(len(new_ids), n_startup_jobs - n_docs))
+        rval = list(rand.suggest(list(new_ids[:k]), domain, trials, seed)) if k else []
+        if k < len(new_ids):
+            pview = _PendingView(trials)
+            pview.trials.extend(rval)
+            for new_id in new_ids[k:]:
+                docs = suggest([new_id], domain, pview, seed, batch=False, **kw)
+                pview.trials.extend(docs)
+                rval.extend(docs)
+        return rval
     if n_docs < n_startup_jobs:
         return rand.suggest(new_ids, domain, trials, seed)      # tpe.py:869-871
     if n_docs == 0:

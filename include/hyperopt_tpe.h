@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 2
+#define TPE_ABI_VERSION 3
 
 /* error codes; the Python layer maps them to the reference's exception types */
 #define TPE_OK 0
@@ -208,7 +208,9 @@ int tpe_set_posterior(tpe_ctx *ctx, const tpe_label_desc *labels, int32_t n_labe
  * The below set is the n_below = min(ceil(gamma sqrt(n_trials)), lf) lowest
  * losses; equal losses and equal observations are ordered by position
  * (a stable sort; the reference's np.argsort order for ties is numpy's
- * unstable quicksort).  n_below_out (may be NULL) receives n_below. */
+ * unstable quicksort -- tpe_build_posterior_resident_ordered takes the
+ * reference's order where it matters).  n_below_out (may be NULL) receives
+ * n_below. */
 int tpe_build_posterior(tpe_ctx *ctx, const tpe_label_spec *specs, int32_t n_labels,
                         const double *cat_p, int64_t n_cat_p,
                         const double *losses, int64_t n_trials,
@@ -234,6 +236,31 @@ int tpe_history_append(tpe_ctx *ctx, const int64_t *n_new, const int32_t *obs_tr
 int tpe_build_posterior_resident(tpe_ctx *ctx, const double *losses, int64_t n_trials,
                                  int64_t n_valid, double gamma, double prior_weight,
                                  int32_t lf, int32_t *n_below_out);
+
+/* tpe_build_posterior_resident with the reference's tie order (ap_filter_trials
+ * tpe.py:637 `l_order = np.argsort(l_vals)` and adaptive_parzen_normal
+ * tpe.py:433 `order = np.argsort(mus)`: numpy's unstable sort, whose order of
+ * equal keys the device cannot reproduce, so the caller computes it with
+ * numpy itself when it matters):
+ *   below (NULL: the device split, ties by position): per trial position
+ *       1 if the trial is in the below set -- exactly n_below trials, each
+ *       with a loss;
+ *   order_off[n_labels + 1], order (NULL: none supplied): label l's entries
+ *       order[order_off[l] .. order_off[l+1]) are np.argsort of its above
+ *       observations (in observation order) -- the above list's indices in
+ *       value order; an empty range keeps the device's position order;
+ *   ties (may be NULL; n_labels + 1 entries) receives what depends on a tie
+ *       order the caller did not supply: ties[l] bit 1 (bit 0) when label l's
+ *       above (below) mixture has equal mus while its linear-forgetting
+ *       weights differ (the tie order decides which weight meets a run end's
+ *       sigma, and the order of the normalising sum); ties[n_labels] = 1
+ *       when equal losses straddle the n_below boundary of the split.
+ * A caller that gets a non-zero flag computes the reference's order for it
+ * and builds again (hyperopt_amd/posterior.py reference_orders). */
+int tpe_build_posterior_resident_ordered(tpe_ctx *ctx, const double *losses, int64_t n_trials,
+                                         int64_t n_valid, double gamma, double prior_weight,
+                                         int32_t lf, const uint8_t *below, const int64_t *order_off,
+                                         const int32_t *order, int32_t *n_below_out, int32_t *ties);
 
 /* Read back one mixture of the resident posterior built by
  * tpe_build_posterior (side 0 below, 1 above): the (weights, mus, sigmas)

@@ -18,7 +18,7 @@ def test_library_built_and_exports_header():
     for name in declared:
         assert hasattr(lib, name), name
         assert name in L.SIGNATURES, 'binding missing for ' + name
-    assert lib.tpe_abi_version() == L.ABI_VERSION == 2
+    assert lib.tpe_abi_version() == L.ABI_VERSION == 3
 
 
 def test_struct_layouts():

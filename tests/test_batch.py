@@ -75,10 +75,36 @@ def test_batch_pending_is_sequential_calls_with_pending_docs(builder):
         seq_trials.refresh()
         seq.extend(d)
     assert _vals(batch) == _vals(seq)
-    # pending docs change the posterior: not all suggestions equal the
-    # batch=True (excluded) ones
+    # the first call sees no pending doc: it equals the batch=True one
     excl = tpe.suggest(ids, dom, trials, 5, batch=True, posterior_builder=builder)
     assert _vals(excl)[0] == _vals(batch)[0]
+    # later calls see the earlier suggestions: with the first one inserted
+    # (pending, loss +inf) every label it set has one more above component
+    with_first = copy.deepcopy(trials)
+    with_first.insert_trial_docs(batch[:1])
+    with_first.refresh()
+    _, _, p0 = tpe.build_posteriors(dom, trials)
+    _, _, p1 = tpe.build_posteriors(dom, with_first)
+    set_labels = [k for k, v in batch[0]['misc']['vals'].items() if v]
+    for a, b in zip(p0, p1):
+        if a.label in set_labels and a.family != 'categorical':
+            assert len(b.above[0]) == len(a.above[0]) + 1, a.label
+
+
+def test_batch_pending_startup_phase_draws_distinct_documents():
+    """a 'pending' batch that starts in the startup phase gets the
+    reference's rand.suggest(new_ids) documents (one RandomState(seed) over
+    the ids: distinct draws), the documents batch=True returns -- not one
+    identically seeded rand.suggest per id.  No GPU needed: every call stays
+    in the startup phase."""
+    trials = _history(5, 6)
+    dom = H.Domain(_loss, SPACE)
+    ids = [40, 41, 42, 43]
+    pend = tpe.suggest(ids, dom, trials, 8, batch='pending')
+    both = tpe.suggest(ids, dom, trials, 8, batch=True)
+    assert _vals(pend) == _vals(both)
+    a_vals = [d['misc']['vals']['a'][0] for d in pend]
+    assert len(set(a_vals)) == len(a_vals)
 
 
 @pytest.mark.gpu

@@ -2,12 +2,14 @@
 against the CPU oracle's restatement of ap_filter_trials + adaptive_parzen_normal
 + the categorical pseudocount posteriors (tpe.py:385-477, 581-648).
 
-Bar: the built (weights, mus, sigmas) are BIT-IDENTICAL to the oracle's with
-stable tie order (sort_kind='stable'; the device orders tied losses / tied
-observations by position, the reference's np.argsort leaves that to numpy's
-unstable quicksort), and identical to the default-order oracle on tie-free
-histories.  The folded records are checked through a full suggestion round
-against the same mixtures uploaded with tpe_set_posterior (host fold)."""
+Bar: the built (weights, mus, sigmas) are BIT-IDENTICAL to the oracle's in
+the reference's own tie order (np.argsort's, sort_kind=None): the device
+flags the mixtures that depend on the order of tied observations / losses and
+the host supplies numpy's order for those (posterior.build_reference_order).
+The position-order build (one tpe_build_posterior call, tie_order='position')
+is bit-identical to the stable-order oracle (sort_kind='stable').  The folded
+records are checked through a full suggestion round against the same
+mixtures uploaded with tpe_set_posterior (host fold)."""
 import numpy as np
 import pytest
 
@@ -53,7 +55,7 @@ def make_history(labels, n_trials, seed, active_frac=1.0, loss_round=None, orpha
     return History(labels, tids, losses, obs)
 
 
-def oracle_mixtures(hist, gamma=0.25, pw=1.0, sort_kind='stable'):
+def oracle_mixtures(hist, gamma=0.25, pw=1.0, sort_kind=None):
     out = []
     for name, kind, args in hist.labels:
         oi, ov = hist.obs[name]
@@ -74,8 +76,8 @@ def eng():
     e.close()
 
 
-def _build(eng, hist, gamma=0.25, pw=1.0):
-    return eng.build_posterior(*hist.device_inputs(), gamma=gamma, prior_weight=pw)
+def _build(eng, hist, gamma=0.25, pw=1.0, tie_order='reference'):
+    return eng.build_posterior(*hist.device_inputs(), gamma=gamma, prior_weight=pw, tie_order=tie_order)
 
 
 def _check_bit_exact(eng, hist, want):
@@ -120,6 +122,16 @@ def test_build_conditional_ties_orphans(eng):
     a loss entry (dropped from both sets, tpe.py:639-646)."""
     hist = make_history(ALL_KINDS, 1500, seed=7, active_frac=0.4, loss_round=1, orphan=17)
     _build(eng, hist)
+    _check_bit_exact(eng, hist, oracle_mixtures(hist))
+    assert eng.tie_labels                      # tied quantized labels took numpy's order
+
+
+@pytest.mark.parametrize('n_trials', [200, 3000])
+def test_build_position_order_is_stable_order(eng, n_trials):
+    """tie_order='position' (tpe_build_posterior alone): ties by position,
+    bit-identical to the stable-order oracle."""
+    hist = make_history(ALL_KINDS, n_trials, seed=n_trials, loss_round=1)
+    _build(eng, hist, tie_order='position')
     _check_bit_exact(eng, hist, oracle_mixtures(hist, sort_kind='stable'))
 
 
@@ -205,6 +217,11 @@ def test_resident_history_incremental(eng):
     specs, cat_p, trs = P.spec_table(hist.labels)
     eng.history_reset(specs, cat_p)
     counts = [0] * len(hist.labels)
+    held = [[np.zeros(0, np.int32), np.zeros(0)] for _ in hist.labels]
+
+    def obs_of(l):
+        return held[l][0], held[l][1]
+    obs_of.n_labels = len(hist.labels)
     for cut in (30, 31, 400, 1999, 2400):
         n_new, tr_parts, val_parts = [], [], []
         for i, (name, kind, args) in enumerate(hist.labels):
@@ -216,16 +233,21 @@ def test_resident_history_incremental(eng):
                 nv = trs[i](nv)
             tr_parts.append(np.searchsorted(hist.tids, ni).astype(np.int32))
             val_parts.append(np.asarray(nv, dtype=float))
+            held[i] = [np.concatenate([held[i][0], tr_parts[-1]]), np.concatenate([held[i][1], val_parts[-1]])]
             n_new.append(len(ni))
             counts[i] = len(oi)
         eng.history_append(np.asarray(n_new), np.concatenate(tr_parts), np.concatenate(val_parts))
         lsub = losses[:cut]
-        eng.build_posterior_resident(lsub, int(np.count_nonzero(lsub == lsub)), 0.25, 1.0)
+        n_valid = int(np.count_nonzero(lsub == lsub))
         ok = lsub == lsub
         from hyperopt_amd.workloads import History
         sub = History(hist.labels, hist.tids[:cut][ok], lsub[ok],
                       {n: hist.obs[n] for n, _, _ in hist.labels})
+        # position order, then the reference's order (the product path)
+        eng.build_posterior_resident(lsub, n_valid, 0.25, 1.0)
         _check_bit_exact(eng, sub, oracle_mixtures(sub, sort_kind='stable'))
+        P.build_reference_order(eng, lsub, n_valid, 0.25, 1.0, 25, obs_of)
+        _check_bit_exact(eng, sub, oracle_mixtures(sub))
 
 
 def test_rebuilds_are_deterministic(eng):
@@ -240,12 +262,13 @@ def test_rebuilds_are_deterministic(eng):
             'loguniform': np.exp(np.linspace(-4.9, 1.9, 257)),
             'quniform': np.arange(0, 101, dtype=float), 'randint': np.arange(5, dtype=float)}
     ref = None
-    specs, cat_p, trs = P.spec_table(hist.labels)
+    specs, cat, losses, off, tr, val = hist.device_inputs()
     for it in range(5):
         if it % 2 == 0:
             _build(eng, hist)
-        else:
-            eng.build_posterior_resident(hist.losses, len(hist.losses), 0.25, 1.0)
+        else:   # the resident history again, with the orders the last build needed
+            P.build_reference_order(eng, losses, len(losses), 0.25, 1.0, 25, P._ObsOf(off, tr, val),
+                                    eng.tie_labels)
         out = []
         for li, (name, kind, _) in enumerate(hist.labels):
             lb, la, _ = eng.score(li, grid[kind])

@@ -149,9 +149,9 @@ def test_splitk_equals_packed_map(eng, monkeypatch):
              if m['variant'] in ('medium', 'plain') and m['n_hist'] in (26, 300, 2000)]
     d, w, m, s = stack_cases(pairs)
     eng.set_posterior(d, w, m, s)
-    monkeypatch.setenv('TPE_NO_SPLITK', '1')
     e2 = Engine(0, 'f64')
     try:
+        e2.set_option('splitk', 0)
         e2.set_posterior(d, w, m, s)
         for C, rounds in ((24, [5]), (24, list(range(40))), (500, [1, 2, 3])):
             a = eng.suggest_batch(77, rounds, C)
@@ -307,7 +307,7 @@ def test_fp32_dense_path(eng32):
 
 def test_quantized_dedup_equals_direct(eng, monkeypatch):
     """The grid-value table path (sampled rounds) picks the same winners as
-    per-candidate evaluation (TPE_NO_DEDUP=1), on quantized labels of all
+    per-candidate evaluation (set_option('dedup', 0)), on quantized labels of all
     four quantized kinds."""
     from hyperopt_amd.engine import Engine
     pairs = [(m, r) for fx, m, r in _all_cases()
@@ -317,8 +317,8 @@ def test_quantized_dedup_equals_direct(eng, monkeypatch):
     eng.set_posterior(d, w, m, s)
     fast = eng.suggest(31, 20000, round=2)
     stats = eng.last_mode_stats()
-    monkeypatch.setenv('TPE_NO_DEDUP', '1')
     slow_eng = Engine(0, 'f64')
+    slow_eng.set_option('dedup', 0)
     slow_eng.set_posterior(d, w, m, s)
     slow = slow_eng.suggest(31, 20000, round=2)
     slow_stats = slow_eng.last_mode_stats()
@@ -335,6 +335,7 @@ def test_quantized_dedup_equals_direct(eng, monkeypatch):
     fast_b = eng.suggest_batch(31, rounds, 24)
     sb = eng.last_mode_stats()
     slow_eng = Engine(0, 'f64')
+    slow_eng.set_option('dedup', 0)
     slow_eng.set_posterior(d, w, m, s)
     slow_b = slow_eng.suggest_batch(31, rounds, 24)
     slow_eng.close()
@@ -397,11 +398,8 @@ def test_single_ops_leave_resident_posterior(eng):
 
 def _chunk_engine(monkeypatch, prec, chunks, hist):
     from hyperopt_amd.engine import Engine
-    if chunks is None:
-        monkeypatch.delenv('TPE_CHUNKS', raising=False)
-    else:
-        monkeypatch.setenv('TPE_CHUNKS', str(chunks))
     e = Engine(0, prec)
+    e.set_option('chunks', 0 if chunks is None else chunks)
     e.build_posterior(*hist.device_inputs(), gamma=0.25, prior_weight=1.0)
     return e
 

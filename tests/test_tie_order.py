@@ -1,67 +1,145 @@
-"""The device builder's tie order at config 3 (ADVICE
-r1): it orders tied observations by position (stable), the reference's
-adaptive_parzen_normal by np.argsort's unstable quicksort (tpe.py:432,
-447-453), so on tied (quantized) labels the linear-forgetting weights can
-land on different slots of a run of equal mus.
+"""The reference's tie order on the device-built posterior.
 
-What that changes, measured on the config-3 history (10k trials, 32 labels,
-quniform labels on an integer grid):
-* the mixtures as functions do not change: per distinct (mu, sigma) the
-  summed weight is the same (to summation rounding) -- inside a run of equal
-  mus every sigma is the clipped minimum, so any weight permutation inside
-  the run gives the same components;
-* the round's winners do not change: identical winners, values and lpdfs
-  (to 1e-12 relative) on identical candidate sets, C = 24 and C = 2^20.
+adaptive_parzen_normal orders the observations with `np.argsort(mus)`
+(tpe.py:433) and ap_filter_trials the losses with `np.argsort(l_vals)`
+(tpe.py:637): numpy's unstable sort, whose placement of equal keys no device
+sort reproduces.  On a quantized label (or any label with repeated values)
+the order of equal mus decides which linear-forgetting weight sits in which
+slot: which weight meets a run end's sigma (the gap to the neighbouring grid
+value) instead of the clipped minimum of the run's inner slots, and the order
+of the normalising np.sum.  On a coarse grid (quniform(0, 10, 1): gap 1,
+clipped minimum 0.1) the mixtures differ as functions.
+
+The device builder flags every mixture that depends on a tie order (k_parzen)
+and every tie of losses across the split (k_split); the host computes numpy's
+own np.argsort for exactly those and the device builds again with it
+(posterior.build_reference_order, tpe_build_posterior_resident_ordered).
+
+Bar: the device mixtures are BIT-IDENTICAL to the host build (posterior.py,
+numpy in the reference's call order) on coarse quantized labels -- quniform,
+qloguniform, qnormal -- at >= 16384 observations, with a tie of losses at the
+split; and tpe.suggest with posterior_builder='auto' (device build past 16384
+observations) proposes the documents posterior_builder='host' proposes.
 """
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
 
+COARSE = [
+    ('qu10', 'quniform', dict(low=0.0, high=10.0, q=1.0)),
+    ('qlu', 'qloguniform', dict(low=0.0, high=float(np.log(40.0)), q=1.0)),
+    ('qn', 'qnormal', dict(mu=0.0, sigma=2.0, q=0.5)),
+    ('qu100', 'quniform', dict(low=0.0, high=100.0, q=1.0)),
+    ('u', 'uniform', dict(low=-5.0, high=5.0)),
+    ('ri', 'randint', dict(upper=4)),
+]
 
-def _groups(w, mu, sg):
-    d = {}
-    for wi, mi, si in zip(w, mu, sg):
-        d[(mi, si)] = d.get((mi, si), 0.0) + wi
-    return d
+
+def coarse_history(n_trials=6000, seed=0, split_tie=True):
+    """6 labels x 6000 trials = 36k observations (>= DEVICE_BUILD_MIN_OBS);
+    losses with a tie straddling the n_below boundary (n_below = 20: 15
+    trials at -6, 10 at -5)."""
+    from hyperopt_amd.workloads import History, prior_draw
+    rng = np.random.RandomState(seed)
+    tids = np.arange(n_trials, dtype=np.int64)
+    obs, loss = {}, 0.1 * rng.normal(size=n_trials)
+    for name, kind, args in COARSE:
+        v = prior_draw(kind, args, rng, n_trials)
+        obs[name] = (tids, v)
+        loss = loss + 0.01 * (v - v.mean()) ** 2 / (v.var() + 1.0)
+    if split_tie:
+        pick = rng.permutation(n_trials)[:25]
+        loss[pick[:15]] = -6.0
+        loss[pick[15:]] = -5.0
+    return History(COARSE, tids, loss, obs)
 
 
-def test_config3_tie_order_changes_nothing_observable():
+def _assert_same(eng, hist, posts):
+    for li, p in enumerate(posts):
+        sides = ((0, p.below), (1, p.above))
+        for side, want in sides:
+            w, m, s = eng.get_mixture(li, side)
+            if p.family == 'categorical':
+                assert np.array_equal(w, want), (p.label, side)
+                continue
+            hw, hm, hs = want
+            assert np.array_equal(m, hm), (p.label, side, 'mus')
+            assert np.array_equal(s, hs), (p.label, side, 'sigmas')
+            assert np.array_equal(w, hw), (p.label, side, 'weights', float(np.max(np.abs(w - hw))))
+
+
+def test_coarse_quantized_mixtures_bit_identical_to_host():
     from hyperopt_amd import posterior as P
     from hyperopt_amd.engine import Engine
-    from hyperopt_amd.workloads import mixed_history
-    hist = mixed_history(32, 10000, seed=0)
-    host_posts = hist.posteriors()
+    hist = coarse_history()
+    inputs = hist.device_inputs()
+    posts = hist.posteriors()                      # host build: the reference's np.argsort
     eng = Engine(0)
     try:
-        eng.build_posterior(*hist.device_inputs(), gamma=0.25, prior_weight=1.0)
-        n_tied = 0
-        for li, p in enumerate(host_posts):
-            if p.family == 'categorical':
-                continue
-            for side, hp_ in ((0, p.below), (1, p.above)):
-                w, mu, sg = eng.get_mixture(li, side)
-                hw, hmu, hsg = hp_
-                assert np.array_equal(mu, hmu) and np.array_equal(sg, hsg), (li, side)
-                gd, gh = _groups(w, mu, sg), _groups(hw, hmu, hsg)
-                assert gd.keys() == gh.keys()
-                for k in gd:
-                    assert abs(gd[k] - gh[k]) <= 1e-14 * max(1.0, abs(gh[k])), (li, side, k)
-                n_tied += int(len(np.unique(hmu)) < len(hmu))
-        assert n_tied > 0          # the history does have tied labels
-        rounds = [(24, 5, 11), (24, 6, 12), (1 << 20, 7, 13)]
-        dev = [eng.suggest(seed, C, round=r) for C, r, seed in rounds]
-        eng.set_posterior(*P.pack(host_posts))
-        host = [eng.suggest(seed, C, round=r) for C, r, seed in rounds]
-        worst = 0.0
-        for a, b in zip(dev, host):
+        # without the reference's order the device flags the tied mixtures
+        # and the split tie -- and its position-order mixtures differ
+        eng.history_reset(inputs[0], inputs[1])
+        eng.history_append(np.diff(inputs[3]), inputs[4], inputs[5])
+        nb, ties = eng.build_posterior_ordered(hist.losses, len(hist.losses), 0.25, 1.0)
+        assert nb == 20 and ties[-1] == 1, ties
+        flagged = {COARSE[l][0] for l in np.flatnonzero(ties[:-1] & 2)}
+        assert {'qu10', 'qlu', 'qn', 'qu100'} <= flagged, flagged
+        assert not flagged & {'u', 'ri'}
+        w_pos = eng.get_mixture(0, 1)[0]
+        assert not np.array_equal(w_pos, posts[0].above[0])   # the test can tell orders apart
+        # the product path: the reference's order where it matters
+        nb = eng.build_posterior(*inputs, gamma=0.25, prior_weight=1.0)
+        assert nb == 20
+        assert {COARSE[l][0] for l in eng.tie_labels} == flagged
+        _assert_same(eng, hist, posts)
+        # the resident history, built incrementally, keeps the order too
+        from hyperopt_amd.history import device_view
+        from hyperopt_amd.base import Domain
+        from hyperopt_amd.workloads import history_trials, hp_space
+        trials = history_trials(hist)
+        dom = Domain(lambda d: 0.0, hp_space(hist.labels))
+        up = P.DeviceHistoryUploader()
+        view = device_view(dom, trials, [n for n, _, _ in COARSE])
+        up.build(eng, COARSE, view, 0.25, 1.0)
+        _assert_same(eng, hist, posts)
+        # and on identical candidates the winners and lpdfs equal those of the
+        # host-built posterior
+        res_dev = [eng.suggest(seed, C, round=r) for C, r, seed in ((24, 3, 5), (1 << 18, 4, 6))]
+        eng.set_posterior(*P.pack(posts))
+        res_host = [eng.suggest(seed, C, round=r) for C, r, seed in ((24, 3, 5), (1 << 18, 4, 6))]
+        for a, b in zip(res_dev, res_host):
             assert np.array_equal(a['index'], b['index'])
             assert np.array_equal(a['value'], b['value'])
-            for f in ('lpdf_below', 'lpdf_above'):
-                rel = np.abs(a[f] - b[f]) / np.maximum(1.0, np.abs(b[f]))
-                worst = max(worst, float(rel.max()))
-        assert worst <= 1e-12, worst
-        print('config 3 tie order: %d tied mixtures; winners identical; worst lpdf rel diff %.2e'
-              % (n_tied, worst))
+            np.testing.assert_allclose(a['lpdf_below'], b['lpdf_below'], rtol=1e-12, atol=1e-12)
+            np.testing.assert_allclose(a['lpdf_above'], b['lpdf_above'], rtol=1e-12, atol=1e-12)
     finally:
         eng.close()
+
+
+def test_auto_and_host_builders_suggest_identical_documents():
+    """tpe.suggest on the coarse history: 'auto' takes the device builder
+    (36k observations), 'host' the numpy one; same documents for several
+    seeds, and again after trials are appended (the resident history grows
+    incrementally, the known tie-dependent labels keep their order)."""
+    from hyperopt_amd import tpe
+    from hyperopt_amd.base import Domain
+    from hyperopt_amd.engine import get_engine
+    from hyperopt_amd.workloads import history_trials, hp_space
+    hist = coarse_history(seed=1)
+    trials = history_trials(hist)
+    dom = Domain(lambda d: 0.0, hp_space(hist.labels))
+    n = len(hist.tids)
+    for step in range(4):
+        new_id = n + step
+        a = tpe.suggest([new_id], dom, trials, 100 + step, posterior_builder='auto')
+        b = tpe.suggest([new_id], dom, trials, 100 + step, posterior_builder='host')
+        assert a[0]['misc']['vals'] == b[0]['misc']['vals'], step
+        # finish the suggested trial with a loss that ties the split boundary
+        doc = a[0]
+        doc['state'] = 2
+        doc['result'] = {'status': 'ok', 'loss': -5.0 if step % 2 else float(step)}
+        trials.insert_trial_docs(a)
+        trials.refresh()
+    up = get_engine(0, 'f64')._history_uploader
+    assert up.tie_labels, 'the device path did not run'

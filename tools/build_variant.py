@@ -1,28 +1,62 @@
-"""Build an engine variant with extra preprocessor definitions into
-tools/var_<name>.so, stamped with the tree's own source hash so the loader
-takes it when it is copied over hyperopt_amd/libhyperopt_tpe.so (timing
-experiments only: tools/var_sweep.sh, tools/var_trace.sh).
+"""Build a timing variant of the engine (experiments only) into
+tools/var_<name>.so from a PATCHED COPY of the sources: the product sources
+carry no experiment switches.  A variant is stamped 'v:<name>:' + a hash of
+the patched sources, so the product loader refuses it unless the process
+opts in explicitly with HYPEROPT_AMD_VARIANT=<path to the variant> (the
+product library in hyperopt_amd/ is never overwritten).
 
-    python tools/build_variant.py bm TPE_EXP_BM_CHEAP
-    python tools/build_variant.py norej TPE_EXP_NO_REJECT
+    python tools/build_variant.py bm        # Box-Muller replaced by a cheap affine map (not a normal draw)
+    python tools/build_variant.py norej     # no truncation rejection (wrong samples)
+    python tools/build_variant.py hot4 -DTPE_HOT_R=4   # a compile-time constant changed
+
+    HYPEROPT_AMD_VARIANT=tools/var_bm.so python bench.py ...
 """
+import hashlib
 import os
+import shutil
 import sys
+import tempfile
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, REPO)
 from hyperopt_amd import _build  # noqa: E402
+
+# name -> [(file, old text, new text)]: result-changing timing experiments
+PATCHES = {
+    'bm': [('tpe_device.h',
+            '    const double u1 = u01_open0(r.y, r.z);\n',
+            '    return fma(sg, (double)(int32_t)r.w * 0x1.0p-29, mu);\n'
+            '    const double u1 = u01_open0(r.y, r.z);\n')],
+    'norej': [('tpe_device.h',
+               '    const bool bounded = (L.flags & 3) == 3;\n    const uint32_t mask0 = pend;',
+               '    const bool bounded = false;\n    const uint32_t mask0 = pend;')],
+}
 
 
 def main(name, defs):
-    base = _build.source_hash()          # the variant loads as the tree's own build
-    _build.source_hash = lambda deps=None: base
-    _build.FLAGS = _build.FLAGS + ['-D' + d for d in defs]
-    _build.TARGET = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'var_%s.so' % name)
+    tmp = tempfile.mkdtemp(prefix='tpe_variant_')
     try:
+        csrc = os.path.join(tmp, 'csrc')
+        shutil.copytree(os.path.join(REPO, 'hyperopt_amd', 'csrc'), csrc)
+        for fname, old, new in PATCHES.get(name, []):
+            p = os.path.join(csrc, fname)
+            txt = open(p).read()
+            if old not in txt:
+                raise SystemExit('patch %s does not apply to %s' % (name, fname))
+            open(p, 'w').write(txt.replace(old, new, 1))
+        srcs = [os.path.join(csrc, os.path.basename(s)) for s in _build.SOURCES]
+        deps = [os.path.join(csrc, os.path.basename(d)) if '/csrc/' in d else d for d in _build.DEPS]
+        h = hashlib.sha256((_build.source_hash(deps) + ' '.join(defs)).encode()).hexdigest()
+        stamp = ('v:%s:%s' % (name, h))[:16]
+        _build.SOURCES = srcs
+        _build.source_hash = lambda deps=None: stamp
+        _build.FLAGS = _build.FLAGS + list(defs)
+        _build.TARGET = os.path.join(HERE, 'var_%s.so' % name)
         _build.build_engine(force=True, verbose=False)
-    except RuntimeError:   # (the post-build check reads the tree's own library)
-        pass
-    print('built', _build.TARGET)
+        print('built %s (stamp %s)' % (_build.TARGET, stamp))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 if __name__ == '__main__':
