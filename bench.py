@@ -102,9 +102,14 @@ def parse():
                     help='the windowed screen\'s cut T (components left out stay below 2^-T)')
     ap.add_argument('--win-groups', type=int, default=0,
                     help='label groups of a windowed round sorted on a second stream (0 = auto)')
-    ap.add_argument('--unscreened-steps', type=int, default=3,
-                    help='f64: steps of the plain fp64 round timed after the main run, for '
-                         'comparison (0 = skip)')
+    ap.add_argument('--unscreened-steps', type=int, default=1,
+                    help='f64: plain fp64 rounds on the seeds of screened rounds, compared bit '
+                         'for bit (screened_equals_fp64; 0 = skip)')
+    ap.add_argument('--mode', default='fresh', choices=['fresh', 'warm'],
+                    help='fresh (default): every step appends a trial and rebuilds the posterior '
+                         'and its index, as fmin does; warm: rounds on one resident posterior')
+    ap.add_argument('--append', type=int, default=1,
+                    help='fresh mode: trials appended to the history per step')
     ap.add_argument('--devices', default=None,
                     help='one process, one multi-device context over these HIP ordinals '
                          '(e.g. 0,1,2,3; tpe_ctx_create_multi): the 1..8-GPU curve without '
@@ -232,20 +237,25 @@ def main():
         dist.init_process_group(args.dist_backend)
     from hyperopt_amd import posterior as P
     from hyperopt_amd.engine import Engine
-    from hyperopt_amd.workloads import conditional_history, hartmann_history, mixed_history
+    from hyperopt_amd.workloads import (FminLoop, conditional_history, hartmann_history,
+                                         mixed_history)
 
+    # the synthetic history holds the trials the fresh-posterior steps append
+    # (fmin's loop: one trial per suggestion) after the first args.trials
+    extra = (args.warmup + args.steps + 2) * args.append
     if args.config == 2:
         args.labels, args.trials, args.cand_log2 = 6, 2000, 20
-        hist = hartmann_history(args.trials, seed=0)
+        hist_full = hartmann_history(args.trials + extra, seed=0)
     elif args.config == 4:
         args.trials, args.cand_log2 = 5000, 20
-        hist = conditional_history(args.trials, seed=0)
-        args.labels = len(hist.labels)
+        hist_full = conditional_history(args.trials + extra, seed=0)
+        args.labels = len(hist_full.labels)
     elif args.config == 5:
         args.labels, args.trials = 128, args.c5_history
-        hist = mixed_history(args.labels, args.trials, seed=0)
+        hist_full = mixed_history(args.labels, args.trials + extra, seed=0)
     else:
-        hist = mixed_history(args.labels, args.trials, seed=0)
+        hist_full = mixed_history(args.labels, args.trials + extra, seed=0)
+    hist = hist_full.prefix(args.trials)
     # the resident posterior: built on the device from the history (the
     # product path for histories this size, tpe.suggest posterior_builder
     # 'auto'); the host numpy build is timed beside it
@@ -282,7 +292,19 @@ def main():
 
     from hyperopt_amd.parallel import exchange_winners, gather_rounds
 
-    def step(i):
+    # fresh-posterior steps (default): each step appends the next trial(s) to
+    # the device-resident history and rebuilds the posterior as tpe.suggest
+    # does (FminLoop), so the round pays the expansion index of a new
+    # posterior -- what every suggestion of fmin's loop pays
+    loop = None
+    if args.mode == 'fresh':
+        loop = FminLoop(hist_full)
+        loop.advance(eng, args.trials)        # untimed: the initial history, uploaded whole
+    results = {}
+
+    def step(i, fresh):
+        if fresh:
+            loop.advance(eng, args.trials + (i + 1) * args.append)
         if args.config == 5:   # independent new_ids split over the GPUs
             ids = [i * args.new_ids + rank * ids_local + k for k in range(ids_local)]
             res = eng.suggest_batch(seed=1234, rounds=ids, n_candidates=C)
@@ -294,16 +316,19 @@ def main():
             res = exchange_winners(res)
         return res
 
-    def timed(n_steps, first):
+    def timed(n_steps, first, fresh, keep=False):
         """Run n_steps steps (barrier + sync on both sides); returns wall
-        seconds (max over ranks) and the summed per-family / screen stats."""
-        mode_ms, mode_ev, scr = {}, {}, [0, 0, 0.0, 0, 0, 0, 0]
+        seconds (max over ranks) and the summed per-family / screen stats
+        (scr[7]: the expansion-index wall ms of the steps that built one)."""
+        mode_ms, mode_ev, scr = {}, {}, [0, 0, 0.0, 0, 0, 0, 0, 0.0]
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(n_steps):
-            step(first + i)
+            res = step(first + i, fresh)
+            if keep:
+                results[first + i] = res
             for k, (ms, ev) in eng.last_mode_stats().items():
                 mode_ms[k] = mode_ms.get(k, 0.0) + ms
                 mode_ev[k] = mode_ev.get(k, 0) + ev
@@ -316,6 +341,8 @@ def main():
             hl, hf = eng.last_hot()
             scr[5] += max(hl, 0)
             scr[6] += hf
+            if fresh:
+                scr[7] += eng.last_prepare_ms()
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
@@ -336,12 +363,15 @@ def main():
         eng.set_option('whole_rounds' if args.config == 5 else 'whole_n',
                        args.new_ids if args.config == 5 else C_total)
     for i in range(args.warmup):
-        step(i)
+        step(i, loop is not None)
     # the expansion screen's index (bin tables, lists, sub-bin bounds) is
-    # built once per posterior, in the first large round: reported beside
-    # the step (a suggest on a fresh posterior pays build + index + step)
+    # built once per posterior, in its first large round
     prep_ms = eng.last_prepare_ms() if args.warmup > 0 else None
-    dt, mode_ms, mode_ev, scr = timed(args.steps, args.warmup)
+    dt, mode_ms, mode_ev, scr = timed(args.steps, args.warmup, loop is not None)
+    # the same rounds on the posterior of the last step, reused (no append):
+    # the round alone, and the reference for the unscreened comparison
+    warm_first = args.warmup + args.steps
+    wdt, _, _, _ = timed(args.steps, warm_first, False, keep=True) if loop is not None else (None,) * 4
     # `value` counts EXECUTED (candidate, component) lpdf terms (BASELINE.md
     # section 3): quantized labels their grid-table evals, screened dense
     # labels the fp32 terms the screen summed plus the fp64 terms of the
@@ -458,12 +488,25 @@ def main():
                                    else 'candidate-sharded x%d') % (len(devs) if devs else world)
                                   + (' (one process, multi-device context %s)' % devs
                                      if devs else '')},
-        'fresh_posterior_round_ms': (round(post_build['device_call_ms'] + prep_ms + dt / args.steps * 1e3, 3)
-                                     if prep_ms else None),
+        'step': ({'kind': 'fresh posterior (fmin loop)',
+                  'note': 'each step appends %d trial(s) to the device-resident history, rebuilds the '
+                          'posterior on the device (split, Parzen, fold; numpy\'s np.argsort tie order '
+                          'where a mixture depends on it), builds the expansion index of the new '
+                          'posterior and runs the round -- what every suggestion of fmin(tpe.suggest) '
+                          'pays (reference: tpe_transform + rec_eval per call, tpe.py:834,900)'
+                          % args.append,
+                  'history_first_step': args.trials + args.append,
+                  'expansion_index_ms': round(scr[7] / args.steps, 3),
+                  'warm_round_ms': round(wdt / args.steps * 1e3, 3),
+                  'warm_note': 'the same rounds on one resident posterior (no append, no rebuild, '
+                               'no index): the round alone'}
+                 if loop is not None else
+                 {'kind': 'warm (one resident posterior)',
+                  'fresh_posterior_round_ms': (round(post_build['device_call_ms'] + prep_ms
+                                                     + dt / args.steps * 1e3, 3) if prep_ms else None)}),
         'posterior_build': dict(post_build, expansion_index_ms=(round(prep_ms, 3) if prep_ms else None),
-                                expansion_index_note='once per posterior (bin tables, lists, sub-bin '
-                                'bounds; wall ms with the kernels), in its first large round; the '
-                                'timed steps reuse the posterior'),
+                                expansion_index_note='the first index of the run (bin tables, lists, '
+                                'sub-bin bounds; wall ms with the kernels)'),
         'per_family_ms': {k: round(v / args.steps, 3) for k, v in mode_ms.items() if v},
         'per_family_evals': {k: v // args.steps for k, v in mode_ev.items() if v},
         'roofline': roof,
@@ -501,20 +544,37 @@ def main():
                     '(tests/test_screen.py).  `value` counts the terms executed (screen + '
                     're-score); the roofline counts the terms the screening kernel summed.  '
                     'other_dense_ms: keys + sort, select, re-score'}
-        if args.unscreened_steps > 0 and world == 1:
+        if args.unscreened_steps > 0 and world == 1 and devs is None:
+            # the plain fp64 round on the SAME (seed, round) as screened steps
+            # on the same posterior: winners, values and lpdfs bit for bit
+            nu = args.unscreened_steps
+            first = warm_first if loop is not None else args.warmup + args.steps
+            if loop is None:
+                timed(nu, first, False, keep=True)
             eng.set_option('screen', 0)
-            step(args.warmup + args.steps)
-            udt, ums, uev, _ = timed(args.unscreened_steps, args.warmup + args.steps + 1)
+            ures = {}
+            t0 = time.perf_counter()
+            for i in range(nu):
+                ures[first + i] = step(first + i, False)
+            torch.cuda.synchronize()
+            udt = time.perf_counter() - t0
             eng.set_option('screen', 1)
+            same = all(results[k].view(np.uint8).tobytes() == ures[k].view(np.uint8).tobytes()
+                       for k in ures)
+            line['screened_equals_fp64'] = bool(same)
             line['screen']['unscreened_fp64'] = {
-                'steps': args.unscreened_steps,
-                'ms_per_step': round(udt / args.unscreened_steps * 1e3, 3),
-                'value': sum(uev.values()) / udt,
-                'dense_ms': round(ums[dom] / args.unscreened_steps, 3)}
+                'steps': nu, 'ms_per_step': round(udt / nu * 1e3, 3),
+                'compared': 'index, value, score, lpdf_below, lpdf_above, status of every label, '
+                            'bytewise, on rounds %d..%d of the last posterior (the screened runs '
+                            'are the warm steps)' % (first, first + nu - 1),
+                'bit_identical': bool(same)}
     if prec == 'f32' and args.agreement_steps > 0 and args.config != 5:
         # fp32 winners vs the exact fp64 round's on the same candidate sets
         ref = Engine(devs if devs else local, 'f64')
-        ref.build_posterior(*inputs, gamma=0.25, prior_weight=1.0)
+        if loop is not None:   # the posterior the fp32 engine holds now
+            FminLoop(hist_full).advance(ref, loop.n)
+        else:
+            ref.build_posterior(*inputs, gamma=0.25, prior_weight=1.0)
         same = total = 0
         worst_regret = 0.0
         for i in range(args.agreement_steps):

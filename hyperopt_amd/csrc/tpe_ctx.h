@@ -89,8 +89,8 @@ struct Posterior {
     std::vector<tpe::BxLabel> bx_h;
     DevBuf<double> bx_tab;               // per label: nbins rows of kBxRow doubles
     DevBuf<int32_t> bx_nc;               // per label at comp_a: unclipped above components
-    DevBuf<int32_t> bx_loff;             // per label: nbins + 1 offsets into its list
-    DevBuf<int32_t> bx_list;             // per bin: the unclipped components reaching it
+    DevBuf<int32_t> bx_loff;             // per bin: the length of its list
+    DevBuf<int32_t> bx_list;             // per bin: a slot of n_nc, the unclipped components reaching it
     DevBuf<double> bx_scan;              // per dense label position: range, a*, counts
     DevBuf<float2> bx_sb;                // hot-bin prefilter: per sub-bin (U, L) of the score
     DevBuf<float> bx_sbp;                //   and the below mixture's sampling mass of it

@@ -895,8 +895,8 @@ struct BxLabel {
     double dwin;              // window half-width: clipped components beyond never reach 2^-T
     double rP;                // rmax^P
     int64_t tab_off;          // first row of the label in bx_tab
-    int64_t cnt_off;          // first of its nbins + 1 list offsets in bx_loff
-    int64_t list_off;         // first of its entries in bx_list
+    int64_t cnt_off;          // first of its nbins list counts in bx_loff
+    int64_t list_off;         // first of its nbins slots of n_nc entries in bx_list
     int32_t nbins, n_nc;      // bins; unclipped components (listed at comp_a in bx_nc)
     double inv_sbw;           // kBxSub / bw: sub-bin of x' = floor((x' - xlo) inv_sbw)
     int64_t sb_off;           // first of its nbins kBxSub sub-bins in bx_sb / bx_sbp

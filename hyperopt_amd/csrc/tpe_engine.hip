@@ -581,8 +581,8 @@ __device__ __forceinline__ int bx_score(const DLabel& L, const BxLabel& B,
         const double et = fma(fma(fma(fma(fma(-1.0 / 120.0, t, 1.0 / 24.0), t, -1.0 / 6.0), t, 0.5), t,
                                   -1.0), t, 1.0);
         const double sclip = et * poly;
-        const int j0 = loff[B.cnt_off + b], j1 = loff[B.cnt_off + b + 1];
-        const int32_t* lst = list + B.list_off;
+        const int j0 = 0, j1 = loff[B.cnt_off + b];   // the bin's count, its slot of n_nc entries
+        const int32_t* lst = list + B.list_off + (int64_t)b * B.n_nc;
         double snc = 0.0;
         for (int j = j0; j < j1; ++j) {
             const Comp<double> rec = ca[lst[j]];

@@ -11,11 +11,12 @@
 //                 2 kappa |d| |delta| stays <= ~0.5, so 15 terms leave a
 //                 truncation ~4e-17 of the bin's mass
 //   k_bx_compact  per label: the unclipped components in record order
-//   k_bx_count    per bin: unclipped components whose term can reach 2^-T in it
-//   k_bx_offsets  per label: their exclusive scan (list offsets), the total
-//   k_bx_fill     per bin: the list
-//   k_bx_table    per bin (one wave): A_0..A_14 over the clipped components within the
-//                 window, and the absolute bound Eabs of truncation + rounding
+//   k_bx_list     per bin: the unclipped components whose term can reach 2^-T
+//                 in it, into the bin's slot of n_nc entries, and their count
+//   k_bx_table    per bin (one thread): A_0..A_14 over the clipped components
+//                 within the window, and the absolute bound Eabs of truncation
+//                 + rounding
+//   k_bx_bounds   per sub-bin: the hot-bin prefilter's [L, U] and sampling mass
 //
 // Bounds (natural-log units, records as tpe_device.h Comp: c'/K = log coef -
 // M <= 0, a'^2 / K = 1 / (2 sigma^2)): a clipped component farther than
@@ -102,7 +103,13 @@ __device__ __forceinline__ bool usable(const Comp<double>& r) {
     return r.a > 0.0 && r.a < kInf && fabs(r.mu) < kInf;
 }
 
-// grid (dense labels): range, a*, counts -> scan[y * kScanFields ...]
+// grid (dense labels): range, a*, counts -> scan[y * kScanFields ...].
+// The candidate range of a label without both bounds covers each sampling
+// component k to z_k sigma_k with w_k Q(z_k) <= kRangeTail (at most 8 sigma):
+// a candidate outside the bins is always listed and scored in fp64 (exact,
+// only slower), and at 2^24 candidates per round that happens ~1e-3 times per
+// label; a one-sided bound cuts the range on its side.
+constexpr double kRangeTail = 1e-10;
 __global__ __launch_bounds__(kBlock) void k_bx_scan(const DLabel* __restrict__ labels,
                                                     const int32_t* __restrict__ grp,
                                                     const Comp<double>* __restrict__ comps64,
@@ -119,11 +126,16 @@ __global__ __launch_bounds__(kBlock) void k_bx_scan(const DLabel* __restrict__ l
     } else {
         for (int k = threadIdx.x; k < L.ns; k += kBlock) {
             const SampRec s = samp[L.samp_off + k];
-            lo = fmin(lo, s.mu - 8.0 * s.sigma);
-            hi = fmax(hi, s.mu + 8.0 * s.sigma);
+            const double w = s.cdf - (k ? samp[L.samp_off + k - 1].cdf : 0.0);
+            // Q(z) <= exp(-z^2 / 2) / 2: z = sqrt(2 ln(w / tail)) suffices
+            const double z = w > kRangeTail ? fmin(8.0, sqrt(2.0 * log(w / kRangeTail))) : 0.0;
+            lo = fmin(lo, s.mu - z * s.sigma);
+            hi = fmax(hi, s.mu + z * s.sigma);
         }
         lo = blk_min(lo, shd);
         hi = blk_max(hi, shd);
+        if (L.flags & 1) lo = fmax(lo, L.low);
+        if (L.flags & 2) hi = fmin(hi, L.high);
     }
     const Comp<double>* c = comps64 + L.comp_a;
     double am = 0.0;
@@ -181,56 +193,30 @@ __device__ __forceinline__ bool reaches(const Comp<double>& r, const BxLabel& B,
     return r.c * kExpScaleInv - kap * dist * dist >= -(kBxT * kLn2 + 1.0);
 }
 
-// grid (ceil(max bins / 256), dense labels): per bin the count of reaching
-// unclipped components (fill = false) or their list (fill = true)
-template <bool FILL>
+// grid (ceil(max bins / 256), dense labels): per bin the unclipped
+// components that reach it, in record order, into the bin's slot of n_nc
+// entries (list_off + b n_nc), their count into cnt[cnt_off + b]
 __global__ __launch_bounds__(kBlock) void k_bx_list(const DLabel* __restrict__ labels,
                                                     const int32_t* __restrict__ grp,
                                                     const Comp<double>* __restrict__ comps64,
                                                     const BxLabel* __restrict__ bx,
                                                     const int32_t* __restrict__ nc,
-                                                    int32_t* __restrict__ loff,
+                                                    int32_t* __restrict__ cnt,
                                                     int32_t* __restrict__ list) {
     const int li = grp[blockIdx.y];
-    const DLabel L = labels[li];
     const BxLabel B = bx[li];
     const int b = blockIdx.x * kBlock + threadIdx.x;
     if (b >= B.nbins) return;
+    const DLabel L = labels[li];
     const Comp<double>* c = comps64 + L.comp_a;
     const int32_t* ncl = nc + L.comp_a;
-    int cnt = 0;
-    int32_t* out = FILL ? list + B.list_off + loff[B.cnt_off + b] : nullptr;
+    int m = 0;
+    int32_t* out = list + B.list_off + (int64_t)b * B.n_nc;
     for (int j = 0; j < B.n_nc; ++j) {
         const int k = ncl[j];
-        if (reaches(c[k], B, b)) {
-            if (FILL) out[cnt] = k;
-            ++cnt;
-        }
+        if (reaches(c[k], B, b)) out[m++] = k;
     }
-    if (!FILL) loff[B.cnt_off + b] = cnt;
-}
-
-// grid (dense labels): counts -> exclusive offsets (nbins + 1 entries), total
-__global__ __launch_bounds__(kBlock) void k_bx_offsets(const int32_t* __restrict__ grp,
-                                                       const BxLabel* __restrict__ bx,
-                                                       int32_t* __restrict__ loff,
-                                                       int64_t* __restrict__ total) {
-    const BxLabel B = bx[grp[blockIdx.x]];
-    __shared__ int shi[kBlock / 64];
-    int32_t* o = loff + B.cnt_off;
-    int64_t base = 0;
-    for (int b0 = 0; b0 < B.nbins; b0 += kBlock) {
-        const int b = b0 + threadIdx.x;
-        const int v = b < B.nbins ? o[b] : 0;
-        int tot;
-        const int pos = blk_prefix(v, shi, tot);
-        if (b < B.nbins) o[b] = (int32_t)(base + pos);
-        base += tot;
-    }
-    if (threadIdx.x == 0) {
-        o[B.nbins] = (int32_t)base;
-        total[blockIdx.x] = base;
-    }
+    cnt[B.cnt_off + b] = m;
 }
 
 // 1 / n!, n <= kBxP
@@ -240,89 +226,165 @@ __constant__ double kInvFact[kBxP + 1] = {
     1.0 / 1307674368000.0};
 
 
-// first record index k in [0, n) with mu'_k >= v (mu' = m'/a', sorted by mu)
-__device__ __forceinline__ int lower_mu(const Comp<double>* __restrict__ c, int n, double v) {
-    int lo = 0, hi = n;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        const Comp<double> r = c[mid];
-        const double mu = r.a > 0.0 ? r.mu / r.a : -kInf;
-        if (mu >= v) hi = mid; else lo = mid + 1;
+__device__ __forceinline__ double rec_mu(const Comp<double>& r) { return r.a > 0.0 ? r.mu / r.a : -kInf; }
+
+// The wave's first record index with mu' >= v0 (-> k0) and with mu' >= v1
+// (-> k1) over records [0, n) sorted by mu (mu' = m'/a'): lanes 0..31 search
+// v0, lanes 32..63 v1, each half probing 32 evenly spaced records per step
+// (~4 dependent loads for 10k records instead of 13)
+__device__ __forceinline__ void wave_window(const Comp<double>* __restrict__ c, int n, double v0, double v1,
+                                            int& k0, int& k1) {
+    const int lane = threadIdx.x & 63, half = lane >> 5, l32 = lane & 31;
+    const double v = half ? v1 : v0;
+    int lo = 0, hi = n;   // the answer lies in [lo, hi]
+    while (__ballot(hi > lo)) {
+        const int span = hi - lo;
+        const int step = (span + 31) >> 5;
+        const int q = lo + l32 * step;
+        bool ge = true;
+        if (span > 0 && q < hi) ge = rec_mu(c[q]) >= v;
+        const uint32_t mh = (uint32_t)(__ballot(ge) >> (half * 32));
+        if (span > 0) {
+            if (mh == 0u) {
+                lo += 31 * step + 1;
+            } else {
+                const int i = __builtin_ctz(mh);
+                if (i == 0) {
+                    hi = lo;
+                } else {
+                    hi = min(lo + i * step, hi);
+                    lo += (i - 1) * step + 1;
+                }
+            }
+        }
     }
-    return lo;
+    k0 = __builtin_amdgcn_readlane(lo, 0);
+    k1 = __builtin_amdgcn_readlane(lo, 32);
 }
 
-// grid (ceil(max bins / 4), dense labels): one wave per bin, its lanes
-// striding over the window's clipped components, the partial sums added by a
-// butterfly at the end (a bin's window holds thousands of components: one
-// thread per bin left the chip ~0.6 waves per SIMD)
+// lane j's value, to every lane (j wave-uniform: v_readlane into SGPRs)
+__device__ __forceinline__ double bcast(double v, int j) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, j);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), j);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// grid (ceil(max bins / 64), dense labels): 64 consecutive bins per
+// workgroup, one bin per lane, their union window of clipped components
+// (wave_window) split over the 4 waves in interleaved batches of 64 records.
+// A batch is loaded coalesced and broadcast lane by lane (v_readlane), each
+// lane adding the components within its own bin's window, branch-free, to
+// its A_0..A_14; the 4 waves' partial sums meet in LDS at the end.  The
+// bound (module comment) per lane: with |d| <= D for every summed component,
+// e^y <= e^Y (Y = 2 kappa D rmax), so the per-component terms of the bound
+// are accumulated as four sums and combined at the end (each term at least
+// what the per-component form gives).
+constexpr int kTabSums = kBxP + 5;   // A_0..A_14, S0..S3, W
+static_assert(3 * kTabSums * 64 <= kExpTabSize, "k_bx_table: 3 waves' partial sums in the exp table's LDS");
 __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ labels,
                                                      const int32_t* __restrict__ grp,
                                                      const Comp<double>* __restrict__ comps64,
                                                      const BxLabel* __restrict__ bx,
                                                      double* __restrict__ tab) {
     const int li = grp[blockIdx.y];
-    const DLabel L = labels[li];
     const BxLabel B = bx[li];
-    __shared__ double exp_tab[kExpTabSize];
-    load_exp_table(exp_tab);
-    const int lane = threadIdx.x & 63;
-    const int b = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-    if (b >= B.nbins) return;   // whole waves (after the table's barrier)
-    const Comp<double>* c = comps64 + L.comp_a;
-    const double xb = B.xlo + ((double)b + 0.5) * B.bw;
+    const int b0 = blockIdx.x * 64;   // the workgroup's first bin
+    if (b0 >= B.nbins) return;        // the whole workgroup
+    const DLabel L = labels[li];
+    __shared__ double lds[kExpTabSize];   // the exp table, then the waves' partial sums
+    load_exp_table(lds);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int b = b0 + lane, blast = min(b0 + 63, B.nbins - 1);
     const double r = B.rmax, kap = B.kappa;
-    const double D = B.dwin * (1.0 + 1e-9) + (fabs(xb) + B.dwin) * 1e-12;
-    // the window: records sorted by mu, so the clipped ones within D of xb
-    // are a contiguous index range (margins cover mu' = m'/a' rounding)
-    const int k0 = lower_mu(c, L.na, xb - D), k1 = lower_mu(c, L.na, xb + D);
+    auto centre = [&](int i) { return B.xlo + ((double)i + 0.5) * B.bw; };
+    auto reach = [&](double x) { return B.dwin * (1.0 + 1e-9) + (fabs(x) + B.dwin) * 1e-12; };
+    const double xb = centre(min(b, blast)), D = reach(xb);
+    // (the window: records sorted by mu, so the clipped ones within D of
+    // any of the workgroup's bins are a contiguous index range; margins cover
+    // mu' = m'/a' rounding)
+    const double xf = centre(b0), xl = centre(blast);
+    int k0, k1;
+    wave_window(comps64 + L.comp_a, L.na, xf - reach(xf), xl + reach(xl), k0, k1);
+    const Comp<double>* c = comps64 + L.comp_a;
     double A[kBxP];
 #pragma unroll
     for (int n = 0; n < kBxP; ++n) A[n] = 0.0;
-    double Rb = 0.0, G = 0.0, ERR = 0.0, W = 0.0;
+    double S0 = 0.0, S1 = 0.0, S2 = 0.0, S3 = 0.0;   // sum g, g |arg|, g |mu|, |g (2 kappa d)^P|
+    double W = 0.0;
     // mu' = m' (1 / a*): <= 1.5 ulp (inside the 2^-51 allowance below);
     // g = exp(arg) through the fp64 round's table exp (<= 2.6e-14 relative,
     // added to the rounding term); the powers g (2 kappa d)^n by one
     // multiply each, A_n += that / n! (one rounding each, inside 3P + 10)
     const double inv_a = 1.0 / B.astar;
-    for (int k = k0 + lane; k < k1; k += 64) {
-        const Comp<double> rec = c[k];
-        if (rec.a != B.astar) continue;
-        const double mu = rec.mu * inv_a, d = mu - xb;
-        const double arg = rec.c * kExpScaleInv - kap * d * d;
-        if (!(arg > -740.0)) continue;   // below 2^-1067 in the whole bin: in the skip term
-        const double g = exp_scaled(fmin(arg * kExpScale, 0.0), exp_tab), two = 2.0 * kap * d;
-        // e^y only enters the bounds: 1 + y + y^2 >= e^y for 0 <= y <= 1.79
-        const double yv = fabs(two) * r, ey = yv <= 1.5 ? fma(yv, yv, 1.0 + yv) : exp(yv) * 1.000001;
-        double t = g;
-        A[0] += t;
-#pragma unroll
-        for (int n = 1; n < kBxP; ++n) {
-            t *= two;
-            A[n] = fma(t, kInvFact[n], A[n]);
+    for (int kc = k0 + wave * 64; kc < k1; kc += kBlock) {
+        const int k = kc + lane;
+        double mu_l = 0.0, c_l = -kInf;
+        if (k < k1) {
+            const Comp<double> rec = c[k];
+            if (rec.a == B.astar) {
+                mu_l = rec.mu * inv_a;
+                c_l = rec.c * kExpScaleInv;
+            }
         }
-        const double tP = fabs(t * two) * kInvFact[kBxP];   // g |2 kappa d|^P / P!
-        const double gy = g * ey;
-        Rb += tP * B.rP * ey;
-        G += gy;
-        ERR += gy * ((3.0 * kBxP + 10.0 + 4.0 * fabs(arg)) * kU + 2.6e-14 +
-                     2.0 * kap * (fabs(d) + r) * (fabs(mu) + fabs(d) + r) * 0x1.0p-51);
-        W += 1.0;
-    }
+        const int cnt = min(64, k1 - kc);
+        for (int j = 0; j < cnt; ++j) {
+            const double cj = bcast(c_l, j);
+            if (!(cj > -kInf)) continue;   // unclipped or weightless (wave-uniform)
+            const double mu = bcast(mu_l, j), d = mu - xb;
+            const double arg = fmax(cj - kap * d * d, -745.0);
+            // outside the bin's window, or below 2^-1067 in the whole bin (in
+            // the skip term): g = 0, so every sum below is unchanged
+            const bool in = fabs(d) <= D && arg > -740.0;
+            const double e = exp_scaled(fmin(arg * kExpScale, 0.0), lds);
+            const double g = in ? e : 0.0, two = 2.0 * kap * d;
+            double t = g;
+            A[0] += t;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-#pragma unroll
-        for (int n = 0; n < kBxP; ++n) A[n] += __shfl_xor(A[n], off);
-        Rb += __shfl_xor(Rb, off);
-        G += __shfl_xor(G, off);
-        ERR += __shfl_xor(ERR, off);
-        W += __shfl_xor(W, off);
+            for (int n = 1; n < kBxP; ++n) {
+                t *= two;
+                A[n] = fma(t, kInvFact[n], A[n]);
+            }
+            S0 += g;
+            S1 = fma(g, fabs(arg), S1);
+            S2 = fma(g, fabs(mu), S2);
+            S3 += fabs(t * two);
+            W += in ? 1.0 : 0.0;
+        }
     }
-    if (lane != 0) return;
+    __syncthreads();   // the exp table is no longer read: partial sums of waves 1..3
+    if (wave > 0) {
+        double* p = lds + ((wave - 1) * kTabSums) * 64 + lane;
+#pragma unroll
+        for (int n = 0; n < kBxP; ++n) p[n * 64] = A[n];
+        p[(kBxP + 0) * 64] = S0;
+        p[(kBxP + 1) * 64] = S1;
+        p[(kBxP + 2) * 64] = S2;
+        p[(kBxP + 3) * 64] = S3;
+        p[(kBxP + 4) * 64] = W;
+    }
+    __syncthreads();
+    if (wave > 0 || b >= B.nbins) return;
+    for (int w = 0; w < 3; ++w) {
+        const double* p = lds + (w * kTabSums) * 64 + lane;
+#pragma unroll
+        for (int n = 0; n < kBxP; ++n) A[n] += p[n * 64];
+        S0 += p[(kBxP + 0) * 64];
+        S1 += p[(kBxP + 1) * 64];
+        S2 += p[(kBxP + 2) * 64];
+        S3 += p[(kBxP + 3) * 64];
+        W += p[(kBxP + 4) * 64];
+    }
+    // e^y <= 1 + y + y^2 for 0 <= y <= 1.79, else exp(y) (1 + 1e-6)
+    const double Y = 2.0 * kap * D * r, eY = Y <= 1.5 ? fma(Y, Y, 1.0 + Y) : exp(Y) * 1.000001;
+    const double G = eY * S0;                                  // sum_k g e^y
+    const double Rb = eY * B.rP * kInvFact[kBxP] * S3;         // truncation (Lagrange)
+    const double ERR = eY * (((3.0 * kBxP + 10.0) * kU + 2.6e-14) * S0 + 4.0 * kU * S1 +
+                             2.0 * kap * (D + r) * (S2 + (D + r) * S0) * 0x1.0p-51);
     double* row = tab + (size_t)(B.tab_off + b) * kBxRow;
 #pragma unroll
     for (int n = 0; n < kBxP; ++n) row[n] = A[n];
-    // sums: each lane's sequential part (<= W terms) then 6 butterfly levels
+    // the sums: each wave's sequential sum, then 3 additions (of <= W terms)
     row[kBxP] = 1.02 * (Rb + ERR + (W + 6.0 + 2.0 * kBxP + 8.0) * kU * G) + 1e-300;
 }
 
@@ -345,12 +407,23 @@ __device__ __forceinline__ void gauss_bounds(const Comp<double>& r, double e0, d
     lo += ul > -4.0e6 ? exp_scaled(ul, etab) : 0.0;   // (below ~2^-980: 0 is a lower bound)
 }
 
-// P(a0 <= draw < a1) of one sampling component N(mu, sg) (draw space), in
-// fp32: the mass only steers tau0, never a bound
-__device__ __forceinline__ double normal_mass(double mu, double sg, double a0, double a1) {
-    const double s = 1.0 / (sg * 1.4142135623730951);
-    const float z0 = (float)((a0 - mu) * s), z1 = (float)((a1 - mu) * s);
-    return z0 > 0.0f ? 0.5 * (double)(erfcf(z0) - erfcf(z1)) : 0.5 * (double)(erfcf(-z1) - erfcf(-z0));
+// A below component, folded once per workgroup for gauss_bounds' arithmetic
+// (the same expressions, evaluated once instead of per sub-bin): c = c'/K,
+// kap = a'^2 / K, mu = m'/a', and eps = ec + es (|e0| + |e1| + |mu|) with
+// ec = 1e-15 (64 + |c|) + 3e-14, es = 64e-15 sqrt(kap)
+struct BelowTerm {
+    double c, kap, mu, ec, es;
+};
+constexpr int kStageBelow = 64;   // below components staged in LDS (more: read per sub-bin)
+
+__device__ __forceinline__ void term_bounds(const BelowTerm& t, double e0, double e1, double& lo, double& hi,
+                                            const double* __restrict__ etab) {
+    const double dn = t.mu < e0 ? e0 - t.mu : (t.mu > e1 ? t.mu - e1 : 0.0);
+    const double df = fmax(fabs(e0 - t.mu), fabs(e1 - t.mu));
+    const double eps = fma(t.es, fabs(e0) + fabs(e1) + fabs(t.mu), t.ec);
+    hi += exp_scaled((t.c - t.kap * dn * dn + eps) * kExpScale, etab);
+    const double ul = (t.c - t.kap * df * df - eps) * kExpScale;
+    lo += ul > -4.0e6 ? exp_scaled(ul, etab) : 0.0;   // (below ~2^-980: 0 is a lower bound)
 }
 
 // grid (ceil(max sub-bins / 256), dense labels): one sub-bin per thread --
@@ -363,22 +436,55 @@ __device__ __forceinline__ double normal_mass(double mu, double sg, double a0, d
 // components' na 2^-T on the upper side.  U, L: log ratio of the bounds plus
 // the shift difference, widened by 1e-7 (1 + |v|) and the fp64 round's own
 // error; +inf / -inf where a sum is not safely inside the normal range or a
-// record is unusable.
+// record is unusable.  The mass only steers tau0, never a bound: the
+// below mixture's density at the sub-bin's midpoint times its width (fp32;
+// a sub-bin is < 1/100 of the narrowest sampling sigma, so the midpoint
+// rule is within ~1e-5 relative).
 __global__ __launch_bounds__(kBlock) void k_bx_bounds(const DLabel* __restrict__ labels,
                                                       const int32_t* __restrict__ grp,
                                                       const Comp<double>* __restrict__ comps64,
                                                       const SampRec* __restrict__ samp,
                                                       const BxLabel* __restrict__ bx,
                                                       const double* __restrict__ tab,
-                                                      const int32_t* __restrict__ loff,
+                                                      const int32_t* __restrict__ cnt,
                                                       const int32_t* __restrict__ list,
                                                       float2* __restrict__ sb, float* __restrict__ sbp) {
     const int li = grp[blockIdx.y];
-    const DLabel L = labels[li];
     const BxLabel B = bx[li];
-    __shared__ double etab[kExpTabSize];
-    load_exp_table(etab);
     const int64_t nsb = (int64_t)B.nbins * kBxSub;
+    if ((int64_t)blockIdx.x * kBlock >= nsb) return;   // the whole workgroup
+    const DLabel L = labels[li];
+    __shared__ double etab[kExpTabSize];
+    __shared__ BelowTerm bt[kStageBelow];
+    __shared__ float4 sm[kStageBelow];   // sampling: mu, 1 / sigma, w / (sigma sqrt(2 pi)), -
+    __shared__ int bad;
+    if (threadIdx.x == 0) bad = 0;
+    for (int i = threadIdx.x; i < kExpTabSize; i += kBlock) etab[i] = kExp2Tab[i];
+    __syncthreads();
+    const bool staged_b = L.nb <= kStageBelow, staged_s = L.ns <= kStageBelow;
+    if (staged_b && threadIdx.x < L.nb) {
+        const Comp<double> r = comps64[L.comp_b + threadIdx.x];
+        BelowTerm t{-kInf, 0.0, 0.0, 0.0, 0.0};
+        if (usable(r)) {
+            t.c = r.c * kExpScaleInv;
+            t.kap = r.a * r.a * kExpScaleInv;
+            t.mu = r.mu / r.a;
+            t.ec = 1e-15 * (64.0 + fabs(t.c)) + 3e-14;
+            t.es = 1e-15 * 64.0 * sqrt(t.kap);
+        } else if (r.c > -kInf) {
+            atomicOr(&bad, 1);   // a weighted unusable record: no bound anywhere
+        }
+        bt[threadIdx.x] = t;
+    }
+    if (staged_s && threadIdx.x < L.ns) {
+        const SampRec s = samp[L.samp_off + threadIdx.x];
+        const double w = s.cdf - (threadIdx.x ? samp[L.samp_off + threadIdx.x - 1].cdf : 0.0);
+        const bool ok = w > 0.0 && s.sigma > 0.0 && s.sigma < kInf;
+        sm[threadIdx.x] = ok ? make_float4((float)(s.mu - L.centre), (float)(1.0 / s.sigma),
+                                           (float)(w / (s.sigma * 2.5066282746310002)), 0.0f)
+                             : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+    __syncthreads();
     const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (j >= nsb) return;
     const int b = (int)(j >> kBxSubBits);
@@ -391,28 +497,50 @@ __global__ __launch_bounds__(kBlock) void k_bx_bounds(const DLabel* __restrict__
     // sampling mass (steers tau0 only: nominal edges, bounded labels cut)
     double p = 0.0;
     {
-        double a0 = L.centre + e0n, a1 = L.centre + e1n;
+        double a0 = e0n, a1 = e1n;   // recentred draw space
         if ((L.flags & 3) == 3) {
-            a0 = fmax(a0, L.low);
-            a1 = fmin(a1, L.high);
+            a0 = fmax(a0, L.low - L.centre);
+            a1 = fmin(a1, L.high - L.centre);
         }
-        double prev = 0.0;
-        for (int k = 0; k < L.ns && a1 > a0; ++k) {
-            const SampRec s = samp[L.samp_off + k];
-            const double w = s.cdf - prev;
-            prev = s.cdf;
-            if (w > 0.0 && s.sigma > 0.0 && s.sigma < kInf) p += w * normal_mass(s.mu, s.sigma, a0, a1);
+        if (a1 > a0) {
+            const float xm = (float)(0.5 * (a0 + a1));
+            float dens = 0.0f;
+            if (staged_s) {
+                for (int k = 0; k < L.ns; ++k) {
+                    const float4 q = sm[k];
+                    const float z = (xm - q.x) * q.y;
+                    dens = fmaf(q.z, __expf(-0.5f * z * z), dens);
+                }
+            } else {
+                double prev = 0.0;
+                for (int k = 0; k < L.ns; ++k) {
+                    const SampRec s = samp[L.samp_off + k];
+                    const double w = s.cdf - prev;
+                    prev = s.cdf;
+                    if (!(w > 0.0 && s.sigma > 0.0 && s.sigma < kInf)) continue;
+                    const float z = (float)((xm - (s.mu - L.centre)) / s.sigma);
+                    dens += (float)(w / (s.sigma * 2.5066282746310002)) * __expf(-0.5f * z * z);
+                }
+            }
+            p = (double)dens * (a1 - a0);
         }
     }
-    bool ok = true;
+    bool ok = bad == 0;
     double blo = 0.0, bhi = 0.0;
-    for (int k = 0; k < L.nb; ++k) {
-        const Comp<double> r = comps64[L.comp_b + k];
-        if (!usable(r)) {
-            ok = ok && !(r.c > -kInf);
-            continue;
+    if (staged_b) {
+        for (int k = 0; k < L.nb; ++k) {
+            const BelowTerm t = bt[k];
+            if (t.c > -kInf) term_bounds(t, e0, e1, blo, bhi, etab);
         }
-        gauss_bounds(r, e0, e1, blo, bhi, etab);
+    } else {
+        for (int k = 0; k < L.nb; ++k) {
+            const Comp<double> r = comps64[L.comp_b + k];
+            if (!usable(r)) {
+                ok = ok && !(r.c > -kInf);
+                continue;
+            }
+            gauss_bounds(r, e0, e1, blo, bhi, etab);
+        }
     }
     // clipped above components: the bin's polynomial around the sub-bin centre
     const double xb = B.xlo + ((double)b + 0.5) * B.bw;
@@ -447,9 +575,10 @@ __global__ __launch_bounds__(kBlock) void k_bx_bounds(const DLabel* __restrict__
     const double emin = exp(-B.kappa * dmax * dmax) * (1.0 - 1e-14);
     double slo = alo > 0.0 ? emin * alo : 0.0, shi = ahi > 0.0 ? emax * ahi : 0.0;
     const Comp<double>* ca = comps64 + L.comp_a;
-    const int j0 = loff[B.cnt_off + b], j1 = loff[B.cnt_off + b + 1];
-    for (int jj = j0; jj < j1; ++jj) {
-        const Comp<double> r = ca[list[B.list_off + jj]];
+    const int32_t* lst = list + B.list_off + (int64_t)b * B.n_nc;
+    const int m = cnt[B.cnt_off + b];
+    for (int jj = 0; jj < m; ++jj) {
+        const Comp<double> r = ca[lst[jj]];
         if (!usable(r)) {
             ok = ok && !(r.c > -kInf);
             continue;
@@ -461,12 +590,13 @@ __global__ __launch_bounds__(kBlock) void k_bx_bounds(const DLabel* __restrict__
     const double mag = fabs(L.shift_b) + fabs(L.shift_a) + 2.0 * (fabs(L.centre) + fabs(e0) + fabs(e1)) + 64.0;
     const double fe = (double)(L.nb + L.na + 64) * 0x1.0p-50 + mag * 0x1.0p-48;
     double U = kInf, Lo = -kInf;
+    // (flog: <= 1 ulp, far inside the 1e-7 widening)
     if (ok && bhi >= 1e-280 && slo >= 1e-280) {
-        const double v = log(bhi) - log(slo) + dsh;
+        const double v = flog(bhi) - flog(slo) + dsh;
         if (v == v) U = v + 1e-7 * (1.0 + fabs(v)) + fe;
     }
     if (ok && blo >= 1e-280 && shi > 0.0 && shi < kInf) {
-        const double v = log(blo) - log(shi) + dsh;
+        const double v = flog(blo) - flog(shi) + dsh;
         if (v == v) Lo = v - 1e-7 * (1.0 + fabs(v)) - fe;
     }
     if (!(U == U) || !(Lo == Lo) || U < Lo) {
@@ -491,7 +621,8 @@ int tpe_rt::bx_prepare(tpe_ctx* ctx) {
     return rc;
 }
 
-// the tables, lists and sub-bin bounds of every dense label (bx_prepare)
+// the tables, lists and sub-bin bounds of every dense label (bx_prepare):
+// one host round trip (the per-label scan decides the bins and the layout)
 int tpe_rt::bx_build(tpe_ctx* ctx) {
     tpe_rt::Posterior& P = *ctx->P;
     P.bx_ok = false;
@@ -511,10 +642,11 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
     HIPCHK(ctx, hipMemcpyAsync(sc.data(), P.bx_scan.p, sc.size() * sizeof(double), hipMemcpyDeviceToHost,
                                ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    // bins per label
+    // bins per label: the fewest (a multiple of 64) whose half-width keeps
+    // the Taylor argument 2 kappa |d| r <= ~0.5 over the window
     P.bx_h.assign(P.n_labels, BxLabel{});
     bool ok = true;
-    int64_t rows = 0, cnts = 0;
+    int64_t rows = 0, lsum = 0;
     int32_t bins_max = 0;
     for (int y = 0; y < nl; ++y) {
         const int li = y < (int)gg.size() ? gg[y] : gl[y - gg.size()];
@@ -535,9 +667,8 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
             ok = false;
             break;
         }
-        int32_t nb = kMinBins;
-        while ((double)nb < want) nb <<= 1;
-        if ((int64_t)nb * std::max(n_nc, 1) > ((int64_t)1 << 27)) {   // list build cost
+        const int32_t nb = std::max<int32_t>(kMinBins, ((int32_t)std::ceil(want) + 63) / 64 * 64);
+        if ((int64_t)nb * n_nc > ((int64_t)1 << 27)) {   // list build cost
             ok = false;
             break;
         }
@@ -552,52 +683,36 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
         B.nbins = nb;
         B.n_nc = n_nc;
         B.inv_sbw = (double)kBxSub / B.bw;
-        B.sb_off = rows * kBxSub;
+        B.sb_off = rows * kBxSub;   // (nb a multiple of 64: a multiple of 32, as k_hot_bx needs)
         B.tab_off = rows;
-        B.cnt_off = cnts;
+        B.cnt_off = rows;           // one list count per bin
+        B.list_off = lsum;          // nb slots of n_nc entries
         rows += nb;
-        cnts += nb + 1;
+        lsum += (int64_t)nb * n_nc;
         bins_max = std::max(bins_max, nb);
         P.bx_h[li] = B;
     }
+    if (ok && lsum > ((int64_t)1 << 28)) ok = false;   // > 1 GB of list slots
     if (!ok) {
         P.bx_ready = true;   // not eligible: the windowed screen runs
         return TPE_OK;
     }
     HIPCHK(ctx, P.bx.reserve(P.n_labels));
     HIPCHK(ctx, P.bx_tab.reserve((size_t)rows * kBxRow));
-    HIPCHK(ctx, P.bx_loff.reserve((size_t)cnts));
-    HIPCHK(ctx, P.bx_nc.reserve(P.comps64.cap));
-    HIPCHK(ctx, hipMemcpyAsync(P.bx.p, P.bx_h.data(), P.n_labels * sizeof(BxLabel), hipMemcpyHostToDevice,
-                               ctx->stream));
-    const dim3 gb((unsigned)((bins_max + kBlock - 1) / kBlock), nl);
-    hipLaunchKernelGGL(k_bx_compact, dim3(nl), dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p,
-                       P.bx.p, P.bx_nc.p);
-    hipLaunchKernelGGL(k_bx_list<false>, gb, dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p,
-                       P.bx.p, P.bx_nc.p, P.bx_loff.p, nullptr);
-    int64_t* tot = reinterpret_cast<int64_t*>(P.bx_scan.p);   // the scan is read: reuse it
-    hipLaunchKernelGGL(k_bx_offsets, dim3(nl), dim3(kBlock), 0, ctx->stream, grp, P.bx.p, P.bx_loff.p, tot);
-    HIPCHK(ctx, hipGetLastError());
-    std::vector<int64_t> tot_h(nl);
-    HIPCHK(ctx, hipMemcpyAsync(tot_h.data(), tot, nl * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-    int64_t lsum = 0;
-    for (int y = 0; y < nl; ++y) {
-        const int li = y < (int)gg.size() ? gg[y] : gl[y - gg.size()];
-        if (tot_h[y] > ((int64_t)1 << 30)) return ctx->fail(TPE_ERR_ARG, "expansion screen: lists too long");
-        P.bx_h[li].list_off = lsum;
-        lsum += tot_h[y];
-    }
+    HIPCHK(ctx, P.bx_loff.reserve((size_t)rows));
     HIPCHK(ctx, P.bx_list.reserve((size_t)std::max<int64_t>(lsum, 1)));
-    HIPCHK(ctx, hipMemcpyAsync(P.bx.p, P.bx_h.data(), P.n_labels * sizeof(BxLabel), hipMemcpyHostToDevice,
-                               ctx->stream));
-    hipLaunchKernelGGL(k_bx_list<true>, gb, dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p,
-                       P.bx.p, P.bx_nc.p, P.bx_loff.p, P.bx_list.p);
-    const dim3 gt((unsigned)((bins_max + kBlock / 64 - 1) / (kBlock / 64)), nl);
-    hipLaunchKernelGGL(k_bx_table, gt, dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p, P.bx.p,
-                       P.bx_tab.p);
+    HIPCHK(ctx, P.bx_nc.reserve(P.comps64.cap));
     HIPCHK(ctx, P.bx_sb.reserve((size_t)rows * kBxSub));
     HIPCHK(ctx, P.bx_sbp.reserve((size_t)rows * kBxSub));
+    HIPCHK(ctx, hipMemcpyAsync(P.bx.p, P.bx_h.data(), P.n_labels * sizeof(BxLabel), hipMemcpyHostToDevice,
+                               ctx->stream));
+    hipLaunchKernelGGL(k_bx_compact, dim3(nl), dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p,
+                       P.bx.p, P.bx_nc.p);
+    const dim3 gb((unsigned)((bins_max + kBlock - 1) / kBlock), nl);
+    hipLaunchKernelGGL(k_bx_list, gb, dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p, P.bx.p,
+                       P.bx_nc.p, P.bx_loff.p, P.bx_list.p);
+    hipLaunchKernelGGL(k_bx_table, dim3((unsigned)((bins_max + 63) / 64), nl), dim3(kBlock), 0, ctx->stream,
+                       P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p);
     P.bx_sb_max = (int64_t)bins_max * kBxSub;
     static uint64_t gen_counter = 0;   // unique over every posterior of the process
     P.bx_gen = __atomic_add_fetch(&gen_counter, 1, __ATOMIC_RELAXED);

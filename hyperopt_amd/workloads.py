@@ -85,6 +85,50 @@ class History(object):
         prior_weight: see posterior.device_inputs)."""
         return P.device_inputs(self.labels, self.tids, self.losses, self.obs)
 
+    def prefix(self, n):
+        """The history of the first n trials (tids 0..n-1)."""
+        obs = {}
+        for name, (oi, ov) in self.obs.items():
+            k = int(np.searchsorted(oi, n))
+            obs[name] = (oi[:k], ov[:k])
+        return History(self.labels, self.tids[:n], self.losses[:n], obs)
+
+
+class FminLoop(object):
+    """The device side of fmin's serial loop over a synthetic history: each
+    `advance` appends the next trials (their losses and observations) and
+    rebuilds the posterior the way tpe.suggest does past
+    DEVICE_BUILD_MIN_OBS -- the device-resident history takes only the new
+    observations (DeviceHistoryUploader), the device builder splits, sorts,
+    fits the Parzen mixtures and folds the records, with numpy's np.argsort
+    tie order for the labels whose mixtures depend on it
+    (posterior.build_reference_order).  The view tuple is the one
+    history.device_view hands tpe.suggest."""
+
+    def __init__(self, hist, gamma=0.25, prior_weight=1.0):
+        self.hist = hist
+        self.gamma, self.prior_weight = gamma, prior_weight
+        self.names = [n for n, _, _ in hist.labels]
+        self.uploader = P.DeviceHistoryUploader()
+        self.n = 0
+
+    def view(self, n):
+        obs = {}
+        for name in self.names:
+            oi, ov = self.hist.obs[name]
+            k = int(np.searchsorted(oi, n))
+            obs[name] = (oi[:k], ov[:k])
+        losses = self.hist.losses[:n]
+        return (self.hist.tids[:n], losses, int(np.count_nonzero(losses == losses)), obs, self)
+
+    def advance(self, eng, n):
+        """History of the first n trials on the device, posterior rebuilt;
+        returns n_below."""
+        if n > len(self.hist.tids):
+            raise ValueError('the synthetic history holds %d trials' % len(self.hist.tids))
+        self.n = n
+        return self.uploader.build(eng, self.hist.labels, self.view(n), self.gamma, self.prior_weight)
+
 
 def mixed_space(n_labels):
     return [('x%03d' % i,) + CYCLE[i % 5] for i in range(n_labels)]
