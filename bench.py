@@ -304,7 +304,8 @@ def main():
 
     def step(i, fresh):
         if fresh:
-            loop.advance(eng, args.trials + (i + 1) * args.append)
+            loop.advance(eng, args.trials + (i + 1) * args.append,
+                         n_candidates=C if args.config != 5 and args.precision == 'f64' else 0)
         if args.config == 5:   # independent new_ids split over the GPUs
             ids = [i * args.new_ids + rank * ids_local + k for k in range(ids_local)]
             res = eng.suggest_batch(seed=1234, rounds=ids, n_candidates=C)

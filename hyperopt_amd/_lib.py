@@ -47,6 +47,8 @@ TPE_OPT_WIN_T = 9
 TPE_OPT_WIN_GROUPS = 10
 TPE_OPT_EXPAND = 11
 TPE_OPT_HOT = 12
+TPE_OPT_EARLY = 13
+TPE_OPT_HOT_DIV = 14
 
 TPE_OBS_IDENTITY = 0
 TPE_OBS_LOG = 1
@@ -123,6 +125,8 @@ SIGNATURES = {
     'tpe_set_option': (ctypes.c_int, [_P, _I32, _I64]),
     'tpe_last_screen_terms': (ctypes.c_int, [_P, _P]),
     'tpe_last_rescore_terms': (ctypes.c_int, [_P, _P]),
+    'tpe_last_drawn': (ctypes.c_int, [_P, _P, _P]),
+    'tpe_prepare': (ctypes.c_int, [_P, ctypes.c_int64]),
     'tpe_last_screen_mode': (ctypes.c_int32, [_P]),
     'tpe_last_hot': (ctypes.c_int, [_P, _P, _P]),
     'tpe_last_prepare': (ctypes.c_int, [_P, _P]),

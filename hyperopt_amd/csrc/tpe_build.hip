@@ -1416,6 +1416,10 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     HIPCHK(ctx, hipMemcpyAsync(&errh, ctx->errflag.p, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     if (ties_out)
         HIPCHK(ctx, hipMemcpyAsync(ties_out, B.ties.p, (n_labels + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    {   // does the expansion index of the previous posterior still hold?
+        const int rc = tpe_rt::bx_keep_check(ctx);
+        if (rc) return rc;
+    }
     HIPCHK(ctx, hipStreamSynchronize(st));
     HIPCHK(ctx, hipEventElapsedTime(&ctx->build_ms, ctx->ev0, ctx->ev1));
     if (errh & 1) return ctx->fail(TPE_ERR_ARG, "observation trial position out of range");
@@ -1429,14 +1433,18 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
         cat.insert(cat.end(), grp[m].begin(), grp[m].end());
         P.h_group[m] = grp[m];
     }
-    if (cat != P.groups_h || !P.groups.p) {   // unchanged between rebuilds of one history
+    const bool groups_changed = cat != P.groups_h || !P.groups.p;
+    if (groups_changed) {   // unchanged between rebuilds of one history
         HIPCHK(ctx, P.groups.reserve(std::max<size_t>(cat.size(), 1)));
         HIPCHK(ctx, hipMemcpy(P.groups.p, cat.data(), cat.size() * sizeof(int32_t), hipMemcpyHostToDevice));
         P.groups_h = cat;
     }
     P.h_labels = dl;
     P.win_ready = false;
-    P.bx_ready = false;
+    // the index is kept when every dense label came out bit-identical (e.g.
+    // a second build of the same history that only supplies the tie order
+    // of quantized labels)
+    P.bx_ready = tpe_rt::bx_keep_after(ctx, groups_changed);
     P.n_labels = n_labels;
     B.n_labels = n_labels;
     B.mix_h = mix;

@@ -34,6 +34,7 @@ struct QInfo {
     int64_t jmin;
     int64_t G;        // table slots; 0 = evaluate every candidate directly
     int64_t tab_off;
+    int64_t jlo, jhi;  // every grid index a candidate can take lies in [jlo, jhi] (empty: unknown)
     int64_t pad;
 };
 
@@ -41,13 +42,23 @@ template <typename T>
 struct DevBuf {
     T* p = nullptr;
     size_t cap = 0;
+    // grows by at least 1/4 (a history that grows by one trial per call
+    // would otherwise reallocate -- and hipFree synchronise the device --
+    // on every build); the contents are not kept
     hipError_t reserve(size_t n) {
         if (n <= cap) return hipSuccess;
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
-        hipError_t e = hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T));
-        if (e == hipSuccess) cap = std::max<size_t>(n, 1);
+        const size_t want = std::max<size_t>(n, 1), grown = want + want / 4;
+        hipError_t e = hipMalloc(&p, grown * sizeof(T));
+        if (e == hipSuccess) {
+            cap = grown;
+            return e;
+        }
+        (void)hipGetLastError();   // (clear the failed allocation) exactly n, then
+        e = hipMalloc(&p, want * sizeof(T));
+        if (e == hipSuccess) cap = want;
         return e;
     }
     void release() {
@@ -55,6 +66,24 @@ struct DevBuf {
         p = nullptr;
         cap = 0;
     }
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : p(o.p), cap(o.cap) {
+        o.p = nullptr;
+        o.cap = 0;
+    }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        if (this != &o) {
+            release();
+            p = o.p;
+            cap = o.cap;
+            o.p = nullptr;
+            o.cap = 0;
+        }
+        return *this;
+    }
+    ~DevBuf() { release(); }   // (every buffer a context holds goes with it)
 };
 
 struct Posterior {
@@ -96,6 +125,16 @@ struct Posterior {
     DevBuf<float> bx_sbp;                //   and the below mixture's sampling mass of it
     int64_t bx_sb_max = 0;               //   the most sub-bins of one label
     uint64_t bx_gen = 0;                 // bumped by every build of the tables (never 0 once built)
+    // what the index was built from (the dense labels' DLabel, records and
+    // sampling records, at the same offsets): a rebuild of the posterior that
+    // leaves them bit-identical keeps the index (bx_keep_check)
+    DevBuf<tpe::DLabel> bx_snap_l;
+    DevBuf<tpe::Comp<double>> bx_snap_c;
+    DevBuf<tpe::SampRec> bx_snap_s;
+    DevBuf<int32_t> bx_snap_g;           // the dense label positions
+    DevBuf<int32_t> bx_diff;             // compare result (0: identical)
+    int32_t bx_diff_h = 1;
+    int32_t bx_snap_nl = 0;
     void release() {
         labels.release();
         comps64.release();
@@ -123,6 +162,12 @@ struct Posterior {
         bx_scan.release();
         bx_sb.release();
         bx_sbp.release();
+        bx_snap_l.release();
+        bx_snap_c.release();
+        bx_snap_s.release();
+        bx_snap_g.release();
+        bx_diff.release();
+        bx_snap_nl = 0;
         bx_ready = bx_ok = false;
         n_labels = 0;
     }
@@ -238,6 +283,12 @@ struct tpe_ctx {
     DevBuf<unsigned long long> qmm;
     DevBuf<QInfo> qinfo;
     DevBuf<double2> qtab;
+    DevBuf<unsigned long long> qkmax;    // per quantized label: the best score key over [jlo, jhi]
+    DevBuf<int64_t> xfound;              // per (round, label) cell: the first candidate index found
+                                         // holding its label's best drawable score (early exit)
+    DevBuf<unsigned long long> xdrawn;   // candidates the early-exit kernels drew: quantized, categorical
+    unsigned long long xdrawn_h[2] = {0, 0};
+    bool cat_early = false;              // the last round's categorical labels ran k_cat_tiles
     DevBuf<double> xs, slice_part;       // split-K map: candidates, slice sums
     bool splitk = true;                  // split-K for small sampled rounds
     DevBuf<double> chunk_part;           // chunked packed map: x | below sum | above chunk sums
@@ -252,6 +303,8 @@ struct tpe_ctx {
     bool expand = true;                  // TPE_OPT_EXPAND: expansion screen when eligible
     // hot-bin prefilter of the expansion screen (TPE_OPT_HOT, tpe_device.h)
     int32_t hot = 1;                     // 0 off, 1 on, 2 test: force the fallback
+    bool early = true;                   // early exit of quantized / categorical tile rounds
+    double hot_cap_div = 16.0;           // hot lists hold n / hot_cap_div per cell (shrinks on overflow)
     DevBuf<double> hot_x;                // per cell: listed candidates' x
     DevBuf<int32_t> hot_i, hot_cnt;      //   their indices; per cell the count
     DevBuf<unsigned long long> hot_t, hot_tau0;   // per cell largest L; per label tau0
@@ -262,7 +315,9 @@ struct tpe_ctx {
     int64_t hot_listed = 0;              // last round: candidates the prefilter listed
     int32_t hot_fallback = 0;            // last round: 1 if it re-ran the plain screen
     bool hot_ran = false;
-    float prep_ms = 0.f;                 // wall ms of the last expansion-index build (bx_prepare)
+    float prep_ms = 0.f;                 // device ms of the last expansion-index build (bx_prepare)
+    hipEvent_t ev_prep[2] = {};          //   its bracket, read when asked (tpe_last_prepare)
+    bool prep_pending = false;
     uint64_t hot_tau0_gen = 0;           // hot_tau0 holds tau0 of this table generation
     int64_t hot_tau0_n = 0;              //   and this n
     DevBuf<int32_t> scr_idx;
@@ -378,6 +433,11 @@ int64_t win_rounds_per_batch(int64_t n, int32_t nl);
 // posterior) and sets P->bx_ok when every dense label has one.
 int bx_prepare(tpe_ctx* ctx);
 int bx_build(tpe_ctx* ctx);
+// Before a rebuild's final sync: queue the comparison of the rebuilt dense
+// labels against the index's snapshot (result in P.bx_diff_h after the
+// sync); bx_keep_after: whether the index stays valid.
+int bx_keep_check(tpe_ctx* ctx);
+bool bx_keep_after(tpe_ctx* ctx, bool groups_changed);
 }  // namespace tpe_rt
 
 // per-device implementations of the entry points a multi-device context
@@ -393,6 +453,7 @@ TPE_DEV int tpe1_suggest_batch(tpe_ctx* ctx, uint64_t seed, const uint32_t* roun
                                int32_t n_rounds, int64_t n_candidates, int64_t cand_offset,
                                tpe_label_result* out);
 TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value);
+TPE_DEV int tpe1_prepare(tpe_ctx* ctx, int64_t n_candidates);
 TPE_DEV int tpe1_history_reset(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
                                const double* cat_p, int64_t n_cat_p);
 TPE_DEV int tpe1_history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial,

@@ -621,7 +621,7 @@ __device__ __forceinline__ int bx_score(const DLabel& L, const BxLabel& B,
 template <int R>
 __device__ __forceinline__ void bx_append(const double (&hv)[R], const bool (&valid)[R],
                                           const int64_t (&ci)[R], uint64_t bk, int nterms, size_t cell,
-                                          int64_t n, double* __restrict__ hi,
+                                          int64_t stride, double* __restrict__ hi,
                                           unsigned long long* __restrict__ lbkey, int32_t* __restrict__ cnt,
                                           int32_t* __restrict__ idx, unsigned long long* __restrict__ terms) {
     __shared__ uint64_t sh[kBlock / 64];
@@ -654,8 +654,8 @@ __device__ __forceinline__ void bx_append(const double (&hv)[R], const bool (&va
 #pragma unroll
     for (int r = 0; r < R; ++r)
         if (take[r]) {
-            idx[cell * (size_t)n + at] = (int32_t)ci[r];
-            hi[cell * (size_t)n + at] = hv[r];
+            idx[cell * (size_t)stride + at] = (int32_t)ci[r];
+            hi[cell * (size_t)stride + at] = hv[r];
             ++at;
         }
     __shared__ int shn[kBlock / 64];
@@ -701,7 +701,7 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
     unsigned long long* __restrict__ lbkey, int32_t* __restrict__ cnt, int32_t* __restrict__ idx,
     unsigned long long* __restrict__ terms,
     int32_t* __restrict__ err, Slots S, const double* __restrict__ cand_in,
-    double* __restrict__ s_out, double* __restrict__ e_out, double2* __restrict__ lohi) {
+    double* __restrict__ s_out, double* __restrict__ e_out, double2* __restrict__ lohi, int64_t stride) {
     const int li = group[blockIdx.y];
     const DLabel L = labels[li];
     const BxLabel B = bx[li];
@@ -744,7 +744,7 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
         double hv[R];
         uint64_t bk = 0;
         bx_bounds<R>(s, E, valid, hv, bk);
-        bx_append<R>(hv, valid, ci, bk, nterms, (size_t)blockIdx.z * nl + blockIdx.y, n, hi, lbkey, cnt, idx,
+        bx_append<R>(hv, valid, ci, bk, nterms, (size_t)blockIdx.z * nl + blockIdx.y, stride, hi, lbkey, cnt, idx,
                      terms);
     }
 }
@@ -819,7 +819,8 @@ __global__ __launch_bounds__(kBlock, 4) void k_hot_bx(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
     const BxLabel* __restrict__ bx, const uint32_t* __restrict__ hbits, int64_t n, int64_t cand_offset,
     uint64_t seed, const uint32_t* __restrict__ rounds, int32_t nl, int32_t* __restrict__ hcnt,
-    int32_t* __restrict__ hidx, double* __restrict__ hx, int32_t* __restrict__ err) {
+    int32_t* __restrict__ hidx, double* __restrict__ hx, int32_t* __restrict__ err, int64_t hstride,
+    int32_t* __restrict__ hflag) {
     const int li = group[blockIdx.y];
     const DLabel L = labels[li];
     const BxLabel B = bx[li];
@@ -891,11 +892,16 @@ __global__ __launch_bounds__(kBlock, 4) void k_hot_bx(
         int at = shb + tw - mine;
         for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) at += shc[w];
         __syncthreads();   // shc / shb are rewritten by the next tile
+        // a cell's list is hstride long: past it the round falls back to
+        // screening every candidate (hflag bit 2), so nothing is lost
+        if (at + mine > hstride) atomicOr(hflag, 2);
 #pragma unroll
         for (int r = 0; r < R; ++r)
             if (take[r]) {
-                hidx[cell * (size_t)n + at] = (int32_t)ci[r];
-                hx[cell * (size_t)n + at] = x[r];
+                if (at < hstride) {
+                    hidx[cell * (size_t)hstride + at] = (int32_t)ci[r];
+                    hx[cell * (size_t)hstride + at] = x[r];
+                }
                 ++at;
             }
     }
@@ -912,9 +918,9 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
     const int32_t* __restrict__ hcnt, const int32_t* __restrict__ hidx, const double* __restrict__ hx,
     double* __restrict__ hi, unsigned long long* __restrict__ lbkey, int32_t* __restrict__ cnt,
     int32_t* __restrict__ idx, unsigned long long* __restrict__ terms, const float2* __restrict__ sb,
-    unsigned long long* __restrict__ tkey) {
+    unsigned long long* __restrict__ tkey, int64_t hstride) {
     const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
-    const int64_t m = hcnt[cell];
+    const int64_t m = min((int64_t)hcnt[cell], hstride);   // (an overflowed list falls back anyway)
     constexpr int64_t per = (int64_t)R * kBlock;
     if ((int64_t)blockIdx.x * per >= m) return;   // uniform over the workgroup
     const int li = group[blockIdx.y];
@@ -933,9 +939,9 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
         for (int r = 0; r < R; ++r) {
             const int64_t j = j0 + r * kBlock + threadIdx.x;
             valid[r] = j < m;
-            const double d = valid[r] ? hx[cell * (size_t)n + j] : 0.0;   // the raw draw
+            const double d = valid[r] ? hx[cell * (size_t)hstride + j] : 0.0;   // the raw draw
             x[r] = lgmm ? lgmm_value(d) : d;
-            ci[r] = valid[r] ? hidx[cell * (size_t)n + j] : 0;
+            ci[r] = valid[r] ? hidx[cell * (size_t)hstride + j] : 0;
             const double f = (d - L.centre - B.xlo) * B.inv_sbw;   // k_hot_bx's sub-bin
             if (valid[r] && f >= 0.0 && f < (double)nsb) {
                 const uint64_t k = order_key((double)sb[B.sb_off + (int64_t)f].y);
@@ -946,7 +952,7 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
         const int nterms = bx_score<R>(L, B, comps64, tab, loff, list, exp_tab, x, valid, s, E);
         uint64_t bk = 0;
         bx_bounds<R>(s, E, valid, hv, bk);
-        bx_append<R>(hv, valid, ci, bk, nterms, cell, n, hi, lbkey, cnt, idx, terms);
+        bx_append<R>(hv, valid, ci, bk, nterms, cell, hstride, hi, lbkey, cnt, idx, terms);
     }
     __shared__ uint64_t shk[kBlock / 64];
     kl = block_max_key(kl, shk);
@@ -994,14 +1000,14 @@ __global__ __launch_bounds__(kBlock) void k_hot_check(int64_t cells, int32_t nl,
 // every candidate whose bound reached its workgroup's best lower bound;
 // keep those that reach the cell's (the round's) best, compacted in place.
 // One workgroup per cell; chunks in order, so writes never pass reads.
-__global__ __launch_bounds__(kBlock) void k_select_list(const double* __restrict__ hi, int64_t n,
+__global__ __launch_bounds__(kBlock) void k_select_list(const double* __restrict__ hi, int64_t stride,
                                                         const unsigned long long* __restrict__ lbkey,
                                                         int32_t* __restrict__ cnt, int32_t* __restrict__ idx) {
     const size_t cell = blockIdx.x;
     const uint64_t lb = lbkey[cell];
     const int len = cnt[cell];
-    int32_t* il = idx + cell * (size_t)n;
-    const double* hl = hi + cell * (size_t)n;
+    int32_t* il = idx + cell * (size_t)stride;
+    const double* hl = hi + cell * (size_t)stride;
     __shared__ int shc[kBlock / 64];
     int out = 0;
     for (int j0 = 0; j0 < len; j0 += kBlock) {
@@ -1136,7 +1142,7 @@ constexpr int kCatR = 8;  // candidates per thread, k_cat_tiles
 template <int R>
 __global__ __launch_bounds__(kBlock) void k_rescore(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
-    const Comp<double>* __restrict__ comps64, const SampRec* __restrict__ samp, int64_t n,
+    const Comp<double>* __restrict__ comps64, const SampRec* __restrict__ samp, int64_t stride,
     int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, int32_t nl,
     int32_t n_labels, int32_t tiles, const int32_t* __restrict__ cnt, const int32_t* __restrict__ idx,
     const RescoreChunk* __restrict__ chunks, Partial* __restrict__ res) {
@@ -1150,7 +1156,7 @@ __global__ __launch_bounds__(kBlock) void k_rescore(
     __shared__ double exp_tab[kExpTabSize];
     load_exp_table(exp_tab);
     const bool lgmm = L.mode == DENSE_LGMM;
-    const int32_t* list = idx + (size_t)ch.cell * (size_t)n;
+    const int32_t* list = idx + (size_t)ch.cell * (size_t)stride;
     const uint32_t rk = rounds[z];
     uint64_t bk = 0;
     int64_t bi = INT64_MAX;
@@ -1207,7 +1213,7 @@ constexpr int kRsW = 64;
 
 __global__ __launch_bounds__(kBlock) void k_rescore_draw(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
-    const SampRec* __restrict__ samp, int64_t n, int64_t cand_offset, uint64_t seed,
+    const SampRec* __restrict__ samp, int64_t stride, int64_t cand_offset, uint64_t seed,
     const uint32_t* __restrict__ rounds, int32_t nl, int32_t n_entries, const int32_t* __restrict__ cnt,
     const int32_t* __restrict__ idx, const RescoreChunk* __restrict__ chunks, double* __restrict__ xbuf,
     int64_t* __restrict__ gbuf) {
@@ -1220,7 +1226,7 @@ __global__ __launch_bounds__(kBlock) void k_rescore_draw(
     double v = __builtin_nan("");
     int64_t g = -1;
     if (j < cnt[ch.cell]) {
-        g = cand_offset + idx[(size_t)ch.cell * (size_t)n + j];
+        g = cand_offset + idx[(size_t)ch.cell * (size_t)stride + j];
         if (L.mode == DENSE_LGMM) (void)sample_below<DENSE_LGMM>(L, samp + L.samp_off, seed, rounds[z], (uint32_t)g, v);
         else (void)sample_below<DENSE_GMM>(L, samp + L.samp_off, seed, rounds[z], (uint32_t)g, v);
     }
@@ -1826,7 +1832,7 @@ template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_qtable(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
     const Comp<double>* __restrict__ comps64, const QInfo* __restrict__ qinfo, int32_t nq,
-    int32_t qbase, double2* __restrict__ tab) {
+    int32_t qbase, double2* __restrict__ tab, unsigned long long* __restrict__ qkmax) {
     const int li = group[blockIdx.y];
     const DLabel L = labels[li];
     const QInfo Q = qinfo[qbase + blockIdx.y];
@@ -1850,7 +1856,10 @@ __global__ __launch_bounds__(kBlock) void k_qtable(
             pb += wp[w].x;
             pa += wp[w].y;
         }
-        tab[Q.tab_off + s] = make_double2(flog(pb) - L.logpacc_b, flog(pa) - L.logpacc_a);
+        const double2 v = make_double2(flog(pb) - L.logpacc_b, flog(pa) - L.logpacc_a);
+        tab[Q.tab_off + s] = v;
+        const int64_t j = Q.jmin + s;
+        if (qkmax && j >= Q.jlo && j <= Q.jhi) atomicMax(qkmax + qbase + blockIdx.y, order_key(v.x - v.y));
     }
 }
 
@@ -1964,26 +1973,68 @@ __device__ __noinline__ double2 quant_pair_direct(const Comp<double>* __restrict
     return make_double2(quant_lpdf<LOG>(cb, nb, ub, lo, lpb), quant_lpdf<LOG>(ca, na, ub, lo, lpa));
 }
 
+// Exact early exit of a round whose scores take few values (quantized and
+// categorical labels): kmax = the best score key any drawable candidate can
+// have.  Once a candidate of index f holds kmax, no candidate after f can win
+// (a later equal score loses the tie), so a workgroup stops at the first tile
+// starting past found[cell] = the smallest such f reported so far; every
+// candidate before the true first kmax index is still processed (its tile
+// starts before any reported f), so the block maxloc over what was
+// processed is the np.argmax winner.  found only decreases; a stale read
+// only costs work.  The stop test is made uniform over the workgroup.
+__device__ __forceinline__ bool tile_stop(const int64_t* __restrict__ found, int64_t gbase, int64_t* sh) {
+    if (threadIdx.x == 0) *sh = __hip_atomic_load(found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const bool stop = *sh <= gbase;
+    __syncthreads();
+    return stop;
+}
+
+// A workgroup of an early-exit launch whose first tile already lies past the
+// cell's find does nothing but empty its partial slot (and its share of the
+// slots after the launch's): the second phase's grid costs little once the
+// first phase has found the winner.  Uniform over the workgroup.
+__device__ __forceinline__ bool early_out(const int64_t* __restrict__ fcell, int64_t gfirst, Partial* prow,
+                                          int32_t slot, int32_t tiles, int32_t empty_from, int64_t* sh) {
+    if (threadIdx.x == 0) *sh = __hip_atomic_load(fcell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*sh > gfirst) return false;
+    for (int64_t t = (int64_t)empty_from + blockIdx.x + (int64_t)threadIdx.x * gridDim.x; t < tiles;
+         t += (int64_t)kBlock * gridDim.x)
+        prow[t] = Partial{0, INT64_MAX, 0.0, 0.0, 0.0};
+    if (threadIdx.x == 0) prow[slot] = Partial{0, INT64_MAX, 0.0, 0.0, 0.0};
+    return true;
+}
+
 // k_qfused for the tile map with workgroups striding over the tiles of
-// R * 256 candidates (the sampling records staged once per workgroup, a
-// running best per thread): the block's winner goes to partial slot
-// blockIdx.x and the workgroup empties the slots t = blockIdx.x + k gridDim.x
-// beyond the grid, so k_reduce sees every tile slot.  Same candidates,
-// values and winner as k_qfused.
+// R * 256 candidates from candidate i0 on (the sampling records staged once
+// per workgroup, a running best per thread): the block's winner goes to
+// partial slot slot_base + blockIdx.x, and the workgroups empty the slots from
+// empty_from on, so k_reduce sees every tile slot.  Same candidates, values
+// and winner as k_qfused; with kmax (bounded labels, qkmax) the early exit
+// above.
 template <int MODE, int R>
 __global__ __launch_bounds__(kBlock, 4) void k_qfused_tiles(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
     const Comp<double>* __restrict__ comps64, const SampRec* __restrict__ samp,
     const QInfo* __restrict__ qinfo, const double2* __restrict__ tab, int64_t n, int64_t cand_offset,
     uint64_t seed, const uint32_t* __restrict__ rounds, int32_t qbase, int32_t n_labels, int32_t tiles,
-    Partial* __restrict__ partials, int32_t* __restrict__ err) {
+    Partial* __restrict__ partials, int32_t* __restrict__ err, const unsigned long long* __restrict__ qkmax,
+    int64_t* __restrict__ found, int64_t i0, int32_t slot_base, int32_t empty_from,
+    unsigned long long* __restrict__ drawn) {
     const int li = group[blockIdx.y];
+    constexpr int64_t per = (int64_t)R * kBlock;
+    __shared__ int64_t sfound;
+    Partial* prow = partials + ((size_t)blockIdx.z * n_labels + li) * tiles;
+    int64_t* fcell = found ? found + (size_t)blockIdx.z * n_labels + li : nullptr;
+    if (fcell && early_out(fcell, cand_offset + i0 + (int64_t)blockIdx.x * per, prow, slot_base + blockIdx.x, tiles,
+                           empty_from, &sfound))
+        return;
     const DLabel L = labels[li];
     __shared__ SampLds sl;
     const bool staged = stage_samp(L, samp, &sl);
     const QInfo Q = qinfo[qbase + blockIdx.y];
     const uint32_t rk = rounds[blockIdx.z];
-    constexpr int64_t per = (int64_t)R * kBlock;
     __shared__ RetryLds<R> retry;
     // the window's scores as order keys in LDS when they fit: per candidate
     // one LDS read; the winner's lpdfs are read from the table at the end
@@ -1995,11 +2046,17 @@ __global__ __launch_bounds__(kBlock, 4) void k_qfused_tiles(
             skey[t] = order_key(v.x - v.y);
         }
     __syncthreads();
+    const bool early = found && Q.G > 0 && Q.jlo <= Q.jhi;
+    const uint64_t kmax = early ? qkmax[qbase + blockIdx.y] : 0;
+    bool reported = false;
+    int64_t ndrawn = 0;
     uint64_t bk = 0;
     int64_t bi = INT64_MAX, bj = 0;
     bool bdirect = false;
     double bl = 0.0, ba = 0.0;
-    for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per) {
+    for (int64_t base = i0 + (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per) {
+        if (early && tile_stop(fcell, cand_offset + base, &sfound)) break;
+        ndrawn += min(per, n - base);
         double v[R];
         uint32_t pend = 0;
 #pragma unroll
@@ -2056,6 +2113,10 @@ __global__ __launch_bounds__(kBlock, 4) void k_qfused_tiles(
                 ba = la;
             }
         }
+        if (early && !reported && bk == kmax && bi != INT64_MAX) {
+            atomicMin((unsigned long long*)fcell, (unsigned long long)bi);
+            reported = true;
+        }
     }
     if (bi != INT64_MAX && !bdirect) {   // the winner came from the LDS keys
         const double2 t = tab[Q.tab_off + (bj - Q.jmin)];
@@ -2063,36 +2124,61 @@ __global__ __launch_bounds__(kBlock, 4) void k_qfused_tiles(
         ba = t.y;
     }
     const double bv = (double)bj * L.q;
-    Partial* prow = partials + ((size_t)blockIdx.z * n_labels + li) * tiles;
-    for (int64_t t = (int64_t)gridDim.x + blockIdx.x + (int64_t)threadIdx.x * gridDim.x; t < tiles;
+    if (drawn && threadIdx.x == 0) atomicAdd(drawn, (unsigned long long)ndrawn);
+    for (int64_t t = (int64_t)empty_from + blockIdx.x + (int64_t)threadIdx.x * gridDim.x; t < tiles;
          t += (int64_t)kBlock * gridDim.x)
         prow[t] = Partial{0, INT64_MAX, 0.0, 0.0, 0.0};
     __shared__ Partial sh[kBlock / 64];
-    block_maxloc(bk, bi, bv, bl, ba, prow + blockIdx.x, sh);
+    block_maxloc(bk, bi, bv, bl, ba, prow + slot_base + blockIdx.x, sh);
 }
 
 // Sampled categorical labels, tile map, workgroups striding over the tiles
-// of R * 256 candidates (sample_below<CAT>'s draws: the first category whose
-// cumulative weight exceeds the Philox word, here from the workgroup's LDS
-// copy of the weights when they fit), log p lookup (tpe.py:56-63), running
-// best per thread; partial slots as k_qfused_tiles.  Same winner as k_round<CAT>.
+// of R * 256 candidates from candidate i0 on (sample_below<CAT>'s draws: the
+// first category whose cumulative weight exceeds the Philox word, here from
+// the workgroup's LDS copy of the weights when they fit), log p lookup
+// (tpe.py:56-63), running best per thread; partial slots and the early exit
+// as k_qfused_tiles, kmax over the categories a draw can return (those of
+// positive weight, and the last, which also takes a rounding overshoot of
+// the cumulative weights).  Same winner as k_round<CAT>.
 template <int R>
 __global__ __launch_bounds__(kBlock) void k_cat_tiles(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
     const Comp<double>* __restrict__ comps64, const SampRec* __restrict__ samp, int64_t n, int64_t cand_offset,
     uint64_t seed, const uint32_t* __restrict__ rounds, int32_t n_labels, int32_t tiles,
-    Partial* __restrict__ partials) {
+    Partial* __restrict__ partials, int64_t* __restrict__ found, int64_t i0, int32_t slot_base,
+    int32_t empty_from, unsigned long long* __restrict__ drawn) {
     const int li = group[blockIdx.y];
+    constexpr int64_t per = (int64_t)R * kBlock;
+    __shared__ int64_t sfound;
+    Partial* prow = partials + ((size_t)blockIdx.z * n_labels + li) * tiles;
+    int64_t* fcell = found ? found + (size_t)blockIdx.z * n_labels + li : nullptr;
+    if (fcell && early_out(fcell, cand_offset + i0 + (int64_t)blockIdx.x * per, prow, slot_base + blockIdx.x, tiles,
+                           empty_from, &sfound))
+        return;
     const DLabel L = labels[li];
     __shared__ SampLds sl;
     const bool staged = stage_samp(L, samp, &sl);
     const uint32_t rk = rounds[blockIdx.z];
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-    constexpr int64_t per = (int64_t)R * kBlock;
+    __shared__ uint64_t shk[kBlock / 64];
+    uint64_t km = 0;
+    for (int k = threadIdx.x; k < L.nb; k += kBlock) {
+        const double w = k < L.ns ? samp[L.samp_off + k].cdf - (k ? samp[L.samp_off + k - 1].cdf : 0.0) : 1.0;
+        if (w > 0.0 || k == L.nb - 1 || k == L.ns - 1) {
+            const uint64_t key = order_key(comps64[L.comp_b + k].c - comps64[L.comp_a + k].c);
+            km = key > km ? key : km;
+        }
+    }
+    const uint64_t kmax = block_max_key(km, shk);
+    const bool early = found != nullptr;
+    bool reported = false;
+    int64_t ndrawn = 0;
     uint64_t bk = 0;
     int64_t bi = INT64_MAX;
     double bv = 0.0, bl = 0.0, ba = 0.0;
-    for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per) {
+    for (int64_t base = i0 + (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per) {
+        if (early && tile_stop(fcell, cand_offset + base, &sfound)) break;
+        ndrawn += min(per, n - base);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const int64_t ci = base + r * kBlock + threadIdx.x;
@@ -2118,13 +2204,17 @@ __global__ __launch_bounds__(kBlock) void k_cat_tiles(
                 ba = la;
             }
         }
+        if (early && !reported && bk == kmax && bi != INT64_MAX) {
+            atomicMin((unsigned long long*)fcell, (unsigned long long)bi);
+            reported = true;
+        }
     }
-    Partial* prow = partials + ((size_t)blockIdx.z * n_labels + li) * tiles;
-    for (int64_t t = (int64_t)gridDim.x + blockIdx.x + (int64_t)threadIdx.x * gridDim.x; t < tiles;
+    if (drawn && threadIdx.x == 0) atomicAdd(drawn, (unsigned long long)ndrawn);
+    for (int64_t t = (int64_t)empty_from + blockIdx.x + (int64_t)threadIdx.x * gridDim.x; t < tiles;
          t += (int64_t)kBlock * gridDim.x)
         prow[t] = Partial{0, INT64_MAX, 0.0, 0.0, 0.0};
     __shared__ Partial sh[kBlock / 64];
-    block_maxloc(bk, bi, bv, bl, ba, prow + blockIdx.x, sh);
+    block_maxloc(bk, bi, bv, bl, ba, prow + slot_base + blockIdx.x, sh);
 }
 
 __device__ __forceinline__ tpe_label_result to_result(const Partial& p, int li) {
@@ -2329,6 +2419,38 @@ struct RoundArgs {
     uint32_t gx_whole;         // grid.x the whole problem would use
 };
 
+// The launches of an early-exit tile round (k_qfused_tiles, k_cat_tiles):
+// a first phase of at most kEarlyTiles tiles per label (where the best
+// drawable score almost always turns up), then -- if the round is longer --
+// the rest with the full grid, whose workgroups stop as soon as they see the
+// first phase's find.  Partial slots: phase 1 [0, g1), phase 2 [g1, g1 + g2),
+// the last launch empties the slots after its own.
+constexpr int64_t kEarlyTiles = 64;
+struct EarlyPhase {
+    unsigned grid;
+    int64_t i0, n;
+    int32_t slot_base, empty_from;
+};
+
+std::vector<EarlyPhase> early_phases(const RoundArgs& a, int64_t per, unsigned grid, bool early) {
+    const int64_t tiles_n = (a.n + per - 1) / per;
+    const int64_t g1 = std::min<int64_t>({tiles_n, kEarlyTiles, (int64_t)a.tiles - 1});
+    if (!early || g1 < 1 || g1 >= tiles_n || (int64_t)a.tiles - g1 < 1)
+        return {EarlyPhase{grid, 0, a.n, 0, (int32_t)grid}};
+    const unsigned g2 = (unsigned)std::max<int64_t>(1, std::min<int64_t>(grid, (int64_t)a.tiles - g1));
+    return {EarlyPhase{(unsigned)g1, 0, g1 * per, 0, a.tiles},
+            EarlyPhase{g2, g1 * per, a.n, (int32_t)g1, (int32_t)(g1 + g2)}};
+}
+
+// the per-(round, label) first-find indices, reset (nullptr: early exit off)
+int64_t* early_found(tpe_ctx* ctx, const RoundArgs& a) {
+    if (!ctx->early) return nullptr;
+    const size_t cells = (size_t)a.n_rounds * ctx->P->n_labels;
+    if (ctx->xfound.reserve(cells) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(ctx->xfound.p, 0x7f, cells * sizeof(int64_t), ctx->stream) != hipSuccess) return nullptr;
+    return ctx->xfound.p;
+}
+
 void bracket(tpe_ctx* ctx, int mode, int which) {
     ctx->mode_ran[mode] = true;
     if (ctx->timing) (void)hipEventRecord(ctx->evm[mode][which], ctx->stream);
@@ -2344,9 +2466,13 @@ void launch_round(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
             const unsigned cgx = (unsigned)std::max<int64_t>(
                 1, std::min<int64_t>({(int64_t)a.gx, (a.n + kCatR * kBlock - 1) / (kCatR * kBlock),
                                       kHotWgs / std::max<int64_t>(1, (int64_t)nl * a.gz)}));
-            hipLaunchKernelGGL((k_cat_tiles<kCatR>), dim3(cgx, nl, a.gz), dim3(kBlock), 0, ctx->stream,
-                               ctx->P->labels.p, g.dev[MODE], ctx->P->comps64.p, ctx->P->samp.p, a.n,
-                               a.cand_offset, a.seed, ctx->rounds.p, ctx->P->n_labels, a.tiles, ctx->partials.p);
+            int64_t* found = early_found(ctx, a);
+            ctx->cat_early = true;
+            for (const EarlyPhase& ph : early_phases(a, (int64_t)kCatR * kBlock, cgx, found != nullptr))
+                hipLaunchKernelGGL((k_cat_tiles<kCatR>), dim3(ph.grid, nl, a.gz), dim3(kBlock), 0, ctx->stream,
+                                   ctx->P->labels.p, g.dev[MODE], ctx->P->comps64.p, ctx->P->samp.p, ph.n,
+                                   a.cand_offset, a.seed, ctx->rounds.p, ctx->P->n_labels, a.tiles,
+                                   ctx->partials.p, found, ph.i0, ph.slot_base, ph.empty_from, ctx->xdrawn.p + 1);
             bracket(ctx, MODE, 1);
             return;
         }
@@ -2452,7 +2578,7 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
                            P.labels.p, grp, P.comps64.p, P.samp.p, P.bx.p, P.bx_tab.p, P.bx_loff.p,
                            P.bx_list.p, a.n, a.cand_offset, a.seed, ctx->rounds.p, nl, nullptr, nullptr,
                            nullptr, nullptr, ctx->win_evals.p, ctx->errflag.p, Sb, nullptr, nullptr, nullptr,
-                           ctx->bx_lohi.p);
+                           ctx->bx_lohi.p, (int64_t)0);
         if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
         hipLaunchKernelGGL(k_pick_win<double2>, dim3((unsigned)((a.n_rounds + kBlock - 1) / kBlock), nl),
                            dim3(kBlock), 0, ctx->stream, ctx->bx_lohi.p, a.n_rounds, (int32_t)a.n,
@@ -2543,7 +2669,42 @@ void screen_bx_all(tpe_ctx* ctx, const int32_t* grp, int nl, const RoundArgs& a)
     hipLaunchKernelGGL((k_screen_bx<kBxR, true>), dim3(bgx, nl, a.gz), dim3(kBlock), 0, ctx->stream, P.labels.p,
                        grp, P.comps64.p, P.samp.p, P.bx.p, P.bx_tab.p, P.bx_loff.p, P.bx_list.p, a.n,
                        a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->scr_hid.p, ctx->scr_lb.p, ctx->scr_cnt.p,
-                       ctx->scr_idx.p, ctx->win_evals.p, ctx->errflag.p, a.S, nullptr, nullptr, nullptr, nullptr);
+                       ctx->scr_idx.p, ctx->win_evals.p, ctx->errflag.p, a.S, nullptr, nullptr, nullptr, nullptr,
+                       a.n);
+}
+
+// The hot-bin prefilter's listing threshold tau0 and its sub-bin bits for
+// rounds of n candidates per label: a function of the posterior's index and
+// n only, kept across rounds (and built ahead by tpe_prepare).
+int hot_tau_prepare(tpe_ctx* ctx, int64_t n) {
+    tpe_rt::Posterior& P = *ctx->P;
+    const int nl = (int)(P.h_group[DENSE_GMM].size() + P.h_group[DENSE_LGMM].size());
+    if (nl == 0 || !P.bx_ok || !P.bx_sb.p) return TPE_OK;
+    const int32_t* grp = P.groups.p + P.group_off[DENSE_GMM];
+    if (ctx->hot_tau0.cap < (size_t)nl) ctx->hot_tau0_gen = 0;   // (re)allocated: recompute
+    HIPCHK(ctx, ctx->hot_tau0.reserve(nl));
+    if (ctx->hot_tau0_gen == P.bx_gen && ctx->hot_tau0_n == n && ctx->hot != 2) return TPE_OK;
+    HIPCHK(ctx, ctx->hot_bits.reserve((size_t)(P.bx_sb.cap + 31) / 32));
+    HIPCHK(ctx, hipMemsetAsync(ctx->hot_tau0.p, 0, nl * sizeof(unsigned long long), ctx->stream));
+    hipLaunchKernelGGL(k_hot_tau0, dim3((unsigned)((P.bx_sb_max + kBlock - 1) / kBlock), nl), dim3(kBlock), 0,
+                       ctx->stream, grp, P.bx.p, P.bx_sb.p, P.bx_sbp.p, (float)(kHotFill / (double)n),
+                       ctx->hot_tau0.p);
+    if (ctx->hot == 2)   // test mode: a threshold no candidate reaches -> the fallback
+        HIPCHK(ctx, hipMemsetAsync(ctx->hot_tau0.p, 0xff, nl * sizeof(unsigned long long), ctx->stream));
+    const int64_t words = (P.bx_sb_max + 31) / 32;
+    hipLaunchKernelGGL(k_hot_bits, dim3((unsigned)((words + kBlock - 1) / kBlock), nl), dim3(kBlock), 0,
+                       ctx->stream, grp, P.bx.p, P.bx_sb.p, ctx->hot_tau0.p, ctx->hot_bits.p);
+    ctx->hot_tau0_gen = ctx->hot == 2 ? 0 : P.bx_gen;
+    ctx->hot_tau0_n = n;
+    return ctx->hip(hipGetLastError(), "hot-bin threshold launch");
+}
+
+// Per-cell capacity of the hot-bin prefilter's lists (and of the expansion
+// screen's appends from them): a fraction of the round, grown after an
+// overflow (which makes that round screen every candidate instead)
+constexpr int64_t kHotMinCap = 1 << 12;
+int64_t hot_stride(const tpe_ctx* ctx, int64_t n) {
+    return std::min<int64_t>(n, std::max<int64_t>(kHotMinCap, (int64_t)((double)n / ctx->hot_cap_div)));
 }
 
 template <typename T>
@@ -2566,8 +2727,13 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
             if (rc) return rc;
             use_bx = ctx->P->bx_ok;
         }
-        HIPCHK(ctx, use_bx ? ctx->scr_hid.reserve(cells * a.n) : ctx->scr_hi.reserve(cells * a.n));
-        HIPCHK(ctx, ctx->scr_idx.reserve(cells * a.n));
+        hot = use_bx && ctx->hot != 0 && ctx->P->bx_sb.p != nullptr;
+        // the expansion screen's appends: a cell's hot list at most (the
+        // prefilter), else any candidate of the round
+        int64_t lst = hot ? hot_stride(ctx, a.n) : a.n;
+        if (use_bx) HIPCHK(ctx, ctx->scr_hid.reserve(cells * lst));
+        else HIPCHK(ctx, ctx->scr_hi.reserve(cells * a.n));
+        HIPCHK(ctx, ctx->scr_idx.reserve(cells * lst));
         HIPCHK(ctx, ctx->scr_lb.reserve(cells));
         HIPCHK(ctx, ctx->scr_cnt.reserve(cells));
         HIPCHK(ctx, hipMemsetAsync(ctx->scr_lb.p, 0, cells * sizeof(unsigned long long), ctx->stream));
@@ -2579,36 +2745,21 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
             tpe_rt::Posterior& P = *ctx->P;
             HIPCHK(ctx, ctx->win_evals.reserve(1));
             HIPCHK(ctx, hipMemsetAsync(ctx->win_evals.p, 0, sizeof(unsigned long long), ctx->stream));
-            hot = ctx->hot != 0 && P.bx_sb.p != nullptr;
             if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
             if (hot) {
                 // hot-bin prefilter: draw + sub-bin bounds, then the
                 // expansion screen over the listed candidates only
-                HIPCHK(ctx, ctx->hot_x.reserve(cells * a.n));
-                HIPCHK(ctx, ctx->hot_i.reserve(cells * a.n));
+                HIPCHK(ctx, ctx->hot_x.reserve(cells * lst));
+                HIPCHK(ctx, ctx->hot_i.reserve(cells * lst));
                 HIPCHK(ctx, ctx->hot_cnt.reserve(cells));
                 HIPCHK(ctx, ctx->hot_t.reserve(cells));
-                if (ctx->hot_tau0.cap < (size_t)nl) ctx->hot_tau0_gen = 0;   // (re)allocated: recompute
-                HIPCHK(ctx, ctx->hot_tau0.reserve(nl));
                 HIPCHK(ctx, ctx->hot_flag.reserve(1));
                 HIPCHK(ctx, hipMemsetAsync(ctx->hot_cnt.p, 0, cells * sizeof(int32_t), ctx->stream));
                 HIPCHK(ctx, hipMemsetAsync(ctx->hot_t.p, 0, cells * sizeof(unsigned long long), ctx->stream));
                 HIPCHK(ctx, hipMemsetAsync(ctx->hot_flag.p, 0, sizeof(int32_t), ctx->stream));
-                // tau0 depends on the posterior's tables and n only: kept across rounds
-                if (ctx->hot_tau0_gen != P.bx_gen || ctx->hot_tau0_n != a.n || ctx->hot == 2) {
-                    HIPCHK(ctx, ctx->hot_bits.reserve((size_t)(P.bx_sb.cap + 31) / 32));
-                    HIPCHK(ctx, hipMemsetAsync(ctx->hot_tau0.p, 0, nl * sizeof(unsigned long long), ctx->stream));
-                    hipLaunchKernelGGL(k_hot_tau0, dim3((unsigned)((P.bx_sb_max + kBlock - 1) / kBlock), nl),
-                                       dim3(kBlock), 0, ctx->stream, grp, P.bx.p, P.bx_sb.p, P.bx_sbp.p,
-                                       (float)(kHotFill / (double)a.n), ctx->hot_tau0.p);
-                    if (ctx->hot == 2)   // test mode: a threshold no candidate reaches -> the fallback
-                        HIPCHK(ctx, hipMemsetAsync(ctx->hot_tau0.p, 0xff, nl * sizeof(unsigned long long),
-                                                   ctx->stream));
-                    const int64_t words = (P.bx_sb_max + 31) / 32;
-                    hipLaunchKernelGGL(k_hot_bits, dim3((unsigned)((words + kBlock - 1) / kBlock), nl), dim3(kBlock),
-                                       0, ctx->stream, grp, P.bx.p, P.bx_sb.p, ctx->hot_tau0.p, ctx->hot_bits.p);
-                    ctx->hot_tau0_gen = ctx->hot == 2 ? 0 : P.bx_gen;
-                    ctx->hot_tau0_n = a.n;
+                {
+                    const int rc = hot_tau_prepare(ctx, a.n);
+                    if (rc) return rc;
                 }
                 const int64_t cells_l = (int64_t)nl * a.gz;
                 // ~kHotWgs workgroups over the round (tiles strided), at most one per tile
@@ -2619,19 +2770,19 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                                         nl, a.gz),
                                    dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.samp.p, P.bx.p, ctx->hot_bits.p,
                                    a.n, a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->hot_cnt.p, ctx->hot_i.p,
-                                   ctx->hot_x.p, ctx->errflag.p);
+                                   ctx->hot_x.p, ctx->errflag.p, lst, ctx->hot_flag.p);
                 const unsigned bgx = (unsigned)((a.n + kBxR * kBlock - 1) / (kBxR * kBlock));
                 hipLaunchKernelGGL((k_screen_hot<kBxR>), dim3(std::min(bgx, kHotScreenWgs), nl, a.gz), dim3(kBlock),
                                    0, ctx->stream, P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p, P.bx_loff.p,
                                    P.bx_list.p, a.n, nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p,
                                    ctx->scr_hid.p, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p,
-                                   ctx->win_evals.p, P.bx_sb.p, ctx->hot_t.p);
+                                   ctx->win_evals.p, P.bx_sb.p, ctx->hot_t.p, lst);
             } else {
                 screen_bx_all(ctx, grp, nl, a);
             }
             if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
             hipLaunchKernelGGL(k_select_list, dim3((unsigned)cells), dim3(kBlock), 0, ctx->stream, ctx->scr_hid.p,
-                               a.n, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p);
+                               lst, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p);
             if (hot) {
                 hipLaunchKernelGGL(k_hot_check, dim3(1), dim3(kBlock), 0, ctx->stream, (int64_t)cells, nl,
                                    ctx->hot_t.p, ctx->hot_tau0.p, ctx->hot_flag.p);
@@ -2737,14 +2888,20 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
             ctx->hot_ran = true;
             for (size_t c = 0; c < cells; ++c) ctx->hot_listed += ctx->hot_cnt_h[c];
             if (ctx->hot_flag_h) {
-                // a cell's best lower bound stayed below tau0: the list may
-                // miss winners -- screen every candidate instead
-                ctx->hot_fallback = 1;
+                // a cell's best lower bound stayed below tau0 (bit 1: the
+                // list may miss winners) or a list overflowed (bit 2) --
+                // screen every candidate instead, into full-length lists
+                ctx->hot_fallback = ctx->hot_flag_h;
+                if ((ctx->hot_flag_h & 2) && ctx->hot_cap_div > 1.0)   // the next rounds list more
+                    ctx->hot_cap_div = std::max(1.0, ctx->hot_cap_div / 4.0);
+                lst = a.n;
+                HIPCHK(ctx, ctx->scr_hid.reserve(cells * lst));
+                HIPCHK(ctx, ctx->scr_idx.reserve(cells * lst));
                 HIPCHK(ctx, hipMemsetAsync(ctx->scr_lb.p, 0, cells * sizeof(unsigned long long), ctx->stream));
                 HIPCHK(ctx, hipMemsetAsync(ctx->scr_cnt.p, 0, cells * sizeof(int32_t), ctx->stream));
                 screen_bx_all(ctx, grp, nl, a);
                 hipLaunchKernelGGL(k_select_list, dim3((unsigned)cells), dim3(kBlock), 0, ctx->stream,
-                                   ctx->scr_hid.p, a.n, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p);
+                                   ctx->scr_hid.p, lst, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p);
                 HIPCHK(ctx, hipMemcpyAsync(&ctx->screen_exec_h, ctx->win_evals.p, sizeof(unsigned long long),
                                            hipMemcpyDeviceToHost, ctx->stream));
                 HIPCHK(ctx, hipMemcpyAsync(ctx->scr_cnt_h.data(), ctx->scr_cnt.p, cells * sizeof(int32_t),
@@ -2785,7 +2942,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                                        hipMemcpyHostToDevice, ctx->stream));
             const RescoreChunk* chp = reinterpret_cast<const RescoreChunk*>(ctx->scr_chunks.p);
             hipLaunchKernelGGL(k_rescore_draw, dim3((unsigned)((ne + kBlock / kRsW - 1) / (kBlock / kRsW))),
-                               dim3(kBlock), 0, ctx->stream, ctx->P->labels.p, grp, ctx->P->samp.p, a.n,
+                               dim3(kBlock), 0, ctx->stream, ctx->P->labels.p, grp, ctx->P->samp.p, lst,
                                a.cand_offset, a.seed, ctx->rounds.p, nl, ne, ctx->scr_cnt.p, ctx->scr_idx.p, chp,
                                ctx->rs_x.p, ctx->rs_g.p);
             hipLaunchKernelGGL(k_rescore_slices, dim3((unsigned)((s_max + 3) / 4), (unsigned)ne), dim3(kBlock), 0,
@@ -2806,7 +2963,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
             HIPCHK(ctx, hipMemcpyAsync(ctx->scr_off.p, range.data(), cells * sizeof(int64_t),
                                        hipMemcpyHostToDevice, ctx->stream));
             hipLaunchKernelGGL((k_rescore<kRescoreR>), dim3((unsigned)tab.size()), dim3(kBlock), 0, ctx->stream,
-                               ctx->P->labels.p, grp, ctx->P->comps64.p, ctx->P->samp.p, a.n,
+                               ctx->P->labels.p, grp, ctx->P->comps64.p, ctx->P->samp.p, lst,
                                a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->P->n_labels, a.tiles,
                                ctx->scr_cnt.p, ctx->scr_idx.p,
                                reinterpret_cast<const RescoreChunk*>(ctx->scr_chunks.p), ctx->scr_res.p);
@@ -2890,7 +3047,12 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
                 fused = false;
                 break;
             }
-            qi[qpos] = QInfo{jmin, G, tab, 0};
+            // the grid indices a draw can take: x in [lo, hi) (LGMM1: exp of a
+            // log-space draw, within an ulp), j = rint(x / q) is monotone in x
+            const double xl = lg ? lo * (1.0 - 0x1.0p-50) : lo, xh = lg ? hi * (1.0 + 0x1.0p-50) : hi;
+            const int64_t jlo = std::max(jmin, (int64_t)std::nearbyint(xl / d.q));
+            const int64_t jhi = std::min(jmax, (int64_t)std::nearbyint(xh / d.q));
+            qi[qpos] = QInfo{jmin, G, tab, jlo, jhi, 0};
             tab += G;
             maxG = std::max(maxG, G);
             evals_q[lg ? 1 : 0] += G * (int64_t)(d.nb + d.na);
@@ -2898,8 +3060,11 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
         if (fused) {
             HIPCHK(ctx, ctx->qinfo.reserve(nq));
             HIPCHK(ctx, ctx->qtab.reserve(std::max<int64_t>(tab, 1)));
+            HIPCHK(ctx, ctx->qkmax.reserve(nq));
             HIPCHK(ctx, hipMemcpyAsync(ctx->qinfo.p, qi.data(), nq * sizeof(QInfo), hipMemcpyHostToDevice,
                                        ctx->stream));
+            HIPCHK(ctx, hipMemsetAsync(ctx->qkmax.p, 0, nq * sizeof(unsigned long long), ctx->stream));
+            int64_t* found = a.S.cpack == 0 ? early_found(ctx, a) : nullptr;
             for (int fam = 0; fam < 2; ++fam) {
                 const int mode = fam ? QUANT_LGMM : QUANT_GMM;
                 const int cnt = fam ? nql : nqg;
@@ -2909,10 +3074,12 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
                 dim3 tg((unsigned)maxG, cnt, 1);
                 if (fam)
                     hipLaunchKernelGGL(k_qtable<QUANT_LGMM>, tg, dim3(kBlock), 0, ctx->stream, ctx->P->labels.p,
-                                       g.dev[mode], ctx->P->comps64.p, ctx->qinfo.p, nq, qbase, ctx->qtab.p);
+                                       g.dev[mode], ctx->P->comps64.p, ctx->qinfo.p, nq, qbase, ctx->qtab.p,
+                                       ctx->qkmax.p);
                 else
                     hipLaunchKernelGGL(k_qtable<QUANT_GMM>, tg, dim3(kBlock), 0, ctx->stream, ctx->P->labels.p,
-                                       g.dev[mode], ctx->P->comps64.p, ctx->qinfo.p, nq, qbase, ctx->qtab.p);
+                                       g.dev[mode], ctx->P->comps64.p, ctx->qinfo.p, nq, qbase, ctx->qtab.p,
+                                       ctx->qkmax.p);
                 dim3 sg(a.gx, cnt, a.gz);
 #define TPE_QFUSED(M, RR)                                                                          \
     hipLaunchKernelGGL((k_qfused<M, RR>), sg, dim3(kBlock), 0, ctx->stream, ctx->P->labels.p,         \
@@ -2923,11 +3090,13 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
                 const unsigned qgx = (unsigned)std::max<int64_t>(
                     1, std::min<int64_t>({(int64_t)a.gx, (a.n + kQR * kBlock - 1) / (kQR * kBlock),
                                           kHotWgs / std::max<int64_t>(1, (int64_t)cnt * a.gz)}));
-#define TPE_QTILES(M)                                                                                  \
-    hipLaunchKernelGGL((k_qfused_tiles<M, kQR>), dim3(qgx, cnt, a.gz), dim3(kBlock), 0, ctx->stream,   \
-                       ctx->P->labels.p, g.dev[mode], ctx->P->comps64.p, ctx->P->samp.p, ctx->qinfo.p,  \
-                       ctx->qtab.p, a.n, a.cand_offset, a.seed, ctx->rounds.p, qbase, ctx->P->n_labels, \
-                       a.tiles, ctx->partials.p, ctx->errflag.p)
+#define TPE_QTILES(M)                                                                                   \
+    for (const EarlyPhase& ph : early_phases(a, (int64_t)kQR * kBlock, qgx, found != nullptr))          \
+        hipLaunchKernelGGL((k_qfused_tiles<M, kQR>), dim3(ph.grid, cnt, a.gz), dim3(kBlock), 0,         \
+                           ctx->stream, ctx->P->labels.p, g.dev[mode], ctx->P->comps64.p, ctx->P->samp.p, \
+                           ctx->qinfo.p, ctx->qtab.p, ph.n, a.cand_offset, a.seed, ctx->rounds.p, qbase,  \
+                           ctx->P->n_labels, a.tiles, ctx->partials.p, ctx->errflag.p, ctx->qkmax.p, found, \
+                           ph.i0, ph.slot_base, ph.empty_from, ctx->xdrawn.p)
                 if (fam) {
                     if (a.S.cpack == 0) TPE_QTILES(QUANT_LGMM);
                     else if (narrow(a.S)) TPE_QFUSED(QUANT_LGMM, kRGroup);
@@ -2989,7 +3158,7 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
         const int64_t jmin = (int64_t)(mm[qpos] ^ 0x8000000000000000ull);
         const int64_t jmax = (int64_t)(mm[nq + qpos] ^ 0x8000000000000000ull);
         const int64_t G = (mm[qpos] <= mm[nq + qpos]) ? jmax - jmin + 1 : 0;
-        qi[qpos] = QInfo{jmin, (ctx->dedup && G > 0 && 2 * G <= total) ? G : 0, tab, 0};
+        qi[qpos] = QInfo{jmin, (ctx->dedup && G > 0 && 2 * G <= total) ? G : 0, tab, 1, 0, 0};
         tab += qi[qpos].G;
         maxG = std::max(maxG, qi[qpos].G);
         const int li = qpos < nqg ? ctx->P->h_group[QUANT_GMM][qpos] : ctx->P->h_group[QUANT_LGMM][qpos - nqg];
@@ -3010,11 +3179,11 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
             if (fam)
                 hipLaunchKernelGGL(k_qtable<QUANT_LGMM>, tg, dim3(kBlock), 0, ctx->stream,
                                    ctx->P->labels.p, g.dev[mode], ctx->P->comps64.p, ctx->qinfo.p, nq,
-                                   qbase, ctx->qtab.p);
+                                   qbase, ctx->qtab.p, nullptr);
             else
                 hipLaunchKernelGGL(k_qtable<QUANT_GMM>, tg, dim3(kBlock), 0, ctx->stream,
                                    ctx->P->labels.p, g.dev[mode], ctx->P->comps64.p, ctx->qinfo.p, nq,
-                                   qbase, ctx->qtab.p);
+                                   qbase, ctx->qtab.p, nullptr);
         }
         dim3 sg(a.gx, cnt, a.gz);
 #define TPE_QSCAN(M, RR)                                                                      \
@@ -3107,6 +3276,8 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     HIPCHK(ctx, hipMemcpyAsync(ctx->rounds.p, rounds_h, n_rounds * sizeof(uint32_t),
                                hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(ctx->errflag.p, 0, sizeof(int32_t), ctx->stream));
+    HIPCHK(ctx, ctx->xdrawn.reserve(2));
+    HIPCHK(ctx, hipMemsetAsync(ctx->xdrawn.p, 0, 2 * sizeof(unsigned long long), ctx->stream));
     Groups g;
     for (int m = 0; m < kNumModes; ++m) {
         g.dev[m] = ctx->P->groups.p + ctx->P->group_off[m];
@@ -3135,6 +3306,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     RoundArgs a{n, cand_offset, seed, n_rounds, tiles, cand_in_dev, olb, ola, S, gx, gz,
                 n_whole * rounds_whole, gx_whole};
     ctx->screen_total = ctx->screen_rescored = 0;
+    ctx->cat_early = false;
     ctx->screen_mode = 0;
     ctx->screen_exec = 0;
     ctx->screen_rescore_terms = 0;
@@ -3201,6 +3373,8 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     int32_t errh = 0;
     HIPCHK(ctx, hipMemcpyAsync(&errh, ctx->errflag.p, sizeof(int32_t), hipMemcpyDeviceToHost,
                                ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->xdrawn_h, ctx->xdrawn.p, 2 * sizeof(unsigned long long),
+                               hipMemcpyDeviceToHost, ctx->stream));
     if (tiles > 0 && out)
         HIPCHK(ctx, hipMemcpyAsync(out, ctx->results.p,
                                    (size_t)n_rounds * L * sizeof(tpe_label_result),
@@ -3249,6 +3423,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         if (only_label >= 0 && l != only_label) continue;
         const DLabel& d = ctx->P->h_labels[l];
         if (sample && (d.mode == QUANT_GMM || d.mode == QUANT_LGMM)) continue;  // counted below
+        if (d.mode == CAT && ctx->cat_early) continue;   // counted below: the candidates drawn
         const int64_t e = ((d.mode == CAT) ? 2 * n : n * (int64_t)(d.nb + d.na)) * n_rounds;
         evals += e;
         // sampled rounds time both dense families in one launch (chain)
@@ -3257,6 +3432,10 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     }
     ctx->mode_evals[QUANT_GMM] += evals_q[0];
     ctx->mode_evals[QUANT_LGMM] += evals_q[1];
+    if (ctx->cat_early) {   // 2 lookups per categorical candidate actually drawn
+        ctx->mode_evals[CAT] += 2 * (int64_t)ctx->xdrawn_h[1];
+        evals += 2 * (int64_t)ctx->xdrawn_h[1];
+    }
     ctx->evals = evals + evals_q[0] + evals_q[1];
     if (tiles == 0 && out) {
         for (int32_t j = 0; j < n_rounds * L; ++j)
@@ -3460,6 +3639,7 @@ int tpe_ctx_create(int device, int precision, tpe_ctx** out) {
         ok = ok && hipEventCreate(&c->evm[m][0]) == hipSuccess &&
              hipEventCreate(&c->evm[m][1]) == hipSuccess;
     ok = ok && hipEventCreate(&c->evs[0]) == hipSuccess && hipEventCreate(&c->evs[1]) == hipSuccess;
+    ok = ok && hipEventCreate(&c->ev_prep[0]) == hipSuccess && hipEventCreate(&c->ev_prep[1]) == hipSuccess;
     ok = ok && hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess &&
          hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess;
     for (int j = 0; j < 2; ++j)
@@ -3502,8 +3682,10 @@ TPE_DEV void tpe1_ctx_destroy(tpe_ctx* c) {
     for (int m = 0; m < kNumModes; ++m)
         for (int j = 0; j < 2; ++j)
             if (c->evm[m][j]) (void)hipEventDestroy(c->evm[m][j]);
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < 2; ++j) {
         if (c->evs[j]) (void)hipEventDestroy(c->evs[j]);
+        if (c->ev_prep[j]) (void)hipEventDestroy(c->ev_prep[j]);
+    }
     c->scr_hi.release();
     c->scr_idx.release();
     c->scr_lb.release();
@@ -3663,7 +3845,7 @@ int tpe_screen_probe(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n,
                            P.labels.p, ctx->one_group.p, P.comps64.p, P.samp.p, P.bx.p, P.bx_tab.p,
                            P.bx_loff.p, P.bx_list.p, n, 0, 0, ctx->rounds.p, 1, nullptr, nullptr, nullptr,
                            nullptr, nullptr, ctx->errflag.p, Slots{0, 0, 1}, ctx->cand.p, ctx->out_lb.p,
-                           ctx->out_la.p, nullptr);
+                           ctx->out_la.p, nullptr, (int64_t)0);
     } else if (ctx->window && n >= 2048) {   // the windowed screen's tiles of sorted neighbours
         int rc = tpe_rt::win_prepare(ctx);
         if (rc) return rc;
@@ -3728,8 +3910,13 @@ int tpe_last_screen_terms(const tpe_ctx* ctx, int64_t* terms) {
 
 int32_t tpe_last_screen_mode(const tpe_ctx* ctx) { return ctx ? ctx->screen_mode : -1; }
 
-int tpe_last_prepare(const tpe_ctx* ctx, float* ms) {
+int tpe_last_prepare(tpe_ctx* ctx, float* ms) {
     if (!ctx) return TPE_ERR_ARG;
+    if (ctx->prep_pending) {
+        HIPCHK(ctx, hipEventSynchronize(ctx->ev_prep[1]));
+        HIPCHK(ctx, hipEventElapsedTime(&ctx->prep_ms, ctx->ev_prep[0], ctx->ev_prep[1]));
+        ctx->prep_pending = false;
+    }
     if (ms) *ms = ctx->prep_ms;
     return TPE_OK;
 }
@@ -3741,10 +3928,27 @@ int tpe_last_hot(const tpe_ctx* ctx, int64_t* listed, int32_t* fallback) {
     return TPE_OK;
 }
 
+int tpe_last_drawn(const tpe_ctx* ctx, int64_t* quantized, int64_t* categorical) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (quantized) *quantized = (int64_t)ctx->xdrawn_h[0];
+    if (categorical) *categorical = (int64_t)ctx->xdrawn_h[1];
+    return TPE_OK;
+}
+
 int tpe_last_rescore_terms(const tpe_ctx* ctx, int64_t* terms) {
     if (!ctx) return TPE_ERR_ARG;
     if (terms) *terms = ctx->screen_rescore_terms;
     return TPE_OK;
+}
+
+TPE_DEV int tpe1_prepare(tpe_ctx* ctx, int64_t n_candidates) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (!ctx->P || ctx->P->n_labels <= 0) return ctx->fail(TPE_ERR_ARG, "no resident posterior");
+    if (ctx->precision != TPE_F64 || !ctx->screen || !ctx->expand || n_candidates < kWinMinN) return TPE_OK;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    int rc = tpe_rt::bx_prepare(ctx);
+    if (rc == TPE_OK && ctx->hot) rc = hot_tau_prepare(ctx, n_candidates);
+    return rc;
 }
 
 TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
@@ -3760,6 +3964,11 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
         case TPE_OPT_TIMING: ctx->timing = value != 0; break;
         case TPE_OPT_WINDOW: ctx->window = value != 0; break;
         case TPE_OPT_EXPAND: ctx->expand = value != 0; break;
+        case TPE_OPT_EARLY: ctx->early = value != 0; break;
+        case TPE_OPT_HOT_DIV:
+            if (value < 1 || value > (1 << 20)) return ctx->fail(TPE_ERR_ARG, "hot list divisor must be in [1, 2^20]");
+            ctx->hot_cap_div = (double)value;
+            break;
         case TPE_OPT_HOT:
             if (value < 0 || value > 2) return ctx->fail(TPE_ERR_ARG, "hot must be 0, 1 or 2");
             ctx->hot = (int32_t)value;

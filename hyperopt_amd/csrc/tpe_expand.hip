@@ -34,7 +34,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <chrono>
 #include <cmath>
 
 #include "../../include/hyperopt_tpe.h"
@@ -607,16 +606,83 @@ __global__ __launch_bounds__(kBlock) void k_bx_bounds(const DLabel* __restrict__
     sbp[B.sb_off + j] = (float)p;
 }
 
+// grid (dense labels of the snapshot): any byte of a dense label's DLabel,
+// records or sampling records that differs from the snapshot -> *diff = 1
+__global__ __launch_bounds__(kBlock) void k_bx_compare(const int32_t* __restrict__ grp,
+                                                       const DLabel* __restrict__ lab, const DLabel* __restrict__ lab0,
+                                                       const Comp<double>* __restrict__ c,
+                                                       const Comp<double>* __restrict__ c0,
+                                                       const SampRec* __restrict__ sr, const SampRec* __restrict__ sr0,
+                                                       int64_t c_cap, int64_t s_cap, int32_t* __restrict__ diff) {
+    const int li = grp[blockIdx.x];
+    const uint32_t* a = reinterpret_cast<const uint32_t*>(lab + li);
+    const uint32_t* b = reinterpret_cast<const uint32_t*>(lab0 + li);
+    __shared__ int bad;
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
+    if (threadIdx.x < sizeof(DLabel) / 4 && a[threadIdx.x] != b[threadIdx.x]) bad = 1;
+    __syncthreads();
+    if (bad) {
+        if (threadIdx.x == 0) atomicOr(diff, 1);
+        return;
+    }
+    const DLabel L = lab[li];
+    if (L.comp_b + L.nb > c_cap || L.comp_a + L.na > c_cap || L.samp_off + L.ns > s_cap) {
+        if (threadIdx.x == 0) atomicOr(diff, 1);
+        return;
+    }
+    bool d = false;
+    auto same = [](const Comp<double>& x, const Comp<double>& y) {
+        return __double_as_longlong(x.mu) == __double_as_longlong(y.mu) &&
+               __double_as_longlong(x.a) == __double_as_longlong(y.a) &&
+               __double_as_longlong(x.c) == __double_as_longlong(y.c) &&
+               __double_as_longlong(x.w) == __double_as_longlong(y.w);
+    };
+    for (int k = threadIdx.x; k < L.nb; k += kBlock) d |= !same(c[L.comp_b + k], c0[L.comp_b + k]);
+    for (int k = threadIdx.x; k < L.na; k += kBlock) d |= !same(c[L.comp_a + k], c0[L.comp_a + k]);
+    for (int k = threadIdx.x; k < L.ns; k += kBlock) {
+        const SampRec x = sr[L.samp_off + k], y = sr0[L.samp_off + k];
+        d |= __double_as_longlong(x.cdf) != __double_as_longlong(y.cdf) ||
+             __double_as_longlong(x.mu) != __double_as_longlong(y.mu) ||
+             __double_as_longlong(x.sigma) != __double_as_longlong(y.sigma);
+    }
+    if (d) atomicOr(diff, 1);
+}
+
 }  // namespace
 
+int tpe_rt::bx_keep_check(tpe_ctx* ctx) {
+    tpe_rt::Posterior& P = *ctx->P;
+    P.bx_diff_h = 1;
+    if (!P.bx_ready || P.bx_snap_nl <= 0) return TPE_OK;
+    HIPCHK(ctx, P.bx_diff.reserve(1));
+    HIPCHK(ctx, hipMemsetAsync(P.bx_diff.p, 0, sizeof(int32_t), ctx->stream));
+    hipLaunchKernelGGL(k_bx_compare, dim3(P.bx_snap_nl), dim3(kBlock), 0, ctx->stream, P.bx_snap_g.p, P.labels.p,
+                       P.bx_snap_l.p, P.comps64.p, P.bx_snap_c.p, P.samp.p, P.bx_snap_s.p,
+                       (int64_t)std::min(P.comps64.cap, P.bx_snap_c.cap),
+                       (int64_t)std::min(P.samp.cap, P.bx_snap_s.cap), P.bx_diff.p);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipMemcpyAsync(&P.bx_diff_h, P.bx_diff.p, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    return TPE_OK;
+}
+
+bool tpe_rt::bx_keep_after(tpe_ctx* ctx, bool groups_changed) {
+    tpe_rt::Posterior& P = *ctx->P;
+    return P.bx_ready && P.bx_snap_nl > 0 && !groups_changed && P.bx_diff_h == 0;
+}
+
+// The index is queued on the context's stream without waiting for it (one
+// short round trip for the layout): a caller can overlap it with host work
+// (tpe_prepare).  Its device time is bracketed by events and read when asked.
 int tpe_rt::bx_prepare(tpe_ctx* ctx) {
     tpe_rt::Posterior& P = *ctx->P;
     if (P.bx_ready) return TPE_OK;
-    const auto t0 = std::chrono::steady_clock::now();
+    const bool timed = ctx->timing && ctx->ev_prep[0];
+    if (timed) HIPCHK(ctx, hipEventRecord(ctx->ev_prep[0], ctx->stream));
     const int rc = bx_build(ctx);
-    if (rc == TPE_OK && ctx->timing) {   // the build's wall time, kernels included
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
-        ctx->prep_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (rc == TPE_OK && timed) {
+        HIPCHK(ctx, hipEventRecord(ctx->ev_prep[1], ctx->stream));
+        ctx->prep_pending = true;
     }
     return rc;
 }
@@ -629,6 +695,7 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
     const std::vector<int32_t>& gg = P.h_group[DENSE_GMM];
     const std::vector<int32_t>& gl = P.h_group[DENSE_LGMM];
     const int nl = (int)(gg.size() + gl.size());
+    P.bx_snap_nl = 0;
     if (nl == 0) {
         P.bx_ready = true;
         return TPE_OK;
@@ -720,6 +787,27 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
     hipLaunchKernelGGL(k_bx_bounds, gs, dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p, P.samp.p,
                        P.bx.p, P.bx_tab.p, P.bx_loff.p, P.bx_list.p, P.bx_sb.p, P.bx_sbp.p);
     HIPCHK(ctx, hipGetLastError());
+    // the snapshot a later rebuild is compared with (bx_keep_check)
+    int64_t c_ext = 0, s_ext = 0;
+    for (int y = 0; y < nl; ++y) {
+        const DLabel& d = P.h_labels[y < (int)gg.size() ? gg[y] : gl[y - gg.size()]];
+        c_ext = std::max<int64_t>({c_ext, (int64_t)d.comp_b + d.nb, (int64_t)d.comp_a + d.na});
+        s_ext = std::max<int64_t>(s_ext, (int64_t)d.samp_off + d.ns);
+    }
+    HIPCHK(ctx, P.bx_snap_l.reserve(P.n_labels));
+    HIPCHK(ctx, P.bx_snap_c.reserve(std::max<int64_t>(c_ext, 1)));
+    HIPCHK(ctx, P.bx_snap_s.reserve(std::max<int64_t>(s_ext, 1)));
+    HIPCHK(ctx, P.bx_snap_g.reserve(nl));
+    HIPCHK(ctx, hipMemcpyAsync(P.bx_snap_l.p, P.labels.p, P.n_labels * sizeof(DLabel), hipMemcpyDeviceToDevice,
+                               ctx->stream));
+    if (c_ext > 0)
+        HIPCHK(ctx, hipMemcpyAsync(P.bx_snap_c.p, P.comps64.p, c_ext * sizeof(Comp<double>), hipMemcpyDeviceToDevice,
+                                   ctx->stream));
+    if (s_ext > 0)
+        HIPCHK(ctx, hipMemcpyAsync(P.bx_snap_s.p, P.samp.p, s_ext * sizeof(SampRec), hipMemcpyDeviceToDevice,
+                                   ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(P.bx_snap_g.p, grp, nl * sizeof(int32_t), hipMemcpyDeviceToDevice, ctx->stream));
+    P.bx_snap_nl = nl;
     P.bx_ok = true;
     P.bx_ready = true;
     return TPE_OK;

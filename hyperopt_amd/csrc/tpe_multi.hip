@@ -136,6 +136,7 @@ struct Shard {
 void aggregate_stats(tpe_ctx* c) {
     const int n = ndev(c);
     int64_t evals = 0, scr_t = 0, scr_r = 0, scr_x = 0, scr_rt = 0;
+    unsigned long long drawn[2] = {0, 0};
     float score_ms = 0.f, round_ms = 0.f, scr_ms = 0.f;
     float mode_ms[tpe_rt::kNumModes] = {};
     int64_t mode_ev[tpe_rt::kNumModes] = {};
@@ -146,6 +147,8 @@ void aggregate_stats(tpe_ctx* c) {
         scr_r += x->screen_rescored;
         scr_x += x->screen_exec;
         scr_rt += x->screen_rescore_terms;
+        drawn[0] += x->xdrawn_h[0];
+        drawn[1] += x->xdrawn_h[1];
         score_ms = std::max(score_ms, x->score_ms);
         round_ms = std::max(round_ms, x->round_ms);
         scr_ms = std::max(scr_ms, x->screen_ms);
@@ -159,6 +162,8 @@ void aggregate_stats(tpe_ctx* c) {
     c->screen_rescored = scr_r;
     c->screen_exec = scr_x;
     c->screen_rescore_terms = scr_rt;
+    c->xdrawn_h[0] = drawn[0];
+    c->xdrawn_h[1] = drawn[1];
     c->screen_mode = dev(c, 0)->screen_mode;
     c->score_ms = score_ms;
     c->round_ms = round_ms;
@@ -276,6 +281,11 @@ int tpe_set_posterior(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_labe
 int tpe_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
     if (!ctx) return TPE_ERR_ARG;
     return for_all(ctx, [&](tpe_ctx* x, int) { return tpe1_set_option(x, option, value); });
+}
+
+int tpe_prepare(tpe_ctx* ctx, int64_t n_candidates) {
+    if (!ctx) return TPE_ERR_ARG;
+    return for_all(ctx, [&](tpe_ctx* x, int) { return tpe1_prepare(x, n_candidates); });
 }
 
 int tpe_history_reset(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,

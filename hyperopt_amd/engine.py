@@ -226,6 +226,11 @@ class Engine(object):
                                              _ptr(s), n.value, ctypes.byref(n)))
         return w, m, s
 
+    def prepare(self, n_candidates):
+        """Build the expansion index of the resident posterior now
+        (tpe_prepare; the first round of n_candidates would build it)."""
+        self._check(self.lib.tpe_prepare(self.h, int(n_candidates)))
+
     def last_build_ms(self):
         ms = ctypes.c_float()
         self._check(self.lib.tpe_last_build_ms(self.h, ctypes.byref(ms)))
@@ -306,6 +311,13 @@ class Engine(object):
         self._check(self.lib.tpe_last_prepare(self.h, ctypes.byref(ms)))
         return ms.value
 
+    def last_drawn(self):
+        """(quantized, categorical) candidates the last round drew: fewer
+        than rounds x n when the exact early exit stopped a label's round."""
+        a, b = ctypes.c_int64(), ctypes.c_int64()
+        self._check(self.lib.tpe_last_drawn(self.h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
     def last_rescore_terms(self):
         """(candidate, component) terms the last round's fp64 re-score
         evaluated (every re-scored candidate over both of its mixtures)."""
@@ -318,12 +330,12 @@ class Engine(object):
                'whole_rounds': L.TPE_OPT_WHOLE_ROUNDS, 'timing': L.TPE_OPT_TIMING,
                'window': L.TPE_OPT_WINDOW, 'win_t': L.TPE_OPT_WIN_T,
                'win_groups': L.TPE_OPT_WIN_GROUPS, 'expand': L.TPE_OPT_EXPAND,
-               'hot': L.TPE_OPT_HOT}
+               'hot': L.TPE_OPT_HOT, 'early': L.TPE_OPT_EARLY, 'hot_div': L.TPE_OPT_HOT_DIV}
 
     def set_option(self, name, value):
         """Engine switches (include/hyperopt_tpe.h TPE_OPT_*): 'screen',
-        'splitk', 'dedup', 'timing', 'window', 'expand', 'hot' (bool), 'chunks'
-        (int, 0 = auto),
+        'splitk', 'dedup', 'timing', 'window', 'expand', 'hot', 'early' (bool), 'chunks'
+        (int, 0 = auto), 'hot_div' (the prefilter's list length n / hot_div),
         'win_t' (the windowed screen's cut, 8..62), 'win_groups' (label
         groups pipelined over two streams, 0 = auto),
         'whole_n' / 'whole_rounds' (the whole problem when this engine runs

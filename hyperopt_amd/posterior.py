@@ -289,27 +289,42 @@ def reference_orders(losses, n_below, obs_of, labels):
     return below, off, order
 
 
-def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of, known=()):
+def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of, known=(), prepare_n=0):
     """Device build whose mixtures follow the reference's tie order
     (tpe.py:433, 637): the device reports which mixtures depend on the order
     of tied observations (or a tie of losses at the split), and only for
     those the host computes numpy's own np.argsort and the build runs again
-    with it.  `known`: labels that needed an order in the previous build of
-    this history (their orders are supplied up front, saving the second
-    build).  Returns (n_below, the labels that needed an order)."""
+    with it.
+
+    * prepare_n == 0: `known` -- the labels that needed an order in the
+      previous build of this history -- get their orders up front (one
+      build when nothing new turns up);
+    * prepare_n > 0 (the round's candidates per label): the first build is
+      made without orders, the expansion index of its dense labels is queued
+      on the device (Engine.prepare), and the host computes the orders while
+      it runs; the ordered rebuild leaves the dense labels bit-identical
+      (continuous values carry no ties), so the device keeps the index.
+
+    Returns (n_below, the labels that needed an order)."""
     n_below = n_below_of(n_valid, gamma, lf)
     known = set(known)
-    if known:
+    if prepare_n:
+        nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf)
+        eng.prepare(prepare_n)
+        have = set()
+    elif known:
         below, off, order = reference_orders(losses, n_below, obs_of, known)
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf, below, off, order)
+        have = known
     else:
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf)
+        have = set()
     if np.any(ties[:-1] & 1):
         # a below mixture holds at most gamma_cap <= lf observations: its
         # weights are all equal, so its order can never matter
         raise AssertionError('below mixture depends on a tie order (n_below > lf?)')
-    need = known | set(np.flatnonzero(ties[:-1] & 2).tolist())
-    if need != known or ties[-1]:
+    need = have | set(np.flatnonzero(ties[:-1] & 2).tolist())
+    if need != have or ties[-1]:
         below, off, order = reference_orders(losses, n_below, obs_of, need)
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf, below, off, order)
         if np.any(ties[:-1]):
@@ -360,7 +375,7 @@ class DeviceHistoryUploader(object):
         self.key = None
         self.owner = None
 
-    def build(self, eng, labels, view, gamma, prior_weight, lf=DEFAULT_LF):
+    def build(self, eng, labels, view, gamma, prior_weight, lf=DEFAULT_LF, prepare_n=0):
         tids, losses, n_valid, cols, owner = view
         key = (tuple((n, k) for n, k, _ in labels), eng.history_generation)
         same_owner = self.owner is not None and self.owner() is owner
@@ -406,7 +421,8 @@ class DeviceHistoryUploader(object):
         self.n_trials = len(tids)
         self.last_tid = tids[-1] if len(tids) else None
         nb, self.tie_labels = build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf,
-                                                    self._obs_of(len(labels)), self.tie_labels)
+                                                    self._obs_of(len(labels)), self.tie_labels,
+                                                    prepare_n=prepare_n)
         return nb
 
     def _obs_of(self, n_labels):

@@ -133,8 +133,11 @@ class _PendingView(object):
         return len(self.trials)
 
 
+PREPARE_MIN = 8192   # candidates per label from which a round builds the expansion index
+
+
 def _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior_weight,
-                        builder):
+                        builder, n_candidates=0):
     """Put the posterior of the current history on the engine, from the
     device-resident history's `view` or the general gather (tids, losses,
     obs); returns the number of trial documents it was built from."""
@@ -155,7 +158,7 @@ def _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior
                 if up is None:
                     up = eng._history_uploader = _post.DeviceHistoryUploader()
                 up.build(eng, [(s.label, s.kind, s.args) for s in specs.values()], view, gamma,
-                         prior_weight)
+                         prior_weight, prepare_n=n_candidates if n_candidates >= PREPARE_MIN else 0)
             else:
                 eng.build_posterior(*device_inputs(specs, tids, losses, obs), gamma=gamma,
                                     prior_weight=prior_weight)
@@ -240,7 +243,7 @@ def suggest(new_ids, domain, trials, seed,
         logger.info('TPE using 0 trials')                     # the prior-only posterior
     eng = _engine.get_engine(list(devices) if devices else device, precision)
     _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior_weight,
-                        posterior_builder)
+                        posterior_builder, n_candidates=n_EI_candidates if precision == 'f64' else 0)
     ids = list(new_ids) if batch else [new_ids[0]]
     if len(ids) == 1:
         res = eng.suggest(seed, n_EI_candidates, round=ids[0])[None]

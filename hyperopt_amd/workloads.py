@@ -6,6 +6,8 @@ import numpy as np
 
 from . import posterior as P
 
+PREPARE_MIN = 8192   # candidates per label from which a round builds the expansion index
+
 # config-3 kind cycle: kind = i mod 5
 CYCLE = (('uniform', dict(low=-5.0, high=5.0)),
          ('loguniform', dict(low=-5.0, high=2.0)),
@@ -121,13 +123,16 @@ class FminLoop(object):
         losses = self.hist.losses[:n]
         return (self.hist.tids[:n], losses, int(np.count_nonzero(losses == losses)), obs, self)
 
-    def advance(self, eng, n):
-        """History of the first n trials on the device, posterior rebuilt;
-        returns n_below."""
+    def advance(self, eng, n, n_candidates=0):
+        """History of the first n trials on the device, posterior rebuilt
+        (its expansion index queued meanwhile when the round will have
+        n_candidates >= 8192 per label, as tpe.suggest does); returns
+        n_below."""
         if n > len(self.hist.tids):
             raise ValueError('the synthetic history holds %d trials' % len(self.hist.tids))
         self.n = n
-        return self.uploader.build(eng, self.hist.labels, self.view(n), self.gamma, self.prior_weight)
+        return self.uploader.build(eng, self.hist.labels, self.view(n), self.gamma, self.prior_weight,
+                                   prepare_n=n_candidates if n_candidates >= PREPARE_MIN else 0)
 
 
 def mixed_space(n_labels):

@@ -341,6 +341,12 @@ int tpe_last_screen_terms(const tpe_ctx *ctx, int64_t *terms);
  * With tpe_last_screen_terms this is the dense work the round executed. */
 int tpe_last_rescore_terms(const tpe_ctx *ctx, int64_t *terms);
 
+/* Candidates the last round actually drew for its quantized and categorical
+ * labels (TPE_OPT_EARLY: the exact early exit stops a label's round once a
+ * candidate holds the best score any draw can have; the rest are never
+ * drawn).  The categorical evals in tpe_last_mode_stats count these. */
+int tpe_last_drawn(const tpe_ctx *ctx, int64_t *quantized, int64_t *categorical);
+
 /* Which screen the last round's dense tile-map labels went through: 0 none
  * (unscreened fp64, fp32 precision, or no dense tile round), 1 the plain
  * fp32 screen, 2 the windowed fp32 screen, 3 the expansion screen
@@ -356,11 +362,12 @@ int32_t tpe_last_screen_mode(const tpe_ctx *ctx);
  * listing threshold).  Winners are unaffected either way. */
 int tpe_last_hot(const tpe_ctx *ctx, int64_t *listed, int32_t *fallback);
 
-/* Wall milliseconds (kernels included; TPE_OPT_TIMING on) of the last build
- * of the expansion screen's index -- bin tables, lists and the prefilter's
+/* Device milliseconds (HIP events; TPE_OPT_TIMING on) of the last build of
+ * the expansion screen's index -- bin tables, lists and the prefilter's
  * sub-bin bounds -- which runs once per posterior, before its first large
- * sampled round (0 if it has not run). */
-int tpe_last_prepare(const tpe_ctx *ctx, float *ms);
+ * sampled round or in tpe_prepare (0 if it has not run).  Waits for the
+ * index if it is still running. */
+int tpe_last_prepare(tpe_ctx *ctx, float *ms);
 
 /* Diagnostic of the hot-bin prefilter (tests): for caller-supplied
  * candidates of one dense resident label, the interval [lower, upper] of
@@ -400,6 +407,14 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *                   interval; only those that can still win are scored
  *                   (2: tests -- a listing threshold no candidate reaches,
  *                   so every round takes the fallback)                  [1]
+ *   TPE_OPT_EARLY   exact early exit of sampled tile rounds of quantized
+ *                   (bounded) and categorical labels: candidates in index
+ *                   order, stopped once one holds the best score any draw
+ *                   can have (its first index is the np.argmax winner)  [1]
+ *   TPE_OPT_HOT_DIV the hot-bin prefilter's lists hold n / HOT_DIV
+ *                   candidates per (round, label) (at least 4096); a round
+ *                   whose list overflows screens every candidate instead
+ *                   and divides HOT_DIV by 4 for the next rounds        [16]
  *   TPE_OPT_WIN_GROUPS  label groups of a windowed round, each sorted on a
  *                   second stream while the previous one is screened
  *                   (0: one group; the chip is busy either way)          [0]
@@ -425,7 +440,19 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_WIN_GROUPS 10
 #define TPE_OPT_EXPAND 11
 #define TPE_OPT_HOT 12
+#define TPE_OPT_EARLY 13
+#define TPE_OPT_HOT_DIV 14
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
+
+/* Build now what the resident posterior's first round of n_candidates per
+ * label would build lazily: the expansion screen's index (bin tables,
+ * lists, sub-bin bounds; fp64 contexts with the screen and TPE_OPT_EXPAND
+ * on, n_candidates >= 8192; otherwise nothing).  Lets a caller overlap the
+ * index with host work (tpe.suggest computes numpy's tie orders meanwhile).
+ * A later rebuild of the posterior that leaves every dense label
+ * bit-identical keeps the index (compared on the device against a snapshot).
+ * No reference counterpart: the reference has no index. */
+int tpe_prepare(tpe_ctx *ctx, int64_t n_candidates);
 
 #ifdef __cplusplus
 }

@@ -307,13 +307,23 @@ def test_hot_prefilter_same_winners(eng, config):
         listed_c, fb_c = eng.last_hot()
     finally:
         eng.set_option('hot', 1)
+    # lists far too short for the listed candidates: the round overflows
+    # them and screens every candidate instead
+    try:
+        eng.set_option('hot_div', 1 << 20)
+        e = run()
+        _, fb_e = eng.last_hot()
+    finally:
+        eng.set_option('hot_div', 16)
     eng.set_option('screen', 0)
     d = run()
     eng.set_option('screen', 1)
     _assert_same(a, d)
     _assert_same(b, d)
     _assert_same(c, d)
+    _assert_same(e, d)
     assert fb == 0 and fb_c == 1
+    assert fb_e & 2 or listed <= 4096 * 32 * 3   # (batched: short rounds list fewer than a minimal list)
     print('%s: hot prefilter listed %d of %d (%.4f), re-scored %d' %
           (config, listed, screened, listed / screened, rescored))
     assert 0 < listed < 0.25 * screened
