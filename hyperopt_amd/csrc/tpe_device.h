@@ -109,14 +109,10 @@ __device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
     return c;
 }
 
-// 52-bit uniform in (0, 1] (never 0: Box-Muller takes its log): 2 - m for
-// m in [1, 2) with the 52 mantissa bits taken from the two words -- exact,
-// two integer operations and one subtraction instead of a 64-bit integer
-// conversion.
-__device__ __forceinline__ double u01_open0(uint32_t hi, uint32_t lo) {
-    const uint64_t bits = (0x3FFull << 52) | ((uint64_t)(hi & 0xFFFFFu) << 32) | (uint64_t)lo;
-    return 2.0 - __builtin_bit_cast(double, bits);
-}
+// 32-bit uniform in [2^-32, 1] (never 0: Box-Muller takes its log): 1 -
+// y 2^-32, exact.  (The radius sqrt(-2 log u) then reaches 6.66 sigma: the
+// draws are normals truncated there, a probability of 2.7e-11 per draw.)
+__device__ __forceinline__ double u01_open0(uint32_t y) { return 1.0 - (double)y * 0x1.0p-32; }
 
 // first k with cdf[k] > u (cdf[n-1] == 1 exactly, u < 1).
 __device__ __forceinline__ int cdf_search(const SampRec* __restrict__ s, int n, double u) {
@@ -196,26 +192,21 @@ __device__ __forceinline__ bool stage_samp(const DLabel& L, const SampRec* __res
     return true;
 }
 
-// cos(2 pi w / 2^32): (cos, sin) of the top 8 bits' angle from a 256-entry
+// (cos, sin)(2 pi w / 2^32): the top 8 bits' angle a from a 256-entry
 // table (tpe_bm_table.h), the residual t = 2 pi (w mod 2^24) / 2^32 <
 // 2 pi / 256 by its Taylor polynomials (t^10 / 10! < 1e-22), then
-// cos(a + t) = cos a cos t - sin a sin t -- ~15 VALU operations and one
-// 16-byte load instead of the library cospi's ~70 operations.
-__device__ __forceinline__ double cos_turn32(uint32_t w) {
+// cos(a + t) = cos a cos t - sin a sin t, sin(a + t) = sin a cos t + cos a
+// sin t -- ~17 VALU operations and one 16-byte load instead of the library
+// sincospi's ~80.
+__device__ __forceinline__ void sincos_turn32(uint32_t w, double& c, double& s) {
     const int k = (int)(w >> 24);
     const double t = (double)(w & 0xFFFFFFu) * (6.283185307179586 * 0x1.0p-32);
     const double t2 = t * t;
     const double ct = fma(fma(fma(fma(1.0 / 40320.0, t2, -1.0 / 720.0), t2, 1.0 / 24.0), t2, -0.5), t2, 1.0);
     const double st = t * fma(fma(fma(-1.0 / 5040.0, t2, 1.0 / 120.0), t2, -1.0 / 6.0), t2, 1.0);
-    return fma(kCosSinTab[2 * k], ct, -kCosSinTab[2 * k + 1] * st);
-}
-
-// One attempt in three parts: the Philox words of (candidate g, attempt,
-// label stream, round); the component ~ weights from word x; x = mu + sigma
-// N(0, 1) by Box-Muller from words y, z (radius) and w (angle).
-__device__ __forceinline__ U4 draw_words(const DLabel& L, uint32_t k0, uint32_t k1, uint32_t g, uint32_t it,
-                                         uint32_t round) {
-    return philox4x32_10(U4{g, it, (uint32_t)L.stream, round}, k0, k1);
+    const double ca = kCosSinTab[2 * k], sa = kCosSinTab[2 * k + 1];
+    c = fma(ca, ct, -sa * st);
+    s = fma(sa, ct, ca * st);
 }
 
 // -log(u) for the Box-Muller uniform u in [2^-52, 1]: u = 2^e m, m in [1,
@@ -239,20 +230,49 @@ __device__ __forceinline__ double bm_neglog(double u) {
     return -fma((double)e, 6.93147180559945286e-01, fma(r, q, kLogTab[2 * j + 1]));
 }
 
-__device__ __forceinline__ double box_muller(const U4& r, double mu, double sg) {
-    const double u1 = u01_open0(r.y, r.z);
-    const double rad = __builtin_amdgcn_sqrt(fmax(0.0, 2.0 * bm_neglog(u1)));
-    const double nrm = rad * cos_turn32(r.w);
-    return fma(sg, nrm, mu);
+// Box-Muller's radius sqrt(-2 log u) from word y
+__device__ __forceinline__ double bm_radius(uint32_t y) {
+    return __builtin_amdgcn_sqrt(fmax(0.0, 2.0 * bm_neglog(u01_open0(y))));
+}
+
+// Candidates 2p and 2p + 1 share one Philox4x32-10 call per attempt: the
+// counter is (p, attempt, label stream, round); word x picks candidate 2p's
+// component ~ weights, word z candidate 2p + 1's, word y gives the
+// Box-Muller radius and word w the angle, and the pair's normals are rad cos
+// and rad sin (independent N(0, 1)).  draw_pair draws both, draw_attempt one
+// of them -- the same arithmetic, so the same bits.
+template <typename Src>
+__device__ __forceinline__ void draw_pair(const DLabel& L, const Src& src, uint32_t k0, uint32_t k1, uint32_t p,
+                                          uint32_t it, uint32_t round, double& d0, double& d1) {
+    const U4 r = philox4x32_10(U4{p, it, (uint32_t)L.stream, round}, k0, k1);
+    double mu0, sg0, mu1, sg1;
+    src.pick((double)r.x * 0x1.0p-32, mu0, sg0);
+    src.pick((double)r.z * 0x1.0p-32, mu1, sg1);
+    const double rad = bm_radius(r.y);
+    double c, s;
+    sincos_turn32(r.w, c, s);
+    d0 = fma(sg0, rad * c, mu0);
+    d1 = fma(sg1, rad * s, mu1);
 }
 
 template <typename Src>
 __device__ __forceinline__ double draw_attempt(const DLabel& L, const Src& src, uint32_t k0, uint32_t k1,
                                                uint32_t g, uint32_t it, uint32_t round) {
-    const U4 r = draw_words(L, k0, k1, g, it, round);
+    const U4 r = philox4x32_10(U4{g >> 1, it, (uint32_t)L.stream, round}, k0, k1);
+    const bool h = (g & 1u) != 0;
     double mu, sg;
-    src.pick((double)r.x * 0x1.0p-32, mu, sg);
-    return box_muller(r, mu, sg);
+    src.pick((double)(h ? r.z : r.x) * 0x1.0p-32, mu, sg);
+    const double rad = bm_radius(r.y);
+    double c, s;
+    sincos_turn32(r.w, c, s);
+    return fma(sg, rad * (h ? s : c), mu);
+}
+
+// Slot r of thread t in a tile of R x nthreads candidates (R even): slots
+// r, r + 1 are one Box-Muller pair, candidates 2 ((r / 2) nthreads + t) and
+// the next one
+__device__ __host__ __forceinline__ uint32_t tile_cand(int r, uint32_t t, uint32_t nthreads) {
+    return 2u * ((uint32_t)(r >> 1) * nthreads + t) + (uint32_t)(r & 1);
 }
 
 // LGMM1 sample value of an accepted log-space draw (tpe.py:255: np.exp);
@@ -356,39 +376,62 @@ __device__ __forceinline__ bool sample_slots(const DLabel& L, const Src& src, ui
 // every slot straight-line; the rejected slots go to an LDS list and the
 // whole workgroup retries them together, each list entry walking its own
 // attempts 1, 2, .. -- so a rejection costs one lane-attempt instead of a
-// wave-wide queue iteration (the same draws, bit for bit).  g0 + slot is a
-// slot's global candidate index (slot = r * blockDim + threadIdx.x).
+// wave-wide queue iteration (the same draws, bit for bit).  Slot r of
+// thread t holds candidate g0 + tile_cand(r, t, blockDim): slots r, r + 1 are
+// a Box-Muller pair, drawn by one Philox call (draw_pair) when g0 is even.
 template <int R>
 struct RetryLds {
-    int n;
-    int32_t slot[R * 256];
+    int n[2];                 // per tile parity: this tile's count, the next tile's (reset)
+    uint16_t slot[R * 256];   // candidate offset within the tile
     double val[R * 256];
 };
 
+// (every thread of the workgroup calls it; q.n[0] = q.n[1] = 0 before the
+// first tile, a barrier in between; `par` alternates 0, 1 over the tiles:
+// two barriers per tile)
 template <int MODE, int R, typename Src, bool RAW = false>
 __device__ __forceinline__ bool sample_tile(const DLabel& L, const Src& src, uint64_t seed, uint32_t rk,
-                                            uint32_t g0, uint32_t pend, double (&out)[R], RetryLds<R>& q) {
+                                            uint32_t g0, uint32_t pend, double (&out)[R], RetryLds<R>& q,
+                                            int par) {
     static_assert(MODE != CAT, "categorical slots draw once each");
+    static_assert(R * 256 <= 65536, "tile offsets are 16-bit");
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     const bool bounded = (L.flags & 3) == 3;
-    __syncthreads();   // the previous tile's list is read
-    if (threadIdx.x == 0) q.n = 0;
-    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = (1ull << lane) - 1ull;
     int pos[R];
+    static_assert(R % 2 == 0, "sample_tile draws Box-Muller pairs");
+    const bool paired = (g0 & 1u) == 0;   // (an odd first index: each slot on its own, the same bits)
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const uint32_t slot = (uint32_t)(r * blockDim.x + threadIdx.x);
-        const double draw = draw_attempt(L, src, k0, k1, g0 + slot, 0u, rk);
-        const bool p = (pend >> r) & 1u;
-        out[r] = p ? draw : out[r];
-        pos[r] = -1;
-        if (p && bounded && !(L.low <= draw && draw < L.high)) {
-            pos[r] = atomicAdd(&q.n, 1);
-            q.slot[pos[r]] = (int32_t)slot;
+    for (int r = 0; r < R; r += 2) {
+        const uint32_t c0 = tile_cand(r, threadIdx.x, blockDim.x);
+        double dd[2];
+        if (paired) {
+            draw_pair(L, src, k0, k1, (g0 + c0) >> 1, 0u, rk, dd[0], dd[1]);
+        } else {
+            dd[0] = draw_attempt(L, src, k0, k1, g0 + c0, 0u, rk);
+            dd[1] = draw_attempt(L, src, k0, k1, g0 + c0 + 1u, 0u, rk);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const double draw = dd[h];
+            const bool p = (pend >> (r + h)) & 1u;
+            out[r + h] = p ? draw : out[r + h];
+            // rejected slots onto the list: one LDS atomic per wave
+            const bool rej = p && bounded && !(L.low <= draw && draw < L.high);
+            const uint64_t bal = __ballot(rej);
+            int base = 0;
+            if (bal) {
+                if (lane == 0) base = atomicAdd(&q.n[par], (int)__popcll(bal));
+                base = __shfl(base, 0);
+            }
+            pos[r + h] = rej ? base + (int)__popcll(bal & lt) : -1;
+            if (rej) q.slot[pos[r + h]] = (uint16_t)(c0 + (uint32_t)h);
         }
     }
-    __syncthreads();
-    const int n = q.n;
+    __syncthreads();   // the list is complete
+    const int n = q.n[par];
+    if (threadIdx.x == 0) q.n[par ^ 1] = 0;   // (its last reader finished before the previous tile's end)
     bool ok = true;
     for (int e = threadIdx.x; e < n; e += blockDim.x) {
         const uint32_t gg = g0 + (uint32_t)q.slot[e];

@@ -807,13 +807,18 @@ __global__ __launch_bounds__(kBlock) void k_hot_bits(const int32_t* __restrict__
 
 // Draw every candidate of the round (the same draws as k_screen_bx) and
 // test its sub-bin's bit (U >= tau0, k_hot_bits: 4 KB per label at config 3,
-// L1-resident): the candidates whose bit is set (and those outside the
-// sub-bins) are listed with their draw -- (hidx, hx)[cell n + position],
-// hcnt[cell].  The largest L of the cell is taken over the LISTED candidates
-// (k_screen_hot): a candidate left out has L <= U < tau0, so the cell's
-// largest L reaches tau0 iff a listed candidate's does.  Tile map only:
-// workgroups stride over the cell's tiles of R * 256 candidates (the
-// sampling records are staged once per workgroup, not once per tile).
+// staged in LDS when it fits): the candidates whose bit is set (and those
+// outside the sub-bins) are listed with their draw -- (hidx, hx)[cell
+// hstride + position], hcnt[cell].  The largest L of the cell is taken over
+// the LISTED candidates (k_screen_hot): a candidate left out has L <= U <
+// tau0, so the cell's largest L reaches tau0 iff a listed candidate's does.
+// Tile map only: workgroups stride over the cell's tiles of R * 256
+// candidates (Box-Muller pairs per thread, the sampling records staged once
+// per workgroup -- the launch requires them in LDS).  The listed candidates
+// gather in an LDS buffer (one LDS atomic per wave and slot pair, no
+// barrier) and go to the cell's list with one global atomic per workgroup
+// at the end; past the buffer a wave appends straight to the list.
+constexpr int kHotBuf = 1024;
 template <int R>
 __global__ __launch_bounds__(kBlock, 4) void k_hot_bx(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
@@ -825,26 +830,35 @@ __global__ __launch_bounds__(kBlock, 4) void k_hot_bx(
     const DLabel L = labels[li];
     const BxLabel B = bx[li];
     __shared__ SampLds sl;
-    const bool staged = stage_samp(L, samp, &sl);
-    const int64_t nsb = (int64_t)B.nbins * kBxSub;
+    (void)stage_samp(L, samp, &sl);   // (the launch checked ns <= kSampLds)
+    const int nsb = B.nbins * kBxSub;
     const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
     const uint32_t rk = rounds[blockIdx.z];
     constexpr int64_t per = (int64_t)R * kBlock;
-    __shared__ int shc[kBlock / 64], shb;
-    // the label's bits in LDS when they fit (config 3: 32k sub-bins, 4 KB)
+    // the label's bits in LDS when they fit (config 3: 19k sub-bins, 2.4 KB)
     __shared__ uint32_t sbits[kHotLdsWords];
-    const bool lds_bits = nsb <= (int64_t)kHotLdsWords * 32;
+    const bool lds_bits = nsb <= kHotLdsWords * 32;
     if (lds_bits)
-        for (int w = threadIdx.x; w < (int)(nsb >> 5); w += kBlock) sbits[w] = hbits[(B.sb_off >> 5) + w];
-    __syncthreads();
+        for (int w = threadIdx.x; w < (nsb >> 5); w += kBlock) sbits[w] = hbits[(B.sb_off >> 5) + w];
     __shared__ RetryLds<R> retry;
-    for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per) {
+    __shared__ int32_t buf_i[kHotBuf];
+    __shared__ double buf_x[kHotBuf];
+    __shared__ int buf_n, gbase;
+    if (threadIdx.x == 0) {
+        retry.n[0] = retry.n[1] = 0;
+        buf_n = 0;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    int par = 0;
+    for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per, par ^= 1) {
         double x[R];
         int64_t ci[R];
         uint32_t pend = 0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            ci[r] = base + r * kBlock + threadIdx.x;
+            ci[r] = base + tile_cand(r, threadIdx.x, kBlock);
             x[r] = 0.0;
             if (ci[r] < n) pend |= 1u << r;
         }
@@ -853,58 +867,56 @@ __global__ __launch_bounds__(kBlock, 4) void k_hot_bx(
         // keeps the draw and k_screen_hot applies the exp.  (The family only
         // changes that exp, which RAW leaves out: one instantiation.)
         const uint32_t g0 = (uint32_t)(cand_offset + base);
-        const bool ok = staged ? sample_tile<DENSE_GMM, R, SampShared, true>(L, SampShared{&sl}, seed, rk, g0,
-                                                                             pend, x, retry)
-                               : sample_tile<DENSE_GMM, R, SampGlobal, true>(
-                                     L, SampGlobal{samp + L.samp_off, L.ns}, seed, rk, g0, pend, x, retry);
-        if (!ok) atomicOr(err, 1);
-        bool take[R];
-        int mine = 0;
+        if (!sample_tile<DENSE_GMM, R, SampShared, true>(L, SampShared{&sl}, seed, rk, g0, pend, x, retry, par))
+            atomicOr(err, 1);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            take[r] = false;
-            if (!((pend >> r) & 1u)) continue;
-            const double f = (x[r] - L.centre - B.xlo) * B.inv_sbw;
-            if (f >= 0.0 && f < (double)nsb) {
-                const int64_t j = (int64_t)f;   // (sb_off: a multiple of 32)
-                const uint32_t word = lds_bits ? sbits[j >> 5] : hbits[((B.sb_off + j) >> 5)];
-                take[r] = (word >> (j & 31)) & 1u;
-            } else {
-                take[r] = true;   // outside the bins (or NaN): always listed
-            }
-            mine += take[r];
-        }
-        // this tile's takers: one atomic per workgroup and tile
-        int tw = mine;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int o = __shfl_up(tw, off);
-            if ((threadIdx.x & 63) >= off) tw += o;
-        }
-        if ((threadIdx.x & 63) == 63) shc[threadIdx.x >> 6] = tw;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int tot = 0;
-            for (int w = 0; w < kBlock / 64; ++w) tot += shc[w];
-            shb = tot ? atomicAdd(hcnt + cell, tot) : 0;
-        }
-        __syncthreads();
-        int at = shb + tw - mine;
-        for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) at += shc[w];
-        __syncthreads();   // shc / shb are rewritten by the next tile
-        // a cell's list is hstride long: past it the round falls back to
-        // screening every candidate (hflag bit 2), so nothing is lost
-        if (at + mine > hstride) atomicOr(hflag, 2);
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-            if (take[r]) {
-                if (at < hstride) {
-                    hidx[cell * (size_t)hstride + at] = (int32_t)ci[r];
-                    hx[cell * (size_t)hstride + at] = x[r];
+            bool take = false;
+            if ((pend >> r) & 1u) {
+                const double f = (x[r] - L.centre - B.xlo) * B.inv_sbw;
+                if (f >= 0.0 && f < (double)nsb) {
+                    const int j = (int)f;   // (sb_off: a multiple of 32)
+                    const uint32_t word = lds_bits ? sbits[j >> 5] : hbits[(B.sb_off >> 5) + (j >> 5)];
+                    take = (word >> (j & 31)) & 1u;
+                } else {
+                    take = true;   // outside the bins (or NaN): always listed
                 }
-                ++at;
             }
+            const uint64_t bal = __ballot(take);
+            if (!bal) continue;
+            int at = 0;
+            if (lane == 0) at = atomicAdd(&buf_n, (int)__popcll(bal));
+            at = __shfl(at, 0);
+            const bool lds = at + (int)__popcll(bal) <= kHotBuf;   // wave-uniform
+            if (!lds) {   // the buffer is full: straight to the cell's list
+                if (lane == 0) at = atomicAdd(hcnt + cell, (int)__popcll(bal));
+                at = __shfl(at, 0);
+            }
+            if (take) {
+                const int k = at + (int)__popcll(bal & lt);
+                if (lds) {
+                    buf_i[k] = (int32_t)ci[r];
+                    buf_x[k] = x[r];
+                } else if (k < hstride) {
+                    hidx[cell * (size_t)hstride + k] = (int32_t)ci[r];
+                    hx[cell * (size_t)hstride + k] = x[r];
+                }
+            }
+            if (!lds && lane == 0 && at + (int)__popcll(bal) > hstride) atomicOr(hflag, 2);
+        }
     }
+    __syncthreads();
+    const int m = min(buf_n, kHotBuf);
+    if (threadIdx.x == 0) gbase = m ? atomicAdd(hcnt + cell, m) : 0;
+    __syncthreads();
+    // a cell's list is hstride long: past it the round falls back to
+    // screening every candidate (hflag bit 2), so nothing is lost
+    if (threadIdx.x == 0 && gbase + m > hstride) atomicOr(hflag, 2);
+    for (int k = threadIdx.x; k < m; k += kBlock)
+        if (gbase + k < hstride) {
+            hidx[cell * (size_t)hstride + gbase + k] = buf_i[k];
+            hx[cell * (size_t)hstride + gbase + k] = buf_x[k];
+        }
 }
 
 // The expansion screen over the listed candidates only: workgroups stride
@@ -2048,6 +2060,9 @@ __global__ __launch_bounds__(kBlock, 4) void k_qfused_tiles(
     __syncthreads();
     const bool early = found && Q.G > 0 && Q.jlo <= Q.jhi;
     const uint64_t kmax = early ? qkmax[qbase + blockIdx.y] : 0;
+    if (threadIdx.x == 0) retry.n[0] = retry.n[1] = 0;
+    __syncthreads();
+    int par = 0;
     bool reported = false;
     int64_t ndrawn = 0;
     uint64_t bk = 0;
@@ -2062,12 +2077,13 @@ __global__ __launch_bounds__(kBlock, 4) void k_qfused_tiles(
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             v[r] = 0.0;
-            if (base + r * kBlock + threadIdx.x < n) pend |= 1u << r;
+            if (base + tile_cand(r, threadIdx.x, kBlock) < n) pend |= 1u << r;
         }
         const uint32_t g0 = (uint32_t)(cand_offset + base);
-        const bool ok = staged ? sample_tile<MODE, R>(L, SampShared{&sl}, seed, rk, g0, pend, v, retry)
+        const bool ok = staged ? sample_tile<MODE, R>(L, SampShared{&sl}, seed, rk, g0, pend, v, retry, par)
                                : sample_tile<MODE, R>(L, SampGlobal{samp + L.samp_off, L.ns}, seed, rk, g0, pend,
-                                                      v, retry);
+                                                      v, retry, par);
+        par ^= 1;
         if (!ok) atomicOr(err, 1);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -2077,7 +2093,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_qfused_tiles(
             if (jd >= -0x1.0p52 && jd <= 0x1.0p52) j = (int64_t)jd;
             else atomicOr(err, 8);
             const int64_t sidx = j - Q.jmin;
-            const int64_t gi = cand_offset + base + r * kBlock + threadIdx.x;
+            const int64_t gi = cand_offset + base + tile_cand(r, threadIdx.x, kBlock);
             if (lds_keys && sidx >= 0 && sidx < Q.G) {
                 const uint64_t key = skey[sidx];
                 if (better(key, gi, bk, bi)) {
@@ -2728,6 +2744,8 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
             use_bx = ctx->P->bx_ok;
         }
         hot = use_bx && ctx->hot != 0 && ctx->P->bx_sb.p != nullptr;
+        for (int m : {DENSE_GMM, DENSE_LGMM})   // k_hot_bx stages every label's sampling records
+            for (int li : ctx->P->h_group[m]) hot = hot && ctx->P->h_labels[li].ns <= kSampLds;
         // the expansion screen's appends: a cell's hot list at most (the
         // prefilter), else any candidate of the round
         int64_t lst = hot ? hot_stride(ctx, a.n) : a.n;

@@ -5,7 +5,7 @@ the patched sources, so the product loader refuses it unless the process
 opts in explicitly with HYPEROPT_AMD_VARIANT=<path to the variant> (the
 product library in hyperopt_amd/ is never overwritten).
 
-    python tools/build_variant.py bm        # Box-Muller replaced by a cheap affine map (not a normal draw)
+    python tools/build_variant.py bm        # Box-Muller radius without its log and sqrt (not a normal draw)
     python tools/build_variant.py norej     # no truncation rejection (wrong samples)
     python tools/build_variant.py hot4 -DTPE_HOT_R=4   # a compile-time constant changed
 
@@ -25,9 +25,8 @@ from hyperopt_amd import _build  # noqa: E402
 # name -> [(file, old text, new text)]: result-changing timing experiments
 PATCHES = {
     'bm': [('tpe_device.h',
-            '    const double u1 = u01_open0(r.y, r.z);\n',
-            '    return fma(sg, (double)(int32_t)r.w * 0x1.0p-29, mu);\n'
-            '    const double u1 = u01_open0(r.y, r.z);\n')],
+            '    return __builtin_amdgcn_sqrt(fmax(0.0, 2.0 * bm_neglog(u01_open0(y))));\n',
+            '    return (double)y * 0x1.0p-31;\n')],
     'norej': [('tpe_device.h',
                '    const bool bounded = (L.flags & 3) == 3;\n    const uint32_t mask0 = pend;',
                '    const bool bounded = false;\n    const uint32_t mask0 = pend;')],
