@@ -98,7 +98,11 @@ struct U4 {
 
 __device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
     // one 32x32 -> 64-bit product per multiplier (v_mad_u64_u32) instead of
-    // separate low and high multiplies: the same words, a third faster
+    // separate low and high multiplies: the same words, a third faster.  The
+    // keys pass through an empty asm, so the 20 round keys are recomputed by
+    // the scalar unit per call instead of being hoisted out of the caller's
+    // loops -- held there, they spilled and came back by v_readlane (VALU).
+    asm volatile("" : "+s"(k0), "+s"(k1));
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
         const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
