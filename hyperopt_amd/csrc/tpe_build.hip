@@ -1411,16 +1411,21 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
                        ctx->errflag.p);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(ctx->ev1, st));
-    int32_t errh = 0;
-    HIPCHK(ctx, hipMemcpyAsync(dl.data(), P.labels.p, n_labels * sizeof(DLabel), hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipMemcpyAsync(&errh, ctx->errflag.p, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, ctx->dl_h.resize(n_labels));
+    HIPCHK(ctx, ctx->ties_h.resize(n_labels + 1));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->dl_h.data(), P.labels.p, n_labels * sizeof(DLabel), hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipMemcpyAsync(&ctx->pin[0].err, ctx->errflag.p, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     if (ties_out)
-        HIPCHK(ctx, hipMemcpyAsync(ties_out, B.ties.p, (n_labels + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->ties_h.data(), B.ties.p, (n_labels + 1) * sizeof(int32_t),
+                                   hipMemcpyDeviceToHost, st));
     {   // does the expansion index of the previous posterior still hold?
         const int rc = tpe_rt::bx_keep_check(ctx);
         if (rc) return rc;
     }
     HIPCHK(ctx, hipStreamSynchronize(st));
+    const int32_t errh = ctx->pin[0].err;
+    std::memcpy(dl.data(), ctx->dl_h.data(), n_labels * sizeof(DLabel));
+    if (ties_out) std::memcpy(ties_out, ctx->ties_h.data(), (n_labels + 1) * sizeof(int32_t));
     HIPCHK(ctx, hipEventElapsedTime(&ctx->build_ms, ctx->ev0, ctx->ev1));
     if (errh & 1) return ctx->fail(TPE_ERR_ARG, "observation trial position out of range");
     if (errh & 2) return ctx->fail(TPE_ERR_ARG, "more below observations than the below set (duplicate trial in a label?)");

@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -86,6 +87,48 @@ struct DevBuf {
     ~DevBuf() { release(); }   // (every buffer a context holds goes with it)
 };
 
+// Page-locked host memory for the per-round read-backs: an async D2H copy
+// into pageable memory runs as a staged copy the host waits for (~20 us
+// each, several per round); into pinned memory it is one DMA on the stream.
+template <typename T>
+struct PinVec {
+    T* p = nullptr;
+    size_t n = 0, cap = 0;
+    hipError_t resize(size_t m) {
+        if (m > cap) {
+            if (p) (void)hipHostFree(p);
+            p = nullptr;
+            cap = n = 0;
+            const size_t c = std::max<size_t>(m + m / 4, 16);
+            const hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), c * sizeof(T), hipHostMallocDefault);
+            if (e != hipSuccess) {
+                p = nullptr;
+                return e;
+            }
+            cap = c;
+        }
+        n = m;
+        return hipSuccess;
+    }
+    T* data() { return p; }
+    const T* data() const { return p; }
+    size_t size() const { return n; }
+    T& operator[](size_t i) { return p[i]; }
+    const T& operator[](size_t i) const { return p[i]; }
+    PinVec() = default;
+    PinVec(const PinVec&) = delete;
+    PinVec& operator=(const PinVec&) = delete;
+    ~PinVec() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+
+// the scalar read-backs of a call, in one pinned block
+struct PinScalars {
+    int32_t err = 0, hot_flag = 0, bx_diff = 1, pad = 0;
+    unsigned long long screen_exec = 0, xdrawn[2] = {0, 0};
+};
+
 struct Posterior {
     std::vector<DLabel> h_labels;
     std::vector<int32_t> h_group[kNumModes];   // label ids per mode
@@ -133,7 +176,6 @@ struct Posterior {
     DevBuf<tpe::SampRec> bx_snap_s;
     DevBuf<int32_t> bx_snap_g;           // the dense label positions
     DevBuf<int32_t> bx_diff;             // compare result (0: identical)
-    int32_t bx_diff_h = 1;
     int32_t bx_snap_nl = 0;
     void release() {
         labels.release();
@@ -310,8 +352,7 @@ struct tpe_ctx {
     DevBuf<unsigned long long> hot_t, hot_tau0;   // per cell largest L; per label tau0
     DevBuf<uint32_t> hot_bits;           // per sub-bin: U >= tau0 (words at sb_off / 32)
     DevBuf<int32_t> hot_flag;            // fallback flag
-    std::vector<int32_t> hot_cnt_h;
-    int32_t hot_flag_h = 0;
+    tpe_rt::PinVec<int32_t> hot_cnt_h;
     int64_t hot_listed = 0;              // last round: candidates the prefilter listed
     int32_t hot_fallback = 0;            // last round: 1 if it re-ran the plain screen
     bool hot_ran = false;
@@ -323,7 +364,11 @@ struct tpe_ctx {
     DevBuf<int32_t> scr_idx;
     DevBuf<unsigned long long> scr_lb;
     DevBuf<int32_t> scr_cnt;
-    std::vector<int32_t> scr_cnt_h;
+    tpe_rt::PinVec<int32_t> scr_cnt_h;
+    tpe_rt::PinVec<tpe_rt::PinScalars> pin;   // one entry: the scalar read-backs
+    tpe_rt::PinVec<tpe_label_result> res_h;   // a round's results, staged before the caller's buffer
+    tpe_rt::PinVec<tpe::DLabel> dl_h;         // a build's label records, read back
+    tpe_rt::PinVec<int32_t> ties_h;           //   and its tie report
     DevBuf<int64_t> scr_chunks;          // k_rescore chunk table ({cell, chunk} int32 pairs)
     DevBuf<int64_t> scr_list;            // packed map: per label, (round << 32 | candidate) to re-score
     DevBuf<Partial> scr_res;             //   their fp64 results
@@ -366,6 +411,7 @@ struct tpe_ctx {
     // one peer context per further device; a peer running one shard of a
     // round gets the whole problem's size and the window exchange
     std::vector<tpe_ctx*> peers;
+    std::shared_ptr<void> workers;       // one persistent host thread per peer (tpe_multi.hip)
     int64_t hint_n = 0;                  // candidates per round over all shards (0: this call's)
     int32_t hint_rounds = 0;             // rounds over all shards (0: this call's)
     // the same, set by the caller for the life of the context (one process
@@ -434,7 +480,7 @@ int64_t win_rounds_per_batch(int64_t n, int32_t nl);
 int bx_prepare(tpe_ctx* ctx);
 int bx_build(tpe_ctx* ctx);
 // Before a rebuild's final sync: queue the comparison of the rebuilt dense
-// labels against the index's snapshot (result in P.bx_diff_h after the
+// labels against the index's snapshot (result in ctx->pin[0].bx_diff after the
 // sync); bx_keep_after: whether the index stays valid.
 int bx_keep_check(tpe_ctx* ctx);
 bool bx_keep_after(tpe_ctx* ctx, bool groups_changed);
@@ -453,7 +499,7 @@ TPE_DEV int tpe1_suggest_batch(tpe_ctx* ctx, uint64_t seed, const uint32_t* roun
                                int32_t n_rounds, int64_t n_candidates, int64_t cand_offset,
                                tpe_label_result* out);
 TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value);
-TPE_DEV int tpe1_prepare(tpe_ctx* ctx, int64_t n_candidates);
+TPE_DEV int tpe1_prepare(tpe_ctx* ctx, int64_t n_candidates, int32_t n_rounds);
 TPE_DEV int tpe1_history_reset(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
                                const double* cat_p, int64_t n_cat_p);
 TPE_DEV int tpe1_history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial,

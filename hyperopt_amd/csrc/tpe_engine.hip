@@ -2599,7 +2599,7 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
         hipLaunchKernelGGL(k_pick_win<double2>, dim3((unsigned)((a.n_rounds + kBlock - 1) / kBlock), nl),
                            dim3(kBlock), 0, ctx->stream, ctx->bx_lohi.p, a.n_rounds, (int32_t)a.n,
                            ctx->scr_cnt.p, ctx->scr_list.p, cap, rsel, nl);
-        HIPCHK(ctx, hipMemcpyAsync(&ctx->screen_exec_h, ctx->win_evals.p, sizeof(unsigned long long),
+        HIPCHK(ctx, hipMemcpyAsync(&ctx->pin[0].screen_exec, ctx->win_evals.p, sizeof(unsigned long long),
                                    hipMemcpyDeviceToHost, ctx->stream));
         ctx->screen_exec_pending = true;
     } else if (ctx->window && cap >= kWinMinN && (int64_t)nl * cap <= ((int64_t)1 << 30)) {
@@ -2618,7 +2618,7 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
         hipLaunchKernelGGL(k_pick_win<float2>, dim3((unsigned)((a.n_rounds + kBlock - 1) / kBlock), nl),
                            dim3(kBlock), 0, ctx->stream, ctx->win_lohi.p, a.n_rounds, (int32_t)a.n,
                            ctx->scr_cnt.p, ctx->scr_list.p, cap, rsel, nl);
-        HIPCHK(ctx, hipMemcpyAsync(&ctx->screen_exec_h, ctx->win_evals.p, sizeof(unsigned long long),
+        HIPCHK(ctx, hipMemcpyAsync(&ctx->pin[0].screen_exec, ctx->win_evals.p, sizeof(unsigned long long),
                                    hipMemcpyDeviceToHost, ctx->stream));
         ctx->screen_exec_pending = true;
     } else {
@@ -2634,7 +2634,7 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
                            ctx->scr_list.p, cap, rsel, S8);
         ctx->screen_exec += (int64_t)a.n_rounds * a.n * dense_terms(ctx);
     }
-    ctx->scr_cnt_h.resize(nl);
+    HIPCHK(ctx, ctx->scr_cnt_h.resize(nl));
     HIPCHK(ctx, hipMemcpyAsync(ctx->scr_cnt_h.data(), ctx->scr_cnt.p, nl * sizeof(int32_t),
                                hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
@@ -2804,13 +2804,13 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
             if (hot) {
                 hipLaunchKernelGGL(k_hot_check, dim3(1), dim3(kBlock), 0, ctx->stream, (int64_t)cells, nl,
                                    ctx->hot_t.p, ctx->hot_tau0.p, ctx->hot_flag.p);
-                ctx->hot_cnt_h.resize(cells);
+                HIPCHK(ctx, ctx->hot_cnt_h.resize(cells));
                 HIPCHK(ctx, hipMemcpyAsync(ctx->hot_cnt_h.data(), ctx->hot_cnt.p, cells * sizeof(int32_t),
                                            hipMemcpyDeviceToHost, ctx->stream));
-                HIPCHK(ctx, hipMemcpyAsync(&ctx->hot_flag_h, ctx->hot_flag.p, sizeof(int32_t),
+                HIPCHK(ctx, hipMemcpyAsync(&ctx->pin[0].hot_flag, ctx->hot_flag.p, sizeof(int32_t),
                                            hipMemcpyDeviceToHost, ctx->stream));
             }
-            HIPCHK(ctx, hipMemcpyAsync(&ctx->screen_exec_h, ctx->win_evals.p, sizeof(unsigned long long),
+            HIPCHK(ctx, hipMemcpyAsync(&ctx->pin[0].screen_exec, ctx->win_evals.p, sizeof(unsigned long long),
                                        hipMemcpyDeviceToHost, ctx->stream));
             ctx->screen_exec_pending = true;
         } else if (ctx->window && a.n >= kWinMinN && a.cand_in == nullptr) {
@@ -2879,7 +2879,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                                    sorted);
                 if (pipe) HIPCHK(ctx, hipEventRecord(ctx->ev_done[slot], ctx->stream));
             }
-            HIPCHK(ctx, hipMemcpyAsync(&ctx->screen_exec_h, ctx->win_evals.p, sizeof(unsigned long long),
+            HIPCHK(ctx, hipMemcpyAsync(&ctx->pin[0].screen_exec, ctx->win_evals.p, sizeof(unsigned long long),
                                        hipMemcpyDeviceToHost, ctx->stream));
             ctx->screen_exec_pending = true;
         } else {
@@ -2898,19 +2898,19 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
         // overwrite theirs (one chunk table per round trip: the counts)
         hipLaunchKernelGGL(k_fill_empty, dim3((unsigned)std::min<int64_t>((a.tiles + kBlock - 1) / kBlock, 64), nl, a.gz),
                            dim3(kBlock), 0, ctx->stream, grp, ctx->P->n_labels, a.tiles, ctx->partials.p);
-        ctx->scr_cnt_h.resize(cells);
+        HIPCHK(ctx, ctx->scr_cnt_h.resize(cells));
         HIPCHK(ctx, hipMemcpyAsync(ctx->scr_cnt_h.data(), ctx->scr_cnt.p, cells * sizeof(int32_t),
                                    hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
         if (hot) {
             ctx->hot_ran = true;
             for (size_t c = 0; c < cells; ++c) ctx->hot_listed += ctx->hot_cnt_h[c];
-            if (ctx->hot_flag_h) {
+            if (ctx->pin[0].hot_flag) {
                 // a cell's best lower bound stayed below tau0 (bit 1: the
                 // list may miss winners) or a list overflowed (bit 2) --
                 // screen every candidate instead, into full-length lists
-                ctx->hot_fallback = ctx->hot_flag_h;
-                if ((ctx->hot_flag_h & 2) && ctx->hot_cap_div > 1.0)   // the next rounds list more
+                ctx->hot_fallback = ctx->pin[0].hot_flag;
+                if ((ctx->pin[0].hot_flag & 2) && ctx->hot_cap_div > 1.0)   // the next rounds list more
                     ctx->hot_cap_div = std::max(1.0, ctx->hot_cap_div / 4.0);
                 lst = a.n;
                 HIPCHK(ctx, ctx->scr_hid.reserve(cells * lst));
@@ -2920,7 +2920,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                 screen_bx_all(ctx, grp, nl, a);
                 hipLaunchKernelGGL(k_select_list, dim3((unsigned)cells), dim3(kBlock), 0, ctx->stream,
                                    ctx->scr_hid.p, lst, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p);
-                HIPCHK(ctx, hipMemcpyAsync(&ctx->screen_exec_h, ctx->win_evals.p, sizeof(unsigned long long),
+                HIPCHK(ctx, hipMemcpyAsync(&ctx->pin[0].screen_exec, ctx->win_evals.p, sizeof(unsigned long long),
                                            hipMemcpyDeviceToHost, ctx->stream));
                 HIPCHK(ctx, hipMemcpyAsync(ctx->scr_cnt_h.data(), ctx->scr_cnt.p, cells * sizeof(int32_t),
                                            hipMemcpyDeviceToHost, ctx->stream));
@@ -3388,19 +3388,24 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         HIPCHK(ctx, hipGetLastError());
     }
     if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->ev2, ctx->stream));
-    int32_t errh = 0;
-    HIPCHK(ctx, hipMemcpyAsync(&errh, ctx->errflag.p, sizeof(int32_t), hipMemcpyDeviceToHost,
-                               ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(ctx->xdrawn_h, ctx->xdrawn.p, 2 * sizeof(unsigned long long),
+    PinScalars& pin = ctx->pin[0];
+    HIPCHK(ctx, hipMemcpyAsync(&pin.err, ctx->errflag.p, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(pin.xdrawn, ctx->xdrawn.p, 2 * sizeof(unsigned long long),
                                hipMemcpyDeviceToHost, ctx->stream));
-    if (tiles > 0 && out)
-        HIPCHK(ctx, hipMemcpyAsync(out, ctx->results.p,
-                                   (size_t)n_rounds * L * sizeof(tpe_label_result),
+    const size_t n_res = (size_t)n_rounds * L;
+    if (tiles > 0 && out) {
+        HIPCHK(ctx, ctx->res_h.resize(n_res));
+        HIPCHK(ctx, hipMemcpyAsync(ctx->res_h.data(), ctx->results.p, n_res * sizeof(tpe_label_result),
                                    hipMemcpyDeviceToHost, ctx->stream));
+    }
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (tiles > 0 && out) std::memcpy(out, ctx->res_h.data(), n_res * sizeof(tpe_label_result));
+    const int32_t errh = pin.err;
+    ctx->xdrawn_h[0] = pin.xdrawn[0];
+    ctx->xdrawn_h[1] = pin.xdrawn[1];
     ctx->screen_ms = 0.f;
     if (ctx->screen_exec_pending) {
-        ctx->screen_exec += (int64_t)ctx->screen_exec_h;
+        ctx->screen_exec += (int64_t)ctx->pin[0].screen_exec;
         ctx->screen_exec_pending = false;
     }
     if (ctx->screen_pending) {
@@ -3663,6 +3668,8 @@ int tpe_ctx_create(int device, int precision, tpe_ctx** out) {
     for (int j = 0; j < 2; ++j)
         ok = ok && hipEventCreateWithFlags(&c->ev_sorted[j], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&c->ev_done[j], hipEventDisableTiming) == hipSuccess;
+    ok = ok && c->pin.resize(1) == hipSuccess;
+    if (ok) c->pin[0] = PinScalars{};
     if (!ok) {
         g_create_error = "stream/event creation failed";
         tpe_ctx_destroy(c);
@@ -3959,13 +3966,17 @@ int tpe_last_rescore_terms(const tpe_ctx* ctx, int64_t* terms) {
     return TPE_OK;
 }
 
-TPE_DEV int tpe1_prepare(tpe_ctx* ctx, int64_t n_candidates) {
+TPE_DEV int tpe1_prepare(tpe_ctx* ctx, int64_t n_candidates, int32_t n_rounds) {
     if (!ctx) return TPE_ERR_ARG;
     if (!ctx->P || ctx->P->n_labels <= 0) return ctx->fail(TPE_ERR_ARG, "no resident posterior");
-    if (ctx->precision != TPE_F64 || !ctx->screen || !ctx->expand || n_candidates < kWinMinN) return TPE_OK;
+    if (n_candidates < 0 || n_rounds < 1) return ctx->fail(TPE_ERR_ARG, "bad candidate/round count");
+    // the rounds that use the index: tile rounds of >= kWinMinN candidates,
+    // packed rounds of >= kWinMinN slots in total (launch_dense)
+    if (ctx->precision != TPE_F64 || !ctx->screen || !ctx->expand || n_candidates * n_rounds < kWinMinN)
+        return TPE_OK;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     int rc = tpe_rt::bx_prepare(ctx);
-    if (rc == TPE_OK && ctx->hot) rc = hot_tau_prepare(ctx, n_candidates);
+    if (rc == TPE_OK && ctx->hot && n_candidates >= kWinMinN) rc = hot_tau_prepare(ctx, n_candidates);
     return rc;
 }
 

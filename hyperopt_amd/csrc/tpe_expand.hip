@@ -279,7 +279,7 @@ __device__ __forceinline__ double bcast(double v, int j) {
 // e^y <= e^Y (Y = 2 kappa D rmax), so the per-component terms of the bound
 // are accumulated as four sums and combined at the end (each term at least
 // what the per-component form gives).
-constexpr int kTabSums = kBxP + 5;   // A_0..A_14, S0..S3, W
+constexpr int kTabSums = kBxP + 3;   // A_0..A_14, S0, S1, S3
 static_assert(3 * kTabSums * 64 <= kExpTabSize, "k_bx_table: 3 waves' partial sums in the exp table's LDS");
 __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ labels,
                                                      const int32_t* __restrict__ grp,
@@ -309,8 +309,7 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
     double A[kBxP];
 #pragma unroll
     for (int n = 0; n < kBxP; ++n) A[n] = 0.0;
-    double S0 = 0.0, S1 = 0.0, S2 = 0.0, S3 = 0.0;   // sum g, g |arg|, g |mu|, |g (2 kappa d)^P|
-    double W = 0.0;
+    double S0 = 0.0, S1 = 0.0, S3 = 0.0;   // sum g, g |arg|, |g (2 kappa d)^P|
     // mu' = m' (1 / a*): <= 1.5 ulp (inside the 2^-51 allowance below);
     // g = exp(arg) through the fp64 round's table exp (<= 2.6e-14 relative,
     // added to the rounding term); the powers g (2 kappa d)^n by one
@@ -327,28 +326,37 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
             }
         }
         const int cnt = min(64, k1 - kc);
-        for (int j = 0; j < cnt; ++j) {
-            const double cj = bcast(c_l, j);
-            if (!(cj > -kInf)) continue;   // unclipped or weightless (wave-uniform)
-            const double mu = bcast(mu_l, j), d = mu - xb;
-            const double arg = fmax(cj - kap * d * d, -745.0);
+        // two components per step: independent exp and power chains
+        for (int j = 0; j < cnt; j += 2) {
+            const int j1 = min(j + 1, 63);
+            const double c0 = bcast(c_l, j), c1 = j + 1 < cnt ? bcast(c_l, j1) : -kInf;
+            if (!(c0 > -kInf) && !(c1 > -kInf)) continue;   // unclipped or weightless (wave-uniform)
+            const double mu0 = bcast(mu_l, j), mu1 = bcast(mu_l, j1);
+            const double d0 = mu0 - xb, d1 = mu1 - xb;
+            const double a0 = fmax(c0 - kap * d0 * d0, -745.0), a1 = fmax(c1 - kap * d1 * d1, -745.0);
             // outside the bin's window, or below 2^-1067 in the whole bin (in
             // the skip term): g = 0, so every sum below is unchanged
-            const bool in = fabs(d) <= D && arg > -740.0;
-            const double e = exp_scaled(fmin(arg * kExpScale, 0.0), lds);
-            const double g = in ? e : 0.0, two = 2.0 * kap * d;
-            double t = g;
-            A[0] += t;
+            const bool in0 = fabs(d0) <= D && a0 > -740.0, in1 = fabs(d1) <= D && a1 > -740.0;
+            const double e0 = exp_scaled(fmin(a0 * kExpScale, 0.0), lds);
+            const double e1 = exp_scaled(fmin(a1 * kExpScale, 0.0), lds);
+            const double g0 = in0 ? e0 : 0.0, g1 = in1 ? e1 : 0.0;
+            const double y0 = 2.0 * kap * d0, y1 = 2.0 * kap * d1;
+            double t0 = g0, t1 = g1;
+            A[0] += t0;
+            A[0] += t1;
 #pragma unroll
             for (int n = 1; n < kBxP; ++n) {
-                t *= two;
-                A[n] = fma(t, kInvFact[n], A[n]);
+                t0 *= y0;
+                t1 *= y1;
+                A[n] = fma(t0, kInvFact[n], A[n]);
+                A[n] = fma(t1, kInvFact[n], A[n]);
             }
-            S0 += g;
-            S1 = fma(g, fabs(arg), S1);
-            S2 = fma(g, fabs(mu), S2);
-            S3 += fabs(t * two);
-            W += in ? 1.0 : 0.0;
+            S0 += g0;
+            S0 += g1;
+            S1 = fma(g0, fabs(a0), S1);
+            S1 = fma(g1, fabs(a1), S1);
+            S3 += fabs(t0 * y0);
+            S3 += fabs(t1 * y1);
         }
     }
     __syncthreads();   // the exp table is no longer read: partial sums of waves 1..3
@@ -358,9 +366,7 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
         for (int n = 0; n < kBxP; ++n) p[n * 64] = A[n];
         p[(kBxP + 0) * 64] = S0;
         p[(kBxP + 1) * 64] = S1;
-        p[(kBxP + 2) * 64] = S2;
-        p[(kBxP + 3) * 64] = S3;
-        p[(kBxP + 4) * 64] = W;
+        p[(kBxP + 2) * 64] = S3;
     }
     __syncthreads();
     if (wave > 0 || b >= B.nbins) return;
@@ -370,10 +376,12 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
         for (int n = 0; n < kBxP; ++n) A[n] += p[n * 64];
         S0 += p[(kBxP + 0) * 64];
         S1 += p[(kBxP + 1) * 64];
-        S2 += p[(kBxP + 2) * 64];
-        S3 += p[(kBxP + 3) * 64];
-        W += p[(kBxP + 4) * 64];
+        S3 += p[(kBxP + 2) * 64];
     }
+    // every summed component has |d| <= D: |mu'| <= |xb| + D, and at most
+    // the window's k1 - k0 of them were summed
+    const double S2 = (fabs(xb) + D) * S0 * (1.0 + 1e-15);   // >= sum g |mu'|
+    const double W = (double)(k1 - k0);
     // e^y <= 1 + y + y^2 for 0 <= y <= 1.79, else exp(y) (1 + 1e-6)
     const double Y = 2.0 * kap * D * r, eY = Y <= 1.5 ? fma(Y, Y, 1.0 + Y) : exp(Y) * 1.000001;
     const double G = eY * S0;                                  // sum_k g e^y
@@ -653,7 +661,7 @@ __global__ __launch_bounds__(kBlock) void k_bx_compare(const int32_t* __restrict
 
 int tpe_rt::bx_keep_check(tpe_ctx* ctx) {
     tpe_rt::Posterior& P = *ctx->P;
-    P.bx_diff_h = 1;
+    ctx->pin[0].bx_diff = 1;
     if (!P.bx_ready || P.bx_snap_nl <= 0) return TPE_OK;
     HIPCHK(ctx, P.bx_diff.reserve(1));
     HIPCHK(ctx, hipMemsetAsync(P.bx_diff.p, 0, sizeof(int32_t), ctx->stream));
@@ -662,13 +670,14 @@ int tpe_rt::bx_keep_check(tpe_ctx* ctx) {
                        (int64_t)std::min(P.comps64.cap, P.bx_snap_c.cap),
                        (int64_t)std::min(P.samp.cap, P.bx_snap_s.cap), P.bx_diff.p);
     HIPCHK(ctx, hipGetLastError());
-    HIPCHK(ctx, hipMemcpyAsync(&P.bx_diff_h, P.bx_diff.p, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(&ctx->pin[0].bx_diff, P.bx_diff.p, sizeof(int32_t), hipMemcpyDeviceToHost,
+                               ctx->stream));
     return TPE_OK;
 }
 
 bool tpe_rt::bx_keep_after(tpe_ctx* ctx, bool groups_changed) {
     tpe_rt::Posterior& P = *ctx->P;
-    return P.bx_ready && P.bx_snap_nl > 0 && !groups_changed && P.bx_diff_h == 0;
+    return P.bx_ready && P.bx_snap_nl > 0 && !groups_changed && ctx->pin[0].bx_diff == 0;
 }
 
 // The index is queued on the context's stream without waiting for it (one

@@ -39,27 +39,87 @@ int ndev(const tpe_ctx* c) { return 1 + (int)c->peers.size(); }
 
 tpe_ctx* dev(tpe_ctx* c, int d) { return d == 0 ? c : c->peers[d - 1]; }
 
+// One persistent host thread per peer device, created with the first
+// fanned-out call and bound to its device once (a call used to spawn and
+// join a thread per device): for_all hands every worker the same job and
+// waits for the count of pending devices to drop to zero.
+struct Workers {
+    std::mutex mu;
+    std::condition_variable cv_job, cv_done;
+    const std::function<int(tpe_ctx*, int)>* job = nullptr;
+    uint64_t gen = 0;
+    int pending = 0;
+    bool stop = false;
+    std::vector<int> rc;
+    std::vector<std::thread> th;
+
+    ~Workers() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv_job.notify_all();
+        for (auto& t : th) t.join();
+    }
+};
+
+void worker_main(Workers* w, tpe_ctx* x, int d) {
+    const bool bound = hipSetDevice(x->device) == hipSuccess;
+    uint64_t seen = 0;
+    for (;;) {
+        std::unique_lock<std::mutex> lk(w->mu);
+        w->cv_job.wait(lk, [&] { return w->stop || w->gen != seen; });
+        if (w->stop) return;
+        seen = w->gen;
+        const auto* job = w->job;
+        lk.unlock();
+        int r;
+        if (bound) {
+            r = (*job)(x, d);
+        } else {
+            x->err = "hipSetDevice failed";
+            r = TPE_ERR_HIP;
+        }
+        lk.lock();
+        w->rc[d] = r;
+        if (--w->pending == 0) w->cv_done.notify_all();
+    }
+}
+
+Workers* workers_of(tpe_ctx* c) {
+    if (!c->workers) {
+        auto w = std::make_shared<Workers>();
+        const int n = ndev(c);
+        w->rc.assign(n, TPE_OK);
+        for (int d = 1; d < n; ++d) w->th.emplace_back(worker_main, w.get(), dev(c, d), d);
+        c->workers = std::static_pointer_cast<void>(w);
+    }
+    return static_cast<Workers*>(c->workers.get());
+}
+
 // Run fn(device context, d) on every device concurrently (the primary on
-// the calling thread); the first failing device's code and message become
-// the primary's.
+// the calling thread, the peers on their workers); the first failing
+// device's code and message become the primary's.
 int for_all(tpe_ctx* c, const std::function<int(tpe_ctx*, int)>& fn) {
     const int n = ndev(c);
     if (n == 1) return fn(c, 0);
-    std::vector<int> rc(n, TPE_OK);
-    std::vector<std::thread> th;
-    th.reserve(n - 1);
-    for (int d = 1; d < n; ++d)
-        th.emplace_back([&, d]() {
-            tpe_ctx* x = dev(c, d);
-            if (hipSetDevice(x->device) != hipSuccess) {
-                x->err = "hipSetDevice failed";
-                rc[d] = TPE_ERR_HIP;
-                return;
-            }
-            rc[d] = fn(x, d);
-        });
-    rc[0] = fn(c, 0);
-    for (auto& t : th) t.join();
+    Workers* w = workers_of(c);
+    {
+        std::lock_guard<std::mutex> lk(w->mu);
+        w->job = &fn;
+        w->pending = n - 1;
+        for (int d = 0; d < n; ++d) w->rc[d] = TPE_OK;
+        ++w->gen;
+    }
+    w->cv_job.notify_all();
+    const int rc0 = fn(c, 0);
+    std::vector<int> rc;
+    {
+        std::unique_lock<std::mutex> lk(w->mu);
+        w->cv_done.wait(lk, [&] { return w->pending == 0; });
+        rc = w->rc;
+    }
+    rc[0] = rc0;
     for (int d = 0; d < n; ++d)
         if (rc[d] != TPE_OK) {
             if (d > 0) c->err = "device " + std::to_string(dev(c, d)->device) + ": " + dev(c, d)->err;
@@ -264,6 +324,7 @@ int32_t tpe_ctx_devices(const tpe_ctx* ctx, int32_t* devices, int32_t cap) {
 
 void tpe_ctx_destroy(tpe_ctx* ctx) {
     if (!ctx) return;
+    ctx->workers.reset();   // (joins the peer workers before their contexts go)
     for (tpe_ctx* p : ctx->peers) tpe1_ctx_destroy(p);
     ctx->peers.clear();
     tpe1_ctx_destroy(ctx);
@@ -283,9 +344,9 @@ int tpe_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
     return for_all(ctx, [&](tpe_ctx* x, int) { return tpe1_set_option(x, option, value); });
 }
 
-int tpe_prepare(tpe_ctx* ctx, int64_t n_candidates) {
+int tpe_prepare(tpe_ctx* ctx, int64_t n_candidates, int32_t n_rounds) {
     if (!ctx) return TPE_ERR_ARG;
-    return for_all(ctx, [&](tpe_ctx* x, int) { return tpe1_prepare(x, n_candidates); });
+    return for_all(ctx, [&](tpe_ctx* x, int) { return tpe1_prepare(x, n_candidates, n_rounds); });
 }
 
 int tpe_history_reset(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,

@@ -226,10 +226,10 @@ class Engine(object):
                                              _ptr(s), n.value, ctypes.byref(n)))
         return w, m, s
 
-    def prepare(self, n_candidates):
+    def prepare(self, n_candidates, n_rounds=1):
         """Build the expansion index of the resident posterior now
-        (tpe_prepare; the first round of n_candidates would build it)."""
-        self._check(self.lib.tpe_prepare(self.h, int(n_candidates)))
+        (tpe_prepare; the first round(s) of n_candidates would build it)."""
+        self._check(self.lib.tpe_prepare(self.h, int(n_candidates), int(n_rounds)))
 
     def last_build_ms(self):
         ms = ctypes.c_float()

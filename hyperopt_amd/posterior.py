@@ -256,7 +256,8 @@ def reference_orders(losses, n_below, obs_of, labels):
     empty ranges for the labels not in `labels`."""
     losses = np.asarray(losses, dtype=np.float64)
     T = len(losses)
-    valid = np.flatnonzero(losses == losses)
+    has = losses == losses
+    valid = np.flatnonzero(has)
     lv = losses[valid]
     below = np.zeros(T, dtype=np.uint8)
     if 0 < n_below < len(lv):
@@ -269,37 +270,63 @@ def reference_orders(losses, n_below, obs_of, labels):
             below[valid[np.argsort(lv)[:n_below]]] = 1      # tpe.py:637
     elif n_below > 0:
         below[valid] = 1
+    # the above set per trial position: a loss, not below (tpe.py:645-646)
+    above = has & (below == 0)
     n_labels = obs_of.n_labels
     off = np.zeros(n_labels + 1, dtype=np.int64)
     parts = []
     for l in range(n_labels):
         if l in labels:
             pos, val = obs_of(l)
-            pos = np.asarray(pos, dtype=np.int64)
-            ok = (pos >= 0) & (pos < T)
-            p = pos[ok]
-            keep = (losses[p] == losses[p]) & (below[p] == 0)   # tpe.py:645-646
-            mus = np.asarray(val, dtype=np.float64)[ok][keep]
-            o = np.argsort(mus).astype(np.int32)                # tpe.py:433
-            parts.append(o)
-            off[l + 1] = off[l] + len(o)
+            val = np.asarray(val, dtype=np.float64)
+            n = len(pos)
+            if n == T and n and pos[0] == 0 and pos[-1] == T - 1:
+                mus = val[above]                     # positions 0..T-1 (one per trial, in order)
+            else:
+                pos = np.asarray(pos, dtype=np.int64)
+                ok = (pos >= 0) & (pos < T)
+                keep = np.zeros(n, dtype=bool)
+                keep[ok] = above[pos[ok]]
+                mus = val[keep]
+            parts.append(mus)
+            off[l + 1] = off[l] + len(mus)
         else:
             off[l + 1] = off[l]
-    order = np.concatenate(parts) if parts else np.zeros(0, dtype=np.int32)
+    # np.argsort(mus) per label (tpe.py:433); numpy sorts without the GIL,
+    # so many long ones go to a thread pool
+    if parts and off[-1] >= _POOL_MIN:
+        parts = list(_sort_pool().map(np.argsort, parts))
+    else:
+        parts = [np.argsort(m) for m in parts]
+    order = np.concatenate(parts).astype(np.int32) if parts else np.zeros(0, dtype=np.int32)
     return below, off, order
 
 
-def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of, known=(), prepare_n=0):
+_POOL_MIN = 1 << 17   # observations to sort, from which the pool pays
+_pool = None
+
+
+def _sort_pool():
+    global _pool
+    if _pool is None:
+        import os
+        from concurrent.futures import ThreadPoolExecutor
+        _pool = ThreadPoolExecutor(max_workers=max(1, min(8, (os.cpu_count() or 2) // 2)))
+    return _pool
+
+
+def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of, known=(), prepare=None):
     """Device build whose mixtures follow the reference's tie order
     (tpe.py:433, 637): the device reports which mixtures depend on the order
     of tied observations (or a tie of losses at the split), and only for
     those the host computes numpy's own np.argsort and the build runs again
     with it.
 
-    * prepare_n == 0: `known` -- the labels that needed an order in the
+    * prepare None: `known` -- the labels that needed an order in the
       previous build of this history -- get their orders up front (one
       build when nothing new turns up);
-    * prepare_n > 0 (the round's candidates per label): the first build is
+    * prepare = (candidates per label, rounds) of the coming round, with
+      enough candidates to use the expansion index: the first build is
       made without orders, the expansion index of its dense labels is queued
       on the device (Engine.prepare), and the host computes the orders while
       it runs; the ordered rebuild leaves the dense labels bit-identical
@@ -308,9 +335,9 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
     Returns (n_below, the labels that needed an order)."""
     n_below = n_below_of(n_valid, gamma, lf)
     known = set(known)
-    if prepare_n:
+    if prepare:
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf)
-        eng.prepare(prepare_n)
+        eng.prepare(*prepare)
         have = set()
     elif known:
         below, off, order = reference_orders(losses, n_below, obs_of, known)
@@ -375,7 +402,7 @@ class DeviceHistoryUploader(object):
         self.key = None
         self.owner = None
 
-    def build(self, eng, labels, view, gamma, prior_weight, lf=DEFAULT_LF, prepare_n=0):
+    def build(self, eng, labels, view, gamma, prior_weight, lf=DEFAULT_LF, prepare=None):
         tids, losses, n_valid, cols, owner = view
         key = (tuple((n, k) for n, k, _ in labels), eng.history_generation)
         same_owner = self.owner is not None and self.owner() is owner
@@ -422,7 +449,7 @@ class DeviceHistoryUploader(object):
         self.last_tid = tids[-1] if len(tids) else None
         nb, self.tie_labels = build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf,
                                                     self._obs_of(len(labels)), self.tie_labels,
-                                                    prepare_n=prepare_n)
+                                                    prepare=prepare)
         return nb
 
     def _obs_of(self, n_labels):

@@ -133,11 +133,11 @@ class _PendingView(object):
         return len(self.trials)
 
 
-PREPARE_MIN = 8192   # candidates per label from which a round builds the expansion index
+PREPARE_MIN = 8192   # candidate slots of a round from which it uses the expansion index
 
 
 def _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior_weight,
-                        builder, n_candidates=0):
+                        builder, n_candidates=0, n_rounds=1):
     """Put the posterior of the current history on the engine, from the
     device-resident history's `view` or the general gather (tids, losses,
     obs); returns the number of trial documents it was built from."""
@@ -158,7 +158,8 @@ def _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior
                 if up is None:
                     up = eng._history_uploader = _post.DeviceHistoryUploader()
                 up.build(eng, [(s.label, s.kind, s.args) for s in specs.values()], view, gamma,
-                         prior_weight, prepare_n=n_candidates if n_candidates >= PREPARE_MIN else 0)
+                         prior_weight, prepare=((n_candidates, n_rounds)
+                                                if n_candidates * n_rounds >= PREPARE_MIN else None))
             else:
                 eng.build_posterior(*device_inputs(specs, tids, losses, obs), gamma=gamma,
                                     prior_weight=prior_weight)
@@ -251,9 +252,9 @@ def suggest(new_ids, domain, trials, seed,
     if n_docs == 0:
         logger.info('TPE using 0 trials')                     # the prior-only posterior
     eng = _engine.get_engine(list(devices) if devices else device, 'f64')
-    _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior_weight,
-                        posterior_builder, n_candidates=n_EI_candidates)
     ids = list(new_ids) if batch else [new_ids[0]]
+    _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior_weight,
+                        posterior_builder, n_candidates=n_EI_candidates, n_rounds=len(ids))
     if len(ids) == 1:
         res = eng.suggest(seed, n_EI_candidates, round=ids[0])[None]
     else:

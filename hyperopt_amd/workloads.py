@@ -6,7 +6,7 @@ import numpy as np
 
 from . import posterior as P
 
-PREPARE_MIN = 8192   # candidates per label from which a round builds the expansion index
+PREPARE_MIN = 8192   # candidate slots of a round from which it uses the expansion index
 
 # config-3 kind cycle: kind = i mod 5
 CYCLE = (('uniform', dict(low=-5.0, high=5.0)),
@@ -123,16 +123,17 @@ class FminLoop(object):
         losses = self.hist.losses[:n]
         return (self.hist.tids[:n], losses, int(np.count_nonzero(losses == losses)), obs, self)
 
-    def advance(self, eng, n, n_candidates=0):
+    def advance(self, eng, n, n_candidates=0, n_rounds=1):
         """History of the first n trials on the device, posterior rebuilt
-        (its expansion index queued meanwhile when the round will have
-        n_candidates >= 8192 per label, as tpe.suggest does); returns
+        (its expansion index queued meanwhile when the coming round(s) of
+        n_candidates per label will use it, as tpe.suggest does); returns
         n_below."""
         if n > len(self.hist.tids):
             raise ValueError('the synthetic history holds %d trials' % len(self.hist.tids))
         self.n = n
         return self.uploader.build(eng, self.hist.labels, self.view(n), self.gamma, self.prior_weight,
-                                   prepare_n=n_candidates if n_candidates >= PREPARE_MIN else 0)
+                                   prepare=((n_candidates, n_rounds)
+                                            if n_candidates * n_rounds >= PREPARE_MIN else None))
 
 
 def mixed_space(n_labels):

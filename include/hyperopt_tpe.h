@@ -444,15 +444,17 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_HOT_DIV 14
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
 
-/* Build now what the resident posterior's first round of n_candidates per
- * label would build lazily: the expansion screen's index (bin tables,
- * lists, sub-bin bounds; fp64 contexts with the screen and TPE_OPT_EXPAND
- * on, n_candidates >= 8192; otherwise nothing).  Lets a caller overlap the
+/* Build now what the resident posterior's first round(s) of n_candidates
+ * per label (n_rounds of them: tpe_suggest_batch) would build lazily: the
+ * expansion screen's index (bin tables, lists, sub-bin bounds; fp64
+ * contexts with the screen and TPE_OPT_EXPAND on, n_candidates x n_rounds
+ * >= 8192; otherwise nothing) and, for rounds of >= 8192 candidates, the
+ * hot-bin prefilter's threshold.  Lets a caller overlap the
  * index with host work (tpe.suggest computes numpy's tie orders meanwhile).
  * A later rebuild of the posterior that leaves every dense label
  * bit-identical keeps the index (compared on the device against a snapshot).
  * No reference counterpart: the reference has no index. */
-int tpe_prepare(tpe_ctx *ctx, int64_t n_candidates);
+int tpe_prepare(tpe_ctx *ctx, int64_t n_candidates, int32_t n_rounds);
 
 #ifdef __cplusplus
 }
