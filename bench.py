@@ -3,16 +3,20 @@
 Workload (BASELINE.json configs[2], the metric's "10k-trial history"):
 32 hyperparameters, kind = i mod 5 in {uniform(-5,5), loguniform(-5,2),
 quniform(0,100,1), normal(0,3), choice(5)}, N = 10000 synthetic trials,
-2^24 EI candidates per label in total, strong-scaled: each of the N ranks
-scores the contiguous global slice [rank C/N, (rank+1) C/N) (the Philox
-counter is the global candidate index, so the candidate set and the winner do
-not depend on N).
+2^24 EI candidates per label.
 
-One step = one fused suggestion round on the resident posterior: Philox
-sampling of every label's candidates from l(x), lpdf under l and g for every
-(candidate, component) pair, broadcast_best maxloc per label, and (N > 1) the
-cross-GPU winner exchange over RCCL.  Inputs (the posterior descriptors) are
-resident in HBM before the timed region.
+One step (default --mode fresh) = one suggestion of fmin's loop: append a
+trial to the device-resident history, rebuild the posterior on the device
+(numpy's tie order where it matters), build its expansion index, and run the
+fused round -- Philox sampling of every label's candidates from l(x), lpdf
+under l and g, broadcast_best maxloc per label -- then (N > 1) the winner
+all-gather over RCCL.  Inputs are resident in HBM before the timed region.
+
+N > 1 (torchrun, one rank per GPU): label shards by default -- rank r holds
+the labels of parallel.label_shards(labels, N), their history columns,
+posterior, index and whole rounds, each label keeping its Philox stream, so
+the winners do not depend on N; --shard candidates splits every label's
+candidates instead (rank r scores [r C/N, (r+1) C/N)).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--precision f64|f32]
 """
@@ -94,6 +98,8 @@ def parse():
     ap.add_argument('--cpu-sample-c', type=int, default=49152,
                     help='candidates per label in the all-cores C baseline sample')
     ap.add_argument('--no-latency', action='store_true')
+    ap.add_argument('--no-projection', action='store_true',
+                    help='skip the one-GPU projection of the 8-GPU step (profiling runs)')
     ap.add_argument('--no-screen', action='store_true',
                     help='f64: plain fp64 rounds (no fp32 screen); the winners are the same')
     ap.add_argument('--no-window', action='store_true',
@@ -114,6 +120,10 @@ def parse():
                     help='one process, one multi-device context over these HIP ordinals '
                          '(e.g. 0,1,2,3; tpe_ctx_create_multi): the 1..8-GPU curve without '
                          'torchrun; a repeated ordinal shares that GPU (tests)')
+    ap.add_argument('--shard', default='auto', choices=['auto', 'labels', 'candidates'],
+                    help='N > 1: label shards (each rank holds a subset of the labels: their '
+                         'history, posterior, index and whole rounds; auto when there are at least '
+                         '2 labels per rank) or candidate shards (every label, C/N candidates each)')
     ap.add_argument('--dist-backend', default='nccl',
                     help='nccl (RCCL over xGMI); gloo only to rehearse N ranks on one GPU')
     return ap.parse_args()
@@ -235,10 +245,10 @@ def workload_name(args, C):
                '2^%d EI candidates per label (C/N per GPU)' % args.cand_log2
     if args.config == 5:
         return 'config5: 128-dim mixed space, N=%d history, %d new_ids per step x 24 EI ' \
-               'candidates (new_ids split over the GPUs, winners all-gathered)' % (
+               'candidates (labels or new_ids split over the GPUs, winners all-gathered)' % (
                    args.trials, args.new_ids)
     return 'config3: %d-dim mixed space, N=%d history, 2^%d EI candidates per label ' \
-           '(C/N per GPU)' % (args.labels, args.trials, args.cand_log2)
+           '(labels split over the GPUs)' % (args.labels, args.trials, args.cand_log2)
 
 
 def main():
@@ -298,7 +308,13 @@ def main():
                   'note': 'tpe_build_posterior (split, sort, Parzen, fold on the GPU; call '
                           'includes the H2D of the history) vs posterior.py + pack'}
     C_total = 24 if args.config == 5 else 1 << args.cand_log2
-    if args.config == 5:
+    from hyperopt_amd.parallel import gather_labels, label_shards
+    by_label = (args.shard == 'labels' or
+                (args.shard == 'auto' and len(hist_full.labels) >= 2 * max(world, 8 if world == 1 else 1)))
+    shards = label_shards(hist_full.labels, world) if by_label else None
+    if by_label:   # whole rounds of this rank's labels
+        ids_local, C = args.new_ids, C_total
+    elif args.config == 5:
         if args.new_ids % world:
             raise SystemExit('--new-ids must divide over %d ranks' % world)
         ids_local, C = args.new_ids // world, C_total
@@ -315,28 +331,34 @@ def main():
     # does (FminLoop), so the round pays the expansion index of a new
     # posterior -- what every suggestion of fmin's loop pays
     loop = None
-    if args.mode == 'fresh':
-        loop = FminLoop(hist_full)
+    fresh_mode = args.mode == 'fresh'
+    if fresh_mode or (by_label and world > 1):
+        loop = FminLoop(hist_full, label_ids=shards[rank] if by_label and world > 1 else None)
         loop.advance(eng, args.trials)        # untimed: the initial history, uploaded whole
     results = {}
 
-    def step(i, fresh, n=None):
-        """One step; n: the candidates per label of this rank's shard
-        (default C) -- the projection runs one eighth of a round."""
+    def step(i, fresh, n=None, e=None, lp=None, gather=True):
+        """One step; n: the candidates per label of this rank's candidate
+        shard (default C) -- the candidate-shard projection runs one eighth
+        of a round; e, lp: another engine and loop (the label-shard
+        projection)."""
+        e = eng if e is None else e
+        lp = loop if lp is None else lp
         nc = C if n is None else n
         if fresh:
-            loop.advance(eng, args.trials + (i + 1) * args.append,
-                         n_candidates=nc if args.precision == 'f64' else 0,
-                         n_rounds=ids_local if args.config == 5 else 1)
-        if args.config == 5:   # independent new_ids split over the GPUs
-            ids = [i * args.new_ids + rank * ids_local + k for k in range(ids_local)]
-            res = eng.suggest_batch(seed=1234, rounds=ids, n_candidates=C)
-            if dist is not None:   # every rank ends with every new_id's winners
-                res = gather_rounds(res)
+            lp.advance(e, args.trials + (i + 1) * args.append,
+                       n_candidates=nc if args.precision == 'f64' else 0,
+                       n_rounds=ids_local if args.config == 5 else 1)
+        if args.config == 5:   # independent new_ids split over the GPUs (or each rank's labels)
+            first_id = i * args.new_ids + (0 if by_label else rank * ids_local)
+            res = e.suggest_batch(seed=1234, rounds=list(range(first_id, first_id + ids_local)),
+                                  n_candidates=C)
+            if dist is not None and gather:   # every rank ends with every new_id's winners
+                res = gather_labels(res, shards, rank) if by_label else gather_rounds(res)
             return res
-        res = eng.suggest(seed=1234 + i, n_candidates=nc, round=i, cand_offset=rank * nc)
-        if dist is not None:   # exchange per-GPU winners (L x 48 B) over RCCL
-            res = exchange_winners(res)
+        res = e.suggest(seed=1234 + i, n_candidates=nc, round=i, cand_offset=0 if by_label else rank * nc)
+        if dist is not None and gather:   # exchange per-GPU winners (L x 48 B) over RCCL
+            res = gather_labels(res, shards, rank) if by_label else exchange_winners(res)
         return res
 
     def timed(n_steps, first, fresh, keep=False, n=None):
@@ -382,39 +404,68 @@ def main():
     eng.set_option('window', int(not args.no_window))
     eng.set_option('win_t', args.win_t)
     eng.set_option('win_groups', args.win_groups)
-    if world > 1:   # this rank holds one shard: size-dependent choices follow the whole round
+    if world > 1 and not by_label:   # one candidate shard: size choices follow the whole round
         eng.set_option('whole_rounds' if args.config == 5 else 'whole_n',
                        args.new_ids if args.config == 5 else C_total)
     for i in range(args.warmup):
-        step(i, loop is not None)
+        step(i, fresh_mode)
     # the expansion screen's index (bin tables, lists, sub-bin bounds) is
     # built once per posterior, in its first large round
     prep_ms = eng.last_prepare_ms() if args.warmup > 0 else None
-    dt, mode_ms, mode_ev, scr = timed(args.steps, args.warmup, loop is not None)
+    dt, mode_ms, mode_ev, scr = timed(args.steps, args.warmup, fresh_mode)
     # the same rounds on the posterior of the last step, reused (no append):
     # the round alone, and the reference for the unscreened comparison
     warm_first = args.warmup + args.steps
-    wdt, _, _, _ = timed(args.steps, warm_first, False, keep=True) if loop is not None else (None,) * 4
-    # one GPU's share of an 8-GPU strong-scaled round (C/8 candidates per
-    # label at the whole round's map choices): the projection of the 8-GPU
-    # step from this one GPU, fresh (append + rebuild + index + shard round,
-    # the rebuild and index replicated on every rank) and warm
+    wdt, _, _, _ = timed(args.steps, warm_first, False, keep=True) if fresh_mode else (None,) * 4
+    # the 8-GPU step projected from this one GPU: each rank's share run
+    # alone (label shards: an engine per shard holding its labels' history,
+    # posterior and index, whole rounds, the slowest shard setting the step;
+    # candidate shards: C/8 candidates per label at the whole round's map
+    # choices, the per-posterior work repeated), fresh and warm
     proj = None
-    if loop is not None and world == 1 and devs is None and args.config != 5 and C % 8 == 0:
-        eng.set_option('whole_n', C)
-        pdt, _, _, _ = timed(args.steps, warm_first + args.steps, True, n=C // 8)
-        pwdt, _, _, _ = timed(args.steps, warm_first + 2 * args.steps, False, n=C // 8)
-        eng.set_option('whole_n', 0)
-        proj = {'shard_candidates_per_label': C // 8,
-                'fresh_step_ms_full': dt / args.steps * 1e3, 'fresh_step_ms_shard': pdt / args.steps * 1e3,
-                'warm_round_ms_full': wdt / args.steps * 1e3, 'warm_round_ms_shard': pwdt / args.steps * 1e3,
-                'projected_8gpu_efficiency_fresh': dt / (8.0 * pdt),
-                'projected_8gpu_efficiency_warm': wdt / (8.0 * pwdt),
-                'note': 'one GPU running one rank\'s share (C/8 per label, map choices of the whole '
-                        'round): efficiency = T(C) / (8 T(C/8)); the shard step keeps the per-posterior '
-                        'work (append, device rebuild, index) that every rank repeats, and the RCCL '
-                        'winner exchange (32 x 48 B) is not in it -- a projection, not a measured '
-                        'scaling curve'}
+    if fresh_mode and world == 1 and devs is None and not args.no_projection and (by_label or (args.config != 5 and C % 8 == 0)):
+        p0 = warm_first + args.steps
+        if by_label:
+            per = []
+            for sh in label_shards(hist_full.labels, 8):
+                e8 = Engine(local, args.precision)
+                for k, v in (('screen', int(screen)), ('window', int(not args.no_window)),
+                             ('win_t', args.win_t), ('win_groups', args.win_groups)):
+                    e8.set_option(k, v)
+                l8 = FminLoop(hist_full, label_ids=sh)
+                l8.advance(e8, args.trials + p0 * args.append)
+                step(p0, True, e=e8, lp=l8, gather=False)      # warm-up
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for i in range(args.steps):
+                    step(p0 + 1 + i, True, e=e8, lp=l8, gather=False)
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                for i in range(args.steps):
+                    step(p0 + 1 + i, False, e=e8, lp=l8, gather=False)
+                torch.cuda.synchronize()
+                t2 = time.perf_counter()
+                per.append((len(sh), (t1 - t0) / args.steps * 1e3, (t2 - t1) / args.steps * 1e3))
+                e8.close()
+            pf, pw = max(x[1] for x in per), max(x[2] for x in per)
+            proj = {'partition': 'label shards (parallel.label_shards, 8 ranks)',
+                    'labels_per_shard': [x[0] for x in per],
+                    'fresh_step_ms_per_shard': [round(x[1], 3) for x in per],
+                    'warm_round_ms_per_shard': [round(x[2], 3) for x in per]}
+        else:
+            eng.set_option('whole_n', C)
+            pf = timed(args.steps, p0, True, n=C // 8)[0] / args.steps * 1e3
+            pw = timed(args.steps, p0 + args.steps, False, n=C // 8)[0] / args.steps * 1e3
+            eng.set_option('whole_n', 0)
+            proj = {'partition': 'candidate shards (C/8 per label)', 'shard_candidates_per_label': C // 8}
+        proj.update({
+            'fresh_step_ms_full': dt / args.steps * 1e3, 'fresh_step_ms_shard': pf,
+            'warm_round_ms_full': wdt / args.steps * 1e3, 'warm_round_ms_shard': pw,
+            'projected_8gpu_efficiency_fresh': dt / args.steps * 1e3 / (8.0 * pf),
+            'projected_8gpu_efficiency_warm': wdt / args.steps * 1e3 / (8.0 * pw),
+            'note': 'one GPU running each rank\'s share of the 8-GPU step in turn: efficiency = '
+                    'T(whole) / (8 max_r T(shard r)); the RCCL all-gather of the winners (48 B per '
+                    'label) is not in it -- a projection, not a measured scaling curve'})
     # `value` counts EXECUTED (candidate, component) lpdf terms (BASELINE.md
     # section 3): quantized labels their grid-table evals, screened dense
     # labels the fp32 terms the screen summed plus the fp64 terms of the
@@ -423,7 +474,13 @@ def main():
     executed = sum(mode_ev.values())
     if scr[0] > 0:
         executed += scr[3] + scr[4] - sum(mode_ev.get(k, 0) for k in DENSE)
-    value = executed * world / dt
+    executed_all = executed * world
+    if dist is not None:   # the ranks' shards differ (label shards): sum what they executed
+        te = torch.tensor([float(executed)], dtype=torch.float64,
+                          device='cuda' if args.dist_backend == 'nccl' else 'cpu')
+        dist.all_reduce(te)
+        executed_all = int(te.item())
+    value = executed_all / dt
     rounds_per_step = args.new_ids if args.config == 5 else 1
     ref_equiv_per_step = sum((2 if p.family == 'categorical' else len(p.below[0]) + len(p.above[0]))
                              * C_total * rounds_per_step for p in posts)
@@ -527,8 +584,10 @@ def main():
         'config': {'workload': workload_name(args, C),
                    'labels': L, 'history': args.trials,
                    'candidates_per_label': C_total, 'candidates_per_label_per_gpu': C,
-                   'parallelism': ('new_id-sharded x%d' if args.config == 5
-                                   else 'candidate-sharded x%d') % (len(devs) if devs else world)
+                   'parallelism': ('label-sharded x%d (labels per rank: %s)'
+                                   % (world, [len(sh) for sh in shards]) if by_label and world > 1 else
+                                   ('new_id-sharded x%d' if args.config == 5
+                                    else 'candidate-sharded x%d') % (len(devs) if devs else world))
                                   + (' (one process, multi-device context %s)' % devs
                                      if devs else '')},
         'step': ({'kind': 'fresh posterior (fmin loop)',
@@ -543,7 +602,7 @@ def main():
                   'warm_round_ms': round(wdt / args.steps * 1e3, 3),
                   'warm_note': 'the same rounds on one resident posterior (no append, no rebuild, '
                                'no index): the round alone'}
-                 if loop is not None else
+                 if fresh_mode else
                  {'kind': 'warm (one resident posterior)',
                   'fresh_posterior_round_ms': (round(post_build['device_call_ms'] + prep_ms
                                                      + dt / args.steps * 1e3, 3) if prep_ms else None)}),
@@ -556,7 +615,7 @@ def main():
         'roofline': roof,
         'evals_basis': {
             'value': 'executed terms per second, whole job',
-            'executed_per_step': executed * world // max(args.steps, 1),
+            'executed_per_step': executed_all // max(args.steps, 1),
             'reference_equivalent_per_step': ref_equiv_per_step,
             'reference_equivalent_per_s': ref_equiv_per_step * args.steps / dt,
             'note': 'reference_equivalent: every (candidate, component) pair of the step '
@@ -592,8 +651,8 @@ def main():
             # the plain fp64 round on the SAME (seed, round) as screened steps
             # on the same posterior: winners, values and lpdfs bit for bit
             nu = args.unscreened_steps
-            first = warm_first if loop is not None else args.warmup + args.steps
-            if loop is None:
+            first = warm_first if fresh_mode else args.warmup + args.steps
+            if not fresh_mode:
                 timed(nu, first, False, keep=True)
             eng.set_option('screen', 0)
             ures = {}
@@ -616,7 +675,7 @@ def main():
         # fp32 winners vs the exact fp64 round's on the same candidate sets
         ref = Engine(devs if devs else local, 'f64')
         if loop is not None:   # the posterior the fp32 engine holds now
-            FminLoop(hist_full).advance(ref, loop.n)
+            FminLoop(hist_full, label_ids=loop.label_ids if loop.streams else None).advance(ref, loop.n)
         else:
             ref.build_posterior(*inputs, gamma=0.25, prior_weight=1.0)
         same = total = 0

@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, 'libhyperopt_tpe.so')
 HEADER = os.path.join(os.path.dirname(HERE), 'include', 'hyperopt_tpe.h')
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 TPE_OK = 0
 TPE_ERR_VALUE = -1
@@ -34,6 +34,7 @@ TPE_CATEGORICAL = 2
 TPE_HAS_LOW = 1
 TPE_HAS_HIGH = 2
 TPE_HAS_Q = 4
+TPE_HAS_STREAM = 8
 
 TPE_OPT_SCREEN = 1
 TPE_OPT_SPLITK = 2
@@ -66,7 +67,8 @@ class LabelSpec(ctypes.Structure):
     _fields_ = [('kind', ctypes.c_int32), ('flags', ctypes.c_int32),
                 ('low', ctypes.c_double), ('high', ctypes.c_double), ('q', ctypes.c_double),
                 ('prior_mu', ctypes.c_double), ('prior_sigma', ctypes.c_double),
-                ('upper', ctypes.c_int32), ('randint', ctypes.c_int32), ('p_off', ctypes.c_int64)]
+                ('upper', ctypes.c_int32), ('randint', ctypes.c_int32), ('p_off', ctypes.c_int64),
+                ('stream', ctypes.c_int32), ('reserved', ctypes.c_int32)]
 
 
 class LabelResult(ctypes.Structure):
@@ -77,7 +79,7 @@ class LabelResult(ctypes.Structure):
 
 assert ctypes.sizeof(LabelDesc) == 56
 assert ctypes.sizeof(LabelResult) == 48
-assert ctypes.sizeof(LabelSpec) == 64
+assert ctypes.sizeof(LabelSpec) == 72
 
 _P = ctypes.c_void_p
 _I32, _I64, _U32, _U64, _D = (ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,

@@ -1108,6 +1108,8 @@ int check_specs(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels, int
         } else {
             return ctx->fail(TPE_ERR_ARG, "label " + std::to_string(l) + ": unknown kind");
         }
+        if ((s.flags & TPE_HAS_STREAM) && s.stream < 0)
+            return ctx->fail(TPE_ERR_ARG, "label " + std::to_string(l) + ": negative stream");
     }
     return TPE_OK;
 }
@@ -1333,13 +1335,13 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
             cap_b = lf + 1;
             cap_a = (int64_t)B.cnt_h[l] + 1;
         }
-        o.flags = s.kind == TPE_CATEGORICAL ? 0 : s.flags;
+        o.flags = s.kind == TPE_CATEGORICAL ? 0 : (s.flags & (TPE_HAS_LOW | TPE_HAS_HIGH | TPE_HAS_Q));
         o.low = s.low;
         o.high = s.high;
         o.q = s.q;
         o.exp_low = std::exp(s.low);
         o.exp_high = std::exp(s.high);
-        o.stream = l;
+        o.stream = (s.flags & TPE_HAS_STREAM) ? s.stream : l;
         o.comp_b = mix[2 * l] = total;
         total += cap_b;
         o.comp_a = mix[2 * l + 1] = total;

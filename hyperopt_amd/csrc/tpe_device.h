@@ -36,7 +36,7 @@ struct DLabel {
     int32_t nb, na;
     int64_t samp_off;           // offset of the below mixture's sampling records
     int32_t ns;
-    int32_t stream;             // Philox stream id (label position)
+    int32_t stream;             // Philox stream id (label position, or the spec's TPE_HAS_STREAM id)
     float amax_b, amax_a;       // dense: largest fp32 record scale a per mixture (screen_err)
 };
 

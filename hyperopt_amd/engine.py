@@ -49,7 +49,8 @@ assert DESC_DTYPE.itemsize == ctypes.sizeof(L.LabelDesc)
 
 SPEC_DTYPE = np.dtype([('kind', '<i4'), ('flags', '<i4'), ('low', '<f8'), ('high', '<f8'),
                        ('q', '<f8'), ('prior_mu', '<f8'), ('prior_sigma', '<f8'),
-                       ('upper', '<i4'), ('randint', '<i4'), ('p_off', '<i8')])
+                       ('upper', '<i4'), ('randint', '<i4'), ('p_off', '<i8'),
+                       ('stream', '<i4'), ('reserved', '<i4')])
 assert SPEC_DTYPE.itemsize == ctypes.sizeof(L.LabelSpec)
 
 

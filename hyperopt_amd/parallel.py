@@ -1,7 +1,18 @@
-"""Multi-GPU suggestion rounds: one process per GPU, candidates sharded by
-global index, one collective per round.
+"""Multi-GPU suggestion rounds: one process per GPU, one collective per
+round.  Two partitions of a round's (label, candidate) set:
 
-Each rank scores candidates [rank*C, (rank+1)*C) of every label (the Philox
+* label shards (label_shards / gather_labels): rank r holds the labels of
+  its shard -- their history columns, posterior, expansion index and every
+  candidate of their rounds -- so the per-posterior work (rebuild, index)
+  divides over the ranks like the candidates do.  Labels are independent in
+  tpe.suggest (one build_posterior_wrapper + broadcast_best per label,
+  tpe.py:678-692, 769-778) and each keeps its Philox stream, so the winners
+  are the single-GPU winners; the all-gather carries 48 B per label.
+* candidate shards (exchange_winners): rank r scores candidates
+  [rank*C, (rank+1)*C) of every label, for spaces with fewer labels than
+  ranks.
+
+Candidate shards: each rank scores candidates [rank*C, (rank+1)*C) of every label (the Philox
 counter is the global index, so the union over ranks is exactly the
 single-GPU candidate set).  The per-label winners (48 B x L) are
 all-gathered -- over RCCL (`nccl` backend) on GPUs, gloo in the CPU tests --
@@ -49,6 +60,59 @@ def gather_rounds(res, group=None):
         return res
     parts = _all_gather_results(res, group)
     return parts.reshape((world * np.shape(res)[0],) + np.shape(res)[1:])
+
+
+# relative cost of a label in a fresh-posterior step (bench config 3, r3
+# profile): a dense label pays the expansion index and the hot-bin round, a
+# quantized one the host's tie order and its table round, a categorical one
+# only its early-exit round
+LABEL_COST = {'dense': 1.0, 'quantized': 0.5, 'categorical': 0.25}
+
+
+def label_cost(kind, args=None):
+    if kind in ('randint', 'categorical'):
+        return LABEL_COST['categorical']
+    if kind.startswith('q'):
+        return LABEL_COST['quantized']
+    return LABEL_COST['dense']
+
+
+def label_shards(labels, world):
+    """Partition of label indices over `world` ranks, longest processing
+    time first (largest cost to the least-loaded rank; ties to the lower
+    rank and label, so every rank computes the same partition); each shard
+    in increasing label order."""
+    if world > len(labels):
+        raise ValueError('%d labels cannot fill %d label shards' % (len(labels), world))
+    load = [0.0] * world
+    shards = [[] for _ in range(world)]
+    order = sorted(range(len(labels)), key=lambda i: (-label_cost(labels[i][1]), i))
+    for i in order:
+        r = min(range(world), key=lambda k: (load[k], k))
+        shards[r].append(i)
+        load[r] += label_cost(labels[i][1])
+    return [sorted(sh) for sh in shards]
+
+
+def gather_labels(res, shards, rank, group=None):
+    """All-gather the winners of label shards: res[..., j] is this rank's
+    result for label shards[rank][j]; every rank returns res[..., L] over all
+    labels in space order, `label` set to the space index."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    n_labels = sum(len(sh) for sh in shards)
+    m = max(len(sh) for sh in shards)
+    res = np.asarray(res, dtype=RESULT_DTYPE)
+    lead = res.shape[:-1]
+    pad = np.zeros(lead + (m,), dtype=RESULT_DTYPE)
+    pad['index'] = -1
+    pad[..., :res.shape[-1]] = res
+    parts = _all_gather_results(pad, group) if world > 1 else pad[None]
+    out = np.zeros(lead + (n_labels,), dtype=RESULT_DTYPE)
+    for r, sh in enumerate(shards):
+        out[..., sh] = parts[r][..., :len(sh)]
+    out['label'] = np.arange(n_labels, dtype=np.int32)
+    return out
 
 
 class ShardedSuggest(object):

@@ -219,9 +219,11 @@ def label_spec(kind, args):
     return spec, tr, None
 
 
-def spec_table(labels):
+def spec_table(labels, streams=None):
     """(SPEC_DTYPE array, concatenated categorical p, per-label observation
-    transform or None) for labels = [(name, kind, args)]."""
+    transform or None) for labels = [(name, kind, args)]; streams: each
+    label's Philox stream (default its position) -- a subset of a space's
+    labels keeps the streams, hence the candidates, it has in the whole space."""
     from .engine import SPEC_DTYPE
     specs = np.zeros(len(labels), dtype=SPEC_DTYPE)
     cat_p, p_len, trs = [], 0, []
@@ -233,6 +235,9 @@ def spec_table(labels):
             specs[i]['p_off'] = p_len
             cat_p.append(p)
             p_len += len(p)
+        if streams is not None:
+            specs[i]['flags'] |= L.TPE_HAS_STREAM
+            specs[i]['stream'] = int(streams[i])
         trs.append(tr)
     return specs, (np.concatenate(cat_p) if cat_p else np.zeros(0)), trs
 
@@ -315,7 +320,8 @@ def _sort_pool():
     return _pool
 
 
-def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of, known=(), prepare=None):
+def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of, known=(), prepare=None,
+                          overlap=True):
     """Device build whose mixtures follow the reference's tie order
     (tpe.py:433, 637): the device reports which mixtures depend on the order
     of tied observations (or a tie of losses at the split), and only for
@@ -330,18 +336,23 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
       made without orders, the expansion index of its dense labels is queued
       on the device (Engine.prepare), and the host computes the orders while
       it runs; the ordered rebuild leaves the dense labels bit-identical
-      (continuous values carry no ties), so the device keeps the index.
+      (continuous values carry no ties), so the device keeps the index;
+      with overlap=False (few labels use the index: it is shorter than the
+      second build it saves) the `known` orders go up front as above and the
+      index is queued after the one build.
 
     Returns (n_below, the labels that needed an order)."""
     n_below = n_below_of(n_valid, gamma, lf)
     known = set(known)
-    if prepare:
+    if prepare and (overlap or not known):
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf)
         eng.prepare(*prepare)
         have = set()
     elif known:
         below, off, order = reference_orders(losses, n_below, obs_of, known)
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf, below, off, order)
+        if prepare:
+            eng.prepare(*prepare)
         have = known
     else:
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf)
@@ -402,9 +413,11 @@ class DeviceHistoryUploader(object):
         self.key = None
         self.owner = None
 
-    def build(self, eng, labels, view, gamma, prior_weight, lf=DEFAULT_LF, prepare=None):
+    def build(self, eng, labels, view, gamma, prior_weight, lf=DEFAULT_LF, prepare=None, streams=None,
+              overlap=True):
         tids, losses, n_valid, cols, owner = view
-        key = (tuple((n, k) for n, k, _ in labels), eng.history_generation)
+        key = (tuple((n, k) for n, k, _ in labels) + (tuple(streams) if streams is not None else (),),
+               eng.history_generation)
         same_owner = self.owner is not None and self.owner() is owner
         fresh = (not same_owner or self.key != key or len(tids) < self.n_trials or
                  (self.n_trials and tids[self.n_trials - 1] != self.last_tid) or
@@ -412,7 +425,7 @@ class DeviceHistoryUploader(object):
         # invalid until the device holds exactly what prev_counts says
         self.key, self.owner = None, None
         if fresh:
-            specs, cat_p, self.trs = spec_table(labels)
+            specs, cat_p, self.trs = spec_table(labels, streams)
             eng.history_reset(specs, cat_p)
             self.prev_counts = [0] * len(labels)
             self.pos_parts = [[] for _ in labels]    # what the device holds, per label
@@ -449,7 +462,7 @@ class DeviceHistoryUploader(object):
         self.last_tid = tids[-1] if len(tids) else None
         nb, self.tie_labels = build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf,
                                                     self._obs_of(len(labels)), self.tie_labels,
-                                                    prepare=prepare)
+                                                    prepare=prepare, overlap=overlap)
         return nb
 
     def _obs_of(self, n_labels):

@@ -7,6 +7,8 @@ import numpy as np
 from . import posterior as P
 
 PREPARE_MIN = 8192   # candidate slots of a round from which it uses the expansion index
+OVERLAP_MIN_DENSE = 8   # index labels from which the index runs beside the host's tie orders
+DENSE_KINDS = ('uniform', 'loguniform', 'normal', 'lognormal')
 
 # config-3 kind cycle: kind = i mod 5
 CYCLE = (('uniform', dict(low=-5.0, high=5.0)),
@@ -105,12 +107,22 @@ class FminLoop(object):
     fits the Parzen mixtures and folds the records, with numpy's np.argsort
     tie order for the labels whose mixtures depend on it
     (posterior.build_reference_order).  The view tuple is the one
-    history.device_view hands tpe.suggest."""
+    history.device_view hands tpe.suggest.
 
-    def __init__(self, hist, gamma=0.25, prior_weight=1.0):
+    label_ids: the subset of the space's labels this loop holds (a
+    label-sharded rank, parallel.label_shards); each keeps its Philox stream
+    (its index in the whole space), so its candidates and winner are the
+    whole space's."""
+
+    def __init__(self, hist, gamma=0.25, prior_weight=1.0, label_ids=None):
         self.hist = hist
         self.gamma, self.prior_weight = gamma, prior_weight
-        self.names = [n for n, _, _ in hist.labels]
+        self.label_ids = (list(range(len(hist.labels))) if label_ids is None
+                          else [int(i) for i in label_ids])
+        self.labels = [hist.labels[i] for i in self.label_ids]
+        self.streams = None if label_ids is None else self.label_ids
+        self.names = [n for n, _, _ in self.labels]
+        self.n_dense = sum(1 for _, k, _ in self.labels if k in DENSE_KINDS)
         self.uploader = P.DeviceHistoryUploader()
         self.n = 0
 
@@ -131,9 +143,10 @@ class FminLoop(object):
         if n > len(self.hist.tids):
             raise ValueError('the synthetic history holds %d trials' % len(self.hist.tids))
         self.n = n
-        return self.uploader.build(eng, self.hist.labels, self.view(n), self.gamma, self.prior_weight,
+        return self.uploader.build(eng, self.labels, self.view(n), self.gamma, self.prior_weight,
                                    prepare=((n_candidates, n_rounds)
-                                            if n_candidates * n_rounds >= PREPARE_MIN else None))
+                                            if n_candidates * n_rounds >= PREPARE_MIN else None),
+                                   streams=self.streams, overlap=self.n_dense >= OVERLAP_MIN_DENSE)
 
 
 def mixed_space(n_labels):

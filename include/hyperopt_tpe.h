@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define TPE_ABI_VERSION 3
+#define TPE_ABI_VERSION 4
 
 /* error codes; the Python layer maps them to the reference's exception types */
 #define TPE_OK 0
@@ -48,6 +48,10 @@ extern "C" {
 #define TPE_HAS_LOW 1
 #define TPE_HAS_HIGH 2
 #define TPE_HAS_Q 4
+/* tpe_label_spec only: `stream` names the label's Philox stream (default: its
+ * position in the spec array) -- a process holding a subset of the labels
+ * (label-sharded ranks) draws the candidates the whole space would */
+#define TPE_HAS_STREAM 8
 
 typedef struct tpe_ctx tpe_ctx;
 
@@ -98,7 +102,9 @@ typedef struct {
                             tpe.py:581-589), 0 pchoice (counts + upper *
                             prior_weight * p, tpe.py:598-617)                  */
     int64_t p_off;       /* pchoice: offset of its p vector in cat_p           */
-} tpe_label_spec;        /* 64 bytes */
+    int32_t stream;      /* with TPE_HAS_STREAM: the label's Philox stream     */
+    int32_t reserved;    /* 0                                                  */
+} tpe_label_spec;        /* 72 bytes */
 
 /* Winner of one label's candidate set (broadcast_best, tpe.py:769-778). */
 typedef struct {

@@ -18,12 +18,14 @@ def test_library_built_and_exports_header():
     for name in declared:
         assert hasattr(lib, name), name
         assert name in L.SIGNATURES, 'binding missing for ' + name
-    assert lib.tpe_abi_version() == L.ABI_VERSION == 3
+    assert lib.tpe_abi_version() == L.ABI_VERSION == 4
 
 
 def test_struct_layouts():
     assert ctypes.sizeof(L.LabelDesc) == 56
     assert ctypes.sizeof(L.LabelResult) == 48
+    assert ctypes.sizeof(L.LabelSpec) == 72
+    assert L.LabelSpec.stream.offset == 64
     assert L.LabelDesc.n_below.offset == 48
     assert L.LabelResult.index.offset == 32
 

@@ -130,3 +130,117 @@ def test_engine_shards_gloo_world2():
         for f in ('index', 'value', 'lpdf_below', 'lpdf_above'):
             assert np.array_equal(merged[f], want[f]), f
             assert np.array_equal(rows[f], want_rows[f]), f
+
+
+def test_label_shards_partition():
+    from hyperopt_amd.parallel import label_cost, label_shards
+    from hyperopt_amd.workloads import mixed_space
+    labels = mixed_space(32)
+    for world in (1, 2, 3, 4, 8, 16):
+        sh = label_shards(labels, world)
+        assert sh == label_shards(labels, world)          # every rank computes the same
+        assert sorted(i for s in sh for i in s) == list(range(32))
+        assert all(s == sorted(s) and s for s in sh)
+        load = [sum(label_cost(labels[i][1]) for i in s) for s in sh]
+        # LPT: no shard exceeds the mean by more than the largest label cost
+        assert max(load) <= sum(load) / world + 1.0
+    with pytest.raises(ValueError):
+        label_shards(labels[:3], 4)
+
+
+def _label_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from hyperopt_amd.parallel import gather_labels
+        shards = [[0, 2, 5], [1, 3, 4, 6]]
+        res = _rank_results(rank, n_labels=len(shards[rank]))
+        res['index'] = np.array(shards[rank]) * 10 + rank
+        rows = np.stack([res, res])                           # two rounds
+        q.put((rank, gather_labels(res, shards, rank).tobytes(),
+               gather_labels(rows, shards, rank).tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_labels_gloo_world2():
+    import multiprocessing as mp
+    from hyperopt_amd.engine import RESULT_DTYPE
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_label_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in procs:
+        r, a, b = q.get(timeout=120)
+        got[r] = (a, b)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    owner = [0, 1, 0, 1, 1, 0, 1]
+    for r in (0, 1):
+        out = np.frombuffer(got[r][0], dtype=RESULT_DTYPE)
+        assert list(out['index']) == [10 * l + owner[l] for l in range(7)]
+        assert list(out['label']) == list(range(7))
+        rows = np.frombuffer(got[r][1], dtype=RESULT_DTYPE).reshape(2, 7)
+        assert rows[0].tobytes() == out.tobytes() == rows[1].tobytes()   # (NaN scores: bytes)
+    assert got[0] == got[1]
+
+
+def _label_engine_worker(rank, world, port, q):
+    """One rank of a label-sharded fmin step on the GPU: its labels' history,
+    posterior and rounds (FminLoop label_ids), winners all-gathered."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from hyperopt_amd.engine import Engine
+        from hyperopt_amd.parallel import gather_labels, label_shards
+        from hyperopt_amd.workloads import FminLoop, mixed_history
+        hist = mixed_history(16, 4000, seed=2)
+        shards = label_shards(hist.labels, world)
+        eng = Engine(0)
+        loop = FminLoop(hist, label_ids=shards[rank])
+        loop.advance(eng, 3990)
+        loop.advance(eng, 3995, n_candidates=1 << 18)
+        one = gather_labels(eng.suggest(42, 1 << 18, round=9), shards, rank)
+        rows = gather_labels(eng.suggest_batch(7, list(range(500, 628)), 24), shards, rank)
+        eng.close()
+        q.put((rank, one.tobytes(), rows.tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_label_shards_gloo_world2():
+    """Label-sharded ranks (bench.py's default N > 1 partition) end with the
+    winners of one engine holding every label, bit for bit."""
+    import multiprocessing as mp
+    from hyperopt_amd.engine import RESULT_DTYPE, Engine
+    from hyperopt_amd.workloads import FminLoop, mixed_history
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_label_engine_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in procs:
+        r, a, b = q.get(timeout=200)
+        got[r] = (a, b)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    hist = mixed_history(16, 4000, seed=2)
+    eng = Engine(0)
+    loop = FminLoop(hist)
+    loop.advance(eng, 3995)
+    want = eng.suggest(42, 1 << 18, round=9)
+    want_rows = eng.suggest_batch(7, list(range(500, 628)), 24)
+    eng.close()
+    for r in (0, 1):
+        assert got[r][0] == want.tobytes()
+        assert got[r][1] == np.ascontiguousarray(want_rows).tobytes()

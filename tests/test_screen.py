@@ -99,6 +99,23 @@ def _assert_same(a, b):
         assert np.array_equal(a[f], b[f], equal_nan=f != 'index' and f != 'label'), f
 
 
+def test_screened_round_is_the_fp64_round_at_2_24(eng):
+    """The bench's own size: config 3 as fmin's loop builds it (device build
+    with numpy's tie order), 2^24 candidates per label -- the hot-bin
+    prefilter, the expansion index, the early exits and the near-tie fp64
+    re-scores against the plain fp64 round, bytewise, on two seeds."""
+    from hyperopt_amd.workloads import FminLoop, mixed_history
+    hist = mixed_history(32, 10001, seed=0)
+    loop = FminLoop(hist)
+    loop.advance(eng, 10000)
+    loop.advance(eng, 10001, n_candidates=1 << 24)
+    for rnd, seed in ((3, 1237), (4, 1238)):
+        a, b, screened, rescored = _suggest_both(eng, 1 << 24, rnd, seed)
+        assert np.ascontiguousarray(a).tobytes() == np.ascontiguousarray(b).tobytes()
+        assert screened == 20 * (1 << 24) and 0 < rescored < screened // 1000
+        assert eng.last_hot()[0] > 0               # the hot-bin prefilter ran
+
+
 @pytest.mark.parametrize('config', ['config2', 'config3', 'config3_device', 'config4_device',
                                     'hartmann_n30'])
 def test_screened_round_is_the_fp64_round(eng, config):

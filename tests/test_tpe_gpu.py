@@ -142,6 +142,24 @@ def test_suggest_deterministic_in_seed():
     assert a == b and a != c
 
 
+def test_precision_f32_suggests_the_f64_documents():
+    """precision='f32' is accepted and runs the exact path (tpe.py docstring:
+    the fp32 round is retired; its throughput comes from the fp64-exact
+    screens), so it suggests what precision='f64' does."""
+    space = {'x': hp.uniform('x', -5, 5), 'y': hp.qloguniform('y', 0, 5, 1),
+             'z': hp.choice('z', [0, 1, 2]), 'w': hp.normal('w', 0, 2)}
+    trials = H.Trials()
+    H.fmin(lambda d: d['x'] ** 2 + d['w'] ** 2, space, algo=tpe.suggest, max_evals=40, trials=trials,
+           rstate=np.random.RandomState(2))
+    dom = H.Domain(lambda d: 0, space)
+    for seed, nei in ((5, 24), (6, 5000)):
+        a = tpe.suggest([100], dom, trials, seed, n_EI_candidates=nei, precision='f32')
+        b = tpe.suggest([100], dom, trials, seed, n_EI_candidates=nei, precision='f64')
+        assert a[0]['misc']['vals'] == b[0]['misc']['vals']
+    with pytest.raises(ValueError):
+        tpe.suggest([100], dom, trials, 5, precision='f16')
+
+
 @pytest.mark.parametrize('name', ['quadratic1', 'many_dists', 'n_arms', 'q1_lognormal'])
 def test_opt_thresholds_device_posterior(name):
     """The same TestOpt thresholds with the posterior built on the device
