@@ -2245,19 +2245,94 @@ __device__ __forceinline__ tpe_label_result to_result(const Partial& p, int li) 
     return r;
 }
 
-__global__ __launch_bounds__(kBlock) void k_reduce(const Partial* __restrict__ partials,
-                                                   int32_t tiles, int32_t n_labels,
-                                                   tpe_label_result* __restrict__ out) {
+// per (label, round): the maxloc over its tiles' partials.  1024 threads, four
+// independent running bests per thread over the (key, idx) words only (16 of
+// the 40 bytes), the winning tile's record fetched once at the end: one
+// workgroup per label streams up to 8192 partials at full memory parallelism
+// instead of one dependent 40-byte load chain per thread.
+constexpr int kReduceBlock = 1024;
+__global__ __launch_bounds__(kReduceBlock) void k_reduce(const Partial* __restrict__ partials,
+                                                         int32_t tiles, int32_t n_labels,
+                                                         tpe_label_result* __restrict__ out) {
     const int li = blockIdx.x, rz = blockIdx.y, tid = threadIdx.x;
     const Partial* p = partials + ((size_t)rz * n_labels + li) * tiles;
-    Partial best{0, INT64_MAX, 0.0, 0.0, 0.0};
-    for (int t = tid; t < tiles; t += kBlock)
-        if (better(p[t].key, p[t].idx, best.key, best.idx)) best = p[t];
-    __shared__ Partial res;
-    __shared__ Partial sh[kBlock / 64];
-    block_maxloc(best.key, best.idx, best.value, best.lb, best.la, &res, sh);
+    uint64_t bk[4] = {0, 0, 0, 0};
+    int64_t bi[4] = {INT64_MAX, INT64_MAX, INT64_MAX, INT64_MAX};
+    int32_t bt[4] = {-1, -1, -1, -1};
+    for (int t0 = tid; t0 < tiles; t0 += 4 * kReduceBlock) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int t = t0 + u * kReduceBlock;
+            if (t < tiles) {
+                const uint64_t k = p[t].key;
+                const int64_t i = p[t].idx;
+                if (better(k, i, bk[u], bi[u])) {
+                    bk[u] = k;
+                    bi[u] = i;
+                    bt[u] = t;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 1; u < 4; ++u)
+        if (better(bk[u], bi[u], bk[0], bi[0])) {
+            bk[0] = bk[u];
+            bi[0] = bi[u];
+            bt[0] = bt[u];
+        }
+    uint64_t k = bk[0];
+    int64_t i = bi[0];
+    int32_t t = bt[0];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t ok = __shfl_xor(k, off);
+        const int64_t oi = __shfl_xor(i, off);
+        const int32_t ot = __shfl_xor(t, off);
+        if (better(ok, oi, k, i)) {
+            k = ok;
+            i = oi;
+            t = ot;
+        }
+    }
+    __shared__ uint64_t shk[kReduceBlock / 64];
+    __shared__ int64_t shi[kReduceBlock / 64];
+    __shared__ int32_t sht[kReduceBlock / 64];
+    if ((tid & 63) == 0) {
+        shk[tid >> 6] = k;
+        shi[tid >> 6] = i;
+        sht[tid >> 6] = t;
+    }
     __syncthreads();
-    if (tid == 0) out[(size_t)rz * n_labels + li] = to_result(res, li);
+    if (tid == 0) {
+        for (int w = 1; w < kReduceBlock / 64; ++w)
+            if (better(shk[w], shi[w], k, i)) {
+                k = shk[w];
+                i = shi[w];
+                t = sht[w];
+            }
+        const Partial best = t >= 0 ? p[t] : Partial{0, INT64_MAX, 0.0, 0.0, 0.0};
+        out[(size_t)rz * n_labels + li] = to_result(best, li);
+    }
+}
+
+// Several small fills in one launch (per-round counters, flags and
+// thresholds): grid.y = the fill, 32-bit words.  A hipMemsetAsync each would
+// cost a host API call and a queue slot apiece -- a round's resets used to be
+// ~10 of them between its kernels.
+constexpr int kMaxFills = 8;
+struct FillSet {
+    uint32_t* p[kMaxFills];
+    int64_t n[kMaxFills];
+    uint32_t v[kMaxFills];
+    int32_t count;
+};
+__global__ __launch_bounds__(kBlock) void k_fill_words(FillSet f) {
+    const int j = blockIdx.y;
+    uint32_t* p = f.p[j];
+    const int64_t n = f.n[j];
+    const uint32_t v = f.v[j];
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) p[i] = v;
 }
 
 // one partial per (round, label) -- packed and split-K maps: a thread each
@@ -2448,24 +2523,46 @@ struct EarlyPhase {
     int32_t slot_base, empty_from;
 };
 
-std::vector<EarlyPhase> early_phases(const RoundArgs& a, int64_t per, unsigned grid, bool early) {
+// the second phase's workgroups over all its (label, round) cells: they
+// stride over the tiles, so a smaller grid costs nothing when the first
+// phase found the winner (every workgroup exits at once) and still fills the
+// chip when it did not
+constexpr int64_t kEarlyWgs2 = 2048;
+
+std::vector<EarlyPhase> early_phases(const RoundArgs& a, int64_t per, unsigned grid, bool early,
+                                     int64_t cells) {
     const int64_t tiles_n = (a.n + per - 1) / per;
     const int64_t g1 = std::min<int64_t>({tiles_n, kEarlyTiles, (int64_t)a.tiles - 1});
     if (!early || g1 < 1 || g1 >= tiles_n || (int64_t)a.tiles - g1 < 1)
         return {EarlyPhase{grid, 0, a.n, 0, (int32_t)grid}};
-    const unsigned g2 = (unsigned)std::max<int64_t>(1, std::min<int64_t>(grid, (int64_t)a.tiles - g1));
+    const unsigned g2 = (unsigned)std::max<int64_t>(
+        1, std::min<int64_t>({(int64_t)grid, (int64_t)a.tiles - g1, kEarlyWgs2 / std::max<int64_t>(1, cells)}));
     return {EarlyPhase{(unsigned)g1, 0, g1 * per, 0, a.tiles},
             EarlyPhase{g2, g1 * per, a.n, (int32_t)g1, (int32_t)(g1 + g2)}};
 }
 
-// the per-(round, label) first-find indices, reset (nullptr: early exit off)
-int64_t* early_found(tpe_ctx* ctx, const RoundArgs& a) {
-    if (!ctx->early) return nullptr;
-    const size_t cells = (size_t)a.n_rounds * ctx->P->n_labels;
-    if (ctx->xfound.reserve(cells) != hipSuccess) return nullptr;
-    if (hipMemsetAsync(ctx->xfound.p, 0x7f, cells * sizeof(int64_t), ctx->stream) != hipSuccess) return nullptr;
-    return ctx->xfound.p;
+// queue a fill of `bytes` (a multiple of 4) with the 32-bit pattern v
+void add_fill(FillSet& f, void* p, size_t bytes, uint32_t v) {
+    if (!bytes) return;
+    f.p[f.count] = (uint32_t*)p;
+    f.n[f.count] = (int64_t)(bytes / 4);
+    f.v[f.count] = v;
+    ++f.count;
 }
+
+int run_fills(tpe_ctx* ctx, FillSet& f) {
+    if (!f.count) return TPE_OK;
+    int64_t mx = 1;
+    for (int j = 0; j < f.count; ++j) mx = std::max(mx, f.n[j]);
+    hipLaunchKernelGGL(k_fill_words, dim3((unsigned)std::min<int64_t>((mx + kBlock - 1) / kBlock, 1024), f.count),
+                       dim3(kBlock), 0, ctx->stream, f);
+    f.count = 0;
+    return ctx->hip(hipGetLastError(), "fill launch");
+}
+
+// the per-(round, label) first-find indices (reset at the round's start,
+// run_round; nullptr: early exit off)
+int64_t* early_found(tpe_ctx* ctx) { return ctx->early ? ctx->xfound.p : nullptr; }
 
 void bracket(tpe_ctx* ctx, int mode, int which) {
     ctx->mode_ran[mode] = true;
@@ -2482,9 +2579,10 @@ void launch_round(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
             const unsigned cgx = (unsigned)std::max<int64_t>(
                 1, std::min<int64_t>({(int64_t)a.gx, (a.n + kCatR * kBlock - 1) / (kCatR * kBlock),
                                       kHotWgs / std::max<int64_t>(1, (int64_t)nl * a.gz)}));
-            int64_t* found = early_found(ctx, a);
+            int64_t* found = early_found(ctx);
             ctx->cat_early = true;
-            for (const EarlyPhase& ph : early_phases(a, (int64_t)kCatR * kBlock, cgx, found != nullptr))
+            for (const EarlyPhase& ph :
+                 early_phases(a, (int64_t)kCatR * kBlock, cgx, found != nullptr, (int64_t)nl * a.gz))
                 hipLaunchKernelGGL((k_cat_tiles<kCatR>), dim3(ph.grid, nl, a.gz), dim3(kBlock), 0, ctx->stream,
                                    ctx->P->labels.p, g.dev[MODE], ctx->P->comps64.p, ctx->P->samp.p, ph.n,
                                    a.cand_offset, a.seed, ctx->rounds.p, ctx->P->n_labels, a.tiles,
@@ -2754,27 +2852,38 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
         HIPCHK(ctx, ctx->scr_idx.reserve(cells * lst));
         HIPCHK(ctx, ctx->scr_lb.reserve(cells));
         HIPCHK(ctx, ctx->scr_cnt.reserve(cells));
-        HIPCHK(ctx, hipMemsetAsync(ctx->scr_lb.p, 0, cells * sizeof(unsigned long long), ctx->stream));
-        HIPCHK(ctx, hipMemsetAsync(ctx->scr_cnt.p, 0, cells * sizeof(int32_t), ctx->stream));
+        FillSet fs{};
+        add_fill(fs, ctx->scr_lb.p, cells * sizeof(unsigned long long), 0);
+        add_fill(fs, ctx->scr_cnt.p, cells * sizeof(int32_t), 0);
         const unsigned sx = (unsigned)std::min<int64_t>((a.n + 8 * kBlock - 1) / (8 * kBlock), 1024);
         ctx->screen_mode = use_bx ? 3 : (ctx->window && a.n >= kWinMinN && a.cand_in == nullptr) ? 2 : 1;
+        if (!use_bx) {   // the expansion screen adds its own resets to the same launch
+            const int rc = run_fills(ctx, fs);
+            if (rc) return rc;
+        }
         if (use_bx) {
             // expansion screen: no sort, ~1e-12 bounds, near-ties re-scored
             tpe_rt::Posterior& P = *ctx->P;
             HIPCHK(ctx, ctx->win_evals.reserve(1));
-            HIPCHK(ctx, hipMemsetAsync(ctx->win_evals.p, 0, sizeof(unsigned long long), ctx->stream));
-            if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
+            add_fill(fs, ctx->win_evals.p, sizeof(unsigned long long), 0);
             if (hot) {
-                // hot-bin prefilter: draw + sub-bin bounds, then the
-                // expansion screen over the listed candidates only
                 HIPCHK(ctx, ctx->hot_x.reserve(cells * lst));
                 HIPCHK(ctx, ctx->hot_i.reserve(cells * lst));
                 HIPCHK(ctx, ctx->hot_cnt.reserve(cells));
                 HIPCHK(ctx, ctx->hot_t.reserve(cells));
                 HIPCHK(ctx, ctx->hot_flag.reserve(1));
-                HIPCHK(ctx, hipMemsetAsync(ctx->hot_cnt.p, 0, cells * sizeof(int32_t), ctx->stream));
-                HIPCHK(ctx, hipMemsetAsync(ctx->hot_t.p, 0, cells * sizeof(unsigned long long), ctx->stream));
-                HIPCHK(ctx, hipMemsetAsync(ctx->hot_flag.p, 0, sizeof(int32_t), ctx->stream));
+                add_fill(fs, ctx->hot_cnt.p, cells * sizeof(int32_t), 0);
+                add_fill(fs, ctx->hot_t.p, cells * sizeof(unsigned long long), 0);
+                add_fill(fs, ctx->hot_flag.p, sizeof(int32_t), 0);
+            }
+            {
+                const int rc = run_fills(ctx, fs);
+                if (rc) return rc;
+            }
+            if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
+            if (hot) {
+                // hot-bin prefilter: draw + sub-bin bounds, then the
+                // expansion screen over the listed candidates only
                 {
                     const int rc = hot_tau_prepare(ctx, a.n);
                     if (rc) return rc;
@@ -3081,8 +3190,13 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
             HIPCHK(ctx, ctx->qkmax.reserve(nq));
             HIPCHK(ctx, hipMemcpyAsync(ctx->qinfo.p, qi.data(), nq * sizeof(QInfo), hipMemcpyHostToDevice,
                                        ctx->stream));
-            HIPCHK(ctx, hipMemsetAsync(ctx->qkmax.p, 0, nq * sizeof(unsigned long long), ctx->stream));
-            int64_t* found = a.S.cpack == 0 ? early_found(ctx, a) : nullptr;
+            FillSet fs{};
+            add_fill(fs, ctx->qkmax.p, nq * sizeof(unsigned long long), 0);
+            {
+                const int rc = run_fills(ctx, fs);
+                if (rc) return rc;
+            }
+            int64_t* found = a.S.cpack == 0 ? early_found(ctx) : nullptr;
             for (int fam = 0; fam < 2; ++fam) {
                 const int mode = fam ? QUANT_LGMM : QUANT_GMM;
                 const int cnt = fam ? nql : nqg;
@@ -3109,7 +3223,8 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
                     1, std::min<int64_t>({(int64_t)a.gx, (a.n + kQR * kBlock - 1) / (kQR * kBlock),
                                           kHotWgs / std::max<int64_t>(1, (int64_t)cnt * a.gz)}));
 #define TPE_QTILES(M)                                                                                   \
-    for (const EarlyPhase& ph : early_phases(a, (int64_t)kQR * kBlock, qgx, found != nullptr))          \
+    for (const EarlyPhase& ph : early_phases(a, (int64_t)kQR * kBlock, qgx, found != nullptr,           \
+                                             (int64_t)cnt * a.gz))                                     \
         hipLaunchKernelGGL((k_qfused_tiles<M, kQR>), dim3(ph.grid, cnt, a.gz), dim3(kBlock), 0,         \
                            ctx->stream, ctx->P->labels.p, g.dev[mode], ctx->P->comps64.p, ctx->P->samp.p, \
                            ctx->qinfo.p, ctx->qtab.p, ph.n, a.cand_offset, a.seed, ctx->rounds.p, qbase,  \
@@ -3293,9 +3408,18 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     HIPCHK(ctx, ctx->errflag.reserve(1));
     HIPCHK(ctx, hipMemcpyAsync(ctx->rounds.p, rounds_h, n_rounds * sizeof(uint32_t),
                                hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(ctx, hipMemsetAsync(ctx->errflag.p, 0, sizeof(int32_t), ctx->stream));
     HIPCHK(ctx, ctx->xdrawn.reserve(2));
-    HIPCHK(ctx, hipMemsetAsync(ctx->xdrawn.p, 0, 2 * sizeof(unsigned long long), ctx->stream));
+    {
+        FillSet f{};
+        add_fill(f, ctx->errflag.p, sizeof(int32_t), 0);
+        add_fill(f, ctx->xdrawn.p, 2 * sizeof(unsigned long long), 0);
+        if (ctx->early && S.cpack == 0 && cand_in_dev == nullptr) {   // early_found: no find yet
+            HIPCHK(ctx, ctx->xfound.reserve((size_t)n_rounds * L));
+            add_fill(f, ctx->xfound.p, (size_t)n_rounds * L * sizeof(int64_t), 0x7f7f7f7fu);
+        }
+        const int rc = run_fills(ctx, f);
+        if (rc) return rc;
+    }
     Groups g;
     for (int m = 0; m < kNumModes; ++m) {
         g.dev[m] = ctx->P->groups.p + ctx->P->group_off[m];
@@ -3383,7 +3507,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
                            ctx->stream, ctx->partials.p, nr, L, ctx->results.p);
         HIPCHK(ctx, hipGetLastError());
     } else if (tiles > 1) {
-        hipLaunchKernelGGL(k_reduce, dim3(L, n_rounds), dim3(kBlock), 0, ctx->stream,
+        hipLaunchKernelGGL(k_reduce, dim3(L, n_rounds), dim3(kReduceBlock), 0, ctx->stream,
                            ctx->partials.p, tiles, L, ctx->results.p);
         HIPCHK(ctx, hipGetLastError());
     }

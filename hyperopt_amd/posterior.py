@@ -307,7 +307,7 @@ def reference_orders(losses, n_below, obs_of, labels):
     return below, off, order
 
 
-_POOL_MIN = 1 << 17   # observations to sort, from which the pool pays
+_POOL_MIN = 1 << 14   # observations to sort (over several labels), from which the pool pays
 _pool = None
 
 

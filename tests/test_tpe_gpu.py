@@ -68,8 +68,8 @@ def test_opt_thresholds(name, np_raise):
     (best -1.935 vs -1.96) and quadratic1 (2.6e-5 vs 1e-5) -- which the
     reference itself misses on 3 and 2 of seeds 0..19
     (tests/golden/testopt_reference_rates.json); test_opt_pass_rates holds
-    them (and every domain) to the reference's pass rate instead, which the
-    engine meets or beats on all eight."""
+    them (and every domain) to the reference's pass rate over 20 seeds
+    instead."""
     if name in ('distractor', 'quadratic1'):
         pytest.xfail('single-seed path misses; see test_opt_pass_rates')
     best, top = _testopt_best(name, 123)
@@ -81,7 +81,10 @@ def test_opt_pass_rates(name, np_raise):
     """TestOpt over seeds 0..19: the engine beats each domain's threshold on
     at least as many seeds as the reference's own tpe.suggest does on the
     same seeds (tests/golden/gen_testopt_rates.py, run in this container),
-    less 3 (a binomial margin: the sample paths differ)."""
+    less 2 (the sample paths differ: a domain the reference passes on 19 of
+    20 seeds, p ~ 0.95, lands on 17 or fewer with probability ~0.08).
+    Measured at r3 (`-s`): branin 17 (reference 19), distractor 18 (17),
+    quadratic1 18 (18), the other five 20 (20)."""
     import json
     import os
     ref = json.load(open(os.path.join(os.path.dirname(__file__), 'golden',
@@ -90,7 +93,7 @@ def test_opt_pass_rates(name, np_raise):
     ours = [_testopt_best(name, seed)[0] for seed in range(ref['n_seeds'])]
     our_pass = sum(b < THRESH[name] for b in ours)
     print('%s: passes %d / %d (reference %d)' % (name, our_pass, len(ours), ref_pass))
-    assert our_pass >= ref_pass - 3, (name, our_pass, ref_pass, ours)
+    assert our_pass >= ref_pass - 2, (name, our_pass, ref_pass, ours)
 
 
 def test_suggest_document_and_conditional_space():
