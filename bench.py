@@ -417,6 +417,14 @@ def main():
     # the round alone, and the reference for the unscreened comparison
     warm_first = args.warmup + args.steps
     wdt, _, _, _ = timed(args.steps, warm_first, False, keep=True) if fresh_mode else (None,) * 4
+    # device memory after the timed steps: the library's buffers (their
+    # high-water mark: they grow by 1/4 and are kept) and the whole device
+    free_b, total_b = torch.cuda.mem_get_info()
+    mem = {'library_bytes': eng.device_bytes(), 'device_used_bytes': int(total_b - free_b),
+           'device_total_bytes': int(total_b),
+           'note': 'library_bytes: tpe_device_bytes (posterior, resident history, expansion index, '
+                   'hot lists, round buffers of this rank); device_used_bytes: hipMemGetInfo, '
+                   'including the HIP / torch runtime'}
     # the 8-GPU step projected from this one GPU: each rank's share run
     # alone (label shards: an engine per shard holding its labels' history,
     # posterior and index, whole rounds, the slowest shard setting the step;
@@ -607,6 +615,7 @@ def main():
                   'fresh_posterior_round_ms': (round(post_build['device_call_ms'] + prep_ms
                                                      + dt / args.steps * 1e3, 3) if prep_ms else None)}),
         'scaling_projection': proj,
+        'device_memory': mem,
         'posterior_build': dict(post_build, expansion_index_ms=(round(prep_ms, 3) if prep_ms else None),
                                 expansion_index_note='the first index of the run (bin tables, lists, '
                                 'sub-bin bounds; wall ms with the kernels)'),

@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 #include <memory>
 #include <string>
 #include <vector>
@@ -39,31 +40,45 @@ struct QInfo {
     int64_t pad;
 };
 
+// device bytes held by every DevBuf of the process (tpe_device_bytes)
+inline std::atomic<int64_t>& device_bytes_held() {
+    static std::atomic<int64_t> n{0};
+    return n;
+}
+
 template <typename T>
 struct DevBuf {
     T* p = nullptr;
     size_t cap = 0;
+    static void account(size_t elems, int sign) {
+        device_bytes_held().fetch_add(sign * (int64_t)(elems * sizeof(T)), std::memory_order_relaxed);
+    }
     // grows by at least 1/4 (a history that grows by one trial per call
     // would otherwise reallocate -- and hipFree synchronise the device --
     // on every build); the contents are not kept
     hipError_t reserve(size_t n) {
         if (n <= cap) return hipSuccess;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
+        release();
         const size_t want = std::max<size_t>(n, 1), grown = want + want / 4;
         hipError_t e = hipMalloc(&p, grown * sizeof(T));
         if (e == hipSuccess) {
             cap = grown;
+            account(cap, 1);
             return e;
         }
         (void)hipGetLastError();   // (clear the failed allocation) exactly n, then
         e = hipMalloc(&p, want * sizeof(T));
-        if (e == hipSuccess) cap = want;
+        if (e == hipSuccess) {
+            cap = want;
+            account(cap, 1);
+        }
         return e;
     }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            (void)hipFree(p);
+            account(cap, -1);
+        }
         p = nullptr;
         cap = 0;
     }

@@ -4084,6 +4084,8 @@ int tpe_last_drawn(const tpe_ctx* ctx, int64_t* quantized, int64_t* categorical)
     return TPE_OK;
 }
 
+int64_t tpe_device_bytes(void) { return tpe_rt::device_bytes_held().load(std::memory_order_relaxed); }
+
 int tpe_last_rescore_terms(const tpe_ctx* ctx, int64_t* terms) {
     if (!ctx) return TPE_ERR_ARG;
     if (terms) *terms = ctx->screen_rescore_terms;

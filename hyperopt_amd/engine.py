@@ -312,6 +312,11 @@ class Engine(object):
         self._check(self.lib.tpe_last_prepare(self.h, ctypes.byref(ms)))
         return ms.value
 
+    def device_bytes(self):
+        """Device memory the library holds (every context of the process),
+        bytes: the high-water mark of its buffers (tpe_device_bytes)."""
+        return int(self.lib.tpe_device_bytes())
+
     def last_drawn(self):
         """(quantized, categorical) candidates the last round drew: fewer
         than rounds x n when the exact early exit stopped a label's round."""

@@ -353,6 +353,13 @@ int tpe_last_rescore_terms(const tpe_ctx *ctx, int64_t *terms);
  * drawn).  The categorical evals in tpe_last_mode_stats count these. */
 int tpe_last_drawn(const tpe_ctx *ctx, int64_t *quantized, int64_t *categorical);
 
+/* Device memory the library holds right now, over every context of the
+ * process (posteriors, resident histories, expansion indexes, round
+ * buffers; the HIP runtime's own allocations not included), in bytes.
+ * Buffers grow by 1/4 and are kept between calls, so after a run this is
+ * its high-water mark. */
+int64_t tpe_device_bytes(void);
+
 /* Which screen the last round's dense tile-map labels went through: 0 none
  * (unscreened fp64, fp32 precision, or no dense tile round), 1 the plain
  * fp32 screen, 2 the windowed fp32 screen, 3 the expansion screen
