@@ -225,9 +225,12 @@ def measured_pmc(kernel_prefix):
     of this bench, tools/prof_round.sh + tools/pmc_summary.py; FETCH doubled
     per the gfx950 correction) -- (None, None, None) if absent."""
     import glob
-    # tags sort by length, then name: r2z < r2aa < r2ai (newest last)
-    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_pmc_summary.json')),
-                   key=lambda f: (len(os.path.basename(f)), os.path.basename(f)))
+    import re
+
+    def tag_key(f):   # r<round><letters>: by round, then r2z < r2aa < r2ai (newest last)
+        m = re.match(r'r(\d+)([a-z]*)_', os.path.basename(f))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, '')
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_pmc_summary.json')), key=tag_key)
     for f in reversed(files):
         d = json.load(open(f))
         for name, v in d.items():

@@ -135,10 +135,13 @@ constexpr uint32_t kMaxAttempts = 1u << 16;
 
 // Component lookup of the draw: the first k with cdf[k] > u.  SampGlobal
 // searches the records in global memory; SampShared (a workgroup's copy in
-// LDS, stage_samp, padded to 64 entries) runs a branch-free lower bound
-// over the LDS copy; the categorical tile kernel walks the 64-entry guide
-// table (guide[j] = the first k with cdf[k] > j / 64).  All return the same
-// component.
+// LDS, stage_samp, padded to 64 entries) starts from a 256-cell guide
+// (gd[j] = the first k with cdf[k] > j / 256, j = the top 8 bits of u's
+// 32-bit word) and takes at most `steps` more comparisons -- the most
+// cumulative weights any cell holds, 1 for mixtures without weights below
+// 1/256 -- else a branch-free lower bound over all 64; the categorical tile
+// kernel walks the 64-entry guide table (guide[j] = the first k with
+// cdf[k] > j / 64).  All return the same component.
 struct SampGlobal {
     const SampRec* __restrict__ s;
     int ns;
@@ -149,21 +152,31 @@ struct SampGlobal {
     }
 };
 
-constexpr int kSampLds = 64;   // below components staged in LDS (K_b <= 26 in practice)
+constexpr int kSampLds = 64;     // below components staged in LDS (K_b <= 26 in practice)
+constexpr int kGuideSteps = 3;   // guided picks take at most this many comparisons
 struct SampLds {
     double cdf[kSampLds], mu[kSampLds], sg[kSampLds];
     uint8_t guide[64];
+    uint8_t gd[256];
+    int steps;
 };
 
 struct SampShared {
     const SampLds* __restrict__ t;
-    // branch-free lower bound over the 64 staged cumulative weights (padded
-    // with 2.0 past the last): six LDS reads, no loop, so the draws of a
-    // thread's slots can interleave
     __device__ __forceinline__ void pick(double u, double& mu, double& sg) const {
-        int k = 0;
+        // (steps is the same for the whole workgroup: a scalar branch)
+        const int steps = __builtin_amdgcn_readfirstlane(t->steps);
+        int k;
+        if (steps <= kGuideSteps) {
+            k = t->gd[(int)(u * 256.0)];   // (u = w 2^-32: exactly w >> 24)
 #pragma unroll
-        for (int step = kSampLds / 2; step > 0; step >>= 1) k = t->cdf[k + step - 1] <= u ? k + step : k;
+            for (int s = 0; s < kGuideSteps; ++s)
+                if (s < steps) k += t->cdf[k] <= u ? 1 : 0;   // (k <= ns - 1 throughout: cdf[ns - 1] = 1 > u)
+        } else {   // branch-free lower bound over the 64 (padded with 2.0)
+            k = 0;
+#pragma unroll
+            for (int step = kSampLds / 2; step > 0; step >>= 1) k = t->cdf[k + step - 1] <= u ? k + step : k;
+        }
         mu = t->mu[k];
         sg = t->sg[k];
     }
@@ -185,12 +198,26 @@ __device__ __forceinline__ bool stage_samp(const DLabel& L, const SampRec* __res
             t->sg[k] = 0.0;
         }
     }
+    if (threadIdx.x == 0) t->steps = 0;
     __syncthreads();
     if (threadIdx.x < 64) {
         const double v = (double)threadIdx.x / 64.0;
         int k = 0;
         while (k < L.ns - 1 && t->cdf[k] <= v) ++k;
         t->guide[threadIdx.x] = (uint8_t)k;
+    }
+    for (int j = threadIdx.x; j < 256; j += blockDim.x) {
+        // the first k with cdf[k] > j / 256, and the cumulative weights
+        // inside [j / 256, (j + 1) / 256): the comparisons a pick in the
+        // cell may need
+        const double v0 = (double)j / 256.0, v1 = (double)(j + 1) / 256.0;
+        int k0 = 0, k1 = 0;
+        for (int k = 0; k < L.ns - 1; ++k) {
+            k0 += t->cdf[k] <= v0 ? 1 : 0;
+            k1 += t->cdf[k] < v1 ? 1 : 0;
+        }
+        t->gd[j] = (uint8_t)k0;
+        if (k1 > k0) atomicMax(&t->steps, k1 - k0);
     }
     __syncthreads();
     return true;
