@@ -420,6 +420,25 @@ def main():
     # the round alone, and the reference for the unscreened comparison
     warm_first = args.warmup + args.steps
     wdt, _, _, _ = timed(args.steps, warm_first, False, keep=True) if fresh_mode else (None,) * 4
+    # the plain fp64 round on the SAME (seed, round) as screened steps on
+    # the same posterior -- before anything else advances it: winners,
+    # values and lpdfs bit for bit
+    unscreened = None
+    if screen and args.unscreened_steps > 0 and world == 1 and devs is None:
+        nu = args.unscreened_steps
+        first = warm_first if fresh_mode else args.warmup + args.steps
+        if not fresh_mode:
+            timed(nu, first, False, keep=True)
+        eng.set_option('screen', 0)
+        ures = {}
+        t0 = time.perf_counter()
+        for i in range(nu):
+            ures[first + i] = step(first + i, False)
+        torch.cuda.synchronize()
+        udt = time.perf_counter() - t0
+        eng.set_option('screen', 1)
+        same = all(results[k].view(np.uint8).tobytes() == ures[k].view(np.uint8).tobytes() for k in ures)
+        unscreened = (same, udt, nu, first)
     # device memory after the timed steps: the library's buffers (their
     # high-water mark: they grow by 1/4 and are kept) and the whole device
     free_b, total_b = torch.cuda.mem_get_info()
@@ -659,23 +678,8 @@ def main():
                     '(tests/test_screen.py).  `value` counts the terms executed (screen + '
                     're-score); the roofline counts the terms the screening kernel summed.  '
                     'other_dense_ms: keys + sort, select, re-score'}
-        if args.unscreened_steps > 0 and world == 1 and devs is None:
-            # the plain fp64 round on the SAME (seed, round) as screened steps
-            # on the same posterior: winners, values and lpdfs bit for bit
-            nu = args.unscreened_steps
-            first = warm_first if fresh_mode else args.warmup + args.steps
-            if not fresh_mode:
-                timed(nu, first, False, keep=True)
-            eng.set_option('screen', 0)
-            ures = {}
-            t0 = time.perf_counter()
-            for i in range(nu):
-                ures[first + i] = step(first + i, False)
-            torch.cuda.synchronize()
-            udt = time.perf_counter() - t0
-            eng.set_option('screen', 1)
-            same = all(results[k].view(np.uint8).tobytes() == ures[k].view(np.uint8).tobytes()
-                       for k in ures)
+        if unscreened is not None:
+            same, udt, nu, first = unscreened
             line['screened_equals_fp64'] = bool(same)
             line['screen']['unscreened_fp64'] = {
                 'steps': nu, 'ms_per_step': round(udt / nu * 1e3, 3),
