@@ -50,6 +50,7 @@ TPE_OPT_EXPAND = 11
 TPE_OPT_HOT = 12
 TPE_OPT_EARLY = 13
 TPE_OPT_HOT_DIV = 14
+TPE_OPT_ZERO_WIN = 15
 
 TPE_OBS_IDENTITY = 0
 TPE_OBS_LOG = 1

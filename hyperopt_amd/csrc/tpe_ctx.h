@@ -158,6 +158,11 @@ struct Posterior {
     // window index of the dense labels' above mixtures (windowed fp32 screen,
     // tpe_engine.hip k_win_*), built on first use after every posterior change
     bool win_ready = false;
+    // exact-zero windows of the dense labels' above mixtures (packed
+    // re-score, k_zero_windows): per component, prefix max of the largest x'
+    // where its fp64 term can be nonzero, suffix min of the smallest
+    bool zw_ready = false;
+    DevBuf<double> zw_hi, zw_lo;
     int32_t win_t = 0;                   // the cut T the index was built for
     DevBuf<tpe::WinLabel> win;           // per label
     DevBuf<double> win_p, win_q;         // per component: prefix max of hi / suffix min of lo
@@ -210,6 +215,9 @@ struct Posterior {
         win_skip.release();
         win_skip_part.release();
         win_ready = false;
+        zw_ready = false;
+        zw_hi.release();
+        zw_lo.release();
         bx.release();
         bx_h.clear();
         bx_tab.release();
@@ -361,6 +369,7 @@ struct tpe_ctx {
     // hot-bin prefilter of the expansion screen (TPE_OPT_HOT, tpe_device.h)
     int32_t hot = 1;                     // 0 off, 1 on, 2 test: force the fallback
     bool early = true;                   // early exit of quantized / categorical tile rounds
+    bool zero_win = true;                // packed re-score skips the exactly-zero above terms
     double hot_cap_div = 16.0;           // hot lists hold n / hot_cap_div per cell (shrinks on overflow)
     DevBuf<double> hot_x;                // per cell: listed candidates' x
     DevBuf<int32_t> hot_i, hot_cnt;      //   their indices; per cell the count

@@ -1481,6 +1481,90 @@ __global__ __launch_bounds__(kBlock) void k_pick_win(const P2* __restrict__ lohi
 // mixture and the candidate) from zero -- the chunked map's own per-chunk
 // sums -- into plane 2 + c (0: below, 1: x) at the entry's place off[y] + e
 // of the compacted order; k_finish_rescore adds the chunks in order.
+// Per dense label (grid.x = label position), over its above records in
+// order: zhi[k] = max over j <= k of the largest x' where record j's fp64
+// term can be nonzero, zlo[k] = min over j >= k of the smallest (kZeroU);
+// +-inf for a record whose term is 0 everywhere.  For x' in [xa, xb] every
+// nonzero term lies in [first k with zhi[k] >= xa, first k with zlo[k] >
+// xb).  Thread t scans a contiguous segment; the segment totals are scanned
+// by thread 0 (once per posterior).
+__device__ __forceinline__ void zero_reach(const Comp<double>& c, double& lo, double& hi) {
+    const double t = c.c + kZeroU;
+    if (!(t >= 0.0) || !(c.a > 0.0)) {   // never nonzero (or an unusable record: keep it always)
+        lo = t >= 0.0 ? -__builtin_inf() : __builtin_inf();
+        hi = t >= 0.0 ? __builtin_inf() : -__builtin_inf();
+        return;
+    }
+    const double mu = c.mu / c.a, w = sqrt(t) / c.a;
+    const double slack = 1e-9 * (fabs(mu) + w + 1.0);
+    lo = mu - w - slack;
+    hi = mu + w + slack;
+}
+
+constexpr int kZwBlock = 1024;
+__global__ __launch_bounds__(kZwBlock) void k_zero_windows(const DLabel* __restrict__ labels,
+                                                           const int32_t* __restrict__ group,
+                                                           const Comp<double>* __restrict__ comps64,
+                                                           double* __restrict__ zhi, double* __restrict__ zlo) {
+    const DLabel L = labels[group[blockIdx.x]];
+    const Comp<double>* c = comps64 + L.comp_a;
+    double* ph = zhi + L.comp_a;
+    double* pl = zlo + L.comp_a;
+    const int n = L.na, seg = (n + kZwBlock - 1) / kZwBlock;
+    const int k0 = min(n, (int)threadIdx.x * seg), k1 = min(n, k0 + seg);
+    __shared__ double sh[kZwBlock], sl[kZwBlock];
+    double mh = -__builtin_inf(), ml = __builtin_inf();
+    for (int k = k0; k < k1; ++k) {
+        double lo, hi;
+        zero_reach(c[k], lo, hi);
+        mh = fmax(mh, hi);
+        ml = fmin(ml, lo);
+    }
+    sh[threadIdx.x] = mh;
+    sl[threadIdx.x] = ml;
+    __syncthreads();
+    if (threadIdx.x == 0) {   // exclusive prefix max / suffix min of the segments
+        double run = -__builtin_inf();
+        for (int t = 0; t < kZwBlock; ++t) {
+            const double v = sh[t];
+            sh[t] = run;
+            run = fmax(run, v);
+        }
+        run = __builtin_inf();
+        for (int t = kZwBlock - 1; t >= 0; --t) {
+            const double v = sl[t];
+            sl[t] = run;
+            run = fmin(run, v);
+        }
+    }
+    __syncthreads();
+    double run = sh[threadIdx.x];
+    for (int k = k0; k < k1; ++k) {
+        double lo, hi;
+        zero_reach(c[k], lo, hi);
+        run = fmax(run, hi);
+        ph[k] = run;
+    }
+    run = sl[threadIdx.x];
+    for (int k = k1 - 1; k >= k0; --k) {
+        double lo, hi;
+        zero_reach(c[k], lo, hi);
+        run = fmin(run, lo);
+        pl[k] = run;
+    }
+}
+
+// first k in [0, n) with v[k] > t (strict) or >= t; v non-decreasing
+__device__ __forceinline__ int first_above(const double* __restrict__ v, int n, double t, bool strict) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        const bool past = strict ? v[mid] > t : v[mid] >= t;
+        if (past) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+}
+
 template <int R>
 __global__ __launch_bounds__(kBlock) void k_rescore_packed(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
@@ -1488,7 +1572,7 @@ __global__ __launch_bounds__(kBlock) void k_rescore_packed(
     int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, int32_t chunk,
     const int32_t* __restrict__ cnt, const int64_t* __restrict__ list, int64_t cap,
     const RescoreChunk* __restrict__ chunks, const int64_t* __restrict__ off, int64_t total,
-    double* __restrict__ planes) {
+    double* __restrict__ planes, const double* __restrict__ zhi, const double* __restrict__ zlo) {
     const RescoreChunk ch = chunks[blockIdx.x];
     const int y = ch.cell, c = blockIdx.y;
     const DLabel L = labels[group[y]];
@@ -1519,7 +1603,31 @@ __global__ __launch_bounds__(kBlock) void k_rescore_packed(
     }
     if (c == 0) lse_acc<R>(comps64 + L.comp_b, L.nb, xr, sb, exp_tab);
     const int k0 = min(c * chunk, L.na), k1 = min(k0 + chunk, L.na);
-    lse_acc<R>(comps64 + L.comp_a + k0, k1 - k0, xr, sa, exp_tab);
+    if (zhi) {
+        // the wave's candidates span [xa, xb]: the above records outside
+        // the window have terms of exactly +0.0 at all of them
+        double xa = __builtin_inf(), xb = -__builtin_inf();
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (valid[r]) {
+                xa = fmin(xa, xr[r]);
+                xb = fmax(xb, xr[r]);
+            }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            xa = fmin(xa, __shfl_xor(xa, o));
+            xb = fmax(xb, __shfl_xor(xb, o));
+        }
+        if (!(xa <= xb)) {   // no valid lane (or NaN): the whole chunk, as lse_acc
+            lse_acc<R>(comps64 + L.comp_a + k0, k1 - k0, xr, sa, exp_tab);
+        } else {
+            const int wlo = __builtin_amdgcn_readfirstlane(first_above(zhi + L.comp_a, L.na, xa, false));
+            const int whi = __builtin_amdgcn_readfirstlane(first_above(zlo + L.comp_a, L.na, xb, true));
+            lse_acc_window<R>(comps64 + L.comp_a + k0, k1 - k0, wlo - k0, whi - k0, xr, sa, exp_tab);
+        }
+    } else {
+        lse_acc<R>(comps64 + L.comp_a + k0, k1 - k0, xr, sa, exp_tab);
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         if (!valid[r]) continue;
@@ -2755,10 +2863,21 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
         HIPCHK(ctx, hipMemcpyAsync(ctx->scr_chunks.p, tab.data(), tab.size() * sizeof(RescoreChunk),
                                    hipMemcpyHostToDevice, ctx->stream));
         const RescoreChunk* tabd = reinterpret_cast<const RescoreChunk*>(ctx->scr_chunks.p);
+        tpe_rt::Posterior& P = *ctx->P;
+        if (ctx->zero_win && !P.zw_ready) {   // once per posterior
+            HIPCHK(ctx, P.zw_hi.reserve(P.comps64.cap));
+            HIPCHK(ctx, P.zw_lo.reserve(P.comps64.cap));
+            // every dense label of the posterior (the GMM1 and LGMM1 groups are adjacent)
+            const int nd = (int)(P.h_group[DENSE_GMM].size() + P.h_group[DENSE_LGMM].size());
+            hipLaunchKernelGGL(k_zero_windows, dim3((unsigned)nd), dim3(kZwBlock), 0, ctx->stream, P.labels.p,
+                               P.groups.p + P.group_off[DENSE_GMM], P.comps64.p, P.zw_hi.p, P.zw_lo.p);
+            P.zw_ready = true;
+        }
         hipLaunchKernelGGL((k_rescore_packed<kRP>), dim3((unsigned)tab.size(), nch), dim3(kBlock), 0,
                            ctx->stream, ctx->P->labels.p, grp, ctx->P->comps64.p, ctx->P->samp.p,
                            a.cand_offset, a.seed, ctx->rounds.p, chunk, ctx->scr_cnt.p,
-                           ctx->scr_list.p, cap, tabd, ctx->scr_off.p, total, ctx->scr_planes.p);
+                           ctx->scr_list.p, cap, tabd, ctx->scr_off.p, total, ctx->scr_planes.p,
+                           ctx->zero_win ? P.zw_hi.p : nullptr, ctx->zero_win ? P.zw_lo.p : nullptr);
         hipLaunchKernelGGL(k_finish_rescore, dim3((unsigned)tab.size()), dim3(kBlock), 0, ctx->stream,
                            ctx->P->labels.p, grp, ctx->P->comps64.p, a.cand_offset, nch, ctx->scr_cnt.p,
                            ctx->scr_list.p, cap, tabd, ctx->scr_off.p, total, ctx->scr_planes.p,
@@ -3728,6 +3847,7 @@ int set_posterior_impl(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_lab
     ctx->P->groups_h = cat;
     ctx->P->h_labels = dl;
     ctx->P->win_ready = false;
+    ctx->P->zw_ready = false;
     ctx->P->bx_ready = false;
     ctx->P->n_labels = n_labels;
     return TPE_OK;
@@ -4120,6 +4240,7 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
         case TPE_OPT_WINDOW: ctx->window = value != 0; break;
         case TPE_OPT_EXPAND: ctx->expand = value != 0; break;
         case TPE_OPT_EARLY: ctx->early = value != 0; break;
+        case TPE_OPT_ZERO_WIN: ctx->zero_win = value != 0; break;
         case TPE_OPT_HOT_DIV:
             if (value < 1 || value > (1 << 20)) return ctx->fail(TPE_ERR_ARG, "hot list divisor must be in [1, 2^20]");
             ctx->hot_cap_div = (double)value;

@@ -428,6 +428,10 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *                   candidates per (round, label) (at least 4096); a round
  *                   whose list overflows screens every candidate instead
  *                   and divides HOT_DIV by 4 for the next rounds        [16]
+ *   TPE_OPT_ZERO_WIN  the packed map's fp64 re-score sums only the above
+ *                   components whose terms can be nonzero at the wave's
+ *                   candidates (the others are exactly +0.0: the same
+ *                   bits)                                                 [1]
  *   TPE_OPT_WIN_GROUPS  label groups of a windowed round, each sorted on a
  *                   second stream while the previous one is screened
  *                   (0: one group; the chip is busy either way)          [0]
@@ -455,6 +459,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_HOT 12
 #define TPE_OPT_EARLY 13
 #define TPE_OPT_HOT_DIV 14
+#define TPE_OPT_ZERO_WIN 15
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
 
 /* Build now what the resident posterior's first round(s) of n_candidates

@@ -191,6 +191,25 @@ def test_screened_packed_rounds_are_the_fp64_rounds(eng, rounds, C, chunks):
     print('packed %d x %d (chunks %d): re-scored %.4f' % (rounds, C, chunks, rescored / screened))
 
 
+def test_packed_rescore_zero_windows_same_bits(eng):
+    """Config 5 (128 labels, N = 50k, 4096 rounds x 24): the packed
+    re-score summing only the above components whose fp64 terms can be
+    nonzero at the wave's candidates (TPE_OPT_ZERO_WIN, k_zero_windows)
+    gives the bytes of the full sums -- and of the unscreened round."""
+    from hyperopt_amd.workloads import FminLoop, mixed_history
+    hist = mixed_history(128, 50000, seed=0)
+    FminLoop(hist).advance(eng, 50000)
+    ids = list(range(9000, 9000 + 4096))
+    out = {}
+    for zw, screen in ((1, 1), (0, 1), (1, 0)):
+        eng.set_option('zero_win', zw)
+        eng.set_option('screen', screen)
+        out[(zw, screen)] = np.ascontiguousarray(eng.suggest_batch(77, ids, 24)).tobytes()
+    eng.set_option('zero_win', 1)
+    eng.set_option('screen', 1)
+    assert out[(1, 1)] == out[(0, 1)] == out[(1, 0)]
+
+
 def test_windowed_screen_skips_terms(eng):
     """Config 3's posterior, 2^20 candidates: the windowed screen sums a
     fraction of the terms the plain screen sums, and both give the fp64
