@@ -163,6 +163,7 @@ struct Posterior {
     // where its fp64 term can be nonzero, suffix min of the smallest
     bool zw_ready = false;
     DevBuf<double> zw_hi, zw_lo;
+    DevBuf<int32_t> zw_wide, zw_n;       // per label at comp_a: its wide records; per label: their count
     int32_t win_t = 0;                   // the cut T the index was built for
     DevBuf<tpe::WinLabel> win;           // per label
     DevBuf<double> win_p, win_q;         // per component: prefix max of hi / suffix min of lo
@@ -218,6 +219,8 @@ struct Posterior {
         zw_ready = false;
         zw_hi.release();
         zw_lo.release();
+        zw_wide.release();
+        zw_n.release();
         bx.release();
         bx_h.clear();
         bx_tab.release();

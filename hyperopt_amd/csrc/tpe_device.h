@@ -683,28 +683,6 @@ __device__ __forceinline__ void lse_acc(const Comp<double>* __restrict__ c, int 
     }
 }
 
-// lse_acc over the components [lo, hi) of [0, n) only, the others' terms
-// being exactly +0.0 at every x of the caller's lanes (k_zero_windows): the
-// same slices, each summed in order from 0 over its part of the window --
-// skipping +0.0 terms and +0.0 slice sums leaves every partial sum, hence
-// the result, bit-identical to lse_acc.  lo, hi wave-uniform.
-template <int R>
-__device__ __forceinline__ void lse_acc_window(const Comp<double>* __restrict__ c, int n, int lo, int hi,
-                                               const double (&x)[R], double (&acc)[R],
-                                               const double* __restrict__ tab) {
-    lo = max(lo, 0);
-    hi = min(hi, n);
-    for (int k0 = (lo / kSumSlice) * kSumSlice; k0 < hi; k0 += kSumSlice) {
-        const int a = max(k0, lo), b = min(k0 + kSumSlice, hi);
-        double part[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) part[r] = 0.0;
-        lse_acc_run<R>(c + a, b - a, x, part, tab);
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] += part[r];
-    }
-}
-
 // A term of exp_scaled_acc is exactly +0.0 once u < -kZeroU: ldexp(p, e)
 // with p < 2 and e = floor(rint(u) / 4096) <= -1076 is below 2^-1075 and
 // rounds to 0.  (u = c' - z^2 with z = x' a' - m', so a component's term can

@@ -1482,54 +1482,94 @@ __global__ __launch_bounds__(kBlock) void k_pick_win(const P2* __restrict__ lohi
 // sums -- into plane 2 + c (0: below, 1: x) at the entry's place off[y] + e
 // of the compacted order; k_finish_rescore adds the chunks in order.
 // Per dense label (grid.x = label position), over its above records in
-// order: zhi[k] = max over j <= k of the largest x' where record j's fp64
-// term can be nonzero, zlo[k] = min over j >= k of the smallest (kZeroU);
-// +-inf for a record whose term is 0 everywhere.  For x' in [xa, xb] every
-// nonzero term lies in [first k with zhi[k] >= xa, first k with zlo[k] >
-// xb).  Thread t scans a contiguous segment; the segment totals are scanned
-// by thread 0 (once per posterior).
+// order.  A record's fp64 term can be nonzero only for x' in [lo, hi]
+// (zero_reach, kZeroU); "wide" records (half-width above 1.5x the clipped
+// sigma's: the prior and the sparse tails' components) are listed
+// (zwide[comp_a + j], count zn[label]); over the others zhi[k] = the
+// prefix max of hi, zlo[k] = the suffix min of lo (+-inf for wide records
+// and records that are 0 everywhere).  For x' in [xa, xb] every nonzero
+// term is a wide record or lies in [first k with zhi[k] >= xa, first k with
+// zlo[k] > xb).  Thread t scans a contiguous segment; thread 0 scans the
+// segment totals (once per posterior).
 __device__ __forceinline__ void zero_reach(const Comp<double>& c, double& lo, double& hi) {
     const double t = c.c + kZeroU;
-    if (!(t >= 0.0) || !(c.a > 0.0)) {   // never nonzero (or an unusable record: keep it always)
-        lo = t >= 0.0 ? -__builtin_inf() : __builtin_inf();
-        hi = t >= 0.0 ? __builtin_inf() : -__builtin_inf();
+    if (t < 0.0) {   // 0 everywhere
+        lo = __builtin_inf();
+        hi = -__builtin_inf();
         return;
     }
     const double mu = c.mu / c.a, w = sqrt(t) / c.a;
     const double slack = 1e-9 * (fabs(mu) + w + 1.0);
     lo = mu - w - slack;
     hi = mu + w + slack;
+    if (!(c.a > 0.0) || !(lo <= hi) || !(t >= 0.0)) {   // NaN / unusable: nonzero anywhere (a wide record)
+        lo = -__builtin_inf();
+        hi = __builtin_inf();
+    }
 }
 
 constexpr int kZwBlock = 1024;
 __global__ __launch_bounds__(kZwBlock) void k_zero_windows(const DLabel* __restrict__ labels,
                                                            const int32_t* __restrict__ group,
                                                            const Comp<double>* __restrict__ comps64,
-                                                           double* __restrict__ zhi, double* __restrict__ zlo) {
-    const DLabel L = labels[group[blockIdx.x]];
+                                                           double* __restrict__ zhi, double* __restrict__ zlo,
+                                                           int32_t* __restrict__ zwide, int32_t* __restrict__ zn) {
+    const int li = group[blockIdx.x];
+    const DLabel L = labels[li];
     const Comp<double>* c = comps64 + L.comp_a;
     double* ph = zhi + L.comp_a;
     double* pl = zlo + L.comp_a;
-    const int n = L.na, seg = (n + kZwBlock - 1) / kZwBlock;
-    const int k0 = min(n, (int)threadIdx.x * seg), k1 = min(n, k0 + seg);
+    int32_t* pw = zwide + L.comp_a;
+    const int n = L.na, seg = (n + kZwBlock - 1) / kZwBlock, tid = threadIdx.x;
+    const int k0 = min(n, tid * seg), k1 = min(n, k0 + seg);
     __shared__ double sh[kZwBlock], sl[kZwBlock];
+    __shared__ int32_t sw[kZwBlock];
+    __shared__ double wmax;
+    // the clipped sigma's half-width: the largest record scale a'
+    double am = 0.0;
+    for (int k = k0; k < k1; ++k) am = fmax(am, c[k].a);
+    sh[tid] = am;
+    __syncthreads();
+    if (tid == 0) {
+        double m = 0.0;
+        for (int t = 0; t < kZwBlock; ++t) m = fmax(m, sh[t]);
+        wmax = m > 0.0 ? 1.5 * sqrt(kZeroU) / m : __builtin_inf();
+    }
+    __syncthreads();
+    const double W = wmax;
+    auto reach = [&](int k, double& lo, double& hi) -> bool {   // true: wide
+        zero_reach(c[k], lo, hi);
+        const bool wide = hi - lo > 2.0 * W;   // (+inf - -inf: an unusable record is wide)
+        if (wide) {
+            lo = __builtin_inf();
+            hi = -__builtin_inf();
+        }
+        return wide;
+    };
     double mh = -__builtin_inf(), ml = __builtin_inf();
+    int nw = 0;
     for (int k = k0; k < k1; ++k) {
         double lo, hi;
-        zero_reach(c[k], lo, hi);
+        nw += reach(k, lo, hi) ? 1 : 0;
         mh = fmax(mh, hi);
         ml = fmin(ml, lo);
     }
-    sh[threadIdx.x] = mh;
-    sl[threadIdx.x] = ml;
+    sh[tid] = mh;
+    sl[tid] = ml;
+    sw[tid] = nw;
     __syncthreads();
-    if (threadIdx.x == 0) {   // exclusive prefix max / suffix min of the segments
+    if (tid == 0) {   // exclusive prefix max / suffix min / prefix sum of the segments
         double run = -__builtin_inf();
+        int cnt = 0;
         for (int t = 0; t < kZwBlock; ++t) {
             const double v = sh[t];
             sh[t] = run;
             run = fmax(run, v);
+            const int w = sw[t];
+            sw[t] = cnt;
+            cnt += w;
         }
+        zn[li] = cnt;
         run = __builtin_inf();
         for (int t = kZwBlock - 1; t >= 0; --t) {
             const double v = sl[t];
@@ -1538,19 +1578,57 @@ __global__ __launch_bounds__(kZwBlock) void k_zero_windows(const DLabel* __restr
         }
     }
     __syncthreads();
-    double run = sh[threadIdx.x];
+    double run = sh[tid];
+    int at = sw[tid];
     for (int k = k0; k < k1; ++k) {
         double lo, hi;
-        zero_reach(c[k], lo, hi);
+        if (reach(k, lo, hi)) pw[at++] = k;
         run = fmax(run, hi);
         ph[k] = run;
     }
-    run = sl[threadIdx.x];
+    run = sl[tid];
     for (int k = k1 - 1; k >= k0; --k) {
         double lo, hi;
-        zero_reach(c[k], lo, hi);
+        (void)reach(k, lo, hi);
         run = fmin(run, lo);
         pl[k] = run;
+    }
+}
+
+// lse_acc over components [k0, k1) of the label's above records c (slices
+// from k0, as lse_acc(c + k0, k1 - k0)) summing only the narrow window [wlo,
+// whi) and the wide records wide[0..nw) (sorted): every other term is
+// exactly +0.0 at the wave's candidates, and skipping +0.0 terms and slice
+// sums leaves every partial sum -- hence the result -- bit-identical.  All
+// bounds wave-uniform.
+template <int R>
+__device__ __forceinline__ void lse_acc_zero_window(const Comp<double>* __restrict__ c, int k0, int k1, int wlo,
+                                                    int whi, const int32_t* __restrict__ wide, int nw,
+                                                    const double (&x)[R], double (&acc)[R],
+                                                    const double* __restrict__ tab) {
+    int p = 0;   // first wide record >= k0
+    {
+        int lo = 0, hi = nw;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (wide[mid] < k0) lo = mid + 1; else hi = mid;
+        }
+        p = lo;
+    }
+    for (int s = k0; s < k1; s += kSumSlice) {
+        const int b = min(s + kSumSlice, k1);
+        const int ra = max(s, wlo), rb = min(b, whi);
+        const bool wide_here = p < nw && wide[p] < b;
+        if (ra >= rb && !wide_here) continue;   // the slice sums to +0.0
+        double part[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) part[r] = 0.0;
+        for (; p < nw && wide[p] < min(b, wlo); ++p) lse_acc_run<R>(c + wide[p], 1, x, part, tab);
+        if (ra < rb) lse_acc_run<R>(c + ra, rb - ra, x, part, tab);
+        for (; p < nw && wide[p] < min(b, whi); ++p) {}   // (inside the window: summed above)
+        for (; p < nw && wide[p] < b; ++p) lse_acc_run<R>(c + wide[p], 1, x, part, tab);
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] += part[r];
     }
 }
 
@@ -1572,7 +1650,8 @@ __global__ __launch_bounds__(kBlock) void k_rescore_packed(
     int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, int32_t chunk,
     const int32_t* __restrict__ cnt, const int64_t* __restrict__ list, int64_t cap,
     const RescoreChunk* __restrict__ chunks, const int64_t* __restrict__ off, int64_t total,
-    double* __restrict__ planes, const double* __restrict__ zhi, const double* __restrict__ zlo) {
+    double* __restrict__ planes, const double* __restrict__ zhi, const double* __restrict__ zlo,
+    const int32_t* __restrict__ zwide, const int32_t* __restrict__ zn) {
     const RescoreChunk ch = chunks[blockIdx.x];
     const int y = ch.cell, c = blockIdx.y;
     const DLabel L = labels[group[y]];
@@ -1623,7 +1702,8 @@ __global__ __launch_bounds__(kBlock) void k_rescore_packed(
         } else {
             const int wlo = __builtin_amdgcn_readfirstlane(first_above(zhi + L.comp_a, L.na, xa, false));
             const int whi = __builtin_amdgcn_readfirstlane(first_above(zlo + L.comp_a, L.na, xb, true));
-            lse_acc_window<R>(comps64 + L.comp_a + k0, k1 - k0, wlo - k0, whi - k0, xr, sa, exp_tab);
+            lse_acc_zero_window<R>(comps64 + L.comp_a, k0, k1, wlo, whi, zwide + L.comp_a, zn[group[y]], xr,
+                                   sa, exp_tab);
         }
     } else {
         lse_acc<R>(comps64 + L.comp_a + k0, k1 - k0, xr, sa, exp_tab);
@@ -2867,17 +2947,21 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
         if (ctx->zero_win && !P.zw_ready) {   // once per posterior
             HIPCHK(ctx, P.zw_hi.reserve(P.comps64.cap));
             HIPCHK(ctx, P.zw_lo.reserve(P.comps64.cap));
+            HIPCHK(ctx, P.zw_wide.reserve(P.comps64.cap));
+            HIPCHK(ctx, P.zw_n.reserve(std::max(P.n_labels, 1)));
             // every dense label of the posterior (the GMM1 and LGMM1 groups are adjacent)
             const int nd = (int)(P.h_group[DENSE_GMM].size() + P.h_group[DENSE_LGMM].size());
             hipLaunchKernelGGL(k_zero_windows, dim3((unsigned)nd), dim3(kZwBlock), 0, ctx->stream, P.labels.p,
-                               P.groups.p + P.group_off[DENSE_GMM], P.comps64.p, P.zw_hi.p, P.zw_lo.p);
+                               P.groups.p + P.group_off[DENSE_GMM], P.comps64.p, P.zw_hi.p, P.zw_lo.p,
+                               P.zw_wide.p, P.zw_n.p);
             P.zw_ready = true;
         }
         hipLaunchKernelGGL((k_rescore_packed<kRP>), dim3((unsigned)tab.size(), nch), dim3(kBlock), 0,
                            ctx->stream, ctx->P->labels.p, grp, ctx->P->comps64.p, ctx->P->samp.p,
                            a.cand_offset, a.seed, ctx->rounds.p, chunk, ctx->scr_cnt.p,
                            ctx->scr_list.p, cap, tabd, ctx->scr_off.p, total, ctx->scr_planes.p,
-                           ctx->zero_win ? P.zw_hi.p : nullptr, ctx->zero_win ? P.zw_lo.p : nullptr);
+                           ctx->zero_win ? P.zw_hi.p : nullptr, ctx->zero_win ? P.zw_lo.p : nullptr,
+                           P.zw_wide.p, P.zw_n.p);
         hipLaunchKernelGGL(k_finish_rescore, dim3((unsigned)tab.size()), dim3(kBlock), 0, ctx->stream,
                            ctx->P->labels.p, grp, ctx->P->comps64.p, a.cand_offset, nch, ctx->scr_cnt.p,
                            ctx->scr_list.p, cap, tabd, ctx->scr_off.p, total, ctx->scr_planes.p,
