@@ -2439,21 +2439,10 @@ __device__ __forceinline__ tpe_label_result to_result(const Partial& p, int li) 
 // workgroup per label streams up to 8192 partials at full memory parallelism
 // instead of one dependent 40-byte load chain per thread.
 constexpr int kReduceBlock = 1024;
-// whether label li's family is in TPE_OPT_MODES' mask (the others' result
-// rows keep what an earlier round of the same step wrote)
-__device__ __forceinline__ bool in_modes(const DLabel* __restrict__ labels, int li, int32_t mask) {
-    if (mask == 7) return true;
-    const int m = labels[li].mode;
-    const int fam = (m == DENSE_GMM || m == DENSE_LGMM) ? 1 : (m == CAT ? 4 : 2);
-    return (fam & mask) != 0;
-}
-
 __global__ __launch_bounds__(kReduceBlock) void k_reduce(const Partial* __restrict__ partials,
                                                          int32_t tiles, int32_t n_labels,
-                                                         tpe_label_result* __restrict__ out,
-                                                         const DLabel* __restrict__ labels, int32_t mask) {
+                                                         tpe_label_result* __restrict__ out) {
     const int li = blockIdx.x, rz = blockIdx.y, tid = threadIdx.x;
-    if (!in_modes(labels, li, mask)) return;   // uniform over the workgroup
     const Partial* p = partials + ((size_t)rz * n_labels + li) * tiles;
     uint64_t bk[4] = {0, 0, 0, 0};
     int64_t bi[4] = {INT64_MAX, INT64_MAX, INT64_MAX, INT64_MAX};
@@ -2537,10 +2526,9 @@ __global__ __launch_bounds__(kBlock) void k_fill_words(FillSet f) {
 // one partial per (round, label) -- packed and split-K maps: a thread each
 __global__ __launch_bounds__(kBlock) void k_emit(const Partial* __restrict__ partials, int64_t n,
                                                  int32_t n_labels,
-                                                 tpe_label_result* __restrict__ out,
-                                                 const DLabel* __restrict__ labels, int32_t mask) {
+                                                 tpe_label_result* __restrict__ out) {
     const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (j < n && in_modes(labels, (int)(j % n_labels), mask)) out[j] = to_result(partials[j], (int)(j % n_labels));
+    if (j < n) out[j] = to_result(partials[j], (int)(j % n_labels));
 }
 
 // argmax of below - above over caller arrays (tpe_broadcast_best)
@@ -3721,17 +3709,14 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     }
     HIPCHK(ctx, hipGetLastError());
     if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->ev1, ctx->stream));
-    // TPE_OPT_MODES: only the families this round ran write their result
-    // rows; the others keep the rows of the step's earlier round
-    const int32_t rmask = only_label >= 0 ? 7 : ctx->mode_mask;
     if (tiles == 1) {
         const int64_t nr = (int64_t)n_rounds * L;
         hipLaunchKernelGGL(k_emit, dim3((unsigned)((nr + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                           ctx->stream, ctx->partials.p, nr, L, ctx->results.p, ctx->P->labels.p, rmask);
+                           ctx->stream, ctx->partials.p, nr, L, ctx->results.p);
         HIPCHK(ctx, hipGetLastError());
     } else if (tiles > 1) {
         hipLaunchKernelGGL(k_reduce, dim3(L, n_rounds), dim3(kReduceBlock), 0, ctx->stream,
-                           ctx->partials.p, tiles, L, ctx->results.p, ctx->P->labels.p, rmask);
+                           ctx->partials.p, tiles, L, ctx->results.p);
         HIPCHK(ctx, hipGetLastError());
     }
     if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->ev2, ctx->stream));

@@ -278,9 +278,11 @@ def suggest(new_ids, domain, trials, seed,
     _, dense = _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior_weight,
                                    posterior_builder, n_candidates=n_EI_candidates, n_rounds=len(ids),
                                    dense_round=(lambda: run(1)) if pipelined else None)
-    # (pipelined: the dense labels' result rows stay on the device from the
-    # first round while the second writes the others')
-    res = run(7) if dense is None else run(6)
+    if dense is None:
+        res = run(7)
+    else:
+        res = run(6)
+        res[..., dense_mask] = dense[..., dense_mask]
     rval = []
     for j, new_id in enumerate(ids):
         values = {s.label: _labels.coerce(s.kind, res[j][i]['value'])

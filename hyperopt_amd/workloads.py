@@ -146,9 +146,7 @@ class FminLoop(object):
         build while a background thread computes numpy's tie orders, and the
         quantized and categorical labels' round on the ordered rebuild (the
         dense winners stand because the rebuild leaves those labels
-        bit-identical -- their result rows stay on the device while the
-        second round writes the others'; else the whole round runs again).
-        on_dense(eng) is
+        bit-identical; else the whole round runs again).  on_dense(eng) is
         called right after the dense round (its statistics); prepare=False:
         no index ahead of the round, no pipelining (fp32 rounds).  Returns
         the results of every label, as one round."""
@@ -179,7 +177,9 @@ class FminLoop(object):
             self.pipelined = False
             return run(7)
         self.pipelined = True
-        return run(6)   # (the dense labels' rows are the first round's, kept on the device)
+        res = run(6)
+        res[..., self.dense_mask] = dense[..., self.dense_mask]
+        return res
 
     pipelined = False   # whether the last suggest ran in two parts
 

@@ -436,10 +436,9 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *                   and divides HOT_DIV by 4 for the next rounds        [16]
  *   TPE_OPT_MODES   the label families a round runs, a mask: 1 dense
  *                   (GMM1 / LGMM1 without q), 2 quantized, 4 categorical;
- *                   the other labels' result rows are not written: they
- *                   keep the previous round's (fmin's step runs the dense
- *                   labels while the host computes the tie orders, then the
- *                   rest on the ordered rebuild, and reads all rows)      [7]
+ *                   the other labels' result rows are undefined (fmin's
+ *                   step runs the dense labels while the host computes the
+ *                   tie orders, then the rest on the ordered rebuild)    [7]
  *   TPE_OPT_ZERO_WIN  the packed map's fp64 re-score sums only the above
  *                   components whose terms can be nonzero at the wave's
  *                   candidates (the others are exactly +0.0: the same
