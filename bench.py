@@ -340,42 +340,26 @@ def main():
         loop.advance(eng, args.trials)        # untimed: the initial history, uploaded whole
     results = {}
 
-    def capture(e):
-        """The statistics of e's last round call."""
-        return (e.last_mode_stats(), e.last_screen(with_ms=True), e.last_screen_terms(),
-                e.last_rescore_terms(), e.last_hot())
-
-    dense_caps = []   # a pipelined step's dense-round statistics (FminLoop.suggest)
-
     def step(i, fresh, n=None, e=None, lp=None, gather=True):
         """One step; n: the candidates per label of this rank's candidate
         shard (default C) -- the candidate-shard projection runs one eighth
         of a round; e, lp: another engine and loop (the label-shard
-        projection).  A fresh step is FminLoop.suggest: advance the history
-        and rebuild, then the round (pipelined: the dense labels' round
-        while the host computes the tie orders)."""
+        projection)."""
         e = eng if e is None else e
         lp = loop if lp is None else lp
         nc = C if n is None else n
-        del dense_caps[:]
+        if fresh:
+            lp.advance(e, args.trials + (i + 1) * args.append,
+                       n_candidates=nc if args.precision == 'f64' else 0,
+                       n_rounds=ids_local if args.config == 5 else 1)
         if args.config == 5:   # independent new_ids split over the GPUs (or each rank's labels)
             first_id = i * args.new_ids + (0 if by_label else rank * ids_local)
-            ids = list(range(first_id, first_id + ids_local))
-            if fresh:
-                res = lp.suggest(e, args.trials + (i + 1) * args.append, 1234, C, rounds=ids,
-                                 on_dense=lambda ee: dense_caps.append(capture(ee)))
-            else:
-                res = e.suggest_batch(seed=1234, rounds=ids, n_candidates=C)
+            res = e.suggest_batch(seed=1234, rounds=list(range(first_id, first_id + ids_local)),
+                                  n_candidates=C)
             if dist is not None and gather:   # every rank ends with every new_id's winners
                 res = gather_labels(res, shards, rank) if by_label else gather_rounds(res)
             return res
-        off = 0 if by_label else rank * nc
-        if fresh:
-            res = lp.suggest(e, args.trials + (i + 1) * args.append, 1234 + i, nc, round=i, cand_offset=off,
-                             on_dense=lambda ee: dense_caps.append(capture(ee)),
-                             prepare=args.precision == 'f64')
-        else:
-            res = e.suggest(seed=1234 + i, n_candidates=nc, round=i, cand_offset=off)
+        res = e.suggest(seed=1234 + i, n_candidates=nc, round=i, cand_offset=0 if by_label else rank * nc)
         if dist is not None and gather:   # exchange per-GPU winners (L x 48 B) over RCCL
             res = gather_labels(res, shards, rank) if by_label else exchange_winners(res)
         return res
@@ -393,17 +377,18 @@ def main():
             res = step(first + i, fresh, n)
             if keep:
                 results[first + i] = res
-            for modes, (a, b, ms), terms, rterms, (hl, hf) in [capture(eng)] + list(dense_caps):
-                for k, (kms, ev) in modes.items():
-                    mode_ms[k] = mode_ms.get(k, 0.0) + kms
-                    mode_ev[k] = mode_ev.get(k, 0) + ev
-                scr[0] += a
-                scr[1] += b
-                scr[2] += ms
-                scr[3] += terms
-                scr[4] += rterms
-                scr[5] += max(hl, 0)
-                scr[6] += hf
+            for k, (ms, ev) in eng.last_mode_stats().items():
+                mode_ms[k] = mode_ms.get(k, 0.0) + ms
+                mode_ev[k] = mode_ev.get(k, 0) + ev
+            a, b, ms = eng.last_screen(with_ms=True)
+            scr[0] += a
+            scr[1] += b
+            scr[2] += ms
+            scr[3] += eng.last_screen_terms()
+            scr[4] += eng.last_rescore_terms()
+            hl, hf = eng.last_hot()
+            scr[5] += max(hl, 0)
+            scr[6] += hf
             if fresh:
                 scr[7] += eng.last_prepare_ms()
         torch.cuda.synchronize()

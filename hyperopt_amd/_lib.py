@@ -51,7 +51,6 @@ TPE_OPT_HOT = 12
 TPE_OPT_EARLY = 13
 TPE_OPT_HOT_DIV = 14
 TPE_OPT_ZERO_WIN = 15
-TPE_OPT_MODES = 16
 
 TPE_OBS_IDENTITY = 0
 TPE_OBS_LOG = 1
@@ -131,7 +130,6 @@ SIGNATURES = {
     'tpe_last_rescore_terms': (ctypes.c_int, [_P, _P]),
     'tpe_last_drawn': (ctypes.c_int, [_P, _P, _P]),
     'tpe_device_bytes': (ctypes.c_int64, []),
-    'tpe_last_build_kept_index': (ctypes.c_int, [_P, _P]),
     'tpe_prepare': (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int32]),
     'tpe_last_screen_mode': (ctypes.c_int32, [_P]),
     'tpe_last_hot': (ctypes.c_int, [_P, _P, _P]),

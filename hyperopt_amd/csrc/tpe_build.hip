@@ -1453,7 +1453,6 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     // a second build of the same history that only supplies the tie order
     // of quantized labels)
     P.bx_ready = tpe_rt::bx_keep_after(ctx, groups_changed);
-    ctx->build_kept_index = P.bx_ready;
     P.n_labels = n_labels;
     B.n_labels = n_labels;
     B.mix_h = mix;

@@ -373,8 +373,6 @@ struct tpe_ctx {
     int32_t hot = 1;                     // 0 off, 1 on, 2 test: force the fallback
     bool early = true;                   // early exit of quantized / categorical tile rounds
     bool zero_win = true;                // packed re-score skips the exactly-zero above terms
-    int32_t mode_mask = 7;               // label families a round runs: 1 dense, 2 quantized, 4 categorical
-    bool build_kept_index = false;       // the last build left the indexed dense labels bit-identical
     double hot_cap_div = 16.0;           // hot lists hold n / hot_cap_div per cell (shrinks on overflow)
     DevBuf<double> hot_x;                // per cell: listed candidates' x
     DevBuf<int32_t> hot_i, hot_cnt;      //   their indices; per cell the count

@@ -3631,11 +3631,6 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         ctx->mode_ms[m] = 0.f;
         ctx->mode_evals[m] = 0;
     }
-    if (ctx->mode_mask != 7 && only_label < 0) {   // TPE_OPT_MODES: some families only
-        if (!(ctx->mode_mask & 1)) g.count[DENSE_GMM] = g.count[DENSE_LGMM] = 0;
-        if (!(ctx->mode_mask & 2)) g.count[QUANT_GMM] = g.count[QUANT_LGMM] = 0;
-        if (!(ctx->mode_mask & 4)) g.count[CAT] = 0;
-    }
     if (only_label >= 0) {  // tpe_score: launch the one label's mode only
         HIPCHK(ctx, ctx->one_group.reserve(1));
         HIPCHK(ctx, hipMemcpyAsync(ctx->one_group.p, &only_label, sizeof(int32_t),
@@ -4293,12 +4288,6 @@ int tpe_last_drawn(const tpe_ctx* ctx, int64_t* quantized, int64_t* categorical)
     return TPE_OK;
 }
 
-int tpe_last_build_kept_index(const tpe_ctx* ctx, int32_t* kept) {
-    if (!ctx || !kept) return TPE_ERR_ARG;
-    *kept = ctx->build_kept_index ? 1 : 0;
-    return TPE_OK;
-}
-
 int64_t tpe_device_bytes(void) { return tpe_rt::device_bytes_held().load(std::memory_order_relaxed); }
 
 int tpe_last_rescore_terms(const tpe_ctx* ctx, int64_t* terms) {
@@ -4336,10 +4325,6 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
         case TPE_OPT_EXPAND: ctx->expand = value != 0; break;
         case TPE_OPT_EARLY: ctx->early = value != 0; break;
         case TPE_OPT_ZERO_WIN: ctx->zero_win = value != 0; break;
-        case TPE_OPT_MODES:
-            if (value < 1 || value > 7) return ctx->fail(TPE_ERR_ARG, "modes must be a mask in [1, 7]");
-            ctx->mode_mask = (int32_t)value;
-            break;
         case TPE_OPT_HOT_DIV:
             if (value < 1 || value > (1 << 20)) return ctx->fail(TPE_ERR_ARG, "hot list divisor must be in [1, 2^20]");
             ctx->hot_cap_div = (double)value;

@@ -146,7 +146,7 @@ class Engine(object):
             self.history_reset(specs, cat_p)
             self.history_append(np.diff(obs_off), obs_trial, obs_val)
             n_valid = int(np.count_nonzero(losses == losses))
-            nb, self.tie_labels, _ = _post.build_reference_order(
+            nb, self.tie_labels = _post.build_reference_order(
                 self, losses, n_valid, gamma, prior_weight, lf, _post._ObsOf(obs_off, obs_trial, obs_val))
             return nb
         if tie_order != 'position':
@@ -312,13 +312,6 @@ class Engine(object):
         self._check(self.lib.tpe_last_prepare(self.h, ctypes.byref(ms)))
         return ms.value
 
-    def last_build_kept_index(self):
-        """True when the last posterior build left the indexed dense labels
-        bit-identical (tpe_last_build_kept_index)."""
-        k = ctypes.c_int32()
-        self._check(self.lib.tpe_last_build_kept_index(self.h, ctypes.byref(k)))
-        return bool(k.value)
-
     def device_bytes(self):
         """Device memory the library holds (every context of the process),
         bytes: the high-water mark of its buffers (tpe_device_bytes)."""
@@ -344,7 +337,7 @@ class Engine(object):
                'window': L.TPE_OPT_WINDOW, 'win_t': L.TPE_OPT_WIN_T,
                'win_groups': L.TPE_OPT_WIN_GROUPS, 'expand': L.TPE_OPT_EXPAND,
                'hot': L.TPE_OPT_HOT, 'early': L.TPE_OPT_EARLY, 'hot_div': L.TPE_OPT_HOT_DIV,
-               'zero_win': L.TPE_OPT_ZERO_WIN, 'modes': L.TPE_OPT_MODES}
+               'zero_win': L.TPE_OPT_ZERO_WIN}
 
     def set_option(self, name, value):
         """Engine switches (include/hyperopt_tpe.h TPE_OPT_*): 'screen',

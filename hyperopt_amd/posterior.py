@@ -307,10 +307,6 @@ def reference_orders(losses, n_below, obs_of, labels):
     return below, off, order
 
 
-# kinds whose posterior is a dense (unquantized) GMM1 / LGMM1 mixture: the
-# labels of the expansion index and of TPE_OPT_MODES bit 1
-DENSE_KINDS = ('uniform', 'loguniform', 'normal', 'lognormal')
-
 _POOL_MIN = 1 << 14   # observations to sort (over several labels), from which the pool pays
 _pool = None
 
@@ -320,29 +316,12 @@ def _sort_pool():
     if _pool is None:
         import os
         from concurrent.futures import ThreadPoolExecutor
-        try:   # the CPUs this process may run on (a GPU box's share), at most 16
-            ncpu = len(os.sched_getaffinity(0))
-        except (AttributeError, OSError):
-            ncpu = os.cpu_count() or 2
-        _pool = ThreadPoolExecutor(max_workers=max(1, min(16, ncpu)))
+        _pool = ThreadPoolExecutor(max_workers=max(1, min(8, (os.cpu_count() or 2) // 2)))
     return _pool
 
 
-_bg = None
-
-
-def _bg_pool():
-    """One background thread for the tie orders of a pipelined fmin step
-    (its argsorts may fan out over _sort_pool)."""
-    global _bg
-    if _bg is None:
-        from concurrent.futures import ThreadPoolExecutor
-        _bg = ThreadPoolExecutor(max_workers=1)
-    return _bg
-
-
 def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of, known=(), prepare=None,
-                          overlap=True, dense_round=None):
+                          overlap=True):
     """Device build whose mixtures follow the reference's tie order
     (tpe.py:433, 637): the device reports which mixtures depend on the order
     of tied observations (or a tie of losses at the split), and only for
@@ -360,29 +339,15 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
       (continuous values carry no ties), so the device keeps the index;
       with overlap=False (few labels use the index: it is shorter than the
       second build it saves) the `known` orders go up front as above and the
-      index is queued after the one build;
-    * dense_round (with prepare and overlap): a callable that runs the round
-      of the dense labels only (TPE_OPT_MODES) on the first build -- while it
-      runs on the device, a background thread computes the orders; the
-      ordered rebuild follows.  Its result stands when the rebuild left the
-      indexed dense labels bit-identical (tpe_last_build_kept_index) or no
-      rebuild was needed; else it is dropped (None).
+      index is queued after the one build.
 
-    Returns (n_below, the labels that needed an order, the dense round's
-    result or None)."""
+    Returns (n_below, the labels that needed an order)."""
     n_below = n_below_of(n_valid, gamma, lf)
     known = set(known)
-    dense = None
-    fut = None
     if prepare and (overlap or not known):
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf)
         eng.prepare(*prepare)
         have = set()
-        if dense_round is not None and not np.any(ties[:-1] & 1):
-            early = frozenset(known | set(np.flatnonzero(ties[:-1] & 2).tolist()))
-            if early or ties[-1]:
-                fut = (early, _bg_pool().submit(reference_orders, losses, n_below, obs_of, early))
-            dense = dense_round()
     elif known:
         below, off, order = reference_orders(losses, n_below, obs_of, known)
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf, below, off, order)
@@ -397,13 +362,8 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
         # weights are all equal, so its order can never matter
         raise AssertionError('below mixture depends on a tie order (n_below > lf?)')
     need = have | set(np.flatnonzero(ties[:-1] & 2).tolist())
-    if fut is not None:
-        got = fut[1].result()
-        if fut[0] != need:   # (the set was computed from the same build's flags: equal unless `known` adds)
-            need = set(fut[0])
     if need != have or ties[-1]:
-        below, off, order = (got if fut is not None and fut[0] == frozenset(need)
-                             else reference_orders(losses, n_below, obs_of, need))
+        below, off, order = reference_orders(losses, n_below, obs_of, need)
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf, below, off, order)
         if np.any(ties[:-1]):
             # a supplied below set can move observations between the sets,
@@ -413,9 +373,7 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
             nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf, below, off,
                                                    order)
             assert not np.any(ties[:-1])
-        if dense is not None and not eng.last_build_kept_index():
-            dense = None   # the dense labels changed (a tie across the split, tied dense values)
-    return nb, frozenset(need), dense
+    return nb, frozenset(need)
 
 
 class _ObsOf(object):
@@ -456,7 +414,7 @@ class DeviceHistoryUploader(object):
         self.owner = None
 
     def build(self, eng, labels, view, gamma, prior_weight, lf=DEFAULT_LF, prepare=None, streams=None,
-              overlap=True, dense_round=None):
+              overlap=True):
         tids, losses, n_valid, cols, owner = view
         key = (tuple((n, k) for n, k, _ in labels) + (tuple(streams) if streams is not None else (),),
                eng.history_generation)
@@ -502,10 +460,9 @@ class DeviceHistoryUploader(object):
         self.owner = weakref.ref(owner)
         self.n_trials = len(tids)
         self.last_tid = tids[-1] if len(tids) else None
-        nb, self.tie_labels, self.dense = build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf,
-                                                                self._obs_of(len(labels)), self.tie_labels,
-                                                                prepare=prepare, overlap=overlap,
-                                                                dense_round=dense_round)
+        nb, self.tie_labels = build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf,
+                                                    self._obs_of(len(labels)), self.tie_labels,
+                                                    prepare=prepare, overlap=overlap)
         return nb
 
     def _obs_of(self, n_labels):
@@ -520,7 +477,6 @@ class DeviceHistoryUploader(object):
         return obs_of
 
     prev_counts = ()
-    dense = None       # the pipelined dense round's result of the last build (or None)
     pos_parts = val_parts = ()
     tie_labels = frozenset()
     n_trials = 0

@@ -134,18 +134,13 @@ class _PendingView(object):
 
 
 PREPARE_MIN = 8192   # candidate slots of a round from which it uses the expansion index
-PIPELINE_MIN_DENSE = 8   # dense labels from which a large round is pipelined with the tie orders
 
 
 def _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior_weight,
-                        builder, n_candidates=0, n_rounds=1, dense_round=None):
+                        builder, n_candidates=0, n_rounds=1):
     """Put the posterior of the current history on the engine, from the
     device-resident history's `view` or the general gather (tids, losses,
-    obs); returns (the number of trial documents it was built from, the
-    result of `dense_round` -- the dense labels' round, run on the first,
-    order-free device build while the host computes numpy's tie orders
-    (posterior.build_reference_order) -- or None when it did not run or
-    does not stand)."""
+    obs); returns the number of trial documents it was built from."""
     labels = list(specs)
     if view is not None:
         n_docs = view[2]
@@ -164,12 +159,11 @@ def _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior
                     up = eng._history_uploader = _post.DeviceHistoryUploader()
                 up.build(eng, [(s.label, s.kind, s.args) for s in specs.values()], view, gamma,
                          prior_weight, prepare=((n_candidates, n_rounds)
-                                                if n_candidates * n_rounds >= PREPARE_MIN else None),
-                         dense_round=dense_round)
-                return n_docs, up.dense
-            eng.build_posterior(*device_inputs(specs, tids, losses, obs), gamma=gamma,
-                                prior_weight=prior_weight)
-            return n_docs, None
+                                                if n_candidates * n_rounds >= PREPARE_MIN else None))
+            else:
+                eng.build_posterior(*device_inputs(specs, tids, losses, obs), gamma=gamma,
+                                    prior_weight=prior_weight)
+            return n_docs
         except _post.NonFiniteObservation:
             # NaN observations: the host build raises what the reference's
             # adaptive_parzen_normal raises (tpe.py:469)
@@ -183,7 +177,7 @@ def _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior
         b, a = splitter.split(*obs[label])
         posts.append(_post.label_posterior(label, sp.kind, sp.args, b, a, prior_weight))
     eng.set_posterior(*_post.pack(posts))
-    return n_docs, None
+    return n_docs
 
 
 def suggest(new_ids, domain, trials, seed,
@@ -259,30 +253,12 @@ def suggest(new_ids, domain, trials, seed,
         logger.info('TPE using 0 trials')                     # the prior-only posterior
     eng = _engine.get_engine(list(devices) if devices else device, 'f64')
     ids = list(new_ids) if batch else [new_ids[0]]
-
-    def run(modes):
-        if modes != 7:
-            eng.set_option('modes', modes)
-        try:
-            if len(ids) == 1:
-                return eng.suggest(seed, n_EI_candidates, round=ids[0])[None]
-            return eng.suggest_batch(seed, ids, n_EI_candidates)
-        finally:
-            if modes != 7:
-                eng.set_option('modes', 7)
-    # large rounds with many dense labels: the dense labels' round runs while
-    # the host computes the tie orders of the others (FminLoop.suggest)
-    dense_mask = np.array([s.kind in _post.DENSE_KINDS for s in specs.values()])
-    pipelined = (n_EI_candidates * len(ids) >= PREPARE_MIN and
-                 PIPELINE_MIN_DENSE <= int(dense_mask.sum()) < len(dense_mask))
-    _, dense = _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior_weight,
-                                   posterior_builder, n_candidates=n_EI_candidates, n_rounds=len(ids),
-                                   dense_round=(lambda: run(1)) if pipelined else None)
-    if dense is None:
-        res = run(7)
+    _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior_weight,
+                        posterior_builder, n_candidates=n_EI_candidates, n_rounds=len(ids))
+    if len(ids) == 1:
+        res = eng.suggest(seed, n_EI_candidates, round=ids[0])[None]
     else:
-        res = run(6)
-        res[..., dense_mask] = dense[..., dense_mask]
+        res = eng.suggest_batch(seed, ids, n_EI_candidates)
     rval = []
     for j, new_id in enumerate(ids):
         values = {s.label: _labels.coerce(s.kind, res[j][i]['value'])

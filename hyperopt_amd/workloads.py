@@ -8,7 +8,7 @@ from . import posterior as P
 
 PREPARE_MIN = 8192   # candidate slots of a round from which it uses the expansion index
 OVERLAP_MIN_DENSE = 8   # index labels from which the index runs beside the host's tie orders
-DENSE_KINDS = P.DENSE_KINDS
+DENSE_KINDS = ('uniform', 'loguniform', 'normal', 'lognormal')
 
 # config-3 kind cycle: kind = i mod 5
 CYCLE = (('uniform', dict(low=-5.0, high=5.0)),
@@ -122,8 +122,7 @@ class FminLoop(object):
         self.labels = [hist.labels[i] for i in self.label_ids]
         self.streams = None if label_ids is None else self.label_ids
         self.names = [n for n, _, _ in self.labels]
-        self.dense_mask = np.array([k in DENSE_KINDS for _, k, _ in self.labels])
-        self.n_dense = int(self.dense_mask.sum())
+        self.n_dense = sum(1 for _, k, _ in self.labels if k in DENSE_KINDS)
         self.uploader = P.DeviceHistoryUploader()
         self.n = 0
 
@@ -136,54 +135,7 @@ class FminLoop(object):
         losses = self.hist.losses[:n]
         return (self.hist.tids[:n], losses, int(np.count_nonzero(losses == losses)), obs, self)
 
-    def suggest(self, eng, n, seed, n_candidates, round=0, rounds=None, cand_offset=0, on_dense=None,
-                prepare=True):
-        """advance(eng, n, ...) and the round(s) on the new posterior:
-        eng.suggest(seed, n_candidates, round=round), or eng.suggest_batch(
-        seed, rounds, n_candidates) when `rounds` is given.  With the
-        expansion index in use and enough dense labels the step is
-        pipelined: the dense labels' round runs on the first, order-free
-        build while a background thread computes numpy's tie orders, and the
-        quantized and categorical labels' round on the ordered rebuild (the
-        dense winners stand because the rebuild leaves those labels
-        bit-identical; else the whole round runs again).  on_dense(eng) is
-        called right after the dense round (its statistics); prepare=False:
-        no index ahead of the round, no pipelining (fp32 rounds).  Returns
-        the results of every label, as one round."""
-        batch = rounds is not None
-        n_rounds = len(rounds) if batch else 1
-
-        def run(modes):
-            if modes != 7:
-                eng.set_option('modes', modes)
-            try:
-                return (eng.suggest_batch(seed, rounds, n_candidates) if batch
-                        else eng.suggest(seed, n_candidates, round=round, cand_offset=cand_offset))
-            finally:
-                if modes != 7:
-                    eng.set_option('modes', 7)
-
-        def dense_round():
-            res = run(1)
-            if on_dense is not None:
-                on_dense(eng)
-            return res
-        pipelined = (prepare and 0 < self.n_dense < len(self.labels) and self.n_dense >= OVERLAP_MIN_DENSE
-                     and n_candidates * n_rounds >= PREPARE_MIN)
-        self.advance(eng, n, n_candidates if prepare else 0, n_rounds,
-                     dense_round=dense_round if pipelined else None)
-        dense = self.uploader.dense if pipelined else None
-        if dense is None:
-            self.pipelined = False
-            return run(7)
-        self.pipelined = True
-        res = run(6)
-        res[..., self.dense_mask] = dense[..., self.dense_mask]
-        return res
-
-    pipelined = False   # whether the last suggest ran in two parts
-
-    def advance(self, eng, n, n_candidates=0, n_rounds=1, dense_round=None):
+    def advance(self, eng, n, n_candidates=0, n_rounds=1):
         """History of the first n trials on the device, posterior rebuilt
         (its expansion index queued meanwhile when the coming round(s) of
         n_candidates per label will use it, as tpe.suggest does); returns
@@ -194,8 +146,7 @@ class FminLoop(object):
         return self.uploader.build(eng, self.labels, self.view(n), self.gamma, self.prior_weight,
                                    prepare=((n_candidates, n_rounds)
                                             if n_candidates * n_rounds >= PREPARE_MIN else None),
-                                   streams=self.streams, overlap=self.n_dense >= OVERLAP_MIN_DENSE,
-                                   dense_round=dense_round)
+                                   streams=self.streams, overlap=self.n_dense >= OVERLAP_MIN_DENSE)
 
 
 def mixed_space(n_labels):

@@ -353,12 +353,6 @@ int tpe_last_rescore_terms(const tpe_ctx *ctx, int64_t *terms);
  * drawn).  The categorical evals in tpe_last_mode_stats count these. */
 int tpe_last_drawn(const tpe_ctx *ctx, int64_t *quantized, int64_t *categorical);
 
-/* 1 when the last posterior build left every dense label the expansion
- * index was built from bit-identical (records, sampling records, DLabel:
- * the index was kept) -- so a round run on the previous build gave those
- * labels the winners this build would; 0 otherwise (or no index). */
-int tpe_last_build_kept_index(const tpe_ctx *ctx, int32_t *kept);
-
 /* Device memory the library holds right now, over every context of the
  * process (posteriors, resident histories, expansion indexes, round
  * buffers; the HIP runtime's own allocations not included), in bytes.
@@ -434,11 +428,6 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *                   candidates per (round, label) (at least 4096); a round
  *                   whose list overflows screens every candidate instead
  *                   and divides HOT_DIV by 4 for the next rounds        [16]
- *   TPE_OPT_MODES   the label families a round runs, a mask: 1 dense
- *                   (GMM1 / LGMM1 without q), 2 quantized, 4 categorical;
- *                   the other labels' result rows are undefined (fmin's
- *                   step runs the dense labels while the host computes the
- *                   tie orders, then the rest on the ordered rebuild)    [7]
  *   TPE_OPT_ZERO_WIN  the packed map's fp64 re-score sums only the above
  *                   components whose terms can be nonzero at the wave's
  *                   candidates (the others are exactly +0.0: the same
@@ -471,7 +460,6 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_EARLY 13
 #define TPE_OPT_HOT_DIV 14
 #define TPE_OPT_ZERO_WIN 15
-#define TPE_OPT_MODES 16
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
 
 /* Build now what the resident posterior's first round(s) of n_candidates
