@@ -316,7 +316,11 @@ def _sort_pool():
     if _pool is None:
         import os
         from concurrent.futures import ThreadPoolExecutor
-        _pool = ThreadPoolExecutor(max_workers=max(1, min(8, (os.cpu_count() or 2) // 2)))
+        try:   # the CPUs this process may run on (a GPU box's share), at most 16
+            ncpu = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            ncpu = os.cpu_count() or 2
+        _pool = ThreadPoolExecutor(max_workers=max(1, min(16, ncpu)))
     return _pool
 
 
