@@ -65,7 +65,7 @@ def build_engine(force=False, verbose=True):
     gfx950 code object), then link the shared library."""
     import tempfile
     want = source_hash()
-    if not force and built_hash() == want:
+    if not force and built_hash(TARGET) == want:
         return TARGET
     flags = FLAGS + ['-DTPE_SOURCE_HASH="%s"' % want]
     with tempfile.TemporaryDirectory(prefix='tpe_build_') as tmp:
@@ -84,7 +84,7 @@ def build_engine(force=False, verbose=True):
         if verbose:
             print(' '.join(cmd), flush=True)
         subprocess.check_call(cmd)
-    got = built_hash()
+    got = built_hash(TARGET)
     if got != want:
         raise RuntimeError('built library carries hash %r, expected %r' % (got, want))
     return TARGET

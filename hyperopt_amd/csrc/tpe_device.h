@@ -410,19 +410,23 @@ __device__ __forceinline__ bool sample_slots(const DLabel& L, const Src& src, ui
 // wave-wide queue iteration (the same draws, bit for bit).  Slot r of
 // thread t holds candidate g0 + tile_cand(r, t, blockDim): slots r, r + 1 are
 // a Box-Muller pair, drawn by one Philox call (draw_pair) when g0 is even.
-template <int R>
+// The accepted values come back through CAP entries at a time (the
+// rejected slots of one tile are a few per cent of R * 256 with bounded
+// labels: one pass; more take several, each retrying the next CAP entries).
+// A smaller value array leaves LDS for more workgroups per CU.
+template <int R, int CAP = R * 256>
 struct RetryLds {
     int n[2];                 // per tile parity: this tile's count, the next tile's (reset)
     uint16_t slot[R * 256];   // candidate offset within the tile
-    double val[R * 256];
+    double val[CAP];
 };
 
 // (every thread of the workgroup calls it; q.n[0] = q.n[1] = 0 before the
 // first tile, a barrier in between; `par` alternates 0, 1 over the tiles:
 // two barriers per tile)
-template <int MODE, int R, typename Src, bool RAW = false>
+template <int MODE, int R, typename Src, bool RAW = false, int CAP = R * 256>
 __device__ __forceinline__ bool sample_tile(const DLabel& L, const Src& src, uint64_t seed, uint32_t rk,
-                                            uint32_t g0, uint32_t pend, double (&out)[R], RetryLds<R>& q,
+                                            uint32_t g0, uint32_t pend, double (&out)[R], RetryLds<R, CAP>& q,
                                             int par) {
     static_assert(MODE != CAT, "categorical slots draw once each");
     static_assert(R * 256 <= 65536, "tile offsets are 16-bit");
@@ -464,23 +468,30 @@ __device__ __forceinline__ bool sample_tile(const DLabel& L, const Src& src, uin
     const int n = q.n[par];
     if (threadIdx.x == 0) q.n[par ^ 1] = 0;   // (its last reader finished before the previous tile's end)
     bool ok = true;
-    for (int e = threadIdx.x; e < n; e += blockDim.x) {
-        const uint32_t gg = g0 + (uint32_t)q.slot[e];
-        double v = __builtin_nan("");
-        for (uint32_t it = 1; it < kMaxAttempts; ++it) {
-            const double draw = draw_attempt(L, src, k0, k1, gg, it, rk);
-            if (L.low <= draw && draw < L.high) {
-                v = draw;
-                break;
+    // (n is the workgroup's: uniform.  At least one barrier follows thread
+    // 0's reset of the next tile's counter before any thread moves on.)
+    if (n == 0) __syncthreads();
+    for (int c0 = 0; c0 < n; c0 += CAP) {
+        const int c1 = min(n, c0 + CAP);
+        for (int e = c0 + (int)threadIdx.x; e < c1; e += blockDim.x) {
+            const uint32_t gg = g0 + (uint32_t)q.slot[e];
+            double v = __builtin_nan("");
+            for (uint32_t it = 1; it < kMaxAttempts; ++it) {
+                const double draw = draw_attempt(L, src, k0, k1, gg, it, rk);
+                if (L.low <= draw && draw < L.high) {
+                    v = draw;
+                    break;
+                }
             }
+            ok = ok && v == v;
+            q.val[e - c0] = v;
         }
-        ok = ok && v == v;
-        q.val[e] = v;
-    }
-    __syncthreads();
+        __syncthreads();
 #pragma unroll
-    for (int r = 0; r < R; ++r)
-        if (pos[r] >= 0) out[r] = q.val[pos[r]];
+        for (int r = 0; r < R; ++r)
+            if (pos[r] >= c0 && pos[r] < c1) out[r] = q.val[pos[r] - c0];
+        if (c1 < n) __syncthreads();   // (the next pass reuses val)
+    }
     if constexpr ((MODE == DENSE_LGMM || MODE == QUANT_LGMM) && !RAW) {
 #pragma unroll
         for (int r = 0; r < R; ++r)

@@ -818,9 +818,10 @@ __global__ __launch_bounds__(kBlock) void k_hot_bits(const int32_t* __restrict__
 // gather in an LDS buffer (one LDS atomic per wave and slot pair, no
 // barrier) and go to the cell's list with one global atomic per workgroup
 // at the end; past the buffer a wave appends straight to the list.
-constexpr int kHotBuf = 1024;
+constexpr int kHotBuf = 256;
+constexpr int kHotRetry = 512;   // rejected draws retried cooperatively per tile (the rest in-thread)
 template <int R>
-__global__ __launch_bounds__(kBlock, 4) void k_hot_bx(
+__global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
     const BxLabel* __restrict__ bx, const uint32_t* __restrict__ hbits, int64_t n, int64_t cand_offset,
     uint64_t seed, const uint32_t* __restrict__ rounds, int32_t nl, int32_t* __restrict__ hcnt,
@@ -840,7 +841,7 @@ __global__ __launch_bounds__(kBlock, 4) void k_hot_bx(
     const bool lds_bits = nsb <= kHotLdsWords * 32;
     if (lds_bits)
         for (int w = threadIdx.x; w < (nsb >> 5); w += kBlock) sbits[w] = hbits[(B.sb_off >> 5) + w];
-    __shared__ RetryLds<R> retry;
+    __shared__ RetryLds<R, kHotRetry> retry;
     __shared__ int32_t buf_i[kHotBuf];
     __shared__ double buf_x[kHotBuf];
     __shared__ int buf_n, gbase;
@@ -854,20 +855,19 @@ __global__ __launch_bounds__(kBlock, 4) void k_hot_bx(
     int par = 0;
     for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per, par ^= 1) {
         double x[R];
-        int64_t ci[R];
         uint32_t pend = 0;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            ci[r] = base + tile_cand(r, threadIdx.x, kBlock);
+        for (int r = 0; r < R; ++r) {   // (candidate indices recomputed where listed: fewer live registers)
             x[r] = 0.0;
-            if (ci[r] < n) pend |= 1u << r;
+            if (base + (int64_t)tile_cand(r, threadIdx.x, kBlock) < n) pend |= 1u << r;
         }
         // raw draws: an LGMM1 label's x' is log(exp(draw)) - centre, within a
         // few ulp of draw - centre (the sub-bins' slack covers it); the list
         // keeps the draw and k_screen_hot applies the exp.  (The family only
         // changes that exp, which RAW leaves out: one instantiation.)
         const uint32_t g0 = (uint32_t)(cand_offset + base);
-        if (!sample_tile<DENSE_GMM, R, SampShared, true>(L, SampShared{&sl}, seed, rk, g0, pend, x, retry, par))
+        if (!sample_tile<DENSE_GMM, R, SampShared, true, kHotRetry>(L, SampShared{&sl}, seed, rk, g0, pend, x, retry,
+                                                                     par))
             atomicOr(err, 1);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -894,11 +894,12 @@ __global__ __launch_bounds__(kBlock, 4) void k_hot_bx(
             }
             if (take) {
                 const int k = at + (int)__popcll(bal & lt);
+                const int32_t ci = (int32_t)(base + (int64_t)tile_cand(r, threadIdx.x, kBlock));
                 if (lds) {
-                    buf_i[k] = (int32_t)ci[r];
+                    buf_i[k] = ci;
                     buf_x[k] = x[r];
                 } else if (k < hstride) {
-                    hidx[cell * (size_t)hstride + k] = (int32_t)ci[r];
+                    hidx[cell * (size_t)hstride + k] = ci;
                     hx[cell * (size_t)hstride + k] = x[r];
                 }
             }

@@ -27,6 +27,8 @@ PATCHES = {
     'bm': [('tpe_device.h',
             '    return __builtin_amdgcn_sqrt(fmax(0.0, 2.0 * bm_neglog(u01_open0(y))));\n',
             '    return (double)y * 0x1.0p-31;\n')],
+    'lb4': [('tpe_engine.hip', '__launch_bounds__(kBlock, 5) void k_hot_bx(',
+             '__launch_bounds__(kBlock, 4) void k_hot_bx(')],
     'norej': [('tpe_device.h',
                '    const bool bounded = (L.flags & 3) == 3;\n    const uint32_t mask0 = pend;',
                '    const bool bounded = false;\n    const uint32_t mask0 = pend;')],
@@ -36,8 +38,9 @@ PATCHES = {
 def main(name, defs):
     tmp = tempfile.mkdtemp(prefix='tpe_variant_')
     try:
-        csrc = os.path.join(tmp, 'csrc')
+        csrc = os.path.join(tmp, 'hyperopt_amd', 'csrc')   # (the sources include ../../include/)
         shutil.copytree(os.path.join(REPO, 'hyperopt_amd', 'csrc'), csrc)
+        shutil.copytree(os.path.join(REPO, 'include'), os.path.join(tmp, 'include'))
         for fname, old, new in PATCHES.get(name, []):
             p = os.path.join(csrc, fname)
             txt = open(p).read()
