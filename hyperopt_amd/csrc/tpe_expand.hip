@@ -281,6 +281,7 @@ __device__ __forceinline__ double bcast(double v, int j) {
 // what the per-component form gives).
 constexpr int kTabSums = kBxP + 3;   // A_0..A_14, S0, S1, S3
 static_assert(3 * kTabSums * 64 <= kExpTabSize, "k_bx_table: 3 waves' partial sums in the exp table's LDS");
+constexpr int kBxChains = 4;   // components per step of k_bx_table (independent chains)
 __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ labels,
                                                      const int32_t* __restrict__ grp,
                                                      const Comp<double>* __restrict__ comps64,
@@ -326,37 +327,46 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
             }
         }
         const int cnt = min(64, k1 - kc);
-        // two components per step: independent exp and power chains
-        for (int j = 0; j < cnt; j += 2) {
-            const int j1 = min(j + 1, 63);
-            const double c0 = bcast(c_l, j), c1 = j + 1 < cnt ? bcast(c_l, j1) : -kInf;
-            if (!(c0 > -kInf) && !(c1 > -kInf)) continue;   // unclipped or weightless (wave-uniform)
-            const double mu0 = bcast(mu_l, j), mu1 = bcast(mu_l, j1);
-            const double d0 = mu0 - xb, d1 = mu1 - xb;
-            const double a0 = fmax(c0 - kap * d0 * d0, -745.0), a1 = fmax(c1 - kap * d1 * d1, -745.0);
-            // outside the bin's window, or below 2^-1067 in the whole bin (in
-            // the skip term): g = 0, so every sum below is unchanged
-            const bool in0 = fabs(d0) <= D && a0 > -740.0, in1 = fabs(d1) <= D && a1 > -740.0;
-            const double e0 = exp_scaled(fmin(a0 * kExpScale, 0.0), lds);
-            const double e1 = exp_scaled(fmin(a1 * kExpScale, 0.0), lds);
-            const double g0 = in0 ? e0 : 0.0, g1 = in1 ? e1 : 0.0;
-            const double y0 = 2.0 * kap * d0, y1 = 2.0 * kap * d1;
-            double t0 = g0, t1 = g1;
-            A[0] += t0;
-            A[0] += t1;
+        // kBxChains components per step: independent exp and power chains
+        for (int j = 0; j < cnt; j += kBxChains) {
+            double cj[kBxChains], dj[kBxChains], aj[kBxChains];
+            bool any = false;
 #pragma unroll
-            for (int n = 1; n < kBxP; ++n) {
-                t0 *= y0;
-                t1 *= y1;
-                A[n] = fma(t0, kInvFact[n], A[n]);
-                A[n] = fma(t1, kInvFact[n], A[n]);
+            for (int q = 0; q < kBxChains; ++q) {
+                const int jj = min(j + q, 63);
+                cj[q] = j + q < cnt ? bcast(c_l, jj) : -kInf;
+                any = any || cj[q] > -kInf;
             }
-            S0 += g0;
-            S0 += g1;
-            S1 = fma(g0, fabs(a0), S1);
-            S1 = fma(g1, fabs(a1), S1);
-            S3 += fabs(t0 * y0);
-            S3 += fabs(t1 * y1);
+            if (!any) continue;   // unclipped or weightless (wave-uniform)
+            double t[kBxChains], y[kBxChains];
+#pragma unroll
+            for (int q = 0; q < kBxChains; ++q) {
+                dj[q] = bcast(mu_l, min(j + q, 63)) - xb;
+                aj[q] = fmax(cj[q] - kap * dj[q] * dj[q], -745.0);
+                // outside the bin's window, or below 2^-1067 in the whole bin
+                // (in the skip term): g = 0, so every sum below is unchanged
+                const bool in = fabs(dj[q]) <= D && aj[q] > -740.0;
+                const double e = exp_scaled(fmin(aj[q] * kExpScale, 0.0), lds);
+                t[q] = in ? e : 0.0;
+                y[q] = 2.0 * kap * dj[q];
+            }
+            // (the sums in the order of the two-chain version: component j,
+            // then j + 1, ...: every addend and its position are unchanged)
+#pragma unroll
+            for (int q = 0; q < kBxChains; ++q) {
+                S0 += t[q];
+                S1 = fma(t[q], fabs(aj[q]), S1);
+                A[0] += t[q];
+            }
+#pragma unroll
+            for (int n = 1; n < kBxP; ++n)
+#pragma unroll
+                for (int q = 0; q < kBxChains; ++q) {
+                    t[q] *= y[q];
+                    A[n] = fma(t[q], kInvFact[n], A[n]);
+                }
+#pragma unroll
+            for (int q = 0; q < kBxChains; ++q) S3 += fabs(t[q] * y[q]);
         }
     }
     __syncthreads();   // the exp table is no longer read: partial sums of waves 1..3

@@ -29,6 +29,9 @@ PATCHES = {
             '    return (double)y * 0x1.0p-31;\n')],
     'lb4': [('tpe_engine.hip', '__launch_bounds__(kBlock, 5) void k_hot_bx(',
              '__launch_bounds__(kBlock, 4) void k_hot_bx(')],
+    'lb6': [('tpe_engine.hip', '__launch_bounds__(kBlock, 5) void k_hot_bx(',
+             '__launch_bounds__(kBlock, 6) void k_hot_bx(')],
+    'bx2': [('tpe_expand.hip', 'constexpr int kBxChains = 4;', 'constexpr int kBxChains = 2;')],
     'norej': [('tpe_device.h',
                '    const bool bounded = (L.flags & 3) == 3;\n    const uint32_t mask0 = pend;',
                '    const bool bounded = false;\n    const uint32_t mask0 = pend;')],
