@@ -123,6 +123,7 @@ SIGNATURES = {
     'tpe_build_posterior_resident': (ctypes.c_int, [_P, _P, _I64, _I64, _D, _D, _I32, _P]),
     'tpe_build_posterior_resident_ordered': (ctypes.c_int, [_P, _P, _I64, _I64, _D, _D, _I32, _P, _P, _P,
                                                             _P, _P]),
+    'tpe_rebuild_labels': (ctypes.c_int, [_P, _P, _I64, _I64, _D, _D, _I32, _P, _P, _P, _I32, _P, _P]),
     'tpe_last_build_ms': (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float)]),
     'tpe_last_screen': (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_float)]),
     'tpe_set_option': (ctypes.c_int, [_P, _I32, _I64]),

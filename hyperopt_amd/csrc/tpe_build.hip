@@ -493,8 +493,8 @@ __global__ __launch_bounds__(kPartBlock) void k_partition(
     const int32_t* __restrict__ s_idx, const uint8_t* __restrict__ below,
     const double* __restrict__ losses, int64_t T, double* __restrict__ below_val,
     int32_t* __restrict__ arank, double* __restrict__ keys, int32_t* __restrict__ idx,
-    int32_t* __restrict__ counts, int32_t* __restrict__ err) {
-    const int l = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    int32_t* __restrict__ counts, int32_t* __restrict__ err, const int32_t* __restrict__ only) {
+    const int l = only ? only[blockIdx.x] : (int)blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int64_t off = p_off[l], M = cnt[l];
     const bool cat = specs[l].kind == TPE_CATEGORICAL;
     __shared__ int wb[kPartBlock / 64], wa[kPartBlock / 64];
@@ -705,9 +705,9 @@ __global__ __launch_bounds__(kParzenBlock) void k_parzen(
     const int64_t* __restrict__ mix_off, double prior_weight, int32_t lf, double* __restrict__ w,
     double* __restrict__ mu, double* __restrict__ sigma, int32_t* __restrict__ kcount,
     double* __restrict__ leaf_sum, const int64_t* __restrict__ order_off, const int32_t* __restrict__ order,
-    int32_t* __restrict__ ties, int32_t* __restrict__ err) {
+    int32_t* __restrict__ ties, int32_t* __restrict__ err, const int32_t* __restrict__ only) {
 #pragma clang fp contract(off)
-    const int l = blockIdx.x, side = blockIdx.y, tid = threadIdx.x;
+    const int l = only ? only[blockIdx.x] : (int)blockIdx.x, side = blockIdx.y, tid = threadIdx.x;
     const tpe_label_spec sp = specs[l];
     const int64_t n = counts[2 * l + side];
     const int64_t o = mix_off[2 * l + side];
@@ -933,9 +933,9 @@ __global__ __launch_bounds__(kTermBlock) void k_fold_terms(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ kcount,
     const int64_t* __restrict__ mix_off, const double* __restrict__ w, const double* __restrict__ mu,
     const double* __restrict__ sigma, double* __restrict__ terms, double* __restrict__ cterm,
-    double* __restrict__ ascale) {
+    double* __restrict__ ascale, const int32_t* __restrict__ only) {
 #pragma clang fp contract(off)
-    const int l = blockIdx.y, side = blockIdx.z;
+    const int l = only ? only[blockIdx.y] : (int)blockIdx.y, side = blockIdx.z;
     const int mode = labels[l].mode;
     if (mode == CAT) return;
     const int64_t K = kcount[2 * l + side];
@@ -967,9 +967,10 @@ __global__ __launch_bounds__(kParzenBlock) void k_fold(
     const int64_t* __restrict__ mix_off, const double* __restrict__ w, const double* __restrict__ mu,
     const double* __restrict__ sigma, Comp<double>* __restrict__ c64, Comp<float>* __restrict__ c32,
     SampRec* __restrict__ samp, const double* __restrict__ terms, double* __restrict__ cterm,
-    const double* __restrict__ ascale, double* __restrict__ leaf_sum, int32_t* __restrict__ err) {
+    const double* __restrict__ ascale, double* __restrict__ leaf_sum, int32_t* __restrict__ err,
+    const int32_t* __restrict__ only) {
 #pragma clang fp contract(off)
-    const int l = blockIdx.x, tid = threadIdx.x;
+    const int l = only ? only[blockIdx.x] : (int)blockIdx.x, tid = threadIdx.x;
     DLabel d = labels[l];
     const int64_t Kb = kcount[2 * l], Ka = kcount[2 * l + 1];
     const int64_t ob = mix_off[2 * l], oa = mix_off[2 * l + 1];
@@ -1138,11 +1139,13 @@ int history_reset(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels, c
     HIPCHK(ctx, hipMemsetAsync(B.cnt.p, 0, n_labels * sizeof(int32_t), ctx->stream));
     HIPCHK(ctx, hipMemsetAsync(B.p_off.p, 0, n_labels * sizeof(int64_t), ctx->stream));
     B.hist_ready = true;
+    ++B.hist_gen;
     return TPE_OK;
 }
 
 int history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial, const double* obs_val) {
     auto& B = ctx->build;
+    ++B.hist_gen;   // (a failed append leaves the history unknown: no subset rebuild after it either)
     if (!B.hist_ready) return ctx->fail(TPE_ERR_ARG, "tpe_history_append before tpe_history_reset");
     const int32_t L = (int32_t)B.specs_h.size();
     std::vector<int64_t> st(L + 1, 0);
@@ -1287,12 +1290,31 @@ int history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial,
 // tpe.py:433; empty range = the device's position order); ties_out
 // (optional, n_labels + 1): which mixtures depend on a tie order the caller
 // did not supply (k_parzen, k_split).
+// only_h / n_only (optional): rebuild just these labels of the resident
+// posterior (with the supplied orders), keeping the others -- valid only
+// right after a build of the same history with the same arguments, whose
+// below set it reuses (so no below_h); the caller's labels are those whose
+// mixtures depend on an order the previous build did not have.
 int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t n_valid,
                    double gamma, double prior_weight, int32_t lf, int32_t* n_below_out,
                    const uint8_t* below_h = nullptr, const int64_t* order_off_h = nullptr,
-                   const int32_t* order_h = nullptr, int32_t* ties_out = nullptr) {
+                   const int32_t* order_h = nullptr, int32_t* ties_out = nullptr,
+                   const int32_t* only_h = nullptr, int32_t n_only = 0) {
     auto& B = ctx->build;
     if (!B.hist_ready) return ctx->fail(TPE_ERR_ARG, "no resident history (tpe_history_reset)");
+    const bool subset = only_h != nullptr && n_only > 0;
+    if (subset) {
+        if (below_h)
+            return ctx->fail(TPE_ERR_ARG, "a label-subset rebuild keeps the previous build's below set");
+        if (!B.built_ok || B.built_gen != B.hist_gen || B.built_T != n_trials || B.built_valid != n_valid ||
+            B.built_gamma != gamma || B.built_pw != prior_weight || B.built_lf != lf ||
+            B.n_labels != (int32_t)B.specs_h.size())
+            return ctx->fail(TPE_ERR_ARG, "a label-subset rebuild must follow a build of the same history");
+        for (int32_t i = 0; i < n_only; ++i)
+            if (only_h[i] < 0 || only_h[i] >= B.n_labels || (i && only_h[i] <= only_h[i - 1]))
+                return ctx->fail(TPE_ERR_ARG, "subset labels must be increasing label indices");
+    }
+    B.built_ok = false;   // (set again once this build completes)
     if (lf < 1 || lf >= kMaxLF) return ctx->fail(TPE_ERR_ARG, "linear forgetting must be in [1, 63]");
     if (n_trials < 0 || n_trials >= INT32_MAX || (n_trials > 0 && !losses) || n_valid < 0 ||
         n_valid > n_trials)
@@ -1387,30 +1409,41 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
         order_off_d = B.order_off.p;
         order_d = B.order.p;
     }
-    if (T > 0) HIPCHK(ctx, hipMemcpyAsync(B.losses.p, losses, T * sizeof(double), hipMemcpyHostToDevice, st));
-    if (T > 0 && below_h) HIPCHK(ctx, hipMemcpyAsync(B.below.p, below_h, T, hipMemcpyHostToDevice, st));
-    HIPCHK(ctx, hipMemcpyAsync(B.mix_off.p, mix.data(), mix.size() * sizeof(int64_t), hipMemcpyHostToDevice, st));
-    HIPCHK(ctx, hipMemcpyAsync(P.labels.p, dl.data(), n_labels * sizeof(DLabel), hipMemcpyHostToDevice, st));
+    const int32_t* only_d = nullptr;
+    const int32_t nl_run = subset ? n_only : n_labels;
+    if (subset) {
+        // the other labels keep the previous build's records, DLabels and
+        // mixtures; the losses, the below set and the offsets are the same
+        HIPCHK(ctx, B.only.reserve(n_only));
+        HIPCHK(ctx, hipMemcpyAsync(B.only.p, only_h, n_only * sizeof(int32_t), hipMemcpyHostToDevice, st));
+        only_d = B.only.p;
+    } else {
+        if (T > 0) HIPCHK(ctx, hipMemcpyAsync(B.losses.p, losses, T * sizeof(double), hipMemcpyHostToDevice, st));
+        if (T > 0 && below_h) HIPCHK(ctx, hipMemcpyAsync(B.below.p, below_h, T, hipMemcpyHostToDevice, st));
+        HIPCHK(ctx, hipMemcpyAsync(B.mix_off.p, mix.data(), mix.size() * sizeof(int64_t), hipMemcpyHostToDevice,
+                                   st));
+        HIPCHK(ctx, hipMemcpyAsync(P.labels.p, dl.data(), n_labels * sizeof(DLabel), hipMemcpyHostToDevice, st));
+    }
     HIPCHK(ctx, hipMemsetAsync(ctx->errflag.p, 0, sizeof(int32_t), st));
 
     HIPCHK(ctx, hipEventRecord(ctx->ev0, st));
-    if (T > 0 && !below_h)
+    if (T > 0 && !below_h && !subset)
         hipLaunchKernelGGL(k_split, dim3(1), dim3(kSplitBlock), 0, st, B.losses.p, T, n_below, B.below.p,
                            B.ties.p + n_labels);
-    hipLaunchKernelGGL(k_partition, dim3(n_labels), dim3(kPartBlock), 0, st, B.specs.p, B.p_off.p, B.cnt.p,
+    hipLaunchKernelGGL(k_partition, dim3(nl_run), dim3(kPartBlock), 0, st, B.specs.p, B.p_off.p, B.cnt.p,
                        B.p_trial.p, B.p_val.p, B.s_key.p, B.s_idx.p, B.below.p, B.losses.p, T,
-                       B.below_val.p, B.arank.p, B.keys.p, B.idx.p, B.counts.p, ctx->errflag.p);
-    hipLaunchKernelGGL(k_parzen, dim3(n_labels, 2), dim3(kParzenBlock), 0, st, B.specs.p, B.cat_p.p,
+                       B.below_val.p, B.arank.p, B.keys.p, B.idx.p, B.counts.p, ctx->errflag.p, only_d);
+    hipLaunchKernelGGL(k_parzen, dim3(nl_run, 2), dim3(kParzenBlock), 0, st, B.specs.p, B.cat_p.p,
                        B.p_off.p, B.counts.p, B.below_val.p, B.keys.p, B.keys.p, B.idx.p, B.mix_off.p,
                        prior_weight, lf, B.w.p, B.mu.p, B.sigma.p, B.kcount.p, B.scratch.p + total, order_off_d,
-                       order_d, B.ties.p, ctx->errflag.p);
-    hipLaunchKernelGGL(k_fold_terms, dim3((unsigned)((max_cap + kTermBlock - 1) / kTermBlock), n_labels, 2),
+                       order_d, B.ties.p, ctx->errflag.p, only_d);
+    hipLaunchKernelGGL(k_fold_terms, dim3((unsigned)((max_cap + kTermBlock - 1) / kTermBlock), nl_run, 2),
                        dim3(kTermBlock), 0, st, P.labels.p, B.kcount.p, B.mix_off.p, B.w.p, B.mu.p,
-                       B.sigma.p, B.scratch.p, B.scratch.p + 2 * total, B.scratch.p + 3 * total);
-    hipLaunchKernelGGL(k_fold, dim3(n_labels), dim3(kParzenBlock), 0, st, P.labels.p, B.kcount.p,
+                       B.sigma.p, B.scratch.p, B.scratch.p + 2 * total, B.scratch.p + 3 * total, only_d);
+    hipLaunchKernelGGL(k_fold, dim3(nl_run), dim3(kParzenBlock), 0, st, P.labels.p, B.kcount.p,
                        B.mix_off.p, B.w.p, B.mu.p, B.sigma.p, P.comps64.p, P.comps32.p, P.samp.p,
                        B.scratch.p, B.scratch.p + 2 * total, B.scratch.p + 3 * total, B.scratch.p + total,
-                       ctx->errflag.p);
+                       ctx->errflag.p, only_d);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(ctx->ev1, st));
     HIPCHK(ctx, ctx->dl_h.resize(n_labels));
@@ -1456,6 +1489,13 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     P.n_labels = n_labels;
     B.n_labels = n_labels;
     B.mix_h = mix;
+    B.built_ok = true;
+    B.built_gen = B.hist_gen;
+    B.built_T = n_trials;
+    B.built_valid = n_valid;
+    B.built_gamma = gamma;
+    B.built_pw = prior_weight;
+    B.built_lf = lf;
     if (n_below_out) *n_below_out = n_below;
     return TPE_OK;
 }
@@ -1491,6 +1531,16 @@ TPE_DEV int tpe1_build_posterior_resident_ordered(tpe_ctx* ctx, const double* lo
     if (!ctx) return TPE_ERR_ARG;
     return build_resident(ctx, losses, n_trials, n_valid, gamma, prior_weight, lf, n_below_out, below,
                           order_off, order, ties);
+}
+
+TPE_DEV int tpe1_rebuild_labels(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t n_valid,
+                                double gamma, double prior_weight, int32_t lf, const int64_t* order_off,
+                                const int32_t* order, const int32_t* labels, int32_t n_only,
+                                int32_t* n_below_out, int32_t* ties) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (!labels || n_only <= 0) return ctx->fail(TPE_ERR_ARG, "tpe_rebuild_labels: no labels");
+    return build_resident(ctx, losses, n_trials, n_valid, gamma, prior_weight, lf, n_below_out, nullptr,
+                          order_off, order, ties, labels, n_only);
 }
 
 TPE_DEV int tpe1_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,

@@ -282,6 +282,14 @@ struct BuildBufs {
     DevBuf<int32_t> order;
     int32_t n_labels = 0;          // labels of the last build (0: none resident)
     std::vector<int64_t> mix_h;    // host copy of mix_off
+    // what the last build was of (a label-subset rebuild requires the same):
+    // the history generation (bumped by every reset / append) and the arguments
+    uint64_t hist_gen = 0, built_gen = 0;
+    bool built_ok = false;
+    int64_t built_T = -1, built_valid = -1;
+    double built_gamma = 0.0, built_pw = 0.0;
+    int32_t built_lf = 0;
+    DevBuf<int32_t> only;          // the labels of a subset rebuild
     void release() {
         specs.release(); cat_p.release(); p_off.release(); cnt.release(); p_trial.release();
         p_val.release(); s_key.release(); s_key2.release(); s_idx.release(); s_idx2.release();
@@ -291,7 +299,8 @@ struct BuildBufs {
         gs_lab2.release(); losses.release(); below.release(); keys.release();
         idx.release(); below_val.release(); counts.release(); kcount.release(); w.release();
         mu.release(); sigma.release(); mix_off.release(); scratch.release(); ties.release();
-        order_off.release(); order.release();
+        order_off.release(); order.release(); only.release();
+        built_ok = false;
         n_labels = 0;
         hist_ready = false;
         pool_cap = 0;
@@ -538,6 +547,10 @@ TPE_DEV int tpe1_build_posterior_resident_ordered(tpe_ctx* ctx, const double* lo
                                                   int64_t n_valid, double gamma, double prior_weight,
                                                   int32_t lf, const uint8_t* below, const int64_t* order_off,
                                                   const int32_t* order, int32_t* n_below_out, int32_t* ties);
+TPE_DEV int tpe1_rebuild_labels(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t n_valid,
+                                double gamma, double prior_weight, int32_t lf, const int64_t* order_off,
+                                const int32_t* order, const int32_t* labels, int32_t n_only,
+                                int32_t* n_below_out, int32_t* ties);
 TPE_DEV int tpe1_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
                                  const double* cat_p, int64_t n_cat_p, const double* losses,
                                  int64_t n_trials, const int64_t* obs_off, const int32_t* obs_trial,

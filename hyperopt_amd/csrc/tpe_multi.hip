@@ -387,6 +387,16 @@ int tpe_build_posterior_resident_ordered(tpe_ctx* ctx, const double* losses, int
     });
 }
 
+int tpe_rebuild_labels(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t n_valid, double gamma,
+                       double prior_weight, int32_t lf, const int64_t* order_off, const int32_t* order,
+                       const int32_t* labels, int32_t n_only, int32_t* n_below_out, int32_t* ties) {
+    if (!ctx) return TPE_ERR_ARG;
+    return for_all(ctx, [&](tpe_ctx* x, int d) {
+        return tpe1_rebuild_labels(x, losses, n_trials, n_valid, gamma, prior_weight, lf, order_off, order, labels,
+                                   n_only, d == 0 ? n_below_out : nullptr, d == 0 ? ties : nullptr);
+    });
+}
+
 int tpe_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
                         const double* cat_p, int64_t n_cat_p, const double* losses,
                         int64_t n_trials, const int64_t* obs_off, const int32_t* obs_trial,

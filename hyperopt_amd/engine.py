@@ -217,6 +217,24 @@ class Engine(object):
         self.n_labels = self.hist_labels
         return nb.value, ties
 
+    def rebuild_labels(self, losses, n_valid, gamma, prior_weight, lf, order_off, order, labels):
+        """The ordered rebuild of `labels` only (tpe_rebuild_labels), right
+        after a build of the same history and arguments; the other labels
+        and the below set are kept.  Returns (n_below, ties)."""
+        losses = _f64(losses)
+        L_ = self.hist_labels
+        order_off = np.ascontiguousarray(order_off, dtype=np.int64)
+        order = np.ascontiguousarray(order, dtype=np.int32)
+        if len(order_off) != L_ + 1 or order_off[-1] != len(order):
+            raise ValueError('order offsets must be n_labels + 1 long and end at len(order)')
+        only = np.ascontiguousarray(sorted(int(l) for l in labels), dtype=np.int32)
+        nb = ctypes.c_int32()
+        ties = np.zeros(L_ + 1, dtype=np.int32)
+        self._check(self.lib.tpe_rebuild_labels(
+            self.h, _ptr(losses), len(losses), int(n_valid), float(gamma), float(prior_weight), int(lf),
+            _ptr(order_off), _ptr(order), _ptr(only), len(only), ctypes.byref(nb), _ptr(ties)))
+        return nb.value, ties
+
     def get_mixture(self, label, side):
         """(weights, mus, sigmas) of a built mixture (side 0 below, 1 above)."""
         n = ctypes.c_int32()

@@ -368,7 +368,13 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
     need = have | set(np.flatnonzero(ties[:-1] & 2).tolist())
     if need != have or ties[-1]:
         below, off, order = reference_orders(losses, n_below, obs_of, need)
-        nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf, below, off, order)
+        if not ties[-1] and len(need) < obs_of.n_labels:
+            # no tie across the split (the below set is the one just built):
+            # rebuild only the labels that needed an order
+            nb, ties = eng.rebuild_labels(losses, n_valid, gamma, prior_weight, lf, off, order, need)
+        else:
+            nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf, below, off,
+                                                   order)
         if np.any(ties[:-1]):
             # a supplied below set can move observations between the sets,
             # creating a dependent label the first pass did not see

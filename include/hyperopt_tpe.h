@@ -268,6 +268,18 @@ int tpe_build_posterior_resident_ordered(tpe_ctx *ctx, const double *losses, int
                                          int32_t lf, const uint8_t *below, const int64_t *order_off,
                                          const int32_t *order, int32_t *n_below_out, int32_t *ties);
 
+/* The ordered rebuild restricted to `labels` (n_only increasing label
+ * indices): right after a build of the same resident history with the same
+ * arguments (no append in between, or TPE_ERR_ARG), rebuild only those
+ * labels with the supplied orders and keep the others' mixtures and records
+ * -- the labels whose ties the previous build flagged, when equal losses did
+ * not straddle the split (the below set is kept too).  Same outputs as
+ * tpe_build_posterior_resident_ordered; the others' tie flags read 0. */
+int tpe_rebuild_labels(tpe_ctx *ctx, const double *losses, int64_t n_trials, int64_t n_valid,
+                       double gamma, double prior_weight, int32_t lf, const int64_t *order_off,
+                       const int32_t *order, const int32_t *labels, int32_t n_only,
+                       int32_t *n_below_out, int32_t *ties);
+
 /* Read back one mixture of the resident posterior built by
  * tpe_build_posterior (side 0 below, 1 above): the (weights, mus, sigmas)
  * that adaptive_parzen_normal returns (categorical: p in weights).  *n

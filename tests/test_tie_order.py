@@ -143,3 +143,47 @@ def test_auto_and_host_builders_suggest_identical_documents():
         trials.refresh()
     up = get_engine(0, 'f64')._history_uploader
     assert up.tie_labels, 'the device path did not run'
+
+
+def test_label_subset_rebuild_equals_full_rebuild():
+    """tpe_rebuild_labels (posterior.build_reference_order's second build
+    when no loss tie straddles the split): rebuilding only the labels whose
+    mixtures needed numpy's order gives the mixtures, records and round
+    results of the full ordered rebuild, and the host build's mixtures; a
+    rebuild after an append, or with different arguments, is refused."""
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.engine import Engine, EngineError
+    hist = coarse_history(6000, seed=3, split_tie=False)
+    specs, cat, losses, off, tr, val = hist.device_inputs()
+    n_valid = int(np.count_nonzero(losses == losses))
+    n_below = P.n_below_of(n_valid, 0.25, 25)
+    out = []
+    for subset in (False, True):
+        eng = Engine(0, 'f64')
+        eng.history_reset(specs, cat)
+        eng.history_append(np.diff(off), tr, val)
+        nb, ties = eng.build_posterior_ordered(losses, n_valid, 0.25, 1.0, 25)
+        assert not ties[-1]
+        need = set(np.flatnonzero(ties[:-1] & 2).tolist())
+        assert need and len(need) < len(hist.labels)
+        below, o_off, order = P.reference_orders(losses, n_below, P._ObsOf(off, tr, val), need)
+        if subset:
+            nb2, ties2 = eng.rebuild_labels(losses, n_valid, 0.25, 1.0, 25, o_off, order, need)
+            with pytest.raises(EngineError):   # different arguments
+                eng.rebuild_labels(losses, n_valid, 0.3, 1.0, 25, o_off, order, need)
+        else:
+            nb2, ties2 = eng.build_posterior_ordered(losses, n_valid, 0.25, 1.0, 25, below, o_off, order)
+        assert nb2 == nb and not np.any(ties2)
+        _assert_same(eng, hist, hist.posteriors())
+        mix = [eng.get_mixture(li, side) for li in range(len(hist.labels)) for side in (0, 1)]
+        res = eng.suggest(5, 1 << 16, round=2)
+        out.append((mix, np.ascontiguousarray(res).tobytes()))
+        if subset:   # after an append the kept state is stale: refused
+            eng.history_append(np.zeros(len(hist.labels), dtype=np.int64), np.zeros(0, np.int32), np.zeros(0))
+            with pytest.raises(EngineError):
+                eng.rebuild_labels(losses, n_valid, 0.25, 1.0, 25, o_off, order, need)
+        eng.close()
+    (m0, r0), (m1, r1) = out
+    assert r0 == r1
+    for a, b in zip(m0, m1):
+        assert all(np.array_equal(x, y) for x, y in zip(a, b))
