@@ -416,6 +416,7 @@ def main():
     # built once per posterior, in its first large round
     prep_ms = eng.last_prepare_ms() if args.warmup > 0 else None
     dt, mode_ms, mode_ev, scr = timed(args.steps, args.warmup, fresh_mode)
+    smode_timed = eng.last_screen_mode()   # (the timed rounds' screen; later legs run others)
     # the same rounds on the posterior of the last step, reused (no append):
     # the round alone, and the reference for the unscreened comparison
     warm_first = args.warmup + args.steps
@@ -520,7 +521,7 @@ def main():
     prec = args.precision
     dom = max((k for k in mode_ms if k in DENSE), key=lambda k: mode_ms[k])
     screened = scr[0] > 0
-    smode = eng.last_screen_mode() if screened else 0
+    smode = smode_timed if screened else 0
     windowed = smode == 2
     slots = None
     hot = smode == 3 and scr[5] > 0
