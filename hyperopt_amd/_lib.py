@@ -164,6 +164,8 @@ def load():
                       '`python -m hyperopt_amd._build` or __graft_entry__.build())' % path)
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
+        if variant and not hasattr(lib, name):   # (a variant of an older commit: fewer entry points)
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -324,6 +324,9 @@ def _sort_pool():
     return _pool
 
 
+SUBSET_REBUILD = True   # the ordered rebuild restricted to the labels that need an order
+
+
 def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of, known=(), prepare=None,
                           overlap=True):
     """Device build whose mixtures follow the reference's tie order
@@ -368,7 +371,7 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
     need = have | set(np.flatnonzero(ties[:-1] & 2).tolist())
     if need != have or ties[-1]:
         below, off, order = reference_orders(losses, n_below, obs_of, need)
-        if not ties[-1] and len(need) < obs_of.n_labels:
+        if SUBSET_REBUILD and not ties[-1] and len(need) < obs_of.n_labels:
             # no tie across the split (the below set is the one just built):
             # rebuild only the labels that needed an order
             nb, ties = eng.rebuild_labels(losses, n_valid, gamma, prior_weight, lf, off, order, need)

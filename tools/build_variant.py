@@ -42,8 +42,15 @@ def main(name, defs):
     tmp = tempfile.mkdtemp(prefix='tpe_variant_')
     try:
         csrc = os.path.join(tmp, 'hyperopt_amd', 'csrc')   # (the sources include ../../include/)
-        shutil.copytree(os.path.join(REPO, 'hyperopt_amd', 'csrc'), csrc)
-        shutil.copytree(os.path.join(REPO, 'include'), os.path.join(tmp, 'include'))
+        rev = os.environ.get('VARIANT_REV')   # the sources of another commit (timing comparisons)
+        if rev:
+            import subprocess
+            for sub in ('hyperopt_amd/csrc', 'include'):
+                out = subprocess.check_output(['git', '-C', REPO, 'archive', rev, sub])
+                subprocess.run(['tar', '-x', '-C', tmp], input=out, check=True)
+        else:
+            shutil.copytree(os.path.join(REPO, 'hyperopt_amd', 'csrc'), csrc)
+            shutil.copytree(os.path.join(REPO, 'include'), os.path.join(tmp, 'include'))
         for fname, old, new in PATCHES.get(name, []):
             p = os.path.join(csrc, fname)
             txt = open(p).read()
