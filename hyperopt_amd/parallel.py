@@ -62,11 +62,14 @@ def gather_rounds(res, group=None):
     return parts.reshape((world * np.shape(res)[0],) + np.shape(res)[1:])
 
 
-# relative cost of a label in a fresh-posterior step (bench config 3, r3
-# profile): a dense label pays the expansion index and the hot-bin round, a
-# quantized one the host's tie order and its table round, a categorical one
-# only its early-exit round
-LABEL_COST = {'dense': 1.0, 'quantized': 0.5, 'categorical': 0.25}
+# relative cost of a label in a fresh-posterior step of a label shard,
+# fitted to the one-GPU projection's shard times (r3ac: 3 dense + 1
+# categorical 1.20 ms, 2 dense + 2 quantized 1.44 ms, 2 dense + 1 quantized
+# + 2 categorical 1.33 ms): a dense label pays its share of the draw kernel
+# and of the index, a quantized one the host's numpy argsort, its part of
+# the ordered rebuild and its table round -- more than a dense one -- a
+# categorical one its early-exit round
+LABEL_COST = {'dense': 1.0, 'quantized': 1.5, 'categorical': 0.5}
 
 
 def label_cost(kind, args=None):
