@@ -464,8 +464,9 @@ def main():
                              ('win_t', args.win_t), ('win_groups', args.win_groups)):
                     e8.set_option(k, v)
                 l8 = FminLoop(hist_full, label_ids=sh)
-                l8.advance(e8, args.trials + p0 * args.append)
-                step(p0, True, e=e8, lp=l8, gather=False)      # warm-up
+                l8.advance(e8, args.trials + (p0 - 1) * args.append)
+                for w in (p0 - 1, p0):                          # warm-up steps
+                    step(w, True, e=e8, lp=l8, gather=False)
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 for i in range(args.steps):
