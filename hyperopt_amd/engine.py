@@ -490,13 +490,15 @@ def merge_results(parts):
 _tls = threading.local()
 
 
-def get_engine(device=0, precision='f64'):
+def get_engine(device=0, precision='f64', role='main'):
     """Per-thread cached Engine (contexts are not thread-safe); `device` an
-    ordinal or a list of them."""
+    ordinal or a list of them; `role` keeps separate contexts -- hence
+    separate device-resident histories -- for callers that would otherwise
+    evict each other's (tpe.suggest's batch='pending' views)."""
     cache = getattr(_tls, 'engines', None)
     if cache is None:
         cache = _tls.engines = {}
-    key = (_devices(device), precision)
+    key = (_devices(device), precision, role)
     if key not in cache:
         eng = Engine(device, precision)
         eng.set_option('timing', 0)          # tpe.suggest reads no device timings

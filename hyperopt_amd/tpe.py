@@ -251,7 +251,12 @@ def suggest(new_ids, domain, trials, seed,
         return rand.suggest(new_ids, domain, trials, seed)      # tpe.py:869-871
     if n_docs == 0:
         logger.info('TPE using 0 trials')                     # the prior-only posterior
-    eng = _engine.get_engine(list(devices) if devices else device, 'f64')
+    # a pending view (batch='pending') keeps its own context: its history
+    # (the trials plus the batch's earlier suggestions) would otherwise
+    # replace the real trials' device-resident history, and the next call
+    # on those would upload it whole again
+    eng = _engine.get_engine(list(devices) if devices else device, 'f64',
+                             'pending' if isinstance(trials, _PendingView) else 'main')
     ids = list(new_ids) if batch else [new_ids[0]]
     _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior_weight,
                         posterior_builder, n_candidates=n_EI_candidates, n_rounds=len(ids))

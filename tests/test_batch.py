@@ -176,3 +176,19 @@ def test_loss_array_pending_is_inf_and_nan_kept():
     assert out[0] == 1.5 and out[1] == np.inf and np.isnan(out[2]) and out[3] == 2.0
     ok = [{'result': {'loss': 0.25}}, {'result': {'loss': -1.0}}]
     assert list(history.loss_array(dom, ok)) == [0.25, -1.0]
+
+
+@pytest.mark.gpu
+def test_pending_batch_keeps_the_main_resident_history():
+    """a batch='pending' view runs on its own context, so
+    the real trials' device-resident history is not replaced (and uploaded
+    whole again by the next regular call)."""
+    from hyperopt_amd import engine as E
+    trials = _history(300, 3)
+    dom = H.Domain(_loss, SPACE)
+    tpe.suggest([1999], dom, trials, 5, posterior_builder='device')
+    main = E.get_engine(0, 'f64')
+    gen, key = main.history_generation, main._history_uploader.key
+    tpe.suggest([2000, 2001, 2002], dom, trials, 5, batch='pending', posterior_builder='device')
+    assert main.history_generation == gen and main._history_uploader.key == key
+    assert E.get_engine(0, 'f64', 'pending') is not main
