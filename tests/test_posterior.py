@@ -59,3 +59,25 @@ def test_splitter_equals_split_label(fixture):
         b, a = sp.split(rec['o_idxs'], rec['o_vals'])
         assert np.array_equal(np.asarray(b, float), rec['below'])
         assert np.array_equal(np.asarray(a, float), rec['above'])
+
+
+def test_spec_table_streams_and_label_subsets():
+    """A label subset (a label-sharded rank) keeps each label's Philox
+    stream: spec_table sets TPE_HAS_STREAM and the space index; without
+    streams the flag is clear (the device uses the position).  FminLoop's
+    view of a subset holds only its labels' observations."""
+    from hyperopt_amd import _lib as L
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.workloads import FminLoop, mixed_history
+    hist = mixed_history(10, 50, seed=1)
+    specs, _, _ = P.spec_table(hist.labels)
+    assert not np.any(specs['flags'] & L.TPE_HAS_STREAM)
+    ids = [1, 4, 7]
+    specs, _, _ = P.spec_table([hist.labels[i] for i in ids], streams=ids)
+    assert np.all(specs['flags'] & L.TPE_HAS_STREAM)
+    assert list(specs['stream']) == ids
+    loop = FminLoop(hist, label_ids=ids)
+    assert loop.streams == ids and [n for n, _, _ in loop.labels] == [hist.labels[i][0] for i in ids]
+    tids, losses, n_valid, obs, owner = loop.view(30)
+    assert set(obs) == {hist.labels[i][0] for i in ids} and len(tids) == 30 and owner is loop
+    assert all(len(obs[n][0]) == 30 for n in obs)
