@@ -203,6 +203,7 @@ def label_spec(kind, args):
         else:
             floor = np.maximum(EPS, np.exp(low))              # tpe.py:536-540
             spec['kind'], tr = L.TPE_LGMM1, (lambda o: np.log(np.maximum(o, floor)))
+            tr.floor = float(floor)
         return spec, tr, None
     spec = dict(prior_mu=float(args['mu']), prior_sigma=float(args['sigma']), flags=0)
     if kind in ('qnormal', 'qlognormal'):
@@ -214,6 +215,7 @@ def label_spec(kind, args):
         spec['kind'], tr = L.TPE_LGMM1, np.log
     elif kind == 'qlognormal':
         spec['kind'], tr = L.TPE_LGMM1, (lambda o: np.log(np.maximum(o, EPS)))
+        tr.floor = float(EPS)
     else:
         raise ValueError('unknown distribution %r' % kind)
     return spec, tr, None
@@ -439,35 +441,52 @@ class DeviceHistoryUploader(object):
         self.key, self.owner = None, None
         if fresh:
             specs, cat_p, self.trs = spec_table(labels, streams)
+            # per label: 0 identity, 1 np.log, 2 np.log(np.maximum(o, floor))
+            self.tr_kind = np.array([0 if t is None else (1 if t is np.log else 2) for t in self.trs])
+            self.tr_floor = np.array([getattr(t, 'floor', -np.inf) for t in self.trs])
             eng.history_reset(specs, cat_p)
             self.prev_counts = [0] * len(labels)
             self.pos_parts = [[] for _ in labels]    # what the device holds, per label
             self.val_parts = [[] for _ in labels]
             self.tie_labels = frozenset()
         counts = list(self.prev_counts)
-        n_new, trial_parts, val_parts = [], [], []
+        # the new observations of every label, transformed and placed in one
+        # vectorised pass (a per-label numpy loop cost ~0.4 ms per fmin step
+        # at 32 labels): np.log / np.log(np.maximum(o, floor)) elementwise,
+        # as the reference's samplers transform them (tpe.py:493-576)
+        n_new, ni_l, nv_l = [], [], []
         for i, (name, _, _) in enumerate(labels):
             oi, ov = cols[name]
             c0 = counts[i]
-            ni, nv = oi[c0:], ov[c0:]
-            if len(ni):
-                tr = self.trs[i]
-                if tr is not None:
-                    nv = tr(nv)
-                nv = np.asarray(nv, dtype=float)
-                _check_finite(name, nv)
-                pos = np.searchsorted(tids, ni)
-                pc = np.minimum(pos, len(tids) - 1)
-                pos = np.where(tids[pc] == ni, pc, -1)
-                trial_parts.append(pos.astype(np.int32))
-                val_parts.append(nv)
-                self.pos_parts[i].append(trial_parts[-1])
-                self.val_parts[i].append(nv)
-            n_new.append(len(ni))
+            m = len(oi) - c0
+            n_new.append(m)
+            if m:
+                ni_l.append(oi[c0:])
+                nv_l.append(ov[c0:])
             counts[i] = len(oi)
-        if sum(n_new):
-            eng.history_append(np.asarray(n_new, dtype=np.int64), np.concatenate(trial_parts),
-                               np.concatenate(val_parts))
+        if ni_l:
+            ni = np.concatenate(ni_l)
+            raw = np.asarray(np.concatenate(nv_l), dtype=float)
+            lab = np.repeat(np.arange(len(labels)), n_new)
+            kind = self.tr_kind[lab]
+            vals = raw.copy()
+            lg = kind > 0
+            if lg.any():
+                vals[lg] = np.log(np.maximum(raw[lg], self.tr_floor[lab[lg]]))
+            nan = np.isnan(vals)
+            if nan.any():
+                raise NonFiniteObservation('label %r: NaN observation value'
+                                           % (labels[int(lab[np.argmax(nan)])][0],))
+            pos = np.searchsorted(tids, ni)
+            pc = np.minimum(pos, len(tids) - 1)
+            trial = np.where(tids[pc] == ni, pc, -1).astype(np.int32)
+            eng.history_append(np.asarray(n_new, dtype=np.int64), trial, vals)
+            o = 0
+            for i, m in enumerate(n_new):
+                if m:
+                    self.pos_parts[i].append(trial[o:o + m])
+                    self.val_parts[i].append(vals[o:o + m])
+                    o += m
         self.prev_counts = counts                  # committed only after the append
         self.key = (key[0], eng.history_generation)
         self.owner = weakref.ref(owner)
