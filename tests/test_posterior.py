@@ -81,3 +81,57 @@ def test_spec_table_streams_and_label_subsets():
     tids, losses, n_valid, obs, owner = loop.view(30)
     assert set(obs) == {hist.labels[i][0] for i in ids} and len(tids) == 30 and owner is loop
     assert all(len(obs[n][0]) == 30 for n in obs)
+
+
+class _RecordingEngine(object):
+    """Captures what DeviceHistoryUploader uploads (no device)."""
+    history_generation = 0
+
+    def __init__(self):
+        self.appends = []
+
+    def history_reset(self, specs, cat_p):
+        self.appends.append(None)
+
+    def history_append(self, n_new, trial, vals):
+        self.appends.append((np.array(n_new), np.array(trial), np.array(vals)))
+
+
+def test_uploader_vectorised_append_matches_per_label_transforms(monkeypatch):
+    """The uploader transforms and places the new observations of every
+    label in one pass: per label the values equal the reference's own
+    transform of that label's new observations (np.log, np.log(np.maximum(o,
+    floor)) for q-log kinds, identity), positions are the trials' rows, and
+    a NaN names its label."""
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.workloads import FminLoop, conditional_history, mixed_history
+    monkeypatch.setattr(P, 'build_reference_order', lambda *a, **k: (0, frozenset()))
+    for hist in (mixed_history(12, 700, seed=0), conditional_history(600, seed=1)):
+        eng = _RecordingEngine()
+        up, loop = P.DeviceHistoryUploader(), FminLoop(hist)
+        steps = [(0, 500), (500, 501), (501, 540)]
+        for _, n in steps:
+            up.build(eng, hist.labels, loop.view(n), 0.25, 1.0)
+        _, _, trs = P.spec_table(hist.labels)
+        got = [a for a in eng.appends if a is not None]
+        assert len(got) == len(steps)
+        for (n_new, trial, vals), (n0, n1) in zip(got, steps):
+            o = 0
+            for i, (name, _, _) in enumerate(hist.labels):
+                oi, ov = hist.obs[name]
+                sel = (oi >= n0) & (oi < n1)
+                want = ov[sel] if trs[i] is None else trs[i](ov[sel])
+                m = int(sel.sum())
+                assert n_new[i] == m
+                assert np.array_equal(vals[o:o + m], np.asarray(want, dtype=float))
+                assert np.array_equal(trial[o:o + m], np.flatnonzero(np.isin(hist.tids[:n1], oi[sel])))
+                o += m
+    # a NaN after the transform (log of a negative value) names its label
+    hist = mixed_history(6, 50, seed=2)
+    name = hist.labels[1][0]                       # loguniform
+    oi, ov = hist.obs[name]
+    hist.obs[name] = (oi, np.where(oi == 40, -1.0, ov))
+    up, loop, eng = P.DeviceHistoryUploader(), FminLoop(hist), _RecordingEngine()
+    up.build(eng, hist.labels, loop.view(30), 0.25, 1.0)
+    with pytest.raises(P.NonFiniteObservation, match=name):
+        up.build(eng, hist.labels, loop.view(45), 0.25, 1.0)
