@@ -464,33 +464,35 @@ __device__ __forceinline__ bool sample_tile(const DLabel& L, const Src& src, uin
             if (rej) q.slot[pos[r + h]] = (uint16_t)(c0 + (uint32_t)h);
         }
     }
-    __syncthreads();   // the list is complete
-    const int n = q.n[par];
-    if (threadIdx.x == 0) q.n[par ^ 1] = 0;   // (its last reader finished before the previous tile's end)
     bool ok = true;
-    // (n is the workgroup's: uniform.  At least one barrier follows thread
-    // 0's reset of the next tile's counter before any thread moves on.)
-    if (n == 0) __syncthreads();
-    for (int c0 = 0; c0 < n; c0 += CAP) {
-        const int c1 = min(n, c0 + CAP);
-        for (int e = c0 + (int)threadIdx.x; e < c1; e += blockDim.x) {
-            const uint32_t gg = g0 + (uint32_t)q.slot[e];
-            double v = __builtin_nan("");
-            for (uint32_t it = 1; it < kMaxAttempts; ++it) {
-                const double draw = draw_attempt(L, src, k0, k1, gg, it, rk);
-                if (L.low <= draw && draw < L.high) {
-                    v = draw;
-                    break;
+    if (bounded) {   // (a label without both bounds never rejects: no list, no barriers)
+        __syncthreads();   // the list is complete
+        const int n = q.n[par];
+        if (threadIdx.x == 0) q.n[par ^ 1] = 0;   // (its last reader finished before the previous tile's end)
+        // (n is the workgroup's: uniform.  At least one barrier follows thread
+        // 0's reset of the next tile's counter before any thread moves on.)
+        if (n == 0) __syncthreads();
+        for (int c0 = 0; c0 < n; c0 += CAP) {
+            const int c1 = min(n, c0 + CAP);
+            for (int e = c0 + (int)threadIdx.x; e < c1; e += blockDim.x) {
+                const uint32_t gg = g0 + (uint32_t)q.slot[e];
+                double v = __builtin_nan("");
+                for (uint32_t it = 1; it < kMaxAttempts; ++it) {
+                    const double draw = draw_attempt(L, src, k0, k1, gg, it, rk);
+                    if (L.low <= draw && draw < L.high) {
+                        v = draw;
+                        break;
+                    }
                 }
+                ok = ok && v == v;
+                q.val[e - c0] = v;
             }
-            ok = ok && v == v;
-            q.val[e - c0] = v;
-        }
-        __syncthreads();
+            __syncthreads();
 #pragma unroll
-        for (int r = 0; r < R; ++r)
-            if (pos[r] >= c0 && pos[r] < c1) out[r] = q.val[pos[r] - c0];
-        if (c1 < n) __syncthreads();   // (the next pass reuses val)
+            for (int r = 0; r < R; ++r)
+                if (pos[r] >= c0 && pos[r] < c1) out[r] = q.val[pos[r] - c0];
+            if (c1 < n) __syncthreads();   // (the next pass reuses val)
+        }
     }
     if constexpr ((MODE == DENSE_LGMM || MODE == QUANT_LGMM) && !RAW) {
 #pragma unroll
