@@ -145,6 +145,8 @@ constexpr uint32_t kMaxAttempts = 1u << 16;
 struct SampGlobal {
     const SampRec* __restrict__ s;
     int ns;
+    __device__ __forceinline__ const double* cos_tab() const { return kCosSinTab; }
+    __device__ __forceinline__ const double* log_tab() const { return kLogTab; }
     __device__ __forceinline__ void pick(double u, double& mu, double& sg) const {
         const int k = cdf_search(s, ns, u);
         mu = s[k].mu;
@@ -163,6 +165,13 @@ struct SampLds {
 
 struct SampShared {
     const SampLds* __restrict__ t;
+    // Box-Muller's tables: the constant ones, or a workgroup's LDS copies
+    // (stage_bm_tables: a per-lane gather from LDS instead of through the
+    // vector memory path)
+    const double* cs = kCosSinTab;
+    const double* lg = kLogTab;
+    __device__ __forceinline__ const double* cos_tab() const { return cs; }
+    __device__ __forceinline__ const double* log_tab() const { return lg; }
     __device__ __forceinline__ void pick(double u, double& mu, double& sg) const {
         // (steps is the same for the whole workgroup: a scalar branch)
         const int steps = __builtin_amdgcn_readfirstlane(t->steps);
@@ -223,19 +232,28 @@ __device__ __forceinline__ bool stage_samp(const DLabel& L, const SampRec* __res
     return true;
 }
 
+// a workgroup's LDS copies of Box-Muller's cos/sin and log tables (every
+// thread must call it; a barrier before use -- stage_samp's serves)
+constexpr int kCosTabLen = 2 * (1 << kCosTabBits), kLogTabLen = 2 * (1 << kLogTabBits);
+__device__ __forceinline__ void stage_bm_tables(double* cs, double* lg) {
+    for (int i = threadIdx.x; i < kCosTabLen; i += blockDim.x) cs[i] = kCosSinTab[i];
+    for (int i = threadIdx.x; i < kLogTabLen; i += blockDim.x) lg[i] = kLogTab[i];
+}
+
 // (cos, sin)(2 pi w / 2^32): the top 8 bits' angle a from a 256-entry
 // table (tpe_bm_table.h), the residual t = 2 pi (w mod 2^24) / 2^32 <
 // 2 pi / 256 by its Taylor polynomials (t^10 / 10! < 1e-22), then
 // cos(a + t) = cos a cos t - sin a sin t, sin(a + t) = sin a cos t + cos a
 // sin t -- ~17 VALU operations and one 16-byte load instead of the library
 // sincospi's ~80.
-__device__ __forceinline__ void sincos_turn32(uint32_t w, double& c, double& s) {
+__device__ __forceinline__ void sincos_turn32(uint32_t w, double& c, double& s,
+                                              const double* __restrict__ tab) {
     const int k = (int)(w >> 24);
     const double t = (double)(w & 0xFFFFFFu) * (6.283185307179586 * 0x1.0p-32);
     const double t2 = t * t;
     const double ct = fma(fma(fma(fma(1.0 / 40320.0, t2, -1.0 / 720.0), t2, 1.0 / 24.0), t2, -0.5), t2, 1.0);
     const double st = t * fma(fma(fma(-1.0 / 5040.0, t2, 1.0 / 120.0), t2, -1.0 / 6.0), t2, 1.0);
-    const double ca = kCosSinTab[2 * k], sa = kCosSinTab[2 * k + 1];
+    const double ca = tab[2 * k], sa = tab[2 * k + 1];
     c = fma(ca, ct, -sa * st);
     s = fma(sa, ct, ca * st);
 }
@@ -246,24 +264,24 @@ __device__ __forceinline__ void sincos_turn32(uint32_t w, double& c, double& s) 
 // by its degree-7 Taylor polynomial (r^8 / 8 < 2^-67) -- ~10 fp64
 // operations instead of flog's ~28 (its division); ~1 ulp.  (Only the
 // draw's radius uses it: every log of a candidate or a sum stays flog.)
-__device__ __forceinline__ double bm_neglog(double u) {
+__device__ __forceinline__ double bm_neglog(double u, const double* __restrict__ tab) {
     const uint64_t b = __builtin_bit_cast(uint64_t, u);
     const int e = (int)(b >> 52) - 1023;
     const int j = (int)((b >> 45) & 127u);
     const double m = __builtin_bit_cast(double, (b & 0xFFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
-    const double r = fma(m, kLogTab[2 * j], -1.0);
+    const double r = fma(m, tab[2 * j], -1.0);
     double q = fma(1.0 / 7.0, r, -1.0 / 6.0);
     q = fma(q, r, 0.2);
     q = fma(q, r, -0.25);
     q = fma(q, r, 1.0 / 3.0);
     q = fma(q, r, -0.5);
     q = fma(q, r, 1.0);
-    return -fma((double)e, 6.93147180559945286e-01, fma(r, q, kLogTab[2 * j + 1]));
+    return -fma((double)e, 6.93147180559945286e-01, fma(r, q, tab[2 * j + 1]));
 }
 
-// Box-Muller's radius sqrt(-2 log u) from word y
-__device__ __forceinline__ double bm_radius(uint32_t y) {
-    return __builtin_amdgcn_sqrt(fmax(0.0, 2.0 * bm_neglog(u01_open0(y))));
+// Box-Muller's radius sqrt(-2 log u) from word y (lt: kLogTab or its LDS copy)
+__device__ __forceinline__ double bm_radius(uint32_t y, const double* __restrict__ lt) {
+    return __builtin_amdgcn_sqrt(fmax(0.0, 2.0 * bm_neglog(u01_open0(y), lt)));
 }
 
 // Candidates 2p and 2p + 1 share one Philox4x32-10 call per attempt: the
@@ -279,9 +297,9 @@ __device__ __forceinline__ void draw_pair(const DLabel& L, const Src& src, uint3
     double mu0, sg0, mu1, sg1;
     src.pick((double)r.x * 0x1.0p-32, mu0, sg0);
     src.pick((double)r.z * 0x1.0p-32, mu1, sg1);
-    const double rad = bm_radius(r.y);
+    const double rad = bm_radius(r.y, src.log_tab());
     double c, s;
-    sincos_turn32(r.w, c, s);
+    sincos_turn32(r.w, c, s, src.cos_tab());
     d0 = fma(sg0, rad * c, mu0);
     d1 = fma(sg1, rad * s, mu1);
 }
@@ -293,9 +311,9 @@ __device__ __forceinline__ double draw_attempt(const DLabel& L, const Src& src, 
     const bool h = (g & 1u) != 0;
     double mu, sg;
     src.pick((double)(h ? r.z : r.x) * 0x1.0p-32, mu, sg);
-    const double rad = bm_radius(r.y);
+    const double rad = bm_radius(r.y, src.log_tab());
     double c, s;
-    sincos_turn32(r.w, c, s);
+    sincos_turn32(r.w, c, s, src.cos_tab());
     return fma(sg, rad * (h ? s : c), mu);
 }
 

@@ -831,6 +831,8 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
     const DLabel L = labels[li];
     const BxLabel B = bx[li];
     __shared__ SampLds sl;
+    __shared__ double bm_cs[kCosTabLen], bm_lg[kLogTabLen];
+    stage_bm_tables(bm_cs, bm_lg);    // (made visible by stage_samp's barriers)
     (void)stage_samp(L, samp, &sl);   // (the launch checked ns <= kSampLds)
     const int nsb = B.nbins * kBxSub;
     const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
@@ -866,8 +868,8 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
         // keeps the draw and k_screen_hot applies the exp.  (The family only
         // changes that exp, which RAW leaves out: one instantiation.)
         const uint32_t g0 = (uint32_t)(cand_offset + base);
-        if (!sample_tile<DENSE_GMM, R, SampShared, true, kHotRetry>(L, SampShared{&sl}, seed, rk, g0, pend, x, retry,
-                                                                     par))
+        if (!sample_tile<DENSE_GMM, R, SampShared, true, kHotRetry>(L, SampShared{&sl, bm_cs, bm_lg}, seed, rk, g0,
+                                                                     pend, x, retry, par))
             atomicOr(err, 1);
 #pragma unroll
         for (int r = 0; r < R; ++r) {

@@ -25,7 +25,7 @@ from hyperopt_amd import _build  # noqa: E402
 # name -> [(file, old text, new text)]: result-changing timing experiments
 PATCHES = {
     'bm': [('tpe_device.h',
-            '    return __builtin_amdgcn_sqrt(fmax(0.0, 2.0 * bm_neglog(u01_open0(y))));\n',
+            '    return __builtin_amdgcn_sqrt(fmax(0.0, 2.0 * bm_neglog(u01_open0(y), lt)));\n',
             '    return (double)y * 0x1.0p-31;\n')],
     'lb4': [('tpe_engine.hip', '__launch_bounds__(kBlock, 5) void k_hot_bx(',
              '__launch_bounds__(kBlock, 4) void k_hot_bx(')],
