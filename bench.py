@@ -126,7 +126,48 @@ def parse():
                          '2 labels per rank) or candidate shards (every label, C/N candidates each)')
     ap.add_argument('--dist-backend', default='nccl',
                     help='nccl (RCCL over xGMI); gloo only to rehearse N ranks on one GPU')
+    ap.add_argument('--no-agreement', action='store_true',
+                    help='skip the oracle leg: argmax agreement with the numpy restatement of the '
+                         'reference on the near-ties of one round (oracle/near_ties.py)')
+    ap.add_argument('--no-other-configs', action='store_true',
+                    help='config 3 at N=1: skip the legs of configs 2, 4 and 5 (child processes)')
     return ap.parse_args()
+
+
+def other_configs(args):
+    """BASELINE configs 2, 4 and 5 on the same box, each its own bench.py
+    child process (started before this process touches the GPU; default
+    steps): fresh step, warm round, screened_equals_fp64 and the one-GPU
+    projection of the 8-GPU step from each child's own line."""
+    import subprocess
+    out = {}
+    for cfg in (2, 4, 5):
+        cmd = [sys.executable, os.path.join(REPO, 'bench.py'), '--config', str(cfg), '--steps',
+               str(args.steps), '--warmup', str(args.warmup), '--no-cpu-baseline', '--no-latency']
+        t0 = time.perf_counter()
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=REPO)
+        except subprocess.TimeoutExpired:
+            out['config%d' % cfg] = {'error': 'timed out after 300 s'}
+            continue
+        wall = time.perf_counter() - t0
+        lines = [l for l in r.stdout.splitlines() if l.startswith('{')]
+        if r.returncode != 0 or not lines:
+            out['config%d' % cfg] = {'error': 'rc %d' % r.returncode, 'stderr_tail': r.stderr[-400:]}
+            continue
+        d = json.loads(lines[-1])
+        st, pr = d.get('step') or {}, d.get('scaling_projection') or {}
+        out['config%d' % cfg] = {
+            'workload': d['config']['workload'], 'value': d['value'], 'unit': d['unit'],
+            'fresh_step_ms': round(d['ms_per_step'], 3), 'warm_round_ms': st.get('warm_round_ms'),
+            'expansion_index_ms': st.get('expansion_index_ms'),
+            'screened_equals_fp64': d.get('screened_equals_fp64'),
+            'projected_8gpu_efficiency_fresh': pr.get('projected_8gpu_efficiency_fresh'),
+            'projected_8gpu_efficiency_warm': pr.get('projected_8gpu_efficiency_warm'),
+            'projection_partition': pr.get('partition'),
+            'rescored_per_step': (d.get('screen') or {}).get('rescored_per_step'),
+            'child_wall_s': round(wall, 1)}
+    return out
 
 
 def cpu_baseline_numpy(posts, n_cand):
@@ -181,6 +222,24 @@ def cpu_baseline_c(eng, posts, n_cand, seed, rnd):
         C.broadcast_best_index(lb, la)
     dt = time.perf_counter() - t0
     return evals / dt, dt, evals, C.threads()
+
+
+def near_tie_leg(eng, hist_full, res, seed, rnd, C):
+    """Oracle leg (test infra, untimed): the round `res` (a warm step on the
+    last fresh posterior) against the numpy restatement of the reference --
+    per label numpy's broadcast_best argmax over the round's candidates (the
+    64 best by HIP fp64 score re-scored in numpy for dense labels, every
+    distinct value for quantized and categorical ones) must be the winner."""
+    from oracle import near_ties as NT
+    t0 = time.perf_counter()
+    posts = NT.posteriors_of(eng, hist_full.labels)
+    cells = NT.round_agreement(eng, posts, res, seed, rnd, C)
+    d = NT.summary(cells)
+    d.update({'round': rnd, 'seed': seed, 'wall_s': round(time.perf_counter() - t0, 1),
+              'note': 'per (round, label) cell: the winner equals numpy\'s argmax (oracle/near_ties.py); '
+                      'numpy_top2_gap = numpy\'s own best-minus-second score among the near-ties, '
+                      'max_abs_hip_minus_numpy = the largest |HIP fp64 - numpy| score difference seen'})
+    return d
 
 
 def config1_fmin(n_reps=3):
@@ -259,6 +318,10 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    others = None
+    if (world == 1 and args.config == 3 and not args.devices and not args.no_other_configs
+            and args.precision == 'f64' and args.labels == 32 and args.cand_log2 == 24):
+        others = other_configs(args)   # (child processes, before this one touches the GPU)
     import torch
     dist = None
     if world > 1:
@@ -440,6 +503,12 @@ def main():
         eng.set_option('screen', 1)
         same = all(results[k].view(np.uint8).tobytes() == ures[k].view(np.uint8).tobytes() for k in ures)
         unscreened = (same, udt, nu, first)
+    # oracle leg (untimed): the first warm round against numpy's argmax, on
+    # the posterior that produced it (before the projection advances it)
+    agree_leg = None
+    if (rank == 0 and world == 1 and devs is None and not args.no_agreement and fresh_mode
+            and args.config in (2, 3, 4) and args.precision == 'f64' and warm_first in results):
+        agree_leg = near_tie_leg(eng, hist_full, results[warm_first], 1234 + warm_first, warm_first, C)
     # device memory after the timed steps: the library's buffers (their
     # high-water mark: they grow by 1/4 and are kept) and the whole device
     free_b, total_b = torch.cuda.mem_get_info()
@@ -748,6 +817,10 @@ def main():
                 'sample': 'all %d labels x %d candidates sampled, scored and argmaxed by the '
                           'numpy restatement (oracle/tpe_oracle.py); %.1f s, %.3g evals'
                           % (L, args.cpu_sample, nsec, nev)}}
+    if agree_leg is not None:
+        line['oracle_near_tie_agree'] = agree_leg
+    if others is not None:
+        line['other_configs'] = others
     if rank == 0:
         print(json.dumps(line), flush=True)
     eng.close()

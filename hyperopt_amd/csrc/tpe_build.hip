@@ -1295,6 +1295,22 @@ int history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial,
 // right after a build of the same history with the same arguments, whose
 // below set it reuses (so no below_h); the caller's labels are those whose
 // mixtures depend on an order the previous build did not have.
+constexpr int32_t kGammaCap = 25;   // ap_filter_trials(gamma_cap=DEFAULT_LF), tpe.py:35, 626
+
+// 64-bit fingerprint of the losses' bit patterns (NaN payloads included):
+// a label-subset rebuild reuses the device copy of the previous build's
+// losses and below set, so it must be handed the same losses
+uint64_t loss_fingerprint(const double* losses, int64_t n) {
+    uint64_t h = 0x9e3779b97f4a7c15ull ^ (uint64_t)n;
+    for (int64_t t = 0; t < n; ++t) {
+        uint64_t v;
+        std::memcpy(&v, losses + t, sizeof(v));
+        h = (h ^ v) * 0xff51afd7ed558ccdull;
+        h ^= h >> 29;
+    }
+    return h;
+}
+
 int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t n_valid,
                    double gamma, double prior_weight, int32_t lf, int32_t* n_below_out,
                    const uint8_t* below_h = nullptr, const int64_t* order_off_h = nullptr,
@@ -1310,6 +1326,9 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
             B.built_gamma != gamma || B.built_pw != prior_weight || B.built_lf != lf ||
             B.n_labels != (int32_t)B.specs_h.size())
             return ctx->fail(TPE_ERR_ARG, "a label-subset rebuild must follow a build of the same history");
+        if (n_trials > 0 && !losses) return ctx->fail(TPE_ERR_ARG, "tpe_build_posterior: bad trial arguments");
+        if (loss_fingerprint(losses, n_trials) != B.built_loss_hash)
+            return ctx->fail(TPE_ERR_ARG, "a label-subset rebuild must be given the previous build's losses");
         for (int32_t i = 0; i < n_only; ++i)
             if (only_h[i] < 0 || only_h[i] >= B.n_labels || (i && only_h[i] <= only_h[i - 1]))
                 return ctx->fail(TPE_ERR_ARG, "subset labels must be increasing label indices");
@@ -1325,9 +1344,11 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     ctx->P = &ctx->resident;
     hipStream_t st = ctx->stream;
 
-    // n_below = min(ceil(gamma sqrt(len(l_vals))), gamma_cap)   tpe.py:636
+    // n_below = min(ceil(gamma sqrt(len(l_vals))), gamma_cap)   tpe.py:636 --
+    // gamma_cap is ap_filter_trials' default DEFAULT_LF (tpe.py:626), which
+    // build_posterior never overrides: independent of the linear forgetting
     const double nbd = std::ceil(gamma * std::sqrt((double)n_valid));
-    const int32_t n_below = (int32_t)std::min<double>(nbd, (double)lf);
+    const int32_t n_below = (int32_t)std::min<double>(nbd, (double)kGammaCap);
     if (below_h) {   // a supplied below set: n_below trials, each with a loss
         int64_t nb = 0;
         for (int64_t t = 0; t < n_trials; ++t)
@@ -1496,6 +1517,7 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     B.built_gamma = gamma;
     B.built_pw = prior_weight;
     B.built_lf = lf;
+    if (!subset) B.built_loss_hash = loss_fingerprint(losses, n_trials);
     if (n_below_out) *n_below_out = n_below;
     return TPE_OK;
 }

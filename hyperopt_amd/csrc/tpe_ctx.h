@@ -289,6 +289,7 @@ struct BuildBufs {
     int64_t built_T = -1, built_valid = -1;
     double built_gamma = 0.0, built_pw = 0.0;
     int32_t built_lf = 0;
+    uint64_t built_loss_hash = 0;  // fingerprint of the losses (a subset rebuild reuses them)
     DevBuf<int32_t> only;          // the labels of a subset rebuild
     void release() {
         specs.release(); cat_p.release(); p_off.release(); cnt.release(); p_trial.release();

@@ -832,7 +832,7 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
     const BxLabel B = bx[li];
     __shared__ SampLds sl;
     __shared__ double bm_cs[kCosTabLen], bm_lg[kLogTabLen];
-    stage_bm_tables(bm_cs, bm_lg);    // (made visible by stage_samp's barriers)
+    stage_bm_tables(bm_cs, bm_lg);    // (visible after the __syncthreads below, whatever stage_samp does)
     (void)stage_samp(L, samp, &sl);   // (the launch checked ns <= kSampLds)
     const int nsb = B.nbins * kBxSub;
     const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
@@ -851,7 +851,7 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
         retry.n[0] = retry.n[1] = 0;
         buf_n = 0;
     }
-    __syncthreads();
+    __syncthreads();   // the Box-Muller tables, the bits and the counters above
     const int lane = threadIdx.x & 63;
     const uint64_t lt = (1ull << lane) - 1ull;
     int par = 0;

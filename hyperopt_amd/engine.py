@@ -65,6 +65,20 @@ def bounds_flags(low, high, q):
     return f
 
 
+DEFAULT_LF = 25   # tpe.py:35: adaptive_parzen_normal's LF and ap_filter_trials' gamma_cap
+
+
+def _check_lf(lf):
+    """The builds cap n_below at gamma_cap = DEFAULT_LF (tpe.py:626, 636)
+    and weight the Parzen components with linear forgetting `lf`
+    (tpe.py:406): with lf >= DEFAULT_LF every below mixture keeps equal
+    weights, the only case in which the reference (and so the tie order it
+    fixes) is defined -- tpe.suggest never passes another."""
+    if int(lf) < DEFAULT_LF:
+        raise ValueError('linear forgetting %d < gamma_cap %d: a below mixture would depend on '
+                         'the order of its observations' % (int(lf), DEFAULT_LF))
+
+
 def _devices(device):
     if isinstance(device, (list, tuple)):
         if not device:
@@ -136,6 +150,7 @@ class Engine(object):
         of ties (posterior.build_reference_order); 'position': one
         tpe_build_posterior call, ties by position.  Returns n_below."""
         from . import posterior as _post
+        _check_lf(lf)
         specs = np.ascontiguousarray(specs, dtype=SPEC_DTYPE)
         cat_p = _f64(cat_p)
         losses = _f64(losses)
@@ -181,6 +196,7 @@ class Engine(object):
     def build_posterior_resident(self, losses, n_valid, gamma, prior_weight, lf=25):
         """Rebuild the posterior from the resident history; losses per trial
         position, NaN for a trial outside the history.  Returns n_below."""
+        _check_lf(lf)
         losses = _f64(losses)
         nb = ctypes.c_int32()
         self._check(self.lib.tpe_build_posterior_resident(
@@ -198,6 +214,7 @@ class Engine(object):
         ties[l] bit 1 (bit 0) when label l's above (below) mixture depends on
         a tie order that was not supplied, ties[-1] when equal losses
         straddle the split."""
+        _check_lf(lf)
         losses = _f64(losses)
         L_ = self.hist_labels
         if below is not None:
@@ -221,6 +238,7 @@ class Engine(object):
         """The ordered rebuild of `labels` only (tpe_rebuild_labels), right
         after a build of the same history and arguments; the other labels
         and the below set are kept.  Returns (n_below, ties)."""
+        _check_lf(lf)
         losses = _f64(losses)
         L_ = self.hist_labels
         order_off = np.ascontiguousarray(order_off, dtype=np.int64)

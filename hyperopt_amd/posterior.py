@@ -14,6 +14,7 @@ same order, including the default, non-stable np.argsort tie order):
   categorical   pseudocount posteriors        tpe.py:581-617
 It is vectorised over the history (no per-trial Python loops).
 """
+import threading
 import weakref
 
 import numpy as np
@@ -244,9 +245,11 @@ def spec_table(labels, streams=None):
     return specs, (np.concatenate(cat_p) if cat_p else np.zeros(0)), trs
 
 
-def n_below_of(n_valid, gamma, lf=DEFAULT_LF):
-    """min(ceil(gamma sqrt(len(l_vals))), gamma_cap), tpe.py:636."""
-    return int(min(np.ceil(gamma * np.sqrt(n_valid)), lf))
+def n_below_of(n_valid, gamma, gamma_cap=DEFAULT_LF):
+    """min(ceil(gamma sqrt(len(l_vals))), gamma_cap), tpe.py:636 (gamma_cap
+    is ap_filter_trials' default DEFAULT_LF, :626, independent of the linear
+    forgetting)."""
+    return int(min(np.ceil(gamma * np.sqrt(n_valid)), gamma_cap))
 
 
 def reference_orders(losses, n_below, obs_of, labels):
@@ -311,18 +314,23 @@ def reference_orders(losses, n_below, obs_of, labels):
 
 _POOL_MIN = 1 << 14   # observations to sort (over several labels), from which the pool pays
 _pool = None
+_pool_lock = threading.Lock()
 
 
 def _sort_pool():
+    """The process's one argsort pool (created once, also under concurrent
+    tpe.suggest callers: each thread has its own engine, not its own pool)."""
     global _pool
     if _pool is None:
-        import os
-        from concurrent.futures import ThreadPoolExecutor
-        try:   # the CPUs this process may run on (a GPU box's share), at most 16
-            ncpu = len(os.sched_getaffinity(0))
-        except (AttributeError, OSError):
-            ncpu = os.cpu_count() or 2
-        _pool = ThreadPoolExecutor(max_workers=max(1, min(16, ncpu)))
+        with _pool_lock:
+            if _pool is None:
+                import os
+                from concurrent.futures import ThreadPoolExecutor
+                try:   # the CPUs this process may run on (a GPU box's share), at most 16
+                    ncpu = len(os.sched_getaffinity(0))
+                except (AttributeError, OSError):
+                    ncpu = os.cpu_count() or 2
+                _pool = ThreadPoolExecutor(max_workers=max(1, min(16, ncpu)))
     return _pool
 
 
@@ -351,7 +359,7 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
       index is queued after the one build.
 
     Returns (n_below, the labels that needed an order)."""
-    n_below = n_below_of(n_valid, gamma, lf)
+    n_below = n_below_of(n_valid, gamma)
     known = set(known)
     if prepare and (overlap or not known):
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf)
@@ -369,7 +377,7 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
     if np.any(ties[:-1] & 1):
         # a below mixture holds at most gamma_cap <= lf observations: its
         # weights are all equal, so its order can never matter
-        raise AssertionError('below mixture depends on a tie order (n_below > lf?)')
+        raise AssertionError('below mixture depends on a tie order (lf < gamma_cap?)')
     need = have | set(np.flatnonzero(ties[:-1] & 2).tolist())
     if need != have or ties[-1]:
         below, off, order = reference_orders(losses, n_below, obs_of, need)

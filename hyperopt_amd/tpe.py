@@ -24,10 +24,14 @@ multi-device context splits every round over those GPUs, same documents as
 one GPU; tpe_ctx_create_multi), `batch` (True: one independent
 suggestion per new_id instead of only new_ids[0]), `posterior_builder`:
 'host' (numpy, posterior.py -- the reference's own np.argsort tie order),
-'device' (tpe_build_posterior on the GPU: split, sort, Parzen and fold in
-HIP kernels, ties ordered by position) or 'auto' (device once the history
-holds DEVICE_BUILD_MIN_OBS observations over all labels, where the host build
-starts to dominate the suggestion).
+'device' (the GPU build: split, sort, Parzen and fold in HIP kernels on the
+device-resident history; the device flags every mixture whose value depends
+on the order of tied losses or observations, and for exactly those the host
+supplies numpy's np.argsort orders and the device builds again --
+posterior.build_reference_order -- so the mixtures are the host build's bit
+for bit) or 'auto' (device once the history holds DEVICE_BUILD_MIN_OBS
+observations over all labels, where the host build starts to dominate the
+suggestion).
 """
 import logging
 import time
@@ -194,10 +198,14 @@ def suggest(new_ids, domain, trials, seed,
     * batch=True -- the documents K sequential calls suggest([new_ids[j]],
       domain, trials, seed) would return with `trials` unchanged between
       them: one posterior, the batch's other suggestions excluded from it;
-    * batch='pending' -- the documents K sequential calls return when each
-      call's document is inserted into the trials, still pending, before the
-      next call (the reference's view of queued trials: loss None -> +inf,
-      tpe.py:844-847; fmin with max_queue_len, fmin.py:193-202).
+    * batch='pending' -- past the startup phase, the documents K sequential
+      calls return when each call's document is inserted into the trials,
+      still pending, before the next call (the reference's view of queued
+      trials: loss None -> +inf, tpe.py:844-847; fmin with max_queue_len,
+      fmin.py:193-202).  The first k = n_startup_jobs - len(docs) ids (the
+      calls that would still be in the startup phase) are answered by ONE
+      rand.suggest(new_ids[:k], ...) call -- distinct draws, as the
+      reference answers a startup batch -- not by k sequential calls.
 
     During the startup phase (fewer than n_startup_jobs documents) the
     reference's rand.suggest(new_ids, ...) answers, for every new_id.

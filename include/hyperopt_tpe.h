@@ -209,9 +209,12 @@ int tpe_set_posterior(tpe_ctx *ctx, const tpe_label_desc *labels, int32_t n_labe
  *   per label l, observations obs_off[l] .. obs_off[l+1]-1 in tid order:
  *       obs_trial = position t of the observation's trial in `losses`,
  *       obs_val   = the (already transformed, TPE_OBS_*) value;
- *   gamma, prior_weight: the tpe.suggest arguments; lf: linear forgetting
- *       (25 in the reference, DEFAULT_LF tpe.py:29 and gamma_cap :636).
- * The below set is the n_below = min(ceil(gamma sqrt(n_trials)), lf) lowest
+ *   gamma, prior_weight: the tpe.suggest arguments; lf: the linear
+ *       forgetting of the Parzen weights (adaptive_parzen_normal's LF,
+ *       tpe.py:406; 25 = DEFAULT_LF in the reference, which never passes
+ *       another -- tpe.suggest's linear_forgetting is unused, :828).
+ * The below set is the n_below = min(ceil(gamma sqrt(n_trials)), 25) lowest
+ * (gamma_cap = DEFAULT_LF, tpe.py:626,636, whatever lf is)
  * losses; equal losses and equal observations are ordered by position
  * (a stable sort; the reference's np.argsort order for ties is numpy's
  * unstable quicksort -- tpe_build_posterior_resident_ordered takes the

@@ -108,6 +108,30 @@ def test_batch_pending_startup_phase_draws_distinct_documents():
 
 
 @pytest.mark.gpu
+def test_batch_pending_crossing_the_startup_phase():
+    """a 'pending' batch that starts 2 documents short of
+    n_startup_jobs: the first 2 ids are ONE rand.suggest(new_ids[:2]) call,
+    the others sequential TPE calls that see every earlier suggestion of the
+    batch as a pending trial."""
+    trials = _history(18, 7)
+    dom = H.Domain(_loss, SPACE)
+    ids = [3000, 3001, 3002, 3003, 3004]
+    pend = tpe.suggest(ids, dom, trials, 11, batch='pending')
+    assert [d['tid'] for d in pend] == ids
+    assert _vals(pend[:2]) == _vals(H.rand.suggest(ids[:2], dom, trials, 11))
+    seq_trials = copy.deepcopy(trials)
+    seq_trials.insert_trial_docs(copy.deepcopy(pend[:2]))
+    seq_trials.refresh()
+    seq = []
+    for i in ids[2:]:
+        d = tpe.suggest([i], dom, seq_trials, 11)
+        seq_trials.insert_trial_docs(d)
+        seq_trials.refresh()
+        seq.extend(d)
+    assert _vals(pend[2:]) == _vals(seq)
+
+
+@pytest.mark.gpu
 def test_tpe_from_scratch_without_startup():
     """n_startup_jobs=0 on an empty history: TPE on the prior-only
     posterior (tpe.py:877-880), not random search."""

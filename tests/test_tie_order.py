@@ -171,6 +171,10 @@ def test_label_subset_rebuild_equals_full_rebuild():
             nb2, ties2 = eng.rebuild_labels(losses, n_valid, 0.25, 1.0, 25, o_off, order, need)
             with pytest.raises(EngineError):   # different arguments
                 eng.rebuild_labels(losses, n_valid, 0.3, 1.0, 25, o_off, order, need)
+            changed = losses.copy()            # one loss changed, same length
+            changed[int(np.flatnonzero(changed == changed)[0])] += 1.0
+            with pytest.raises(EngineError):
+                eng.rebuild_labels(changed, n_valid, 0.25, 1.0, 25, o_off, order, need)
         else:
             nb2, ties2 = eng.build_posterior_ordered(losses, n_valid, 0.25, 1.0, 25, below, o_off, order)
         assert nb2 == nb and not np.any(ties2)
