@@ -51,6 +51,8 @@ TPE_OPT_HOT = 12
 TPE_OPT_EARLY = 13
 TPE_OPT_HOT_DIV = 14
 TPE_OPT_ZERO_WIN = 15
+TPE_OPT_VALUE_ONLY = 16
+TPE_OPT_RESCORE_CAP = 17
 
 TPE_OBS_IDENTITY = 0
 TPE_OBS_LOG = 1

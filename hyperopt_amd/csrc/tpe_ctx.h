@@ -22,6 +22,13 @@ namespace tpe_rt {
 struct RescoreChunkH {   // k_rescore work item: (round * labels + label position, chunk)
     int32_t cell, j;
 };
+// the re-score's plan, made on the device (k_rescore_plan): candidates to
+// re-score, table entries, sliced or chunked, and whether the candidates
+// exceed the buffers the host sized (the round then runs again)
+struct RescorePlanH {
+    int64_t total;
+    int32_t ne, sliced, overflow, pad;
+};
 
 using tpe::Comp;
 using tpe::DLabel;
@@ -142,6 +149,7 @@ struct PinVec {
 struct PinScalars {
     int32_t err = 0, hot_flag = 0, bx_diff = 1, pad = 0;
     unsigned long long screen_exec = 0, xdrawn[2] = {0, 0};
+    RescorePlanH plan{};   // the packed map's re-score plan of the last round
 };
 
 struct Posterior {
@@ -393,6 +401,13 @@ struct tpe_ctx {
     int64_t hot_listed = 0;              // last round: candidates the prefilter listed
     int32_t hot_fallback = 0;            // last round: 1 if it re-ran the plain screen
     bool hot_ran = false;
+    int64_t hot_cells = 0;               //   cells of its lists (hot_cnt_h, read after the round's sync)
+    bool hot_redo = false;               // the round runs again without the prefilter (its check failed)
+    DevBuf<int64_t> rs_plan;             // the re-score's plan (k_rescore_plan: total, entries, sliced)
+    bool value_only = false;             // TPE_OPT_VALUE_ONLY: packed rounds skip the lpdfs of certified winners
+    int64_t pk_cap = 1 << 16;            // packed re-score: candidates its buffers hold (grows)
+    bool pk_plan_pending = false;        // the packed plan awaits the round's sync
+    bool pk_redo = false;                // the round runs again after a plan overflow
     float prep_ms = 0.f;                 // device ms of the last expansion-index build (bx_prepare)
     hipEvent_t ev_prep[2] = {};          //   its bracket, read when asked (tpe_last_prepare)
     bool prep_pending = false;
@@ -411,6 +426,7 @@ struct tpe_ctx {
     DevBuf<Partial> scr_res;             //   their fp64 results
     DevBuf<int64_t> scr_rsel;            //   per (round, label): {first, count} int32 pairs
     DevBuf<int64_t> scr_off;             //   per label: offset of its entries in the compacted order
+    DevBuf<int64_t> scr_range;           //   per label: its range of re-score table entries
     DevBuf<double> scr_planes;           //   re-score sums: below | x | above chunk c, per entry
     DevBuf<double> rs_x, rs_part;        // sliced re-score: candidates, slice sums
     DevBuf<int64_t> rs_g;                //   and their global indices

@@ -1124,6 +1124,7 @@ using RescoreChunk = tpe_rt::RescoreChunkH;
 constexpr int kRescoreR = TPE_RESCORE_R;
 // at most this many candidates to re-score in a round: split by slices
 constexpr int64_t kSlicedRescoreMax = 1 << 16;
+constexpr int kRsW = 64;   // candidates per sliced re-score entry (one per lane)
 
 // candidates per thread in k_screen (its own tile width): the component's
 // m shared by more candidates costs fewer v_mov_b64 per eval
@@ -1154,22 +1155,112 @@ constexpr int kQR = 8;   // candidates per thread, k_qfused_tiles
 constexpr int kQLdsKeys = 1024;   // grid values whose keys k_qfused_tiles stages in LDS
 constexpr int kCatR = 8;  // candidates per thread, k_cat_tiles
 
+// The re-score's work table, built on the device from the cells' counts --
+// no read-back in the middle of a round (the mid-round sync was
+// fixed latency of every round).  total = the sum of the counts; the
+// re-score is `sliced` (one wave per kRsW candidates and summation slice)
+// when total <= kSlicedRescoreMax, otherwise chunks of `per_full` candidates
+// per workgroup (packed map: always chunks).  Per cell: its range of entries
+// (first << 32 | count) and the offset of its candidates in the cell order
+// (eoff[cells] = total); the entries {cell, j} in cell order.  One workgroup
+// of kPlanBlock threads; the re-score kernels read `plan` and stride over
+// its entries with grids sized for the largest table.
+using RescorePlan = tpe_rt::RescorePlanH;
+constexpr int kPlanBlock = 1024;
+__global__ __launch_bounds__(kPlanBlock) void k_rescore_plan(const int32_t* __restrict__ cnt, int64_t cells,
+                                                             int32_t per_full, int32_t allow_sliced, int64_t cap,
+                                                             RescoreChunk* __restrict__ chunks,
+                                                             int64_t* __restrict__ range, int64_t* __restrict__ eoff,
+                                                             RescorePlan* __restrict__ plan) {
+    constexpr int W = kPlanBlock / 64;
+    __shared__ int64_t wsum[W];
+    __shared__ int64_t tot_sh;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int64_t t = 0;
+    for (int64_t c = threadIdx.x; c < cells; c += kPlanBlock) t += cnt[c];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+    if (lane == 0) wsum[wave] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t a = 0;
+        for (int w = 0; w < W; ++w) a += wsum[w];
+        tot_sh = a;
+    }
+    __syncthreads();
+    const int64_t total = tot_sh;
+    if (total > cap) {   // more than the buffers hold: no entries, the host re-runs the round
+        if (threadIdx.x == 0) *plan = RescorePlan{total, 0, 0, 1, 0};
+        return;
+    }
+    const bool sliced = allow_sliced && total <= kSlicedRescoreMax;
+    const int64_t per = sliced ? (int64_t)kRsW : (int64_t)per_full;
+    int64_t carry = 0, ecarry = 0;   // entries and candidates before this block of cells
+    for (int64_t c0 = 0; c0 < cells; c0 += kPlanBlock) {
+        __syncthreads();   // (wsum reuse)
+        const int64_t c = c0 + threadIdx.x;
+        const int64_t k = c < cells ? (int64_t)cnt[c] : 0;
+        const int64_t nc = (k + per - 1) / per;
+        // inclusive scans of (entries, candidates) over the block
+        int64_t se = nc, sk = k;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t oe = __shfl_up(se, o), ok = __shfl_up(sk, o);
+            if (lane >= o) {
+                se += oe;
+                sk += ok;
+            }
+        }
+        __shared__ int64_t wk[W];
+        if (lane == 63) {
+            wsum[wave] = se;
+            wk[wave] = sk;
+        }
+        __syncthreads();
+        int64_t be = 0, bk = 0, te = 0, tk = 0;
+        for (int w = 0; w < W; ++w) {
+            if (w < wave) {
+                be += wsum[w];
+                bk += wk[w];
+            }
+            te += wsum[w];
+            tk += wk[w];
+        }
+        if (c < cells) {
+            const int64_t first = carry + be + se - nc;
+            range[c] = (first << 32) | nc;
+            if (eoff) eoff[c] = ecarry + bk + sk - k;
+            for (int64_t j = 0; j < nc; ++j) chunks[first + j] = RescoreChunk{(int32_t)c, (int32_t)j};
+        }
+        carry += te;
+        ecarry += tk;
+    }
+    if (threadIdx.x == 0) {
+        if (eoff) eoff[cells] = ecarry;
+        *plan = RescorePlan{total, (int32_t)carry, sliced ? 1 : 0, 0, 0};
+    }
+}
+
 template <int R>
 __global__ __launch_bounds__(kBlock) void k_rescore(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
     const Comp<double>* __restrict__ comps64, const SampRec* __restrict__ samp, int64_t stride,
     int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, int32_t nl,
     int32_t n_labels, int32_t tiles, const int32_t* __restrict__ cnt, const int32_t* __restrict__ idx,
-    const RescoreChunk* __restrict__ chunks, Partial* __restrict__ res) {
-    const RescoreChunk ch = chunks[blockIdx.x];
+    const RescoreChunk* __restrict__ chunks, const RescorePlan* __restrict__ plan, Partial* __restrict__ res) {
+    if (plan->sliced) return;   // (uniform: the sliced kernels take this round)
+    const int32_t ne = plan->ne;
+    if ((int32_t)blockIdx.x >= ne) return;
+    __shared__ double exp_tab[kExpTabSize];
+    load_exp_table(exp_tab);
+    for (int32_t e = blockIdx.x; e < ne; e += gridDim.x) {
+    const RescoreChunk ch = chunks[e];
     const int32_t z = ch.cell / nl, y = ch.cell % nl;
     const int li = group[y];
     const int64_t count = cnt[ch.cell];
     constexpr int64_t per = (int64_t)R * kBlock;
     const int64_t base = (int64_t)ch.j * per;
     const DLabel L = labels[li];
-    __shared__ double exp_tab[kExpTabSize];
-    load_exp_table(exp_tab);
     const bool lgmm = L.mode == DENSE_LGMM;
     const int32_t* list = idx + (size_t)ch.cell * (size_t)stride;
     const uint32_t rk = rounds[z];
@@ -1211,8 +1302,10 @@ __global__ __launch_bounds__(kBlock) void k_rescore(
         }
     }
     __shared__ Partial sh[kBlock / 64];
-    block_maxloc(bk, bi, bv, bl, ba, res + blockIdx.x, sh);
+    block_maxloc(bk, bi, bv, bl, ba, res + e, sh);
+    __syncthreads();   // (sh is read by thread 0 before the next entry writes it)
     (void)z;
+    }
 }
 
 // The re-score of a few candidates per (round, dense label) -- the
@@ -1223,17 +1316,20 @@ __global__ __launch_bounds__(kBlock) void k_rescore(
 // candidates of a table entry per wave, and k_rescore_fin adds the slices in
 // order (lse_acc's order: the bits of the fp64 round) and keeps the entry's
 // best.  Entry = RescoreChunk{cell, j}: candidates [64 j, 64 j + 64) of the
-// cell's list.  part: [entry][s_max slices][64].
-constexpr int kRsW = 64;
+// cell's list.  part: [entry][s_max slices][64].  The entries come from
+// k_rescore_plan; the kernels stride over them (grids sized for the largest
+// table) and leave a round whose plan is not sliced to k_rescore.
 
 __global__ __launch_bounds__(kBlock) void k_rescore_draw(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
     const SampRec* __restrict__ samp, int64_t stride, int64_t cand_offset, uint64_t seed,
-    const uint32_t* __restrict__ rounds, int32_t nl, int32_t n_entries, const int32_t* __restrict__ cnt,
-    const int32_t* __restrict__ idx, const RescoreChunk* __restrict__ chunks, double* __restrict__ xbuf,
-    int64_t* __restrict__ gbuf) {
-    const int e = blockIdx.x * (kBlock / kRsW) + threadIdx.x / kRsW, lane = threadIdx.x % kRsW;
-    if (e >= n_entries) return;
+    const uint32_t* __restrict__ rounds, int32_t nl, const RescorePlan* __restrict__ plan,
+    const int32_t* __restrict__ cnt, const int32_t* __restrict__ idx, const RescoreChunk* __restrict__ chunks,
+    double* __restrict__ xbuf, int64_t* __restrict__ gbuf) {
+    if (!plan->sliced) return;
+    const int32_t ne = plan->ne;
+    const int lane = threadIdx.x % kRsW;
+    for (int e = blockIdx.x * (kBlock / kRsW) + threadIdx.x / kRsW; e < ne; e += gridDim.x * (kBlock / kRsW)) {
     const RescoreChunk ch = chunks[e];
     const int32_t z = ch.cell / nl, y = ch.cell % nl;
     const DLabel L = labels[group[y]];
@@ -1247,20 +1343,26 @@ __global__ __launch_bounds__(kBlock) void k_rescore_draw(
     }
     xbuf[(size_t)e * kRsW + lane] = v;
     gbuf[(size_t)e * kRsW + lane] = g;
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_rescore_slices(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
     const Comp<double>* __restrict__ comps64, int32_t nl, const RescoreChunk* __restrict__ chunks,
-    const double* __restrict__ xbuf, int32_t s_max, double* __restrict__ part) {
+    const RescorePlan* __restrict__ plan, const double* __restrict__ xbuf, int32_t s_max,
+    double* __restrict__ part) {
+    if (!plan->sliced) return;
+    const int32_t ne = plan->ne;
+    if ((int32_t)blockIdx.y >= ne) return;   // (uniform, before the table's barrier)
     __shared__ double exp_tab[kExpTabSize];
     load_exp_table(exp_tab);   // (every wave takes part before any leaves)
-    const int e = blockIdx.y, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int e = blockIdx.y; e < ne; e += gridDim.y) {
     const RescoreChunk ch = chunks[e];
     const DLabel L = labels[group[ch.cell % nl]];
     const int nsb = (L.nb + kSumSlice - 1) / kSumSlice, nsa = (L.na + kSumSlice - 1) / kSumSlice;
     const int slice = blockIdx.x * (kBlock / 64) + wave;
-    if (slice >= nsb + nsa) return;
+    if (slice >= nsb + nsa) continue;   // (no barrier below)
     const bool above = slice >= nsb;
     const int k0 = (above ? slice - nsb : slice) * kSumSlice;
     const int k1 = min(k0 + kSumSlice, above ? L.na : L.nb);
@@ -1269,14 +1371,18 @@ __global__ __launch_bounds__(kBlock) void k_rescore_slices(
     double acc[1] = {0.0};
     lse_acc_run<1>(comps64 + (above ? L.comp_a : L.comp_b) + k0, k1 - k0, xr, acc, exp_tab);
     part[((size_t)e * s_max + slice) * kRsW + lane] = acc[0];
+    }
 }
 
 __global__ __launch_bounds__(kRsW) void k_rescore_fin(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
     const Comp<double>* __restrict__ comps64, int32_t nl, const RescoreChunk* __restrict__ chunks,
-    const double* __restrict__ xbuf, const int64_t* __restrict__ gbuf, int32_t s_max,
-    const double* __restrict__ part, Partial* __restrict__ res) {
-    const int e = blockIdx.x, lane = threadIdx.x;
+    const RescorePlan* __restrict__ plan, const double* __restrict__ xbuf, const int64_t* __restrict__ gbuf,
+    int32_t s_max, const double* __restrict__ part, Partial* __restrict__ res) {
+    if (!plan->sliced) return;
+    const int32_t ne = plan->ne;
+    const int lane = threadIdx.x;
+    for (int e = blockIdx.x; e < ne; e += gridDim.x) {
     const RescoreChunk ch = chunks[e];
     const DLabel L = labels[group[ch.cell % nl]];
     const bool lgmm = L.mode == DENSE_LGMM;
@@ -1318,6 +1424,7 @@ __global__ __launch_bounds__(kRsW) void k_rescore_fin(
         }
     }
     if (lane == 0) res[e] = Partial{bk, bi, bv, bl, ba};
+    }
 }
 
 // one thread per (round, dense label) cell: the best of its re-score chunks
@@ -1435,21 +1542,39 @@ __global__ __launch_bounds__(kBlock) void k_pick_packed(
 // (round, label) takes the round's largest lower bound and lists, in
 // candidate order, the candidates whose upper bound reaches it -- the same
 // list and per-round ranges k_pick_packed makes.
+// value_only (TPE_OPT_VALUE_ONLY): a round whose selection is ONE candidate
+// whose lower bound clears every other candidate's upper bound by at least
+// kValueMargin (relative) is decided: it is the argmax under any fp64
+// evaluation of the reference's formulas (the HIP round's, numpy's --
+// rounding moves a score by ~1e-12 at most), so its lpdfs are not computed
+// (rsel = {candidate, -1}; k_pick_rounds re-draws its value, lpdfs NaN).
+constexpr double kValueMargin = 1e-9;
 template <typename P2>
 __global__ __launch_bounds__(kBlock) void k_pick_win(const P2* __restrict__ lohi, int32_t n_rounds,
                                                      int32_t C, int32_t* __restrict__ cnt,
                                                      int64_t* __restrict__ list, int64_t cap,
-                                                     RoundSel* __restrict__ rsel, int32_t nl) {
+                                                     RoundSel* __restrict__ rsel, int32_t nl, int32_t value_only) {
     using V = decltype(lohi->x);
     const int y = blockIdx.y;
     const int64_t z = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const bool valid = z < n_rounds;
     const P2* row = lohi + ((size_t)y * n_rounds + (valid ? z : 0)) * C;
     V m = -(V)__builtin_inf();
-    int k = 0;
+    int k = 0, single = -1;
     if (valid) {
         for (int c = 0; c < C; ++c) m = row[c].x > m ? row[c].x : m;
         for (int c = 0; c < C; ++c) k += row[c].y >= m;
+        if (value_only && k == 1) {
+            double second = -__builtin_inf();
+            int cs = -1;
+            for (int c = 0; c < C; ++c) {
+                if (row[c].y >= m) cs = c;
+                else second = fmax(second, (double)row[c].y);
+            }
+            const double md = (double)m;
+            if (md - second >= kValueMargin * fmax(1.0, fabs(md))) single = cs;   // (NaN: not decided)
+        }
+        if (single >= 0) k = 0;   // nothing to re-score
     }
     __shared__ int sh[kBlock / 64 + 1];
     // exclusive prefix of the counts over the workgroup's rounds
@@ -1474,6 +1599,10 @@ __global__ __launch_bounds__(kBlock) void k_pick_win(const P2* __restrict__ lohi
     __syncthreads();
     if (!valid) return;
     int at = sh[kBlock / 64] + sh[wave] + inc - k;
+    if (single >= 0) {
+        rsel[(size_t)z * nl + y] = RoundSel{single, -1};
+        return;
+    }
     rsel[(size_t)z * nl + y] = RoundSel{at, k};
     for (int c = 0; c < C; ++c)
         if (row[c].y >= m) list[(size_t)y * cap + at++] = (z << 32) | (int64_t)c;
@@ -1652,16 +1781,20 @@ __global__ __launch_bounds__(kBlock) void k_rescore_packed(
     const Comp<double>* __restrict__ comps64, const SampRec* __restrict__ samp,
     int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, int32_t chunk,
     const int32_t* __restrict__ cnt, const int64_t* __restrict__ list, int64_t cap,
-    const RescoreChunk* __restrict__ chunks, const int64_t* __restrict__ off, int64_t total,
-    double* __restrict__ planes, const double* __restrict__ zhi, const double* __restrict__ zlo,
+    const RescoreChunk* __restrict__ chunks, const int64_t* __restrict__ off, const RescorePlan* __restrict__ plan,
+    int64_t total, double* __restrict__ planes, const double* __restrict__ zhi, const double* __restrict__ zlo,
     const int32_t* __restrict__ zwide, const int32_t* __restrict__ zn) {
-    const RescoreChunk ch = chunks[blockIdx.x];
+    if (plan->overflow) return;
+    const int32_t ne = plan->ne;
+    if ((int32_t)blockIdx.x >= ne) return;   // (uniform, before the table's barrier)
+    __shared__ double exp_tab[kExpTabSize];
+    load_exp_table(exp_tab);
+    for (int32_t ei = blockIdx.x; ei < ne; ei += gridDim.x) {
+    const RescoreChunk ch = chunks[ei];
     const int y = ch.cell, c = blockIdx.y;
     const DLabel L = labels[group[y]];
     const int64_t count = cnt[y];
     constexpr int64_t per = (int64_t)R * kBlock;
-    __shared__ double exp_tab[kExpTabSize];
-    load_exp_table(exp_tab);
     const bool lgmm = L.mode == DENSE_LGMM;
     double x[R], xr[R], sb[R], sa[R];
     int64_t e[R];
@@ -1721,15 +1854,19 @@ __global__ __launch_bounds__(kBlock) void k_rescore_packed(
         }
         planes[(size_t)(2 + c) * total + g] = sa[r];
     }
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_finish_rescore(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
     const Comp<double>* __restrict__ comps64, int64_t cand_offset, int32_t nch,
     const int32_t* __restrict__ cnt, const int64_t* __restrict__ list, int64_t cap,
-    const RescoreChunk* __restrict__ chunks, const int64_t* __restrict__ off, int64_t total,
-    const double* __restrict__ planes, Partial* __restrict__ res) {
-    const RescoreChunk ch = chunks[blockIdx.x];
+    const RescoreChunk* __restrict__ chunks, const int64_t* __restrict__ off, const RescorePlan* __restrict__ plan,
+    int64_t total, const double* __restrict__ planes, Partial* __restrict__ res) {
+    if (plan->overflow) return;
+    const int32_t ne = plan->ne;
+    for (int32_t ei = blockIdx.x; ei < ne; ei += gridDim.x) {
+    const RescoreChunk ch = chunks[ei];
     const int y = ch.cell;
     const DLabel L = labels[group[y]];
     const bool lgmm = L.mode == DENSE_LGMM;
@@ -1751,21 +1888,38 @@ __global__ __launch_bounds__(kBlock) void k_finish_rescore(
         const int64_t i = list[(size_t)y * cap + e] & 0xffffffffll;
         res[g] = Partial{order_key(lb - la), cand_offset + i, x, lb, la};
     }
+    }
 }
 
 // one thread per (round, dense label): the best re-scored candidate of the
 // round (its entries are in candidate order) -> the round's partial
-__global__ __launch_bounds__(kBlock) void k_pick_rounds(const int32_t* __restrict__ group, int32_t nl,
+// (a value-only cell, rs.count = -1: its one candidate rs.first is re-drawn,
+// its lpdfs left NaN)
+__global__ __launch_bounds__(kBlock) void k_pick_rounds(const DLabel* __restrict__ labels,
+                                                        const int32_t* __restrict__ group, int32_t nl,
                                                         int32_t n_rounds, int32_t n_labels,
                                                         const RoundSel* __restrict__ rsel,
                                                         const Partial* __restrict__ res,
                                                         const int64_t* __restrict__ off,
+                                                        const RescorePlan* __restrict__ plan,
+                                                        const SampRec* __restrict__ samp, int64_t cand_offset,
+                                                        uint64_t seed, const uint32_t* __restrict__ rounds,
                                                         Partial* __restrict__ partials) {
     const int64_t cell = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (cell >= (int64_t)n_rounds * nl) return;
+    if (cell >= (int64_t)n_rounds * nl || plan->overflow) return;
     const int64_t z = cell / nl;
     const int y = (int)(cell % nl);
     const RoundSel rs = rsel[cell];
+    if (rs.count < 0) {
+        const DLabel L = labels[group[y]];
+        const uint32_t gi = (uint32_t)(cand_offset + rs.first);
+        double v = 0.0;
+        if (L.mode == DENSE_LGMM) (void)sample_below<DENSE_LGMM>(L, samp + L.samp_off, seed, rounds[z], gi, v);
+        else (void)sample_below<DENSE_GMM>(L, samp + L.samp_off, seed, rounds[z], gi, v);
+        partials[(size_t)z * n_labels + group[y]] =
+            Partial{order_key(0.0), cand_offset + rs.first, v, __builtin_nan(""), __builtin_nan("")};
+        return;
+    }
     Partial best{0, INT64_MAX, 0.0, 0.0, 0.0};
     for (int k = 0; k < rs.count; ++k) {
         const Partial& p = res[(size_t)(off[y] + rs.first + k)];
@@ -2887,7 +3041,7 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
         if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
         hipLaunchKernelGGL(k_pick_win<double2>, dim3((unsigned)((a.n_rounds + kBlock - 1) / kBlock), nl),
                            dim3(kBlock), 0, ctx->stream, ctx->bx_lohi.p, a.n_rounds, (int32_t)a.n,
-                           ctx->scr_cnt.p, ctx->scr_list.p, cap, rsel, nl);
+                           ctx->scr_cnt.p, ctx->scr_list.p, cap, rsel, nl, ctx->value_only ? 1 : 0);
         HIPCHK(ctx, hipMemcpyAsync(&ctx->pin[0].screen_exec, ctx->win_evals.p, sizeof(unsigned long long),
                                    hipMemcpyDeviceToHost, ctx->stream));
         ctx->screen_exec_pending = true;
@@ -2906,7 +3060,7 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
         if ((rc = tpe_rt::win_screen(ctx, wa, &sorted))) return rc;
         hipLaunchKernelGGL(k_pick_win<float2>, dim3((unsigned)((a.n_rounds + kBlock - 1) / kBlock), nl),
                            dim3(kBlock), 0, ctx->stream, ctx->win_lohi.p, a.n_rounds, (int32_t)a.n,
-                           ctx->scr_cnt.p, ctx->scr_list.p, cap, rsel, nl);
+                           ctx->scr_cnt.p, ctx->scr_list.p, cap, rsel, nl, ctx->value_only ? 1 : 0);
         HIPCHK(ctx, hipMemcpyAsync(&ctx->pin[0].screen_exec, ctx->win_evals.p, sizeof(unsigned long long),
                                    hipMemcpyDeviceToHost, ctx->stream));
         ctx->screen_exec_pending = true;
@@ -2923,29 +3077,28 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
                            ctx->scr_list.p, cap, rsel, S8);
         ctx->screen_exec += (int64_t)a.n_rounds * a.n * dense_terms(ctx);
     }
+    // the re-score planned on the device (no mid-round read-back): per
+    // label chunks of kRP * 256 listed candidates, buffers for pk_cap of
+    // them (a round listing more runs again with larger ones)
     HIPCHK(ctx, ctx->scr_cnt_h.resize(nl));
     HIPCHK(ctx, hipMemcpyAsync(ctx->scr_cnt_h.data(), ctx->scr_cnt.p, nl * sizeof(int32_t),
                                hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     constexpr int64_t per = (int64_t)kRP * kBlock;
-    std::vector<RescoreChunk>& tab = ctx->scr_chunks_h;
-    tab.clear();
-    std::vector<int64_t> off(nl + 1, 0);
-    for (int y = 0; y < nl; ++y) {
-        off[y + 1] = off[y] + ctx->scr_cnt_h[y];
-        for (int32_t j = 0; (int64_t)j * per < ctx->scr_cnt_h[y]; ++j) tab.push_back(RescoreChunk{y, j});
-    }
-    const int64_t total = std::max<int64_t>(off[nl], 1);
-    HIPCHK(ctx, ctx->scr_res.reserve(total));
+    const int64_t pcap = std::max<int64_t>(1, std::min<int64_t>(ctx->pk_cap, (int64_t)nl * cap));
+    const int64_t ne_max = nl + (pcap + per - 1) / per;
+    HIPCHK(ctx, ctx->scr_res.reserve(pcap));
     HIPCHK(ctx, ctx->scr_off.reserve(nl + 1));
-    HIPCHK(ctx, hipMemcpyAsync(ctx->scr_off.p, off.data(), (nl + 1) * sizeof(int64_t),
-                               hipMemcpyHostToDevice, ctx->stream));
-    if (!tab.empty()) {
-        HIPCHK(ctx, ctx->scr_chunks.reserve(tab.size()));
-        HIPCHK(ctx, ctx->scr_planes.reserve((size_t)(nch + 2) * total));
-        HIPCHK(ctx, hipMemcpyAsync(ctx->scr_chunks.p, tab.data(), tab.size() * sizeof(RescoreChunk),
-                                   hipMemcpyHostToDevice, ctx->stream));
-        const RescoreChunk* tabd = reinterpret_cast<const RescoreChunk*>(ctx->scr_chunks.p);
+    HIPCHK(ctx, ctx->scr_chunks.reserve(ne_max));
+    HIPCHK(ctx, ctx->scr_range.reserve(nl));
+    HIPCHK(ctx, ctx->scr_planes.reserve((size_t)(nch + 2) * pcap));
+    HIPCHK(ctx, ctx->rs_plan.reserve(3));
+    RescoreChunk* tabd = reinterpret_cast<RescoreChunk*>(ctx->scr_chunks.p);
+    RescorePlan* plan = reinterpret_cast<RescorePlan*>(ctx->rs_plan.p);
+    hipLaunchKernelGGL(k_rescore_plan, dim3(1), dim3(kPlanBlock), 0, ctx->stream, ctx->scr_cnt.p, (int64_t)nl,
+                       (int32_t)per, 0, pcap, tabd, ctx->scr_range.p, ctx->scr_off.p, plan);
+    HIPCHK(ctx, hipMemcpyAsync(&ctx->pin[0].plan, plan, sizeof(RescorePlan), hipMemcpyDeviceToHost, ctx->stream));
+    ctx->pk_plan_pending = true;
+    {
         tpe_rt::Posterior& P = *ctx->P;
         if (ctx->zero_win && !P.zw_ready) {   // once per posterior
             HIPCHK(ctx, P.zw_hi.reserve(P.comps64.cap));
@@ -2959,21 +3112,23 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
                                P.zw_wide.p, P.zw_n.p);
             P.zw_ready = true;
         }
-        hipLaunchKernelGGL((k_rescore_packed<kRP>), dim3((unsigned)tab.size(), nch), dim3(kBlock), 0,
+        const unsigned g = (unsigned)std::min<int64_t>(ne_max, 2048);
+        hipLaunchKernelGGL((k_rescore_packed<kRP>), dim3(g, nch), dim3(kBlock), 0,
                            ctx->stream, ctx->P->labels.p, grp, ctx->P->comps64.p, ctx->P->samp.p,
                            a.cand_offset, a.seed, ctx->rounds.p, chunk, ctx->scr_cnt.p,
-                           ctx->scr_list.p, cap, tabd, ctx->scr_off.p, total, ctx->scr_planes.p,
+                           ctx->scr_list.p, cap, tabd, ctx->scr_off.p, plan, pcap, ctx->scr_planes.p,
                            ctx->zero_win ? P.zw_hi.p : nullptr, ctx->zero_win ? P.zw_lo.p : nullptr,
                            P.zw_wide.p, P.zw_n.p);
-        hipLaunchKernelGGL(k_finish_rescore, dim3((unsigned)tab.size()), dim3(kBlock), 0, ctx->stream,
+        hipLaunchKernelGGL(k_finish_rescore, dim3(g), dim3(kBlock), 0, ctx->stream,
                            ctx->P->labels.p, grp, ctx->P->comps64.p, a.cand_offset, nch, ctx->scr_cnt.p,
-                           ctx->scr_list.p, cap, tabd, ctx->scr_off.p, total, ctx->scr_planes.p,
+                           ctx->scr_list.p, cap, tabd, ctx->scr_off.p, plan, pcap, ctx->scr_planes.p,
                            ctx->scr_res.p);
     }
     const int64_t cells = (int64_t)a.n_rounds * nl;
     hipLaunchKernelGGL(k_pick_rounds, dim3((unsigned)((cells + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                       ctx->stream, grp, nl, a.n_rounds, ctx->P->n_labels, rsel, ctx->scr_res.p,
-                       ctx->scr_off.p, ctx->partials.p);
+                       ctx->stream, ctx->P->labels.p, grp, nl, a.n_rounds, ctx->P->n_labels, rsel, ctx->scr_res.p,
+                       ctx->scr_off.p, plan, ctx->P->samp.p, a.cand_offset, a.seed, ctx->rounds.p,
+                       ctx->partials.p);
     ctx->screen_total += cells * a.n;
     ctx->screen_pending = true;
     return ctx->hip(hipGetLastError(), "packed screen launch");
@@ -3047,7 +3202,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
             if (rc) return rc;
             use_bx = ctx->P->bx_ok;
         }
-        hot = use_bx && ctx->hot != 0 && ctx->P->bx_sb.p != nullptr;
+        hot = use_bx && ctx->hot != 0 && ctx->P->bx_sb.p != nullptr && !ctx->hot_redo;
         for (int m : {DENSE_GMM, DENSE_LGMM})   // k_hot_bx stages every label's sampling records
             for (int li : ctx->P->h_group[m]) hot = hot && ctx->P->h_labels[li].ns <= kSampLds;
         // the expansion screen's appends: a cell's hot list at most (the
@@ -3209,101 +3364,59 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                                a.n, nl, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p, 0, 0, nl, nullptr);
             ctx->screen_exec += (int64_t)a.n_rounds * a.n * dense_terms(ctx);
         }
-        // the dense rows' partial slots start empty; the re-score chunks
-        // overwrite theirs (one chunk table per round trip: the counts)
+        // the dense rows' partial slots start empty; the re-score entries
+        // overwrite theirs
         hipLaunchKernelGGL(k_fill_empty, dim3((unsigned)std::min<int64_t>((a.tiles + kBlock - 1) / kBlock, 64), nl, a.gz),
                            dim3(kBlock), 0, ctx->stream, grp, ctx->P->n_labels, a.tiles, ctx->partials.p);
         HIPCHK(ctx, ctx->scr_cnt_h.resize(cells));
         HIPCHK(ctx, hipMemcpyAsync(ctx->scr_cnt_h.data(), ctx->scr_cnt.p, cells * sizeof(int32_t),
                                    hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
         if (hot) {
-            ctx->hot_ran = true;
-            for (size_t c = 0; c < cells; ++c) ctx->hot_listed += ctx->hot_cnt_h[c];
-            if (ctx->pin[0].hot_flag) {
-                // a cell's best lower bound stayed below tau0 (bit 1: the
-                // list may miss winners) or a list overflowed (bit 2) --
-                // screen every candidate instead, into full-length lists
-                ctx->hot_fallback = ctx->pin[0].hot_flag;
-                if ((ctx->pin[0].hot_flag & 2) && ctx->hot_cap_div > 1.0)   // the next rounds list more
-                    ctx->hot_cap_div = std::max(1.0, ctx->hot_cap_div / 4.0);
-                lst = a.n;
-                HIPCHK(ctx, ctx->scr_hid.reserve(cells * lst));
-                HIPCHK(ctx, ctx->scr_idx.reserve(cells * lst));
-                HIPCHK(ctx, hipMemsetAsync(ctx->scr_lb.p, 0, cells * sizeof(unsigned long long), ctx->stream));
-                HIPCHK(ctx, hipMemsetAsync(ctx->scr_cnt.p, 0, cells * sizeof(int32_t), ctx->stream));
-                screen_bx_all(ctx, grp, nl, a);
-                hipLaunchKernelGGL(k_select_list, dim3((unsigned)cells), dim3(kBlock), 0, ctx->stream,
-                                   ctx->scr_hid.p, lst, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p);
-                HIPCHK(ctx, hipMemcpyAsync(&ctx->pin[0].screen_exec, ctx->win_evals.p, sizeof(unsigned long long),
-                                           hipMemcpyDeviceToHost, ctx->stream));
-                HIPCHK(ctx, hipMemcpyAsync(ctx->scr_cnt_h.data(), ctx->scr_cnt.p, cells * sizeof(int32_t),
-                                           hipMemcpyDeviceToHost, ctx->stream));
-                HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+            ctx->hot_ran = true;   // (its lists and flag are read after the round's one sync)
+            ctx->hot_cells = (int64_t)cells;
+        }
+        // the re-score, planned on the device from the counts: sliced for a
+        // few near-ties, chunks of kRescoreR * 256 otherwise (grids sized for
+        // the largest table either plan can make)
+        int32_t s_max = 1;
+        for (int m : {DENSE_GMM, DENSE_LGMM})
+            for (int li : ctx->P->h_group[m]) {
+                const DLabel& d = ctx->P->h_labels[li];
+                s_max = std::max(s_max, (d.nb + kSumSlice - 1) / kSumSlice + (d.na + kSumSlice - 1) / kSumSlice);
             }
-        }
-        // few candidates (the expansion screen's near-ties): split by slices
-        int64_t total_rs = 0;
-        for (size_t c = 0; c < cells; ++c) total_rs += ctx->scr_cnt_h[c];
-        const bool sliced = total_rs <= kSlicedRescoreMax;
-        const int64_t per = sliced ? (int64_t)kRsW : (int64_t)kRescoreR * kBlock;
-        std::vector<RescoreChunk>& tab = ctx->scr_chunks_h;
-        tab.clear();
-        std::vector<int64_t> range(cells);
-        for (size_t c = 0; c < cells; ++c) {
-            const int64_t first = (int64_t)tab.size();
-            for (int32_t j = 0; (int64_t)j * per < ctx->scr_cnt_h[c]; ++j) tab.push_back(RescoreChunk{(int32_t)c, j});
-            range[c] = (first << 32) | ((int64_t)tab.size() - first);
-        }
-        if (!tab.empty() && sliced) {
-            int32_t s_max = 1;
-            for (int m : {DENSE_GMM, DENSE_LGMM})
-                for (int li : ctx->P->h_group[m]) {
-                    const DLabel& d = ctx->P->h_labels[li];
-                    s_max = std::max(s_max, (d.nb + kSumSlice - 1) / kSumSlice + (d.na + kSumSlice - 1) / kSumSlice);
-                }
-            const int32_t ne = (int32_t)tab.size();
-            HIPCHK(ctx, ctx->scr_chunks.reserve(ne));
-            HIPCHK(ctx, ctx->scr_res.reserve(ne));
-            HIPCHK(ctx, ctx->scr_off.reserve(cells));
-            HIPCHK(ctx, ctx->rs_x.reserve((size_t)ne * kRsW));
-            HIPCHK(ctx, ctx->rs_g.reserve((size_t)ne * kRsW));
-            HIPCHK(ctx, ctx->rs_part.reserve((size_t)ne * s_max * kRsW));
-            HIPCHK(ctx, hipMemcpyAsync(ctx->scr_chunks.p, tab.data(), ne * sizeof(RescoreChunk),
-                                       hipMemcpyHostToDevice, ctx->stream));
-            HIPCHK(ctx, hipMemcpyAsync(ctx->scr_off.p, range.data(), cells * sizeof(int64_t),
-                                       hipMemcpyHostToDevice, ctx->stream));
-            const RescoreChunk* chp = reinterpret_cast<const RescoreChunk*>(ctx->scr_chunks.p);
-            hipLaunchKernelGGL(k_rescore_draw, dim3((unsigned)((ne + kBlock / kRsW - 1) / (kBlock / kRsW))),
-                               dim3(kBlock), 0, ctx->stream, ctx->P->labels.p, grp, ctx->P->samp.p, lst,
-                               a.cand_offset, a.seed, ctx->rounds.p, nl, ne, ctx->scr_cnt.p, ctx->scr_idx.p, chp,
-                               ctx->rs_x.p, ctx->rs_g.p);
-            hipLaunchKernelGGL(k_rescore_slices, dim3((unsigned)((s_max + 3) / 4), (unsigned)ne), dim3(kBlock), 0,
-                               ctx->stream, ctx->P->labels.p, grp, ctx->P->comps64.p, nl, chp, ctx->rs_x.p, s_max,
-                               ctx->rs_part.p);
-            hipLaunchKernelGGL(k_rescore_fin, dim3((unsigned)ne), dim3(kRsW), 0, ctx->stream, ctx->P->labels.p, grp,
-                               ctx->P->comps64.p, nl, chp, ctx->rs_x.p, ctx->rs_g.p, s_max, ctx->rs_part.p,
-                               ctx->scr_res.p);
-            hipLaunchKernelGGL(k_rescore_merge, dim3((unsigned)((cells + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                               ctx->stream, grp, nl, (int64_t)cells, ctx->P->n_labels, a.tiles, ctx->scr_off.p,
-                               ctx->scr_res.p, ctx->partials.p);
-        } else if (!tab.empty()) {
-            HIPCHK(ctx, ctx->scr_chunks.reserve(tab.size()));
-            HIPCHK(ctx, ctx->scr_res.reserve(tab.size()));
-            HIPCHK(ctx, ctx->scr_off.reserve(cells));
-            HIPCHK(ctx, hipMemcpyAsync(ctx->scr_chunks.p, tab.data(), tab.size() * sizeof(RescoreChunk),
-                                       hipMemcpyHostToDevice, ctx->stream));
-            HIPCHK(ctx, hipMemcpyAsync(ctx->scr_off.p, range.data(), cells * sizeof(int64_t),
-                                       hipMemcpyHostToDevice, ctx->stream));
-            hipLaunchKernelGGL((k_rescore<kRescoreR>), dim3((unsigned)tab.size()), dim3(kBlock), 0, ctx->stream,
-                               ctx->P->labels.p, grp, ctx->P->comps64.p, ctx->P->samp.p, lst,
-                               a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->P->n_labels, a.tiles,
-                               ctx->scr_cnt.p, ctx->scr_idx.p,
-                               reinterpret_cast<const RescoreChunk*>(ctx->scr_chunks.p), ctx->scr_res.p);
-            hipLaunchKernelGGL(k_rescore_merge, dim3((unsigned)((cells + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                               ctx->stream, grp, nl, (int64_t)cells, ctx->P->n_labels, a.tiles, ctx->scr_off.p,
-                               ctx->scr_res.p, ctx->partials.p);
-        }
+        const int64_t per_full = (int64_t)kRescoreR * kBlock;
+        const int64_t ne_sliced = (int64_t)cells + kSlicedRescoreMax / kRsW;
+        const int64_t ne_full = (int64_t)cells + ((int64_t)cells * lst + per_full - 1) / per_full;
+        const int64_t ne_cap = std::max(ne_sliced, ne_full);
+        HIPCHK(ctx, ctx->scr_chunks.reserve(ne_cap));
+        HIPCHK(ctx, ctx->scr_res.reserve(ne_cap));
+        HIPCHK(ctx, ctx->scr_off.reserve(cells));
+        HIPCHK(ctx, ctx->rs_plan.reserve(3));   // (RescorePlan: 24 B)
+        HIPCHK(ctx, ctx->rs_x.reserve((size_t)ne_sliced * kRsW));
+        HIPCHK(ctx, ctx->rs_g.reserve((size_t)ne_sliced * kRsW));
+        HIPCHK(ctx, ctx->rs_part.reserve((size_t)ne_sliced * s_max * kRsW));
+        RescoreChunk* chp = reinterpret_cast<RescoreChunk*>(ctx->scr_chunks.p);
+        RescorePlan* plan = reinterpret_cast<RescorePlan*>(ctx->rs_plan.p);
+        hipLaunchKernelGGL(k_rescore_plan, dim3(1), dim3(kPlanBlock), 0, ctx->stream, ctx->scr_cnt.p, (int64_t)cells,
+                           (int32_t)per_full, 1, (int64_t)cells * lst, chp, ctx->scr_off.p, nullptr, plan);
+        const unsigned g_sl = (unsigned)std::min<int64_t>(ne_sliced, 1024);
+        hipLaunchKernelGGL(k_rescore_draw, dim3((unsigned)((ne_sliced + kBlock / kRsW - 1) / (kBlock / kRsW))),
+                           dim3(kBlock), 0, ctx->stream, ctx->P->labels.p, grp, ctx->P->samp.p, lst,
+                           a.cand_offset, a.seed, ctx->rounds.p, nl, plan, ctx->scr_cnt.p, ctx->scr_idx.p, chp,
+                           ctx->rs_x.p, ctx->rs_g.p);
+        hipLaunchKernelGGL(k_rescore_slices, dim3((unsigned)((s_max + 3) / 4), g_sl), dim3(kBlock), 0,
+                           ctx->stream, ctx->P->labels.p, grp, ctx->P->comps64.p, nl, chp, plan, ctx->rs_x.p, s_max,
+                           ctx->rs_part.p);
+        hipLaunchKernelGGL(k_rescore_fin, dim3(g_sl), dim3(kRsW), 0, ctx->stream, ctx->P->labels.p, grp,
+                           ctx->P->comps64.p, nl, chp, plan, ctx->rs_x.p, ctx->rs_g.p, s_max, ctx->rs_part.p,
+                           ctx->scr_res.p);
+        hipLaunchKernelGGL((k_rescore<kRescoreR>), dim3((unsigned)std::min<int64_t>(ne_full, 512)), dim3(kBlock), 0,
+                           ctx->stream, ctx->P->labels.p, grp, ctx->P->comps64.p, ctx->P->samp.p, lst,
+                           a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->P->n_labels, a.tiles,
+                           ctx->scr_cnt.p, ctx->scr_idx.p, chp, plan, ctx->scr_res.p);
+        hipLaunchKernelGGL(k_rescore_merge, dim3((unsigned)((cells + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                           ctx->stream, grp, nl, (int64_t)cells, ctx->P->n_labels, a.tiles, ctx->scr_off.p,
+                           ctx->scr_res.p, ctx->partials.p);
         ctx->screen_total += (int64_t)cells * a.n;
         ctx->screen_pending = true;
         bracket(ctx, DENSE_GMM, 1);
@@ -3654,6 +3767,10 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     RoundArgs a{n, cand_offset, seed, n_rounds, tiles, cand_in_dev, olb, ola, S, gx, gz,
                 n_whole * rounds_whole, gx_whole};
     ctx->screen_total = ctx->screen_rescored = 0;
+    ctx->hot_ran = false;
+    ctx->hot_listed = 0;
+    ctx->hot_fallback = 0;
+    ctx->pk_plan_pending = false;
     ctx->cat_early = false;
     ctx->screen_mode = 0;
     ctx->screen_exec = 0;
@@ -3730,6 +3847,37 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     }
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     if (tiles > 0 && out) std::memcpy(out, ctx->res_h.data(), n_res * sizeof(tpe_label_result));
+    if (ctx->pk_plan_pending && pin.plan.overflow && !ctx->pk_redo) {
+        // the packed re-score listed more candidates than its buffers hold:
+        // nothing was re-scored; the round again with buffers for them all
+        ctx->pk_cap = pin.plan.total + pin.plan.total / 4 + 1024;
+        ctx->pk_redo = true;
+        const int rc = run_round(ctx, seed, rounds_h, n_rounds, n, cand_offset, cand_in_dev, olb, ola, out,
+                                 only_label);
+        ctx->pk_redo = false;
+        return rc;
+    }
+    if (ctx->hot_ran) {
+        for (int64_t c = 0; c < ctx->hot_cells; ++c) ctx->hot_listed += ctx->hot_cnt_h[c];
+        const int32_t hf = pin.hot_flag;
+        if (hf && !ctx->hot_redo) {
+            // a cell's best lower bound stayed below tau0 (bit 1: its list may
+            // miss a winner) or a list overflowed (bit 2): the round runs
+            // again with every candidate through the expansion screen (the
+            // same draws; its results replace these), and later rounds list
+            // more after an overflow
+            if ((hf & 2) && ctx->hot_cap_div > 1.0) ctx->hot_cap_div = std::max(1.0, ctx->hot_cap_div / 4.0);
+            const int64_t listed = ctx->hot_listed;
+            ctx->hot_redo = true;
+            const int rc = run_round(ctx, seed, rounds_h, n_rounds, n, cand_offset, cand_in_dev, olb, ola, out,
+                                     only_label);
+            ctx->hot_redo = false;
+            ctx->hot_ran = true;
+            ctx->hot_fallback = hf;
+            ctx->hot_listed = listed;
+            return rc;
+        }
+    }
     const int32_t errh = pin.err;
     ctx->xdrawn_h[0] = pin.xdrawn[0];
     ctx->xdrawn_h[1] = pin.xdrawn[1];
@@ -4044,6 +4192,8 @@ TPE_DEV void tpe1_ctx_destroy(tpe_ctx* c) {
     }
     c->scr_hi.release();
     c->scr_idx.release();
+    c->scr_range.release();
+    c->rs_plan.release();
     c->scr_lb.release();
     c->scr_cnt.release();
     c->scr_chunks.release();
@@ -4328,6 +4478,11 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
         case TPE_OPT_EXPAND: ctx->expand = value != 0; break;
         case TPE_OPT_EARLY: ctx->early = value != 0; break;
         case TPE_OPT_ZERO_WIN: ctx->zero_win = value != 0; break;
+        case TPE_OPT_VALUE_ONLY: ctx->value_only = value != 0; break;
+        case TPE_OPT_RESCORE_CAP:
+            if (value < 1) return ctx->fail(TPE_ERR_ARG, "re-score capacity must be positive");
+            ctx->pk_cap = value;
+            break;
         case TPE_OPT_HOT_DIV:
             if (value < 1 || value > (1 << 20)) return ctx->fail(TPE_ERR_ARG, "hot list divisor must be in [1, 2^20]");
             ctx->hot_cap_div = (double)value;

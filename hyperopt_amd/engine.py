@@ -373,11 +373,14 @@ class Engine(object):
                'window': L.TPE_OPT_WINDOW, 'win_t': L.TPE_OPT_WIN_T,
                'win_groups': L.TPE_OPT_WIN_GROUPS, 'expand': L.TPE_OPT_EXPAND,
                'hot': L.TPE_OPT_HOT, 'early': L.TPE_OPT_EARLY, 'hot_div': L.TPE_OPT_HOT_DIV,
-               'zero_win': L.TPE_OPT_ZERO_WIN}
+               'zero_win': L.TPE_OPT_ZERO_WIN, 'value_only': L.TPE_OPT_VALUE_ONLY,
+               'rescore_cap': L.TPE_OPT_RESCORE_CAP}
 
     def set_option(self, name, value):
         """Engine switches (include/hyperopt_tpe.h TPE_OPT_*): 'screen',
-        'splitk', 'dedup', 'timing', 'window', 'expand', 'hot', 'early' (bool), 'chunks'
+        'splitk', 'dedup', 'timing', 'window', 'expand', 'hot', 'early',
+        'value_only' (bool: batched rounds report the winner's index and value
+        only where the screen alone decided it, lpdfs NaN), 'chunks'
         (int, 0 = auto), 'hot_div' (the prefilter's list length n / hot_div),
         'win_t' (the windowed screen's cut, 8..62), 'win_groups' (label
         groups pipelined over two streams, 0 = auto),
@@ -520,5 +523,10 @@ def get_engine(device=0, precision='f64', role='main'):
     if key not in cache:
         eng = Engine(device, precision)
         eng.set_option('timing', 0)          # tpe.suggest reads no device timings
+        if len(_devices(device)) == 1:
+            # tpe.suggest reads the winners' values only (tpe.py:906-916):
+            # no lpdfs for a batched round the screen alone decided (a
+            # multi-device context merges its shards by score: exact there)
+            eng.set_option('value_only', 1)
         cache[key] = eng
     return cache[key]

@@ -447,6 +447,17 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *                   components whose terms can be nonzero at the wave's
  *                   candidates (the others are exactly +0.0: the same
  *                   bits)                                                 [1]
+ *   TPE_OPT_VALUE_ONLY  packed-map rounds (batched small rounds) report
+ *                   only the winner's index and value for a (round, label)
+ *                   whose screen selected one candidate clearing every
+ *                   other's upper bound by 1e-9 (relative): no fp64 lpdfs
+ *                   are computed for it (score, lpdf_below, lpdf_above NaN);
+ *                   the same index and value as the exact round.  For
+ *                   callers that read the value only (tpe.suggest); not for
+ *                   shards whose winners are merged by score            [0]
+ *   TPE_OPT_RESCORE_CAP  candidates the packed map's re-score buffers hold
+ *                   (grown when a round lists more: that round runs again;
+ *                   tests set it small to take that path)               [65536]
  *   TPE_OPT_WIN_GROUPS  label groups of a windowed round, each sorted on a
  *                   second stream while the previous one is screened
  *                   (0: one group; the chip is busy either way)          [0]
@@ -459,7 +470,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *                   summation order follow the whole problem, so the merged
  *                   shards equal one context's round bit for bit     [0: this call's]
  * None of them changes a winner; they exist for tests, experiments and
- * sharded runs. */
+ * sharded runs (TPE_OPT_VALUE_ONLY drops the lpdfs a caller does not read). */
 #define TPE_OPT_SCREEN 1
 #define TPE_OPT_SPLITK 2
 #define TPE_OPT_DEDUP 3
@@ -475,6 +486,8 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_EARLY 13
 #define TPE_OPT_HOT_DIV 14
 #define TPE_OPT_ZERO_WIN 15
+#define TPE_OPT_VALUE_ONLY 16
+#define TPE_OPT_RESCORE_CAP 17
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
 
 /* Build now what the resident posterior's first round(s) of n_candidates

@@ -1,0 +1,90 @@
+"""Value-only batched rounds (TPE_OPT_VALUE_ONLY): the
+reference's suggestion document carries only the chosen values
+(tpe.py:906-916), so a packed-map round whose screen selected ONE candidate
+clearing every other's upper bound by 1e-9 (relative) reports its index and
+value without computing its fp64 lpdfs.  The index and value must be the
+exact round's bytewise (configs 3 and 5); the lpdfs of the decided cells are
+NaN and every other cell's result is the exact round's.  Also the device-
+planned re-score's overflow path (a round listing more candidates than the
+buffers hold runs again with larger ones): same bytes."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def eng():
+    from hyperopt_amd.engine import Engine
+    e = Engine(0, 'f64')
+    yield e
+    e.close()
+
+
+def _both(eng, fn):
+    eng.set_option('value_only', 0)
+    exact = fn()
+    eng.set_option('value_only', 1)
+    try:
+        vo = fn()
+    finally:
+        eng.set_option('value_only', 0)
+    return exact, vo
+
+
+def _check(exact, vo):
+    assert np.array_equal(exact['index'], vo['index'])
+    assert exact['value'].tobytes() == vo['value'].tobytes()
+    decided = np.isnan(vo['lpdf_below']) & ~np.isnan(exact['lpdf_below'])
+    # the cells the screen did not decide alone are the exact round's, bit for bit
+    same = ~decided
+    assert np.ascontiguousarray(exact[same]).tobytes() == np.ascontiguousarray(vo[same]).tobytes()
+    return int(decided.sum())
+
+
+def test_value_only_config5(eng):
+    """Config 5 at its BASELINE size (128 labels, N = 50k, 4096 new_ids x
+    24): most (round, dense label) cells are decided by the screen."""
+    from hyperopt_amd.workloads import FminLoop, mixed_history
+    hist = mixed_history(128, 50000, seed=0)
+    FminLoop(hist).advance(eng, 50000, n_candidates=24, n_rounds=4096)
+    ids = list(range(9000, 9000 + 4096))
+    exact, vo = _both(eng, lambda: eng.suggest_batch(77, ids, 24))
+    n = _check(exact, vo)
+    dense = sum(1 for _, k, _ in hist.labels if k in ('uniform', 'loguniform', 'normal'))
+    print('value-only config 5: %d of %d dense cells decided by the screen' % (n, dense * len(ids)))
+    assert n > 0.5 * dense * len(ids)
+
+
+def test_value_only_leaves_tile_rounds_exact(eng):
+    """Config 3 (tile map, 2^20 candidates): value-only changes nothing --
+    the near-tie re-score stays (the tile map's winners are merged across
+    shards by score)."""
+    from hyperopt_amd.workloads import FminLoop, mixed_history
+    hist = mixed_history(32, 10000, seed=0)
+    FminLoop(hist).advance(eng, 10000, n_candidates=1 << 20)
+    exact, vo = _both(eng, lambda: eng.suggest(5, 1 << 20, round=3))
+    assert np.ascontiguousarray(exact).tobytes() == np.ascontiguousarray(vo).tobytes()
+
+
+@pytest.mark.parametrize('value_only', [0, 1])
+def test_packed_rescore_overflow_runs_again(eng, value_only):
+    """A packed round whose selection exceeds the re-score buffers (capacity
+    forced to 1) runs again with buffers for all of them: the same bytes as
+    with room to spare."""
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.workloads import mixed_history
+    hist = mixed_history(64, 20000, seed=1)
+    eng.set_posterior(*P.pack(hist.posteriors()))
+    ids = list(range(7000, 7512))
+    eng.set_option('value_only', value_only)
+    try:
+        eng.set_option('rescore_cap', 1 << 20)
+        a = eng.suggest_batch(31, ids, 24)
+        eng.set_option('rescore_cap', 1)
+        b = eng.suggest_batch(31, ids, 24)
+        c = eng.suggest_batch(31, ids, 24)   # (the grown buffers, no second run)
+    finally:
+        eng.set_option('value_only', 0)
+    assert np.ascontiguousarray(a).tobytes() == np.ascontiguousarray(b).tobytes()
+    assert np.ascontiguousarray(a).tobytes() == np.ascontiguousarray(c).tobytes()
