@@ -390,7 +390,9 @@ def main():
         C = C_total // world
     L = len(posts)
 
-    from hyperopt_amd.parallel import exchange_winners, gather_rounds
+    from hyperopt_amd.parallel import DeviceExchange
+    xch = (DeviceExchange(eng, 'labels' if by_label else ('rounds' if args.config == 5 else 'candidates'),
+                          shards=shards, rank=rank) if dist is not None else None)
 
     # fresh-posterior steps (default): each step appends the next trial(s) to
     # the device-resident history and rebuilds the posterior as tpe.suggest
@@ -417,15 +419,14 @@ def main():
                        n_rounds=ids_local if args.config == 5 else 1)
         if args.config == 5:   # independent new_ids split over the GPUs (or each rank's labels)
             first_id = i * args.new_ids + (0 if by_label else rank * ids_local)
-            res = e.suggest_batch(seed=1234, rounds=list(range(first_id, first_id + ids_local)),
-                                  n_candidates=C)
+            ids = list(range(first_id, first_id + ids_local))
             if dist is not None and gather:   # every rank ends with every new_id's winners
-                res = gather_labels(res, shards, rank) if by_label else gather_rounds(res)
-            return res
-        res = e.suggest(seed=1234 + i, n_candidates=nc, round=i, cand_offset=0 if by_label else rank * nc)
-        if dist is not None and gather:   # exchange per-GPU winners (L x 48 B) over RCCL
-            res = gather_labels(res, shards, rank) if by_label else exchange_winners(res)
-        return res
+                return xch.round(1234, ids, C)
+            return e.suggest_batch(seed=1234, rounds=ids, n_candidates=C)
+        off = 0 if by_label else rank * nc
+        if dist is not None and gather:   # the winners (L x 48 B) all-gathered device to device
+            return xch.round(1234 + i, [i], nc, cand_offset=off)[0]
+        return e.suggest(seed=1234 + i, n_candidates=nc, round=i, cand_offset=off)
 
     def timed(n_steps, first, fresh, keep=False, n=None):
         """Run n_steps steps (barrier + sync on both sides); returns wall

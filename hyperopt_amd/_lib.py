@@ -112,6 +112,8 @@ SIGNATURES = {
     'tpe_suggest_batch': (ctypes.c_int, [_P, _U64, _P, _I32, _I64, _I64, _P]),
     'tpe_score': (ctypes.c_int, [_P, _I32, _P, _I64, _P, _P, _P]),
     'tpe_merge_results': (ctypes.c_int, [_P, _I32, _I32, _P]),
+    'tpe_suggest_batch_device': (ctypes.c_int, [_P, _U64, _P, _I32, _I64, _I64, _P, _P]),
+    'tpe_merge_results_device': (ctypes.c_int, [_P, _P, _I32, _I32, _P]),
     'tpe_last_timing': (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float),
                                        ctypes.POINTER(ctypes.c_float)]),
     'tpe_last_evals': (ctypes.c_int64, [_P]),

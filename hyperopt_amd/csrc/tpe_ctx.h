@@ -408,6 +408,7 @@ struct tpe_ctx {
     int64_t pk_cap = 1 << 16;            // packed re-score: candidates its buffers hold (grows)
     bool pk_plan_pending = false;        // the packed plan awaits the round's sync
     bool pk_redo = false;                // the round runs again after a plan overflow
+    tpe_label_result* dev_out = nullptr; // tpe_suggest_batch_device: the caller's device buffer
     float prep_ms = 0.f;                 // device ms of the last expansion-index build (bx_prepare)
     hipEvent_t ev_prep[2] = {};          //   its bracket, read when asked (tpe_last_prepare)
     bool prep_pending = false;

@@ -3840,6 +3840,9 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     HIPCHK(ctx, hipMemcpyAsync(pin.xdrawn, ctx->xdrawn.p, 2 * sizeof(unsigned long long),
                                hipMemcpyDeviceToHost, ctx->stream));
     const size_t n_res = (size_t)n_rounds * L;
+    if (tiles > 0 && ctx->dev_out)
+        HIPCHK(ctx, hipMemcpyAsync(ctx->dev_out, ctx->results.p, n_res * sizeof(tpe_label_result),
+                                   hipMemcpyDeviceToDevice, ctx->stream));
     if (tiles > 0 && out) {
         HIPCHK(ctx, ctx->res_h.resize(n_res));
         HIPCHK(ctx, hipMemcpyAsync(ctx->res_h.data(), ctx->results.p, n_res * sizeof(tpe_label_result),
@@ -4099,6 +4102,24 @@ double tpe_rt::np_pairwise_sum(const double* a, size_t n) {
 }
 
 // ================================================================ C ABI ====
+namespace {
+// one thread per result: the best of the parts, tpe_merge_results' order
+__global__ __launch_bounds__(kBlock) void k_merge_results(const tpe_label_result* __restrict__ parts,
+                                                          int32_t n_parts, int32_t n,
+                                                          tpe_label_result* __restrict__ out) {
+    const int32_t j = blockIdx.x * kBlock + threadIdx.x;
+    if (j >= n) return;
+    tpe_label_result best = parts[j];
+    for (int32_t p = 1; p < n_parts; ++p) {
+        const tpe_label_result c = parts[(size_t)p * n + j];
+        if (c.index < 0) continue;
+        if (best.index < 0 || better(order_key(c.score), c.index, order_key(best.score), best.index)) best = c;
+    }
+    out[j] = best;
+}
+
+}  // namespace
+
 extern "C" {
 
 int tpe_abi_version(void) { return TPE_ABI_VERSION; }
@@ -4372,6 +4393,31 @@ int tpe_screen_probe(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n,
     HIPCHK(ctx, hipMemcpyAsync(err_bound, ctx->out_la.p, n * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     return TPE_OK;
+}
+
+int tpe_suggest_batch_device(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds, int32_t n_rounds,
+                             int64_t n_candidates, int64_t cand_offset, tpe_label_result* d_out,
+                             tpe_label_result* out) {
+    if (!ctx || !d_out || !rounds) return TPE_ERR_ARG;
+    if (!ctx->peers.empty()) return ctx->fail(TPE_ERR_ARG, "device results: single-device contexts only");
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    if (n_candidates <= 0) return ctx->fail(TPE_ERR_ARG, "device results need candidates");
+    ctx->dev_out = d_out;
+    const int rc = run_round(ctx, seed, rounds, n_rounds, n_candidates, cand_offset, nullptr, nullptr, nullptr, out,
+                             -1);
+    ctx->dev_out = nullptr;
+    return rc;
+}
+
+int tpe_merge_results_device(tpe_ctx* ctx, const tpe_label_result* d_parts, int32_t n_parts, int32_t n,
+                             tpe_label_result* d_out) {
+    if (!ctx || !d_parts || !d_out || n_parts <= 0 || n < 0) return TPE_ERR_ARG;
+    HIPCHK(ctx, hipSetDevice(ctx->device));
+    if (n == 0) return TPE_OK;
+    hipLaunchKernelGGL(k_merge_results, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
+                       d_parts, n_parts, n, d_out);
+    HIPCHK(ctx, hipGetLastError());
+    return ctx->hip(hipStreamSynchronize(ctx->stream), "device merge");
 }
 
 int tpe_merge_results(const tpe_label_result* parts, int32_t n_parts, int32_t n,

@@ -294,6 +294,28 @@ class Engine(object):
                                                int(cand_offset), _ptr(out)))
         return out.reshape(len(rounds), self.n_labels)
 
+    def suggest_batch_device(self, seed, rounds, n_candidates, d_out, cand_offset=0):
+        """tpe_suggest_batch into a device buffer: d_out a torch uint8 tensor
+        on this engine's GPU holding len(rounds) * n_labels records
+        (RESULT_DTYPE bytes), complete on return -- for an RCCL all-gather
+        without a host round trip."""
+        rounds = np.ascontiguousarray(np.asarray(rounds, dtype=np.uint32))
+        need = len(rounds) * self._labels() * RESULT_DTYPE.itemsize
+        if not d_out.is_cuda or d_out.numel() * d_out.element_size() < need or not d_out.is_contiguous():
+            raise ValueError('d_out must be a contiguous device tensor of %d bytes' % need)
+        self._check(self.lib.tpe_suggest_batch_device(
+            self.h, int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(rounds), len(rounds), int(n_candidates),
+            int(cand_offset), ctypes.c_void_p(d_out.data_ptr()), None))
+        return d_out
+
+    def merge_results_device(self, d_parts, n_parts, n, d_out):
+        """tpe_merge_results over device tensors (n_parts blocks of n records
+        -> n records), on this engine's GPU."""
+        self._check(self.lib.tpe_merge_results_device(
+            self.h, ctypes.c_void_p(d_parts.data_ptr()), int(n_parts), int(n),
+            ctypes.c_void_p(d_out.data_ptr())))
+        return d_out
+
     def score(self, label, cand, want_lpdf=True):
         cand = _f64(cand).ravel()
         lb = np.empty(len(cand)) if want_lpdf else None

@@ -40,6 +40,107 @@ def _all_gather_results(res, group):
     return out.cpu().numpy().view(RESULT_DTYPE).reshape((world,) + res.shape)
 
 
+def all_gather_raw(raw, group=None):
+    """One all-gather of a rank's raw result records (a contiguous uint8
+    tensor: on the GPU under RCCL, on the CPU under gloo); returns the
+    (world * nbytes,) tensor on the same device."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    out = torch.empty(world * raw.numel(), dtype=torch.uint8, device=raw.device)
+    dist.all_gather_into_tensor(out, raw.reshape(-1), group=group)
+    return out
+
+
+def _records(t, shape):
+    return t.cpu().numpy().view(RESULT_DTYPE).reshape(shape)
+
+
+def assemble_labels(gathered, lead, m, shards):
+    """Label-shard assembly of an all-gather of padded [lead][m] record
+    blocks (one per rank, in rank order): [lead][n_labels] in space order,
+    `label` set to the space index."""
+    world = len(shards)
+    parts = gathered.reshape((world,) + tuple(lead) + (m,))
+    n_labels = sum(len(sh) for sh in shards)
+    out = np.zeros(tuple(lead) + (n_labels,), dtype=RESULT_DTYPE)
+    for r, sh in enumerate(shards):
+        out[..., sh] = parts[r][..., :len(sh)]
+    out['label'] = np.arange(n_labels, dtype=np.int32)
+    return out
+
+
+class DeviceExchange(object):
+    """Winners exchanged where they are computed: the
+    engine leaves a round's results in a device buffer (tpe_suggest_batch_
+    device), ONE all-gather moves every rank's buffer -- RCCL over xGMI,
+    device to device -- candidate shards are merged on the GPU
+    (tpe_merge_results_device), and only the final winners come to the host
+    (tpe.suggest's documents need them there).  The round-2/3 path staged the
+    records through host numpy, H2D, the collective and D2H every round.
+
+    mode 'labels' (rank r holds shards[r]'s labels: records padded to the
+    largest shard), 'candidates' (every rank the same rounds over its slice
+    of the candidates: broadcast_best merge) or 'rounds' (rank r holds rounds
+    [r n, (r + 1) n) of every label).  Under gloo (CPU rehearsals) the same
+    gather runs on host tensors."""
+
+    def __init__(self, engine, mode, shards=None, rank=0, group=None):
+        import torch.distributed as dist
+        if mode not in ('labels', 'candidates', 'rounds'):
+            raise ValueError(mode)
+        self.engine, self.mode, self.shards, self.rank, self.group = engine, mode, shards, rank, group
+        self.world = dist.get_world_size(group)
+        self.device = dist.get_backend(group) == 'nccl'
+        self._bufs = {}
+
+    def _buf(self, key, nbytes):
+        import torch
+        b = self._bufs.get(key)
+        if b is None or b.numel() < nbytes:
+            b = self._bufs[key] = torch.empty(nbytes, dtype=torch.uint8, device='cuda')
+        return b[:nbytes]
+
+    def round(self, seed, rounds, n_candidates, cand_offset=0):
+        """Run this rank's share of the rounds and exchange: every rank
+        returns [len(rounds) (x world for 'rounds')][n_labels] records."""
+        import torch
+        eng = self.engine
+        nr = len(rounds)
+        L = eng._labels()
+        rec = RESULT_DTYPE.itemsize
+        if self.device:
+            raw = eng.suggest_batch_device(seed, rounds, n_candidates, self._buf('res', nr * L * rec),
+                                           cand_offset=cand_offset)
+        else:
+            res = eng.suggest_batch(seed, rounds, n_candidates, cand_offset=cand_offset)
+            raw = torch.from_numpy(np.ascontiguousarray(res).view(np.uint8).reshape(-1))
+        return self.exchange(raw, nr, L)
+
+    def exchange(self, raw, nr, L):
+        """The collective and the assembly for raw = this rank's [nr][L]
+        records as a uint8 tensor (device or host)."""
+        import torch
+        rec = RESULT_DTYPE.itemsize
+        if self.mode == 'labels':
+            m = max(len(sh) for sh in self.shards)
+            if m != L:   # pad each round's block to the largest shard
+                pad = (self._buf('pad', nr * m * rec) if raw.is_cuda
+                       else torch.zeros(nr * m * rec, dtype=torch.uint8))
+                pad.view(nr, m * rec)[:, :L * rec] = raw.view(nr, L * rec)
+                raw = pad
+            g = all_gather_raw(raw, self.group)
+            return assemble_labels(_records(g, (-1,)), (nr,), m, self.shards)
+        g = all_gather_raw(raw, self.group)
+        if self.mode == 'rounds':
+            return _records(g, (self.world * nr, L))
+        if raw.is_cuda:   # candidates: the broadcast_best merge on the GPU
+            out = self._buf('merged', nr * L * rec)
+            self.engine.merge_results_device(g, self.world, nr * L, out)
+            return _records(out, (nr, L))
+        return merge_results(_records(g, (self.world, nr * L))).reshape(nr, L)
+
+
 def exchange_winners(res, group=None):
     """All-gather per-rank winners of the SAME rounds (candidate shards) and
     merge them; every rank returns the merged winners."""

@@ -313,6 +313,22 @@ int tpe_suggest_batch(tpe_ctx *ctx, uint64_t seed, const uint32_t *rounds,
                       int32_t n_rounds, int64_t n_candidates, int64_t cand_offset,
                       tpe_label_result *out);
 
+/* tpe_suggest_batch with the results left in DEVICE memory: d_out (on this
+ * single-device context's GPU, n_rounds * n_labels entries) receives them
+ * by a device-to-device copy, complete when the call returns -- the buffer a
+ * process-per-GPU caller all-gathers over RCCL without a host round trip
+ * (the reference's one algo call per round, fmin.py:201-202).
+ * out (host, may be NULL) receives them too. */
+int tpe_suggest_batch_device(tpe_ctx *ctx, uint64_t seed, const uint32_t *rounds,
+                             int32_t n_rounds, int64_t n_candidates, int64_t cand_offset,
+                             tpe_label_result *d_out, tpe_label_result *out);
+
+/* tpe_merge_results on device buffers of ctx's GPU (d_parts: n_parts blocks
+ * of n results, e.g. an RCCL all-gather of the ranks' tpe_suggest_batch_device
+ * outputs; d_out: n results), on the context's stream, complete on return. */
+int tpe_merge_results_device(tpe_ctx *ctx, const tpe_label_result *d_parts, int32_t n_parts,
+                             int32_t n, tpe_label_result *d_out);
+
 /* Score a caller-supplied candidate set for one resident label (the parity
  * entry point: identical candidates in, both lpdf vectors and the winner
  * out).  lpdf_below / lpdf_above may be NULL. */

@@ -244,3 +244,134 @@ def test_label_shards_gloo_world2():
     for r in (0, 1):
         assert got[r][0] == want.tobytes()
         assert got[r][1] == np.ascontiguousarray(want_rows).tobytes()
+
+
+def _xch_worker(rank, world, port, q):
+    """DeviceExchange's collective + assembly on host tensors (gloo): the
+    config-5 shape -- 4096 new_ids x a rank's labels (label shards: 64 and
+    64 of 128), 2048 of the 4096 new_ids (rounds), and candidate shards."""
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from hyperopt_amd.engine import RESULT_DTYPE
+        from hyperopt_amd.parallel import DeviceExchange
+        from hyperopt_amd.workloads import mixed_space
+        from hyperopt_amd.parallel import label_shards
+        shards = label_shards(mixed_space(128), world)
+        nr = 4096
+        L = len(shards[rank])
+        res = np.zeros((nr, L), dtype=RESULT_DTYPE)
+        res['index'] = (np.arange(nr)[:, None] * 1000 + np.array(shards[rank])[None]) * 10 + rank
+        res['value'] = res['index'] * 0.5
+        raw = torch.from_numpy(np.ascontiguousarray(res).view(np.uint8).reshape(-1))
+        out_l = DeviceExchange(None, 'labels', shards=shards, rank=rank).exchange(raw, nr, L)
+        half = np.zeros((2048, 128), dtype=RESULT_DTYPE)
+        half['index'] = rank * 2048 + np.arange(2048)[:, None]
+        raw = torch.from_numpy(np.ascontiguousarray(half).view(np.uint8).reshape(-1))
+        out_r = DeviceExchange(None, 'rounds', rank=rank).exchange(raw, 2048, 128)
+        cand = np.stack([_rank_results(rank), _rank_results(rank + 10)])
+        raw = torch.from_numpy(np.ascontiguousarray(cand).view(np.uint8).reshape(-1))
+        out_c = DeviceExchange(None, 'candidates', rank=rank).exchange(raw, 2, cand.shape[1])
+        q.put((rank, out_l.tobytes(), out_r.tobytes(), out_c.tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_device_exchange_gloo_world2_config5_shapes():
+    """the device-resident exchange's collective and
+    assembly at world size 2 with config-5-shaped payloads (4096 rounds x
+    64 labels per rank, label shards; 2048 rounds x 128 labels per rank, new_id
+    shards) and candidate shards merged in the broadcast_best order."""
+    import multiprocessing as mp
+    from hyperopt_amd.engine import RESULT_DTYPE, merge_results
+    from hyperopt_amd.parallel import label_shards
+    from hyperopt_amd.workloads import mixed_space
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_xch_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in procs:
+        r, a, b, c = q.get(timeout=180)
+        got[r] = (a, b, c)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    shards = label_shards(mixed_space(128), 2)
+    owner = np.zeros(128, dtype=np.int64)
+    for r, sh in enumerate(shards):
+        owner[sh] = r
+    want_l = (np.arange(4096)[:, None] * 1000 + np.arange(128)[None]) * 10 + owner[None]
+    want_c = merge_results(np.stack([np.stack([_rank_results(0), _rank_results(10)]).reshape(-1),
+                                     np.stack([_rank_results(1), _rank_results(11)]).reshape(-1)]))
+    for r in (0, 1):
+        out_l = np.frombuffer(got[r][0], dtype=RESULT_DTYPE).reshape(4096, 128)
+        assert np.array_equal(out_l['index'], want_l)
+        assert np.array_equal(out_l['label'][0], np.arange(128))
+        out_r = np.frombuffer(got[r][1], dtype=RESULT_DTYPE).reshape(4096, 128)
+        assert np.array_equal(out_r['index'][:, 0], np.arange(4096))
+        out_c = np.frombuffer(got[r][2], dtype=RESULT_DTYPE).reshape(-1)
+        assert np.array_equal(out_c['index'], want_c['index'])
+    assert got[0] == got[1]
+
+
+def _nccl_world1_worker(port, q):
+    """DeviceExchange on the GPU under RCCL at world size 1 (a one-GPU box
+    cannot hold two RCCL ranks): results written to a device buffer by the
+    engine, all-gathered device to device, candidate shards merged on the GPU
+    -- against the engine's host results."""
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group('nccl', rank=0, world_size=1)
+    try:
+        from hyperopt_amd.engine import Engine, RESULT_DTYPE
+        from hyperopt_amd.parallel import DeviceExchange
+        from hyperopt_amd.workloads import mixed_history
+        hist = mixed_history(16, 4000, seed=2)
+        eng = Engine(0)
+        eng.build_posterior(*hist.device_inputs(), gamma=0.25, prior_weight=1.0)
+        out = {}
+        for mode in ('candidates', 'rounds', 'labels'):
+            x = DeviceExchange(eng, mode, shards=[list(range(16))], rank=0)
+            out[mode] = (x.round(42, [9], 1 << 16)[0].tobytes(),
+                         x.round(7, list(range(500, 628)), 24).tobytes())
+        out['host'] = (eng.suggest(42, 1 << 16, round=9).tobytes(),
+                       eng.suggest_batch(7, list(range(500, 628)), 24).tobytes())
+        # the device merge against the host merge over 3 parts
+        a = eng.suggest(1, 4096, round=1, cand_offset=0)
+        b = eng.suggest(1, 4096, round=1, cand_offset=4096)
+        c = eng.suggest(1, 4096, round=1, cand_offset=8192)
+        parts = np.ascontiguousarray(np.stack([a, b, c]))
+        d_parts = torch.from_numpy(parts.view(np.uint8).reshape(-1)).cuda()
+        d_out = torch.empty(len(a) * RESULT_DTYPE.itemsize, dtype=torch.uint8, device='cuda')
+        eng.merge_results_device(d_parts, 3, len(a), d_out)
+        out['merge'] = d_out.cpu().numpy().tobytes()
+        from hyperopt_amd.engine import merge_results
+        out['merge_host'] = np.ascontiguousarray(merge_results(parts)).tobytes()
+        eng.close()
+        q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_device_exchange_rccl_world1():
+    import multiprocessing as mp
+    from hyperopt_amd.engine import merge_results, RESULT_DTYPE
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_world1_worker, args=(_free_port(), q))
+    p.start()
+    out = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    for mode in ('candidates', 'rounds', 'labels'):
+        assert out[mode][0] == out['host'][0], mode
+        assert out[mode][1] == out['host'][1], mode
+    assert out['merge'] == out['merge_host']
