@@ -261,18 +261,13 @@ __device__ __forceinline__ void wave_window(const Comp<double>* __restrict__ c, 
     k1 = __builtin_amdgcn_readlane(lo, 32);
 }
 
-// lane j's value, to every lane (j wave-uniform: v_readlane into SGPRs)
-__device__ __forceinline__ double bcast(double v, int j) {
-    const uint64_t u = (uint64_t)__double_as_longlong(v);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, j);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), j);
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-
 // grid (ceil(max bins / 64), dense labels): 64 consecutive bins per
 // workgroup, one bin per lane, their union window of clipped components
 // (wave_window) split over the 4 waves in interleaved batches of 64 records.
-// A batch is loaded coalesced and broadcast lane by lane (v_readlane), each
+// A batch is loaded coalesced into the wave's LDS slot as (mu', c') pairs and
+// read back by every lane at the same address (an LDS broadcast: one
+// ds_read_b128 per component instead of four v_readlane VALU operations and
+// their SGPR hazards -- round 3 measured the kernel at 0.33 VALU busy), each
 // lane adding the components within its own bin's window, branch-free, to
 // its A_0..A_14; the 4 waves' partial sums meet in LDS at the end.  The
 // bound (module comment) per lane: with |d| <= D for every summed component,
@@ -293,6 +288,7 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
     if (b0 >= B.nbins) return;        // the whole workgroup
     const DLabel L = labels[li];
     __shared__ double lds[kExpTabSize];   // the exp table, then the waves' partial sums
+    __shared__ double2 stage[kBlock / 64][64];   // per wave: its batch's (mu', c')
     load_exp_table(lds);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int b = b0 + lane, blast = min(b0 + 63, B.nbins - 1);
@@ -327,21 +323,25 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
             }
         }
         const int cnt = min(64, k1 - kc);
+        __builtin_amdgcn_wave_barrier();   // (the previous batch's reads come first: LDS is in order per wave)
+        stage[wave][lane] = double2{mu_l, c_l};
+        __builtin_amdgcn_wave_barrier();
         // kBxChains components per step: independent exp and power chains
         for (int j = 0; j < cnt; j += kBxChains) {
-            double cj[kBxChains], dj[kBxChains], aj[kBxChains];
+            double cj[kBxChains], dj[kBxChains], aj[kBxChains], mj[kBxChains];
             bool any = false;
 #pragma unroll
             for (int q = 0; q < kBxChains; ++q) {
-                const int jj = min(j + q, 63);
-                cj[q] = j + q < cnt ? bcast(c_l, jj) : -kInf;
+                const double2 v = stage[wave][min(j + q, 63)];   // (the same address on every lane)
+                cj[q] = j + q < cnt ? v.y : -kInf;
+                mj[q] = v.x;
                 any = any || cj[q] > -kInf;
             }
             if (!any) continue;   // unclipped or weightless (wave-uniform)
             double t[kBxChains], y[kBxChains];
 #pragma unroll
             for (int q = 0; q < kBxChains; ++q) {
-                dj[q] = bcast(mu_l, min(j + q, 63)) - xb;
+                dj[q] = mj[q] - xb;
                 aj[q] = fmax(cj[q] - kap * dj[q] * dj[q], -745.0);
                 // outside the bin's window, or below 2^-1067 in the whole bin
                 // (in the skip term): g = 0, so every sum below is unchanged
