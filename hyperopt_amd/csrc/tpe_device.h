@@ -96,6 +96,15 @@ struct U4 {
     uint32_t x, y, z, w;
 };
 
+// a ^ b ^ k in ONE VALU operation: gfx950's three-input bit operation
+// (truth table 0x96 = odd parity); k wave-uniform (an SGPR operand).  The
+// compiler forms two v_xor_b32 from the C expression.
+__device__ __forceinline__ uint32_t xor3_vvs(uint32_t a, uint32_t b, uint32_t k) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+}
+
 __device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
     // one 32x32 -> 64-bit product per multiplier (v_mad_u64_u32) instead of
     // separate low and high multiplies: the same words, a third faster.  The
@@ -103,10 +112,27 @@ __device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
     // the scalar unit per call instead of being hoisted out of the caller's
     // loops -- held there, they spilled and came back by v_readlane (VALU).
     asm volatile("" : "+s"(k0), "+s"(k1));
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
+    {   // round 1: the counter's y, z, w words are uniform in every caller
+        // (attempt, stream, round): the compiler keeps their part scalar
         const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
         c = U4{(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0};
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    {   // round 2: y = the low product of round 1's uniform z, still scalar
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+        c = U4{(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, xor3_vvs((uint32_t)(p0 >> 32), c.w, k1),
+               (uint32_t)p0};
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    // rounds 3..10: every word per lane; the two 3-input xors per round as
+    // v_bitop3 (6 -> 4 VALU operations per round, the same words)
+#pragma unroll
+    for (int i = 2; i < 10; ++i) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+        c = U4{xor3_vvs((uint32_t)(p1 >> 32), c.y, k0), (uint32_t)p1, xor3_vvs((uint32_t)(p0 >> 32), c.w, k1),
+               (uint32_t)p0};
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
     }
@@ -142,12 +168,17 @@ constexpr uint32_t kMaxAttempts = 1u << 16;
 // 1/256 -- else a branch-free lower bound over all 64; the categorical tile
 // kernel walks the 64-entry guide table (guide[j] = the first k with
 // cdf[k] > j / 64).  All return the same component.
+// The uniform is the Philox word w (u = w 2^-32, exact): SampShared
+// compares w with integer thresholds thr[k] = ceil(cdf[k] 2^32), and
+// cdf[k] <= u  <=>  cdf[k] 2^32 <= w  <=>  thr[k] <= w (w an integer, the
+// scaling exact) -- the same component without the conversion to double.
 struct SampGlobal {
     const SampRec* __restrict__ s;
     int ns;
     __device__ __forceinline__ const double* cos_tab() const { return kCosSinTab; }
     __device__ __forceinline__ const double* log_tab() const { return kLogTab; }
-    __device__ __forceinline__ void pick(double u, double& mu, double& sg) const {
+    __device__ __forceinline__ void pick(uint32_t w, double& mu, double& sg) const {
+        const double u = (double)w * 0x1.0p-32;
         const int k = cdf_search(s, ns, u);
         mu = s[k].mu;
         sg = s[k].sigma;
@@ -158,6 +189,7 @@ constexpr int kSampLds = 64;     // below components staged in LDS (K_b <= 26 in
 constexpr int kGuideSteps = 3;   // guided picks take at most this many comparisons
 struct SampLds {
     double cdf[kSampLds], mu[kSampLds], sg[kSampLds];
+    uint64_t thr[kSampLds];   // ceil(cdf 2^32)
     uint8_t guide[64];
     uint8_t gd[256];
     int steps;
@@ -170,21 +202,22 @@ struct SampShared {
     // vector memory path)
     const double* cs = kCosSinTab;
     const double* lg = kLogTab;
+    int steps = -1;   // t->steps read once by the caller (-1: read per pick)
     __device__ __forceinline__ const double* cos_tab() const { return cs; }
     __device__ __forceinline__ const double* log_tab() const { return lg; }
-    __device__ __forceinline__ void pick(double u, double& mu, double& sg) const {
+    __device__ __forceinline__ void pick(uint32_t w, double& mu, double& sg) const {
         // (steps is the same for the whole workgroup: a scalar branch)
-        const int steps = __builtin_amdgcn_readfirstlane(t->steps);
+        const int st = steps >= 0 ? steps : __builtin_amdgcn_readfirstlane(t->steps);
         int k;
-        if (steps <= kGuideSteps) {
-            k = t->gd[(int)(u * 256.0)];   // (u = w 2^-32: exactly w >> 24)
+        if (st <= kGuideSteps) {
+            k = t->gd[w >> 24];
 #pragma unroll
             for (int s = 0; s < kGuideSteps; ++s)
-                if (s < steps) k += t->cdf[k] <= u ? 1 : 0;   // (k <= ns - 1 throughout: cdf[ns - 1] = 1 > u)
-        } else {   // branch-free lower bound over the 64 (padded with 2.0)
+                if (s < st) k += t->thr[k] <= w ? 1 : 0;   // (k <= ns - 1 throughout: thr[ns - 1] = 2^32 > w)
+        } else {   // branch-free lower bound over the 64 (padded with 2.0: thr 2^33)
             k = 0;
 #pragma unroll
-            for (int step = kSampLds / 2; step > 0; step >>= 1) k = t->cdf[k + step - 1] <= u ? k + step : k;
+            for (int step = kSampLds / 2; step > 0; step >>= 1) k = t->thr[k + step - 1] <= w ? k + step : k;
         }
         mu = t->mu[k];
         sg = t->sg[k];
@@ -199,10 +232,12 @@ __device__ __forceinline__ bool stage_samp(const DLabel& L, const SampRec* __res
         if (k < L.ns) {
             const SampRec r = samp[L.samp_off + k];
             t->cdf[k] = r.cdf;
+            t->thr[k] = (uint64_t)ceil(r.cdf * 0x1.0p32);   // (exact: a power-of-two scaling, cdf in [0, 1])
             t->mu[k] = r.mu;
             t->sg[k] = r.sigma;
         } else {   // padding: never picked (u < 1 <= cdf[ns - 1])
             t->cdf[k] = 2.0;
+            t->thr[k] = 1ull << 33;
             t->mu[k] = 0.0;
             t->sg[k] = 0.0;
         }
@@ -295,8 +330,8 @@ __device__ __forceinline__ void draw_pair(const DLabel& L, const Src& src, uint3
                                           uint32_t it, uint32_t round, double& d0, double& d1) {
     const U4 r = philox4x32_10(U4{p, it, (uint32_t)L.stream, round}, k0, k1);
     double mu0, sg0, mu1, sg1;
-    src.pick((double)r.x * 0x1.0p-32, mu0, sg0);
-    src.pick((double)r.z * 0x1.0p-32, mu1, sg1);
+    src.pick(r.x, mu0, sg0);
+    src.pick(r.z, mu1, sg1);
     const double rad = bm_radius(r.y, src.log_tab());
     double c, s;
     sincos_turn32(r.w, c, s, src.cos_tab());
@@ -310,7 +345,7 @@ __device__ __forceinline__ double draw_attempt(const DLabel& L, const Src& src, 
     const U4 r = philox4x32_10(U4{g >> 1, it, (uint32_t)L.stream, round}, k0, k1);
     const bool h = (g & 1u) != 0;
     double mu, sg;
-    src.pick((double)(h ? r.z : r.x) * 0x1.0p-32, mu, sg);
+    src.pick(h ? r.z : r.x, mu, sg);
     const double rad = bm_radius(r.y, src.log_tab());
     double c, s;
     sincos_turn32(r.w, c, s, src.cos_tab());
@@ -420,6 +455,11 @@ __device__ __forceinline__ bool sample_slots(const DLabel& L, const Src& src, ui
     return ok;
 }
 
+// set bits of a wave mask below this lane (v_mbcnt_lo + v_mbcnt_hi)
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // The workgroup-cooperative form of sample_slots for tile kernels (every
 // thread of the workgroup calls it, uniform control flow): attempt 0 of
 // every slot straight-line; the rejected slots go to an LDS list and the
@@ -432,27 +472,39 @@ __device__ __forceinline__ bool sample_slots(const DLabel& L, const Src& src, ui
 // rejected slots of one tile are a few per cent of R * 256 with bounded
 // labels: one pass; more take several, each retrying the next CAP entries).
 // A smaller value array leaves LDS for more workgroups per CU.
+//
+// The list: each wave appends to its own segment of R * 64 entries, in
+// slot order, at the running count it keeps in a scalar register -- the
+// rejection mask of a slot IS its comparison's wave mask, so a slot costs
+// two v_mbcnt and an add (round 3: one LDS atomic and ~17 VALU operations
+// per slot); after the barrier the segments are read as one list in wave
+// order through their counts.
+constexpr int kTileWaves = 4;   // sample_tile: 256-thread workgroups
 template <int R, int CAP = R * 256>
 struct RetryLds {
-    int n[2];                 // per tile parity: this tile's count, the next tile's (reset)
-    uint16_t slot[R * 256];   // candidate offset within the tile
+    int wn[kTileWaves];       // per wave: its rejected slots of this tile
+    uint16_t slot[R * 256];   // per wave a segment of R * 64: candidate offset within the tile
     double val[CAP];
 };
 
-// (every thread of the workgroup calls it; q.n[0] = q.n[1] = 0 before the
-// first tile, a barrier in between; `par` alternates 0, 1 over the tiles:
-// two barriers per tile)
+// (every thread of the workgroup calls it, blockDim.x == 256; two barriers
+// per tile of a bounded label -- `par` is unused, kept for the callers.
+// Slots outside `pend` receive unspecified values: both callers read the
+// pending slots only.)
 template <int MODE, int R, typename Src, bool RAW = false, int CAP = R * 256>
 __device__ __forceinline__ bool sample_tile(const DLabel& L, const Src& src, uint64_t seed, uint32_t rk,
                                             uint32_t g0, uint32_t pend, double (&out)[R], RetryLds<R, CAP>& q,
                                             int par) {
     static_assert(MODE != CAT, "categorical slots draw once each");
     static_assert(R * 256 <= 65536, "tile offsets are 16-bit");
+    (void)par;
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     const bool bounded = (L.flags & 3) == 3;
-    const int lane = threadIdx.x & 63;
-    const uint64_t lt = (1ull << lane) - 1ull;
-    int pos[R];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint16_t* __restrict__ seg = q.slot + wave * (R * 64);
+    constexpr int kAccepted = 1 << 20;   // pos of an accepted slot: past any list
+    int pos[R];     // this lane's slots in its wave's segment (kAccepted: not listed)
+    int run = 0;    // the wave's rejected slots so far (uniform)
     static_assert(R % 2 == 0, "sample_tile draws Box-Muller pairs");
     const bool paired = (g0 & 1u) == 0;   // (an odd first index: each slot on its own, the same bits)
 #pragma unroll
@@ -469,31 +521,37 @@ __device__ __forceinline__ bool sample_tile(const DLabel& L, const Src& src, uin
         for (int h = 0; h < 2; ++h) {
             const double draw = dd[h];
             const bool p = (pend >> (r + h)) & 1u;
-            out[r + h] = p ? draw : out[r + h];
-            // rejected slots onto the list: one LDS atomic per wave
+            out[r + h] = draw;
             const bool rej = p && bounded && !(L.low <= draw && draw < L.high);
-            const uint64_t bal = __ballot(rej);
-            int base = 0;
-            if (bal) {
-                if (lane == 0) base = atomicAdd(&q.n[par], (int)__popcll(bal));
-                base = __shfl(base, 0);
-            }
-            pos[r + h] = rej ? base + (int)__popcll(bal & lt) : -1;
-            if (rej) q.slot[pos[r + h]] = (uint16_t)(c0 + (uint32_t)h);
+            const uint64_t m = __ballot(rej);
+            pos[r + h] = rej ? run + (int)lanes_below(m) : kAccepted;
+            if (rej) seg[pos[r + h]] = (uint16_t)(c0 + (uint32_t)h);
+            run += (int)__popcll(m);
         }
     }
     bool ok = true;
     if (bounded) {   // (a label without both bounds never rejects: no list, no barriers)
+        if (lane == 0) q.wn[wave] = run;
         __syncthreads();   // the list is complete
-        const int n = q.n[par];
-        if (threadIdx.x == 0) q.n[par ^ 1] = 0;   // (its last reader finished before the previous tile's end)
-        // (n is the workgroup's: uniform.  At least one barrier follows thread
-        // 0's reset of the next tile's counter before any thread moves on.)
-        if (n == 0) __syncthreads();
+        // the segments as one list: entry e of wave w's segment is list
+        // entry b[w] + e (b: the earlier waves' counts)
+        int b[kTileWaves + 1];
+        b[0] = 0;
+#pragma unroll
+        for (int w = 0; w < kTileWaves; ++w) b[w + 1] = b[w] + q.wn[w];
+        const int n = b[kTileWaves];   // (the workgroup's: uniform)
+        const int mine = b[wave];
+        if (n == 0) __syncthreads();   // (the counts are read before the next tile writes them)
         for (int c0 = 0; c0 < n; c0 += CAP) {
             const int c1 = min(n, c0 + CAP);
             for (int e = c0 + (int)threadIdx.x; e < c1; e += blockDim.x) {
-                const uint32_t gg = g0 + (uint32_t)q.slot[e];
+                int w = 0;
+#pragma unroll
+                for (int k = 1; k < kTileWaves; ++k) w += e >= b[k] ? 1 : 0;
+                int bw = b[0];
+#pragma unroll
+                for (int k = 1; k < kTileWaves; ++k) bw = w == k ? b[k] : bw;
+                const uint32_t gg = g0 + (uint32_t)q.slot[w * (R * 64) + (e - bw)];
                 double v = __builtin_nan("");
                 for (uint32_t it = 1; it < kMaxAttempts; ++it) {
                     const double draw = draw_attempt(L, src, k0, k1, gg, it, rk);
@@ -507,8 +565,10 @@ __device__ __forceinline__ bool sample_tile(const DLabel& L, const Src& src, uin
             }
             __syncthreads();
 #pragma unroll
-            for (int r = 0; r < R; ++r)
-                if (pos[r] >= c0 && pos[r] < c1) out[r] = q.val[pos[r] - c0];
+            for (int r = 0; r < R; ++r) {   // (list entry mine + pos in [c0, c1); kAccepted never is)
+                const uint32_t k = (uint32_t)(pos[r] + (mine - c0));
+                if (k < (uint32_t)(c1 - c0)) out[r] = q.val[k];
+            }
             if (c1 < n) __syncthreads();   // (the next pass reuses val)
         }
     }

@@ -820,7 +820,11 @@ __global__ __launch_bounds__(kBlock) void k_hot_bits(const int32_t* __restrict__
 // at the end; past the buffer a wave appends straight to the list.
 constexpr int kHotBuf = 256;
 constexpr int kHotRetry = 512;   // rejected draws retried cooperatively per tile (the rest in-thread)
-template <int R>
+// LDS_BITS: every label's bits fit in LDS (the host knows the largest
+// label's sub-bins) -- the bit test is then a ds_read; otherwise every
+// label reads them from global memory.  (One kernel choosing per label
+// compiled to a generic-address load with per-lane address selects.)
+template <int R, bool LDS_BITS>
 __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
     const BxLabel* __restrict__ bx, const uint32_t* __restrict__ hbits, int64_t n, int64_t cand_offset,
@@ -838,22 +842,21 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
     const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
     const uint32_t rk = rounds[blockIdx.z];
     constexpr int64_t per = (int64_t)R * kBlock;
-    // the label's bits in LDS when they fit (config 3: 19k sub-bins, 2.4 KB)
-    __shared__ uint32_t sbits[kHotLdsWords];
-    const bool lds_bits = nsb <= kHotLdsWords * 32;
-    if (lds_bits)
+    // the label's bits in LDS (config 3: 19k sub-bins, 2.4 KB)
+    __shared__ uint32_t sbits[LDS_BITS ? kHotLdsWords : 1];
+    if constexpr (LDS_BITS)
         for (int w = threadIdx.x; w < (nsb >> 5); w += kBlock) sbits[w] = hbits[(B.sb_off >> 5) + w];
+    const uint32_t* __restrict__ gbits = hbits + (B.sb_off >> 5);
     __shared__ RetryLds<R, kHotRetry> retry;
     __shared__ int32_t buf_i[kHotBuf];
     __shared__ double buf_x[kHotBuf];
     __shared__ int buf_n, gbase;
     if (threadIdx.x == 0) {
-        retry.n[0] = retry.n[1] = 0;
         buf_n = 0;
     }
     __syncthreads();   // the Box-Muller tables, the bits and the counters above
     const int lane = threadIdx.x & 63;
-    const uint64_t lt = (1ull << lane) - 1ull;
+    const int steps = __builtin_amdgcn_readfirstlane(sl.steps);   // (read once, not per pick)
     int par = 0;
     for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per, par ^= 1) {
         double x[R];
@@ -868,8 +871,8 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
         // keeps the draw and k_screen_hot applies the exp.  (The family only
         // changes that exp, which RAW leaves out: one instantiation.)
         const uint32_t g0 = (uint32_t)(cand_offset + base);
-        if (!sample_tile<DENSE_GMM, R, SampShared, true, kHotRetry>(L, SampShared{&sl, bm_cs, bm_lg}, seed, rk, g0,
-                                                                     pend, x, retry, par))
+        if (!sample_tile<DENSE_GMM, R, SampShared, true, kHotRetry>(L, SampShared{&sl, bm_cs, bm_lg, steps}, seed,
+                                                                     rk, g0, pend, x, retry, par))
             atomicOr(err, 1);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -878,7 +881,9 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
                 const double f = (x[r] - L.centre - B.xlo) * B.inv_sbw;
                 if (f >= 0.0 && f < (double)nsb) {
                     const int j = (int)f;   // (sb_off: a multiple of 32)
-                    const uint32_t word = lds_bits ? sbits[j >> 5] : hbits[(B.sb_off >> 5) + (j >> 5)];
+                    uint32_t word;
+                    if constexpr (LDS_BITS) word = sbits[j >> 5];
+                    else word = gbits[j >> 5];
                     take = (word >> (j & 31)) & 1u;
                 } else {
                     take = true;   // outside the bins (or NaN): always listed
@@ -888,14 +893,14 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
             if (!bal) continue;
             int at = 0;
             if (lane == 0) at = atomicAdd(&buf_n, (int)__popcll(bal));
-            at = __shfl(at, 0);
+            at = __builtin_amdgcn_readfirstlane(__shfl(at, 0));
             const bool lds = at + (int)__popcll(bal) <= kHotBuf;   // wave-uniform
             if (!lds) {   // the buffer is full: straight to the cell's list
                 if (lane == 0) at = atomicAdd(hcnt + cell, (int)__popcll(bal));
-                at = __shfl(at, 0);
+                at = __builtin_amdgcn_readfirstlane(__shfl(at, 0));
             }
             if (take) {
-                const int k = at + (int)__popcll(bal & lt);
+                const int k = at + (int)lanes_below(bal);
                 const int32_t ci = (int32_t)(base + (int64_t)tile_cand(r, threadIdx.x, kBlock));
                 if (lds) {
                     buf_i[k] = ci;
@@ -2405,7 +2410,6 @@ __global__ __launch_bounds__(kBlock, 4) void k_qfused_tiles(
     __syncthreads();
     const bool early = found && Q.G > 0 && Q.jlo <= Q.jhi;
     const uint64_t kmax = early ? qkmax[qbase + blockIdx.y] : 0;
-    if (threadIdx.x == 0) retry.n[0] = retry.n[1] = 0;
     __syncthreads();
     int par = 0;
     bool reported = false;
@@ -3251,14 +3255,19 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                 }
                 const int64_t cells_l = (int64_t)nl * a.gz;
                 // ~kHotWgs workgroups over the round (tiles strided), at most one per tile
-                hipLaunchKernelGGL((k_hot_bx<kHotR>),
-                                   dim3((unsigned)std::max<int64_t>(
-                                            1, std::min<int64_t>((a.n + kHotR * kBlock - 1) / (kHotR * kBlock),
-                                                                 kHotWgs / cells_l)),
-                                        nl, a.gz),
-                                   dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.samp.p, P.bx.p, ctx->hot_bits.p,
-                                   a.n, a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->hot_cnt.p, ctx->hot_i.p,
-                                   ctx->hot_x.p, ctx->errflag.p, lst, ctx->hot_flag.p);
+                const dim3 hg((unsigned)std::max<int64_t>(
+                                  1, std::min<int64_t>((a.n + kHotR * kBlock - 1) / (kHotR * kBlock), kHotWgs / cells_l)),
+                              nl, a.gz);
+                if (P.bx_sb_max <= (int64_t)kHotLdsWords * 32)
+                    hipLaunchKernelGGL((k_hot_bx<kHotR, true>), hg, dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
+                                       P.samp.p, P.bx.p, ctx->hot_bits.p, a.n, a.cand_offset, a.seed, ctx->rounds.p,
+                                       nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p, ctx->errflag.p, lst,
+                                       ctx->hot_flag.p);
+                else
+                    hipLaunchKernelGGL((k_hot_bx<kHotR, false>), hg, dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
+                                       P.samp.p, P.bx.p, ctx->hot_bits.p, a.n, a.cand_offset, a.seed, ctx->rounds.p,
+                                       nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p, ctx->errflag.p, lst,
+                                       ctx->hot_flag.p);
                 const unsigned bgx = (unsigned)((a.n + kBxR * kBlock - 1) / (kBxR * kBlock));
                 hipLaunchKernelGGL((k_screen_hot<kBxR>), dim3(std::min(bgx, kHotScreenWgs), nl, a.gz), dim3(kBlock),
                                    0, ctx->stream, P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p, P.bx_loff.p,
