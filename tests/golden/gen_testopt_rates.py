@@ -29,6 +29,10 @@ from hyperopt.tests import test_domains as TD  # noqa: E402  (reference)
 from hyperopt.tests.test_tpe import TestOpt  # noqa: E402  (reference)
 
 N_SEEDS = int(os.environ.get('N_SEEDS', '20'))
+# a subset of the domains (comma-separated) into its own fixture, e.g.
+#   N_SEEDS=100 DOMAINS=branin OUT=testopt_reference_branin100.json
+DOMAINS = [d for d in os.environ.get('DOMAINS', '').split(',') if d]
+OUT = os.environ.get('OUT', 'testopt_reference_rates.json')
 
 
 def passthrough(x):
@@ -40,7 +44,7 @@ def main():
     olderr = np.seterr('raise')
     np.seterr(under='ignore')
     try:
-        for name in sorted(TestOpt.thresholds):
+        for name in sorted(DOMAINS or TestOpt.thresholds):
             bandit = getattr(TD, name)()
             algo = partial(tpe.suggest,
                            gamma=TestOpt.gammas.get(name, tpe._default_gamma),
@@ -58,7 +62,7 @@ def main():
             print('%-14s pass rate %.2f' % (name, rate), flush=True)
     finally:
         np.seterr(**olderr)
-    with open(os.path.join(HERE, 'testopt_reference_rates.json'), 'w') as f:
+    with open(os.path.join(HERE, OUT), 'w') as f:
         json.dump(out, f, indent=1)
 
 
