@@ -850,9 +850,10 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
     __shared__ RetryLds<R, kHotRetry> retry;
     __shared__ int32_t buf_i[kHotBuf];
     __shared__ double buf_x[kHotBuf];
-    __shared__ int buf_n, gbase;
+    __shared__ int buf_n, buf_end, gbase;
     if (threadIdx.x == 0) {
         buf_n = 0;
+        buf_end = kHotBuf;   // the LDS entries actually written (a wave straddling the end lowers it)
     }
     __syncthreads();   // the Box-Muller tables, the bits and the counters above
     const int lane = threadIdx.x & 63;
@@ -896,6 +897,9 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
             at = __builtin_amdgcn_readfirstlane(__shfl(at, 0));
             const bool lds = at + (int)__popcll(bal) <= kHotBuf;   // wave-uniform
             if (!lds) {   // the buffer is full: straight to the cell's list
+                // (the one wave whose reservation straddles the end leaves
+                // [at, kHotBuf) unwritten: the flush stops there)
+                if (lane == 0 && at < kHotBuf) buf_end = at;
                 if (lane == 0) at = atomicAdd(hcnt + cell, (int)__popcll(bal));
                 at = __builtin_amdgcn_readfirstlane(__shfl(at, 0));
             }
@@ -914,7 +918,7 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
         }
     }
     __syncthreads();
-    const int m = min(buf_n, kHotBuf);
+    const int m = min(buf_n, buf_end);   // (round 3 flushed min(buf_n, kHotBuf): unwritten entries too)
     if (threadIdx.x == 0) gbase = m ? atomicAdd(hcnt + cell, m) : 0;
     __syncthreads();
     // a cell's list is hstride long: past it the round falls back to

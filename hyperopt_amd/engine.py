@@ -303,6 +303,7 @@ class Engine(object):
         need = len(rounds) * self._labels() * RESULT_DTYPE.itemsize
         if not d_out.is_cuda or d_out.numel() * d_out.element_size() < need or not d_out.is_contiguous():
             raise ValueError('d_out must be a contiguous device tensor of %d bytes' % need)
+        _torch_stream_done(d_out)
         self._check(self.lib.tpe_suggest_batch_device(
             self.h, int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(rounds), len(rounds), int(n_candidates),
             int(cand_offset), ctypes.c_void_p(d_out.data_ptr()), None))
@@ -311,6 +312,11 @@ class Engine(object):
     def merge_results_device(self, d_parts, n_parts, n, d_out):
         """tpe_merge_results over device tensors (n_parts blocks of n records
         -> n records), on this engine's GPU."""
+        rec = RESULT_DTYPE.itemsize
+        for t, need, what in ((d_parts, n_parts * n * rec, 'd_parts'), (d_out, n * rec, 'd_out')):
+            if not t.is_cuda or t.numel() * t.element_size() < need or not t.is_contiguous():
+                raise ValueError('%s must be a contiguous device tensor of %d bytes' % (what, need))
+        _torch_stream_done(d_parts)
         self._check(self.lib.tpe_merge_results_device(
             self.h, ctypes.c_void_p(d_parts.data_ptr()), int(n_parts), int(n),
             ctypes.c_void_p(d_out.data_ptr())))
@@ -515,6 +521,16 @@ class Engine(object):
                                                     int(stream), int(round), int(offset), n,
                                                     _ptr(out)))
         return out.reshape(size if size != () else (1,))
+
+
+def _torch_stream_done(t):
+    """The device entry points run on the context's own stream: work torch
+    queued on its current stream for these buffers (the H2D copy that filled
+    them, the RCCL all-gather that wrote them, a read of the previous round)
+    must be complete before the call.  (Round 4's first GPU run merged a
+    buffer whose H2D copy had not landed.)"""
+    import torch
+    torch.cuda.current_stream(t.device).synchronize()
 
 
 def merge_results(parts):

@@ -318,14 +318,18 @@ int tpe_suggest_batch(tpe_ctx *ctx, uint64_t seed, const uint32_t *rounds,
  * by a device-to-device copy, complete when the call returns -- the buffer a
  * process-per-GPU caller all-gathers over RCCL without a host round trip
  * (the reference's one algo call per round, fmin.py:201-202).
- * out (host, may be NULL) receives them too. */
+ * out (host, may be NULL) receives them too.  The call runs on the
+ * context's own stream: the caller completes any work of its own streams on
+ * d_out first. */
 int tpe_suggest_batch_device(tpe_ctx *ctx, uint64_t seed, const uint32_t *rounds,
                              int32_t n_rounds, int64_t n_candidates, int64_t cand_offset,
                              tpe_label_result *d_out, tpe_label_result *out);
 
 /* tpe_merge_results on device buffers of ctx's GPU (d_parts: n_parts blocks
  * of n results, e.g. an RCCL all-gather of the ranks' tpe_suggest_batch_device
- * outputs; d_out: n results), on the context's stream, complete on return. */
+ * outputs; d_out: n results), on the context's stream, complete on return.
+ * d_parts must be complete when called (an H2D copy or collective on another
+ * stream synchronised first: nothing orders it against this stream). */
 int tpe_merge_results_device(tpe_ctx *ctx, const tpe_label_result *d_parts, int32_t n_parts,
                              int32_t n, tpe_label_result *d_out);
 

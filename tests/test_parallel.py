@@ -371,7 +371,12 @@ def test_device_exchange_rccl_world1():
     out = q.get(timeout=240)
     p.join(timeout=60)
     assert p.exitcode == 0
+    def diff(a, b):
+        a = np.frombuffer(a, dtype=RESULT_DTYPE)
+        b = np.frombuffer(b, dtype=RESULT_DTYPE)
+        return [(int(i), a[i]['index'], b[i]['index'], a[i]['value'], b[i]['value'], a[i]['score'],
+                 b[i]['score']) for i in range(len(a)) if a[i].tobytes() != b[i].tobytes()][:5]
     for mode in ('candidates', 'rounds', 'labels'):
-        assert out[mode][0] == out['host'][0], mode
-        assert out[mode][1] == out['host'][1], mode
+        assert out[mode][0] == out['host'][0], (mode, diff(out[mode][0], out['host'][0]))
+        assert out[mode][1] == out['host'][1], (mode, diff(out[mode][1], out['host'][1]))
     assert out['merge'] == out['merge_host']
