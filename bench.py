@@ -278,6 +278,9 @@ def suggest_latency(n_labels, n_trials, n_reps=20, n_warm=3):
     return float(np.median(times[n_warm:])) * 1e3
 
 
+PMC_MIN_CLOCK_GHZ = 2.0
+
+
 def measured_pmc(kernel_prefix):
     """HBM bytes per launch and VALU issue utilisation of the dominant kernel
     from the newest committed PMC summary that has it (rocprofv3 --pmc passes
@@ -294,7 +297,14 @@ def measured_pmc(kernel_prefix):
         d = json.load(open(f))
         for name, v in d.items():
             if name.startswith(kernel_prefix) and '_hbm_bytes_per_launch' in v:
-                return v['_hbm_bytes_per_launch'], v.get('_valu_busy'), os.path.relpath(f, REPO)
+                # a counter run well below the bench's clock says little
+                # about the timed kernel: refuse it
+                clk = v.get('_eff_clock_ghz')
+                src = os.path.relpath(f, REPO)
+                if clk is None or clk < PMC_MIN_CLOCK_GHZ:
+                    return None, None, '%s refused: effective clock %s GHz < %.1f' % (
+                        src, 'unrecorded' if clk is None else '%.2f' % clk, PMC_MIN_CLOCK_GHZ)
+                return v['_hbm_bytes_per_launch'], v.get('_valu_busy'), '%s (%.2f GHz)' % (src, clk)
     return None, None, None
 
 

@@ -274,6 +274,26 @@ def test_sampler_ks(eng, log, bounds):
     assert kstest(x, _mix_cdf(W4, mus, S4, low, high, log)).pvalue > 1e-4
 
 
+# The Box-Muller radius sqrt(-2 log u) takes u = 1 - y 2^-32 from one 32-bit
+# Philox word (tpe_device.h u01_open0), so every normal the samplers draw
+# has |z| <= sqrt(-2 log 2^-32) = sqrt(64 ln 2): the draws are N(0, 1)
+# truncated there.  The reference's MT19937 normals (53-bit) reach ~8.3
+# sigma; the distributions differ by total variation 2 sf(Z_CAP) per draw
+# (test_oracle.py test_normal_draw_cap_mass: < 2.8e-11).
+Z_CAP = float(np.sqrt(64.0 * np.log(2.0)))
+
+
+def test_normal_draw_cap(eng):
+    """Every draw within the cap (a bound, not a tendency), and the tail up to
+    it present: the count beyond 4.5 sigma is N(0, 1)'s (Poisson, 5 sd)."""
+    n = 1 << 22
+    x = eng.GMM1([1.0], [0.0], [1.0], seed=7, size=(n,))
+    assert np.abs(x).max() <= Z_CAP * (1 + 1e-12)
+    lam = n * 2 * 3.3976731247300535e-06           # 2 sf(4.5)
+    k = int(np.count_nonzero(np.abs(x) > 4.5))
+    assert abs(k - lam) < 5 * np.sqrt(lam)
+
+
 def test_categorical_sampler_distribution(eng):
     p = np.array([0.1, 0.2, 0.3, 0.4])
     x = eng.categorical(p, seed=5, size=(200000,))

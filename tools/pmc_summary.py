@@ -42,12 +42,17 @@ def short(name):
 def pmc(path):
     per = defaultdict(lambda: defaultdict(float))
     launches = defaultdict(set)
+    dur = defaultdict(dict)
     for row in csv.DictReader(open(path)):
         k = short(row['Kernel_Name'])
         per[k][row['Counter_Name']] += float(row['Counter_Value'])
         launches[k].add(row['Dispatch_Id'])
-    return {k: {c: v / len(launches[k]) for c, v in d.items()} for k, d in per.items()}, \
-        {k: len(v) for k, v in launches.items()}
+        if row.get('Start_Timestamp') and row.get('End_Timestamp'):
+            dur[k][row['Dispatch_Id']] = float(row['End_Timestamp']) - float(row['Start_Timestamp'])
+    out = {k: {c: v / len(launches[k]) for c, v in d.items()} for k, d in per.items()}
+    for k, d in dur.items():   # the launch duration IN THIS (counter) run
+        out[k]['_pmc_run_ns_per_launch'] = sum(d.values()) / len(d)
+    return out, {k: len(v) for k, v in launches.items()}
 
 
 def main(src, tag):
@@ -94,9 +99,12 @@ def main(src, tag):
             ev = win_terms * steps / max(nlaunch.get(k, 1), 1)
             v['_evals_per_launch'] = ev
             v['_valu_instr_per_eval'] = v['SQ_INSTS_VALU'] * 64 / ev
-        if k.startswith('k_screen_bx') and cands and 'SQ_INSTS_VALU' in v:
-            # the expansion screen: VALU instructions per candidate
-            c = cands * steps / max(nlaunch.get(k, 1), 1)
+        if k.startswith(('k_screen_bx', 'k_hot_bx')) and cands and 'SQ_INSTS_VALU' in v:
+            # the expansion screen / hot prefilter: VALU instructions per
+            # candidate (k_hot_bx: ONE launch per round over every dense
+            # label's candidates, whatever extra rounds the run made)
+            c = (cands if k.startswith('k_hot_bx')
+                 else cands * steps / max(nlaunch.get(k, 1), 1))
             v['_candidates_per_launch'] = c
             v['_valu_instr_per_candidate'] = v['SQ_INSTS_VALU'] * 64 / c
         if 'SQ_INSTS_VALU' in v and v.get('GRBM_GUI_ACTIVE'):
@@ -105,6 +113,12 @@ def main(src, tag):
             # = the launch's GPU cycles
             cycles = 1024 * v['GRBM_GUI_ACTIVE'] / 8
             v['_valu_busy'] = v['SQ_INSTS_VALU'] * 4 / cycles
+            # the clock the counter run actually ran at: GPU cycles per XCD
+            # over the launch's duration in that run (bench.py refuses PMC
+            # figures from a run below 2 GHz)
+            ns = v.get('_pmc_run_ns_per_launch')
+            if ns:
+                v['_eff_clock_ghz'] = v['GRBM_GUI_ACTIVE'] / 8 / ns
             if k.startswith('k_screen') and '_evals_per_launch' in v:
                 # one v_exp_f32 (8-cycle issue) per eval: 4 extra cycles per
                 # 64 evals on top of the 4-cycle count
@@ -116,7 +130,8 @@ def main(src, tag):
                         'FETCH_SIZE correction of MI355X_MICROARCH.md; SQ_INSTS_VALU counts wave '
                         'instructions (x64 lanes for _valu_instr_per_eval); GRBM_GUI_ACTIVE is '
                         'summed over the 8 XCDs; _valu_busy = SQ_INSTS_VALU x 4 cycles / '
-                        '(1024 SIMDs x GRBM_GUI_ACTIVE / 8)')
+                        '(1024 SIMDs x GRBM_GUI_ACTIVE / 8); _eff_clock_ghz = GRBM_GUI_ACTIVE / 8 / '
+                        'the launch duration in the counter run (_pmc_run_ns_per_launch)')
     json.dump(summary, open(os.path.join(dst, '%s_pmc_summary.json' % tag), 'w'), indent=1,
               sort_keys=True)
     print(json.dumps({k: v for k, v in summary.items() if k.startswith(('k_round', 'k_screen'))},
