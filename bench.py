@@ -424,9 +424,11 @@ def main():
         lp = loop if lp is None else lp
         nc = C if n is None else n
         if fresh:
+            t0 = time.perf_counter()
             lp.advance(e, args.trials + (i + 1) * args.append,
                        n_candidates=nc if args.precision == 'f64' else 0,
                        n_rounds=ids_local if args.config == 5 else 1)
+            P._phase('advance_total', t0)
         if args.config == 5:   # independent new_ids split over the GPUs (or each rank's labels)
             first_id = i * args.new_ids + (0 if by_label else rank * ids_local)
             ids = list(range(first_id, first_id + ids_local))
@@ -489,7 +491,9 @@ def main():
     # the expansion screen's index (bin tables, lists, sub-bin bounds) is
     # built once per posterior, in its first large round
     prep_ms = eng.last_prepare_ms() if args.warmup > 0 else None
+    P.PHASES = {}     # host-timer breakdown of the timed steps' posterior work
     dt, mode_ms, mode_ev, scr = timed(args.steps, args.warmup, fresh_mode)
+    phases, P.PHASES = P.PHASES, None
     smode_timed = eng.last_screen_mode()   # (the timed rounds' screen; later legs run others)
     # the same rounds on the posterior of the last step, reused (no append):
     # the round alone, and the reference for the unscreened comparison
@@ -711,6 +715,14 @@ def main():
                           % args.append,
                   'history_first_step': args.trials + args.append,
                   'expansion_index_ms': round(scr[7] / args.steps, 3),
+                  'advance_breakdown_ms': {k: round(v[1] / args.steps * 1e3, 3)
+                                           for k, v in sorted(phases.items())},
+                  'advance_breakdown_note': 'host wall ms per step: append (transform + upload of the '
+                                            'new observations), build (device build + its tie report, '
+                                            'synchronous), prepare_enqueue (the expansion index queued), '
+                                            'argsorts (numpy np.argsort for tie-dependent labels, while '
+                                            'the index runs), rebuild (those labels again); '
+                                            'advance_total = all of it; the round follows',
                   'warm_round_ms': round(wdt / args.steps * 1e3, 3),
                   'warm_note': 'the same rounds on one resident posterior (no append, no rebuild, '
                                'no index): the round alone'}

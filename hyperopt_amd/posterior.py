@@ -15,12 +15,28 @@ same order, including the default, non-stable np.argsort tie order):
 It is vectorised over the history (no per-trial Python loops).
 """
 import threading
+import time
 import weakref
 
 import numpy as np
 
 from . import _lib as L
 from .engine import DESC_DTYPE
+
+# host-timer breakdown of the fmin step's posterior work (bench.py's
+# `advance_breakdown_ms`): None, or a dict phase -> [calls, seconds]
+PHASES = None
+
+
+def _phase(name, t0):
+    """Account perf_counter() - t0 to `name` (when PHASES is on); returns
+    the new t0."""
+    t = time.perf_counter()
+    if PHASES is not None:
+        c = PHASES.setdefault(name, [0, 0.0])
+        c[0] += 1
+        c[1] += t - t0
+    return t
 
 EPS = 1e-12
 DEFAULT_LF = 25
@@ -361,18 +377,25 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
     Returns (n_below, the labels that needed an order)."""
     n_below = n_below_of(n_valid, gamma)
     known = set(known)
+    t0 = time.perf_counter()
     if prepare and (overlap or not known):
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf)
+        t0 = _phase('build', t0)
         eng.prepare(*prepare)
+        t0 = _phase('prepare_enqueue', t0)
         have = set()
     elif known:
         below, off, order = reference_orders(losses, n_below, obs_of, known)
+        t0 = _phase('argsorts', t0)
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf, below, off, order)
+        t0 = _phase('build', t0)
         if prepare:
             eng.prepare(*prepare)
+            t0 = _phase('prepare_enqueue', t0)
         have = known
     else:
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf)
+        t0 = _phase('build', t0)
         have = set()
     if np.any(ties[:-1] & 1):
         # a below mixture holds at most gamma_cap <= lf observations: its
@@ -381,6 +404,7 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
     need = have | set(np.flatnonzero(ties[:-1] & 2).tolist())
     if need != have or ties[-1]:
         below, off, order = reference_orders(losses, n_below, obs_of, need)
+        t0 = _phase('argsorts', t0)
         if SUBSET_REBUILD and not ties[-1] and len(need) < obs_of.n_labels:
             # no tie across the split (the below set is the one just built):
             # rebuild only the labels that needed an order
@@ -388,6 +412,7 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
         else:
             nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf, below, off,
                                                    order)
+        t0 = _phase('rebuild', t0)
         if np.any(ties[:-1]):
             # a supplied below set can move observations between the sets,
             # creating a dependent label the first pass did not see
@@ -457,6 +482,7 @@ class DeviceHistoryUploader(object):
             self.pos_parts = [[] for _ in labels]    # what the device holds, per label
             self.val_parts = [[] for _ in labels]
             self.tie_labels = frozenset()
+        t0 = time.perf_counter()
         counts = list(self.prev_counts)
         # the new observations of every label, transformed and placed in one
         # vectorised pass (a per-label numpy loop cost ~0.4 ms per fmin step
@@ -500,6 +526,7 @@ class DeviceHistoryUploader(object):
         self.owner = weakref.ref(owner)
         self.n_trials = len(tids)
         self.last_tid = tids[-1] if len(tids) else None
+        _phase('append', t0)
         nb, self.tie_labels = build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf,
                                                     self._obs_of(len(labels)), self.tie_labels,
                                                     prepare=prepare, overlap=overlap)

@@ -352,6 +352,8 @@ def _nccl_world1_worker(port, q):
         d_out = torch.empty(len(a) * RESULT_DTYPE.itemsize, dtype=torch.uint8, device='cuda')
         eng.merge_results_device(d_parts, 3, len(a), d_out)
         out['merge'] = d_out.cpu().numpy().tobytes()
+        out['parts'] = parts.tobytes()
+        out['d_parts'] = d_parts.cpu().numpy().tobytes()
         from hyperopt_amd.engine import merge_results
         out['merge_host'] = np.ascontiguousarray(merge_results(parts)).tobytes()
         eng.close()
@@ -379,4 +381,11 @@ def test_device_exchange_rccl_world1():
     for mode in ('candidates', 'rounds', 'labels'):
         assert out[mode][0] == out['host'][0], (mode, diff(out[mode][0], out['host'][0]))
         assert out[mode][1] == out['host'][1], (mode, diff(out[mode][1], out['host'][1]))
-    assert out['merge'] == out['merge_host']
+    assert out['d_parts'] == out['parts']
+    if out['merge'] != out['merge_host']:
+        parts = np.frombuffer(out['parts'], dtype=RESULT_DTYPE).reshape(3, -1)
+        a = np.frombuffer(out['merge'], dtype=RESULT_DTYPE)
+        b = np.frombuffer(out['merge_host'], dtype=RESULT_DTYPE)
+        bad = [j for j in range(len(a)) if a[j].tobytes() != b[j].tobytes()]
+        raise AssertionError('device merge differs at %s: device %s host %s parts %s' % (
+            bad, a[bad[0]], b[bad[0]], parts[:, bad[0]]))
