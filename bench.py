@@ -423,22 +423,36 @@ def main():
         e = eng if e is None else e
         lp = loop if lp is None else lp
         nc = C if n is None else n
-        if fresh:
-            t0 = time.perf_counter()
-            lp.advance(e, args.trials + (i + 1) * args.append,
-                       n_candidates=nc if args.precision == 'f64' else 0,
-                       n_rounds=ids_local if args.config == 5 else 1)
-            P._phase('advance_total', t0)
+        exchange = dist is not None and gather
+        off = 0 if by_label else rank * nc
         if args.config == 5:   # independent new_ids split over the GPUs (or each rank's labels)
             first_id = i * args.new_ids + (0 if by_label else rank * ids_local)
             ids = list(range(first_id, first_id + ids_local))
-            if dist is not None and gather:   # every rank ends with every new_id's winners
-                return xch.round(1234, ids, C)
-            return e.suggest_batch(seed=1234, rounds=ids, n_candidates=C)
-        off = 0 if by_label else rank * nc
-        if dist is not None and gather:   # the winners (L x 48 B) all-gathered device to device
-            return xch.round(1234 + i, [i], nc, cand_offset=off)[0]
-        return e.suggest(seed=1234 + i, n_candidates=nc, round=i, cand_offset=off)
+            if exchange:   # every rank ends with every new_id's winners
+                def rnd():
+                    return xch.round(1234, ids, C)
+            else:
+                def rnd():
+                    return e.suggest_batch(seed=1234, rounds=ids, n_candidates=C)
+        elif exchange:   # the winners (L x 48 B) all-gathered device to device
+            def rnd():
+                return xch.round(1234 + i, [i], nc, cand_offset=off)[0]
+        else:
+            def rnd():
+                return e.suggest(seed=1234 + i, n_candidates=nc, round=i, cand_offset=off)
+        if fresh:
+            # the round runs inside advance as tpe.suggest runs it (the dense
+            # labels' round under the host's tie-order argsorts), except
+            # under the device exchange (its collective follows the round)
+            t0 = time.perf_counter()
+            out = lp.advance(e, args.trials + (i + 1) * args.append,
+                             n_candidates=nc if args.precision == 'f64' else 0,
+                             n_rounds=ids_local if args.config == 5 else 1,
+                             round_call=None if exchange else rnd)
+            P._phase('step_total', t0)
+            if not exchange:
+                return out[1]
+        return rnd()
 
     def timed(n_steps, first, fresh, keep=False, n=None):
         """Run n_steps steps (barrier + sync on both sides); returns wall
@@ -721,8 +735,11 @@ def main():
                                             'new observations), build (device build + its tie report, '
                                             'synchronous), prepare_enqueue (the expansion index queued), '
                                             'argsorts (numpy np.argsort for tie-dependent labels, while '
-                                            'the index runs), rebuild (those labels again); '
-                                            'advance_total = all of it; the round follows',
+                                            'the index runs), rebuild (those labels again), round; with '
+                                            'the dense labels\' round under the argsorts: '
+                                            'argsorts_under_round (max of the two), rebuild, quant_round '
+                                            '(the quantized labels after their rebuild); step_total = '
+                                            'all of it',
                   'warm_round_ms': round(wdt / args.steps * 1e3, 3),
                   'warm_note': 'the same rounds on one resident posterior (no append, no rebuild, '
                                'no index): the round alone'}

@@ -405,6 +405,7 @@ struct tpe_ctx {
     bool hot_redo = false;               // the round runs again without the prefilter (its check failed)
     DevBuf<int64_t> rs_plan;             // the re-score's plan (k_rescore_plan: total, entries, sliced)
     bool value_only = false;             // TPE_OPT_VALUE_ONLY: packed rounds skip the lpdfs of certified winners
+    int32_t mode_mask = 31;              // TPE_OPT_MODE_MASK: the label families sampled rounds launch
     int64_t pk_cap = 1 << 16;            // packed re-score: candidates its buffers hold (grows)
     bool pk_plan_pending = false;        // the packed plan awaits the round's sync
     bool pk_redo = false;                // the round runs again after a plan overflow

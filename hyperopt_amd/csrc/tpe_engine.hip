@@ -3752,10 +3752,16 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         const int rc = run_fills(ctx, f);
         if (rc) return rc;
     }
+    // the families this round launches (TPE_OPT_MODE_MASK); the others keep
+    // their statistics from the round that last ran them, and their result
+    // entries are unspecified
+    const int32_t fam = only_label >= 0 ? 31 : ctx->mode_mask;
+    const bool dense_on = (fam & 3) != 0;
     Groups g;
     for (int m = 0; m < kNumModes; ++m) {
         g.dev[m] = ctx->P->groups.p + ctx->P->group_off[m];
-        g.count[m] = (int32_t)ctx->P->h_group[m].size();
+        g.count[m] = (fam >> m) & 1 ? (int32_t)ctx->P->h_group[m].size() : 0;
+        if (!((fam >> m) & 1)) continue;
         ctx->mode_ran[m] = false;
         ctx->mode_ms[m] = 0.f;
         ctx->mode_evals[m] = 0;
@@ -3779,15 +3785,17 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         S.cpack ? (uint32_t)((rounds_whole + S.rpb - 1) / S.rpb) : gx;
     RoundArgs a{n, cand_offset, seed, n_rounds, tiles, cand_in_dev, olb, ola, S, gx, gz,
                 n_whole * rounds_whole, gx_whole};
-    ctx->screen_total = ctx->screen_rescored = 0;
-    ctx->hot_ran = false;
-    ctx->hot_listed = 0;
-    ctx->hot_fallback = 0;
+    if (dense_on) {
+        ctx->screen_total = ctx->screen_rescored = 0;
+        ctx->hot_ran = false;
+        ctx->hot_listed = 0;
+        ctx->hot_fallback = 0;
+        ctx->screen_mode = 0;
+        ctx->screen_exec = 0;
+        ctx->screen_rescore_terms = 0;
+    }
+    if (fam & (1 << CAT)) ctx->cat_early = false;
     ctx->pk_plan_pending = false;
-    ctx->cat_early = false;
-    ctx->screen_mode = 0;
-    ctx->screen_exec = 0;
-    ctx->screen_rescore_terms = 0;
     ctx->evw_used = 0;
     ctx->screen_pending = false;
     ctx->screen_exec_pending = false;
@@ -3873,7 +3881,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         ctx->pk_redo = false;
         return rc;
     }
-    if (ctx->hot_ran) {
+    if (dense_on && ctx->hot_ran) {
         for (int64_t c = 0; c < ctx->hot_cells; ++c) ctx->hot_listed += ctx->hot_cnt_h[c];
         const int32_t hf = pin.hot_flag;
         if (hf && !ctx->hot_redo) {
@@ -3897,7 +3905,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     const int32_t errh = pin.err;
     ctx->xdrawn_h[0] = pin.xdrawn[0];
     ctx->xdrawn_h[1] = pin.xdrawn[1];
-    ctx->screen_ms = 0.f;
+    if (dense_on) ctx->screen_ms = 0.f;
     if (ctx->screen_exec_pending) {
         ctx->screen_exec += (int64_t)ctx->pin[0].screen_exec;
         ctx->screen_exec_pending = false;
@@ -3939,6 +3947,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     for (int32_t l = 0; l < L; ++l) {
         if (only_label >= 0 && l != only_label) continue;
         const DLabel& d = ctx->P->h_labels[l];
+        if (!((fam >> d.mode) & 1)) continue;   // not launched (TPE_OPT_MODE_MASK)
         if (sample && (d.mode == QUANT_GMM || d.mode == QUANT_LGMM)) continue;  // counted below
         if (d.mode == CAT && ctx->cat_early) continue;   // counted below: the candidates drawn
         const int64_t e = ((d.mode == CAT) ? 2 * n : n * (int64_t)(d.nb + d.na)) * n_rounds;
@@ -4538,6 +4547,10 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
         case TPE_OPT_EARLY: ctx->early = value != 0; break;
         case TPE_OPT_ZERO_WIN: ctx->zero_win = value != 0; break;
         case TPE_OPT_VALUE_ONLY: ctx->value_only = value != 0; break;
+        case TPE_OPT_MODE_MASK:
+            if (value < 1 || value > 31) return ctx->fail(TPE_ERR_ARG, "family mask must be in [1, 31]");
+            ctx->mode_mask = (int32_t)value;
+            break;
         case TPE_OPT_RESCORE_CAP:
             if (value < 1) return ctx->fail(TPE_ERR_ARG, "re-score capacity must be positive");
             ctx->pk_cap = value;

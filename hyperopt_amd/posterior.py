@@ -353,8 +353,59 @@ def _sort_pool():
 SUBSET_REBUILD = True   # the ordered rebuild restricted to the labels that need an order
 
 
+MASK_ALL = 31                      # TPE_OPT_MODE_MASK: every label family
+MASK_QUANT = (1 << 2) | (1 << 3)   # the quantized GMM1 / LGMM1 families
+
+
+def _run_deferred(eng, round_call, reference, rebuild, quant, t0):
+    """The round of a posterior whose quantized labels still wait for their
+    tie orders: the dense and categorical labels' round runs on a second
+    thread (the engine call releases the GIL) while this one computes the
+    orders (`reference`, numpy's argsorts: they release it too); then the
+    quantized labels are rebuilt (`rebuild`, which returns the build's tie
+    report) and their round runs.  The dense labels' mixtures are
+    bit-identical before and after that rebuild (continuous values carry no
+    ties), so the merged results are those of the one round on the ordered
+    posterior.  Returns (results or None, the rebuild's (n_below, ties)):
+    None when the rebuild reports a dependent label (a defensive path: a
+    rebuild over the same split leaves none; the caller then rebuilds in full
+    and runs the whole round)."""
+    eng.set_option('mode_mask', MASK_ALL & ~MASK_QUANT)
+    box = {}
+
+    def run():
+        try:
+            box['res'] = round_call()
+        except BaseException as e:   # re-raised on the caller's thread
+            box['err'] = e
+    th = threading.Thread(target=run, name='tpe-dense-round')
+    th.start()
+    try:
+        orders = reference()
+    finally:
+        th.join()
+        eng.set_option('mode_mask', MASK_ALL)
+    if 'err' in box:
+        raise box['err']
+    t0 = _phase('argsorts_under_round', t0)
+    built = rebuild(orders)
+    t0 = _phase('rebuild', t0)
+    if np.any(built[1][:-1]):
+        return None, built
+    eng.set_option('mode_mask', MASK_QUANT)
+    try:
+        res_q = round_call()
+    finally:
+        eng.set_option('mode_mask', MASK_ALL)
+    _phase('quant_round', t0)
+    res = box['res']
+    cols = sorted(quant)
+    res[..., cols] = res_q[..., cols]
+    return res, built
+
+
 def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of, known=(), prepare=None,
-                          overlap=True):
+                          overlap=True, round_call=None, quant=frozenset()):
     """Device build whose mixtures follow the reference's tie order
     (tpe.py:433, 637): the device reports which mixtures depend on the order
     of tied observations (or a tie of losses at the split), and only for
@@ -374,7 +425,14 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
       second build it saves) the `known` orders go up front as above and the
       index is queued after the one build.
 
-    Returns (n_below, the labels that needed an order)."""
+    round_call (optional): the coming round, a callable returning the
+    engine's results; it then runs here and its results are returned as a
+    third value.  When the labels still needing an order after the first
+    build are all quantized (`quant`: their positions), the round of the
+    other labels runs while the host computes those orders (_run_deferred):
+    the argsorts leave the step's critical path.
+
+    Returns (n_below, the labels that needed an order[, results])."""
     n_below = n_below_of(n_valid, gamma)
     known = set(known)
     t0 = time.perf_counter()
@@ -402,6 +460,21 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
         # weights are all equal, so its order can never matter
         raise AssertionError('below mixture depends on a tie order (lf < gamma_cap?)')
     need = have | set(np.flatnonzero(ties[:-1] & 2).tolist())
+    res = None
+    if (round_call is not None and need != have and not ties[-1] and SUBSET_REBUILD
+            and need <= set(quant) and len(need) < obs_of.n_labels):
+        res, (nb, ties) = _run_deferred(
+            eng, round_call, lambda: reference_orders(losses, n_below, obs_of, need),
+            lambda o: eng.rebuild_labels(losses, n_valid, gamma, prior_weight, lf, o[1], o[2], need),
+            quant, t0)
+        if res is not None:
+            return nb, frozenset(need), res
+        # a dependent label the rebuild reported: the full ordered build
+        # (with it) and the whole round below
+        need |= set(np.flatnonzero(ties[:-1] & 2).tolist())
+        have = set()
+        ties = np.ones_like(ties)
+        t0 = time.perf_counter()
     if need != have or ties[-1]:
         below, off, order = reference_orders(losses, n_below, obs_of, need)
         t0 = _phase('argsorts', t0)
@@ -421,6 +494,10 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
             nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf, below, off,
                                                    order)
             assert not np.any(ties[:-1])
+    if round_call is not None:
+        res = round_call()
+        _phase('round', t0)
+        return nb, frozenset(need), res
     return nb, frozenset(need)
 
 
@@ -462,7 +539,10 @@ class DeviceHistoryUploader(object):
         self.owner = None
 
     def build(self, eng, labels, view, gamma, prior_weight, lf=DEFAULT_LF, prepare=None, streams=None,
-              overlap=True):
+              overlap=True, round_call=None):
+        """Upload what is new and build the posterior; returns n_below, or
+        (n_below, results) with round_call (the coming round: see
+        build_reference_order)."""
         tids, losses, n_valid, cols, owner = view
         key = (tuple((n, k) for n, k, _ in labels) + (tuple(streams) if streams is not None else (),),
                eng.history_generation)
@@ -482,6 +562,8 @@ class DeviceHistoryUploader(object):
             self.pos_parts = [[] for _ in labels]    # what the device holds, per label
             self.val_parts = [[] for _ in labels]
             self.tie_labels = frozenset()
+            self.quant = frozenset(i for i in range(len(labels))
+                                   if specs[i]['flags'] & L.TPE_HAS_Q and specs[i]['kind'] != L.TPE_CATEGORICAL)
         t0 = time.perf_counter()
         counts = list(self.prev_counts)
         # the new observations of every label, transformed and placed in one
@@ -527,10 +609,12 @@ class DeviceHistoryUploader(object):
         self.n_trials = len(tids)
         self.last_tid = tids[-1] if len(tids) else None
         _phase('append', t0)
-        nb, self.tie_labels = build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf,
-                                                    self._obs_of(len(labels)), self.tie_labels,
-                                                    prepare=prepare, overlap=overlap)
-        return nb
+        out = build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf,
+                                    self._obs_of(len(labels)), self.tie_labels,
+                                    prepare=prepare, overlap=overlap, round_call=round_call,
+                                    quant=self.quant)
+        self.tie_labels = out[1]
+        return (out[0], out[2]) if round_call is not None else out[0]
 
     def _obs_of(self, n_labels):
         def obs_of(l):
@@ -546,6 +630,7 @@ class DeviceHistoryUploader(object):
     prev_counts = ()
     pos_parts = val_parts = ()
     tie_labels = frozenset()
+    quant = frozenset()
     n_trials = 0
     last_tid = None
     trs = ()

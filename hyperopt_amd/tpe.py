@@ -141,10 +141,12 @@ PREPARE_MIN = 8192   # candidate slots of a round from which it uses the expansi
 
 
 def _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior_weight,
-                        builder, n_candidates=0, n_rounds=1):
+                        builder, n_candidates=0, n_rounds=1, round_call=None):
     """Put the posterior of the current history on the engine, from the
     device-resident history's `view` or the general gather (tids, losses,
-    obs); returns the number of trial documents it was built from."""
+    obs); returns (the number of trial documents it was built from, the
+    results of round_call when the incremental device build ran it -- the
+    dense labels' round under the host's tie-order argsorts -- else None)."""
     labels = list(specs)
     if view is not None:
         n_docs = view[2]
@@ -161,13 +163,14 @@ def _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior
                 up = getattr(eng, '_history_uploader', None)
                 if up is None:
                     up = eng._history_uploader = _post.DeviceHistoryUploader()
-                up.build(eng, [(s.label, s.kind, s.args) for s in specs.values()], view, gamma,
-                         prior_weight, prepare=((n_candidates, n_rounds)
-                                                if n_candidates * n_rounds >= PREPARE_MIN else None))
-            else:
-                eng.build_posterior(*device_inputs(specs, tids, losses, obs), gamma=gamma,
-                                    prior_weight=prior_weight)
-            return n_docs
+                _, res = up.build(eng, [(s.label, s.kind, s.args) for s in specs.values()], view, gamma,
+                                  prior_weight, prepare=((n_candidates, n_rounds)
+                                                         if n_candidates * n_rounds >= PREPARE_MIN else None),
+                                  round_call=round_call)
+                return n_docs, res
+            eng.build_posterior(*device_inputs(specs, tids, losses, obs), gamma=gamma,
+                                prior_weight=prior_weight)
+            return n_docs, None
         except _post.NonFiniteObservation:
             # NaN observations: the host build raises what the reference's
             # adaptive_parzen_normal raises (tpe.py:469)
@@ -181,7 +184,7 @@ def _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior
         b, a = splitter.split(*obs[label])
         posts.append(_post.label_posterior(label, sp.kind, sp.args, b, a, prior_weight))
     eng.set_posterior(*_post.pack(posts))
-    return n_docs
+    return n_docs, None
 
 
 def suggest(new_ids, domain, trials, seed,
@@ -266,12 +269,16 @@ def suggest(new_ids, domain, trials, seed,
     eng = _engine.get_engine(list(devices) if devices else device, 'f64',
                              'pending' if isinstance(trials, _PendingView) else 'main')
     ids = list(new_ids) if batch else [new_ids[0]]
-    _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior_weight,
-                        posterior_builder, n_candidates=n_EI_candidates, n_rounds=len(ids))
-    if len(ids) == 1:
-        res = eng.suggest(seed, n_EI_candidates, round=ids[0])[None]
-    else:
-        res = eng.suggest_batch(seed, ids, n_EI_candidates)
+
+    def round_call():
+        if len(ids) == 1:
+            return eng.suggest(seed, n_EI_candidates, round=ids[0])[None]
+        return eng.suggest_batch(seed, ids, n_EI_candidates)
+    _, res = _resident_posterior(eng, domain, trials, specs, view, gathered, gamma, prior_weight,
+                                 posterior_builder, n_candidates=n_EI_candidates, n_rounds=len(ids),
+                                 round_call=round_call)
+    if res is None:
+        res = round_call()
     rval = []
     for j, new_id in enumerate(ids):
         values = {s.label: _labels.coerce(s.kind, res[j][i]['value'])

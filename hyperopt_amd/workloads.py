@@ -135,18 +135,20 @@ class FminLoop(object):
         losses = self.hist.losses[:n]
         return (self.hist.tids[:n], losses, int(np.count_nonzero(losses == losses)), obs, self)
 
-    def advance(self, eng, n, n_candidates=0, n_rounds=1):
+    def advance(self, eng, n, n_candidates=0, n_rounds=1, round_call=None):
         """History of the first n trials on the device, posterior rebuilt
         (its expansion index queued meanwhile when the coming round(s) of
         n_candidates per label will use it, as tpe.suggest does); returns
-        n_below."""
+        n_below, or (n_below, results) with round_call (the step's round,
+        run as tpe.suggest runs it: see posterior.build_reference_order)."""
         if n > len(self.hist.tids):
             raise ValueError('the synthetic history holds %d trials' % len(self.hist.tids))
         self.n = n
         return self.uploader.build(eng, self.labels, self.view(n), self.gamma, self.prior_weight,
                                    prepare=((n_candidates, n_rounds)
                                             if n_candidates * n_rounds >= PREPARE_MIN else None),
-                                   streams=self.streams, overlap=self.n_dense >= OVERLAP_MIN_DENSE)
+                                   streams=self.streams, overlap=self.n_dense >= OVERLAP_MIN_DENSE,
+                                   round_call=round_call)
 
 
 def mixed_space(n_labels):

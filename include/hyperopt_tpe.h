@@ -478,6 +478,14 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *   TPE_OPT_RESCORE_CAP  candidates the packed map's re-score buffers hold
  *                   (grown when a round lists more: that round runs again;
  *                   tests set it small to take that path)               [65536]
+ *   TPE_OPT_MODE_MASK  bit m set: rounds launch the labels of family m
+ *                   (tpe_last_mode_stats' index: 1 | 2 dense, 4 | 8
+ *                   quantized, 16 categorical); the other labels' result
+ *                   entries are unspecified and their families' statistics
+ *                   stay those of the round that last ran them.  Lets a
+ *                   caller run the dense labels while the host still
+ *                   computes the quantized labels' tie orders, then those
+ *                   after their rebuild (posterior.py)                 [31]
  *   TPE_OPT_WIN_GROUPS  label groups of a windowed round, each sorted on a
  *                   second stream while the previous one is screened
  *                   (0: one group; the chip is busy either way)          [0]
@@ -508,6 +516,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_ZERO_WIN 15
 #define TPE_OPT_VALUE_ONLY 16
 #define TPE_OPT_RESCORE_CAP 17
+#define TPE_OPT_MODE_MASK 18
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
 
 /* Build now what the resident posterior's first round(s) of n_candidates

@@ -40,3 +40,46 @@ def test_fmin_loop_rounds_equal_fresh_engine():
         # quantized labels needed numpy's order; the loop supplied it
         assert {2, 7, 12, 17, 22, 27} <= set(loop.uploader.tie_labels)
     eng.close()
+
+
+@pytest.mark.parametrize('C, n_rounds, labels', [(1 << 20, 1, 32), (24, 512, 64)])
+def test_deferred_quantized_round_equals_sequential(C, n_rounds, labels):
+    """round_call (tpe.suggest's and bench.py's step): the dense and
+    categorical labels' round runs on a second thread while the host
+    computes the quantized labels' numpy tie orders, then those labels are
+    rebuilt and their round runs (TPE_OPT_MODE_MASK) -- bytewise the results
+    of the sequential step (ordered rebuild, then the whole round), tile
+    rounds (config 3) and batched packed rounds (config 5) alike."""
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.engine import Engine
+    from hyperopt_amd.workloads import FminLoop, mixed_history
+    hist = mixed_history(labels, 10000 + 4, seed=3)
+    a, b = Engine(0, 'f64'), Engine(0, 'f64')
+    la, lb = FminLoop(hist), FminLoop(hist)
+    la.advance(a, 10000)
+    lb.advance(b, 10000)
+    P.PHASES = {}
+    try:
+        for i in range(3):
+            n = 10001 + i
+            rounds = list(range(100 * i, 100 * i + n_rounds))
+
+            def rnd(e=a):
+                if n_rounds == 1:
+                    return e.suggest(seed=5 + i, n_candidates=C, round=rounds[0])
+                return e.suggest_batch(seed=5 + i, rounds=rounds, n_candidates=C)
+            _, got = la.advance(a, n, n_candidates=C, n_rounds=n_rounds, round_call=rnd)
+            lb.advance(b, n, n_candidates=C, n_rounds=n_rounds)
+            want = rnd(b)
+            assert np.ascontiguousarray(got).view(np.uint8).tobytes() == \
+                np.ascontiguousarray(want).view(np.uint8).tobytes(), i
+            # the statistics of both halves survive: the dense screen's and
+            # the quantized families' of the last round that ran them
+            assert a.last_screen() == b.last_screen()
+            ms_a, ms_b = a.last_mode_stats(), b.last_mode_stats()
+            assert {k: v[1] for k, v in ms_a.items()} == {k: v[1] for k, v in ms_b.items()}
+        assert P.PHASES.get('quant_round', [0])[0] == 3      # the deferred path ran every step
+    finally:
+        P.PHASES = None
+        a.close()
+        b.close()
