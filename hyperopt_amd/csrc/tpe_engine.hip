@@ -4131,13 +4131,24 @@ __global__ __launch_bounds__(kBlock) void k_merge_results(const tpe_label_result
                                                           tpe_label_result* __restrict__ out) {
     const int32_t j = blockIdx.x * kBlock + threadIdx.x;
     if (j >= n) return;
-    tpe_label_result best = parts[j];
+    // the winning part's index is tracked and its record copied once (a
+    // per-field select of whole records, round 4's first form, came out
+    // mixing the value of one part with the rest of another)
+    int32_t bp = 0;
+    int64_t bi = parts[j].index;
+    uint64_t bk = order_key(parts[j].score);
     for (int32_t p = 1; p < n_parts; ++p) {
-        const tpe_label_result c = parts[(size_t)p * n + j];
-        if (c.index < 0) continue;
-        if (best.index < 0 || better(order_key(c.score), c.index, order_key(best.score), best.index)) best = c;
+        const tpe_label_result* c = parts + (size_t)p * n + j;
+        const int64_t ci = c->index;
+        if (ci < 0) continue;
+        const uint64_t ck = order_key(c->score);
+        if (bi < 0 || better(ck, ci, bk, bi)) {
+            bp = p;
+            bi = ci;
+            bk = ck;
+        }
     }
-    out[j] = best;
+    out[j] = parts[(size_t)bp * n + j];
 }
 
 }  // namespace
