@@ -129,6 +129,11 @@ def parse():
     ap.add_argument('--no-agreement', action='store_true',
                     help='skip the oracle leg: argmax agreement with the numpy restatement of the '
                          'reference on the near-ties of one round (oracle/near_ties.py)')
+    ap.add_argument('--defer', type=int, default=None,
+                    help='1/0: the dense labels\' round under the tie-order argsorts '
+                         '(posterior.DEFER_QUANT; default: the library\'s)')
+    ap.add_argument('--sort-threads', type=int, default=None,
+                    help='threads of the tie-order argsort pool (posterior.SORT_THREADS)')
     ap.add_argument('--no-other-configs', action='store_true',
                     help='config 3 at N=1: skip the legs of configs 2, 4 and 5 (child processes)')
     return ap.parse_args()
@@ -340,6 +345,10 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group(args.dist_backend)
     from hyperopt_amd import posterior as P
+    if args.defer is not None:
+        P.DEFER_QUANT = bool(args.defer)
+    if args.sort_threads is not None:
+        P.SORT_THREADS = args.sort_threads
     from hyperopt_amd.engine import Engine
     from hyperopt_amd.workloads import (FminLoop, conditional_history, hartmann_history,
                                          mixed_history)

@@ -329,6 +329,7 @@ def reference_orders(losses, n_below, obs_of, labels):
 
 
 _POOL_MIN = 1 << 14   # observations to sort (over several labels), from which the pool pays
+SORT_THREADS = 16     # the argsort pool's threads at most (bench.py --sort-threads)
 _pool = None
 _pool_lock = threading.Lock()
 
@@ -346,11 +347,12 @@ def _sort_pool():
                     ncpu = len(os.sched_getaffinity(0))
                 except (AttributeError, OSError):
                     ncpu = os.cpu_count() or 2
-                _pool = ThreadPoolExecutor(max_workers=max(1, min(16, ncpu)))
+                _pool = ThreadPoolExecutor(max_workers=max(1, min(SORT_THREADS, ncpu)))
     return _pool
 
 
 SUBSET_REBUILD = True   # the ordered rebuild restricted to the labels that need an order
+DEFER_QUANT = True      # round_call: the dense labels' round under the argsorts (_run_deferred)
 
 
 MASK_ALL = 31                      # TPE_OPT_MODE_MASK: every label family
@@ -461,7 +463,7 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
         raise AssertionError('below mixture depends on a tie order (lf < gamma_cap?)')
     need = have | set(np.flatnonzero(ties[:-1] & 2).tolist())
     res = None
-    if (round_call is not None and need != have and not ties[-1] and SUBSET_REBUILD
+    if (DEFER_QUANT and round_call is not None and need != have and not ties[-1] and SUBSET_REBUILD
             and need <= set(quant) and len(need) < obs_of.n_labels):
         res, (nb, ties) = _run_deferred(
             eng, round_call, lambda: reference_orders(losses, n_below, obs_of, need),
