@@ -352,7 +352,7 @@ def _sort_pool():
 
 
 SUBSET_REBUILD = True   # the ordered rebuild restricted to the labels that need an order
-DEFER_QUANT = True      # round_call: the dense labels' round under the argsorts (_run_deferred)
+DEFER_QUANT = False     # round_call: the dense labels' round under the argsorts (_run_deferred; measured slower)
 
 
 MASK_ALL = 31                      # TPE_OPT_MODE_MASK: every label family

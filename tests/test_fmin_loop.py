@@ -59,6 +59,7 @@ def test_deferred_quantized_round_equals_sequential(C, n_rounds, labels):
     la.advance(a, 10000)
     lb.advance(b, 10000)
     P.PHASES = {}
+    defer, P.DEFER_QUANT = P.DEFER_QUANT, True     # (off by default: measured slower)
     try:
         for i in range(3):
             n = 10001 + i
@@ -81,5 +82,6 @@ def test_deferred_quantized_round_equals_sequential(C, n_rounds, labels):
         assert P.PHASES.get('quant_round', [0])[0] == 3      # the deferred path ran every step
     finally:
         P.PHASES = None
+        P.DEFER_QUANT = defer
         a.close()
         b.close()
