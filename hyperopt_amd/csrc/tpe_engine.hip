@@ -817,13 +817,45 @@ __global__ __launch_bounds__(kBlock) void k_hot_bits(const int32_t* __restrict__
 // per workgroup -- the launch requires them in LDS).  The listed candidates
 // gather in an LDS buffer (one LDS atomic per wave and slot pair, no
 // barrier) and go to the cell's list with one global atomic per workgroup
-// at the end; past the buffer a wave appends straight to the list.
-constexpr int kHotBuf = 256;
+// flush: after a tile that leaves kHotFlush or more entries, and at the end;
+// past the buffer (a tile listing more than its free room) a wave appends
+// straight to the list.  (Round 4 measured the flush-at-the-end-only form:
+// with ~2k listed per workgroup nearly every listing wave went straight to
+// the list, an atomic per wave on ONE counter per cell.)
+constexpr int kHotBuf = 512;
+constexpr int kHotFlush = 256;
 constexpr int kHotRetry = 512;   // rejected draws retried cooperatively per tile (the rest in-thread)
 // LDS_BITS: every label's bits fit in LDS (the host knows the largest
 // label's sub-bins) -- the bit test is then a ds_read; otherwise every
 // label reads them from global memory.  (One kernel choosing per label
 // compiled to a generic-address load with per-lane address selects.)
+// k_hot_bx's buffer to the cell's list: one global atomic for the
+// workgroup, the entries copied, the buffer emptied.  Called by every thread
+// after a barrier that follows the last append (buf_n, buf_end settled); it
+// returns after a barrier, before which every thread has read them.
+__device__ __forceinline__ void hot_flush(int& buf_n, int& buf_end, int& gbase, const int32_t* buf_i,
+                                          const double* buf_x, int32_t* __restrict__ hcnt,
+                                          int32_t* __restrict__ hidx, double* __restrict__ hx, size_t cell,
+                                          int64_t hstride, int32_t* __restrict__ hflag) {
+    const int m = min(buf_n, buf_end);   // (round 3 flushed min(buf_n, kHotBuf): unwritten entries too)
+    if (threadIdx.x == 0) gbase = m ? atomicAdd(hcnt + cell, m) : 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // a cell's list is hstride long: past it the round falls back to
+        // screening every candidate (hflag bit 2), so nothing is lost
+        if (gbase + m > hstride) atomicOr(hflag, 2);
+        buf_n = 0;
+        buf_end = kHotBuf;
+    }
+    const int gb = gbase;
+    for (int k = threadIdx.x; k < m; k += kBlock)
+        if (gb + k < hstride) {
+            hidx[cell * (size_t)hstride + gb + k] = buf_i[k];
+            hx[cell * (size_t)hstride + gb + k] = buf_x[k];
+        }
+    __syncthreads();
+}
+
 template <int R, bool LDS_BITS>
 __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
@@ -850,7 +882,7 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
     __shared__ RetryLds<R, kHotRetry> retry;
     __shared__ int32_t buf_i[kHotBuf];
     __shared__ double buf_x[kHotBuf];
-    __shared__ int buf_n, buf_end, gbase;
+    __shared__ int buf_n, buf_end, gbase, flush_at[2];
     if (threadIdx.x == 0) {
         buf_n = 0;
         buf_end = kHotBuf;   // the LDS entries actually written (a wave straddling the end lowers it)
@@ -916,19 +948,17 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
             }
             if (!lds && lane == 0 && at + (int)__popcll(bal) > hstride) atomicOr(hflag, 2);
         }
+        // flush decided by thread 0 BEFORE the barrier (any value will do, so
+        // long as every thread takes the same one: a wave reading the counter
+        // after it could see the next tile's appends), in a flag per tile
+        // parity (the next write to this one is two barriers away); the trip
+        // count is the workgroup's, so every wave reaches these barriers
+        if (threadIdx.x == 0) flush_at[par] = min(buf_n, buf_end) >= kHotFlush;
+        __syncthreads();
+        if (flush_at[par]) hot_flush(buf_n, buf_end, gbase, buf_i, buf_x, hcnt, hidx, hx, cell, hstride, hflag);
     }
     __syncthreads();
-    const int m = min(buf_n, buf_end);   // (round 3 flushed min(buf_n, kHotBuf): unwritten entries too)
-    if (threadIdx.x == 0) gbase = m ? atomicAdd(hcnt + cell, m) : 0;
-    __syncthreads();
-    // a cell's list is hstride long: past it the round falls back to
-    // screening every candidate (hflag bit 2), so nothing is lost
-    if (threadIdx.x == 0 && gbase + m > hstride) atomicOr(hflag, 2);
-    for (int k = threadIdx.x; k < m; k += kBlock)
-        if (gbase + k < hstride) {
-            hidx[cell * (size_t)hstride + gbase + k] = buf_i[k];
-            hx[cell * (size_t)hstride + gbase + k] = buf_x[k];
-        }
+    hot_flush(buf_n, buf_end, gbase, buf_i, buf_x, hcnt, hidx, hx, cell, hstride, hflag);
 }
 
 // The expansion screen over the listed candidates only: workgroups stride
