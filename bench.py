@@ -129,6 +129,9 @@ def parse():
     ap.add_argument('--no-agreement', action='store_true',
                     help='skip the oracle leg: argmax agreement with the numpy restatement of the '
                          'reference on the near-ties of one round (oracle/near_ties.py)')
+    ap.add_argument('--value-only', type=int, default=None,
+                    help='1/0: TPE_OPT_VALUE_ONLY (default: on, as tpe.suggest, except for '
+                         'candidate shards)')
     ap.add_argument('--defer', type=int, default=None,
                     help='1/0: the dense labels\' round under the tie-order argsorts '
                          '(posterior.DEFER_QUANT; default: the library\'s)')
@@ -503,6 +506,13 @@ def main():
 
     screen = args.precision == 'f64' and not args.no_screen
     eng.set_option('screen', int(screen))
+    # value-only rounds as tpe.suggest runs them (engine.get_engine: the
+    # winners' values are all a document needs, tpe.py:906-916) -- except
+    # for candidate shards, whose winners merge by score (the packed map's
+    # certified cells otherwise carry no fp64 lpdfs; tile rounds unchanged)
+    value_only = (args.value_only if args.value_only is not None
+                  else int(not (dist is not None and not by_label and args.config != 5)))
+    eng.set_option('value_only', value_only)
     eng.set_option('window', int(not args.no_window))
     eng.set_option('win_t', args.win_t)
     eng.set_option('win_groups', args.win_groups)
@@ -539,7 +549,11 @@ def main():
         torch.cuda.synchronize()
         udt = time.perf_counter() - t0
         eng.set_option('screen', 1)
-        same = all(results[k].view(np.uint8).tobytes() == ures[k].view(np.uint8).tobytes() for k in ures)
+        if value_only:   # index and value: the fields a value-only round reports for every cell
+            same = all(np.array_equal(results[k]['index'], ures[k]['index']) and
+                       results[k]['value'].tobytes() == ures[k]['value'].tobytes() for k in ures)
+        else:
+            same = all(results[k].view(np.uint8).tobytes() == ures[k].view(np.uint8).tobytes() for k in ures)
         unscreened = (same, udt, nu, first)
     # oracle leg (untimed): the first warm round against numpy's argmax, on
     # the posterior that produced it (before the projection advances it)
@@ -568,7 +582,7 @@ def main():
             for sh in label_shards(hist_full.labels, 8):
                 e8 = Engine(local, args.precision)
                 for k, v in (('screen', int(screen)), ('window', int(not args.no_window)),
-                             ('win_t', args.win_t), ('win_groups', args.win_groups)):
+                             ('win_t', args.win_t), ('win_groups', args.win_groups), ('value_only', value_only)):
                     e8.set_option(k, v)
                 l8 = FminLoop(hist_full, label_ids=sh)
                 l8.advance(e8, args.trials + (p0 - 1) * args.append)
@@ -720,6 +734,7 @@ def main():
         'higher_is_better': True, 'scaling': 'strong', 'vs_baseline': None,
         'dtype': ('f32+f64' if screened else args.precision),
         'data': 'synthetic (prior draws, seed 0)',
+        'value_only': bool(value_only),
         'config': {'workload': workload_name(args, C),
                    'labels': L, 'history': args.trials,
                    'candidates_per_label': C_total, 'candidates_per_label_per_gpu': C,
@@ -803,9 +818,11 @@ def main():
             line['screened_equals_fp64'] = bool(same)
             line['screen']['unscreened_fp64'] = {
                 'steps': nu, 'ms_per_step': round(udt / nu * 1e3, 3),
-                'compared': 'index, value, score, lpdf_below, lpdf_above, status of every label, '
-                            'bytewise, on rounds %d..%d of the last posterior (the screened runs '
-                            'are the warm steps)' % (first, first + nu - 1),
+                'compared': ('index and value (value-only rounds: a certified cell carries no '
+                             'lpdfs)' if value_only else
+                             'index, value, score, lpdf_below, lpdf_above, status') +
+                            ' of every label, bytewise, on rounds %d..%d of the last posterior (the '
+                            'screened runs are the warm steps)' % (first, first + nu - 1),
                 'bit_identical': bool(same)}
     if prec == 'f32' and args.agreement_steps > 0 and args.config != 5:
         # fp32 winners vs the exact fp64 round's on the same candidate sets
