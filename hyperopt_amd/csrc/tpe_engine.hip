@@ -815,47 +815,42 @@ __global__ __launch_bounds__(kBlock) void k_hot_bits(const int32_t* __restrict__
 // Tile map only: workgroups stride over the cell's tiles of R * 256
 // candidates (Box-Muller pairs per thread, the sampling records staged once
 // per workgroup -- the launch requires them in LDS).  The listed candidates
-// gather in an LDS buffer (one LDS atomic per wave and slot pair, no
-// barrier) and go to the cell's list with one global atomic per workgroup
-// flush: after a tile that leaves kHotFlush or more entries, and at the end;
-// past the buffer (a tile listing more than its free room) a wave appends
-// straight to the list.  (Round 4 measured the flush-at-the-end-only form:
-// with ~2k listed per workgroup nearly every listing wave went straight to
-// the list, an atomic per wave on ONE counter per cell.)
-constexpr int kHotBuf = 512;
-constexpr int kHotFlush = 256;
+// gather in a buffer per WAVE in LDS (its count wave-uniform, in a scalar
+// register: no LDS atomics, no barriers) and go to the cell's list with one
+// global atomic per wave flush -- when a slot's listings would not fit, and
+// at the end.  (Round 4 measured two other forms on the same box: one
+// workgroup buffer flushed only at the end, past which nearly every listing
+// wave appended with its own atomic on the cell's ONE counter, 2.34 ms at
+// 0.35 VALU busy; flushed after every tile that left 256 entries, behind a
+// barrier per tile, 1.37 ms at 0.75.)
+constexpr int kHotBuf = 128;     // entries per wave
 constexpr int kHotRetry = 512;   // rejected draws retried cooperatively per tile (the rest in-thread)
+
+// one wave's buffer to the cell's list (count n, wave-uniform)
+__device__ __forceinline__ void hot_wave_flush(int n, const int32_t* bi, const double* bxv,
+                                               int32_t* __restrict__ hcnt, int32_t* __restrict__ hidx,
+                                               double* __restrict__ hx, size_t cell, int64_t hstride,
+                                               int32_t* __restrict__ hflag) {
+    const int lane = threadIdx.x & 63;
+    int gb = 0;
+    if (lane == 0) gb = atomicAdd(hcnt + cell, n);
+    gb = __builtin_amdgcn_readfirstlane(__shfl(gb, 0));
+    // a cell's list is hstride long: past it the round falls back to
+    // screening every candidate (hflag bit 2), so nothing is lost
+    if (lane == 0 && gb + n > hstride) atomicOr(hflag, 2);
+    __builtin_amdgcn_wave_barrier();   // (the wave's own LDS writes above: in order per wave)
+    for (int k = lane; k < n; k += 64)
+        if (gb + k < hstride) {
+            hidx[cell * (size_t)hstride + gb + k] = bi[k];
+            hx[cell * (size_t)hstride + gb + k] = bxv[k];
+        }
+    __builtin_amdgcn_wave_barrier();   // (read before the buffer is refilled)
+}
+
 // LDS_BITS: every label's bits fit in LDS (the host knows the largest
 // label's sub-bins) -- the bit test is then a ds_read; otherwise every
 // label reads them from global memory.  (One kernel choosing per label
 // compiled to a generic-address load with per-lane address selects.)
-// k_hot_bx's buffer to the cell's list: one global atomic for the
-// workgroup, the entries copied, the buffer emptied.  Called by every thread
-// after a barrier that follows the last append (buf_n, buf_end settled); it
-// returns after a barrier, before which every thread has read them.
-__device__ __forceinline__ void hot_flush(int& buf_n, int& buf_end, int& gbase, const int32_t* buf_i,
-                                          const double* buf_x, int32_t* __restrict__ hcnt,
-                                          int32_t* __restrict__ hidx, double* __restrict__ hx, size_t cell,
-                                          int64_t hstride, int32_t* __restrict__ hflag) {
-    const int m = min(buf_n, buf_end);   // (round 3 flushed min(buf_n, kHotBuf): unwritten entries too)
-    if (threadIdx.x == 0) gbase = m ? atomicAdd(hcnt + cell, m) : 0;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        // a cell's list is hstride long: past it the round falls back to
-        // screening every candidate (hflag bit 2), so nothing is lost
-        if (gbase + m > hstride) atomicOr(hflag, 2);
-        buf_n = 0;
-        buf_end = kHotBuf;
-    }
-    const int gb = gbase;
-    for (int k = threadIdx.x; k < m; k += kBlock)
-        if (gb + k < hstride) {
-            hidx[cell * (size_t)hstride + gb + k] = buf_i[k];
-            hx[cell * (size_t)hstride + gb + k] = buf_x[k];
-        }
-    __syncthreads();
-}
-
 template <int R, bool LDS_BITS>
 __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
@@ -880,15 +875,11 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
         for (int w = threadIdx.x; w < (nsb >> 5); w += kBlock) sbits[w] = hbits[(B.sb_off >> 5) + w];
     const uint32_t* __restrict__ gbits = hbits + (B.sb_off >> 5);
     __shared__ RetryLds<R, kHotRetry> retry;
-    __shared__ int32_t buf_i[kHotBuf];
-    __shared__ double buf_x[kHotBuf];
-    __shared__ int buf_n, buf_end, gbase, flush_at[2];
-    if (threadIdx.x == 0) {
-        buf_n = 0;
-        buf_end = kHotBuf;   // the LDS entries actually written (a wave straddling the end lowers it)
-    }
-    __syncthreads();   // the Box-Muller tables, the bits and the counters above
-    const int lane = threadIdx.x & 63;
+    __shared__ int32_t buf_i[kBlock / 64][kHotBuf];
+    __shared__ double buf_x[kBlock / 64][kHotBuf];
+    __syncthreads();   // the Box-Muller tables and the bits above
+    const int wv = threadIdx.x >> 6;
+    int wn = 0;   // this wave's buffered entries (wave-uniform)
     const int steps = __builtin_amdgcn_readfirstlane(sl.steps);   // (read once, not per pick)
     int par = 0;
     for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per, par ^= 1) {
@@ -924,41 +915,20 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
             }
             const uint64_t bal = __ballot(take);
             if (!bal) continue;
-            int at = 0;
-            if (lane == 0) at = atomicAdd(&buf_n, (int)__popcll(bal));
-            at = __builtin_amdgcn_readfirstlane(__shfl(at, 0));
-            const bool lds = at + (int)__popcll(bal) <= kHotBuf;   // wave-uniform
-            if (!lds) {   // the buffer is full: straight to the cell's list
-                // (the one wave whose reservation straddles the end leaves
-                // [at, kHotBuf) unwritten: the flush stops there)
-                if (lane == 0 && at < kHotBuf) buf_end = at;
-                if (lane == 0) at = atomicAdd(hcnt + cell, (int)__popcll(bal));
-                at = __builtin_amdgcn_readfirstlane(__shfl(at, 0));
+            const int c = __builtin_amdgcn_readfirstlane((int)__popcll(bal));
+            if (wn + c > kHotBuf) {   // (wave-uniform)
+                hot_wave_flush(wn, buf_i[wv], buf_x[wv], hcnt, hidx, hx, cell, hstride, hflag);
+                wn = 0;
             }
             if (take) {
-                const int k = at + (int)lanes_below(bal);
-                const int32_t ci = (int32_t)(base + (int64_t)tile_cand(r, threadIdx.x, kBlock));
-                if (lds) {
-                    buf_i[k] = ci;
-                    buf_x[k] = x[r];
-                } else if (k < hstride) {
-                    hidx[cell * (size_t)hstride + k] = ci;
-                    hx[cell * (size_t)hstride + k] = x[r];
-                }
+                const int k = wn + (int)lanes_below(bal);
+                buf_i[wv][k] = (int32_t)(base + (int64_t)tile_cand(r, threadIdx.x, kBlock));
+                buf_x[wv][k] = x[r];
             }
-            if (!lds && lane == 0 && at + (int)__popcll(bal) > hstride) atomicOr(hflag, 2);
+            wn += c;
         }
-        // flush decided by thread 0 BEFORE the barrier (any value will do, so
-        // long as every thread takes the same one: a wave reading the counter
-        // after it could see the next tile's appends), in a flag per tile
-        // parity (the next write to this one is two barriers away); the trip
-        // count is the workgroup's, so every wave reaches these barriers
-        if (threadIdx.x == 0) flush_at[par] = min(buf_n, buf_end) >= kHotFlush;
-        __syncthreads();
-        if (flush_at[par]) hot_flush(buf_n, buf_end, gbase, buf_i, buf_x, hcnt, hidx, hx, cell, hstride, hflag);
     }
-    __syncthreads();
-    hot_flush(buf_n, buf_end, gbase, buf_i, buf_x, hcnt, hidx, hx, cell, hstride, hflag);
+    if (wn) hot_wave_flush(wn, buf_i[wv], buf_x[wv], hcnt, hidx, hx, cell, hstride, hflag);
 }
 
 // The expansion screen over the listed candidates only: workgroups stride
