@@ -135,6 +135,9 @@ def parse():
     ap.add_argument('--defer', type=int, default=None,
                     help='1/0: the dense labels\' round under the tie-order argsorts '
                          '(posterior.DEFER_QUANT; default: the library\'s)')
+    ap.add_argument('--early-orders', type=int, default=None,
+                    help='1/0: the known labels\' argsorts under the first build '
+                         '(posterior.EARLY_ORDERS)')
     ap.add_argument('--sort-threads', type=int, default=None,
                     help='threads of the tie-order argsort pool (posterior.SORT_THREADS)')
     ap.add_argument('--no-other-configs', action='store_true',
@@ -352,6 +355,8 @@ def main():
         P.DEFER_QUANT = bool(args.defer)
     if args.sort_threads is not None:
         P.SORT_THREADS = args.sort_threads
+    if args.early_orders is not None:
+        P.EARLY_ORDERS = bool(args.early_orders)
     from hyperopt_amd.engine import Engine
     from hyperopt_amd.workloads import (FminLoop, conditional_history, hartmann_history,
                                          mixed_history)
