@@ -898,20 +898,33 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
         if (!sample_tile<DENSE_GMM, R, SampShared, true, kHotRetry>(L, SampShared{&sl, bm_cs, bm_lg, steps}, seed,
                                                                      rk, g0, pend, x, retry, par))
             atomicOr(err, 1);
+        // the bit words of H slots first (global: H loads in flight at once,
+        // one wait -- round 4's first form waited on each before its ballot;
+        // all R at once spilled registers)
+        constexpr int H = R >= 4 ? 4 : R;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
+        for (int h = 0; h < R; h += H) {
+        uint32_t wd[H];
+#pragma unroll
+        for (int q = 0; q < H; ++q) {
+            const int r = h + q;
+            const double f = (x[r] - L.centre - B.xlo) * B.inv_sbw;
+            wd[q] = 0u;
+            if (((pend >> r) & 1u) && f >= 0.0 && f < (double)nsb) {
+                const int j = (int)f;   // (sb_off: a multiple of 32)
+                if constexpr (LDS_BITS) wd[q] = sbits[j >> 5];
+                else wd[q] = gbits[j >> 5];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < H; ++q) {
+            const int r = h + q;
             bool take = false;
             if ((pend >> r) & 1u) {
+                // (the same arithmetic as above: the same sub-bin)
                 const double f = (x[r] - L.centre - B.xlo) * B.inv_sbw;
-                if (f >= 0.0 && f < (double)nsb) {
-                    const int j = (int)f;   // (sb_off: a multiple of 32)
-                    uint32_t word;
-                    if constexpr (LDS_BITS) word = sbits[j >> 5];
-                    else word = gbits[j >> 5];
-                    take = (word >> (j & 31)) & 1u;
-                } else {
-                    take = true;   // outside the bins (or NaN): always listed
-                }
+                if (f >= 0.0 && f < (double)nsb) take = (wd[q] >> ((int)f & 31)) & 1u;
+                else take = true;   // outside the bins (or NaN): always listed
             }
             const uint64_t bal = __ballot(take);
             if (!bal) continue;
@@ -926,6 +939,7 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
                 buf_x[wv][k] = x[r];
             }
             wn += c;
+        }
         }
     }
     if (wn) hot_wave_flush(wn, buf_i[wv], buf_x[wv], hcnt, hidx, hx, cell, hstride, hflag);
