@@ -396,7 +396,6 @@ struct tpe_ctx {
     DevBuf<int32_t> hot_i, hot_cnt;      //   their indices; per cell the count
     DevBuf<unsigned long long> hot_t, hot_tau0;   // per cell largest L; per label tau0
     DevBuf<uint32_t> hot_bits;           // per sub-bin: U >= tau0 (words at sb_off / 32)
-    DevBuf<uint32_t> hot_coarse;         // per dense label position: bit w = (hot_bits word w != 0)
     DevBuf<int32_t> hot_flag;            // fallback flag
     tpe_rt::PinVec<int32_t> hot_cnt_h;
     int64_t hot_listed = 0;              // last round: candidates the prefilter listed

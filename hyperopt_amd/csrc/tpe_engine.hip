@@ -784,35 +784,25 @@ __global__ __launch_bounds__(kBlock) void k_hot_tau0(const int32_t* __restrict__
 }
 
 constexpr int kHotLdsWords = 1024;   // k_hot_bx stages up to 32k sub-bin bits in LDS
-constexpr int kHotCoarseLds = 512;   // else up to 512 coarse words (2^19 sub-bins; beyond: every word loaded)
-inline int64_t hot_coarse_stride(int64_t sb_max) { return (((sb_max + 31) / 32 + 31) / 32 + 1) & ~int64_t(1); }
 
 // per label position: bit j of the label's words = (order key of U_j >=
-// tau0), and the coarse map over them: bit w of the position's coarse words
-// (stride cws) = (word w is not 0); grid (ceil(max words / 256), dense
-// labels), one word per thread
+// tau0); grid (ceil(max words / 256), dense labels), one word per thread
 __global__ __launch_bounds__(kBlock) void k_hot_bits(const int32_t* __restrict__ group,
                                                      const BxLabel* __restrict__ bx,
                                                      const float2* __restrict__ sb,
                                                      const unsigned long long* __restrict__ tau0,
-                                                     uint32_t* __restrict__ hbits,
-                                                     uint32_t* __restrict__ hcoarse, int64_t cws) {
+                                                     uint32_t* __restrict__ hbits) {
     const BxLabel B = bx[group[blockIdx.y]];
     const int64_t nsb = (int64_t)B.nbins * kBxSub;
     const int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (w * 32 >= nsb) return;
+    const uint64_t t0 = tau0[blockIdx.y];
     uint32_t word = 0;
-    if (w * 32 < nsb) {
-        const uint64_t t0 = tau0[blockIdx.y];
-        for (int b = 0; b < 32; ++b) {
-            const int64_t j = w * 32 + b;
-            if (j < nsb && order_key((double)sb[B.sb_off + j].x) >= t0) word |= 1u << b;
-        }
-        hbits[(B.sb_off >> 5) + w] = word;
+    for (int b = 0; b < 32; ++b) {
+        const int64_t j = w * 32 + b;
+        if (j < nsb && order_key((double)sb[B.sb_off + j].x) >= t0) word |= 1u << b;
     }
-    // a wave's 64 words are 2 coarse words (w of lane 0: a multiple of 64)
-    const uint64_t nz = __ballot(word != 0u);
-    const int lane = threadIdx.x & 63;
-    if ((lane & 31) == 0 && (w >> 5) < cws) hcoarse[(size_t)blockIdx.y * cws + (w >> 5)] = (uint32_t)(nz >> lane);
+    hbits[(B.sb_off >> 5) + w] = word;
 }
 
 // Draw every candidate of the round (the same draws as k_screen_bx) and
@@ -864,8 +854,7 @@ __device__ __forceinline__ void hot_wave_flush(int n, const int32_t* bi, const d
 template <int R, bool LDS_BITS>
 __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
-    const BxLabel* __restrict__ bx, const uint32_t* __restrict__ hbits, const uint32_t* __restrict__ hcoarse,
-    int64_t cws, int64_t n, int64_t cand_offset,
+    const BxLabel* __restrict__ bx, const uint32_t* __restrict__ hbits, int64_t n, int64_t cand_offset,
     uint64_t seed, const uint32_t* __restrict__ rounds, int32_t nl, int32_t* __restrict__ hcnt,
     int32_t* __restrict__ hidx, double* __restrict__ hx, int32_t* __restrict__ err, int64_t hstride,
     int32_t* __restrict__ hflag) {
@@ -885,12 +874,6 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
     if constexpr (LDS_BITS)
         for (int w = threadIdx.x; w < (nsb >> 5); w += kBlock) sbits[w] = hbits[(B.sb_off >> 5) + w];
     const uint32_t* __restrict__ gbits = hbits + (B.sb_off >> 5);
-    // otherwise the coarse map in LDS: a sub-bin whose word is 0 (the great
-    // majority) is decided there; only the others load their word
-    __shared__ uint32_t scoarse[LDS_BITS ? 1 : kHotCoarseLds];
-    if constexpr (!LDS_BITS)
-        for (int w = threadIdx.x; w < min<int64_t>(cws, kHotCoarseLds); w += kBlock)
-            scoarse[w] = hcoarse[(size_t)blockIdx.y * cws + w];
     __shared__ RetryLds<R, kHotRetry> retry;
     __shared__ int32_t buf_i[kBlock / 64][kHotBuf];
     __shared__ double buf_x[kBlock / 64][kHotBuf];
@@ -915,37 +898,20 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
         if (!sample_tile<DENSE_GMM, R, SampShared, true, kHotRetry>(L, SampShared{&sl, bm_cs, bm_lg, steps}, seed,
                                                                      rk, g0, pend, x, retry, par))
             atomicOr(err, 1);
-        // the bit words of H slots first (global: H loads in flight at once,
-        // one wait -- round 4's first form waited on each before its ballot;
-        // all R at once spilled registers)
-        constexpr int H = R >= 4 ? 4 : R;
 #pragma unroll
-        for (int h = 0; h < R; h += H) {
-        uint32_t wd[H];
-#pragma unroll
-        for (int q = 0; q < H; ++q) {
-            const int r = h + q;
-            const double f = (x[r] - L.centre - B.xlo) * B.inv_sbw;
-            wd[q] = 0u;
-            if (((pend >> r) & 1u) && f >= 0.0 && f < (double)nsb) {
-                const int fw = (int)f >> 5;   // (sb_off: a multiple of 32)
-                if constexpr (LDS_BITS) {
-                    wd[q] = sbits[fw];
-                } else {
-                    const int ci = fw >> 5;
-                    if (ci >= kHotCoarseLds || ((scoarse[ci] >> (fw & 31)) & 1u)) wd[q] = gbits[fw];
-                }
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < H; ++q) {
-            const int r = h + q;
+        for (int r = 0; r < R; ++r) {
             bool take = false;
             if ((pend >> r) & 1u) {
-                // (the same arithmetic as above: the same sub-bin)
                 const double f = (x[r] - L.centre - B.xlo) * B.inv_sbw;
-                if (f >= 0.0 && f < (double)nsb) take = (wd[q] >> ((int)f & 31)) & 1u;
-                else take = true;   // outside the bins (or NaN): always listed
+                if (f >= 0.0 && f < (double)nsb) {
+                    const int j = (int)f;   // (sb_off: a multiple of 32)
+                    uint32_t word;
+                    if constexpr (LDS_BITS) word = sbits[j >> 5];
+                    else word = gbits[j >> 5];
+                    take = (word >> (j & 31)) & 1u;
+                } else {
+                    take = true;   // outside the bins (or NaN): always listed
+                }
             }
             const uint64_t bal = __ballot(take);
             if (!bal) continue;
@@ -960,7 +926,6 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
                 buf_x[wv][k] = x[r];
             }
             wn += c;
-        }
         }
     }
     if (wn) hot_wave_flush(wn, buf_i[wv], buf_x[wv], hcnt, hidx, hx, cell, hstride, hflag);
@@ -3210,11 +3175,8 @@ int hot_tau_prepare(tpe_ctx* ctx, int64_t n) {
     if (ctx->hot == 2)   // test mode: a threshold no candidate reaches -> the fallback
         HIPCHK(ctx, hipMemsetAsync(ctx->hot_tau0.p, 0xff, nl * sizeof(unsigned long long), ctx->stream));
     const int64_t words = (P.bx_sb_max + 31) / 32;
-    const int64_t cws = hot_coarse_stride(P.bx_sb_max);
-    HIPCHK(ctx, ctx->hot_coarse.reserve((size_t)nl * cws));
     hipLaunchKernelGGL(k_hot_bits, dim3((unsigned)((words + kBlock - 1) / kBlock), nl), dim3(kBlock), 0,
-                       ctx->stream, grp, P.bx.p, P.bx_sb.p, ctx->hot_tau0.p, ctx->hot_bits.p, ctx->hot_coarse.p,
-                       cws);
+                       ctx->stream, grp, P.bx.p, P.bx_sb.p, ctx->hot_tau0.p, ctx->hot_bits.p);
     ctx->hot_tau0_gen = ctx->hot == 2 ? 0 : P.bx_gen;
     ctx->hot_tau0_n = n;
     return ctx->hip(hipGetLastError(), "hot-bin threshold launch");
@@ -3302,14 +3264,12 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                               nl, a.gz);
                 if (P.bx_sb_max <= (int64_t)kHotLdsWords * 32)
                     hipLaunchKernelGGL((k_hot_bx<kHotR, true>), hg, dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
-                                       P.samp.p, P.bx.p, ctx->hot_bits.p, ctx->hot_coarse.p,
-                                       hot_coarse_stride(P.bx_sb_max), a.n, a.cand_offset, a.seed, ctx->rounds.p,
+                                       P.samp.p, P.bx.p, ctx->hot_bits.p, a.n, a.cand_offset, a.seed, ctx->rounds.p,
                                        nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p, ctx->errflag.p, lst,
                                        ctx->hot_flag.p);
                 else
                     hipLaunchKernelGGL((k_hot_bx<kHotR, false>), hg, dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
-                                       P.samp.p, P.bx.p, ctx->hot_bits.p, ctx->hot_coarse.p,
-                                       hot_coarse_stride(P.bx_sb_max), a.n, a.cand_offset, a.seed, ctx->rounds.p,
+                                       P.samp.p, P.bx.p, ctx->hot_bits.p, a.n, a.cand_offset, a.seed, ctx->rounds.p,
                                        nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p, ctx->errflag.p, lst,
                                        ctx->hot_flag.p);
                 const unsigned bgx = (unsigned)((a.n + kBxR * kBlock - 1) / (kBxR * kBlock));
