@@ -34,6 +34,8 @@ PATCHES = {
     'bx2': [('tpe_expand.hip', 'constexpr int kBxChains = 4;', 'constexpr int kBxChains = 2;')],
     'nolist': [('tpe_engine.hip', '            const uint64_t bal = __ballot(take);\n            if (!bal) continue;\n            const int c = __builtin_amdgcn_readfirstlane',
                 '            const uint64_t bal = __ballot(take && (pend >> 31));\n            if (!bal) continue;\n            const int c = __builtin_amdgcn_readfirstlane')],
+    'nolist2': [('tpe_engine.hip', '            const uint64_t bal = __ballot(take);\n            if (!bal) continue;\n            const int c = __builtin_amdgcn_readfirstlane',
+                 '            const uint64_t bal = __ballot(x[r] == 1234.5678);\n            if (!bal) continue;\n            const int c = __builtin_amdgcn_readfirstlane')],
     'norej': [('tpe_device.h',
                '    const bool bounded = (L.flags & 3) == 3;\n    const uint32_t mask0 = pend;',
                '    const bool bounded = false;\n    const uint32_t mask0 = pend;')],
