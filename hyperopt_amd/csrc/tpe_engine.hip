@@ -816,13 +816,15 @@ __global__ __launch_bounds__(kBlock) void k_hot_bits(const int32_t* __restrict__
 // candidates (Box-Muller pairs per thread, the sampling records staged once
 // per workgroup -- the launch requires them in LDS).  The listed candidates
 // gather in a buffer per WAVE in LDS (its count wave-uniform, in a scalar
-// register: no LDS atomics, no barriers) and go to the cell's list with one
-// global atomic per wave flush -- when a slot's listings would not fit, and
-// at the end.  (Round 4 measured two other forms on the same box: one
-// workgroup buffer flushed only at the end, past which nearly every listing
-// wave appended with its own atomic on the cell's ONE counter, 2.34 ms at
-// 0.35 VALU busy; flushed after every tile that left 256 entries, behind a
-// barrier per tile, 1.37 ms at 0.75.)
+// register: no LDS atomics, no barriers in the loop) and go to the cell's
+// list with one global atomic per wave flush when a slot's listings would
+// not fit, and one per workgroup for the waves' remainders at the end.
+// (Round 4 measured other forms on the same box: one workgroup buffer
+// flushed only at the end, past which nearly every listing wave appended
+// with its own atomic on the cell's ONE counter, 2.34 ms at 0.35 VALU busy;
+// flushed after every tile that left 256 entries, behind a barrier per tile,
+// 1.37 ms at 0.75; per-wave buffers each ending with its own atomic, 1.38 ms
+// on the whole round but 1.0 ms for a label shard's few cells.)
 constexpr int kHotBuf = 128;     // entries per wave
 constexpr int kHotRetry = 512;   // rejected draws retried cooperatively per tile (the rest in-thread)
 
@@ -928,7 +930,28 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
             wn += c;
         }
     }
-    if (wn) hot_wave_flush(wn, buf_i[wv], buf_x[wv], hcnt, hidx, hx, cell, hstride, hflag);
+    // the end: every wave's remainder to the cell's list behind ONE atomic
+    // for the workgroup (a shard's round has few cells, each striped over
+    // many workgroups: per-wave atomics on its one counter cost 0.5 ms)
+    __shared__ int wcnt[kBlock / 64], wbase;
+    if ((threadIdx.x & 63) == 0) wcnt[wv] = wn;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) tot += wcnt[w];
+        wbase = tot ? atomicAdd(hcnt + cell, tot) : 0;
+        // a cell's list is hstride long: past it the round falls back to
+        // screening every candidate (hflag bit 2), so nothing is lost
+        if (tot && wbase + tot > hstride) atomicOr(hflag, 2);
+    }
+    __syncthreads();
+    int off = wbase;
+    for (int w = 0; w < wv; ++w) off += wcnt[w];
+    for (int k = threadIdx.x & 63; k < wn; k += 64)
+        if (off + k < hstride) {
+            hidx[cell * (size_t)hstride + off + k] = buf_i[wv][k];
+            hx[cell * (size_t)hstride + off + k] = buf_x[wv][k];
+        }
 }
 
 // The expansion screen over the listed candidates only: workgroups stride
@@ -1160,6 +1183,10 @@ constexpr unsigned kHotScreenWgs = 128;
 #define TPE_HOT_WGS 16384
 #endif
 constexpr int64_t kHotWgs = TPE_HOT_WGS;
+#ifndef TPE_HOT_BX_WGS
+#define TPE_HOT_BX_WGS 16384
+#endif
+constexpr int64_t kHotBxWgs = TPE_HOT_BX_WGS;   // k_hot_bx's workgroups over a round
 constexpr int kQR = 8;   // candidates per thread, k_qfused_tiles
 constexpr int kQLdsKeys = 1024;   // grid values whose keys k_qfused_tiles stages in LDS
 constexpr int kCatR = 8;  // candidates per thread, k_cat_tiles
@@ -3260,7 +3287,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                 const int64_t cells_l = (int64_t)nl * a.gz;
                 // ~kHotWgs workgroups over the round (tiles strided), at most one per tile
                 const dim3 hg((unsigned)std::max<int64_t>(
-                                  1, std::min<int64_t>((a.n + kHotR * kBlock - 1) / (kHotR * kBlock), kHotWgs / cells_l)),
+                                  1, std::min<int64_t>((a.n + kHotR * kBlock - 1) / (kHotR * kBlock), kHotBxWgs / cells_l)),
                               nl, a.gz);
                 if (P.bx_sb_max <= (int64_t)kHotLdsWords * 32)
                     hipLaunchKernelGGL((k_hot_bx<kHotR, true>), hg, dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
