@@ -1186,7 +1186,9 @@ constexpr int64_t kHotWgs = TPE_HOT_WGS;
 #ifndef TPE_HOT_BX_WGS
 #define TPE_HOT_BX_WGS 16384
 #endif
-constexpr int64_t kHotBxWgs = TPE_HOT_BX_WGS;   // k_hot_bx's workgroups over a round
+constexpr int64_t kHotBxWgs = TPE_HOT_BX_WGS;   // k_hot_bx's workgroups over a round, at most
+constexpr int64_t kHotFillWgs = 2560;           //   at least (5 per CU resident: two passes)
+constexpr int64_t kHotMinTiles = 6;             //   tiles per workgroup, at least (unless filling)
 constexpr int kQR = 8;   // candidates per thread, k_qfused_tiles
 constexpr int kQLdsKeys = 1024;   // grid values whose keys k_qfused_tiles stages in LDS
 constexpr int kCatR = 8;  // candidates per thread, k_cat_tiles
@@ -3285,10 +3287,16 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                     if (rc) return rc;
                 }
                 const int64_t cells_l = (int64_t)nl * a.gz;
-                // ~kHotWgs workgroups over the round (tiles strided), at most one per tile
-                const dim3 hg((unsigned)std::max<int64_t>(
-                                  1, std::min<int64_t>((a.n + kHotR * kBlock - 1) / (kHotR * kBlock), kHotBxWgs / cells_l)),
-                              nl, a.gz);
+                // workgroups per cell (tiles strided): at most one per tile and
+                // kHotBxWgs over the round; at least kHotMinTiles tiles each
+                // (a workgroup stages its tables first: a label shard's few
+                // cells at one or two tiles per workgroup ran 0.54 ms instead
+                // of 0.46) unless the chip needs more to fill it
+                const int64_t tiles_c = (a.n + kHotR * kBlock - 1) / (kHotR * kBlock);
+                const int64_t per_cell = std::min<int64_t>(
+                    {tiles_c, kHotBxWgs / cells_l,
+                     std::max<int64_t>((kHotFillWgs + cells_l - 1) / cells_l, tiles_c / kHotMinTiles)});
+                const dim3 hg((unsigned)std::max<int64_t>(1, per_cell), nl, a.gz);
                 if (P.bx_sb_max <= (int64_t)kHotLdsWords * 32)
                     hipLaunchKernelGGL((k_hot_bx<kHotR, true>), hg, dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
                                        P.samp.p, P.bx.p, ctx->hot_bits.p, a.n, a.cand_offset, a.seed, ctx->rounds.p,
