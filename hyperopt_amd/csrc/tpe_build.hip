@@ -1342,7 +1342,18 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     const int32_t n_labels = (int32_t)B.specs_h.size();
     Posterior& P = ctx->resident;
     ctx->P = &ctx->resident;
-    hipStream_t st = ctx->stream;
+    // a subset rebuild of labels that are all non-dense (the quantized labels
+    // given numpy's tie order) touches no dense label's DLabel, records or
+    // sampling records -- what the expansion index reads: it runs on the aux
+    // stream beside an index queued on the main one (tpe_prepare), and the
+    // index is kept without the snapshot comparison.  (On the main stream it
+    // waited for the whole index: ~0.35 ms of the config-3 fmin step.)
+    bool beside = subset;
+    for (int32_t i = 0; beside && i < n_only; ++i) {
+        const tpe_label_spec& s = B.specs_h[only_h[i]];
+        beside = s.kind == TPE_CATEGORICAL || (s.flags & TPE_HAS_Q) != 0;
+    }
+    hipStream_t st = beside ? ctx->aux : ctx->stream;
 
     // n_below = min(ceil(gamma sqrt(len(l_vals))), gamma_cap)   tpe.py:636 --
     // gamma_cap is ap_filter_trials' default DEFAULT_LF (tpe.py:626), which
@@ -1474,7 +1485,7 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     if (ties_out)
         HIPCHK(ctx, hipMemcpyAsync(ctx->ties_h.data(), B.ties.p, (n_labels + 1) * sizeof(int32_t),
                                    hipMemcpyDeviceToHost, st));
-    {   // does the expansion index of the previous posterior still hold?
+    if (!beside) {   // does the expansion index of the previous posterior still hold?
         const int rc = tpe_rt::bx_keep_check(ctx);
         if (rc) return rc;
     }
@@ -1506,7 +1517,7 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     // the index is kept when every dense label came out bit-identical (e.g.
     // a second build of the same history that only supplies the tie order
     // of quantized labels)
-    P.bx_ready = tpe_rt::bx_keep_after(ctx, groups_changed);
+    if (!beside) P.bx_ready = tpe_rt::bx_keep_after(ctx, groups_changed);
     P.n_labels = n_labels;
     B.n_labels = n_labels;
     B.mix_h = mix;
