@@ -312,18 +312,15 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
     // added to the rounding term); the powers g (2 kappa d)^n by one
     // multiply each, A_n += that / n! (one rounding each, inside 3P + 10)
     const double inv_a = 1.0 / B.astar;
-    // the next batch's record loaded while this one is summed (round 4: the
-    // kernel waited on each batch's load, 0.32 of its wave cycles parked)
-    Comp<double> nxt{};
-    if (k0 + wave * 64 + lane < k1) nxt = c[k0 + wave * 64 + lane];
     for (int kc = k0 + wave * 64; kc < k1; kc += kBlock) {
         const int k = kc + lane;
-        const Comp<double> rec = nxt;
-        if (kc + kBlock + lane < k1) nxt = c[kc + kBlock + lane];
         double mu_l = 0.0, c_l = -kInf;
-        if (k < k1 && rec.a == B.astar) {
-            mu_l = rec.mu * inv_a;
-            c_l = rec.c * kExpScaleInv;
+        if (k < k1) {
+            const Comp<double> rec = c[k];
+            if (rec.a == B.astar) {
+                mu_l = rec.mu * inv_a;
+                c_l = rec.c * kExpScaleInv;
+            }
         }
         const int cnt = min(64, k1 - kc);
         __builtin_amdgcn_wave_barrier();   // (the previous batch's reads come first: LDS is in order per wave)
