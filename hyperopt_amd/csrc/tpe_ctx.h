@@ -397,6 +397,7 @@ struct tpe_ctx {
     DevBuf<unsigned long long> hot_t, hot_tau0;   // per cell largest L; per label tau0
     DevBuf<uint32_t> hot_bits;           // per sub-bin: U >= tau0 (words at sb_off / 32)
     DevBuf<int32_t> hot_flag;            // fallback flag
+    DevBuf<int32_t> hot_items;           // k_screen_hot's work items: per cell the first, then the counter
     tpe_rt::PinVec<int32_t> hot_cnt_h;
     int64_t hot_listed = 0;              // last round: candidates the prefilter listed
     int32_t hot_fallback = 0;            // last round: 1 if it re-ran the plain screen

@@ -954,31 +954,89 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
         }
 }
 
-// The expansion screen over the listed candidates only: workgroups stride
-// over the cell's list in passes of R * 256; the same scores, bounds and
-// appends as k_screen_bx.
+// k_hot_bx's lists as work items of R * 256 listed candidates (the passes
+// of k_screen_hot): pre[c] = the first item of cell c (cell c has
+// ceil(min(hcnt[c], hstride) / (R 256)) of them), pre[cells] = all; one
+// workgroup of 1024, which also zeroes the item counter.
+template <int R>
+__global__ __launch_bounds__(1024) void k_hot_items(const int32_t* __restrict__ hcnt, int64_t cells,
+                                                    int64_t hstride, int32_t* __restrict__ pre,
+                                                    int32_t* __restrict__ next) {
+    constexpr int64_t per = (int64_t)R * kBlock;
+    __shared__ int32_t wsum[16];
+    __shared__ int32_t carry;
+    if (threadIdx.x == 0) {
+        carry = 0;
+        *next = 0;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int64_t c0 = 0; c0 < cells; c0 += 1024) {
+        const int64_t c = c0 + threadIdx.x;
+        int32_t v = 0;
+        if (c < cells) v = (int32_t)((min((int64_t)hcnt[c], hstride) + per - 1) / per);
+        int32_t x = v;   // inclusive scan over the wave
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int32_t y = __shfl_up(x, off);
+            if (lane >= off) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        int32_t wp = carry;
+        for (int u = 0; u < w; ++u) wp += wsum[u];
+        if (c < cells) pre[c] = wp + x - v;
+        __syncthreads();   // (carry and wsum read by every thread)
+        if (threadIdx.x == 1023) carry = wp + x;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) pre[cells] = carry;
+}
+
+// The expansion screen over the listed candidates only, one pass of R * 256
+// listed candidates per work item (k_hot_items): a persistent grid whose
+// workgroups stage the exp table once and take items from a counter until
+// none are left -- round 3's grid of 128 workgroups per cell staged the 32 KB
+// table for about one pass each and left the cells with long lists to a
+// tail.  The same scores, bounds and appends as k_screen_bx (the passes are
+// the same R * 256-aligned slices of each cell's list).
 template <int R>
 __global__ __launch_bounds__(kBlock) void k_screen_hot(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
     const Comp<double>* __restrict__ comps64, const BxLabel* __restrict__ bx, const double* __restrict__ tab,
-    const int32_t* __restrict__ loff, const int32_t* __restrict__ list, int64_t n, int32_t nl,
+    const int32_t* __restrict__ loff, const int32_t* __restrict__ list, int64_t n, int32_t nl, int64_t cells,
+    const int32_t* __restrict__ pre, int32_t* __restrict__ next,
     const int32_t* __restrict__ hcnt, const int32_t* __restrict__ hidx, const double* __restrict__ hx,
     double* __restrict__ hi, unsigned long long* __restrict__ lbkey, int32_t* __restrict__ cnt,
     int32_t* __restrict__ idx, unsigned long long* __restrict__ terms, const float2* __restrict__ sb,
     unsigned long long* __restrict__ tkey, int64_t hstride) {
-    const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
-    const int64_t m = min((int64_t)hcnt[cell], hstride);   // (an overflowed list falls back anyway)
     constexpr int64_t per = (int64_t)R * kBlock;
-    if ((int64_t)blockIdx.x * per >= m) return;   // uniform over the workgroup
-    const int li = group[blockIdx.y];
-    const DLabel L = labels[li];
-    const BxLabel B = bx[li];
     __shared__ double exp_tab[kExpTabSize];
+    __shared__ int item_sh;
+    __shared__ uint64_t shk[kBlock / 64];
+    const int32_t total = pre[cells];
+    if (threadIdx.x == 0) item_sh = total > 0 ? atomicAdd(next, 1) : total;
+    __syncthreads();
+    int32_t item = item_sh;
+    if (item >= total) return;   // (uniform: a workgroup with nothing to do stages nothing)
     load_exp_table(exp_tab);
-    const bool lgmm = L.mode == DENSE_LGMM;
-    const int64_t nsb = (int64_t)B.nbins * kBxSub;
-    uint64_t kl = 0;   // the largest sub-bin L of the listed candidates
-    for (int64_t j0 = (int64_t)blockIdx.x * per; j0 < m; j0 += (int64_t)gridDim.x * per) {
+    for (;;) {
+        // the item's cell: the last c with pre[c] <= item (empty cells share
+        // their successor's start)
+        int64_t lo = 0, up = cells;
+        while (up - lo > 1) {
+            const int64_t mid = (lo + up) >> 1;
+            if (pre[mid] <= item) lo = mid; else up = mid;
+        }
+        const size_t cell = (size_t)lo;
+        const int64_t m = min((int64_t)hcnt[cell], hstride);   // (an overflowed list falls back anyway)
+        const int64_t j0 = (int64_t)(item - pre[cell]) * per;
+        const int li = group[cell % (size_t)nl];
+        const DLabel L = labels[li];
+        const BxLabel B = bx[li];
+        const bool lgmm = L.mode == DENSE_LGMM;
+        const int64_t nsb = (int64_t)B.nbins * kBxSub;
+        uint64_t kl = 0;   // the largest sub-bin L of the listed candidates
         double x[R];
         int64_t ci[R];
         bool valid[R];
@@ -1000,10 +1058,16 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
         uint64_t bk = 0;
         bx_bounds<R>(s, E, valid, hv, bk);
         bx_append<R>(hv, valid, ci, bk, nterms, cell, hstride, hi, lbkey, cnt, idx, terms);
+        kl = block_max_key(kl, shk);
+        if (threadIdx.x == 0) {
+            if (kl) atomicMax(tkey + cell, kl);
+            item_sh = atomicAdd(next, 1);
+        }
+        __syncthreads();   // (shk read by every thread before thread 0 wrote item_sh: block_max_key's barrier)
+        item = item_sh;
+        if (item >= total) break;
+        __syncthreads();   // item_sh read by every thread before the next write
     }
-    __shared__ uint64_t shk[kBlock / 64];
-    kl = block_max_key(kl, shk);
-    if (threadIdx.x == 0 && kl) atomicMax(tkey + cell, kl);
 }
 
 // tpe_hot_probe: the sub-bin (U, L) of caller-supplied candidates of one
@@ -1178,7 +1242,7 @@ constexpr int kBxR = TPE_BX_R;
 #define TPE_HOT_R 8
 #endif
 constexpr int kHotR = TPE_HOT_R;
-constexpr unsigned kHotScreenWgs = 128;
+constexpr unsigned kHotScreenWgs = 1024;   // k_screen_hot's persistent grid (4 workgroups per CU: LDS)
 #ifndef TPE_HOT_WGS
 #define TPE_HOT_WGS 16384
 #endif
@@ -3307,12 +3371,14 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                                        P.samp.p, P.bx.p, ctx->hot_bits.p, a.n, a.cand_offset, a.seed, ctx->rounds.p,
                                        nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p, ctx->errflag.p, lst,
                                        ctx->hot_flag.p);
-                const unsigned bgx = (unsigned)((a.n + kBxR * kBlock - 1) / (kBxR * kBlock));
-                hipLaunchKernelGGL((k_screen_hot<kBxR>), dim3(std::min(bgx, kHotScreenWgs), nl, a.gz), dim3(kBlock),
-                                   0, ctx->stream, P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p, P.bx_loff.p,
-                                   P.bx_list.p, a.n, nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p,
-                                   ctx->scr_hid.p, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p,
-                                   ctx->win_evals.p, P.bx_sb.p, ctx->hot_t.p, lst);
+                HIPCHK(ctx, ctx->hot_items.reserve((size_t)cells + 2));
+                hipLaunchKernelGGL((k_hot_items<kBxR>), dim3(1), dim3(1024), 0, ctx->stream, ctx->hot_cnt.p,
+                                   (int64_t)cells, lst, ctx->hot_items.p, ctx->hot_items.p + cells + 1);
+                hipLaunchKernelGGL((k_screen_hot<kBxR>), dim3(kHotScreenWgs), dim3(kBlock), 0, ctx->stream,
+                                   P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p, P.bx_loff.p, P.bx_list.p, a.n,
+                                   nl, (int64_t)cells, ctx->hot_items.p, ctx->hot_items.p + cells + 1,
+                                   ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p, ctx->scr_hid.p, ctx->scr_lb.p,
+                                   ctx->scr_cnt.p, ctx->scr_idx.p, ctx->win_evals.p, P.bx_sb.p, ctx->hot_t.p, lst);
             } else {
                 screen_bx_all(ctx, grp, nl, a);
             }
