@@ -4297,12 +4297,7 @@ int tpe_ctx_create(int device, int precision, tpe_ctx** out) {
              hipEventCreate(&c->evm[m][1]) == hipSuccess;
     ok = ok && hipEventCreate(&c->evs[0]) == hipSuccess && hipEventCreate(&c->evs[1]) == hipSuccess;
     ok = ok && hipEventCreate(&c->ev_prep[0]) == hipSuccess && hipEventCreate(&c->ev_prep[1]) == hipSuccess;
-    // the aux stream at the highest priority: its work (the quantized labels'
-    // ordered rebuild beside the expansion index, a windowed group's sort)
-    // is small and on the step's critical path, the main stream's is wide
-    int prio_least = 0, prio_greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
-    ok = ok && hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, prio_greatest) == hipSuccess &&
+    ok = ok && hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess &&
          hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess;
     for (int j = 0; j < 2; ++j)
         ok = ok && hipEventCreateWithFlags(&c->ev_sorted[j], hipEventDisableTiming) == hipSuccess &&
