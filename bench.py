@@ -138,6 +138,9 @@ def parse():
     ap.add_argument('--early-orders', type=int, default=None,
                     help='1/0: the known labels\' argsorts under the first build '
                          '(posterior.EARLY_ORDERS)')
+    ap.add_argument('--overlap-min-dense', type=int, default=None,
+                    help='dense labels from which a fresh step builds order-free first and runs the '
+                         'index beside the tie orders (workloads.OVERLAP_MIN_DENSE)')
     ap.add_argument('--sort-threads', type=int, default=None,
                     help='threads of the tie-order argsort pool (posterior.SORT_THREADS)')
     ap.add_argument('--no-other-configs', action='store_true',
@@ -357,6 +360,9 @@ def main():
         P.SORT_THREADS = args.sort_threads
     if args.early_orders is not None:
         P.EARLY_ORDERS = bool(args.early_orders)
+    if args.overlap_min_dense is not None:
+        from hyperopt_amd import workloads as W
+        W.OVERLAP_MIN_DENSE = args.overlap_min_dense
     from hyperopt_amd.engine import Engine
     from hyperopt_amd.workloads import (FminLoop, conditional_history, hartmann_history,
                                          mixed_history)
