@@ -391,6 +391,7 @@ struct tpe_ctx {
     int32_t hot = 1;                     // 0 off, 1 on, 2 test: force the fallback
     bool early = true;                   // early exit of quantized / categorical tile rounds
     bool zero_win = true;                // packed re-score skips the exactly-zero above terms
+    bool zw_pending = false;             //   its windows launched this round (built iff its plan was not empty)
     double hot_cap_div = 16.0;           // hot lists hold n / hot_cap_div per cell (shrinks on overflow)
     DevBuf<double> hot_x;                // per cell: listed candidates' x
     DevBuf<int32_t> hot_i, hot_cnt;      //   their indices; per cell the count

@@ -1743,11 +1743,16 @@ __device__ __forceinline__ void zero_reach(const Comp<double>& c, double& lo, do
 }
 
 constexpr int kZwBlock = 1024;
-__global__ __launch_bounds__(kZwBlock) void k_zero_windows(const DLabel* __restrict__ labels,
+// (skipped when the round's device-planned re-score holds nothing: a
+// value-only round that certified every cell needs no windows; the host
+// marks them built only when the plan was not empty)
+__global__ __launch_bounds__(kZwBlock) void k_zero_windows(const RescorePlan* __restrict__ plan,
+                                                           const DLabel* __restrict__ labels,
                                                            const int32_t* __restrict__ group,
                                                            const Comp<double>* __restrict__ comps64,
                                                            double* __restrict__ zhi, double* __restrict__ zlo,
                                                            int32_t* __restrict__ zwide, int32_t* __restrict__ zn) {
+    if (plan->total == 0) return;   // (uniform)
     const int li = group[blockIdx.x];
     const DLabel L = labels[li];
     const Comp<double>* c = comps64 + L.comp_a;
@@ -3208,10 +3213,10 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
             HIPCHK(ctx, P.zw_n.reserve(std::max(P.n_labels, 1)));
             // every dense label of the posterior (the GMM1 and LGMM1 groups are adjacent)
             const int nd = (int)(P.h_group[DENSE_GMM].size() + P.h_group[DENSE_LGMM].size());
-            hipLaunchKernelGGL(k_zero_windows, dim3((unsigned)nd), dim3(kZwBlock), 0, ctx->stream, P.labels.p,
+            hipLaunchKernelGGL(k_zero_windows, dim3((unsigned)nd), dim3(kZwBlock), 0, ctx->stream, plan, P.labels.p,
                                P.groups.p + P.group_off[DENSE_GMM], P.comps64.p, P.zw_hi.p, P.zw_lo.p,
                                P.zw_wide.p, P.zw_n.p);
-            P.zw_ready = true;
+            ctx->zw_pending = true;   // built iff the plan was not empty (read after the round's sync)
         }
         const unsigned g = (unsigned)std::min<int64_t>(ne_max, 2048);
         hipLaunchKernelGGL((k_rescore_packed<kRP>), dim3(g, nch), dim3(kBlock), 0,
@@ -3897,6 +3902,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     }
     if (fam & (1 << CAT)) ctx->cat_early = false;
     ctx->pk_plan_pending = false;
+    ctx->zw_pending = false;
     ctx->evw_used = 0;
     ctx->screen_pending = false;
     ctx->screen_exec_pending = false;
@@ -3972,6 +3978,10 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     }
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     if (tiles > 0 && out) std::memcpy(out, ctx->res_h.data(), n_res * sizeof(tpe_label_result));
+    if (ctx->zw_pending) {
+        ctx->P->zw_ready = pin.plan.total > 0;
+        ctx->zw_pending = false;
+    }
     if (ctx->pk_plan_pending && pin.plan.overflow && !ctx->pk_redo) {
         // the packed re-score listed more candidates than its buffers hold:
         // nothing was re-scored; the round again with buffers for them all
