@@ -141,8 +141,6 @@ def parse():
     ap.add_argument('--overlap-min-dense', type=int, default=None,
                     help='dense labels from which a fresh step builds order-free first and runs the '
                          'index beside the tie orders (workloads.OVERLAP_MIN_DENSE)')
-    ap.add_argument('--pin-orders', type=int, default=None,
-                    help='1/0: the tie orders handed to the rebuild in pinned memory (posterior.PIN_ORDERS)')
     ap.add_argument('--sort-threads', type=int, default=None,
                     help='threads of the tie-order argsort pool (posterior.SORT_THREADS)')
     ap.add_argument('--no-other-configs', action='store_true',
@@ -362,8 +360,6 @@ def main():
         P.SORT_THREADS = args.sort_threads
     if args.early_orders is not None:
         P.EARLY_ORDERS = bool(args.early_orders)
-    if args.pin_orders is not None:
-        P.PIN_ORDERS = bool(args.pin_orders)
     if args.overlap_min_dense is not None:
         from hyperopt_amd import workloads as W
         W.OVERLAP_MIN_DENSE = args.overlap_min_dense

@@ -268,7 +268,7 @@ def n_below_of(n_valid, gamma, gamma_cap=DEFAULT_LF):
     return int(min(np.ceil(gamma * np.sqrt(n_valid)), gamma_cap))
 
 
-def reference_orders(losses, n_below, obs_of, labels, pinned=False):
+def reference_orders(losses, n_below, obs_of, labels):
     """The reference's own np.argsort orders, for the device builder's
     `tpe_build_posterior_resident_ordered`: the below set as
     ap_filter_trials picks it (`l_order = np.argsort(l_vals)`, tpe.py:637;
@@ -279,9 +279,7 @@ def reference_orders(losses, n_below, obs_of, labels, pinned=False):
     land where the reference puts them.  obs_of(l) -> (trial position per
     observation, -1 for none; transformed value); obs_of.n_labels = L.
     Returns (below mask per trial position, order_off[L + 1], order), with
-    empty ranges for the labels not in `labels`; pinned=True puts `order` in
-    the calling thread's reused pinned buffer (_order_buffer: valid until the
-    thread's next pinned call)."""
+    empty ranges for the labels not in `labels`."""
     losses = np.asarray(losses, dtype=np.float64)
     T = len(losses)
     has = losses == losses
@@ -326,36 +324,8 @@ def reference_orders(losses, n_below, obs_of, labels, pinned=False):
         parts = list(_sort_pool().map(np.argsort, parts))
     else:
         parts = [np.argsort(m) for m in parts]
-    order = (_order_buffer(int(off[-1])) if pinned and PIN_ORDERS
-             else np.empty(int(off[-1]), dtype=np.int32))
-    if parts:
-        np.concatenate(parts, out=order, casting='same_kind')
+    order = np.concatenate(parts).astype(np.int32) if parts else np.zeros(0, dtype=np.int32)
     return below, off, order
-
-
-_pin_tls = threading.local()
-PIN_ORDERS = True   # the build's orders in pinned memory (bench.py --pin-orders)
-
-
-def _order_buffer(n):
-    """The int32 order array reference_orders fills, in PINNED host memory
-    when a GPU runtime is there (torch's pinned allocator: the rebuild's H2D
-    of the orders is then a DMA, not a staged pageable copy -- 4 MB per step
-    at config 5, ~0.8 ms pageable).  One buffer per thread, reused: the
-    build that reads it copies and synchronises before returning, and one
-    thread computes one set of orders at a time."""
-    buf = getattr(_pin_tls, 'order', None)
-    if buf is None or buf.size < n:
-        cap = max(n + n // 4, 1 << 16)
-        try:
-            import torch
-            t = torch.empty(cap, dtype=torch.int32, pin_memory=True)
-            _pin_tls.tensor = t          # (keeps the pinned block alive)
-            buf = t.numpy()
-        except Exception:                # no GPU runtime (CPU tests): pageable
-            buf = np.empty(cap, dtype=np.int32)
-        _pin_tls.order = buf
-    return buf[:n]
 
 
 EARLY_ORDERS = True   # known labels' argsorts started before the first build (build_reference_order)
@@ -490,14 +460,14 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
         if known and EARLY_ORDERS:
             # the previous build's order-dependent labels: their argsorts
             # start now, on the host, under the first build and the index
-            early = _order_thread().submit(reference_orders, losses, n_below, obs_of, known, True)
+            early = _order_thread().submit(reference_orders, losses, n_below, obs_of, known)
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf)
         t0 = _phase('build', t0)
         eng.prepare(*prepare)
         t0 = _phase('prepare_enqueue', t0)
         have = set()
     elif known:
-        below, off, order = reference_orders(losses, n_below, obs_of, known, True)
+        below, off, order = reference_orders(losses, n_below, obs_of, known)
         t0 = _phase('argsorts', t0)
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf, below, off, order)
         t0 = _phase('build', t0)
@@ -519,7 +489,7 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
             and SUBSET_REBUILD
             and need <= set(quant) and len(need) < obs_of.n_labels):
         res, (nb, ties) = _run_deferred(
-            eng, round_call, lambda: reference_orders(losses, n_below, obs_of, need, True),
+            eng, round_call, lambda: reference_orders(losses, n_below, obs_of, need),
             lambda o: eng.rebuild_labels(losses, n_valid, gamma, prior_weight, lf, o[1], o[2], need),
             quant, t0)
         if res is not None:
@@ -540,7 +510,7 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
             early = None
     if need != have or ties[-1]:
         if early is None:
-            below, off, order = reference_orders(losses, n_below, obs_of, need, True)
+            below, off, order = reference_orders(losses, n_below, obs_of, need)
         t0 = _phase('argsorts', t0)
         if SUBSET_REBUILD and not ties[-1] and len(need) < obs_of.n_labels:
             # no tie across the split (the below set is the one just built):
@@ -554,7 +524,7 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
             # a supplied below set can move observations between the sets,
             # creating a dependent label the first pass did not see
             need |= set(np.flatnonzero(ties[:-1] & 2).tolist())
-            below, off, order = reference_orders(losses, n_below, obs_of, need, True)
+            below, off, order = reference_orders(losses, n_below, obs_of, need)
             nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf, below, off,
                                                    order)
             assert not np.any(ties[:-1])
