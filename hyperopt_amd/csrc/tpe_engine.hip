@@ -1239,7 +1239,7 @@ constexpr int kBxR = TPE_BX_R;
 // candidates per thread in k_hot_bx (draw + one sub-bin read each), and the
 // workgroups per cell striding over the listed candidates in k_screen_hot
 #ifndef TPE_HOT_R
-#define TPE_HOT_R 8
+#define TPE_HOT_R 6   // (8 spilled 8 VGPRs at the 96-register cap: 48 MB of scratch writes per round, r4aj)
 #endif
 constexpr int kHotR = TPE_HOT_R;
 constexpr unsigned kHotScreenWgs = 1024;   // k_screen_hot's persistent grid (4 workgroups per CU: LDS)
