@@ -88,3 +88,26 @@ def test_packed_rescore_overflow_runs_again(eng, value_only):
         eng.set_option('value_only', 0)
     assert np.ascontiguousarray(a).tobytes() == np.ascontiguousarray(b).tobytes()
     assert np.ascontiguousarray(a).tobytes() == np.ascontiguousarray(c).tobytes()
+
+
+def test_exact_round_after_an_empty_value_only_plan(eng):
+    """A value-only round whose screen decides every cell plans no re-score
+    and skips the zero windows (k_zero_windows exits on the empty plan); an
+    exact round on the same posterior afterwards must build them: its bytes
+    equal those of an exact round on a fresh posterior."""
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.workloads import mixed_history
+    hist = mixed_history(64, 20000, seed=2)
+    posts = P.pack(hist.posteriors())
+    ids = list(range(300, 812))
+    eng.set_posterior(*posts)
+    eng.set_option('value_only', 1)
+    try:
+        vo = eng.suggest_batch(13, ids, 24)
+    finally:
+        eng.set_option('value_only', 0)
+    after = eng.suggest_batch(13, ids, 24)
+    eng.set_posterior(*posts)              # a fresh posterior: windows built in its first round
+    fresh = eng.suggest_batch(13, ids, 24)
+    assert np.ascontiguousarray(after).tobytes() == np.ascontiguousarray(fresh).tobytes()
+    assert np.isnan(vo['lpdf_below']).any()   # (the value-only round decided cells alone)
