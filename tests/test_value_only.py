@@ -104,8 +104,10 @@ def test_exact_round_after_an_empty_value_only_plan(eng):
     eng.set_option('value_only', 1)
     try:
         vo = eng.suggest_batch(13, ids, 24)
+        rescored = eng.last_screen()[1]
     finally:
         eng.set_option('value_only', 0)
+    assert rescored == 0, rescored            # the plan was empty: no zero windows built
     after = eng.suggest_batch(13, ids, 24)
     eng.set_posterior(*posts)              # a fresh posterior: windows built in its first round
     fresh = eng.suggest_batch(13, ids, 24)
