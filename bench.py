@@ -122,8 +122,8 @@ def parse():
                          'torchrun; a repeated ordinal shares that GPU (tests)')
     ap.add_argument('--shard', default='auto', choices=['auto', 'labels', 'candidates'],
                     help='N > 1: label shards (each rank holds a subset of the labels: their '
-                         'history, posterior, index and whole rounds; auto when there are at least '
-                         '2 labels per rank) or candidate shards (every label, C/N candidates each)')
+                         'history, posterior, index and whole rounds; auto when every rank gets at '
+                         'least one label) or candidate shards (every label, C/N candidates each)')
     ap.add_argument('--dist-backend', default='nccl',
                     help='nccl (RCCL over xGMI); gloo only to rehearse N ranks on one GPU')
     ap.add_argument('--no-agreement', action='store_true',
@@ -408,8 +408,10 @@ def main():
                           'includes the H2D of the history) vs posterior.py + pack'}
     C_total = 24 if args.config == 5 else 1 << args.cand_log2
     from hyperopt_amd.parallel import gather_labels, label_shards
+    # label shards whenever every rank gets a label (r4am: config 4's 13 labels
+    # over 8 ranks project 0.25 / 0.28 against 0.14 / 0.15 as candidate shards)
     by_label = (args.shard == 'labels' or
-                (args.shard == 'auto' and len(hist_full.labels) >= 2 * max(world, 8 if world == 1 else 1)))
+                (args.shard == 'auto' and len(hist_full.labels) >= max(world, 8 if world == 1 else 1)))
     shards = label_shards(hist_full.labels, world) if by_label else None
     if by_label:   # whole rounds of this rank's labels
         ids_local, C = args.new_ids, C_total
