@@ -456,20 +456,15 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
     known = set(known)
     t0 = time.perf_counter()
     early = None
-    # with the previous step's order-dependent labels known, their argsorts
-    # run beside an order-free first build (and the index, when one is
-    # prepared) and only those labels are rebuilt -- also for small rounds,
-    # where the build alone (no index) is what the argsorts overlap
-    if (prepare and (overlap or not known)) or (known and EARLY_ORDERS and overlap):
+    if prepare and (overlap or not known):
         if known and EARLY_ORDERS:
             # the previous build's order-dependent labels: their argsorts
             # start now, on the host, under the first build and the index
             early = _order_thread().submit(reference_orders, losses, n_below, obs_of, known)
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf)
         t0 = _phase('build', t0)
-        if prepare:
-            eng.prepare(*prepare)
-            t0 = _phase('prepare_enqueue', t0)
+        eng.prepare(*prepare)
+        t0 = _phase('prepare_enqueue', t0)
         have = set()
     elif known:
         below, off, order = reference_orders(losses, n_below, obs_of, known)
