@@ -135,6 +135,9 @@ def parse():
     ap.add_argument('--defer', type=int, default=None,
                     help='1/0: the dense labels\' round under the tie-order argsorts '
                          '(posterior.DEFER_QUANT; default: the library\'s)')
+    ap.add_argument('--early-orders', type=int, default=None,
+                    help='1/0: the known labels\' argsorts under the first build '
+                         '(posterior.EARLY_ORDERS)')
     ap.add_argument('--overlap-min-dense', type=int, default=None,
                     help='dense labels from which a fresh step builds order-free first and runs the '
                          'index beside the tie orders (workloads.OVERLAP_MIN_DENSE)')
@@ -355,6 +358,8 @@ def main():
         P.DEFER_QUANT = bool(args.defer)
     if args.sort_threads is not None:
         P.SORT_THREADS = args.sort_threads
+    if args.early_orders is not None:
+        P.EARLY_ORDERS = bool(args.early_orders)
     if args.overlap_min_dense is not None:
         from hyperopt_amd import workloads as W
         W.OVERLAP_MIN_DENSE = args.overlap_min_dense

@@ -328,6 +328,23 @@ def reference_orders(losses, n_below, obs_of, labels):
     return below, off, order
 
 
+EARLY_ORDERS = True   # known labels' argsorts started before the first build (build_reference_order)
+_order_exec = None
+
+
+def _order_thread():
+    """One worker for reference_orders started ahead of the build (its
+    argsorts go on to the sort pool: a separate executor, so the pool's
+    workers never wait on themselves)."""
+    global _order_exec
+    if _order_exec is None:
+        with _pool_lock:
+            if _order_exec is None:
+                from concurrent.futures import ThreadPoolExecutor
+                _order_exec = ThreadPoolExecutor(max_workers=1)
+    return _order_exec
+
+
 _POOL_MIN = 1 << 14   # observations to sort (over several labels), from which the pool pays
 SORT_THREADS = 16     # the argsort pool's threads at most (bench.py --sort-threads)
 _pool = None
@@ -438,7 +455,12 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
     n_below = n_below_of(n_valid, gamma)
     known = set(known)
     t0 = time.perf_counter()
+    early = None
     if prepare and (overlap or not known):
+        if known and EARLY_ORDERS:
+            # the previous build's order-dependent labels: their argsorts
+            # start now, on the host, under the first build and the index
+            early = _order_thread().submit(reference_orders, losses, n_below, obs_of, known)
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf)
         t0 = _phase('build', t0)
         eng.prepare(*prepare)
@@ -463,7 +485,8 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
         raise AssertionError('below mixture depends on a tie order (lf < gamma_cap?)')
     need = have | set(np.flatnonzero(ties[:-1] & 2).tolist())
     res = None
-    if (DEFER_QUANT and round_call is not None and need != have and not ties[-1] and SUBSET_REBUILD
+    if (DEFER_QUANT and early is None and round_call is not None and need != have and not ties[-1]
+            and SUBSET_REBUILD
             and need <= set(quant) and len(need) < obs_of.n_labels):
         res, (nb, ties) = _run_deferred(
             eng, round_call, lambda: reference_orders(losses, n_below, obs_of, need),
@@ -477,8 +500,17 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
         have = set()
         ties = np.ones_like(ties)
         t0 = time.perf_counter()
+    if early is not None:
+        orders = early.result()   # (waited for even when unused: obs_of is not shared)
+        if need != have and need <= known:
+            # rebuild every known label (an ordered build is right for any)
+            need = set(known)
+            below, off, order = orders
+        else:
+            early = None
     if need != have or ties[-1]:
-        below, off, order = reference_orders(losses, n_below, obs_of, need)
+        if early is None:
+            below, off, order = reference_orders(losses, n_below, obs_of, need)
         t0 = _phase('argsorts', t0)
         if SUBSET_REBUILD and not ties[-1] and len(need) < obs_of.n_labels:
             # no tie across the split (the below set is the one just built):

@@ -60,6 +60,7 @@ def test_deferred_quantized_round_equals_sequential(C, n_rounds, labels):
     lb.advance(b, 10000)
     P.PHASES = {}
     defer, P.DEFER_QUANT = P.DEFER_QUANT, True     # (off by default: measured slower)
+    early, P.EARLY_ORDERS = P.EARLY_ORDERS, False   # (the deferred path computes its own)
     try:
         for i in range(3):
             n = 10001 + i
@@ -83,5 +84,6 @@ def test_deferred_quantized_round_equals_sequential(C, n_rounds, labels):
     finally:
         P.PHASES = None
         P.DEFER_QUANT = defer
+        P.EARLY_ORDERS = early
         a.close()
         b.close()
