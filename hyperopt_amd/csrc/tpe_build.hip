@@ -1514,6 +1514,7 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     P.h_labels = dl;
     P.win_ready = false;
     P.zw_ready = false;
+    P.qc_ready = false;
     // the index is kept when every dense label came out bit-identical (e.g.
     // a second build of the same history that only supplies the tie order
     // of quantized labels)

@@ -172,6 +172,11 @@ struct Posterior {
     bool zw_ready = false;
     DevBuf<double> zw_hi, zw_lo;
     DevBuf<int32_t> zw_wide, zw_n;       // per label at comp_a: its wide records; per label: their count
+    // the quantized labels' above mixtures as runs of equal (mu, a)
+    // (k_qcompress, for k_qtable): per label at comp_a, and their count
+    bool qc_ready = false;
+    DevBuf<Comp<double>> qcomp;
+    DevBuf<int32_t> qc_n;
     int32_t win_t = 0;                   // the cut T the index was built for
     DevBuf<tpe::WinLabel> win;           // per label
     DevBuf<double> win_p, win_q;         // per component: prefix max of hi / suffix min of lo
@@ -225,6 +230,9 @@ struct Posterior {
         win_skip_part.release();
         win_ready = false;
         zw_ready = false;
+        qc_ready = false;
+        qcomp.release();
+        qc_n.release();
         zw_hi.release();
         zw_lo.release();
         zw_wide.release();

@@ -2296,7 +2296,8 @@ template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_qtable(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
     const Comp<double>* __restrict__ comps64, const QInfo* __restrict__ qinfo, int32_t nq,
-    int32_t qbase, double2* __restrict__ tab, unsigned long long* __restrict__ qkmax) {
+    int32_t qbase, double2* __restrict__ tab, unsigned long long* __restrict__ qkmax,
+    const Comp<double>* __restrict__ qcomp, const int32_t* __restrict__ qc_n) {
     const int li = group[blockIdx.y];
     const DLabel L = labels[li];
     const QInfo Q = qinfo[qbase + blockIdx.y];
@@ -2308,7 +2309,9 @@ __global__ __launch_bounds__(kBlock) void k_qtable(
     quant_bounds<MODE>(L, x, ub, lo, neg);
     constexpr bool kLog = MODE == QUANT_LGMM;
     double pb = wave_sum(quant_share<kLog, kBlock>(comps64 + L.comp_b, L.nb, ub, lo, threadIdx.x));
-    double pa = wave_sum(quant_share<kLog, kBlock>(comps64 + L.comp_a, L.na, ub, lo, threadIdx.x));
+    // the above mixture as its runs of equal (mu, a): a quantized label's
+    // observations take few distinct values (k_qcompress)
+    double pa = wave_sum(quant_share<kLog, kBlock>(qcomp + L.comp_a, qc_n[li], ub, lo, threadIdx.x));
     __shared__ double2 wp[kBlock / 64];
     if ((threadIdx.x & 63) == 0) wp[threadIdx.x >> 6] = make_double2(pb, pa);
     __syncthreads();
@@ -2325,6 +2328,60 @@ __global__ __launch_bounds__(kBlock) void k_qtable(
         const int64_t j = Q.jmin + s;
         if (qkmax && j >= Q.jlo && j <= Q.jhi) atomicMax(qkmax + qbase + blockIdx.y, order_key(v.x - v.y));
     }
+}
+
+// The quantized labels' above mixtures as runs of equal (mu, a) -- records
+// sorted by mu, the ties of a quantized label's observations adjacent (the
+// run's interior shares the clipped minimum sigma): each run becomes one
+// record whose weight is the run's weights summed in order, so k_qtable sums
+// ~(distinct values x 3) erf pairs per grid value instead of one per
+// observation (config 5: 50k -> a few hundred).  prob = sum_k w_k (Phi_u -
+// Phi_l) regrouped as sum_runs (sum w) (Phi_u - Phi_l): the quantized lpdf
+// bar (relative 1e-9, absolute 1e-13 on the probability; the run sums and
+// the reference's own term-by-term sum both round at ~1e-16 x the total).
+// One workgroup per quantized label position.
+constexpr int kQcBlock = 1024;
+__global__ __launch_bounds__(kQcBlock) void k_qcompress(const DLabel* __restrict__ labels,
+                                                        const int32_t* __restrict__ group,
+                                                        const Comp<double>* __restrict__ comps64,
+                                                        Comp<double>* __restrict__ qcomp,
+                                                        int32_t* __restrict__ qc_n) {
+    const int li = group[blockIdx.x];
+    const DLabel L = labels[li];
+    const Comp<double>* c = comps64 + L.comp_a;
+    Comp<double>* out = qcomp + L.comp_a;
+    const int n = L.na, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    auto same = [&](int k) {   // record k continues the run of k - 1 (bit-equal mu and a)
+        return k > 0 && __double_as_longlong(c[k].mu) == __double_as_longlong(c[k - 1].mu) &&
+               __double_as_longlong(c[k].a) == __double_as_longlong(c[k - 1].a);
+    };
+    __shared__ int32_t wsum[kQcBlock / 64];
+    __shared__ int32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < n; c0 += kQcBlock) {
+        const int k = c0 + (int)threadIdx.x;
+        const bool start = k < n && !same(k);
+        const uint64_t m = __ballot(start);
+        if (lane == 0) wsum[w] = (int32_t)__popcll(m);
+        __syncthreads();
+        int32_t r = carry;
+        for (int u = 0; u < w; ++u) r += wsum[u];
+        r += (int32_t)lanes_below(m);
+        if (start) {   // the run's weight, its records in order
+            double W = c[k].w;
+            for (int j = k + 1; j < n && same(j); ++j) W += c[j].w;
+            out[r] = Comp<double>{c[k].mu, c[k].a, c[k].c, W};
+        }
+        __syncthreads();   // (carry and wsum read by every thread)
+        if (threadIdx.x == 0) {
+            int32_t t = 0;
+            for (int u = 0; u < kQcBlock / 64; ++u) t += wsum[u];
+            carry += t;
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) qc_n[li] = carry;
 }
 
 // Quantized families, pass 3: per candidate look up its grid value's lpdf
@@ -3589,6 +3646,18 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
     const int nq = nqg + nql;
     evals_q[0] = evals_q[1] = 0;
     if (nq == 0 || a.tiles == 0) return TPE_OK;
+    {   // the above mixtures' runs (k_qtable), once per posterior
+        tpe_rt::Posterior& P = *ctx->P;
+        const int nall = (int)(P.h_group[QUANT_GMM].size() + P.h_group[QUANT_LGMM].size());
+        if (!P.qc_ready && nall > 0) {
+            HIPCHK(ctx, P.qcomp.reserve(P.comps64.cap));
+            HIPCHK(ctx, P.qc_n.reserve(std::max(P.n_labels, 1)));
+            hipLaunchKernelGGL(k_qcompress, dim3((unsigned)nall), dim3(kQcBlock), 0, ctx->stream, P.labels.p,
+                               P.groups.p + P.group_off[QUANT_GMM], P.comps64.p, P.qcomp.p, P.qc_n.p);
+            HIPCHK(ctx, hipGetLastError());
+            P.qc_ready = true;
+        }
+    }
     // bounded labels: the grid window from [low, high] / q before sampling
     // (a margin of one step each side); fused when every label has one
     {
@@ -3645,11 +3714,11 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
                 if (fam)
                     hipLaunchKernelGGL(k_qtable<QUANT_LGMM>, tg, dim3(kBlock), 0, ctx->stream, ctx->P->labels.p,
                                        g.dev[mode], ctx->P->comps64.p, ctx->qinfo.p, nq, qbase, ctx->qtab.p,
-                                       ctx->qkmax.p);
+                                       ctx->qkmax.p, ctx->P->qcomp.p, ctx->P->qc_n.p);
                 else
                     hipLaunchKernelGGL(k_qtable<QUANT_GMM>, tg, dim3(kBlock), 0, ctx->stream, ctx->P->labels.p,
                                        g.dev[mode], ctx->P->comps64.p, ctx->qinfo.p, nq, qbase, ctx->qtab.p,
-                                       ctx->qkmax.p);
+                                       ctx->qkmax.p, ctx->P->qcomp.p, ctx->P->qc_n.p);
                 dim3 sg(a.gx, cnt, a.gz);
 #define TPE_QFUSED(M, RR)                                                                          \
     hipLaunchKernelGGL((k_qfused<M, RR>), sg, dim3(kBlock), 0, ctx->stream, ctx->P->labels.p,         \
@@ -3750,11 +3819,11 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
             if (fam)
                 hipLaunchKernelGGL(k_qtable<QUANT_LGMM>, tg, dim3(kBlock), 0, ctx->stream,
                                    ctx->P->labels.p, g.dev[mode], ctx->P->comps64.p, ctx->qinfo.p, nq,
-                                   qbase, ctx->qtab.p, nullptr);
+                                   qbase, ctx->qtab.p, nullptr, ctx->P->qcomp.p, ctx->P->qc_n.p);
             else
                 hipLaunchKernelGGL(k_qtable<QUANT_GMM>, tg, dim3(kBlock), 0, ctx->stream,
                                    ctx->P->labels.p, g.dev[mode], ctx->P->comps64.p, ctx->qinfo.p, nq,
-                                   qbase, ctx->qtab.p, nullptr);
+                                   qbase, ctx->qtab.p, nullptr, ctx->P->qcomp.p, ctx->P->qc_n.p);
         }
         dim3 sg(a.gx, cnt, a.gz);
 #define TPE_QSCAN(M, RR)                                                                      \
@@ -4219,6 +4288,7 @@ int set_posterior_impl(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_lab
     ctx->P->h_labels = dl;
     ctx->P->win_ready = false;
     ctx->P->zw_ready = false;
+    ctx->P->qc_ready = false;
     ctx->P->bx_ready = false;
     ctx->P->n_labels = n_labels;
     return TPE_OK;
