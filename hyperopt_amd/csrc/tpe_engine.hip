@@ -2333,13 +2333,15 @@ __global__ __launch_bounds__(kBlock) void k_qtable(
 // The quantized labels' above mixtures as runs of equal (mu, a) -- records
 // sorted by mu, the ties of a quantized label's observations adjacent (the
 // run's interior shares the clipped minimum sigma): each run becomes one
-// record whose weight is the run's weights summed in order, so k_qtable sums
-// ~(distinct values x 3) erf pairs per grid value instead of one per
-// observation (config 5: 50k -> a few hundred).  prob = sum_k w_k (Phi_u -
-// Phi_l) regrouped as sum_runs (sum w) (Phi_u - Phi_l): the quantized lpdf
-// bar (relative 1e-9, absolute 1e-13 on the probability; the run sums and
-// the reference's own term-by-term sum both round at ~1e-16 x the total).
-// One workgroup per quantized label position.
+// record carrying the run's total weight, so k_qtable sums ~(distinct values
+// x 3) erf pairs per grid value instead of one per observation (config 5:
+// 50k -> a few hundred).  prob = sum_k w_k (Phi_u - Phi_l) regrouped as
+// sum_runs W_run (Phi_u - Phi_l), W_run a difference of the label's weight
+// prefix sums (~1e-16 of the total weight each): inside the quantized lpdf
+// bar (relative 1e-9, absolute 1e-13 on the probability).  One workgroup per
+// quantized label position, chunks of 1024 records: the run starts and the
+// prefix by block scans; a start stores the prefix before it, the run's end
+// (after a barrier) the difference.
 constexpr int kQcBlock = 1024;
 __global__ __launch_bounds__(kQcBlock) void k_qcompress(const DLabel* __restrict__ labels,
                                                         const int32_t* __restrict__ group,
@@ -2351,37 +2353,60 @@ __global__ __launch_bounds__(kQcBlock) void k_qcompress(const DLabel* __restrict
     const Comp<double>* c = comps64 + L.comp_a;
     Comp<double>* out = qcomp + L.comp_a;
     const int n = L.na, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    auto same = [&](int k) {   // record k continues the run of k - 1 (bit-equal mu and a)
-        return k > 0 && __double_as_longlong(c[k].mu) == __double_as_longlong(c[k - 1].mu) &&
-               __double_as_longlong(c[k].a) == __double_as_longlong(c[k - 1].a);
+    auto starts = [&](int k) {   // record k opens a run (bit-unequal mu or a to record k - 1)
+        return k == 0 || __double_as_longlong(c[k].mu) != __double_as_longlong(c[k - 1].mu) ||
+               __double_as_longlong(c[k].a) != __double_as_longlong(c[k - 1].a);
     };
-    __shared__ int32_t wsum[kQcBlock / 64];
-    __shared__ int32_t carry;
-    if (threadIdx.x == 0) carry = 0;
+    __shared__ int32_t wcnt[kQcBlock / 64];
+    __shared__ double wsum[kQcBlock / 64];
+    __shared__ int32_t runs;
+    __shared__ double pre;
+    if (threadIdx.x == 0) {
+        runs = 0;
+        pre = 0.0;
+    }
     __syncthreads();
     for (int c0 = 0; c0 < n; c0 += kQcBlock) {
         const int k = c0 + (int)threadIdx.x;
-        const bool start = k < n && !same(k);
-        const uint64_t m = __ballot(start);
-        if (lane == 0) wsum[w] = (int32_t)__popcll(m);
-        __syncthreads();
-        int32_t r = carry;
-        for (int u = 0; u < w; ++u) r += wsum[u];
-        r += (int32_t)lanes_below(m);
-        if (start) {   // the run's weight, its records in order
-            double W = c[k].w;
-            for (int j = k + 1; j < n && same(j); ++j) W += c[j].w;
-            out[r] = Comp<double>{c[k].mu, c[k].a, c[k].c, W};
+        const bool in = k < n;
+        const bool st = in && starts(k);
+        const bool en = in && (k == n - 1 || starts(k + 1));
+        const double wk = in ? c[k].w : 0.0;
+        // inclusive scans over the wave: weights and starts
+        double x = wk;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const double y = __shfl_up(x, off);
+            if (lane >= off) x += y;
         }
-        __syncthreads();   // (carry and wsum read by every thread)
-        if (threadIdx.x == 0) {
-            int32_t t = 0;
-            for (int u = 0; u < kQcBlock / 64; ++u) t += wsum[u];
-            carry += t;
+        const uint64_t m = __ballot(st);
+        if (lane == 63) wsum[w] = x;
+        if (lane == 0) wcnt[w] = (int32_t)__popcll(m);
+        __syncthreads();
+        double e = pre;   // the weight before record k
+        int32_t r = runs;
+        for (int u = 0; u < w; ++u) {
+            e += wsum[u];
+            r += wcnt[u];
+        }
+        e += x - wk;
+        r += (int32_t)lanes_below(m) + (st ? 0 : -1);   // the run holding record k
+        if (st) out[r] = Comp<double>{c[k].mu, c[k].a, c[k].c, e};
+        __syncthreads();   // every start of this chunk written (and the shared sums read)
+        if (en) out[r].w = (e + wk) - out[r].w;
+        if (threadIdx.x == kQcBlock - 1) {   // the chunk's totals onward
+            double t = pre;
+            int32_t q = runs;
+            for (int u = 0; u < kQcBlock / 64; ++u) {
+                t += wsum[u];
+                q += wcnt[u];
+            }
+            pre = t;
+            runs = q;
         }
         __syncthreads();
     }
-    if (threadIdx.x == 0) qc_n[li] = carry;
+    if (threadIdx.x == 0) qc_n[li] = runs;
 }
 
 // Quantized families, pass 3: per candidate look up its grid value's lpdf
