@@ -480,3 +480,37 @@ def test_chunked_packed_map(monkeypatch, prec, C, n_rounds):
         assert int(r[rnd, li]['index']) == best, (name, rnd)
         assert r[rnd, li]['value'] == cand[best]
         np.testing.assert_allclose(r[rnd, li]['lpdf_above'], la[best], rtol=1e-9, atol=1e-9)
+
+
+def test_quantized_tables_over_runs_match_oracle(eng):
+    """The quantized tables sum the above mixture's runs of equal (mu,
+    sigma) (k_qcompress): at 20k trials a quniform(0, 100, q=1) label's above
+    mixture holds ~15k records on 101 values.  The round's quantized winners
+    (fused table path, 2^13 candidates) are the oracle's argmax over the
+    same re-drawn candidates and their lpdfs the oracle's within the
+    quantized bar (tpe.py:110-172 at the reference's term-by-term sum)."""
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.workloads import mixed_history
+    hist = mixed_history(10, 20000, seed=5)
+    posts = hist.posteriors()
+    eng.set_posterior(*P.pack(posts))
+    C, seed, rnd = 1 << 13, 21, 4
+    res = eng.suggest(seed, C, round=rnd)
+    checked = 0
+    for li, post in enumerate(posts):
+        if post.q is None or post.family != 'GMM1':
+            continue
+        kw = dict(low=post.low, high=post.high, q=post.q)
+        wb, mb, sb = post.below
+        wa, ma, sa = post.above
+        cand = eng.GMM1(wb, mb, sb, seed=seed, size=(C,), stream=li, round=rnd, **kw)
+        vals, inv = np.unique(cand, return_inverse=True)      # (<= 101 grid values: the oracle on those)
+        lb = O.gmm1_lpdf(vals, wb, mb, sb, **kw)[inv]
+        la = O.gmm1_lpdf(vals, wa, ma, sa, **kw)[inv]
+        best = O.broadcast_best_index(lb, la)
+        assert res[li]['value'] == cand[best], li
+        assert_lpdf_close([res[li]['lpdf_below']], [lb[best]], quantized=True)
+        assert_lpdf_close([res[li]['lpdf_above']], [la[best]], quantized=True)
+        assert len(np.unique(ma)) < len(ma) / 50          # (heavy ties: the runs are long)
+        checked += 1
+    assert checked == 2
