@@ -1524,7 +1524,22 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
         const int rc = tpe_rt::bx_keep_check(ctx);
         if (rc) return rc;
     }
+    // beside the index: the quantized labels' runs for the coming round
+    // (k_qcompress) go on the aux stream too, under the same sync -- over the
+    // previous build's label groups, which a subset rebuild of the same
+    // history keeps (checked)
+    bool qc_queued = false;
+    if (beside && P.groups.p) {
+        std::vector<int32_t> cat_now;
+        for (int m = 0; m < kNumModes; ++m) cat_now.insert(cat_now.end(), grp[m].begin(), grp[m].end());
+        if (cat_now == P.groups_h) {
+            const int rc = tpe_rt::qc_launch(ctx, st);
+            if (rc) return rc;
+            qc_queued = true;
+        }
+    }
     HIPCHK(ctx, hipStreamSynchronize(st));
+    P.qc_ready = false;   // (set again below when the build succeeds)
     const int32_t errh = ctx->pin[0].err;
     std::memcpy(dl.data(), ctx->dl_h.data(), n_labels * sizeof(DLabel));
     if (ties_out) std::memcpy(ties_out, ctx->ties_h.data(), (n_labels + 1) * sizeof(int32_t));
@@ -1549,7 +1564,7 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     P.h_labels = dl;
     P.win_ready = false;
     P.zw_ready = false;
-    P.qc_ready = false;
+    P.qc_ready = qc_queued;
     // the index is kept when every dense label came out bit-identical (e.g.
     // a second build of the same history that only supplies the tie order
     // of quantized labels)

@@ -549,6 +549,11 @@ int bx_build(tpe_ctx* ctx);
 // sync); bx_keep_after: whether the index stays valid.
 int bx_keep_check(tpe_ctx* ctx);
 bool bx_keep_after(tpe_ctx* ctx, bool groups_changed);
+// The quantized labels' above mixtures as runs (k_qcompress, tpe_engine.hip)
+// queued on `st`; sets P->qc_ready.  The round queues it on its own stream
+// when not ready; the subset rebuild beside the expansion index queues it on
+// the aux stream, off the round's path.
+int qc_launch(tpe_ctx* ctx, hipStream_t st);
 }  // namespace tpe_rt
 
 // per-device implementations of the entry points a multi-device context

@@ -3671,17 +3671,9 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
     const int nq = nqg + nql;
     evals_q[0] = evals_q[1] = 0;
     if (nq == 0 || a.tiles == 0) return TPE_OK;
-    {   // the above mixtures' runs (k_qtable), once per posterior
-        tpe_rt::Posterior& P = *ctx->P;
-        const int nall = (int)(P.h_group[QUANT_GMM].size() + P.h_group[QUANT_LGMM].size());
-        if (!P.qc_ready && nall > 0) {
-            HIPCHK(ctx, P.qcomp.reserve(P.comps64.cap));
-            HIPCHK(ctx, P.qc_n.reserve(std::max(P.n_labels, 1)));
-            hipLaunchKernelGGL(k_qcompress, dim3((unsigned)nall), dim3(kQcBlock), 0, ctx->stream, P.labels.p,
-                               P.groups.p + P.group_off[QUANT_GMM], P.comps64.p, P.qcomp.p, P.qc_n.p);
-            HIPCHK(ctx, hipGetLastError());
-            P.qc_ready = true;
-        }
+    if (!ctx->P->qc_ready) {   // the above mixtures' runs (k_qtable), once per posterior
+        const int rc = tpe_rt::qc_launch(ctx, ctx->stream);
+        if (rc) return rc;
     }
     // bounded labels: the grid window from [low, high] / q before sampling
     // (a margin of one step each side); fused when every label has one
@@ -4327,6 +4319,20 @@ double tpe_rt::np_pairwise_sum(const double* a, size_t n) {
     double r = 0.0;
     for (size_t c = 0; c < n; c += 8192) r += np_pairwise_sum_impl(a + c, std::min<size_t>(8192, n - c));
     return r;
+}
+
+int tpe_rt::qc_launch(tpe_ctx* ctx, hipStream_t st) {
+    tpe_rt::Posterior& P = *ctx->P;
+    const int nall = (int)(P.h_group[QUANT_GMM].size() + P.h_group[QUANT_LGMM].size());
+    if (nall > 0) {
+        HIPCHK(ctx, P.qcomp.reserve(P.comps64.cap));
+        HIPCHK(ctx, P.qc_n.reserve(std::max(P.n_labels, 1)));
+        hipLaunchKernelGGL(k_qcompress, dim3((unsigned)nall), dim3(kQcBlock), 0, st, P.labels.p,
+                           P.groups.p + P.group_off[QUANT_GMM], P.comps64.p, P.qcomp.p, P.qc_n.p);
+        HIPCHK(ctx, hipGetLastError());
+    }
+    P.qc_ready = true;
+    return TPE_OK;
 }
 
 // ================================================================ C ABI ====
