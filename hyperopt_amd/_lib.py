@@ -137,6 +137,7 @@ SIGNATURES = {
     'tpe_last_drawn': (ctypes.c_int, [_P, _P, _P]),
     'tpe_device_bytes': (ctypes.c_int64, []),
     'tpe_prepare': (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int32]),
+    'tpe_arm_prepare': (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int32]),
     'tpe_last_screen_mode': (ctypes.c_int32, [_P]),
     'tpe_last_hot': (ctypes.c_int, [_P, _P, _P]),
     'tpe_last_prepare': (ctypes.c_int, [_P, _P]),

@@ -1355,6 +1355,10 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     auto& B = ctx->build;
     if (!B.hist_ready) return ctx->fail(TPE_ERR_ARG, "no resident history (tpe_history_reset)");
     const bool subset = only_h != nullptr && n_only > 0;
+    // an armed tpe_prepare (tpe_arm_prepare): consumed by a full build
+    const int64_t arm_c = subset ? 0 : ctx->arm_c;
+    const int32_t arm_r = subset ? 0 : ctx->arm_r;
+    if (!subset) ctx->arm_c = ctx->arm_r = 0;
     if (subset) {
         if (below_h)
             return ctx->fail(TPE_ERR_ARG, "a label-subset rebuild keeps the previous build's below set");
@@ -1581,6 +1585,8 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     B.built_lf = lf;
     if (!subset) B.built_loss_hash = loss_fingerprint(losses, n_trials);
     if (n_below_out) *n_below_out = n_below;
+    // the armed index, queued now: no caller round trip before it starts
+    if (arm_c > 0) return tpe1_prepare(ctx, arm_c, arm_r);
     return TPE_OK;
 }
 

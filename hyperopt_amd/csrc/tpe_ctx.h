@@ -425,6 +425,8 @@ struct tpe_ctx {
     bool prep_pending = false;
     uint64_t hot_tau0_gen = 0;           // hot_tau0 holds tau0 of this table generation
     int64_t hot_tau0_n = 0;              //   and this n
+    int64_t arm_c = 0;                   // tpe_arm_prepare: the next full build queues the index for
+    int32_t arm_r = 0;                   //   rounds of arm_c candidates x arm_r (0: disarmed)
     DevBuf<int32_t> scr_idx;
     DevBuf<unsigned long long> scr_lb;
     DevBuf<int32_t> scr_cnt;
@@ -570,6 +572,7 @@ TPE_DEV int tpe1_suggest_batch(tpe_ctx* ctx, uint64_t seed, const uint32_t* roun
                                tpe_label_result* out);
 TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value);
 TPE_DEV int tpe1_prepare(tpe_ctx* ctx, int64_t n_candidates, int32_t n_rounds);
+TPE_DEV int tpe1_arm_prepare(tpe_ctx* ctx, int64_t n_candidates, int32_t n_rounds);
 TPE_DEV int tpe1_history_reset(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
                                const double* cat_p, int64_t n_cat_p);
 TPE_DEV int tpe1_history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial,

@@ -4754,6 +4754,15 @@ TPE_DEV int tpe1_prepare(tpe_ctx* ctx, int64_t n_candidates, int32_t n_rounds) {
     return rc;
 }
 
+TPE_DEV int tpe1_arm_prepare(tpe_ctx* ctx, int64_t n_candidates, int32_t n_rounds) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (n_candidates < 0 || (n_candidates > 0 && n_rounds < 1))
+        return ctx->fail(TPE_ERR_ARG, "bad candidate/round count");
+    ctx->arm_c = n_candidates;
+    ctx->arm_r = n_candidates > 0 ? n_rounds : 0;
+    return TPE_OK;
+}
+
 TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
     if (!ctx) return TPE_ERR_ARG;
     switch (option) {

@@ -349,6 +349,11 @@ int tpe_prepare(tpe_ctx* ctx, int64_t n_candidates, int32_t n_rounds) {
     return for_all(ctx, [&](tpe_ctx* x, int) { return tpe1_prepare(x, n_candidates, n_rounds); });
 }
 
+int tpe_arm_prepare(tpe_ctx* ctx, int64_t n_candidates, int32_t n_rounds) {
+    if (!ctx) return TPE_ERR_ARG;
+    return for_all(ctx, [&](tpe_ctx* x, int) { return tpe1_arm_prepare(x, n_candidates, n_rounds); });
+}
+
 int tpe_history_reset(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
                       const double* cat_p, int64_t n_cat_p) {
     if (!ctx) return TPE_ERR_ARG;

@@ -268,6 +268,11 @@ class Engine(object):
         (tpe_prepare; the first round(s) of n_candidates would build it)."""
         self._check(self.lib.tpe_prepare(self.h, int(n_candidates), int(n_rounds)))
 
+    def arm_prepare(self, n_candidates, n_rounds=1):
+        """Have the next device build of the resident history queue the
+        expansion index itself, before it returns (tpe_arm_prepare)."""
+        self._check(self.lib.tpe_arm_prepare(self.h, int(n_candidates), int(n_rounds)))
+
     def last_build_ms(self):
         ms = ctypes.c_float()
         self._check(self.lib.tpe_last_build_ms(self.h, ctypes.byref(ms)))

@@ -461,6 +461,9 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
             # the previous build's order-dependent labels: their argsorts
             # start now, on the host, under the first build and the index
             early = _order_thread().submit(reference_orders, losses, n_below, obs_of, known)
+        # the build queues the index itself before it returns (tpe_arm_prepare);
+        # the prepare after it is then a no-op
+        eng.arm_prepare(*prepare)
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf)
         t0 = _phase('build', t0)
         eng.prepare(*prepare)
@@ -469,6 +472,8 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
     elif known:
         below, off, order = reference_orders(losses, n_below, obs_of, known)
         t0 = _phase('argsorts', t0)
+        if prepare:
+            eng.arm_prepare(*prepare)
         nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf, below, off, order)
         t0 = _phase('build', t0)
         if prepare:

@@ -531,6 +531,16 @@ int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
  * No reference counterpart: the reference has no index. */
 int tpe_prepare(tpe_ctx *ctx, int64_t n_candidates, int32_t n_rounds);
 
+/* Arm tpe_prepare(n_candidates, n_rounds) for the next device build of the
+ * resident history (tpe_build_posterior_resident[_ordered], not a
+ * label-subset rebuild): that build queues the index itself, right after its
+ * own sync and before it returns -- tpe_prepare's work without the caller's
+ * round trip between the two calls.  Every such build consumes the arm,
+ * whether or not it queued anything (and a failed build queues nothing);
+ * n_candidates = 0 disarms.  A tpe_prepare after it is a no-op.  No
+ * reference counterpart (tpe.suggest's fresh posterior every step). */
+int tpe_arm_prepare(tpe_ctx *ctx, int64_t n_candidates, int32_t n_rounds);
+
 #ifdef __cplusplus
 }
 #endif

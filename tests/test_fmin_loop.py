@@ -87,3 +87,37 @@ def test_deferred_quantized_round_equals_sequential(C, n_rounds, labels):
         P.EARLY_ORDERS = early
         a.close()
         b.close()
+
+
+def test_armed_prepare_is_queued_by_the_build():
+    """tpe_arm_prepare (what FminLoop / tpe.suggest do before a build that a
+    large round follows): the build itself queues the expansion index
+    before it returns, the round on it equals a fresh engine's bytewise, and
+    the arm is consumed -- the next build queues nothing."""
+    from hyperopt_amd.engine import Engine
+    from hyperopt_amd.workloads import FminLoop, mixed_history
+    hist = mixed_history(8, 3000 + 3, seed=1)
+    C = 1 << 16
+    eng = Engine(0, 'f64')
+    eng.set_option('timing', 1)
+    loop = FminLoop(hist)
+    loop.advance(eng, 3000)
+    eng.last_prepare_ms()
+    eng.arm_prepare(C)
+    loop.advance(eng, 3001)           # the caller asks for no index: the armed build queues it
+    ms = eng.last_prepare_ms()
+    assert ms > 0
+    got = eng.suggest(seed=3, n_candidates=C, round=0)
+    ref = Engine(0, 'f64')
+    FminLoop(hist).advance(ref, 3001)
+    want = ref.suggest(seed=3, n_candidates=C, round=0)
+    ref.close()
+    assert np.ascontiguousarray(got).view(np.uint8).tobytes() == \
+        np.ascontiguousarray(want).view(np.uint8).tobytes()
+    loop.advance(eng, 3002)           # consumed: this build queues no index
+    assert eng.last_prepare_ms() == ms
+    eng.arm_prepare(C)
+    eng.arm_prepare(0)                # disarmed
+    loop.advance(eng, 3003)
+    assert eng.last_prepare_ms() == ms
+    eng.close()
