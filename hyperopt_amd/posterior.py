@@ -424,7 +424,7 @@ def _run_deferred(eng, round_call, reference, rebuild, quant, t0):
 
 
 def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of, known=(), prepare=None,
-                          overlap=True, round_call=None, quant=frozenset()):
+                          overlap=True, round_call=None, quant=frozenset(), early=None):
     """Device build whose mixtures follow the reference's tie order
     (tpe.py:433, 637): the device reports which mixtures depend on the order
     of tied observations (or a tie of losses at the split), and only for
@@ -451,13 +451,16 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
     other labels runs while the host computes those orders (_run_deferred):
     the argsorts leave the step's critical path.
 
+    early (optional): reference_orders(losses, n_below, obs_of, known)
+    already running (a future: DeviceHistoryUploader.build starts it before
+    its upload).
+
     Returns (n_below, the labels that needed an order[, results])."""
     n_below = n_below_of(n_valid, gamma)
     known = set(known)
     t0 = time.perf_counter()
-    early = None
     if prepare and (overlap or not known):
-        if known and EARLY_ORDERS:
+        if known and EARLY_ORDERS and early is None:
             # the previous build's order-dependent labels: their argsorts
             # start now, on the host, under the first build and the index
             early = _order_thread().submit(reference_orders, losses, n_below, obs_of, known)
@@ -635,13 +638,21 @@ class DeviceHistoryUploader(object):
             pos = np.searchsorted(tids, ni)
             pc = np.minimum(pos, len(tids) - 1)
             trial = np.where(tids[pc] == ni, pc, -1).astype(np.int32)
-            eng.history_append(np.asarray(n_new, dtype=np.int64), trial, vals)
             o = 0
             for i, m in enumerate(n_new):
                 if m:
                     self.pos_parts[i].append(trial[o:o + m])
                     self.val_parts[i].append(vals[o:o + m])
                     o += m
+        # the previous step's order-dependent labels: their argsorts start
+        # now, under the upload as well as the first build and the index
+        # (a failed upload leaves this uploader invalid: the next call resets)
+        early = None
+        if prepare and overlap and self.tie_labels and EARLY_ORDERS:
+            early = _order_thread().submit(reference_orders, losses, n_below_of(n_valid, gamma),
+                                           self._obs_of(len(labels)), self.tie_labels)
+        if ni_l:
+            eng.history_append(np.asarray(n_new, dtype=np.int64), trial, vals)
         self.prev_counts = counts                  # committed only after the append
         self.key = (key[0], eng.history_generation)
         self.owner = weakref.ref(owner)
@@ -651,7 +662,7 @@ class DeviceHistoryUploader(object):
         out = build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf,
                                     self._obs_of(len(labels)), self.tie_labels,
                                     prepare=prepare, overlap=overlap, round_call=round_call,
-                                    quant=self.quant)
+                                    quant=self.quant, early=early)
         self.tie_labels = out[1]
         return (out[0], out[2]) if round_call is not None else out[0]
 
