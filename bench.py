@@ -135,6 +135,9 @@ def parse():
     ap.add_argument('--defer', type=int, default=None,
                     help='1/0: the dense labels\' round under the tie-order argsorts '
                          '(posterior.DEFER_QUANT; default: the library\'s)')
+    ap.add_argument('--early-upload', type=int, default=None,
+                    help='1/0: the early argsorts start before the history upload, or after it '
+                         '(posterior.EARLY_BEFORE_UPLOAD)')
     ap.add_argument('--early-orders', type=int, default=None,
                     help='1/0: the known labels\' argsorts under the first build '
                          '(posterior.EARLY_ORDERS)')
@@ -360,6 +363,8 @@ def main():
         P.SORT_THREADS = args.sort_threads
     if args.early_orders is not None:
         P.EARLY_ORDERS = bool(args.early_orders)
+    if args.early_upload is not None:
+        P.EARLY_BEFORE_UPLOAD = bool(args.early_upload)
     if args.overlap_min_dense is not None:
         from hyperopt_amd import workloads as W
         W.OVERLAP_MIN_DENSE = args.overlap_min_dense

@@ -329,6 +329,7 @@ def reference_orders(losses, n_below, obs_of, labels):
 
 
 EARLY_ORDERS = True   # known labels' argsorts started before the first build (build_reference_order)
+EARLY_BEFORE_UPLOAD = False  # ... or before the history upload (DeviceHistoryUploader.build): no gain, r4ay
 _order_exec = None
 
 
@@ -648,7 +649,7 @@ class DeviceHistoryUploader(object):
         # now, under the upload as well as the first build and the index
         # (a failed upload leaves this uploader invalid: the next call resets)
         early = None
-        if prepare and overlap and self.tie_labels and EARLY_ORDERS:
+        if prepare and overlap and self.tie_labels and EARLY_ORDERS and EARLY_BEFORE_UPLOAD:
             early = _order_thread().submit(reference_orders, losses, n_below_of(n_valid, gamma),
                                            self._obs_of(len(labels)), self.tie_labels)
         if ni_l:
