@@ -4019,11 +4019,25 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
             }
         launch_round<double, CAT, true>(ctx, g, a);
     } else if (sample) {
+        // the categorical labels (few short kernels) on the second stream,
+        // beside the quantized labels and the dense draw: their own partial
+        // rows, early-exit slots and draw counter; forked after the round's
+        // resets, joined before the reduction
+        const bool cat_aux = ctx->cat_aux && ctx->aux && g.count[CAT] > 0 && a.tiles > 0;
+        if (cat_aux) {
+            HIPCHK(ctx, hipEventRecord(ctx->ev_cat[0], ctx->stream));
+            HIPCHK(ctx, hipStreamWaitEvent(ctx->aux, ctx->ev_cat[0], 0));
+            std::swap(ctx->stream, ctx->aux);
+            launch_round<double, CAT, true>(ctx, g, a);
+            std::swap(ctx->stream, ctx->aux);
+            HIPCHK(ctx, hipEventRecord(ctx->ev_cat[1], ctx->aux));
+        }
         int rc = launch_quantized(ctx, g, a, evals_q);
+        if (rc == TPE_OK)
+            rc = ctx->precision == TPE_F32 ? launch_dense<float>(ctx, g, a) : launch_dense<double>(ctx, g, a);
+        if (cat_aux) HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_cat[1], 0));
         if (rc) return rc;
-        rc = ctx->precision == TPE_F32 ? launch_dense<float>(ctx, g, a) : launch_dense<double>(ctx, g, a);
-        if (rc) return rc;
-        launch_round<double, CAT, true>(ctx, g, a);
+        if (!cat_aux) launch_round<double, CAT, true>(ctx, g, a);
     } else {
         launch_round<double, QUANT_GMM, false>(ctx, g, a);
         launch_round<double, QUANT_LGMM, false>(ctx, g, a);
@@ -4409,7 +4423,9 @@ int tpe_ctx_create(int device, int precision, tpe_ctx** out) {
     ok = ok && hipEventCreate(&c->evs[0]) == hipSuccess && hipEventCreate(&c->evs[1]) == hipSuccess;
     ok = ok && hipEventCreate(&c->ev_prep[0]) == hipSuccess && hipEventCreate(&c->ev_prep[1]) == hipSuccess;
     ok = ok && hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess &&
-         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess;
+         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&c->ev_cat[0], hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&c->ev_cat[1], hipEventDisableTiming) == hipSuccess;
     for (int j = 0; j < 2; ++j)
         ok = ok && hipEventCreateWithFlags(&c->ev_sorted[j], hipEventDisableTiming) == hipSuccess &&
              hipEventCreateWithFlags(&c->ev_done[j], hipEventDisableTiming) == hipSuccess;
@@ -4484,6 +4500,8 @@ TPE_DEV void tpe1_ctx_destroy(tpe_ctx* c) {
     c->win_lohi.release();
     for (hipEvent_t e : c->evw) (void)hipEventDestroy(e);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    for (hipEvent_t e : c->ev_cat)
+        if (e) (void)hipEventDestroy(e);
     if (c->aux) (void)hipStreamDestroy(c->aux);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -4783,6 +4801,7 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
             if (value < 1 || value > 31) return ctx->fail(TPE_ERR_ARG, "family mask must be in [1, 31]");
             ctx->mode_mask = (int32_t)value;
             break;
+        case TPE_OPT_CAT_AUX: ctx->cat_aux = value != 0; break;
         case TPE_OPT_RESCORE_CAP:
             if (value < 1) return ctx->fail(TPE_ERR_ARG, "re-score capacity must be positive");
             ctx->pk_cap = value;
