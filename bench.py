@@ -135,9 +135,9 @@ def parse():
     ap.add_argument('--defer', type=int, default=None,
                     help='1/0: the dense labels\' round under the tie-order argsorts '
                          '(posterior.DEFER_QUANT; default: the library\'s)')
-    ap.add_argument('--cat-aux', type=int, default=None,
-                    help='1/0: the categorical labels on the second stream during sampled rounds '
-                         '(TPE_OPT_CAT_AUX, default on)')
+    ap.add_argument('--aux-families', type=int, default=None,
+                    help='1/0: the quantized and categorical labels on the second stream during sampled rounds '
+                         '(TPE_OPT_AUX_FAMILIES, default off)')
     ap.add_argument('--early-upload', type=int, default=None,
                     help='1/0: the early argsorts start before the history upload, or after it '
                          '(posterior.EARLY_BEFORE_UPLOAD)')
@@ -534,8 +534,8 @@ def main():
     value_only = (args.value_only if args.value_only is not None
                   else int(not (dist is not None and not by_label and args.config != 5)))
     eng.set_option('value_only', value_only)
-    if args.cat_aux is not None:
-        eng.set_option('cat_aux', args.cat_aux)
+    if args.aux_families is not None:
+        eng.set_option('aux_families', args.aux_families)
     eng.set_option('window', int(not args.no_window))
     eng.set_option('win_t', args.win_t)
     eng.set_option('win_groups', args.win_groups)

@@ -54,7 +54,7 @@ TPE_OPT_ZERO_WIN = 15
 TPE_OPT_VALUE_ONLY = 16
 TPE_OPT_RESCORE_CAP = 17
 TPE_OPT_MODE_MASK = 18
-TPE_OPT_CAT_AUX = 19
+TPE_OPT_AUX_FAMILIES = 19
 
 TPE_OBS_IDENTITY = 0
 TPE_OBS_LOG = 1

@@ -459,8 +459,8 @@ struct tpe_ctx {
     DevBuf<uint8_t> win_tmp[2];
     hipStream_t aux = nullptr;           // key + sort of the next label group
     hipEvent_t ev_fork = nullptr, ev_sorted[2] = {}, ev_done[2] = {};
-    hipEvent_t ev_cat[2] = {};           // the categorical labels' round on aux: fork, join
-    bool cat_aux = true;                 // TPE_OPT_CAT_AUX
+    hipEvent_t ev_cat[2] = {};           // the quantized + categorical labels' round on aux: fork, join
+    bool aux_families = false;                 // TPE_OPT_AUX_FAMILIES
     std::vector<hipEvent_t> evw;         // per unit: k_screen_win brackets (timing)
     int32_t evw_used = 0;
     DevBuf<unsigned long long> win_evals;   // (candidate, component) terms the screen summed

@@ -4019,25 +4019,31 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
             }
         launch_round<double, CAT, true>(ctx, g, a);
     } else if (sample) {
-        // the categorical labels (few short kernels) on the second stream,
-        // beside the quantized labels and the dense draw: their own partial
-        // rows, early-exit slots and draw counter; forked after the round's
-        // resets, joined before the reduction
-        const bool cat_aux = ctx->cat_aux && ctx->aux && g.count[CAT] > 0 && a.tiles > 0;
-        if (cat_aux) {
+        // the quantized and categorical labels (short kernels) on the second
+        // stream, beside the dense draw: their own partial rows, early-exit
+        // slots, tables and draw counters; forked after the round's resets,
+        // joined before the reduction.  (A multi-device shard's quantized
+        // window exchange stays on the main stream.)
+        const bool side = ctx->aux_families && ctx->aux && !ctx->qx && a.tiles > 0 &&
+                          g.count[CAT] + g.count[QUANT_GMM] + g.count[QUANT_LGMM] > 0;
+        int rc = TPE_OK;
+        if (side) {
             HIPCHK(ctx, hipEventRecord(ctx->ev_cat[0], ctx->stream));
             HIPCHK(ctx, hipStreamWaitEvent(ctx->aux, ctx->ev_cat[0], 0));
+            std::swap(ctx->stream, ctx->aux);   // (every launch below on the second stream)
+            rc = launch_quantized(ctx, g, a, evals_q);
+            if (rc == TPE_OK) launch_round<double, CAT, true>(ctx, g, a);
             std::swap(ctx->stream, ctx->aux);
-            launch_round<double, CAT, true>(ctx, g, a);
-            std::swap(ctx->stream, ctx->aux);
-            HIPCHK(ctx, hipEventRecord(ctx->ev_cat[1], ctx->aux));
+            const hipError_t e = hipEventRecord(ctx->ev_cat[1], ctx->aux);
+            if (rc == TPE_OK && e != hipSuccess) rc = ctx->hip(e, "second-stream join");
+        } else {
+            rc = launch_quantized(ctx, g, a, evals_q);
         }
-        int rc = launch_quantized(ctx, g, a, evals_q);
         if (rc == TPE_OK)
             rc = ctx->precision == TPE_F32 ? launch_dense<float>(ctx, g, a) : launch_dense<double>(ctx, g, a);
-        if (cat_aux) HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_cat[1], 0));
+        if (side) HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_cat[1], 0));
         if (rc) return rc;
-        if (!cat_aux) launch_round<double, CAT, true>(ctx, g, a);
+        if (!side) launch_round<double, CAT, true>(ctx, g, a);
     } else {
         launch_round<double, QUANT_GMM, false>(ctx, g, a);
         launch_round<double, QUANT_LGMM, false>(ctx, g, a);
@@ -4801,7 +4807,7 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
             if (value < 1 || value > 31) return ctx->fail(TPE_ERR_ARG, "family mask must be in [1, 31]");
             ctx->mode_mask = (int32_t)value;
             break;
-        case TPE_OPT_CAT_AUX: ctx->cat_aux = value != 0; break;
+        case TPE_OPT_AUX_FAMILIES: ctx->aux_families = value != 0; break;
         case TPE_OPT_RESCORE_CAP:
             if (value < 1) return ctx->fail(TPE_ERR_ARG, "re-score capacity must be positive");
             ctx->pk_cap = value;

@@ -486,9 +486,12 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *                   caller run the dense labels while the host still
  *                   computes the quantized labels' tie orders, then those
  *                   after their rebuild (posterior.py)                 [31]
- *   TPE_OPT_CAT_AUX  sampled rounds run the categorical labels on the
- *                   context's second stream, beside the quantized and dense
- *                   labels (joined before the reduction)                 [1]
+ *   TPE_OPT_AUX_FAMILIES  sampled rounds run the quantized and categorical
+ *                   labels on the context's second stream, beside the dense
+ *                   labels' draw (joined before the reduction; results
+ *                   unchanged; single-device contexts).  Their early exit's
+ *                   draw counts (tpe_last_drawn, the families' evals) then
+ *                   depend on the interleaving                            [0]
  *   TPE_OPT_WIN_GROUPS  label groups of a windowed round, each sorted on a
  *                   second stream while the previous one is screened
  *                   (0: one group; the chip is busy either way)          [0]
@@ -520,7 +523,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_VALUE_ONLY 16
 #define TPE_OPT_RESCORE_CAP 17
 #define TPE_OPT_MODE_MASK 18
-#define TPE_OPT_CAT_AUX 19
+#define TPE_OPT_AUX_FAMILIES 19
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
 
 /* Build now what the resident posterior's first round(s) of n_candidates
