@@ -137,7 +137,7 @@ def parse():
                          '(posterior.DEFER_QUANT; default: the library\'s)')
     ap.add_argument('--aux-families', type=int, default=None,
                     help='1/0: the quantized and categorical labels on the second stream during sampled rounds '
-                         '(TPE_OPT_AUX_FAMILIES, default off)')
+                         '(TPE_OPT_AUX_FAMILIES; default: on, as tpe.suggest runs them, except candidate shards)')
     ap.add_argument('--early-upload', type=int, default=None,
                     help='1/0: the early argsorts start before the history upload, or after it '
                          '(posterior.EARLY_BEFORE_UPLOAD)')
@@ -534,8 +534,11 @@ def main():
     value_only = (args.value_only if args.value_only is not None
                   else int(not (dist is not None and not by_label and args.config != 5)))
     eng.set_option('value_only', value_only)
-    if args.aux_families is not None:
-        eng.set_option('aux_families', args.aux_families)
+    # the side families on the second stream, as tpe.suggest runs them
+    # (engine.get_engine), except for candidate shards (as value_only)
+    aux_families = (args.aux_families if args.aux_families is not None
+                    else int(not (dist is not None and not by_label and args.config != 5)))
+    eng.set_option('aux_families', aux_families)
     eng.set_option('window', int(not args.no_window))
     eng.set_option('win_t', args.win_t)
     eng.set_option('win_groups', args.win_groups)

@@ -572,5 +572,9 @@ def get_engine(device=0, precision='f64', role='main'):
             # no lpdfs for a batched round the screen alone decided (a
             # multi-device context merges its shards by score: exact there)
             eng.set_option('value_only', 1)
+            # the quantized and categorical labels beside the dense draw on
+            # the second stream (same documents; only their draw-count
+            # statistics depend on the interleaving, and tpe.suggest reads none)
+            eng.set_option('aux_families', 1)
         cache[key] = eng
     return cache[key]
