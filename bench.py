@@ -151,7 +151,62 @@ def parse():
                     help='threads of the tie-order argsort pool (posterior.SORT_THREADS)')
     ap.add_argument('--no-other-configs', action='store_true',
                     help='config 3 at N=1: skip the legs of configs 2, 4 and 5 (child processes)')
+    ap.add_argument('--dry-run', action='store_true',
+                    help='launch and check the N ranks (rendezvous, world size, devices) and print '
+                         'a {"dry_run": ...} line instead of measuring (CPU tests of the launcher)')
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """`--gpus N > 1` without a torchrun environment: start N rank processes
+    of this script under torch.distributed.run (one per GPU, rendezvous on
+    127.0.0.1) and return their exit code.  Runs before this process touches
+    the GPU: torch.cuda.device_count() does not initialise HIP on this image,
+    so the check below is safe, and the ranks are children, not an exec."""
+    import subprocess
+    if args.dist_backend == 'nccl':
+        import torch
+        n_dev = torch.cuda.device_count()
+        if n_dev < args.gpus:
+            sys.stderr.write('bench.py: --gpus %d needs %d GPUs, this node has %d: refusing to run %d '
+                             'ranks on fewer devices (use --dist-backend gloo for a rehearsal on a '
+                             'shared GPU)\n' % (args.gpus, args.gpus, n_dev, args.gpus))
+            return 3
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           '--nproc-per-node', str(args.gpus), '--master-addr', '127.0.0.1',
+           '--master-port', str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault('OMP_NUM_THREADS', '4')
+    return subprocess.call(cmd, env=env, cwd=REPO)
+
+
+def check_world(args, dist, torch):
+    """Every rank: the process group is the N ranks --gpus asked for, and
+    under RCCL each rank has a GPU of its own.  Returns the per-rank device
+    ordinals (all-gathered) or exits non-zero."""
+    world = dist.get_world_size()
+    if world != args.gpus:
+        sys.stderr.write('bench.py: --gpus %d but the process group has %d ranks\n' % (args.gpus, world))
+        sys.exit(3)
+    local_world = int(os.environ.get('LOCAL_WORLD_SIZE', str(world)))
+    n_dev = torch.cuda.device_count()
+    if args.dist_backend == 'nccl' and n_dev < local_world:
+        sys.stderr.write('bench.py: %d ranks on this node but %d GPUs: RCCL needs one GPU per rank\n'
+                         % (local_world, n_dev))
+        sys.exit(3)
+    dev = int(os.environ.get('LOCAL_RANK', '0')) % max(n_dev, 1) if n_dev else -1
+    devs = [None] * world
+    dist.all_gather_object(devs, dev)
+    return devs
 
 
 def other_configs(args):
@@ -345,20 +400,43 @@ def workload_name(args, C):
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit('--gpus must be >= 1')
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1 and not args.devices:
+        sys.exit(launch_ranks(args))   # N rank processes under torch.distributed.run
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != (1 if args.devices else args.gpus):
+        sys.stderr.write('bench.py: WORLD_SIZE=%d but --gpus %d%s\n' % (
+            world, args.gpus, ' (--devices runs one process)' if args.devices else ''))
+        sys.exit(3)
     others = None
     if (world == 1 and args.config == 3 and not args.devices and not args.no_other_configs
-            and args.precision == 'f64' and args.labels == 32 and args.cand_log2 == 24):
+            and args.precision == 'f64' and args.labels == 32 and args.cand_log2 == 24
+            and not args.dry_run):
         others = other_configs(args)   # (child processes, before this one touches the GPU)
     import torch
     dist = None
+    rank_devices = [local]
     if world > 1:
         import torch.distributed as dist
-        local = local % max(torch.cuda.device_count(), 1)
-        torch.cuda.set_device(local)
+        if args.dist_backend == 'nccl' or torch.cuda.device_count():
+            local = local % max(torch.cuda.device_count(), 1)
+            if not args.dry_run:
+                torch.cuda.set_device(local)
         dist.init_process_group(args.dist_backend)
+        rank_devices = check_world(args, dist, torch)
+    if args.dry_run:
+        if dist is not None:
+            dist.barrier()
+        if rank == 0:
+            print(json.dumps({'dry_run': True, 'n_gpus': world, 'rccl_world': world if dist else 1,
+                              'dist_backend': args.dist_backend if dist else None,
+                              'rank_devices': rank_devices}), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     from hyperopt_amd import posterior as P
     if args.defer is not None:
         P.DEFER_QUANT = bool(args.defer)
@@ -760,6 +838,8 @@ def main():
         'higher_is_better': True, 'scaling': 'strong', 'vs_baseline': None,
         'dtype': ('f32+f64' if screened else args.precision),
         'data': 'synthetic (prior draws, seed 0)',
+        'rccl_world': world, 'dist_backend': args.dist_backend if dist is not None else None,
+        'rank_devices': rank_devices, 'distinct_gpus': len(set(devs)) if devs else len(set(rank_devices)),
         'value_only': bool(value_only),
         'config': {'workload': workload_name(args, C),
                    'labels': L, 'history': args.trials,

@@ -1,0 +1,66 @@
+#!/bin/bash
+# One gpurun call: the named steps in order, each under its own time limit,
+# output under gpurun_out/<tag>/; the call stops at the first failing step.
+#
+#   bash tools/gpu.sh <tag> <step> [<step> ...]
+#
+# steps:
+#   tests            the whole -m gpu suite (one pytest process)
+#   tests=<expr>     the -m gpu tests matching pytest -k <expr>
+#   smoke            __graft_entry__.smoke()
+#   bench            the default bench.py line (what the driver runs)
+#   bench=<args>     bench.py with extra arguments (commas for spaces)
+#   prof             tools/prof_round.sh <tag> (kernel trace + PMC passes of the default line)
+#   lpdf             PMC passes of the plain fp64 round (tools/prof_lpdf.sh)
+#   shard=<r>        label shard r of config 3 alone: probe + kernel/HIP-API trace
+#   py=<script,args> any python script of the tree (commas for spaces)
+set -u
+T=${1:?tag}
+shift
+OUT=gpurun_out/$T
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+
+run() {   # run <name> <seconds> <command...>
+    local name=$1 secs=$2
+    shift 2
+    echo "== $name: $*"
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    tail -n 4 "$OUT/$name.log"
+    echo "== $name rc=$rc"
+    return $rc
+}
+
+n=0
+for s in "$@"; do
+    n=$((n + 1))
+    case "$s" in
+        tests)
+            run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
+        tests=*)
+            run tests$n 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${s#tests=}" || exit 1 ;;
+        smoke)
+            run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
+        bench)
+            run bench 600 python -u bench.py || exit 1 ;;
+        bench=*)
+            a=${s#bench=}
+            run bench$n 600 python -u bench.py ${a//,/ } || exit 1 ;;
+        prof)
+            bash tools/prof_round.sh "$T" --steps 5 --warmup 2 --no-other-configs --no-agreement || exit 1 ;;
+        lpdf)
+            bash tools/prof_lpdf.sh "$T" || exit 1 ;;
+        shard=*)
+            r=${s#shard=}
+            run shard$r 200 python -u tools/shard_probe.py "$r" 20 || exit 1
+            run shard${r}_trace 240 rocprofv3 --kernel-trace --hip-runtime-trace --memory-copy-trace --stats \
+                -d "$OUT/shard${r}_trace" -o run --output-format csv -- python -u tools/shard_probe.py "$r" 10 || exit 1 ;;
+        py=*)
+            a=${s#py=}
+            run py$n 600 python -u ${a//,/ } || exit 1 ;;
+        *)
+            echo "unknown step $s"; exit 2 ;;
+    esac
+done
+echo "== all steps done"
