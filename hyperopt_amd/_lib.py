@@ -21,6 +21,7 @@ TPE_OK = 0
 TPE_ERR_VALUE = -1
 TPE_ERR_TYPE = -2
 TPE_ERR_ARG = -3
+TPE_STATUS_VALUE_ONLY = 1   # tpe_label_result.status of a value-only cell
 TPE_ERR_HIP = -4
 TPE_ERR_SAMPLE = -5
 

@@ -2774,7 +2774,9 @@ __device__ __forceinline__ tpe_label_result to_result(const Partial& p, int li) 
     r.lpdf_above = p.la;
     r.index = p.idx != INT64_MAX ? p.idx : -1;
     r.label = li;
-    r.status = 0;
+    // a value-only cell (k_pick_rounds: key of 0.0, both lpdfs NaN; a real
+    // NaN score carries the NaN key, the greatest) has no score to merge by
+    r.status = (p.key == order_key(0.0) && p.lb != p.lb && p.la != p.la) ? TPE_STATUS_VALUE_ONLY : 0;
     return r;
 }
 
@@ -4106,7 +4108,13 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
             // miss a winner) or a list overflowed (bit 2): the round runs
             // again with every candidate through the expansion screen (the
             // same draws; its results replace these), and later rounds list
-            // more after an overflow
+            // more after an overflow.  The re-run repeats the WHOLE round --
+            // quantized and categorical families, reduction, copies -- so a
+            // fallback round costs about two rounds, and the families' draw
+            // statistics are the second run's (the same draws, the same
+            // winners); tpe_last_hot reports the fallback (bench:
+            // hot_fallbacks), which no test or bench has seen outside the
+            // forced TPE_OPT_HOT = 2
             if ((hf & 2) && ctx->hot_cap_div > 1.0) ctx->hot_cap_div = std::max(1.0, ctx->hot_cap_div / 4.0);
             const int64_t listed = ctx->hot_listed;
             ctx->hot_redo = true;
@@ -4360,9 +4368,14 @@ namespace {
 // one thread per result: the best of the parts, tpe_merge_results' order
 __global__ __launch_bounds__(kBlock) void k_merge_results(const tpe_label_result* __restrict__ parts,
                                                           int32_t n_parts, int32_t n,
-                                                          tpe_label_result* __restrict__ out) {
+                                                          tpe_label_result* __restrict__ out,
+                                                          int32_t* __restrict__ err) {
     const int32_t j = blockIdx.x * kBlock + threadIdx.x;
     if (j >= n) return;
+    for (int32_t p = 0; p < n_parts; ++p) {
+        const tpe_label_result* c = parts + (size_t)p * n + j;
+        if (c->index >= 0 && c->status == TPE_STATUS_VALUE_ONLY) *err = 1;   // no score to merge by
+    }
     // the winning part's index is tracked and its record copied once (a
     // per-field select of whole records, round 4's first form, came out
     // mixing the value of one part with the rest of another)
@@ -4683,15 +4696,27 @@ int tpe_merge_results_device(tpe_ctx* ctx, const tpe_label_result* d_parts, int3
     if (!ctx || !d_parts || !d_out || n_parts <= 0 || n < 0) return TPE_ERR_ARG;
     HIPCHK(ctx, hipSetDevice(ctx->device));
     if (n == 0) return TPE_OK;
+    HIPCHK(ctx, ctx->errflag.reserve(1));
+    HIPCHK(ctx, ctx->pin.resize(1));
+    ctx->pin[0].err = 0;
+    HIPCHK(ctx, hipMemsetAsync(ctx->errflag.p, 0, sizeof(int32_t), ctx->stream));
     hipLaunchKernelGGL(k_merge_results, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
-                       d_parts, n_parts, n, d_out);
+                       d_parts, n_parts, n, d_out, ctx->errflag.p);
     HIPCHK(ctx, hipGetLastError());
-    return ctx->hip(hipStreamSynchronize(ctx->stream), "device merge");
+    HIPCHK(ctx, hipMemcpyAsync(&ctx->pin[0].err, ctx->errflag.p, sizeof(int32_t), hipMemcpyDeviceToHost,
+                               ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->pin[0].err)
+        return ctx->fail(TPE_ERR_ARG, "tpe_merge_results_device: a part holds a value-only record "
+                                      "(TPE_OPT_VALUE_ONLY): it has no score to merge by");
+    return TPE_OK;
 }
 
 int tpe_merge_results(const tpe_label_result* parts, int32_t n_parts, int32_t n,
                       tpe_label_result* out) {
     if (!parts || !out || n_parts <= 0 || n < 0) return TPE_ERR_ARG;
+    for (int64_t j = 0; j < (int64_t)n_parts * n; ++j)
+        if (parts[j].index >= 0 && parts[j].status == TPE_STATUS_VALUE_ONLY) return TPE_ERR_ARG;
     for (int32_t j = 0; j < n; ++j) {
         tpe_label_result best = parts[j];
         for (int32_t p = 1; p < n_parts; ++p) {

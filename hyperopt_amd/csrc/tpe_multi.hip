@@ -272,8 +272,12 @@ int sharded_round(tpe_ctx* c, uint64_t seed, const uint32_t* rounds, int32_t n_r
         x->shard_id = d;
         tpe_label_result* o = by_cand ? parts.data() + (size_t)d * n_rounds * L
                                       : out + (size_t)sh[d].round_lo * L;
+        // candidate shards merge by score: a value-only cell has none
+        const bool vo = x->value_only;
+        if (by_cand) x->value_only = false;
         int r = tpe1_suggest_batch(x, seed, rounds + sh[d].round_lo, sh[d].n_rounds, sh[d].n_cand,
                                    cand_offset + sh[d].cand_lo, o);
+        x->value_only = vo;
         x->hint_n = 0;
         x->hint_rounds = 0;
         x->qx = nullptr;

@@ -308,11 +308,20 @@ class Engine(object):
         need = len(rounds) * self._labels() * RESULT_DTYPE.itemsize
         if not d_out.is_cuda or d_out.numel() * d_out.element_size() < need or not d_out.is_contiguous():
             raise ValueError('d_out must be a contiguous device tensor of %d bytes' % need)
+        self._check_device(d_out, 'd_out')
         _torch_stream_done(d_out)
         self._check(self.lib.tpe_suggest_batch_device(
             self.h, int(seed) & 0xFFFFFFFFFFFFFFFF, _ptr(rounds), len(rounds), int(n_candidates),
             int(cand_offset), ctypes.c_void_p(d_out.data_ptr()), None))
         return d_out
+
+    def _check_device(self, t, what):
+        """The device entry points copy on this context's stream: a buffer
+        on another GPU would be written across devices (or fault)."""
+        if len(self.devices) != 1 or t.device.index != self.device:
+            raise ValueError('%s is on cuda:%s, this engine runs on cuda:%d%s'
+                             % (what, t.device.index, self.device,
+                                '' if len(self.devices) == 1 else ' (multi-device contexts take host buffers)'))
 
     def merge_results_device(self, d_parts, n_parts, n, d_out):
         """tpe_merge_results over device tensors (n_parts blocks of n records
@@ -321,6 +330,7 @@ class Engine(object):
         for t, need, what in ((d_parts, n_parts * n * rec, 'd_parts'), (d_out, n * rec, 'd_out')):
             if not t.is_cuda or t.numel() * t.element_size() < need or not t.is_contiguous():
                 raise ValueError('%s must be a contiguous device tensor of %d bytes' % (what, need))
+            self._check_device(t, what)
         _torch_stream_done(d_parts)
         self._check(self.lib.tpe_merge_results_device(
             self.h, ctypes.c_void_p(d_parts.data_ptr()), int(n_parts), int(n),

@@ -91,6 +91,10 @@ class DeviceExchange(object):
             raise ValueError(mode)
         self.engine, self.mode, self.shards, self.rank, self.group = engine, mode, shards, rank, group
         self.world = dist.get_world_size(group)
+        if mode == 'candidates' and engine is not None:
+            # the shards' winners merge by score: a value-only round
+            # (get_engine's default) leaves a certified cell without one
+            engine.set_option('value_only', 0)
         self.device = dist.get_backend(group) == 'nccl'
         self._bufs = {}
 

@@ -426,6 +426,22 @@ def _run_deferred(eng, round_call, reference, rebuild, quant, t0):
 
 def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of, known=(), prepare=None,
                           overlap=True, round_call=None, quant=frozenset(), early=None):
+    """_build_reference_order (below), waiting on the early argsorts' future
+    whatever happens: its worker reads (and caches into) the uploader's
+    observation lists, which a failed build must not leave it writing to
+    while the next call appends."""
+    holder = {'early': early}
+    try:
+        return _build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of, known,
+                                      prepare, overlap, round_call, quant, holder)
+    finally:
+        if holder['early'] is not None:
+            from concurrent.futures import wait
+            wait([holder['early']])
+
+
+def _build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of, known, prepare,
+                           overlap, round_call, quant, holder):
     """Device build whose mixtures follow the reference's tie order
     (tpe.py:433, 637): the device reports which mixtures depend on the order
     of tied observations (or a tie of losses at the split), and only for
@@ -452,11 +468,12 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
     other labels runs while the host computes those orders (_run_deferred):
     the argsorts leave the step's critical path.
 
-    early (optional): reference_orders(losses, n_below, obs_of, known)
-    already running (a future: DeviceHistoryUploader.build starts it before
-    its upload).
+    holder['early'] (optional): reference_orders(losses, n_below, obs_of,
+    known) already running (a future: DeviceHistoryUploader.build starts it
+    before its upload); a future started here is left there too.
 
     Returns (n_below, the labels that needed an order[, results])."""
+    early = holder['early']
     n_below = n_below_of(n_valid, gamma)
     known = set(known)
     t0 = time.perf_counter()
@@ -464,7 +481,8 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
         if known and EARLY_ORDERS and early is None:
             # the previous build's order-dependent labels: their argsorts
             # start now, on the host, under the first build and the index
-            early = _order_thread().submit(reference_orders, losses, n_below, obs_of, known)
+            early = holder['early'] = _order_thread().submit(reference_orders, losses, n_below, obs_of,
+                                                             known)
         # the build queues the index itself before it returns (tpe_arm_prepare);
         # the prepare after it is then a no-op
         eng.arm_prepare(*prepare)
@@ -583,9 +601,9 @@ class DeviceHistoryUploader(object):
 
     def build(self, eng, labels, view, gamma, prior_weight, lf=DEFAULT_LF, prepare=None, streams=None,
               overlap=True, round_call=None):
-        """Upload what is new and build the posterior; returns n_below, or
-        (n_below, results) with round_call (the coming round: see
-        build_reference_order)."""
+        """Upload what is new and build the posterior; returns (n_below,
+        results): results of round_call (the coming round: see
+        build_reference_order), None without one."""
         tids, losses, n_valid, cols, owner = view
         key = (tuple((n, k) for n, k, _ in labels) + (tuple(streams) if streams is not None else (),),
                eng.history_generation)
@@ -653,7 +671,13 @@ class DeviceHistoryUploader(object):
             early = _order_thread().submit(reference_orders, losses, n_below_of(n_valid, gamma),
                                            self._obs_of(len(labels)), self.tie_labels)
         if ni_l:
-            eng.history_append(np.asarray(n_new, dtype=np.int64), trial, vals)
+            try:
+                eng.history_append(np.asarray(n_new, dtype=np.int64), trial, vals)
+            except BaseException:
+                if early is not None:   # (its worker reads pos_parts / val_parts)
+                    from concurrent.futures import wait
+                    wait([early])
+                raise
         self.prev_counts = counts                  # committed only after the append
         self.key = (key[0], eng.history_generation)
         self.owner = weakref.ref(owner)
@@ -665,7 +689,7 @@ class DeviceHistoryUploader(object):
                                     prepare=prepare, overlap=overlap, round_call=round_call,
                                     quant=self.quant, early=early)
         self.tie_labels = out[1]
-        return (out[0], out[2]) if round_call is not None else out[0]
+        return out[0], (out[2] if round_call is not None else None)
 
     def _obs_of(self, n_labels):
         def obs_of(l):

@@ -139,8 +139,8 @@ class FminLoop(object):
         """History of the first n trials on the device, posterior rebuilt
         (its expansion index queued meanwhile when the coming round(s) of
         n_candidates per label will use it, as tpe.suggest does); returns
-        n_below, or (n_below, results) with round_call (the step's round,
-        run as tpe.suggest runs it: see posterior.build_reference_order)."""
+        (n_below, results of round_call -- the step's round, run as
+        tpe.suggest runs it: see posterior.build_reference_order -- or None)."""
         if n > len(self.hist.tids):
             raise ValueError('the synthetic history holds %d trials' % len(self.hist.tids))
         self.n = n

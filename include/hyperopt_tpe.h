@@ -114,8 +114,14 @@ typedef struct {
     double lpdf_above;
     int64_t index;      /* GLOBAL candidate index of the winner (-1: no candidates) */
     int32_t label;
-    int32_t status;     /* 0 ok                                                     */
+    int32_t status;     /* 0 ok; TPE_STATUS_VALUE_ONLY: index and value only        */
 } tpe_label_result;     /* 48 bytes */
+
+/* status of a TPE_OPT_VALUE_ONLY round's cell that the screen alone decided:
+ * index and value are the winner's, score / lpdf_below / lpdf_above are NaN
+ * (not computed).  Such records carry no order key, so tpe_merge_results and
+ * tpe_merge_results_device refuse them (TPE_ERR_ARG). */
+#define TPE_STATUS_VALUE_ONLY 1
 
 int tpe_abi_version(void);
 

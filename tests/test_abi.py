@@ -77,3 +77,16 @@ def test_bad_precision_rejected():
     lib = L.load()
     h = ctypes.c_void_p()
     assert lib.tpe_ctx_create(0, 7, ctypes.byref(h)) == L.TPE_ERR_ARG
+
+
+def test_merge_results_refuses_value_only():
+    """A TPE_STATUS_VALUE_ONLY record (index and value, no score) cannot be
+    ranked by broadcast_best's order: the host merge refuses it; records
+    without a winner (index -1) are skipped as before."""
+    from hyperopt_amd.engine import EngineError, merge_results
+    a, b = _res(1.0, 3), _res(float('nan'), 7)
+    b['status'] = L.TPE_STATUS_VALUE_ONLY
+    with pytest.raises(EngineError):
+        merge_results(np.stack([a, b]))
+    b['index'] = -1
+    assert merge_results(np.stack([a, b]))['index'][0] == 3

@@ -36,6 +36,9 @@ def _check(exact, vo):
     assert np.array_equal(exact['index'], vo['index'])
     assert exact['value'].tobytes() == vo['value'].tobytes()
     decided = np.isnan(vo['lpdf_below']) & ~np.isnan(exact['lpdf_below'])
+    # a decided cell says so (TPE_STATUS_VALUE_ONLY); every other one is ok
+    assert np.all(vo['status'][decided] == 1) and np.all(vo['status'][~decided] == 0)
+    assert np.all(exact['status'] == 0)
     # the cells the screen did not decide alone are the exact round's, bit for bit
     same = ~decided
     assert np.ascontiguousarray(exact[same]).tobytes() == np.ascontiguousarray(vo[same]).tobytes()
@@ -113,3 +116,36 @@ def test_exact_round_after_an_empty_value_only_plan(eng):
     fresh = eng.suggest_batch(13, ids, 24)
     assert np.ascontiguousarray(after).tobytes() == np.ascontiguousarray(fresh).tobytes()
     assert np.isnan(vo['lpdf_below']).any()   # (the value-only round decided cells alone)
+
+
+def test_merge_refuses_value_only_records(eng):
+    """Candidate shards merge by score (broadcast_best): a value-only record
+    has none, so both merges refuse it instead of ranking its NaN (ADVICE
+    r4), and parallel.DeviceExchange turns value-only off for candidate
+    shards."""
+    import torch
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.engine import EngineError, merge_results
+    from hyperopt_amd.workloads import mixed_history
+    hist = mixed_history(32, 20000, seed=2)
+    eng.set_posterior(*P.pack(hist.posteriors()))
+    ids = list(range(300, 556))
+    eng.set_option('value_only', 1)
+    try:
+        vo = eng.suggest_batch(13, ids, 24)
+    finally:
+        eng.set_option('value_only', 0)
+    exact = eng.suggest_batch(13, ids, 24)
+    assert (vo['status'] == 1).any()
+    with pytest.raises(EngineError):
+        merge_results(np.stack([vo.ravel(), exact.ravel()]))
+    parts = torch.from_numpy(np.ascontiguousarray(np.stack([exact.ravel(), vo.ravel()])).view(np.uint8)
+                             .reshape(-1)).cuda()
+    out = torch.empty(exact.size * exact.dtype.itemsize, dtype=torch.uint8, device='cuda')
+    with pytest.raises(EngineError, match='value-only'):
+        eng.merge_results_device(parts, 2, exact.size, out)
+    # two exact parts merge as before
+    ok = torch.from_numpy(np.ascontiguousarray(np.stack([exact.ravel(), exact.ravel()])).view(np.uint8)
+                          .reshape(-1)).cuda()
+    eng.merge_results_device(ok, 2, exact.size, out)
+    assert out.cpu().numpy().tobytes() == np.ascontiguousarray(exact.ravel()).tobytes()
