@@ -14,6 +14,8 @@
 #   lpdf             PMC passes of the plain fp64 round (tools/prof_lpdf.sh)
 #   shard=<r>        label shard r of config 3 alone: probe + kernel/HIP-API trace
 #   py=<script,args> any python script of the tree (commas for spaces)
+#   ubench           tools/ubench_issue (built beforehand): VALU issue costs -> issue_costs.json
+#   listpmc          rocprofv3 --list-avail (the counters this box offers)
 set -u
 T=${1:?tag}
 shift
@@ -56,6 +58,12 @@ for s in "$@"; do
             run shard$r 200 python -u tools/shard_probe.py "$r" 20 || exit 1
             run shard${r}_trace 240 rocprofv3 --kernel-trace --hip-runtime-trace --memory-copy-trace --stats \
                 -d "$OUT/shard${r}_trace" -o run --output-format csv -- python -u tools/shard_probe.py "$r" 10 || exit 1 ;;
+        ubench)
+            echo "== ubench"
+            timeout -k 10 120 tools/ubench_issue > "$OUT/issue_costs.json" 2> "$OUT/ubench.err" || { cat "$OUT/ubench.err"; exit 1; }
+            cat "$OUT/issue_costs.json" ;;
+        listpmc)
+            run listpmc 120 rocprofv3 --list-avail || exit 1 ;;
         py=*)
             a=${s#py=}
             run py$n 600 python -u ${a//,/ } || exit 1 ;;
