@@ -108,7 +108,7 @@ def parse():
                     help='the windowed screen\'s cut T (components left out stay below 2^-T)')
     ap.add_argument('--win-groups', type=int, default=0,
                     help='label groups of a windowed round sorted on a second stream (0 = auto)')
-    ap.add_argument('--unscreened-steps', type=int, default=1,
+    ap.add_argument('--unscreened-steps', type=int, default=4,
                     help='f64: plain fp64 rounds on the seeds of screened rounds, compared bit '
                          'for bit (screened_equals_fp64; 0 = skip)')
     ap.add_argument('--mode', default='fresh', choices=['fresh', 'warm'],
@@ -641,7 +641,8 @@ def main():
     # values and lpdfs bit for bit
     unscreened = None
     if screen and args.unscreened_steps > 0 and world == 1 and devs is None:
-        nu = args.unscreened_steps
+        # (fresh mode compares the warm steps' rounds: at most args.steps of them)
+        nu = min(args.unscreened_steps, args.steps) if fresh_mode else args.unscreened_steps
         first = warm_first if fresh_mode else args.warmup + args.steps
         if not fresh_mode:
             timed(nu, first, False, keep=True)

@@ -3099,6 +3099,40 @@ int run_fills(tpe_ctx* ctx, FillSet& f) {
 // run_round; nullptr: early exit off)
 int64_t* early_found(tpe_ctx* ctx) { return ctx->early ? ctx->xfound.p : nullptr; }
 
+// The candidates an early-exit tile round of one family drew, counted the
+// same way whatever order the workgroups ran in: per
+// (round, label) cell every tile that starts at or before the cell's first
+// index holding its best drawable score (found, exact), or all n when it was
+// never found (or the early exit is off) -- the work a scan in index order
+// must do.  The workgroups' own counts also include the tiles they drew
+// before another's find reached them, which depends on the interleaving
+// (with TPE_OPT_AUX_FAMILIES: on the dense draw beside them).
+__global__ __launch_bounds__(kBlock) void k_early_drawn(const int64_t* __restrict__ found,
+                                                        const int32_t* __restrict__ group, int32_t nl,
+                                                        int32_t nz, int32_t n_labels, int64_t n,
+                                                        int64_t cand_offset, int64_t per,
+                                                        unsigned long long* __restrict__ drawn) {
+    const int64_t cell = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    unsigned long long c = 0;
+    if (cell < (int64_t)nl * nz) {
+        const int64_t z = cell / nl;
+        const int y = (int)(cell % nl);
+        const int64_t f = found ? found[(size_t)z * n_labels + group[y]] : INT64_MAX;
+        const int64_t i = f - cand_offset;
+        c = (unsigned long long)((f == INT64_MAX || i < 0 || i >= n) ? n : std::min<int64_t>(n, (i / per + 1) * per));
+    }
+    // one atomic per wave
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(drawn, c);
+}
+
+void launch_early_drawn(tpe_ctx* ctx, const int32_t* group, int nl, const RoundArgs& a, int64_t* found,
+                        int64_t per, unsigned long long* drawn) {
+    const int64_t cells = (int64_t)nl * a.gz;
+    hipLaunchKernelGGL(k_early_drawn, dim3((unsigned)((cells + kBlock - 1) / kBlock)), dim3(kBlock), 0, ctx->stream,
+                       found, group, nl, (int32_t)a.gz, ctx->P->n_labels, a.n, a.cand_offset, per, drawn);
+}
+
 void bracket(tpe_ctx* ctx, int mode, int which) {
     ctx->mode_ran[mode] = true;
     if (ctx->timing) (void)hipEventRecord(ctx->evm[mode][which], ctx->stream);
@@ -3121,7 +3155,8 @@ void launch_round(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                 hipLaunchKernelGGL((k_cat_tiles<kCatR>), dim3(ph.grid, nl, a.gz), dim3(kBlock), 0, ctx->stream,
                                    ctx->P->labels.p, g.dev[MODE], ctx->P->comps64.p, ctx->P->samp.p, ph.n,
                                    a.cand_offset, a.seed, ctx->rounds.p, ctx->P->n_labels, a.tiles,
-                                   ctx->partials.p, found, ph.i0, ph.slot_base, ph.empty_from, ctx->xdrawn.p + 1);
+                                   ctx->partials.p, found, ph.i0, ph.slot_base, ph.empty_from, nullptr);
+            launch_early_drawn(ctx, g.dev[MODE], nl, a, found, (int64_t)kCatR * kBlock, ctx->xdrawn.p + 1);
             bracket(ctx, MODE, 1);
             return;
         }
@@ -3749,13 +3784,16 @@ int launch_quantized(tpe_ctx* ctx, const Groups& g, const RoundArgs& a, int64_t*
                     1, std::min<int64_t>({(int64_t)a.gx, (a.n + kQR * kBlock - 1) / (kQR * kBlock),
                                           kHotWgs / std::max<int64_t>(1, (int64_t)cnt * a.gz)}));
 #define TPE_QTILES(M)                                                                                   \
+    do {                                                                                                \
     for (const EarlyPhase& ph : early_phases(a, (int64_t)kQR * kBlock, qgx, found != nullptr,           \
                                              (int64_t)cnt * a.gz))                                     \
         hipLaunchKernelGGL((k_qfused_tiles<M, kQR>), dim3(ph.grid, cnt, a.gz), dim3(kBlock), 0,         \
                            ctx->stream, ctx->P->labels.p, g.dev[mode], ctx->P->comps64.p, ctx->P->samp.p, \
                            ctx->qinfo.p, ctx->qtab.p, ph.n, a.cand_offset, a.seed, ctx->rounds.p, qbase,  \
                            ctx->P->n_labels, a.tiles, ctx->partials.p, ctx->errflag.p, ctx->qkmax.p, found, \
-                           ph.i0, ph.slot_base, ph.empty_from, ctx->xdrawn.p)
+                           ph.i0, ph.slot_base, ph.empty_from, nullptr);                                \
+    launch_early_drawn(ctx, g.dev[mode], cnt, a, found, (int64_t)kQR * kBlock, ctx->xdrawn.p);          \
+    } while (0)
                 if (fam) {
                     if (a.S.cpack == 0) TPE_QTILES(QUANT_LGMM);
                     else if (narrow(a.S)) TPE_QFUSED(QUANT_LGMM, kRGroup);

@@ -101,3 +101,33 @@ def test_early_exit_rare_best_value(kind, dedup):
         assert all(f[1] < s[1] for f, s in zip(d_fast, d_full))
     elif dedup:
         assert all(f[0] < s[0] for f, s in zip(d_fast, d_full))
+
+
+def test_early_exit_draw_counts_are_deterministic():
+    """The drawn counts (and so the categorical evals on the bench line) are
+    those of a scan in index order -- every tile starting at or before the
+    first index holding the best drawable score -- whatever order the
+    workgroups ran in: equal with the side families beside the dense draw on
+    the second stream and without, and over repeats.
+    A categorical cell's winner IS that first index, so its count is known
+    exactly: min(C, (index // 2048 + 1) * 2048) (tiles of 8 x 256)."""
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.engine import Engine
+    from hyperopt_amd.workloads import mixed_history
+    hist = mixed_history(32, 10000, seed=0)
+    eng = Engine(0, 'f64')
+    eng.set_posterior(*P.pack(hist.posteriors()))
+    C = 1 << 22
+    cat = [i for i, (_, k, _) in enumerate(hist.labels) if k == 'randint']
+    seen = {}
+    for aux in (0, 1, 1, 0):
+        eng.set_option('aux_families', aux)
+        for s in (21, 22):
+            res = eng.suggest(seed=s, n_candidates=C, round=s)
+            d = eng.last_drawn()
+            seen.setdefault(s, []).append(d)
+            want = sum(min(C, (int(res[li]['index']) // 2048 + 1) * 2048) for li in cat)
+            assert d[1] == want, (s, aux, d, want)
+    eng.close()
+    for s, ds in seen.items():
+        assert len(set(ds)) == 1, (s, ds)
