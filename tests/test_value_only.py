@@ -127,9 +127,9 @@ def test_merge_refuses_value_only_records(eng):
     from hyperopt_amd import posterior as P
     from hyperopt_amd.engine import EngineError, merge_results
     from hyperopt_amd.workloads import mixed_history
-    hist = mixed_history(32, 20000, seed=2)
+    hist = mixed_history(64, 20000, seed=2)
     eng.set_posterior(*P.pack(hist.posteriors()))
-    ids = list(range(300, 556))
+    ids = list(range(300, 812))
     eng.set_option('value_only', 1)
     try:
         vo = eng.suggest_batch(13, ids, 24)

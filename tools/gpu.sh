@@ -11,7 +11,7 @@
 #   bench            the default bench.py line (what the driver runs)
 #   bench=<args>     bench.py with extra arguments (commas for spaces)
 #   prof             tools/prof_round.sh <tag> (kernel trace + PMC passes of the default line)
-#   lpdf             PMC passes of the plain fp64 round (tools/prof_lpdf.sh)
+#   lpdf             the plain fp64 round's trace + PMC passes (tools/prof_round.sh <tag>_lpdf)
 #   shard=<r>        label shard r of config 3 alone: probe + kernel/HIP-API trace
 #   py=<script,args> any python script of the tree (commas for spaces)
 #   ubench           tools/ubench_issue (built beforehand): VALU issue costs -> issue_costs.json
@@ -38,10 +38,12 @@ n=0
 for s in "$@"; do
     n=$((n + 1))
     case "$s" in
-        tests)
-            run tests 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
+        tests)   # (a failed test -- pytest rc 1 -- does not stop the later steps; anything else does)
+            run tests 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread
+            rc=$?; [ $rc -le 1 ] || exit 1 ;;
         tests=*)
-            run tests$n 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${s#tests=}" || exit 1 ;;
+            run tests$n 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "${s#tests=}"
+            rc=$?; [ $rc -le 1 ] || exit 1 ;;
         smoke)
             run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
         bench)
@@ -51,8 +53,8 @@ for s in "$@"; do
             run bench$n 600 python -u bench.py ${a//,/ } || exit 1 ;;
         prof)
             bash tools/prof_round.sh "$T" --steps 5 --warmup 2 --no-other-configs --no-agreement || exit 1 ;;
-        lpdf)
-            bash tools/prof_lpdf.sh "$T" || exit 1 ;;
+        lpdf)   # the plain fp64 round (k_round<double>, no screen) at config 3: trace + PMC passes
+            bash tools/prof_round.sh "${T}_lpdf" --mode warm --no-screen --steps 2 --warmup 1 || exit 1 ;;
         shard=*)
             r=${s#shard=}
             run shard$r 200 python -u tools/shard_probe.py "$r" 20 || exit 1

@@ -2,12 +2,15 @@
 // and the fp64 lpdf kernel (k_round<double>) on one MI355X: cycles per
 // wave64 instruction per SIMD, measured with 1, 2, 4 and 8 waves per SIMD
 // (every CU busy).  Each kernel runs 8 independent register chains of one
-// instruction; a wave's cycles come from clock64() (shader clock, so the
-// figure does not depend on the clock the chip holds), and
-//   cycles per instruction per SIMD = wave cycles / (instructions x waves per SIMD)
-// is the issue cost once the waves saturate the SIMD (dependency latency
-// hidden).  bench.py / tools/pmc_summary.py weight the PMC instruction
-// counts with these costs (the cycle-weighted issue model).
+// instruction.  Every wave stamps the shader clock (clock64) and the 100 MHz
+// real-time clock (wall_clock64) around its loop; the host takes the clock
+// the chip held (shader ticks / real time, median over waves) and the span
+// from the first wave's start to the last wave's end, so
+//   cycles per instruction per SIMD = span x clock / (instructions / SIMDs)
+// does not depend on how the launch staggered the waves; with enough waves
+// per SIMD it is the issue cost (dependency latency hidden).  bench.py /
+// tools/pmc_summary.py weight the PMC instruction counts with these costs
+// (the cycle-weighted issue model).
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/ubench_issue tools/ubench_issue.hip
 //   tools/ubench_issue > profiles/<tag>_issue_costs.json
@@ -85,7 +88,7 @@ __device__ __forceinline__ void step(double* d, float* f, uint32_t* u, uint64_t*
 }
 
 template <int OP>
-__global__ __launch_bounds__(256) void k_issue(uint64_t* __restrict__ cycles, double* __restrict__ sink) {
+__global__ __launch_bounds__(256) void k_issue(uint64_t* __restrict__ stamps, double* __restrict__ sink) {
     double d[8];
     float f[8];
     uint32_t u[8];
@@ -100,6 +103,7 @@ __global__ __launch_bounds__(256) void k_issue(uint64_t* __restrict__ cycles, do
     const float fb = 0.9999f, fc = 1e-6f;
     const uint32_t ub = 3u + (threadIdx.x & 1);
     __syncthreads();
+    const uint64_t r0 = wall_clock64();
     const uint64_t t0 = clock64();
     for (int it = 0; it < kIters; ++it) {
 #pragma unroll
@@ -108,30 +112,49 @@ __global__ __launch_bounds__(256) void k_issue(uint64_t* __restrict__ cycles, do
             for (int c = 0; c < 8; ++c) step<OP>(d, f, u, w, db, dc, fb, fc, ub, c);
     }
     const uint64_t t1 = clock64();
+    const uint64_t r1 = wall_clock64();
     double s = 0.0;
     for (int c = 0; c < 8; ++c) s += d[c] + f[c] + (double)u[c] + (double)w[c];
     if (s == 12345.678) sink[threadIdx.x] = s;   // (keeps the chains live)
-    if ((threadIdx.x & 63) == 0) cycles[blockIdx.x * 4 + (threadIdx.x >> 6)] = t1 - t0;
+    if ((threadIdx.x & 63) == 0) {
+        uint64_t* st = stamps + 4 * ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6));
+        st[0] = t0;
+        st[1] = t1;
+        st[2] = r0;
+        st[3] = r1;
+    }
 }
 
 template <int OP>
-int run(int n_cu, uint64_t* d_cyc, double* d_sink, std::vector<uint64_t>& h) {
+int run(int n_cu, uint64_t* d_st, double* d_sink, std::vector<uint64_t>& h) {
     printf("  \"%s\": {", kNames[OP]);
+    double ghz_all = 0.0;
     for (int wps = 1; wps <= 8; wps *= 2) {
         const int blocks = n_cu * wps;   // 256 threads = 4 waves (one per SIMD) per workgroup
-        hipLaunchKernelGGL(k_issue<OP>, dim3(blocks), dim3(256), 0, 0, d_cyc, d_sink);
+        const int waves = blocks * 4;
+        hipLaunchKernelGGL(k_issue<OP>, dim3(blocks), dim3(256), 0, 0, d_st, d_sink);   // (warm)
         CHK(hipGetLastError());
         CHK(hipDeviceSynchronize());
-        hipLaunchKernelGGL(k_issue<OP>, dim3(blocks), dim3(256), 0, 0, d_cyc, d_sink);   // (warm)
+        hipLaunchKernelGGL(k_issue<OP>, dim3(blocks), dim3(256), 0, 0, d_st, d_sink);
         CHK(hipDeviceSynchronize());
-        CHK(hipMemcpy(h.data(), d_cyc, (size_t)blocks * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
-        std::vector<uint64_t> v(h.begin(), h.begin() + (size_t)blocks * 4);
-        std::sort(v.begin(), v.end());
-        const double med = (double)v[v.size() / 2];
+        CHK(hipMemcpy(h.data(), d_st, (size_t)waves * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+        std::vector<double> ghz;
+        uint64_t rmin = UINT64_MAX, rmax = 0;
+        for (int w = 0; w < waves; ++w) {
+            const uint64_t* st = h.data() + 4 * (size_t)w;
+            if (st[3] > st[2]) ghz.push_back((double)(st[1] - st[0]) / (double)(st[3] - st[2]) * 0.1);
+            rmin = std::min(rmin, st[2]);
+            rmax = std::max(rmax, st[3]);
+        }
+        std::sort(ghz.begin(), ghz.end());
+        const double clk = ghz.empty() ? 0.0 : ghz[ghz.size() / 2];   // GHz (real-time clock: 100 MHz)
+        const double span_cycles = (double)(rmax - rmin) * 10.0 * clk;  // ns x GHz
         const double n_instr = (double)kIters * kPerTrip * (OP == CNDMASK || OP == CMP_U64 ? 2 : 1);
-        printf("%s\"%d\": %.3f", wps > 1 ? ", " : "", wps, med / (n_instr * wps));
+        const double per_simd = n_instr * waves / (4.0 * n_cu);
+        printf("%s\"%d\": %.3f", wps > 1 ? ", " : "", wps, span_cycles / per_simd);
+        ghz_all = clk;
     }
-    printf("}%s\n", OP + 1 < N_OPS ? "," : "");
+    printf(", \"ghz\": %.3f}%s\n", ghz_all, OP + 1 < N_OPS ? "," : "");
     return 0;
 }
 
@@ -148,12 +171,14 @@ int main() {
     const int n_cu = prop.multiProcessorCount;
     uint64_t* d_cyc;
     double* d_sink;
-    CHK(hipMalloc(&d_cyc, (size_t)n_cu * 8 * 4 * sizeof(uint64_t)));
+    CHK(hipMalloc(&d_cyc, (size_t)n_cu * 8 * 4 * 4 * sizeof(uint64_t)));
     CHK(hipMalloc(&d_sink, 256 * sizeof(double)));
-    std::vector<uint64_t> h((size_t)n_cu * 8 * 4);
+    std::vector<uint64_t> h((size_t)n_cu * 8 * 4 * 4);
     printf("{\"device\": \"%s\", \"cus\": %d, \"note\": \"shader cycles per wave64 instruction per SIMD "
-           "at 1/2/4/8 waves per SIMD (8 independent chains per wave; v_cndmask_b32 and v_cmp_gt_u64 "
-           "are measured in pairs with a compare / select and counted per instruction)\",\n",
+           "at 1/2/4/8 waves per SIMD over the launch's span at the clock the chip held (ghz: the "
+           "8-wave run's, shader ticks over the 100 MHz real-time clock); 8 independent chains per "
+           "wave; v_cndmask_b32 and v_cmp_gt_u64 are measured in pairs with a compare / select and "
+           "counted per instruction\",\n",
            prop.gcnArchName, n_cu);
     printf(" \"cycles_per_instr_per_simd\": {\n");
     if (run_all<0>(n_cu, d_cyc, d_sink, h)) return 1;
