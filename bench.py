@@ -37,21 +37,6 @@ sys.path.insert(0, REPO)
 # e = exp(t), acc += e = 5 FLOP + 1 exp, quoted as 6 FLOP/eval, against the
 # vendor vector peak for the dtype.
 FLOPS_PER_EVAL = {'f64': 6.0, 'f32': 6.0}
-# The issue-slot roofline (what actually bounds the kernel) counts the
-# 4-cycle wave64 issue slots of the gfx950 inner loop per eval
-# (tools/isa_loop_mix.py):
-#   fp64 (k_round): v_fma (z), v_fma (u), v_rndne, v_add (f), 2 x v_fma
-#         (2^(f/4096)), v_cvt_i32, v_ldexp, v_fmac (table product +
-#         accumulate) = 9 fp64, 3 int32 (table index, byte offset, exponent)
-#         and 1/4 v_mov_b64 (the component's m, shared by 4 candidates) =
-#         12.25 slots, plus one ds_read_b64
-#   fp32 (k_screen / k_round<float>): candidate pairs in packed fp32 --
-#         v_pk_fma_f32 (z), v_pk_fma_f32 (t) and 1/2 v_pk_add_f32 (tree of
-#         8, then the running sum) per two evals, 1/8 v_mov_b64 per eval, and
-#         one v_exp_f32 (8-cycle issue = 2 slots) per eval = 3.625 slots
-#   k_screen: the same with 8 candidates per thread (v_mov_b64 per 8 evals) =
-#         3.5625 slots
-VALU_SLOTS_PER_EVAL = {'f64': 12.25, 'f32': 3.625, 'screen': 3.5625}
 # expansion screen (k_screen_bx): per candidate a 15-coefficient Horner
 # polynomial (15 FMA) and the degree-5 exp(-kappa delta^2) factor (5 FMA)
 BX_FLOPS_PER_CAND = 2 * 15 + 2 * 5
@@ -63,11 +48,14 @@ BX_FLOPS_PER_CAND = 2 * 15 + 2 * 5
 # Philox words (20 32x32-bit products + 40 xors per attempt) are integer work
 # and are not counted; neither are rejected attempts.
 DRAW_FLOPS_PER_CAND = 51
-PEAK_FP64_VECTOR_TFLOPS = 78.6        # MI355X spec (MI355X_MICROARCH.md)
+# Vector peaks.  FP32 157.3 TFLOP/s is MI355X_MICROARCH.md's figure (256 CUs
+# x 4 SIMD-32 x 32 lanes x 2 FLOP x 2.4 GHz).  The guide lists no FP64
+# figure: 78.6 TFLOP/s is AMD's MI355X specification for vector FP64 -- half
+# the FP32 rate, which tools/ubench_issue.hip confirms on the box: a wave64
+# v_fma_f64 issues in 4 cycles per SIMD against v_fma_f32's 2
+# (profiles/r5b_issue_costs.json).
+PEAK_FP64_VECTOR_TFLOPS = 78.6
 PEAK_FP32_VECTOR_TFLOPS = 157.3
-# 4-cycle wave64 VALU issue slots per second at 2.4 GHz, in lanes: 256 CU x
-# 4 SIMD x 16 lanes per clock (unpacked fp32 and fp64 issue at the same rate)
-PEAK_VALU_LANE_INSTR = {'f64': 256 * 4 * 16 * 2.4e9, 'f32': 256 * 4 * 16 * 2.4e9}
 DENSE = ('dense', 'dense_lgmm1')   # 'dense': GMM1 + LGMM1 labels in one launch
 
 
@@ -356,18 +344,23 @@ def suggest_latency(n_labels, n_trials, n_reps=20, n_warm=3):
 PMC_MIN_CLOCK_GHZ = 2.0
 
 
-def measured_pmc(kernel_prefix):
-    """HBM bytes per launch and VALU issue utilisation of the dominant kernel
-    from the newest committed PMC summary that has it (rocprofv3 --pmc passes
-    of this bench, tools/prof_round.sh + tools/pmc_summary.py; FETCH doubled
-    per the gfx950 correction) -- (None, None, None) if absent."""
+def measured_pmc(kernel_prefix, summary_glob='r*_pmc_summary.json'):
+    """The dominant kernel's counters from the newest committed PMC summary
+    that has it (rocprofv3 --pmc passes of this bench, tools/prof_round.sh +
+    tools/pmc_summary.py): {} if absent; {'source': ... refused} when the
+    counter run held a clock below 2 GHz.  Keys: hbm_bytes (2 x FETCH_SIZE +
+    WRITE_SIZE per launch, the gfx950 correction), valu_busy (rocprofv3
+    VALUBusy), issue_frac (the cycle-weighted issue model: per instruction
+    class its count x the issue cost tools/ubench_issue.hip measured, over the
+    launch's SIMD cycles), wave_cycles (where the waves' cycles go),
+    instructions per candidate / eval, the counter run's clock."""
     import glob
     import re
 
     def tag_key(f):   # r<round><letters>: by round, then r2z < r2aa < r2ai (newest last)
         m = re.match(r'r(\d+)([a-z]*)_', os.path.basename(f))
         return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, '')
-    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_pmc_summary.json')), key=tag_key)
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', summary_glob)), key=tag_key)
     for f in reversed(files):
         d = json.load(open(f))
         for name, v in d.items():
@@ -377,10 +370,47 @@ def measured_pmc(kernel_prefix):
                 clk = v.get('_eff_clock_ghz')
                 src = os.path.relpath(f, REPO)
                 if clk is None or clk < PMC_MIN_CLOCK_GHZ:
-                    return None, None, '%s refused: effective clock %s GHz < %.1f' % (
-                        src, 'unrecorded' if clk is None else '%.2f' % clk, PMC_MIN_CLOCK_GHZ)
-                return v['_hbm_bytes_per_launch'], v.get('_valu_busy'), '%s (%.2f GHz)' % (src, clk)
-    return None, None, None
+                    return {'source': '%s refused: effective clock %s GHz < %.1f' % (
+                        src, 'unrecorded' if clk is None else '%.2f' % clk, PMC_MIN_CLOCK_GHZ)}
+                out = {'source': '%s (%.2f GHz)' % (src, clk), 'kernel': name,
+                       'hbm_bytes': v['_hbm_bytes_per_launch'], 'valu_busy': v.get('_valu_busy'),
+                       'issue_frac': v.get('_issue_frac'), 'issue_split': v.get('_issue_split'),
+                       'issue_costs': v.get('_issue_costs_source'),
+                       'wave_cycles': v.get('_wave_cycle_split'),
+                       'instr_per_candidate': v.get('_valu_instr_per_candidate'),
+                       'instr_per_eval': v.get('_valu_instr_per_eval'), 'clock_ghz': clk}
+                return {k: x for k, x in out.items() if x is not None}
+    return {}
+
+
+def roofline_lpdf(launch_ms, evals, args):
+    """The lpdf kernel north_star's target describes:
+    the plain fp64 round k_round<double> (GMM1_lpdf / LGMM1_lpdf of every
+    (candidate, component) pair, tpe.py:110-172, logsum_rows :259-262), timed
+    by HIP events on the engine's stream in this run's unscreened leg, with
+    the counters of its committed PMC passes (tools/gpu.sh lpdf ->
+    profiles/r*_lpdf_pmc_summary.json)."""
+    pmc = (measured_pmc('k_round<double, 8, true', 'r*_lpdf_pmc_summary.json')
+           if args.config == 3 and args.cand_log2 == 24 and args.labels == 32 else {})
+    rate = evals / (launch_ms * 1e-3)
+    achieved = rate * FLOPS_PER_EVAL['f64'] / 1e12
+    issue = pmc.get('issue_frac')
+    return {'kernel': 'k_round<double, DENSE_ANY, SAMPLE> (plain fp64 round: Philox draw, GMM1/LGMM1 lpdf '
+                      'under l and g of every (candidate, component) pair, block maxloc)',
+            'evals_per_launch': evals, 'launch_ms': round(launch_ms, 3), 'evals_per_s': rate,
+            'target_evals_per_s': 1e11, 'meets_rate_target': rate >= 1e11,
+            'achieved': round(achieved, 3), 'peak': PEAK_FP64_VECTOR_TFLOPS, 'unit': 'TFLOP/s',
+            'frac': round(achieved / PEAK_FP64_VECTOR_TFLOPS, 4), 'flops_per_eval': FLOPS_PER_EVAL['f64'],
+            'valu_instr_per_eval': pmc.get('instr_per_eval'), 'issue_frac_measured': issue,
+            'issue_split': pmc.get('issue_split'), 'valu_busy_measured': pmc.get('valu_busy'),
+            'wave_cycles': pmc.get('wave_cycles'), 'pmc_source': pmc.get('source'),
+            'meets_50pct_valu_roofline': (issue >= 0.5) if issue is not None else None,
+            'note': 'north_star: >= 1e11 lpdf evals/s at >= 50 % of the VALU roofline.  The VALU roofline '
+                    'here is the cycle-weighted issue rate (issue_frac_measured: PMC instruction classes '
+                    'x the issue costs tools/ubench_issue.hip measured); frac counts only the 6 '
+                    'algorithmic FLOP of an eval against the fp64 vector peak -- the fp64 exp costs ~7 '
+                    'instructions beyond them (an LDS-table + degree-3 polynomial sequence), so the '
+                    'kernel is issue-bound well below that FLOP peak'}
 
 
 def workload_name(args, C):
@@ -648,9 +678,13 @@ def main():
             timed(nu, first, False, keep=True)
         eng.set_option('screen', 0)
         ures = {}
+        u_ms = u_ev = 0.0   # the plain fp64 round's dense launch: device ms (HIP events), evals
         t0 = time.perf_counter()
         for i in range(nu):
             ures[first + i] = step(first + i, False)
+            ms_ev = eng.last_mode_stats()
+            u_ms += sum(ms_ev[k][0] for k in DENSE)
+            u_ev += sum(ms_ev[k][1] for k in DENSE)
         torch.cuda.synchronize()
         udt = time.perf_counter() - t0
         eng.set_option('screen', 1)
@@ -659,7 +693,7 @@ def main():
                        results[k]['value'].tobytes() == ures[k]['value'].tobytes() for k in ures)
         else:
             same = all(results[k].view(np.uint8).tobytes() == ures[k].view(np.uint8).tobytes() for k in ures)
-        unscreened = (same, udt, nu, first)
+        unscreened = (same, udt, nu, first, u_ms, u_ev)
     # oracle leg (untimed): the first warm round against numpy's argmax, on
     # the posterior that produced it (before the projection advances it)
     agree_leg = None
@@ -750,7 +784,6 @@ def main():
     screened = scr[0] > 0
     smode = smode_timed if screened else 0
     windowed = smode == 2
-    slots = None
     hot = smode == 3 and scr[5] > 0
     if hot:
         # the hot-bin prefilter: every candidate drawn and bounded by its
@@ -790,7 +823,6 @@ def main():
             kname, kdesc = 'k_screen<', 'k_screen (fp32 screen of the fp64 round, GMM1+LGMM1 labels)'
         dom_rate = scr[3] / (dom_ms * 1e-3)
         dom_flops = scr[3] * FLOPS_PER_EVAL['f32']
-        slots = VALU_SLOTS_PER_EVAL['screen']
     else:
         dom_ms = mode_ms[dom]
         kprec = prec
@@ -799,23 +831,30 @@ def main():
         kdesc = 'k_round<%s,%s>' % (prec, dom + ' (GMM1+LGMM1 labels)')
         dom_rate = mode_ev[dom] / (dom_ms * 1e-3)
         dom_flops = mode_ev[dom] * FLOPS_PER_EVAL[prec]
-        slots = VALU_SLOTS_PER_EVAL[prec]
     peak = PEAK_FP64_VECTOR_TFLOPS if kprec == 'f64' else PEAK_FP32_VECTOR_TFLOPS
     # PMC figures come from the committed profile of the default workload
     # (config 3, tools/prof_round.sh): only that workload's line carries them
-    traffic, valu_busy, traffic_src = (measured_pmc(kname) if args.config == 3 and world == 1
-                                       and args.cand_log2 == 24 and args.labels == 32
-                                       else (None, None, None))
+    pmc = (measured_pmc(kname) if args.config == 3 and world == 1 and args.cand_log2 == 24
+           and args.labels == 32 else {})
     achieved = dom_flops / (dom_ms * 1e-3) / 1e12
     roof = {'bound': 'valu', 'kernel': kdesc,
             'achieved': round(achieved, 3), 'peak': peak, 'unit': 'TFLOP/s',
-            'frac': round(achieved / peak, 4), 'traffic': traffic,
-            'traffic_source': traffic_src, 'valu_busy_measured': valu_busy,
-            'valu_busy_source': traffic_src,
+            'frac': round(achieved / peak, 4), 'traffic': pmc.get('hbm_bytes'),
+            'traffic_source': pmc.get('source'), 'valu_busy_measured': pmc.get('valu_busy'),
+            'issue_frac_measured': pmc.get('issue_frac'), 'issue_split': pmc.get('issue_split'),
+            'issue_costs_source': ('profiles/' + pmc['issue_costs']) if pmc.get('issue_costs') else None,
+            'wave_cycles': pmc.get('wave_cycles'),
+            'pmc_source': pmc.get('source'),
             'evals_per_s': dom_rate, 'flops_per_eval': FLOPS_PER_EVAL[kprec],
-            'valu_issue_frac': (round(dom_rate * slots / PEAK_VALU_LANE_INSTR[kprec], 4)
-                                if slots else None),
-            'launch_ms': dom_ms / args.steps}
+            'launch_ms': dom_ms / args.steps,
+            'issue_model_note': 'issue_frac_measured: PMC instruction classes (SQ_INSTS_VALU_{ADD,MUL,FMA,'
+                                'TRANS}_F64 / _F32, _INT32, _INT64, _CVT, the rest) x the cycles per wave64 '
+                                'instruction per SIMD tools/ubench_issue.hip measured at 8 waves per SIMD '
+                                '(SIMD-32: 2 for int32 / fp32, 4 for fp64 and v_mad_u64_u32, 8 for v_exp_f32, '
+                                '16 for v_sqrt_f64), over 1024 SIMDs x the launch\'s cycles; valu_busy_measured: '
+                                'rocprofv3 VALUBusy (SQ_ACTIVE_INST_VALU / CUs / GRBM_GUI_ACTIVE); wave_cycles: '
+                                'SQ_* cycles / SQ_WAVE_CYCLES (WAIT_ANY = parked on s_waitcnt / barriers, '
+                                'WAIT_INST_ANY = waiting to issue)'}
     if hot:
         roof['flops_per_candidate_draw'] = DRAW_FLOPS_PER_CAND
         roof['flops_per_listed_poly'] = BX_FLOPS_PER_CAND
@@ -824,7 +863,7 @@ def main():
                         'queued rejection); achieved counts the draw\'s fp64 arithmetic (51 FLOP per '
                         'candidate, the Philox integer work not counted), the listed candidates\' '
                         'polynomials (40) and direct lpdf terms (6 each) over the bracket\'s device '
-                        'time; valu_busy_measured is the PMC utilisation of k_hot_bx')
+                        'time; the PMC figures are k_hot_bx\'s')
     elif smode == 3:
         roof['flops_per_candidate_poly'] = BX_FLOPS_PER_CAND
         roof['note'] = ('VALU-issue bound: per candidate the Philox + Box-Muller draw, the fp64 '
@@ -921,7 +960,9 @@ def main():
                     're-score); the roofline counts the terms the screening kernel summed.  '
                     'other_dense_ms: keys + sort, select, re-score'}
         if unscreened is not None:
-            same, udt, nu, first = unscreened
+            same, udt, nu, first, u_ms, u_ev = unscreened
+            if u_ms > 0:
+                line['roofline_lpdf'] = roofline_lpdf(u_ms / nu, u_ev / nu, args)
             line['screened_equals_fp64'] = bool(same)
             line['screen']['unscreened_fp64'] = {
                 'steps': nu, 'ms_per_step': round(udt / nu * 1e3, 3),

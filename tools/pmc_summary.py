@@ -55,6 +55,52 @@ def pmc(path):
     return out, {k: len(v) for k, v in launches.items()}
 
 
+# the cycle-weighted issue model (CDNA4 has SIMD-32
+# units, so a wave64 VALU instruction does not take one 4-cycle slot across
+# the board): each PMC instruction class is charged the issue cost that
+# tools/ubench_issue.hip measured for a representative opcode at 8 waves per
+# SIMD (profiles/<tag>_issue_costs.json); VALU instructions outside the
+# counted classes (moves, selects, compares, bit ops) the v_cndmask_b32 cost
+CLASS_OPCODE = {'SQ_INSTS_VALU_ADD_F64': 'v_add_f64', 'SQ_INSTS_VALU_MUL_F64': 'v_mul_f64',
+                'SQ_INSTS_VALU_FMA_F64': 'v_fma_f64', 'SQ_INSTS_VALU_TRANS_F64': 'v_sqrt_f64',
+                'SQ_INSTS_VALU_INT32': 'v_add_u32', 'SQ_INSTS_VALU_INT64': 'v_mad_u64_u32',
+                'SQ_INSTS_VALU_CVT': 'v_cvt_f64_u32', 'SQ_INSTS_VALU_ADD_F32': 'v_fma_f32',
+                'SQ_INSTS_VALU_MUL_F32': 'v_fma_f32', 'SQ_INSTS_VALU_FMA_F32': 'v_fma_f32',
+                'SQ_INSTS_VALU_TRANS_F32': 'v_exp_f32'}
+OTHER_OPCODE = 'v_cndmask_b32'
+
+
+def issue_costs(path=None):
+    """{opcode: cycles per wave64 instruction per SIMD} at 8 waves per SIMD,
+    from the newest committed tools/ubench_issue output."""
+    if path is None:
+        here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        files = sorted(glob.glob(os.path.join(here, 'profiles', 'r*_issue_costs.json')))
+        if not files:
+            return None, None
+        path = files[-1]
+    d = json.load(open(path))
+    return {k: v['8'] for k, v in d['cycles_per_instr_per_simd'].items()}, os.path.basename(path)
+
+
+def issue_model(v, costs):
+    """Cycle-weighted VALU issue of one launch (per-launch counters v):
+    (issue cycles per SIMD, fraction of the launch's cycles, per-class split)."""
+    if not costs or 'SQ_INSTS_VALU' not in v or not v.get('GRBM_GUI_ACTIVE'):
+        return None
+    if not all(c in v for c in ('SQ_INSTS_VALU_FMA_F64', 'SQ_INSTS_VALU_INT32')):
+        return None
+    split, counted = {}, 0.0
+    for c, op in CLASS_OPCODE.items():
+        if c in v:
+            split[c] = v[c] * costs[op]
+            counted += v[c]
+    split['other'] = max(v['SQ_INSTS_VALU'] - counted, 0.0) * costs[OTHER_OPCODE]
+    cyc = sum(split.values()) / 1024.0          # per SIMD (1024 SIMDs)
+    gpu_cycles = v['GRBM_GUI_ACTIVE'] / 8.0     # the launch's cycles (summed over 8 XCDs)
+    return cyc, cyc / gpu_cycles, {k: x / 1024.0 / gpu_cycles for k, x in split.items()}
+
+
 def main(src, tag):
     dst = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'profiles')
     for kind in ('kernel_stats', 'domain_stats'):
@@ -69,6 +115,7 @@ def main(src, tag):
                 bench = json.loads(line)
         if bench:
             json.dump(bench, open(os.path.join(dst, '%s_bench.json' % tag), 'w'))
+    costs, costs_src = issue_costs()
     summary, nlaunch = defaultdict(dict), {}
     for f in sorted(glob.glob(os.path.join(src, 'pmc_*', '*counter_collection.csv'))):
         d, n = pmc(f)
@@ -107,31 +154,43 @@ def main(src, tag):
                  else cands * steps / max(nlaunch.get(k, 1), 1))
             v['_candidates_per_launch'] = c
             v['_valu_instr_per_candidate'] = v['SQ_INSTS_VALU'] * 64 / c
-        if 'SQ_INSTS_VALU' in v and v.get('GRBM_GUI_ACTIVE'):
-            # VALU issue utilisation: every wave64 VALU instruction holds a
-            # 16-lane SIMD for 4 cycles; 1024 SIMDs; GRBM_GUI_ACTIVE / 8 XCDs
-            # = the launch's GPU cycles
-            cycles = 1024 * v['GRBM_GUI_ACTIVE'] / 8
-            v['_valu_busy'] = v['SQ_INSTS_VALU'] * 4 / cycles
+        if v.get('GRBM_GUI_ACTIVE'):
             # the clock the counter run actually ran at: GPU cycles per XCD
             # over the launch's duration in that run (bench.py refuses PMC
             # figures from a run below 2 GHz)
             ns = v.get('_pmc_run_ns_per_launch')
             if ns:
                 v['_eff_clock_ghz'] = v['GRBM_GUI_ACTIVE'] / 8 / ns
-            if k.startswith('k_screen') and '_evals_per_launch' in v:
-                # one v_exp_f32 (8-cycle issue) per eval: 4 extra cycles per
-                # 64 evals on top of the 4-cycle count
-                v['_valu_busy'] = (v['SQ_INSTS_VALU'] + v['_evals_per_launch'] / 64) * 4 / cycles
+        if 'SQ_ACTIVE_INST_VALU' in v and v.get('GRBM_GUI_ACTIVE'):
+            # rocprofv3's own VALUBusy: SQ_ACTIVE_INST_VALU (quad-cycles, summed
+            # over the SEs) / CUs / the launch's cycles
+            v['_valu_busy'] = v['SQ_ACTIVE_INST_VALU'] / 256 / (v['GRBM_GUI_ACTIVE'] / 8)
+        m = issue_model(v, costs)
+        if m:
+            v['_issue_cycles_per_simd'], v['_issue_frac'], v['_issue_split'] = m
+            v['_issue_costs_source'] = costs_src
+        if 'SQ_WAVE_CYCLES' in v and 'SQ_WAIT_INST_ANY' in v:
+            # where the waves' (quad-)cycles go: issuing, waiting for a
+            # dependency / pipe (WAIT_INST_ANY), parked on s_waitcnt / barrier
+            wc = v['SQ_WAVE_CYCLES']
+            v['_wave_cycle_split'] = {c: v[c] / wc for c in ('SQ_ACTIVE_INST_ANY', 'SQ_WAIT_INST_ANY',
+                                                             'SQ_WAIT_ANY', 'SQ_ACTIVE_INST_VALU',
+                                                             'SQ_ACTIVE_INST_LDS', 'SQ_ACTIVE_INST_SCA',
+                                                             'SQ_ACTIVE_INST_MISC') if c in v}
         if 'FETCH_SIZE' in v:
             v['_hbm_bytes_per_launch'] = (v['FETCH_SIZE'] * 2 + v.get('WRITE_SIZE', 0)) * 1024
     summary['_note'] = ('counters averaged per launch; FETCH_SIZE/WRITE_SIZE in KB; '
                         '_hbm_bytes_per_launch = (2 x FETCH_SIZE + WRITE_SIZE) KB per the gfx950 '
                         'FETCH_SIZE correction of MI355X_MICROARCH.md; SQ_INSTS_VALU counts wave '
                         'instructions (x64 lanes for _valu_instr_per_eval); GRBM_GUI_ACTIVE is '
-                        'summed over the 8 XCDs; _valu_busy = SQ_INSTS_VALU x 4 cycles / '
-                        '(1024 SIMDs x GRBM_GUI_ACTIVE / 8); _eff_clock_ghz = GRBM_GUI_ACTIVE / 8 / '
-                        'the launch duration in the counter run (_pmc_run_ns_per_launch)')
+                        'summed over the 8 XCDs; _valu_busy = rocprofv3 VALUBusy = '
+                        'SQ_ACTIVE_INST_VALU / 256 CUs / (GRBM_GUI_ACTIVE / 8); _issue_frac = the '
+                        'cycle-weighted issue model: per instruction class its count x the issue '
+                        'cost tools/ubench_issue.hip measured (cycles per wave64 instruction per '
+                        'SIMD at 8 waves per SIMD, _issue_costs_source), over 1024 SIMDs x the '
+                        'launch\'s cycles; _wave_cycle_split: SQ_* cycles / SQ_WAVE_CYCLES; '
+                        '_eff_clock_ghz = GRBM_GUI_ACTIVE / 8 / the launch duration in the counter '
+                        'run (_pmc_run_ns_per_launch)')
     json.dump(summary, open(os.path.join(dst, '%s_pmc_summary.json' % tag), 'w'), indent=1,
               sort_keys=True)
     print(json.dumps({k: v for k, v in summary.items() if k.startswith(('k_round', 'k_screen'))},
