@@ -1194,6 +1194,10 @@ int history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial,
     if (!obs_trial || !obs_val) return ctx->fail(TPE_ERR_ARG, "observations missing");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     hipStream_t sm = ctx->stream;
+    // the previous append's copies out of the pinned staging buffers
+    if (B.staged_pending) HIPCHK(ctx, hipEventSynchronize(B.ev_staged));
+    B.staged_pending = false;
+    if (!B.ev_staged) HIPCHK(ctx, hipEventCreateWithFlags(&B.ev_staged, hipEventDisableTiming));
     // growth: re-lay the pool out when a label outgrows its region
     bool grow = false;
     for (int32_t l = 0; l < L; ++l)
@@ -1252,16 +1256,25 @@ int history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial,
     HIPCHK(ctx, B.st_key_sorted.reserve(total));
     HIPCHK(ctx, B.seg_begin.reserve(L));
     HIPCHK(ctx, B.seg_end.reserve(L));
-    std::vector<int32_t> sb(L), se(L);
+    // the caller's arrays and this call's offsets into page-locked staging:
+    // the copies below run on the stream while the host returns
+    HIPCHK(ctx, B.h_st_off.resize(L + 1));
+    HIPCHK(ctx, B.h_seg.resize(2 * (size_t)L));
+    HIPCHK(ctx, B.h_trial.resize(total));
+    HIPCHK(ctx, B.h_val.resize(total));
+    HIPCHK(ctx, B.h_cnt.resize(L));
+    std::memcpy(B.h_st_off.data(), st.data(), (L + 1) * sizeof(int64_t));
     for (int32_t l = 0; l < L; ++l) {
-        sb[l] = (int32_t)st[l];
-        se[l] = (int32_t)(B.specs_h[l].kind == TPE_CATEGORICAL ? st[l] : st[l + 1]);
+        B.h_seg[l] = (int32_t)st[l];
+        B.h_seg[L + l] = (int32_t)(B.specs_h[l].kind == TPE_CATEGORICAL ? st[l] : st[l + 1]);
     }
-    HIPCHK(ctx, hipMemcpyAsync(B.st_off.p, st.data(), (L + 1) * sizeof(int64_t), hipMemcpyHostToDevice, sm));
-    HIPCHK(ctx, hipMemcpyAsync(B.st_trial.p, obs_trial, total * sizeof(int32_t), hipMemcpyHostToDevice, sm));
-    HIPCHK(ctx, hipMemcpyAsync(B.st_val.p, obs_val, total * sizeof(double), hipMemcpyHostToDevice, sm));
-    HIPCHK(ctx, hipMemcpyAsync(B.seg_begin.p, sb.data(), L * sizeof(int32_t), hipMemcpyHostToDevice, sm));
-    HIPCHK(ctx, hipMemcpyAsync(B.seg_end.p, se.data(), L * sizeof(int32_t), hipMemcpyHostToDevice, sm));
+    std::memcpy(B.h_trial.data(), obs_trial, total * sizeof(int32_t));
+    std::memcpy(B.h_val.data(), obs_val, total * sizeof(double));
+    HIPCHK(ctx, hipMemcpyAsync(B.st_off.p, B.h_st_off.data(), (L + 1) * sizeof(int64_t), hipMemcpyHostToDevice, sm));
+    HIPCHK(ctx, hipMemcpyAsync(B.st_trial.p, B.h_trial.data(), total * sizeof(int32_t), hipMemcpyHostToDevice, sm));
+    HIPCHK(ctx, hipMemcpyAsync(B.st_val.p, B.h_val.data(), total * sizeof(double), hipMemcpyHostToDevice, sm));
+    HIPCHK(ctx, hipMemcpyAsync(B.seg_begin.p, B.h_seg.data(), L * sizeof(int32_t), hipMemcpyHostToDevice, sm));
+    HIPCHK(ctx, hipMemcpyAsync(B.seg_end.p, B.h_seg.data() + L, L * sizeof(int32_t), hipMemcpyHostToDevice, sm));
     int64_t mx_new = 0, mx_all = 0;
     for (int32_t l = 0; l < L; ++l) {
         mx_new = std::max(mx_new, n_new[l]);
@@ -1314,9 +1327,12 @@ int history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial,
     std::swap(B.s_key, B.s_key2);
     std::swap(B.s_idx, B.s_idx2);
     for (int32_t l = 0; l < L; ++l) B.cnt_h[l] += (int32_t)n_new[l];
-    HIPCHK(ctx, hipMemcpyAsync(B.cnt.p, B.cnt_h.data(), L * sizeof(int32_t), hipMemcpyHostToDevice, sm));
-    // the host staging buffers are the caller's: make sure the copies are done
-    HIPCHK(ctx, hipStreamSynchronize(sm));
+    std::memcpy(B.h_cnt.data(), B.cnt_h.data(), L * sizeof(int32_t));
+    HIPCHK(ctx, hipMemcpyAsync(B.cnt.p, B.h_cnt.data(), L * sizeof(int32_t), hipMemcpyHostToDevice, sm));
+    // no wait here: the next append waits for these copies before it
+    // rewrites the staging buffers (round 4 synchronised every append)
+    HIPCHK(ctx, hipEventRecord(B.ev_staged, sm));
+    B.staged_pending = true;
     return TPE_OK;
 }
 

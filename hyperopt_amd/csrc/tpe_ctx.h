@@ -282,6 +282,14 @@ struct BuildBufs {
     DevBuf<uint8_t> sort_tmp;
     DevBuf<int32_t> gs_a, gs_b;    // large appends: staging positions through the two sorts
     DevBuf<uint32_t> gs_lab, gs_lab2; //   and the label of each position
+    // an append's host side, page-locked: its H2D copies run on the stream
+    // without the host waiting for them (the next append first waits for
+    // ev_staged, the copies out of these buffers)
+    PinVec<int64_t> h_st_off;
+    PinVec<int32_t> h_trial, h_seg, h_cnt;
+    PinVec<double> h_val;
+    hipEvent_t ev_staged = nullptr;
+    bool staged_pending = false;
     // per build
     DevBuf<double> losses;
     DevBuf<uint8_t> below;         // per trial: in the below set
@@ -317,6 +325,9 @@ struct BuildBufs {
         idx.release(); below_val.release(); counts.release(); kcount.release(); w.release();
         mu.release(); sigma.release(); mix_off.release(); scratch.release(); ties.release();
         order_off.release(); order.release(); only.release();
+        if (ev_staged) (void)hipEventDestroy(ev_staged);
+        ev_staged = nullptr;
+        staged_pending = false;
         built_ok = false;
         n_labels = 0;
         hist_ready = false;

@@ -605,12 +605,21 @@ class DeviceHistoryUploader(object):
         results): results of round_call (the coming round: see
         build_reference_order), None without one."""
         tids, losses, n_valid, cols, owner = view
-        key = (tuple((n, k) for n, k, _ in labels) + (tuple(streams) if streams is not None else (),),
-               eng.history_generation)
+        if labels is not self._labels_obj or streams is not self._streams_obj:
+            # (the label key of a caller that passes the same list every
+            # step -- FminLoop -- is built once)
+            self._labels_obj, self._streams_obj = labels, streams
+            self._label_key = (tuple((n, k) for n, k, _ in labels) +
+                               (tuple(streams) if streams is not None else (),))
+            self._names = [n for n, _, _ in labels]
+        key = (self._label_key, eng.history_generation)
+        names = self._names
+        obs_now = [cols[n] for n in names]
+        lens = [len(o[0]) for o in obs_now]
         same_owner = self.owner is not None and self.owner() is owner
         fresh = (not same_owner or self.key != key or len(tids) < self.n_trials or
                  (self.n_trials and tids[self.n_trials - 1] != self.last_tid) or
-                 any(len(cols[n][0]) < c for (n, _, _), c in zip(labels, self.prev_counts)))
+                 any(a < c for a, c in zip(lens, self.prev_counts)))
         # invalid until the device holds exactly what prev_counts says
         self.key, self.owner = None, None
         if fresh:
@@ -626,21 +635,14 @@ class DeviceHistoryUploader(object):
             self.quant = frozenset(i for i in range(len(labels))
                                    if specs[i]['flags'] & L.TPE_HAS_Q and specs[i]['kind'] != L.TPE_CATEGORICAL)
         t0 = time.perf_counter()
-        counts = list(self.prev_counts)
+        counts = lens
         # the new observations of every label, transformed and placed in one
         # vectorised pass (a per-label numpy loop cost ~0.4 ms per fmin step
         # at 32 labels): np.log / np.log(np.maximum(o, floor)) elementwise,
         # as the reference's samplers transform them (tpe.py:493-576)
-        n_new, ni_l, nv_l = [], [], []
-        for i, (name, _, _) in enumerate(labels):
-            oi, ov = cols[name]
-            c0 = counts[i]
-            m = len(oi) - c0
-            n_new.append(m)
-            if m:
-                ni_l.append(oi[c0:])
-                nv_l.append(ov[c0:])
-            counts[i] = len(oi)
+        n_new = [a - c for a, c in zip(lens, self.prev_counts)]
+        ni_l = [o[0][c:] for o, c, m in zip(obs_now, self.prev_counts, n_new) if m]
+        nv_l = [o[1][c:] for o, c, m in zip(obs_now, self.prev_counts, n_new) if m]
         if ni_l:
             ni = np.concatenate(ni_l)
             raw = np.asarray(np.concatenate(nv_l), dtype=float)
@@ -703,6 +705,7 @@ class DeviceHistoryUploader(object):
         return obs_of
 
     prev_counts = ()
+    _labels_obj = _streams_obj = None
     pos_parts = val_parts = ()
     tie_labels = frozenset()
     quant = frozenset()

@@ -122,15 +122,19 @@ class FminLoop(object):
         self.labels = [hist.labels[i] for i in self.label_ids]
         self.streams = None if label_ids is None else self.label_ids
         self.names = [n for n, _, _ in self.labels]
+        # labels observed in every trial: their view is a prefix slice
+        self.full = [np.array_equal(hist.obs[n][0], hist.tids) for n in self.names]
         self.n_dense = sum(1 for _, k, _ in self.labels if k in DENSE_KINDS)
         self.uploader = P.DeviceHistoryUploader()
         self.n = 0
 
     def view(self, n):
         obs = {}
-        for name in self.names:
-            oi, ov = self.hist.obs[name]
-            k = int(np.searchsorted(oi, n))
+        hobs = self.hist.obs
+        kt = int(np.searchsorted(self.hist.tids, n))   # (a label in every trial: the same prefix)
+        for name, full in zip(self.names, self.full):
+            oi, ov = hobs[name]
+            k = kt if full else int(np.searchsorted(oi, n))
             obs[name] = (oi[:k], ov[:k])
         losses = self.hist.losses[:n]
         return (self.hist.tids[:n], losses, int(np.count_nonzero(losses == losses)), obs, self)
