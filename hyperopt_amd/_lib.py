@@ -56,6 +56,7 @@ TPE_OPT_VALUE_ONLY = 16
 TPE_OPT_RESCORE_CAP = 17
 TPE_OPT_MODE_MASK = 18
 TPE_OPT_AUX_FAMILIES = 19
+TPE_OPT_HOT32 = 20
 
 TPE_OBS_IDENTITY = 0
 TPE_OBS_LOG = 1

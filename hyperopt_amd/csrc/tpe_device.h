@@ -190,6 +190,7 @@ constexpr int kGuideSteps = 3;   // guided picks take at most this many comparis
 struct SampLds {
     double cdf[kSampLds], mu[kSampLds], sg[kSampLds];
     uint64_t thr[kSampLds];   // ceil(cdf 2^32)
+    float mu32[kSampLds], sg32[kSampLds];   // fp32 copies (k_hot_bx's fp32 draw)
     uint8_t guide[64];
     uint8_t gd[256];
     int steps;
@@ -205,7 +206,7 @@ struct SampShared {
     int steps = -1;   // t->steps read once by the caller (-1: read per pick)
     __device__ __forceinline__ const double* cos_tab() const { return cs; }
     __device__ __forceinline__ const double* log_tab() const { return lg; }
-    __device__ __forceinline__ void pick(uint32_t w, double& mu, double& sg) const {
+    __device__ __forceinline__ int pick_index(uint32_t w) const {
         // (steps is the same for the whole workgroup: a scalar branch)
         const int st = steps >= 0 ? steps : __builtin_amdgcn_readfirstlane(t->steps);
         int k;
@@ -219,6 +220,10 @@ struct SampShared {
 #pragma unroll
             for (int step = kSampLds / 2; step > 0; step >>= 1) k = t->thr[k + step - 1] <= w ? k + step : k;
         }
+        return k;
+    }
+    __device__ __forceinline__ void pick(uint32_t w, double& mu, double& sg) const {
+        const int k = pick_index(w);
         mu = t->mu[k];
         sg = t->sg[k];
     }
@@ -235,11 +240,15 @@ __device__ __forceinline__ bool stage_samp(const DLabel& L, const SampRec* __res
             t->thr[k] = (uint64_t)ceil(r.cdf * 0x1.0p32);   // (exact: a power-of-two scaling, cdf in [0, 1])
             t->mu[k] = r.mu;
             t->sg[k] = r.sigma;
+            t->mu32[k] = (float)r.mu;
+            t->sg32[k] = (float)r.sigma;
         } else {   // padding: never picked (u < 1 <= cdf[ns - 1])
             t->cdf[k] = 2.0;
             t->thr[k] = 1ull << 33;
             t->mu[k] = 0.0;
             t->sg[k] = 0.0;
+            t->mu32[k] = 0.0f;
+            t->sg32[k] = 0.0f;
         }
     }
     if (threadIdx.x == 0) t->steps = 0;
@@ -317,6 +326,47 @@ __device__ __forceinline__ double bm_neglog(double u, const double* __restrict__
 // Box-Muller's radius sqrt(-2 log u) from word y (lt: kLogTab or its LDS copy)
 __device__ __forceinline__ double bm_radius(uint32_t y, const double* __restrict__ lt) {
     return __builtin_amdgcn_sqrt(fmax(0.0, 2.0 * bm_neglog(u01_open0(y), lt)));
+}
+
+// ---------------------------------------------------- fp32 Box-Muller ----
+// The same radius and angle in fp32 with the hardware transcendentals
+// (v_log_f32 = log2, v_sqrt_f32, v_sin_f32 / v_cos_f32 of revolutions):
+// about a third of the fp64 sequences' issue cycles (fp64 runs at half rate
+// on CDNA4 and the fp64 log / sincos are ~25 operations each).  Their error
+// against the fp64 functions above is measured EXHAUSTIVELY -- every one of
+// the 2^32 words, tools/ubench_bm32.hip (profiles/r5*_bm32_sweep.txt) -- and
+// the bounds below cover the largest error found with a margin; k_hot_bx's
+// fp32 draw carries them into a per-candidate bound on |x32 - x64|.
+constexpr float kBm32RadRel = 2.0e-6f;    // |rad32 - rad64| <= kBm32RadRel rad64 (and 0 at rad64 = 0)
+constexpr float kBm32TrigAbs = 2.0e-6f;   // |cos32 - cos64|, |sin32 - sin64| <= kBm32TrigAbs
+
+// -ln(u) for u = 1 - y 2^-32 (u01_open0's uniform) in fp32: for u <= 1/2
+// the exact integer m = 2^32 - y gives u = m 2^-32 (one fp32 rounding) and
+// -ln u = -log2(u) ln 2; above 1/2, -ln(1 - t) with t = y 2^-32 by Kahan's
+// log1p form (the rounding of w = 1 - t corrected by t / (1 - w))
+__device__ __forceinline__ float bm_neglog32(uint32_t y) {
+    constexpr float kLn2f = 0.6931471805599453f;
+    if (y >= 0x80000000u) {
+        const float u = (float)(0u - y) * 0x1.0p-32f;   // (y > 0: 2^32 - y in [1, 2^31])
+        return -__builtin_amdgcn_logf(u) * kLn2f;
+    }
+    const float t = (float)y * 0x1.0p-32f;
+    const float w = 1.0f - t;
+    if (w == 1.0f) return t;
+    return (-__builtin_amdgcn_logf(w) * kLn2f) * (t * __builtin_amdgcn_rcpf(1.0f - w));
+}
+
+__device__ __forceinline__ float bm_radius32(uint32_t y) {
+    return __builtin_amdgcn_sqrtf(2.0f * bm_neglog32(y));
+}
+
+// (cos, sin)(2 pi w 2^-32) in fp32: w - 2^31 as a signed turn fraction in
+// [-1/2, 1/2) (half the input rounding of [0, 1)), cos(2 pi (x + 1/2)) =
+// -cos(2 pi x), likewise sin
+__device__ __forceinline__ void sincos_turn32f(uint32_t w, float& c, float& s) {
+    const float x = (float)(int32_t)(w ^ 0x80000000u) * 0x1.0p-32f;
+    c = -__builtin_amdgcn_cosf(x);
+    s = -__builtin_amdgcn_sinf(x);
 }
 
 // Candidates 2p and 2p + 1 share one Philox4x32-10 call per attempt: the
@@ -580,7 +630,180 @@ __device__ __forceinline__ bool sample_tile(const DLabel& L, const Src& src, uin
     return ok;
 }
 
-// np.round(x / q) * q (round half to even), tpe.py:99 / :255// np.round(x / q) * q (round half to even), tpe.py:99 / :255
+// sample_tile's draws in fp32 with a rigorous bound, for k_hot_bx (RAW,
+// dense GMM1 / LGMM1, every thread of the 256-thread workgroup calls it):
+// slot r gets xf[r] and ef[r]: ef >= 0 -- the draw's attempt 0 was accepted
+// and |xf - x64| <= ef, x64 being the value the fp64 draw (draw_attempt /
+// draw_pair) gives the same candidate; ef = -a <= 0 -- the fp64 draw decided
+// (attempt a accepted) and xf is its value rounded to fp32.  k_screen_hot re-draws
+// a listed candidate in fp64 from (index, attempt), so every value that is
+// scored is the fp64 draw's, bit for bit.
+//   attempt 0: Philox as draw_pair; the component picked by the same
+//     integer thresholds (the same component); radius and angle by the fp32
+//     functions above; x = fma(sg, rad cos|sin, mu) in fp32.  The bound (the
+//     measured kBm32RadRel / kBm32TrigAbs, the fp32 roundings of mu, sigma,
+//     the products and the fma, and the fp64 draw's own rounding):
+//       ef = 1.001 (sg rad (eps_r + eps_t + 2^-23) + 2^-23 (|mu| + |x|))
+//   truncation: x64 in [low, high) is decided by xf +- ef where the
+//     interval clears a bound; where it straddles one (or xf is NaN) the
+//     slot joins the rejected ones, flagged to start from attempt 0 --
+//     so the accepted attempt of every slot is the fp64 draw's;
+//   those slots: sample_tile's cooperative fp64 retries (exact values),
+//     recording the accepted attempt.
+// escale > 1 widens every bound (tests: TPE_OPT_HOT32 = 2 sends many more
+// slots through the fp64 decisions and the margins; the round is the same).
+// Returns false if a slot hit the attempt cap.
+template <int R>
+struct RetryLds32 {
+    int wn[kTileWaves];
+    uint16_t slot[R * 256];
+    double val[R * 256 / 2];   // (a pass holds up to R * 128 retried slots)
+    int32_t att[R * 256 / 2];
+};
+
+__device__ __forceinline__ float f32_step(float f, bool up) {   // the adjacent float (f finite)
+    const uint32_t u = __float_as_uint(f);
+    if (f == 0.0f) return __uint_as_float(up ? 1u : 0x80000001u);
+    return __uint_as_float((f > 0.0f) == up ? u + 1u : u - 1u);
+}
+__device__ __forceinline__ float f32_up(double v) {   // the smallest float >= v
+    const float f = (float)v;
+    return (double)f >= v ? f : f32_step(f, true);
+}
+__device__ __forceinline__ float f32_dn(double v) {   // the largest float <= v
+    const float f = (float)v;
+    return (double)f <= v ? f : f32_step(f, false);
+}
+
+template <int R, typename Src>
+__device__ __forceinline__ bool sample_tile32(const DLabel& L, const Src& src, uint64_t seed, uint32_t rk,
+                                              uint32_t g0, uint32_t pend, float (&xf)[R], float (&ef)[R],
+                                              RetryLds32<R>& q, float escale = 1.0f) {
+    static_assert(R % 2 == 0, "Box-Muller pairs");
+    static_assert(R * 256 <= 32768, "tile offsets are 15-bit (bit 15: start at attempt 0)");
+    constexpr int CAP = R * 256 / 2;
+    constexpr uint16_t kFrom0 = 0x8000;   // list entry flag: decide attempt 0 in fp64 too
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    const bool bounded = (L.flags & 3) == 3;
+    // the bounds as floats that keep the decisions exact (f32_up / f32_dn)
+    const float lo_up = f32_up(L.low), lo_dn = f32_dn(L.low), hi_up = f32_up(L.high), hi_dn = f32_dn(L.high);
+    constexpr float kEpsDraw = kBm32RadRel + kBm32TrigAbs + 0x1.0p-23f;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint16_t* __restrict__ seg = q.slot + wave * (R * 64);
+    constexpr int kAccepted = 1 << 20;
+    int pos[R];
+    int run = 0;
+    const bool paired = (g0 & 1u) == 0;
+#pragma unroll
+    for (int r = 0; r < R; r += 2) {
+        const uint32_t c0 = tile_cand(r, threadIdx.x, blockDim.x);
+        float x2[2], e2[2];
+        bool ex2[2] = {false, false};   // exact fp64 values (the odd-start tile)
+        if (paired) {
+            const U4 w = philox4x32_10(U4{(g0 + c0) >> 1, 0u, (uint32_t)L.stream, rk}, k0, k1);
+            const int ka = src.pick_index(w.x), kb = src.pick_index(w.z);
+            const float rad = bm_radius32(w.y);
+            float c, s;
+            sincos_turn32f(w.w, c, s);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int k = h ? kb : ka;
+                const float mu = src.t->mu32[k], sg = src.t->sg32[k];
+                const float x = __builtin_fmaf(sg, rad * (h ? s : c), mu);
+                x2[h] = x;
+                e2[h] = escale * 1.001f *
+                        (sg * rad * kEpsDraw + 0x1.0p-23f * (__builtin_fabsf(mu) + __builtin_fabsf(x)));
+            }
+        } else {   // (an odd first index, uniform: no shared pair -- each slot's fp64 draw)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const double d = draw_attempt(L, src, k0, k1, g0 + c0 + (uint32_t)h, 0u, rk);
+                x2[h] = (float)d;
+                e2[h] = 0.0f;
+                ex2[h] = !bounded || (L.low <= d && d < L.high);   // (accepted: exact)
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const bool p = (pend >> (r + h)) & 1u;
+            const float x = x2[h], e = e2[h];
+            bool list = false;
+            uint16_t flag = 0;
+            if (p && bounded && !ex2[h]) {
+                if (!paired) {
+                    list = true;   // rejected at attempt 0 (exactly)
+                } else {
+                    const float e2u = e + 0x1.0p-22f * __builtin_fabsf(x);   // (+ the roundings of x -+ e)
+                    const bool acc_sure = x - e2u >= lo_up && x + e2u < hi_dn;
+                    const bool rej_sure = x + e2u < lo_dn || x - e2u >= hi_up;
+                    // straddling a bound (or NaN): the fp64 draw decides from attempt 0
+                    list = !acc_sure;
+                    flag = rej_sure ? 0 : kFrom0;
+                }
+            }
+            xf[r + h] = x;
+            ef[r + h] = e;
+            const uint64_t m = __ballot(list);
+            pos[r + h] = list ? run + (int)lanes_below(m) : kAccepted;
+            if (list) seg[pos[r + h]] = (uint16_t)((c0 + (uint32_t)h) | flag);
+            run += (int)__popcll(m);
+        }
+    }
+    bool ok = true;
+    if (bounded) {
+        if (lane == 0) q.wn[wave] = run;
+        __syncthreads();
+        int b[kTileWaves + 1];
+        b[0] = 0;
+#pragma unroll
+        for (int w = 0; w < kTileWaves; ++w) b[w + 1] = b[w] + q.wn[w];
+        const int n = b[kTileWaves];
+        const int mine = b[wave];
+        if (n == 0) __syncthreads();
+        for (int c0 = 0; c0 < n; c0 += CAP) {
+            const int c1 = min(n, c0 + CAP);
+            for (int e = c0 + (int)threadIdx.x; e < c1; e += blockDim.x) {
+                int w = 0;
+#pragma unroll
+                for (int k = 1; k < kTileWaves; ++k) w += e >= b[k] ? 1 : 0;
+                int bw = b[0];
+#pragma unroll
+                for (int k = 1; k < kTileWaves; ++k) bw = w == k ? b[k] : bw;
+                const uint16_t ent = q.slot[w * (R * 64) + (e - bw)];
+                const uint32_t gg = g0 + (uint32_t)(ent & 0x7FFFu);
+                double v = __builtin_nan("");
+                int32_t a = -1;
+                for (uint32_t it = (ent & kFrom0) ? 0u : 1u; it < kMaxAttempts; ++it) {
+                    const double draw = draw_attempt(L, src, k0, k1, gg, it, rk);
+                    if (L.low <= draw && draw < L.high) {
+                        v = draw;
+                        a = (int32_t)it;
+                        break;
+                    }
+                }
+                ok = ok && v == v;
+                q.val[e - c0] = v;
+                q.att[e - c0] = a;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t k = (uint32_t)(pos[r] + (mine - c0));
+                if (k < (uint32_t)(c1 - c0)) {
+                    // the fp64 draw's value and accepted attempt a, carried as
+                    // ef = -a (the cap: NaN value, ef = -1 -- k_hot_bx32 raises
+                    // the error flag through the return value)
+                    xf[r] = (float)q.val[k];
+                    ef[r] = q.att[k] < 0 ? -1.0f : -(float)q.att[k];
+                }
+            }
+            if (c1 < n) __syncthreads();
+        }
+    }
+    return ok;
+}
+
+// np.round(x / q) * q (round half to even), tpe.py:99 / :255
 __device__ __forceinline__ double quantize(double v, double q) { return rint(v / q) * q; }
 
 template <int MODE>

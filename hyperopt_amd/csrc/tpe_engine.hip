@@ -849,6 +849,25 @@ __device__ __forceinline__ void hot_wave_flush(int n, const int32_t* bi, const d
     __builtin_amdgcn_wave_barrier();   // (read before the buffer is refilled)
 }
 
+// hot_wave_flush for k_hot_bx32's (index, attempt) entries
+__device__ __forceinline__ void hot_wave_flush32(int n, const int32_t* bi, const int32_t* ba,
+                                                 int32_t* __restrict__ hcnt, int32_t* __restrict__ hidx,
+                                                 int32_t* __restrict__ hatt, size_t cell, int64_t hstride,
+                                                 int32_t* __restrict__ hflag) {
+    const int lane = threadIdx.x & 63;
+    int gb = 0;
+    if (lane == 0) gb = atomicAdd(hcnt + cell, n);
+    gb = __builtin_amdgcn_readfirstlane(__shfl(gb, 0));
+    if (lane == 0 && gb + n > hstride) atomicOr(hflag, 2);
+    __builtin_amdgcn_wave_barrier();
+    for (int k = lane; k < n; k += 64)
+        if (gb + k < hstride) {
+            hidx[cell * (size_t)hstride + gb + k] = bi[k];
+            hatt[cell * (size_t)hstride + gb + k] = ba[k];
+        }
+    __builtin_amdgcn_wave_barrier();
+}
+
 // LDS_BITS: every label's bits fit in LDS (the host knows the largest
 // label's sub-bins) -- the bit test is then a ds_read; otherwise every
 // label reads them from global memory.  (One kernel choosing per label
@@ -954,6 +973,128 @@ __global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
         }
 }
 
+// k_hot_bx with the fp32 draw (sample_tile32; TPE_OPT_HOT32, the default):
+// every candidate drawn in fp32 with its bound |xf - x64| <= ef, its fp64
+// sub-bin index located within [floor(f - ef'), floor(f + ef')] (ef' adds
+// the fp32 roundings of the index and the fp64 index's own), and the
+// candidate listed when ANY sub-bin it can fall in has its bit -- or it can
+// lie outside the bins -- so the list holds every candidate the fp64 draw
+// would have listed (and, near a sub-bin edge, a few more: harmless, tau is
+// taken over the listed candidates' own fp64 sub-bins, a lower bound of
+// their scores either way).  The list keeps (index, accepted attempt):
+// k_screen_hot re-draws the value in fp64.  No Box-Muller tables in LDS:
+// the fp64 draws (retries, decisions at a truncation bound) read the
+// constant ones.
+template <int R, bool LDS_BITS>
+__global__ __launch_bounds__(kBlock, 5) void k_hot_bx32(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
+    const BxLabel* __restrict__ bx, const uint32_t* __restrict__ hbits, int64_t n, int64_t cand_offset,
+    uint64_t seed, const uint32_t* __restrict__ rounds, int32_t nl, int32_t* __restrict__ hcnt,
+    int32_t* __restrict__ hidx, int32_t* __restrict__ hatt, int32_t* __restrict__ err, int64_t hstride,
+    int32_t* __restrict__ hflag, float escale) {
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    const BxLabel B = bx[li];
+    __shared__ SampLds sl;
+    (void)stage_samp(L, samp, &sl);   // (the launch checked ns <= kSampLds; its barrier covers sbits below)
+    const int nsb = B.nbins * kBxSub;
+    const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
+    const uint32_t rk = rounds[blockIdx.z];
+    constexpr int64_t per = (int64_t)R * kBlock;
+    __shared__ uint32_t sbits[LDS_BITS ? kHotLdsWords : 1];
+    if constexpr (LDS_BITS)
+        for (int w = threadIdx.x; w < (nsb >> 5); w += kBlock) sbits[w] = hbits[(B.sb_off >> 5) + w];
+    const uint32_t* __restrict__ gbits = hbits + (B.sb_off >> 5);
+    __shared__ RetryLds32<R> retry;
+    __shared__ int32_t buf_i[kBlock / 64][kHotBuf];
+    __shared__ int32_t buf_a[kBlock / 64][kHotBuf];
+    __syncthreads();   // the bits above
+    // the fp64 sub-bin index f = (x - centre - xlo) inv_sbw, in fp32: the
+    // base and scale rounded once (their errors go into the margin)
+    const double base64 = L.centre + B.xlo;
+    const float base = (float)base64, isbw = (float)B.inv_sbw;
+    const float eb = (float)fabs((double)base - base64) * 1.0001f;
+    const float fsb = (float)nsb;
+    const int wv = threadIdx.x >> 6;
+    int wn = 0;   // this wave's buffered entries (wave-uniform)
+    const int steps = __builtin_amdgcn_readfirstlane(sl.steps);
+    const SampShared src{&sl, kCosSinTab, kLogTab, steps};
+    for (int64_t base_i = (int64_t)blockIdx.x * per; base_i < n; base_i += (int64_t)gridDim.x * per) {
+        float xf[R], ef[R];
+        uint32_t pend = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (base_i + (int64_t)tile_cand(r, threadIdx.x, kBlock) < n) pend |= 1u << r;
+        const uint32_t g0 = (uint32_t)(cand_offset + base_i);
+        if (!sample_tile32<R>(L, src, seed, rk, g0, pend, xf, ef, retry, escale)) atomicOr(err, 1);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            bool take = false;
+            if ((pend >> r) & 1u) {
+                const float x = xf[r];
+                const float fv = (x - base) * isbw;
+                // |fv - f64| <= (ef + eb + the subtraction's and the
+                // scale's roundings, and an exact value's fp32 rounding)
+                // isbw + the product's rounding + the fp64 index's own
+                // (~1e-16 relative, inside the 2^-21)
+                const float ax = __builtin_fabsf(x) + __builtin_fabsf(base);
+                const float em = 1.01f * ((fmaxf(ef[r], 0.0f) + eb + 0x1.0p-21f * ax) * isbw +
+                                          0x1.0p-21f * __builtin_fabsf(fv)) +
+                                 0x1.0p-20f;
+                const float flo = fv - em, fhi = fv + em;
+                if (flo >= 0.0f && fhi < fsb) {   // (false for NaN: listed)
+                    const int jlo = (int)flo, jhi = (int)fhi;
+                    if (jhi - jlo > 1) {
+                        take = true;   // (a bound wider than a sub-bin: listed)
+                    } else {
+                        uint32_t wlo, whi;
+                        if constexpr (LDS_BITS) {
+                            wlo = sbits[jlo >> 5];
+                            whi = sbits[jhi >> 5];
+                        } else {
+                            wlo = gbits[jlo >> 5];
+                            whi = gbits[jhi >> 5];
+                        }
+                        take = ((wlo >> (jlo & 31)) | (whi >> (jhi & 31))) & 1u;
+                    }
+                } else {
+                    take = true;   // possibly outside the bins (or NaN): always listed
+                }
+            }
+            const uint64_t bal = __ballot(take);
+            if (!bal) continue;
+            const int c = __builtin_amdgcn_readfirstlane((int)__popcll(bal));
+            if (wn + c > kHotBuf) {   // (wave-uniform)
+                hot_wave_flush32(wn, buf_i[wv], buf_a[wv], hcnt, hidx, hatt, cell, hstride, hflag);
+                wn = 0;
+            }
+            if (take) {
+                const int k = wn + (int)lanes_below(bal);
+                buf_i[wv][k] = (int32_t)(base_i + (int64_t)tile_cand(r, threadIdx.x, kBlock));
+                buf_a[wv][k] = ef[r] < 0.0f ? (int32_t)(-ef[r]) : 0;   // the accepted attempt
+            }
+            wn += c;
+        }
+    }
+    __shared__ int wcnt[kBlock / 64], wbase;
+    if ((threadIdx.x & 63) == 0) wcnt[wv] = wn;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) tot += wcnt[w];
+        wbase = tot ? atomicAdd(hcnt + cell, tot) : 0;
+        if (tot && wbase + tot > hstride) atomicOr(hflag, 2);
+    }
+    __syncthreads();
+    int off = wbase;
+    for (int w = 0; w < wv; ++w) off += wcnt[w];
+    for (int k = threadIdx.x & 63; k < wn; k += 64)
+        if (off + k < hstride) {
+            hidx[cell * (size_t)hstride + off + k] = buf_i[wv][k];
+            hatt[cell * (size_t)hstride + off + k] = buf_a[wv][k];
+        }
+}
+
 // k_hot_bx's lists as work items of R * 256 listed candidates (the passes
 // of k_screen_hot): pre[c] = the first item of cell c (cell c has
 // ceil(min(hcnt[c], hstride) / (R 256)) of them), pre[cells] = all; one
@@ -1009,7 +1150,8 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
     const int32_t* __restrict__ hcnt, const int32_t* __restrict__ hidx, const double* __restrict__ hx,
     double* __restrict__ hi, unsigned long long* __restrict__ lbkey, int32_t* __restrict__ cnt,
     int32_t* __restrict__ idx, unsigned long long* __restrict__ terms, const float2* __restrict__ sb,
-    unsigned long long* __restrict__ tkey, int64_t hstride) {
+    unsigned long long* __restrict__ tkey, int64_t hstride, const int32_t* __restrict__ hatt,
+    const SampRec* __restrict__ samp, uint64_t seed, const uint32_t* __restrict__ rounds, int64_t cand_offset) {
     constexpr int64_t per = (int64_t)R * kBlock;
     __shared__ double exp_tab[kExpTabSize];
     __shared__ int item_sh;
@@ -1036,6 +1178,7 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
         const BxLabel B = bx[li];
         const bool lgmm = L.mode == DENSE_LGMM;
         const int64_t nsb = (int64_t)B.nbins * kBxSub;
+        const uint32_t rk = hatt ? rounds[cell / (size_t)nl] : 0u;
         uint64_t kl = 0;   // the largest sub-bin L of the listed candidates
         double x[R];
         int64_t ci[R];
@@ -1044,7 +1187,18 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
         for (int r = 0; r < R; ++r) {
             const int64_t j = j0 + r * kBlock + threadIdx.x;
             valid[r] = j < m;
-            const double d = valid[r] ? hx[cell * (size_t)hstride + j] : 0.0;   // the raw draw
+            double d = 0.0;   // the raw draw
+            if (valid[r]) {
+                if (hatt) {   // k_hot_bx32's (index, attempt): the fp64 draw again, bit for bit
+                    const int32_t a = hatt[cell * (size_t)hstride + j];
+                    const uint32_t g = (uint32_t)(cand_offset + hidx[cell * (size_t)hstride + j]);
+                    d = a >= 0 ? draw_attempt(L, SampGlobal{samp + L.samp_off, L.ns}, (uint32_t)seed,
+                                              (uint32_t)(seed >> 32), g, (uint32_t)a, rk)
+                               : __builtin_nan("");   // (the attempt cap: k_hot_bx32 raised err)
+                } else {
+                    d = hx[cell * (size_t)hstride + j];
+                }
+            }
             x[r] = lgmm ? lgmm_value(d) : d;
             ci[r] = valid[r] ? hidx[cell * (size_t)hstride + j] : 0;
             const double f = (d - L.centre - B.xlo) * B.inv_sbw;   // k_hot_bx's sub-bin
@@ -1242,6 +1396,10 @@ constexpr int kBxR = TPE_BX_R;
 #define TPE_HOT_R 6   // (8 spilled 8 VGPRs at the 96-register cap: 48 MB of scratch writes per round, r4aj)
 #endif
 constexpr int kHotR = TPE_HOT_R;
+#ifndef TPE_HOT_R32
+#define TPE_HOT_R32 4   // k_hot_bx32 (fp32 draw)
+#endif
+constexpr int kHotR32 = TPE_HOT_R32;
 constexpr unsigned kHotScreenWgs = 1024;   // k_screen_hot's persistent grid (4 workgroups per CU: LDS)
 #ifndef TPE_HOT_WGS
 #define TPE_HOT_WGS 16384
@@ -3453,7 +3611,8 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
             HIPCHK(ctx, ctx->win_evals.reserve(1));
             add_fill(fs, ctx->win_evals.p, sizeof(unsigned long long), 0);
             if (hot) {
-                HIPCHK(ctx, ctx->hot_x.reserve(cells * lst));
+                if (ctx->hot32) HIPCHK(ctx, ctx->hot_a.reserve(cells * lst));
+                else HIPCHK(ctx, ctx->hot_x.reserve(cells * lst));
                 HIPCHK(ctx, ctx->hot_i.reserve(cells * lst));
                 HIPCHK(ctx, ctx->hot_cnt.reserve(cells));
                 HIPCHK(ctx, ctx->hot_t.reserve(cells));
@@ -3480,12 +3639,24 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                 // (a workgroup stages its tables first: a label shard's few
                 // cells at one or two tiles per workgroup ran 0.54 ms instead
                 // of 0.46) unless the chip needs more to fill it
-                const int64_t tiles_c = (a.n + kHotR * kBlock - 1) / (kHotR * kBlock);
+                const int64_t hr = ctx->hot32 ? kHotR32 : kHotR;
+                const int64_t tiles_c = (a.n + hr * kBlock - 1) / (hr * kBlock);
                 const int64_t per_cell = std::min<int64_t>(
                     {tiles_c, kHotBxWgs / cells_l,
                      std::max<int64_t>((kHotFillWgs + cells_l - 1) / cells_l, tiles_c / kHotMinTiles)});
                 const dim3 hg((unsigned)std::max<int64_t>(1, per_cell), nl, a.gz);
-                if (P.bx_sb_max <= (int64_t)kHotLdsWords * 32)
+                if (ctx->hot32) {
+                    if (P.bx_sb_max <= (int64_t)kHotLdsWords * 32)
+                        hipLaunchKernelGGL((k_hot_bx32<kHotR32, true>), hg, dim3(kBlock), 0, ctx->stream, P.labels.p,
+                                           grp, P.samp.p, P.bx.p, ctx->hot_bits.p, a.n, a.cand_offset, a.seed,
+                                           ctx->rounds.p, nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_a.p,
+                                           ctx->errflag.p, lst, ctx->hot_flag.p, ctx->hot32 == 2 ? 4096.0f : 1.0f);
+                    else
+                        hipLaunchKernelGGL((k_hot_bx32<kHotR32, false>), hg, dim3(kBlock), 0, ctx->stream, P.labels.p,
+                                           grp, P.samp.p, P.bx.p, ctx->hot_bits.p, a.n, a.cand_offset, a.seed,
+                                           ctx->rounds.p, nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_a.p,
+                                           ctx->errflag.p, lst, ctx->hot_flag.p, ctx->hot32 == 2 ? 4096.0f : 1.0f);
+                } else if (P.bx_sb_max <= (int64_t)kHotLdsWords * 32)
                     hipLaunchKernelGGL((k_hot_bx<kHotR, true>), hg, dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
                                        P.samp.p, P.bx.p, ctx->hot_bits.p, a.n, a.cand_offset, a.seed, ctx->rounds.p,
                                        nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p, ctx->errflag.p, lst,
@@ -3502,7 +3673,9 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                                    P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p, P.bx_loff.p, P.bx_list.p, a.n,
                                    nl, (int64_t)cells, ctx->hot_items.p, ctx->hot_items.p + cells + 1,
                                    ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p, ctx->scr_hid.p, ctx->scr_lb.p,
-                                   ctx->scr_cnt.p, ctx->scr_idx.p, ctx->win_evals.p, P.bx_sb.p, ctx->hot_t.p, lst);
+                                   ctx->scr_cnt.p, ctx->scr_idx.p, ctx->win_evals.p, P.bx_sb.p, ctx->hot_t.p, lst,
+                                   ctx->hot32 ? ctx->hot_a.p : nullptr, P.samp.p, a.seed, ctx->rounds.p,
+                                   a.cand_offset);
             } else {
                 screen_bx_all(ctx, grp, nl, a);
             }
@@ -4866,6 +5039,7 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
         case TPE_OPT_EARLY: ctx->early = value != 0; break;
         case TPE_OPT_ZERO_WIN: ctx->zero_win = value != 0; break;
         case TPE_OPT_VALUE_ONLY: ctx->value_only = value != 0; break;
+        case TPE_OPT_HOT32: ctx->hot32 = (int32_t)value; break;
         case TPE_OPT_MODE_MASK:
             if (value < 1 || value > 31) return ctx->fail(TPE_ERR_ARG, "family mask must be in [1, 31]");
             ctx->mode_mask = (int32_t)value;

@@ -418,7 +418,7 @@ class Engine(object):
                'hot': L.TPE_OPT_HOT, 'early': L.TPE_OPT_EARLY, 'hot_div': L.TPE_OPT_HOT_DIV,
                'zero_win': L.TPE_OPT_ZERO_WIN, 'value_only': L.TPE_OPT_VALUE_ONLY,
                'rescore_cap': L.TPE_OPT_RESCORE_CAP, 'mode_mask': L.TPE_OPT_MODE_MASK,
-               'aux_families': L.TPE_OPT_AUX_FAMILIES}
+               'aux_families': L.TPE_OPT_AUX_FAMILIES, 'hot32': L.TPE_OPT_HOT32}
 
     def set_option(self, name, value):
         """Engine switches (include/hyperopt_tpe.h TPE_OPT_*): 'screen',

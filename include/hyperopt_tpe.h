@@ -496,8 +496,13 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *                   labels on the context's second stream, beside the dense
  *                   labels' draw (joined before the reduction; results
  *                   unchanged; single-device contexts).  Their early exit's
- *                   draw counts (tpe_last_drawn, the families' evals) then
- *                   depend on the interleaving                            [0]
+ *                   draw counts (tpe_last_drawn, the families' evals) are
+ *                   those of a scan in index order either way              [0]
+ *   TPE_OPT_HOT32   the hot-bin prefilter draws every candidate in fp32
+ *                   with a rigorous bound on its distance from the fp64
+ *                   draw and lists (index, accepted attempt); the listed
+ *                   candidates are re-drawn in fp64 (0: the fp64 draw
+ *                   kernel; 2: every bound x 4096, tests)                 [1]
  *   TPE_OPT_WIN_GROUPS  label groups of a windowed round, each sorted on a
  *                   second stream while the previous one is screened
  *                   (0: one group; the chip is busy either way)          [0]
@@ -530,6 +535,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_RESCORE_CAP 17
 #define TPE_OPT_MODE_MASK 18
 #define TPE_OPT_AUX_FAMILIES 19
+#define TPE_OPT_HOT32 20
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
 
 /* Build now what the resident posterior's first round(s) of n_candidates

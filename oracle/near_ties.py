@@ -140,3 +140,34 @@ def summary(cells):
         'max_abs_hip_minus_numpy_dense': max((c['max_abs_diff'] for c in dense), default=None),
         'min_span_dense': min((c['span'] for c in dense), default=None),
     }
+
+
+def batched_agreement(eng, posts, res, seed, ids, C, rows, streams=None):
+    """Config 5's batched rounds (packed map, C = 24 candidates per (new_id,
+    label) cell) against the C restatement of the reference's scoring
+    (oracle/tpe_score.c, OpenMP): for every label and each row j in `rows`
+    of res ([len(ids)][labels] results of suggest_batch(seed, ids, C)), the
+    C candidates of round ids[j] re-drawn through the sampler entry points,
+    scored under l and g in fp64, and broadcast_best's argmax (tpe.py:769-778)
+    compared with the round's index and value (a value-only round reports
+    those two for every cell).  Returns the per-cell agreement records."""
+    from . import c_oracle as Cor
+    cells = []
+    for j in rows:
+        rnd = int(ids[j])
+        for li, p in enumerate(posts):
+            stream = li if streams is None else int(streams[li])
+            x = _draw(eng, p, stream, seed, rnd, C)
+            if p.family == 'categorical':
+                xi = x.astype(np.int64)
+                lb, la = Cor.categorical_lpdf(xi, p.below), Cor.categorical_lpdf(xi, p.above)
+            else:
+                f = Cor.gmm1_lpdf if p.family == 'GMM1' else Cor.lgmm1_lpdf
+                lb = f(x, *p.below, low=p.low, high=p.high, q=p.q)
+                la = f(x, *p.above, low=p.low, high=p.high, q=p.q)
+            best = Cor.broadcast_best_index(lb, la)
+            r = res[j][li]
+            cells.append({'row': int(j), 'label': li, 'family': p.family,
+                          'agree': int(r['index']) == best and float(r['value']) == float(x[best]),
+                          'hip': int(r['index']), 'oracle': best})
+    return cells

@@ -16,6 +16,7 @@
 #   py=<script,args> any python script of the tree (commas for spaces)
 #   ubench           tools/ubench_issue (built beforehand): VALU issue costs -> issue_costs.json
 #   listpmc          rocprofv3 --list-avail (the counters this box offers)
+#   bm32             tools/ubench_bm32 (built beforehand): exhaustive fp32 Box-Muller error sweep
 set -u
 T=${1:?tag}
 shift
@@ -64,6 +65,9 @@ for s in "$@"; do
             echo "== ubench"
             timeout -k 10 120 tools/ubench_issue > "$OUT/issue_costs.json" 2> "$OUT/ubench.err" || { cat "$OUT/ubench.err"; exit 1; }
             cat "$OUT/issue_costs.json" ;;
+        bm32)
+            run bm32 300 tools/ubench_bm32 || exit 1
+            grep -q "BOUNDS HOLD" "$OUT/bm32.log" || { echo "fp32 Box-Muller bounds violated"; exit 1; } ;;
         listpmc)
             run listpmc 120 rocprofv3 --list-avail || exit 1 ;;
         py=*)
