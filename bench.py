@@ -108,10 +108,17 @@ def parse():
                     help='one process, one multi-device context over these HIP ordinals '
                          '(e.g. 0,1,2,3; tpe_ctx_create_multi): the 1..8-GPU curve without '
                          'torchrun; a repeated ordinal shares that GPU (tests)')
-    ap.add_argument('--shard', default='auto', choices=['auto', 'labels', 'candidates'],
+    ap.add_argument('--shard', default='auto', choices=['auto', 'labels', 'candidates', 'descriptors'],
                     help='N > 1: label shards (each rank holds a subset of the labels: their '
                          'history, posterior, index and whole rounds; auto when every rank gets at '
-                         'least one label) or candidate shards (every label, C/N candidates each)')
+                         'least one label), candidate shards (every label, C/N candidates each) or '
+                         'descriptors (label shards build the posteriors and index, one all-gather '
+                         'shares them, candidate shards score: parallel.DescriptorExchange)')
+    ap.add_argument('--hot32', type=int, default=None,
+                    help='TPE_OPT_HOT32: the prefilter\'s fp32 draw (1, the library default) or the fp64 '
+                         'draw kernel (0)')
+    ap.add_argument('--bx-split', type=int, default=None,
+                    help='TPE_OPT_BX_SPLIT: workgroups per 64-bin block of the index tables (0 = auto)')
     ap.add_argument('--dist-backend', default='nccl',
                     help='nccl (RCCL over xGMI); gloo only to rehearse N ranks on one GPU')
     ap.add_argument('--no-agreement', action='store_true',
@@ -220,6 +227,8 @@ def other_configs(args):
             continue
         d = json.loads(lines[-1])
         st, pr = d.get('step') or {}, d.get('scaling_projection') or {}
+        dp = d.get('scaling_projection_descriptors') or {}
+        ag = d.get('oracle_near_tie_agree') or d.get('oracle_batched_agree')
         out['config%d' % cfg] = {
             'workload': d['config']['workload'], 'value': d['value'], 'unit': d['unit'],
             'fresh_step_ms': round(d['ms_per_step'], 3), 'warm_round_ms': st.get('warm_round_ms'),
@@ -228,7 +237,10 @@ def other_configs(args):
             'projected_8gpu_efficiency_fresh': pr.get('projected_8gpu_efficiency_fresh'),
             'projected_8gpu_efficiency_warm': pr.get('projected_8gpu_efficiency_warm'),
             'projection_partition': pr.get('partition'),
+            'projected_8gpu_efficiency_fresh_descriptors': dp.get('projected_8gpu_efficiency_fresh'),
+            'projected_8gpu_efficiency_warm_descriptors': dp.get('projected_8gpu_efficiency_warm'),
             'rescored_per_step': (d.get('screen') or {}).get('rescored_per_step'),
+            'oracle_agree': {k: ag.get(k) for k in ('cells', 'agree', 'rate')} if ag else None,
             'child_wall_s': round(wall, 1)}
     return out
 
@@ -303,6 +315,26 @@ def near_tie_leg(eng, hist_full, res, seed, rnd, C):
                       'numpy_top2_gap = numpy\'s own best-minus-second score among the near-ties, '
                       'max_abs_hip_minus_numpy = the largest |HIP fp64 - numpy| score difference seen'})
     return d
+
+
+def batched_oracle_leg(eng, hist_full, res, seed, ids, C, n_rows=8):
+    """Config 5's oracle leg (test infra, untimed): n_rows random rounds of
+    the first warm step x every label, the 24 candidates re-drawn and scored
+    by the C restatement of the reference (oracle/tpe_score.c) -- numpy's
+    broadcast_best argmax must be the round's index and value
+    (oracle/near_ties.batched_agreement)."""
+    from oracle import near_ties as NT
+    t0 = time.perf_counter()
+    posts = NT.posteriors_of(eng, hist_full.labels)
+    rows = np.random.RandomState(11).choice(len(ids), min(n_rows, len(ids)), replace=False)
+    cells = NT.batched_agreement(eng, posts, res, seed, ids, C, rows)
+    agree = sum(c['agree'] for c in cells)
+    return {'cells': len(cells), 'agree': agree, 'rate': agree / max(len(cells), 1),
+            'rows': [int(r) for r in rows], 'wall_s': round(time.perf_counter() - t0, 1),
+            'note': 'config 5: %d random rounds of the first warm step x all labels; per cell the 24 '
+                    'candidates re-drawn and scored by oracle/tpe_score.c (the C restatement of '
+                    'tpe.py:110-172, 265-307, 56-63), broadcast_best argmax (tpe.py:769-778) vs the '
+                    'round\'s index and value' % len(rows)}
 
 
 def config1_fmin(n_reps=3):
@@ -381,6 +413,127 @@ def measured_pmc(kernel_prefix, summary_glob='r*_pmc_summary.json'):
                        'instr_per_eval': v.get('_valu_instr_per_eval'), 'clock_ghz': clk}
                 return {k: x for k, x in out.items() if x is not None}
     return {}
+
+
+def descriptor_projection(args, hist_full, dev, screen, value_only, C_total, p0, full_fresh_ms, full_warm_ms):
+    """One GPU running each rank's share of the descriptor-exchange step
+    (parallel.DescriptorExchange) in turn: max over shards of (append +
+    rebuild + index + export) + the import of all 8 blobs + one rank's slice
+    of the round (the slices cost alike: whole_n / whole_rounds keep the
+    whole round's size choices).  The two all-gathers are not run (one GPU):
+    the blobs' bytes are reported with a ring estimate beside."""
+    import torch
+    from hyperopt_amd.engine import Engine
+    from hyperopt_amd.parallel import _align, label_shards
+    from hyperopt_amd.workloads import FminLoop
+    world = 8
+    c5 = args.config == 5
+    rounds_total = args.new_ids if c5 else 1
+    shards = label_shards(hist_full.labels, world)
+
+    def opts(e):
+        for k, v in (('screen', int(screen)), ('window', int(not args.no_window)), ('win_t', args.win_t),
+                     ('win_groups', args.win_groups),
+                     ('value_only', value_only if c5 else 0), ('aux_families', 1 if c5 else 0)):
+            e.set_option(k, v)
+
+    engs, loops, blobs = [], [], []
+    per = []
+    try:
+        for sh in shards:
+            e = Engine(dev, args.precision)
+            engs.append(e)
+            opts(e)
+            lp = FminLoop(hist_full, label_ids=sh)
+            lp.advance(e, args.trials + (p0 - 1) * args.append)
+            loops.append(lp)
+            blobs.append(None)
+
+        def build(k, pos):
+            loops[k].advance(engs[k], args.trials + pos * args.append, n_candidates=C_total,
+                             n_rounds=rounds_total)
+            n = engs[k].export_size()
+            if blobs[k] is None or blobs[k].numel() < n:
+                blobs[k] = torch.empty(_align(n) + (1 << 20), dtype=torch.uint8, device='cuda')
+            return engs[k].export_posterior(blobs[k])
+
+        sizes = [0] * world
+        for k in range(world):
+            for w in (p0, p0 + 1):
+                build(k, w)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(args.steps):
+                sizes[k] = build(k, p0 + 2 + i)
+            torch.cuda.synchronize()
+            per.append((time.perf_counter() - t0) / args.steps * 1e3)
+        slot = _align(max(sizes))
+        allb = torch.empty(world * slot, dtype=torch.uint8, device='cuda')
+        for k in range(world):
+            allb[k * slot:k * slot + sizes[k]] = blobs[k][:sizes[k]]
+        for e in engs:
+            e.close()
+        engs = []
+        imp = Engine(dev, args.precision)
+        engs.append(imp)
+        opts(imp)
+        offs = [k * slot for k in range(world)]
+        imp.import_posterior(allb, offs, shards)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            imp.import_posterior(allb, offs, shards)
+        torch.cuda.synchronize()
+        t_imp = (time.perf_counter() - t0) / args.steps * 1e3
+        if c5:
+            imp.set_option('whole_rounds', args.new_ids)
+            nloc = args.new_ids // world
+
+            def rnd(i):
+                return imp.suggest_batch(1234, list(range(i * args.new_ids, i * args.new_ids + nloc)), C_total)
+        else:
+            imp.set_option('whole_n', C_total)
+
+            def rnd(i):
+                return imp.suggest(1234 + i, C_total // world, round=i, cand_offset=0)
+        # (a fresh import: the first round builds the per-posterior caches
+        # the fresh step pays -- timed as such; the warm slice after it)
+        t_first = []
+        t_warm = []
+        for i in range(args.steps + 1):
+            imp.import_posterior(allb, offs, shards)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            rnd(p0 + i)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            rnd(p0 + i)
+            torch.cuda.synchronize()
+            if i:
+                t_first.append((t1 - t0) * 1e3)
+                t_warm.append((time.perf_counter() - t1) * 1e3)
+        t_first, t_warm = float(np.mean(t_first)), float(np.mean(t_warm))
+    finally:
+        for e in engs:
+            e.close()
+    # ring all-gather of the blobs over xGMI: 7 hops of one slot at ~64 GB/s
+    # achieved per link (MI355X_MICROARCH.md: 153 GB/s peak) + ~10 us a hop
+    gather_ms = 7 * (slot / 64e9 * 1e3 + 0.010)
+    fresh = max(per) + t_imp + t_first
+    return {'partition': 'descriptor exchange (label shards build, one all-gather of the posteriors, '
+                         '%s)' % ('new_id shards' if c5 else 'candidate shards, C/8 per label'),
+            'labels_per_shard': [len(sh) for sh in shards],
+            'build_export_ms_per_shard': [round(x, 3) for x in per],
+            'import_ms': round(t_imp, 3), 'slice_round_first_ms': round(t_first, 3),
+            'slice_round_warm_ms': round(t_warm, 3),
+            'blob_bytes_per_shard': sizes, 'allgather_estimate_ms': round(gather_ms, 3),
+            'fresh_step_ms_shard': round(fresh, 3), 'warm_round_ms_shard': round(t_warm, 3),
+            'projected_8gpu_efficiency_fresh': full_fresh_ms / (8.0 * fresh),
+            'projected_8gpu_efficiency_fresh_with_gather_estimate': full_fresh_ms / (8.0 * (fresh + gather_ms)),
+            'projected_8gpu_efficiency_warm': full_warm_ms / (8.0 * t_warm),
+            'note': 'one GPU running each rank\'s share in turn: T(whole) / (8 T(rank)), T(rank) = '
+                    'max_r(build_r + export_r) + import + the first slice round on the imported posterior '
+                    '(warm: the slice round); the all-gathers are estimated, not run -- a projection'}
 
 
 def roofline_lpdf(launch_ms, evals, args):
@@ -528,8 +681,19 @@ def main():
     # over 8 ranks project 0.25 / 0.28 against 0.14 / 0.15 as candidate shards)
     by_label = (args.shard == 'labels' or
                 (args.shard == 'auto' and len(hist_full.labels) >= max(world, 8 if world == 1 else 1)))
-    shards = label_shards(hist_full.labels, world) if by_label else None
-    if by_label:   # whole rounds of this rank's labels
+    # descriptor exchange: this rank builds its label shard's posteriors and
+    # index, every rank scores its candidate slice (config 5: its new_ids) of
+    # every label on the shared posterior
+    desc = args.shard == 'descriptors' and world > 1
+    if desc:
+        by_label = False
+    shards = label_shards(hist_full.labels, world) if (by_label or desc) else None
+    if desc:
+        ids_local = args.new_ids // world
+        C = C_total   # (the exchange slices every label's candidates: rank r's [r C/N, (r+1) C/N))
+        if args.config == 5 and args.new_ids % world:
+            raise SystemExit('--new-ids must divide over %d ranks' % world)
+    elif by_label:   # whole rounds of this rank's labels
         ids_local, C = args.new_ids, C_total
     elif args.config == 5:
         if args.new_ids % world:
@@ -541,9 +705,12 @@ def main():
         C = C_total // world
     L = len(posts)
 
-    from hyperopt_amd.parallel import DeviceExchange
-    xch = (DeviceExchange(eng, 'labels' if by_label else ('rounds' if args.config == 5 else 'candidates'),
-                          shards=shards, rank=rank) if dist is not None else None)
+    from hyperopt_amd.parallel import DescriptorExchange, DeviceExchange
+    if desc:
+        xch = DescriptorExchange(eng, shards, rank, split='rounds' if args.config == 5 else 'candidates')
+    else:
+        xch = (DeviceExchange(eng, 'labels' if by_label else ('rounds' if args.config == 5 else 'candidates'),
+                              shards=shards, rank=rank) if dist is not None else None)
 
     # fresh-posterior steps (default): each step appends the next trial(s) to
     # the device-resident history and rebuilds the posterior as tpe.suggest
@@ -551,9 +718,11 @@ def main():
     # posterior -- what every suggestion of fmin's loop pays
     loop = None
     fresh_mode = args.mode == 'fresh'
-    if fresh_mode or (by_label and world > 1):
-        loop = FminLoop(hist_full, label_ids=shards[rank] if by_label and world > 1 else None)
+    if fresh_mode or ((by_label or desc) and world > 1):
+        loop = FminLoop(hist_full, label_ids=shards[rank] if (by_label or desc) and world > 1 else None)
         loop.advance(eng, args.trials)        # untimed: the initial history, uploaded whole
+        if desc:
+            xch.share()                       # (warm mode: the shared posterior of that history)
     results = {}
 
     def step(i, fresh, n=None, e=None, lp=None, gather=True):
@@ -565,6 +734,20 @@ def main():
         lp = loop if lp is None else lp
         nc = C if n is None else n
         exchange = dist is not None and gather
+        if desc:
+            # this rank's labels rebuilt (their index queued for the whole
+            # round's size), the posteriors shared, this rank's slice scored
+            if fresh:
+                t0 = time.perf_counter()
+                lp.advance(e, args.trials + (i + 1) * args.append,
+                           n_candidates=C_total if args.precision == 'f64' else 0,
+                           n_rounds=args.new_ids if args.config == 5 else 1)
+                xch.share()
+                P._phase('step_total', t0)
+            if args.config == 5:
+                first_id = i * args.new_ids + rank * ids_local
+                return xch.round(1234, list(range(first_id, first_id + ids_local)), C)
+            return xch.round(1234 + i, [i], C)[0]
         off = 0 if by_label else rank * nc
         if args.config == 5:   # independent new_ids split over the GPUs (or each rank's labels)
             first_id = i * args.new_ids + (0 if by_label else rank * ids_local)
@@ -647,6 +830,10 @@ def main():
     aux_families = (args.aux_families if args.aux_families is not None
                     else int(not (dist is not None and not by_label and args.config != 5)))
     eng.set_option('aux_families', aux_families)
+    if args.hot32 is not None:
+        eng.set_option('hot32', args.hot32)
+    if args.bx_split is not None:
+        eng.set_option('bx_split', args.bx_split)
     eng.set_option('window', int(not args.no_window))
     eng.set_option('win_t', args.win_t)
     eng.set_option('win_groups', args.win_groups)
@@ -700,6 +887,11 @@ def main():
     if (rank == 0 and world == 1 and devs is None and not args.no_agreement and fresh_mode
             and args.config in (2, 3, 4) and args.precision == 'f64' and warm_first in results):
         agree_leg = near_tie_leg(eng, hist_full, results[warm_first], 1234 + warm_first, warm_first, C)
+    if (rank == 0 and world == 1 and devs is None and not args.no_agreement and fresh_mode
+            and args.config == 5 and args.precision == 'f64' and warm_first in results):
+        agree_leg = batched_oracle_leg(eng, hist_full, results[warm_first], 1234,
+                                       list(range(warm_first * args.new_ids, warm_first * args.new_ids + ids_local)),
+                                       C)
     # device memory after the timed steps: the library's buffers (their
     # high-water mark: they grow by 1/4 and are kept) and the whole device
     free_b, total_b = torch.cuda.mem_get_info()
@@ -758,6 +950,18 @@ def main():
             'note': 'one GPU running each rank\'s share of the 8-GPU step in turn: efficiency = '
                     'T(whole) / (8 max_r T(shard r)); the RCCL all-gather of the winners (48 B per '
                     'label) is not in it -- a projection, not a measured scaling curve'})
+    # the descriptor-exchange partition projected the same way: each rank's
+    # fresh build of its label shard (history append, posterior, index) and
+    # export, run shard by shard; one engine importing the 8 blobs, then its
+    # slice of the round (C/8 candidates of every label; config 5: 1/8 of
+    # the new_ids) -- the slowest build + import + slice
+    dproj = None
+    if (fresh_mode and world == 1 and devs is None and not args.no_projection and args.precision == 'f64'
+            and args.shard in ('auto', 'descriptors') and (args.config == 5 or C % 8 == 0)
+            and len(hist_full.labels) >= 8):
+        dproj = descriptor_projection(args, hist_full, local, screen, value_only, C_total,
+                                      warm_first + args.steps, dt / args.steps * 1e3,
+                                      wdt / args.steps * 1e3)
     # `value` counts EXECUTED (candidate, component) lpdf terms (BASELINE.md
     # section 3): quantized labels their grid-table evals, screened dense
     # labels the fp32 terms the screen summed plus the fp64 terms of the
@@ -791,7 +995,7 @@ def main():
         # the expansion screen (k_screen_hot); the bracket holds both
         dom_ms = scr[2]
         kprec = 'f64'
-        kname = 'k_hot_bx<'
+        kname = 'k_hot_bx<' if args.hot32 == 0 else 'k_hot_bx32<'
         kdesc = 'k_hot_bx + k_screen_hot (hot-bin prefilter of the expansion screen: every candidate ' \
                 'drawn and bounded by its sub-bin\'s score interval, the 0.5 % that can still win ' \
                 'scored by the expansion screen), GMM1+LGMM1 labels'
@@ -884,7 +1088,11 @@ def main():
         'config': {'workload': workload_name(args, C),
                    'labels': L, 'history': args.trials,
                    'candidates_per_label': C_total, 'candidates_per_label_per_gpu': C,
-                   'parallelism': ('label-sharded x%d (labels per rank: %s)'
+                   'parallelism': ('descriptor exchange x%d (posteriors of label shards %s all-gathered; '
+                                   '%s)' % (world, [len(sh) for sh in shards],
+                                            'new_id shards' if args.config == 5 else 'candidate shards')
+                                   if desc else
+                                   'label-sharded x%d (labels per rank: %s)'
                                    % (world, [len(sh) for sh in shards]) if by_label and world > 1 else
                                    ('new_id-sharded x%d' if args.config == 5
                                     else 'candidate-sharded x%d') % (len(devs) if devs else world))
@@ -918,6 +1126,7 @@ def main():
                   'fresh_posterior_round_ms': (round(post_build['device_call_ms'] + prep_ms
                                                      + dt / args.steps * 1e3, 3) if prep_ms else None)}),
         'scaling_projection': proj,
+        'scaling_projection_descriptors': dproj,
         'device_memory': mem,
         'posterior_build': dict(post_build, expansion_index_ms=(round(prep_ms, 3) if prep_ms else None),
                                 expansion_index_note='the first index of the run (bin tables, lists, '
@@ -1032,7 +1241,7 @@ def main():
                           'numpy restatement (oracle/tpe_oracle.py); %.1f s, %.3g evals'
                           % (L, args.cpu_sample, nsec, nev)}}
     if agree_leg is not None:
-        line['oracle_near_tie_agree'] = agree_leg
+        line['oracle_batched_agree' if args.config == 5 else 'oracle_near_tie_agree'] = agree_leg
     if others is not None:
         line['other_configs'] = others
     if rank == 0:

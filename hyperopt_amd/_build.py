@@ -22,7 +22,8 @@ SOURCES = [os.path.join(HERE, 'csrc', 'tpe_engine.hip'),
            os.path.join(HERE, 'csrc', 'tpe_build.hip'),
            os.path.join(HERE, 'csrc', 'tpe_multi.hip'),
            os.path.join(HERE, 'csrc', 'tpe_window.hip'),
-           os.path.join(HERE, 'csrc', 'tpe_expand.hip')]
+           os.path.join(HERE, 'csrc', 'tpe_expand.hip'),
+           os.path.join(HERE, 'csrc', 'tpe_share.hip')]
 DEPS = SOURCES + [os.path.join(HERE, 'csrc', 'tpe_device.h'),
                   os.path.join(HERE, 'csrc', 'tpe_ctx.h'),
                   os.path.join(HERE, 'csrc', 'tpe_exp_table.h'),

@@ -57,6 +57,7 @@ TPE_OPT_RESCORE_CAP = 17
 TPE_OPT_MODE_MASK = 18
 TPE_OPT_AUX_FAMILIES = 19
 TPE_OPT_HOT32 = 20
+TPE_OPT_BX_SPLIT = 21
 
 TPE_OBS_IDENTITY = 0
 TPE_OBS_LOG = 1
@@ -146,6 +147,8 @@ SIGNATURES = {
     'tpe_last_prepare': (ctypes.c_int, [_P, _P]),
     'tpe_hot_probe': (ctypes.c_int, [_P, ctypes.c_int32, _P, ctypes.c_int64, _P, _P, _P]),
     'tpe_screen_probe': (ctypes.c_int, [_P, _I32, _P, _I64, _P, _P]),
+    'tpe_export_posterior': (ctypes.c_int, [_P, _P, _I64, _P]),
+    'tpe_import_posterior': (ctypes.c_int, [_P, _P, _I64, _P, _I32, _P, _P]),
 }
 
 _lib = None

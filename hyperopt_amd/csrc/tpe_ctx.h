@@ -200,6 +200,7 @@ struct Posterior {
     DevBuf<double> bx_scan;              // per dense label position: range, a*, counts
     DevBuf<float2> bx_sb;                // hot-bin prefilter: per sub-bin (U, L) of the score
     DevBuf<float> bx_sbp;                //   and the below mixture's sampling mass of it
+    DevBuf<double> bx_part;              // k_bx_table's split-window partial sums
     int64_t bx_sb_max = 0;               //   the most sub-bins of one label
     uint64_t bx_gen = 0;                 // bumped by every build of the tables (never 0 once built)
     // what the index was built from (the dense labels' DLabel, records and
@@ -246,6 +247,7 @@ struct Posterior {
         bx_scan.release();
         bx_sb.release();
         bx_sbp.release();
+        bx_part.release();
         bx_snap_l.release();
         bx_snap_c.release();
         bx_snap_s.release();
@@ -415,6 +417,7 @@ struct tpe_ctx {
     DevBuf<double> hot_x;                // per cell: listed candidates' x (the fp64 draw kernel)
     DevBuf<int32_t> hot_a;               //   or their accepted attempts (k_hot_bx32: re-drawn in fp64)
     int32_t hot32 = 1;                   // TPE_OPT_HOT32: the prefilter draws in fp32 (k_hot_bx32; 2: bounds x 4096, tests)
+    int32_t bx_split = 0;                // TPE_OPT_BX_SPLIT (0: auto)
     DevBuf<int32_t> hot_i, hot_cnt;      //   their indices; per cell the count
     DevBuf<unsigned long long> hot_t, hot_tau0;   // per cell largest L; per label tau0
     DevBuf<uint32_t> hot_bits;           // per sub-bin: U >= tau0 (words at sb_off / 32)
@@ -494,6 +497,7 @@ struct tpe_ctx {
     // round gets the whole problem's size and the window exchange
     std::vector<tpe_ctx*> peers;
     std::shared_ptr<void> workers;       // one persistent host thread per peer (tpe_multi.hip)
+    std::shared_ptr<void> share;         // posterior export / import scratch (tpe_share.hip)
     int64_t hint_n = 0;                  // candidates per round over all shards (0: this call's)
     int32_t hint_rounds = 0;             // rounds over all shards (0: this call's)
     // the same, set by the caller for the life of the context (one process
@@ -560,6 +564,7 @@ int64_t win_rounds_per_batch(int64_t n, int32_t nl);
 // and lists of every dense label of the resident posterior (once per
 // posterior) and sets P->bx_ok when every dense label has one.
 int bx_prepare(tpe_ctx* ctx);
+uint64_t next_bx_gen();
 int bx_build(tpe_ctx* ctx);
 // Before a rebuild's final sync: queue the comparison of the rebuilt dense
 // labels against the index's snapshot (result in ctx->pin[0].bx_diff after the

@@ -335,10 +335,11 @@ __device__ __forceinline__ double bm_radius(uint32_t y, const double* __restrict
 // on CDNA4 and the fp64 log / sincos are ~25 operations each).  Their error
 // against the fp64 functions above is measured EXHAUSTIVELY -- every one of
 // the 2^32 words, tools/ubench_bm32.hip (profiles/r5*_bm32_sweep.txt) -- and
-// the bounds below cover the largest error found with a margin; k_hot_bx's
+// the bounds below cover the largest error found with a margin (r5d: radius
+// 2.48e-7 relative, cos / sin 1.88e-7 absolute; x1.6); k_hot_bx's
 // fp32 draw carries them into a per-candidate bound on |x32 - x64|.
-constexpr float kBm32RadRel = 2.0e-6f;    // |rad32 - rad64| <= kBm32RadRel rad64 (and 0 at rad64 = 0)
-constexpr float kBm32TrigAbs = 2.0e-6f;   // |cos32 - cos64|, |sin32 - sin64| <= kBm32TrigAbs
+constexpr float kBm32RadRel = 4.0e-7f;    // |rad32 - rad64| <= kBm32RadRel rad64 (and 0 at rad64 = 0)
+constexpr float kBm32TrigAbs = 3.0e-7f;   // |cos32 - cos64|, |sin32 - sin64| <= kBm32TrigAbs
 
 // -ln(u) for u = 1 - y 2^-32 (u01_open0's uniform) in fp32: for u <= 1/2
 // the exact integer m = 2^32 - y gives u = m 2^-32 (one fp32 rounding) and

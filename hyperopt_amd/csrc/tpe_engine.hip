@@ -5040,6 +5040,10 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
         case TPE_OPT_ZERO_WIN: ctx->zero_win = value != 0; break;
         case TPE_OPT_VALUE_ONLY: ctx->value_only = value != 0; break;
         case TPE_OPT_HOT32: ctx->hot32 = (int32_t)value; break;
+        case TPE_OPT_BX_SPLIT:
+            if (value < 0 || value > 8) return ctx->fail(TPE_ERR_ARG, "index window split must be in [0, 8]");
+            ctx->bx_split = (int32_t)value;
+            break;
         case TPE_OPT_MODE_MASK:
             if (value < 1 || value > 31) return ctx->fail(TPE_ERR_ARG, "family mask must be in [1, 31]");
             ctx->mode_mask = (int32_t)value;

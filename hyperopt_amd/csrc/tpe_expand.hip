@@ -274,14 +274,50 @@ __device__ __forceinline__ void wave_window(const Comp<double>* __restrict__ c, 
 // e^y <= e^Y (Y = 2 kappa D rmax), so the per-component terms of the bound
 // are accumulated as four sums and combined at the end (each term at least
 // what the per-component form gives).
+//
+// Split window (grid z = nsplit > 1, for occupancy: a config-3 index has
+// ~400 workgroups of 64 bins, one wave per SIMD): workgroup z sums the z-th
+// 64-aligned part of the window and stores its sums in part (split-major,
+// [z][sum][row]); k_bx_table_fin adds the parts in z order and writes the
+// rows.  The bound counts the nsplit - 1 extra additions.
 constexpr int kTabSums = kBxP + 3;   // A_0..A_14, S0, S1, S3
+constexpr int kPartSums = kTabSums + 1;   // + the window size W
 static_assert(3 * kTabSums * 64 <= kExpTabSize, "k_bx_table: 3 waves' partial sums in the exp table's LDS");
 constexpr int kBxChains = 4;   // components per step of k_bx_table (independent chains)
+constexpr int kBxMaxSplit = 8;
+
+__device__ __forceinline__ double bin_reach(const BxLabel& B, double x) {
+    return B.dwin * (1.0 + 1e-9) + (fabs(x) + B.dwin) * 1e-12;
+}
+
+// a bin's row: A_0..A_14 and Eabs from its sums (module comment)
+__device__ __forceinline__ void table_row(const BxLabel& B, int b, const double* A, double S0, double S1,
+                                          double S3, double W, int nsplit, double* __restrict__ tab) {
+    const double r = B.rmax, kap = B.kappa;
+    const double xb = B.xlo + ((double)b + 0.5) * B.bw, D = bin_reach(B, xb);
+    // every summed component has |d| <= D: |mu'| <= |xb| + D, and at most
+    // the window's W of them were summed
+    const double S2 = (fabs(xb) + D) * S0 * (1.0 + 1e-15);   // >= sum g |mu'|
+    // e^y <= 1 + y + y^2 for 0 <= y <= 1.79, else exp(y) (1 + 1e-6)
+    const double Y = 2.0 * kap * D * r, eY = Y <= 1.5 ? fma(Y, Y, 1.0 + Y) : exp(Y) * 1.000001;
+    const double G = eY * S0;                                  // sum_k g e^y
+    const double Rb = eY * B.rP * kInvFact[kBxP] * S3;         // truncation (Lagrange)
+    const double ERR = eY * (((3.0 * kBxP + 10.0) * kU + 2.6e-14) * S0 + 4.0 * kU * S1 +
+                             2.0 * kap * (D + r) * (S2 + (D + r) * S0) * 0x1.0p-51);
+    double* row = tab + (size_t)(B.tab_off + b) * kBxRow;
+#pragma unroll
+    for (int n = 0; n < kBxP; ++n) row[n] = A[n];
+    // the sums: each wave's sequential sum, then 3 additions (of <= W terms),
+    // then nsplit - 1 more (split window)
+    row[kBxP] = 1.02 * (Rb + ERR + (W + 6.0 + (double)(nsplit - 1) + 2.0 * kBxP + 8.0) * kU * G) + 1e-300;
+}
+
 __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ labels,
                                                      const int32_t* __restrict__ grp,
                                                      const Comp<double>* __restrict__ comps64,
                                                      const BxLabel* __restrict__ bx,
-                                                     double* __restrict__ tab) {
+                                                     double* __restrict__ tab, int nsplit,
+                                                     double* __restrict__ part, int64_t rows) {
     const int li = grp[blockIdx.y];
     const BxLabel B = bx[li];
     const int b0 = blockIdx.x * 64;   // the workgroup's first bin
@@ -292,9 +328,9 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
     load_exp_table(lds);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int b = b0 + lane, blast = min(b0 + 63, B.nbins - 1);
-    const double r = B.rmax, kap = B.kappa;
+    const double kap = B.kappa;
     auto centre = [&](int i) { return B.xlo + ((double)i + 0.5) * B.bw; };
-    auto reach = [&](double x) { return B.dwin * (1.0 + 1e-9) + (fabs(x) + B.dwin) * 1e-12; };
+    auto reach = [&](double x) { return bin_reach(B, x); };
     const double xb = centre(min(b, blast)), D = reach(xb);
     // (the window: records sorted by mu, so the clipped ones within D of
     // any of the workgroup's bins are a contiguous index range; margins cover
@@ -312,17 +348,20 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
     // added to the rounding term); the powers g (2 kappa d)^n by one
     // multiply each, A_n += that / n! (one rounding each, inside 3P + 10)
     const double inv_a = 1.0 / B.astar;
-    for (int kc = k0 + wave * 64; kc < k1; kc += kBlock) {
+    // this workgroup's part of the window: [ks, ke)
+    const int chunk = ((k1 - k0 + nsplit - 1) / nsplit + 63) & ~63;
+    const int ks = min(k1, k0 + (int)blockIdx.z * chunk), ke = min(k1, ks + chunk);
+    for (int kc = ks + wave * 64; kc < ke; kc += kBlock) {
         const int k = kc + lane;
         double mu_l = 0.0, c_l = -kInf;
-        if (k < k1) {
+        if (k < ke) {
             const Comp<double> rec = c[k];
             if (rec.a == B.astar) {
                 mu_l = rec.mu * inv_a;
                 c_l = rec.c * kExpScaleInv;
             }
         }
-        const int cnt = min(64, k1 - kc);
+        const int cnt = min(64, ke - kc);
         __builtin_amdgcn_wave_barrier();   // (the previous batch's reads come first: LDS is in order per wave)
         stage[wave][lane] = double2{mu_l, c_l};
         __builtin_amdgcn_wave_barrier();
@@ -388,21 +427,43 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
         S1 += p[(kBxP + 1) * 64];
         S3 += p[(kBxP + 2) * 64];
     }
-    // every summed component has |d| <= D: |mu'| <= |xb| + D, and at most
-    // the window's k1 - k0 of them were summed
-    const double S2 = (fabs(xb) + D) * S0 * (1.0 + 1e-15);   // >= sum g |mu'|
-    const double W = (double)(k1 - k0);
-    // e^y <= 1 + y + y^2 for 0 <= y <= 1.79, else exp(y) (1 + 1e-6)
-    const double Y = 2.0 * kap * D * r, eY = Y <= 1.5 ? fma(Y, Y, 1.0 + Y) : exp(Y) * 1.000001;
-    const double G = eY * S0;                                  // sum_k g e^y
-    const double Rb = eY * B.rP * kInvFact[kBxP] * S3;         // truncation (Lagrange)
-    const double ERR = eY * (((3.0 * kBxP + 10.0) * kU + 2.6e-14) * S0 + 4.0 * kU * S1 +
-                             2.0 * kap * (D + r) * (S2 + (D + r) * S0) * 0x1.0p-51);
-    double* row = tab + (size_t)(B.tab_off + b) * kBxRow;
+    if (nsplit > 1) {   // (coalesced over the bins: [z][sum][row])
+        double* q = part + (size_t)blockIdx.z * kPartSums * rows + B.tab_off + b;
 #pragma unroll
-    for (int n = 0; n < kBxP; ++n) row[n] = A[n];
-    // the sums: each wave's sequential sum, then 3 additions (of <= W terms)
-    row[kBxP] = 1.02 * (Rb + ERR + (W + 6.0 + 2.0 * kBxP + 8.0) * kU * G) + 1e-300;
+        for (int n = 0; n < kBxP; ++n) q[(size_t)n * rows] = A[n];
+        q[(size_t)(kBxP + 0) * rows] = S0;
+        q[(size_t)(kBxP + 1) * rows] = S1;
+        q[(size_t)(kBxP + 2) * rows] = S3;
+        q[(size_t)(kBxP + 3) * rows] = (double)(k1 - k0);
+        return;
+    }
+    table_row(B, b, A, S0, S1, S3, (double)(k1 - k0), 1, tab);
+}
+
+// grid (ceil(max bins / 256), dense labels): a split window's parts added in
+// z order, the rows written
+__global__ __launch_bounds__(kBlock) void k_bx_table_fin(const int32_t* __restrict__ grp,
+                                                         const BxLabel* __restrict__ bx,
+                                                         double* __restrict__ tab, int nsplit,
+                                                         const double* __restrict__ part, int64_t rows) {
+    const BxLabel B = bx[grp[blockIdx.y]];
+    const int b = blockIdx.x * kBlock + threadIdx.x;
+    if (b >= B.nbins) return;
+    double A[kBxP], S[3];
+    const double* q = part + B.tab_off + b;
+#pragma unroll
+    for (int n = 0; n < kBxP; ++n) A[n] = q[(size_t)n * rows];
+#pragma unroll
+    for (int n = 0; n < 3; ++n) S[n] = q[(size_t)(kBxP + n) * rows];
+    const double W = q[(size_t)(kBxP + 3) * rows];
+    for (int z = 1; z < nsplit; ++z) {
+        const double* qz = q + (size_t)z * kPartSums * rows;
+#pragma unroll
+        for (int n = 0; n < kBxP; ++n) A[n] += qz[(size_t)n * rows];
+#pragma unroll
+        for (int n = 0; n < 3; ++n) S[n] += qz[(size_t)(kBxP + n) * rows];
+    }
+    table_row(B, b, A, S[0], S[1], S[2], W, nsplit, tab);
 }
 
 // lo += the smallest, hi += the largest value of one component's term
@@ -690,6 +751,13 @@ bool tpe_rt::bx_keep_after(tpe_ctx* ctx, bool groups_changed) {
     return P.bx_ready && P.bx_snap_nl > 0 && !groups_changed && ctx->pin[0].bx_diff == 0;
 }
 
+// unique over every posterior of the process (an index built here or
+// imported, tpe_share.hip): the hot-bin caches are keyed by it
+uint64_t tpe_rt::next_bx_gen() {
+    static uint64_t gen_counter = 0;
+    return __atomic_add_fetch(&gen_counter, 1, __ATOMIC_RELAXED);
+}
+
 // The index is queued on the context's stream without waiting for it (one
 // short round trip for the layout): a caller can overlap it with host work
 // (tpe_prepare).  Its device time is bracketed by events and read when asked.
@@ -797,11 +865,18 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
     const dim3 gb((unsigned)((bins_max + kBlock - 1) / kBlock), nl);
     hipLaunchKernelGGL(k_bx_list, gb, dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p, P.bx.p,
                        P.bx_nc.p, P.bx_loff.p, P.bx_list.p);
-    hipLaunchKernelGGL(k_bx_table, dim3((unsigned)((bins_max + 63) / 64), nl), dim3(kBlock), 0, ctx->stream,
-                       P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p);
+    // the window split for occupancy: >= ~2048 workgroups (4 per CU, LDS-bound, x2)
+    const int64_t wgs = (rows + 63) / 64;
+    const int nsplit = ctx->bx_split > 0 ? std::min(ctx->bx_split, kBxMaxSplit)
+                                         : (int)std::max<int64_t>(1, std::min<int64_t>(kBxMaxSplit, 2048 / std::max<int64_t>(wgs, 1)));
+    if (nsplit > 1) HIPCHK(ctx, P.bx_part.reserve((size_t)nsplit * kPartSums * rows));
+    hipLaunchKernelGGL(k_bx_table, dim3((unsigned)((bins_max + 63) / 64), nl, nsplit), dim3(kBlock), 0,
+                       ctx->stream, P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p, nsplit, P.bx_part.p, rows);
+    if (nsplit > 1)
+        hipLaunchKernelGGL(k_bx_table_fin, dim3((unsigned)((bins_max + kBlock - 1) / kBlock), nl), dim3(kBlock), 0,
+                           ctx->stream, grp, P.bx.p, P.bx_tab.p, nsplit, P.bx_part.p, rows);
     P.bx_sb_max = (int64_t)bins_max * kBxSub;
-    static uint64_t gen_counter = 0;   // unique over every posterior of the process
-    P.bx_gen = __atomic_add_fetch(&gen_counter, 1, __ATOMIC_RELAXED);
+    P.bx_gen = tpe_rt::next_bx_gen();
     const dim3 gs((unsigned)((P.bx_sb_max + kBlock - 1) / kBlock), nl);
     hipLaunchKernelGGL(k_bx_bounds, gs, dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p, P.samp.p,
                        P.bx.p, P.bx_tab.p, P.bx_loff.p, P.bx_list.p, P.bx_sb.p, P.bx_sbp.p);

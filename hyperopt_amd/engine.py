@@ -337,6 +337,48 @@ class Engine(object):
             ctypes.c_void_p(d_out.data_ptr())))
         return d_out
 
+    def export_size(self):
+        """Bytes tpe_export_posterior writes for the resident posterior (its
+        expansion index queued first when the rounds would use one)."""
+        n = ctypes.c_int64()
+        self._check(self.lib.tpe_export_posterior(self.h, None, 0, ctypes.byref(n)))
+        return int(n.value)
+
+    def export_posterior(self, d_out):
+        """The resident posterior and its expansion index as one blob in
+        d_out (a contiguous device uint8 tensor on this engine's GPU, at
+        least export_size() bytes), complete on return; returns its size."""
+        n = ctypes.c_int64()
+        cap = d_out.numel() * d_out.element_size()
+        if not d_out.is_cuda or not d_out.is_contiguous():
+            raise ValueError('d_out must be a contiguous device tensor')
+        self._check_device(d_out, 'd_out')
+        _torch_stream_done(d_out)
+        self._check(self.lib.tpe_export_posterior(self.h, ctypes.c_void_p(d_out.data_ptr()), cap,
+                                                  ctypes.byref(n)))
+        if n.value > cap:
+            raise ValueError('d_out holds %d bytes, the posterior needs %d' % (cap, n.value))
+        return int(n.value)
+
+    def import_posterior(self, d_blobs, part_off, part_labels):
+        """Resident posterior = the labels of the blobs in d_blobs (device
+        uint8 tensor on this engine's GPU): part p at byte part_off[p] holds
+        the labels part_labels[p] (their space indices, in the exporter's
+        label order); together the label lists cover 0..L-1 once."""
+        if not d_blobs.is_cuda or not d_blobs.is_contiguous():
+            raise ValueError('d_blobs must be a contiguous device tensor')
+        self._check_device(d_blobs, 'd_blobs')
+        off = np.ascontiguousarray(np.asarray(part_off, dtype=np.int64))
+        counts = np.ascontiguousarray(np.asarray([len(p) for p in part_labels], dtype=np.int32))
+        ids = np.ascontiguousarray(np.concatenate([np.asarray(p, dtype=np.int32) for p in part_labels]))
+        if len(off) != len(counts):
+            raise ValueError('one offset per part')
+        _torch_stream_done(d_blobs)
+        self._check(self.lib.tpe_import_posterior(
+            self.h, ctypes.c_void_p(d_blobs.data_ptr()), d_blobs.numel() * d_blobs.element_size(),
+            _ptr(off), len(off), _ptr(counts), _ptr(ids)))
+        self._labels()
+
     def score(self, label, cand, want_lpdf=True):
         cand = _f64(cand).ravel()
         lb = np.empty(len(cand)) if want_lpdf else None
@@ -418,7 +460,8 @@ class Engine(object):
                'hot': L.TPE_OPT_HOT, 'early': L.TPE_OPT_EARLY, 'hot_div': L.TPE_OPT_HOT_DIV,
                'zero_win': L.TPE_OPT_ZERO_WIN, 'value_only': L.TPE_OPT_VALUE_ONLY,
                'rescore_cap': L.TPE_OPT_RESCORE_CAP, 'mode_mask': L.TPE_OPT_MODE_MASK,
-               'aux_families': L.TPE_OPT_AUX_FAMILIES, 'hot32': L.TPE_OPT_HOT32}
+               'aux_families': L.TPE_OPT_AUX_FAMILIES, 'hot32': L.TPE_OPT_HOT32,
+               'bx_split': L.TPE_OPT_BX_SPLIT}
 
     def set_option(self, name, value):
         """Engine switches (include/hyperopt_tpe.h TPE_OPT_*): 'screen',

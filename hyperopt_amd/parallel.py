@@ -11,6 +11,9 @@ round.  Two partitions of a round's (label, candidate) set:
 * candidate shards (exchange_winners): rank r scores candidates
   [rank*C, (rank+1)*C) of every label, for spaces with fewer labels than
   ranks.
+* descriptor exchange (DescriptorExchange): label shards for the posterior
+  and index builds, then one all-gather of the built posteriors and
+  candidate shards for the round -- north_star's partition.
 
 Candidate shards: each rank scores candidates [rank*C, (rank+1)*C) of every label (the Philox
 counter is the global index, so the union over ranks is exactly the
@@ -143,6 +146,95 @@ class DeviceExchange(object):
             self.engine.merge_results_device(g, self.world, nr * L, out)
             return _records(out, (nr, L))
         return merge_results(_records(g, (self.world, nr * L))).reshape(nr, L)
+
+
+def _align(n, a=256):
+    return (int(n) + a - 1) // a * a
+
+
+class DescriptorExchange(object):
+    """north_star's partition: the
+    per-posterior work divides over the ranks like label shards -- rank r
+    appends its labels' observations, rebuilds their posteriors and their
+    expansion index (FminLoop over label_shards(...)[r]) -- and the rounds
+    divide like candidate shards: share() exports this rank's posterior as
+    one device blob (tpe_export_posterior), ONE all-gather over RCCL moves
+    every rank's blob device to device, and every rank imports the whole
+    space's posterior (tpe_import_posterior: each label's records and index,
+    rebased, in space order); round() then scores candidates [r C/N, (r+1)
+    C/N) of every label and the winners merge on the GPU with broadcast_best's
+    order (DeviceExchange 'candidates').  Labels are independent in
+    tpe.suggest (tpe.py:678-692) and each keeps its Philox stream, so the
+    merged winners are one context's winners over the whole round.
+
+    Two collectives per step beyond the winners' all-gather: the blob sizes
+    (N int64) and the blobs (N x the largest, 256-byte slots)."""
+
+    def __init__(self, engine, shards, rank, group=None, split='candidates'):
+        import torch.distributed as dist
+        if split not in ('candidates', 'rounds'):
+            raise ValueError(split)
+        self.engine, self.shards, self.rank, self.group = engine, shards, rank, group
+        self.world = dist.get_world_size(group)
+        if len(shards) != self.world:
+            raise ValueError('%d label shards for %d ranks' % (len(shards), self.world))
+        self.device = dist.get_backend(group) == 'nccl'
+        self.split = split
+        self.winners = DeviceExchange(engine, split, rank=rank, group=group)
+        self._bufs = {}
+        self.last_sizes = None
+
+    def _buf(self, key, nbytes, dtype=None, device=None):
+        import torch
+        dev = device or ('cuda' if self.device else 'cpu')
+        b = self._bufs.get(key)
+        if b is None or b.numel() < nbytes or b.device.type != dev:
+            b = self._bufs[key] = torch.empty(nbytes, dtype=dtype or torch.uint8, device=dev)
+        return b[:nbytes]
+
+    def share(self):
+        """Export, all-gather, import: afterwards this rank's engine holds
+        every label's posterior and index.  Returns the ranks' blob sizes.
+        (Under gloo -- the CPU and one-GPU rehearsals -- the blobs are staged
+        through host tensors around the collective.)"""
+        import torch
+        import torch.distributed as dist
+        eng = self.engine
+        # the engine's side: its GPU (a stub engine of the CPU tests: host)
+        edev = 'cuda' if torch.cuda.is_available() else 'cpu'
+        sz = self._buf('size', 1, torch.int64)
+        sz.fill_(eng.export_size())
+        allsz = self._buf('sizes', self.world, torch.int64)
+        dist.all_gather_into_tensor(allsz, sz, group=self.group)
+        sizes = [int(v) for v in allsz.tolist()]
+        slot = _align(max(sizes))
+        blob = self._buf('blob', slot, device=edev)
+        eng.export_posterior(blob)
+        blobs = self._buf('blobs', self.world * slot, device=edev)
+        if blob.device.type == ('cuda' if self.device else 'cpu'):
+            dist.all_gather_into_tensor(blobs, blob, group=self.group)
+        else:
+            staged = self._buf('staged', self.world * slot)
+            dist.all_gather_into_tensor(staged, blob.to(staged.device), group=self.group)
+            blobs.copy_(staged)
+        eng.import_posterior(blobs, [r * slot for r in range(self.world)], self.shards)
+        self.last_sizes = sizes
+        return sizes
+
+    def slice(self, n_candidates):
+        """(cand_offset, count) of this rank's candidates of every label."""
+        lo = n_candidates * self.rank // self.world
+        return lo, n_candidates * (self.rank + 1) // self.world - lo
+
+    def round(self, seed, rounds, n_candidates):
+        """split 'candidates': this rank's slice of the rounds (n_candidates
+        per label over all ranks); 'rounds' (batched new_ids, config 5): this
+        rank's rounds whole.  Then the winners' exchange: [len(rounds) (x
+        world for 'rounds')][n_labels] records."""
+        if self.split == 'rounds':
+            return self.winners.round(seed, rounds, n_candidates)
+        off, n = self.slice(n_candidates)
+        return self.winners.round(seed, rounds, n, cand_offset=off)
 
 
 def exchange_winners(res, group=None):

@@ -339,6 +339,33 @@ int tpe_suggest_batch_device(tpe_ctx *ctx, uint64_t seed, const uint32_t *rounds
 int tpe_merge_results_device(tpe_ctx *ctx, const tpe_label_result *d_parts, int32_t n_parts,
                              int32_t n, tpe_label_result *d_out);
 
+/* north_star's multi-GPU partition (the reference builds each
+ * label's posterior once per suggest call, tpe.py:678-692, and the ranks here
+ * split that work): a rank builds the posterior and expansion index of the
+ * labels it owns (tpe_build_posterior_resident* over its label shard, each
+ * spec carrying its TPE_HAS_STREAM space index), exports them as one device
+ * blob, the ranks all-gather the blobs over RCCL, and each imports the
+ * assembled posterior of every label to score its slice of the candidates
+ * (cand_offset) -- the slices' winners merge with tpe_merge_results_device.
+ *
+ * tpe_export_posterior: the resident posterior, with its expansion index
+ * (queued first when the context's screen would build one), into d_out on
+ * this context's GPU.  *bytes receives the blob size; d_out NULL or cap
+ * smaller than it is a size query (nothing written).  Complete on return.
+ *
+ * tpe_import_posterior: replace the resident posterior with the labels of
+ * n_parts blobs in d_blobs (blob_bytes long; part p at part_off[p], a
+ * multiple of 256, holding part_labels[p] labels).  label_ids lists, part
+ * by part, the space index of each blob label: together a permutation of
+ * 0..L-1, L = sum part_labels; imported label label_ids[i] is the resident
+ * label of that index.  The records, sampling records and index come over
+ * device to device (one copy kernel); rounds on the result are the rounds of
+ * one context that built every label.  Complete on return.  The built
+ * mixtures are not imported (tpe_get_mixture refuses until the next build). */
+int tpe_export_posterior(tpe_ctx *ctx, void *d_out, int64_t cap, int64_t *bytes);
+int tpe_import_posterior(tpe_ctx *ctx, const void *d_blobs, int64_t blob_bytes, const int64_t *part_off,
+                         int32_t n_parts, const int32_t *part_labels, const int32_t *label_ids);
+
 /* Score a caller-supplied candidate set for one resident label (the parity
  * entry point: identical candidates in, both lpdf vectors and the winner
  * out).  lpdf_below / lpdf_above may be NULL. */
@@ -503,6 +530,10 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *                   draw and lists (index, accepted attempt); the listed
  *                   candidates are re-drawn in fp64 (0: the fp64 draw
  *                   kernel; 2: every bound x 4096, tests)                 [1]
+ *   TPE_OPT_BX_SPLIT  workgroups per 64-bin block of the expansion index's
+ *                   Taylor tables, each summing one part of the bins' window
+ *                   (k_bx_table / k_bx_table_fin; 1..8, 0: enough for ~2048
+ *                   workgroups)                                            [0]
  *   TPE_OPT_WIN_GROUPS  label groups of a windowed round, each sorted on a
  *                   second stream while the previous one is screened
  *                   (0: one group; the chip is busy either way)          [0]
@@ -536,6 +567,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_MODE_MASK 18
 #define TPE_OPT_AUX_FAMILIES 19
 #define TPE_OPT_HOT32 20
+#define TPE_OPT_BX_SPLIT 21
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
 
 /* Build now what the resident posterior's first round(s) of n_candidates

@@ -481,3 +481,37 @@ def test_hot32_draw_same_round_2_24(eng):
     _assert_same(a, d)
     print('2^24: listed fp32 %d, fp64 %d' % (la, lb))
     assert lb <= la <= 1.05 * lb + 64
+
+
+@pytest.mark.parametrize('split', [3, 8, 0])
+def test_index_window_split_same_round(eng, split):
+    """k_bx_table's split window (TPE_OPT_BX_SPLIT: the bins' component
+    window summed by several workgroups, the parts added by k_bx_table_fin):
+    the Taylor rows round differently, the winners do not -- the round equals
+    the unsplit index's bytewise, and the sub-bin bounds built on the split
+    rows still bracket the fp64 score."""
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.workloads import mixed_history
+    hist = mixed_history(32, 10000, seed=0)
+    packed = P.pack(hist.posteriors())
+    posts = hist.posteriors()
+    C = 1 << 20
+    try:
+        eng.set_option('bx_split', 1)
+        eng.set_posterior(*packed)
+        a = eng.suggest(23, C, round=4)
+        eng.set_option('bx_split', split)
+        eng.set_posterior(*packed)
+        b = eng.suggest(23, C, round=4)
+        for li in (0, 1, 3):
+            p = posts[li]
+            samp = eng.GMM1 if p.family == 'GMM1' else eng.LGMM1
+            x = samp(*p.below, low=p.low, high=p.high, q=None, seed=3, size=(20000,), stream=li)
+            u, l, _ = eng.hot_probe(li, x)
+            lb, la, _ = eng.score(li, x)
+            s64 = lb - la
+            fin = np.isfinite(s64)
+            assert np.all(l[fin] <= s64[fin]) and np.all(s64[fin] <= u[fin]), li
+    finally:
+        eng.set_option('bx_split', 0)
+    _assert_same(a, b)

@@ -17,6 +17,7 @@
 #   ubench           tools/ubench_issue (built beforehand): VALU issue costs -> issue_costs.json
 #   listpmc          rocprofv3 --list-avail (the counters this box offers)
 #   bm32             tools/ubench_bm32 (built beforehand): exhaustive fp32 Box-Muller error sweep
+#   ab               tools/ab_hot.py (option A/B in one process), its trace and PMC passes -> profiles/<tag>_ab_*
 set -u
 T=${1:?tag}
 shift
@@ -68,6 +69,21 @@ for s in "$@"; do
         bm32)
             run bm32 300 tools/ubench_bm32 || exit 1
             grep -q "BOUNDS HOLD" "$OUT/bm32.log" || { echo "fp32 Box-Muller bounds violated"; exit 1; } ;;
+        ab)      # tools/ab_hot.py: hot32 0/1 and bx_split 1/auto alternating, its kernel trace and PMC passes
+            run ab 300 python -u tools/ab_hot.py 8 || exit 1
+            run ab_trace 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
+                -- python -u tools/ab_hot.py 2 || exit 1
+            for p in "valu SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+                     "mix SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT GRBM_GUI_ACTIVE" \
+                     "mix32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM GRBM_GUI_ACTIVE" \
+                     "stall SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE"; do
+                set -- $p
+                name=$1; shift
+                echo "== pmc_$name"
+                timeout -s KILL 90 rocprofv3 --pmc "$@" -d "$OUT/pmc_$name" -o run --output-format csv \
+                    -- python -u tools/ab_hot.py 1 > "$OUT/pmc_$name.log" 2>&1 || { tail -5 "$OUT/pmc_$name.log"; exit 1; }
+            done
+            python tools/pmc_summary.py "$OUT" "${T}_ab" > /dev/null || exit 1 ;;
         listpmc)
             run listpmc 120 rocprofv3 --list-avail || exit 1 ;;
         py=*)
