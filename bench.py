@@ -115,8 +115,8 @@ def parse():
                          'descriptors (label shards build the posteriors and index, one all-gather '
                          'shares them, candidate shards score: parallel.DescriptorExchange)')
     ap.add_argument('--hot32', type=int, default=None,
-                    help='TPE_OPT_HOT32: the prefilter\'s fp32 draw (1, the library default) or the fp64 '
-                         'draw kernel (0)')
+                    help='TPE_OPT_HOT32: the prefilter\'s fp32 draw (1) or the fp64 draw kernel (0, the '
+                         'library default: faster on gfx950)')
     ap.add_argument('--bx-split', type=int, default=None,
                     help='TPE_OPT_BX_SPLIT: workgroups per 64-bin block of the index tables (0 = auto)')
     ap.add_argument('--dist-backend', default='nccl',
@@ -995,7 +995,7 @@ def main():
         # the expansion screen (k_screen_hot); the bracket holds both
         dom_ms = scr[2]
         kprec = 'f64'
-        kname = 'k_hot_bx<' if args.hot32 == 0 else 'k_hot_bx32<'
+        kname = 'k_hot_bx32<' if args.hot32 else 'k_hot_bx<'
         kdesc = 'k_hot_bx + k_screen_hot (hot-bin prefilter of the expansion screen: every candidate ' \
                 'drawn and bounded by its sub-bin\'s score interval, the 0.5 % that can still win ' \
                 'scored by the expansion screen), GMM1+LGMM1 labels'

@@ -416,7 +416,7 @@ struct tpe_ctx {
     double hot_cap_div = 16.0;           // hot lists hold n / hot_cap_div per cell (shrinks on overflow)
     DevBuf<double> hot_x;                // per cell: listed candidates' x (the fp64 draw kernel)
     DevBuf<int32_t> hot_a;               //   or their accepted attempts (k_hot_bx32: re-drawn in fp64)
-    int32_t hot32 = 1;                   // TPE_OPT_HOT32: the prefilter draws in fp32 (k_hot_bx32; 2: bounds x 4096, tests)
+    int32_t hot32 = 0;                   // TPE_OPT_HOT32: the prefilter draws in fp32 (k_hot_bx32; 2: bounds x 4096, tests)
     int32_t bx_split = 0;                // TPE_OPT_BX_SPLIT (0: auto)
     DevBuf<int32_t> hot_i, hot_cnt;      //   their indices; per cell the count
     DevBuf<unsigned long long> hot_t, hot_tau0;   // per cell largest L; per label tau0

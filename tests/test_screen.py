@@ -405,7 +405,7 @@ def test_hot_bounds_hold(eng):
 
 @pytest.mark.parametrize('config', ['config2', 'config3', 'config3_device', 'config4', 'config3_batched'])
 def test_hot32_draw_same_round(eng, config):
-    """The prefilter's fp32 draw (k_hot_bx32, TPE_OPT_HOT32, the default):
+    """The prefilter's fp32 draw (k_hot_bx32, TPE_OPT_HOT32 = 1):
     every candidate drawn in fp32 with a rigorous bound on its distance from
     the fp64 draw, listed when any sub-bin it can fall in is hot, the listed
     ones re-drawn in fp64 from (index, accepted attempt).  The round equals
@@ -451,7 +451,7 @@ def test_hot32_draw_same_round(eng, config):
             assert lb <= la <= 1.05 * lb + 64
             assert lc >= la
     finally:
-        eng.set_option('hot32', 1)
+        eng.set_option('hot32', 0)
         eng.set_option('screen', 1)
 
 
@@ -471,7 +471,7 @@ def test_hot32_draw_same_round_2_24(eng):
         b = eng.suggest(41, C, round=3)
         lb, _ = eng.last_hot()
     finally:
-        eng.set_option('hot32', 1)
+        eng.set_option('hot32', 0)
     eng.set_option('screen', 0)
     try:
         d = eng.suggest(41, C, round=3)

@@ -24,6 +24,10 @@ from hyperopt_amd import _build  # noqa: E402
 
 # name -> [(file, old text, new text)]: result-changing timing experiments
 PATCHES = {
+    # round 4's index geometry: bins half as wide (Taylor argument <= ~0.5), 16 sub-bins each
+    'sub16': [('tpe_device.h', 'constexpr int kBxSubBits = 5;', 'constexpr int kBxSubBits = 4;'),
+              ('tpe_expand.hip', 'const double r_target = 0.5 / (kap * d0); ',
+               'const double r_target = 0.25 / (kap * d0);')],
     'bm': [('tpe_device.h',
             '    return __builtin_amdgcn_sqrt(fmax(0.0, 2.0 * bm_neglog(u01_open0(y), lt)));\n',
             '    return (double)y * 0x1.0p-31;\n')],

@@ -6,10 +6,11 @@
 #
 # steps:
 #   tests            the whole -m gpu suite (one pytest process)
-#   tests=<expr>     the -m gpu tests matching pytest -k <expr>
+#   tests=<expr>     the -m gpu tests matching pytest -k <expr> (commas for spaces)
 #   smoke            __graft_entry__.smoke()
 #   bench            the default bench.py line (what the driver runs)
 #   bench=<args>     bench.py with extra arguments (commas for spaces)
+#   var=<name>[,args] bench.py on the variant library tools/var_<name>.so (tools/build_variant.py)
 #   prof             tools/prof_round.sh <tag> (kernel trace + PMC passes of the default line)
 #   lpdf             the plain fp64 round's trace + PMC passes (tools/prof_round.sh <tag>_lpdf)
 #   shard=<r>        label shard r of config 3 alone: probe + kernel/HIP-API trace
@@ -44,7 +45,8 @@ for s in "$@"; do
             run tests 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread
             rc=$?; [ $rc -le 1 ] || exit 1 ;;
         tests=*)
-            run tests$n 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "${s#tests=}"
+            k=${s#tests=}
+            run tests$n 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "${k//,/ }"
             rc=$?; [ $rc -le 1 ] || exit 1 ;;
         smoke)
             run smoke 200 python -u -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
@@ -53,6 +55,11 @@ for s in "$@"; do
         bench=*)
             a=${s#bench=}
             run bench$n 600 python -u bench.py ${a//,/ } || exit 1 ;;
+        var=*)   # bench.py on a tools/build_variant.py library: var=<name>[,bench args]
+            a=${s#var=}
+            v=${a%%,*}
+            rest=""; [ "$a" != "$v" ] && rest=${a#*,}
+            run var_$v$n 600 env HYPEROPT_AMD_VARIANT=tools/var_$v.so python -u bench.py ${rest//,/ } || exit 1 ;;
         prof)
             bash tools/prof_round.sh "$T" --steps 5 --warmup 2 --no-other-configs --no-agreement || exit 1 ;;
         lpdf)   # the plain fp64 round (k_round<double>, no screen) at config 3: trace + PMC passes
