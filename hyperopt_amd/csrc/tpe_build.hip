@@ -1111,6 +1111,35 @@ __global__ __launch_bounds__(kParzenBlock) void k_fold(
     }
 }
 
+// One scatter launch for a build's inputs: task y copies its bytes from the
+// staging block (src >= 0: byte offset) or zero-fills them (src < 0).  Grid
+// (<= 32, tasks).
+constexpr int kUpBlock = 256;
+__global__ __launch_bounds__(kUpBlock) void k_build_inputs(const UpTask* __restrict__ tasks,
+                                                           const uint8_t* __restrict__ stage) {
+    const UpTask t = tasks[blockIdx.y];
+    const int64_t words = t.bytes >> 2;
+    uint32_t* d = reinterpret_cast<uint32_t*>(t.dst);
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(stage + (t.src >= 0 ? t.src : 0));
+    for (int64_t i = (int64_t)blockIdx.x * kUpBlock + threadIdx.x; i < words; i += (int64_t)gridDim.x * kUpBlock)
+        d[i] = t.src >= 0 ? sw[i] : 0u;
+    if (blockIdx.x == 0 && threadIdx.x < (t.bytes & 3)) {
+        const int64_t b = (words << 2) + threadIdx.x;
+        t.dst[b] = t.src >= 0 ? stage[t.src + b] : (uint8_t)0;
+    }
+}
+
+// A build's report in one block: the DLabels (dl_words 32-bit words), the
+// error flag (16 bytes later) and the tie report (n_ties int32)
+__global__ __launch_bounds__(kUpBlock) void k_build_report(const uint32_t* __restrict__ dl, int32_t dl_words,
+                                                           const int32_t* __restrict__ err,
+                                                           const int32_t* __restrict__ ties, int32_t n_ties,
+                                                           uint32_t* __restrict__ out) {
+    for (int32_t i = threadIdx.x; i < dl_words; i += kUpBlock) out[i] = dl[i];
+    if (threadIdx.x == 0) out[dl_words] = (uint32_t)err[0];
+    for (int32_t i = threadIdx.x; i < n_ties; i += kUpBlock) out[dl_words + 4 + i] = (uint32_t)ties[i];
+}
+
 }  // namespace
 
 // ============================================================ host side ====
@@ -1481,19 +1510,29 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     HIPCHK(ctx, P.samp.reserve(samp_total));
     HIPCHK(ctx, ctx->errflag.reserve(1));
     HIPCHK(ctx, B.ties.reserve(n_labels + 1));
-    HIPCHK(ctx, hipMemsetAsync(B.ties.p, 0, (n_labels + 1) * sizeof(int32_t), st));
+    // the build's inputs -- supplied orders, subset labels, losses, below
+    // set, mixture offsets, DLabels, and the zeroed tie report and error
+    // flag -- in ONE H2D copy from pinned staging and one scatter launch
+    // (k_build_inputs) instead of up to 8 copies and memsets (~8 us of host
+    // API time each, on the fmin step's critical path)
     const int64_t* order_off_d = nullptr;
     const int32_t* order_d = nullptr;
+    std::vector<UpTask> up;
+    std::vector<const void*> up_src;
+    auto put = [&](const void* src, int64_t bytes, void* dst) {
+        if (bytes <= 0) return;
+        up.push_back(UpTask{0, (uint8_t*)dst, bytes, 0});
+        up_src.push_back(src);
+    };
+    put(nullptr, (n_labels + 1) * (int64_t)sizeof(int32_t), B.ties.p);
     if (order_off_h && order_h && order_off_h[n_labels] > 0) {
         for (int32_t l = 0; l < n_labels; ++l)
             if (order_off_h[l + 1] < order_off_h[l] || order_off_h[l] < 0)
                 return ctx->fail(TPE_ERR_ARG, "order offsets must not decrease");
         HIPCHK(ctx, B.order_off.reserve(n_labels + 1));
         HIPCHK(ctx, B.order.reserve(order_off_h[n_labels]));
-        HIPCHK(ctx, hipMemcpyAsync(B.order_off.p, order_off_h, (n_labels + 1) * sizeof(int64_t),
-                                   hipMemcpyHostToDevice, st));
-        HIPCHK(ctx, hipMemcpyAsync(B.order.p, order_h, order_off_h[n_labels] * sizeof(int32_t),
-                                   hipMemcpyHostToDevice, st));
+        put(order_off_h, (n_labels + 1) * (int64_t)sizeof(int64_t), B.order_off.p);
+        put(order_h, order_off_h[n_labels] * (int64_t)sizeof(int32_t), B.order.p);
         order_off_d = B.order_off.p;
         order_d = B.order.p;
     }
@@ -1503,16 +1542,42 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
         // the other labels keep the previous build's records, DLabels and
         // mixtures; the losses, the below set and the offsets are the same
         HIPCHK(ctx, B.only.reserve(n_only));
-        HIPCHK(ctx, hipMemcpyAsync(B.only.p, only_h, n_only * sizeof(int32_t), hipMemcpyHostToDevice, st));
+        put(only_h, n_only * (int64_t)sizeof(int32_t), B.only.p);
         only_d = B.only.p;
     } else {
-        if (T > 0) HIPCHK(ctx, hipMemcpyAsync(B.losses.p, losses, T * sizeof(double), hipMemcpyHostToDevice, st));
-        if (T > 0 && below_h) HIPCHK(ctx, hipMemcpyAsync(B.below.p, below_h, T, hipMemcpyHostToDevice, st));
-        HIPCHK(ctx, hipMemcpyAsync(B.mix_off.p, mix.data(), mix.size() * sizeof(int64_t), hipMemcpyHostToDevice,
-                                   st));
-        HIPCHK(ctx, hipMemcpyAsync(P.labels.p, dl.data(), n_labels * sizeof(DLabel), hipMemcpyHostToDevice, st));
+        put(losses, T * (int64_t)sizeof(double), B.losses.p);
+        if (below_h) put(below_h, T, B.below.p);
+        put(mix.data(), (int64_t)mix.size() * (int64_t)sizeof(int64_t), B.mix_off.p);
+        put(dl.data(), n_labels * (int64_t)sizeof(DLabel), P.labels.p);
     }
-    HIPCHK(ctx, hipMemsetAsync(ctx->errflag.p, 0, sizeof(int32_t), st));
+    put(nullptr, sizeof(int32_t), ctx->errflag.p);
+    {
+        const int64_t head = ((int64_t)up.size() * (int64_t)sizeof(UpTask) + 255) / 256 * 256;
+        int64_t o = head;
+        for (UpTask& u : up) {
+            u.src = up_src[&u - up.data()] ? o : -1;
+            if (u.src >= 0) o += (u.bytes + 15) / 16 * 16;
+        }
+        if (B.up_pending) {   // (the previous build's copy out of the staging)
+            HIPCHK(ctx, hipEventSynchronize(B.ev_up));
+            B.up_pending = false;
+        }
+        HIPCHK(ctx, B.h_up.resize(o));
+        HIPCHK(ctx, B.d_up.reserve(o));
+        std::memcpy(B.h_up.data(), up.data(), up.size() * sizeof(UpTask));
+        for (size_t i = 0; i < up.size(); ++i)
+            if (up[i].src >= 0) std::memcpy(B.h_up.data() + up[i].src, up_src[i], up[i].bytes);
+        HIPCHK(ctx, hipMemcpyAsync(B.d_up.p, B.h_up.data(), o, hipMemcpyHostToDevice, st));
+        if (!B.ev_up) HIPCHK(ctx, hipEventCreateWithFlags(&B.ev_up, hipEventDisableTiming));
+        HIPCHK(ctx, hipEventRecord(B.ev_up, st));
+        B.up_pending = true;
+        int64_t mx = 1;
+        for (const UpTask& u : up) mx = std::max(mx, u.bytes);
+        hipLaunchKernelGGL(k_build_inputs, dim3((unsigned)std::min<int64_t>((mx + 4 * kUpBlock - 1) / (4 * kUpBlock), 32),
+                                                (unsigned)up.size()),
+                           dim3(kUpBlock), 0, st, (const UpTask*)B.d_up.p, B.d_up.p);
+        HIPCHK(ctx, hipGetLastError());
+    }
 
     HIPCHK(ctx, hipEventRecord(ctx->ev0, st));
     if (T > 0 && !below_h && !subset)
@@ -1533,13 +1598,16 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
                        ctx->errflag.p, only_d);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(ctx->ev1, st));
-    HIPCHK(ctx, ctx->dl_h.resize(n_labels));
-    HIPCHK(ctx, ctx->ties_h.resize(n_labels + 1));
-    HIPCHK(ctx, hipMemcpyAsync(ctx->dl_h.data(), P.labels.p, n_labels * sizeof(DLabel), hipMemcpyDeviceToHost, st));
-    HIPCHK(ctx, hipMemcpyAsync(&ctx->pin[0].err, ctx->errflag.p, sizeof(int32_t), hipMemcpyDeviceToHost, st));
-    if (ties_out)
-        HIPCHK(ctx, hipMemcpyAsync(ctx->ties_h.data(), B.ties.p, (n_labels + 1) * sizeof(int32_t),
-                                   hipMemcpyDeviceToHost, st));
+    // the report -- DLabels, error flag, tie report -- packed by one launch
+    // into one block and read back with ONE copy (three before)
+    const int64_t rep_dl = (int64_t)n_labels * (int64_t)sizeof(DLabel);
+    const int64_t rep_bytes = rep_dl + 16 + (int64_t)(n_labels + 1) * (int64_t)sizeof(int32_t);
+    HIPCHK(ctx, B.d_rep.reserve(rep_bytes));
+    HIPCHK(ctx, B.h_rep.resize(rep_bytes));
+    hipLaunchKernelGGL(k_build_report, dim3(1), dim3(kUpBlock), 0, st, (const uint32_t*)P.labels.p,
+                       (int32_t)(rep_dl / 4), ctx->errflag.p, B.ties.p, n_labels + 1, (uint32_t*)B.d_rep.p);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipMemcpyAsync(B.h_rep.data(), B.d_rep.p, rep_bytes, hipMemcpyDeviceToHost, st));
     if (!beside) {   // does the expansion index of the previous posterior still hold?
         const int rc = tpe_rt::bx_keep_check(ctx);
         if (rc) return rc;
@@ -1560,9 +1628,10 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     }
     HIPCHK(ctx, hipStreamSynchronize(st));
     P.qc_ready = false;   // (set again below when the build succeeds)
-    const int32_t errh = ctx->pin[0].err;
-    std::memcpy(dl.data(), ctx->dl_h.data(), n_labels * sizeof(DLabel));
-    if (ties_out) std::memcpy(ties_out, ctx->ties_h.data(), (n_labels + 1) * sizeof(int32_t));
+    int32_t errh;
+    std::memcpy(&errh, B.h_rep.data() + rep_dl, sizeof(int32_t));
+    std::memcpy(dl.data(), B.h_rep.data(), rep_dl);
+    if (ties_out) std::memcpy(ties_out, B.h_rep.data() + rep_dl + 16, (n_labels + 1) * sizeof(int32_t));
     HIPCHK(ctx, hipEventElapsedTime(&ctx->build_ms, ctx->ev0, ctx->ev1));
     if (errh & 1) return ctx->fail(TPE_ERR_ARG, "observation trial position out of range");
     if (errh & 2) return ctx->fail(TPE_ERR_ARG, "more below observations than the below set (duplicate trial in a label?)");

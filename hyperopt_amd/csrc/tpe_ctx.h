@@ -259,6 +259,14 @@ struct Posterior {
     }
 };
 
+// one input of a build in its staging block (k_build_inputs)
+struct UpTask {
+    int64_t src;     // byte offset in the staging block; < 0: zero-fill
+    uint8_t* dst;
+    int64_t bytes;
+    int64_t pad;
+};
+
 // The device posterior builder (tpe_build.hip): the resident history pool
 // and the per-build scratch, grown on demand.
 struct BuildBufs {
@@ -317,6 +325,12 @@ struct BuildBufs {
     int32_t built_lf = 0;
     uint64_t built_loss_hash = 0;  // fingerprint of the losses (a subset rebuild reuses them)
     DevBuf<int32_t> only;          // the labels of a subset rebuild
+    // a build's inputs: one pinned staging block, one H2D copy, one scatter
+    // launch (tpe_build.hip k_build_inputs); the next build waits for ev_up
+    PinVec<uint8_t> h_up, h_rep;
+    DevBuf<uint8_t> d_up, d_rep;   // (d_rep: the build's report, k_build_report)
+    hipEvent_t ev_up = nullptr;
+    bool up_pending = false;
     void release() {
         specs.release(); cat_p.release(); p_off.release(); cnt.release(); p_trial.release();
         p_val.release(); s_key.release(); s_key2.release(); s_idx.release(); s_idx2.release();
@@ -326,7 +340,10 @@ struct BuildBufs {
         gs_lab2.release(); losses.release(); below.release(); keys.release();
         idx.release(); below_val.release(); counts.release(); kcount.release(); w.release();
         mu.release(); sigma.release(); mix_off.release(); scratch.release(); ties.release();
-        order_off.release(); order.release(); only.release();
+        order_off.release(); order.release(); only.release(); d_up.release(); d_rep.release();
+        if (ev_up) (void)hipEventDestroy(ev_up);
+        ev_up = nullptr;
+        up_pending = false;
         if (ev_staged) (void)hipEventDestroy(ev_staged);
         ev_staged = nullptr;
         staged_pending = false;

@@ -254,6 +254,10 @@ def _gpu_rank_worker(rank, world, port, q):
         res = x.round(42, [9], 1 << 18)
         eng.close()
         q.put((rank, np.ascontiguousarray(res[0]).tobytes()))
+    except Exception:   # (reported, so the parent fails at once instead of waiting out its timeout)
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -269,7 +273,8 @@ def test_descriptor_exchange_two_ranks_gpu():
         p.start()
     got = {}
     for _ in procs:
-        r, a = q.get(timeout=200)
+        r, a = q.get(timeout=100)
+        assert isinstance(a, bytes), a
         got[r] = a
     for p in procs:
         p.join(timeout=60)
