@@ -1317,7 +1317,7 @@ struct BxLabel {
 // otherwise re-runs the plain expansion screen -- the filter never changes a
 // winner, tau0 only decides how often that fallback runs.  Only the listed
 // candidates go through the expansion screen (k_screen_hot).
-constexpr int kBxSubBits = 5;
+constexpr int kBxSubBits = 4;
 constexpr int kBxSub = 1 << kBxSubBits;
 constexpr double kHotFill = 16.0;   // P(a run of that mass stays empty) <= e^-16
 

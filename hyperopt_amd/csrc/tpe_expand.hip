@@ -8,11 +8,13 @@
 //   k_bx_scan     per label: candidate range, a* (the largest above record
 //                 scale = the clipped sigma's), unclipped count
 //   (host)        bins per label from kappa and the cut T: the Taylor argument
-//                 2 kappa |d| |delta| stays <= ~1, so 15 terms leave a
-//                 truncation <= ~2e-12 of the bin's mass (round 4: <= ~0.5 and
-//                 ~4e-17 with twice the bins; the screen's bound E, ~3e-12, is
-//                 the fp64 round's own rounding either way, and the index's
-//                 table and list work halved)
+//                 2 kappa |d| |delta| stays <= ~0.5, so 15 terms leave a
+//                 truncation ~4e-17 of the bin's mass.  (Bins twice as wide,
+//                 argument <= ~1, were measured in round 5: the index 0.63 ->
+//                 0.49 ms, but the screen certified only 70-80 % of the
+//                 candidates -- the bound's e^y and cancellation terms -- and
+//                 the round re-scored 419k near-ties instead of 186: 1.48 ->
+//                 4.37 ms, r5g.)
 //   k_bx_compact  per label: the unclipped components in record order
 //   k_bx_list     per bin: the unclipped components whose term can reach 2^-T
 //                 in it, into the bin's slot of n_nc entries, and their count
@@ -800,7 +802,7 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
                                ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     // bins per label: the fewest (a multiple of 64) whose half-width keeps
-    // the Taylor argument 2 kappa |d| r <= ~1 over the window
+    // the Taylor argument 2 kappa |d| r <= ~0.5 over the window
     P.bx_h.assign(P.n_labels, BxLabel{});
     bool ok = true;
     int64_t rows = 0, lsum = 0;
@@ -818,7 +820,7 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
             break;
         }
         const double d0 = std::sqrt(kBxT * kLn2 / kap);
-        const double r_target = 0.5 / (kap * d0);    // Taylor argument 2 kappa |d| r <= ~1
+        const double r_target = 0.25 / (kap * d0);   // Taylor argument 2 kappa |d| r <= ~0.5
         const double want = (xhi - xlo) / (2.0 * r_target);
         if (!(want <= (double)kMaxBins)) {
             ok = false;

@@ -24,6 +24,80 @@ from hyperopt_amd import _build  # noqa: E402
 
 # name -> [(file, old text, new text)]: result-changing timing experiments
 PATCHES = {
+    # k_bx_table: the 15 powers of each component's Taylor argument as a tree
+    # (y^2, y^4, y^8; depth ~5 instead of a 14-multiply chain)
+    'bxtree': [('tpe_expand.hip',
+                """#pragma unroll
+            for (int n = 1; n < kBxP; ++n)
+#pragma unroll
+                for (int q = 0; q < kBxChains; ++q) {
+                    t[q] *= y[q];
+                    A[n] = fma(t[q], kInvFact[n], A[n]);
+                }
+#pragma unroll
+            for (int q = 0; q < kBxChains; ++q) S3 += fabs(t[q] * y[q]);""",
+                """#pragma unroll
+            for (int q = 0; q < kBxChains; ++q) {
+                const double y1 = y[q], y2 = y1 * y1, y4 = y2 * y2, y8 = y4 * y4;
+                double p[kBxP + 1];
+                p[1] = t[q] * y1;
+                p[2] = t[q] * y2;
+                p[4] = t[q] * y4;
+                p[8] = t[q] * y8;
+                p[3] = p[1] * y2;
+                p[5] = p[1] * y4;
+                p[6] = p[2] * y4;
+                p[9] = p[1] * y8;
+                p[10] = p[2] * y8;
+                p[12] = p[4] * y8;
+                p[7] = p[3] * y4;
+                p[11] = p[3] * y8;
+                p[13] = p[5] * y8;
+                p[14] = p[6] * y8;
+                p[15] = p[7] * y8;
+#pragma unroll
+                for (int n = 1; n < kBxP; ++n) A[n] = fma(p[n], kInvFact[n], A[n]);
+                S3 += fabs(p[15]);
+            }""")],
+    # bins twice as wide (Taylor argument <= ~1) with 32 sub-bins each: measured slower (r5g)
+    'sub32': [('tpe_device.h', 'constexpr int kBxSubBits = 4;', 'constexpr int kBxSubBits = 5;'),
+              ('tpe_expand.hip', 'const double r_target = 0.25 / (kap * d0);',
+               'const double r_target = 0.5 / (kap * d0); ')],
+    # k_bx_table: the 15 powers of each component's Taylor argument as a tree
+    # (y^2, y^4, y^8; depth ~5 instead of a 14-multiply chain)
+    'bxtree': [('tpe_expand.hip',
+                """#pragma unroll
+            for (int n = 1; n < kBxP; ++n)
+#pragma unroll
+                for (int q = 0; q < kBxChains; ++q) {
+                    t[q] *= y[q];
+                    A[n] = fma(t[q], kInvFact[n], A[n]);
+                }
+#pragma unroll
+            for (int q = 0; q < kBxChains; ++q) S3 += fabs(t[q] * y[q]);""",
+                """#pragma unroll
+            for (int q = 0; q < kBxChains; ++q) {
+                const double y1 = y[q], y2 = y1 * y1, y4 = y2 * y2, y8 = y4 * y4;
+                double p[kBxP + 1];
+                p[1] = t[q] * y1;
+                p[2] = t[q] * y2;
+                p[4] = t[q] * y4;
+                p[8] = t[q] * y8;
+                p[3] = p[1] * y2;
+                p[5] = p[1] * y4;
+                p[6] = p[2] * y4;
+                p[9] = p[1] * y8;
+                p[10] = p[2] * y8;
+                p[12] = p[4] * y8;
+                p[7] = p[3] * y4;
+                p[11] = p[3] * y8;
+                p[13] = p[5] * y8;
+                p[14] = p[6] * y8;
+                p[15] = p[7] * y8;
+#pragma unroll
+                for (int n = 1; n < kBxP; ++n) A[n] = fma(p[n], kInvFact[n], A[n]);
+                S3 += fabs(p[15]);
+            }""")],
     # round 4's index geometry: bins half as wide (Taylor argument <= ~0.5), 16 sub-bins each
     'sub16': [('tpe_device.h', 'constexpr int kBxSubBits = 5;', 'constexpr int kBxSubBits = 4;'),
               ('tpe_expand.hip', 'const double r_target = 0.5 / (kap * d0); ',
