@@ -24,6 +24,14 @@ from hyperopt_amd import _build  # noqa: E402
 
 # name -> [(file, old text, new text)]: result-changing timing experiments
 PATCHES = {
+    # k_bx_table: ocml's fp64 exp (<= 1 ulp) instead of the 32 KB LDS table exp: no
+    # table load per workgroup, no dependent LDS read per term, 5 workgroups per CU
+    'bxexp': [('tpe_expand.hip', '    __shared__ double lds[kExpTabSize];   // the exp table, then the waves\' partial sums',
+               '    __shared__ double lds[3 * kTabSums * 64];   // the waves\' partial sums'),
+              ('tpe_expand.hip', '    load_exp_table(lds);\n    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;\n    const int b = b0 + lane, blast',
+               '    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;\n    const int b = b0 + lane, blast'),
+              ('tpe_expand.hip', 'const double e = exp_scaled(fmin(aj[q] * kExpScale, 0.0), lds);',
+               'const double e = exp(fmin(aj[q], 0.0));')],
     # k_bx_table: the 15 powers of each component's Taylor argument as a tree
     # (y^2, y^4, y^8; depth ~5 instead of a 14-multiply chain)
     'bxtree': [('tpe_expand.hip',

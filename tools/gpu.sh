@@ -55,6 +55,13 @@ for s in "$@"; do
         bench=*)
             a=${s#bench=}
             run bench$n 600 python -u bench.py ${a//,/ } || exit 1 ;;
+        vtests=*)   # -m gpu tests on a variant library: vtests=<name>,<pytest -k expr, commas for spaces>
+            a=${s#vtests=}
+            v=${a%%,*}
+            k=${a#*,}
+            run vtests_$v$n 600 env HYPEROPT_AMD_VARIANT=tools/var_$v.so python -u -m pytest tests -m gpu -v \
+                --timeout 300 --timeout-method thread -k "${k//,/ }"
+            rc=$?; [ $rc -le 1 ] || exit 1 ;;
         var=*)   # bench.py on a tools/build_variant.py library: var=<name>[,bench args]
             a=${s#var=}
             v=${a%%,*}
