@@ -4,7 +4,7 @@ a call): config-3 warm rounds (2^24 candidates x 32 labels) with the hot-bin
 prefilter's draw kernels (TPE_OPT_HOT32 0 / 1), and the expansion index's
 build with the window split (TPE_OPT_BX_SPLIT 1 / auto), alternating.
 
-    python tools/ab_hot.py [reps]
+    python tools/ab_hot.py [reps]        (AB_SPLITS=1,2,4,8: the bx_split values to alternate)
 """
 import json
 import os
@@ -41,7 +41,8 @@ def main():
         _, _, ms = eng.last_screen(with_ms=True)
         out['hot32'].setdefault(v, []).append((wall, ms))
     eng.set_option('hot32', 1)
-    for v in [1, 0] * reps:
+    splits = [int(x) for x in os.environ.get('AB_SPLITS', '1,0').split(',')]
+    for v in splits * reps:
         eng.set_option('bx_split', v)
         eng.set_posterior(*packed)           # a new posterior: the index is rebuilt
         torch.cuda.synchronize()

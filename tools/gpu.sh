@@ -83,6 +83,8 @@ for s in "$@"; do
         bm32)
             run bm32 300 tools/ubench_bm32 || exit 1
             grep -q "BOUNDS HOLD" "$OUT/bm32.log" || { echo "fp32 Box-Muller bounds violated"; exit 1; } ;;
+        absplit)   # tools/ab_hot.py over index window splits 1, 2, 4, 8 (the hot32 A/B too)
+            run absplit 300 env AB_SPLITS=1,2,4,8 python -u tools/ab_hot.py 6 || exit 1 ;;
         ab)      # tools/ab_hot.py: hot32 0/1 and bx_split 1/auto alternating, its kernel trace and PMC passes
             run ab 300 python -u tools/ab_hot.py 8 || exit 1
             run ab_trace 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv \
