@@ -913,7 +913,8 @@ def main():
             for sh in label_shards(hist_full.labels, 8):
                 e8 = Engine(local, args.precision)
                 for k, v in (('screen', int(screen)), ('window', int(not args.no_window)),
-                             ('win_t', args.win_t), ('win_groups', args.win_groups), ('value_only', value_only)):
+                             ('win_t', args.win_t), ('win_groups', args.win_groups), ('value_only', value_only),
+                             ('aux_families', aux_families)):
                     e8.set_option(k, v)
                 l8 = FminLoop(hist_full, label_ids=sh)
                 l8.advance(e8, args.trials + (p0 - 1) * args.append)

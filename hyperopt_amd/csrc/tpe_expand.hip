@@ -870,10 +870,12 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
     const dim3 gb((unsigned)((bins_max + kBlock - 1) / kBlock), nl);
     hipLaunchKernelGGL(k_bx_list, gb, dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p, P.bx.p,
                        P.bx_nc.p, P.bx_loff.p, P.bx_list.p);
-    // the window split for occupancy: >= ~2048 workgroups (4 per CU, LDS-bound, x2)
+    // the window split: ~8192 workgroups (4 per CU at a time, LDS-bound; the
+    // heavy dense-region blocks split too, so the tail shortens -- config 3's
+    // ~2000 blocks: split 1 / 2 / 4 / 8 -> 0.628 / 0.592 / 0.564 / 0.604 ms, r5j)
     const int64_t wgs = (rows + 63) / 64;
     const int nsplit = ctx->bx_split > 0 ? std::min(ctx->bx_split, kBxMaxSplit)
-                                         : (int)std::max<int64_t>(1, std::min<int64_t>(kBxMaxSplit, 2048 / std::max<int64_t>(wgs, 1)));
+                                         : (int)std::max<int64_t>(1, std::min<int64_t>(kBxMaxSplit, 8192 / std::max<int64_t>(wgs, 1)));
     if (nsplit > 1) HIPCHK(ctx, P.bx_part.reserve((size_t)nsplit * kPartSums * rows));
     hipLaunchKernelGGL(k_bx_table, dim3((unsigned)((bins_max + 63) / 64), nl, nsplit), dim3(kBlock), 0,
                        ctx->stream, P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p, nsplit, P.bx_part.p, rows);

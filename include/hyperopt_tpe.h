@@ -534,7 +534,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *                   and conversion work than the fp64 it saves)          [0]
  *   TPE_OPT_BX_SPLIT  workgroups per 64-bin block of the expansion index's
  *                   Taylor tables, each summing one part of the bins' window
- *                   (k_bx_table / k_bx_table_fin; 1..8, 0: enough for ~2048
+ *                   (k_bx_table / k_bx_table_fin; 1..8, 0: enough for ~8192
  *                   workgroups)                                            [0]
  *   TPE_OPT_WIN_GROUPS  label groups of a windowed round, each sorted on a
  *                   second stream while the previous one is screened
