@@ -465,6 +465,17 @@ struct tpe_ctx {
     DevBuf<int32_t> scr_cnt;
     tpe_rt::PinVec<int32_t> scr_cnt_h;
     tpe_rt::PinVec<tpe_rt::PinScalars> pin;   // one entry: the scalar read-backs
+    // a round's small read-backs (counts, flags, statistics, small result
+    // sets): registered by defer_read, packed by ONE launch into one device
+    // block and copied with ONE D2H before the round's sync (tpe_engine.hip)
+    struct RepTask {
+        const void* src;
+        void* dst;
+        int64_t bytes;
+    };
+    std::vector<RepTask> rep;
+    tpe_rt::DevBuf<uint8_t> rep_d;
+    tpe_rt::PinVec<uint8_t> rep_h;
     tpe_rt::PinVec<tpe_label_result> res_h;   // a round's results, staged before the caller's buffer
     tpe_rt::PinVec<tpe::DLabel> dl_h;         // a build's label records, read back
     tpe_rt::PinVec<int32_t> ties_h;           //   and its tie report

@@ -3009,6 +3009,70 @@ __global__ __launch_bounds__(kReduceBlock) void k_reduce(const Partial* __restri
     }
 }
 
+// A round's small read-backs in one copy: each was its own hipMemcpyAsync
+// (a blit launch of ~4 us on the device and ~7 us of host API time each, 5-7
+// per round, on the round's critical path); now defer_read registers them,
+// flush_reads packs them with one launch (k_pack_reads) into one block and
+// copies it with one D2H, unpack_reads scatters it after the round's sync.
+constexpr int kPackMax = 8;
+struct PackArgs {
+    const uint32_t* src[kPackMax];
+    int64_t off[kPackMax];   // (32-bit words)
+    int64_t words[kPackMax];
+    int32_t n;
+};
+__global__ __launch_bounds__(kBlock) void k_pack_reads(PackArgs a, uint32_t* __restrict__ out) {
+    for (int t = 0; t < a.n; ++t)
+        for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < a.words[t]; i += (int64_t)gridDim.x * kBlock)
+            out[a.off[t] + i] = a.src[t][i];
+}
+
+int defer_read(tpe_ctx* ctx, void* dst, const void* src, int64_t bytes) {
+    if (bytes <= 0) return TPE_OK;
+    if ((bytes & 3) || ((uintptr_t)src & 3) || bytes > (1 << 16))   // (large or odd: its own copy)
+        return ctx->hip(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream), "read-back");
+    ctx->rep.push_back(tpe_ctx::RepTask{src, dst, bytes});
+    return TPE_OK;
+}
+
+int flush_reads(tpe_ctx* ctx) {
+    if (ctx->rep.empty()) return TPE_OK;
+    int64_t total = 0, mx = 1;
+    for (const auto& r : ctx->rep) {
+        total += r.bytes;
+        mx = std::max(mx, r.bytes / 4);
+    }
+    HIPCHK(ctx, ctx->rep_d.reserve(total));
+    HIPCHK(ctx, ctx->rep_h.resize(total));
+    int64_t off = 0;
+    for (size_t i = 0; i < ctx->rep.size(); i += kPackMax) {
+        PackArgs a{};
+        a.n = (int32_t)std::min<size_t>(kPackMax, ctx->rep.size() - i);
+        for (int t = 0; t < a.n; ++t) {
+            const auto& r = ctx->rep[i + t];
+            a.src[t] = (const uint32_t*)r.src;
+            a.off[t] = off / 4;
+            a.words[t] = r.bytes / 4;
+            off += r.bytes;
+        }
+        hipLaunchKernelGGL(k_pack_reads, dim3((unsigned)std::min<int64_t>((mx + kBlock - 1) / kBlock, 16)),
+                           dim3(kBlock), 0, ctx->stream, a, (uint32_t*)ctx->rep_d.p);
+        HIPCHK(ctx, hipGetLastError());
+    }
+    return ctx->hip(hipMemcpyAsync(ctx->rep_h.data(), ctx->rep_d.p, total, hipMemcpyDeviceToHost, ctx->stream),
+                    "packed read-back");
+}
+
+// after the stream's sync
+void unpack_reads(tpe_ctx* ctx) {
+    int64_t off = 0;
+    for (const auto& r : ctx->rep) {
+        std::memcpy(r.dst, ctx->rep_h.data() + off, r.bytes);
+        off += r.bytes;
+    }
+    ctx->rep.clear();
+}
+
 // Several small fills in one launch (per-round counters, flags and
 // thresholds): grid.y = the fill, 32-bit words.  A hipMemsetAsync each would
 // cost a host API call and a queue slot apiece -- a round's resets used to be
@@ -3686,13 +3750,14 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                 hipLaunchKernelGGL(k_hot_check, dim3(1), dim3(kBlock), 0, ctx->stream, (int64_t)cells, nl,
                                    ctx->hot_t.p, ctx->hot_tau0.p, ctx->hot_flag.p);
                 HIPCHK(ctx, ctx->hot_cnt_h.resize(cells));
-                HIPCHK(ctx, hipMemcpyAsync(ctx->hot_cnt_h.data(), ctx->hot_cnt.p, cells * sizeof(int32_t),
-                                           hipMemcpyDeviceToHost, ctx->stream));
-                HIPCHK(ctx, hipMemcpyAsync(&ctx->pin[0].hot_flag, ctx->hot_flag.p, sizeof(int32_t),
-                                           hipMemcpyDeviceToHost, ctx->stream));
+                int rc = defer_read(ctx, ctx->hot_cnt_h.data(), ctx->hot_cnt.p, cells * sizeof(int32_t));
+                if (!rc) rc = defer_read(ctx, &ctx->pin[0].hot_flag, ctx->hot_flag.p, sizeof(int32_t));
+                if (rc) return rc;
             }
-            HIPCHK(ctx, hipMemcpyAsync(&ctx->pin[0].screen_exec, ctx->win_evals.p, sizeof(unsigned long long),
-                                       hipMemcpyDeviceToHost, ctx->stream));
+            {
+                const int rc = defer_read(ctx, &ctx->pin[0].screen_exec, ctx->win_evals.p, sizeof(unsigned long long));
+                if (rc) return rc;
+            }
             ctx->screen_exec_pending = true;
         } else if (ctx->window && a.n >= kWinMinN && a.cand_in == nullptr) {
             // windowed: units of (batch of rounds, group of labels); with
@@ -3760,8 +3825,10 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                                    sorted);
                 if (pipe) HIPCHK(ctx, hipEventRecord(ctx->ev_done[slot], ctx->stream));
             }
-            HIPCHK(ctx, hipMemcpyAsync(&ctx->pin[0].screen_exec, ctx->win_evals.p, sizeof(unsigned long long),
-                                       hipMemcpyDeviceToHost, ctx->stream));
+            {
+                const int rc = defer_read(ctx, &ctx->pin[0].screen_exec, ctx->win_evals.p, sizeof(unsigned long long));
+                if (rc) return rc;
+            }
             ctx->screen_exec_pending = true;
         } else {
             if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[0], ctx->stream));
@@ -3780,8 +3847,10 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
         hipLaunchKernelGGL(k_fill_empty, dim3((unsigned)std::min<int64_t>((a.tiles + kBlock - 1) / kBlock, 64), nl, a.gz),
                            dim3(kBlock), 0, ctx->stream, grp, ctx->P->n_labels, a.tiles, ctx->partials.p);
         HIPCHK(ctx, ctx->scr_cnt_h.resize(cells));
-        HIPCHK(ctx, hipMemcpyAsync(ctx->scr_cnt_h.data(), ctx->scr_cnt.p, cells * sizeof(int32_t),
-                                   hipMemcpyDeviceToHost, ctx->stream));
+        {
+            const int rc = defer_read(ctx, ctx->scr_cnt_h.data(), ctx->scr_cnt.p, cells * sizeof(int32_t));
+            if (rc) return rc;
+        }
         if (hot) {
             ctx->hot_ran = true;   // (its lists and flag are read after the round's one sync)
             ctx->hot_cells = (int64_t)cells;
@@ -4139,6 +4208,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         gz = (uint32_t)n_rounds;
     }
     const int32_t L = ctx->P->n_labels;
+    ctx->rep.clear();   // (an earlier round that failed between its reads and its flush)
     HIPCHK(ctx, ctx->partials.reserve((size_t)n_rounds * L * std::max(tiles, 1)));
     HIPCHK(ctx, ctx->results.reserve((size_t)n_rounds * L));
     HIPCHK(ctx, ctx->rounds.reserve(n_rounds));
@@ -4283,19 +4353,22 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     }
     if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->ev2, ctx->stream));
     PinScalars& pin = ctx->pin[0];
-    HIPCHK(ctx, hipMemcpyAsync(&pin.err, ctx->errflag.p, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(pin.xdrawn, ctx->xdrawn.p, 2 * sizeof(unsigned long long),
-                               hipMemcpyDeviceToHost, ctx->stream));
     const size_t n_res = (size_t)n_rounds * L;
     if (tiles > 0 && ctx->dev_out)
         HIPCHK(ctx, hipMemcpyAsync(ctx->dev_out, ctx->results.p, n_res * sizeof(tpe_label_result),
                                    hipMemcpyDeviceToDevice, ctx->stream));
-    if (tiles > 0 && out) {
-        HIPCHK(ctx, ctx->res_h.resize(n_res));
-        HIPCHK(ctx, hipMemcpyAsync(ctx->res_h.data(), ctx->results.p, n_res * sizeof(tpe_label_result),
-                                   hipMemcpyDeviceToHost, ctx->stream));
+    {
+        int rc = defer_read(ctx, &pin.err, ctx->errflag.p, sizeof(int32_t));
+        if (!rc) rc = defer_read(ctx, pin.xdrawn, ctx->xdrawn.p, 2 * sizeof(unsigned long long));
+        if (!rc && tiles > 0 && out) {
+            HIPCHK(ctx, ctx->res_h.resize(n_res));
+            rc = defer_read(ctx, ctx->res_h.data(), ctx->results.p, n_res * sizeof(tpe_label_result));
+        }
+        if (!rc) rc = flush_reads(ctx);
+        if (rc) return rc;
     }
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    unpack_reads(ctx);
     if (tiles > 0 && out) std::memcpy(out, ctx->res_h.data(), n_res * sizeof(tpe_label_result));
     if (ctx->zw_pending) {
         ctx->P->zw_ready = pin.plan.total > 0;
