@@ -538,8 +538,9 @@ struct RetryLds {
     double val[CAP];
 };
 
-// (every thread of the workgroup calls it, blockDim.x == 256; two barriers
-// per tile of a bounded label -- `par` is unused, kept for the callers.
+// (every thread of the workgroup calls it, blockDim.x == 256; no workgroup
+// barrier: each wave retries its own rejected slots -- `par` is unused, kept
+// for the callers.
 // Slots outside `pend` receive unspecified values: both callers read the
 // pending slots only.)
 template <int MODE, int R, typename Src, bool RAW = false, int CAP = R * 256>
@@ -581,28 +582,19 @@ __device__ __forceinline__ bool sample_tile(const DLabel& L, const Src& src, uin
         }
     }
     bool ok = true;
-    if (bounded) {   // (a label without both bounds never rejects: no list, no barriers)
-        if (lane == 0) q.wn[wave] = run;
-        __syncthreads();   // the list is complete
-        // the segments as one list: entry e of wave w's segment is list
-        // entry b[w] + e (b: the earlier waves' counts)
-        int b[kTileWaves + 1];
-        b[0] = 0;
-#pragma unroll
-        for (int w = 0; w < kTileWaves; ++w) b[w + 1] = b[w] + q.wn[w];
-        const int n = b[kTileWaves];   // (the workgroup's: uniform)
-        const int mine = b[wave];
-        if (n == 0) __syncthreads();   // (the counts are read before the next tile writes them)
-        for (int c0 = 0; c0 < n; c0 += CAP) {
-            const int c1 = min(n, c0 + CAP);
-            for (int e = c0 + (int)threadIdx.x; e < c1; e += blockDim.x) {
-                int w = 0;
-#pragma unroll
-                for (int k = 1; k < kTileWaves; ++k) w += e >= b[k] ? 1 : 0;
-                int bw = b[0];
-#pragma unroll
-                for (int k = 1; k < kTileWaves; ++k) bw = w == k ? b[k] : bw;
-                const uint32_t gg = g0 + (uint32_t)q.slot[w * (R * 64) + (e - bw)];
+    if (bounded && run > 0) {   // (a label without both bounds never rejects: no list)
+        // the wave retries its own rejected slots -- no workgroup barrier:
+        // its segment and its share of val are its own, and LDS operations
+        // of one wave complete in order (the wave barriers only keep the
+        // compiler from moving them); a retry is the slot's own attempts 1,
+        // 2, .. either way, so the values are the cooperative retry's
+        constexpr int WC = CAP / kTileWaves;
+        double* __restrict__ wval = q.val + wave * WC;
+        for (int c0 = 0; c0 < run; c0 += WC) {
+            const int c1 = min(run, c0 + WC);
+            __builtin_amdgcn_wave_barrier();
+            for (int e = c0 + lane; e < c1; e += 64) {
+                const uint32_t gg = g0 + (uint32_t)seg[e];
                 double v = __builtin_nan("");
                 for (uint32_t it = 1; it < kMaxAttempts; ++it) {
                     const double draw = draw_attempt(L, src, k0, k1, gg, it, rk);
@@ -612,15 +604,15 @@ __device__ __forceinline__ bool sample_tile(const DLabel& L, const Src& src, uin
                     }
                 }
                 ok = ok && v == v;
-                q.val[e - c0] = v;
+                wval[e - c0] = v;
             }
-            __syncthreads();
+            __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (int r = 0; r < R; ++r) {   // (list entry mine + pos in [c0, c1); kAccepted never is)
-                const uint32_t k = (uint32_t)(pos[r] + (mine - c0));
-                if (k < (uint32_t)(c1 - c0)) out[r] = q.val[k];
+            for (int r = 0; r < R; ++r) {   // (segment entry pos in [c0, c1); kAccepted never is)
+                const uint32_t k = (uint32_t)(pos[r] - c0);
+                if (k < (uint32_t)(c1 - c0)) out[r] = wval[k];
             }
-            if (c1 < n) __syncthreads();   // (the next pass reuses val)
+            __builtin_amdgcn_wave_barrier();
         }
     }
     if constexpr ((MODE == DENSE_LGMM || MODE == QUANT_LGMM) && !RAW) {
