@@ -1111,6 +1111,19 @@ __global__ __launch_bounds__(kParzenBlock) void k_fold(
     }
 }
 
+struct CopyArgs {
+    uint32_t* dst[kCopyBatch];
+    const uint32_t* src[kCopyBatch];
+    int64_t words[kCopyBatch];
+    int32_t n;
+};
+__global__ __launch_bounds__(kBlock) void k_copy_batch(CopyArgs a) {
+    const int t = blockIdx.y;
+    if (t >= a.n) return;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < a.words[t]; i += (int64_t)gridDim.x * kBlock)
+        a.dst[t][i] = a.src[t][i];
+}
+
 // One scatter launch for a build's inputs: task y copies its bytes from the
 // staging block (src >= 0: byte offset) or zero-fills them (src < 0).  Grid
 // (<= 32, tasks).
@@ -1141,6 +1154,29 @@ __global__ __launch_bounds__(kUpBlock) void k_build_report(const uint32_t* __res
 }
 
 }  // namespace
+
+int tpe_rt::copy_batch(tpe_ctx* ctx, hipStream_t st, const CopySpec* specs, int n) {
+    for (int i0 = 0; i0 < n; i0 += kCopyBatch) {
+        CopyArgs a{};
+        int64_t mx = 1;
+        for (int t = 0; t < kCopyBatch && i0 + t < n; ++t) {
+            const CopySpec& c = specs[i0 + t];
+            if (c.bytes <= 0) continue;
+            if ((c.bytes & 3) || ((uintptr_t)c.dst & 3) || ((uintptr_t)c.src & 3))
+                return ctx->fail(TPE_ERR_ARG, "copy_batch: unaligned copy");
+            a.dst[a.n] = (uint32_t*)c.dst;
+            a.src[a.n] = (const uint32_t*)c.src;
+            a.words[a.n] = c.bytes / 4;
+            mx = std::max(mx, a.words[a.n]);
+            ++a.n;
+        }
+        if (a.n == 0) continue;
+        hipLaunchKernelGGL(k_copy_batch, dim3((unsigned)std::min<int64_t>((mx + kBlock - 1) / kBlock, 1024), a.n),
+                           dim3(kBlock), 0, st, a);
+        HIPCHK(ctx, hipGetLastError());
+    }
+    return TPE_OK;
+}
 
 // ============================================================ host side ====
 namespace {
@@ -1287,23 +1323,36 @@ int history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial,
     HIPCHK(ctx, B.seg_end.reserve(L));
     // the caller's arrays and this call's offsets into page-locked staging:
     // the copies below run on the stream while the host returns
-    HIPCHK(ctx, B.h_st_off.resize(L + 1));
-    HIPCHK(ctx, B.h_seg.resize(2 * (size_t)L));
-    HIPCHK(ctx, B.h_trial.resize(total));
-    HIPCHK(ctx, B.h_val.resize(total));
-    HIPCHK(ctx, B.h_cnt.resize(L));
-    std::memcpy(B.h_st_off.data(), st.data(), (L + 1) * sizeof(int64_t));
+    // one staging block (offsets, values, trials, segments, the new counts),
+    // one H2D copy and one scatter launch (six copies before)
+    auto al = [](int64_t v) { return (v + 15) / 16 * 16; };
+    const int64_t o_off = 0, o_val = al((L + 1) * 8), o_trial = o_val + al(total * 8),
+                  o_seg = o_trial + al(total * 4), o_cnt = o_seg + al(2 * (int64_t)L * 4),
+                  o_end = o_cnt + al((int64_t)L * 4);
+    HIPCHK(ctx, B.h_stage.resize(o_end));
+    HIPCHK(ctx, B.d_stage.reserve(o_end));
+    uint8_t* hs = B.h_stage.data();
+    std::memcpy(hs + o_off, st.data(), (L + 1) * sizeof(int64_t));
+    int32_t* seg = (int32_t*)(hs + o_seg);
     for (int32_t l = 0; l < L; ++l) {
-        B.h_seg[l] = (int32_t)st[l];
-        B.h_seg[L + l] = (int32_t)(B.specs_h[l].kind == TPE_CATEGORICAL ? st[l] : st[l + 1]);
+        seg[l] = (int32_t)st[l];
+        seg[L + l] = (int32_t)(B.specs_h[l].kind == TPE_CATEGORICAL ? st[l] : st[l + 1]);
     }
-    std::memcpy(B.h_trial.data(), obs_trial, total * sizeof(int32_t));
-    std::memcpy(B.h_val.data(), obs_val, total * sizeof(double));
-    HIPCHK(ctx, hipMemcpyAsync(B.st_off.p, B.h_st_off.data(), (L + 1) * sizeof(int64_t), hipMemcpyHostToDevice, sm));
-    HIPCHK(ctx, hipMemcpyAsync(B.st_trial.p, B.h_trial.data(), total * sizeof(int32_t), hipMemcpyHostToDevice, sm));
-    HIPCHK(ctx, hipMemcpyAsync(B.st_val.p, B.h_val.data(), total * sizeof(double), hipMemcpyHostToDevice, sm));
-    HIPCHK(ctx, hipMemcpyAsync(B.seg_begin.p, B.h_seg.data(), L * sizeof(int32_t), hipMemcpyHostToDevice, sm));
-    HIPCHK(ctx, hipMemcpyAsync(B.seg_end.p, B.h_seg.data() + L, L * sizeof(int32_t), hipMemcpyHostToDevice, sm));
+    std::memcpy(hs + o_trial, obs_trial, total * sizeof(int32_t));
+    std::memcpy(hs + o_val, obs_val, total * sizeof(double));
+    int32_t* cnt_new = (int32_t*)(hs + o_cnt);
+    for (int32_t l = 0; l < L; ++l) cnt_new[l] = B.cnt_h[l] + (int32_t)n_new[l];
+    HIPCHK(ctx, hipMemcpyAsync(B.d_stage.p, hs, o_end, hipMemcpyHostToDevice, sm));
+    {
+        const uint8_t* ds = B.d_stage.p;
+        const CopySpec cs[5] = {{B.st_off.p, ds + o_off, (L + 1) * 8},
+                                {B.st_trial.p, ds + o_trial, total * 4},
+                                {B.st_val.p, ds + o_val, total * 8},
+                                {B.seg_begin.p, ds + o_seg, (int64_t)L * 4},
+                                {B.seg_end.p, ds + o_seg + (int64_t)L * 4, (int64_t)L * 4}};
+        const int rc = tpe_rt::copy_batch(ctx, sm, cs, 5);
+        if (rc) return rc;
+    }
     int64_t mx_new = 0, mx_all = 0;
     for (int32_t l = 0; l < L; ++l) {
         mx_new = std::max(mx_new, n_new[l]);
@@ -1356,8 +1405,11 @@ int history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial,
     std::swap(B.s_key, B.s_key2);
     std::swap(B.s_idx, B.s_idx2);
     for (int32_t l = 0; l < L; ++l) B.cnt_h[l] += (int32_t)n_new[l];
-    std::memcpy(B.h_cnt.data(), B.cnt_h.data(), L * sizeof(int32_t));
-    HIPCHK(ctx, hipMemcpyAsync(B.cnt.p, B.h_cnt.data(), L * sizeof(int32_t), hipMemcpyHostToDevice, sm));
+    {   // the new counts, from the staging block
+        const CopySpec cs{B.cnt.p, B.d_stage.p + o_cnt, (int64_t)L * 4};
+        const int rc = tpe_rt::copy_batch(ctx, sm, &cs, 1);
+        if (rc) return rc;
+    }
     // no wait here: the next append waits for these copies before it
     // rewrites the staging buffers (round 4 synchronised every append)
     HIPCHK(ctx, hipEventRecord(B.ev_staged, sm));

@@ -259,6 +259,17 @@ struct Posterior {
     }
 };
 
+// device-to-device copies in ONE launch, the specs passed by value (no
+// table to upload): each was its own hipMemcpyAsync -- a blit kernel of ~5
+// us on the device and ~7 us of host API time (tpe_build.hip)
+struct CopySpec {
+    void* dst;
+    const void* src;
+    int64_t bytes;   // a multiple of 4, both pointers 4-byte aligned
+};
+constexpr int kCopyBatch = 8;
+int copy_batch(tpe_ctx* ctx, hipStream_t st, const CopySpec* specs, int n);
+
 // one input of a build in its staging block (k_build_inputs)
 struct UpTask {
     int64_t src;     // byte offset in the staging block; < 0: zero-fill
@@ -295,9 +306,8 @@ struct BuildBufs {
     // an append's host side, page-locked: its H2D copies run on the stream
     // without the host waiting for them (the next append first waits for
     // ev_staged, the copies out of these buffers)
-    PinVec<int64_t> h_st_off;
-    PinVec<int32_t> h_trial, h_seg, h_cnt;
-    PinVec<double> h_val;
+    PinVec<uint8_t> h_stage;       // offsets, values, trials, segments, new counts
+    DevBuf<uint8_t> d_stage;
     hipEvent_t ev_staged = nullptr;
     bool staged_pending = false;
     // per build
@@ -340,7 +350,7 @@ struct BuildBufs {
         gs_lab2.release(); losses.release(); below.release(); keys.release();
         idx.release(); below_val.release(); counts.release(); kcount.release(); w.release();
         mu.release(); sigma.release(); mix_off.release(); scratch.release(); ties.release();
-        order_off.release(); order.release(); only.release(); d_up.release(); d_rep.release();
+        order_off.release(); order.release(); only.release(); d_up.release(); d_rep.release(); d_stage.release();
         if (ev_up) (void)hipEventDestroy(ev_up);
         ev_up = nullptr;
         up_pending = false;

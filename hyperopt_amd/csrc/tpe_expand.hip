@@ -899,15 +899,14 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
     HIPCHK(ctx, P.bx_snap_c.reserve(std::max<int64_t>(c_ext, 1)));
     HIPCHK(ctx, P.bx_snap_s.reserve(std::max<int64_t>(s_ext, 1)));
     HIPCHK(ctx, P.bx_snap_g.reserve(nl));
-    HIPCHK(ctx, hipMemcpyAsync(P.bx_snap_l.p, P.labels.p, P.n_labels * sizeof(DLabel), hipMemcpyDeviceToDevice,
-                               ctx->stream));
-    if (c_ext > 0)
-        HIPCHK(ctx, hipMemcpyAsync(P.bx_snap_c.p, P.comps64.p, c_ext * sizeof(Comp<double>), hipMemcpyDeviceToDevice,
-                                   ctx->stream));
-    if (s_ext > 0)
-        HIPCHK(ctx, hipMemcpyAsync(P.bx_snap_s.p, P.samp.p, s_ext * sizeof(SampRec), hipMemcpyDeviceToDevice,
-                                   ctx->stream));
-    HIPCHK(ctx, hipMemcpyAsync(P.bx_snap_g.p, grp, nl * sizeof(int32_t), hipMemcpyDeviceToDevice, ctx->stream));
+    {   // (one launch: four copies before)
+        const tpe_rt::CopySpec cs[4] = {{P.bx_snap_l.p, P.labels.p, (int64_t)P.n_labels * (int64_t)sizeof(DLabel)},
+                                        {P.bx_snap_c.p, P.comps64.p, c_ext * (int64_t)sizeof(Comp<double>)},
+                                        {P.bx_snap_s.p, P.samp.p, s_ext * (int64_t)sizeof(SampRec)},
+                                        {P.bx_snap_g.p, grp, (int64_t)nl * (int64_t)sizeof(int32_t)}};
+        const int rc = tpe_rt::copy_batch(ctx, ctx->stream, cs, 4);
+        if (rc) return rc;
+    }
     P.bx_snap_nl = nl;
     P.bx_ok = true;
     P.bx_ready = true;
