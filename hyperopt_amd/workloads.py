@@ -7,7 +7,13 @@ import numpy as np
 from . import posterior as P
 
 PREPARE_MIN = 8192   # candidate slots of a round from which it uses the expansion index
-OVERLAP_MIN_DENSE = 1   # index labels from which the index runs beside the host's tie orders (r4ab: with the ordered rebuild beside the index, a 4-label step 1.35 -> 1.22 ms)
+# index labels from which the first build goes without the tie orders and
+# the index runs beside the host's argsorts and the ordered subset rebuild;
+# below it the known labels' argsorts come first and ONE ordered build
+# follows (r5q, config 3: a 4-label shard's step 1.19 -> 1.10 ms without the
+# overlap, the whole 32-label step 2.57 -> 2.88 ms: the index is long enough
+# to hide the argsorts only with many dense labels)
+OVERLAP_MIN_DENSE = 8
 DENSE_KINDS = ('uniform', 'loguniform', 'normal', 'lognormal')
 
 # config-3 kind cycle: kind = i mod 5
