@@ -11,6 +11,7 @@
 #   bench            the default bench.py line (what the driver runs)
 #   bench=<args>     bench.py with extra arguments (commas for spaces)
 #   var=<name>[,args] bench.py on the variant library tools/var_<name>.so (tools/build_variant.py)
+#   trace=<args>     rocprofv3 --kernel-trace --stats of bench.py <args> -> <tag>/trace<n>
 #   prof             tools/prof_round.sh <tag> (kernel trace + PMC passes of the default line)
 #   lpdf             the plain fp64 round's trace + PMC passes (tools/prof_round.sh <tag>_lpdf)
 #   shard=<r>        label shard r of config 3 alone: probe + kernel/HIP-API trace
@@ -67,6 +68,10 @@ for s in "$@"; do
             v=${a%%,*}
             rest=""; [ "$a" != "$v" ] && rest=${a#*,}
             run var_$v$n 600 env HYPEROPT_AMD_VARIANT=tools/var_$v.so python -u bench.py ${rest//,/ } || exit 1 ;;
+        trace=*)   # rocprofv3 kernel trace + stats of bench.py with these arguments (commas for spaces)
+            a=${s#trace=}
+            run trace$n 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace$n" -o run --output-format csv \
+                -- python -u bench.py ${a//,/ } || exit 1 ;;
         prof)
             bash tools/prof_round.sh "$T" --steps 5 --warmup 2 --no-other-configs --no-agreement || exit 1 ;;
         lpdf)   # the plain fp64 round (k_round<double>, no screen) at config 3: trace + PMC passes
