@@ -445,6 +445,8 @@ struct tpe_ctx {
     DevBuf<int32_t> hot_a;               //   or their accepted attempts (k_hot_bx32: re-drawn in fp64)
     int32_t hot32 = 0;                   // TPE_OPT_HOT32: the prefilter draws in fp32 (k_hot_bx32; 2: bounds x 4096, tests)
     int32_t bx_split = 0;                // TPE_OPT_BX_SPLIT (0: auto)
+    int32_t bx_t_force = 0;              // TPE_OPT_BX_T (0: auto)
+    double bx_t_next = 96.0;             // the cut T of the next index built (set by its caller)
     DevBuf<int32_t> hot_i, hot_cnt;      //   their indices; per cell the count
     DevBuf<unsigned long long> hot_t, hot_tau0;   // per cell largest L; per label tau0
     DevBuf<uint32_t> hot_bits;           // per sub-bin: U >= tau0 (words at sb_off / 32)

@@ -1276,7 +1276,13 @@ __device__ __host__ __forceinline__ int win_bin(const WinLabel& W, double x) {
 // best score are re-scored.
 constexpr int kBxP = 15;          // Taylor coefficients per bin
 constexpr int kBxRow = 16;        // doubles per bin row (one 128-B line): A_0..A_14, Eabs
-constexpr double kBxT = 96.0;     // components left out stay below 2^-kBxT
+// components left out of a bin's window stay below 2^-T of the largest
+// term (T per index, BxLabel.tcut): 96 for the packed map's rounds (their
+// value-only certification needs the tighter bound), 64 for tile rounds
+// through the hot-bin prefilter (narrower windows, fewer bins: config 3's
+// index 0.53 -> 0.45 ms with the same re-scores, r5t)
+constexpr double kBxT = 96.0;
+constexpr double kBxTTile = 64.0;
 
 struct BxLabel {
     double xlo, inv_bw, bw;   // bin b = floor((x' - xlo) inv_bw), centre xlo + (b + 1/2) bw
@@ -1290,6 +1296,7 @@ struct BxLabel {
     int32_t nbins, n_nc;      // bins; unclipped components (listed at comp_a in bx_nc)
     double inv_sbw;           // kBxSub / bw: sub-bin of x' = floor((x' - xlo) inv_sbw)
     int64_t sb_off;           // first of its nbins kBxSub sub-bins in bx_sb / bx_sbp
+    double tcut;              // the window's cut T: components left out stay below 2^-T
 };
 
 // Hot-bin prefilter of the expansion screen.  Each bin is cut into kBxSub

@@ -560,7 +560,7 @@ __device__ __forceinline__ int bx_score(const DLabel& L, const BxLabel& B,
     // log instead of two; candidates whose below sum underflows -- the fp64
     // round's two-pass fallback -- are uncertified)
     const Comp<double>* ca = comps64 + L.comp_a;
-    const double skip_abs = (double)L.na * exp2(-kBxT);
+    const double skip_abs = (double)L.na * exp2(-B.tcut);
     int nterms = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -575,7 +575,7 @@ __device__ __forceinline__ int bx_score(const DLabel& L, const BxLabel& B,
 #pragma unroll
         for (int k = kBxP - 2; k >= 0; --k) poly = fma(poly, delta, rw[k]);
         const double eabs = rw[kBxP];
-        // exp(-t), t = kappa delta^2 <= kappa rmax^2 <= 0.0625 / (T ln 2) < 1e-3:
+        // exp(-t), t = kappa delta^2 <= kappa rmax^2 <= 0.0625 / (T ln 2) < 3e-3 (T >= 32):
         // degree 5 leaves t^6 / 720 < 2e-21 (inside the 8 u S_clip term)
         const double t = B.kappa * delta * delta;
         const double et = fma(fma(fma(fma(fma(-1.0 / 120.0, t, 1.0 / 24.0), t, -1.0 / 6.0), t, 0.5), t,
@@ -3464,6 +3464,7 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
     RoundSel* rsel = reinterpret_cast<RoundSel*>(ctx->scr_rsel.p);
     bool use_bx = false;
     if (ctx->expand && cap >= kWinMinN && a.n <= kBxR * kBlock) {
+        ctx->bx_t_next = kBxT;   // (the packed map: value-only certification)
         int rc = tpe_rt::bx_prepare(ctx);
         if (rc) return rc;
         use_bx = ctx->P->bx_ok;
@@ -3645,6 +3646,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
         ctx->hot_listed = 0;
         ctx->hot_fallback = 0;
         if (ctx->expand && a.n >= kWinMinN && a.cand_in == nullptr) {
+            ctx->bx_t_next = kBxTTile;   // (tile rounds: the hot-bin prefilter)
             int rc = tpe_rt::bx_prepare(ctx);
             if (rc) return rc;
             use_bx = ctx->P->bx_ok;
@@ -4887,6 +4889,7 @@ int tpe_hot_probe(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, do
     if (d.mode != DENSE_GMM && d.mode != DENSE_LGMM)
         return ctx->fail(TPE_ERR_ARG, "hot probe: label is not a dense GMM1/LGMM1 label");
     HIPCHK(ctx, hipSetDevice(ctx->device));
+    ctx->bx_t_next = kBxTTile;   // (the probes check the tile rounds' index)
     int rc = tpe_rt::bx_prepare(ctx);
     if (rc) return rc;
     tpe_rt::Posterior& P = *ctx->P;
@@ -4927,6 +4930,7 @@ int tpe_screen_probe(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n,
     HIPCHK(ctx, hipMemcpyAsync(ctx->cand.p, cand, n * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
     bool use_bx = false;
     if (ctx->expand && n >= 2048) {
+        ctx->bx_t_next = kBxTTile;
         int rc = tpe_rt::bx_prepare(ctx);
         if (rc) return rc;
         use_bx = ctx->P->bx_ok;
@@ -5082,6 +5086,7 @@ TPE_DEV int tpe1_prepare(tpe_ctx* ctx, int64_t n_candidates, int32_t n_rounds) {
     if (ctx->precision != TPE_F64 || !ctx->screen || !ctx->expand || n_candidates * n_rounds < kWinMinN)
         return TPE_OK;
     HIPCHK(ctx, hipSetDevice(ctx->device));
+    ctx->bx_t_next = n_candidates >= kTile ? kBxTTile : kBxT;   // (the map the rounds take)
     int rc = tpe_rt::bx_prepare(ctx);
     if (rc == TPE_OK && ctx->hot && n_candidates >= kWinMinN) rc = hot_tau_prepare(ctx, n_candidates);
     return rc;
@@ -5113,6 +5118,10 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
         case TPE_OPT_ZERO_WIN: ctx->zero_win = value != 0; break;
         case TPE_OPT_VALUE_ONLY: ctx->value_only = value != 0; break;
         case TPE_OPT_HOT32: ctx->hot32 = (int32_t)value; break;
+        case TPE_OPT_BX_T:
+            if (value != 0 && (value < 32 || value > 128)) return ctx->fail(TPE_ERR_ARG, "index cut T must be 0 or in [32, 128]");
+            ctx->bx_t_force = (int32_t)value;
+            break;
         case TPE_OPT_BX_SPLIT:
             if (value < 0 || value > 8) return ctx->fail(TPE_ERR_ARG, "index window split must be in [0, 8]");
             ctx->bx_split = (int32_t)value;

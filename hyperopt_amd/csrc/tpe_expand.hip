@@ -194,7 +194,7 @@ __device__ __forceinline__ bool reaches(const Comp<double>& r, const BxLabel& B,
     const double e0 = B.xlo + (double)b * B.bw, e1 = e0 + B.bw;
     const double slack = (fabs(e0) + fabs(e1) + B.bw) * 1e-12;
     const double dist = fmax(0.0, fmax(e0 - slack - mu, mu - e1 - slack)) * (1.0 - 1e-9);
-    return r.c * kExpScaleInv - kap * dist * dist >= -(kBxT * kLn2 + 1.0);
+    return r.c * kExpScaleInv - kap * dist * dist >= -(B.tcut * kLn2 + 1.0);
 }
 
 // grid (ceil(max bins / 256), dense labels): per bin the unclipped
@@ -668,7 +668,7 @@ __global__ __launch_bounds__(kBlock) void k_bx_bounds(const DLabel* __restrict__
         }
         gauss_bounds(r, e0, e1, slo, shi, etab);
     }
-    shi += (double)L.na * exp2(-kBxT);
+    shi += (double)L.na * exp2(-B.tcut);
     const double dsh = L.shift_b - L.shift_a;
     const double mag = fabs(L.shift_b) + fabs(L.shift_a) + 2.0 * (fabs(L.centre) + fabs(e0) + fabs(e1)) + 64.0;
     const double fe = (double)(L.nb + L.na + 64) * 0x1.0p-50 + mag * 0x1.0p-48;
@@ -804,6 +804,9 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
     // bins per label: the fewest (a multiple of 64) whose half-width keeps
     // the Taylor argument 2 kappa |d| r <= ~0.5 over the window
     P.bx_h.assign(P.n_labels, BxLabel{});
+    // the window's cut: forced (TPE_OPT_BX_T), else what the coming rounds
+    // need (tile rounds through the hot-bin prefilter: kBxTTile)
+    const double T = ctx->bx_t_force > 0 ? (double)ctx->bx_t_force : ctx->bx_t_next;
     bool ok = true;
     int64_t rows = 0, lsum = 0;
     int32_t bins_max = 0;
@@ -819,7 +822,7 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
             ok = false;
             break;
         }
-        const double d0 = std::sqrt(kBxT * kLn2 / kap);
+        const double d0 = std::sqrt(T * kLn2 / kap);
         const double r_target = 0.25 / (kap * d0);   // Taylor argument 2 kappa |d| r <= ~0.5
         const double want = (xhi - xlo) / (2.0 * r_target);
         if (!(want <= (double)kMaxBins)) {
@@ -842,6 +845,7 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
         B.nbins = nb;
         B.n_nc = n_nc;
         B.inv_sbw = (double)kBxSub / B.bw;
+        B.tcut = T;
         B.sb_off = rows * kBxSub;   // (nb a multiple of 64: a multiple of 32, as k_hot_bx needs)
         B.tab_off = rows;
         B.cnt_off = rows;           // one list count per bin

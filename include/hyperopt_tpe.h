@@ -536,6 +536,9 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *                   Taylor tables, each summing one part of the bins' window
  *                   (k_bx_table / k_bx_table_fin; 1..8, 0: enough for ~8192
  *                   workgroups)                                            [0]
+ *   TPE_OPT_BX_T    the expansion index's window cut T (components left
+ *                   out stay below 2^-T of the largest term; 32..128; 0:
+ *                   64 for tile rounds, 96 for the packed map's)           [0]
  *   TPE_OPT_WIN_GROUPS  label groups of a windowed round, each sorted on a
  *                   second stream while the previous one is screened
  *                   (0: one group; the chip is busy either way)          [0]
@@ -570,6 +573,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_AUX_FAMILIES 19
 #define TPE_OPT_HOT32 20
 #define TPE_OPT_BX_SPLIT 21
+#define TPE_OPT_BX_T 22
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
 
 /* Build now what the resident posterior's first round(s) of n_candidates

@@ -515,3 +515,37 @@ def test_index_window_split_same_round(eng, split):
     finally:
         eng.set_option('bx_split', 0)
     _assert_same(a, b)
+
+
+@pytest.mark.parametrize('cut', [48, 96, 128])
+def test_index_cut_same_round(eng, cut):
+    """The expansion index's window cut T (TPE_OPT_BX_T; auto: 64 for tile
+    rounds, 96 for the packed map's): fewer or more components in a bin's
+    window and its bound's skipped mass na 2^-T -- the winners do not move,
+    and the sub-bin bounds of the forced-T index still bracket the fp64
+    score."""
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.workloads import mixed_history
+    hist = mixed_history(32, 10000, seed=0)
+    packed = P.pack(hist.posteriors())
+    posts = hist.posteriors()
+    C = 1 << 20
+    try:
+        eng.set_option('bx_t', 0)
+        eng.set_posterior(*packed)
+        a = eng.suggest(29, C, round=6)
+        eng.set_option('bx_t', cut)
+        eng.set_posterior(*packed)
+        b = eng.suggest(29, C, round=6)
+        for li in (0, 1, 3):
+            p = posts[li]
+            samp = eng.GMM1 if p.family == 'GMM1' else eng.LGMM1
+            x = samp(*p.below, low=p.low, high=p.high, q=None, seed=4, size=(20000,), stream=li)
+            u, l, _ = eng.hot_probe(li, x)
+            lb, la, _ = eng.score(li, x)
+            s64 = lb - la
+            fin = np.isfinite(s64)
+            assert np.all(l[fin] <= s64[fin]) and np.all(s64[fin] <= u[fin]), li
+    finally:
+        eng.set_option('bx_t', 0)
+    _assert_same(a, b)

@@ -24,6 +24,11 @@ from hyperopt_amd import _build  # noqa: E402
 
 # name -> [(file, old text, new text)]: result-changing timing experiments
 PATCHES = {
+    # the expansion index's cut: components left out below 2^-64 / 2^-48 of the
+    # largest term instead of 2^-96 (narrower windows and fewer bins; the
+    # screen's bound carries the skipped mass)
+    'bxt64': [('tpe_device.h', 'constexpr double kBxT = 96.0;', 'constexpr double kBxT = 64.0;')],
+    'bxt48': [('tpe_device.h', 'constexpr double kBxT = 96.0;', 'constexpr double kBxT = 48.0;')],
     # k_bx_table: ocml's fp64 exp (<= 1 ulp) instead of the 32 KB LDS table exp: no
     # table load per workgroup, no dependent LDS read per term, 5 workgroups per CU
     'bxexp': [('tpe_expand.hip', '    __shared__ double lds[kExpTabSize];   // the exp table, then the waves\' partial sums',
