@@ -868,12 +868,16 @@ __device__ __forceinline__ void hot_wave_flush32(int n, const int32_t* bi, const
     __builtin_amdgcn_wave_barrier();
 }
 
+// Six workgroups per CU (80 VGPRs, a few spilled): the draw loop's waits
+// on LDS and the list are hidden by more waves -- 1.26 -> 1.215 ms against
+// five per CU without spills, twice in one call (r5x: tools/build_variant.py
+// lb6).
 // LDS_BITS: every label's bits fit in LDS (the host knows the largest
 // label's sub-bins) -- the bit test is then a ds_read; otherwise every
 // label reads them from global memory.  (One kernel choosing per label
 // compiled to a generic-address load with per-lane address selects.)
 template <int R, bool LDS_BITS>
-__global__ __launch_bounds__(kBlock, 5) void k_hot_bx(
+__global__ __launch_bounds__(kBlock, 6) void k_hot_bx(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
     const BxLabel* __restrict__ bx, const uint32_t* __restrict__ hbits, int64_t n, int64_t cand_offset,
     uint64_t seed, const uint32_t* __restrict__ rounds, int32_t nl, int32_t* __restrict__ hcnt,

@@ -118,10 +118,10 @@ PATCHES = {
     'bm': [('tpe_device.h',
             '    return __builtin_amdgcn_sqrt(fmax(0.0, 2.0 * bm_neglog(u01_open0(y), lt)));\n',
             '    return (double)y * 0x1.0p-31;\n')],
-    'lb4': [('tpe_engine.hip', '__launch_bounds__(kBlock, 5) void k_hot_bx(',
+    'lb4': [('tpe_engine.hip', '__launch_bounds__(kBlock, 6) void k_hot_bx(',
              '__launch_bounds__(kBlock, 4) void k_hot_bx(')],
-    'lb6': [('tpe_engine.hip', '__launch_bounds__(kBlock, 5) void k_hot_bx(',
-             '__launch_bounds__(kBlock, 6) void k_hot_bx(')],
+    'lb5': [('tpe_engine.hip', '__launch_bounds__(kBlock, 6) void k_hot_bx(',
+             '__launch_bounds__(kBlock, 5) void k_hot_bx(')],
     'bxlb4': [('tpe_expand.hip', '__global__ __launch_bounds__(kBlock) void k_bx_table(',
                '__global__ __launch_bounds__(kBlock, 4) void k_bx_table(')],
     'bx3': [('tpe_expand.hip', 'constexpr int kBxChains = 4;', 'constexpr int kBxChains = 3;')],
