@@ -877,13 +877,12 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
     // the window split: ~8192 workgroups (4 per CU at a time, LDS-bound; the
     // heavy dense-region blocks split too, so the tail shortens -- config 3's
     // ~2000 blocks: split 1 / 2 / 4 / 8 -> 0.628 / 0.592 / 0.564 / 0.604 ms, r5j)
-    // (at least 2 up to 16384 blocks: config 5's ~6000 blocks split in 2,
-    // 4.81 -> 4.60 ms, r5s)
+    // (config 5's ~6000 blocks split in 2: the index 4.8 -> 4.6 ms, but the
+    // quantized labels' rebuild beside it on the second stream 1.5 -> 2.1 ms,
+    // the step unchanged -- r5z: not split)
     const int64_t wgs = (rows + 63) / 64;
-    const int nsplit = ctx->bx_split > 0
-                           ? std::min(ctx->bx_split, kBxMaxSplit)
-                           : wgs > 16384 ? 1
-                                         : (int)std::max<int64_t>(2, std::min<int64_t>(kBxMaxSplit, (8192 + wgs / 2) / std::max<int64_t>(wgs, 1)));
+    const int nsplit = ctx->bx_split > 0 ? std::min(ctx->bx_split, kBxMaxSplit)
+                                         : (int)std::max<int64_t>(1, std::min<int64_t>(kBxMaxSplit, 8192 / std::max<int64_t>(wgs, 1)));
     if (nsplit > 1) HIPCHK(ctx, P.bx_part.reserve((size_t)nsplit * kPartSums * rows));
     hipLaunchKernelGGL(k_bx_table, dim3((unsigned)((bins_max + 63) / 64), nl, nsplit), dim3(kBlock), 0,
                        ctx->stream, P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p, nsplit, P.bx_part.p, rows);
