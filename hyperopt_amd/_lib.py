@@ -59,6 +59,7 @@ TPE_OPT_AUX_FAMILIES = 19
 TPE_OPT_HOT32 = 20
 TPE_OPT_BX_SPLIT = 21
 TPE_OPT_BX_T = 22
+TPE_OPT_PK_SLICED = 23
 
 TPE_OBS_IDENTITY = 0
 TPE_OBS_LOG = 1

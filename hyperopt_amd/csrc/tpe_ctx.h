@@ -445,6 +445,7 @@ struct tpe_ctx {
     DevBuf<int32_t> hot_a;               //   or their accepted attempts (k_hot_bx32: re-drawn in fp64)
     int32_t hot32 = 0;                   // TPE_OPT_HOT32: the prefilter draws in fp32 (k_hot_bx32; 2: bounds x 4096, tests)
     int32_t bx_split = 0;                // TPE_OPT_BX_SPLIT (0: auto)
+    int64_t pk_sliced = 8192;            // TPE_OPT_PK_SLICED (0: never sliced)
     int32_t bx_t_force = 0;              // TPE_OPT_BX_T (0: auto)
     double bx_t_next = 96.0;             // the cut T of the next index built (set by its caller)
     DevBuf<int32_t> hot_i, hot_cnt;      //   their indices; per cell the count
@@ -489,6 +490,8 @@ struct tpe_ctx {
     tpe_rt::DevBuf<uint8_t> rep_d;
     tpe_rt::PinVec<uint8_t> rep_h;
     tpe_rt::PinVec<tpe_label_result> res_h;   // a round's results, staged before the caller's buffer
+    static constexpr int kResPieces = 4;      //   read back in pieces when large (copy_out overlaps)
+    hipEvent_t ev_res[kResPieces] = {};
     tpe_rt::PinVec<tpe::DLabel> dl_h;         // a build's label records, read back
     tpe_rt::PinVec<int32_t> ties_h;           //   and its tie report
     DevBuf<int64_t> scr_chunks;          // k_rescore chunk table ({cell, chunk} int32 pairs)

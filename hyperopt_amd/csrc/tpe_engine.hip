@@ -31,6 +31,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/hyperopt_tpe.h"
@@ -1432,7 +1433,7 @@ constexpr int kCatR = 8;  // candidates per thread, k_cat_tiles
 using RescorePlan = tpe_rt::RescorePlanH;
 constexpr int kPlanBlock = 1024;
 __global__ __launch_bounds__(kPlanBlock) void k_rescore_plan(const int32_t* __restrict__ cnt, int64_t cells,
-                                                             int32_t per_full, int32_t allow_sliced, int64_t cap,
+                                                             int32_t per_full, int64_t sliced_max, int64_t cap,
                                                              RescoreChunk* __restrict__ chunks,
                                                              int64_t* __restrict__ range, int64_t* __restrict__ eoff,
                                                              RescorePlan* __restrict__ plan) {
@@ -1457,7 +1458,7 @@ __global__ __launch_bounds__(kPlanBlock) void k_rescore_plan(const int32_t* __re
         if (threadIdx.x == 0) *plan = RescorePlan{total, 0, 0, 1, 0};
         return;
     }
-    const bool sliced = allow_sliced && total <= kSlicedRescoreMax;
+    const bool sliced = sliced_max > 0 && total <= sliced_max;
     const int64_t per = sliced ? (int64_t)kRsW : (int64_t)per_full;
     int64_t carry = 0, ecarry = 0;   // entries and candidates before this block of cells
     for (int64_t c0 = 0; c0 < cells; c0 += kPlanBlock) {
@@ -2053,7 +2054,7 @@ __global__ __launch_bounds__(kBlock) void k_rescore_packed(
     const RescoreChunk* __restrict__ chunks, const int64_t* __restrict__ off, const RescorePlan* __restrict__ plan,
     int64_t total, double* __restrict__ planes, const double* __restrict__ zhi, const double* __restrict__ zlo,
     const int32_t* __restrict__ zwide, const int32_t* __restrict__ zn) {
-    if (plan->overflow) return;
+    if (plan->overflow || plan->sliced) return;
     const int32_t ne = plan->ne;
     if ((int32_t)blockIdx.x >= ne) return;   // (uniform, before the table's barrier)
     __shared__ double exp_tab[kExpTabSize];
@@ -2132,7 +2133,7 @@ __global__ __launch_bounds__(kBlock) void k_finish_rescore(
     const int32_t* __restrict__ cnt, const int64_t* __restrict__ list, int64_t cap,
     const RescoreChunk* __restrict__ chunks, const int64_t* __restrict__ off, const RescorePlan* __restrict__ plan,
     int64_t total, const double* __restrict__ planes, Partial* __restrict__ res) {
-    if (plan->overflow) return;
+    if (plan->overflow || plan->sliced) return;
     const int32_t ne = plan->ne;
     for (int32_t ei = blockIdx.x; ei < ne; ei += gridDim.x) {
     const RescoreChunk ch = chunks[ei];
@@ -2157,6 +2158,134 @@ __global__ __launch_bounds__(kBlock) void k_finish_rescore(
         const int64_t i = list[(size_t)y * cap + e] & 0xffffffffll;
         res[g] = Partial{order_key(lb - la), cand_offset + i, x, lb, la};
     }
+    }
+}
+
+// The packed map's re-score of a few listed candidates (plan->sliced: at most
+// TPE_OPT_PK_SLICED, 8192 by default).  k_rescore_packed gives each listed candidate one
+// thread walking its chunk of the above mixture -- config 5 lists ~1
+// candidate in some rounds, and that one thread's chain of ~7k dependent
+// fp64 terms took 1.6 ms (r5ac).  Here one wave sums one kSumSlice slice for
+// kRsW listed candidates of a label (entry {label, j}), in the packed map's
+// order: the below mixture's slices from record 0, the above mixture's per
+// chunk of `chunk` records (slices from the chunk's start, spc per chunk),
+// each chunk's slice sums added in order and the chunk sums added in order
+// (k_round_chunk / k_finish_chunks / k_rescore_packed: the same bits).
+// Slices outside the wave's zero window are exactly +0.0 and skipped.
+// part: [entry][s_max][kRsW], s_max = below slices + nch * spc.
+
+__global__ __launch_bounds__(kBlock) void k_rescore_draw_packed(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
+    int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, const RescorePlan* __restrict__ plan,
+    const int32_t* __restrict__ cnt, const int64_t* __restrict__ list, int64_t cap,
+    const RescoreChunk* __restrict__ chunks, double* __restrict__ xbuf, int64_t* __restrict__ gbuf) {
+    if (plan->overflow || !plan->sliced) return;
+    const int32_t ne = plan->ne;
+    const int lane = threadIdx.x % kRsW;
+    for (int e = blockIdx.x * (kBlock / kRsW) + threadIdx.x / kRsW; e < ne; e += gridDim.x * (kBlock / kRsW)) {
+    const RescoreChunk ch = chunks[e];
+    const DLabel L = labels[group[ch.cell]];
+    const bool lgmm = L.mode == DENSE_LGMM;
+    const int64_t j = (int64_t)ch.j * kRsW + lane;
+    double v = lgmm ? 1.0 : 0.0;
+    int64_t g = -1;
+    if (j < cnt[ch.cell]) {
+        const int64_t ent = list[(size_t)ch.cell * cap + j];
+        const uint32_t rk = rounds[ent >> 32], gi = (uint32_t)(cand_offset + (ent & 0xffffffffll));
+        if (lgmm) (void)sample_below<DENSE_LGMM>(L, samp + L.samp_off, seed, rk, gi, v);
+        else (void)sample_below<DENSE_GMM>(L, samp + L.samp_off, seed, rk, gi, v);
+        g = j;
+    }
+    xbuf[(size_t)e * kRsW + lane] = v;
+    gbuf[(size_t)e * kRsW + lane] = g;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_rescore_slices_packed(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const Comp<double>* __restrict__ comps64,
+    const RescoreChunk* __restrict__ chunks, const RescorePlan* __restrict__ plan, const double* __restrict__ xbuf,
+    const int64_t* __restrict__ gbuf, int32_t s_max, int32_t chunk, int32_t spc, double* __restrict__ part,
+    const double* __restrict__ zhi, const double* __restrict__ zlo, const int32_t* __restrict__ zwide,
+    const int32_t* __restrict__ zn) {
+    if (plan->overflow || !plan->sliced) return;
+    const int32_t ne = plan->ne;
+    if ((int32_t)blockIdx.y >= ne) return;   // (uniform, before the table's barrier)
+    __shared__ double exp_tab[kExpTabSize];
+    load_exp_table(exp_tab);   // (every wave takes part before any leaves)
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int slice = blockIdx.x * (kBlock / 64) + wave;
+    if (slice >= s_max) return;   // (no barrier below)
+    for (int e = blockIdx.y; e < ne; e += gridDim.y) {
+    const RescoreChunk ch = chunks[e];
+    const DLabel L = labels[group[ch.cell]];
+    const int nsb = (L.nb + kSumSlice - 1) / kSumSlice;
+    const double x = xbuf[(size_t)e * kRsW + lane];
+    const bool valid = gbuf[(size_t)e * kRsW + lane] >= 0;
+    const double xr[1] = {(L.mode == DENSE_LGMM ? flog(x) : x) - L.centre};
+    double acc[1] = {0.0};
+    if (slice < nsb) {
+        const int k0 = slice * kSumSlice, k1 = min(k0 + kSumSlice, L.nb);
+        lse_acc_run<1>(comps64 + L.comp_b + k0, k1 - k0, xr, acc, exp_tab);
+    } else {
+        const int s = slice - nsb, c = s / spc;
+        const int kb = min((c + 1) * chunk, L.na);
+        const int k0 = c * chunk + (s - c * spc) * kSumSlice, k1 = min(k0 + kSumSlice, kb);
+        if (k0 < k1) {
+            double xa = valid ? xr[0] : __builtin_inf(), xb = valid ? xr[0] : -__builtin_inf();
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                xa = fmin(xa, __shfl_xor(xa, o));
+                xb = fmax(xb, __shfl_xor(xb, o));
+            }
+            if (zhi && xa <= xb) {
+                const int wlo = __builtin_amdgcn_readfirstlane(first_above(zhi + L.comp_a, L.na, xa, false));
+                const int whi = __builtin_amdgcn_readfirstlane(first_above(zlo + L.comp_a, L.na, xb, true));
+                lse_acc_zero_window<1>(comps64 + L.comp_a, k0, k1, wlo, whi, zwide + L.comp_a,
+                                       zn[group[ch.cell]], xr, acc, exp_tab);
+            } else {
+                lse_acc_run<1>(comps64 + L.comp_a + k0, k1 - k0, xr, acc, exp_tab);
+            }
+        }
+    }
+    part[((size_t)e * s_max + slice) * kRsW + lane] = acc[0];
+    }
+}
+
+__global__ __launch_bounds__(kRsW) void k_rescore_fin_packed(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const Comp<double>* __restrict__ comps64,
+    int64_t cand_offset, int32_t nch, int32_t spc, const int64_t* __restrict__ list, int64_t cap,
+    const RescoreChunk* __restrict__ chunks, const int64_t* __restrict__ off, const RescorePlan* __restrict__ plan,
+    const double* __restrict__ xbuf, const int64_t* __restrict__ gbuf, int32_t s_max,
+    const double* __restrict__ part, Partial* __restrict__ res) {
+    if (plan->overflow || !plan->sliced) return;
+    const int32_t ne = plan->ne;
+    const int lane = threadIdx.x;
+    for (int e = blockIdx.x; e < ne; e += gridDim.x) {
+    const RescoreChunk ch = chunks[e];
+    const int y = ch.cell;
+    const DLabel L = labels[group[y]];
+    const bool lgmm = L.mode == DENSE_LGMM;
+    const int64_t j = gbuf[(size_t)e * kRsW + lane];
+    if (j < 0) continue;
+    const int nsb = (L.nb + kSumSlice - 1) / kSumSlice;
+    const double x = xbuf[(size_t)e * kRsW + lane];
+    const double* p = part + (size_t)e * s_max * kRsW + lane;
+    double sb = 0.0, sa = 0.0;
+    for (int s = 0; s < nsb; ++s) sb += p[(size_t)s * kRsW];
+    for (int c = 0; c < nch; ++c) {
+        double t = 0.0;
+        for (int q = 0; q < spc; ++q) t += p[(size_t)(nsb + c * spc + q) * kRsW];
+        sa += t;
+    }
+    const double yv = lgmm ? flog(x) : x;
+    double lb = lse_finish(comps64 + L.comp_b, L.nb, sb, yv - L.centre, L.shift_b);
+    double la = lse_finish(comps64 + L.comp_a, L.na, sa, yv - L.centre, L.shift_a);
+    if (lgmm) {
+        lb -= yv;
+        la -= yv;
+    }
+    const int64_t i = list[(size_t)y * cap + j] & 0xffffffffll;
+    res[off[y] + j] = Partial{order_key(lb - la), cand_offset + i, x, lb, la};
     }
 }
 
@@ -3039,6 +3168,30 @@ int defer_read(tpe_ctx* ctx, void* dst, const void* src, int64_t bytes) {
     return TPE_OK;
 }
 
+// A round's results from the pinned staging buffer into the caller's array:
+// config 5's batched round returns 25 MB (4096 rounds x 128 labels x 48 B),
+// which one thread copies (first touch of the caller's fresh pages included)
+// in about as long as the round's kernels take; 2 MB slices over up to 8
+// threads (4.20 -> 3.80 ms per config-5 round, r5ab).
+static void copy_out(void* dst, const void* src, size_t bytes) {
+    constexpr size_t kSlice = (size_t)2 << 20;
+    const int nt = (int)std::min<size_t>(8, bytes / kSlice);
+    if (nt < 2) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    const size_t per = (bytes / nt + 63) & ~(size_t)63;
+    auto part = [&](int t) {
+        const size_t a = std::min(bytes, (size_t)t * per), b = std::min(bytes, a + per);
+        if (b > a) std::memcpy((char*)dst + a, (const char*)src + a, b - a);
+    };
+    std::vector<std::thread> th;
+    th.reserve(nt - 1);
+    for (int t = 1; t < nt; ++t) th.emplace_back(part, t);
+    part(0);
+    for (auto& x : th) x.join();
+}
+
 int flush_reads(tpe_ctx* ctx) {
     if (ctx->rep.empty()) return TPE_OK;
     int64_t total = 0, mx = 1;
@@ -3538,16 +3691,30 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
     constexpr int64_t per = (int64_t)kRP * kBlock;
     const int64_t pcap = std::max<int64_t>(1, std::min<int64_t>(ctx->pk_cap, (int64_t)nl * cap));
     const int64_t ne_max = nl + (pcap + per - 1) / per;
+    // a few listed candidates: sliced (k_rescore_slices_packed), entries of
+    // kRsW candidates, s_max slices each
+    const int64_t sl_max = std::min<int64_t>(ctx->pk_sliced, pcap);
+    const int64_t ne_sl = sl_max > 0 ? nl + (sl_max + kRsW - 1) / kRsW : 0;
+    const int32_t spc = (chunk + kSumSlice - 1) / kSumSlice;
+    int32_t s_max = 0;
+    for (int m : {DENSE_GMM, DENSE_LGMM})
+        for (int li : ctx->P->h_group[m])
+            s_max = std::max(s_max, (ctx->P->h_labels[li].nb + kSumSlice - 1) / kSumSlice + nch * spc);
     HIPCHK(ctx, ctx->scr_res.reserve(pcap));
     HIPCHK(ctx, ctx->scr_off.reserve(nl + 1));
-    HIPCHK(ctx, ctx->scr_chunks.reserve(ne_max));
+    HIPCHK(ctx, ctx->scr_chunks.reserve(std::max(ne_max, ne_sl)));
+    if (ne_sl > 0) {
+        HIPCHK(ctx, ctx->rs_x.reserve((size_t)ne_sl * kRsW));
+        HIPCHK(ctx, ctx->rs_g.reserve((size_t)ne_sl * kRsW));
+        HIPCHK(ctx, ctx->rs_part.reserve((size_t)ne_sl * s_max * kRsW));
+    }
     HIPCHK(ctx, ctx->scr_range.reserve(nl));
     HIPCHK(ctx, ctx->scr_planes.reserve((size_t)(nch + 2) * pcap));
     HIPCHK(ctx, ctx->rs_plan.reserve(3));
     RescoreChunk* tabd = reinterpret_cast<RescoreChunk*>(ctx->scr_chunks.p);
     RescorePlan* plan = reinterpret_cast<RescorePlan*>(ctx->rs_plan.p);
     hipLaunchKernelGGL(k_rescore_plan, dim3(1), dim3(kPlanBlock), 0, ctx->stream, ctx->scr_cnt.p, (int64_t)nl,
-                       (int32_t)per, 0, pcap, tabd, ctx->scr_range.p, ctx->scr_off.p, plan);
+                       (int32_t)per, sl_max, pcap, tabd, ctx->scr_range.p, ctx->scr_off.p, plan);
     HIPCHK(ctx, hipMemcpyAsync(&ctx->pin[0].plan, plan, sizeof(RescorePlan), hipMemcpyDeviceToHost, ctx->stream));
     ctx->pk_plan_pending = true;
     {
@@ -3563,6 +3730,20 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
                                P.groups.p + P.group_off[DENSE_GMM], P.comps64.p, P.zw_hi.p, P.zw_lo.p,
                                P.zw_wide.p, P.zw_n.p);
             ctx->zw_pending = true;   // built iff the plan was not empty (read after the round's sync)
+        }
+        if (ne_sl > 0) {
+            const unsigned g_sl = (unsigned)std::min<int64_t>(ne_sl, 1024);
+            hipLaunchKernelGGL(k_rescore_draw_packed, dim3((unsigned)((ne_sl + kBlock / kRsW - 1) / (kBlock / kRsW))),
+                               dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.samp.p, a.cand_offset, a.seed,
+                               ctx->rounds.p, plan, ctx->scr_cnt.p, ctx->scr_list.p, cap, tabd, ctx->rs_x.p,
+                               ctx->rs_g.p);
+            hipLaunchKernelGGL(k_rescore_slices_packed, dim3((unsigned)((s_max + 3) / 4), g_sl), dim3(kBlock), 0,
+                               ctx->stream, P.labels.p, grp, P.comps64.p, tabd, plan, ctx->rs_x.p, ctx->rs_g.p,
+                               s_max, chunk, spc, ctx->rs_part.p, ctx->zero_win ? P.zw_hi.p : nullptr,
+                               ctx->zero_win ? P.zw_lo.p : nullptr, P.zw_wide.p, P.zw_n.p);
+            hipLaunchKernelGGL(k_rescore_fin_packed, dim3(g_sl), dim3(kRsW), 0, ctx->stream, P.labels.p, grp,
+                               P.comps64.p, a.cand_offset, nch, spc, ctx->scr_list.p, cap, tabd, ctx->scr_off.p,
+                               plan, ctx->rs_x.p, ctx->rs_g.p, s_max, ctx->rs_part.p, ctx->scr_res.p);
         }
         const unsigned g = (unsigned)std::min<int64_t>(ne_max, 2048);
         hipLaunchKernelGGL((k_rescore_packed<kRP>), dim3(g, nch), dim3(kBlock), 0,
@@ -3884,7 +4065,8 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
         RescoreChunk* chp = reinterpret_cast<RescoreChunk*>(ctx->scr_chunks.p);
         RescorePlan* plan = reinterpret_cast<RescorePlan*>(ctx->rs_plan.p);
         hipLaunchKernelGGL(k_rescore_plan, dim3(1), dim3(kPlanBlock), 0, ctx->stream, ctx->scr_cnt.p, (int64_t)cells,
-                           (int32_t)per_full, 1, (int64_t)cells * lst, chp, ctx->scr_off.p, nullptr, plan);
+                           (int32_t)per_full, kSlicedRescoreMax, (int64_t)cells * lst, chp, ctx->scr_off.p, nullptr,
+                           plan);
         const unsigned g_sl = (unsigned)std::min<int64_t>(ne_sliced, 1024);
         hipLaunchKernelGGL(k_rescore_draw, dim3((unsigned)((ne_sliced + kBlock / kRsW - 1) / (kBlock / kRsW))),
                            dim3(kBlock), 0, ctx->stream, ctx->P->labels.p, grp, ctx->P->samp.p, lst,
@@ -4363,19 +4545,39 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     if (tiles > 0 && ctx->dev_out)
         HIPCHK(ctx, hipMemcpyAsync(ctx->dev_out, ctx->results.p, n_res * sizeof(tpe_label_result),
                                    hipMemcpyDeviceToDevice, ctx->stream));
+    // large results (config 5: 25 MB) come back in pieces, each copied into
+    // the caller's array as soon as it lands, under the next piece's transfer
+    const size_t res_bytes = n_res * sizeof(tpe_label_result);
+    const int pieces = (tiles > 0 && out && res_bytes >= ((size_t)8 << 20)) ? tpe_ctx::kResPieces : 0;
+    const size_t piece = ((res_bytes + std::max(pieces, 1) - 1) / std::max(pieces, 1) + 4095) & ~(size_t)4095;
     {
         int rc = defer_read(ctx, &pin.err, ctx->errflag.p, sizeof(int32_t));
         if (!rc) rc = defer_read(ctx, pin.xdrawn, ctx->xdrawn.p, 2 * sizeof(unsigned long long));
-        if (!rc && tiles > 0 && out) {
-            HIPCHK(ctx, ctx->res_h.resize(n_res));
-            rc = defer_read(ctx, ctx->res_h.data(), ctx->results.p, n_res * sizeof(tpe_label_result));
+        if (!rc && tiles > 0 && out) HIPCHK(ctx, ctx->res_h.resize(n_res));
+        if (!rc && pieces) {
+            for (int k = 0; k < pieces; ++k) {
+                const size_t a0 = std::min(res_bytes, k * piece), a1 = std::min(res_bytes, a0 + piece);
+                if (!ctx->ev_res[k])
+                    HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_res[k], hipEventDisableTiming));
+                if (a1 > a0)
+                    HIPCHK(ctx, hipMemcpyAsync((char*)ctx->res_h.data() + a0, (const char*)ctx->results.p + a0,
+                                               a1 - a0, hipMemcpyDeviceToHost, ctx->stream));
+                HIPCHK(ctx, hipEventRecord(ctx->ev_res[k], ctx->stream));
+            }
+        } else if (!rc && tiles > 0 && out) {
+            rc = defer_read(ctx, ctx->res_h.data(), ctx->results.p, res_bytes);
         }
         if (!rc) rc = flush_reads(ctx);
         if (rc) return rc;
     }
+    for (int k = 0; k < pieces; ++k) {
+        const size_t a0 = std::min(res_bytes, k * piece), a1 = std::min(res_bytes, a0 + piece);
+        HIPCHK(ctx, hipEventSynchronize(ctx->ev_res[k]));
+        if (a1 > a0) copy_out((char*)out + a0, (const char*)ctx->res_h.data() + a0, a1 - a0);
+    }
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     unpack_reads(ctx);
-    if (tiles > 0 && out) std::memcpy(out, ctx->res_h.data(), n_res * sizeof(tpe_label_result));
+    if (tiles > 0 && out && !pieces) copy_out(out, ctx->res_h.data(), res_bytes);
     if (ctx->zw_pending) {
         ctx->P->zw_ready = pin.plan.total > 0;
         ctx->zw_pending = false;
@@ -4781,6 +4983,8 @@ TPE_DEV void tpe1_ctx_destroy(tpe_ctx* c) {
         if (c->evs[j]) (void)hipEventDestroy(c->evs[j]);
         if (c->ev_prep[j]) (void)hipEventDestroy(c->ev_prep[j]);
     }
+    for (hipEvent_t& e : c->ev_res)
+        if (e) (void)hipEventDestroy(e);
     c->scr_hi.release();
     c->scr_idx.release();
     c->scr_range.release();
@@ -5125,6 +5329,11 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
         case TPE_OPT_BX_T:
             if (value != 0 && (value < 32 || value > 128)) return ctx->fail(TPE_ERR_ARG, "index cut T must be 0 or in [32, 128]");
             ctx->bx_t_force = (int32_t)value;
+            break;
+        case TPE_OPT_PK_SLICED:
+            if (value < 0 || value > kSlicedRescoreMax)
+                return ctx->fail(TPE_ERR_ARG, "packed sliced re-score limit must be in [0, 65536]");
+            ctx->pk_sliced = value;
             break;
         case TPE_OPT_BX_SPLIT:
             if (value < 0 || value > 8) return ctx->fail(TPE_ERR_ARG, "index window split must be in [0, 8]");

@@ -461,7 +461,8 @@ class Engine(object):
                'zero_win': L.TPE_OPT_ZERO_WIN, 'value_only': L.TPE_OPT_VALUE_ONLY,
                'rescore_cap': L.TPE_OPT_RESCORE_CAP, 'mode_mask': L.TPE_OPT_MODE_MASK,
                'aux_families': L.TPE_OPT_AUX_FAMILIES, 'hot32': L.TPE_OPT_HOT32,
-               'bx_split': L.TPE_OPT_BX_SPLIT, 'bx_t': L.TPE_OPT_BX_T}
+               'bx_split': L.TPE_OPT_BX_SPLIT, 'bx_t': L.TPE_OPT_BX_T,
+               'pk_sliced': L.TPE_OPT_PK_SLICED}
 
     def set_option(self, name, value):
         """Engine switches (include/hyperopt_tpe.h TPE_OPT_*): 'screen',

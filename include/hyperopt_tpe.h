@@ -539,6 +539,10 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *   TPE_OPT_BX_T    the expansion index's window cut T (components left
  *                   out stay below 2^-T of the largest term; 32..128; 0:
  *                   64 for tile rounds, 96 for the packed map's)           [0]
+ *   TPE_OPT_PK_SLICED  a packed-map round re-scores up to this many listed
+ *                   candidates one wave per (64 candidates, summation slice)
+ *                   instead of one thread per candidate walking its chunk
+ *                   (same bits; 0: never; at most 65536)                [8192]
  *   TPE_OPT_WIN_GROUPS  label groups of a windowed round, each sorted on a
  *                   second stream while the previous one is screened
  *                   (0: one group; the chip is busy either way)          [0]
@@ -574,6 +578,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_HOT32 20
 #define TPE_OPT_BX_SPLIT 21
 #define TPE_OPT_BX_T 22
+#define TPE_OPT_PK_SLICED 23
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
 
 /* Build now what the resident posterior's first round(s) of n_candidates

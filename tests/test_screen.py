@@ -211,6 +211,44 @@ def test_packed_rescore_zero_windows_same_bits(eng):
     assert out[(1, 1)] == out[(0, 1)] == out[(1, 0)]
 
 
+@pytest.mark.parametrize('value_only', [0, 1])
+@pytest.mark.parametrize('rounds,chunks', [(128, 0), (96, 3), (600, 0)])
+def test_packed_rescore_sliced_same_bits(eng, value_only, rounds, chunks):
+    """The packed map's re-score of a few listed candidates split by
+    summation slices (TPE_OPT_PK_SLICED: one wave per 64 candidates and
+    slice, the chunk sums added in the chunked map's order) gives the bytes
+    of the one-thread-per-candidate re-score (and, with lpdfs, of the
+    unscreened round); value_only 0 re-scores every cell's winner (a few thousand candidates:
+    sliced at 128 and 96 rounds, chunked at 600 by default)."""
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.workloads import mixed_history
+    hist = mixed_history(64, 20000, seed=1)
+    eng.set_posterior(*P.pack(hist.posteriors()))
+    ids = list(range(3000, 3000 + rounds))
+    out, counts = {}, {}
+    eng.set_option('value_only', value_only)
+    eng.set_option('chunks', chunks)
+    try:
+        for pk, screen in ((0, 1), (8192, 1), (65536, 1), (8192, 0)):
+            eng.set_option('pk_sliced', pk)
+            eng.set_option('screen', screen)
+            out[(pk, screen)] = np.ascontiguousarray(eng.suggest_batch(41, ids, 24)).tobytes()
+            counts[(pk, screen)] = eng.last_screen()
+    finally:
+        eng.set_option('pk_sliced', 8192)
+        eng.set_option('screen', 1)
+        eng.set_option('chunks', 0)
+        eng.set_option('value_only', 0)
+    assert out[(0, 1)] == out[(8192, 1)] == out[(65536, 1)]
+    if not value_only:   # (value-only cells the screen decided carry no lpdfs)
+        assert out[(8192, 1)] == out[(8192, 0)]
+    rescored = counts[(65536, 1)][1]
+    assert rescored > 0 or (value_only and rounds == 600)   # (none left there)
+    if not value_only:
+        assert rescored >= rounds   # (every cell's winner)
+    print('packed %d rounds, value_only %d: re-scored %d' % (rounds, value_only, rescored))
+
+
 def test_windowed_screen_skips_terms(eng):
     """Config 3's posterior, 2^20 candidates: the windowed screen sums a
     fraction of the terms the plain screen sums, and both give the fp64

@@ -124,6 +124,7 @@ PATCHES = {
              '__launch_bounds__(kBlock, 5) void k_hot_bx(')],
     'bxlb4': [('tpe_expand.hip', '__global__ __launch_bounds__(kBlock) void k_bx_table(',
                '__global__ __launch_bounds__(kBlock, 4) void k_bx_table(')],
+    'nopieces': [('tpe_engine.hip', 'res_bytes >= ((size_t)8 << 20)', 'res_bytes >= ((size_t)1 << 62)')],
     'bx3': [('tpe_expand.hip', 'constexpr int kBxChains = 4;', 'constexpr int kBxChains = 3;')],
     'bx2': [('tpe_expand.hip', 'constexpr int kBxChains = 4;', 'constexpr int kBxChains = 2;')],
     'nolist': [('tpe_engine.hip', '            const uint64_t bal = __ballot(take);\n            if (!bal) continue;\n            const int c = __builtin_amdgcn_readfirstlane',

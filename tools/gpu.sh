@@ -11,6 +11,8 @@
 #   bench            the default bench.py line (what the driver runs)
 #   bench=<args>     bench.py with extra arguments (commas for spaces)
 #   var=<name>[,args] bench.py on the variant library tools/var_<name>.so (tools/build_variant.py)
+#   htrace=<script,args> rocprofv3 kernel + memory-copy + HIP API trace of a script -> <tag>/htrace<n>
+#   vpy=<name>,<script,args> a python script of the tree on that variant library
 #   trace=<args>     rocprofv3 --kernel-trace --stats of bench.py <args> -> <tag>/trace<n>
 #   prof             tools/prof_round.sh <tag> (kernel trace + PMC passes of the default line)
 #   lpdf             the plain fp64 round's trace + PMC passes (tools/prof_round.sh <tag>_lpdf)
@@ -68,6 +70,15 @@ for s in "$@"; do
             v=${a%%,*}
             rest=""; [ "$a" != "$v" ] && rest=${a#*,}
             run var_$v$n 600 env HYPEROPT_AMD_VARIANT=tools/var_$v.so python -u bench.py ${rest//,/ } || exit 1 ;;
+        vpy=*)   # a python script of the tree on a variant library: vpy=<name>,<script>[,args]
+            a=${s#vpy=}
+            v=${a%%,*}
+            rest=${a#*,}
+            run vpy_$v$n 600 env HYPEROPT_AMD_VARIANT=tools/var_$v.so python -u ${rest//,/ } || exit 1 ;;
+        htrace=*)   # kernel + copy + HIP API trace of a python script: htrace=<script,args>
+            a=${s#htrace=}
+            run htrace$n 400 rocprofv3 --kernel-trace --memory-copy-trace --hip-runtime-trace -d "$OUT/htrace$n" -o run \
+                --output-format csv -- python -u ${a//,/ } || exit 1 ;;
         trace=*)   # rocprofv3 kernel trace + stats of bench.py with these arguments (commas for spaces)
             a=${s#trace=}
             run trace$n 400 rocprofv3 --kernel-trace --stats -d "$OUT/trace$n" -o run --output-format csv \

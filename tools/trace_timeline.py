@@ -1,6 +1,6 @@
 """Print the kernel / copy timeline from the k-th last launch of a marker
 kernel on (k = 1: the last), from a rocprofv3 --kernel-trace
-[--memory-copy-trace] csv directory.
+[--memory-copy-trace] [--hip-trace] csv directory.
 
     python tools/trace_timeline.py <trace dir> [marker=k_split] [k=1] [before=3] [count=40]
 """
@@ -18,6 +18,9 @@ def main(d, marker='k_split', k=1, before=3, count=40):
         for r in csv.DictReader(open(f)):
             ev.append((int(r['Start_Timestamp']), int(r['End_Timestamp']),
                        'M %s %s' % (r.get('Direction', ''), r.get('Size', ''))))
+    for f in glob.glob(d + '/**/*hip_api_trace.csv', recursive=True):
+        for r in csv.DictReader(open(f)):
+            ev.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), 'A ' + r['Function'][:60]))
     ev.sort()
     idx = [i for i, e in enumerate(ev) if marker in e[2]]
     s = max(idx[-int(k)] - int(before), 0)
