@@ -447,7 +447,7 @@ struct tpe_ctx {
     int32_t bx_split = 0;                // TPE_OPT_BX_SPLIT (0: auto)
     int64_t pk_sliced = 8192;            // TPE_OPT_PK_SLICED (0: never sliced)
     int32_t bx_t_force = 0;              // TPE_OPT_BX_T (0: auto)
-    double bx_t_next = 96.0;             // the cut T of the next index built (set by its caller)
+    double bx_t_next = 64.0;             // the cut T of the next index built (set by its caller)
     DevBuf<int32_t> hot_i, hot_cnt;      //   their indices; per cell the count
     DevBuf<unsigned long long> hot_t, hot_tau0;   // per cell largest L; per label tau0
     DevBuf<uint32_t> hot_bits;           // per sub-bin: U >= tau0 (words at sb_off / 32)
@@ -502,6 +502,7 @@ struct tpe_ctx {
     DevBuf<int64_t> scr_range;           //   per label: its range of re-score table entries
     DevBuf<double> scr_planes;           //   re-score sums: below | x | above chunk c, per entry
     DevBuf<double> rs_x, rs_part;        // sliced re-score: candidates, slice sums
+    DevBuf<int32_t> rs_win;              //   packed map: each entry's zero window
     DevBuf<int64_t> rs_g;                //   and their global indices
     std::vector<tpe_rt::RescoreChunkH> scr_chunks_h;
     int64_t screen_total = 0, screen_rescored = 0;   // last round

@@ -1277,11 +1277,13 @@ __device__ __host__ __forceinline__ int win_bin(const WinLabel& W, double x) {
 constexpr int kBxP = 15;          // Taylor coefficients per bin
 constexpr int kBxRow = 16;        // doubles per bin row (one 128-B line): A_0..A_14, Eabs
 // components left out of a bin's window stay below 2^-T of the largest
-// term (T per index, BxLabel.tcut): 96 for the packed map's rounds (their
-// value-only certification needs the tighter bound), 64 for tile rounds
-// through the hot-bin prefilter (narrower windows, fewer bins: config 3's
-// index 0.53 -> 0.45 ms with the same re-scores, r5t)
-constexpr double kBxT = 96.0;
+// term (T per index, BxLabel.tcut): 64 for tile rounds through the hot-bin
+// prefilter (narrower windows, fewer bins: config 3's index 0.53 -> 0.45 ms
+// with the same re-scores, r5t) and, since the packed map re-scores a few
+// near-ties by slices, for the packed map's rounds too (96 certified every
+// value-only cell of config 5, 64 leaves ~14 near-ties per step to the fp64
+// re-score: index 4.42 -> 3.55 ms, step 8.7 -> 7.8 ms, r5aj)
+constexpr double kBxT = 64.0;
 constexpr double kBxTTile = 64.0;
 
 struct BxLabel {

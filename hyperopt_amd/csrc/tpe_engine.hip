@@ -1585,6 +1585,22 @@ __global__ __launch_bounds__(kBlock) void k_rescore(
 // k_rescore_plan; the kernels stride over them (grids sized for the largest
 // table) and leave a round whose plan is not sliced to k_rescore.
 
+// acc + p[0] + p[stride] + ... + p[(n-1) stride], added in that order, the
+// loads issued 8 at a time (the slice sums of a sliced re-score: one
+// dependent L2 round trip per slice took ~50 us for 200 slices, r5ag)
+__device__ __forceinline__ double ordered_sum(const double* __restrict__ p, int n, size_t stride, double acc) {
+    int s = 0;
+    for (; s + 8 <= n; s += 8) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = p[(size_t)(s + u) * stride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; s < n; ++s) acc += p[(size_t)s * stride];
+    return acc;
+}
+
 __global__ __launch_bounds__(kBlock) void k_rescore_draw(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
     const SampRec* __restrict__ samp, int64_t stride, int64_t cand_offset, uint64_t seed,
@@ -1659,9 +1675,8 @@ __global__ __launch_bounds__(kRsW) void k_rescore_fin(
     int64_t bi = INT64_MAX;
     double bv = 0.0, bl = 0.0, ba = 0.0;
     if (g >= 0) {   // (padding lanes would take lse_finish's two-pass fallback)
-        double sb = 0.0, sa = 0.0;
-        for (int s = 0; s < nsb; ++s) sb += p[(size_t)s * kRsW];
-        for (int s = nsb; s < nsb + nsa; ++s) sa += p[(size_t)s * kRsW];
+        const double sb = ordered_sum(p, nsb, kRsW, 0.0);
+        const double sa = ordered_sum(p + (size_t)nsb * kRsW, nsa, kRsW, 0.0);
         const double y = lgmm ? flog(x) : x;
         double lb = lse_finish(comps64 + L.comp_b, L.nb, sb, y - L.centre, L.shift_b);
         double la = lse_finish(comps64 + L.comp_a, L.na, sa, y - L.centre, L.shift_a);
@@ -1915,7 +1930,7 @@ __global__ __launch_bounds__(kZwBlock) void k_zero_windows(const RescorePlan* __
                                                            const Comp<double>* __restrict__ comps64,
                                                            double* __restrict__ zhi, double* __restrict__ zlo,
                                                            int32_t* __restrict__ zwide, int32_t* __restrict__ zn) {
-    if (plan->total == 0) return;   // (uniform)
+    if (plan->total == 0 || plan->sliced) return;   // (uniform; the sliced re-score sums every slice)
     const int li = group[blockIdx.x];
     const DLabel L = labels[li];
     const Comp<double>* c = comps64 + L.comp_a;
@@ -2178,7 +2193,8 @@ __global__ __launch_bounds__(kBlock) void k_rescore_draw_packed(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
     int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, const RescorePlan* __restrict__ plan,
     const int32_t* __restrict__ cnt, const int64_t* __restrict__ list, int64_t cap,
-    const RescoreChunk* __restrict__ chunks, double* __restrict__ xbuf, int64_t* __restrict__ gbuf) {
+    const RescoreChunk* __restrict__ chunks, double* __restrict__ xbuf, int64_t* __restrict__ gbuf,
+    const double* __restrict__ zhi, const double* __restrict__ zlo, int32_t* __restrict__ win) {
     if (plan->overflow || !plan->sliced) return;
     const int32_t ne = plan->ne;
     const int lane = threadIdx.x % kRsW;
@@ -2198,15 +2214,31 @@ __global__ __launch_bounds__(kBlock) void k_rescore_draw_packed(
     }
     xbuf[(size_t)e * kRsW + lane] = v;
     gbuf[(size_t)e * kRsW + lane] = g;
+    if (zhi) {
+        // the entry's zero window (the posterior's windows built by an
+        // earlier round): the above records whose terms can be nonzero at
+        // some candidate of the entry
+        const double xr = (lgmm ? flog(v) : v) - L.centre;
+        double xa = g >= 0 ? xr : __builtin_inf(), xb = g >= 0 ? xr : -__builtin_inf();
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            xa = fmin(xa, __shfl_xor(xa, o));
+            xb = fmax(xb, __shfl_xor(xb, o));
+        }
+        if (lane == 0) {
+            const bool any = xa <= xb;
+            win[2 * e] = any ? first_above(zhi + L.comp_a, L.na, xa, false) : 0;
+            win[2 * e + 1] = any ? first_above(zlo + L.comp_a, L.na, xb, true) : L.na;
+        }
+    }
     }
 }
 
 __global__ __launch_bounds__(kBlock) void k_rescore_slices_packed(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const Comp<double>* __restrict__ comps64,
     const RescoreChunk* __restrict__ chunks, const RescorePlan* __restrict__ plan, const double* __restrict__ xbuf,
-    const int64_t* __restrict__ gbuf, int32_t s_max, int32_t chunk, int32_t spc, double* __restrict__ part,
-    const double* __restrict__ zhi, const double* __restrict__ zlo, const int32_t* __restrict__ zwide,
-    const int32_t* __restrict__ zn) {
+    int32_t s_max, int32_t chunk, int32_t spc, double* __restrict__ part, const int32_t* __restrict__ win,
+    const int32_t* __restrict__ zwide, const int32_t* __restrict__ zn) {
     if (plan->overflow || !plan->sliced) return;
     const int32_t ne = plan->ne;
     if ((int32_t)blockIdx.y >= ne) return;   // (uniform, before the table's barrier)
@@ -2220,7 +2252,6 @@ __global__ __launch_bounds__(kBlock) void k_rescore_slices_packed(
     const DLabel L = labels[group[ch.cell]];
     const int nsb = (L.nb + kSumSlice - 1) / kSumSlice;
     const double x = xbuf[(size_t)e * kRsW + lane];
-    const bool valid = gbuf[(size_t)e * kRsW + lane] >= 0;
     const double xr[1] = {(L.mode == DENSE_LGMM ? flog(x) : x) - L.centre};
     double acc[1] = {0.0};
     if (slice < nsb) {
@@ -2231,15 +2262,9 @@ __global__ __launch_bounds__(kBlock) void k_rescore_slices_packed(
         const int kb = min((c + 1) * chunk, L.na);
         const int k0 = c * chunk + (s - c * spc) * kSumSlice, k1 = min(k0 + kSumSlice, kb);
         if (k0 < k1) {
-            double xa = valid ? xr[0] : __builtin_inf(), xb = valid ? xr[0] : -__builtin_inf();
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                xa = fmin(xa, __shfl_xor(xa, o));
-                xb = fmax(xb, __shfl_xor(xb, o));
-            }
-            if (zhi && xa <= xb) {
-                const int wlo = __builtin_amdgcn_readfirstlane(first_above(zhi + L.comp_a, L.na, xa, false));
-                const int whi = __builtin_amdgcn_readfirstlane(first_above(zlo + L.comp_a, L.na, xb, true));
+            if (win) {
+                const int wlo = __builtin_amdgcn_readfirstlane(win[2 * e]);
+                const int whi = __builtin_amdgcn_readfirstlane(win[2 * e + 1]);
                 lse_acc_zero_window<1>(comps64 + L.comp_a, k0, k1, wlo, whi, zwide + L.comp_a,
                                        zn[group[ch.cell]], xr, acc, exp_tab);
             } else {
@@ -2270,13 +2295,9 @@ __global__ __launch_bounds__(kRsW) void k_rescore_fin_packed(
     const int nsb = (L.nb + kSumSlice - 1) / kSumSlice;
     const double x = xbuf[(size_t)e * kRsW + lane];
     const double* p = part + (size_t)e * s_max * kRsW + lane;
-    double sb = 0.0, sa = 0.0;
-    for (int s = 0; s < nsb; ++s) sb += p[(size_t)s * kRsW];
-    for (int c = 0; c < nch; ++c) {
-        double t = 0.0;
-        for (int q = 0; q < spc; ++q) t += p[(size_t)(nsb + c * spc + q) * kRsW];
-        sa += t;
-    }
+    const double sb = ordered_sum(p, nsb, kRsW, 0.0);
+    double sa = 0.0;
+    for (int c = 0; c < nch; ++c) sa += ordered_sum(p + (size_t)(nsb + c * spc) * kRsW, spc, kRsW, 0.0);
     const double yv = lgmm ? flog(x) : x;
     double lb = lse_finish(comps64 + L.comp_b, L.nb, sb, yv - L.centre, L.shift_b);
     double la = lse_finish(comps64 + L.comp_a, L.na, sa, yv - L.centre, L.shift_a);
@@ -3729,18 +3750,22 @@ int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, cons
             hipLaunchKernelGGL(k_zero_windows, dim3((unsigned)nd), dim3(kZwBlock), 0, ctx->stream, plan, P.labels.p,
                                P.groups.p + P.group_off[DENSE_GMM], P.comps64.p, P.zw_hi.p, P.zw_lo.p,
                                P.zw_wide.p, P.zw_n.p);
-            ctx->zw_pending = true;   // built iff the plan was not empty (read after the round's sync)
+            ctx->zw_pending = true;   // built iff the plan was chunked (read after the round's sync)
         }
         if (ne_sl > 0) {
+            // (zero windows only when an earlier round of this posterior
+            // built them: k_zero_windows skips a sliced plan -- 0.67 ms at
+            // config 5, more than the slices it would let a re-score skip)
+            const bool zw = ctx->zero_win && P.zw_ready;
+            HIPCHK(ctx, ctx->rs_win.reserve((size_t)2 * ne_sl));
             const unsigned g_sl = (unsigned)std::min<int64_t>(ne_sl, 1024);
             hipLaunchKernelGGL(k_rescore_draw_packed, dim3((unsigned)((ne_sl + kBlock / kRsW - 1) / (kBlock / kRsW))),
                                dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.samp.p, a.cand_offset, a.seed,
                                ctx->rounds.p, plan, ctx->scr_cnt.p, ctx->scr_list.p, cap, tabd, ctx->rs_x.p,
-                               ctx->rs_g.p);
+                               ctx->rs_g.p, zw ? P.zw_hi.p : nullptr, zw ? P.zw_lo.p : nullptr, ctx->rs_win.p);
             hipLaunchKernelGGL(k_rescore_slices_packed, dim3((unsigned)((s_max + 3) / 4), g_sl), dim3(kBlock), 0,
-                               ctx->stream, P.labels.p, grp, P.comps64.p, tabd, plan, ctx->rs_x.p, ctx->rs_g.p,
-                               s_max, chunk, spc, ctx->rs_part.p, ctx->zero_win ? P.zw_hi.p : nullptr,
-                               ctx->zero_win ? P.zw_lo.p : nullptr, P.zw_wide.p, P.zw_n.p);
+                               ctx->stream, P.labels.p, grp, P.comps64.p, tabd, plan, ctx->rs_x.p, s_max, chunk,
+                               spc, ctx->rs_part.p, zw ? ctx->rs_win.p : nullptr, P.zw_wide.p, P.zw_n.p);
             hipLaunchKernelGGL(k_rescore_fin_packed, dim3(g_sl), dim3(kRsW), 0, ctx->stream, P.labels.p, grp,
                                P.comps64.p, a.cand_offset, nch, spc, ctx->scr_list.p, cap, tabd, ctx->scr_off.p,
                                plan, ctx->rs_x.p, ctx->rs_g.p, s_max, ctx->rs_part.p, ctx->scr_res.p);
@@ -4579,7 +4604,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     unpack_reads(ctx);
     if (tiles > 0 && out && !pieces) copy_out(out, ctx->res_h.data(), res_bytes);
     if (ctx->zw_pending) {
-        ctx->P->zw_ready = pin.plan.total > 0;
+        ctx->P->zw_ready = pin.plan.total > 0 && !pin.plan.sliced;
         ctx->zw_pending = false;
     }
     if (ctx->pk_plan_pending && pin.plan.overflow && !ctx->pk_redo) {

@@ -538,7 +538,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *                   workgroups)                                            [0]
  *   TPE_OPT_BX_T    the expansion index's window cut T (components left
  *                   out stay below 2^-T of the largest term; 32..128; 0:
- *                   64 for tile rounds, 96 for the packed map's)           [0]
+ *                   64)                                                   [0]
  *   TPE_OPT_PK_SLICED  a packed-map round re-scores up to this many listed
  *                   candidates one wave per (64 candidates, summation slice)
  *                   instead of one thread per candidate walking its chunk

@@ -229,7 +229,9 @@ def test_packed_rescore_sliced_same_bits(eng, value_only, rounds, chunks):
     eng.set_option('value_only', value_only)
     eng.set_option('chunks', chunks)
     try:
-        for pk, screen in ((0, 1), (8192, 1), (65536, 1), (8192, 0)):
+        # sliced before the posterior's zero windows exist, chunked (builds
+        # them), sliced inside them, unscreened
+        for pk, screen in ((8192, 1), (0, 1), (65536, 1), (8192, 0)):
             eng.set_option('pk_sliced', pk)
             eng.set_option('screen', screen)
             out[(pk, screen)] = np.ascontiguousarray(eng.suggest_batch(41, ids, 24)).tobytes()
@@ -557,8 +559,7 @@ def test_index_window_split_same_round(eng, split):
 
 @pytest.mark.parametrize('cut', [48, 96, 128])
 def test_index_cut_same_round(eng, cut):
-    """The expansion index's window cut T (TPE_OPT_BX_T; auto: 64 for tile
-    rounds, 96 for the packed map's): fewer or more components in a bin's
+    """The expansion index's window cut T (TPE_OPT_BX_T; auto: 64): fewer or more components in a bin's
     window and its bound's skipped mass na 2^-T -- the winners do not move,
     and the sub-bin bounds of the forced-T index still bracket the fp64
     score."""
