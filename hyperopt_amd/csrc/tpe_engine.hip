@@ -4603,6 +4603,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     unpack_reads(ctx);
     if (tiles > 0 && out && !pieces) copy_out(out, ctx->res_h.data(), res_bytes);
+    if (tiles == 0 && out) std::memset(out, 0, res_bytes);   // (no candidates: empty records; the caller's array is uninitialised)
     if (ctx->zw_pending) {
         ctx->P->zw_ready = pin.plan.total > 0 && !pin.plan.sliced;
         ctx->zw_pending = false;

@@ -285,7 +285,7 @@ class Engine(object):
         return self.n_labels
 
     def suggest(self, seed, n_candidates, round=0, cand_offset=0):
-        out = np.zeros(self._labels(), dtype=RESULT_DTYPE)
+        out = np.empty(self._labels(), dtype=RESULT_DTYPE)   # (every record written)
         self._check(self.lib.tpe_suggest(self.h, int(seed) & 0xFFFFFFFFFFFFFFFF,
                                          int(round) & 0xFFFFFFFF, int(n_candidates),
                                          int(cand_offset), _ptr(out)))
@@ -293,7 +293,8 @@ class Engine(object):
 
     def suggest_batch(self, seed, rounds, n_candidates, cand_offset=0):
         rounds = np.ascontiguousarray(np.asarray(rounds, dtype=np.uint32))
-        out = np.zeros(len(rounds) * self._labels(), dtype=RESULT_DTYPE)
+        # (every record written: np.zeros cost 0.17-1.6 ms at config 5's 25 MB)
+        out = np.empty(len(rounds) * self._labels(), dtype=RESULT_DTYPE)
         self._check(self.lib.tpe_suggest_batch(self.h, int(seed) & 0xFFFFFFFFFFFFFFFF,
                                                _ptr(rounds), len(rounds), int(n_candidates),
                                                int(cand_offset), _ptr(out)))
