@@ -300,31 +300,42 @@ def reference_orders(losses, n_below, obs_of, labels):
     above = has & (below == 0)
     n_labels = obs_of.n_labels
     off = np.zeros(n_labels + 1, dtype=np.int64)
-    parts = []
+    jobs = []   # (label, values, selection mask) in label order
+    n_above = None
     for l in range(n_labels):
+        n = 0
         if l in labels:
             pos, val = obs_of(l)
             val = np.asarray(val, dtype=np.float64)
-            n = len(pos)
-            if n == T and n and pos[0] == 0 and pos[-1] == T - 1:
-                mus = val[above]                     # positions 0..T-1 (one per trial, in order)
+            if len(pos) == T and T and pos[0] == 0 and pos[-1] == T - 1:
+                sel = above                          # positions 0..T-1 (one per trial, in order)
+                if n_above is None:
+                    n_above = int(np.count_nonzero(above))
+                n = n_above
             else:
                 pos = np.asarray(pos, dtype=np.int64)
                 ok = (pos >= 0) & (pos < T)
-                keep = np.zeros(n, dtype=bool)
-                keep[ok] = above[pos[ok]]
-                mus = val[keep]
-            parts.append(mus)
-            off[l + 1] = off[l] + len(mus)
-        else:
-            off[l + 1] = off[l]
-    # np.argsort(mus) per label (tpe.py:433); numpy sorts without the GIL,
-    # so many long ones go to a thread pool
-    if parts and off[-1] >= _POOL_MIN:
-        parts = list(_sort_pool().map(np.argsort, parts))
+                sel = np.zeros(len(pos), dtype=bool)
+                sel[ok] = above[pos[ok]]
+                n = int(np.count_nonzero(sel))
+            jobs.append((l, val, sel))
+        off[l + 1] = off[l] + n
+    order = np.empty(int(off[-1]), dtype=np.int32)
+
+    def sort_one(job):
+        # np.argsort(mus) (tpe.py:433) into the label's range of `order`
+        l, val, sel = job
+        order[off[l]:off[l + 1]] = np.argsort(val[sel])
+
+    # numpy sorts (and gathers) without the GIL, so many long ones -- their
+    # gathers and int32 stores too, 2/3 of the work on one thread (r5am) --
+    # go to a thread pool
+    if jobs and off[-1] >= _POOL_MIN:
+        for _ in _sort_pool().map(sort_one, jobs):
+            pass
     else:
-        parts = [np.argsort(m) for m in parts]
-    order = np.concatenate(parts).astype(np.int32) if parts else np.zeros(0, dtype=np.int32)
+        for job in jobs:
+            sort_one(job)
     return below, off, order
 
 
