@@ -1073,6 +1073,11 @@ def main():
                         'candidate, the Philox integer work not counted), the listed candidates\' '
                         'polynomials (40) and direct lpdf terms (6 each) over the bracket\'s device '
                         'time; the PMC figures are k_hot_bx\'s')
+        roof['traffic_note'] = ('traffic (2 x FETCH_SIZE + WRITE_SIZE per launch) counts, beside the hot '
+                                'lists (~21 MB: 1.7e6 listed x 12 B) and the sub-bin bits, the scratch stores '
+                                'of the 8 VGPRs k_hot_bx spills at six workgroups per CU (80 VGPRs): 86 MB '
+                                'against 33 MB at five per CU without spills (r5aq vs r5r), for a kernel 3.5 % '
+                                'faster (r5x); ~75 GB/s, 1 % of HBM')
     elif smode == 3:
         roof['flops_per_candidate_poly'] = BX_FLOPS_PER_CAND
         roof['note'] = ('VALU-issue bound: per candidate the Philox + Box-Muller draw, the fp64 '
