@@ -119,6 +119,9 @@ def parse():
                          'library default: faster on gfx950)')
     ap.add_argument('--bx-split', type=int, default=None,
                     help='TPE_OPT_BX_SPLIT: workgroups per 64-bin block of the index tables (0 = auto)')
+    ap.add_argument('--no-defer-report', action='store_true',
+                    help='the quantized labels\' subset rebuild waits for its report before the round '
+                         '(posterior.DEFER_REPORT off)')
     ap.add_argument('--bx-t', type=int, default=None,
                     help='TPE_OPT_BX_T: the expansion index\'s window cut T (0 = auto: 64 for tile rounds)')
     ap.add_argument('--dist-backend', default='nccl',
@@ -836,6 +839,8 @@ def main():
         eng.set_option('hot32', args.hot32)
     if args.bx_split is not None:
         eng.set_option('bx_split', args.bx_split)
+    if args.no_defer_report:
+        P.DEFER_REPORT = False
     if args.bx_t is not None:
         eng.set_option('bx_t', args.bx_t)
     eng.set_option('window', int(not args.no_window))

@@ -60,6 +60,7 @@ TPE_OPT_HOT32 = 20
 TPE_OPT_BX_SPLIT = 21
 TPE_OPT_BX_T = 22
 TPE_OPT_PK_SLICED = 23
+TPE_OPT_DEFER_REPORT = 24
 
 TPE_OBS_IDENTITY = 0
 TPE_OBS_LOG = 1
@@ -136,6 +137,7 @@ SIGNATURES = {
                                                             _P, _P]),
     'tpe_rebuild_labels': (ctypes.c_int, [_P, _P, _I64, _I64, _D, _D, _I32, _P, _P, _P, _I32, _P, _P]),
     'tpe_last_build_ms': (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_float)]),
+    'tpe_build_report': (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int32), ctypes.c_void_p]),
     'tpe_last_screen': (ctypes.c_int, [_P, _P, _P, ctypes.POINTER(ctypes.c_float)]),
     'tpe_set_option': (ctypes.c_int, [_P, _I32, _I64]),
     'tpe_last_screen_terms': (ctypes.c_int, [_P, _P]),

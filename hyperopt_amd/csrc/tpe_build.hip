@@ -1444,12 +1444,80 @@ uint64_t loss_fingerprint(const double* losses, int64_t n) {
     return h;
 }
 
+// The end of a build, once its report is in (build_resident, or a deferred
+// subset rebuild settled by the next call on the context): the error flags,
+// the DLabels, the label groups, the posterior's flags and what the build
+// was of.
+int finish_build(tpe_ctx* ctx, BuildTail& t, int32_t* ties_out, int32_t* n_below_out) {
+    auto& B = ctx->build;
+    Posterior& P = ctx->resident;
+    const int32_t n_labels = t.n_labels;
+    const int64_t rep_dl = t.rep_dl;
+    std::vector<DLabel>& dl = t.dl;
+    const std::vector<int32_t>* grp = t.grp;
+    const bool beside = t.beside, subset = t.subset;
+    HIPCHK(ctx, hipStreamSynchronize(t.st));
+    P.qc_ready = false;   // (set again below when the build succeeds)
+    int32_t errh;
+    std::memcpy(&errh, B.h_rep.data() + rep_dl, sizeof(int32_t));
+    std::memcpy(dl.data(), B.h_rep.data(), rep_dl);
+    B.last_ties.resize(n_labels + 1);
+    std::memcpy(B.last_ties.data(), B.h_rep.data() + rep_dl + 16, (n_labels + 1) * sizeof(int32_t));
+    B.last_n_below = t.n_below;
+    if (ties_out) std::memcpy(ties_out, B.last_ties.data(), (n_labels + 1) * sizeof(int32_t));
+    // (a deferred report: the round that settles it re-recorded ev0 / ev1)
+    if (t.deferred) ctx->build_ms = -1.f;
+    else HIPCHK(ctx, hipEventElapsedTime(&ctx->build_ms, ctx->ev0, ctx->ev1));
+    if (errh & 1) return ctx->fail(TPE_ERR_ARG, "observation trial position out of range");
+    if (errh & 2) return ctx->fail(TPE_ERR_ARG, "more below observations than the below set (duplicate trial in a label?)");
+    if (errh & 4) return ctx->fail(TPE_ERR_VALUE, "below weights sum to zero");
+    if (errh & 8) return ctx->fail(TPE_ERR_ARG, "supplied observation order does not fit the above set");
+
+    std::vector<int32_t> cat;
+    for (int m = 0; m < kNumModes; ++m) {
+        P.group_off[m] = (int32_t)cat.size();
+        cat.insert(cat.end(), grp[m].begin(), grp[m].end());
+        P.h_group[m] = grp[m];
+    }
+    const bool groups_changed = cat != P.groups_h || !P.groups.p;
+    if (groups_changed) {   // unchanged between rebuilds of one history
+        HIPCHK(ctx, P.groups.reserve(std::max<size_t>(cat.size(), 1)));
+        HIPCHK(ctx, hipMemcpy(P.groups.p, cat.data(), cat.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+        P.groups_h = cat;
+    }
+    P.h_labels = dl;
+    P.win_ready = false;
+    P.zw_ready = false;
+    P.qc_ready = t.qc_queued;
+    // the index is kept when every dense label came out bit-identical (e.g.
+    // a second build of the same history that only supplies the tie order
+    // of quantized labels)
+    if (!beside) P.bx_ready = tpe_rt::bx_keep_after(ctx, groups_changed);
+    P.n_labels = n_labels;
+    B.n_labels = n_labels;
+    B.mix_h = t.mix;
+    B.built_ok = true;
+    B.built_gen = B.hist_gen;
+    B.built_T = t.n_trials;
+    B.built_valid = t.n_valid;
+    B.built_gamma = t.gamma;
+    B.built_pw = t.pw;
+    B.built_lf = t.lf;
+    if (!subset) B.built_loss_hash = t.loss_hash;
+    if (n_below_out) *n_below_out = t.n_below;
+    // the armed index, queued now: no caller round trip before it starts
+    if (t.arm_c > 0) return tpe1_prepare(ctx, t.arm_c, t.arm_r);
+    return TPE_OK;
+}
+
 int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t n_valid,
                    double gamma, double prior_weight, int32_t lf, int32_t* n_below_out,
                    const uint8_t* below_h = nullptr, const int64_t* order_off_h = nullptr,
                    const int32_t* order_h = nullptr, int32_t* ties_out = nullptr,
                    const int32_t* only_h = nullptr, int32_t n_only = 0) {
     auto& B = ctx->build;
+    const bool defer_report = B.defer;   // (consumed by this build, whatever happens)
+    B.defer = false;
     if (!B.hist_ready) return ctx->fail(TPE_ERR_ARG, "no resident history (tpe_history_reset)");
     const bool subset = only_h != nullptr && n_only > 0;
     // an armed tpe_prepare (tpe_arm_prepare): consumed by a full build
@@ -1678,56 +1746,48 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
             qc_queued = true;
         }
     }
-    HIPCHK(ctx, hipStreamSynchronize(st));
-    P.qc_ready = false;   // (set again below when the build succeeds)
-    int32_t errh;
-    std::memcpy(&errh, B.h_rep.data() + rep_dl, sizeof(int32_t));
-    std::memcpy(dl.data(), B.h_rep.data(), rep_dl);
-    if (ties_out) std::memcpy(ties_out, B.h_rep.data() + rep_dl + 16, (n_labels + 1) * sizeof(int32_t));
-    HIPCHK(ctx, hipEventElapsedTime(&ctx->build_ms, ctx->ev0, ctx->ev1));
-    if (errh & 1) return ctx->fail(TPE_ERR_ARG, "observation trial position out of range");
-    if (errh & 2) return ctx->fail(TPE_ERR_ARG, "more below observations than the below set (duplicate trial in a label?)");
-    if (errh & 4) return ctx->fail(TPE_ERR_VALUE, "below weights sum to zero");
-    if (errh & 8) return ctx->fail(TPE_ERR_ARG, "supplied observation order does not fit the above set");
-
-    std::vector<int32_t> cat;
-    for (int m = 0; m < kNumModes; ++m) {
-        P.group_off[m] = (int32_t)cat.size();
-        cat.insert(cat.end(), grp[m].begin(), grp[m].end());
-        P.h_group[m] = grp[m];
+    BuildTail t;
+    t.st = st;
+    t.rep_dl = rep_dl;
+    t.n_labels = n_labels;
+    t.lf = lf;
+    t.n_below = n_below;
+    t.dl = std::move(dl);
+    for (int m = 0; m < kNumModes; ++m) t.grp[m] = std::move(grp[m]);
+    t.mix = std::move(mix);
+    t.beside = beside;
+    t.qc_queued = qc_queued;
+    t.subset = subset;
+    t.n_trials = n_trials;
+    t.n_valid = n_valid;
+    t.arm_c = arm_c;
+    t.arm_r = arm_r;
+    t.gamma = gamma;
+    t.pw = prior_weight;
+    if (!subset) t.loss_hash = loss_fingerprint(losses, n_trials);
+    if (beside && subset && qc_queued && defer_report) {
+        // deferred (TPE_OPT_DEFER_REPORT): the rebuild runs on the second
+        // stream; the next round applies its report after queuing the dense
+        // labels' kernels, which it does not touch (settle_build).  The
+        // caller's tie report comes from tpe_build_report.
+        t.deferred = true;
+        B.pending.reset(new BuildTail(std::move(t)));
+        if (ties_out) std::memset(ties_out, 0, (n_labels + 1) * sizeof(int32_t));
+        if (n_below_out) *n_below_out = n_below;
+        return TPE_OK;
     }
-    const bool groups_changed = cat != P.groups_h || !P.groups.p;
-    if (groups_changed) {   // unchanged between rebuilds of one history
-        HIPCHK(ctx, P.groups.reserve(std::max<size_t>(cat.size(), 1)));
-        HIPCHK(ctx, hipMemcpy(P.groups.p, cat.data(), cat.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-        P.groups_h = cat;
-    }
-    P.h_labels = dl;
-    P.win_ready = false;
-    P.zw_ready = false;
-    P.qc_ready = qc_queued;
-    // the index is kept when every dense label came out bit-identical (e.g.
-    // a second build of the same history that only supplies the tie order
-    // of quantized labels)
-    if (!beside) P.bx_ready = tpe_rt::bx_keep_after(ctx, groups_changed);
-    P.n_labels = n_labels;
-    B.n_labels = n_labels;
-    B.mix_h = mix;
-    B.built_ok = true;
-    B.built_gen = B.hist_gen;
-    B.built_T = n_trials;
-    B.built_valid = n_valid;
-    B.built_gamma = gamma;
-    B.built_pw = prior_weight;
-    B.built_lf = lf;
-    if (!subset) B.built_loss_hash = loss_fingerprint(losses, n_trials);
-    if (n_below_out) *n_below_out = n_below;
-    // the armed index, queued now: no caller round trip before it starts
-    if (arm_c > 0) return tpe1_prepare(ctx, arm_c, arm_r);
-    return TPE_OK;
+    return finish_build(ctx, t, ties_out, n_below_out);
 }
 
 }  // namespace
+
+int tpe_rt::settle_build(tpe_ctx* ctx) {
+    if (!ctx) return TPE_OK;
+    auto& B = ctx->build;
+    if (!B.pending) return TPE_OK;
+    std::unique_ptr<BuildTail> t = std::move(B.pending);
+    return finish_build(ctx, *t, nullptr, nullptr);
+}
 
 // ================================================================ C ABI ====
 extern "C" {
@@ -1735,12 +1795,14 @@ extern "C" {
 TPE_DEV int tpe1_history_reset(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
                       const double* cat_p, int64_t n_cat_p) {
     if (!ctx) return TPE_ERR_ARG;
+    TPE_SETTLE(ctx);
     return history_reset(ctx, specs, n_labels, cat_p, n_cat_p);
 }
 
 TPE_DEV int tpe1_history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial,
                        const double* obs_val) {
     if (!ctx || !n_new) return TPE_ERR_ARG;
+    TPE_SETTLE(ctx);
     return history_append(ctx, n_new, obs_trial, obs_val);
 }
 
@@ -1748,6 +1810,7 @@ TPE_DEV int tpe1_build_posterior_resident(tpe_ctx* ctx, const double* losses, in
                                  int64_t n_valid, double gamma, double prior_weight, int32_t lf,
                                  int32_t* n_below_out) {
     if (!ctx) return TPE_ERR_ARG;
+    TPE_SETTLE(ctx);
     return build_resident(ctx, losses, n_trials, n_valid, gamma, prior_weight, lf, n_below_out);
 }
 
@@ -1756,6 +1819,7 @@ TPE_DEV int tpe1_build_posterior_resident_ordered(tpe_ctx* ctx, const double* lo
                                                   int32_t lf, const uint8_t* below, const int64_t* order_off,
                                                   const int32_t* order, int32_t* n_below_out, int32_t* ties) {
     if (!ctx) return TPE_ERR_ARG;
+    TPE_SETTLE(ctx);
     return build_resident(ctx, losses, n_trials, n_valid, gamma, prior_weight, lf, n_below_out, below,
                           order_off, order, ties);
 }
@@ -1765,6 +1829,7 @@ TPE_DEV int tpe1_rebuild_labels(tpe_ctx* ctx, const double* losses, int64_t n_tr
                                 const int32_t* order, const int32_t* labels, int32_t n_only,
                                 int32_t* n_below_out, int32_t* ties) {
     if (!ctx) return TPE_ERR_ARG;
+    TPE_SETTLE(ctx);
     if (!labels || n_only <= 0) return ctx->fail(TPE_ERR_ARG, "tpe_rebuild_labels: no labels");
     return build_resident(ctx, losses, n_trials, n_valid, gamma, prior_weight, lf, n_below_out, nullptr,
                           order_off, order, ties, labels, n_only);
@@ -1776,6 +1841,7 @@ TPE_DEV int tpe1_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int3
                         const double* obs_val, double gamma, double prior_weight, int32_t lf,
                         int32_t* n_below_out) {
     if (!ctx) return TPE_ERR_ARG;
+    TPE_SETTLE(ctx);
     if (n_labels <= 0 || !specs || !obs_off || n_trials < 0 || (n_trials > 0 && !losses))
         return ctx->fail(TPE_ERR_ARG, "tpe_build_posterior: bad arguments");
     if (obs_off[0] != 0 || obs_off[n_labels] < 0 || obs_off[n_labels] >= INT32_MAX)
@@ -1797,6 +1863,7 @@ TPE_DEV int tpe1_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int3
 int tpe_get_mixture(tpe_ctx* ctx, int32_t label, int32_t side, double* weights, double* mus,
                     double* sigmas, int32_t cap, int32_t* n) {
     if (!ctx) return TPE_ERR_ARG;
+    TPE_SETTLE(ctx);
     auto& B = ctx->build;
     if (label < 0 || label >= B.n_labels || side < 0 || side > 1 || ctx->resident.n_labels != B.n_labels)
         return ctx->fail(TPE_ERR_ARG, "tpe_get_mixture: no such built mixture");
@@ -1818,7 +1885,20 @@ int32_t tpe_resident_labels(const tpe_ctx* ctx) { return ctx ? ctx->resident.n_l
 
 int tpe_last_build_ms(const tpe_ctx* ctx, float* ms) {
     if (!ctx || !ms) return TPE_ERR_ARG;
+    TPE_SETTLE(const_cast<tpe_ctx*>(ctx));
     *ms = ctx->build_ms;
+    return TPE_OK;
+}
+
+int tpe_build_report(tpe_ctx* ctx, int32_t* n_below, int32_t* ties) {
+    if (!ctx) return TPE_ERR_ARG;
+    TPE_SETTLE(ctx);
+    if (n_below) *n_below = ctx->build.last_n_below;
+    if (ties) {
+        const auto& t = ctx->build.last_ties;
+        if (t.empty()) return ctx->fail(TPE_ERR_ARG, "tpe_build_report: no build");
+        std::memcpy(ties, t.data(), t.size() * sizeof(int32_t));
+    }
     return TPE_OK;
 }
 

@@ -278,6 +278,26 @@ struct UpTask {
     int64_t pad;
 };
 
+// What the end of a build applies on the host once its report is in
+// (tpe_build.hip finish_build).  A subset rebuild beside the index with
+// TPE_OPT_DEFER_REPORT leaves it pending: the next round settles it after
+// queuing the dense labels' kernels (settle_build), every other entry point
+// first thing.
+struct BuildTail {
+    hipStream_t st = nullptr;
+    int64_t rep_dl = 0;
+    int32_t n_labels = 0, lf = 0, n_below = 0;
+    std::vector<DLabel> dl;
+    std::vector<int32_t> grp[kNumModes];
+    std::vector<int64_t> mix;
+    bool beside = false, qc_queued = false, subset = false, deferred = false;
+    int64_t n_trials = 0, n_valid = 0, arm_c = 0;
+    int32_t arm_r = 0;
+    double gamma = 0.0, pw = 0.0;
+    uint64_t loss_hash = 0;
+};
+int settle_build(tpe_ctx* ctx);
+
 // The device posterior builder (tpe_build.hip): the resident history pool
 // and the per-build scratch, grown on demand.
 struct BuildBufs {
@@ -335,6 +355,10 @@ struct BuildBufs {
     int32_t built_lf = 0;
     uint64_t built_loss_hash = 0;  // fingerprint of the losses (a subset rebuild reuses them)
     DevBuf<int32_t> only;          // the labels of a subset rebuild
+    bool defer = false;            // TPE_OPT_DEFER_REPORT: the next subset rebuild beside the index
+    std::unique_ptr<BuildTail> pending;   //   its report, not yet applied
+    std::vector<int32_t> last_ties;       // the last applied build's tie report (tpe_build_report)
+    int32_t last_n_below = 0;
     // a build's inputs: one pinned staging block, one H2D copy, one scatter
     // launch (tpe_build.hip k_build_inputs); the next build waits for ev_up
     PinVec<uint8_t> h_up, h_rep;
@@ -624,6 +648,15 @@ int qc_launch(tpe_ctx* ctx, hipStream_t st);
 
 // per-device implementations of the entry points a multi-device context
 // forwards or shards (tpe_multi.hip exports the public names)
+// a deferred rebuild's report is applied before anything else reads or
+// changes the context's posterior (every entry point that touches it;
+// rounds settle it themselves after queuing the dense labels' kernels)
+#define TPE_SETTLE(ctx)                                   \
+    do {                                                  \
+        const int settle_rc_ = tpe_rt::settle_build(ctx); \
+        if (settle_rc_) return settle_rc_;                \
+    } while (0)
+
 #define TPE_DEV __attribute__((visibility("hidden")))
 extern "C" {
 TPE_DEV int tpe1_set_posterior(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_labels,

@@ -4403,6 +4403,13 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     if (n < 0 || n_rounds <= 0) return ctx->fail(TPE_ERR_ARG, "bad candidate/round count");
     if (cand_offset < 0 || cand_offset + n > (int64_t)UINT32_MAX)
         return ctx->fail(TPE_ERR_ARG, "candidate indices must stay below 2^32");
+    // a deferred subset rebuild (TPE_OPT_DEFER_REPORT: quantized /
+    // categorical labels on the second stream) is settled after the dense
+    // labels' kernels are queued when this round takes the side families to
+    // the second stream; first thing otherwise
+    if (!(ctx->build.pending && only_label < 0 && cand_in_dev == nullptr && n > 0 && ctx->aux_families &&
+          ctx->aux && !ctx->qx))
+        TPE_SETTLE(ctx);
     // slot map: packed (whole rounds per workgroup) for candidate sets smaller
     // than a tile, tiled otherwise
     Slots S{0, 0, n_rounds};
@@ -4495,6 +4502,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
     const bool splitk = sample && ctx->splitk && n > 0 && S.cpack != 0 &&
                         a.total_slots <= kSplitKMaxSlots;
     if (splitk) {
+        TPE_SETTLE(ctx);
         int32_t s_max = 1;
         for (int m = 0; m < CAT; ++m)
             for (int li : ctx->P->h_group[m]) s_max = std::max(s_max, slices_of(ctx->P->h_labels[li]));
@@ -4523,8 +4531,19 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         const bool side = ctx->aux_families && ctx->aux && !ctx->qx && a.tiles > 0 &&
                           g.count[CAT] + g.count[QUANT_GMM] + g.count[QUANT_LGMM] > 0;
         int rc = TPE_OK;
+        bool dense_done = false;
         if (side) {
             HIPCHK(ctx, hipEventRecord(ctx->ev_cat[0], ctx->stream));
+            if (ctx->build.pending) {
+                // the deferred rebuild: the dense labels' kernels first (they
+                // read none of its labels' records), then its report (the
+                // host waits for the second stream), then the side families
+                // after it on that stream
+                rc = ctx->precision == TPE_F32 ? launch_dense<float>(ctx, g, a) : launch_dense<double>(ctx, g, a);
+                if (rc) return rc;
+                dense_done = true;
+                TPE_SETTLE(ctx);
+            }
             HIPCHK(ctx, hipStreamWaitEvent(ctx->aux, ctx->ev_cat[0], 0));
             std::swap(ctx->stream, ctx->aux);   // (every launch below on the second stream)
             rc = launch_quantized(ctx, g, a, evals_q);
@@ -4533,9 +4552,10 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
             const hipError_t e = hipEventRecord(ctx->ev_cat[1], ctx->aux);
             if (rc == TPE_OK && e != hipSuccess) rc = ctx->hip(e, "second-stream join");
         } else {
+            TPE_SETTLE(ctx);
             rc = launch_quantized(ctx, g, a, evals_q);
         }
-        if (rc == TPE_OK)
+        if (rc == TPE_OK && !dense_done)
             rc = ctx->precision == TPE_F32 ? launch_dense<float>(ctx, g, a) : launch_dense<double>(ctx, g, a);
         if (side) HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_cat[1], 0));
         if (rc) return rc;
@@ -4553,6 +4573,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         launch_round<double, CAT, false>(ctx, g, a);
     }
     HIPCHK(ctx, hipGetLastError());
+    TPE_SETTLE(ctx);   // (every path above settled it; a guard)
     if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->ev1, ctx->stream));
     if (tiles == 1) {
         const int64_t nr = (int64_t)n_rounds * L;
@@ -4959,7 +4980,13 @@ int tpe_ctx_create(int device, int precision, tpe_ctx** out) {
              hipEventCreate(&c->evm[m][1]) == hipSuccess;
     ok = ok && hipEventCreate(&c->evs[0]) == hipSuccess && hipEventCreate(&c->evs[1]) == hipSuccess;
     ok = ok && hipEventCreate(&c->ev_prep[0]) == hipSuccess && hipEventCreate(&c->ev_prep[1]) == hipSuccess;
-    ok = ok && hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) == hipSuccess &&
+    // the second stream at the device's highest priority: its short
+    // kernels (a deferred rebuild's tail, the side families) get workgroup
+    // slots as the dense draw's free up instead of after its whole grid
+    // (config 3 2.42 -> 2.37 ms, config 5 6.93 -> 6.71, r5au)
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    ok = ok && hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, prio_hi) == hipSuccess &&
          hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&c->ev_cat[0], hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&c->ev_cat[1], hipEventDisableTiming) == hipSuccess;
@@ -5053,6 +5080,7 @@ const char* tpe_last_error(const tpe_ctx* c) {
 TPE_DEV int tpe1_set_posterior(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_labels,
                       const double* weights, const double* mus, const double* sigmas,
                       int64_t n_components) {
+    TPE_SETTLE(ctx);
     return set_posterior_impl(ctx, labels, n_labels, weights, mus, sigmas, n_components, true);
 }
 
@@ -5075,6 +5103,7 @@ TPE_DEV int tpe1_suggest_batch(tpe_ctx* ctx, uint64_t seed, const uint32_t* roun
 int tpe_score(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, double* lpdf_below,
               double* lpdf_above, tpe_label_result* out) {
     if (!ctx || (!cand && n > 0)) return TPE_ERR_ARG;
+    TPE_SETTLE(ctx);
     if (label < 0 || label >= ctx->P->n_labels) return ctx->fail(TPE_ERR_ARG, "label out of range");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     // host-side argument checks that the reference raises before computing
@@ -5118,6 +5147,7 @@ int tpe_score(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, double
 int tpe_hot_probe(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, double* upper, double* lower,
                   double* mass) {
     if (!ctx || (n > 0 && (!cand || !upper || !lower || !mass))) return TPE_ERR_ARG;
+    TPE_SETTLE(ctx);
     if (label < 0 || label >= ctx->P->n_labels) return ctx->fail(TPE_ERR_ARG, "label out of range");
     const DLabel& d = ctx->P->h_labels[label];
     if (d.mode != DENSE_GMM && d.mode != DENSE_LGMM)
@@ -5148,6 +5178,7 @@ int tpe_hot_probe(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, do
 int tpe_screen_probe(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, double* score32,
                      double* err_bound) {
     if (!ctx || (n > 0 && (!cand || !score32 || !err_bound))) return TPE_ERR_ARG;
+    TPE_SETTLE(ctx);
     if (label < 0 || label >= ctx->P->n_labels) return ctx->fail(TPE_ERR_ARG, "label out of range");
     const DLabel& d = ctx->P->h_labels[label];
     if (d.mode != DENSE_GMM && d.mode != DENSE_LGMM)
@@ -5313,6 +5344,7 @@ int tpe_last_rescore_terms(const tpe_ctx* ctx, int64_t* terms) {
 
 TPE_DEV int tpe1_prepare(tpe_ctx* ctx, int64_t n_candidates, int32_t n_rounds) {
     if (!ctx) return TPE_ERR_ARG;
+    TPE_SETTLE(ctx);
     if (!ctx->P || ctx->P->n_labels <= 0) return ctx->fail(TPE_ERR_ARG, "no resident posterior");
     if (n_candidates < 0 || n_rounds < 1) return ctx->fail(TPE_ERR_ARG, "bad candidate/round count");
     // the rounds that use the index: tile rounds of >= kWinMinN candidates,
@@ -5328,6 +5360,7 @@ TPE_DEV int tpe1_prepare(tpe_ctx* ctx, int64_t n_candidates, int32_t n_rounds) {
 
 TPE_DEV int tpe1_arm_prepare(tpe_ctx* ctx, int64_t n_candidates, int32_t n_rounds) {
     if (!ctx) return TPE_ERR_ARG;
+    TPE_SETTLE(ctx);
     if (n_candidates < 0 || (n_candidates > 0 && n_rounds < 1))
         return ctx->fail(TPE_ERR_ARG, "bad candidate/round count");
     ctx->arm_c = n_candidates;
@@ -5360,6 +5393,10 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
             if (value < 0 || value > kSlicedRescoreMax)
                 return ctx->fail(TPE_ERR_ARG, "packed sliced re-score limit must be in [0, 65536]");
             ctx->pk_sliced = value;
+            break;
+        case TPE_OPT_DEFER_REPORT:
+            if (!ctx->peers.empty() && value) return ctx->fail(TPE_ERR_ARG, "deferred reports: single-device contexts only");
+            ctx->build.defer = value != 0;
             break;
         case TPE_OPT_BX_SPLIT:
             if (value < 0 || value > 8) return ctx->fail(TPE_ERR_ARG, "index window split must be in [0, 8]");
@@ -5448,18 +5485,21 @@ static int one_label_lpdf(tpe_ctx* ctx, int kind, const double* samples, int64_t
 int tpe_gmm1_lpdf(tpe_ctx* ctx, const double* samples, int64_t n, const double* weights,
                   const double* mus, const double* sigmas, int32_t k, int32_t flags, double low,
                   double high, double q, double* out) {
+    TPE_SETTLE(ctx);
     return one_label_lpdf(ctx, TPE_GMM1, samples, n, weights, mus, sigmas, k, flags, low, high, q, out);
 }
 
 int tpe_lgmm1_lpdf(tpe_ctx* ctx, const double* samples, int64_t n, const double* weights,
                    const double* mus, const double* sigmas, int32_t k, int32_t flags, double low,
                    double high, double q, double* out) {
+    TPE_SETTLE(ctx);
     return one_label_lpdf(ctx, TPE_LGMM1, samples, n, weights, mus, sigmas, k, flags, low, high, q, out);
 }
 
 int tpe_categorical_lpdf(tpe_ctx* ctx, const int64_t* samples, int64_t n, const double* p,
                          int32_t upper, double* out) {
     if (!ctx) return TPE_ERR_ARG;
+    TPE_SETTLE(ctx);
     SingleSlot slot(ctx);
     if (n == 0) return TPE_OK;
     if (!samples || !p || !out || upper <= 0) return ctx->fail(TPE_ERR_ARG, "bad arguments");
@@ -5545,6 +5585,7 @@ static int one_label_sample(tpe_ctx* ctx, int kind, const double* w, const doubl
 int tpe_gmm1_sample(tpe_ctx* ctx, const double* w, const double* mu, const double* sg, int32_t k,
                     int32_t flags, double low, double high, double q, uint64_t seed,
                     uint32_t stream, uint32_t round, int64_t offset, int64_t n, double* out) {
+    TPE_SETTLE(ctx);
     return one_label_sample(ctx, TPE_GMM1, w, mu, sg, k, flags, low, high, q, seed, stream, round,
                             offset, n, out);
 }
@@ -5552,6 +5593,7 @@ int tpe_gmm1_sample(tpe_ctx* ctx, const double* w, const double* mu, const doubl
 int tpe_lgmm1_sample(tpe_ctx* ctx, const double* w, const double* mu, const double* sg, int32_t k,
                      int32_t flags, double low, double high, double q, uint64_t seed,
                      uint32_t stream, uint32_t round, int64_t offset, int64_t n, double* out) {
+    TPE_SETTLE(ctx);
     return one_label_sample(ctx, TPE_LGMM1, w, mu, sg, k, flags, low, high, q, seed, stream, round,
                             offset, n, out);
 }
@@ -5560,6 +5602,7 @@ int tpe_categorical_sample(tpe_ctx* ctx, const double* p, int32_t upper, uint64_
                            uint32_t stream, uint32_t round, int64_t offset, int64_t n,
                            int64_t* out) {
     if (!ctx) return TPE_ERR_ARG;
+    TPE_SETTLE(ctx);
     if (n == 0) return TPE_OK;
     if (!out) return ctx->fail(TPE_ERR_ARG, "null pointer");
     std::vector<double> tmp(n);

@@ -234,10 +234,15 @@ class Engine(object):
         self.n_labels = self.hist_labels
         return nb.value, ties
 
-    def rebuild_labels(self, losses, n_valid, gamma, prior_weight, lf, order_off, order, labels):
+    def rebuild_labels(self, losses, n_valid, gamma, prior_weight, lf, order_off, order, labels,
+                       defer=False):
         """The ordered rebuild of `labels` only (tpe_rebuild_labels), right
         after a build of the same history and arguments; the other labels
-        and the below set are kept.  Returns (n_below, ties)."""
+        and the below set are kept.  Returns (n_below, ties).  defer: a
+        rebuild of quantized / categorical labels only returns without
+        waiting for its report (TPE_OPT_DEFER_REPORT; ties then zeros): the
+        next round applies it after queuing the dense labels' kernels, and
+        build_report() returns the real ties."""
         _check_lf(lf)
         losses = _f64(losses)
         L_ = self.hist_labels
@@ -248,9 +253,19 @@ class Engine(object):
         only = np.ascontiguousarray(sorted(int(l) for l in labels), dtype=np.int32)
         nb = ctypes.c_int32()
         ties = np.zeros(L_ + 1, dtype=np.int32)
+        if defer:
+            self.set_option('defer_report', 1)   # (consumed by this rebuild)
         self._check(self.lib.tpe_rebuild_labels(
             self.h, _ptr(losses), len(losses), int(n_valid), float(gamma), float(prior_weight), int(lf),
             _ptr(order_off), _ptr(order), _ptr(only), len(only), ctypes.byref(nb), _ptr(ties)))
+        return nb.value, ties
+
+    def build_report(self):
+        """(n_below, ties) of the last build, applying a deferred rebuild's
+        report first (tpe_build_report)."""
+        nb = ctypes.c_int32()
+        ties = np.zeros(self.hist_labels + 1, dtype=np.int32)
+        self._check(self.lib.tpe_build_report(self.h, ctypes.byref(nb), _ptr(ties)))
         return nb.value, ties
 
     def get_mixture(self, label, side):
@@ -463,7 +478,7 @@ class Engine(object):
                'rescore_cap': L.TPE_OPT_RESCORE_CAP, 'mode_mask': L.TPE_OPT_MODE_MASK,
                'aux_families': L.TPE_OPT_AUX_FAMILIES, 'hot32': L.TPE_OPT_HOT32,
                'bx_split': L.TPE_OPT_BX_SPLIT, 'bx_t': L.TPE_OPT_BX_T,
-               'pk_sliced': L.TPE_OPT_PK_SLICED}
+               'pk_sliced': L.TPE_OPT_PK_SLICED, 'defer_report': L.TPE_OPT_DEFER_REPORT}
 
     def set_option(self, name, value):
         """Engine switches (include/hyperopt_tpe.h TPE_OPT_*): 'screen',

@@ -381,6 +381,7 @@ def _sort_pool():
 
 
 SUBSET_REBUILD = True   # the ordered rebuild restricted to the labels that need an order
+DEFER_REPORT = True     # round_call: that rebuild's report read after the round (Engine.rebuild_labels(defer=))
 DEFER_QUANT = False     # round_call: the dense labels' round under the argsorts (_run_deferred; measured slower)
 
 
@@ -538,6 +539,7 @@ def _build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of
         have = set()
         ties = np.ones_like(ties)
         t0 = time.perf_counter()
+    deferred = False
     if early is not None:
         orders = early.result()   # (waited for even when unused: obs_of is not shared)
         if need != have and need <= known:
@@ -552,8 +554,15 @@ def _build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of
         t0 = _phase('argsorts', t0)
         if SUBSET_REBUILD and not ties[-1] and len(need) < obs_of.n_labels:
             # no tie across the split (the below set is the one just built):
-            # rebuild only the labels that needed an order
-            nb, ties = eng.rebuild_labels(losses, n_valid, gamma, prior_weight, lf, off, order, need)
+            # rebuild only the labels that needed an order -- with a round
+            # to follow, without waiting for its report (a rebuild of
+            # quantized / categorical labels runs on the second stream; the
+            # round queues the dense labels' kernels before it waits), its
+            # tie check made after the round
+            deferred = (DEFER_REPORT and round_call is not None and len(getattr(eng, 'devices', ())) == 1
+                        and hasattr(eng, 'build_report'))
+            nb, ties = eng.rebuild_labels(losses, n_valid, gamma, prior_weight, lf, off, order, need,
+                                          defer=deferred)
         else:
             nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf, below, off,
                                                    order)
@@ -568,6 +577,17 @@ def _build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of
             assert not np.any(ties[:-1])
     if round_call is not None:
         res = round_call()
+        if deferred:
+            nb, ties = eng.build_report()
+            if np.any(ties[:-1]):
+                # (as above, found after the round: the ordered build with
+                # the dependent labels, and the round again)
+                need |= set(np.flatnonzero(ties[:-1] & 2).tolist())
+                below, off, order = reference_orders(losses, n_below, obs_of, need)
+                nb, ties = eng.build_posterior_ordered(losses, n_valid, gamma, prior_weight, lf, below, off,
+                                                       order)
+                assert not np.any(ties[:-1])
+                res = round_call()
         _phase('round', t0)
         return nb, frozenset(need), res
     return nb, frozenset(need)

@@ -300,8 +300,16 @@ int tpe_get_mixture(tpe_ctx *ctx, int32_t label, int32_t side, double *weights,
  * writes per round). */
 int32_t tpe_resident_labels(const tpe_ctx *ctx);
 
-/* Device time (ms, HIP events) of the last tpe_build_posterior's kernels. */
+/* Device time (ms, HIP events) of the last tpe_build_posterior's kernels
+ * (-1 for a rebuild whose report was deferred, TPE_OPT_DEFER_REPORT). */
 int tpe_last_build_ms(const tpe_ctx *ctx, float *ms);
+
+/* The last build's report, applied first if it was deferred
+ * (TPE_OPT_DEFER_REPORT): n_below and the tie report tpe_rebuild_labels
+ * returns (ties: n_labels + 1 entries, NULL to skip).  Replaces nothing in
+ * the reference: the deferral is this library's (posterior.py
+ * _build_reference_order reads it after the round). */
+int tpe_build_report(tpe_ctx *ctx, int32_t *n_below, int32_t *ties);
 
 /* One suggestion round over every resident label: sample n_candidates per
  * label from the below posterior (global candidate indices
@@ -543,6 +551,14 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *                   candidates one wave per (64 candidates, summation slice)
  *                   instead of one thread per candidate walking its chunk
  *                   (same bits; 0: never; at most 65536)                [8192]
+ *   TPE_OPT_DEFER_REPORT  1: the next tpe_rebuild_labels of quantized /
+ *                   categorical labels only (run on the second stream
+ *                   beside the expansion index) returns without waiting
+ *                   for its report: its ties output is zeros, the next
+ *                   round applies the report after queuing the dense
+ *                   labels' kernels, any other call on the context first;
+ *                   tpe_build_report then returns the real tie report
+ *                   (single-device contexts; consumed by that rebuild)  [0]
  *   TPE_OPT_WIN_GROUPS  label groups of a windowed round, each sorted on a
  *                   second stream while the previous one is screened
  *                   (0: one group; the chip is busy either way)          [0]
@@ -579,6 +595,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_BX_SPLIT 21
 #define TPE_OPT_BX_T 22
 #define TPE_OPT_PK_SLICED 23
+#define TPE_OPT_DEFER_REPORT 24
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
 
 /* Build now what the resident posterior's first round(s) of n_candidates

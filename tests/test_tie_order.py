@@ -191,3 +191,52 @@ def test_label_subset_rebuild_equals_full_rebuild():
     assert r0 == r1
     for a, b in zip(m0, m1):
         assert all(np.array_equal(x, y) for x, y in zip(a, b))
+
+
+@pytest.mark.parametrize('aux,first', [(1, 'round'), (0, 'round'), (1, 'mixture'), (1, 'batch')])
+def test_deferred_rebuild_report(aux, first):
+    """A subset rebuild of quantized labels whose report is deferred
+    (TPE_OPT_DEFER_REPORT, Engine.rebuild_labels(defer=True)): it returns
+    zero ties, the next call on the context applies the report -- a round
+    after queuing the dense labels' kernels (aux families on), or any other
+    call first -- and the round, the mixtures and build_report()'s ties are
+    those of the rebuild that waited."""
+    from hyperopt_amd import posterior as P
+    from hyperopt_amd.engine import Engine
+    from hyperopt_amd.workloads import mixed_history
+    hist = mixed_history(32, 4000, seed=2)
+    specs, cat, losses, off, tr, val = hist.device_inputs()
+    n_valid = int(np.count_nonzero(losses == losses))
+    n_below = P.n_below_of(n_valid, 0.25, 25)
+    out = []
+    for defer in (False, True):
+        eng = Engine(0, 'f64')
+        eng.set_option('aux_families', aux)
+        eng.history_reset(specs, cat)
+        eng.history_append(np.diff(off), tr, val)
+        eng.arm_prepare(1 << 16, 1)
+        nb, ties = eng.build_posterior_ordered(losses, n_valid, 0.25, 1.0, 25)
+        need = set(np.flatnonzero(ties[:-1] & 2).tolist())
+        assert need and all(hist.labels[l][1].startswith('q') for l in need)
+        _, o_off, order = P.reference_orders(losses, n_below, P._ObsOf(off, tr, val), need)
+        nb2, ties2 = eng.rebuild_labels(losses, n_valid, 0.25, 1.0, 25, o_off, order, need, defer=defer)
+        if defer:
+            assert not np.any(ties2)
+        if first == 'mixture':
+            mix = [eng.get_mixture(li, side) for li in sorted(need) for side in (0, 1)]
+            res = eng.suggest(5, 1 << 16, round=2)
+        elif first == 'batch':
+            res = eng.suggest_batch(5, list(range(64)), 24)
+            mix = [eng.get_mixture(li, side) for li in sorted(need) for side in (0, 1)]
+        else:
+            res = eng.suggest(5, 1 << 16, round=2)
+            mix = [eng.get_mixture(li, side) for li in sorted(need) for side in (0, 1)]
+        nb3, ties3 = eng.build_report()
+        assert nb3 == nb2 == nb and not np.any(ties3)
+        res2 = eng.suggest(6, 1 << 16, round=3)   # (a second round: nothing left pending)
+        out.append((mix, np.ascontiguousarray(res).tobytes(), np.ascontiguousarray(res2).tobytes()))
+        eng.close()
+    (m0, r0, s0), (m1, r1, s1) = out
+    assert r0 == r1 and s0 == s1
+    for a, b in zip(m0, m1):
+        assert all(np.array_equal(x, y) for x, y in zip(a, b))
