@@ -45,7 +45,14 @@ namespace {
 
 constexpr int kSplitBlock = 1024;
 constexpr int kPartBlock = 1024;
+constexpr int kPartU = 4;   // k_partition: sub-chunks of kPartBlock per step
 constexpr int kParzenBlock = 1024;
+// k_parzen's and k_fold's loops take kFoldU components per thread per step,
+// their loads issued together: one workgroup per label walks ~37k
+// components at config 5, and one load round trip per element and loop made
+// each ~0.2 ms (r5an).  Per component the arithmetic is unchanged; the
+// loops' reductions are counts, min / max and flags (order-free).
+constexpr int kFoldU = 4;
 constexpr int kMaxLF = 64;          // below-list capacity per label (lf <= kMaxLF)
 constexpr int kCatChunk = 8192;     // categorical bincount: observations staged in LDS
 constexpr int kCatFewBins = 32;     // categorical bincount by ordered bin compaction up to here
@@ -522,56 +529,83 @@ __global__ __launch_bounds__(kPartBlock) void k_partition(
     const int l = only ? only[blockIdx.x] : (int)blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int64_t off = p_off[l], M = cnt[l];
     const bool cat = specs[l].kind == TPE_CATEGORICAL;
-    __shared__ int wb[kPartBlock / 64], wa[kPartBlock / 64];
     __shared__ int base_b, base_a;
     if (tid == 0) base_b = base_a = 0;
     __syncthreads();
     const uint64_t lt = (1ull << lane) - 1ull;
-    for (int64_t c0 = 0; c0 < M; c0 += kPartBlock) {
-        const int64_t i = c0 + tid;
-        bool isb = false, isa = false;
-        double v = 0.0;
-        if (i < M) {
-            const int32_t t = p_trial[off + i];
-            v = p_val[off + i];
-            if (t >= 0 && t < T) {
-                const double ls = losses[t];
-                isb = below[t] != 0;
-                isa = !isb && ls == ls;
-            } else if (t >= T) {
-                atomicOr(err, 1);
+    // kPartU sub-chunks of kPartBlock observations per step: their loads
+    // issued together, their ballots counted per wave, ONE barrier pair for
+    // all of them (4 loads and 3 barriers per 1024 observations before: ~0.16
+    // ms per 50k-observation label, r5an); positions and ranks unchanged
+    constexpr int kW = kPartBlock / 64;
+    __shared__ int wbu[kPartU][kW], wau[kPartU][kW];
+    for (int64_t c0 = 0; c0 < M; c0 += (int64_t)kPartU * kPartBlock) {
+        int32_t tr[kPartU];
+        double vv[kPartU];
+#pragma unroll
+        for (int u = 0; u < kPartU; ++u) {
+            const int64_t i = c0 + (int64_t)u * kPartBlock + tid;
+            tr[u] = i < M ? p_trial[off + i] : -1;
+            vv[u] = i < M ? p_val[off + i] : 0.0;
+        }
+        bool isb[kPartU], isa[kPartU];
+#pragma unroll
+        for (int u = 0; u < kPartU; ++u) {
+            const int64_t i = c0 + (int64_t)u * kPartBlock + tid;
+            const int32_t t = tr[u];
+            isb[u] = isa[u] = false;
+            if (i < M) {
+                if (t >= 0 && t < T) {
+                    const double ls = losses[t];
+                    isb[u] = below[t] != 0;
+                    isa[u] = !isb[u] && ls == ls;
+                } else if (t >= T) {
+                    atomicOr(err, 1);
+                }
             }
         }
-        const uint64_t bb = __ballot(isb), ba = __ballot(isa);
-        if (lane == 0) {
-            wb[wv] = __popcll(bb);
-            wa[wv] = __popcll(ba);
+        uint64_t bb[kPartU], ba[kPartU];
+#pragma unroll
+        for (int u = 0; u < kPartU; ++u) {
+            bb[u] = __ballot(isb[u]);
+            ba[u] = __ballot(isa[u]);
+            if (lane == 0) {
+                wbu[u][wv] = __popcll(bb[u]);
+                wau[u][wv] = __popcll(ba[u]);
+            }
         }
         __syncthreads();
         int ob = base_b, oa = base_a;
-        for (int w = 0; w < wv; ++w) {
-            ob += wb[w];
-            oa += wa[w];
-        }
-        if (isb) {
-            const int p = ob + __popcll(bb & lt);
-            if (p < kMaxLF) below_val[(size_t)l * kMaxLF + p] = v;
-            else atomicOr(err, 2);
-        }
-        if (i < M) {
-            const int p = oa + __popcll(ba & lt);
-            if (cat) {
-                if (isa) keys[off + p] = v;
-            } else {
-                arank[off + i] = isa ? p : -1;
+#pragma unroll
+        for (int u = 0; u < kPartU; ++u) {
+            int pb = ob, pa = oa;   // this sub-chunk's wave offsets
+            for (int w = 0; w < wv; ++w) {
+                pb += wbu[u][w];
+                pa += wau[u][w];
+            }
+            const int64_t i = c0 + (int64_t)u * kPartBlock + tid;
+            if (isb[u]) {
+                const int p = pb + __popcll(bb[u] & lt);
+                if (p < kMaxLF) below_val[(size_t)l * kMaxLF + p] = vv[u];
+                else atomicOr(err, 2);
+            }
+            if (i < M) {
+                const int p = pa + __popcll(ba[u] & lt);
+                if (cat) {
+                    if (isa[u]) keys[off + p] = vv[u];
+                } else {
+                    arank[off + i] = isa[u] ? p : -1;
+                }
+            }
+            for (int w = 0; w < kW; ++w) {   // (the sub-chunk's totals)
+                ob += wbu[u][w];
+                oa += wau[u][w];
             }
         }
         __syncthreads();
         if (tid == 0) {
-            for (int w = 0; w < kPartBlock / 64; ++w) {
-                base_b += wb[w];
-                base_a += wa[w];
-            }
+            base_b = ob;
+            base_a = oa;
         }
         __syncthreads();
     }
@@ -580,28 +614,42 @@ __global__ __launch_bounds__(kPartBlock) void k_partition(
         __syncthreads();
         if (tid == 0) base_a = 0;
         __syncthreads();
-        for (int64_t c0 = 0; c0 < M; c0 += kPartBlock) {
-            const int64_t i = c0 + tid;
-            int32_t r = -1;
-            double k = 0.0;
-            if (i < M) {
-                k = s_key[off + i];
-                r = arank[off + s_idx[off + i]];
+        for (int64_t c0 = 0; c0 < M; c0 += (int64_t)kPartU * kPartBlock) {
+            int32_t si_[kPartU];
+            double kk[kPartU];
+#pragma unroll
+            for (int u = 0; u < kPartU; ++u) {
+                const int64_t i = c0 + (int64_t)u * kPartBlock + tid;
+                si_[u] = i < M ? s_idx[off + i] : 0;
+                kk[u] = i < M ? s_key[off + i] : 0.0;
             }
-            const bool keep = r >= 0;
-            const uint64_t ba = __ballot(keep);
-            if (lane == 0) wa[wv] = __popcll(ba);
+            int32_t r[kPartU];
+#pragma unroll
+            for (int u = 0; u < kPartU; ++u) {
+                const int64_t i = c0 + (int64_t)u * kPartBlock + tid;
+                r[u] = i < M ? arank[off + si_[u]] : -1;
+            }
+            uint64_t ba[kPartU];
+#pragma unroll
+            for (int u = 0; u < kPartU; ++u) {
+                ba[u] = __ballot(r[u] >= 0);
+                if (lane == 0) wau[u][wv] = __popcll(ba[u]);
+            }
             __syncthreads();
             int oa = base_a;
-            for (int w = 0; w < wv; ++w) oa += wa[w];
-            if (keep) {
-                const int p = oa + __popcll(ba & lt);
-                keys[off + p] = k;
-                idx[off + p] = r;
+#pragma unroll
+            for (int u = 0; u < kPartU; ++u) {
+                int pa = oa;
+                for (int w = 0; w < wv; ++w) pa += wau[u][w];
+                if (r[u] >= 0) {
+                    const int p = pa + __popcll(ba[u] & lt);
+                    keys[off + p] = kk[u];
+                    idx[off + p] = r[u];
+                }
+                for (int w = 0; w < kW; ++w) oa += wau[u][w];
             }
             __syncthreads();
-            if (tid == 0)
-                for (int w = 0; w < kPartBlock / 64; ++w) base_a += wa[w];
+            if (tid == 0) base_a = oa;
             __syncthreads();
         }
     }
@@ -862,7 +910,16 @@ __global__ __launch_bounds__(kParzenBlock) void k_parzen(
         // np.searchsorted(sorted, prior_mu), side='left' = the number of
         // sorted values < prior_mu: counted by every thread, summed per wave
         int cnt = 0;
-        for (int64_t j = tid; j < n; j += kParzenBlock) cnt += sk[j] < pmu ? 1 : 0;
+        for (int64_t j0 = tid; j0 < n; j0 += (int64_t)kFoldU * kParzenBlock) {
+            double v[kFoldU];
+#pragma unroll
+            for (int u = 0; u < kFoldU; ++u) {
+                const int64_t j = j0 + (int64_t)u * kParzenBlock;
+                v[u] = j < n ? sk[j] : pmu;   // (pmu: not counted)
+            }
+#pragma unroll
+            for (int u = 0; u < kFoldU; ++u) cnt += v[u] < pmu ? 1 : 0;
+        }
         for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
         if ((tid & 63) == 0 && cnt) atomicAdd(&pos_sh, cnt);
     }
@@ -872,37 +929,55 @@ __global__ __launch_bounds__(kParzenBlock) void k_parzen(
     const LFRamp ramp = lf_ramp(n, lf);
     const double maxsigma = psig / 1.0;
     const double minsigma = psig / fmin(100.0, 1.0 + (double)K);
-    for (int64_t j = tid; j < K; j += kParzenBlock) {
-        auto srtd = [&](int64_t q) { return q < pos ? sk[q] : (q == pos ? pmu : sk[q - 1]); };
-        double s;
-        if (n == 0) {
-            s = psig;
-        } else if (n == 1) {
-            s = (j == pos) ? psig : psig * .5;
-        } else if (j == 0) {
-            s = srtd(1) - srtd(0);
-        } else if (j == K - 1) {
-            s = srtd(K - 1) - srtd(K - 2);
-        } else {
-            s = np_maximum(srtd(j) - srtd(j - 1), srtd(j + 1) - srtd(j));
+    // (kFoldU slots per thread per step, their loads issued together: the
+    // values around each slot and its observation's rank; r5an)
+    auto srtd = [&](int64_t q) { return q < pos ? sk[q] : (q == pos ? pmu : sk[q - 1]); };
+    for (int64_t j0 = tid; j0 < K; j0 += (int64_t)kFoldU * kParzenBlock) {
+        double vm[kFoldU], v0[kFoldU], vp[kFoldU];
+        int32_t rr[kFoldU];
+#pragma unroll
+        for (int u = 0; u < kFoldU; ++u) {
+            const int64_t j = j0 + (int64_t)u * kParzenBlock;
+            const bool ok = j < K;
+            vm[u] = ok && j >= 1 ? srtd(j - 1) : 0.0;
+            v0[u] = ok ? srtd(j) : 0.0;
+            vp[u] = ok && j + 1 < K ? srtd(j + 1) : 0.0;
+            rr[u] = ok && j != pos ? si[j < pos ? j : j - 1] : 0;
         }
-        s = np_minimum(np_maximum(s, minsigma), maxsigma);   // np.clip
-        if (j == pos) s = psig;
-        double wt;
-        if (j == pos) {
-            wt = pw;
-        } else {
-            const int32_t r = si[j < pos ? j : j - 1];
-            if (r < 0 || r >= n) {   // (a supplied order out of range)
-                atomicOr(err, 8);
-                wt = 0.0;
+#pragma unroll
+        for (int u = 0; u < kFoldU; ++u) {
+            const int64_t j = j0 + (int64_t)u * kParzenBlock;
+            if (j >= K) continue;
+            double s;
+            if (n == 0) {
+                s = psig;
+            } else if (n == 1) {
+                s = (j == pos) ? psig : psig * .5;
+            } else if (j == 0) {
+                s = vp[u] - v0[u];
+            } else if (j == K - 1) {
+                s = v0[u] - vm[u];
             } else {
-                wt = use_lf ? lf_weight(r, ramp) : 1.0;
+                s = np_maximum(v0[u] - vm[u], vp[u] - v0[u]);
             }
+            s = np_minimum(np_maximum(s, minsigma), maxsigma);   // np.clip
+            if (j == pos) s = psig;
+            double wt;
+            if (j == pos) {
+                wt = pw;
+            } else {
+                const int32_t r = rr[u];
+                if (r < 0 || r >= n) {   // (a supplied order out of range)
+                    atomicOr(err, 8);
+                    wt = 0.0;
+                } else {
+                    wt = use_lf ? lf_weight(r, ramp) : 1.0;
+                }
+            }
+            w[o + j] = wt;
+            mu[o + j] = v0[u];
+            sigma[o + j] = s;
         }
-        w[o + j] = wt;
-        mu[o + j] = srtd(j);
-        sigma[o + j] = s;
     }
     __syncthreads();
     // does the mixture depend on the order of tied observations?  Whenever
@@ -913,12 +988,36 @@ __global__ __launch_bounds__(kParzenBlock) void k_parzen(
     // slots, and the order of the normalising np.sum.
     if (use_lf && !supplied) {
         bool dep = false;
-        for (int64_t j = 1 + tid; j < K; j += kParzenBlock)
-            if (j != pos && j - 1 != pos && mu[o + j] == mu[o + j - 1]) dep = true;
+        for (int64_t j0 = 1 + tid; j0 < K; j0 += (int64_t)kFoldU * kParzenBlock) {
+            double a[kFoldU], b[kFoldU];
+#pragma unroll
+            for (int u = 0; u < kFoldU; ++u) {
+                const int64_t j = j0 + (int64_t)u * kParzenBlock;
+                a[u] = j < K ? mu[o + j] : 0.0;
+                b[u] = j < K ? mu[o + j - 1] : 1.0;
+            }
+#pragma unroll
+            for (int u = 0; u < kFoldU; ++u) {
+                const int64_t j = j0 + (int64_t)u * kParzenBlock;
+                if (j < K && j != pos && j - 1 != pos && a[u] == b[u]) dep = true;
+            }
+        }
         if (__ballot(dep) && (tid & 63) == 0) atomicOr(ties + l, 1 << side);
     }
     const double tot = block_np_sum(w + o, K, leaf_sum + o);
-    for (int64_t j = tid; j < K; j += kParzenBlock) w[o + j] = w[o + j] / tot;
+    for (int64_t j0 = tid; j0 < K; j0 += (int64_t)kFoldU * kParzenBlock) {
+        double v[kFoldU];
+#pragma unroll
+        for (int u = 0; u < kFoldU; ++u) {
+            const int64_t j = j0 + (int64_t)u * kParzenBlock;
+            if (j < K) v[u] = w[o + j];
+        }
+#pragma unroll
+        for (int u = 0; u < kFoldU; ++u) {
+            const int64_t j = j0 + (int64_t)u * kParzenBlock;
+            if (j < K) w[o + j] = v[u] / tot;
+        }
+    }
     if (tid == 0) kcount[2 * l + side] = (int32_t)K;
 }
 
@@ -1018,9 +1117,18 @@ __global__ __launch_bounds__(kParzenBlock) void k_fold(
                 lo = fmin(lo, mu[ob + k]);
                 hi = fmax(hi, mu[ob + k]);
             }
-            for (int64_t k = tid; k < Ka; k += kParzenBlock) {
-                lo = fmin(lo, mu[oa + k]);
-                hi = fmax(hi, mu[oa + k]);
+            for (int64_t k0 = tid; k0 < Ka; k0 += (int64_t)kFoldU * kParzenBlock) {
+                double v[kFoldU];
+#pragma unroll
+                for (int u = 0; u < kFoldU; ++u) {
+                    const int64_t k = k0 + (int64_t)u * kParzenBlock;
+                    v[u] = k < Ka ? mu[oa + k] : mu[oa + k0];
+                }
+#pragma unroll
+                for (int u = 0; u < kFoldU; ++u) {
+                    lo = fmin(lo, v[u]);
+                    hi = fmax(hi, v[u]);
+                }
             }
             lo = block_min(lo);
             hi = block_max(hi);
@@ -1037,35 +1145,75 @@ __global__ __launch_bounds__(kParzenBlock) void k_fold(
                 p_accept = block_np_sum(terms + o, K, leaf_sum + o);
             if (quant) {
                 (side ? d.logpacc_a : d.logpacc_b) = log(p_accept);
-                for (int64_t k = tid; k < K; k += kParzenBlock) {
-                    const double a = 1.0 / fmax(sqrt(2.0) * sigma[o + k], kEps);
-                    c64[o + k] = Comp<double>{mu[o + k], a, 0.0, w[o + k]};
-                    c32[o + k] = Comp<float>{(float)mu[o + k], (float)a, 0.f, (float)w[o + k]};
+                for (int64_t k0 = tid; k0 < K; k0 += (int64_t)kFoldU * kParzenBlock) {
+                    double sg[kFoldU], mk[kFoldU], wk[kFoldU];
+#pragma unroll
+                    for (int u = 0; u < kFoldU; ++u) {
+                        const int64_t k = k0 + (int64_t)u * kParzenBlock;
+                        if (k < K) {
+                            sg[u] = sigma[o + k];
+                            mk[u] = mu[o + k];
+                            wk[u] = w[o + k];
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < kFoldU; ++u) {
+                        const int64_t k = k0 + (int64_t)u * kParzenBlock;
+                        if (k >= K) continue;
+                        const double a = 1.0 / fmax(sqrt(2.0) * sg[u], kEps);
+                        c64[o + k] = Comp<double>{mk[u], a, 0.0, wk[u]};
+                        c32[o + k] = Comp<float>{(float)mk[u], (float)a, 0.f, (float)wk[u]};
+                    }
                 }
                 continue;
             }
             double M = -INFINITY;
-            for (int64_t k = tid; k < K; k += kParzenBlock) {
-                // GMM1: (w / Z) from k_fold_terms, then / p_accept and log
-                // (tpe.py:148-150); LGMM1: the whole constant (tpe.py:199-208)
-                const double c = !is_lgmm ? log(cterm[o + k] / p_accept) : cterm[o + k];
-                cterm[o + k] = c;
-                M = fmax(M, c);
+            for (int64_t k0 = tid; k0 < K; k0 += (int64_t)kFoldU * kParzenBlock) {
+                double ct[kFoldU];
+#pragma unroll
+                for (int u = 0; u < kFoldU; ++u) {
+                    const int64_t k = k0 + (int64_t)u * kParzenBlock;
+                    if (k < K) ct[u] = cterm[o + k];
+                }
+#pragma unroll
+                for (int u = 0; u < kFoldU; ++u) {
+                    const int64_t k = k0 + (int64_t)u * kParzenBlock;
+                    if (k >= K) continue;
+                    // GMM1: (w / Z) from k_fold_terms, then / p_accept and log
+                    // (tpe.py:148-150); LGMM1: the whole constant (tpe.py:199-208)
+                    const double c = !is_lgmm ? log(ct[u] / p_accept) : ct[u];
+                    if (!is_lgmm) cterm[o + k] = c;
+                    M = fmax(M, c);
+                }
             }
             M = block_max(M);
             if (!isfinite(M)) M = 0.0;
             (side ? d.shift_a : d.shift_b) = M;
             double amax = 0.0;
-            for (int64_t k = tid; k < K; k += kParzenBlock) {
-                const double a = ascale[o + k];
-                const double c = cterm[o + k];
-                c64[o + k] = Comp<double>{(mu[o + k] - centre) * (a * sK), a * sK, (c - M) * kExpScale,
-                                          w[o + k]};
-                const double a2 = a * sqrt(l2e);
-                const float a32 = (float)a2;
-                c32[o + k] = Comp<float>{(float)((mu[o + k] - centre) * a2), a32, (float)((c - M) * l2e),
-                                         (float)w[o + k]};
-                amax = fmax(amax, (double)a32);
+            for (int64_t k0 = tid; k0 < K; k0 += (int64_t)kFoldU * kParzenBlock) {
+                double av[kFoldU], cv[kFoldU], mv[kFoldU], wv[kFoldU];
+#pragma unroll
+                for (int u = 0; u < kFoldU; ++u) {
+                    const int64_t k = k0 + (int64_t)u * kParzenBlock;
+                    if (k < K) {
+                        av[u] = ascale[o + k];
+                        cv[u] = cterm[o + k];
+                        mv[u] = mu[o + k];
+                        wv[u] = w[o + k];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kFoldU; ++u) {
+                    const int64_t k = k0 + (int64_t)u * kParzenBlock;
+                    if (k >= K) continue;
+                    const double a = av[u], c = cv[u];
+                    c64[o + k] = Comp<double>{(mv[u] - centre) * (a * sK), a * sK, (c - M) * kExpScale, wv[u]};
+                    const double a2 = a * sqrt(l2e);
+                    const float a32 = (float)a2;
+                    c32[o + k] = Comp<float>{(float)((mv[u] - centre) * a2), a32, (float)((c - M) * l2e),
+                                             (float)wv[u]};
+                    amax = fmax(amax, (double)a32);
+                }
             }
             amax = block_max(amax);
             (side ? d.amax_a : d.amax_b) = (float)amax;
