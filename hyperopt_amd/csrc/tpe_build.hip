@@ -280,11 +280,35 @@ __device__ __forceinline__ double np_minimum(double a, double b) { return (a != 
 // keys (positions tid, tid + kSplitBlock, ...; T <= R kSplitBlock) in
 // registers across the passes instead of reloading them (a history of 10^4
 // trials: 32 -> ~10 us); R = 0 walks the losses in every pass.
+//
+// Slice mode (cand_key != nullptr; k_split_merge finishes): workgroup x
+// takes the positions [x R kSplitBlock, (x + 1) R kSplitBlock) of the
+// losses, zeroes their below flags and writes its m_sel smallest (key,
+// position) pairs -- the keys < its K* and the first by position of those ==
+// K* -- to cand[x m_sel ..] (unused slots: key ~0, position -1).  The
+// n_below smallest pairs of all T -- the below set, ties by position -- are
+// among the slices' n_below + 1 smallest, and so is the next one, whose key
+// tells a tie across the boundary (one workgroup walking 50k losses 8 times
+// took 115 us, r5an).
 template <int R>
-__global__ __launch_bounds__(kSplitBlock) void k_split(const double* __restrict__ losses, int64_t T,
-                                                       int32_t n_below, uint8_t* __restrict__ below,
-                                                       int32_t* __restrict__ split_tie) {
+__global__ __launch_bounds__(kSplitBlock) void k_split(const double* __restrict__ losses_all, int64_t T_all,
+                                                       int32_t n_below_all, uint8_t* __restrict__ below_all,
+                                                       int32_t* __restrict__ split_tie, int32_t m_sel,
+                                                       uint64_t* __restrict__ cand_key,
+                                                       int64_t* __restrict__ cand_pos) {
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const bool slice = cand_key != nullptr;
+    const int64_t base = slice ? (int64_t)blockIdx.x * R * kSplitBlock : 0;
+    const double* losses = losses_all + base;
+    uint8_t* below = below_all + base;
+    const int64_t T = !slice ? T_all : (T_all - base < (int64_t)R * kSplitBlock ? T_all - base
+                                                                                 : (int64_t)R * kSplitBlock);
+    const int32_t n_below = !slice ? n_below_all : (int32_t)((int64_t)m_sel < T ? (int64_t)m_sel : T);
+    if (slice)
+        for (int32_t j = tid; j < m_sel; j += kSplitBlock) {
+            cand_key[(size_t)blockIdx.x * m_sel + j] = ~0ull;
+            cand_pos[(size_t)blockIdx.x * m_sel + j] = -1;
+        }
     uint64_t kr[R > 0 ? R : 1];
     if constexpr (R > 0) {
 #pragma unroll
@@ -367,6 +391,46 @@ __global__ __launch_bounds__(kSplitBlock) void k_split(const double* __restrict_
     }
     const uint64_t kstar = prefix_sh;
     const int64_t take_eq = need_sh;      // how many keys == K* join, in position order
+    if (slice) {
+        // the keys < K* (any slots), then the first take_eq keys == K* by
+        // position after them
+        __shared__ int32_t less_sh;
+        if (tid == 0) {
+            less_sh = 0;
+            base_sh = 0;
+        }
+        __syncthreads();
+        uint64_t* ck = cand_key + (size_t)blockIdx.x * m_sel;
+        int64_t* cp = cand_pos + (size_t)blockIdx.x * m_sel;
+        const int32_t n_less = n_below - (int32_t)take_eq;
+        each([&](int64_t i, uint64_t k, bool valid) {
+            if (valid && k < kstar) {
+                const int32_t q = atomicAdd(&less_sh, 1);
+                ck[q] = k;
+                cp[q] = base + i;
+            }
+        });
+        const uint64_t lt = (1ull << lane) - 1ull;
+        for (int64_t c0 = 0; c0 < T; c0 += kSplitBlock) {
+            const int64_t i = c0 + tid;
+            const uint64_t k = i < T ? asc_key(losses[i]) : ~0ull;
+            const bool eq = i < T && k == kstar;
+            const uint64_t m = __ballot(eq);
+            if (lane == 0) wcnt[wv] = __popcll(m);
+            __syncthreads();
+            int64_t r = base_sh + __popcll(m & lt);
+            for (int w = 0; w < wv; ++w) r += wcnt[w];
+            if (eq && r < take_eq) {
+                ck[n_less + r] = k;
+                cp[n_less + r] = base + i;
+            }
+            __syncthreads();
+            if (tid == 0)
+                for (int w = 0; w < kSplitBlock / 64; ++w) base_sh += wcnt[w];
+            __syncthreads();
+        }
+        return;
+    }
     if (take_eq == (int64_t)eq_sh) {      // every key == K* joins: no position order needed
         each([&](int64_t i, uint64_t k, bool valid) {
             if (valid && k <= kstar) below[i] = 1;
@@ -395,6 +459,43 @@ __global__ __launch_bounds__(kSplitBlock) void k_split(const double* __restrict_
             for (int w = 0; w < kSplitBlock / 64; ++w) base_sh += wcnt[w];
         __syncthreads();
     }
+}
+
+// The slices' candidates (k_split slice mode) -> the below set: each
+// candidate's rank among all by (key, position), the n_below smallest
+// flagged; a tie across the boundary when the next one has the key of the
+// last taken.  One workgroup, up to kSplitMergeMax candidates.
+constexpr int kSplitMergeMax = 2 * kSplitBlock;
+__global__ __launch_bounds__(kSplitBlock) void k_split_merge(const uint64_t* __restrict__ cand_key,
+                                                             const int64_t* __restrict__ cand_pos, int32_t n_cand,
+                                                             int32_t n_below, uint8_t* __restrict__ below,
+                                                             int32_t* __restrict__ split_tie) {
+    __shared__ uint64_t ks[kSplitMergeMax];
+    __shared__ int64_t ps[kSplitMergeMax];
+    __shared__ uint64_t k_last, k_next;
+    __shared__ int has_next;
+    const int tid = threadIdx.x;
+    for (int j = tid; j < n_cand; j += kSplitBlock) {
+        ks[j] = cand_key[j];
+        ps[j] = cand_pos[j] < 0 ? INT64_MAX : cand_pos[j];   // (unused slots last)
+    }
+    if (tid == 0) has_next = 0;
+    __syncthreads();
+    for (int j = tid; j < n_cand; j += kSplitBlock) {
+        if (ps[j] == INT64_MAX) continue;
+        const uint64_t k = ks[j];
+        const int64_t p = ps[j];
+        int32_t rank = 0;
+        for (int q = 0; q < n_cand; ++q) rank += (ks[q] < k || (ks[q] == k && ps[q] < p)) ? 1 : 0;
+        if (rank < n_below) below[p] = 1;
+        if (rank == n_below - 1) k_last = k;
+        if (rank == n_below) {
+            k_next = k;
+            has_next = 1;
+        }
+    }
+    __syncthreads();
+    if (tid == 0 && has_next && k_next == k_last) *split_tie = 1;
 }
 
 // ---------------------------------------------- device-resident history --
@@ -1330,14 +1431,32 @@ int tpe_rt::copy_batch(tpe_ctx* ctx, hipStream_t st, const CopySpec* specs, int 
 namespace {
 
 // k_split with the register form for histories of up to 16 kSplitBlock trials (32 spill)
-void launch_split(hipStream_t st, const double* losses, int64_t T, int32_t n_below, uint8_t* below,
-                  int32_t* split_tie) {
+int launch_split(tpe_ctx* ctx, hipStream_t st, const double* losses, int64_t T, int32_t n_below, uint8_t* below,
+                 int32_t* split_tie) {
     const int64_t per = (T + kSplitBlock - 1) / kSplitBlock;
     const dim3 g(1), b(kSplitBlock);
-    if (per <= 4) hipLaunchKernelGGL(k_split<4>, g, b, 0, st, losses, T, n_below, below, split_tie);
-    else if (per <= 8) hipLaunchKernelGGL(k_split<8>, g, b, 0, st, losses, T, n_below, below, split_tie);
-    else if (per <= 16) hipLaunchKernelGGL(k_split<16>, g, b, 0, st, losses, T, n_below, below, split_tie);
-    else hipLaunchKernelGGL(k_split<0>, g, b, 0, st, losses, T, n_below, below, split_tie);
+    constexpr int64_t kSliceT = 16 * (int64_t)kSplitBlock;
+    const int32_t m_sel = n_below + 1;
+    const int64_t slices = (T + kSliceT - 1) / kSliceT;
+    if (per <= 4) {
+        hipLaunchKernelGGL(k_split<4>, g, b, 0, st, losses, T, n_below, below, split_tie, 0, nullptr, nullptr);
+    } else if (per <= 8) {
+        hipLaunchKernelGGL(k_split<8>, g, b, 0, st, losses, T, n_below, below, split_tie, 0, nullptr, nullptr);
+    } else if (per <= 16) {
+        hipLaunchKernelGGL(k_split<16>, g, b, 0, st, losses, T, n_below, below, split_tie, 0, nullptr, nullptr);
+    } else if (n_below > 0 && slices * m_sel <= kSplitMergeMax) {
+        // slices of 16 Ki losses, each in registers, merged by one workgroup
+        auto& B = ctx->build;
+        HIPCHK(ctx, B.split_key.reserve((size_t)slices * m_sel));
+        HIPCHK(ctx, B.split_pos.reserve((size_t)slices * m_sel));
+        hipLaunchKernelGGL(k_split<16>, dim3((unsigned)slices), b, 0, st, losses, T, n_below, below, split_tie,
+                           m_sel, B.split_key.p, B.split_pos.p);
+        hipLaunchKernelGGL(k_split_merge, g, b, 0, st, B.split_key.p, B.split_pos.p, (int32_t)(slices * m_sel),
+                           n_below, below, split_tie);
+    } else {
+        hipLaunchKernelGGL(k_split<0>, g, b, 0, st, losses, T, n_below, below, split_tie, 0, nullptr, nullptr);
+    }
+    return TPE_OK;
 }
 
 int check_specs(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels, int64_t n_cat_p,
@@ -1848,8 +1967,10 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     }
 
     HIPCHK(ctx, hipEventRecord(ctx->ev0, st));
-    if (T > 0 && !below_h && !subset)
-        launch_split(st, B.losses.p, T, n_below, B.below.p, B.ties.p + n_labels);
+    if (T > 0 && !below_h && !subset) {
+        const int rc = launch_split(ctx, st, B.losses.p, T, n_below, B.below.p, B.ties.p + n_labels);
+        if (rc) return rc;
+    }
     hipLaunchKernelGGL(k_partition, dim3(nl_run), dim3(kPartBlock), 0, st, B.specs.p, B.p_off.p, B.cnt.p,
                        B.p_trial.p, B.p_val.p, B.s_key.p, B.s_idx.p, B.below.p, B.losses.p, T,
                        B.below_val.p, B.arank.p, B.keys.p, B.idx.p, B.counts.p, ctx->errflag.p, only_d);

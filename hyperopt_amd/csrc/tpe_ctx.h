@@ -355,6 +355,8 @@ struct BuildBufs {
     int32_t built_lf = 0;
     uint64_t built_loss_hash = 0;  // fingerprint of the losses (a subset rebuild reuses them)
     DevBuf<int32_t> only;          // the labels of a subset rebuild
+    DevBuf<uint64_t> split_key;    // k_split's slices: their n_below + 1 smallest (key, position)
+    DevBuf<int64_t> split_pos;
     bool defer = false;            // TPE_OPT_DEFER_REPORT: the next subset rebuild beside the index
     std::unique_ptr<BuildTail> pending;   //   its report, not yet applied
     std::vector<int32_t> last_ties;       // the last applied build's tie report (tpe_build_report)
@@ -374,7 +376,8 @@ struct BuildBufs {
         gs_lab2.release(); losses.release(); below.release(); keys.release();
         idx.release(); below_val.release(); counts.release(); kcount.release(); w.release();
         mu.release(); sigma.release(); mix_off.release(); scratch.release(); ties.release();
-        order_off.release(); order.release(); only.release(); d_up.release(); d_rep.release(); d_stage.release();
+        order_off.release(); order.release(); only.release(); split_key.release(); split_pos.release();
+        d_up.release(); d_rep.release(); d_stage.release();
         if (ev_up) (void)hipEventDestroy(ev_up);
         ev_up = nullptr;
         up_pending = false;

@@ -240,3 +240,32 @@ def test_deferred_rebuild_report(aux, first):
     assert r0 == r1 and s0 == s1
     for a, b in zip(m0, m1):
         assert all(np.array_equal(x, y) for x, y in zip(a, b))
+
+
+@pytest.mark.parametrize('n_trials,tie', [(40000, False), (40000, True), (70000, True), (200000, False)])
+def test_split_over_slices(n_trials, tie):
+    """Histories past 16k trials take k_split in slices of 16 Ki losses
+    (each slice's n_below + 1 smallest (loss, position) pairs, merged by
+    one workgroup): the below set is the reference's when no tie straddles
+    the n_below boundary (the mixtures equal the host build's), and a tie
+    there is reported (ties[-1]) -- the product then supplies numpy's below
+    set and again matches the host build."""
+    from hyperopt_amd.engine import Engine
+    hist = coarse_history(n_trials, seed=7, split_tie=False)
+    if tie:   # 15 trials at -6, 20 at -5: n_below = 25 takes 10 of the 20
+        rng = np.random.RandomState(1)
+        pick = rng.permutation(n_trials)[:35]
+        hist.losses[pick[:15]] = -6.0
+        hist.losses[pick[15:]] = -5.0
+    inputs = hist.device_inputs()
+    eng = Engine(0)
+    try:
+        eng.history_reset(inputs[0], inputs[1])
+        eng.history_append(np.diff(inputs[3]), inputs[4], inputs[5])
+        nb, ties = eng.build_posterior_ordered(hist.losses, len(hist.losses), 0.25, 1.0)
+        assert nb == 25 and ties[-1] == (1 if tie else 0), (nb, ties[-1])
+        nb = eng.build_posterior(*inputs, gamma=0.25, prior_weight=1.0)
+        assert nb == 25
+        _assert_same(eng, hist, hist.posteriors())
+    finally:
+        eng.close()
