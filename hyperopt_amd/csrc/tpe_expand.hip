@@ -876,12 +876,13 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
                        P.bx_nc.p, P.bx_loff.p, P.bx_list.p);
     // the window split: ~8192 workgroups (4 per CU at a time, LDS-bound; the
     // heavy dense-region blocks split too, so the tail shortens -- config 3's
-    // ~2000 blocks: split 1 / 2 / 4 / 8 -> 0.628 / 0.592 / 0.564 / 0.604 ms, r5j)
-    // (config 5's ~6000 blocks split in 2: the index 4.8 -> 4.6 ms, but the
-    // quantized labels' rebuild beside it on the second stream 1.5 -> 2.1 ms,
-    // the step unchanged -- r5z: not split)
+    // ~2000 blocks: split 1 / 2 / 4 / 8 -> 0.538 / 0.492 / 0.469 / 0.503 ms in
+    // one process, r5be); past 4096 blocks in 3 parts -- config 5's ~6000:
+    // 1 / 2 / 3 / 4 -> 3.36 / 3.13 / 3.03 / 3.05 ms, r5bf (unsplit until the
+    // quantized labels' rebuild beside it stopped holding the host, r5z)
     const int64_t wgs = (rows + 63) / 64;
     const int nsplit = ctx->bx_split > 0 ? std::min(ctx->bx_split, kBxMaxSplit)
+                       : wgs >= 4096     ? 3
                                          : (int)std::max<int64_t>(1, std::min<int64_t>(kBxMaxSplit, 8192 / std::max<int64_t>(wgs, 1)));
     if (nsplit > 1) HIPCHK(ctx, P.bx_part.reserve((size_t)nsplit * kPartSums * rows));
     hipLaunchKernelGGL(k_bx_table, dim3((unsigned)((bins_max + 63) / 64), nl, nsplit), dim3(kBlock), 0,
