@@ -12,8 +12,11 @@ PREPARE_MIN = 8192   # candidate slots of a round from which it uses the expansi
 # below it the known labels' argsorts come first and ONE ordered build
 # follows (r5q, config 3: a 4-label shard's step 1.19 -> 1.10 ms without the
 # overlap, the whole 32-label step 2.57 -> 2.88 ms: the index is long enough
-# to hide the argsorts only with many dense labels)
-OVERLAP_MIN_DENSE = 8
+# to hide the argsorts only with many dense labels) -- until the subset
+# rebuild's report was deferred into the round (posterior.DEFER_REPORT): the
+# overlap then wins for shards too (config 3's 4-label shards 0.95-1.03 ->
+# 0.85-0.97 ms, r5bh)
+OVERLAP_MIN_DENSE = 1
 DENSE_KINDS = ('uniform', 'loguniform', 'normal', 'lognormal')
 
 # config-3 kind cycle: kind = i mod 5
