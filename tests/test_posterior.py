@@ -135,3 +135,48 @@ def test_uploader_vectorised_append_matches_per_label_transforms(monkeypatch):
     up.build(eng, hist.labels, loop.view(30), 0.25, 1.0)
     with pytest.raises(P.NonFiniteObservation, match=name):
         up.build(eng, hist.labels, loop.view(45), 0.25, 1.0)
+
+
+@pytest.mark.parametrize('n_trials', [300, 40000])
+def test_reference_orders_matches_per_label_argsort(n_trials):
+    """posterior.reference_orders (the tie orders the device build takes:
+    gathers, argsorts and int32 stores in the sort pool past _POOL_MIN
+    observations) equals a plain per-label np.argsort of the above
+    observations in observation order (tpe.py:433), for labels observed in
+    every trial and for conditional labels (some trials without the label,
+    a trial position of -1, NaN losses)."""
+    rng = np.random.RandomState(5)
+    T = n_trials
+    losses = np.round(rng.normal(size=T), 1)
+    losses[rng.rand(T) < 0.05] = np.nan
+    offs, trials, vals = [0], [], []
+    for l in range(6):
+        if l % 2 == 0:   # in every trial, quantized (many ties)
+            tr = np.arange(T, dtype=np.int32)
+        else:            # conditional, with a trial of no position
+            tr = np.sort(rng.choice(T, size=T // 3, replace=False)).astype(np.int32)
+            tr[0] = -1
+        v = np.round(rng.uniform(0, 20, size=len(tr)))
+        trials.append(tr)
+        vals.append(v)
+        offs.append(offs[-1] + len(tr))
+    off = np.asarray(offs, dtype=np.int64)
+    tr_all, val_all = np.concatenate(trials), np.concatenate(vals)
+    obs_of = P._ObsOf(off, tr_all, val_all)
+    n_valid = int(np.count_nonzero(losses == losses))
+    n_below = P.n_below_of(n_valid, 0.25, 25)
+    labels = {0, 1, 3, 4}
+    below, o_off, order = P.reference_orders(losses, n_below, obs_of, labels)
+    above = (losses == losses) & (below == 0)
+    assert int(below.sum()) == n_below
+    for l in range(6):
+        got = order[o_off[l]:o_off[l + 1]]
+        if l not in labels:
+            assert len(got) == 0
+            continue
+        tr, v = trials[l], vals[l]
+        ok = (tr >= 0) & (tr < T)
+        keep = np.zeros(len(tr), dtype=bool)
+        keep[ok] = above[tr[ok]]
+        want = np.argsort(v[keep])
+        assert got.dtype == np.int32 and np.array_equal(got, want), l
