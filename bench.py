@@ -132,15 +132,9 @@ def parse():
     ap.add_argument('--value-only', type=int, default=None,
                     help='1/0: TPE_OPT_VALUE_ONLY (default: on, as tpe.suggest, except for '
                          'candidate shards)')
-    ap.add_argument('--defer', type=int, default=None,
-                    help='1/0: the dense labels\' round under the tie-order argsorts '
-                         '(posterior.DEFER_QUANT; default: the library\'s)')
     ap.add_argument('--aux-families', type=int, default=None,
                     help='1/0: the quantized and categorical labels on the second stream during sampled rounds '
                          '(TPE_OPT_AUX_FAMILIES; default: on, as tpe.suggest runs them, except candidate shards)')
-    ap.add_argument('--early-upload', type=int, default=None,
-                    help='1/0: the early argsorts start before the history upload, or after it '
-                         '(posterior.EARLY_BEFORE_UPLOAD)')
     ap.add_argument('--early-orders', type=int, default=None,
                     help='1/0: the known labels\' argsorts under the first build '
                          '(posterior.EARLY_ORDERS)')
@@ -187,6 +181,12 @@ def launch_ranks(args):
     env = dict(os.environ)
     env.setdefault('OMP_NUM_THREADS', '4')
     return subprocess.call(cmd, env=env, cwd=REPO)
+
+
+def distinct_gpus(rank_devices):
+    """The GPUs the ranks ran on, each counted once (a rank without one:
+    device -1, the CPU dry runs)."""
+    return len({d for d in rank_devices if d is not None and d >= 0})
 
 
 def check_world(args, dist, torch):
@@ -619,21 +619,18 @@ def main():
         if dist is not None:
             dist.barrier()
         if rank == 0:
-            print(json.dumps({'dry_run': True, 'n_gpus': world, 'rccl_world': world if dist else 1,
+            print(json.dumps({'dry_run': True, 'n_gpus': distinct_gpus(rank_devices),
+                              'rccl_world': world if dist else 1,
                               'dist_backend': args.dist_backend if dist else None,
                               'rank_devices': rank_devices}), flush=True)
         if dist is not None:
             dist.destroy_process_group()
         return
     from hyperopt_amd import posterior as P
-    if args.defer is not None:
-        P.DEFER_QUANT = bool(args.defer)
     if args.sort_threads is not None:
         P.SORT_THREADS = args.sort_threads
     if args.early_orders is not None:
         P.EARLY_ORDERS = bool(args.early_orders)
-    if args.early_upload is not None:
-        P.EARLY_BEFORE_UPLOAD = bool(args.early_upload)
     if args.overlap_min_dense is not None:
         from hyperopt_amd import workloads as W
         W.OVERLAP_MIN_DENSE = args.overlap_min_dense
@@ -1091,14 +1088,16 @@ def main():
                         'polynomial); valu_busy_measured is the PMC utilisation of the same kernel')
     line = {
         'metric': 'TPE candidate x component lpdf evals/sec (10k-trial history)',
-        'value': value, 'unit': 'evals/s', 'n_gpus': len(set(devs)) if devs else world,
+        # n_gpus: the distinct GPUs the ranks ran on (ranks sharing one card
+        # -- the gloo rehearsals -- count it once; rccl_world counts ranks)
+        'value': value, 'unit': 'evals/s', 'n_gpus': len(set(devs)) if devs else distinct_gpus(rank_devices),
         'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': dt / args.steps * 1e3,
         'higher_is_better': True, 'scaling': 'strong', 'vs_baseline': None,
         'dtype': ('f32+f64' if screened else args.precision),
         'data': 'synthetic (prior draws, seed 0)',
         'rccl_world': world, 'dist_backend': args.dist_backend if dist is not None else None,
-        'rank_devices': rank_devices, 'distinct_gpus': len(set(devs)) if devs else len(set(rank_devices)),
+        'rank_devices': rank_devices, 'distinct_gpus': len(set(devs)) if devs else distinct_gpus(rank_devices),
         'value_only': bool(value_only),
         'config': {'workload': workload_name(args, C),
                    'labels': L, 'history': args.trials,

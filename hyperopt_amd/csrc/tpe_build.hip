@@ -1895,7 +1895,7 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     HIPCHK(ctx, P.comps64.reserve(total));
     HIPCHK(ctx, P.comps32.reserve(total));
     HIPCHK(ctx, P.samp.reserve(samp_total));
-    HIPCHK(ctx, ctx->errflag.reserve(1));
+    HIPCHK(ctx, ctx->build_err.reserve(1));
     HIPCHK(ctx, B.ties.reserve(n_labels + 1));
     // the build's inputs -- supplied orders, subset labels, losses, below
     // set, mixture offsets, DLabels, and the zeroed tie report and error
@@ -1937,7 +1937,7 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
         put(mix.data(), (int64_t)mix.size() * (int64_t)sizeof(int64_t), B.mix_off.p);
         put(dl.data(), n_labels * (int64_t)sizeof(DLabel), P.labels.p);
     }
-    put(nullptr, sizeof(int32_t), ctx->errflag.p);
+    put(nullptr, sizeof(int32_t), ctx->build_err.p);
     {
         const int64_t head = ((int64_t)up.size() * (int64_t)sizeof(UpTask) + 255) / 256 * 256;
         int64_t o = head;
@@ -1973,18 +1973,18 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     }
     hipLaunchKernelGGL(k_partition, dim3(nl_run), dim3(kPartBlock), 0, st, B.specs.p, B.p_off.p, B.cnt.p,
                        B.p_trial.p, B.p_val.p, B.s_key.p, B.s_idx.p, B.below.p, B.losses.p, T,
-                       B.below_val.p, B.arank.p, B.keys.p, B.idx.p, B.counts.p, ctx->errflag.p, only_d);
+                       B.below_val.p, B.arank.p, B.keys.p, B.idx.p, B.counts.p, ctx->build_err.p, only_d);
     hipLaunchKernelGGL(k_parzen, dim3(nl_run, 2), dim3(kParzenBlock), 0, st, B.specs.p, B.cat_p.p,
                        B.p_off.p, B.counts.p, B.below_val.p, B.keys.p, B.keys.p, B.idx.p, B.mix_off.p,
                        prior_weight, lf, B.w.p, B.mu.p, B.sigma.p, B.kcount.p, B.scratch.p + total, order_off_d,
-                       order_d, B.ties.p, ctx->errflag.p, only_d);
+                       order_d, B.ties.p, ctx->build_err.p, only_d);
     hipLaunchKernelGGL(k_fold_terms, dim3((unsigned)((max_cap + kTermBlock - 1) / kTermBlock), nl_run, 2),
                        dim3(kTermBlock), 0, st, P.labels.p, B.kcount.p, B.mix_off.p, B.w.p, B.mu.p,
                        B.sigma.p, B.scratch.p, B.scratch.p + 2 * total, B.scratch.p + 3 * total, only_d);
     hipLaunchKernelGGL(k_fold, dim3(nl_run), dim3(kParzenBlock), 0, st, P.labels.p, B.kcount.p,
                        B.mix_off.p, B.w.p, B.mu.p, B.sigma.p, P.comps64.p, P.comps32.p, P.samp.p,
                        B.scratch.p, B.scratch.p + 2 * total, B.scratch.p + 3 * total, B.scratch.p + total,
-                       ctx->errflag.p, only_d);
+                       ctx->build_err.p, only_d);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipEventRecord(ctx->ev1, st));
     // the report -- DLabels, error flag, tie report -- packed by one launch
@@ -1994,7 +1994,7 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     HIPCHK(ctx, B.d_rep.reserve(rep_bytes));
     HIPCHK(ctx, B.h_rep.resize(rep_bytes));
     hipLaunchKernelGGL(k_build_report, dim3(1), dim3(kUpBlock), 0, st, (const uint32_t*)P.labels.p,
-                       (int32_t)(rep_dl / 4), ctx->errflag.p, B.ties.p, n_labels + 1, (uint32_t*)B.d_rep.p);
+                       (int32_t)(rep_dl / 4), ctx->build_err.p, B.ties.p, n_labels + 1, (uint32_t*)B.d_rep.p);
     HIPCHK(ctx, hipGetLastError());
     HIPCHK(ctx, hipMemcpyAsync(B.h_rep.data(), B.d_rep.p, rep_bytes, hipMemcpyDeviceToHost, st));
     if (!beside) {   // does the expansion index of the previous posterior still hold?

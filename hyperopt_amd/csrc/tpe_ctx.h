@@ -438,6 +438,11 @@ struct tpe_ctx {
     DevBuf<tpe_label_result> results;
     DevBuf<uint32_t> rounds;
     DevBuf<int32_t> errflag;
+    // the posterior builds' own error word (k_build_inputs zeroes it,
+    // k_partition / k_parzen / k_fold set bits, k_build_report packs it):
+    // a deferred rebuild still running on the second stream never shares a
+    // word with the round's kernels on the main one
+    DevBuf<int32_t> build_err;
     DevBuf<double> cand, out_lb, out_la;
     DevBuf<int32_t> one_group;
     DevBuf<int64_t> qj;

@@ -5015,6 +5015,7 @@ TPE_DEV void tpe1_ctx_destroy(tpe_ctx* c) {
     c->results.release();
     c->rounds.release();
     c->errflag.release();
+    c->build_err.release();
     c->cand.release();
     c->out_lb.release();
     c->out_la.release();
@@ -5247,6 +5248,7 @@ int tpe_suggest_batch_device(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds
 int tpe_merge_results_device(tpe_ctx* ctx, const tpe_label_result* d_parts, int32_t n_parts, int32_t n,
                              tpe_label_result* d_out) {
     if (!ctx || !d_parts || !d_out || n_parts <= 0 || n < 0) return TPE_ERR_ARG;
+    TPE_SETTLE(ctx);   // (a pending deferred rebuild first, as every entry point but a round)
     HIPCHK(ctx, hipSetDevice(ctx->device));
     if (n == 0) return TPE_OK;
     HIPCHK(ctx, ctx->errflag.reserve(1));
@@ -5370,6 +5372,7 @@ TPE_DEV int tpe1_arm_prepare(tpe_ctx* ctx, int64_t n_candidates, int32_t n_round
 
 TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
     if (!ctx) return TPE_ERR_ARG;
+    TPE_SETTLE(ctx);   // (the header's rule: a pending deferred rebuild's report first)
     switch (option) {
         case TPE_OPT_SCREEN: ctx->screen = value != 0; break;
         case TPE_OPT_SPLITK: ctx->splitk = value != 0; break;

@@ -276,6 +276,13 @@ int tpe_import_posterior(tpe_ctx* ctx, const void* d_blobs, int64_t blob_bytes, 
             const int32_t g = label_ids[li0 + i];
             DLabel d;
             std::memcpy(&d, base + h.off[S_LAB] + (size_t)i * sizeof(DLabel), sizeof(DLabel));
+            // each label must keep its space position as its Philox stream
+            // (a part built without TPE_HAS_STREAM numbers its labels from 0:
+            // its rounds would not be one context's rounds -- ADVICE r5)
+            if (d.stream != g)
+                return ctx->fail(TPE_ERR_ARG, "import: part " + std::to_string(p) + " label " + std::to_string(i) +
+                                                  " has Philox stream " + std::to_string(d.stream) +
+                                                  ", its space index is " + std::to_string(g));
             d.comp_b += nc;
             d.comp_a += nc;
             d.samp_off += ns;

@@ -186,9 +186,10 @@ class DescriptorExchange(object):
 
     def _buf(self, key, nbytes, dtype=None, device=None):
         import torch
-        dev = device or ('cuda' if self.device else 'cpu')
+        dev = torch.device(device or ('cuda' if self.device else 'cpu'))
         b = self._bufs.get(key)
-        if b is None or b.numel() < nbytes or b.device.type != dev:
+        if b is None or b.numel() < nbytes or b.device.type != dev.type or (
+                dev.index is not None and b.device.index != dev.index):
             b = self._bufs[key] = torch.empty(nbytes, dtype=dtype or torch.uint8, device=dev)
         return b[:nbytes]
 
@@ -201,7 +202,10 @@ class DescriptorExchange(object):
         import torch.distributed as dist
         eng = self.engine
         # the engine's side: its GPU (a stub engine of the CPU tests: host)
-        edev = 'cuda' if torch.cuda.is_available() else 'cpu'
+        # (the engine's own card, not torch's current device: a rank need not
+        # have called torch.cuda.set_device(engine.device) -- ADVICE r5)
+        edev = (torch.device('cuda', int(getattr(eng, 'device', 0))) if torch.cuda.is_available()
+                else torch.device('cpu'))
         sz = self._buf('size', 1, torch.int64)
         sz.fill_(eng.export_size())
         allsz = self._buf('sizes', self.world, torch.int64)
@@ -211,7 +215,7 @@ class DescriptorExchange(object):
         blob = self._buf('blob', slot, device=edev)
         eng.export_posterior(blob)
         blobs = self._buf('blobs', self.world * slot, device=edev)
-        if blob.device.type == ('cuda' if self.device else 'cpu'):
+        if blob.device.type == ('cuda' if self.device else 'cpu'):   # (the collective's side)
             dist.all_gather_into_tensor(blobs, blob, group=self.group)
         else:
             staged = self._buf('staged', self.world * slot)

@@ -340,7 +340,6 @@ def reference_orders(losses, n_below, obs_of, labels):
 
 
 EARLY_ORDERS = True   # known labels' argsorts started before the first build (build_reference_order)
-EARLY_BEFORE_UPLOAD = False  # ... or before the history upload (DeviceHistoryUploader.build): no gain, r4ay
 _order_exec = None
 
 
@@ -382,62 +381,10 @@ def _sort_pool():
 
 SUBSET_REBUILD = True   # the ordered rebuild restricted to the labels that need an order
 DEFER_REPORT = True     # round_call: that rebuild's report read after the round (Engine.rebuild_labels(defer=))
-DEFER_QUANT = False     # round_call: the dense labels' round under the argsorts (_run_deferred; measured slower)
-
-
-MASK_ALL = 31                      # TPE_OPT_MODE_MASK: every label family
-MASK_QUANT = (1 << 2) | (1 << 3)   # the quantized GMM1 / LGMM1 families
-
-
-def _run_deferred(eng, round_call, reference, rebuild, quant, t0):
-    """The round of a posterior whose quantized labels still wait for their
-    tie orders: the dense and categorical labels' round runs on a second
-    thread (the engine call releases the GIL) while this one computes the
-    orders (`reference`, numpy's argsorts: they release it too); then the
-    quantized labels are rebuilt (`rebuild`, which returns the build's tie
-    report) and their round runs.  The dense labels' mixtures are
-    bit-identical before and after that rebuild (continuous values carry no
-    ties), so the merged results are those of the one round on the ordered
-    posterior.  Returns (results or None, the rebuild's (n_below, ties)):
-    None when the rebuild reports a dependent label (a defensive path: a
-    rebuild over the same split leaves none; the caller then rebuilds in full
-    and runs the whole round)."""
-    eng.set_option('mode_mask', MASK_ALL & ~MASK_QUANT)
-    box = {}
-
-    def run():
-        try:
-            box['res'] = round_call()
-        except BaseException as e:   # re-raised on the caller's thread
-            box['err'] = e
-    th = threading.Thread(target=run, name='tpe-dense-round')
-    th.start()
-    try:
-        orders = reference()
-    finally:
-        th.join()
-        eng.set_option('mode_mask', MASK_ALL)
-    if 'err' in box:
-        raise box['err']
-    t0 = _phase('argsorts_under_round', t0)
-    built = rebuild(orders)
-    t0 = _phase('rebuild', t0)
-    if np.any(built[1][:-1]):
-        return None, built
-    eng.set_option('mode_mask', MASK_QUANT)
-    try:
-        res_q = round_call()
-    finally:
-        eng.set_option('mode_mask', MASK_ALL)
-    _phase('quant_round', t0)
-    res = box['res']
-    cols = sorted(quant)
-    res[..., cols] = res_q[..., cols]
-    return res, built
 
 
 def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of, known=(), prepare=None,
-                          overlap=True, round_call=None, quant=frozenset(), early=None):
+                          overlap=True, round_call=None, early=None):
     """_build_reference_order (below), waiting on the early argsorts' future
     whatever happens: its worker reads (and caches into) the uploader's
     observation lists, which a failed build must not leave it writing to
@@ -445,7 +392,7 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
     holder = {'early': early}
     try:
         return _build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of, known,
-                                      prepare, overlap, round_call, quant, holder)
+                                      prepare, overlap, round_call, holder)
     finally:
         if holder['early'] is not None:
             from concurrent.futures import wait
@@ -453,7 +400,7 @@ def build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of,
 
 
 def _build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of, known, prepare,
-                           overlap, round_call, quant, holder):
+                           overlap, round_call, holder):
     """Device build whose mixtures follow the reference's tie order
     (tpe.py:433, 637): the device reports which mixtures depend on the order
     of tied observations (or a tie of losses at the split), and only for
@@ -475,10 +422,8 @@ def _build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of
 
     round_call (optional): the coming round, a callable returning the
     engine's results; it then runs here and its results are returned as a
-    third value.  When the labels still needing an order after the first
-    build are all quantized (`quant`: their positions), the round of the
-    other labels runs while the host computes those orders (_run_deferred):
-    the argsorts leave the step's critical path.
+    third value (a subset rebuild's report is then read after the round:
+    DEFER_REPORT).
 
     holder['early'] (optional): reference_orders(losses, n_below, obs_of,
     known) already running (a future: DeviceHistoryUploader.build starts it
@@ -524,21 +469,6 @@ def _build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf, obs_of
         raise AssertionError('below mixture depends on a tie order (lf < gamma_cap?)')
     need = have | set(np.flatnonzero(ties[:-1] & 2).tolist())
     res = None
-    if (DEFER_QUANT and early is None and round_call is not None and need != have and not ties[-1]
-            and SUBSET_REBUILD
-            and need <= set(quant) and len(need) < obs_of.n_labels):
-        res, (nb, ties) = _run_deferred(
-            eng, round_call, lambda: reference_orders(losses, n_below, obs_of, need),
-            lambda o: eng.rebuild_labels(losses, n_valid, gamma, prior_weight, lf, o[1], o[2], need),
-            quant, t0)
-        if res is not None:
-            return nb, frozenset(need), res
-        # a dependent label the rebuild reported: the full ordered build
-        # (with it) and the whole round below
-        need |= set(np.flatnonzero(ties[:-1] & 2).tolist())
-        have = set()
-        ties = np.ones_like(ties)
-        t0 = time.perf_counter()
     deferred = False
     if early is not None:
         orders = early.result()   # (waited for even when unused: obs_of is not shared)
@@ -636,10 +566,13 @@ class DeviceHistoryUploader(object):
         results): results of round_call (the coming round: see
         build_reference_order), None without one."""
         tids, losses, n_valid, cols, owner = view
-        if labels is not self._labels_obj or streams is not self._streams_obj:
+        names_now = tuple(n for n, _, _ in labels)
+        if (labels is not self._labels_obj or streams is not self._streams_obj or
+                names_now != self._names_t):
             # (the label key of a caller that passes the same list every
-            # step -- FminLoop -- is built once)
-            self._labels_obj, self._streams_obj = labels, streams
+            # step -- FminLoop -- is built once; the names tuple catches a
+            # list changed in place -- ADVICE r5)
+            self._labels_obj, self._streams_obj, self._names_t = labels, streams, names_now
             self._label_key = (tuple((n, k) for n, k, _ in labels) +
                                (tuple(streams) if streams is not None else (),))
             self._names = [n for n, _, _ in labels]
@@ -663,8 +596,6 @@ class DeviceHistoryUploader(object):
             self.pos_parts = [[] for _ in labels]    # what the device holds, per label
             self.val_parts = [[] for _ in labels]
             self.tie_labels = frozenset()
-            self.quant = frozenset(i for i in range(len(labels))
-                                   if specs[i]['flags'] & L.TPE_HAS_Q and specs[i]['kind'] != L.TPE_CATEGORICAL)
         t0 = time.perf_counter()
         counts = lens
         # the new observations of every label, transformed and placed in one
@@ -696,21 +627,9 @@ class DeviceHistoryUploader(object):
                     self.pos_parts[i].append(trial[o:o + m])
                     self.val_parts[i].append(vals[o:o + m])
                     o += m
-        # the previous step's order-dependent labels: their argsorts start
-        # now, under the upload as well as the first build and the index
         # (a failed upload leaves this uploader invalid: the next call resets)
-        early = None
-        if prepare and overlap and self.tie_labels and EARLY_ORDERS and EARLY_BEFORE_UPLOAD:
-            early = _order_thread().submit(reference_orders, losses, n_below_of(n_valid, gamma),
-                                           self._obs_of(len(labels)), self.tie_labels)
         if ni_l:
-            try:
-                eng.history_append(np.asarray(n_new, dtype=np.int64), trial, vals)
-            except BaseException:
-                if early is not None:   # (its worker reads pos_parts / val_parts)
-                    from concurrent.futures import wait
-                    wait([early])
-                raise
+            eng.history_append(np.asarray(n_new, dtype=np.int64), trial, vals)
         self.prev_counts = counts                  # committed only after the append
         self.key = (key[0], eng.history_generation)
         self.owner = weakref.ref(owner)
@@ -719,8 +638,7 @@ class DeviceHistoryUploader(object):
         _phase('append', t0)
         out = build_reference_order(eng, losses, n_valid, gamma, prior_weight, lf,
                                     self._obs_of(len(labels)), self.tie_labels,
-                                    prepare=prepare, overlap=overlap, round_call=round_call,
-                                    quant=self.quant, early=early)
+                                    prepare=prepare, overlap=overlap, round_call=round_call)
         self.tie_labels = out[1]
         return out[0], (out[2] if round_call is not None else None)
 
@@ -736,10 +654,9 @@ class DeviceHistoryUploader(object):
         return obs_of
 
     prev_counts = ()
-    _labels_obj = _streams_obj = None
+    _labels_obj = _streams_obj = _names_t = None
     pos_parts = val_parts = ()
     tie_labels = frozenset()
-    quant = frozenset()
     n_trials = 0
     last_tid = None
     trs = ()

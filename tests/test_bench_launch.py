@@ -34,14 +34,18 @@ def test_gpus2_starts_two_ranks_gloo():
     assert r.returncode == 0, r.stderr[-2000:]
     d = _line(r.stdout)
     assert d['dry_run'] is True
-    assert d['n_gpus'] == 2 and d['rccl_world'] == 2 and d['dist_backend'] == 'gloo'
+    assert d['rccl_world'] == 2 and d['dist_backend'] == 'gloo'
     assert len(d['rank_devices']) == 2
+    # n_gpus counts distinct cards (none here: gloo ranks on the CPU)
+    assert d['n_gpus'] == len({x for x in d['rank_devices'] if x >= 0})
 
 
 def test_gpus3_starts_three_ranks_gloo():
     r = _run(['--gpus', '3', '--dist-backend', 'gloo', '--dry-run'])
     assert r.returncode == 0, r.stderr[-2000:]
-    assert _line(r.stdout)['n_gpus'] == 3
+    d = _line(r.stdout)
+    assert d['rccl_world'] == 3 and len(d['rank_devices']) == 3
+    assert d['n_gpus'] == len({x for x in d['rank_devices'] if x >= 0})
 
 
 def test_gpus2_without_enough_gpus_is_refused():

@@ -43,13 +43,13 @@ def test_fmin_loop_rounds_equal_fresh_engine():
 
 
 @pytest.mark.parametrize('C, n_rounds, labels', [(1 << 20, 1, 32), (24, 512, 64)])
-def test_deferred_quantized_round_equals_sequential(C, n_rounds, labels):
-    """round_call (tpe.suggest's and bench.py's step): the dense and
-    categorical labels' round runs on a second thread while the host
-    computes the quantized labels' numpy tie orders, then those labels are
-    rebuilt and their round runs (TPE_OPT_MODE_MASK) -- bytewise the results
-    of the sequential step (ordered rebuild, then the whole round), tile
-    rounds (config 3) and batched packed rounds (config 5) alike."""
+def test_round_call_step_equals_sequential(C, n_rounds, labels):
+    """round_call (tpe.suggest's and bench.py's step): the ordered subset
+    rebuild's report deferred into the round (DEFER_REPORT: the dense labels'
+    kernels queued first, the quantized / categorical families after the
+    rebuild on the second stream) -- bytewise the results of the sequential
+    step (ordered rebuild, then the whole round), tile rounds (config 3) and
+    batched packed rounds (config 5) alike."""
     from hyperopt_amd import posterior as P
     from hyperopt_amd.engine import Engine
     from hyperopt_amd.workloads import FminLoop, mixed_history
@@ -59,8 +59,6 @@ def test_deferred_quantized_round_equals_sequential(C, n_rounds, labels):
     la.advance(a, 10000)
     lb.advance(b, 10000)
     P.PHASES = {}
-    defer, P.DEFER_QUANT = P.DEFER_QUANT, True     # (off by default: measured slower)
-    early, P.EARLY_ORDERS = P.EARLY_ORDERS, False   # (the deferred path computes its own)
     try:
         for i in range(3):
             n = 10001 + i
@@ -80,11 +78,8 @@ def test_deferred_quantized_round_equals_sequential(C, n_rounds, labels):
             assert a.last_screen() == b.last_screen()
             ms_a, ms_b = a.last_mode_stats(), b.last_mode_stats()
             assert {k: v[1] for k, v in ms_a.items()} == {k: v[1] for k, v in ms_b.items()}
-        assert P.PHASES.get('quant_round', [0])[0] == 3      # the deferred path ran every step
     finally:
         P.PHASES = None
-        P.DEFER_QUANT = defer
-        P.EARLY_ORDERS = early
         a.close()
         b.close()
 

@@ -185,6 +185,25 @@ def test_build_config3_and_round_matches_host_fold(eng):
         np.testing.assert_allclose(res_dev[f], res_host[f], rtol=1e-12, atol=1e-12)
 
 
+def test_build_config5_scale_bit_exact(eng):
+    """Config-5-sized history: 128 labels of config 3's
+    kind pattern, N = 50k trials, losses rounded to one decimal so that ties
+    straddle the split -- the sliced k_split (past 16k trials: slices of 16 Ki
+    losses, k_split_merge) and every label's mixtures bit-identical to the
+    oracle's (numpy's tie orders supplied where the device reports them)."""
+    kinds = [('uniform', dict(low=-5.0, high=5.0)), ('loguniform', dict(low=-5.0, high=2.0)),
+             ('quniform', dict(low=0.0, high=100.0, q=1.0)), ('normal', dict(mu=0.0, sigma=3.0)),
+             ('randint', dict(upper=5))]
+    labels = [('x%d' % i, kinds[i % 5][0], kinds[i % 5][1]) for i in range(128)]
+    hist = make_history(labels, 50000, seed=5, active_frac=0.8, loss_round=1)
+    nb = _build(eng, hist)
+    assert nb == 25
+    srt = np.sort(hist.losses)
+    assert srt[nb - 1] == srt[nb]                # a loss tie straddles the split
+    _check_bit_exact(eng, hist, oracle_mixtures(hist))
+    assert eng.tie_labels                        # numpy's orders were needed and supplied
+
+
 def test_build_errors(eng):
     from hyperopt_amd.engine import SPEC_DTYPE
     hist = make_history(ALL_KINDS[:1], 50, seed=1)
