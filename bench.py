@@ -114,9 +114,6 @@ def parse():
                          'least one label), candidate shards (every label, C/N candidates each) or '
                          'descriptors (label shards build the posteriors and index, one all-gather '
                          'shares them, candidate shards score: parallel.DescriptorExchange)')
-    ap.add_argument('--hot32', type=int, default=None,
-                    help='TPE_OPT_HOT32: the prefilter\'s fp32 draw (1) or the fp64 draw kernel (0, the '
-                         'library default: faster on gfx950)')
     ap.add_argument('--bx-split', type=int, default=None,
                     help='TPE_OPT_BX_SPLIT: workgroups per 64-bin block of the index tables (0 = auto)')
     ap.add_argument('--no-defer-report', action='store_true',
@@ -832,8 +829,6 @@ def main():
     aux_families = (args.aux_families if args.aux_families is not None
                     else int(not (dist is not None and not by_label and args.config != 5)))
     eng.set_option('aux_families', aux_families)
-    if args.hot32 is not None:
-        eng.set_option('hot32', args.hot32)
     if args.bx_split is not None:
         eng.set_option('bx_split', args.bx_split)
     if args.no_defer_report:
@@ -1002,7 +997,7 @@ def main():
         # the expansion screen (k_screen_hot); the bracket holds both
         dom_ms = scr[2]
         kprec = 'f64'
-        kname = 'k_hot_bx32<' if args.hot32 else 'k_hot_bx<'
+        kname = 'k_hot_bx<'
         kdesc = 'k_hot_bx + k_screen_hot (hot-bin prefilter of the expansion screen: every candidate ' \
                 'drawn and bounded by its sub-bin\'s score interval, the 0.5 % that can still win ' \
                 'scored by the expansion screen), GMM1+LGMM1 labels'

@@ -27,7 +27,6 @@ SOURCES = [os.path.join(HERE, 'csrc', 'tpe_engine.hip'),
 DEPS = SOURCES + [os.path.join(HERE, 'csrc', 'tpe_device.h'),
                   os.path.join(HERE, 'csrc', 'tpe_ctx.h'),
                   os.path.join(HERE, 'csrc', 'tpe_exp_table.h'),
-                  os.path.join(HERE, 'csrc', 'tpe_bm_table.h'),
                   os.path.join(REPO, 'include', 'hyperopt_tpe.h')]
 TARGET = os.path.join(HERE, 'libhyperopt_tpe.so')
 

@@ -56,7 +56,6 @@ TPE_OPT_VALUE_ONLY = 16
 TPE_OPT_RESCORE_CAP = 17
 TPE_OPT_MODE_MASK = 18
 TPE_OPT_AUX_FAMILIES = 19
-TPE_OPT_HOT32 = 20
 TPE_OPT_BX_SPLIT = 21
 TPE_OPT_BX_T = 22
 TPE_OPT_PK_SLICED = 23

@@ -1320,44 +1320,23 @@ __global__ __launch_bounds__(kParzenBlock) void k_fold(
             (side ? d.amax_a : d.amax_b) = (float)amax;
         }
     }
-    // sampling records of the below mixture: cumulative normalised weights,
-    // summed in order by one thread -- over an LDS copy of the weights when
-    // they fit (the serial walk then costs LDS, not global, latency)
-    __shared__ double wst[kParzenBlock];
-    const bool staged = Kb <= kParzenBlock;
-    if (staged) {
-        if (tid < Kb) wst[tid] = w[ob + tid];
-        __syncthreads();
-    }
-    const double* wb = staged ? wst : w + ob;
+    // sampling records of the below mixture: the component, its raw weight,
+    // then the shared fold (cumulative w m, truncation terms: samp_fold_block)
     if (tid == 0) {
-        double tot = 0.0;
-        for (int64_t k = 0; k < Kb; ++k) tot += wb[k];
-        if (!(tot > 0)) {
-            atomicOr(err, 4);
-            tot = 1.0;
-        }
-        double run = 0.0;
-        for (int64_t k = 0; k < Kb; ++k) {
-            run += wb[k];
-            const double cdf = (k == Kb - 1) ? 1.0 : run / tot;
-            if (staged) wst[k] = cdf;
-            else samp[d.samp_off + k].cdf = cdf;
-        }
         d.nb = (int32_t)Kb;
         d.na = (int32_t)Ka;
         d.ns = (int32_t)Kb;
         labels[l] = d;
     }
-    __syncthreads();
     for (int64_t k = tid; k < Kb; k += kParzenBlock) {
-        SampRec r;
-        r.cdf = staged ? wst[k] : samp[d.samp_off + k].cdf;
+        SampRec r{};
         r.mu = d.mode == CAT ? 0.0 : mu[ob + k];
         r.sigma = d.mode == CAT ? 0.0 : sigma[ob + k];
-        r.pad = 0.0;
+        r.wd = w[ob + k];
         samp[d.samp_off + k] = r;
     }
+    __syncthreads();
+    if (!samp_fold_block(d, samp + d.samp_off, (int)Kb)) atomicOr(err, 4);
 }
 
 struct CopyArgs {

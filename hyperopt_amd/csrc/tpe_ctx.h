@@ -474,8 +474,10 @@ struct tpe_ctx {
     bool zw_pending = false;             //   its windows launched this round (built iff its plan was not empty)
     double hot_cap_div = 16.0;           // hot lists hold n / hot_cap_div per cell (shrinks on overflow)
     DevBuf<double> hot_x;                // per cell: listed candidates' x (the fp64 draw kernel)
-    DevBuf<int32_t> hot_a;               //   or their accepted attempts (k_hot_bx32: re-drawn in fp64)
-    int32_t hot32 = 0;                   // TPE_OPT_HOT32: the prefilter draws in fp32 (k_hot_bx32; 2: bounds x 4096, tests)
+    DevBuf<uint32_t> rs_done;            // the round tail's last-workgroup counters (zeroed by its fills)
+    bool dense_one = false;              // this round's dense rows hold their winner in slot 0 only (k_reduce)
+    DevBuf<int32_t> hot_pc;              // per sub-bin word: the label's set bits before it (k_hot_prefix)
+    DevBuf<uint32_t> hot_ucell;          // per (dense label, sampling component): its u-cells (k_hot_ucells)
     int32_t bx_split = 0;                // TPE_OPT_BX_SPLIT (0: auto)
     int64_t pk_sliced = 8192;            // TPE_OPT_PK_SLICED (0: never sliced)
     int32_t bx_t_force = 0;              // TPE_OPT_BX_T (0: auto)

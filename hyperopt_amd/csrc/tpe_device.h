@@ -11,7 +11,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "tpe_bm_table.h"
 #include "tpe_exp_table.h"
 
 namespace tpe {
@@ -50,9 +49,18 @@ struct alignas(4 * sizeof(T)) Comp {
     T mu, a, c, w;
 };
 
-// Sampling record of the below mixture: cumulative weight, raw mu and sigma.
-struct alignas(32) SampRec {
-    double cdf, mu, sigma, pad;
+// Sampling record of one component of the below mixture: the pick's
+// cumulative weight and the component's inverse-CDF draw of its normal
+// truncated to [low, high) -- folded on the device for every posterior
+// (samp_fold_block: host-uploaded and device-built posteriors draw the same
+// bits).
+struct alignas(64) SampRec {
+    double cdf;         // cumulative normalised w_k m_k (the component pick)
+    double mu, sigma;   // the component
+    double wd;          // w_k / sum_i w_i m_i: the truncated mixture's density is sum_k wd_k phi_k(x) in [low, high)
+    double ssg;         // sigma, or -sigma when the interval is mirrored (the mean at or below low)
+    double p0, q0;      // Phi(a'), Phi(-b'): the normal's mass below / above the (mirrored) interval [a', b')
+    double m;           // the interval's mass (0: never picked)
 };
 
 struct Partial {
@@ -139,10 +147,94 @@ __device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
     return c;
 }
 
-// 32-bit uniform in [2^-32, 1] (never 0: Box-Muller takes its log): 1 -
-// y 2^-32, exact.  (The radius sqrt(-2 log u) then reaches 6.66 sigma: the
-// draws are normals truncated there, a probability of 2.7e-11 per draw.)
-__device__ __forceinline__ double u01_open0(uint32_t y) { return 1.0 - (double)y * 0x1.0p-32; }
+// ------------------------------------------------ the inverse-CDF draw ----
+// AS241 (Wichura 1988, "PPND16"): the lower-tail normal quantile
+// z = Phi^-1(t) for t in (0, 1/2] -- rational approximations in three
+// regions, ~7e-16 relative against 40-digit arithmetic over uniform t and
+// t down to 1e-300 (checked when this was written).  One function for every
+// kernel, so every kernel draws the same bits.
+__device__ __forceinline__ double ndtri_lower(double t) {
+    const double q = t - 0.5;   // (exact: t in [1/4, 1/2] by Sterbenz, the product below rounds once)
+    if (q >= -0.425) {
+        const double r = 0.180625 - q * q;
+        const double num =
+            fma(fma(fma(fma(fma(fma(fma(2.5090809287301226727e+3, r, 3.3430575583588128105e+4), r,
+                                    6.7265770927008700853e+4), r, 4.5921953931549871457e+4), r,
+                            1.3731693765509461125e+4), r, 1.9715909503065514427e+3), r,
+                    1.3314166789178437745e+2), r, 3.3871328727963666080e0);
+        const double den =
+            fma(fma(fma(fma(fma(fma(fma(5.2264952788528545610e+3, r, 2.8729085735721942674e+4), r,
+                                    3.9307895800092710610e+4), r, 2.1213794301586595867e+4), r,
+                            5.3941960214247511077e+3), r, 6.8718700749205790830e+2), r,
+                    4.2313330701600911252e+1), r, 1.0);
+        return q * num / den;
+    }
+    double r = sqrt(-flog(t));
+    if (r <= 5.0) {
+        r -= 1.6;
+        const double num =
+            fma(fma(fma(fma(fma(fma(fma(7.74545014278341407640e-4, r, 2.27238449892691845833e-2), r,
+                                    2.41780725177450611770e-1), r, 1.27045825245236838258e0), r,
+                            3.64784832476320460504e0), r, 5.76949722146069140550e0), r,
+                    4.63033784615654529590e0), r, 1.42343711074968357734e0);
+        const double den =
+            fma(fma(fma(fma(fma(fma(fma(1.05075007164441684324e-9, r, 5.47593808499534494600e-4), r,
+                                    1.51986665636164571966e-2), r, 1.48103976427480074590e-1), r,
+                            6.89767334985100004550e-1), r, 1.67638483018380384940e0), r,
+                    2.05319162663775882187e0), r, 1.0);
+        return -(num / den);
+    }
+    r -= 5.0;
+    const double num =
+        fma(fma(fma(fma(fma(fma(fma(2.01033439929228813265e-7, r, 2.71155556874348757815e-5), r,
+                                1.24266094738807843860e-3), r, 2.65321895265761230930e-2), r,
+                        2.96560571828504891230e-1), r, 1.78482653991729133580e0), r,
+                5.46378491116411436990e0), r, 6.65790464350110377720e0);
+    const double den =
+        fma(fma(fma(fma(fma(fma(fma(2.04426310338993978564e-15, r, 1.42151175831644588870e-7), r,
+                                1.84631831751005468180e-5), r, 7.86869131145613259100e-4), r,
+                        1.48753612908506148525e-2), r, 1.36929880922735805310e-1), r,
+                5.99832206555887937690e-1), r, 1.0);
+    return -(num / den);
+}
+
+// The component data a draw needs (SampRec's fields, or a workgroup's LDS
+// copy): mean, signed sigma, the interval's cut masses and mass, and the
+// pick's threshold interval [tlo, thi) of the component (integers,
+// thr = ceil(cdf 2^32)) with iw = 1 / (thi - tlo).
+struct DrawComp {
+    double mu, ssg, p0, q0, m, iw;
+    uint64_t tlo, thi;
+};
+
+// One candidate from its two Philox words: wp picked the component (its
+// threshold interval holds wp), wu is the uniform.
+//   v = (wu + r) 2^-32 in (0, 1): r = (wp - tlo + 1/2) / (thi - tlo) is wp's
+//     position inside the picked component's interval -- uniform and
+//     independent of the component and of wu (~log2(w 2^32) more bits, so
+//     the tails reach ~9 sigma); 1 - v is formed the same way from the other
+//     end, exactly;
+//   p = p0 + m v and q = q0 + m (1 - v): the normal's CDF at the draw and its
+//     complement, each accurate where it is small;
+//   z = Phi^-1(p) (lower tail of p or of q), x = mu + ssg z;
+//   bounded labels: x clamped into [low, high) -- a rounding at an end of
+//     the interval, ~1e-16 of the draws.
+// A component of zero mass (m = 0: the mixture's truncated mass is zero,
+// k_samp_fold) returns NaN -- the callers raise the sampler error.
+__device__ __forceinline__ double icdf_draw(const DLabel& L, const DrawComp& c, uint32_t wp, uint32_t wu) {
+    const double r = ((double)(wp - (uint32_t)c.tlo) + 0.5) * c.iw;
+    const double rb = ((double)((uint32_t)(c.thi - 1 - c.tlo) - (wp - (uint32_t)c.tlo)) + 0.5) * c.iw;
+    const double v = ((double)wu + r) * 0x1.0p-32;
+    const double vb = ((double)(0xFFFFFFFFu - wu) + rb) * 0x1.0p-32;
+    const double p = fma(c.m, v, c.p0), q = fma(c.m, vb, c.q0);
+    const double z = p <= 0.5 ? ndtri_lower(p) : -ndtri_lower(q);
+    double x = fma(c.ssg, z, c.mu);
+    if ((L.flags & 3) == 3) {
+        x = x < L.low ? L.low : x;
+        x = x >= L.high ? nextafter(L.high, -__builtin_inf()) : x;
+    }
+    return c.m > 0.0 ? x : __builtin_nan("");
+}
 
 // first k with cdf[k] > u (cdf[n-1] == 1 exactly, u < 1).
 __device__ __forceinline__ int cdf_search(const SampRec* __restrict__ s, int n, double u) {
@@ -154,43 +246,43 @@ __device__ __forceinline__ int cdf_search(const SampRec* __restrict__ s, int n, 
     return lo;
 }
 
-// One attempt of the below mixture's draw for global candidate g: component
-// ~ weights (inverse cdf), x = mu + sigma N(0, 1) by Box-Muller, before any
-// truncation test.  The counter is (g, attempt, label stream, round).
-constexpr uint32_t kMaxAttempts = 1u << 16;
+// The pick's integer threshold of cumulative weight c: ceil(c 2^32) (exact: a
+// power-of-two scaling, c in [0, 1]); cdf[k] <= u = w 2^-32  <=>  thr[k] <= w
+__device__ __forceinline__ uint64_t pick_thr(double c) { return (uint64_t)ceil(c * 0x1.0p32); }
 
-// Component lookup of the draw: the first k with cdf[k] > u.  SampGlobal
+// Component lookup of the draw: the first k with thr[k] > w.  SampGlobal
 // searches the records in global memory; SampShared (a workgroup's copy in
 // LDS, stage_samp, padded to 64 entries) starts from a 256-cell guide
-// (gd[j] = the first k with cdf[k] > j / 256, j = the top 8 bits of u's
-// 32-bit word) and takes at most `steps` more comparisons -- the most
-// cumulative weights any cell holds, 1 for mixtures without weights below
-// 1/256 -- else a branch-free lower bound over all 64; the categorical tile
-// kernel walks the 64-entry guide table (guide[j] = the first k with
-// cdf[k] > j / 64).  All return the same component.
-// The uniform is the Philox word w (u = w 2^-32, exact): SampShared
-// compares w with integer thresholds thr[k] = ceil(cdf[k] 2^32), and
-// cdf[k] <= u  <=>  cdf[k] 2^32 <= w  <=>  thr[k] <= w (w an integer, the
-// scaling exact) -- the same component without the conversion to double.
+// (gd[j] = the first k with cdf[k] > j / 256, j = the top 8 bits of w) and
+// takes at most `steps` more comparisons -- the most cumulative weights any
+// cell holds, 1 for mixtures without weights below 1/256 -- else a
+// branch-free lower bound over all 64; the categorical tile kernel walks
+// the 64-entry guide table (guide[j] = the first k with cdf[k] > j / 64).
+// All return the same component and the same DrawComp bits.
 struct SampGlobal {
     const SampRec* __restrict__ s;
     int ns;
-    __device__ __forceinline__ const double* cos_tab() const { return kCosSinTab; }
-    __device__ __forceinline__ const double* log_tab() const { return kLogTab; }
-    __device__ __forceinline__ void pick(uint32_t w, double& mu, double& sg) const {
-        const double u = (double)w * 0x1.0p-32;
-        const int k = cdf_search(s, ns, u);
-        mu = s[k].mu;
-        sg = s[k].sigma;
+    __device__ __forceinline__ DrawComp comp(uint32_t w) const {
+        const int k = cdf_search(s, ns, (double)w * 0x1.0p-32);
+        const SampRec r = s[k];
+        DrawComp c;
+        c.mu = r.mu;
+        c.ssg = r.ssg;
+        c.p0 = r.p0;
+        c.q0 = r.q0;
+        c.m = r.m;
+        c.tlo = k ? pick_thr(s[k - 1].cdf) : 0;
+        c.thi = pick_thr(r.cdf);
+        c.iw = 1.0 / (double)(c.thi - c.tlo);
+        return c;
     }
 };
 
 constexpr int kSampLds = 64;     // below components staged in LDS (K_b <= 26 in practice)
 constexpr int kGuideSteps = 3;   // guided picks take at most this many comparisons
 struct SampLds {
-    double cdf[kSampLds], mu[kSampLds], sg[kSampLds];
+    double cdf[kSampLds], mu[kSampLds], ssg[kSampLds], p0[kSampLds], q0[kSampLds], m[kSampLds], iw[kSampLds];
     uint64_t thr[kSampLds];   // ceil(cdf 2^32)
-    float mu32[kSampLds], sg32[kSampLds];   // fp32 copies (k_hot_bx's fp32 draw)
     uint8_t guide[64];
     uint8_t gd[256];
     int steps;
@@ -198,14 +290,7 @@ struct SampLds {
 
 struct SampShared {
     const SampLds* __restrict__ t;
-    // Box-Muller's tables: the constant ones, or a workgroup's LDS copies
-    // (stage_bm_tables: a per-lane gather from LDS instead of through the
-    // vector memory path)
-    const double* cs = kCosSinTab;
-    const double* lg = kLogTab;
     int steps = -1;   // t->steps read once by the caller (-1: read per pick)
-    __device__ __forceinline__ const double* cos_tab() const { return cs; }
-    __device__ __forceinline__ const double* log_tab() const { return lg; }
     __device__ __forceinline__ int pick_index(uint32_t w) const {
         // (steps is the same for the whole workgroup: a scalar branch)
         const int st = steps >= 0 ? steps : __builtin_amdgcn_readfirstlane(t->steps);
@@ -222,11 +307,19 @@ struct SampShared {
         }
         return k;
     }
-    __device__ __forceinline__ void pick(uint32_t w, double& mu, double& sg) const {
-        const int k = pick_index(w);
-        mu = t->mu[k];
-        sg = t->sg[k];
+    __device__ __forceinline__ DrawComp comp_at(int k) const {
+        DrawComp c;
+        c.mu = t->mu[k];
+        c.ssg = t->ssg[k];
+        c.p0 = t->p0[k];
+        c.q0 = t->q0[k];
+        c.m = t->m[k];
+        c.iw = t->iw[k];
+        c.tlo = k ? t->thr[k - 1] : 0;
+        c.thi = t->thr[k];
+        return c;
     }
+    __device__ __forceinline__ DrawComp comp(uint32_t w) const { return comp_at(pick_index(w)); }
 };
 
 // a workgroup's LDS copy of label L's below sampling records (false, and
@@ -236,19 +329,24 @@ __device__ __forceinline__ bool stage_samp(const DLabel& L, const SampRec* __res
     for (int k = threadIdx.x; k < kSampLds; k += blockDim.x) {
         if (k < L.ns) {
             const SampRec r = samp[L.samp_off + k];
+            const uint64_t thi = pick_thr(r.cdf), tlo = k ? pick_thr(samp[L.samp_off + k - 1].cdf) : 0;
             t->cdf[k] = r.cdf;
-            t->thr[k] = (uint64_t)ceil(r.cdf * 0x1.0p32);   // (exact: a power-of-two scaling, cdf in [0, 1])
+            t->thr[k] = thi;
             t->mu[k] = r.mu;
-            t->sg[k] = r.sigma;
-            t->mu32[k] = (float)r.mu;
-            t->sg32[k] = (float)r.sigma;
+            t->ssg[k] = r.ssg;
+            t->p0[k] = r.p0;
+            t->q0[k] = r.q0;
+            t->m[k] = r.m;
+            t->iw[k] = 1.0 / (double)(thi - tlo);   // (SampGlobal::comp's expression: the same bits)
         } else {   // padding: never picked (u < 1 <= cdf[ns - 1])
             t->cdf[k] = 2.0;
             t->thr[k] = 1ull << 33;
             t->mu[k] = 0.0;
-            t->sg[k] = 0.0;
-            t->mu32[k] = 0.0f;
-            t->sg32[k] = 0.0f;
+            t->ssg[k] = 0.0;
+            t->p0[k] = 0.0;
+            t->q0[k] = 0.0;
+            t->m[k] = 0.0;
+            t->iw[k] = 0.0;
         }
     }
     if (threadIdx.x == 0) t->steps = 0;
@@ -276,151 +374,134 @@ __device__ __forceinline__ bool stage_samp(const DLabel& L, const SampRec* __res
     return true;
 }
 
-// a workgroup's LDS copies of Box-Muller's cos/sin and log tables (every
-// thread must call it; a barrier before use -- stage_samp's serves)
-constexpr int kCosTabLen = 2 * (1 << kCosTabBits), kLogTabLen = 2 * (1 << kLogTabBits);
-__device__ __forceinline__ void stage_bm_tables(double* cs, double* lg) {
-    for (int i = threadIdx.x; i < kCosTabLen; i += blockDim.x) cs[i] = kCosSinTab[i];
-    for (int i = threadIdx.x; i < kLogTabLen; i += blockDim.x) lg[i] = kLogTab[i];
-}
+// Phi(x) = erfc(-x / sqrt 2) / 2 (accurate in both tails)
+__device__ __forceinline__ double ncdf(double x) { return 0.5 * erfc(-x * 0.70710678118654752440); }
 
-// (cos, sin)(2 pi w / 2^32): the top 8 bits' angle a from a 256-entry
-// table (tpe_bm_table.h), the residual t = 2 pi (w mod 2^24) / 2^32 <
-// 2 pi / 256 by its Taylor polynomials (t^10 / 10! < 1e-22), then
-// cos(a + t) = cos a cos t - sin a sin t, sin(a + t) = sin a cos t + cos a
-// sin t -- ~17 VALU operations and one 16-byte load instead of the library
-// sincospi's ~80.
-__device__ __forceinline__ void sincos_turn32(uint32_t w, double& c, double& s,
-                                              const double* __restrict__ tab) {
-    const int k = (int)(w >> 24);
-    const double t = (double)(w & 0xFFFFFFu) * (6.283185307179586 * 0x1.0p-32);
-    const double t2 = t * t;
-    const double ct = fma(fma(fma(fma(1.0 / 40320.0, t2, -1.0 / 720.0), t2, 1.0 / 24.0), t2, -0.5), t2, 1.0);
-    const double st = t * fma(fma(fma(-1.0 / 5040.0, t2, 1.0 / 120.0), t2, -1.0 / 6.0), t2, 1.0);
-    const double ca = tab[2 * k], sa = tab[2 * k + 1];
-    c = fma(ca, ct, -sa * st);
-    s = fma(sa, ct, ca * st);
-}
-
-// -log(u) for the Box-Muller uniform u in [2^-52, 1]: u = 2^e m, m in [1,
-// 2); the 7-bit interval j of m gives a 24-bit reciprocal inv ~ 1 / c_j
-// and log(1 / inv) (tpe_bm_table.h), r = m inv - 1 (|r| < 2^-8) and log1p(r)
-// by its degree-7 Taylor polynomial (r^8 / 8 < 2^-67) -- ~10 fp64
-// operations instead of flog's ~28 (its division); ~1 ulp.  (Only the
-// draw's radius uses it: every log of a candidate or a sum stays flog.)
-__device__ __forceinline__ double bm_neglog(double u, const double* __restrict__ tab) {
-    const uint64_t b = __builtin_bit_cast(uint64_t, u);
-    const int e = (int)(b >> 52) - 1023;
-    const int j = (int)((b >> 45) & 127u);
-    const double m = __builtin_bit_cast(double, (b & 0xFFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
-    const double r = fma(m, tab[2 * j], -1.0);
-    double q = fma(1.0 / 7.0, r, -1.0 / 6.0);
-    q = fma(q, r, 0.2);
-    q = fma(q, r, -0.25);
-    q = fma(q, r, 1.0 / 3.0);
-    q = fma(q, r, -0.5);
-    q = fma(q, r, 1.0);
-    return -fma((double)e, 6.93147180559945286e-01, fma(r, q, tab[2 * j + 1]));
-}
-
-// Box-Muller's radius sqrt(-2 log u) from word y (lt: kLogTab or its LDS copy)
-__device__ __forceinline__ double bm_radius(uint32_t y, const double* __restrict__ lt) {
-    return __builtin_amdgcn_sqrt(fmax(0.0, 2.0 * bm_neglog(u01_open0(y), lt)));
-}
-
-// ---------------------------------------------------- fp32 Box-Muller ----
-// The same radius and angle in fp32 with the hardware transcendentals
-// (v_log_f32 = log2, v_sqrt_f32, v_sin_f32 / v_cos_f32 of revolutions):
-// about a third of the fp64 sequences' issue cycles (fp64 runs at half rate
-// on CDNA4 and the fp64 log / sincos are ~25 operations each).  Their error
-// against the fp64 functions above is measured EXHAUSTIVELY -- every one of
-// the 2^32 words, tools/ubench_bm32.hip (profiles/r5*_bm32_sweep.txt) -- and
-// the bounds below cover the largest error found with a margin (r5d: radius
-// 2.48e-7 relative, cos / sin 1.88e-7 absolute; x1.6); k_hot_bx's
-// fp32 draw carries them into a per-candidate bound on |x32 - x64|.
-constexpr float kBm32RadRel = 4.0e-7f;    // |rad32 - rad64| <= kBm32RadRel rad64 (and 0 at rad64 = 0)
-constexpr float kBm32TrigAbs = 3.0e-7f;   // |cos32 - cos64|, |sin32 - sin64| <= kBm32TrigAbs
-
-// -ln(u) for u = 1 - y 2^-32 (u01_open0's uniform) in fp32: for u <= 1/2
-// the exact integer m = 2^32 - y gives u = m 2^-32 (one fp32 rounding) and
-// -ln u = -log2(u) ln 2; above 1/2, -ln(1 - t) with t = y 2^-32 by Kahan's
-// log1p form (the rounding of w = 1 - t corrected by t / (1 - w))
-__device__ __forceinline__ float bm_neglog32(uint32_t y) {
-    constexpr float kLn2f = 0.6931471805599453f;
-    if (y >= 0x80000000u) {
-        const float u = (float)(0u - y) * 0x1.0p-32f;   // (y > 0: 2^32 - y in [1, 2^31])
-        return -__builtin_amdgcn_logf(u) * kLn2f;
+// The truncated-normal terms of one sampling component (SampRec.ssg, p0,
+// q0, m).  tpe.py:88-93 retries (component ~ w, x ~ N(mu, sigma)) until low
+// <= x < high: component k is accepted with probability m_k, its mass in the
+// bounds, so the accepted draw takes k with probability w_k m_k / sum w m
+// and x ~ N(mu_k, sigma_k) restricted to the bounds.  With a = (low - mu) /
+// sigma, b = (high - mu) / sigma: a component whose mean is at or below low
+// (a >= 0) is mirrored (z -> -z: [a', b') = [-b, -a), ssg = -sigma) so that
+// a' < 0 always and p0 = Phi(a'), q0 = Phi(-b') are both accurate; m =
+// Phi(b') - p0 when b' <= 0, else 1 - p0 - q0.  Labels without both bounds
+// (and categorical ones): m = 1, p0 = q0 = 0.
+__device__ __forceinline__ void samp_trunc(const DLabel& L, SampRec& s) {
+#pragma clang fp contract(off)
+    s.ssg = s.sigma;
+    s.p0 = 0.0;
+    s.q0 = 0.0;
+    s.m = 1.0;
+    if (L.mode == CAT || (L.flags & 3) != 3) return;
+    if (!(s.sigma > 0.0 && s.sigma < __builtin_inf())) {   // (a point mass, or no distribution)
+        s.ssg = 0.0;
+        s.m = (L.low <= s.mu && s.mu < L.high) ? 1.0 : 0.0;
+        return;
     }
-    const float t = (float)y * 0x1.0p-32f;
-    const float w = 1.0f - t;
-    if (w == 1.0f) return t;
-    return (-__builtin_amdgcn_logf(w) * kLn2f) * (t * __builtin_amdgcn_rcpf(1.0f - w));
+    const double a = (L.low - s.mu) / s.sigma, b = (L.high - s.mu) / s.sigma;
+    const bool flip = a >= 0.0;
+    const double a2 = flip ? -b : a, b2 = flip ? -a : b;
+    s.ssg = flip ? -s.sigma : s.sigma;
+    s.p0 = ncdf(a2);
+    s.q0 = ncdf(-b2);
+    const double m = b2 <= 0.0 ? ncdf(b2) - s.p0 : (1.0 - s.p0) - s.q0;
+    s.m = m > 0.0 ? m : 0.0;
 }
 
-__device__ __forceinline__ float bm_radius32(uint32_t y) {
-    return __builtin_amdgcn_sqrtf(2.0f * bm_neglog32(y));
+// The below mixture's sampling records of one label, folded in place by
+// every thread of one block (k_fold for device builds, k_samp_fold for
+// host-uploaded posteriors: one function, so both draw the same bits).  On
+// entry s[k] holds mu, sigma and wd = the raw weight w_k; on exit the pick's
+// cumulative weights cdf_k = sum_{i<=k} w_i m_i / Z (summed in order by one
+// thread; cdf_{ns-1} = 1 exactly), wd_k = w_k / Z and the truncation terms.
+// Z = 0 (the bounds hold none of the mixture's mass: the reference's loop
+// would never end) leaves every m = 0, so every draw fails loudly.  Returns
+// (thread 0) whether sum w > 0.
+__device__ __forceinline__ bool samp_fold_block(const DLabel& L, SampRec* __restrict__ s, int ns) {
+#pragma clang fp contract(off)
+    for (int k = threadIdx.x; k < ns; k += blockDim.x) {
+        SampRec r = s[k];
+        samp_trunc(L, r);
+        s[k] = r;
+    }
+    __syncthreads();
+    bool ok = true;
+    if (threadIdx.x == 0) {
+        double tot = 0.0, Z = 0.0;
+        for (int k = 0; k < ns; ++k) {
+            tot += s[k].wd;
+            Z += s[k].wd * s[k].m;
+        }
+        ok = tot > 0.0;
+        const bool zero = !(Z > 0.0);
+        double run = 0.0;
+        for (int k = 0; k < ns; ++k) {
+            const double w = s[k].wd;
+            run += w * s[k].m;
+            s[k].cdf = (k == ns - 1 || zero) ? 1.0 : run / Z;
+            s[k].wd = zero ? 0.0 : w / Z;
+            if (zero) s[k].m = 0.0;
+        }
+    }
+    __syncthreads();
+    return ok;
 }
 
-// (cos, sin)(2 pi w 2^-32) in fp32: w - 2^31 as a signed turn fraction in
-// [-1/2, 1/2) (half the input rounding of [0, 1)), cos(2 pi (x + 1/2)) =
-// -cos(2 pi x), likewise sin
-__device__ __forceinline__ void sincos_turn32f(uint32_t w, float& c, float& s) {
-    const float x = (float)(int32_t)(w ^ 0x80000000u) * 0x1.0p-32f;
-    c = -__builtin_amdgcn_cosf(x);
-    s = -__builtin_amdgcn_sinf(x);
-}
-
-// Candidates 2p and 2p + 1 share one Philox4x32-10 call per attempt: the
-// counter is (p, attempt, label stream, round); word x picks candidate 2p's
-// component ~ weights, word z candidate 2p + 1's, word y gives the
-// Box-Muller radius and word w the angle, and the pair's normals are rad cos
-// and rad sin (independent N(0, 1)).  draw_pair draws both, draw_attempt one
-// of them -- the same arithmetic, so the same bits.
+// Candidates 2p and 2p + 1 share one Philox4x32-10 call: the counter is (p,
+// 0, label stream, round); words x, y are candidate 2p's pick and uniform,
+// words z, w candidate 2p + 1's.  draw_pair draws both, draw_one one of
+// them -- the same arithmetic, so the same bits.  The value is the draw
+// space's (LGMM1: log space, before the exp).
 template <typename Src>
 __device__ __forceinline__ void draw_pair(const DLabel& L, const Src& src, uint32_t k0, uint32_t k1, uint32_t p,
-                                          uint32_t it, uint32_t round, double& d0, double& d1) {
-    const U4 r = philox4x32_10(U4{p, it, (uint32_t)L.stream, round}, k0, k1);
-    double mu0, sg0, mu1, sg1;
-    src.pick(r.x, mu0, sg0);
-    src.pick(r.z, mu1, sg1);
-    const double rad = bm_radius(r.y, src.log_tab());
-    double c, s;
-    sincos_turn32(r.w, c, s, src.cos_tab());
-    d0 = fma(sg0, rad * c, mu0);
-    d1 = fma(sg1, rad * s, mu1);
+                                          uint32_t round, double& d0, double& d1) {
+    const U4 r = philox4x32_10(U4{p, 0u, (uint32_t)L.stream, round}, k0, k1);
+    d0 = icdf_draw(L, src.comp(r.x), r.x, r.y);
+    d1 = icdf_draw(L, src.comp(r.z), r.z, r.w);
 }
 
 template <typename Src>
-__device__ __forceinline__ double draw_attempt(const DLabel& L, const Src& src, uint32_t k0, uint32_t k1,
-                                               uint32_t g, uint32_t it, uint32_t round) {
-    const U4 r = philox4x32_10(U4{g >> 1, it, (uint32_t)L.stream, round}, k0, k1);
+__device__ __forceinline__ double draw_one(const DLabel& L, const Src& src, uint32_t k0, uint32_t k1, uint32_t g,
+                                           uint32_t round) {
+    const U4 r = philox4x32_10(U4{g >> 1, 0u, (uint32_t)L.stream, round}, k0, k1);
     const bool h = (g & 1u) != 0;
-    double mu, sg;
-    src.pick(h ? r.z : r.x, mu, sg);
-    const double rad = bm_radius(r.y, src.log_tab());
-    double c, s;
-    sincos_turn32(r.w, c, s, src.cos_tab());
-    return fma(sg, rad * (h ? s : c), mu);
+    const uint32_t wp = h ? r.z : r.x, wu = h ? r.w : r.y;
+    return icdf_draw(L, src.comp(wp), wp, wu);
+}
+
+// the Philox words of candidate g (pick, uniform): k_hot_bx's prefilter
+// decides most candidates from them alone
+__device__ __forceinline__ void draw_words(const DLabel& L, uint32_t k0, uint32_t k1, uint32_t g, uint32_t round,
+                                           uint32_t& wp, uint32_t& wu) {
+    const U4 r = philox4x32_10(U4{g >> 1, 0u, (uint32_t)L.stream, round}, k0, k1);
+    const bool h = (g & 1u) != 0;
+    wp = h ? r.z : r.x;
+    wu = h ? r.w : r.y;
 }
 
 // Slot r of thread t in a tile of R x nthreads candidates (R even): slots
-// r, r + 1 are one Box-Muller pair, candidates 2 ((r / 2) nthreads + t) and
+// r, r + 1 are one Philox pair, candidates 2 ((r / 2) nthreads + t) and
 // the next one
 __device__ __host__ __forceinline__ uint32_t tile_cand(int r, uint32_t t, uint32_t nthreads) {
     return 2u * ((uint32_t)(r >> 1) * nthreads + t) + (uint32_t)(r & 1);
 }
 
-// LGMM1 sample value of an accepted log-space draw (tpe.py:255: np.exp);
-// RAW sample_slots leave this step to the caller
+// LGMM1 sample value of a log-space draw (tpe.py:255: np.exp); RAW
+// sample_slots leave this step to the caller
 __device__ __forceinline__ double lgmm_value(double draw) { return exp(draw); }
 
 // Draw one sample of the below posterior for global candidate g, BEFORE
 // quantization (LGMM1: after the exp).
-// GMM1 / LGMM1 (tpe.py:68-99 / 222-256): component ~ weights, x ~ N(mu, sigma),
-// bounded: retry until low <= x < high (re-selecting the component, exactly as
-// the reference loop does), LGMM1 then exp(x).
+// GMM1 / LGMM1 (tpe.py:68-99 / 222-256): the reference draws component ~
+// weights and x ~ N(mu, sigma), retrying both until low <= x < high; the
+// accepted draw is component k with probability w_k m_k / sum w m (m_k: the
+// component's mass inside the bounds) and x ~ N(mu_k, sigma_k) restricted to
+// [low, high) -- drawn here directly by the inverse CDF (icdf_draw), no
+// retries.  LGMM1 then exp(x).
 // categorical (stochastic.py:109-147): index ~ p.
-// Returns false if the truncation interval was not reached within the cap.
+// Returns false when the bounds hold no mass (NaN: the reference's loop
+// would never end).
 template <int MODE>
 __device__ __forceinline__ bool sample_raw(const DLabel& L, const SampRec* __restrict__ s,
                                            uint64_t seed, uint32_t round, uint32_t g,
@@ -431,189 +512,29 @@ __device__ __forceinline__ bool sample_raw(const DLabel& L, const SampRec* __res
         out = (double)cdf_search(s, L.ns, (double)r.x * 0x1.0p-32);
         return true;
     } else {
-        const bool bounded = (L.flags & 3) == 3;
-        for (uint32_t it = 0; it < kMaxAttempts; ++it) {
-            const double draw = draw_attempt(L, SampGlobal{s, L.ns}, k0, k1, g, it, round);
-            if (!bounded || (L.low <= draw && draw < L.high)) {
-                out = (MODE == DENSE_LGMM || MODE == QUANT_LGMM) ? lgmm_value(draw) : draw;
-                return true;
-            }
-        }
-        out = __builtin_nan("");
-        return false;
+        const double draw = draw_one(L, SampGlobal{s, L.ns}, k0, k1, g, round);
+        out = (MODE == DENSE_LGMM || MODE == QUANT_LGMM) ? lgmm_value(draw) : draw;
+        return draw == draw;
     }
 }
 
-// sample_raw for the R slots of a thread (bit for bit the same draws): the
-// lane keeps a queue of its pending slots (bit mask) and spends every
-// attempt of the rejection loop on the first of them, so a wave runs ~R +
-// (the largest excess of one lane) attempts instead of R times the largest
-// attempt count of each slot -- with a prior component reaching far out of
-// [low, high), nearly every wave has a lane that retries.  Slots outside
-// `pend` keep their value.  Returns false if a slot hit the attempt cap
-// (its value is NaN).
+// sample_raw for the R slots of a thread (bit for bit the same draws).
+// Slots outside `pend` keep their value.  Returns false if a slot's draw
+// failed (NaN).
 template <int MODE, int R, typename Src, bool RAW = false>
 __device__ __forceinline__ bool sample_slots(const DLabel& L, const Src& src, uint64_t seed,
                                              const uint32_t (&rk)[R], const uint32_t (&g)[R], uint32_t pend,
                                              double (&out)[R]) {
     static_assert(MODE != CAT, "categorical slots draw once each");
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-    const bool bounded = (L.flags & 3) == 3;
-    const uint32_t mask0 = pend;
     bool ok = true;
-    // attempt 0 of every pending slot, straight-line; the queue below takes
-    // the rejected ones from attempt 1 (the same attempt sequence per slot)
-    // (every slot is drawn, pending or not: no branch, so with a branch-free
-    // pick the slots' sequences can interleave)
-    uint32_t rej = 0;
+    // (every slot is drawn, pending or not: no branch)
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const double draw = draw_attempt(L, src, k0, k1, g[r], 0u, rk[r]);
+        const double draw = draw_one(L, src, k0, k1, g[r], rk[r]);
         const bool p = (pend >> r) & 1u;
         out[r] = p ? draw : out[r];
-        if (p && bounded && !(L.low <= draw && draw < L.high)) rej |= 1u << r;
-    }
-    pend = rej;
-    uint32_t it = 1;
-    while (pend) {
-        const int cur = __builtin_ctz(pend);
-        uint32_t gg = g[0], rr = rk[0];
-#pragma unroll
-        for (int r = 1; r < R; ++r)
-            if (cur == r) {
-                gg = g[r];
-                rr = rk[r];
-            }
-        const double draw = draw_attempt(L, src, k0, k1, gg, it, rr);
-        const bool acc = !bounded || (L.low <= draw && draw < L.high);
-        if (acc || it + 1 >= kMaxAttempts) {
-            const double v = acc ? draw : __builtin_nan("");
-            ok = ok && acc;
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-                if (cur == r) out[r] = v;
-            pend &= pend - 1;
-            it = 1;
-        } else {
-            ++it;
-        }
-    }
-    if constexpr ((MODE == DENSE_LGMM || MODE == QUANT_LGMM) && !RAW) {
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-            if ((mask0 >> r) & 1u) out[r] = lgmm_value(out[r]);
-    }
-    return ok;
-}
-
-// set bits of a wave mask below this lane (v_mbcnt_lo + v_mbcnt_hi)
-__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-// The workgroup-cooperative form of sample_slots for tile kernels (every
-// thread of the workgroup calls it, uniform control flow): attempt 0 of
-// every slot straight-line; the rejected slots go to an LDS list and the
-// whole workgroup retries them together, each list entry walking its own
-// attempts 1, 2, .. -- so a rejection costs one lane-attempt instead of a
-// wave-wide queue iteration (the same draws, bit for bit).  Slot r of
-// thread t holds candidate g0 + tile_cand(r, t, blockDim): slots r, r + 1 are
-// a Box-Muller pair, drawn by one Philox call (draw_pair) when g0 is even.
-// The accepted values come back through CAP entries at a time (the
-// rejected slots of one tile are a few per cent of R * 256 with bounded
-// labels: one pass; more take several, each retrying the next CAP entries).
-// A smaller value array leaves LDS for more workgroups per CU.
-//
-// The list: each wave appends to its own segment of R * 64 entries, in
-// slot order, at the running count it keeps in a scalar register -- the
-// rejection mask of a slot IS its comparison's wave mask, so a slot costs
-// two v_mbcnt and an add (round 3: one LDS atomic and ~17 VALU operations
-// per slot); after the barrier the segments are read as one list in wave
-// order through their counts.
-constexpr int kTileWaves = 4;   // sample_tile: 256-thread workgroups
-template <int R, int CAP = R * 256>
-struct RetryLds {
-    int wn[kTileWaves];       // per wave: its rejected slots of this tile
-    uint16_t slot[R * 256];   // per wave a segment of R * 64: candidate offset within the tile
-    double val[CAP];
-};
-
-// (every thread of the workgroup calls it, blockDim.x == 256; no workgroup
-// barrier: each wave retries its own rejected slots -- `par` is unused, kept
-// for the callers.
-// Slots outside `pend` receive unspecified values: both callers read the
-// pending slots only.)
-template <int MODE, int R, typename Src, bool RAW = false, int CAP = R * 256>
-__device__ __forceinline__ bool sample_tile(const DLabel& L, const Src& src, uint64_t seed, uint32_t rk,
-                                            uint32_t g0, uint32_t pend, double (&out)[R], RetryLds<R, CAP>& q,
-                                            int par) {
-    static_assert(MODE != CAT, "categorical slots draw once each");
-    static_assert(R * 256 <= 65536, "tile offsets are 16-bit");
-    (void)par;
-    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-    const bool bounded = (L.flags & 3) == 3;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint16_t* __restrict__ seg = q.slot + wave * (R * 64);
-    constexpr int kAccepted = 1 << 20;   // pos of an accepted slot: past any list
-    int pos[R];     // this lane's slots in its wave's segment (kAccepted: not listed)
-    int run = 0;    // the wave's rejected slots so far (uniform)
-    static_assert(R % 2 == 0, "sample_tile draws Box-Muller pairs");
-    const bool paired = (g0 & 1u) == 0;   // (an odd first index: each slot on its own, the same bits)
-#pragma unroll
-    for (int r = 0; r < R; r += 2) {
-        const uint32_t c0 = tile_cand(r, threadIdx.x, blockDim.x);
-        double dd[2];
-        if (paired) {
-            draw_pair(L, src, k0, k1, (g0 + c0) >> 1, 0u, rk, dd[0], dd[1]);
-        } else {
-            dd[0] = draw_attempt(L, src, k0, k1, g0 + c0, 0u, rk);
-            dd[1] = draw_attempt(L, src, k0, k1, g0 + c0 + 1u, 0u, rk);
-        }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const double draw = dd[h];
-            const bool p = (pend >> (r + h)) & 1u;
-            out[r + h] = draw;
-            const bool rej = p && bounded && !(L.low <= draw && draw < L.high);
-            const uint64_t m = __ballot(rej);
-            pos[r + h] = rej ? run + (int)lanes_below(m) : kAccepted;
-            if (rej) seg[pos[r + h]] = (uint16_t)(c0 + (uint32_t)h);
-            run += (int)__popcll(m);
-        }
-    }
-    bool ok = true;
-    if (bounded && run > 0) {   // (a label without both bounds never rejects: no list)
-        // the wave retries its own rejected slots -- no workgroup barrier:
-        // its segment and its share of val are its own, and LDS operations
-        // of one wave complete in order (the wave barriers only keep the
-        // compiler from moving them); a retry is the slot's own attempts 1,
-        // 2, .. either way, so the values are the cooperative retry's
-        constexpr int WC = CAP / kTileWaves;
-        double* __restrict__ wval = q.val + wave * WC;
-        for (int c0 = 0; c0 < run; c0 += WC) {
-            const int c1 = min(run, c0 + WC);
-            __builtin_amdgcn_wave_barrier();
-            for (int e = c0 + lane; e < c1; e += 64) {
-                const uint32_t gg = g0 + (uint32_t)seg[e];
-                double v = __builtin_nan("");
-                for (uint32_t it = 1; it < kMaxAttempts; ++it) {
-                    const double draw = draw_attempt(L, src, k0, k1, gg, it, rk);
-                    if (L.low <= draw && draw < L.high) {
-                        v = draw;
-                        break;
-                    }
-                }
-                ok = ok && v == v;
-                wval[e - c0] = v;
-            }
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (int r = 0; r < R; ++r) {   // (segment entry pos in [c0, c1); kAccepted never is)
-                const uint32_t k = (uint32_t)(pos[r] - c0);
-                if (k < (uint32_t)(c1 - c0)) out[r] = wval[k];
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
+        ok = ok && (!p || draw == draw);
     }
     if constexpr ((MODE == DENSE_LGMM || MODE == QUANT_LGMM) && !RAW) {
 #pragma unroll
@@ -623,175 +544,39 @@ __device__ __forceinline__ bool sample_tile(const DLabel& L, const Src& src, uin
     return ok;
 }
 
-// sample_tile's draws in fp32 with a rigorous bound, for k_hot_bx (RAW,
-// dense GMM1 / LGMM1, every thread of the 256-thread workgroup calls it):
-// slot r gets xf[r] and ef[r]: ef >= 0 -- the draw's attempt 0 was accepted
-// and |xf - x64| <= ef, x64 being the value the fp64 draw (draw_attempt /
-// draw_pair) gives the same candidate; ef = -a <= 0 -- the fp64 draw decided
-// (attempt a accepted) and xf is its value rounded to fp32.  k_screen_hot re-draws
-// a listed candidate in fp64 from (index, attempt), so every value that is
-// scored is the fp64 draw's, bit for bit.
-//   attempt 0: Philox as draw_pair; the component picked by the same
-//     integer thresholds (the same component); radius and angle by the fp32
-//     functions above; x = fma(sg, rad cos|sin, mu) in fp32.  The bound (the
-//     measured kBm32RadRel / kBm32TrigAbs, the fp32 roundings of mu, sigma,
-//     the products and the fma, and the fp64 draw's own rounding):
-//       ef = 1.001 (sg rad (eps_r + eps_t + 2^-23) + 2^-23 (|mu| + |x|))
-//   truncation: x64 in [low, high) is decided by xf +- ef where the
-//     interval clears a bound; where it straddles one (or xf is NaN) the
-//     slot joins the rejected ones, flagged to start from attempt 0 --
-//     so the accepted attempt of every slot is the fp64 draw's;
-//   those slots: sample_tile's cooperative fp64 retries (exact values),
-//     recording the accepted attempt.
-// escale > 1 widens every bound (tests: TPE_OPT_HOT32 = 2 sends many more
-// slots through the fp64 decisions and the margins; the round is the same).
-// Returns false if a slot hit the attempt cap.
-template <int R>
-struct RetryLds32 {
-    int wn[kTileWaves];
-    uint16_t slot[R * 256];
-    double val[R * 256 / 2];   // (a pass holds up to R * 128 retried slots)
-    int32_t att[R * 256 / 2];
-};
-
-__device__ __forceinline__ float f32_step(float f, bool up) {   // the adjacent float (f finite)
-    const uint32_t u = __float_as_uint(f);
-    if (f == 0.0f) return __uint_as_float(up ? 1u : 0x80000001u);
-    return __uint_as_float((f > 0.0f) == up ? u + 1u : u - 1u);
-}
-__device__ __forceinline__ float f32_up(double v) {   // the smallest float >= v
-    const float f = (float)v;
-    return (double)f >= v ? f : f32_step(f, true);
-}
-__device__ __forceinline__ float f32_dn(double v) {   // the largest float <= v
-    const float f = (float)v;
-    return (double)f <= v ? f : f32_step(f, false);
+// set bits of a wave mask below this lane (v_mbcnt_lo + v_mbcnt_hi)
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-template <int R, typename Src>
-__device__ __forceinline__ bool sample_tile32(const DLabel& L, const Src& src, uint64_t seed, uint32_t rk,
-                                              uint32_t g0, uint32_t pend, float (&xf)[R], float (&ef)[R],
-                                              RetryLds32<R>& q, float escale = 1.0f) {
-    static_assert(R % 2 == 0, "Box-Muller pairs");
-    static_assert(R * 256 <= 32768, "tile offsets are 15-bit (bit 15: start at attempt 0)");
-    constexpr int CAP = R * 256 / 2;
-    constexpr uint16_t kFrom0 = 0x8000;   // list entry flag: decide attempt 0 in fp64 too
+// sample_slots for tile kernels: slot r of thread t holds candidate g0 +
+// tile_cand(r, t, blockDim): slots r, r + 1 are a Philox pair, drawn by one
+// call (draw_pair) when g0 is even.  Slots outside `pend` receive
+// unspecified values (the callers read the pending slots only).
+template <int MODE, int R, typename Src, bool RAW = false>
+__device__ __forceinline__ bool sample_tile(const DLabel& L, const Src& src, uint64_t seed, uint32_t rk,
+                                            uint32_t g0, uint32_t pend, double (&out)[R]) {
+    static_assert(MODE != CAT, "categorical slots draw once each");
+    static_assert(R % 2 == 0, "sample_tile draws Philox pairs");
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-    const bool bounded = (L.flags & 3) == 3;
-    // the bounds as floats that keep the decisions exact (f32_up / f32_dn)
-    const float lo_up = f32_up(L.low), lo_dn = f32_dn(L.low), hi_up = f32_up(L.high), hi_dn = f32_dn(L.high);
-    constexpr float kEpsDraw = kBm32RadRel + kBm32TrigAbs + 0x1.0p-23f;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint16_t* __restrict__ seg = q.slot + wave * (R * 64);
-    constexpr int kAccepted = 1 << 20;
-    int pos[R];
-    int run = 0;
-    const bool paired = (g0 & 1u) == 0;
+    const bool paired = (g0 & 1u) == 0;   // (an odd first index: each slot on its own, the same bits)
+    bool ok = true;
 #pragma unroll
     for (int r = 0; r < R; r += 2) {
         const uint32_t c0 = tile_cand(r, threadIdx.x, blockDim.x);
-        float x2[2], e2[2];
-        bool ex2[2] = {false, false};   // exact fp64 values (the odd-start tile)
         if (paired) {
-            const U4 w = philox4x32_10(U4{(g0 + c0) >> 1, 0u, (uint32_t)L.stream, rk}, k0, k1);
-            const int ka = src.pick_index(w.x), kb = src.pick_index(w.z);
-            const float rad = bm_radius32(w.y);
-            float c, s;
-            sincos_turn32f(w.w, c, s);
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int k = h ? kb : ka;
-                const float mu = src.t->mu32[k], sg = src.t->sg32[k];
-                const float x = __builtin_fmaf(sg, rad * (h ? s : c), mu);
-                x2[h] = x;
-                e2[h] = escale * 1.001f *
-                        (sg * rad * kEpsDraw + 0x1.0p-23f * (__builtin_fabsf(mu) + __builtin_fabsf(x)));
-            }
-        } else {   // (an odd first index, uniform: no shared pair -- each slot's fp64 draw)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const double d = draw_attempt(L, src, k0, k1, g0 + c0 + (uint32_t)h, 0u, rk);
-                x2[h] = (float)d;
-                e2[h] = 0.0f;
-                ex2[h] = !bounded || (L.low <= d && d < L.high);   // (accepted: exact)
-            }
+            draw_pair(L, src, k0, k1, (g0 + c0) >> 1, rk, out[r], out[r + 1]);
+        } else {
+            out[r] = draw_one(L, src, k0, k1, g0 + c0, rk);
+            out[r + 1] = draw_one(L, src, k0, k1, g0 + c0 + 1u, rk);
         }
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const bool p = (pend >> (r + h)) & 1u;
-            const float x = x2[h], e = e2[h];
-            bool list = false;
-            uint16_t flag = 0;
-            if (p && bounded && !ex2[h]) {
-                if (!paired) {
-                    list = true;   // rejected at attempt 0 (exactly)
-                } else {
-                    const float e2u = e + 0x1.0p-22f * __builtin_fabsf(x);   // (+ the roundings of x -+ e)
-                    const bool acc_sure = x - e2u >= lo_up && x + e2u < hi_dn;
-                    const bool rej_sure = x + e2u < lo_dn || x - e2u >= hi_up;
-                    // straddling a bound (or NaN): the fp64 draw decides from attempt 0
-                    list = !acc_sure;
-                    flag = rej_sure ? 0 : kFrom0;
-                }
-            }
-            xf[r + h] = x;
-            ef[r + h] = e;
-            const uint64_t m = __ballot(list);
-            pos[r + h] = list ? run + (int)lanes_below(m) : kAccepted;
-            if (list) seg[pos[r + h]] = (uint16_t)((c0 + (uint32_t)h) | flag);
-            run += (int)__popcll(m);
-        }
+        for (int h = 0; h < 2; ++h) ok = ok && (!((pend >> (r + h)) & 1u) || out[r + h] == out[r + h]);
     }
-    bool ok = true;
-    if (bounded) {
-        if (lane == 0) q.wn[wave] = run;
-        __syncthreads();
-        int b[kTileWaves + 1];
-        b[0] = 0;
+    if constexpr ((MODE == DENSE_LGMM || MODE == QUANT_LGMM) && !RAW) {
 #pragma unroll
-        for (int w = 0; w < kTileWaves; ++w) b[w + 1] = b[w] + q.wn[w];
-        const int n = b[kTileWaves];
-        const int mine = b[wave];
-        if (n == 0) __syncthreads();
-        for (int c0 = 0; c0 < n; c0 += CAP) {
-            const int c1 = min(n, c0 + CAP);
-            for (int e = c0 + (int)threadIdx.x; e < c1; e += blockDim.x) {
-                int w = 0;
-#pragma unroll
-                for (int k = 1; k < kTileWaves; ++k) w += e >= b[k] ? 1 : 0;
-                int bw = b[0];
-#pragma unroll
-                for (int k = 1; k < kTileWaves; ++k) bw = w == k ? b[k] : bw;
-                const uint16_t ent = q.slot[w * (R * 64) + (e - bw)];
-                const uint32_t gg = g0 + (uint32_t)(ent & 0x7FFFu);
-                double v = __builtin_nan("");
-                int32_t a = -1;
-                for (uint32_t it = (ent & kFrom0) ? 0u : 1u; it < kMaxAttempts; ++it) {
-                    const double draw = draw_attempt(L, src, k0, k1, gg, it, rk);
-                    if (L.low <= draw && draw < L.high) {
-                        v = draw;
-                        a = (int32_t)it;
-                        break;
-                    }
-                }
-                ok = ok && v == v;
-                q.val[e - c0] = v;
-                q.att[e - c0] = a;
-            }
-            __syncthreads();
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const uint32_t k = (uint32_t)(pos[r] + (mine - c0));
-                if (k < (uint32_t)(c1 - c0)) {
-                    // the fp64 draw's value and accepted attempt a, carried as
-                    // ef = -a (the cap: NaN value, ef = -1 -- k_hot_bx32 raises
-                    // the error flag through the return value)
-                    xf[r] = (float)q.val[k];
-                    ef[r] = q.att[k] < 0 ? -1.0f : -(float)q.att[k];
-                }
-            }
-            if (c1 < n) __syncthreads();
-        }
+        for (int r = 0; r < R; ++r)
+            if ((pend >> r) & 1u) out[r] = lgmm_value(out[r]);
     }
     return ok;
 }
@@ -976,7 +761,7 @@ __device__ __forceinline__ void lse_acc_run(const Comp<double>* __restrict__ c, 
 // consecutive components, each summed in order from 0, the slice sums
 // added in order to acc.  Fixing it lets a sum be split across waves by
 // slices (k_score_slices, k_rescore_slices) with the same bits.
-constexpr int kSumSlice = 256;
+constexpr int kSumSlice = 64;
 
 template <int R>
 __device__ __forceinline__ void lse_acc(const Comp<double>* __restrict__ c, int n,

@@ -813,21 +813,22 @@ __global__ __launch_bounds__(kBlock) void k_hot_bits(const int32_t* __restrict__
 // hstride + position], hcnt[cell].  The largest L of the cell is taken over
 // the LISTED candidates (k_screen_hot): a candidate left out has L <= U <
 // tau0, so the cell's largest L reaches tau0 iff a listed candidate's does.
-// Tile map only: workgroups stride over the cell's tiles of R * 256
-// candidates (Box-Muller pairs per thread, the sampling records staged once
-// per workgroup -- the launch requires them in LDS).  The listed candidates
-// gather in a buffer per WAVE in LDS (its count wave-uniform, in a scalar
-// register: no LDS atomics, no barriers in the loop) and go to the cell's
-// list with one global atomic per wave flush when a slot's listings would
-// not fit, and one per workgroup for the waves' remainders at the end.
-// (Round 4 measured other forms on the same box: one workgroup buffer
-// flushed only at the end, past which nearly every listing wave appended
-// with its own atomic on the cell's ONE counter, 2.34 ms at 0.35 VALU busy;
-// flushed after every tile that left 256 entries, behind a barrier per tile,
-// 1.37 ms at 0.75; per-wave buffers each ending with its own atomic, 1.38 ms
-// on the whole round but 1.0 ms for a label shard's few cells.)
-constexpr int kHotBuf = 128;     // entries per wave
-constexpr int kHotRetry = 512;   // rejected draws retried cooperatively per tile (the rest in-thread)
+//
+// Most candidates are decided from their Philox words alone (round 6): the
+// draw is x = mu_k + ssg_k Phi^-1(p0_k + m_k v), monotone in v = (wu + r)
+// 2^-32 within the picked component k, so each component's uniform is cut
+// into kHotCells u-cells (the top bits of wu) and a cell is marked
+// (k_hot_ucells, once per posterior and n) when the x-range of its v-range
+// can touch a set bit or leave the bins.  A candidate in an unmarked cell
+// cannot be listed; the others (~1 %) queue per wave and are drawn in fp64
+// 64 at a time (icdf_draw, the exact draw of every kernel) and tested
+// against the sub-bit bits as before -- so the list is exactly the one the
+// full draw gives.
+constexpr int kHotBuf = 128;      // listed entries per wave
+constexpr int kHotCellBits = 11;
+constexpr int kHotCells = 1 << kHotCellBits;   // u-cells per sampling component
+constexpr int kHotCellWords = kHotCells / 32;
+constexpr int kHotQ = 128;        // a wave's ring of candidates to draw in fp64
 
 // one wave's buffer to the cell's list (count n, wave-uniform)
 __device__ __forceinline__ void hot_wave_flush(int n, const int32_t* bi, const double* bxv,
@@ -850,266 +851,124 @@ __device__ __forceinline__ void hot_wave_flush(int n, const int32_t* bi, const d
     __builtin_amdgcn_wave_barrier();   // (read before the buffer is refilled)
 }
 
-// hot_wave_flush for k_hot_bx32's (index, attempt) entries
-__device__ __forceinline__ void hot_wave_flush32(int n, const int32_t* bi, const int32_t* ba,
-                                                 int32_t* __restrict__ hcnt, int32_t* __restrict__ hidx,
-                                                 int32_t* __restrict__ hatt, size_t cell, int64_t hstride,
-                                                 int32_t* __restrict__ hflag) {
-    const int lane = threadIdx.x & 63;
-    int gb = 0;
-    if (lane == 0) gb = atomicAdd(hcnt + cell, n);
-    gb = __builtin_amdgcn_readfirstlane(__shfl(gb, 0));
-    if (lane == 0 && gb + n > hstride) atomicOr(hflag, 2);
-    __builtin_amdgcn_wave_barrier();
-    for (int k = lane; k < n; k += 64)
-        if (gb + k < hstride) {
-            hidx[cell * (size_t)hstride + gb + k] = bi[k];
-            hatt[cell * (size_t)hstride + gb + k] = ba[k];
-        }
-    __builtin_amdgcn_wave_barrier();
-}
-
-// Six workgroups per CU (80 VGPRs, a few spilled): the draw loop's waits
-// on LDS and the list are hidden by more waves -- 1.26 -> 1.215 ms against
-// five per CU without spills, twice in one call (r5x: tools/build_variant.py
-// lb6).
-// LDS_BITS: every label's bits fit in LDS (the host knows the largest
-// label's sub-bins) -- the bit test is then a ds_read; otherwise every
-// label reads them from global memory.  (One kernel choosing per label
-// compiled to a generic-address load with per-lane address selects.)
-template <int R, bool LDS_BITS>
-__global__ __launch_bounds__(kBlock, 6) void k_hot_bx(
-    const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
-    const BxLabel* __restrict__ bx, const uint32_t* __restrict__ hbits, int64_t n, int64_t cand_offset,
-    uint64_t seed, const uint32_t* __restrict__ rounds, int32_t nl, int32_t* __restrict__ hcnt,
-    int32_t* __restrict__ hidx, double* __restrict__ hx, int32_t* __restrict__ err, int64_t hstride,
-    int32_t* __restrict__ hflag) {
-    const int li = group[blockIdx.y];
-    const DLabel L = labels[li];
-    const BxLabel B = bx[li];
-    __shared__ SampLds sl;
-    __shared__ double bm_cs[kCosTabLen], bm_lg[kLogTabLen];
-    stage_bm_tables(bm_cs, bm_lg);    // (visible after the __syncthreads below, whatever stage_samp does)
-    (void)stage_samp(L, samp, &sl);   // (the launch checked ns <= kSampLds)
-    const int nsb = B.nbins * kBxSub;
-    const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
-    const uint32_t rk = rounds[blockIdx.z];
-    constexpr int64_t per = (int64_t)R * kBlock;
-    // the label's bits in LDS (config 3: 19k sub-bins, 2.4 KB)
-    __shared__ uint32_t sbits[LDS_BITS ? kHotLdsWords : 1];
-    if constexpr (LDS_BITS)
-        for (int w = threadIdx.x; w < (nsb >> 5); w += kBlock) sbits[w] = hbits[(B.sb_off >> 5) + w];
-    const uint32_t* __restrict__ gbits = hbits + (B.sb_off >> 5);
-    __shared__ RetryLds<R, kHotRetry> retry;
-    __shared__ int32_t buf_i[kBlock / 64][kHotBuf];
-    __shared__ double buf_x[kBlock / 64][kHotBuf];
-    __syncthreads();   // the Box-Muller tables and the bits above
-    const int wv = threadIdx.x >> 6;
-    int wn = 0;   // this wave's buffered entries (wave-uniform)
-    const int steps = __builtin_amdgcn_readfirstlane(sl.steps);   // (read once, not per pick)
-    int par = 0;
-    for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per, par ^= 1) {
-        double x[R];
-        uint32_t pend = 0;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {   // (candidate indices recomputed where listed: fewer live registers)
-            x[r] = 0.0;
-            if (base + (int64_t)tile_cand(r, threadIdx.x, kBlock) < n) pend |= 1u << r;
-        }
-        // raw draws: an LGMM1 label's x' is log(exp(draw)) - centre, within a
-        // few ulp of draw - centre (the sub-bins' slack covers it); the list
-        // keeps the draw and k_screen_hot applies the exp.  (The family only
-        // changes that exp, which RAW leaves out: one instantiation.)
-        const uint32_t g0 = (uint32_t)(cand_offset + base);
-        if (!sample_tile<DENSE_GMM, R, SampShared, true, kHotRetry>(L, SampShared{&sl, bm_cs, bm_lg, steps}, seed,
-                                                                     rk, g0, pend, x, retry, par))
-            atomicOr(err, 1);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            bool take = false;
-            if ((pend >> r) & 1u) {
-                const double f = (x[r] - L.centre - B.xlo) * B.inv_sbw;
-                if (f >= 0.0 && f < (double)nsb) {
-                    const int j = (int)f;   // (sb_off: a multiple of 32)
-                    uint32_t word;
-                    if constexpr (LDS_BITS) word = sbits[j >> 5];
-                    else word = gbits[j >> 5];
-                    take = (word >> (j & 31)) & 1u;
-                } else {
-                    take = true;   // outside the bins (or NaN): always listed
-                }
-            }
-            const uint64_t bal = __ballot(take);
-            if (!bal) continue;
-            const int c = __builtin_amdgcn_readfirstlane((int)__popcll(bal));
-            if (wn + c > kHotBuf) {   // (wave-uniform)
-                hot_wave_flush(wn, buf_i[wv], buf_x[wv], hcnt, hidx, hx, cell, hstride, hflag);
-                wn = 0;
-            }
-            if (take) {
-                const int k = wn + (int)lanes_below(bal);
-                buf_i[wv][k] = (int32_t)(base + (int64_t)tile_cand(r, threadIdx.x, kBlock));
-                buf_x[wv][k] = x[r];
-            }
-            wn += c;
-        }
-    }
-    // the end: every wave's remainder to the cell's list behind ONE atomic
-    // for the workgroup (a shard's round has few cells, each striped over
-    // many workgroups: per-wave atomics on its one counter cost 0.5 ms)
-    __shared__ int wcnt[kBlock / 64], wbase;
-    if ((threadIdx.x & 63) == 0) wcnt[wv] = wn;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int tot = 0;
-        for (int w = 0; w < kBlock / 64; ++w) tot += wcnt[w];
-        wbase = tot ? atomicAdd(hcnt + cell, tot) : 0;
-        // a cell's list is hstride long: past it the round falls back to
-        // screening every candidate (hflag bit 2), so nothing is lost
-        if (tot && wbase + tot > hstride) atomicOr(hflag, 2);
-    }
-    __syncthreads();
-    int off = wbase;
-    for (int w = 0; w < wv; ++w) off += wcnt[w];
-    for (int k = threadIdx.x & 63; k < wn; k += 64)
-        if (off + k < hstride) {
-            hidx[cell * (size_t)hstride + off + k] = buf_i[wv][k];
-            hx[cell * (size_t)hstride + off + k] = buf_x[wv][k];
-        }
-}
-
-// k_hot_bx with the fp32 draw (sample_tile32; TPE_OPT_HOT32, the default):
-// every candidate drawn in fp32 with its bound |xf - x64| <= ef, its fp64
-// sub-bin index located within [floor(f - ef'), floor(f + ef')] (ef' adds
-// the fp32 roundings of the index and the fp64 index's own), and the
-// candidate listed when ANY sub-bin it can fall in has its bit -- or it can
-// lie outside the bins -- so the list holds every candidate the fp64 draw
-// would have listed (and, near a sub-bin edge, a few more: harmless, tau is
-// taken over the listed candidates' own fp64 sub-bins, a lower bound of
-// their scores either way).  The list keeps (index, accepted attempt):
-// k_screen_hot re-draws the value in fp64.  No Box-Muller tables in LDS:
-// the fp64 draws (retries, decisions at a truncation bound) read the
-// constant ones.
-template <int R, bool LDS_BITS>
-__global__ __launch_bounds__(kBlock, 5) void k_hot_bx32(
-    const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
-    const BxLabel* __restrict__ bx, const uint32_t* __restrict__ hbits, int64_t n, int64_t cand_offset,
-    uint64_t seed, const uint32_t* __restrict__ rounds, int32_t nl, int32_t* __restrict__ hcnt,
-    int32_t* __restrict__ hidx, int32_t* __restrict__ hatt, int32_t* __restrict__ err, int64_t hstride,
-    int32_t* __restrict__ hflag, float escale) {
-    const int li = group[blockIdx.y];
-    const DLabel L = labels[li];
-    const BxLabel B = bx[li];
-    __shared__ SampLds sl;
-    (void)stage_samp(L, samp, &sl);   // (the launch checked ns <= kSampLds; its barrier covers sbits below)
-    const int nsb = B.nbins * kBxSub;
-    const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
-    const uint32_t rk = rounds[blockIdx.z];
-    constexpr int64_t per = (int64_t)R * kBlock;
-    __shared__ uint32_t sbits[LDS_BITS ? kHotLdsWords : 1];
-    if constexpr (LDS_BITS)
-        for (int w = threadIdx.x; w < (nsb >> 5); w += kBlock) sbits[w] = hbits[(B.sb_off >> 5) + w];
-    const uint32_t* __restrict__ gbits = hbits + (B.sb_off >> 5);
-    __shared__ RetryLds32<R> retry;
-    __shared__ int32_t buf_i[kBlock / 64][kHotBuf];
-    __shared__ int32_t buf_a[kBlock / 64][kHotBuf];
-    __syncthreads();   // the bits above
-    // the fp64 sub-bin index f = (x - centre - xlo) inv_sbw, in fp32: the
-    // base and scale rounded once (their errors go into the margin)
-    const double base64 = L.centre + B.xlo;
-    const float base = (float)base64, isbw = (float)B.inv_sbw;
-    const float eb = (float)fabs((double)base - base64) * 1.0001f;
-    const float fsb = (float)nsb;
-    const int wv = threadIdx.x >> 6;
-    int wn = 0;   // this wave's buffered entries (wave-uniform)
-    const int steps = __builtin_amdgcn_readfirstlane(sl.steps);
-    const SampShared src{&sl, kCosSinTab, kLogTab, steps};
-    for (int64_t base_i = (int64_t)blockIdx.x * per; base_i < n; base_i += (int64_t)gridDim.x * per) {
-        float xf[R], ef[R];
-        uint32_t pend = 0;
-#pragma unroll
-        for (int r = 0; r < R; ++r)
-            if (base_i + (int64_t)tile_cand(r, threadIdx.x, kBlock) < n) pend |= 1u << r;
-        const uint32_t g0 = (uint32_t)(cand_offset + base_i);
-        if (!sample_tile32<R>(L, src, seed, rk, g0, pend, xf, ef, retry, escale)) atomicOr(err, 1);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            bool take = false;
-            if ((pend >> r) & 1u) {
-                const float x = xf[r];
-                const float fv = (x - base) * isbw;
-                // |fv - f64| <= (ef + eb + the subtraction's and the
-                // scale's roundings, and an exact value's fp32 rounding)
-                // isbw + the product's rounding + the fp64 index's own
-                // (~1e-16 relative, inside the 2^-21)
-                const float ax = __builtin_fabsf(x) + __builtin_fabsf(base);
-                const float em = 1.01f * ((fmaxf(ef[r], 0.0f) + eb + 0x1.0p-21f * ax) * isbw +
-                                          0x1.0p-21f * __builtin_fabsf(fv)) +
-                                 0x1.0p-20f;
-                const float flo = fv - em, fhi = fv + em;
-                if (flo >= 0.0f && fhi < fsb) {   // (false for NaN: listed)
-                    const int jlo = (int)flo, jhi = (int)fhi;
-                    if (jhi - jlo > 1) {
-                        take = true;   // (a bound wider than a sub-bin: listed)
-                    } else {
-                        uint32_t wlo, whi;
-                        if constexpr (LDS_BITS) {
-                            wlo = sbits[jlo >> 5];
-                            whi = sbits[jhi >> 5];
-                        } else {
-                            wlo = gbits[jlo >> 5];
-                            whi = gbits[jhi >> 5];
-                        }
-                        take = ((wlo >> (jlo & 31)) | (whi >> (jhi & 31))) & 1u;
-                    }
-                } else {
-                    take = true;   // possibly outside the bins (or NaN): always listed
-                }
-            }
-            const uint64_t bal = __ballot(take);
-            if (!bal) continue;
-            const int c = __builtin_amdgcn_readfirstlane((int)__popcll(bal));
-            if (wn + c > kHotBuf) {   // (wave-uniform)
-                hot_wave_flush32(wn, buf_i[wv], buf_a[wv], hcnt, hidx, hatt, cell, hstride, hflag);
-                wn = 0;
-            }
-            if (take) {
-                const int k = wn + (int)lanes_below(bal);
-                buf_i[wv][k] = (int32_t)(base_i + (int64_t)tile_cand(r, threadIdx.x, kBlock));
-                buf_a[wv][k] = ef[r] < 0.0f ? (int32_t)(-ef[r]) : 0;   // the accepted attempt
-            }
-            wn += c;
-        }
-    }
-    __shared__ int wcnt[kBlock / 64], wbase;
-    if ((threadIdx.x & 63) == 0) wcnt[wv] = wn;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int tot = 0;
-        for (int w = 0; w < kBlock / 64; ++w) tot += wcnt[w];
-        wbase = tot ? atomicAdd(hcnt + cell, tot) : 0;
-        if (tot && wbase + tot > hstride) atomicOr(hflag, 2);
-    }
-    __syncthreads();
-    int off = wbase;
-    for (int w = 0; w < wv; ++w) off += wcnt[w];
-    for (int k = threadIdx.x & 63; k < wn; k += 64)
-        if (off + k < hstride) {
-            hidx[cell * (size_t)hstride + off + k] = buf_i[wv][k];
-            hatt[cell * (size_t)hstride + off + k] = buf_a[wv][k];
-        }
-}
-
-// k_hot_bx's lists as work items of R * 256 listed candidates (the passes
-// of k_screen_hot): pre[c] = the first item of cell c (cell c has
-// ceil(min(hcnt[c], hstride) / (R 256)) of them), pre[cells] = all; one
-// workgroup of 1024, which also zeroes the item counter.
-template <int R>
-__global__ __launch_bounds__(1024) void k_hot_items(const int32_t* __restrict__ hcnt, int64_t cells,
-                                                    int64_t hstride, int32_t* __restrict__ pre,
-                                                    int32_t* __restrict__ next) {
-    constexpr int64_t per = (int64_t)R * kBlock;
+// per dense label position: the set bits of the label's sub-bin words
+// before each word (exclusive prefix), one workgroup per label
+__global__ __launch_bounds__(1024) void k_hot_prefix(const int32_t* __restrict__ group,
+                                                     const BxLabel* __restrict__ bx,
+                                                     const uint32_t* __restrict__ hbits,
+                                                     int32_t* __restrict__ pc) {
+    const BxLabel B = bx[group[blockIdx.x]];
+    const int64_t nw = ((int64_t)B.nbins * kBxSub + 31) / 32;
+    const uint32_t* wd = hbits + (B.sb_off >> 5);
+    int32_t* out = pc + (B.sb_off >> 5);
+    const int64_t per = (nw + 1023) / 1024;
+    const int64_t w0 = (int64_t)threadIdx.x * per, w1 = min(nw, w0 + per);
+    int32_t v = 0;
+    for (int64_t w = w0; w < w1; ++w) v += __popc(wd[w]);
     __shared__ int32_t wsum[16];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int32_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    int32_t run = x - v;
+    for (int u = 0; u < wv; ++u) run += wsum[u];
+    for (int64_t w = w0; w < w1; ++w) {
+        out[w] = run;
+        run += __popc(wd[w]);
+    }
+}
+
+// the x an edge of u-cells meets: v = e / kHotCells exactly (1 - v too),
+// then icdf_draw's own arithmetic (p, q, z, x, the clamp); p or q = 0 at an
+// unbounded tail: -inf / +inf
+__device__ __forceinline__ double hot_edge_x(const DLabel& L, const DrawComp& c, int e) {
+    const double v = (double)e * (1.0 / kHotCells), vb = (double)(kHotCells - e) * (1.0 / kHotCells);
+    const double p = fma(c.m, v, c.p0), q = fma(c.m, vb, c.q0);
+    double z;
+    if (p <= 0.5) z = p > 0.0 ? ndtri_lower(p) : -__builtin_inf();
+    else z = q > 0.0 ? -ndtri_lower(q) : __builtin_inf();
+    double x = fma(c.ssg, z, c.mu);
+    if ((L.flags & 3) == 3) {
+        x = x < L.low ? L.low : x;
+        x = x >= L.high ? nextafter(L.high, -__builtin_inf()) : x;
+    }
+    return x;
+}
+
+// set bits of the label's words at sub-bins < j (prefix pc)
+__device__ __forceinline__ int64_t hot_bits_before(const uint32_t* __restrict__ wd, const int32_t* __restrict__ pc,
+                                                   int64_t j) {
+    const int64_t w = j >> 5;
+    const int b = (int)(j & 31);
+    return (int64_t)pc[w] + __popc(wd[w] & ((1u << b) - 1u));
+}
+
+// The u-cells of every sampling component of every dense label: bit c of
+// component k is set when some v in [c, c + 1) / kHotCells can draw x (any
+// r, with the rounding of the draw and of the candidate's sub-bin index:
+// ~1e-12 relative of slack) into a sub-bin whose bit is set, or outside the
+// bins.  Grid (kHotCells / 256, kSampLds, dense labels); layout
+// ucell[((y kSampLds + k) kHotCellWords + word].
+__global__ __launch_bounds__(kBlock) void k_hot_ucells(const DLabel* __restrict__ labels,
+                                                       const int32_t* __restrict__ group,
+                                                       const SampRec* __restrict__ samp,
+                                                       const BxLabel* __restrict__ bx,
+                                                       const uint32_t* __restrict__ hbits,
+                                                       const int32_t* __restrict__ pc,
+                                                       uint32_t* __restrict__ ucell) {
+    const int li = group[blockIdx.z];
+    const DLabel L = labels[li];
+    const int k = blockIdx.y;
+    if (k >= L.ns) return;   // (the whole workgroup)
+    const BxLabel B = bx[li];
+    const int64_t nsb = (int64_t)B.nbins * kBxSub;
+    const SampRec r = samp[L.samp_off + k];
+    DrawComp c{};
+    c.mu = r.mu;
+    c.ssg = r.ssg;
+    c.p0 = r.p0;
+    c.q0 = r.q0;
+    c.m = r.m;
+    const int cell = (int)blockIdx.x * kBlock + (int)threadIdx.x;
+    bool hot = true;
+    if (c.m > 0.0) {
+        const double x0 = hot_edge_x(L, c, cell), x1 = hot_edge_x(L, c, cell + 1);
+        const double xa = fmin(x0, x1), xb = fmax(x0, x1);
+        if (xa == xa && xb == xb && fabs(xa) < __builtin_inf() && fabs(xb) < __builtin_inf()) {
+            const double slop = 1e-12 * (fabs(c.mu) + fabs(xa - c.mu) + fabs(xb - c.mu) + fabs(c.ssg));
+            double f0 = (xa - slop - L.centre - B.xlo) * B.inv_sbw;
+            double f1 = (xb + slop - L.centre - B.xlo) * B.inv_sbw;
+            f0 -= 1e-6 + 1e-12 * fabs(f0);
+            f1 += 1e-6 + 1e-12 * fabs(f1);
+            if (f0 >= 0.0 && f1 < (double)nsb) {
+                const int64_t j0 = (int64_t)f0, j1 = (int64_t)f1;
+                const uint32_t* wd = hbits + (B.sb_off >> 5);
+                const int32_t* pp = pc + (B.sb_off >> 5);
+                const int64_t n1 = hot_bits_before(wd, pp, j1) + ((wd[j1 >> 5] >> (j1 & 31)) & 1u);
+                hot = n1 - hot_bits_before(wd, pp, j0) > 0;
+            }
+        }
+    }
+    const uint64_t m = __ballot(hot);
+    const int lane = threadIdx.x & 63;
+    uint32_t* o = ucell + ((size_t)blockIdx.z * kSampLds + k) * kHotCellWords + (cell >> 5);
+    if (lane == 0) o[0] = (uint32_t)m;
+    if (lane == 32) o[0] = (uint32_t)(m >> 32);
+}
+
+// the work items of k_screen_hot: per cell ceil(min(count, stride) / per)
+// passes of `per` listed candidates, pre[c] their exclusive prefix (pre[cells]
+// = the total), *next (its item counter) zeroed; every thread of a B-thread
+// workgroup calls it
+template <int B>
+__device__ __forceinline__ void hot_items_body(const int32_t* __restrict__ hcnt, int64_t cells, int64_t hstride,
+                                               int64_t per, int32_t* __restrict__ pre, int32_t* __restrict__ next) {
+    __shared__ int32_t wsum[B / 64];
     __shared__ int32_t carry;
     if (threadIdx.x == 0) {
         carry = 0;
@@ -1117,7 +976,7 @@ __global__ __launch_bounds__(1024) void k_hot_items(const int32_t* __restrict__ 
     }
     __syncthreads();
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int64_t c0 = 0; c0 < cells; c0 += 1024) {
+    for (int64_t c0 = 0; c0 < cells; c0 += B) {
         const int64_t c = c0 + threadIdx.x;
         int32_t v = 0;
         if (c < cells) v = (int32_t)((min((int64_t)hcnt[c], hstride) + per - 1) / per);
@@ -1133,14 +992,183 @@ __global__ __launch_bounds__(1024) void k_hot_items(const int32_t* __restrict__ 
         for (int u = 0; u < w; ++u) wp += wsum[u];
         if (c < cells) pre[c] = wp + x - v;
         __syncthreads();   // (carry and wsum read by every thread)
-        if (threadIdx.x == 1023) carry = wp + x;
+        if (threadIdx.x == B - 1) carry = wp + x;
         __syncthreads();
     }
     if (threadIdx.x == 0) pre[cells] = carry;
 }
 
+// The draw kernel.  Tile map only: workgroups stride over the cell's tiles
+// of R * 256 candidates (Philox pairs per thread), the sampling records and
+// the label's u-cells staged once per workgroup (the launch requires the
+// records in LDS).  Per candidate: the Philox words, the pick, one u-cell
+// bit; a marked candidate joins its wave's ring (index, words; count in a
+// scalar register), which is drawn in fp64 whenever it holds 64, then its
+// sub-bin's bit is read.  The listed candidates gather in a buffer per WAVE
+// in LDS and go to the cell's list with one global atomic per wave flush
+// when the buffer would overflow, and one per workgroup for the waves'
+// remainders at the end.  (Round 4 measured other list forms on the same
+// box: one workgroup buffer flushed only at the end, 2.34 ms at 0.35 VALU
+// busy; flushed after every tile behind a barrier, 1.37 ms at 0.75.)
+// LDS_BITS: every label's bits fit in LDS (the host knows the largest
+// label's sub-bins) -- the bit test is then a ds_read; otherwise every
+// label reads them from global memory.
+template <int R, bool LDS_BITS>
+__global__ __launch_bounds__(kBlock, 4) void k_hot_bx(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
+    const BxLabel* __restrict__ bx, const uint32_t* __restrict__ hbits, const uint32_t* __restrict__ ucell,
+    int64_t n, int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, int32_t nl,
+    int32_t* __restrict__ hcnt, int32_t* __restrict__ hidx, double* __restrict__ hx, int32_t* __restrict__ err,
+    int64_t hstride, int32_t* __restrict__ hflag, uint32_t* __restrict__ done, int32_t* __restrict__ items,
+    int64_t item_per) {
+    static_assert(R % 2 == 0, "Philox pairs");
+    const int li = group[blockIdx.y];
+    const DLabel L = labels[li];
+    const BxLabel B = bx[li];
+    __shared__ SampLds sl;
+    __shared__ uint32_t ucw[kSampLds * kHotCellWords];
+    __shared__ uint32_t sbits[LDS_BITS ? kHotLdsWords : 1];
+    __shared__ uint32_t q_i[kBlock / 64][kHotQ], q_p[kBlock / 64][kHotQ], q_u[kBlock / 64][kHotQ];
+    __shared__ int32_t buf_i[kBlock / 64][kHotBuf];
+    __shared__ double buf_x[kBlock / 64][kHotBuf];
+    const int nsb = B.nbins * kBxSub;
+    if constexpr (LDS_BITS)
+        for (int w = threadIdx.x; w < (nsb >> 5); w += kBlock) sbits[w] = hbits[(B.sb_off >> 5) + w];
+    const uint32_t* __restrict__ gbits = hbits + (B.sb_off >> 5);
+    {
+        const uint32_t* uc = ucell + (size_t)blockIdx.y * kSampLds * kHotCellWords;
+        for (int w = threadIdx.x; w < L.ns * kHotCellWords; w += kBlock) ucw[w] = uc[w];
+    }
+    (void)stage_samp(L, samp, &sl);   // (its barriers publish the stages above; the launch checked ns <= kSampLds)
+    const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
+    const uint32_t rk = rounds[blockIdx.z];
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    constexpr int64_t per = (int64_t)R * kBlock;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const SampShared src{&sl, __builtin_amdgcn_readfirstlane(sl.steps)};
+    int wn = 0;        // this wave's buffered list entries (wave-uniform)
+    int qh = 0, qn = 0;   // its ring's head and count (wave-uniform)
+    bool bad = false;
+    // the ring's first min(qn, 64) entries drawn in fp64 and tested
+    auto drain = [&](int cnt) {
+        bool take = false;
+        int32_t ci = 0;
+        double x = 0.0;
+        if (lane < cnt) {
+            const int e = (qh + lane) & (kHotQ - 1);
+            ci = (int32_t)q_i[wv][e];
+            const uint32_t wp = q_p[wv][e], wu = q_u[wv][e];
+            x = icdf_draw(L, src.comp(wp), wp, wu);
+            bad = bad || x != x;
+            const double f = (x - L.centre - B.xlo) * B.inv_sbw;
+            if (f >= 0.0 && f < (double)nsb) {
+                const int j = (int)f;
+                uint32_t word;
+                if constexpr (LDS_BITS) word = sbits[j >> 5];
+                else word = gbits[j >> 5];
+                take = (word >> (j & 31)) & 1u;
+            } else {
+                take = true;   // outside the bins (or NaN): always listed
+            }
+        }
+        const uint64_t bal = __ballot(take);
+        if (bal) {
+            const int c = __builtin_amdgcn_readfirstlane((int)__popcll(bal));
+            if (wn + c > kHotBuf) {   // (wave-uniform)
+                hot_wave_flush(wn, buf_i[wv], buf_x[wv], hcnt, hidx, hx, cell, hstride, hflag);
+                wn = 0;
+            }
+            if (take) {
+                const int k = wn + (int)lanes_below(bal);
+                buf_i[wv][k] = ci;
+                buf_x[wv][k] = x;
+            }
+            wn += c;
+        }
+        __builtin_amdgcn_wave_barrier();   // (the ring's entries read before they are overwritten)
+    };
+    for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per) {
+        const uint32_t g0 = (uint32_t)(cand_offset + base);
+        const bool paired = (g0 & 1u) == 0;   // (uniform)
+#pragma unroll
+        for (int r = 0; r < R; r += 2) {
+            const uint32_t c0 = tile_cand(r, threadIdx.x, kBlock);
+            uint32_t wp[2], wu[2];
+            if (paired) {
+                const U4 W = philox4x32_10(U4{(g0 + c0) >> 1, 0u, (uint32_t)L.stream, rk}, k0, k1);
+                wp[0] = W.x;
+                wu[0] = W.y;
+                wp[1] = W.z;
+                wu[1] = W.w;
+            } else {
+                draw_words(L, k0, k1, g0 + c0, rk, wp[0], wu[0]);
+                draw_words(L, k0, k1, g0 + c0 + 1u, rk, wp[1], wu[1]);
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int64_t i = base + (int64_t)c0 + h;
+                const int k = src.pick_index(wp[h]);
+                const uint32_t uc = wu[h] >> (32 - kHotCellBits);
+                const bool mark = i < n && ((ucw[k * kHotCellWords + (uc >> 5)] >> (uc & 31)) & 1u);
+                const uint64_t bal = __ballot(mark);
+                if (!bal) continue;
+                if (mark) {
+                    const int e = (qh + qn + (int)lanes_below(bal)) & (kHotQ - 1);
+                    q_i[wv][e] = (uint32_t)i;
+                    q_p[wv][e] = wp[h];
+                    q_u[wv][e] = wu[h];
+                }
+                qn += (int)__popcll(bal);
+                __builtin_amdgcn_wave_barrier();
+                if (qn >= 64) {   // (wave-uniform)
+                    drain(64);
+                    qh = (qh + 64) & (kHotQ - 1);
+                    qn -= 64;
+                }
+            }
+        }
+    }
+    if (qn > 0) drain(qn);
+    if (bad) atomicOr(err, 1);
+    // the end: every wave's remainder to the cell's list behind ONE atomic
+    // for the workgroup (a shard's round has few cells, each striped over
+    // many workgroups: per-wave atomics on its one counter cost 0.5 ms)
+    __shared__ int wcnt[kBlock / 64], wbase;
+    if (lane == 0) wcnt[wv] = wn;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) tot += wcnt[w];
+        wbase = tot ? atomicAdd(hcnt + cell, tot) : 0;
+        // a cell's list is hstride long: past it the round falls back to
+        // screening every candidate (hflag bit 2), so nothing is lost
+        if (tot && wbase + tot > hstride) atomicOr(hflag, 2);
+    }
+    __syncthreads();
+    int off = wbase;
+    for (int w = 0; w < wv; ++w) off += wcnt[w];
+    for (int k = lane; k < wn; k += 64)
+        if (off + k < hstride) {
+            hidx[cell * (size_t)hstride + off + k] = buf_i[wv][k];
+            hx[cell * (size_t)hstride + off + k] = buf_x[wv][k];
+        }
+    // the workgroup that finishes last numbers k_screen_hot's work items
+    // (round 6: k_hot_items was a launch of its own)
+    __shared__ bool last;
+    if (threadIdx.x == 0) {
+        __threadfence();   // (this workgroup's count and entries before the counter)
+        last = atomicAdd(done, 1u) == gridDim.x * gridDim.y * gridDim.z - 1;
+    }
+    __syncthreads();
+    if (!last) return;   // (uniform)
+    __threadfence();     // (acquire: every cell's count)
+    const int64_t cells = (int64_t)gridDim.y * gridDim.z;
+    hot_items_body<kBlock>(hcnt, cells, hstride, item_per, items, items + cells + 1);
+}
+
+
 // The expansion screen over the listed candidates only, one pass of R * 256
-// listed candidates per work item (k_hot_items): a persistent grid whose
+// listed candidates per work item (numbered by k_hot_bx's last workgroup): a persistent grid whose
 // workgroups stage the exp table once and take items from a counter until
 // none are left -- round 3's grid of 128 workgroups per cell staged the 32 KB
 // table for about one pass each and left the cells with long lists to a
@@ -1155,8 +1183,7 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
     const int32_t* __restrict__ hcnt, const int32_t* __restrict__ hidx, const double* __restrict__ hx,
     double* __restrict__ hi, unsigned long long* __restrict__ lbkey, int32_t* __restrict__ cnt,
     int32_t* __restrict__ idx, unsigned long long* __restrict__ terms, const float2* __restrict__ sb,
-    unsigned long long* __restrict__ tkey, int64_t hstride, const int32_t* __restrict__ hatt,
-    const SampRec* __restrict__ samp, uint64_t seed, const uint32_t* __restrict__ rounds, int64_t cand_offset) {
+    unsigned long long* __restrict__ tkey, int64_t hstride) {
     constexpr int64_t per = (int64_t)R * kBlock;
     __shared__ double exp_tab[kExpTabSize];
     __shared__ int item_sh;
@@ -1183,7 +1210,6 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
         const BxLabel B = bx[li];
         const bool lgmm = L.mode == DENSE_LGMM;
         const int64_t nsb = (int64_t)B.nbins * kBxSub;
-        const uint32_t rk = hatt ? rounds[cell / (size_t)nl] : 0u;
         uint64_t kl = 0;   // the largest sub-bin L of the listed candidates
         double x[R];
         int64_t ci[R];
@@ -1192,18 +1218,7 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
         for (int r = 0; r < R; ++r) {
             const int64_t j = j0 + r * kBlock + threadIdx.x;
             valid[r] = j < m;
-            double d = 0.0;   // the raw draw
-            if (valid[r]) {
-                if (hatt) {   // k_hot_bx32's (index, attempt): the fp64 draw again, bit for bit
-                    const int32_t a = hatt[cell * (size_t)hstride + j];
-                    const uint32_t g = (uint32_t)(cand_offset + hidx[cell * (size_t)hstride + j]);
-                    d = a >= 0 ? draw_attempt(L, SampGlobal{samp + L.samp_off, L.ns}, (uint32_t)seed,
-                                              (uint32_t)(seed >> 32), g, (uint32_t)a, rk)
-                               : __builtin_nan("");   // (the attempt cap: k_hot_bx32 raised err)
-                } else {
-                    d = hx[cell * (size_t)hstride + j];
-                }
-            }
+            const double d = valid[r] ? hx[cell * (size_t)hstride + j] : 0.0;   // the raw draw
             x[r] = lgmm ? lgmm_value(d) : d;
             ci[r] = valid[r] ? hidx[cell * (size_t)hstride + j] : 0;
             const double f = (d - L.centre - B.xlo) * B.inv_sbw;   // k_hot_bx's sub-bin
@@ -1256,50 +1271,6 @@ __global__ __launch_bounds__(kBlock) void k_hot_probe(const DLabel* __restrict__
     p_out[i] = pm;
 }
 
-// fallback flag: a cell whose largest candidate L stayed below tau0 (the
-// list may miss candidates that can win: the round re-runs k_screen_bx)
-__global__ __launch_bounds__(kBlock) void k_hot_check(int64_t cells, int32_t nl,
-                                                      const unsigned long long* __restrict__ tkey,
-                                                      const unsigned long long* __restrict__ tau0,
-                                                      int32_t* __restrict__ flag) {
-    for (int64_t c = threadIdx.x; c < cells; c += kBlock)
-        if (tkey[c] < tau0[c % nl]) atomicOr(flag, 1);
-}
-
-// The expansion screen's per-cell lists (candidate index, upper bound) hold
-// every candidate whose bound reached its workgroup's best lower bound;
-// keep those that reach the cell's (the round's) best, compacted in place.
-// One workgroup per cell; chunks in order, so writes never pass reads.
-__global__ __launch_bounds__(kBlock) void k_select_list(const double* __restrict__ hi, int64_t stride,
-                                                        const unsigned long long* __restrict__ lbkey,
-                                                        int32_t* __restrict__ cnt, int32_t* __restrict__ idx) {
-    const size_t cell = blockIdx.x;
-    const uint64_t lb = lbkey[cell];
-    const int len = cnt[cell];
-    int32_t* il = idx + cell * (size_t)stride;
-    const double* hl = hi + cell * (size_t)stride;
-    __shared__ int shc[kBlock / 64];
-    int out = 0;
-    for (int j0 = 0; j0 < len; j0 += kBlock) {
-        const int j = j0 + threadIdx.x;
-        const bool keep = j < len && order_key(hl[j]) >= lb;
-        const int32_t v = j < len ? il[j] : 0;
-        const uint64_t m = __ballot(keep);
-        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-        if (lane == 0) shc[wave] = __popcll(m);
-        __syncthreads();   // every read of this chunk is done
-        int at = out + __popcll(m & ((1ull << lane) - 1ull));
-        int tot = 0;
-        for (int w = 0; w < kBlock / 64; ++w) {
-            if (w < wave) at += shc[w];
-            tot += shc[w];
-        }
-        if (keep) il[at] = v;
-        out += tot;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) cnt[cell] = out;
-}
 
 // Each workgroup owns a contiguous slice of its (round, label) row: it
 // counts its takers, reserves their places with ONE atomic (a per-wave
@@ -1355,13 +1326,6 @@ __global__ __launch_bounds__(kBlock) void k_select(const H* __restrict__ hi, int
 }
 
 // empty partials for the rows (round blockIdx.z, label group[blockIdx.y])
-__global__ __launch_bounds__(kBlock) void k_fill_empty(const int32_t* __restrict__ group,
-                                                       int32_t n_labels, int32_t tiles,
-                                                       Partial* __restrict__ partials) {
-    Partial* prow = partials + ((size_t)blockIdx.z * n_labels + group[blockIdx.y]) * tiles;
-    for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < tiles; t += (int64_t)gridDim.x * kBlock)
-        prow[t] = Partial{0, INT64_MAX, 0.0, 0.0, 0.0};
-}
 
 // One workgroup per kRescoreR * 256 re-scored candidates of one (round,
 // label) (chunk table from the host: cell = round * nl + label position);
@@ -1401,10 +1365,6 @@ constexpr int kBxR = TPE_BX_R;
 #define TPE_HOT_R 6   // (8 spilled 8 VGPRs at the 96-register cap: 48 MB of scratch writes per round, r4aj)
 #endif
 constexpr int kHotR = TPE_HOT_R;
-#ifndef TPE_HOT_R32
-#define TPE_HOT_R32 4   // k_hot_bx32 (fp32 draw)
-#endif
-constexpr int kHotR32 = TPE_HOT_R32;
 constexpr unsigned kHotScreenWgs = 1024;   // k_screen_hot's persistent grid (4 workgroups per CU: LDS)
 #ifndef TPE_HOT_WGS
 #define TPE_HOT_WGS 16384
@@ -1432,11 +1392,13 @@ constexpr int kCatR = 8;  // candidates per thread, k_cat_tiles
 // its entries with grids sized for the largest table.
 using RescorePlan = tpe_rt::RescorePlanH;
 constexpr int kPlanBlock = 1024;
-__global__ __launch_bounds__(kPlanBlock) void k_rescore_plan(const int32_t* __restrict__ cnt, int64_t cells,
-                                                             int32_t per_full, int64_t sliced_max, int64_t cap,
-                                                             RescoreChunk* __restrict__ chunks,
-                                                             int64_t* __restrict__ range, int64_t* __restrict__ eoff,
-                                                             RescorePlan* __restrict__ plan) {
+// (every thread of a B-thread workgroup calls it)
+template <int B>
+__device__ __forceinline__ void rescore_plan_body(const int32_t* __restrict__ cnt, int64_t cells, int32_t per_full,
+                                                  int64_t sliced_max, int64_t cap, RescoreChunk* __restrict__ chunks,
+                                                  int64_t* __restrict__ range, int64_t* __restrict__ eoff,
+                                                  RescorePlan* __restrict__ plan) {
+    constexpr int kPlanBlock = B;
     constexpr int W = kPlanBlock / 64;
     __shared__ int64_t wsum[W];
     __shared__ int64_t tot_sh;
@@ -1504,6 +1466,70 @@ __global__ __launch_bounds__(kPlanBlock) void k_rescore_plan(const int32_t* __re
         if (eoff) eoff[cells] = ecarry;
         *plan = RescorePlan{total, (int32_t)carry, sliced ? 1 : 0, 0, 0};
     }
+}
+
+// The expansion screen's per-cell lists (candidate index, upper bound) hold
+// every candidate whose bound reached its workgroup's best lower bound;
+// keep those that reach the cell's (the round's) best, compacted in place.
+// One workgroup per cell; chunks in order, so writes never pass reads.
+// Fused into the same launch (round 6: two launches fewer on every round's
+// critical path): the hot-bin prefilter's check of the cell (tkey: its
+// largest listed L against tau0 -> the fallback flag; nullptr without the
+// prefilter), and, by the workgroup that finishes last (done: a counter the
+// round's fills zero), the re-score plan over every cell's count.
+__global__ __launch_bounds__(kBlock) void k_select_plan(const double* __restrict__ hi, int64_t stride,
+                                                        const unsigned long long* __restrict__ lbkey,
+                                                        int32_t* __restrict__ cnt, int32_t* __restrict__ idx,
+                                                        const unsigned long long* __restrict__ tkey,
+                                                        const unsigned long long* __restrict__ tau0, int32_t nl,
+                                                        int32_t* __restrict__ hflag, uint32_t* __restrict__ done,
+                                                        int32_t per_full, int64_t sliced_max, int64_t cap,
+                                                        RescoreChunk* __restrict__ chunks,
+                                                        int64_t* __restrict__ range, RescorePlan* __restrict__ plan) {
+    const size_t cell = blockIdx.x;
+    const uint64_t lb = lbkey[cell];
+    const int len = cnt[cell];
+    int32_t* il = idx + cell * (size_t)stride;
+    const double* hl = hi + cell * (size_t)stride;
+    __shared__ int shc[kBlock / 64];
+    __shared__ bool last;
+    int out = 0;
+    for (int j0 = 0; j0 < len; j0 += kBlock) {
+        const int j = j0 + threadIdx.x;
+        const bool keep = j < len && order_key(hl[j]) >= lb;
+        const int32_t v = j < len ? il[j] : 0;
+        const uint64_t m = __ballot(keep);
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        if (lane == 0) shc[wave] = __popcll(m);
+        __syncthreads();   // every read of this chunk is done
+        int at = out + __popcll(m & ((1ull << lane) - 1ull));
+        int tot = 0;
+        for (int w = 0; w < kBlock / 64; ++w) {
+            if (w < wave) at += shc[w];
+            tot += shc[w];
+        }
+        if (keep) il[at] = v;
+        out += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        cnt[cell] = out;
+        if (tkey && tkey[cell] < tau0[cell % (size_t)nl]) atomicOr(hflag, 1);
+        __threadfence();   // (the count and the list before the counter)
+        last = atomicAdd(done, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;   // (uniform)
+    __threadfence();     // (acquire: every cell's count and list)
+    rescore_plan_body<kBlock>(cnt, (int64_t)gridDim.x, per_full, sliced_max, cap, chunks, range, nullptr, plan);
+}
+
+__global__ __launch_bounds__(kPlanBlock) void k_rescore_plan(const int32_t* __restrict__ cnt, int64_t cells,
+                                                             int32_t per_full, int64_t sliced_max, int64_t cap,
+                                                             RescoreChunk* __restrict__ chunks,
+                                                             int64_t* __restrict__ range, int64_t* __restrict__ eoff,
+                                                             RescorePlan* __restrict__ plan) {
+    rescore_plan_body<kPlanBlock>(cnt, cells, per_full, sliced_max, cap, chunks, range, eoff, plan);
 }
 
 template <int R>
@@ -1576,9 +1602,9 @@ __global__ __launch_bounds__(kBlock) void k_rescore(
 // The re-score of a few candidates per (round, dense label) -- the
 // expansion screen leaves a handful of near-ties -- split by summation
 // slices so it fills the chip instead of one wave per label walking 10k
-// components: k_rescore_draw re-draws each listed candidate once,
-// k_rescore_slices sums one kSumSlice slice of one mixture for the 64
-// candidates of a table entry per wave, and k_rescore_fin adds the slices in
+// components: k_rescore_slices re-draws an entry's candidates and sums one
+// kSumSlice slice of one mixture for the 64 candidates of the entry per
+// wave, and k_rescore_fin adds the slices in
 // order (lse_acc's order: the bits of the fp64 round) and keeps the entry's
 // best.  Entry = RescoreChunk{cell, j}: candidates [64 j, 64 j + 64) of the
 // cell's list.  part: [entry][s_max slices][64].  The entries come from
@@ -1601,36 +1627,35 @@ __device__ __forceinline__ double ordered_sum(const double* __restrict__ p, int 
     return acc;
 }
 
-__global__ __launch_bounds__(kBlock) void k_rescore_draw(
-    const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
-    const SampRec* __restrict__ samp, int64_t stride, int64_t cand_offset, uint64_t seed,
-    const uint32_t* __restrict__ rounds, int32_t nl, const RescorePlan* __restrict__ plan,
-    const int32_t* __restrict__ cnt, const int32_t* __restrict__ idx, const RescoreChunk* __restrict__ chunks,
-    double* __restrict__ xbuf, int64_t* __restrict__ gbuf) {
-    if (!plan->sliced) return;
-    const int32_t ne = plan->ne;
-    const int lane = threadIdx.x % kRsW;
-    for (int e = blockIdx.x * (kBlock / kRsW) + threadIdx.x / kRsW; e < ne; e += gridDim.x * (kBlock / kRsW)) {
-    const RescoreChunk ch = chunks[e];
-    const int32_t z = ch.cell / nl, y = ch.cell % nl;
-    const DLabel L = labels[group[y]];
+// The entry's candidate of this lane (the round's draw, re-drawn from its
+// index): value and global index, NaN / -1 past the cell's count
+__device__ __forceinline__ void rescore_cand(const DLabel& L, const SampRec* __restrict__ samp, int64_t stride,
+                                             int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds,
+                                             int32_t nl, const int32_t* __restrict__ cnt,
+                                             const int32_t* __restrict__ idx, const RescoreChunk& ch, int lane,
+                                             double& v, int64_t& g) {
+    const int32_t z = ch.cell / nl;
     const int64_t j = (int64_t)ch.j * kRsW + lane;
-    double v = __builtin_nan("");
-    int64_t g = -1;
+    v = __builtin_nan("");
+    g = -1;
     if (j < cnt[ch.cell]) {
         g = cand_offset + idx[(size_t)ch.cell * (size_t)stride + j];
         if (L.mode == DENSE_LGMM) (void)sample_below<DENSE_LGMM>(L, samp + L.samp_off, seed, rounds[z], (uint32_t)g, v);
         else (void)sample_below<DENSE_GMM>(L, samp + L.samp_off, seed, rounds[z], (uint32_t)g, v);
     }
-    xbuf[(size_t)e * kRsW + lane] = v;
-    gbuf[(size_t)e * kRsW + lane] = g;
-    }
 }
 
+// One wave per (entry of kRsW candidates, summation slice): each wave
+// re-draws its entry's candidates (round 6: the draw kernel before it was a
+// launch of its own) and sums its slice in order; the first slice's wave
+// also stores the candidates for k_rescore_fin.  Grid (slice groups,
+// entries strided).
 __global__ __launch_bounds__(kBlock) void k_rescore_slices(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
-    const Comp<double>* __restrict__ comps64, int32_t nl, const RescoreChunk* __restrict__ chunks,
-    const RescorePlan* __restrict__ plan, const double* __restrict__ xbuf, int32_t s_max,
+    const Comp<double>* __restrict__ comps64, const SampRec* __restrict__ samp, int64_t stride,
+    int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, int32_t nl,
+    const int32_t* __restrict__ cnt, const int32_t* __restrict__ idx, const RescoreChunk* __restrict__ chunks,
+    const RescorePlan* __restrict__ plan, double* __restrict__ xbuf, int64_t* __restrict__ gbuf, int32_t s_max,
     double* __restrict__ part) {
     if (!plan->sliced) return;
     const int32_t ne = plan->ne;
@@ -1644,10 +1669,16 @@ __global__ __launch_bounds__(kBlock) void k_rescore_slices(
     const int nsb = (L.nb + kSumSlice - 1) / kSumSlice, nsa = (L.na + kSumSlice - 1) / kSumSlice;
     const int slice = blockIdx.x * (kBlock / 64) + wave;
     if (slice >= nsb + nsa) continue;   // (no barrier below)
+    double x;
+    int64_t g;
+    rescore_cand(L, samp, stride, cand_offset, seed, rounds, nl, cnt, idx, ch, lane, x, g);
+    if (slice == 0) {
+        xbuf[(size_t)e * kRsW + lane] = x;
+        gbuf[(size_t)e * kRsW + lane] = g;
+    }
     const bool above = slice >= nsb;
     const int k0 = (above ? slice - nsb : slice) * kSumSlice;
     const int k1 = min(k0 + kSumSlice, above ? L.na : L.nb);
-    const double x = xbuf[(size_t)e * kRsW + lane];
     const double xr[1] = {(L.mode == DENSE_LGMM ? flog(x) : x) - L.centre};
     double acc[1] = {0.0};
     lse_acc_run<1>(comps64 + (above ? L.comp_a : L.comp_b) + k0, k1 - k0, xr, acc, exp_tab);
@@ -1655,15 +1686,26 @@ __global__ __launch_bounds__(kBlock) void k_rescore_slices(
     }
 }
 
+// The re-score's end: per entry (one wave each, entries strided) the slice
+// sums added in order, the logs and the entry's maxloc into res[entry];
+// then the workgroup that finishes last (done: zeroed by the round's fills)
+// keeps each (round, dense label) cell's best entry in the row's first
+// partial slot -- an empty record when the cell listed nothing -- which is
+// all k_reduce reads of a dense row on this path (round 6: k_rescore_merge
+// and k_fill_empty were launches of their own).  The chunked re-score
+// (k_rescore, a plan past kSlicedRescoreMax) runs before this kernel and
+// leaves its entries' records in res too.
 __global__ __launch_bounds__(kRsW) void k_rescore_fin(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
     const Comp<double>* __restrict__ comps64, int32_t nl, const RescoreChunk* __restrict__ chunks,
     const RescorePlan* __restrict__ plan, const double* __restrict__ xbuf, const int64_t* __restrict__ gbuf,
-    int32_t s_max, const double* __restrict__ part, Partial* __restrict__ res) {
-    if (!plan->sliced) return;
+    int32_t s_max, const double* __restrict__ part, Partial* __restrict__ res, uint32_t* __restrict__ done,
+    int64_t cells, int32_t n_labels, int32_t tiles, const int64_t* __restrict__ range,
+    Partial* __restrict__ partials) {
+    const bool sliced = plan->sliced != 0;
     const int32_t ne = plan->ne;
     const int lane = threadIdx.x;
-    for (int e = blockIdx.x; e < ne; e += gridDim.x) {
+    for (int e = blockIdx.x; sliced && e < ne; e += gridDim.x) {
     const RescoreChunk ch = chunks[e];
     const DLabel L = labels[group[ch.cell % nl]];
     const bool lgmm = L.mode == DENSE_LGMM;
@@ -1705,25 +1747,23 @@ __global__ __launch_bounds__(kRsW) void k_rescore_fin(
     }
     if (lane == 0) res[e] = Partial{bk, bi, bv, bl, ba};
     }
-}
-
-// one thread per (round, dense label) cell: the best of its re-score chunks
-// (consecutive in the table from first = range >> 32, count = low bits) into
-// the row's first partial slot (k_fill_empty cleared the row)
-__global__ __launch_bounds__(kBlock) void k_rescore_merge(const int32_t* __restrict__ group, int32_t nl,
-                                                          int64_t cells, int32_t n_labels, int32_t tiles,
-                                                          const int64_t* __restrict__ range,
-                                                          const Partial* __restrict__ res,
-                                                          Partial* __restrict__ partials) {
-    const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (c >= cells) return;
-    const int64_t first = range[c] >> 32, count = range[c] & 0xffffffffll;
-    if (count == 0) return;
-    Partial best = res[first];
-    for (int64_t j = 1; j < count; ++j)
-        if (better(res[first + j].key, res[first + j].idx, best.key, best.idx)) best = res[first + j];
-    const int64_t z = c / nl;
-    partials[((size_t)z * n_labels + group[c % nl]) * tiles] = best;
+    __shared__ bool last;
+    if (lane == 0) {
+        __threadfence();   // (this workgroup's records before the counter)
+        last = atomicAdd(done, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;   // (uniform)
+    __threadfence();     // (acquire: every entry's record)
+    const bool over = plan->overflow != 0;   // (no table: every cell empty -- cannot happen on the tile map)
+    for (int64_t c = lane; c < cells; c += kRsW) {
+        const int64_t first = over ? 0 : range[c] >> 32, count = over ? 0 : range[c] & 0xffffffffll;
+        Partial best{0, INT64_MAX, 0.0, 0.0, 0.0};
+        for (int64_t j = 0; j < count; ++j)
+            if (better(res[first + j].key, res[first + j].idx, best.key, best.idx)) best = res[first + j];
+        const int64_t z = c / nl;
+        partials[((size_t)z * n_labels + group[c % nl]) * tiles] = best;
+    }
 }
 
 // ---------------------------------------- fp32 screen (packed map) ----
@@ -2893,7 +2933,6 @@ __global__ __launch_bounds__(kBlock, 4) void k_qfused_tiles(
     const bool staged = stage_samp(L, samp, &sl);
     const QInfo Q = qinfo[qbase + blockIdx.y];
     const uint32_t rk = rounds[blockIdx.z];
-    __shared__ RetryLds<R> retry;
     // the window's scores as order keys in LDS when they fit: per candidate
     // one LDS read; the winner's lpdfs are read from the table at the end
     __shared__ unsigned long long skey[kQLdsKeys];
@@ -2907,7 +2946,6 @@ __global__ __launch_bounds__(kBlock, 4) void k_qfused_tiles(
     const bool early = found && Q.G > 0 && Q.jlo <= Q.jhi;
     const uint64_t kmax = early ? qkmax[qbase + blockIdx.y] : 0;
     __syncthreads();
-    int par = 0;
     bool reported = false;
     int64_t ndrawn = 0;
     uint64_t bk = 0;
@@ -2925,10 +2963,8 @@ __global__ __launch_bounds__(kBlock, 4) void k_qfused_tiles(
             if (base + tile_cand(r, threadIdx.x, kBlock) < n) pend |= 1u << r;
         }
         const uint32_t g0 = (uint32_t)(cand_offset + base);
-        const bool ok = staged ? sample_tile<MODE, R>(L, SampShared{&sl}, seed, rk, g0, pend, v, retry, par)
-                               : sample_tile<MODE, R>(L, SampGlobal{samp + L.samp_off, L.ns}, seed, rk, g0, pend,
-                                                      v, retry, par);
-        par ^= 1;
+        const bool ok = staged ? sample_tile<MODE, R>(L, SampShared{&sl}, seed, rk, g0, pend, v)
+                               : sample_tile<MODE, R>(L, SampGlobal{samp + L.samp_off, L.ns}, seed, rk, g0, pend, v);
         if (!ok) atomicOr(err, 1);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -3098,11 +3134,19 @@ __device__ __forceinline__ tpe_label_result to_result(const Partial& p, int li) 
 // workgroup per label streams up to 8192 partials at full memory parallelism
 // instead of one dependent 40-byte load chain per thread.
 constexpr int kReduceBlock = 1024;
+// (dense_one: the dense labels' rows hold their winner in the first slot
+// only -- the screened tile map's k_rescore_fin -- and the rest is not read)
 __global__ __launch_bounds__(kReduceBlock) void k_reduce(const Partial* __restrict__ partials,
-                                                         int32_t tiles, int32_t n_labels,
-                                                         tpe_label_result* __restrict__ out) {
+                                                         int32_t tiles_all, int32_t n_labels,
+                                                         tpe_label_result* __restrict__ out,
+                                                         const DLabel* __restrict__ labels, int32_t dense_one) {
     const int li = blockIdx.x, rz = blockIdx.y, tid = threadIdx.x;
-    const Partial* p = partials + ((size_t)rz * n_labels + li) * tiles;
+    const Partial* p = partials + ((size_t)rz * n_labels + li) * tiles_all;
+    int32_t tiles = tiles_all;
+    if (dense_one) {
+        const int32_t mode = labels[li].mode;
+        if (mode == DENSE_GMM || mode == DENSE_LGMM) tiles = 1;
+    }
     uint64_t bk[4] = {0, 0, 0, 0};
     int64_t bi[4] = {INT64_MAX, INT64_MAX, INT64_MAX, INT64_MAX};
     int32_t bt[4] = {-1, -1, -1, -1};
@@ -3827,6 +3871,13 @@ int hot_tau_prepare(tpe_ctx* ctx, int64_t n) {
     const int64_t words = (P.bx_sb_max + 31) / 32;
     hipLaunchKernelGGL(k_hot_bits, dim3((unsigned)((words + kBlock - 1) / kBlock), nl), dim3(kBlock), 0,
                        ctx->stream, grp, P.bx.p, P.bx_sb.p, ctx->hot_tau0.p, ctx->hot_bits.p);
+    // the sampling components' u-cells (k_hot_bx decides most candidates from them)
+    HIPCHK(ctx, ctx->hot_pc.reserve((size_t)(P.bx_sb.cap + 31) / 32));
+    HIPCHK(ctx, ctx->hot_ucell.reserve((size_t)nl * kSampLds * kHotCellWords));
+    hipLaunchKernelGGL(k_hot_prefix, dim3((unsigned)nl), dim3(1024), 0, ctx->stream, grp, P.bx.p, ctx->hot_bits.p,
+                       ctx->hot_pc.p);
+    hipLaunchKernelGGL(k_hot_ucells, dim3(kHotCells / kBlock, kSampLds, nl), dim3(kBlock), 0, ctx->stream, P.labels.p,
+                       grp, P.samp.p, P.bx.p, ctx->hot_bits.p, ctx->hot_pc.p, ctx->hot_ucell.p);
     ctx->hot_tau0_gen = ctx->hot == 2 ? 0 : P.bx_gen;
     ctx->hot_tau0_n = n;
     return ctx->hip(hipGetLastError(), "hot-bin threshold launch");
@@ -3840,6 +3891,23 @@ int64_t hot_stride(const tpe_ctx* ctx, int64_t n) {
     return std::min<int64_t>(n, std::max<int64_t>(kHotMinCap, (int64_t)((double)n / ctx->hot_cap_div)));
 }
 
+// the re-score's table, plan and sliced buffers for `cells` lists of up
+// to lst candidates
+int rescore_reserve(tpe_ctx* ctx, size_t cells, int64_t lst, int32_t s_max) {
+    const int64_t per_full = (int64_t)kRescoreR * kBlock;
+    const int64_t ne_sliced = (int64_t)cells + kSlicedRescoreMax / kRsW;
+    const int64_t ne_full = (int64_t)cells + ((int64_t)cells * lst + per_full - 1) / per_full;
+    const int64_t ne_cap = std::max(ne_sliced, ne_full);
+    HIPCHK(ctx, ctx->scr_chunks.reserve(ne_cap));
+    HIPCHK(ctx, ctx->scr_res.reserve(ne_cap));
+    HIPCHK(ctx, ctx->scr_off.reserve(cells));
+    HIPCHK(ctx, ctx->rs_plan.reserve(3));   // (RescorePlan: 24 B)
+    HIPCHK(ctx, ctx->rs_x.reserve((size_t)ne_sliced * kRsW));
+    HIPCHK(ctx, ctx->rs_g.reserve((size_t)ne_sliced * kRsW));
+    HIPCHK(ctx, ctx->rs_part.reserve((size_t)ne_sliced * s_max * kRsW));
+    return TPE_OK;
+}
+
 template <typename T>
 int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
     const int nl = g.count[DENSE_GMM] + g.count[DENSE_LGMM];
@@ -3851,7 +3919,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
     const int nch = a.S.cpack ? dense_chunks(ctx, a.gx_whole, nl) : 1;
     if (sizeof(T) == 8 && ctx->screen && a.S.cpack == 0) {   // fp32 screen + fp64 re-score
         const size_t cells = (size_t)a.n_rounds * nl;
-        bool use_bx = false, hot = false;
+        bool use_bx = false, hot = false, plan_done = false;
         ctx->hot_ran = false;
         ctx->hot_listed = 0;
         ctx->hot_fallback = 0;
@@ -3875,6 +3943,19 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
         FillSet fs{};
         add_fill(fs, ctx->scr_lb.p, cells * sizeof(unsigned long long), 0);
         add_fill(fs, ctx->scr_cnt.p, cells * sizeof(int32_t), 0);
+        // the tail's last-workgroup counters (k_select_plan, k_rescore_fin)
+        // and the hot list's item counter (k_hot_bx's last workgroup)
+        HIPCHK(ctx, ctx->rs_done.reserve(4));
+        add_fill(fs, ctx->rs_done.p, 4 * sizeof(uint32_t), 0);
+        // the re-score's buffers, planned on the device from the counts:
+        // sliced for a few near-ties, chunks of kRescoreR * 256 otherwise
+        // (sized for the largest table either plan can make)
+        int32_t s_max = 1;
+        for (int m : {DENSE_GMM, DENSE_LGMM})
+            for (int li : ctx->P->h_group[m]) {
+                const DLabel& d = ctx->P->h_labels[li];
+                s_max = std::max(s_max, (d.nb + kSumSlice - 1) / kSumSlice + (d.na + kSumSlice - 1) / kSumSlice);
+            }
         const unsigned sx = (unsigned)std::min<int64_t>((a.n + 8 * kBlock - 1) / (8 * kBlock), 1024);
         ctx->screen_mode = use_bx ? 3 : (ctx->window && a.n >= kWinMinN && a.cand_in == nullptr) ? 2 : 1;
         if (!use_bx) {   // the expansion screen adds its own resets to the same launch
@@ -3887,8 +3968,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
             HIPCHK(ctx, ctx->win_evals.reserve(1));
             add_fill(fs, ctx->win_evals.p, sizeof(unsigned long long), 0);
             if (hot) {
-                if (ctx->hot32) HIPCHK(ctx, ctx->hot_a.reserve(cells * lst));
-                else HIPCHK(ctx, ctx->hot_x.reserve(cells * lst));
+                HIPCHK(ctx, ctx->hot_x.reserve(cells * lst));
                 HIPCHK(ctx, ctx->hot_i.reserve(cells * lst));
                 HIPCHK(ctx, ctx->hot_cnt.reserve(cells));
                 HIPCHK(ctx, ctx->hot_t.reserve(cells));
@@ -3915,52 +3995,46 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                 // (a workgroup stages its tables first: a label shard's few
                 // cells at one or two tiles per workgroup ran 0.54 ms instead
                 // of 0.46) unless the chip needs more to fill it
-                const int64_t hr = ctx->hot32 ? kHotR32 : kHotR;
+                const int64_t hr = kHotR;
                 const int64_t tiles_c = (a.n + hr * kBlock - 1) / (hr * kBlock);
                 const int64_t per_cell = std::min<int64_t>(
                     {tiles_c, kHotBxWgs / cells_l,
                      std::max<int64_t>((kHotFillWgs + cells_l - 1) / cells_l, tiles_c / kHotMinTiles)});
                 const dim3 hg((unsigned)std::max<int64_t>(1, per_cell), nl, a.gz);
-                if (ctx->hot32) {
-                    if (P.bx_sb_max <= (int64_t)kHotLdsWords * 32)
-                        hipLaunchKernelGGL((k_hot_bx32<kHotR32, true>), hg, dim3(kBlock), 0, ctx->stream, P.labels.p,
-                                           grp, P.samp.p, P.bx.p, ctx->hot_bits.p, a.n, a.cand_offset, a.seed,
-                                           ctx->rounds.p, nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_a.p,
-                                           ctx->errflag.p, lst, ctx->hot_flag.p, ctx->hot32 == 2 ? 4096.0f : 1.0f);
-                    else
-                        hipLaunchKernelGGL((k_hot_bx32<kHotR32, false>), hg, dim3(kBlock), 0, ctx->stream, P.labels.p,
-                                           grp, P.samp.p, P.bx.p, ctx->hot_bits.p, a.n, a.cand_offset, a.seed,
-                                           ctx->rounds.p, nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_a.p,
-                                           ctx->errflag.p, lst, ctx->hot_flag.p, ctx->hot32 == 2 ? 4096.0f : 1.0f);
-                } else if (P.bx_sb_max <= (int64_t)kHotLdsWords * 32)
+                HIPCHK(ctx, ctx->hot_items.reserve((size_t)cells + 2));
+                if (P.bx_sb_max <= (int64_t)kHotLdsWords * 32)
                     hipLaunchKernelGGL((k_hot_bx<kHotR, true>), hg, dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
-                                       P.samp.p, P.bx.p, ctx->hot_bits.p, a.n, a.cand_offset, a.seed, ctx->rounds.p,
-                                       nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p, ctx->errflag.p, lst,
-                                       ctx->hot_flag.p);
+                                       P.samp.p, P.bx.p, ctx->hot_bits.p, ctx->hot_ucell.p, a.n, a.cand_offset,
+                                       a.seed, ctx->rounds.p, nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p,
+                                       ctx->errflag.p, lst, ctx->hot_flag.p, ctx->rs_done.p + 2, ctx->hot_items.p,
+                                       (int64_t)kBxR * kBlock);
                 else
                     hipLaunchKernelGGL((k_hot_bx<kHotR, false>), hg, dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
-                                       P.samp.p, P.bx.p, ctx->hot_bits.p, a.n, a.cand_offset, a.seed, ctx->rounds.p,
-                                       nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p, ctx->errflag.p, lst,
-                                       ctx->hot_flag.p);
-                HIPCHK(ctx, ctx->hot_items.reserve((size_t)cells + 2));
-                hipLaunchKernelGGL((k_hot_items<kBxR>), dim3(1), dim3(1024), 0, ctx->stream, ctx->hot_cnt.p,
-                                   (int64_t)cells, lst, ctx->hot_items.p, ctx->hot_items.p + cells + 1);
+                                       P.samp.p, P.bx.p, ctx->hot_bits.p, ctx->hot_ucell.p, a.n, a.cand_offset,
+                                       a.seed, ctx->rounds.p, nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p,
+                                       ctx->errflag.p, lst, ctx->hot_flag.p, ctx->rs_done.p + 2, ctx->hot_items.p,
+                                       (int64_t)kBxR * kBlock);
                 hipLaunchKernelGGL((k_screen_hot<kBxR>), dim3(kHotScreenWgs), dim3(kBlock), 0, ctx->stream,
                                    P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p, P.bx_loff.p, P.bx_list.p, a.n,
                                    nl, (int64_t)cells, ctx->hot_items.p, ctx->hot_items.p + cells + 1,
                                    ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p, ctx->scr_hid.p, ctx->scr_lb.p,
-                                   ctx->scr_cnt.p, ctx->scr_idx.p, ctx->win_evals.p, P.bx_sb.p, ctx->hot_t.p, lst,
-                                   ctx->hot32 ? ctx->hot_a.p : nullptr, P.samp.p, a.seed, ctx->rounds.p,
-                                   a.cand_offset);
+                                   ctx->scr_cnt.p, ctx->scr_idx.p, ctx->win_evals.p, P.bx_sb.p, ctx->hot_t.p, lst);
             } else {
                 screen_bx_all(ctx, grp, nl, a);
             }
             if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
-            hipLaunchKernelGGL(k_select_list, dim3((unsigned)cells), dim3(kBlock), 0, ctx->stream, ctx->scr_hid.p,
-                               lst, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p);
+            {
+                const int rc = rescore_reserve(ctx, cells, lst, s_max);
+                if (rc) return rc;
+            }
+            hipLaunchKernelGGL(k_select_plan, dim3((unsigned)cells), dim3(kBlock), 0, ctx->stream, ctx->scr_hid.p,
+                               lst, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p, hot ? ctx->hot_t.p : nullptr,
+                               ctx->hot_tau0.p, nl, ctx->hot_flag.p, ctx->rs_done.p, (int32_t)(kRescoreR * kBlock),
+                               kSlicedRescoreMax, (int64_t)cells * lst,
+                               reinterpret_cast<RescoreChunk*>(ctx->scr_chunks.p), ctx->scr_off.p,
+                               reinterpret_cast<RescorePlan*>(ctx->rs_plan.p));
+            plan_done = true;
             if (hot) {
-                hipLaunchKernelGGL(k_hot_check, dim3(1), dim3(kBlock), 0, ctx->stream, (int64_t)cells, nl,
-                                   ctx->hot_t.p, ctx->hot_tau0.p, ctx->hot_flag.p);
                 HIPCHK(ctx, ctx->hot_cnt_h.resize(cells));
                 int rc = defer_read(ctx, ctx->hot_cnt_h.data(), ctx->hot_cnt.p, cells * sizeof(int32_t));
                 if (!rc) rc = defer_read(ctx, &ctx->pin[0].hot_flag, ctx->hot_flag.p, sizeof(int32_t));
@@ -4054,10 +4128,6 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                                a.n, nl, ctx->scr_lb.p, ctx->scr_cnt.p, ctx->scr_idx.p, 0, 0, nl, nullptr);
             ctx->screen_exec += (int64_t)a.n_rounds * a.n * dense_terms(ctx);
         }
-        // the dense rows' partial slots start empty; the re-score entries
-        // overwrite theirs
-        hipLaunchKernelGGL(k_fill_empty, dim3((unsigned)std::min<int64_t>((a.tiles + kBlock - 1) / kBlock, 64), nl, a.gz),
-                           dim3(kBlock), 0, ctx->stream, grp, ctx->P->n_labels, a.tiles, ctx->partials.p);
         HIPCHK(ctx, ctx->scr_cnt_h.resize(cells));
         {
             const int rc = defer_read(ctx, ctx->scr_cnt_h.data(), ctx->scr_cnt.p, cells * sizeof(int32_t));
@@ -4067,49 +4137,37 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
             ctx->hot_ran = true;   // (its lists and flag are read after the round's one sync)
             ctx->hot_cells = (int64_t)cells;
         }
-        // the re-score, planned on the device from the counts: sliced for a
-        // few near-ties, chunks of kRescoreR * 256 otherwise (grids sized for
-        // the largest table either plan can make)
-        int32_t s_max = 1;
-        for (int m : {DENSE_GMM, DENSE_LGMM})
-            for (int li : ctx->P->h_group[m]) {
-                const DLabel& d = ctx->P->h_labels[li];
-                s_max = std::max(s_max, (d.nb + kSumSlice - 1) / kSumSlice + (d.na + kSumSlice - 1) / kSumSlice);
-            }
         const int64_t per_full = (int64_t)kRescoreR * kBlock;
         const int64_t ne_sliced = (int64_t)cells + kSlicedRescoreMax / kRsW;
         const int64_t ne_full = (int64_t)cells + ((int64_t)cells * lst + per_full - 1) / per_full;
-        const int64_t ne_cap = std::max(ne_sliced, ne_full);
-        HIPCHK(ctx, ctx->scr_chunks.reserve(ne_cap));
-        HIPCHK(ctx, ctx->scr_res.reserve(ne_cap));
-        HIPCHK(ctx, ctx->scr_off.reserve(cells));
-        HIPCHK(ctx, ctx->rs_plan.reserve(3));   // (RescorePlan: 24 B)
-        HIPCHK(ctx, ctx->rs_x.reserve((size_t)ne_sliced * kRsW));
-        HIPCHK(ctx, ctx->rs_g.reserve((size_t)ne_sliced * kRsW));
-        HIPCHK(ctx, ctx->rs_part.reserve((size_t)ne_sliced * s_max * kRsW));
         RescoreChunk* chp = reinterpret_cast<RescoreChunk*>(ctx->scr_chunks.p);
         RescorePlan* plan = reinterpret_cast<RescorePlan*>(ctx->rs_plan.p);
-        hipLaunchKernelGGL(k_rescore_plan, dim3(1), dim3(kPlanBlock), 0, ctx->stream, ctx->scr_cnt.p, (int64_t)cells,
-                           (int32_t)per_full, kSlicedRescoreMax, (int64_t)cells * lst, chp, ctx->scr_off.p, nullptr,
-                           plan);
-        const unsigned g_sl = (unsigned)std::min<int64_t>(ne_sliced, 1024);
-        hipLaunchKernelGGL(k_rescore_draw, dim3((unsigned)((ne_sliced + kBlock / kRsW - 1) / (kBlock / kRsW))),
-                           dim3(kBlock), 0, ctx->stream, ctx->P->labels.p, grp, ctx->P->samp.p, lst,
-                           a.cand_offset, a.seed, ctx->rounds.p, nl, plan, ctx->scr_cnt.p, ctx->scr_idx.p, chp,
-                           ctx->rs_x.p, ctx->rs_g.p);
-        hipLaunchKernelGGL(k_rescore_slices, dim3((unsigned)((s_max + 3) / 4), g_sl), dim3(kBlock), 0,
-                           ctx->stream, ctx->P->labels.p, grp, ctx->P->comps64.p, nl, chp, plan, ctx->rs_x.p, s_max,
-                           ctx->rs_part.p);
-        hipLaunchKernelGGL(k_rescore_fin, dim3(g_sl), dim3(kRsW), 0, ctx->stream, ctx->P->labels.p, grp,
-                           ctx->P->comps64.p, nl, chp, plan, ctx->rs_x.p, ctx->rs_g.p, s_max, ctx->rs_part.p,
-                           ctx->scr_res.p);
+        if (!plan_done) {   // (the windowed and fp32 screens' k_select: the plan on its own)
+            const int rc = rescore_reserve(ctx, cells, lst, s_max);
+            if (rc) return rc;
+            chp = reinterpret_cast<RescoreChunk*>(ctx->scr_chunks.p);
+            plan = reinterpret_cast<RescorePlan*>(ctx->rs_plan.p);
+            hipLaunchKernelGGL(k_rescore_plan, dim3(1), dim3(kPlanBlock), 0, ctx->stream, ctx->scr_cnt.p,
+                               (int64_t)cells, (int32_t)per_full, kSlicedRescoreMax, (int64_t)cells * lst, chp,
+                               ctx->scr_off.p, nullptr, plan);
+        }
+        // the chunked re-score (a plan past kSlicedRescoreMax; returns at once
+        // otherwise), then the sliced one, whose end keeps each cell's best in
+        // the row's first partial slot (k_rescore_fin); the grids stride over
+        // the entries -- a round lists a few dozen near-ties
         hipLaunchKernelGGL((k_rescore<kRescoreR>), dim3((unsigned)std::min<int64_t>(ne_full, 512)), dim3(kBlock), 0,
                            ctx->stream, ctx->P->labels.p, grp, ctx->P->comps64.p, ctx->P->samp.p, lst,
                            a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->P->n_labels, a.tiles,
                            ctx->scr_cnt.p, ctx->scr_idx.p, chp, plan, ctx->scr_res.p);
-        hipLaunchKernelGGL(k_rescore_merge, dim3((unsigned)((cells + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                           ctx->stream, grp, nl, (int64_t)cells, ctx->P->n_labels, a.tiles, ctx->scr_off.p,
-                           ctx->scr_res.p, ctx->partials.p);
+        hipLaunchKernelGGL(k_rescore_slices, dim3((unsigned)((s_max + 3) / 4), (unsigned)std::min<int64_t>(ne_sliced, 64)),
+                           dim3(kBlock), 0, ctx->stream, ctx->P->labels.p, grp, ctx->P->comps64.p, ctx->P->samp.p, lst,
+                           a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->scr_cnt.p, ctx->scr_idx.p, chp, plan,
+                           ctx->rs_x.p, ctx->rs_g.p, s_max, ctx->rs_part.p);
+        hipLaunchKernelGGL(k_rescore_fin, dim3((unsigned)std::min<int64_t>(ne_sliced, 256)), dim3(kRsW), 0, ctx->stream,
+                           ctx->P->labels.p, grp, ctx->P->comps64.p, nl, chp, plan, ctx->rs_x.p, ctx->rs_g.p, s_max,
+                           ctx->rs_part.p, ctx->scr_res.p, ctx->rs_done.p + 1, (int64_t)cells, ctx->P->n_labels,
+                           a.tiles, ctx->scr_off.p, ctx->partials.p);
+        ctx->dense_one = true;   // (k_reduce reads a dense row's first slot only)
         ctx->screen_total += (int64_t)cells * a.n;
         ctx->screen_pending = true;
         bracket(ctx, DENSE_GMM, 1);
@@ -4490,6 +4548,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         ctx->screen_rescore_terms = 0;
     }
     if (fam & (1 << CAT)) ctx->cat_early = false;
+    ctx->dense_one = false;
     ctx->pk_plan_pending = false;
     ctx->zw_pending = false;
     ctx->evw_used = 0;
@@ -4582,7 +4641,7 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         HIPCHK(ctx, hipGetLastError());
     } else if (tiles > 1) {
         hipLaunchKernelGGL(k_reduce, dim3(L, n_rounds), dim3(kReduceBlock), 0, ctx->stream,
-                           ctx->partials.p, tiles, L, ctx->results.p);
+                           ctx->partials.p, tiles, L, ctx->results.p, ctx->P->labels.p, ctx->dense_one ? 1 : 0);
         HIPCHK(ctx, hipGetLastError());
     }
     if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->ev2, ctx->stream));
@@ -4638,33 +4697,6 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
                                  only_label);
         ctx->pk_redo = false;
         return rc;
-    }
-    if (dense_on && ctx->hot_ran) {
-        for (int64_t c = 0; c < ctx->hot_cells; ++c) ctx->hot_listed += ctx->hot_cnt_h[c];
-        const int32_t hf = pin.hot_flag;
-        if (hf && !ctx->hot_redo) {
-            // a cell's best lower bound stayed below tau0 (bit 1: its list may
-            // miss a winner) or a list overflowed (bit 2): the round runs
-            // again with every candidate through the expansion screen (the
-            // same draws; its results replace these), and later rounds list
-            // more after an overflow.  The re-run repeats the WHOLE round --
-            // quantized and categorical families, reduction, copies -- so a
-            // fallback round costs about two rounds, and the families' draw
-            // statistics are the second run's (the same draws, the same
-            // winners); tpe_last_hot reports the fallback (bench:
-            // hot_fallbacks), which no test or bench has seen outside the
-            // forced TPE_OPT_HOT = 2
-            if ((hf & 2) && ctx->hot_cap_div > 1.0) ctx->hot_cap_div = std::max(1.0, ctx->hot_cap_div / 4.0);
-            const int64_t listed = ctx->hot_listed;
-            ctx->hot_redo = true;
-            const int rc = run_round(ctx, seed, rounds_h, n_rounds, n, cand_offset, cand_in_dev, olb, ola, out,
-                                     only_label);
-            ctx->hot_redo = false;
-            ctx->hot_ran = true;
-            ctx->hot_fallback = hf;
-            ctx->hot_listed = listed;
-            return rc;
-        }
     }
     const int32_t errh = pin.err;
     ctx->xdrawn_h[0] = pin.xdrawn[0];
@@ -4731,11 +4763,56 @@ int run_round(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds_h, int32_t n_r
         for (int32_t j = 0; j < n_rounds * L; ++j)
             out[j] = tpe_label_result{NAN, NAN, NAN, NAN, -1, j % L, 0};
     }
+    if (dense_on && ctx->hot_ran) {
+        for (int64_t c = 0; c < ctx->hot_cells; ++c) ctx->hot_listed += ctx->hot_cnt_h[c];
+        const int32_t hf = pin.hot_flag;
+        if (hf && !ctx->hot_redo && errh == 0) {
+            // a cell's best lower bound stayed below tau0 (bit 1: its list may
+            // miss a winner) or a list overflowed (bit 2): the dense labels run
+            // again with every candidate through the expansion screen (the
+            // same draws; their results replace these), and later rounds list
+            // more after an overflow.  Only the dense families re-run
+            // (TPE_OPT_MODE_MASK): the quantized and categorical labels'
+            // partial rows, draw counts and evaluations stay this run's, and
+            // the reduction reads them again.  tpe_last_hot reports the
+            // fallback (bench: hot_fallbacks), which no test or bench has seen
+            // outside the forced TPE_OPT_HOT = 2
+            if ((hf & 2) && ctx->hot_cap_div > 1.0) ctx->hot_cap_div = std::max(1.0, ctx->hot_cap_div / 4.0);
+            const int64_t listed = ctx->hot_listed;
+            int64_t side_evals = 0;
+            for (int m = QUANT_GMM; m <= CAT; ++m)
+                if ((fam >> m) & 1) side_evals += ctx->mode_evals[m];
+            const unsigned long long drawn0 = ctx->xdrawn_h[0], drawn1 = ctx->xdrawn_h[1];
+            const bool cat_early = ctx->cat_early;
+            const int32_t mask = ctx->mode_mask;
+            ctx->mode_mask = fam & ((1 << DENSE_GMM) | (1 << DENSE_LGMM));
+            ctx->hot_redo = true;
+            const int rc = run_round(ctx, seed, rounds_h, n_rounds, n, cand_offset, cand_in_dev, olb, ola, out,
+                                     only_label);
+            ctx->hot_redo = false;
+            ctx->mode_mask = mask;
+            ctx->hot_ran = true;
+            ctx->hot_fallback = hf;
+            ctx->hot_listed = listed;
+            ctx->evals += side_evals;
+            ctx->xdrawn_h[0] = drawn0;
+            ctx->xdrawn_h[1] = drawn1;
+            ctx->cat_early = cat_early;
+            return rc;
+        }
+    }
     if (errh & 1) return ctx->fail(TPE_ERR_SAMPLE, "truncated sampler: interval [low, high) not reached");
     if (errh & 2) return ctx->fail(TPE_ERR_VALUE, "negative arg to lognormal_cdf");
     if (errh & 4) return ctx->fail(TPE_ERR_VALUE, "categorical sample out of range");
     if (errh & 8) return ctx->fail(TPE_ERR_VALUE, "quantized sample beyond 2^52 grid steps");
     return TPE_OK;
+}
+
+// the sampling records of a host-uploaded posterior: one block per label,
+// the device build's fold (samp_fold_block)
+__global__ __launch_bounds__(64) void k_samp_fold(const DLabel* __restrict__ labels, SampRec* __restrict__ samp) {
+    const DLabel L = labels[blockIdx.x];
+    (void)samp_fold_block(L, samp + L.samp_off, L.ns);
 }
 
 void launch_sample_only(tpe_ctx* ctx, int mode, int64_t n, int64_t offset, uint64_t seed,
@@ -4831,23 +4908,19 @@ int set_posterior_impl(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_lab
             }
             (side ? o.comp_a : o.comp_b) = at;
         }
-        // sampling records of the below mixture (cumulative normalised weights)
+        // sampling records of the below mixture: the components and their raw
+        // weights, folded on the device after the upload (k_samp_fold: the
+        // device build's own fold, so both posteriors draw the same bits)
         o.samp_off = (int64_t)sr.size();
         o.ns = d.n_below;
         double tot = 0.0;
         for (int k = 0; k < d.n_below; ++k) tot += weights[d.below_off + k];
-        if (!(tot > 0)) {
-            if (sampler_checks) return ctx->fail(TPE_ERR_VALUE, "below weights sum to zero");
-            tot = 1.0;
-        }
-        double run = 0.0;
+        if (!(tot > 0) && sampler_checks) return ctx->fail(TPE_ERR_VALUE, "below weights sum to zero");
         for (int k = 0; k < d.n_below; ++k) {
-            run += weights[d.below_off + k];
-            SampRec s;
-            s.cdf = (k == d.n_below - 1) ? 1.0 : run / tot;
+            SampRec s{};
             s.mu = d.kind == TPE_CATEGORICAL ? 0.0 : mus[d.below_off + k];
             s.sigma = d.kind == TPE_CATEGORICAL ? 0.0 : sigmas[d.below_off + k];
-            s.pad = 0.0;
+            s.wd = weights[d.below_off + k];
             sr.push_back(s);
         }
         grp[o.mode].push_back(l);
@@ -4868,6 +4941,10 @@ int set_posterior_impl(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_lab
     HIPCHK(ctx, hipMemcpy(ctx->P->comps32.p, c32.data(), c32.size() * sizeof(Comp<float>), hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->P->samp.p, sr.data(), sr.size() * sizeof(SampRec), hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->P->groups.p, cat.data(), cat.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_samp_fold, dim3((unsigned)n_labels), dim3(64), 0, ctx->stream, ctx->P->labels.p,
+                       ctx->P->samp.p);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     ctx->P->groups_h = cat;
     ctx->P->h_labels = dl;
     ctx->P->win_ready = false;
@@ -5387,7 +5464,6 @@ TPE_DEV int tpe1_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
         case TPE_OPT_EARLY: ctx->early = value != 0; break;
         case TPE_OPT_ZERO_WIN: ctx->zero_win = value != 0; break;
         case TPE_OPT_VALUE_ONLY: ctx->value_only = value != 0; break;
-        case TPE_OPT_HOT32: ctx->hot32 = (int32_t)value; break;
         case TPE_OPT_BX_T:
             if (value != 0 && (value < 32 || value > 128)) return ctx->fail(TPE_ERR_ARG, "index cut T must be 0 or in [32, 128]");
             ctx->bx_t_force = (int32_t)value;

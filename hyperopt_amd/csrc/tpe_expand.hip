@@ -130,7 +130,7 @@ __global__ __launch_bounds__(kBlock) void k_bx_scan(const DLabel* __restrict__ l
     } else {
         for (int k = threadIdx.x; k < L.ns; k += kBlock) {
             const SampRec s = samp[L.samp_off + k];
-            const double w = s.cdf - (k ? samp[L.samp_off + k - 1].cdf : 0.0);
+            const double w = s.wd;   // (no bounds here: the pick's weight)
             // Q(z) <= exp(-z^2 / 2) / 2: z = sqrt(2 ln(w / tail)) suffices
             const double z = w > kRangeTail ? fmin(8.0, sqrt(2.0 * log(w / kRangeTail))) : 0.0;
             lo = fmin(lo, s.mu - z * s.sigma);
@@ -561,7 +561,7 @@ __global__ __launch_bounds__(kBlock) void k_bx_bounds(const DLabel* __restrict__
     }
     if (staged_s && threadIdx.x < L.ns) {
         const SampRec s = samp[L.samp_off + threadIdx.x];
-        const double w = s.cdf - (threadIdx.x ? samp[L.samp_off + threadIdx.x - 1].cdf : 0.0);
+        const double w = s.wd;   // (the truncated mixture's density weight, k_samp_fold)
         const bool ok = w > 0.0 && s.sigma > 0.0 && s.sigma < kInf;
         sm[threadIdx.x] = ok ? make_float4((float)(s.mu - L.centre), (float)(1.0 / s.sigma),
                                            (float)(w / (s.sigma * 2.5066282746310002)), 0.0f)
@@ -595,11 +595,9 @@ __global__ __launch_bounds__(kBlock) void k_bx_bounds(const DLabel* __restrict__
                     dens = fmaf(q.z, __expf(-0.5f * z * z), dens);
                 }
             } else {
-                double prev = 0.0;
                 for (int k = 0; k < L.ns; ++k) {
                     const SampRec s = samp[L.samp_off + k];
-                    const double w = s.cdf - prev;
-                    prev = s.cdf;
+                    const double w = s.wd;
                     if (!(w > 0.0 && s.sigma > 0.0 && s.sigma < kInf)) continue;
                     const float z = (float)((xm - (s.mu - L.centre)) / s.sigma);
                     dens += (float)(w / (s.sigma * 2.5066282746310002)) * __expf(-0.5f * z * z);

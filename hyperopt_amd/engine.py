@@ -476,7 +476,7 @@ class Engine(object):
                'hot': L.TPE_OPT_HOT, 'early': L.TPE_OPT_EARLY, 'hot_div': L.TPE_OPT_HOT_DIV,
                'zero_win': L.TPE_OPT_ZERO_WIN, 'value_only': L.TPE_OPT_VALUE_ONLY,
                'rescore_cap': L.TPE_OPT_RESCORE_CAP, 'mode_mask': L.TPE_OPT_MODE_MASK,
-               'aux_families': L.TPE_OPT_AUX_FAMILIES, 'hot32': L.TPE_OPT_HOT32,
+               'aux_families': L.TPE_OPT_AUX_FAMILIES,
                'bx_split': L.TPE_OPT_BX_SPLIT, 'bx_t': L.TPE_OPT_BX_T,
                'pk_sliced': L.TPE_OPT_PK_SLICED, 'defer_report': L.TPE_OPT_DEFER_REPORT}
 

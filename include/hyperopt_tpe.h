@@ -533,13 +533,6 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *                   unchanged; single-device contexts).  Their early exit's
  *                   draw counts (tpe_last_drawn, the families' evals) are
  *                   those of a scan in index order either way              [0]
- *   TPE_OPT_HOT32   1: the hot-bin prefilter draws every candidate in fp32
- *                   with a rigorous bound on its distance from the fp64
- *                   draw and lists (index, accepted attempt); the listed
- *                   candidates are re-drawn in fp64; 2: every bound x 4096
- *                   (tests); 0: the fp64 draw kernel -- 19 % faster on
- *                   gfx950 (r5e: 1.20 vs 1.42 ms at config 3, more integer
- *                   and conversion work than the fp64 it saves)          [0]
  *   TPE_OPT_BX_SPLIT  workgroups per 64-bin block of the expansion index's
  *                   Taylor tables, each summing one part of the bins' window
  *                   (k_bx_table / k_bx_table_fin; 1..8, 0: enough for ~8192
@@ -591,7 +584,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_RESCORE_CAP 17
 #define TPE_OPT_MODE_MASK 18
 #define TPE_OPT_AUX_FAMILIES 19
-#define TPE_OPT_HOT32 20
+/* (20: TPE_OPT_HOT32, the fp32 draw kernel -- measured slower, removed in round 6) */
 #define TPE_OPT_BX_SPLIT 21
 #define TPE_OPT_BX_T 22
 #define TPE_OPT_PK_SLICED 23

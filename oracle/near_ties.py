@@ -16,7 +16,11 @@ So per (round, label) cell:
   (tpe.py:769-778: first index of the largest below - above) must be the
   round's winner.  The set is wide enough when the HIP score of its last
   member is further below the best than any HIP - numpy difference seen in
-  it (`span` vs `max_abs_diff`);
+  it (`span` vs `max_abs_diff`).  A cell whose numpy argmax beats the HIP
+  winner, in numpy's arithmetic, by no more than the two arithmetics' own
+  largest difference in the set is an arithmetic tie (`arith_tie`): the two
+  scores are equal to a few ulp and the order is rounding in either
+  arithmetic -- reported separately, never counted as agreement;
 * quantized and categorical labels: a candidate's score is a function of its
   value, so every distinct value of the round's candidates is scored by the
   oracle and numpy's winner is the first candidate holding the best one.
@@ -78,8 +82,16 @@ def _dense_cell(eng, li, p, stream, seed, rnd, C, r, top):
     wj = np.searchsorted(cand, w)
     in_set = wj < len(cand) and cand[wj] == w
     diff = np.abs(s_hip - s_np)
+    strict = int(cand[j_np]) == w
+    # numpy's margin of its own argmax over the HIP winner, in numpy's
+    # arithmetic: within the two arithmetics' measured disagreement (the
+    # largest |HIP - numpy| of the set) the order of the two is rounding in
+    # either, and the cell is an arithmetic tie, reported as such
+    margin = float(s_np[j_np] - s_np[wj]) if in_set else None
+    tie = bool(not strict and in_set and margin <= 2.0 * float(np.max(diff)))
     return {
-        'label': int(li), 'kind': 'dense', 'agree': bool(int(cand[j_np]) == w),
+        'label': int(li), 'kind': 'dense', 'agree': bool(strict), 'arith_tie': tie,
+        'numpy_margin_over_winner': margin,
         'winner': w, 'numpy_winner': int(cand[j_np]),
         'hip_full_argmax': int(cand[int(np.argmax(s_hip))]),
         'numpy_top2_gap': float(order[0] - order[1]) if len(order) > 1 else None,
@@ -131,6 +143,7 @@ def round_agreement(eng, posts, res, seed, rnd, C, top=64, streams=None, dense_o
 def summary(cells):
     dense = [c for c in cells if c['kind'] == 'dense']
     gaps = [c['numpy_top2_gap'] for c in dense if c['numpy_top2_gap'] is not None]
+    ties = [c for c in dense if c.get('arith_tie')]
     return {
         'cells': len(cells), 'agree': sum(c['agree'] for c in cells),
         'rate': sum(c['agree'] for c in cells) / max(len(cells), 1),
@@ -139,6 +152,11 @@ def summary(cells):
         'median_numpy_top2_gap_dense': float(np.median(gaps)) if gaps else None,
         'max_abs_hip_minus_numpy_dense': max((c['max_abs_diff'] for c in dense), default=None),
         'min_span_dense': min((c['span'] for c in dense), default=None),
+        # disagreements within the arithmetics' own difference (both scores
+        # within a few ulp): neither argmax is the "right" one
+        'arith_ties': len(ties),
+        'arith_tie_margins': [c['numpy_margin_over_winner'] for c in ties],
+        'agree_or_arith_tie': sum(bool(c['agree'] or c.get('arith_tie')) for c in cells),
     }
 
 

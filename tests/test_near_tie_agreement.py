@@ -57,8 +57,14 @@ def _run(config, C, steps=4):
 
 
 def _check(cells, summ):
-    bad = [c for c in cells if not c['agree']]
+    # a disagreement is allowed only as an arithmetic tie: numpy's margin
+    # over the HIP winner within the two arithmetics' measured difference
+    # (~1e-15), i.e. scores equal to a few ulp (oracle/near_ties.py); rare
+    bad = [c for c in cells if not (c['agree'] or c.get('arith_tie'))]
     assert not bad, bad
+    ties = [c for c in cells if c.get('arith_tie')]
+    assert len(ties) <= max(1, len(cells) // 50), ties
+    assert all(c['numpy_margin_over_winner'] < 1e-14 for c in ties), ties
     assert all(c['winner_value_equal'] for c in cells)
     for c in cells:
         if c['kind'] == 'dense':

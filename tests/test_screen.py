@@ -443,86 +443,6 @@ def test_hot_bounds_hold(eng):
         assert hot < 0.02, (li, hot)
 
 
-@pytest.mark.parametrize('config', ['config2', 'config3', 'config3_device', 'config4', 'config3_batched'])
-def test_hot32_draw_same_round(eng, config):
-    """The prefilter's fp32 draw (k_hot_bx32, TPE_OPT_HOT32 = 1):
-    every candidate drawn in fp32 with a rigorous bound on its distance from
-    the fp64 draw, listed when any sub-bin it can fall in is hot, the listed
-    ones re-drawn in fp64 from (index, accepted attempt).  The round equals
-    the fp64 draw kernel's (hot32 = 0) and the plain fp64 round bytewise --
-    also with every bound x 4096 (hot32 = 2: many slots decided by the fp64
-    draw at a truncation bound, many more listed) -- and it lists at least
-    the fp64 kernel's candidates and hardly more."""
-    from hyperopt_amd import posterior as P
-    from hyperopt_amd.workloads import conditional_history, hartmann_history, mixed_history
-    if config == 'config2':
-        hist = hartmann_history(2000, seed=0)
-    elif config == 'config4':
-        hist = conditional_history(5000, seed=0)
-    else:
-        hist = mixed_history(32, 10000, seed=0)
-    if config.endswith('device'):
-        eng.build_posterior(*hist.device_inputs(), gamma=0.25, prior_weight=1.0)
-    else:
-        eng.set_posterior(*P.pack(hist.posteriors()))
-    C = 1 << 20
-    run = (lambda s: eng.suggest_batch(s, [5, 6, 7], C // 4)) if config.endswith('batched') else \
-        (lambda s: eng.suggest(s, C, round=5))
-    try:
-        for seed in (17, 29):
-            eng.set_option('hot32', 1)
-            a = run(seed)
-            la, fa = eng.last_hot()
-            eng.set_option('hot32', 0)
-            b = run(seed)
-            lb, fb = eng.last_hot()
-            eng.set_option('hot32', 2)
-            c = run(seed)
-            lc, fc = eng.last_hot()
-            eng.set_option('hot32', 1)
-            eng.set_option('screen', 0)
-            d = run(seed)
-            eng.set_option('screen', 1)
-            _assert_same(a, b)
-            _assert_same(a, c)
-            _assert_same(a, d)
-            assert fa == fb == 0
-            print('%s seed %d: listed fp32 %d, fp64 %d, fp32 x 4096 bounds %d' % (config, seed, la, lb, lc))
-            assert lb <= la <= 1.05 * lb + 64
-            assert lc >= la
-    finally:
-        eng.set_option('hot32', 0)
-        eng.set_option('screen', 1)
-
-
-def test_hot32_draw_same_round_2_24(eng):
-    """The headline size: config 3 at 2^24 candidates per label, fp32 draw
-    against the fp64 draw kernel and the plain fp64 round, bytewise."""
-    from hyperopt_amd import posterior as P
-    from hyperopt_amd.workloads import mixed_history
-    hist = mixed_history(32, 10000, seed=0)
-    eng.set_posterior(*P.pack(hist.posteriors()))
-    C = 1 << 24
-    try:
-        eng.set_option('hot32', 1)
-        a = eng.suggest(41, C, round=3)
-        la, _ = eng.last_hot()
-        eng.set_option('hot32', 0)
-        b = eng.suggest(41, C, round=3)
-        lb, _ = eng.last_hot()
-    finally:
-        eng.set_option('hot32', 0)
-    eng.set_option('screen', 0)
-    try:
-        d = eng.suggest(41, C, round=3)
-    finally:
-        eng.set_option('screen', 1)
-    _assert_same(a, b)
-    _assert_same(a, d)
-    print('2^24: listed fp32 %d, fp64 %d' % (la, lb))
-    assert lb <= la <= 1.05 * lb + 64
-
-
 @pytest.mark.parametrize('split', [3, 8, 0])
 def test_index_window_split_same_round(eng, split):
     """k_bx_table's split window (TPE_OPT_BX_SPLIT: the bins' component
