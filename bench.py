@@ -40,14 +40,17 @@ FLOPS_PER_EVAL = {'f64': 6.0, 'f32': 6.0}
 # expansion screen (k_screen_bx): per candidate a 15-coefficient Horner
 # polynomial (15 FMA) and the degree-5 exp(-kappa delta^2) factor (5 FMA)
 BX_FLOPS_PER_CAND = 2 * 15 + 2 * 5
-# One draw of the below mixture (tpe_device.h draw_attempt), algorithmic fp64
-# FLOP as implemented: u1 = 2 - m (1), the fdlibm log (2 + f, f / (2 + f),
-# z = s^2, the 7-coefficient polynomial, hf and the recombination: 24),
-# -2 log, sqrt (2), the angle's residual, t^2, the cos / sin polynomials and
-# cos(a + t) (20), sg * n + mu (2): ~49, plus the sub-bin index (2).  The
-# Philox words (20 32x32-bit products + 40 xors per attempt) are integer work
-# and are not counted; neither are rejected attempts.
-DRAW_FLOPS_PER_CAND = 51
+# The draw kernel k_hot_bx (round 6: the inverse-CDF draw, most candidates
+# decided from their Philox words), algorithmic 32-bit lane operations per
+# candidate: half a Philox4x32-10 call -- 10 rounds of two 32x32 -> 64-bit
+# products (2 operations each: the low and high words) and two 3-input
+# xors (2 each), 80 per call -- 40; the component pick (the guide's lookup
+# and up to 3 threshold comparisons) 4; the u-cell bit (index, load, test)
+# 3.  The fp64 draw of the ~1-2 % marked candidates and their sub-bin test
+# are not counted.  Against the 32-bit VALU lane rate of MI355X_MICROARCH.md's
+# vector figure (256 CUs x 4 SIMD-32 x 32 lanes x 2.4 GHz = 78.6 T/s).
+DRAW_OPS_PER_CAND = 47
+PEAK_INT32_VECTOR_TOPS = 78.6
 # Vector peaks.  FP32 157.3 TFLOP/s is MI355X_MICROARCH.md's figure (256 CUs
 # x 4 SIMD-32 x 32 lanes x 2 FLOP x 2.4 GHz).  The guide lists no FP64
 # figure: 78.6 TFLOP/s is AMD's MI355X specification for vector FP64 -- half
@@ -992,18 +995,18 @@ def main():
     windowed = smode == 2
     hot = smode == 3 and scr[5] > 0
     if hot:
-        # the hot-bin prefilter: every candidate drawn and bounded by its
-        # sub-bin (k_hot_bx, the dominant kernel), the listed ones through
-        # the expansion screen (k_screen_hot); the bracket holds both
+        # the hot-bin prefilter's draw kernel (k_hot_bx, the dominant
+        # kernel; its HIP-event bracket holds it alone): every candidate's
+        # Philox words, pick and u-cell bit, the marked ~1-2 % drawn in fp64
+        # and tested against their sub-bin's bit
         dom_ms = scr[2]
-        kprec = 'f64'
+        kprec = 'int32'
         kname = 'k_hot_bx<'
-        kdesc = 'k_hot_bx + k_screen_hot (hot-bin prefilter of the expansion screen: every candidate ' \
-                'drawn and bounded by its sub-bin\'s score interval, the 0.5 % that can still win ' \
-                'scored by the expansion screen), GMM1+LGMM1 labels'
+        kdesc = 'k_hot_bx (the hot-bin prefilter\'s draw: every candidate\'s Philox4x32-10 words, ' \
+                'component pick and u-cell bit; the marked ones drawn by the inverse CDF in fp64 and ' \
+                'listed when their sub-bin can hold the winner), GMM1+LGMM1 labels'
         dom_rate = scr[3] / (dom_ms * 1e-3)
-        dom_flops = (scr[0] * DRAW_FLOPS_PER_CAND + scr[3] * FLOPS_PER_EVAL['f64']
-                     + scr[5] * BX_FLOPS_PER_CAND)
+        dom_flops = scr[0] * DRAW_OPS_PER_CAND
     elif smode == 3:
         # the expansion screen: per candidate the below mixture and the
         # bin's list of unclipped components as direct fp64 terms (6 FLOP
@@ -1037,21 +1040,22 @@ def main():
         kdesc = 'k_round<%s,%s>' % (prec, dom + ' (GMM1+LGMM1 labels)')
         dom_rate = mode_ev[dom] / (dom_ms * 1e-3)
         dom_flops = mode_ev[dom] * FLOPS_PER_EVAL[prec]
-    peak = PEAK_FP64_VECTOR_TFLOPS if kprec == 'f64' else PEAK_FP32_VECTOR_TFLOPS
+    peak = {'f64': PEAK_FP64_VECTOR_TFLOPS, 'f32': PEAK_FP32_VECTOR_TFLOPS,
+            'int32': PEAK_INT32_VECTOR_TOPS}[kprec]
     # PMC figures come from the committed profile of the default workload
     # (config 3, tools/prof_round.sh): only that workload's line carries them
     pmc = (measured_pmc(kname) if args.config == 3 and world == 1 and args.cand_log2 == 24
            and args.labels == 32 else {})
     achieved = dom_flops / (dom_ms * 1e-3) / 1e12
     roof = {'bound': 'valu', 'kernel': kdesc,
-            'achieved': round(achieved, 3), 'peak': peak, 'unit': 'TFLOP/s',
+            'achieved': round(achieved, 3), 'peak': peak, 'unit': 'Tops/s' if kprec == 'int32' else 'TFLOP/s',
             'frac': round(achieved / peak, 4), 'traffic': pmc.get('hbm_bytes'),
             'traffic_source': pmc.get('source'), 'valu_busy_measured': pmc.get('valu_busy'),
             'issue_frac_measured': pmc.get('issue_frac'), 'issue_split': pmc.get('issue_split'),
             'issue_costs_source': ('profiles/' + pmc['issue_costs']) if pmc.get('issue_costs') else None,
             'wave_cycles': pmc.get('wave_cycles'),
             'pmc_source': pmc.get('source'),
-            'evals_per_s': dom_rate, 'flops_per_eval': FLOPS_PER_EVAL[kprec],
+            'evals_per_s': dom_rate, 'flops_per_eval': FLOPS_PER_EVAL.get(kprec),
             'launch_ms': dom_ms / args.steps,
             'issue_model_note': 'issue_frac_measured: PMC instruction classes (SQ_INSTS_VALU_{ADD,MUL,FMA,'
                                 'TRANS}_F64 / _F32, _INT32, _INT64, _CVT, the rest) x the cycles per wave64 '
@@ -1062,19 +1066,13 @@ def main():
                                 'SQ_* cycles / SQ_WAVE_CYCLES (WAIT_ANY = parked on s_waitcnt / barriers, '
                                 'WAIT_INST_ANY = waiting to issue)'}
     if hot:
-        roof['flops_per_candidate_draw'] = DRAW_FLOPS_PER_CAND
-        roof['flops_per_listed_poly'] = BX_FLOPS_PER_CAND
+        roof['ops_per_candidate_draw'] = DRAW_OPS_PER_CAND
         roof['candidates_per_s'] = scr[0] / (dom_ms * 1e-3)
-        roof['note'] = ('VALU-issue bound: the step draws every candidate (Philox4x32-10 + Box-Muller, '
-                        'queued rejection); achieved counts the draw\'s fp64 arithmetic (51 FLOP per '
-                        'candidate, the Philox integer work not counted), the listed candidates\' '
-                        'polynomials (40) and direct lpdf terms (6 each) over the bracket\'s device '
-                        'time; the PMC figures are k_hot_bx\'s')
-        roof['traffic_note'] = ('traffic (2 x FETCH_SIZE + WRITE_SIZE per launch) counts, beside the hot '
-                                'lists (~21 MB: 1.7e6 listed x 12 B) and the sub-bin bits, the scratch stores '
-                                'of the 8 VGPRs k_hot_bx spills at six workgroups per CU (80 VGPRs): 86 MB '
-                                'against 33 MB at five per CU without spills (r5aq vs r5r), for a kernel 3.5 % '
-                                'faster (r5x); ~75 GB/s, 1 % of HBM')
+        roof['note'] = ('VALU-issue bound on integer work: achieved counts the draw\'s algorithmic 32-bit '
+                        'lane operations (Philox4x32-10: 40 per candidate; the pick 4; the u-cell bit 3) '
+                        'over the kernel\'s HIP-event time, against the 32-bit VALU lane rate; the fp64 '
+                        'draws of the marked candidates and the expansion screen of the listed ones '
+                        '(k_screen_hot, other_dense_ms) are not counted; the PMC figures are k_hot_bx\'s')
     elif smode == 3:
         roof['flops_per_candidate_poly'] = BX_FLOPS_PER_CAND
         roof['note'] = ('VALU-issue bound: per candidate the Philox + Box-Muller draw, the fp64 '

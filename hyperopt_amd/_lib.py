@@ -60,6 +60,7 @@ TPE_OPT_BX_SPLIT = 21
 TPE_OPT_BX_T = 22
 TPE_OPT_PK_SLICED = 23
 TPE_OPT_DEFER_REPORT = 24
+TPE_OPT_LABEL_SHARDS = 25
 
 TPE_OBS_IDENTITY = 0
 TPE_OBS_LOG = 1
@@ -103,6 +104,7 @@ SIGNATURES = {
     'tpe_ctx_create': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(_P)]),
     'tpe_ctx_create_multi': (ctypes.c_int, [_P, _I32, ctypes.c_int, ctypes.POINTER(_P)]),
     'tpe_ctx_devices': (ctypes.c_int32, [_P, _P, _I32]),
+    'tpe_label_device': (ctypes.c_int32, [_P, _I32]),
     'tpe_ctx_destroy': (None, [_P]),
     'tpe_last_error': (ctypes.c_char_p, [_P]),
     'tpe_gmm1_lpdf': (ctypes.c_int, [_P, _P, _I64, _P, _P, _P, _I32, _I32, _D, _D, _D, _P]),

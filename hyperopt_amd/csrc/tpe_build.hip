@@ -2108,8 +2108,8 @@ TPE_DEV int tpe1_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int3
     return rc;
 }
 
-int tpe_get_mixture(tpe_ctx* ctx, int32_t label, int32_t side, double* weights, double* mus,
-                    double* sigmas, int32_t cap, int32_t* n) {
+TPE_DEV int tpe1_get_mixture(tpe_ctx* ctx, int32_t label, int32_t side, double* weights, double* mus,
+                             double* sigmas, int32_t cap, int32_t* n) {
     if (!ctx) return TPE_ERR_ARG;
     TPE_SETTLE(ctx);
     auto& B = ctx->build;
@@ -2129,16 +2129,16 @@ int tpe_get_mixture(tpe_ctx* ctx, int32_t label, int32_t side, double* weights, 
     return TPE_OK;
 }
 
-int32_t tpe_resident_labels(const tpe_ctx* ctx) { return ctx ? ctx->resident.n_labels : 0; }
+TPE_DEV int32_t tpe1_resident_labels(const tpe_ctx* ctx) { return ctx ? ctx->resident.n_labels : 0; }
 
-int tpe_last_build_ms(const tpe_ctx* ctx, float* ms) {
+TPE_DEV int tpe1_last_build_ms(const tpe_ctx* ctx, float* ms) {
     if (!ctx || !ms) return TPE_ERR_ARG;
     TPE_SETTLE(const_cast<tpe_ctx*>(ctx));
     *ms = ctx->build_ms;
     return TPE_OK;
 }
 
-int tpe_build_report(tpe_ctx* ctx, int32_t* n_below, int32_t* ties) {
+TPE_DEV int tpe1_build_report(tpe_ctx* ctx, int32_t* n_below, int32_t* ties) {
     if (!ctx) return TPE_ERR_ARG;
     TPE_SETTLE(ctx);
     if (n_below) *n_below = ctx->build.last_n_below;

@@ -483,6 +483,7 @@ struct tpe_ctx {
     int32_t bx_t_force = 0;              // TPE_OPT_BX_T (0: auto)
     double bx_t_next = 64.0;             // the cut T of the next index built (set by its caller)
     DevBuf<int32_t> hot_i, hot_cnt;      //   their indices; per cell the count
+    DevBuf<int32_t> hot_mi, hot_mcnt;    //   the marked candidates (k_hot_bx -> k_hot_draw); per cell the count
     DevBuf<unsigned long long> hot_t, hot_tau0;   // per cell largest L; per label tau0
     DevBuf<uint32_t> hot_bits;           // per sub-bin: U >= tau0 (words at sb_off / 32)
     DevBuf<int32_t> hot_flag;            // fallback flag
@@ -584,6 +585,14 @@ struct tpe_ctx {
     int32_t opt_whole_rounds = 0;
     tpe_rt::QExchange* qx = nullptr;
     int32_t shard_id = 0;                // this context's position in a sharded round
+    // label shards of a multi-device context (tpe_multi.hip; set by
+    // tpe_history_reset with at least one label per device): device d holds
+    // the global labels lsh_ids[d] (increasing) of the resident history;
+    // per global label its device and local index
+    std::vector<std::vector<int32_t>> lsh_ids;
+    std::vector<int32_t> lsh_dev, lsh_local;
+    int32_t lsh_L = 0;
+    bool lsh_enable = true;              // TPE_OPT_LABEL_SHARDS
 
     int fail(int code, const std::string& m) {
         err = m;
@@ -701,7 +710,22 @@ TPE_DEV int tpe1_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int3
                                  const double* obs_val, double gamma, double prior_weight,
                                  int32_t lf, int32_t* n_below_out);
 TPE_DEV void tpe1_ctx_destroy(tpe_ctx* ctx);
+TPE_DEV int tpe1_get_mixture(tpe_ctx* ctx, int32_t label, int32_t side, double* weights, double* mus,
+                             double* sigmas, int32_t cap, int32_t* n);
+TPE_DEV int32_t tpe1_resident_labels(const tpe_ctx* ctx);
+TPE_DEV int tpe1_last_build_ms(const tpe_ctx* ctx, float* ms);
+TPE_DEV int tpe1_build_report(tpe_ctx* ctx, int32_t* n_below, int32_t* ties);
+TPE_DEV int tpe1_score(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, double* lpdf_below,
+                       double* lpdf_above, tpe_label_result* out);
 }
+
+// entry points that read the primary context's posterior alone refuse a
+// label-sharded multi-device context (its labels are spread over devices)
+#define TPE_NOT_LSHARD(ctx)                                                                        \
+    do {                                                                                         \
+        if (!(ctx)->lsh_ids.empty())                                                             \
+            return (ctx)->fail(TPE_ERR_ARG, "not available on a label-sharded multi-device context"); \
+    } while (0)
 
 #define HIPCHK(ctx, call)                                  \
     do {                                                   \

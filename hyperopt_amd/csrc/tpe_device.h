@@ -153,48 +153,57 @@ __device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
 // regions, ~7e-16 relative against 40-digit arithmetic over uniform t and
 // t down to 1e-300 (checked when this was written).  One function for every
 // kernel, so every kernel draws the same bits.
+// a constant materialised in SGPRs where it is used: without it the
+// compiler hoists ndtri_lower's 48 fp64 coefficients out of the callers'
+// loops into VGPRs (k_hot_bx: 150 VGPRs, spills); fp64 FMA takes one SGPR
+// operand, and the scalar unit's moves issue beside the VALU
+__device__ __forceinline__ double sk(double c) {
+    asm volatile("" : "+s"(c));
+    return c;
+}
+
 __device__ __forceinline__ double ndtri_lower(double t) {
     const double q = t - 0.5;   // (exact: t in [1/4, 1/2] by Sterbenz, the product below rounds once)
     if (q >= -0.425) {
         const double r = 0.180625 - q * q;
         const double num =
-            fma(fma(fma(fma(fma(fma(fma(2.5090809287301226727e+3, r, 3.3430575583588128105e+4), r,
-                                    6.7265770927008700853e+4), r, 4.5921953931549871457e+4), r,
-                            1.3731693765509461125e+4), r, 1.9715909503065514427e+3), r,
-                    1.3314166789178437745e+2), r, 3.3871328727963666080e0);
+            fma(fma(fma(fma(fma(fma(fma(sk(2.5090809287301226727e+3), r, sk(3.3430575583588128105e+4)), r,
+                                    sk(6.7265770927008700853e+4)), r, sk(4.5921953931549871457e+4)), r,
+                            sk(1.3731693765509461125e+4)), r, sk(1.9715909503065514427e+3)), r,
+                    sk(1.3314166789178437745e+2)), r, sk(3.3871328727963666080e0));
         const double den =
-            fma(fma(fma(fma(fma(fma(fma(5.2264952788528545610e+3, r, 2.8729085735721942674e+4), r,
-                                    3.9307895800092710610e+4), r, 2.1213794301586595867e+4), r,
-                            5.3941960214247511077e+3), r, 6.8718700749205790830e+2), r,
-                    4.2313330701600911252e+1), r, 1.0);
+            fma(fma(fma(fma(fma(fma(fma(sk(5.2264952788528545610e+3), r, sk(2.8729085735721942674e+4)), r,
+                                    sk(3.9307895800092710610e+4)), r, sk(2.1213794301586595867e+4)), r,
+                            sk(5.3941960214247511077e+3)), r, sk(6.8718700749205790830e+2)), r,
+                    sk(4.2313330701600911252e+1)), r, 1.0);
         return q * num / den;
     }
     double r = sqrt(-flog(t));
     if (r <= 5.0) {
         r -= 1.6;
         const double num =
-            fma(fma(fma(fma(fma(fma(fma(7.74545014278341407640e-4, r, 2.27238449892691845833e-2), r,
-                                    2.41780725177450611770e-1), r, 1.27045825245236838258e0), r,
-                            3.64784832476320460504e0), r, 5.76949722146069140550e0), r,
-                    4.63033784615654529590e0), r, 1.42343711074968357734e0);
+            fma(fma(fma(fma(fma(fma(fma(sk(7.74545014278341407640e-4), r, sk(2.27238449892691845833e-2)), r,
+                                    sk(2.41780725177450611770e-1)), r, sk(1.27045825245236838258e0)), r,
+                            sk(3.64784832476320460504e0)), r, sk(5.76949722146069140550e0)), r,
+                    sk(4.63033784615654529590e0)), r, sk(1.42343711074968357734e0));
         const double den =
-            fma(fma(fma(fma(fma(fma(fma(1.05075007164441684324e-9, r, 5.47593808499534494600e-4), r,
-                                    1.51986665636164571966e-2), r, 1.48103976427480074590e-1), r,
-                            6.89767334985100004550e-1), r, 1.67638483018380384940e0), r,
-                    2.05319162663775882187e0), r, 1.0);
+            fma(fma(fma(fma(fma(fma(fma(sk(1.05075007164441684324e-9), r, sk(5.47593808499534494600e-4)), r,
+                                    sk(1.51986665636164571966e-2)), r, sk(1.48103976427480074590e-1)), r,
+                            sk(6.89767334985100004550e-1)), r, sk(1.67638483018380384940e0)), r,
+                    sk(2.05319162663775882187e0)), r, 1.0);
         return -(num / den);
     }
     r -= 5.0;
     const double num =
-        fma(fma(fma(fma(fma(fma(fma(2.01033439929228813265e-7, r, 2.71155556874348757815e-5), r,
-                                1.24266094738807843860e-3), r, 2.65321895265761230930e-2), r,
-                        2.96560571828504891230e-1), r, 1.78482653991729133580e0), r,
-                5.46378491116411436990e0), r, 6.65790464350110377720e0);
+        fma(fma(fma(fma(fma(fma(fma(sk(2.01033439929228813265e-7), r, sk(2.71155556874348757815e-5)), r,
+                                sk(1.24266094738807843860e-3)), r, sk(2.65321895265761230930e-2)), r,
+                        sk(2.96560571828504891230e-1)), r, sk(1.78482653991729133580e0)), r,
+                sk(5.46378491116411436990e0)), r, sk(6.65790464350110377720e0));
     const double den =
-        fma(fma(fma(fma(fma(fma(fma(2.04426310338993978564e-15, r, 1.42151175831644588870e-7), r,
-                                1.84631831751005468180e-5), r, 7.86869131145613259100e-4), r,
-                        1.48753612908506148525e-2), r, 1.36929880922735805310e-1), r,
-                5.99832206555887937690e-1), r, 1.0);
+        fma(fma(fma(fma(fma(fma(fma(sk(2.04426310338993978564e-15), r, sk(1.42151175831644588870e-7)), r,
+                                sk(1.84631831751005468180e-5)), r, sk(7.86869131145613259100e-4)), r,
+                        sk(1.48753612908506148525e-2)), r, sk(1.36929880922735805310e-1)), r,
+                sk(5.99832206555887937690e-1)), r, 1.0);
     return -(num / den);
 }
 

@@ -784,7 +784,6 @@ __global__ __launch_bounds__(kBlock) void k_hot_tau0(const int32_t* __restrict__
     if (threadIdx.x == 0 && k) atomicMax(tau0 + blockIdx.y, k);
 }
 
-constexpr int kHotLdsWords = 1024;   // k_hot_bx stages up to 32k sub-bin bits in LDS
 
 // per label position: bit j of the label's words = (order key of U_j >=
 // tau0); grid (ceil(max words / 256), dense labels), one word per thread
@@ -820,36 +819,13 @@ __global__ __launch_bounds__(kBlock) void k_hot_bits(const int32_t* __restrict__
 // into kHotCells u-cells (the top bits of wu) and a cell is marked
 // (k_hot_ucells, once per posterior and n) when the x-range of its v-range
 // can touch a set bit or leave the bins.  A candidate in an unmarked cell
-// cannot be listed; the others (~1 %) queue per wave and are drawn in fp64
-// 64 at a time (icdf_draw, the exact draw of every kernel) and tested
-// against the sub-bit bits as before -- so the list is exactly the one the
+// cannot be listed; the others (~1 %) go to a mark list per cell and are
+// drawn in fp64 by k_hot_draw (icdf_draw, the exact draw of every kernel)
+// and tested against the sub-bin bits -- so the list is exactly the one the
 // full draw gives.
-constexpr int kHotBuf = 128;      // listed entries per wave
 constexpr int kHotCellBits = 11;
 constexpr int kHotCells = 1 << kHotCellBits;   // u-cells per sampling component
 constexpr int kHotCellWords = kHotCells / 32;
-constexpr int kHotQ = 128;        // a wave's ring of candidates to draw in fp64
-
-// one wave's buffer to the cell's list (count n, wave-uniform)
-__device__ __forceinline__ void hot_wave_flush(int n, const int32_t* bi, const double* bxv,
-                                               int32_t* __restrict__ hcnt, int32_t* __restrict__ hidx,
-                                               double* __restrict__ hx, size_t cell, int64_t hstride,
-                                               int32_t* __restrict__ hflag) {
-    const int lane = threadIdx.x & 63;
-    int gb = 0;
-    if (lane == 0) gb = atomicAdd(hcnt + cell, n);
-    gb = __builtin_amdgcn_readfirstlane(__shfl(gb, 0));
-    // a cell's list is hstride long: past it the round falls back to
-    // screening every candidate (hflag bit 2), so nothing is lost
-    if (lane == 0 && gb + n > hstride) atomicOr(hflag, 2);
-    __builtin_amdgcn_wave_barrier();   // (the wave's own LDS writes above: in order per wave)
-    for (int k = lane; k < n; k += 64)
-        if (gb + k < hstride) {
-            hidx[cell * (size_t)hstride + gb + k] = bi[k];
-            hx[cell * (size_t)hstride + gb + k] = bxv[k];
-        }
-    __builtin_amdgcn_wave_barrier();   // (read before the buffer is refilled)
-}
 
 // per dense label position: the set bits of the label's sub-bin words
 // before each word (exclusive prefix), one workgroup per label
@@ -998,172 +974,179 @@ __device__ __forceinline__ void hot_items_body(const int32_t* __restrict__ hcnt,
     if (threadIdx.x == 0) pre[cells] = carry;
 }
 
-// The draw kernel.  Tile map only: workgroups stride over the cell's tiles
-// of R * 256 candidates (Philox pairs per thread), the sampling records and
-// the label's u-cells staged once per workgroup (the launch requires the
-// records in LDS).  Per candidate: the Philox words, the pick, one u-cell
-// bit; a marked candidate joins its wave's ring (index, words; count in a
-// scalar register), which is drawn in fp64 whenever it holds 64, then its
-// sub-bin's bit is read.  The listed candidates gather in a buffer per WAVE
-// in LDS and go to the cell's list with one global atomic per wave flush
-// when the buffer would overflow, and one per workgroup for the waves'
-// remainders at the end.  (Round 4 measured other list forms on the same
-// box: one workgroup buffer flushed only at the end, 2.34 ms at 0.35 VALU
-// busy; flushed after every tile behind a barrier, 1.37 ms at 0.75.)
-// LDS_BITS: every label's bits fit in LDS (the host knows the largest
-// label's sub-bins) -- the bit test is then a ds_read; otherwise every
-// label reads them from global memory.
-template <int R, bool LDS_BITS>
-__global__ __launch_bounds__(kBlock, 4) void k_hot_bx(
+// The draw kernel, in two launches (round 6).  k_hot_bx (tile map only:
+// workgroups stride over the cell's tiles of R * 256 candidates, Philox
+// pairs per thread, the sampling records and the label's u-cells staged once
+// per workgroup -- the launch requires the records in LDS): per candidate
+// the Philox words, the component pick and one u-cell bit; the marked
+// candidates' indices (~1-2 %) gather in a buffer per WAVE in LDS (count in a
+// scalar register) and go to the cell's mark list with one global atomic per
+// flush.  No fp64 in it: ~40 VGPRs, 8 waves per SIMD to hide the dependent
+// LDS lookups of the pick.  k_hot_draw then draws the marked candidates by
+// the inverse CDF in fp64 (full lanes) and lists those whose sub-bin's bit
+// is set (or that fall outside the bins) -- exactly the list the full draw
+// gives.  (Round 4 measured list forms on the same box: one workgroup
+// buffer flushed only at the end, 2.34 ms at 0.35 VALU busy; flushed after
+// every tile behind a barrier, 1.37 ms at 0.75 -- hence per-wave buffers.)
+constexpr int kMarkBuf = 128;     // marked indices per wave
+
+// one wave's buffered indices to the cell's list (count n, wave-uniform);
+// past mstride the list overflows: hflag bit 2 (the round re-runs with the
+// expansion screen over every candidate)
+__device__ __forceinline__ void mark_wave_flush(int n, const int32_t* bi, int32_t* __restrict__ mcnt,
+                                                int32_t* __restrict__ midx, size_t cell, int64_t mstride,
+                                                int32_t* __restrict__ hflag) {
+    const int lane = threadIdx.x & 63;
+    int gb = 0;
+    if (lane == 0) gb = atomicAdd(mcnt + cell, n);
+    gb = __builtin_amdgcn_readfirstlane(__shfl(gb, 0));
+    if (lane == 0 && gb + n > mstride) atomicOr(hflag, 2);
+    __builtin_amdgcn_wave_barrier();
+    for (int k = lane; k < n; k += 64)
+        if (gb + k < mstride) midx[cell * (size_t)mstride + gb + k] = bi[k];
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <int R>
+__global__ __launch_bounds__(kBlock, 8) void k_hot_bx(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
-    const BxLabel* __restrict__ bx, const uint32_t* __restrict__ hbits, const uint32_t* __restrict__ ucell,
-    int64_t n, int64_t cand_offset, uint64_t seed, const uint32_t* __restrict__ rounds, int32_t nl,
-    int32_t* __restrict__ hcnt, int32_t* __restrict__ hidx, double* __restrict__ hx, int32_t* __restrict__ err,
-    int64_t hstride, int32_t* __restrict__ hflag, uint32_t* __restrict__ done, int32_t* __restrict__ items,
-    int64_t item_per) {
+    const uint32_t* __restrict__ ucell, int64_t n, int64_t cand_offset, uint64_t seed,
+    const uint32_t* __restrict__ rounds, int32_t nl, int32_t* __restrict__ mcnt, int32_t* __restrict__ midx,
+    int64_t mstride, int32_t* __restrict__ hflag) {
     static_assert(R % 2 == 0, "Philox pairs");
     const int li = group[blockIdx.y];
     const DLabel L = labels[li];
-    const BxLabel B = bx[li];
     __shared__ SampLds sl;
-    __shared__ uint32_t ucw[kSampLds * kHotCellWords];
-    __shared__ uint32_t sbits[LDS_BITS ? kHotLdsWords : 1];
-    __shared__ uint32_t q_i[kBlock / 64][kHotQ], q_p[kBlock / 64][kHotQ], q_u[kBlock / 64][kHotQ];
-    __shared__ int32_t buf_i[kBlock / 64][kHotBuf];
-    __shared__ double buf_x[kBlock / 64][kHotBuf];
-    const int nsb = B.nbins * kBxSub;
-    if constexpr (LDS_BITS)
-        for (int w = threadIdx.x; w < (nsb >> 5); w += kBlock) sbits[w] = hbits[(B.sb_off >> 5) + w];
-    const uint32_t* __restrict__ gbits = hbits + (B.sb_off >> 5);
+    extern __shared__ uint32_t ucw[];   // (dynamic: the largest label's ns x kHotCellWords)
+    __shared__ int32_t buf[kBlock / 64][kMarkBuf];
     {
         const uint32_t* uc = ucell + (size_t)blockIdx.y * kSampLds * kHotCellWords;
         for (int w = threadIdx.x; w < L.ns * kHotCellWords; w += kBlock) ucw[w] = uc[w];
     }
-    (void)stage_samp(L, samp, &sl);   // (its barriers publish the stages above; the launch checked ns <= kSampLds)
+    (void)stage_samp(L, samp, &sl);   // (its barriers publish the stage above; the launch checked ns <= kSampLds)
     const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
     const uint32_t rk = rounds[blockIdx.z];
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     constexpr int64_t per = (int64_t)R * kBlock;
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
     const SampShared src{&sl, __builtin_amdgcn_readfirstlane(sl.steps)};
-    int wn = 0;        // this wave's buffered list entries (wave-uniform)
-    int qh = 0, qn = 0;   // its ring's head and count (wave-uniform)
+    int wn = 0;   // this wave's buffered indices (wave-uniform)
+    for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per) {
+        const uint32_t g0 = (uint32_t)(cand_offset + base);
+        const bool paired = (g0 & 1u) == 0;   // (uniform)
+        // the tile's words, picks and u-cell bits for all R slots at once
+        // (independent chains: their LDS lookups overlap)
+        uint32_t wp[R], wu[R];
+#pragma unroll
+        for (int r = 0; r < R; r += 2) {
+            const uint32_t c0 = tile_cand(r, threadIdx.x, kBlock);
+            if (paired) {
+                const U4 W = philox4x32_10(U4{(g0 + c0) >> 1, 0u, (uint32_t)L.stream, rk}, k0, k1);
+                wp[r] = W.x;
+                wu[r] = W.y;
+                wp[r + 1] = W.z;
+                wu[r + 1] = W.w;
+            } else {
+                draw_words(L, k0, k1, g0 + c0, rk, wp[r], wu[r]);
+                draw_words(L, k0, k1, g0 + c0 + 1u, rk, wp[r + 1], wu[r + 1]);
+            }
+        }
+        uint32_t mark = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int k = src.pick_index(wp[r]);
+            const uint32_t uc = wu[r] >> (32 - kHotCellBits);
+            const bool m = base + (int64_t)tile_cand(r, threadIdx.x, kBlock) < n &&
+                           ((ucw[k * kHotCellWords + (uc >> 5)] >> (uc & 31)) & 1u);
+            mark |= (uint32_t)m << r;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const bool m = (mark >> r) & 1u;
+            const uint64_t bal = __ballot(m);
+            if (!bal) continue;
+            const int c = (int)__popcll(bal);
+            if (wn + c > kMarkBuf) {   // (wave-uniform)
+                mark_wave_flush(wn, buf[wv], mcnt, midx, cell, mstride, hflag);
+                wn = 0;
+            }
+            if (m) buf[wv][wn + (int)lanes_below(bal)] = (int32_t)(base + (int64_t)tile_cand(r, threadIdx.x, kBlock));
+            wn += c;
+        }
+    }
+    if (wn > 0) mark_wave_flush(wn, buf[wv], mcnt, midx, cell, mstride, hflag);
+}
+
+// The marked candidates of every (round, dense label) cell: the words
+// again (one Philox call each), the inverse-CDF draw in fp64 and the sub-bin
+// test; listed ones -- bit set, or outside the bins (or NaN) -- go to the
+// cell's hot list (hidx, hx) with one atomic per wave.  Grid (workgroups
+// per cell, cells); the workgroup that finishes last numbers k_screen_hot's
+// work items (hot_items_body).
+__global__ __launch_bounds__(kBlock) void k_hot_draw(
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
+    const BxLabel* __restrict__ bx, const uint32_t* __restrict__ hbits, int64_t cand_offset, uint64_t seed,
+    const uint32_t* __restrict__ rounds, int32_t nl, const int32_t* __restrict__ mcnt,
+    const int32_t* __restrict__ midx, int64_t mstride, int32_t* __restrict__ hcnt, int32_t* __restrict__ hidx,
+    double* __restrict__ hx, int32_t* __restrict__ err, int64_t hstride, int32_t* __restrict__ hflag,
+    uint32_t* __restrict__ done, int32_t* __restrict__ items, int64_t item_per) {
+    const size_t cell = blockIdx.y;
+    const int li = group[cell % (size_t)nl];
+    const DLabel L = labels[li];
+    const BxLabel B = bx[li];
+    __shared__ SampLds sl;
+    (void)stage_samp(L, samp, &sl);
+    const SampShared src{&sl, __builtin_amdgcn_readfirstlane(sl.steps)};
+    const int64_t nsb = (int64_t)B.nbins * kBxSub;
+    const uint32_t* __restrict__ gbits = hbits + (B.sb_off >> 5);
+    const uint32_t rk = rounds[cell / (size_t)nl];
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    const int64_t m = min((int64_t)mcnt[cell], mstride);
     bool bad = false;
-    // the ring's first min(qn, 64) entries drawn in fp64 and tested
-    auto drain = [&](int cnt) {
+    for (int64_t j0 = (int64_t)blockIdx.x * kBlock; j0 < m; j0 += (int64_t)gridDim.x * kBlock) {
+        const int64_t j = j0 + threadIdx.x;
         bool take = false;
         int32_t ci = 0;
         double x = 0.0;
-        if (lane < cnt) {
-            const int e = (qh + lane) & (kHotQ - 1);
-            ci = (int32_t)q_i[wv][e];
-            const uint32_t wp = q_p[wv][e], wu = q_u[wv][e];
+        if (j < m) {
+            ci = midx[cell * (size_t)mstride + j];
+            uint32_t wp, wu;
+            draw_words(L, k0, k1, (uint32_t)(cand_offset + ci), rk, wp, wu);
             x = icdf_draw(L, src.comp(wp), wp, wu);
             bad = bad || x != x;
             const double f = (x - L.centre - B.xlo) * B.inv_sbw;
             if (f >= 0.0 && f < (double)nsb) {
-                const int j = (int)f;
-                uint32_t word;
-                if constexpr (LDS_BITS) word = sbits[j >> 5];
-                else word = gbits[j >> 5];
-                take = (word >> (j & 31)) & 1u;
+                const int64_t s = (int64_t)f;
+                take = (gbits[s >> 5] >> (s & 31)) & 1u;
             } else {
                 take = true;   // outside the bins (or NaN): always listed
             }
         }
         const uint64_t bal = __ballot(take);
         if (bal) {
-            const int c = __builtin_amdgcn_readfirstlane((int)__popcll(bal));
-            if (wn + c > kHotBuf) {   // (wave-uniform)
-                hot_wave_flush(wn, buf_i[wv], buf_x[wv], hcnt, hidx, hx, cell, hstride, hflag);
-                wn = 0;
-            }
-            if (take) {
-                const int k = wn + (int)lanes_below(bal);
-                buf_i[wv][k] = ci;
-                buf_x[wv][k] = x;
-            }
-            wn += c;
-        }
-        __builtin_amdgcn_wave_barrier();   // (the ring's entries read before they are overwritten)
-    };
-    for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per) {
-        const uint32_t g0 = (uint32_t)(cand_offset + base);
-        const bool paired = (g0 & 1u) == 0;   // (uniform)
-#pragma unroll
-        for (int r = 0; r < R; r += 2) {
-            const uint32_t c0 = tile_cand(r, threadIdx.x, kBlock);
-            uint32_t wp[2], wu[2];
-            if (paired) {
-                const U4 W = philox4x32_10(U4{(g0 + c0) >> 1, 0u, (uint32_t)L.stream, rk}, k0, k1);
-                wp[0] = W.x;
-                wu[0] = W.y;
-                wp[1] = W.z;
-                wu[1] = W.w;
-            } else {
-                draw_words(L, k0, k1, g0 + c0, rk, wp[0], wu[0]);
-                draw_words(L, k0, k1, g0 + c0 + 1u, rk, wp[1], wu[1]);
-            }
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int64_t i = base + (int64_t)c0 + h;
-                const int k = src.pick_index(wp[h]);
-                const uint32_t uc = wu[h] >> (32 - kHotCellBits);
-                const bool mark = i < n && ((ucw[k * kHotCellWords + (uc >> 5)] >> (uc & 31)) & 1u);
-                const uint64_t bal = __ballot(mark);
-                if (!bal) continue;
-                if (mark) {
-                    const int e = (qh + qn + (int)lanes_below(bal)) & (kHotQ - 1);
-                    q_i[wv][e] = (uint32_t)i;
-                    q_p[wv][e] = wp[h];
-                    q_u[wv][e] = wu[h];
-                }
-                qn += (int)__popcll(bal);
-                __builtin_amdgcn_wave_barrier();
-                if (qn >= 64) {   // (wave-uniform)
-                    drain(64);
-                    qh = (qh + 64) & (kHotQ - 1);
-                    qn -= 64;
-                }
+            const int lane = threadIdx.x & 63;
+            int gb = 0;
+            if (lane == 0) gb = atomicAdd(hcnt + cell, (int)__popcll(bal));
+            gb = __builtin_amdgcn_readfirstlane(__shfl(gb, 0));
+            if (lane == 0 && gb + (int)__popcll(bal) > hstride) atomicOr(hflag, 2);
+            const int at = gb + (int)lanes_below(bal);
+            if (take && at < hstride) {
+                hidx[cell * (size_t)hstride + at] = ci;
+                hx[cell * (size_t)hstride + at] = x;
             }
         }
     }
-    if (qn > 0) drain(qn);
     if (bad) atomicOr(err, 1);
-    // the end: every wave's remainder to the cell's list behind ONE atomic
-    // for the workgroup (a shard's round has few cells, each striped over
-    // many workgroups: per-wave atomics on its one counter cost 0.5 ms)
-    __shared__ int wcnt[kBlock / 64], wbase;
-    if (lane == 0) wcnt[wv] = wn;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int tot = 0;
-        for (int w = 0; w < kBlock / 64; ++w) tot += wcnt[w];
-        wbase = tot ? atomicAdd(hcnt + cell, tot) : 0;
-        // a cell's list is hstride long: past it the round falls back to
-        // screening every candidate (hflag bit 2), so nothing is lost
-        if (tot && wbase + tot > hstride) atomicOr(hflag, 2);
-    }
-    __syncthreads();
-    int off = wbase;
-    for (int w = 0; w < wv; ++w) off += wcnt[w];
-    for (int k = lane; k < wn; k += 64)
-        if (off + k < hstride) {
-            hidx[cell * (size_t)hstride + off + k] = buf_i[wv][k];
-            hx[cell * (size_t)hstride + off + k] = buf_x[wv][k];
-        }
     // the workgroup that finishes last numbers k_screen_hot's work items
-    // (round 6: k_hot_items was a launch of its own)
     __shared__ bool last;
     if (threadIdx.x == 0) {
-        __threadfence();   // (this workgroup's count and entries before the counter)
-        last = atomicAdd(done, 1u) == gridDim.x * gridDim.y * gridDim.z - 1;
+        __threadfence();   // (this workgroup's counts and entries before the counter)
+        last = atomicAdd(done, 1u) == gridDim.x * gridDim.y - 1;
     }
     __syncthreads();
     if (!last) return;   // (uniform)
     __threadfence();     // (acquire: every cell's count)
-    const int64_t cells = (int64_t)gridDim.y * gridDim.z;
-    hot_items_body<kBlock>(hcnt, cells, hstride, item_per, items, items + cells + 1);
+    hot_items_body<kBlock>(hcnt, (int64_t)gridDim.y, hstride, item_per, items, items + gridDim.y + 1);
 }
 
 
@@ -1359,10 +1342,11 @@ constexpr int kScreenR = TPE_SCREEN_R;
 #endif
 constexpr int kBxR = TPE_BX_R;
 
-// candidates per thread in k_hot_bx (draw + one sub-bin read each), and the
-// workgroups per cell striding over the listed candidates in k_screen_hot
+// candidates per thread and tile in k_hot_bx (Philox words, pick and u-cell
+// bit each), and the workgroups per cell striding over the listed
+// candidates in k_screen_hot
 #ifndef TPE_HOT_R
-#define TPE_HOT_R 6   // (8 spilled 8 VGPRs at the 96-register cap: 48 MB of scratch writes per round, r4aj)
+#define TPE_HOT_R 8
 #endif
 constexpr int kHotR = TPE_HOT_R;
 constexpr unsigned kHotScreenWgs = 1024;   // k_screen_hot's persistent grid (4 workgroups per CU: LDS)
@@ -1374,7 +1358,7 @@ constexpr int64_t kHotWgs = TPE_HOT_WGS;
 #define TPE_HOT_BX_WGS 16384
 #endif
 constexpr int64_t kHotBxWgs = TPE_HOT_BX_WGS;   // k_hot_bx's workgroups over a round, at most
-constexpr int64_t kHotFillWgs = 2560;           //   at least (5 per CU resident: two passes)
+constexpr int64_t kHotFillWgs = 2560;           //   at least (two passes of the resident workgroups)
 constexpr int64_t kHotMinTiles = 6;             //   tiles per workgroup, at least (unless filling)
 constexpr int kQR = 8;   // candidates per thread, k_qfused_tiles
 constexpr int kQLdsKeys = 1024;   // grid values whose keys k_qfused_tiles stages in LDS
@@ -3622,30 +3606,28 @@ void launch_round(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
     bracket(ctx, MODE, 1);
 }
 
-// Chunks of the above mixtures for a packed sampled round: enough
-// workgroups for ~6-8 generations of the 1280 resident ones (5 per CU: the
-// 32 KB exp table is k_round_chunk's only LDS), so the tail is short; no
-// chunk shorter than kMinChunk components, where the redundant sampling of
-// every chunk would start to show.  Config 5 (~1200 workgroups): 7 chunks
-// (sweep in DESIGN.md section 6).
-constexpr int64_t kChunkTargetWG = 8192;
+// Chunks of the above mixtures for a packed sampled round: a fixed length
+// of kChunkLen components (round 6; the count followed the workgroups of the
+// round before), so a label's summation order -- chunk sums added in order
+// -- depends on the label alone and a label-sharded multi-device context
+// (or a label-shard rank) returns the one-context bits.  Config 5 (50k
+// above components): 7 chunks, as the workgroup rule picked there.
+// TPE_OPT_CHUNKS forces a count (tests): chunk = ceil(na_max / count).
+constexpr int32_t kChunkLen = 8192;
 
-constexpr int32_t kMinChunk = 2048;
-constexpr int32_t kMaxChunk = 16384;
-
-int dense_chunks(const tpe_ctx* ctx, uint32_t gx, int nl) {
-    if (ctx->chunks_forced) return ctx->chunks_forced;
-    int32_t na_max = 0;
+int dense_chunks(const tpe_ctx* ctx) {
+    int32_t na_max = 1;
     for (int m : {DENSE_GMM, DENSE_LGMM})
         for (int li : ctx->P->h_group[m]) na_max = std::max(na_max, ctx->P->h_labels[li].na);
-    // never longer than kMaxChunk components: the screened map's fp64
-    // re-score repeats these chunks, and ~1 candidate per (round, label)
-    // over an unchunked 50k-component mixture left it 2 waves per SIMD
-    const int min_nch = (int)((na_max + kMaxChunk - 1) / kMaxChunk);
-    const int64_t wg = (int64_t)gx * nl;
-    if (wg >= kChunkTargetWG / 2) return std::max(1, min_nch);
-    const int64_t want = (kChunkTargetWG + wg - 1) / wg;
-    return (int)std::max<int64_t>(std::max(1, min_nch), std::min<int64_t>(want, na_max / kMinChunk));
+    if (ctx->chunks_forced) return ctx->chunks_forced;
+    return (int)((na_max + kChunkLen - 1) / kChunkLen);
+}
+
+int32_t dense_chunk_len(const tpe_ctx* ctx, int nch) {
+    int32_t na_max = 1;
+    for (int m : {DENSE_GMM, DENSE_LGMM})
+        for (int li : ctx->P->h_group[m]) na_max = std::max(na_max, ctx->P->h_labels[li].na);
+    return ctx->chunks_forced ? (na_max + nch - 1) / nch : kChunkLen;
 }
 
 // nb + na summed over the dense labels: the terms an unwindowed screen sums
@@ -3668,10 +3650,7 @@ constexpr int64_t kWinMinN = 8192;
 // k_pick_packed): fp32 chunk sums, per-round selection, fp64 re-score with
 // the chunked map's summation order, per-round pick.
 int launch_screen_packed(tpe_ctx* ctx, const int32_t* grp, int nl, int nch, const RoundArgs& a) {
-    int32_t na_max = 1;
-    for (int m : {DENSE_GMM, DENSE_LGMM})
-        for (int li : ctx->P->h_group[m]) na_max = std::max(na_max, ctx->P->h_labels[li].na);
-    const int32_t chunk = (na_max + nch - 1) / nch;
+    const int32_t chunk = dense_chunk_len(ctx, nch);
     // the fp32 pass and the pick use their own, wider slot map: kScreenR
     // candidates per thread (whole rounds per workgroup, as the packed map);
     // the chunks stay those of the fp64 packed map, which the re-score repeats
@@ -3916,7 +3895,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
     const Comp<T>* comps;
     if constexpr (sizeof(T) == 8) comps = ctx->P->comps64.p; else comps = ctx->P->comps32.p;
     const int32_t* grp = ctx->P->groups.p + ctx->P->group_off[DENSE_GMM];
-    const int nch = a.S.cpack ? dense_chunks(ctx, a.gx_whole, nl) : 1;
+    const int nch = a.S.cpack ? dense_chunks(ctx) : 1;
     if (sizeof(T) == 8 && ctx->screen && a.S.cpack == 0) {   // fp32 screen + fp64 re-score
         const size_t cells = (size_t)a.n_rounds * nl;
         bool use_bx = false, hot = false, plan_done = false;
@@ -3974,6 +3953,8 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                 HIPCHK(ctx, ctx->hot_t.reserve(cells));
                 HIPCHK(ctx, ctx->hot_flag.reserve(1));
                 add_fill(fs, ctx->hot_cnt.p, cells * sizeof(int32_t), 0);
+                HIPCHK(ctx, ctx->hot_mcnt.reserve(cells));
+                add_fill(fs, ctx->hot_mcnt.p, cells * sizeof(int32_t), 0);
                 add_fill(fs, ctx->hot_t.p, cells * sizeof(unsigned long long), 0);
                 add_fill(fs, ctx->hot_flag.p, sizeof(int32_t), 0);
             }
@@ -4002,18 +3983,29 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                      std::max<int64_t>((kHotFillWgs + cells_l - 1) / cells_l, tiles_c / kHotMinTiles)});
                 const dim3 hg((unsigned)std::max<int64_t>(1, per_cell), nl, a.gz);
                 HIPCHK(ctx, ctx->hot_items.reserve((size_t)cells + 2));
-                if (P.bx_sb_max <= (int64_t)kHotLdsWords * 32)
-                    hipLaunchKernelGGL((k_hot_bx<kHotR, true>), hg, dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
-                                       P.samp.p, P.bx.p, ctx->hot_bits.p, ctx->hot_ucell.p, a.n, a.cand_offset,
-                                       a.seed, ctx->rounds.p, nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p,
-                                       ctx->errflag.p, lst, ctx->hot_flag.p, ctx->rs_done.p + 2, ctx->hot_items.p,
-                                       (int64_t)kBxR * kBlock);
-                else
-                    hipLaunchKernelGGL((k_hot_bx<kHotR, false>), hg, dim3(kBlock), 0, ctx->stream, P.labels.p, grp,
-                                       P.samp.p, P.bx.p, ctx->hot_bits.p, ctx->hot_ucell.p, a.n, a.cand_offset,
-                                       a.seed, ctx->rounds.p, nl, ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p,
-                                       ctx->errflag.p, lst, ctx->hot_flag.p, ctx->rs_done.p + 2, ctx->hot_items.p,
-                                       (int64_t)kBxR * kBlock);
+                int32_t ns_max = 1;
+                for (int m : {DENSE_GMM, DENSE_LGMM})
+                    for (int li : ctx->P->h_group[m]) ns_max = std::max(ns_max, ctx->P->h_labels[li].ns);
+                const size_t ucw_bytes = (size_t)ns_max * kHotCellWords * sizeof(uint32_t);
+                // the mark lists: a multiple of the hot list (marked >= listed)
+                const int64_t mst = std::min<int64_t>(a.n, 2 * lst);
+                HIPCHK(ctx, ctx->hot_mi.reserve(cells * mst));
+                hipLaunchKernelGGL((k_hot_bx<kHotR>), hg, dim3(kBlock), ucw_bytes, ctx->stream, P.labels.p, grp,
+                                   P.samp.p, ctx->hot_ucell.p, a.n, a.cand_offset, a.seed, ctx->rounds.p, nl,
+                                   ctx->hot_mcnt.p, ctx->hot_mi.p, mst, ctx->hot_flag.p);
+                // the exact draw of the marked: workgroups per cell for ~1.5 % of
+                // the round at 256 per workgroup, the chip filled once
+                const int64_t dw = std::max<int64_t>(
+                    1, std::min<int64_t>((mst + kBlock - 1) / kBlock,
+                                         std::max<int64_t>((a.n / 64 + kBlock - 1) / kBlock,
+                                                           (kHotFillWgs + (int64_t)cells - 1) / (int64_t)cells)));
+                hipLaunchKernelGGL(k_hot_draw, dim3((unsigned)dw, (unsigned)cells), dim3(kBlock), 0, ctx->stream,
+                                   P.labels.p, grp, P.samp.p, P.bx.p, ctx->hot_bits.p, a.cand_offset, a.seed,
+                                   ctx->rounds.p, nl, ctx->hot_mcnt.p, ctx->hot_mi.p, mst, ctx->hot_cnt.p,
+                                   ctx->hot_i.p, ctx->hot_x.p, ctx->errflag.p, lst, ctx->hot_flag.p,
+                                   ctx->rs_done.p + 2, ctx->hot_items.p, (int64_t)kBxR * kBlock);
+                // (the screen's bracket: the two draw kernels)
+                if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
                 hipLaunchKernelGGL((k_screen_hot<kBxR>), dim3(kHotScreenWgs), dim3(kBlock), 0, ctx->stream,
                                    P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p, P.bx_loff.p, P.bx_list.p, a.n,
                                    nl, (int64_t)cells, ctx->hot_items.p, ctx->hot_items.p + cells + 1,
@@ -4021,8 +4013,8 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                                    ctx->scr_cnt.p, ctx->scr_idx.p, ctx->win_evals.p, P.bx_sb.p, ctx->hot_t.p, lst);
             } else {
                 screen_bx_all(ctx, grp, nl, a);
+                if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
             }
-            if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
             {
                 const int rc = rescore_reserve(ctx, cells, lst, s_max);
                 if (rc) return rc;
@@ -4179,10 +4171,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
         return rc;
     }
     if (nch > 1) {
-        int32_t na_max = 1;
-        for (int m : {DENSE_GMM, DENSE_LGMM})
-            for (int li : ctx->P->h_group[m]) na_max = std::max(na_max, ctx->P->h_labels[li].na);
-        const int32_t chunk = (na_max + nch - 1) / nch;
+        const int32_t chunk = dense_chunk_len(ctx, nch);
         const size_t planes = (size_t)nl * (nch + 2) * a.gx * (kR * kBlock);
         HIPCHK(ctx, ctx->chunk_part.reserve(planes));
 #define TPE_CHUNKED(RR)                                                                          \
@@ -5178,8 +5167,8 @@ TPE_DEV int tpe1_suggest_batch(tpe_ctx* ctx, uint64_t seed, const uint32_t* roun
                      nullptr, out, -1);
 }
 
-int tpe_score(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, double* lpdf_below,
-              double* lpdf_above, tpe_label_result* out) {
+TPE_DEV int tpe1_score(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, double* lpdf_below,
+                       double* lpdf_above, tpe_label_result* out) {
     if (!ctx || (!cand && n > 0)) return TPE_ERR_ARG;
     TPE_SETTLE(ctx);
     if (label < 0 || label >= ctx->P->n_labels) return ctx->fail(TPE_ERR_ARG, "label out of range");
@@ -5225,6 +5214,7 @@ int tpe_score(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, double
 int tpe_hot_probe(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, double* upper, double* lower,
                   double* mass) {
     if (!ctx || (n > 0 && (!cand || !upper || !lower || !mass))) return TPE_ERR_ARG;
+    TPE_NOT_LSHARD(ctx);
     TPE_SETTLE(ctx);
     if (label < 0 || label >= ctx->P->n_labels) return ctx->fail(TPE_ERR_ARG, "label out of range");
     const DLabel& d = ctx->P->h_labels[label];
@@ -5256,6 +5246,7 @@ int tpe_hot_probe(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, do
 int tpe_screen_probe(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, double* score32,
                      double* err_bound) {
     if (!ctx || (n > 0 && (!cand || !score32 || !err_bound))) return TPE_ERR_ARG;
+    TPE_NOT_LSHARD(ctx);
     TPE_SETTLE(ctx);
     if (label < 0 || label >= ctx->P->n_labels) return ctx->fail(TPE_ERR_ARG, "label out of range");
     const DLabel& d = ctx->P->h_labels[label];
@@ -5312,6 +5303,7 @@ int tpe_suggest_batch_device(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds
                              int64_t n_candidates, int64_t cand_offset, tpe_label_result* d_out,
                              tpe_label_result* out) {
     if (!ctx || !d_out || !rounds) return TPE_ERR_ARG;
+    TPE_NOT_LSHARD(ctx);
     if (!ctx->peers.empty()) return ctx->fail(TPE_ERR_ARG, "device results: single-device contexts only");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     if (n_candidates <= 0) return ctx->fail(TPE_ERR_ARG, "device results need candidates");

@@ -19,9 +19,25 @@
 //     sharding returns the single-device winners bit for bit.
 // Candidate indices are global (the Philox counter), so the shards draw
 // exactly the single-device candidate set.
+//
+// Label shards (round 6; the resident-history path -- tpe_history_reset,
+// append, the device builds, the index, the rounds -- with at least one
+// label per device, TPE_OPT_LABEL_SHARDS on): labels are independent (one
+// build_posterior_wrapper + broadcast_best per label, tpe.py:678-692,
+// 769-778), so device d holds only its labels (longest processing time
+// first: dense 1, quantized 1.5, categorical 0.5 -- parallel.label_shards'
+// partition), keeps each label's Philox stream (TPE_HAS_STREAM = its space
+// index), and uploads, appends, builds, indexes and runs whole rounds for
+// those labels alone; the host scatters each device's winners (48 B per
+// label) to their space positions.  The per-posterior work -- history
+// append, build, tie orders, expansion index -- then divides over the
+// devices with the candidates, where the candidate split repeats it on
+// every device.  Spaces with fewer labels than devices, tpe_set_posterior
+// and the one-shot tpe_build_posterior keep the candidate / round split.
 #include <hip/hip_runtime.h>
 
 #include <condition_variable>
+#include <algorithm>
 #include <functional>
 #include <mutex>
 #include <string>
@@ -295,6 +311,95 @@ int sharded_round(tpe_ctx* c, uint64_t seed, const uint32_t* rounds, int32_t n_r
     return TPE_OK;
 }
 
+// -------------------------------------------------------- label shards ----
+bool lsharded(const tpe_ctx* c) { return !c->lsh_ids.empty(); }
+
+double label_cost(const tpe_label_spec& s) {
+    if (s.kind == TPE_CATEGORICAL) return 0.5;
+    return (s.flags & TPE_HAS_Q) ? 1.5 : 1.0;
+}
+
+// the partition: largest cost to the least-loaded device (ties: lower
+// device, lower label), each device's labels in increasing order
+void lsh_assign(tpe_ctx* c, const tpe_label_spec* specs, int32_t L) {
+    const int nd = ndev(c);
+    c->lsh_ids.assign(nd, {});
+    std::vector<double> load(nd, 0.0);
+    std::vector<int32_t> order(L);
+    for (int32_t i = 0; i < L; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int32_t a, int32_t b) { return label_cost(specs[a]) > label_cost(specs[b]); });
+    for (int32_t i : order) {
+        int d = 0;
+        for (int k = 1; k < nd; ++k)
+            if (load[k] < load[d]) d = k;
+        c->lsh_ids[d].push_back(i);
+        load[d] += label_cost(specs[i]);
+    }
+    c->lsh_dev.assign(L, 0);
+    c->lsh_local.assign(L, 0);
+    for (int d = 0; d < nd; ++d) {
+        std::sort(c->lsh_ids[d].begin(), c->lsh_ids[d].end());
+        for (size_t j = 0; j < c->lsh_ids[d].size(); ++j) {
+            c->lsh_dev[c->lsh_ids[d][j]] = d;
+            c->lsh_local[c->lsh_ids[d][j]] = (int32_t)j;
+        }
+    }
+    c->lsh_L = L;
+}
+
+void lsh_clear(tpe_ctx* c) {
+    c->lsh_ids.clear();
+    c->lsh_dev.clear();
+    c->lsh_local.clear();
+    c->lsh_L = 0;
+}
+
+// a device's share of per-label orders (order_off[L + 1] / order over the
+// global labels) in its local numbering
+void lsh_orders(const std::vector<int32_t>& ids, const int64_t* order_off, const int32_t* order,
+                std::vector<int64_t>& off, std::vector<int32_t>& ord) {
+    off.assign(ids.size() + 1, 0);
+    ord.clear();
+    for (size_t j = 0; j < ids.size(); ++j) {
+        const int64_t a = order_off[ids[j]], b = order_off[ids[j] + 1];
+        ord.insert(ord.end(), order + a, order + b);
+        off[j + 1] = (int64_t)ord.size();
+    }
+}
+
+// a device's tie report (local labels + the split flag) into the global one
+void lsh_ties_merge(const std::vector<int32_t>& ids, const std::vector<int32_t>& t, int32_t L, int32_t* ties) {
+    for (size_t j = 0; j < ids.size(); ++j) ties[ids[j]] = t[j];
+    ties[L] |= t[ids.size()];
+}
+
+// one round of every device's labels, scattered into out[round][label]
+int lsh_round(tpe_ctx* c, uint64_t seed, const uint32_t* rounds, int32_t n_rounds, int64_t n, int64_t cand_offset,
+              tpe_label_result* out) {
+    const int nd = ndev(c);
+    const int32_t L = c->lsh_L;
+    std::vector<std::vector<tpe_label_result>> parts(nd);
+    int rc = for_all(c, [&](tpe_ctx* x, int d) {
+        const std::vector<int32_t>& ids = c->lsh_ids[d];
+        parts[d].resize((size_t)n_rounds * ids.size());
+        return tpe1_suggest_batch(x, seed, rounds, n_rounds, n, cand_offset, parts[d].data());
+    });
+    if (rc) return rc;
+    for (int d = 0; d < nd; ++d) {
+        const std::vector<int32_t>& ids = c->lsh_ids[d];
+        const size_t Ld = ids.size();
+        for (int32_t r = 0; r < n_rounds; ++r)
+            for (size_t j = 0; j < Ld; ++j) {
+                tpe_label_result v = parts[d][(size_t)r * Ld + j];
+                v.label = ids[j];
+                out[(size_t)r * L + ids[j]] = v;
+            }
+    }
+    aggregate_stats(c);
+    return TPE_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -338,6 +443,7 @@ int tpe_set_posterior(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_labe
                       const double* weights, const double* mus, const double* sigmas,
                       int64_t n_components) {
     if (!ctx) return TPE_ERR_ARG;
+    lsh_clear(ctx);   // (uploaded posteriors: replicated, candidate / round split)
     return for_all(ctx, [&](tpe_ctx* x, int) {
         return tpe1_set_posterior(x, labels, n_labels, weights, mus, sigmas, n_components);
     });
@@ -345,6 +451,10 @@ int tpe_set_posterior(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_labe
 
 int tpe_set_option(tpe_ctx* ctx, int32_t option, int64_t value) {
     if (!ctx) return TPE_ERR_ARG;
+    if (option == TPE_OPT_LABEL_SHARDS) {   // (the multi-device context's own: from the next history reset)
+        ctx->lsh_enable = value != 0;
+        return TPE_OK;
+    }
     return for_all(ctx, [&](tpe_ctx* x, int) { return tpe1_set_option(x, option, value); });
 }
 
@@ -361,16 +471,58 @@ int tpe_arm_prepare(tpe_ctx* ctx, int64_t n_candidates, int32_t n_rounds) {
 int tpe_history_reset(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
                       const double* cat_p, int64_t n_cat_p) {
     if (!ctx) return TPE_ERR_ARG;
-    return for_all(ctx, [&](tpe_ctx* x, int) {
-        return tpe1_history_reset(x, specs, n_labels, cat_p, n_cat_p);
+    const int nd = ndev(ctx);
+    if (nd == 1 || !ctx->lsh_enable || !specs || n_labels < nd) {
+        lsh_clear(ctx);
+        return for_all(ctx, [&](tpe_ctx* x, int) {
+            return tpe1_history_reset(x, specs, n_labels, cat_p, n_cat_p);
+        });
+    }
+    lsh_assign(ctx, specs, n_labels);
+    const int rc = for_all(ctx, [&](tpe_ctx* x, int d) {
+        std::vector<tpe_label_spec> sub;
+        for (int32_t g : ctx->lsh_ids[d]) {
+            tpe_label_spec sp = specs[g];
+            if (!(sp.flags & TPE_HAS_STREAM)) {   // (its stream: its space position)
+                sp.flags |= TPE_HAS_STREAM;
+                sp.stream = g;
+            }
+            sub.push_back(sp);
+        }
+        return tpe1_history_reset(x, sub.data(), (int32_t)sub.size(), cat_p, n_cat_p);
     });
+    if (rc) lsh_clear(ctx);
+    return rc;
 }
 
 int tpe_history_append(tpe_ctx* ctx, const int64_t* n_new, const int32_t* obs_trial,
                        const double* obs_val) {
     if (!ctx) return TPE_ERR_ARG;
-    return for_all(ctx, [&](tpe_ctx* x, int) {
-        return tpe1_history_append(x, n_new, obs_trial, obs_val);
+    if (!lsharded(ctx))
+        return for_all(ctx, [&](tpe_ctx* x, int) {
+            return tpe1_history_append(x, n_new, obs_trial, obs_val);
+        });
+    if (!n_new) return ctx->fail(TPE_ERR_ARG, "tpe_history_append: no counts");
+    const int32_t L = ctx->lsh_L;
+    std::vector<int64_t> off(L + 1, 0);   // (the new observations: label after label)
+    for (int32_t l = 0; l < L; ++l) {
+        if (n_new[l] < 0) return ctx->fail(TPE_ERR_ARG, "tpe_history_append: negative count");
+        off[l + 1] = off[l] + n_new[l];
+    }
+    return for_all(ctx, [&](tpe_ctx* x, int d) {
+        const std::vector<int32_t>& ids = ctx->lsh_ids[d];
+        std::vector<int64_t> nn(ids.size());
+        std::vector<int32_t> tr;
+        std::vector<double> va;
+        for (size_t j = 0; j < ids.size(); ++j) {
+            const int64_t a = off[ids[j]], b = off[ids[j] + 1];
+            nn[j] = b - a;
+            if (b > a) {
+                tr.insert(tr.end(), obs_trial + a, obs_trial + b);
+                va.insert(va.end(), obs_val + a, obs_val + b);
+            }
+        }
+        return tpe1_history_append(x, nn.data(), tr.data(), va.data());
     });
 }
 
@@ -389,21 +541,147 @@ int tpe_build_posterior_resident_ordered(tpe_ctx* ctx, const double* losses, int
                                          const uint8_t* below, const int64_t* order_off, const int32_t* order,
                                          int32_t* n_below_out, int32_t* ties) {
     if (!ctx) return TPE_ERR_ARG;
-    return for_all(ctx, [&](tpe_ctx* x, int d) {
-        return tpe1_build_posterior_resident_ordered(x, losses, n_trials, n_valid, gamma, prior_weight, lf,
-                                                     below, order_off, order, d == 0 ? n_below_out : nullptr,
-                                                     d == 0 ? ties : nullptr);
+    if (!lsharded(ctx))
+        return for_all(ctx, [&](tpe_ctx* x, int d) {
+            return tpe1_build_posterior_resident_ordered(x, losses, n_trials, n_valid, gamma, prior_weight, lf,
+                                                         below, order_off, order, d == 0 ? n_below_out : nullptr,
+                                                         d == 0 ? ties : nullptr);
+        });
+    const int nd = ndev(ctx);
+    const int32_t L = ctx->lsh_L;
+    std::vector<std::vector<int32_t>> td(nd);
+    const int rc = for_all(ctx, [&](tpe_ctx* x, int d) {
+        const std::vector<int32_t>& ids = ctx->lsh_ids[d];
+        std::vector<int64_t> off;
+        std::vector<int32_t> ord;
+        const bool orders = order_off && order && order_off[L] > 0;
+        if (orders) lsh_orders(ids, order_off, order, off, ord);
+        td[d].assign(ids.size() + 1, 0);
+        return tpe1_build_posterior_resident_ordered(x, losses, n_trials, n_valid, gamma, prior_weight, lf, below,
+                                                     orders ? off.data() : nullptr, orders ? ord.data() : nullptr,
+                                                     d == 0 ? n_below_out : nullptr, td[d].data());
     });
+    if (rc) return rc;
+    if (ties) {
+        std::fill(ties, ties + L + 1, 0);
+        for (int d = 0; d < nd; ++d) lsh_ties_merge(ctx->lsh_ids[d], td[d], L, ties);
+    }
+    return TPE_OK;
 }
 
 int tpe_rebuild_labels(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t n_valid, double gamma,
                        double prior_weight, int32_t lf, const int64_t* order_off, const int32_t* order,
                        const int32_t* labels, int32_t n_only, int32_t* n_below_out, int32_t* ties) {
     if (!ctx) return TPE_ERR_ARG;
-    return for_all(ctx, [&](tpe_ctx* x, int d) {
-        return tpe1_rebuild_labels(x, losses, n_trials, n_valid, gamma, prior_weight, lf, order_off, order, labels,
-                                   n_only, d == 0 ? n_below_out : nullptr, d == 0 ? ties : nullptr);
+    if (!lsharded(ctx))
+        return for_all(ctx, [&](tpe_ctx* x, int d) {
+            return tpe1_rebuild_labels(x, losses, n_trials, n_valid, gamma, prior_weight, lf, order_off, order,
+                                       labels, n_only, d == 0 ? n_below_out : nullptr, d == 0 ? ties : nullptr);
+        });
+    if (!labels || n_only <= 0 || !order_off) return ctx->fail(TPE_ERR_ARG, "tpe_rebuild_labels: no labels");
+    const int nd = ndev(ctx);
+    const int32_t L = ctx->lsh_L;
+    std::vector<std::vector<int32_t>> td(nd);
+    std::vector<int32_t> nbd(nd, -1);
+    const int rc = for_all(ctx, [&](tpe_ctx* x, int d) {
+        const std::vector<int32_t>& ids = ctx->lsh_ids[d];
+        td[d].assign(ids.size() + 1, 0);
+        std::vector<int32_t> mine;   // (its labels of the subset, local numbers: increasing)
+        for (int32_t i = 0; i < n_only; ++i) {
+            const int32_t g = labels[i];
+            if (g < 0 || g >= L) return x->fail(TPE_ERR_ARG, "tpe_rebuild_labels: label out of range");
+            if (ctx->lsh_dev[g] == d) mine.push_back(ctx->lsh_local[g]);
+        }
+        if (mine.empty()) return TPE_OK;   // (its labels keep their build)
+        std::vector<int64_t> off;
+        std::vector<int32_t> ord;
+        lsh_orders(ids, order_off, order, off, ord);
+        return tpe1_rebuild_labels(x, losses, n_trials, n_valid, gamma, prior_weight, lf, off.data(), ord.data(),
+                                   mine.data(), (int32_t)mine.size(), &nbd[d], td[d].data());
     });
+    if (rc) return rc;
+    if (n_below_out) {
+        *n_below_out = 0;
+        for (int d = 0; d < nd; ++d)
+            if (nbd[d] >= 0) {
+                *n_below_out = nbd[d];
+                break;
+            }
+    }
+    if (ties) {
+        std::fill(ties, ties + L + 1, 0);
+        for (int d = 0; d < nd; ++d) lsh_ties_merge(ctx->lsh_ids[d], td[d], L, ties);
+    }
+    return TPE_OK;
+}
+
+int tpe_build_report(tpe_ctx* ctx, int32_t* n_below, int32_t* ties) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (!lsharded(ctx)) return tpe1_build_report(ctx, n_below, ties);
+    const int nd = ndev(ctx);
+    const int32_t L = ctx->lsh_L;
+    std::vector<std::vector<int32_t>> td(nd);
+    int32_t nb0 = 0;
+    const int rc = for_all(ctx, [&](tpe_ctx* x, int d) {
+        td[d].assign(ctx->lsh_ids[d].size() + 1, 0);
+        return tpe1_build_report(x, d == 0 ? &nb0 : nullptr, td[d].data());
+    });
+    if (rc) return rc;
+    if (n_below) *n_below = nb0;
+    if (ties) {
+        std::fill(ties, ties + L + 1, 0);
+        for (int d = 0; d < nd; ++d) lsh_ties_merge(ctx->lsh_ids[d], td[d], L, ties);
+    }
+    return TPE_OK;
+}
+
+int tpe_get_mixture(tpe_ctx* ctx, int32_t label, int32_t side, double* weights, double* mus, double* sigmas,
+                    int32_t cap, int32_t* n) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (!lsharded(ctx)) return tpe1_get_mixture(ctx, label, side, weights, mus, sigmas, cap, n);
+    if (label < 0 || label >= ctx->lsh_L) return ctx->fail(TPE_ERR_ARG, "tpe_get_mixture: no such built mixture");
+    tpe_ctx* x = dev(ctx, ctx->lsh_dev[label]);
+    HIPCHK(ctx, hipSetDevice(x->device));
+    const int rc = tpe1_get_mixture(x, ctx->lsh_local[label], side, weights, mus, sigmas, cap, n);
+    if (rc) ctx->err = x->err;
+    return rc;
+}
+
+int32_t tpe_label_device(const tpe_ctx* ctx, int32_t label) {
+    if (!ctx || !lsharded(ctx) || label < 0 || label >= ctx->lsh_L) return -1;
+    return ctx->lsh_dev[label];
+}
+
+int32_t tpe_resident_labels(const tpe_ctx* ctx) {
+    if (!ctx) return 0;
+    return lsharded(ctx) ? ctx->lsh_L : tpe1_resident_labels(ctx);
+}
+
+int tpe_last_build_ms(const tpe_ctx* ctx, float* ms) {
+    if (!ctx || !ms) return TPE_ERR_ARG;
+    if (!lsharded(ctx)) return tpe1_last_build_ms(ctx, ms);
+    float m = 0.f;
+    for (int d = 0; d < ndev(const_cast<tpe_ctx*>(ctx)); ++d) {
+        float v = 0.f;
+        const int rc = tpe1_last_build_ms(dev(const_cast<tpe_ctx*>(ctx), d), &v);
+        if (rc) return rc;
+        m = std::max(m, v);
+    }
+    *ms = m;
+    return TPE_OK;
+}
+
+int tpe_score(tpe_ctx* ctx, int32_t label, const double* cand, int64_t n, double* lpdf_below, double* lpdf_above,
+              tpe_label_result* out) {
+    if (!ctx) return TPE_ERR_ARG;
+    if (!lsharded(ctx)) return tpe1_score(ctx, label, cand, n, lpdf_below, lpdf_above, out);
+    if (label < 0 || label >= ctx->lsh_L) return ctx->fail(TPE_ERR_ARG, "tpe_score: label out of range");
+    tpe_ctx* x = dev(ctx, ctx->lsh_dev[label]);
+    HIPCHK(ctx, hipSetDevice(x->device));
+    const int rc = tpe1_score(x, ctx->lsh_local[label], cand, n, lpdf_below, lpdf_above, out);
+    if (rc) ctx->err = x->err;
+    if (!rc && out) out->label = label;
+    return rc;
 }
 
 int tpe_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_labels,
@@ -412,6 +690,7 @@ int tpe_build_posterior(tpe_ctx* ctx, const tpe_label_spec* specs, int32_t n_lab
                         const double* obs_val, double gamma, double prior_weight, int32_t lf,
                         int32_t* n_below_out) {
     if (!ctx) return TPE_ERR_ARG;
+    lsh_clear(ctx);   // (the one-shot build: replicated, candidate / round split)
     return for_all(ctx, [&](tpe_ctx* x, int d) {
         return tpe1_build_posterior(x, specs, n_labels, cat_p, n_cat_p, losses, n_trials, obs_off,
                                     obs_trial, obs_val, gamma, prior_weight, lf,
@@ -423,6 +702,7 @@ int tpe_suggest(tpe_ctx* ctx, uint64_t seed, uint32_t round, int64_t n_candidate
                 int64_t cand_offset, tpe_label_result* out) {
     if (!ctx || !out) return TPE_ERR_ARG;
     if (ctx->peers.empty()) return tpe1_suggest(ctx, seed, round, n_candidates, cand_offset, out);
+    if (lsharded(ctx)) return lsh_round(ctx, seed, &round, 1, n_candidates, cand_offset, out);
     return sharded_round(ctx, seed, &round, 1, n_candidates, cand_offset, out);
 }
 
@@ -432,6 +712,7 @@ int tpe_suggest_batch(tpe_ctx* ctx, uint64_t seed, const uint32_t* rounds, int32
     if (ctx->peers.empty())
         return tpe1_suggest_batch(ctx, seed, rounds, n_rounds, n_candidates, cand_offset, out);
     if (n_rounds <= 0) return ctx->fail(TPE_ERR_ARG, "bad candidate/round count");
+    if (lsharded(ctx)) return lsh_round(ctx, seed, rounds, n_rounds, n_candidates, cand_offset, out);
     return sharded_round(ctx, seed, rounds, n_rounds, n_candidates, cand_offset, out);
 }
 

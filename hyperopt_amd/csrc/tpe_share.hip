@@ -140,6 +140,7 @@ extern "C" {
 
 int tpe_export_posterior(tpe_ctx* ctx, void* d_out, int64_t cap, int64_t* bytes_out) {
     if (!ctx || !bytes_out) return TPE_ERR_ARG;
+    TPE_NOT_LSHARD(ctx);
     TPE_SETTLE(ctx);
     if (!ctx->peers.empty()) return ctx->fail(TPE_ERR_ARG, "tpe_export_posterior: single-device contexts only");
     tpe_rt::Posterior& P = ctx->resident;
@@ -211,6 +212,7 @@ int tpe_export_posterior(tpe_ctx* ctx, void* d_out, int64_t cap, int64_t* bytes_
 int tpe_import_posterior(tpe_ctx* ctx, const void* d_blobs, int64_t blob_bytes, const int64_t* part_off,
                          int32_t n_parts, const int32_t* part_labels, const int32_t* label_ids) {
     if (!ctx || !d_blobs || !part_off || n_parts <= 0 || !part_labels || !label_ids) return TPE_ERR_ARG;
+    TPE_NOT_LSHARD(ctx);
     TPE_SETTLE(ctx);
     if (!ctx->peers.empty()) return ctx->fail(TPE_ERR_ARG, "tpe_import_posterior: single-device contexts only");
     HIPCHK(ctx, hipSetDevice(ctx->device));

@@ -478,7 +478,8 @@ class Engine(object):
                'rescore_cap': L.TPE_OPT_RESCORE_CAP, 'mode_mask': L.TPE_OPT_MODE_MASK,
                'aux_families': L.TPE_OPT_AUX_FAMILIES,
                'bx_split': L.TPE_OPT_BX_SPLIT, 'bx_t': L.TPE_OPT_BX_T,
-               'pk_sliced': L.TPE_OPT_PK_SLICED, 'defer_report': L.TPE_OPT_DEFER_REPORT}
+               'pk_sliced': L.TPE_OPT_PK_SLICED, 'defer_report': L.TPE_OPT_DEFER_REPORT,
+               'label_shards': L.TPE_OPT_LABEL_SHARDS}
 
     def set_option(self, name, value):
         """Engine switches (include/hyperopt_tpe.h TPE_OPT_*): 'screen',

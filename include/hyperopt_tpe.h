@@ -148,6 +148,12 @@ int tpe_ctx_create_multi(const int *devices, int32_t n_devices, int precision, t
 /* Devices of a context (writes at most cap ordinals); returns their count. */
 int32_t tpe_ctx_devices(const tpe_ctx *ctx, int32_t *devices, int32_t cap);
 
+/* Label shards of a multi-device context (TPE_OPT_LABEL_SHARDS): the
+ * position in tpe_ctx_devices' list of the device holding `label` of the
+ * resident history, or -1 when the context's labels are not sharded (one
+ * device, replicated posteriors, no such label). */
+int32_t tpe_label_device(const tpe_ctx *ctx, int32_t label);
+
 void tpe_ctx_destroy(tpe_ctx *ctx);
 const char *tpe_last_error(const tpe_ctx *ctx);
 
@@ -552,6 +558,13 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
  *                   labels' kernels, any other call on the context first;
  *                   tpe_build_report then returns the real tie report
  *                   (single-device contexts; consumed by that rebuild)  [0]
+ *   TPE_OPT_LABEL_SHARDS  multi-device contexts: the resident history's
+ *                   labels partitioned over the devices (each device
+ *                   appends, builds, indexes and runs whole rounds of its
+ *                   labels; winners scattered to their space positions)
+ *                   from the next tpe_history_reset with at least one label
+ *                   per device; 0: every device holds every label and the
+ *                   rounds split by candidates / rounds                  [1]
  *   TPE_OPT_WIN_GROUPS  label groups of a windowed round, each sorted on a
  *                   second stream while the previous one is screened
  *                   (0: one group; the chip is busy either way)          [0]
@@ -589,6 +602,7 @@ int tpe_screen_probe(tpe_ctx *ctx, int32_t label, const double *cand, int64_t n,
 #define TPE_OPT_BX_T 22
 #define TPE_OPT_PK_SLICED 23
 #define TPE_OPT_DEFER_REPORT 24
+#define TPE_OPT_LABEL_SHARDS 25
 int tpe_set_option(tpe_ctx *ctx, int32_t option, int64_t value);
 
 /* Build now what the resident posterior's first round(s) of n_candidates
