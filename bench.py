@@ -40,14 +40,14 @@ FLOPS_PER_EVAL = {'f64': 6.0, 'f32': 6.0}
 # expansion screen (k_screen_bx): per candidate a 15-coefficient Horner
 # polynomial (15 FMA) and the degree-5 exp(-kappa delta^2) factor (5 FMA)
 BX_FLOPS_PER_CAND = 2 * 15 + 2 * 5
-# The draw kernel k_hot_bx (round 6: the inverse-CDF draw, most candidates
-# decided from their Philox words), algorithmic 32-bit lane operations per
+# The mark kernel k_hot_bx (round 6: the inverse-CDF draw, every candidate
+# decided from its Philox words and a u-cell bit), algorithmic 32-bit lane operations per
 # candidate: half a Philox4x32-10 call -- 10 rounds of two 32x32 -> 64-bit
 # products (2 operations each: the low and high words) and two 3-input
 # xors (2 each), 80 per call -- 40; the component pick (the guide's lookup
 # and up to 3 threshold comparisons) 4; the u-cell bit (index, load, test)
-# 3.  The fp64 draw of the ~1-2 % marked candidates and their sub-bin test
-# are not counted.  Against the 32-bit VALU lane rate of MI355X_MICROARCH.md's
+# 3.  The fp64 draw of the ~0.8 % marked candidates and their sub-bin test
+# run in k_hot_draw (not counted here).  Against the 32-bit VALU lane rate of MI355X_MICROARCH.md's
 # vector figure (256 CUs x 4 SIMD-32 x 32 lanes x 2.4 GHz = 78.6 T/s).
 DRAW_OPS_PER_CAND = 47
 PEAK_INT32_VECTOR_TOPS = 78.6
@@ -995,16 +995,16 @@ def main():
     windowed = smode == 2
     hot = smode == 3 and scr[5] > 0
     if hot:
-        # the hot-bin prefilter's draw kernel (k_hot_bx, the dominant
+        # the hot-bin prefilter's mark kernel (k_hot_bx, the dominant
         # kernel; its HIP-event bracket holds it alone): every candidate's
-        # Philox words, pick and u-cell bit, the marked ~1-2 % drawn in fp64
-        # and tested against their sub-bin's bit
+        # Philox words, pick and u-cell bit; the marked ~0.8 % go to
+        # k_hot_draw (fp64 draw + sub-bin bit, in other_dense_ms)
         dom_ms = scr[2]
         kprec = 'int32'
         kname = 'k_hot_bx<'
-        kdesc = 'k_hot_bx (the hot-bin prefilter\'s draw: every candidate\'s Philox4x32-10 words, ' \
-                'component pick and u-cell bit; the marked ones drawn by the inverse CDF in fp64 and ' \
-                'listed when their sub-bin can hold the winner), GMM1+LGMM1 labels'
+        kdesc = 'k_hot_bx (the hot-bin prefilter\'s mark kernel: every candidate\'s Philox4x32-10 words, ' \
+                'component pick and u-cell bit; the marked ones go to k_hot_draw, which draws them by the ' \
+                'inverse CDF in fp64 and lists those whose sub-bin can hold the winner), GMM1+LGMM1 labels'
         dom_rate = scr[3] / (dom_ms * 1e-3)
         dom_flops = scr[0] * DRAW_OPS_PER_CAND
     elif smode == 3:
@@ -1071,8 +1071,8 @@ def main():
         roof['note'] = ('VALU-issue bound on integer work: achieved counts the draw\'s algorithmic 32-bit '
                         'lane operations (Philox4x32-10: 40 per candidate; the pick 4; the u-cell bit 3) '
                         'over the kernel\'s HIP-event time, against the 32-bit VALU lane rate; the fp64 '
-                        'draws of the marked candidates and the expansion screen of the listed ones '
-                        '(k_screen_hot, other_dense_ms) are not counted; the PMC figures are k_hot_bx\'s')
+                        'draws of the marked candidates (k_hot_draw) and the expansion screen of the listed '
+                        'ones (k_screen_hot) are other_dense_ms; the PMC figures are k_hot_bx\'s')
     elif smode == 3:
         roof['flops_per_candidate_poly'] = BX_FLOPS_PER_CAND
         roof['note'] = ('VALU-issue bound: per candidate the Philox + Box-Muller draw, the fp64 '

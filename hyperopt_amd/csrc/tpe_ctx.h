@@ -478,12 +478,13 @@ struct tpe_ctx {
     bool dense_one = false;              // this round's dense rows hold their winner in slot 0 only (k_reduce)
     DevBuf<int32_t> hot_pc;              // per sub-bin word: the label's set bits before it (k_hot_prefix)
     DevBuf<uint32_t> hot_ucell;          // per (dense label, sampling component): its u-cells (k_hot_ucells)
+    DevBuf<uint4> samp_img;              // per dense label: stage_samp's LDS image (k_samp_image)
     int32_t bx_split = 0;                // TPE_OPT_BX_SPLIT (0: auto)
     int64_t pk_sliced = 8192;            // TPE_OPT_PK_SLICED (0: never sliced)
     int32_t bx_t_force = 0;              // TPE_OPT_BX_T (0: auto)
     double bx_t_next = 64.0;             // the cut T of the next index built (set by its caller)
     DevBuf<int32_t> hot_i, hot_cnt;      //   their indices; per cell the count
-    DevBuf<int32_t> hot_mi, hot_mcnt;    //   the marked candidates (k_hot_bx -> k_hot_draw); per cell the count
+    DevBuf<int32_t> hot_mi, hot_mcnt;    //   the marked candidates (k_hot_bx -> k_hot_draw); per segment the count
     DevBuf<unsigned long long> hot_t, hot_tau0;   // per cell largest L; per label tau0
     DevBuf<uint32_t> hot_bits;           // per sub-bin: U >= tau0 (words at sb_off / 32)
     DevBuf<int32_t> hot_flag;            // fallback flag

@@ -289,7 +289,7 @@ struct SampGlobal {
 
 constexpr int kSampLds = 64;     // below components staged in LDS (K_b <= 26 in practice)
 constexpr int kGuideSteps = 3;   // guided picks take at most this many comparisons
-struct SampLds {
+struct alignas(16) SampLds {
     double cdf[kSampLds], mu[kSampLds], ssg[kSampLds], p0[kSampLds], q0[kSampLds], m[kSampLds], iw[kSampLds];
     uint64_t thr[kSampLds];   // ceil(cdf 2^32)
     uint8_t guide[64];
@@ -381,6 +381,16 @@ __device__ __forceinline__ bool stage_samp(const DLabel& L, const SampRec* __res
     }
     __syncthreads();
     return true;
+}
+
+// stage_samp's LDS image kept in global memory (k_samp_image, once per
+// posterior): a workgroup that only needs the staged table copies it with
+// 16-byte loads instead of rebuilding the thresholds and guides
+constexpr int kSampImgVec = (int)((sizeof(SampLds) + 15) / 16);
+__device__ __forceinline__ void stage_samp_image(const uint4* __restrict__ img, SampLds* t) {
+    uint4* d = reinterpret_cast<uint4*>(t);
+    for (int k = threadIdx.x; k < kSampImgVec; k += blockDim.x) d[k] = img[k];
+    __syncthreads();
 }
 
 // Phi(x) = erfc(-x / sqrt 2) / 2 (accurate in both tails)

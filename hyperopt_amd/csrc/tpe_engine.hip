@@ -827,6 +827,17 @@ constexpr int kHotCellBits = 11;
 constexpr int kHotCells = 1 << kHotCellBits;   // u-cells per sampling component
 constexpr int kHotCellWords = kHotCells / 32;
 
+// per dense label position: stage_samp's LDS table written out (the draw
+// kernels copy it instead of rebuilding it per workgroup)
+__global__ __launch_bounds__(kBlock) void k_samp_image(const DLabel* __restrict__ labels,
+                                                       const int32_t* __restrict__ group,
+                                                       const SampRec* __restrict__ samp, uint4* __restrict__ img) {
+    __shared__ SampLds sl;
+    (void)stage_samp(labels[group[blockIdx.x]], samp, &sl);   // (launched for ns <= kSampLds only)
+    const uint4* s = reinterpret_cast<const uint4*>(&sl);
+    for (int k = threadIdx.x; k < kSampImgVec; k += kBlock) img[(size_t)blockIdx.x * kSampImgVec + k] = s[k];
+}
+
 // per dense label position: the set bits of the label's sub-bin words
 // before each word (exclusive prefix), one workgroup per label
 __global__ __launch_bounds__(1024) void k_hot_prefix(const int32_t* __restrict__ group,
@@ -976,60 +987,56 @@ __device__ __forceinline__ void hot_items_body(const int32_t* __restrict__ hcnt,
 
 // The draw kernel, in two launches (round 6).  k_hot_bx (tile map only:
 // workgroups stride over the cell's tiles of R * 256 candidates, Philox
-// pairs per thread, the sampling records and the label's u-cells staged once
-// per workgroup -- the launch requires the records in LDS): per candidate
-// the Philox words, the component pick and one u-cell bit; the marked
-// candidates' indices (~1-2 %) gather in a buffer per WAVE in LDS (count in a
-// scalar register) and go to the cell's mark list with one global atomic per
-// flush.  No fp64 in it: ~40 VGPRs, 8 waves per SIMD to hide the dependent
-// LDS lookups of the pick.  k_hot_draw then draws the marked candidates by
-// the inverse CDF in fp64 (full lanes) and lists those whose sub-bin's bit
+// pairs per thread, the label's staged sampling table (k_samp_image) and
+// u-cells copied once per workgroup): per candidate the Philox words, the
+// component pick and one u-cell bit; the marked candidates' indices (~0.8 %,
+// r6h) gather in a buffer per WAVE in LDS and go to the workgroup's own
+// segment of the mark list (an LDS counter: no global atomics -- a counter
+// per cell shared by every workgroup serialised the flushes, r6i).  No fp64
+// in it: ~54 VGPRs, 8 waves per SIMD.  k_hot_draw then draws the marked
+// candidates by the inverse CDF in fp64 and lists those whose sub-bin's bit
 // is set (or that fall outside the bins) -- exactly the list the full draw
-// gives.  (Round 4 measured list forms on the same box: one workgroup
-// buffer flushed only at the end, 2.34 ms at 0.35 VALU busy; flushed after
-// every tile behind a barrier, 1.37 ms at 0.75 -- hence per-wave buffers.)
+// gives.
 constexpr int kMarkBuf = 128;     // marked indices per wave
-
-// one wave's buffered indices to the cell's list (count n, wave-uniform);
-// past mstride the list overflows: hflag bit 2 (the round re-runs with the
-// expansion screen over every candidate)
-__device__ __forceinline__ void mark_wave_flush(int n, const int32_t* bi, int32_t* __restrict__ mcnt,
-                                                int32_t* __restrict__ midx, size_t cell, int64_t mstride,
-                                                int32_t* __restrict__ hflag) {
-    const int lane = threadIdx.x & 63;
-    int gb = 0;
-    if (lane == 0) gb = atomicAdd(mcnt + cell, n);
-    gb = __builtin_amdgcn_readfirstlane(__shfl(gb, 0));
-    if (lane == 0 && gb + n > mstride) atomicOr(hflag, 2);
-    __builtin_amdgcn_wave_barrier();
-    for (int k = lane; k < n; k += 64)
-        if (gb + k < mstride) midx[cell * (size_t)mstride + gb + k] = bi[k];
-    __builtin_amdgcn_wave_barrier();
-}
 
 template <int R>
 __global__ __launch_bounds__(kBlock, 8) void k_hot_bx(
-    const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const uint4* __restrict__ img,
     const uint32_t* __restrict__ ucell, int64_t n, int64_t cand_offset, uint64_t seed,
-    const uint32_t* __restrict__ rounds, int32_t nl, int32_t* __restrict__ mcnt, int32_t* __restrict__ midx,
-    int64_t mstride, int32_t* __restrict__ hflag) {
+    const uint32_t* __restrict__ rounds, int32_t nl, int32_t* __restrict__ mseg, int32_t* __restrict__ midx,
+    int64_t mcap, int32_t* __restrict__ hflag) {
     static_assert(R % 2 == 0, "Philox pairs");
     const int li = group[blockIdx.y];
     const DLabel L = labels[li];
     __shared__ SampLds sl;
     extern __shared__ uint32_t ucw[];   // (dynamic: the largest label's ns x kHotCellWords)
     __shared__ int32_t buf[kBlock / 64][kMarkBuf];
+    __shared__ int32_t wg_n;
     {
         const uint32_t* uc = ucell + (size_t)blockIdx.y * kSampLds * kHotCellWords;
         for (int w = threadIdx.x; w < L.ns * kHotCellWords; w += kBlock) ucw[w] = uc[w];
+        if (threadIdx.x == 0) wg_n = 0;
     }
-    (void)stage_samp(L, samp, &sl);   // (its barriers publish the stage above; the launch checked ns <= kSampLds)
+    stage_samp_image(img + (size_t)blockIdx.y * kSampImgVec, &sl);   // (its barrier publishes the stage above)
     const size_t cell = (size_t)blockIdx.z * nl + blockIdx.y;
+    const size_t seg = cell * gridDim.x + blockIdx.x;
+    int32_t* __restrict__ out = midx + seg * (size_t)mcap;
     const uint32_t rk = rounds[blockIdx.z];
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     constexpr int64_t per = (int64_t)R * kBlock;
-    const int wv = threadIdx.x >> 6;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const SampShared src{&sl, __builtin_amdgcn_readfirstlane(sl.steps)};
+    // one wave's buffered indices (count c, wave-uniform) to the segment;
+    // past mcap it overflows: hflag bit 2 (below)
+    auto flush = [&](int c) {
+        int gb = 0;
+        if (lane == 0) gb = atomicAdd(&wg_n, c);
+        gb = __builtin_amdgcn_readfirstlane(__shfl(gb, 0));
+        __builtin_amdgcn_wave_barrier();
+        for (int k = lane; k < c; k += 64)
+            if (gb + k < mcap) out[gb + k] = buf[wv][k];
+        __builtin_amdgcn_wave_barrier();
+    };
     int wn = 0;   // this wave's buffered indices (wave-uniform)
     for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per) {
         const uint32_t g0 = (uint32_t)(cand_offset + base);
@@ -1067,27 +1074,34 @@ __global__ __launch_bounds__(kBlock, 8) void k_hot_bx(
             if (!bal) continue;
             const int c = (int)__popcll(bal);
             if (wn + c > kMarkBuf) {   // (wave-uniform)
-                mark_wave_flush(wn, buf[wv], mcnt, midx, cell, mstride, hflag);
+                flush(wn);
                 wn = 0;
             }
             if (m) buf[wv][wn + (int)lanes_below(bal)] = (int32_t)(base + (int64_t)tile_cand(r, threadIdx.x, kBlock));
             wn += c;
         }
     }
-    if (wn > 0) mark_wave_flush(wn, buf[wv], mcnt, midx, cell, mstride, hflag);
+    if (wn > 0) flush(wn);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        mseg[seg] = wg_n;
+        if (wg_n > mcap) atomicOr(hflag, 2);
+    }
 }
 
 // The marked candidates of every (round, dense label) cell: the words
 // again (one Philox call each), the inverse-CDF draw in fp64 and the sub-bin
-// test; listed ones -- bit set, or outside the bins (or NaN) -- go to the
-// cell's hot list (hidx, hx) with one atomic per wave.  Grid (workgroups
-// per cell, cells); the workgroup that finishes last numbers k_screen_hot's
-// work items (hot_items_body).
+// test; listed ones -- bit set, or outside the bins (or NaN) -- gather in
+// LDS and go to the cell's hot list (hidx, hx) with one global atomic per
+// workgroup (per kDrawBuf listed).  Grid (workgroups per cell, cells): the
+// workgroups of a cell share its mark segments; the one that finishes last
+// numbers k_screen_hot's work items (hot_items_body).
+constexpr int kDrawBuf = 1024;
 __global__ __launch_bounds__(kBlock) void k_hot_draw(
-    const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const SampRec* __restrict__ samp,
+    const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const uint4* __restrict__ img,
     const BxLabel* __restrict__ bx, const uint32_t* __restrict__ hbits, int64_t cand_offset, uint64_t seed,
-    const uint32_t* __restrict__ rounds, int32_t nl, const int32_t* __restrict__ mcnt,
-    const int32_t* __restrict__ midx, int64_t mstride, int32_t* __restrict__ hcnt, int32_t* __restrict__ hidx,
+    const uint32_t* __restrict__ rounds, int32_t nl, const int32_t* __restrict__ mseg, int32_t nseg,
+    const int32_t* __restrict__ midx, int64_t mcap, int32_t* __restrict__ hcnt, int32_t* __restrict__ hidx,
     double* __restrict__ hx, int32_t* __restrict__ err, int64_t hstride, int32_t* __restrict__ hflag,
     uint32_t* __restrict__ done, int32_t* __restrict__ items, int64_t item_per) {
     const size_t cell = blockIdx.y;
@@ -1095,47 +1109,76 @@ __global__ __launch_bounds__(kBlock) void k_hot_draw(
     const DLabel L = labels[li];
     const BxLabel B = bx[li];
     __shared__ SampLds sl;
-    (void)stage_samp(L, samp, &sl);
+    __shared__ int32_t lidx[kDrawBuf];
+    __shared__ double lx[kDrawBuf];
+    __shared__ int32_t ln, lbase;
+    if (threadIdx.x == 0) ln = 0;
+    stage_samp_image(img + (cell % (size_t)nl) * kSampImgVec, &sl);
     const SampShared src{&sl, __builtin_amdgcn_readfirstlane(sl.steps)};
     const int64_t nsb = (int64_t)B.nbins * kBxSub;
     const uint32_t* __restrict__ gbits = hbits + (B.sb_off >> 5);
     const uint32_t rk = rounds[cell / (size_t)nl];
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-    const int64_t m = min((int64_t)mcnt[cell], mstride);
-    bool bad = false;
-    for (int64_t j0 = (int64_t)blockIdx.x * kBlock; j0 < m; j0 += (int64_t)gridDim.x * kBlock) {
-        const int64_t j = j0 + threadIdx.x;
-        bool take = false;
-        int32_t ci = 0;
-        double x = 0.0;
-        if (j < m) {
-            ci = midx[cell * (size_t)mstride + j];
-            uint32_t wp, wu;
-            draw_words(L, k0, k1, (uint32_t)(cand_offset + ci), rk, wp, wu);
-            x = icdf_draw(L, src.comp(wp), wp, wu);
-            bad = bad || x != x;
-            const double f = (x - L.centre - B.xlo) * B.inv_sbw;
-            if (f >= 0.0 && f < (double)nsb) {
-                const int64_t s = (int64_t)f;
-                take = (gbits[s >> 5] >> (s & 31)) & 1u;
-            } else {
-                take = true;   // outside the bins (or NaN): always listed
-            }
+    const int lane = threadIdx.x & 63;
+    // the buffered entries to the cell's list (every thread; uniform)
+    auto flush = [&]() {
+        __syncthreads();
+        const int c = ln;
+        if (threadIdx.x == 0) {
+            lbase = atomicAdd(hcnt + cell, c);
+            if (lbase + c > hstride) atomicOr(hflag, 2);   // (the round screens every candidate instead)
         }
-        const uint64_t bal = __ballot(take);
-        if (bal) {
-            const int lane = threadIdx.x & 63;
-            int gb = 0;
-            if (lane == 0) gb = atomicAdd(hcnt + cell, (int)__popcll(bal));
-            gb = __builtin_amdgcn_readfirstlane(__shfl(gb, 0));
-            if (lane == 0 && gb + (int)__popcll(bal) > hstride) atomicOr(hflag, 2);
-            const int at = gb + (int)lanes_below(bal);
-            if (take && at < hstride) {
-                hidx[cell * (size_t)hstride + at] = ci;
-                hx[cell * (size_t)hstride + at] = x;
+        __syncthreads();
+        const int64_t b = lbase;
+        for (int k = threadIdx.x; k < c; k += kBlock)
+            if (b + k < hstride) {
+                hidx[cell * (size_t)hstride + b + k] = lidx[k];
+                hx[cell * (size_t)hstride + b + k] = lx[k];
             }
+        __syncthreads();
+        if (threadIdx.x == 0) ln = 0;
+        __syncthreads();
+    };
+    bool bad = false;
+    for (int s = blockIdx.x; s < nseg; s += gridDim.x) {
+        const size_t sg = cell * (size_t)nseg + s;
+        const int64_t m = min((int64_t)mseg[sg], mcap);
+        const int32_t* __restrict__ mi = midx + sg * (size_t)mcap;
+        for (int64_t j0 = 0; j0 < m; j0 += kBlock) {
+            if (ln > kDrawBuf - kBlock) flush();   // (ln read by every thread after a barrier: uniform)
+            const int64_t j = j0 + threadIdx.x;
+            bool take = false;
+            int32_t ci = 0;
+            double x = 0.0;
+            if (j < m) {
+                ci = mi[j];
+                uint32_t wp, wu;
+                draw_words(L, k0, k1, (uint32_t)(cand_offset + ci), rk, wp, wu);
+                x = icdf_draw(L, src.comp(wp), wp, wu);
+                bad = bad || x != x;
+                const double f = (x - L.centre - B.xlo) * B.inv_sbw;
+                if (f >= 0.0 && f < (double)nsb) {
+                    const int64_t sb = (int64_t)f;
+                    take = (gbits[sb >> 5] >> (sb & 31)) & 1u;
+                } else {
+                    take = true;   // outside the bins (or NaN): always listed
+                }
+            }
+            const uint64_t bal = __ballot(take);
+            if (bal) {
+                int gb = 0;
+                if (lane == 0) gb = atomicAdd(&ln, (int)__popcll(bal));
+                gb = __builtin_amdgcn_readfirstlane(__shfl(gb, 0));
+                if (take) {
+                    const int at = gb + (int)lanes_below(bal);
+                    lidx[at] = ci;
+                    lx[at] = x;
+                }
+            }
+            __syncthreads();   // (ln settled before the next chunk's check)
         }
     }
+    flush();
     if (bad) atomicOr(err, 1);
     // the workgroup that finishes last numbers k_screen_hot's work items
     __shared__ bool last;
@@ -1355,11 +1398,15 @@ constexpr unsigned kHotScreenWgs = 1024;   // k_screen_hot's persistent grid (4 
 #endif
 constexpr int64_t kHotWgs = TPE_HOT_WGS;
 #ifndef TPE_HOT_BX_WGS
-#define TPE_HOT_BX_WGS 16384
+#define TPE_HOT_BX_WGS 8192   // (the two draw kernels: 2048 0.54 ms, 4096 0.52, 8192 0.48, r6j)
 #endif
 constexpr int64_t kHotBxWgs = TPE_HOT_BX_WGS;   // k_hot_bx's workgroups over a round, at most
 constexpr int64_t kHotFillWgs = 2560;           //   at least (two passes of the resident workgroups)
 constexpr int64_t kHotMinTiles = 6;             //   tiles per workgroup, at least (unless filling)
+#ifndef TPE_HOT_DRAW_WGS
+#define TPE_HOT_DRAW_WGS 2048
+#endif
+constexpr int64_t kHotDrawWgs = TPE_HOT_DRAW_WGS;   // k_hot_draw's workgroups over a round, about
 constexpr int kQR = 8;   // candidates per thread, k_qfused_tiles
 constexpr int kQLdsKeys = 1024;   // grid values whose keys k_qfused_tiles stages in LDS
 constexpr int kCatR = 8;  // candidates per thread, k_cat_tiles
@@ -3857,6 +3904,14 @@ int hot_tau_prepare(tpe_ctx* ctx, int64_t n) {
                        ctx->hot_pc.p);
     hipLaunchKernelGGL(k_hot_ucells, dim3(kHotCells / kBlock, kSampLds, nl), dim3(kBlock), 0, ctx->stream, P.labels.p,
                        grp, P.samp.p, P.bx.p, ctx->hot_bits.p, ctx->hot_pc.p, ctx->hot_ucell.p);
+    bool staged = true;   // (k_hot_bx runs only when every dense label's records fit in LDS)
+    for (int m : {DENSE_GMM, DENSE_LGMM})
+        for (int li : P.h_group[m]) staged = staged && P.h_labels[li].ns >= 1 && P.h_labels[li].ns <= kSampLds;
+    if (staged) {
+        HIPCHK(ctx, ctx->samp_img.reserve((size_t)nl * kSampImgVec));
+        hipLaunchKernelGGL(k_samp_image, dim3((unsigned)nl), dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.samp.p,
+                           ctx->samp_img.p);
+    }
     ctx->hot_tau0_gen = ctx->hot == 2 ? 0 : P.bx_gen;
     ctx->hot_tau0_n = n;
     return ctx->hip(hipGetLastError(), "hot-bin threshold launch");
@@ -3910,7 +3965,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
         }
         hot = use_bx && ctx->hot != 0 && ctx->P->bx_sb.p != nullptr && !ctx->hot_redo;
         for (int m : {DENSE_GMM, DENSE_LGMM})   // k_hot_bx stages every label's sampling records
-            for (int li : ctx->P->h_group[m]) hot = hot && ctx->P->h_labels[li].ns <= kSampLds;
+            for (int li : ctx->P->h_group[m]) hot = hot && ctx->P->h_labels[li].ns >= 1 && ctx->P->h_labels[li].ns <= kSampLds;
         // the expansion screen's appends: a cell's hot list at most (the
         // prefilter), else any candidate of the round
         int64_t lst = hot ? hot_stride(ctx, a.n) : a.n;
@@ -3953,8 +4008,6 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                 HIPCHK(ctx, ctx->hot_t.reserve(cells));
                 HIPCHK(ctx, ctx->hot_flag.reserve(1));
                 add_fill(fs, ctx->hot_cnt.p, cells * sizeof(int32_t), 0);
-                HIPCHK(ctx, ctx->hot_mcnt.reserve(cells));
-                add_fill(fs, ctx->hot_mcnt.p, cells * sizeof(int32_t), 0);
                 add_fill(fs, ctx->hot_t.p, cells * sizeof(unsigned long long), 0);
                 add_fill(fs, ctx->hot_flag.p, sizeof(int32_t), 0);
             }
@@ -3987,25 +4040,27 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                 for (int m : {DENSE_GMM, DENSE_LGMM})
                     for (int li : ctx->P->h_group[m]) ns_max = std::max(ns_max, ctx->P->h_labels[li].ns);
                 const size_t ucw_bytes = (size_t)ns_max * kHotCellWords * sizeof(uint32_t);
-                // the mark lists: a multiple of the hot list (marked >= listed)
-                const int64_t mst = std::min<int64_t>(a.n, 2 * lst);
-                HIPCHK(ctx, ctx->hot_mi.reserve(cells * mst));
+                // the mark lists: a segment per k_hot_bx workgroup, sized like
+                // the hot lists (n / hot_cap_div of its candidates; marked ~1.2x
+                // listed)
+                const int64_t segs = (int64_t)hg.x;
+                const int64_t mcap = std::max<int64_t>(
+                    1024, (int64_t)((double)((tiles_c + segs - 1) / segs * hr * kBlock) / ctx->hot_cap_div));
+                HIPCHK(ctx, ctx->hot_mi.reserve(cells * segs * mcap));
+                HIPCHK(ctx, ctx->hot_mcnt.reserve(cells * segs));
                 hipLaunchKernelGGL((k_hot_bx<kHotR>), hg, dim3(kBlock), ucw_bytes, ctx->stream, P.labels.p, grp,
-                                   P.samp.p, ctx->hot_ucell.p, a.n, a.cand_offset, a.seed, ctx->rounds.p, nl,
-                                   ctx->hot_mcnt.p, ctx->hot_mi.p, mst, ctx->hot_flag.p);
-                // the exact draw of the marked: workgroups per cell for ~1.5 % of
-                // the round at 256 per workgroup, the chip filled once
-                const int64_t dw = std::max<int64_t>(
-                    1, std::min<int64_t>((mst + kBlock - 1) / kBlock,
-                                         std::max<int64_t>((a.n / 64 + kBlock - 1) / kBlock,
-                                                           (kHotFillWgs + (int64_t)cells - 1) / (int64_t)cells)));
-                hipLaunchKernelGGL(k_hot_draw, dim3((unsigned)dw, (unsigned)cells), dim3(kBlock), 0, ctx->stream,
-                                   P.labels.p, grp, P.samp.p, P.bx.p, ctx->hot_bits.p, a.cand_offset, a.seed,
-                                   ctx->rounds.p, nl, ctx->hot_mcnt.p, ctx->hot_mi.p, mst, ctx->hot_cnt.p,
-                                   ctx->hot_i.p, ctx->hot_x.p, ctx->errflag.p, lst, ctx->hot_flag.p,
-                                   ctx->rs_done.p + 2, ctx->hot_items.p, (int64_t)kBxR * kBlock);
-                // (the screen's bracket: the two draw kernels)
+                                   ctx->samp_img.p, ctx->hot_ucell.p, a.n, a.cand_offset, a.seed, ctx->rounds.p, nl,
+                                   ctx->hot_mcnt.p, ctx->hot_mi.p, mcap, ctx->hot_flag.p);
+                // (the screen's bracket: the mark kernel alone -- the roofline's kernel)
                 if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
+                // the exact draw of the marked: a workgroup per mark segment, at
+                // most kHotDrawWgs over the round
+                const int64_t dw = std::max<int64_t>(1, std::min<int64_t>(segs, kHotDrawWgs / (int64_t)cells));
+                hipLaunchKernelGGL(k_hot_draw, dim3((unsigned)dw, (unsigned)cells), dim3(kBlock), 0, ctx->stream,
+                                   P.labels.p, grp, ctx->samp_img.p, P.bx.p, ctx->hot_bits.p, a.cand_offset, a.seed,
+                                   ctx->rounds.p, nl, ctx->hot_mcnt.p, (int32_t)segs, ctx->hot_mi.p, mcap,
+                                   ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p, ctx->errflag.p, lst, ctx->hot_flag.p,
+                                   ctx->rs_done.p + 2, ctx->hot_items.p, (int64_t)kBxR * kBlock);
                 hipLaunchKernelGGL((k_screen_hot<kBxR>), dim3(kHotScreenWgs), dim3(kBlock), 0, ctx->stream,
                                    P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p, P.bx_loff.p, P.bx_list.p, a.n,
                                    nl, (int64_t)cells, ctx->hot_items.p, ctx->hot_items.p + cells + 1,
