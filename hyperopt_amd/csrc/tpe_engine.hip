@@ -1093,17 +1093,17 @@ __global__ __launch_bounds__(kBlock, 8) void k_hot_bx(
 // again (one Philox call each), the inverse-CDF draw in fp64 and the sub-bin
 // test; listed ones -- bit set, or outside the bins (or NaN) -- gather in
 // LDS and go to the cell's hot list (hidx, hx) with one global atomic per
-// workgroup (per kDrawBuf listed).  Grid (workgroups per cell, cells): the
-// workgroups of a cell share its mark segments; the one that finishes last
-// numbers k_screen_hot's work items (hot_items_body).
+// workgroup (per kDrawBuf listed).  Grid (workgroups per cell, cells): each
+// workgroup takes a contiguous run of the cell's mark segments and numbers
+// their entries flat (full lanes).
 constexpr int kDrawBuf = 1024;
+constexpr int kDrawSegs = 64;     // mark segments per k_hot_draw workgroup, at most
 __global__ __launch_bounds__(kBlock) void k_hot_draw(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group, const uint4* __restrict__ img,
     const BxLabel* __restrict__ bx, const uint32_t* __restrict__ hbits, int64_t cand_offset, uint64_t seed,
     const uint32_t* __restrict__ rounds, int32_t nl, const int32_t* __restrict__ mseg, int32_t nseg,
     const int32_t* __restrict__ midx, int64_t mcap, int32_t* __restrict__ hcnt, int32_t* __restrict__ hidx,
-    double* __restrict__ hx, int32_t* __restrict__ err, int64_t hstride, int32_t* __restrict__ hflag,
-    uint32_t* __restrict__ done, int32_t* __restrict__ items, int64_t item_per) {
+    double* __restrict__ hx, int32_t* __restrict__ err, int64_t hstride, int32_t* __restrict__ hflag) {
     const size_t cell = blockIdx.y;
     const int li = group[cell % (size_t)nl];
     const DLabel L = labels[li];
@@ -1139,57 +1139,69 @@ __global__ __launch_bounds__(kBlock) void k_hot_draw(
         if (threadIdx.x == 0) ln = 0;
         __syncthreads();
     };
-    bool bad = false;
-    for (int s = blockIdx.x; s < nseg; s += gridDim.x) {
-        const size_t sg = cell * (size_t)nseg + s;
-        const int64_t m = min((int64_t)mseg[sg], mcap);
-        const int32_t* __restrict__ mi = midx + sg * (size_t)mcap;
-        for (int64_t j0 = 0; j0 < m; j0 += kBlock) {
-            if (ln > kDrawBuf - kBlock) flush();   // (ln read by every thread after a barrier: uniform)
-            const int64_t j = j0 + threadIdx.x;
-            bool take = false;
-            int32_t ci = 0;
-            double x = 0.0;
-            if (j < m) {
-                ci = mi[j];
-                uint32_t wp, wu;
-                draw_words(L, k0, k1, (uint32_t)(cand_offset + ci), rk, wp, wu);
-                x = icdf_draw(L, src.comp(wp), wp, wu);
-                bad = bad || x != x;
-                const double f = (x - L.centre - B.xlo) * B.inv_sbw;
-                if (f >= 0.0 && f < (double)nsb) {
-                    const int64_t sb = (int64_t)f;
-                    take = (gbits[sb >> 5] >> (sb & 31)) & 1u;
-                } else {
-                    take = true;   // outside the bins (or NaN): always listed
-                }
-            }
-            const uint64_t bal = __ballot(take);
-            if (bal) {
-                int gb = 0;
-                if (lane == 0) gb = atomicAdd(&ln, (int)__popcll(bal));
-                gb = __builtin_amdgcn_readfirstlane(__shfl(gb, 0));
-                if (take) {
-                    const int at = gb + (int)lanes_below(bal);
-                    lidx[at] = ci;
-                    lx[at] = x;
-                }
-            }
-            __syncthreads();   // (ln settled before the next chunk's check)
+    // this workgroup's mark segments [s0, s1) of the cell, numbered flat
+    // (full lanes: a segment holds ~100-300 marks)
+    __shared__ int32_t spre[kDrawSegs + 1];
+    const int s0 = (int)((int64_t)blockIdx.x * nseg / gridDim.x);
+    const int s1 = (int)((int64_t)(blockIdx.x + 1) * nseg / gridDim.x);   // (s1 - s0 <= kDrawSegs: the launch)
+    if (threadIdx.x == 0) {
+        int32_t t = 0;
+        for (int k = s0; k < s1; ++k) {
+            spre[k - s0] = t;
+            t += (int32_t)min((int64_t)mseg[cell * (size_t)nseg + k], mcap);
         }
+        spre[s1 - s0] = t;
+    }
+    __syncthreads();
+    const int32_t total = spre[s1 - s0];
+    bool bad = false;
+    for (int32_t j0 = 0; j0 < total; j0 += kBlock) {
+        if (ln > kDrawBuf - kBlock) flush();   // (ln read by every thread after a barrier: uniform)
+        const int32_t j = j0 + (int32_t)threadIdx.x;
+        bool take = false;
+        int32_t ci = 0;
+        double x = 0.0;
+        if (j < total) {
+            int k = 0;
+            while (spre[k + 1] <= j) ++k;   // (the segment holding flat entry j)
+            ci = midx[(cell * (size_t)nseg + s0 + k) * (size_t)mcap + (j - spre[k])];
+            uint32_t wp, wu;
+            draw_words(L, k0, k1, (uint32_t)(cand_offset + ci), rk, wp, wu);
+            x = icdf_draw(L, src.comp(wp), wp, wu);
+            bad = bad || x != x;
+            const double f = (x - L.centre - B.xlo) * B.inv_sbw;
+            if (f >= 0.0 && f < (double)nsb) {
+                const int64_t sb = (int64_t)f;
+                take = (gbits[sb >> 5] >> (sb & 31)) & 1u;
+            } else {
+                take = true;   // outside the bins (or NaN): always listed
+            }
+        }
+        const uint64_t bal = __ballot(take);
+        if (bal) {
+            int gb = 0;
+            if (lane == 0) gb = atomicAdd(&ln, (int)__popcll(bal));
+            gb = __builtin_amdgcn_readfirstlane(__shfl(gb, 0));
+            if (take) {
+                const int at = gb + (int)lanes_below(bal);
+                lidx[at] = ci;
+                lx[at] = x;
+            }
+        }
+        __syncthreads();   // (ln settled before the next chunk's check)
     }
     flush();
     if (bad) atomicOr(err, 1);
-    // the workgroup that finishes last numbers k_screen_hot's work items
-    __shared__ bool last;
-    if (threadIdx.x == 0) {
-        __threadfence();   // (this workgroup's counts and entries before the counter)
-        last = atomicAdd(done, 1u) == gridDim.x * gridDim.y - 1;
-    }
-    __syncthreads();
-    if (!last) return;   // (uniform)
-    __threadfence();     // (acquire: every cell's count)
-    hot_items_body<kBlock>(hcnt, (int64_t)gridDim.y, hstride, item_per, items, items + gridDim.y + 1);
+}
+
+// k_screen_hot's work items numbered from the hot lists' counts (one
+// workgroup).  A launch of its own: the last-workgroup pattern in
+// k_hot_draw cost every workgroup a device-scope release + acquire -- an L2
+// write-back and invalidate each (r6m: 2046 of them, 76 us for a shard's
+// ~0.5M draws)
+__global__ __launch_bounds__(1024) void k_hot_items(const int32_t* __restrict__ hcnt, int64_t cells, int64_t hstride,
+                                                   int64_t per, int32_t* __restrict__ items) {
+    hot_items_body<1024>(hcnt, cells, hstride, per, items, items + cells + 1);
 }
 
 
@@ -4055,12 +4067,15 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                 if (ctx->timing) HIPCHK(ctx, hipEventRecord(ctx->evs[1], ctx->stream));
                 // the exact draw of the marked: a workgroup per mark segment, at
                 // most kHotDrawWgs over the round
-                const int64_t dw = std::max<int64_t>(1, std::min<int64_t>(segs, kHotDrawWgs / (int64_t)cells));
+                const int64_t dw = std::max<int64_t>(
+                    (segs + kDrawSegs - 1) / kDrawSegs,
+                    std::max<int64_t>(1, std::min<int64_t>(segs, kHotDrawWgs / (int64_t)cells)));
                 hipLaunchKernelGGL(k_hot_draw, dim3((unsigned)dw, (unsigned)cells), dim3(kBlock), 0, ctx->stream,
                                    P.labels.p, grp, ctx->samp_img.p, P.bx.p, ctx->hot_bits.p, a.cand_offset, a.seed,
                                    ctx->rounds.p, nl, ctx->hot_mcnt.p, (int32_t)segs, ctx->hot_mi.p, mcap,
-                                   ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p, ctx->errflag.p, lst, ctx->hot_flag.p,
-                                   ctx->rs_done.p + 2, ctx->hot_items.p, (int64_t)kBxR * kBlock);
+                                   ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p, ctx->errflag.p, lst, ctx->hot_flag.p);
+                hipLaunchKernelGGL(k_hot_items, dim3(1), dim3(1024), 0, ctx->stream, ctx->hot_cnt.p, (int64_t)cells, lst,
+                                   (int64_t)kBxR * kBlock, ctx->hot_items.p);
                 hipLaunchKernelGGL((k_screen_hot<kBxR>), dim3(kHotScreenWgs), dim3(kBlock), 0, ctx->stream,
                                    P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p, P.bx_loff.p, P.bx_list.p, a.n,
                                    nl, (int64_t)cells, ctx->hot_items.p, ctx->hot_items.p + cells + 1,
