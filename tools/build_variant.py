@@ -115,6 +115,12 @@ PATCHES = {
     'sub16': [('tpe_device.h', 'constexpr int kBxSubBits = 5;', 'constexpr int kBxSubBits = 4;'),
               ('tpe_expand.hip', 'const double r_target = 0.5 / (kap * d0); ',
                'const double r_target = 0.25 / (kap * d0);')],
+    'sub8': [('tpe_device.h', 'constexpr int kBxSubBits = 4;', 'constexpr int kBxSubBits = 3;')],
+    'fin32': [('tpe_engine.hip', 'hipLaunchKernelGGL(k_rescore_fin, dim3((unsigned)std::min<int64_t>(ne_sliced, 256))',
+               'hipLaunchKernelGGL(k_rescore_fin, dim3((unsigned)std::min<int64_t>(ne_sliced, 32))')],
+    # k_screen_hot's persistent grid
+    'hsw512': [('tpe_engine.hip', 'constexpr unsigned kHotScreenWgs = 1024;', 'constexpr unsigned kHotScreenWgs = 512;')],
+    'hsw2k': [('tpe_engine.hip', 'constexpr unsigned kHotScreenWgs = 1024;', 'constexpr unsigned kHotScreenWgs = 2048;')],
     'bm': [('tpe_device.h',
             '    return __builtin_amdgcn_sqrt(fmax(0.0, 2.0 * bm_neglog(u01_open0(y), lt)));\n',
             '    return (double)y * 0x1.0p-31;\n')],
