@@ -445,26 +445,52 @@ __device__ __forceinline__ bool samp_fold_block(const DLabel& L, SampRec* __rest
         s[k] = r;
     }
     __syncthreads();
-    bool ok = true;
+    // the cumulative sums in order on one thread, from LDS copies when the
+    // mixture fits (a dependent global load per step cost ~40 us per build)
+    constexpr int kFoldLds = 64;
+    __shared__ double fw[kFoldLds], fm[kFoldLds], fc[kFoldLds];
+    __shared__ bool fok;
+    const bool lds = ns <= kFoldLds;
+    if (lds)
+        for (int k = threadIdx.x; k < ns; k += blockDim.x) {
+            fw[k] = s[k].wd;
+            fm[k] = s[k].m;
+        }
+    __syncthreads();
     if (threadIdx.x == 0) {
         double tot = 0.0, Z = 0.0;
         for (int k = 0; k < ns; ++k) {
-            tot += s[k].wd;
-            Z += s[k].wd * s[k].m;
+            const double w = lds ? fw[k] : s[k].wd, m = lds ? fm[k] : s[k].m;
+            tot += w;
+            Z += w * m;
         }
-        ok = tot > 0.0;
+        fok = tot > 0.0;
         const bool zero = !(Z > 0.0);
         double run = 0.0;
         for (int k = 0; k < ns; ++k) {
-            const double w = s[k].wd;
-            run += w * s[k].m;
-            s[k].cdf = (k == ns - 1 || zero) ? 1.0 : run / Z;
-            s[k].wd = zero ? 0.0 : w / Z;
-            if (zero) s[k].m = 0.0;
+            const double w = lds ? fw[k] : s[k].wd, m = lds ? fm[k] : s[k].m;
+            run += w * m;
+            const double c = (k == ns - 1 || zero) ? 1.0 : run / Z;
+            if (lds) {
+                fc[k] = c;
+                fw[k] = zero ? 0.0 : w / Z;
+                fm[k] = zero ? 0.0 : m;
+            } else {
+                s[k].cdf = c;
+                s[k].wd = zero ? 0.0 : w / Z;
+                if (zero) s[k].m = 0.0;
+            }
         }
     }
     __syncthreads();
-    return ok;
+    if (lds)
+        for (int k = threadIdx.x; k < ns; k += blockDim.x) {
+            s[k].cdf = fc[k];
+            s[k].wd = fw[k];
+            s[k].m = fm[k];
+        }
+    __syncthreads();
+    return fok;
 }
 
 // Candidates 2p and 2p + 1 share one Philox4x32-10 call: the counter is (p,

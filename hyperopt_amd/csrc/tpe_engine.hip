@@ -765,13 +765,24 @@ __global__ __launch_bounds__(kBlock) void k_hot_tau0(const int32_t* __restrict__
                                                      unsigned long long* __restrict__ tau0) {
     const BxLabel B = bx[group[blockIdx.y]];
     const int64_t nsb = (int64_t)B.nbins * kBxSub;
+    // the workgroup's sub-bins and the kHotRun after them, staged in LDS with
+    // coalesced loads (a run walked in global memory was one dependent load
+    // per step: 36 us a launch)
+    __shared__ float tp[kBlock + kHotRun], tl[kBlock + kHotRun];
+    const int64_t j0 = (int64_t)blockIdx.x * kBlock;
+    for (int t = threadIdx.x; t < kBlock + kHotRun; t += kBlock)
+        if (j0 + t < nsb) {
+            tp[t] = sbp[B.sb_off + j0 + t];
+            tl[t] = sb[B.sb_off + j0 + t].y;
+        }
+    __syncthreads();
     uint64_t k = 0;
-    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t j = j0 + threadIdx.x;
     if (j < nsb) {
         float p = 0.0f, lmin = __builtin_inff();
         for (int w = 0; w < kHotRun && j + w < nsb; ++w) {
-            p += sbp[B.sb_off + j + w];
-            lmin = fminf(lmin, sb[B.sb_off + j + w].y);
+            p += tp[threadIdx.x + w];
+            lmin = fminf(lmin, tl[threadIdx.x + w]);
             if (p >= pmin) {
                 const uint64_t v = order_key((double)lmin);
                 k = v > k ? v : k;
@@ -786,7 +797,8 @@ __global__ __launch_bounds__(kBlock) void k_hot_tau0(const int32_t* __restrict__
 
 
 // per label position: bit j of the label's words = (order key of U_j >=
-// tau0); grid (ceil(max words / 256), dense labels), one word per thread
+// tau0); grid (ceil(max sub-bins / 256), dense labels), one sub-bin per
+// thread (coalesced), a wave's 64 bits written as two words
 __global__ __launch_bounds__(kBlock) void k_hot_bits(const int32_t* __restrict__ group,
                                                      const BxLabel* __restrict__ bx,
                                                      const float2* __restrict__ sb,
@@ -794,15 +806,15 @@ __global__ __launch_bounds__(kBlock) void k_hot_bits(const int32_t* __restrict__
                                                      uint32_t* __restrict__ hbits) {
     const BxLabel B = bx[group[blockIdx.y]];
     const int64_t nsb = (int64_t)B.nbins * kBxSub;
-    const int64_t w = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (w * 32 >= nsb) return;
+    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t jw = j - (threadIdx.x & 63);   // the wave's first sub-bin (a multiple of 64)
+    if (jw >= nsb) return;   // (wave-uniform)
     const uint64_t t0 = tau0[blockIdx.y];
-    uint32_t word = 0;
-    for (int b = 0; b < 32; ++b) {
-        const int64_t j = w * 32 + b;
-        if (j < nsb && order_key((double)sb[B.sb_off + j].x) >= t0) word |= 1u << b;
-    }
-    hbits[(B.sb_off >> 5) + w] = word;
+    const bool set = j < nsb && order_key((double)sb[B.sb_off + j].x) >= t0;
+    const uint64_t m = __ballot(set);
+    const int lane = threadIdx.x & 63;
+    if (lane == 0) hbits[(B.sb_off >> 5) + (jw >> 5)] = (uint32_t)m;
+    if (lane == 32 && jw + 32 < nsb) hbits[(B.sb_off >> 5) + (jw >> 5) + 1] = (uint32_t)(m >> 32);
 }
 
 // Draw every candidate of the round (the same draws as k_screen_bx) and
@@ -3906,8 +3918,7 @@ int hot_tau_prepare(tpe_ctx* ctx, int64_t n) {
                        ctx->hot_tau0.p);
     if (ctx->hot == 2)   // test mode: a threshold no candidate reaches -> the fallback
         HIPCHK(ctx, hipMemsetAsync(ctx->hot_tau0.p, 0xff, nl * sizeof(unsigned long long), ctx->stream));
-    const int64_t words = (P.bx_sb_max + 31) / 32;
-    hipLaunchKernelGGL(k_hot_bits, dim3((unsigned)((words + kBlock - 1) / kBlock), nl), dim3(kBlock), 0,
+    hipLaunchKernelGGL(k_hot_bits, dim3((unsigned)((P.bx_sb_max + kBlock - 1) / kBlock), nl), dim3(kBlock), 0,
                        ctx->stream, grp, P.bx.p, P.bx_sb.p, ctx->hot_tau0.p, ctx->hot_bits.p);
     // the sampling components' u-cells (k_hot_bx decides most candidates from them)
     HIPCHK(ctx, ctx->hot_pc.reserve((size_t)(P.bx_sb.cap + 31) / 32));

@@ -142,15 +142,37 @@ __global__ __launch_bounds__(kBlock) void k_bx_scan(const DLabel* __restrict__ l
         if (L.flags & 2) hi = fmin(hi, L.high);
     }
     const Comp<double>* c = comps64 + L.comp_a;
+    // (kScanU records per thread loaded before use: a dependent load per
+    // record left the 10k-record passes latency-bound)
+    constexpr int kScanU = 8;
     double am = 0.0;
-    for (int k = threadIdx.x; k < L.na; k += kBlock)
-        if (usable(c[k])) am = fmax(am, c[k].a);
+    for (int k0 = threadIdx.x; k0 < L.na; k0 += kBlock * kScanU) {
+        Comp<double> r[kScanU];
+#pragma unroll
+        for (int u = 0; u < kScanU; ++u) {
+            const int k = k0 + u * kBlock;
+            r[u] = k < L.na ? c[k] : Comp<double>{0.0, 0.0, 0.0, 0.0};
+        }
+#pragma unroll
+        for (int u = 0; u < kScanU; ++u)
+            if (k0 + u * kBlock < L.na && usable(r[u])) am = fmax(am, r[u].a);
+    }
     am = blk_max(am, shd);
     int nc = 0, ncl = 0;
-    for (int k = threadIdx.x; k < L.na; k += kBlock) {
-        const bool cl = c[k].a == am;
-        nc += !cl;
-        ncl += cl;
+    for (int k0 = threadIdx.x; k0 < L.na; k0 += kBlock * kScanU) {
+        double a[kScanU];
+#pragma unroll
+        for (int u = 0; u < kScanU; ++u) {
+            const int k = k0 + u * kBlock;
+            a[u] = k < L.na ? c[k].a : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kScanU; ++u)
+            if (k0 + u * kBlock < L.na) {
+                const bool cl = a[u] == am;
+                nc += !cl;
+                ncl += cl;
+            }
     }
     nc = blk_sum(nc, shi);
     ncl = blk_sum(ncl, shi);
@@ -175,13 +197,25 @@ __global__ __launch_bounds__(kBlock) void k_bx_compact(const DLabel* __restrict_
     const DLabel L = labels[li];
     const double am = bx[li].astar;
     __shared__ int shi[kBlock / 64];
+    // kCompactU consecutive records per thread (record order kept): one
+    // block scan per kBlock x kCompactU records (per kBlock, the 40 scans
+    // of a 10k-record label took ~20 us)
+    constexpr int kCompactU = 8;
     int base = 0;
-    for (int k0 = 0; k0 < L.na; k0 += kBlock) {
-        const int k = k0 + threadIdx.x;
-        const bool f = k < L.na && comps64[L.comp_a + k].a != am;
+    for (int k0 = 0; k0 < L.na; k0 += kBlock * kCompactU) {
+        const int kt = k0 + (int)threadIdx.x * kCompactU;
+        bool f[kCompactU];
+        int mine = 0;
+#pragma unroll
+        for (int u = 0; u < kCompactU; ++u) {
+            f[u] = kt + u < L.na && comps64[L.comp_a + kt + u].a != am;
+            mine += f[u];
+        }
         int tot;
-        const int pos = blk_prefix((int)f, shi, tot);
-        if (f) nc[L.comp_a + base + pos] = k;
+        int at = base + blk_prefix(mine, shi, tot);
+#pragma unroll
+        for (int u = 0; u < kCompactU; ++u)
+            if (f[u]) nc[L.comp_a + at++] = kt + u;
         base += tot;
     }
 }
@@ -210,17 +244,31 @@ __global__ __launch_bounds__(kBlock) void k_bx_list(const DLabel* __restrict__ l
     const int li = grp[blockIdx.y];
     const BxLabel B = bx[li];
     const int b = blockIdx.x * kBlock + threadIdx.x;
-    if (b >= B.nbins) return;
+    if ((int)(blockIdx.x * kBlock) >= B.nbins) return;   // (the whole workgroup)
     const DLabel L = labels[li];
     const Comp<double>* c = comps64 + L.comp_a;
     const int32_t* ncl = nc + L.comp_a;
+    // the unclipped records staged kBlock at a time in LDS (every lane reads
+    // every record: walked in global memory they were two dependent loads
+    // per record, ~45 us a launch)
+    __shared__ Comp<double> sc[kBlock];
+    __shared__ int32_t sk[kBlock];
     int m = 0;
     int32_t* out = list + B.list_off + (int64_t)b * B.n_nc;
-    for (int j = 0; j < B.n_nc; ++j) {
-        const int k = ncl[j];
-        if (reaches(c[k], B, b)) out[m++] = k;
+    for (int j0 = 0; j0 < B.n_nc; j0 += kBlock) {
+        const int nj = min(kBlock, B.n_nc - j0);
+        __syncthreads();   // (the previous chunk read by every lane)
+        if ((int)threadIdx.x < nj) {
+            const int k = ncl[j0 + threadIdx.x];
+            sk[threadIdx.x] = k;
+            sc[threadIdx.x] = c[k];
+        }
+        __syncthreads();
+        if (b < B.nbins)
+            for (int j = 0; j < nj; ++j)
+                if (reaches(sc[j], B, b)) out[m++] = sk[j];
     }
-    cnt[B.cnt_off + b] = m;
+    if (b < B.nbins) cnt[B.cnt_off + b] = m;
 }
 
 // 1 / n!, n <= kBxP

@@ -118,6 +118,7 @@ PATCHES = {
     'sub8': [('tpe_device.h', 'constexpr int kBxSubBits = 4;', 'constexpr int kBxSubBits = 3;')],
     'fin32': [('tpe_engine.hip', 'hipLaunchKernelGGL(k_rescore_fin, dim3((unsigned)std::min<int64_t>(ne_sliced, 256))',
                'hipLaunchKernelGGL(k_rescore_fin, dim3((unsigned)std::min<int64_t>(ne_sliced, 32))')],
+    'mt16': [('tpe_engine.hip', 'constexpr int64_t kHotMinTiles = 6;', 'constexpr int64_t kHotMinTiles = 16;')],
     # k_screen_hot's persistent grid
     'hsw512': [('tpe_engine.hip', 'constexpr unsigned kHotScreenWgs = 1024;', 'constexpr unsigned kHotScreenWgs = 512;')],
     'hsw2k': [('tpe_engine.hip', 'constexpr unsigned kHotScreenWgs = 1024;', 'constexpr unsigned kHotScreenWgs = 2048;')],
