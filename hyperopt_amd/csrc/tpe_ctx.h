@@ -195,6 +195,7 @@ struct Posterior {
     std::vector<tpe::BxLabel> bx_h;
     DevBuf<double> bx_tab;               // per label: nbins rows of kBxRow doubles
     DevBuf<int32_t> bx_nc;               // per label at comp_a: unclipped above components
+    DevBuf<tpe::BxTerm> bx_terms;        // per above record of a dense label: its bound terms (k_bx_terms)
     DevBuf<int32_t> bx_loff;             // per bin: the length of its list
     DevBuf<int32_t> bx_list;             // per bin: a slot of n_nc, the unclipped components reaching it
     DevBuf<double> bx_scan;              // per dense label position: range, a*, counts
@@ -242,6 +243,7 @@ struct Posterior {
         bx_h.clear();
         bx_tab.release();
         bx_nc.release();
+        bx_terms.release();
         bx_loff.release();
         bx_list.release();
         bx_scan.release();

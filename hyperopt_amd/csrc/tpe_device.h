@@ -63,6 +63,15 @@ struct alignas(64) SampRec {
     double m;           // the interval's mass (0: never picked)
 };
 
+// The expansion index's per-record bound terms of an above record (k_bx_terms,
+// once per index; k_bx_bounds reads them for its bins' lists): c = c'/K, kap
+// = a'^2 / K, mu = m'/a', ec = 1e-15 (64 + |c|) + 3e-14, es = 64e-15
+// sqrt(kap); ec < 0 marks a weighted unusable record, c = -inf one without a
+// term
+struct alignas(16) BxTerm {
+    double c, kap, mu, ec, es, pad;
+};
+
 struct Partial {
     uint64_t key;
     int64_t idx;

@@ -1245,6 +1245,10 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
     if (item >= total) return;   // (uniform: a workgroup with nothing to do stages nothing)
     load_exp_table(exp_tab);
     for (;;) {
+        // the following item claimed now, its atomic's latency under this
+        // item's work
+        int32_t nxt = 0;
+        if (threadIdx.x == 0) nxt = atomicAdd(next, 1);
         // the item's cell: the last c with pre[c] <= item (empty cells share
         // their successor's start)
         int64_t lo = 0, up = cells;
@@ -1285,7 +1289,7 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
         kl = block_max_key(kl, shk);
         if (threadIdx.x == 0) {
             if (kl) atomicMax(tkey + cell, kl);
-            item_sh = atomicAdd(next, 1);
+            item_sh = nxt;
         }
         __syncthreads();   // (shk read by every thread before thread 0 wrote item_sh: block_max_key's barrier)
         item = item_sh;
@@ -1740,6 +1744,11 @@ __global__ __launch_bounds__(kBlock) void k_rescore_slices(
     part[((size_t)e * s_max + slice) * kRsW + lane] = acc[0];
     }
 }
+
+// k_rescore_fin's workgroups: every one pays a device-scope release (an L2
+// write-back) for the last-workgroup merge, and a round re-scores a few
+// dozen entries (256 before round 6's measurements of that fence)
+constexpr int64_t kRsFinWgs = 64;
 
 // The re-score's end: per entry (one wave each, entries strided) the slice
 // sums added in order, the logs and the entry's maxloc into res[entry];
@@ -4236,7 +4245,7 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                            dim3(kBlock), 0, ctx->stream, ctx->P->labels.p, grp, ctx->P->comps64.p, ctx->P->samp.p, lst,
                            a.cand_offset, a.seed, ctx->rounds.p, nl, ctx->scr_cnt.p, ctx->scr_idx.p, chp, plan,
                            ctx->rs_x.p, ctx->rs_g.p, s_max, ctx->rs_part.p);
-        hipLaunchKernelGGL(k_rescore_fin, dim3((unsigned)std::min<int64_t>(ne_sliced, 256)), dim3(kRsW), 0, ctx->stream,
+        hipLaunchKernelGGL(k_rescore_fin, dim3((unsigned)std::min<int64_t>(ne_sliced, kRsFinWgs)), dim3(kRsW), 0, ctx->stream,
                            ctx->P->labels.p, grp, ctx->P->comps64.p, nl, chp, plan, ctx->rs_x.p, ctx->rs_g.p, s_max,
                            ctx->rs_part.p, ctx->scr_res.p, ctx->rs_done.p + 1, (int64_t)cells, ctx->P->n_labels,
                            a.tiles, ctx->scr_off.p, ctx->partials.p);

@@ -557,6 +557,30 @@ __device__ __forceinline__ void term_bounds(const BelowTerm& t, double e0, doubl
     lo += ul > -4.0e6 ? exp_scaled(ul, etab) : 0.0;   // (below ~2^-980: 0 is a lower bound)
 }
 
+// grid (ceil(max above records / 256), dense labels): each above record's
+// bound terms (BxTerm), the per-record part of gauss_bounds evaluated once
+// instead of per sub-bin of every bin whose list holds the record
+__global__ __launch_bounds__(kBlock) void k_bx_terms(const DLabel* __restrict__ labels,
+                                                     const int32_t* __restrict__ grp,
+                                                     const Comp<double>* __restrict__ comps64,
+                                                     BxTerm* __restrict__ terms) {
+    const DLabel L = labels[grp[blockIdx.y]];
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    if (k >= L.na) return;
+    const Comp<double> r = comps64[L.comp_a + k];
+    BxTerm t{-kInf, 0.0, 0.0, 0.0, 0.0, 0.0};
+    if (usable(r)) {
+        t.c = r.c * kExpScaleInv;
+        t.kap = r.a * r.a * kExpScaleInv;
+        t.mu = r.mu / r.a;
+        t.ec = 1e-15 * (64.0 + fabs(t.c)) + 3e-14;
+        t.es = 1e-15 * 64.0 * sqrt(t.kap);
+    } else if (r.c > -kInf) {
+        t.ec = -1.0;   // a weighted unusable record: no bound anywhere
+    }
+    terms[L.comp_a + k] = t;
+}
+
 // grid (ceil(max sub-bins / 256), dense labels): one sub-bin per thread --
 // the hot-bin prefilter's [L, U] of the fp64 score over the sub-bin (float,
 // rounded outward) and the sampling mass p of the sub-bin (tpe_device.h,
@@ -579,6 +603,7 @@ __global__ __launch_bounds__(kBlock) void k_bx_bounds(const DLabel* __restrict__
                                                       const double* __restrict__ tab,
                                                       const int32_t* __restrict__ cnt,
                                                       const int32_t* __restrict__ list,
+                                                      const BxTerm* __restrict__ terms,
                                                       float2* __restrict__ sb, float* __restrict__ sbp) {
     const int li = grp[blockIdx.y];
     const BxLabel B = bx[li];
@@ -703,16 +728,13 @@ __global__ __launch_bounds__(kBlock) void k_bx_bounds(const DLabel* __restrict__
     const double emax = exp(-B.kappa * dmin * dmin) * (1.0 + 1e-14);
     const double emin = exp(-B.kappa * dmax * dmax) * (1.0 - 1e-14);
     double slo = alo > 0.0 ? emin * alo : 0.0, shi = ahi > 0.0 ? emax * ahi : 0.0;
-    const Comp<double>* ca = comps64 + L.comp_a;
+    const BxTerm* ta = terms + L.comp_a;
     const int32_t* lst = list + B.list_off + (int64_t)b * B.n_nc;
     const int m = cnt[B.cnt_off + b];
     for (int jj = 0; jj < m; ++jj) {
-        const Comp<double> r = ca[lst[jj]];
-        if (!usable(r)) {
-            ok = ok && !(r.c > -kInf);
-            continue;
-        }
-        gauss_bounds(r, e0, e1, slo, shi, etab);
+        const BxTerm q = ta[lst[jj]];
+        if (q.ec < 0.0) ok = false;
+        else if (q.c > -kInf) term_bounds(BelowTerm{q.c, q.kap, q.mu, q.ec, q.es}, e0, e1, slo, shi, etab);
     }
     shi += (double)L.na * exp2(-B.tcut);
     const double dsh = L.shift_b - L.shift_a;
@@ -938,9 +960,15 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
                            ctx->stream, grp, P.bx.p, P.bx_tab.p, nsplit, P.bx_part.p, rows);
     P.bx_sb_max = (int64_t)bins_max * kBxSub;
     P.bx_gen = tpe_rt::next_bx_gen();
+    int32_t na_max = 1;
+    for (int y = 0; y < nl; ++y)
+        na_max = std::max(na_max, P.h_labels[y < (int)gg.size() ? gg[y] : gl[y - gg.size()]].na);
+    HIPCHK(ctx, P.bx_terms.reserve(P.comps64.cap));
+    hipLaunchKernelGGL(k_bx_terms, dim3((unsigned)((na_max + kBlock - 1) / kBlock), nl), dim3(kBlock), 0,
+                       ctx->stream, P.labels.p, grp, P.comps64.p, P.bx_terms.p);
     const dim3 gs((unsigned)((P.bx_sb_max + kBlock - 1) / kBlock), nl);
     hipLaunchKernelGGL(k_bx_bounds, gs, dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p, P.samp.p,
-                       P.bx.p, P.bx_tab.p, P.bx_loff.p, P.bx_list.p, P.bx_sb.p, P.bx_sbp.p);
+                       P.bx.p, P.bx_tab.p, P.bx_loff.p, P.bx_list.p, P.bx_terms.p, P.bx_sb.p, P.bx_sbp.p);
     HIPCHK(ctx, hipGetLastError());
     // the snapshot a later rebuild is compared with (bx_keep_check)
     int64_t c_ext = 0, s_ext = 0;
