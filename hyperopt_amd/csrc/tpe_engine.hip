@@ -540,6 +540,7 @@ __global__ __launch_bounds__(kBlock) void k_screen(
 // s = NaN, E = +inf (always re-scored).  E is ~1e-12, far below an fp32
 // rounding of the score.  Returns the terms the R candidates summed
 // directly (nb + list each).
+constexpr int kListU = 4;   // bin-list entries loaded per step (bx_score)
 template <int R>
 __device__ __forceinline__ int bx_score(const DLabel& L, const BxLabel& B,
                                         const Comp<double>* __restrict__ comps64,
@@ -585,10 +586,23 @@ __device__ __forceinline__ int bx_score(const DLabel& L, const BxLabel& B,
         const int j0 = 0, j1 = loff[B.cnt_off + b];   // the bin's count, its slot of n_nc entries
         const int32_t* lst = list + B.list_off + (int64_t)b * B.n_nc;
         double snc = 0.0;
-        for (int j = j0; j < j1; ++j) {
-            const Comp<double> rec = ca[lst[j]];
-            const double zz = fma(xr[r], rec.a, -rec.mu);
-            snc = exp_scaled_acc(fma(-zz, zz, rec.c), exp_tab, snc);
+        // the list walked kListU entries at a time: their indices, then
+        // their records, loaded before the terms are added in order (one
+        // entry per step was two dependent loads per term: the screen's
+        // latency, r6r)
+        for (int j = j0; j < j1; j += kListU) {
+            int32_t kk[kListU];
+#pragma unroll
+            for (int u = 0; u < kListU; ++u) kk[u] = lst[min(j + u, j1 - 1)];
+            Comp<double> rr[kListU];
+#pragma unroll
+            for (int u = 0; u < kListU; ++u) rr[u] = ca[kk[u]];
+#pragma unroll
+            for (int u = 0; u < kListU; ++u)
+                if (j + u < j1) {
+                    const double zz = fma(xr[r], rr[u].a, -rr[u].mu);
+                    snc = exp_scaled_acc(fma(-zz, zz, rr[u].c), exp_tab, snc);
+                }
         }
         nterms += L.nb + (j1 - j0);
         const double sum = sclip + snc;
@@ -1241,7 +1255,7 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
     const int32_t total = pre[cells];
     if (threadIdx.x == 0) item_sh = total > 0 ? atomicAdd(next, 1) : total;
     __syncthreads();
-    int32_t item = item_sh;
+    int32_t item = __builtin_amdgcn_readfirstlane(item_sh);   // (uniform: the item's fields live in scalar registers)
     if (item >= total) return;   // (uniform: a workgroup with nothing to do stages nothing)
     load_exp_table(exp_tab);
     for (;;) {
@@ -1256,10 +1270,10 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
             const int64_t mid = (lo + up) >> 1;
             if (pre[mid] <= item) lo = mid; else up = mid;
         }
-        const size_t cell = (size_t)lo;
+        const size_t cell = (size_t)__builtin_amdgcn_readfirstlane((int)lo);   // (uniform: scalar loads below)
         const int64_t m = min((int64_t)hcnt[cell], hstride);   // (an overflowed list falls back anyway)
         const int64_t j0 = (int64_t)(item - pre[cell]) * per;
-        const int li = group[cell % (size_t)nl];
+        const int li = __builtin_amdgcn_readfirstlane(group[cell % (size_t)nl]);
         const DLabel L = labels[li];
         const BxLabel B = bx[li];
         const bool lgmm = L.mode == DENSE_LGMM;
@@ -1292,7 +1306,7 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
             item_sh = nxt;
         }
         __syncthreads();   // (shk read by every thread before thread 0 wrote item_sh: block_max_key's barrier)
-        item = item_sh;
+        item = __builtin_amdgcn_readfirstlane(item_sh);
         if (item >= total) break;
         __syncthreads();   // item_sh read by every thread before the next write
     }
