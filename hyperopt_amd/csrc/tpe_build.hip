@@ -1752,6 +1752,7 @@ int finish_build(tpe_ctx* ctx, BuildTail& t, int32_t* ties_out, int32_t* n_below
     if (!subset) B.built_loss_hash = t.loss_hash;
     if (n_below_out) *n_below_out = t.n_below;
     // the armed index, queued now: no caller round trip before it starts
+    P.bx_prescan_ok = t.prescan && !P.bx_ready;
     if (t.arm_c > 0) return tpe1_prepare(ctx, t.arm_c, t.arm_r);
     return TPE_OK;
 }
@@ -1785,6 +1786,7 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
                 return ctx->fail(TPE_ERR_ARG, "subset labels must be increasing label indices");
     }
     B.built_ok = false;   // (set again once this build completes)
+    ctx->resident.bx_prescan_ok = false;
     if (lf < 1 || lf >= kMaxLF) return ctx->fail(TPE_ERR_ARG, "linear forgetting must be in [1, 63]");
     if (n_trials < 0 || n_trials >= INT32_MAX || (n_trials > 0 && !losses) || n_valid < 0 ||
         n_valid > n_trials)
@@ -1980,6 +1982,20 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
         const int rc = tpe_rt::bx_keep_check(ctx);
         if (rc) return rc;
     }
+    // the armed index's per-label scan rides on this sync when the label
+    // groups (on the device since the previous build) are unchanged: the
+    // index then starts without a round trip of its own
+    bool prescan = false;
+    if (!subset && arm_c > 0 && P.groups.p) {
+        std::vector<int32_t> cat_now;
+        for (int m = 0; m < kNumModes; ++m) cat_now.insert(cat_now.end(), grp[m].begin(), grp[m].end());
+        bool same = cat_now == P.groups_h;
+        for (int m = 0; same && m < kNumModes; ++m) same = grp[m] == P.h_group[m];
+        if (same) {
+            const int rc = tpe_rt::bx_prescan(ctx, st, &prescan);
+            if (rc) return rc;
+        }
+    }
     // beside the index: the quantized labels' runs for the coming round
     // (k_qcompress) go on the aux stream too, under the same sync -- over the
     // previous build's label groups, which a subset rebuild of the same
@@ -2010,6 +2026,7 @@ int build_resident(tpe_ctx* ctx, const double* losses, int64_t n_trials, int64_t
     t.n_valid = n_valid;
     t.arm_c = arm_c;
     t.arm_r = arm_r;
+    t.prescan = prescan;
     t.gamma = gamma;
     t.pw = prior_weight;
     if (!subset) t.loss_hash = loss_fingerprint(losses, n_trials);

@@ -191,6 +191,10 @@ struct Posterior {
     // posterior change; bx_ok: every dense label has one (else the windowed
     // screen runs)
     bool bx_ready = false, bx_ok = false;
+    // the index's per-label scan, queued by a full build under its report's
+    // sync (bx_prescan) and consumed by the next bx_build: no round trip of its own
+    bool bx_prescan_ok = false;
+    PinVec<double> bx_scan_h;
     DevBuf<tpe::BxLabel> bx;             // per label
     std::vector<tpe::BxLabel> bx_h;
     DevBuf<double> bx_tab;               // per label: nbins rows of kBxRow doubles
@@ -295,6 +299,7 @@ struct BuildTail {
     bool beside = false, qc_queued = false, subset = false, deferred = false;
     int64_t n_trials = 0, n_valid = 0, arm_c = 0;
     int32_t arm_r = 0;
+    bool prescan = false;                // the index's scan queued under this build's sync (bx_prescan)
     double gamma = 0.0, pw = 0.0;
     uint64_t loss_hash = 0;
 };
@@ -661,6 +666,10 @@ int bx_build(tpe_ctx* ctx);
 // sync); bx_keep_after: whether the index stays valid.
 int bx_keep_check(tpe_ctx* ctx);
 bool bx_keep_after(tpe_ctx* ctx, bool groups_changed);
+// A full build with an armed index and unchanged label groups: queue the
+// index's per-label scan and its read-back on `st` before the build's sync
+// (bx_build then starts from it); *queued says whether it was
+int bx_prescan(tpe_ctx* ctx, hipStream_t st, bool* queued);
 // The quantized labels' above mixtures as runs (k_qcompress, tpe_engine.hip)
 // queued on `st`; sets P->qc_ready.  The round queues it on its own stream
 // when not ready; the subset rebuild beside the expansion index queues it on

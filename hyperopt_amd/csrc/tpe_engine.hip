@@ -4930,6 +4930,7 @@ int set_posterior_impl(tpe_ctx* ctx, const tpe_label_desc* labels, int32_t n_lab
                        int64_t n_components, bool sampler_checks) {
     if (!ctx) return TPE_ERR_ARG;
     if (ctx->P == &ctx->resident) ctx->build.n_labels = 0;   // no built mixtures resident
+    ctx->P->bx_prescan_ok = false;   // (a build's pre-scan is of that build's posterior)
     if (n_labels <= 0 || !labels || !weights) return ctx->fail(TPE_ERR_ARG, "empty posterior");
     HIPCHK(ctx, hipSetDevice(ctx->device));
     std::vector<DLabel> dl(n_labels);

@@ -39,6 +39,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 #include <cmath>
 
 #include "../../include/hyperopt_tpe.h"
@@ -824,6 +825,22 @@ bool tpe_rt::bx_keep_after(tpe_ctx* ctx, bool groups_changed) {
     return P.bx_ready && P.bx_snap_nl > 0 && !groups_changed && ctx->pin[0].bx_diff == 0;
 }
 
+int tpe_rt::bx_prescan(tpe_ctx* ctx, hipStream_t st, bool* queued) {
+    tpe_rt::Posterior& P = *ctx->P;
+    *queued = false;
+    const int nl = (int)(P.h_group[DENSE_GMM].size() + P.h_group[DENSE_LGMM].size());
+    if (nl == 0 || !P.groups.p) return TPE_OK;
+    HIPCHK(ctx, P.bx_scan.reserve((size_t)nl * kScanFields));
+    HIPCHK(ctx, P.bx_scan_h.resize((size_t)nl * kScanFields));
+    hipLaunchKernelGGL(k_bx_scan, dim3(nl), dim3(kBlock), 0, st, P.labels.p, P.groups.p + P.group_off[DENSE_GMM],
+                       P.comps64.p, P.samp.p, P.bx_scan.p);
+    HIPCHK(ctx, hipGetLastError());
+    HIPCHK(ctx, hipMemcpyAsync(P.bx_scan_h.data(), P.bx_scan.p, (size_t)nl * kScanFields * sizeof(double),
+                               hipMemcpyDeviceToHost, st));
+    *queued = true;
+    return TPE_OK;
+}
+
 // unique over every posterior of the process (an index built here or
 // imported, tpe_share.hip): the hot-bin caches are keyed by it
 uint64_t tpe_rt::next_bx_gen() {
@@ -861,14 +878,20 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
         return TPE_OK;
     }
     const int32_t* grp = P.groups.p + P.group_off[DENSE_GMM];
-    HIPCHK(ctx, P.bx_scan.reserve((size_t)nl * kScanFields));
-    hipLaunchKernelGGL(k_bx_scan, dim3(nl), dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p,
-                       P.samp.p, P.bx_scan.p);
-    HIPCHK(ctx, hipGetLastError());
     std::vector<double> sc((size_t)nl * kScanFields);
-    HIPCHK(ctx, hipMemcpyAsync(sc.data(), P.bx_scan.p, sc.size() * sizeof(double), hipMemcpyDeviceToHost,
-                               ctx->stream));
-    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    if (P.bx_prescan_ok && P.bx_scan_h.n == sc.size()) {
+        // (the build queued the scan and its read-back before its own sync)
+        std::memcpy(sc.data(), P.bx_scan_h.data(), sc.size() * sizeof(double));
+    } else {
+        HIPCHK(ctx, P.bx_scan.reserve((size_t)nl * kScanFields));
+        hipLaunchKernelGGL(k_bx_scan, dim3(nl), dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p,
+                           P.samp.p, P.bx_scan.p);
+        HIPCHK(ctx, hipGetLastError());
+        HIPCHK(ctx, hipMemcpyAsync(sc.data(), P.bx_scan.p, sc.size() * sizeof(double), hipMemcpyDeviceToHost,
+                                   ctx->stream));
+        HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    P.bx_prescan_ok = false;
     // bins per label: the fewest (a multiple of 64) whose half-width keeps
     // the Taylor argument 2 kappa |d| r <= ~0.5 over the window
     P.bx_h.assign(P.n_labels, BxLabel{});

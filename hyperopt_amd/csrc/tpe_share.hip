@@ -375,6 +375,7 @@ int tpe_import_posterior(tpe_ctx* ctx, const void* d_blobs, int64_t blob_bytes, 
     P.bx_h = bx_ok ? bxh : std::vector<BxLabel>();
     P.bx_sb_max = bx_ok ? (int64_t)bins_max * kBxSub : 0;
     P.bx_snap_nl = 0;    // (no snapshot: a later build replaces the whole posterior)
+    P.bx_prescan_ok = false;
     P.bx_ready = true;   // (ineligible parts: the windowed screen runs, as a build would decide)
     P.bx_gen = tpe_rt::next_bx_gen();
     return TPE_OK;
