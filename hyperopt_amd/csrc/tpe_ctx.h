@@ -206,6 +206,8 @@ struct Posterior {
     DevBuf<float2> bx_sb;                // hot-bin prefilter: per sub-bin (U, L) of the score
     DevBuf<float> bx_sbp;                //   and the below mixture's sampling mass of it
     DevBuf<double> bx_part;              // k_bx_table's split-window partial sums
+    DevBuf<int2> bx_blocks;              // k_bx_table's 64-bin blocks (label position, first bin)
+    PinVec<int2> bx_blocks_h;            //   staged (pinned: the copy is asynchronous)
     int64_t bx_sb_max = 0;               //   the most sub-bins of one label
     uint64_t bx_gen = 0;                 // bumped by every build of the tables (never 0 once built)
     // what the index was built from (the dense labels' DLabel, records and
@@ -254,6 +256,7 @@ struct Posterior {
         bx_sb.release();
         bx_sbp.release();
         bx_part.release();
+        bx_blocks.release();
         bx_snap_l.release();
         bx_snap_c.release();
         bx_snap_s.release();

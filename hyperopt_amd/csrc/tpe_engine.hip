@@ -769,9 +769,11 @@ __global__ __launch_bounds__(kBlock) void k_screen_bx(
 // of 1, 2, 4, .. kHotRun consecutive sub-bins whose sampling mass reaches
 // pmin together (a candidate lands in the run with near certainty, and then
 // its L is at least the run's smallest), the largest smallest L (0 = no
-// such run: every candidate is listed).  grid (ceil(max sub-bins / 256),
+// such run: every candidate is listed).  grid (blocks of 256 sub-bins strided,
 // dense labels), one run start per thread, atomicMax into tau0 (zeroed).
 constexpr int kHotRun = 32;
+constexpr int64_t kHotPrepWgs = (int64_t)1 << 30;   // k_hot_tau0 / k_hot_bits: workgroups over the labels, at most
+// (2048 measured 30 -> 34 us for k_hot_tau0 at config 3, r6x)
 __global__ __launch_bounds__(kBlock) void k_hot_tau0(const int32_t* __restrict__ group,
                                                      const BxLabel* __restrict__ bx,
                                                      const float2* __restrict__ sb,
@@ -779,28 +781,30 @@ __global__ __launch_bounds__(kBlock) void k_hot_tau0(const int32_t* __restrict__
                                                      unsigned long long* __restrict__ tau0) {
     const BxLabel B = bx[group[blockIdx.y]];
     const int64_t nsb = (int64_t)B.nbins * kBxSub;
-    // the workgroup's sub-bins and the kHotRun after them, staged in LDS with
-    // coalesced loads (a run walked in global memory was one dependent load
-    // per step: 36 us a launch)
+    // per block of the label (strided over the grid when it is capped) its
+    // sub-bins and the kHotRun after them, staged in LDS with coalesced
+    // loads (a run walked in global memory was one dependent load per step)
     __shared__ float tp[kBlock + kHotRun], tl[kBlock + kHotRun];
-    const int64_t j0 = (int64_t)blockIdx.x * kBlock;
-    for (int t = threadIdx.x; t < kBlock + kHotRun; t += kBlock)
-        if (j0 + t < nsb) {
-            tp[t] = sbp[B.sb_off + j0 + t];
-            tl[t] = sb[B.sb_off + j0 + t].y;
-        }
-    __syncthreads();
     uint64_t k = 0;
-    const int64_t j = j0 + threadIdx.x;
-    if (j < nsb) {
-        float p = 0.0f, lmin = __builtin_inff();
-        for (int w = 0; w < kHotRun && j + w < nsb; ++w) {
-            p += tp[threadIdx.x + w];
-            lmin = fminf(lmin, tl[threadIdx.x + w]);
-            if (p >= pmin) {
-                const uint64_t v = order_key((double)lmin);
-                k = v > k ? v : k;
-                break;
+    for (int64_t j0 = (int64_t)blockIdx.x * kBlock; j0 < nsb; j0 += (int64_t)gridDim.x * kBlock) {
+        __syncthreads();   // (the previous block's reads)
+        for (int t = threadIdx.x; t < kBlock + kHotRun; t += kBlock)
+            if (j0 + t < nsb) {
+                tp[t] = sbp[B.sb_off + j0 + t];
+                tl[t] = sb[B.sb_off + j0 + t].y;
+            }
+        __syncthreads();
+        const int64_t j = j0 + threadIdx.x;
+        if (j < nsb) {
+            float p = 0.0f, lmin = __builtin_inff();
+            for (int w = 0; w < kHotRun && j + w < nsb; ++w) {
+                p += tp[threadIdx.x + w];
+                lmin = fminf(lmin, tl[threadIdx.x + w]);
+                if (p >= pmin) {
+                    const uint64_t v = order_key((double)lmin);
+                    k = v > k ? v : k;
+                    break;
+                }
             }
         }
     }
@@ -811,7 +815,7 @@ __global__ __launch_bounds__(kBlock) void k_hot_tau0(const int32_t* __restrict__
 
 
 // per label position: bit j of the label's words = (order key of U_j >=
-// tau0); grid (ceil(max sub-bins / 256), dense labels), one sub-bin per
+// tau0); grid (blocks of 256 sub-bins strided, dense labels), one sub-bin per
 // thread (coalesced), a wave's 64 bits written as two words
 __global__ __launch_bounds__(kBlock) void k_hot_bits(const int32_t* __restrict__ group,
                                                      const BxLabel* __restrict__ bx,
@@ -820,15 +824,15 @@ __global__ __launch_bounds__(kBlock) void k_hot_bits(const int32_t* __restrict__
                                                      uint32_t* __restrict__ hbits) {
     const BxLabel B = bx[group[blockIdx.y]];
     const int64_t nsb = (int64_t)B.nbins * kBxSub;
-    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    const int64_t jw = j - (threadIdx.x & 63);   // the wave's first sub-bin (a multiple of 64)
-    if (jw >= nsb) return;   // (wave-uniform)
     const uint64_t t0 = tau0[blockIdx.y];
-    const bool set = j < nsb && order_key((double)sb[B.sb_off + j].x) >= t0;
-    const uint64_t m = __ballot(set);
     const int lane = threadIdx.x & 63;
-    if (lane == 0) hbits[(B.sb_off >> 5) + (jw >> 5)] = (uint32_t)m;
-    if (lane == 32 && jw + 32 < nsb) hbits[(B.sb_off >> 5) + (jw >> 5) + 1] = (uint32_t)(m >> 32);
+    for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j - lane < nsb; j += (int64_t)gridDim.x * kBlock) {
+        const int64_t jw = j - lane;   // the wave's first sub-bin (a multiple of 64; the loop wave-uniform)
+        const bool set = j < nsb && order_key((double)sb[B.sb_off + j].x) >= t0;
+        const uint64_t m = __ballot(set);
+        if (lane == 0) hbits[(B.sb_off >> 5) + (jw >> 5)] = (uint32_t)m;
+        if (lane == 32 && jw + 32 < nsb) hbits[(B.sb_off >> 5) + (jw >> 5) + 1] = (uint32_t)(m >> 32);
+    }
 }
 
 // Draw every candidate of the round (the same draws as k_screen_bx) and
@@ -3936,19 +3940,24 @@ int hot_tau_prepare(tpe_ctx* ctx, int64_t n) {
     if (ctx->hot_tau0_gen == P.bx_gen && ctx->hot_tau0_n == n && ctx->hot != 2) return TPE_OK;
     HIPCHK(ctx, ctx->hot_bits.reserve((size_t)(P.bx_sb.cap + 31) / 32));
     HIPCHK(ctx, hipMemsetAsync(ctx->hot_tau0.p, 0, nl * sizeof(unsigned long long), ctx->stream));
-    hipLaunchKernelGGL(k_hot_tau0, dim3((unsigned)((P.bx_sb_max + kBlock - 1) / kBlock), nl), dim3(kBlock), 0,
+    const unsigned sbw = (unsigned)std::min<int64_t>((P.bx_sb_max + kBlock - 1) / kBlock,
+                                                     std::max<int64_t>(1, kHotPrepWgs / nl));
+    hipLaunchKernelGGL(k_hot_tau0, dim3(sbw, nl), dim3(kBlock), 0,
                        ctx->stream, grp, P.bx.p, P.bx_sb.p, P.bx_sbp.p, (float)(kHotFill / (double)n),
                        ctx->hot_tau0.p);
     if (ctx->hot == 2)   // test mode: a threshold no candidate reaches -> the fallback
         HIPCHK(ctx, hipMemsetAsync(ctx->hot_tau0.p, 0xff, nl * sizeof(unsigned long long), ctx->stream));
-    hipLaunchKernelGGL(k_hot_bits, dim3((unsigned)((P.bx_sb_max + kBlock - 1) / kBlock), nl), dim3(kBlock), 0,
+    hipLaunchKernelGGL(k_hot_bits, dim3(sbw, nl), dim3(kBlock), 0,
                        ctx->stream, grp, P.bx.p, P.bx_sb.p, ctx->hot_tau0.p, ctx->hot_bits.p);
     // the sampling components' u-cells (k_hot_bx decides most candidates from them)
     HIPCHK(ctx, ctx->hot_pc.reserve((size_t)(P.bx_sb.cap + 31) / 32));
     HIPCHK(ctx, ctx->hot_ucell.reserve((size_t)nl * kSampLds * kHotCellWords));
     hipLaunchKernelGGL(k_hot_prefix, dim3((unsigned)nl), dim3(1024), 0, ctx->stream, grp, P.bx.p, ctx->hot_bits.p,
                        ctx->hot_pc.p);
-    hipLaunchKernelGGL(k_hot_ucells, dim3(kHotCells / kBlock, kSampLds, nl), dim3(kBlock), 0, ctx->stream, P.labels.p,
+    int32_t ns_max = 1;   // (workgroups past a label's ns exit at once; none past the largest)
+    for (int m : {DENSE_GMM, DENSE_LGMM})
+        for (int li : P.h_group[m]) ns_max = std::max(ns_max, std::min(P.h_labels[li].ns, kSampLds));
+    hipLaunchKernelGGL(k_hot_ucells, dim3(kHotCells / kBlock, ns_max, nl), dim3(kBlock), 0, ctx->stream, P.labels.p,
                        grp, P.samp.p, P.bx.p, ctx->hot_bits.p, ctx->hot_pc.p, ctx->hot_ucell.p);
     bool staged = true;   // (k_hot_bx runs only when every dense label's records fit in LDS)
     for (int m : {DENSE_GMM, DENSE_LGMM})

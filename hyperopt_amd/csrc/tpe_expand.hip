@@ -371,11 +371,14 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
                                                      const Comp<double>* __restrict__ comps64,
                                                      const BxLabel* __restrict__ bx,
                                                      double* __restrict__ tab, int nsplit,
-                                                     double* __restrict__ part, int64_t rows) {
-    const int li = grp[blockIdx.y];
+                                                     double* __restrict__ part, int64_t rows,
+                                                     const int2* __restrict__ blocks) {
+    // (the grid numbers the labels' 64-bin blocks flat: a grid of the
+    // largest label's blocks per label left most of the others' empty)
+    const int2 blk = blocks[blockIdx.x];   // (dense label position, first bin)
+    const int li = grp[blk.x];
     const BxLabel B = bx[li];
-    const int b0 = blockIdx.x * 64;   // the workgroup's first bin
-    if (b0 >= B.nbins) return;        // the whole workgroup
+    const int b0 = blk.y;             // the workgroup's first bin
     const DLabel L = labels[li];
     __shared__ double lds[kExpTabSize];   // the exp table, then the waves' partial sums
     __shared__ double2 stage[kBlock / 64][64];   // per wave: its batch's (mu', c')
@@ -547,6 +550,8 @@ struct BelowTerm {
     double c, kap, mu, ec, es;
 };
 constexpr int kStageBelow = 64;   // below components staged in LDS (more: read per sub-bin)
+constexpr int64_t kBoundsWgs = (int64_t)1 << 30;   // k_bx_bounds' workgroups over the labels, at most
+// (4096 -- each workgroup striding over several blocks -- measured 127 -> 144 us at config 3, r6x)
 
 __device__ __forceinline__ void term_bounds(const BelowTerm& t, double e0, double e1, double& lo, double& hi,
                                             const double* __restrict__ etab) {
@@ -582,7 +587,7 @@ __global__ __launch_bounds__(kBlock) void k_bx_terms(const DLabel* __restrict__ 
     terms[L.comp_a + k] = t;
 }
 
-// grid (ceil(max sub-bins / 256), dense labels): one sub-bin per thread --
+// grid (blocks of 256 sub-bins strided, dense labels): one sub-bin per thread --
 // the hot-bin prefilter's [L, U] of the fp64 score over the sub-bin (float,
 // rounded outward) and the sampling mass p of the sub-bin (tpe_device.h,
 // "hot-bin prefilter").  Below mixture: every component bounded term by
@@ -642,8 +647,8 @@ __global__ __launch_bounds__(kBlock) void k_bx_bounds(const DLabel* __restrict__
                              : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
     __syncthreads();
-    const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (j >= nsb) return;
+    // (blocks of the label strided over the grid when it is capped)
+    for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < nsb; j += (int64_t)gridDim.x * kBlock) {
     const int b = (int)(j >> kBxSubBits);
     const double sw = B.bw / kBxSub;
     const double e0n = B.xlo + (double)j * sw, e1n = e0n + sw;
@@ -757,6 +762,7 @@ __global__ __launch_bounds__(kBlock) void k_bx_bounds(const DLabel* __restrict__
     }
     sb[B.sb_off + j] = make_float2(float_up(U), float_down(Lo));
     sbp[B.sb_off + j] = (float)p;
+    }
 }
 
 // grid (dense labels of the snapshot): any byte of a dense label's DLabel,
@@ -976,8 +982,23 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
                        : wgs >= 4096     ? 3
                                          : (int)std::max<int64_t>(1, std::min<int64_t>(kBxMaxSplit, 8192 / std::max<int64_t>(wgs, 1)));
     if (nsplit > 1) HIPCHK(ctx, P.bx_part.reserve((size_t)nsplit * kPartSums * rows));
-    hipLaunchKernelGGL(k_bx_table, dim3((unsigned)((bins_max + 63) / 64), nl, nsplit), dim3(kBlock), 0,
-                       ctx->stream, P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p, nsplit, P.bx_part.p, rows);
+    {   // the labels' 64-bin blocks, numbered flat (the previous index's
+        // copy out of the pinned buffer is done: bx_build's scan read-back
+        // or the build's report synchronised the stream since)
+        HIPCHK(ctx, P.bx_blocks_h.resize((size_t)((rows + 63) / 64)));
+        int64_t n = 0;
+        for (int y = 0; y < nl; ++y) {
+            const int li = y < (int)gg.size() ? gg[y] : gl[y - gg.size()];
+            for (int b0 = 0; b0 < P.bx_h[li].nbins; b0 += 64) P.bx_blocks_h.data()[n++] = make_int2(y, b0);
+        }
+        P.bx_blocks_h.n = (size_t)n;
+        HIPCHK(ctx, P.bx_blocks.reserve((size_t)n));
+        HIPCHK(ctx, hipMemcpyAsync(P.bx_blocks.p, P.bx_blocks_h.data(), (size_t)n * sizeof(int2),
+                                   hipMemcpyHostToDevice, ctx->stream));
+    }
+    hipLaunchKernelGGL(k_bx_table, dim3((unsigned)P.bx_blocks_h.n, 1, nsplit), dim3(kBlock), 0,
+                       ctx->stream, P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p, nsplit, P.bx_part.p, rows,
+                       P.bx_blocks.p);
     if (nsplit > 1)
         hipLaunchKernelGGL(k_bx_table_fin, dim3((unsigned)((bins_max + kBlock - 1) / kBlock), nl), dim3(kBlock), 0,
                            ctx->stream, grp, P.bx.p, P.bx_tab.p, nsplit, P.bx_part.p, rows);
@@ -989,7 +1010,8 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
     HIPCHK(ctx, P.bx_terms.reserve(P.comps64.cap));
     hipLaunchKernelGGL(k_bx_terms, dim3((unsigned)((na_max + kBlock - 1) / kBlock), nl), dim3(kBlock), 0,
                        ctx->stream, P.labels.p, grp, P.comps64.p, P.bx_terms.p);
-    const dim3 gs((unsigned)((P.bx_sb_max + kBlock - 1) / kBlock), nl);
+    const dim3 gs((unsigned)std::min<int64_t>((P.bx_sb_max + kBlock - 1) / kBlock,
+                                              std::max<int64_t>(1, kBoundsWgs / nl)), nl);
     hipLaunchKernelGGL(k_bx_bounds, gs, dim3(kBlock), 0, ctx->stream, P.labels.p, grp, P.comps64.p, P.samp.p,
                        P.bx.p, P.bx_tab.p, P.bx_loff.p, P.bx_list.p, P.bx_terms.p, P.bx_sb.p, P.bx_sbp.p);
     HIPCHK(ctx, hipGetLastError());
