@@ -2773,10 +2773,11 @@ __global__ __launch_bounds__(kBlock) void k_qtable(
 // sum_runs W_run (Phi_u - Phi_l), W_run a difference of the label's weight
 // prefix sums (~1e-16 of the total weight each): inside the quantized lpdf
 // bar (relative 1e-9, absolute 1e-13 on the probability).  One workgroup per
-// quantized label position, chunks of 1024 records: the run starts and the
-// prefix by block scans; a start stores the prefix before it, the run's end
-// (after a barrier) the difference.
+// quantized label position, chunks of 4096 records (4 per thread): the run
+// starts and the prefix by block scans; a start stores the prefix before
+// it, the run's end (after a barrier) the difference.
 constexpr int kQcBlock = 1024;
+constexpr int kQcU = 4;   // records per thread per chunk
 __global__ __launch_bounds__(kQcBlock) void k_qcompress(const DLabel* __restrict__ labels,
                                                         const int32_t* __restrict__ group,
                                                         const Comp<double>* __restrict__ comps64,
@@ -2787,10 +2788,6 @@ __global__ __launch_bounds__(kQcBlock) void k_qcompress(const DLabel* __restrict
     const Comp<double>* c = comps64 + L.comp_a;
     Comp<double>* out = qcomp + L.comp_a;
     const int n = L.na, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    auto starts = [&](int k) {   // record k opens a run (bit-unequal mu or a to record k - 1)
-        return k == 0 || __double_as_longlong(c[k].mu) != __double_as_longlong(c[k - 1].mu) ||
-               __double_as_longlong(c[k].a) != __double_as_longlong(c[k - 1].a);
-    };
     __shared__ int32_t wcnt[kQcBlock / 64];
     __shared__ double wsum[kQcBlock / 64];
     __shared__ int32_t runs;
@@ -2800,34 +2797,83 @@ __global__ __launch_bounds__(kQcBlock) void k_qcompress(const DLabel* __restrict
         pre = 0.0;
     }
     __syncthreads();
-    for (int c0 = 0; c0 < n; c0 += kQcBlock) {
-        const int k = c0 + (int)threadIdx.x;
-        const bool in = k < n;
-        const bool st = in && starts(k);
-        const bool en = in && (k == n - 1 || starts(k + 1));
-        const double wk = in ? c[k].w : 0.0;
-        // inclusive scans over the wave: weights and starts
-        double x = wk;
+    // kQcU consecutive records per thread per chunk (one chunk of kQcBlock
+    // was three barriers and a dependent round of loads per 1024 records:
+    // ~70 us for a 7.5k-record label); the thread's records and the two
+    // around them loaded first
+    for (int c0 = 0; c0 < n; c0 += kQcBlock * kQcU) {
+        const int kb = c0 + (int)threadIdx.x * kQcU;
+        double mu[kQcU + 2], av[kQcU + 2], wv[kQcU], cv[kQcU];
+#pragma unroll
+        for (int i = 0; i < kQcU + 2; ++i) {
+            const int k = kb - 1 + i;
+            const bool ok = k >= 0 && k < n;
+            mu[i] = ok ? c[k].mu : 0.0;
+            av[i] = ok ? c[k].a : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < kQcU; ++u) {
+            const bool ok = kb + u < n;
+            wv[u] = ok ? c[kb + u].w : 0.0;
+            cv[u] = ok ? c[kb + u].c : 0.0;
+        }
+        auto differ = [&](int i, int j) {   // (bit-unequal mu or a)
+            return __double_as_longlong(mu[i]) != __double_as_longlong(mu[j]) ||
+                   __double_as_longlong(av[i]) != __double_as_longlong(av[j]);
+        };
+        bool st[kQcU], en[kQcU];
+        double loc[kQcU];
+        double run = 0.0;
+        int nst = 0;
+#pragma unroll
+        for (int u = 0; u < kQcU; ++u) {
+            const int k = kb + u;
+            const bool in = k < n;
+            st[u] = in && (k == 0 || differ(u + 1, u));
+            en[u] = in && (k == n - 1 || differ(u + 2, u + 1));
+            loc[u] = run;   // the thread's weight before record u
+            run += wv[u];
+            nst += st[u];
+        }
+        // inclusive scans over the wave: the threads' weights and starts
+        double x = run;
+        int xs = nst;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
             const double y = __shfl_up(x, off);
-            if (lane >= off) x += y;
+            const int ys = __shfl_up(xs, off);
+            if (lane >= off) {
+                x += y;
+                xs += ys;
+            }
         }
-        const uint64_t m = __ballot(st);
-        if (lane == 63) wsum[w] = x;
-        if (lane == 0) wcnt[w] = (int32_t)__popcll(m);
+        if (lane == 63) {
+            wsum[w] = x;
+            wcnt[w] = xs;
+        }
         __syncthreads();
-        double e = pre;   // the weight before record k
-        int32_t r = runs;
+        double e0 = pre;   // the weight before this thread's first record
+        int32_t r0 = runs;
         for (int u = 0; u < w; ++u) {
-            e += wsum[u];
-            r += wcnt[u];
+            e0 += wsum[u];
+            r0 += wcnt[u];
         }
-        e += x - wk;
-        r += (int32_t)lanes_below(m) + (st ? 0 : -1);   // the run holding record k
-        if (st) out[r] = Comp<double>{c[k].mu, c[k].a, c[k].c, e};
+        e0 += x - run;
+        r0 += xs - nst;   // the starts before this thread's first record
+        int32_t rr[kQcU];
+        double ek[kQcU];
+        int32_t sc = 0;
+#pragma unroll
+        for (int u = 0; u < kQcU; ++u) {
+            sc += st[u];
+            rr[u] = r0 + sc - 1;   // the run holding record u
+            ek[u] = e0 + loc[u];
+            if (st[u]) out[rr[u]] = Comp<double>{mu[u + 1], av[u + 1], cv[u], ek[u]};
+        }
         __syncthreads();   // every start of this chunk written (and the shared sums read)
-        if (en) out[r].w = (e + wk) - out[r].w;
+#pragma unroll
+        for (int u = 0; u < kQcU; ++u)
+            if (en[u]) out[rr[u]].w = (ek[u] + wv[u]) - out[rr[u]].w;
         if (threadIdx.x == kQcBlock - 1) {   // the chunk's totals onward
             double t = pre;
             int32_t q = runs;
