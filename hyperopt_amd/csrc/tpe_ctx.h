@@ -197,6 +197,7 @@ struct Posterior {
     PinVec<double> bx_scan_h;
     DevBuf<tpe::BxLabel> bx;             // per label
     std::vector<tpe::BxLabel> bx_h;
+    PinVec<tpe::BxLabel> bx_up_h;        //   its upload's staging (pinned)
     DevBuf<double> bx_tab;               // per label: nbins rows of kBxRow doubles
     DevBuf<int32_t> bx_nc;               // per label at comp_a: unclipped above components
     DevBuf<tpe::BxTerm> bx_terms;        // per above record of a dense label: its bound terms (k_bx_terms)
