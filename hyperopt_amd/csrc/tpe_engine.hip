@@ -1236,12 +1236,14 @@ __global__ __launch_bounds__(1024) void k_hot_items(const int32_t* __restrict__ 
 
 
 // The expansion screen over the listed candidates only, one pass of R * 256
-// listed candidates per work item (numbered by k_hot_bx's last workgroup): a persistent grid whose
-// workgroups stage the exp table once and take items from a counter until
-// none are left -- round 3's grid of 128 workgroups per cell staged the 32 KB
-// table for about one pass each and left the cells with long lists to a
-// tail.  The same scores, bounds and appends as k_screen_bx (the passes are
-// the same R * 256-aligned slices of each cell's list).
+// listed candidates per work item (numbered by k_hot_items): one workgroup
+// per item, the grid the most items the lists can hold (the ones past the
+// round's items exit at once).  Round 4-6's persistent grid took items from
+// a counter and staged the exp table once per workgroup, but its loop let
+// the compiler hoist ~80 VGPRs of per-thread addresses out of it: 192 VGPRs,
+// two waves per SIMD, against 111 and four without the loop (r6ad).  The
+// same scores, bounds and appends as k_screen_bx (the passes are the same
+// R * 256-aligned slices of each cell's list).
 template <int R>
 __global__ __launch_bounds__(kBlock) void k_screen_hot(
     const DLabel* __restrict__ labels, const int32_t* __restrict__ group,
@@ -1254,66 +1256,50 @@ __global__ __launch_bounds__(kBlock) void k_screen_hot(
     unsigned long long* __restrict__ tkey, int64_t hstride) {
     constexpr int64_t per = (int64_t)R * kBlock;
     __shared__ double exp_tab[kExpTabSize];
-    __shared__ int item_sh;
     __shared__ uint64_t shk[kBlock / 64];
     const int32_t total = pre[cells];
-    if (threadIdx.x == 0) item_sh = total > 0 ? atomicAdd(next, 1) : total;
-    __syncthreads();
-    int32_t item = __builtin_amdgcn_readfirstlane(item_sh);   // (uniform: the item's fields live in scalar registers)
-    if (item >= total) return;   // (uniform: a workgroup with nothing to do stages nothing)
+    const int32_t item = (int32_t)blockIdx.x;
+    if (item >= total) return;   // (uniform: a workgroup past the items stages nothing)
     load_exp_table(exp_tab);
-    for (;;) {
-        // the following item claimed now, its atomic's latency under this
-        // item's work
-        int32_t nxt = 0;
-        if (threadIdx.x == 0) nxt = atomicAdd(next, 1);
-        // the item's cell: the last c with pre[c] <= item (empty cells share
-        // their successor's start)
-        int64_t lo = 0, up = cells;
-        while (up - lo > 1) {
-            const int64_t mid = (lo + up) >> 1;
-            if (pre[mid] <= item) lo = mid; else up = mid;
-        }
-        const size_t cell = (size_t)__builtin_amdgcn_readfirstlane((int)lo);   // (uniform: scalar loads below)
-        const int64_t m = min((int64_t)hcnt[cell], hstride);   // (an overflowed list falls back anyway)
-        const int64_t j0 = (int64_t)(item - pre[cell]) * per;
-        const int li = __builtin_amdgcn_readfirstlane(group[cell % (size_t)nl]);
-        const DLabel L = labels[li];
-        const BxLabel B = bx[li];
-        const bool lgmm = L.mode == DENSE_LGMM;
-        const int64_t nsb = (int64_t)B.nbins * kBxSub;
-        uint64_t kl = 0;   // the largest sub-bin L of the listed candidates
-        double x[R];
-        int64_t ci[R];
-        bool valid[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int64_t j = j0 + r * kBlock + threadIdx.x;
-            valid[r] = j < m;
-            const double d = valid[r] ? hx[cell * (size_t)hstride + j] : 0.0;   // the raw draw
-            x[r] = lgmm ? lgmm_value(d) : d;
-            ci[r] = valid[r] ? hidx[cell * (size_t)hstride + j] : 0;
-            const double f = (d - L.centre - B.xlo) * B.inv_sbw;   // k_hot_bx's sub-bin
-            if (valid[r] && f >= 0.0 && f < (double)nsb) {
-                const uint64_t k = order_key((double)sb[B.sb_off + (int64_t)f].y);
-                kl = k > kl ? k : kl;
-            }
-        }
-        double s[R], E[R], hv[R];
-        const int nterms = bx_score<R>(L, B, comps64, tab, loff, list, exp_tab, x, valid, s, E);
-        uint64_t bk = 0;
-        bx_bounds<R>(s, E, valid, hv, bk);
-        bx_append<R>(hv, valid, ci, bk, nterms, cell, hstride, hi, lbkey, cnt, idx, terms);
-        kl = block_max_key(kl, shk);
-        if (threadIdx.x == 0) {
-            if (kl) atomicMax(tkey + cell, kl);
-            item_sh = nxt;
-        }
-        __syncthreads();   // (shk read by every thread before thread 0 wrote item_sh: block_max_key's barrier)
-        item = __builtin_amdgcn_readfirstlane(item_sh);
-        if (item >= total) break;
-        __syncthreads();   // item_sh read by every thread before the next write
+    // the item's cell: the last c with pre[c] <= item (empty cells share
+    // their successor's start)
+    int64_t lo = 0, up = cells;
+    while (up - lo > 1) {
+        const int64_t mid = (lo + up) >> 1;
+        if (pre[mid] <= item) lo = mid; else up = mid;
     }
+    const size_t cell = (size_t)__builtin_amdgcn_readfirstlane((int)lo);   // (uniform: scalar loads below)
+    const int64_t m = min((int64_t)hcnt[cell], hstride);   // (an overflowed list falls back anyway)
+    const int64_t j0 = (int64_t)(item - pre[cell]) * per;
+    const int li = __builtin_amdgcn_readfirstlane(group[cell % (size_t)nl]);
+    const DLabel L = labels[li];
+    const BxLabel B = bx[li];
+    const bool lgmm = L.mode == DENSE_LGMM;
+    const int64_t nsb = (int64_t)B.nbins * kBxSub;
+    uint64_t kl = 0;   // the largest sub-bin L of the listed candidates
+    double x[R];
+    int64_t ci[R];
+    bool valid[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int64_t j = j0 + r * kBlock + threadIdx.x;
+        valid[r] = j < m;
+        const double d = valid[r] ? hx[cell * (size_t)hstride + j] : 0.0;   // the raw draw
+        x[r] = lgmm ? lgmm_value(d) : d;
+        ci[r] = valid[r] ? hidx[cell * (size_t)hstride + j] : 0;
+        const double f = (d - L.centre - B.xlo) * B.inv_sbw;   // k_hot_bx's sub-bin
+        if (valid[r] && f >= 0.0 && f < (double)nsb) {
+            const uint64_t k = order_key((double)sb[B.sb_off + (int64_t)f].y);
+            kl = k > kl ? k : kl;
+        }
+    }
+    double s[R], E[R], hv[R];
+    const int nterms = bx_score<R>(L, B, comps64, tab, loff, list, exp_tab, x, valid, s, E);
+    uint64_t bk = 0;
+    bx_bounds<R>(s, E, valid, hv, bk);
+    bx_append<R>(hv, valid, ci, bk, nterms, cell, hstride, hi, lbkey, cnt, idx, terms);
+    kl = block_max_key(kl, shk);
+    if (threadIdx.x == 0 && kl) atomicMax(tkey + cell, kl);
 }
 
 // tpe_hot_probe: the sub-bin (U, L) of caller-supplied candidates of one
@@ -1438,7 +1424,6 @@ constexpr int kBxR = TPE_BX_R;
 #define TPE_HOT_R 8
 #endif
 constexpr int kHotR = TPE_HOT_R;
-constexpr unsigned kHotScreenWgs = 1024;   // k_screen_hot's persistent grid (4 workgroups per CU: LDS)
 #ifndef TPE_HOT_WGS
 #define TPE_HOT_WGS 16384
 #endif
@@ -4165,7 +4150,9 @@ int launch_dense(tpe_ctx* ctx, const Groups& g, const RoundArgs& a) {
                                    ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p, ctx->errflag.p, lst, ctx->hot_flag.p);
                 hipLaunchKernelGGL(k_hot_items, dim3(1), dim3(1024), 0, ctx->stream, ctx->hot_cnt.p, (int64_t)cells, lst,
                                    (int64_t)kBxR * kBlock, ctx->hot_items.p);
-                hipLaunchKernelGGL((k_screen_hot<kBxR>), dim3(kHotScreenWgs), dim3(kBlock), 0, ctx->stream,
+                const int64_t items_max = (int64_t)cells * ((lst + (int64_t)kBxR * kBlock - 1) / ((int64_t)kBxR * kBlock));
+                hipLaunchKernelGGL((k_screen_hot<kBxR>), dim3((unsigned)std::max<int64_t>(1, items_max)), dim3(kBlock), 0,
+                                   ctx->stream,
                                    P.labels.p, grp, P.comps64.p, P.bx.p, P.bx_tab.p, P.bx_loff.p, P.bx_list.p, a.n,
                                    nl, (int64_t)cells, ctx->hot_items.p, ctx->hot_items.p + cells + 1,
                                    ctx->hot_cnt.p, ctx->hot_i.p, ctx->hot_x.p, ctx->scr_hid.p, ctx->scr_lb.p,

@@ -119,13 +119,6 @@ PATCHES = {
     'fin32': [('tpe_engine.hip', 'hipLaunchKernelGGL(k_rescore_fin, dim3((unsigned)std::min<int64_t>(ne_sliced, 256))',
                'hipLaunchKernelGGL(k_rescore_fin, dim3((unsigned)std::min<int64_t>(ne_sliced, 32))')],
     'mt16': [('tpe_engine.hip', 'constexpr int64_t kHotMinTiles = 6;', 'constexpr int64_t kHotMinTiles = 16;')],
-    'sh3': [('tpe_engine.hip', '__global__ __launch_bounds__(kBlock) void k_screen_hot(',
-             '__global__ __launch_bounds__(kBlock, 3) void k_screen_hot(')],
-    'sh4': [('tpe_engine.hip', '__global__ __launch_bounds__(kBlock) void k_screen_hot(',
-             '__global__ __launch_bounds__(kBlock, 4) void k_screen_hot(')],
-    # k_screen_hot's persistent grid
-    'hsw512': [('tpe_engine.hip', 'constexpr unsigned kHotScreenWgs = 1024;', 'constexpr unsigned kHotScreenWgs = 512;')],
-    'hsw2k': [('tpe_engine.hip', 'constexpr unsigned kHotScreenWgs = 1024;', 'constexpr unsigned kHotScreenWgs = 2048;')],
     'bm': [('tpe_device.h',
             '    return __builtin_amdgcn_sqrt(fmax(0.0, 2.0 * bm_neglog(u01_open0(y), lt)));\n',
             '    return (double)y * 0x1.0p-31;\n')],
