@@ -315,28 +315,27 @@ __device__ __forceinline__ void wave_window(const Comp<double>* __restrict__ c, 
     k1 = __builtin_amdgcn_readlane(lo, 32);
 }
 
-// grid (ceil(max bins / 64), dense labels): 64 consecutive bins per
-// workgroup, one bin per lane, their union window of clipped components
-// (wave_window) split over the 4 waves in interleaved batches of 64 records.
-// A batch is loaded coalesced into the wave's LDS slot as (mu', c') pairs and
-// read back by every lane at the same address (an LDS broadcast: one
-// ds_read_b128 per component instead of four v_readlane VALU operations and
-// their SGPR hazards -- round 3 measured the kernel at 0.33 VALU busy), each
-// lane adding the components within its own bin's window, branch-free, to
-// its A_0..A_14; the 4 waves' partial sums meet in LDS at the end.  The
-// bound (module comment) per lane: with |d| <= D for every summed component,
-// e^y <= e^Y (Y = 2 kappa D rmax), so the per-component terms of the bound
-// are accumulated as four sums and combined at the end (each term at least
-// what the per-component form gives).
+// grid (the labels' 64-bin blocks, flat): 64 consecutive bins per
+// workgroup, 16 per wave; a wave's union window of clipped components
+// (wave_window over its 16 bins) in batches of 64 records, loaded coalesced
+// into the wave's LDS slot as (mu', c') pairs and read back by lane groups
+// of 16 at 4 addresses a step (LDS broadcasts: one ds_read_b128 per
+// component instead of four v_readlane VALU operations and their SGPR
+// hazards -- round 3 measured the kernel at 0.33 VALU busy); each lane adds
+// every 4th component within its own bin's window, branch-free, to its
+// A_0..A_14, and the 4 groups' sums meet by shuffles at the end (round 6;
+// one bin per lane over the 64 bins' union window, 4 waves splitting it,
+// before).  The bound (module comment) per lane: with |d| <= D for every
+// summed component, e^y <= e^Y (Y = 2 kappa D rmax), so the per-component
+// terms of the bound are accumulated as four sums and combined at the end
+// (each term at least what the per-component form gives).
 //
-// Split window (grid z = nsplit > 1, for occupancy: a config-3 index has
-// ~400 workgroups of 64 bins, one wave per SIMD): workgroup z sums the z-th
-// 64-aligned part of the window and stores its sums in part (split-major,
-// [z][sum][row]); k_bx_table_fin adds the parts in z order and writes the
-// rows.  The bound counts the nsplit - 1 extra additions.
+// Split window (grid z = nsplit > 1, for occupancy): workgroup z sums the
+// z-th 64-aligned part of each wave's window and stores its sums in part
+// (split-major, [z][sum][row]); k_bx_table_fin adds the parts in z order
+// and writes the rows.  The bound counts the nsplit - 1 extra additions.
 constexpr int kTabSums = kBxP + 3;   // A_0..A_14, S0, S1, S3
 constexpr int kPartSums = kTabSums + 1;   // + the window size W
-static_assert(3 * kTabSums * 64 <= kExpTabSize, "k_bx_table: 3 waves' partial sums in the exp table's LDS");
 constexpr int kBxChains = 4;   // components per step of k_bx_table (independent chains)
 constexpr int kBxMaxSplit = 8;
 
@@ -361,7 +360,8 @@ __device__ __forceinline__ void table_row(const BxLabel& B, int b, const double*
     double* row = tab + (size_t)(B.tab_off + b) * kBxRow;
 #pragma unroll
     for (int n = 0; n < kBxP; ++n) row[n] = A[n];
-    // the sums: each wave's sequential sum, then 3 additions (of <= W terms),
+    // the sums: each lane group's sequential sum, then 2 additions (of <= W
+    // terms; 6 counted, from the 4-wave form),
     // then nsplit - 1 more (split window)
     row[kBxP] = 1.02 * (Rb + ERR + (W + 6.0 + (double)(nsplit - 1) + 2.0 * kBxP + 8.0) * kU * G) + 1e-300;
 }
@@ -378,21 +378,27 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
     const int2 blk = blocks[blockIdx.x];   // (dense label position, first bin)
     const int li = grp[blk.x];
     const BxLabel B = bx[li];
-    const int b0 = blk.y;             // the workgroup's first bin
+    const int b0 = blk.y;             // the workgroup's first bin (nbins: a multiple of 64)
     const DLabel L = labels[li];
-    __shared__ double lds[kExpTabSize];   // the exp table, then the waves' partial sums
+    __shared__ double lds[kExpTabSize];   // the exp table
     __shared__ double2 stage[kBlock / 64][64];   // per wave: its batch's (mu', c')
     load_exp_table(lds);
+    // wave w: the 16 bins b0 + 16 w .. + 15; lane = (component group g,
+    // bin bl): each lane sums every 4th component of its wave's window for
+    // its bin, the 4 groups added at the end (round 6: the 64 bins' union
+    // window over all 64 lanes evaluated ~1.36x the (bin, component) pairs
+    // that can reach a bin at T = 64; 16 bins' union ~1.09x)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int b = b0 + lane, blast = min(b0 + 63, B.nbins - 1);
+    const int bl = lane & 15, g = lane >> 4;
+    const int bw0 = b0 + 16 * wave, b = bw0 + bl;
     const double kap = B.kappa;
     auto centre = [&](int i) { return B.xlo + ((double)i + 0.5) * B.bw; };
     auto reach = [&](double x) { return bin_reach(B, x); };
-    const double xb = centre(min(b, blast)), D = reach(xb);
-    // (the window: records sorted by mu, so the clipped ones within D of
-    // any of the workgroup's bins are a contiguous index range; margins cover
-    // mu' = m'/a' rounding)
-    const double xf = centre(b0), xl = centre(blast);
+    const double xb = centre(b), D = reach(xb);
+    // (the wave's window: records sorted by mu, so the clipped ones within D
+    // of any of its bins are a contiguous index range; margins cover mu' =
+    // m'/a' rounding)
+    const double xf = centre(bw0), xl = centre(bw0 + 15);
     int k0, k1;
     wave_window(comps64 + L.comp_a, L.na, xf - reach(xf), xl + reach(xl), k0, k1);
     const Comp<double>* c = comps64 + L.comp_a;
@@ -405,10 +411,10 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
     // added to the rounding term); the powers g (2 kappa d)^n by one
     // multiply each, A_n += that / n! (one rounding each, inside 3P + 10)
     const double inv_a = 1.0 / B.astar;
-    // this workgroup's part of the window: [ks, ke)
+    // this workgroup's part of the wave's window: [ks, ke)
     const int chunk = ((k1 - k0 + nsplit - 1) / nsplit + 63) & ~63;
     const int ks = min(k1, k0 + (int)blockIdx.z * chunk), ke = min(k1, ks + chunk);
-    for (int kc = ks + wave * 64; kc < ke; kc += kBlock) {
+    for (int kc = ks; kc < ke; kc += 64) {
         const int k = kc + lane;
         double mu_l = 0.0, c_l = -kInf;
         if (k < ke) {
@@ -422,18 +428,20 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
         __builtin_amdgcn_wave_barrier();   // (the previous batch's reads come first: LDS is in order per wave)
         stage[wave][lane] = double2{mu_l, c_l};
         __builtin_amdgcn_wave_barrier();
-        // kBxChains components per step: independent exp and power chains
-        for (int j = 0; j < cnt; j += kBxChains) {
+        // kBxChains components per lane per step (independent exp and power
+        // chains): lane group g takes components j + g + 4 q
+        for (int j = 0; j < cnt; j += 4 * kBxChains) {
             double cj[kBxChains], dj[kBxChains], aj[kBxChains], mj[kBxChains];
             bool any = false;
 #pragma unroll
             for (int q = 0; q < kBxChains; ++q) {
-                const double2 v = stage[wave][min(j + q, 63)];   // (the same address on every lane)
-                cj[q] = j + q < cnt ? v.y : -kInf;
+                const int jj = j + g + 4 * q;
+                const double2 v = stage[wave][min(jj, 63)];   // (4 addresses per wave: LDS broadcasts)
+                cj[q] = jj < cnt ? v.y : -kInf;
                 mj[q] = v.x;
                 any = any || cj[q] > -kInf;
             }
-            if (!any) continue;   // unclipped or weightless (wave-uniform)
+            if (!__ballot(any)) continue;   // unclipped or weightless (wave-uniform)
             double t[kBxChains], y[kBxChains];
 #pragma unroll
             for (int q = 0; q < kBxChains; ++q) {
@@ -446,8 +454,6 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
                 t[q] = in ? e : 0.0;
                 y[q] = 2.0 * kap * dj[q];
             }
-            // (the sums in the order of the two-chain version: component j,
-            // then j + 1, ...: every addend and its position are unchanged)
 #pragma unroll
             for (int q = 0; q < kBxChains; ++q) {
                 S0 += t[q];
@@ -465,25 +471,18 @@ __global__ __launch_bounds__(kBlock) void k_bx_table(const DLabel* __restrict__ 
             for (int q = 0; q < kBxChains; ++q) S3 += fabs(t[q] * y[q]);
         }
     }
-    __syncthreads();   // the exp table is no longer read: partial sums of waves 1..3
-    if (wave > 0) {
-        double* p = lds + ((wave - 1) * kTabSums) * 64 + lane;
+    // the 4 groups' sums per bin: (g0 + g2) + (g1 + g3) into lanes 0..15
+    auto fold = [&](double v) {
+        v += __shfl_down(v, 32);
+        v += __shfl_down(v, 16);
+        return v;
+    };
 #pragma unroll
-        for (int n = 0; n < kBxP; ++n) p[n * 64] = A[n];
-        p[(kBxP + 0) * 64] = S0;
-        p[(kBxP + 1) * 64] = S1;
-        p[(kBxP + 2) * 64] = S3;
-    }
-    __syncthreads();
-    if (wave > 0 || b >= B.nbins) return;
-    for (int w = 0; w < 3; ++w) {
-        const double* p = lds + (w * kTabSums) * 64 + lane;
-#pragma unroll
-        for (int n = 0; n < kBxP; ++n) A[n] += p[n * 64];
-        S0 += p[(kBxP + 0) * 64];
-        S1 += p[(kBxP + 1) * 64];
-        S3 += p[(kBxP + 2) * 64];
-    }
+    for (int n = 0; n < kBxP; ++n) A[n] = fold(A[n]);
+    S0 = fold(S0);
+    S1 = fold(S1);
+    S3 = fold(S3);
+    if (g != 0) return;
     if (nsplit > 1) {   // (coalesced over the bins: [z][sum][row])
         double* q = part + (size_t)blockIdx.z * kPartSums * rows + B.tab_off + b;
 #pragma unroll
