@@ -981,9 +981,12 @@ int tpe_rt::bx_build(tpe_ctx* ctx) {
     // 1 / 2 / 3 / 4 -> 3.36 / 3.13 / 3.03 / 3.05 ms, r5bf (unsplit until the
     // quantized labels' rebuild beside it stopped holding the host, r5z)
     const int64_t wgs = (rows + 63) / 64;
+    // (round 6, 16 bins per wave: config 3 split 1 / 2 / 4 / 8 -> 0.364 /
+    // 0.361 / 0.354 / 0.382 ms index, config 5 1 / 2 / 3 / 4 / 6 -> 2.97 /
+    // 2.73 / 2.68 / 2.67 / 2.75 ms, r6ag: at most 4 parts)
     const int nsplit = ctx->bx_split > 0 ? std::min(ctx->bx_split, kBxMaxSplit)
                        : wgs >= 4096     ? 3
-                                         : (int)std::max<int64_t>(1, std::min<int64_t>(kBxMaxSplit, 8192 / std::max<int64_t>(wgs, 1)));
+                                         : (int)std::max<int64_t>(1, std::min<int64_t>(4, 8192 / std::max<int64_t>(wgs, 1)));
     if (nsplit > 1) HIPCHK(ctx, P.bx_part.reserve((size_t)nsplit * kPartSums * rows));
     {   // the labels' 64-bin blocks, numbered flat (the previous index's
         // copy out of the pinned buffer is done: bx_build's scan read-back
