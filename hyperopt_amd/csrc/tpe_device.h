@@ -301,6 +301,7 @@ constexpr int kGuideSteps = 3;   // guided picks take at most this many comparis
 struct alignas(16) SampLds {
     double cdf[kSampLds], mu[kSampLds], ssg[kSampLds], p0[kSampLds], q0[kSampLds], m[kSampLds], iw[kSampLds];
     uint64_t thr[kSampLds];   // ceil(cdf 2^32)
+    uint32_t thr1[kSampLds];  // thr - 1 (thr >= 1 wherever the guided pick compares: thr <= w <=> thr1 < w)
     uint8_t guide[64];
     uint8_t gd[256];
     int steps;
@@ -314,10 +315,12 @@ struct SampShared {
         const int st = steps >= 0 ? steps : __builtin_amdgcn_readfirstlane(t->steps);
         int k;
         if (st <= kGuideSteps) {
+            // (from the guide on, cdf[k] > (w >> 24) 2^-8 >= 0: thr[k] >= 1, so
+            // the 32-bit thr1 compare is the 64-bit one)
             k = t->gd[w >> 24];
 #pragma unroll
             for (int s = 0; s < kGuideSteps; ++s)
-                if (s < st) k += t->thr[k] <= w ? 1 : 0;   // (k <= ns - 1 throughout: thr[ns - 1] = 2^32 > w)
+                if (s < st) k += t->thr1[k] < w ? 1 : 0;   // (k <= ns - 1 throughout: thr[ns - 1] = 2^32 > w)
         } else {   // branch-free lower bound over the 64 (padded with 2.0: thr 2^33)
             k = 0;
 #pragma unroll
@@ -350,6 +353,7 @@ __device__ __forceinline__ bool stage_samp(const DLabel& L, const SampRec* __res
             const uint64_t thi = pick_thr(r.cdf), tlo = k ? pick_thr(samp[L.samp_off + k - 1].cdf) : 0;
             t->cdf[k] = r.cdf;
             t->thr[k] = thi;
+            t->thr1[k] = (uint32_t)(thi - 1);   // (thi = 0: never compared by the guided pick)
             t->mu[k] = r.mu;
             t->ssg[k] = r.ssg;
             t->p0[k] = r.p0;
@@ -359,6 +363,7 @@ __device__ __forceinline__ bool stage_samp(const DLabel& L, const SampRec* __res
         } else {   // padding: never picked (u < 1 <= cdf[ns - 1])
             t->cdf[k] = 2.0;
             t->thr[k] = 1ull << 33;
+            t->thr1[k] = 0xffffffffu;   // (never reached: thr[ns - 1] = 2^32 stops the pick)
             t->mu[k] = 0.0;
             t->ssg[k] = 0.0;
             t->p0[k] = 0.0;
