@@ -1089,13 +1089,18 @@ __global__ __launch_bounds__(kBlock, 8) void k_hot_bx(
             }
         }
         uint32_t mark = 0;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
+        auto mark_one = [&](int r) {
             const int k = src.pick_index(wp[r]);
             const uint32_t uc = wu[r] >> (32 - kHotCellBits);
-            const bool m = base + (int64_t)tile_cand(r, threadIdx.x, kBlock) < n &&
-                           ((ucw[k * kHotCellWords + (uc >> 5)] >> (uc & 31)) & 1u);
-            mark |= (uint32_t)m << r;
+            return (bool)((ucw[k * kHotCellWords + (uc >> 5)] >> (uc & 31)) & 1u);
+        };
+        if (base + per <= n) {   // (uniform: a whole tile, no range check per candidate)
+#pragma unroll
+            for (int r = 0; r < R; ++r) mark |= (uint32_t)mark_one(r) << r;
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                mark |= (uint32_t)(base + (int64_t)tile_cand(r, threadIdx.x, kBlock) < n && mark_one(r)) << r;
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
