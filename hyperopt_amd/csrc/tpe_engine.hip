@@ -1074,16 +1074,20 @@ __global__ __launch_bounds__(kBlock, 8) void k_hot_bx(
         // the tile's words, picks and u-cell bits for all R slots at once
         // (independent chains: their LDS lookups overlap)
         uint32_t wp[R], wu[R];
+        if (paired) {   // (one uniform branch per tile: the pairs' chains interleave)
 #pragma unroll
-        for (int r = 0; r < R; r += 2) {
-            const uint32_t c0 = tile_cand(r, threadIdx.x, kBlock);
-            if (paired) {
+            for (int r = 0; r < R; r += 2) {
+                const uint32_t c0 = tile_cand(r, threadIdx.x, kBlock);
                 const U4 W = philox4x32_10(U4{(g0 + c0) >> 1, 0u, (uint32_t)L.stream, rk}, k0, k1);
                 wp[r] = W.x;
                 wu[r] = W.y;
                 wp[r + 1] = W.z;
                 wu[r + 1] = W.w;
-            } else {
+            }
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; r += 2) {
+                const uint32_t c0 = tile_cand(r, threadIdx.x, kBlock);
                 draw_words(L, k0, k1, g0 + c0, rk, wp[r], wu[r]);
                 draw_words(L, k0, k1, g0 + c0 + 1u, rk, wp[r + 1], wu[r + 1]);
             }
