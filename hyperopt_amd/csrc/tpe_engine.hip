@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -1068,57 +1069,77 @@ __global__ __launch_bounds__(kBlock, 8) void k_hot_bx(
         __builtin_amdgcn_wave_barrier();
     };
     int wn = 0;   // this wave's buffered indices (wave-uniform)
-    for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per) {
-        const uint32_t g0 = (uint32_t)(cand_offset + base);
-        const bool paired = (g0 & 1u) == 0;   // (uniform)
-        // the tile's words, picks and u-cell bits for all R slots at once
-        // (independent chains: their LDS lookups overlap)
-        uint32_t wp[R], wu[R];
-        if (paired) {   // (one uniform branch per tile: the pairs' chains interleave)
+    // the tile loop, its guided pick's step count (uniform over the
+    // workgroup: the label's) a compile-time constant -- the candidates'
+    // pick chains then interleave, without a branch per step
+    auto tiles = [&](auto st_c) {
+        constexpr int ST = decltype(st_c)::value;
+        for (int64_t base = (int64_t)blockIdx.x * per; base < n; base += (int64_t)gridDim.x * per) {
+            const uint32_t g0 = (uint32_t)(cand_offset + base);
+            const bool paired = (g0 & 1u) == 0;   // (uniform)
+            // the tile's words, picks and u-cell bits for all R slots at once
+            // (independent chains: their LDS lookups overlap)
+            uint32_t wp[R], wu[R];
+            if (paired) {   // (one uniform branch per tile: the pairs' chains interleave)
 #pragma unroll
-            for (int r = 0; r < R; r += 2) {
-                const uint32_t c0 = tile_cand(r, threadIdx.x, kBlock);
-                const U4 W = philox4x32_10(U4{(g0 + c0) >> 1, 0u, (uint32_t)L.stream, rk}, k0, k1);
-                wp[r] = W.x;
-                wu[r] = W.y;
-                wp[r + 1] = W.z;
-                wu[r + 1] = W.w;
+                for (int r = 0; r < R; r += 2) {
+                    const uint32_t c0 = tile_cand(r, threadIdx.x, kBlock);
+                    const U4 W = philox4x32_10(U4{(g0 + c0) >> 1, 0u, (uint32_t)L.stream, rk}, k0, k1);
+                    wp[r] = W.x;
+                    wu[r] = W.y;
+                    wp[r + 1] = W.z;
+                    wu[r + 1] = W.w;
+                }
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; r += 2) {
+                    const uint32_t c0 = tile_cand(r, threadIdx.x, kBlock);
+                    draw_words(L, k0, k1, g0 + c0, rk, wp[r], wu[r]);
+                    draw_words(L, k0, k1, g0 + c0 + 1u, rk, wp[r + 1], wu[r + 1]);
+                }
             }
-        } else {
+            uint32_t mark = 0;
+            auto mark_one = [&](int r) {
+                int k;
+                if constexpr (ST >= 0) {   // the guided pick with its step count fixed: no branch per step
+                    k = sl.gd[wp[r] >> 24];
 #pragma unroll
-            for (int r = 0; r < R; r += 2) {
-                const uint32_t c0 = tile_cand(r, threadIdx.x, kBlock);
-                draw_words(L, k0, k1, g0 + c0, rk, wp[r], wu[r]);
-                draw_words(L, k0, k1, g0 + c0 + 1u, rk, wp[r + 1], wu[r + 1]);
+                    for (int t = 0; t < ST; ++t) k += sl.thr1[k] < wp[r] ? 1 : 0;
+                } else {
+                    k = src.pick_index(wp[r]);
+                }
+                const uint32_t uc = wu[r] >> (32 - kHotCellBits);
+                return (bool)((ucw[k * kHotCellWords + (uc >> 5)] >> (uc & 31)) & 1u);
+            };
+            if (base + per <= n) {   // (uniform: a whole tile, no range check per candidate)
+#pragma unroll
+                for (int r = 0; r < R; ++r) mark |= (uint32_t)mark_one(r) << r;
+            } else {
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+                    mark |= (uint32_t)(base + (int64_t)tile_cand(r, threadIdx.x, kBlock) < n && mark_one(r)) << r;
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const bool m = (mark >> r) & 1u;
+                const uint64_t bal = __ballot(m);
+                if (!bal) continue;
+                const int c = (int)__popcll(bal);
+                if (wn + c > kMarkBuf) {   // (wave-uniform)
+                    flush(wn);
+                    wn = 0;
+                }
+                if (m) buf[wv][wn + (int)lanes_below(bal)] = (int32_t)(base + (int64_t)tile_cand(r, threadIdx.x, kBlock));
+                wn += c;
             }
         }
-        uint32_t mark = 0;
-        auto mark_one = [&](int r) {
-            const int k = src.pick_index(wp[r]);
-            const uint32_t uc = wu[r] >> (32 - kHotCellBits);
-            return (bool)((ucw[k * kHotCellWords + (uc >> 5)] >> (uc & 31)) & 1u);
-        };
-        if (base + per <= n) {   // (uniform: a whole tile, no range check per candidate)
-#pragma unroll
-            for (int r = 0; r < R; ++r) mark |= (uint32_t)mark_one(r) << r;
-        } else {
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-                mark |= (uint32_t)(base + (int64_t)tile_cand(r, threadIdx.x, kBlock) < n && mark_one(r)) << r;
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const bool m = (mark >> r) & 1u;
-            const uint64_t bal = __ballot(m);
-            if (!bal) continue;
-            const int c = (int)__popcll(bal);
-            if (wn + c > kMarkBuf) {   // (wave-uniform)
-                flush(wn);
-                wn = 0;
-            }
-            if (m) buf[wv][wn + (int)lanes_below(bal)] = (int32_t)(base + (int64_t)tile_cand(r, threadIdx.x, kBlock));
-            wn += c;
-        }
+    };
+    switch (src.steps) {
+    case 0: tiles(std::integral_constant<int, 0>{}); break;
+    case 1: tiles(std::integral_constant<int, 1>{}); break;
+    case 2: tiles(std::integral_constant<int, 2>{}); break;
+    case 3: tiles(std::integral_constant<int, 3>{}); break;
+    default: tiles(std::integral_constant<int, -1>{}); break;
     }
     if (wn > 0) flush(wn);
     __syncthreads();
